@@ -1,0 +1,130 @@
+#!/usr/bin/env python
+"""Headline benchmark: whole-job MNIST-CNN training images/sec on N MI355X GPUs.
+
+Metric/config from BASELINE.json: "images/sec (whole node) MNIST CNN at 1/2/4/8
+MI355X; step time ms".  Model = the reference's Keras MNIST CNN
+(distributed_with_keras.py:33-43: Conv2D(32,3,relu) · MaxPool · Flatten ·
+Dense(64,relu) · Dense(10), SCCE(from_logits), SGD(0.001)), random-init weights,
+synthetic 28x28x1 inputs, per-GPU batch 64 (the reference's BATCH_SIZE per
+worker, distributed_with_keras.py:13) -> weak scaling, global batch 64*N.
+Distribution: MultiWorkerMirroredStrategy, one process per GPU, RCCL gradient
+all-reduce over xGMI.  Every timed step runs the full forward, backward, gradient
+all-reduce and SGD update (bf16 MFMA compute, fp32 master weights).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+METRIC = "images/sec (whole node) MNIST CNN at 1/2/4/8 MI355X; step time ms"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=64)
+    ap.add_argument("--model", default="mnist_cnn", choices=["mnist_cnn", "mnist_bn_cnn"])
+    ap.add_argument("--batch-per-gpu", type=int, default=64)
+    ap.add_argument("--spe", type=int, default=16, help="steps_per_execution (steps per hipGraph replay)")
+    ap.add_argument("--lr", type=float, default=0.001)
+    ap.add_argument("--executor", default=None, help="fused|reference (default: fused on GPU)")
+    ap.add_argument("--no-graph", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    if a.no_graph:
+        os.environ["TDE_GRAPH"] = "0"
+    if a.executor:
+        os.environ["TDE_EXECUTOR"] = a.executor
+    import numpy as np
+    import torch
+
+    import tensorflow_distributed_example_amd as tde
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torchrun --nproc-per-node N")
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local_rank)
+    tde.backend.set_random_seed(1234)
+    strategy = tde.distribute.MultiWorkerMirroredStrategy()
+    n = strategy.num_replicas_in_sync
+    B = a.batch_per_gpu
+    GB = B * n
+    spe = a.spe
+    while a.steps % spe:
+        spe -= 1
+    with strategy.scope():
+        model = tde.zoo.mnist_cnn() if a.model == "mnist_cnn" else tde.zoo.mnist_bn_cnn()
+        from_logits = a.model == "mnist_cnn"
+        model.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=from_logits),
+                      optimizer=tde.optimizers.SGD(learning_rate=a.lr), metrics=["accuracy"],
+                      steps_per_execution=spe)
+    prog = model._program("train", GB)
+    dev = strategy.local_devices[0]
+    in_shape = prog.x_shape
+    # Synthetic MNIST-shaped data resident on the device: a pool of batches,
+    # staged into the program's input ring once per execution (D2D copy).
+    pool_execs = 4
+    g = torch.Generator(device="cpu").manual_seed(1000 + strategy.worker_index)
+    xs = torch.rand((pool_execs, spe, B) + tuple(in_shape), generator=g).to(dev)
+    ys = torch.randint(0, 10, (pool_execs, spe, B), generator=g).to(torch.int32).to(dev)
+
+    def run_exec(i):
+        k = i % pool_execs
+        prog.stage([(xs[k], ys[k])])
+        prog.run()
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+
+    n_warm = max(1, math.ceil(a.warmup / spe))
+    for i in range(n_warm):
+        run_exec(i)
+    prog.sync()
+    barrier()
+    prog.sync()
+    t0 = time.perf_counter()
+    n_exec = a.steps // spe
+    for i in range(n_exec):
+        run_exec(i)
+    prog.sync()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    logs = tde.metrics.logs_from(prog.global_metrics(), ["accuracy"])
+    ms = elapsed / a.steps * 1e3
+    ips = GB * a.steps / elapsed
+    if strategy.worker_index == 0:
+        print(f"[bench] plan={prog.plan_kind} graph={prog.use_graph} spe={spe} world={n} "
+              f"loss={logs['loss']:.4f} acc={logs['accuracy']:.4f}", file=sys.stderr)
+        print(json.dumps({
+            "metric": METRIC, "value": round(ips, 1), "unit": "images/sec", "n_gpus": n, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random 28x28x1 images, random labels; "
+            "random-init weights)",
+            "config": {"model": a.model, "global_batch": GB, "seq_len": None, "image_shape": [28, 28, 1],
+                       "per_gpu_batch": B, "parallelism": f"dp{n}", "strategy": "MultiWorkerMirroredStrategy",
+                       "steps_per_execution": spe, "optimizer": f"SGD(lr={a.lr})", "plan": prog.plan_kind,
+                       "hipgraph": prog.use_graph}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,62 @@
+// Shared device/host helpers for the CDNA4 (gfx950) kernel library.
+//
+// Everything in csrc/kernels is written for MI355X only: 64-lane wavefronts,
+// MFMA 16x16x32 bf16 matrix cores, 160 KiB LDS per CU.  Host entry points are
+// exported with C linkage (TDE_API) and take raw device pointers plus the
+// hipStream_t of the caller, so they can be driven from Python via ctypes and
+// captured into hipGraphs (no allocation, no synchronisation inside any entry).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define TDE_API extern "C" __attribute__((visibility("default")))
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+
+namespace tde {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float bf2f(bf16 v) { return (float)v; }
+__device__ __forceinline__ bf16 f2bf(float v) { return (bf16)v; }
+
+// Wave-wide sum over 64 lanes.
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// MFMA 16x16x32 bf16 -> f32.  Lane l holds A[row l&15][k 8*(l>>4) .. +7] and
+// B[k 8*(l>>4) .. +7][col l&15]; the accumulator holds C[row 4*(l>>4)+r][col l&15].
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// 16-byte fragment load with a zero fill outside [0, limit) (limit counted in
+// elements along K).  `p` points at element k0 of the row.
+__device__ __forceinline__ bf16x8 load_frag(const bf16* p, int k0, int K, bool row_ok) {
+  if (row_ok && k0 + 8 <= K) return *reinterpret_cast<const bf16x8*>(p);
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (row_ok && k0 + j < K) ? p[j] : (bf16)0.0f;
+  return r;
+}
+
+}  // namespace tde
+
+#define TDE_LAUNCH_CHECK() \
+  do {                     \
+    hipError_t e__ = hipGetLastError(); \
+    if (e__ != hipSuccess) return (int)e__; \
+  } while (0)

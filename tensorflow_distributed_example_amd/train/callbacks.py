@@ -1,0 +1,137 @@
+"""Keras-style callbacks: History, ProgbarLogger, ModelCheckpoint, plus the
+progress bar that prints ``ms/step`` / loss / accuracy (the only timing the
+reference's DWK path reports — distributed_with_keras.py:63)."""
+from __future__ import annotations
+
+import sys
+import time
+
+
+class Callback:
+    def __init__(self):
+        self.model = None
+        self.params = {}
+
+    def set_model(self, model):
+        self.model = model
+
+    def set_params(self, params):
+        self.params = params
+
+    def on_train_begin(self, logs=None): pass
+    def on_train_end(self, logs=None): pass
+    def on_epoch_begin(self, epoch, logs=None): pass
+    def on_epoch_end(self, epoch, logs=None): pass
+    def on_train_batch_begin(self, batch, logs=None): pass
+    def on_train_batch_end(self, batch, logs=None): pass
+    def on_test_begin(self, logs=None): pass
+    def on_test_end(self, logs=None): pass
+
+
+class History(Callback):
+    def on_train_begin(self, logs=None):
+        self.epoch = []
+        self.history = {}
+
+    def on_epoch_end(self, epoch, logs=None):
+        self.epoch.append(epoch)
+        for k, v in (logs or {}).items():
+            self.history.setdefault(k, []).append(v)
+
+
+class Progbar:
+    def __init__(self, target, width=30, verbose=1, stream=None):
+        self.target = target
+        self.width = width
+        self.verbose = verbose
+        self.stream = stream or sys.stdout
+        self.start = time.perf_counter()
+        self._last = 0.0
+
+    def update(self, current, values=None, finalize=False):
+        if not self.verbose:
+            return
+        now = time.perf_counter()
+        if not finalize and now - self._last < 0.1:
+            return
+        self._last = now
+        elapsed = now - self.start
+        vals = " - ".join(f"{k}: {v:.4f}" for k, v in (values or {}).items())
+        if self.target:
+            frac = min(current / self.target, 1.0)
+            bar = "=" * int(self.width * frac)
+            if frac < 1:
+                bar = bar[:-1] + ">" if bar else ">"
+            bar = bar.ljust(self.width, ".")
+            per = elapsed / max(current, 1)
+            unit = f"{per * 1e3:.0f}ms/step" if per >= 1e-3 else f"{per * 1e6:.0f}us/step"
+            line = f"{current}/{self.target} [{bar}] - {elapsed:.0f}s {unit}"
+        else:
+            line = f"{current} - {elapsed:.0f}s"
+        if vals:
+            line += " - " + vals
+        end = "\n" if finalize or self.verbose == 2 else "\r"
+        if self.verbose == 2 and not finalize:
+            return
+        self.stream.write(line + end)
+        self.stream.flush()
+
+
+class ProgbarLogger(Callback):
+    def __init__(self, verbose=1):
+        super().__init__()
+        self.verbose = verbose
+        self.bar = None
+
+    def on_epoch_begin(self, epoch, logs=None):
+        if self.verbose:
+            print(f"Epoch {epoch + 1}/{self.params.get('epochs', '?')}")
+        self.bar = Progbar(self.params.get("steps"), verbose=self.verbose)
+
+    def on_train_batch_end(self, batch, logs=None):
+        if self.bar:
+            self.bar.update(batch + 1, logs)
+
+    def on_epoch_end(self, epoch, logs=None):
+        if self.bar:
+            self.bar.update(self.params.get("steps") or self.params.get("seen", 0), logs, finalize=True)
+
+
+class ModelCheckpoint(Callback):
+    def __init__(self, filepath, save_weights_only=True, save_freq="epoch", **kw):
+        super().__init__()
+        self.filepath = filepath
+        self.save_weights_only = save_weights_only
+
+    def on_epoch_end(self, epoch, logs=None):
+        path = self.filepath.format(epoch=epoch + 1, **(logs or {}))
+        self.model.save_weights(path)
+
+
+class LambdaCallback(Callback):
+    def __init__(self, on_epoch_end=None, on_train_batch_end=None, **kw):
+        super().__init__()
+        self._oee = on_epoch_end
+        self._otbe = on_train_batch_end
+
+    def on_epoch_end(self, epoch, logs=None):
+        if self._oee:
+            self._oee(epoch, logs)
+
+    def on_train_batch_end(self, batch, logs=None):
+        if self._otbe:
+            self._otbe(batch, logs)
+
+
+class CallbackList:
+    def __init__(self, cbs, model, params):
+        self.cbs = list(cbs)
+        for c in self.cbs:
+            c.set_model(model)
+            c.set_params(params)
+
+    def __getattr__(self, name):
+        def f(*a, **k):
+            for c in self.cbs:
+                getattr(c, name)(*a, **k)
+        return f

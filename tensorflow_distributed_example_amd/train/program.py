@@ -1,0 +1,372 @@
+"""Per-replica execution plans and the multi-step training program.
+
+A *plan* executes one replica's work for one step on one device:
+
+* ``ConvNetPlan`` (GPU): the DWK/TF2M small CNN as five
+  fused gfx950 HIP kernels —
+      conv+bias+ReLU+maxpool (VALU)  → Dense split-K MFMA (atomic f32)
+      → head: bias+ReLU, Dense, softmax-CE, accuracy, and the whole head backward
+      → dW of the big Dense (MFMA) → conv backward with the Dense input-gradient
+        computed in-kernel (MFMA) and routed through pool argmax / ReLU mask;
+  followed by the RCCL all-reduce of the flat gradient bucket and ONE
+  multi-tensor optimizer kernel.
+* ``LayerwisePlan`` (GPU): any Sequential model built from the supported layers,
+  one HIP kernel family per layer (ops/layerwise.py) — Model B, ResNet-18.
+* ``ReferencePlan`` (CPU, or GPU when explicitly requested for testing): torch
+  ops + autograd — the CPU backend's kernel library and the numerics oracle.
+
+``TrainProgram`` strings ``steps_per_execution`` steps (Keras
+``compile(steps_per_execution=N)``) of every local replica together with the
+gradient all-reduce and optimizer, and on a single-local-replica GPU captures the
+whole N-step sequence — RCCL collective included — into one hipGraph replayed
+per execution, so the host issues one launch per N steps.
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import numpy as np
+import torch
+
+from .. import backend as Kb
+from ..models import layers as L
+from . import params as P
+
+
+def _round8(n):
+    return (n + 7) // 8 * 8
+
+
+class ReplicaPlan:
+    kind = "base"
+
+    def __init__(self, model, store, device, batch, global_batch, optimizer):
+        self.model = model
+        self.store = store
+        self.device = torch.device(device)
+        self.B = int(batch)
+        self.global_batch = int(global_batch)
+        self.scale = 1.0 / float(global_batch)
+        self.optimizer = optimizer
+        self.metrics = torch.zeros(4, dtype=torch.float32, device=self.device)
+        self.iterations = torch.zeros(1, dtype=torch.int64, device=self.device)
+        for s in optimizer.slot_names() if optimizer is not None else []:
+            store.slot(s)
+
+    def reset_metrics(self):
+        self.metrics.zero_()
+
+    def train_step(self, x, y, B=None):
+        raise NotImplementedError
+
+    def apply(self):
+        raise NotImplementedError
+
+    def eval_step(self, x, y, B=None):
+        raise NotImplementedError
+
+    def predict(self, x, B=None):
+        raise NotImplementedError
+
+    def on_weights_loaded(self):
+        pass
+
+
+# ---------------------------------------------------------------------------------------
+def _last_softmax(model, loss):
+    last = model.layers[-1]
+    act = getattr(last, "activation", None)
+    if act == "softmax" and not getattr(loss, "from_logits", False):
+        return True
+    return False
+
+
+class ReferencePlan(ReplicaPlan):
+    kind = "reference"
+
+    def __init__(self, model, store, device, batch, global_batch, optimizer, loss):
+        super().__init__(model, store, device, batch, global_batch, optimizer)
+        self.loss = loss
+        self.strip_softmax = _last_softmax(model, loss)
+        self.rng = Kb.make_generator(1234)
+
+    def _weights(self, wl):
+        W = {}
+        st = self.store
+        for layer in self.model.layers:
+            d = {}
+            for s in layer.weight_specs:
+                seg = st.segments[s.full_name]
+                if seg.trainable and wl is not None:
+                    d[s.name] = wl[seg.offset: seg.offset + seg.numel].view(seg.shape)
+                else:
+                    d[s.name] = st.view(s.full_name)
+            W[layer.name] = d
+        return W
+
+    def _forward(self, x, W, training, updates=None):
+        h = x.float()
+        layers = self.model.layers
+        for i, layer in enumerate(layers):
+            if i == len(layers) - 1 and self.strip_softmax:
+                act = layer.activation
+                layer.activation = None
+                try:
+                    h = layer.ref_call(h, W[layer.name], training, self.rng, updates)
+                finally:
+                    layer.activation = act
+            else:
+                h = layer.ref_call(h, W[layer.name], training, self.rng, updates)
+        return h
+
+    def train_step(self, x, y, B=None):
+        B = x.shape[0] if B is None else B
+        x, y = x[:B], y[:B]
+        wl = self.store.w.detach().requires_grad_(True)
+        W = self._weights(wl)
+        updates = []
+        out = self._forward(x, W, True, updates)
+        ls = self.loss.per_sample(y, out, pred_is_logits=self.strip_softmax)
+        (ls.sum() * self.scale).backward()
+        with torch.no_grad():
+            self.store.g.add_(wl.grad)
+            for name, val in updates:
+                self.store.view(name).copy_(val)
+            self._acc(out, y, ls)
+
+    def _acc(self, out, y, ls):
+        yy = torch.as_tensor(y, device=out.device).reshape(-1).long()
+        correct = (out.argmax(dim=1) == yy).sum().float()
+        self.metrics += torch.stack([ls.sum().float(), correct, torch.tensor(float(ls.shape[0]), device=out.device),
+                                     torch.zeros((), device=out.device)])
+
+    @torch.no_grad()
+    def apply(self):
+        st = self.store
+        slots = {n: st.slot(n) for n in self.optimizer.slot_names()}
+        self.optimizer.apply_reference(st.w, st.g, slots, int(self.iterations.item()))
+        st.g.zero_()
+        self.iterations += 1
+
+    @torch.no_grad()
+    def eval_step(self, x, y, B=None):
+        B = x.shape[0] if B is None else B
+        out = self._forward(x[:B], self._weights(None), False)
+        ls = self.loss.per_sample(y[:B], out, pred_is_logits=self.strip_softmax)
+        self._acc(out, y[:B], ls)
+
+    @torch.no_grad()
+    def predict(self, x, B=None):
+        B = x.shape[0] if B is None else B
+        out = self._forward(x[:B], self._weights(None), False)
+        if self.strip_softmax:
+            out = torch.softmax(out, dim=-1)
+        return out
+
+
+# ---------------------------------------------------------------------------------------
+class OptimizerKernel:
+    """Device-side state for the multi-tensor optimizer kernel of one replica."""
+
+    def __init__(self, store: P.ParamStore, optimizer, shadows: dict, iterations):
+        from .. import _native as N
+        self.N = N
+        self.store = store
+        self.optimizer = optimizer
+        self.iterations = iterations
+        segs = []
+        sh_total = 0
+        self.shadow_views = {}
+        layout = []
+        for name in store.names(trainable=True):
+            seg = store.segments[name]
+            rows, cols = (seg.shape[0], int(np.prod(seg.shape[1:]))) if len(seg.shape) >= 2 else (1, seg.numel)
+            sh = sht = -1
+            if name in shadows:
+                want = shadows[name]
+                if "row" in want:
+                    sh = sh_total
+                    sh_total += _round8(seg.numel)
+                if "col" in want:
+                    sht = sh_total
+                    sh_total += _round8(seg.numel)
+            segs.append((seg.offset, rows, cols, sh, sht))
+            layout.append((name, rows, cols, sh, sht))
+        self.shadow = torch.zeros(max(sh_total, 8), dtype=torch.bfloat16, device=store.device)
+        for name, rows, cols, sh, sht in layout:
+            if sh >= 0:
+                self.shadow_views[(name, "row")] = self.shadow[sh: sh + rows * cols].view(rows, cols)
+            if sht >= 0:
+                self.shadow_views[(name, "col")] = self.shadow[sht: sht + rows * cols].view(cols, rows)
+        dt = np.dtype([("off", "<i8"), ("rows", "<i4"), ("cols", "<i4"), ("sh", "<i8"), ("sht", "<i8")])
+        arr = np.array(segs, dtype=dt)
+        self._segs_host = arr
+        lib = N.hip()
+        nb = lib.tde_optim_table_size(arr.ctypes.data, len(arr))
+        table = np.zeros((max(nb, 1), 4), dtype=np.int32)
+        lib.tde_optim_build_table(arr.ctypes.data, len(arr), table.ctypes.data)
+        self.nblocks = nb
+        self.segs_dev = torch.from_numpy(arr.view(np.uint8).copy()).to(store.device)
+        self.table_dev = torch.from_numpy(table).to(store.device)
+        self.done = torch.zeros(1, dtype=torch.int32, device=store.device)
+        self.refresh_shadows()
+
+    def refresh_shadows(self):
+        N = self.N
+        with torch.cuda.device(self.store.device):
+            rc = N.hip().tde_shadow_refresh(self.store.w.data_ptr(), self.shadow.data_ptr(),
+                                            self.segs_dev.data_ptr(), self.table_dev.data_ptr(), self.nblocks,
+                                            N.stream_ptr())
+        N.check(rc, "tde_shadow_refresh")
+
+    def apply(self, zero_grad=True):
+        N = self.N
+        st = self.store
+        opt = self.optimizer
+        hp = opt.hparams()
+        m = st.slot(opt.slot_names()[0]) if opt.slot_names() else None
+        v = st.slot(opt.slot_names()[1]) if len(opt.slot_names()) > 1 else None
+        rc = N.hip().tde_optim_apply(st.w.data_ptr(), st.g.data_ptr(), N.ptr(m), N.ptr(v), self.shadow.data_ptr(),
+                                     self.segs_dev.data_ptr(), self.table_dev.data_ptr(), self.nblocks,
+                                     self.iterations.data_ptr(), self.done.data_ptr(), opt.kind_id,
+                                     float(opt.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"], 1.0,
+                                     int(zero_grad), None, N.stream_ptr())
+        N.check(rc, "tde_optim_apply")
+
+
+def match_convnet(model, loss):
+    """Pattern of the DWK/TF2M small CNN: Conv2D(3x3,relu,bias) on 1 channel ·
+    MaxPooling2D(2) · Flatten · Dense(bias[,relu]) · Dense(bias[,softmax]) + SCCE."""
+    from ..losses import SparseCategoricalCrossentropy
+    ls = [l for l in model.layers if not isinstance(l, L.InputLayer)]
+    if ls and isinstance(ls[0], L.Reshape) and len(ls[0].target_shape) == 3:
+        ls = ls[1:]
+    if len(ls) != 5 or not isinstance(loss, SparseCategoricalCrossentropy):
+        return None
+    c, p, f, d1, d2 = ls
+    ok = (isinstance(c, L.Conv2D) and c.kernel_size == (3, 3) and c.strides == (1, 1) and c.padding == "valid"
+          and c.activation == "relu" and c.use_bias and c.input_shape[-1] == 1 and c.filters % 16 == 0
+          and c.input_shape[1] % 2 == 0
+          and isinstance(p, L.MaxPooling2D) and p.pool_size == (2, 2) and p.strides == (2, 2) and p.padding == "valid"
+          and isinstance(f, L.Flatten)
+          and isinstance(d1, L.Dense) and d1.activation in (None, "relu")
+          and isinstance(d2, L.Dense) and d2.use_bias and d2.activation in (None, "softmax"))
+    if not ok:
+        return None
+    if (d2.activation == "softmax") == bool(loss.from_logits):
+        return None  # probabilities fed to from_logits=True (or logits w/o from_logits): not fusable
+    if d2.units > 64 or d1.units * d2.units > 16384 or d1.units % 32:
+        return None
+    return dict(conv=c, pool=p, dense1=d1, dense2=d2)
+
+
+class ConvNetPlan(ReplicaPlan):
+    kind = "fused_convnet"
+
+    def __init__(self, model, store, device, batch, global_batch, optimizer, loss, pattern):
+        super().__init__(model, store, device, batch, global_batch, optimizer)
+        from ..ops import kernels as K
+        self.K = K
+        self.loss = loss
+        c, d1, d2 = pattern["conv"], pattern["dense1"], pattern["dense2"]
+        self.c, self.d1, self.d2 = c, d1, d2
+        H, W = c.input_shape[0], c.input_shape[1]
+        self.H, self.W, self.C = H, W, c.filters
+        Hp, Wp = (H - 2) // 2, (W - 2) // 2
+        self.Kf = Hp * Wp * self.C
+        self.Hd, self.Cls = d1.units, d2.units
+        B, Bp = self.B, _round8(self.B)
+        self.Bp = Bp
+        dev = self.device
+        bf = torch.bfloat16
+        self.Pb = torch.zeros(B, self.Kf, dtype=bf, device=dev)
+        self.Pt = torch.zeros(self.Kf, Bp, dtype=bf, device=dev)
+        self.amax = torch.zeros(B, self.Kf, dtype=torch.uint8, device=dev)
+        self.hpre = torch.zeros(B, self.Hd, dtype=torch.float32, device=dev)
+        self.G = torch.zeros(B, self.Hd, dtype=bf, device=dev)
+        self.Gt = torch.zeros(self.Hd, Bp, dtype=bf, device=dev)
+        self.probs = torch.zeros(B, self.Cls, dtype=torch.float32, device=dev)
+        self.pre_relu = d1.activation == "relu"
+        self.logits_out = d2.activation is None
+        n = lambda l, w: f"{l.name}/{w}"  # noqa: E731
+        self.names = dict(wc=n(c, "kernel"), bc=n(c, "bias"), w1=n(d1, "kernel"),
+                          b1=n(d1, "bias") if d1.use_bias else None, w2=n(d2, "kernel"), b2=n(d2, "bias"))
+        self.opt = OptimizerKernel(store, optimizer, {self.names["w1"]: ("row", "col")}, self.iterations) \
+            if optimizer is not None else None
+        self._shadow_only = None
+        if self.opt is None:
+            # eval/predict-only plan still needs the bf16 weight copies
+            from ..optimizers import SGD
+            self._shadow_only = OptimizerKernel(store, SGD(0.0), {self.names["w1"]: ("row", "col")}, self.iterations)
+        ok = self.opt or self._shadow_only
+        self.W1row = ok.shadow_views[(self.names["w1"], "row")]
+        self.W1col = ok.shadow_views[(self.names["w1"], "col")]
+        self.splits = K.gemm_pick_splits(self.B, self.Hd, self.Kf)
+
+    def on_weights_loaded(self):
+        (self.opt or self._shadow_only).refresh_shadows()
+
+    def _v(self, key):
+        nm = self.names[key]
+        return None if nm is None else self.store.view(nm)
+
+    def _g(self, key):
+        nm = self.names[key]
+        return None if nm is None else self.store.grad(nm)
+
+    def _forward(self, x, B, with_pt):
+        K = self.K
+        K.conv3x3c1_relu_pool_fwd(x, self._v("wc"), self._v("bc"), self.Pb, self.Pt if with_pt else None, self.amax,
+                                  zbuf=self.hpre)
+        K.gemm_nt(self.Pb, self.W1col, self.hpre, M=B, N_=self.Hd, K=self.Kf, mode="atomic", splits=self.splits)
+
+    def train_step(self, x, y, B=None):
+        K = self.K
+        B = self.B if B is None else B
+        self._forward(x, B, True)
+        K.head_xent(self.hpre, self._v("w2"), self._v("b2"), y, B=B, scale=self.scale, pre_bias=self._v("b1"),
+                    pre_relu=self.pre_relu, compute_grad=True, dW2=self._g("w2"), db2=self._g("b2"),
+                    dpre_bias=self._g("b1"), G=self.G, Gt=self.Gt, metrics=self.metrics)
+        K.gemm_nt(self.Pt, self.Gt, self._g("w1"), M=self.Kf, N_=self.Hd, K=B, mode="store", splits=1)
+        K.conv3x3c1_relu_pool_bwd(x, self.amax, self.G, self.W1row, self._g("wc"), self._g("bc"))
+
+    def apply(self):
+        self.opt.apply()
+
+    def eval_step(self, x, y, B=None):
+        B = self.B if B is None else B
+        self._forward(x, B, False)
+        self.K.head_xent(self.hpre, self._v("w2"), self._v("b2"), y, B=B, scale=self.scale, pre_bias=self._v("b1"),
+                         pre_relu=self.pre_relu, compute_grad=False, metrics=self.metrics)
+
+    def predict(self, x, B=None):
+        B = self.B if B is None else B
+        self._forward(x, B, False)
+        self.K.head_xent(self.hpre, self._v("w2"), self._v("b2"), self._dummy_labels(B), B=B, scale=1.0,
+                         pre_bias=self._v("b1"), pre_relu=self.pre_relu, compute_grad=False, probs=self.probs,
+                         probs_are_logits=self.logits_out)
+        return self.probs[:B]
+
+    def _dummy_labels(self, B):
+        if not hasattr(self, "_zl") or self._zl.shape[0] < B:
+            self._zl = torch.zeros(max(B, self.B), dtype=torch.int32, device=self.device)
+        return self._zl
+
+
+# ---------------------------------------------------------------------------------------
+def make_plan(model, store, device, batch, global_batch, optimizer, loss, prefer=None):
+    device = torch.device(device)
+    prefer = prefer or os.environ.get("TDE_EXECUTOR")
+    if device.type == "cuda" and prefer != "reference":
+        pat = match_convnet(model, loss)
+        if pat is not None and prefer in (None, "fused"):
+            return ConvNetPlan(model, store, device, batch, global_batch, optimizer, loss, pat)
+        from . import layerwise
+        plan = layerwise.try_make(model, store, device, batch, global_batch, optimizer, loss)
+        if plan is not None:
+            return plan
+        raise NotImplementedError(
+            f"model {model.name!r} has layers without a HIP kernel path; set TDE_EXECUTOR=reference to run it "
+            "with torch reference ops")
+    return ReferencePlan(model, store, device, batch, global_batch, optimizer, loss)

@@ -1,0 +1,223 @@
+"""Multi-replica / multi-step programs driving the per-replica plans.
+
+``TrainProgram.run()`` executes ``steps_per_execution`` training steps:
+    for each step:  every local replica: fwd+bwd (HIP plan)      [compute stream]
+                    RCCL all-reduce(SUM) of each replica's flat grad bucket
+                    every local replica: optimizer kernel
+On a GPU with one local replica and a capturable communicator the whole
+sequence is captured ONCE into a hipGraph (torch.cuda.CUDAGraph) and replayed:
+the host enqueues one graph launch per execution, the inputs arrive in static
+device ring buffers [S, B, ...] filled by one async H2D (or D2D) copy.
+"""
+from __future__ import annotations
+
+import contextlib
+import os
+
+import numpy as np
+import torch
+
+from . import program as PG
+
+
+def _ctx(dev):
+    return torch.cuda.device(dev) if dev.type == "cuda" else contextlib.nullcontext()
+
+
+class _Stager:
+    """Double-buffered pinned host staging for async H2D copies into a ring."""
+
+    def __init__(self, shape, dtype, device):
+        self.device = device
+        self.cuda = device.type == "cuda"
+        self.bufs = [torch.empty(shape, dtype=dtype, pin_memory=self.cuda) for _ in range(2 if self.cuda else 1)]
+        self.events = [None] * len(self.bufs)
+        self.k = 0
+
+    def stage(self, arr, dst):
+        """Copy numpy/torch ``arr`` into device tensor ``dst`` (same numel)."""
+        if torch.is_tensor(arr) and arr.device == dst.device:
+            dst.view(-1)[: arr.numel()].copy_(arr.reshape(-1).to(dst.dtype), non_blocking=True)
+            return
+        if torch.is_tensor(arr):
+            arr = arr.detach().cpu().numpy()
+        arr = np.asarray(arr)
+        buf = self.bufs[self.k]
+        ev = self.events[self.k]
+        if ev is not None:
+            ev.synchronize()
+        flat = buf.view(-1)
+        n = arr.size
+        np.copyto(flat[:n].numpy(), arr.reshape(-1), casting="unsafe")
+        dst.view(-1)[:n].copy_(flat[:n], non_blocking=self.cuda)
+        if self.cuda:
+            e = torch.cuda.Event()
+            e.record(torch.cuda.current_stream(self.device))
+            self.events[self.k] = e
+        self.k = (self.k + 1) % len(self.bufs)
+
+
+class Program:
+    def __init__(self, model, strategy, global_batch, training, steps_per_execution=1):
+        self.model = model
+        self.strategy = strategy
+        self.world = strategy.num_replicas_in_sync
+        if global_batch % self.world:
+            raise ValueError(f"global batch {global_batch} is not divisible by {self.world} replicas")
+        self.global_batch = global_batch
+        self.B = global_batch // self.world
+        self.S = max(1, int(steps_per_execution)) if training else 1
+        self.stores = model._replica_stores(strategy)
+        self.devices = list(strategy.local_devices)
+        opt = model.optimizer if training else None
+        self.plans = [PG.make_plan(model, st, dev, self.B, global_batch, opt, model.loss)
+                      for st, dev in zip(self.stores, self.devices)]
+        self.comm = strategy.comm if self.world > 1 else None
+        xs = tuple(model.input_shape[1:])
+        self.x_shape = xs
+        self.x_ring = [torch.zeros((self.S, self.B) + xs, dtype=torch.float32, device=d) for d in self.devices]
+        self.y_ring = [torch.zeros((self.S, self.B), dtype=torch.int32, device=d) for d in self.devices]
+        self.x_stage = [_Stager((self.S, self.B) + xs, torch.float32, d) for d in self.devices]
+        self.y_stage = [_Stager((self.S, self.B), torch.int32, d) for d in self.devices]
+        self.graph = None
+        self._graph_key = None
+        cuda = all(d.type == "cuda" for d in self.devices)
+        env = os.environ.get("TDE_GRAPH", "1") != "0"
+        self.use_graph = bool(training and cuda and env and len(self.devices) == 1 and
+                              (self.comm is None or self.comm.capturable))
+        self._comm_warm = False
+
+    @property
+    def plan_kind(self):
+        return self.plans[0].kind
+
+    # ------------------------------------------------------------------ staging
+    def stage(self, per_replica_steps):
+        """per_replica_steps[r] = (x [S,B,...], y [S,B]) for local replica r."""
+        for r, (x, y) in enumerate(per_replica_steps):
+            with _ctx(self.devices[r]):
+                self.x_stage[r].stage(x, self.x_ring[r])
+                self.y_stage[r].stage(y, self.y_ring[r])
+
+    # ------------------------------------------------------------------ training
+    def _steps(self, S, B=None):
+        for s in range(S):
+            for r, plan in enumerate(self.plans):
+                with _ctx(plan.device):
+                    plan.train_step(self.x_ring[r][s], self.y_ring[r][s], B)
+            if self.comm is not None:
+                self.comm.all_reduce_([p.store.g for p in self.plans])
+            for plan in self.plans:
+                with _ctx(plan.device):
+                    plan.apply()
+
+    def _warm_comm(self):
+        if self.comm is not None and not self._comm_warm:
+            scratch = [torch.zeros(64, device=d) for d in self.devices]
+            self.comm.all_reduce_(scratch)
+            for d in self.devices:
+                if d.type == "cuda":
+                    torch.cuda.synchronize(d)
+            self._comm_warm = True
+
+    def _key(self):
+        return (float(self.model.optimizer.learning_rate), self.model.optimizer.kind)
+
+    def capture(self):
+        self._warm_comm()
+        dev = self.devices[0]
+        with torch.cuda.device(dev):
+            torch.cuda.synchronize(dev)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._steps(self.S)
+            torch.cuda.synchronize(dev)
+        self.graph = g
+        self._graph_key = self._key()
+
+    def run(self):
+        if self.use_graph:
+            if self.graph is None or self._graph_key != self._key():
+                self.capture()
+            with torch.cuda.device(self.devices[0]):
+                self.graph.replay()
+        else:
+            self._warm_comm()
+            self._steps(self.S)
+
+    def run_single(self, per_replica, global_actual):
+        """One (possibly partial) step executed eagerly. per_replica[r] = (x[B_r,...], y[B_r])."""
+        self._warm_comm()
+        for r, (x, y) in enumerate(per_replica):
+            with _ctx(self.devices[r]):
+                n = len(y)
+                self.x_stage[r].stage(x, self.x_ring[r][0])
+                self.y_stage[r].stage(y, self.y_ring[r][0])
+        scales = [p.scale for p in self.plans]
+        for p in self.plans:
+            p.scale = 1.0 / float(global_actual)
+        try:
+            for r, plan in enumerate(self.plans):
+                n = len(per_replica[r][1])
+                with _ctx(plan.device):
+                    if n > 0:
+                        plan.train_step(self.x_ring[r][0], self.y_ring[r][0], n)
+            if self.comm is not None:
+                self.comm.all_reduce_([p.store.g for p in self.plans])
+            for plan in self.plans:
+                with _ctx(plan.device):
+                    plan.apply()
+        finally:
+            for p, s in zip(self.plans, scales):
+                p.scale = s
+
+    # ------------------------------------------------------------------ eval / predict
+    def eval_batch(self, per_replica):
+        for r, (x, y) in enumerate(per_replica):
+            n = len(y)
+            if n == 0:
+                continue
+            with _ctx(self.devices[r]):
+                self.x_stage[r].stage(x, self.x_ring[r][0])
+                self.y_stage[r].stage(y, self.y_ring[r][0])
+                self.plans[r].eval_step(self.x_ring[r][0], self.y_ring[r][0], n)
+
+    def predict_batch(self, x):
+        n = len(x)
+        with _ctx(self.devices[0]):
+            self.x_stage[0].stage(x, self.x_ring[0][0])
+            out = self.plans[0].predict(self.x_ring[0][0], n)
+            return out[:n].float().cpu().numpy()
+
+    # ------------------------------------------------------------------ metrics
+    def reset_metrics(self):
+        for p in self.plans:
+            p.reset_metrics()
+
+    def local_metrics(self):
+        acc = None
+        for p in self.plans:
+            m = p.metrics.detach().double().cpu()
+            acc = m if acc is None else acc + m
+        return acc
+
+    def global_metrics(self):
+        """SUM of the metric accumulators over ALL replicas (SyncOnRead SUM, C3/C5)."""
+        if self.comm is None:
+            return self.local_metrics()
+        bufs = [p.metrics.clone() for p in self.plans]
+        self.comm.all_reduce_(bufs)
+        for d in self.devices:
+            if d.type == "cuda":
+                torch.cuda.synchronize(d)
+        return bufs[0].double().cpu()
+
+    def on_weights_loaded(self):
+        for p in self.plans:
+            with _ctx(p.device):
+                p.on_weights_loaded()
+
+    def sync(self):
+        for d in self.devices:
+            if d.type == "cuda":
+                torch.cuda.synchronize(d)

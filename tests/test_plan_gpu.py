@@ -1,0 +1,77 @@
+"""T1/T4: the fused HIP training plan vs the torch reference plan, step by step,
+and hipGraph multi-step execution vs eager execution."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(n, seed=0):
+    rng = np.random.default_rng(seed)
+    return rng.random((n, 28, 28, 1), dtype=np.float32), rng.integers(0, 10, size=n)
+
+
+def _model(tde, lr=0.05, spe=1):
+    m = tde.zoo.mnist_cnn()
+    m.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True), optimizer=tde.optimizers.SGD(lr),
+              metrics=["accuracy"], steps_per_execution=spe)
+    return m
+
+
+def test_fused_plan_matches_reference(monkeypatch):
+    import tensorflow_distributed_example_amd as tde
+    x, y = _data(64 * 6)
+    tde.backend.set_random_seed(7)
+    mf = _model(tde)
+    w0 = mf.get_weights()
+    tde.backend.clear_session()
+    mr = _model(tde)
+    mr.set_weights(w0)
+    hf = mf.fit(x, y, batch_size=64, epochs=1, shuffle=False, verbose=0)
+    assert mf._program("train", 64).plan_kind == "fused_convnet"
+    monkeypatch.setenv("TDE_EXECUTOR", "reference")
+    hr = mr.fit(x, y, batch_size=64, epochs=1, shuffle=False, verbose=0)
+    assert mr._program("train", 64).plan_kind == "reference"
+    for a, b in zip(mf.get_weights(), mr.get_weights()):
+        scale = np.abs(b).max() + 1e-6
+        assert np.abs(a - b).max() / scale < 2e-2, np.abs(a - b).max()
+    assert abs(hf.history["loss"][0] - hr.history["loss"][0]) < 2e-2
+    assert abs(hf.history["accuracy"][0] - hr.history["accuracy"][0]) < 0.05
+
+
+def test_graph_multi_step_matches_eager(monkeypatch):
+    import tensorflow_distributed_example_amd as tde
+    x, y = _data(64 * 8, 1)
+    tde.backend.set_random_seed(3)
+    mg = _model(tde, spe=4)
+    w0 = mg.get_weights()
+    tde.backend.clear_session()
+    monkeypatch.setenv("TDE_GRAPH", "0")
+    me = _model(tde, spe=1)
+    me.set_weights(w0)
+    mg.fit(x, y, batch_size=64, epochs=1, shuffle=False, verbose=0)
+    assert mg._program("train", 64).use_graph
+    me.fit(x, y, batch_size=64, epochs=1, shuffle=False, verbose=0)
+    for a, b in zip(mg.get_weights(), me.get_weights()):
+        assert np.allclose(a, b, atol=1e-5, rtol=1e-4)
+
+
+def test_loss_decreases_and_eval_predict():
+    import tensorflow_distributed_example_amd as tde
+    (xt, yt), (xe, ye) = tde.data.mnist.load_data()
+    xt = (xt[:8192] / 255.0).astype(np.float32)[..., None]
+    yt = yt[:8192]
+    m = _model(tde, lr=0.05, spe=8)
+    ds = tde.data.Dataset.from_tensor_slices((xt, yt)).shuffle(1000).repeat().batch(128)
+    h = m.fit(ds, epochs=3, steps_per_epoch=32, verbose=0)
+    assert h.history["loss"][-1] < h.history["loss"][0]
+    xe = (xe[:1000] / 255.0).astype(np.float32)[..., None]
+    loss, acc = m.evaluate(xe, ye[:1000], batch_size=250, verbose=0)
+    assert acc > 0.5
+    p = m.predict(xe[:37], batch_size=16)
+    assert p.shape == (37, 10)
+    torch_logits = m(xe[:37]).cpu().numpy()
+    assert np.allclose(p, torch_logits, atol=5e-2, rtol=5e-2)
