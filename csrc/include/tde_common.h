@@ -53,6 +53,25 @@ __device__ __forceinline__ bf16x8 load_frag(const bf16* p, int k0, int K, bool r
   return r;
 }
 
+// Workgroup barrier that orders LDS only.  __syncthreads() also waits for every
+// outstanding global store/atomic of the wave (vmcnt(0)); at MNIST sizes those
+// scattered stores cost microseconds, and no wave reads them back in-kernel, so
+// the barriers between LDS producer/consumer phases use lgkmcnt(0) + s_barrier.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Diagnostic phase stamps (wall clock, 100 MHz): thread 0 of each workgroup
+// records stamps[blockIdx * kMaxStamps + slot]. Only used when a kernel is given
+// a non-null stamp buffer (profiling builds/runs); never feeds any output.
+constexpr int kMaxStamps = 8;
+__device__ __forceinline__ void stamp(long long* st, int slot) {
+  if (st && threadIdx.x == 0) {
+    const int blk = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    st[(size_t)blk * kMaxStamps + slot] = (long long)__builtin_amdgcn_s_memrealtime();
+  }
+}
+
 }  // namespace tde
 
 #define TDE_LAUNCH_CHECK() \

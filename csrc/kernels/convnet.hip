@@ -1,0 +1,404 @@
+// Fused forward and backward of the DWK/TF2M small CNN trunk
+//   Conv2D(32,3x3,VALID,bias,ReLU) · MaxPooling2D(2) · Flatten · Dense(64)  (matmul part)
+// (distributed_with_keras.py:34-37, tf2_mnist_distributed.py:67-70;
+//  SURVEY.md §2.5 A1-A4 forward, A10-A13 backward).
+//
+// Design (latency-bound regime; measured with in-kernel s_memrealtime stamps):
+//  * 1024-thread workgroups (16 waves): enough waves per CU to hide load latency;
+//  * every global operand is loaded ONCE per workgroup with coalesced 16-byte
+//    loads issued in the prologue and staged in LDS (rows padded so the
+//    16x16x32 MFMA fragment reads are bank-conflict free);
+//  * LDS-only barriers (lds_barrier): the scattered global stores of a phase
+//    drain in the background instead of stalling the barrier;
+//  * the pool-argmax side output is stored lane-contiguous ([P][C/8][ldA] u64).
+//
+// Forward: a workgroup owns PPW=4 pooled positions x 64 images.
+//   phase 1 (VALU; wave = (position, 8-channel group), lane = image): 3x3 conv of
+//           the 2x2 pool window from a 4x4 register patch, bias, ReLU, max ->
+//           bf16 pooled tile in LDS, argmax bytes, P^T (for the weight grad);
+//   phase 2 (MFMA; wave = 16x16 output tile): tile . W1^T rows of the 4 positions
+//           -> split-K partial of the Dense pre-activation, f32 atomics into hpre.
+// Backward, per workgroup of 4 positions, looping 64-image chunks:
+//   dP   = G . W1[p*32:(p+1)*32]^T      (MFMA; Dense input-gradient, in-kernel)
+//   dW1[p*32:(p+1)*32] = P^T . G        (MFMA; Dense weight-gradient rows, stored)
+//   route dP through the pool argmax and ReLU mask and reduce over (image, window
+//   slot) with MFMA: dWc[tap][c] = sum_k X[tap][k] D[k][c], k=(pos,b,q) — the
+//   bias gradient is the extra all-ones tap row.
+#include "tde_common.h"
+
+namespace tde {
+
+constexpr int PPW = 4;   // pooled positions per workgroup
+constexpr int NW = 16;   // waves per workgroup
+constexpr int CC = 32;   // conv filters
+constexpr int HD = 64;   // Dense units
+constexpr int PSTR = 40; // padded LDS row stride (bf16) of the pooled tile
+constexpr int RSTR = 72; // padded LDS row stride (bf16) of 64-wide operand rows
+
+struct ConvNetFwdArgs {
+  const float* x; const float* wc; const float* bc;
+  const bf16* W1c; int ldw1c;       // [HD][K] bf16 (W1^T shadow)
+  float* hpre;                      // [B][HD] f32, += (pre-zeroed by the previous head launch)
+  bf16* Pt; int ldPt;               // [K][ldPt] (nullable)
+  uint64_t* amax; int lda;          // [P][CC/8][lda] (nullable)
+  int B, H, W;
+  long long* stamps;
+};
+
+__global__ __launch_bounds__(1024) void convnet_fwd_kernel(ConvNetFwdArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 Ps[PPW * 64 * PSTR];
+  stamp(a.stamps, 0);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, fk = (lane >> 4) * 8;
+  const int W = a.W, H = a.H;
+  const int Wp = (W - 2) / 2, Hp = (H - 2) / 2, P = Hp * Wp;
+  const int p0 = blockIdx.x * PPW;
+  const int b0 = blockIdx.y * 64;
+  const int b = b0 + lane;
+  const bool bok = b < a.B;
+  const int pp = wave >> 2, cg = wave & 3, c0 = cg * 8;
+  const int p = p0 + pp;
+  const bool pok = p < P;
+
+  // ---- prologue: all global loads, independent, issued back to back
+  float patch[16];
+  if (bok && pok) {
+    const int py = p / Wp, px = p - py * Wp;
+    const float* xb = a.x + (size_t)b * H * W + (2 * py) * W + 2 * px;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float2* row = reinterpret_cast<const float2*>(xb + r * W);
+      const float2 u = row[0], v = row[1];
+      patch[r * 4 + 0] = u.x; patch[r * 4 + 1] = u.y; patch[r * 4 + 2] = v.x; patch[r * 4 + 3] = v.y;
+    }
+  }
+  float4 wlo[9], whi[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    wlo[t] = *reinterpret_cast<const float4*>(a.wc + t * CC + c0);
+    whi[t] = *reinterpret_cast<const float4*>(a.wc + t * CC + c0 + 4);
+  }
+  const float4 blo = *reinterpret_cast<const float4*>(a.bc + c0);
+  const float4 bhi = *reinterpret_cast<const float4*>(a.bc + c0 + 4);
+  // W1^T fragments of this wave's output tile: mt = wave>>2 (image rows), nt = wave&3 (units)
+  const int mt = wave >> 2, nt = wave & 3;
+  bf16x8 wfr[PPW];
+#pragma unroll
+  for (int ks = 0; ks < PPW; ++ks) {
+    const int kp = p0 + ks;
+    wfr[ks] = kp < P ? *reinterpret_cast<const bf16x8*>(a.W1c + (size_t)(nt * 16 + fr) * a.ldw1c + (size_t)kp * CC + fk)
+                     : bf16x8{};
+  }
+  stamp(a.stamps, 1);
+
+  // ---- phase 1: conv + bias + ReLU + 2x2 max-pool for 8 channels
+  bf16x8 outv;
+  if (bok && pok) {
+    uint64_t packed = 0;
+#pragma unroll
+    for (int cc = 0; cc < 8; ++cc) {
+      float wt[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const float4 q = cc < 4 ? wlo[t] : whi[t];
+        const int k = cc & 3;
+        wt[t] = k == 0 ? q.x : (k == 1 ? q.y : (k == 2 ? q.z : q.w));
+      }
+      const float4 bq = cc < 4 ? blo : bhi;
+      const int kb = cc & 3;
+      const float bcv = kb == 0 ? bq.x : (kb == 1 ? bq.y : (kb == 2 ? bq.z : bq.w));
+      float best = -3.0e38f;
+      int bi = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int dy = q >> 1, dx = q & 1;
+        float z = bcv;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) z = fmaf(patch[(dy + ky) * 4 + dx + kx], wt[ky * 3 + kx], z);
+        if (z > best) { best = z; bi = q; }
+      }
+      outv[cc] = f2bf(fmaxf(best, 0.f));
+      packed |= (uint64_t)(best > 0.f ? (unsigned)bi : 0xFFu) << (8 * cc);
+    }
+    if (a.amax) a.amax[((size_t)p * (CC / 8) + cg) * a.lda + b] = packed;
+    if (a.Pt) {
+#pragma unroll
+      for (int cc = 0; cc < 8; ++cc) a.Pt[(size_t)(p * CC + c0 + cc) * a.ldPt + b] = outv[cc];
+    }
+  } else {
+#pragma unroll
+    for (int cc = 0; cc < 8; ++cc) outv[cc] = f2bf(0.f);
+    if (pok && a.Pt && b < a.ldPt) {
+#pragma unroll
+      for (int cc = 0; cc < 8; ++cc) a.Pt[(size_t)(p * CC + c0 + cc) * a.ldPt + b] = outv[cc];
+    }
+  }
+  *reinterpret_cast<bf16x8*>(Ps + ((size_t)pp * 64 + lane) * PSTR + c0) = outv;
+  stamp(a.stamps, 2);
+  lds_barrier();
+  stamp(a.stamps, 3);
+
+  // ---- phase 2: hpre[64 x 64] += Ps(64 x 4*32) . W1^T(4*32 x 64); one 16x16 tile per wave
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < PPW; ++ks) {
+    if (p0 + ks < P) {
+      const bf16x8 av = *reinterpret_cast<const bf16x8*>(Ps + ((size_t)ks * 64 + mt * 16 + fr) * PSTR + fk);
+      acc = mfma16(av, wfr[ks], acc);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = b0 + mt * 16 + (lane >> 4) * 4 + r;
+    if (row < a.B) atomicAdd(a.hpre + (size_t)row * HD + nt * 16 + fr, acc[r]);
+  }
+  stamp(a.stamps, 4);
+}
+
+struct ConvNetBwdArgs {
+  const float* x; const uint64_t* amax; int lda;
+  const bf16* G; int ldg;            // [B][HD] bf16 (dHpre)
+  const bf16* Gt; int ldgt;          // [HD][ldgt] bf16
+  const bf16* W1r; int ldw1r;        // [K][HD] bf16 (row-major shadow)
+  const bf16* Pt; int ldPt;          // [K][ldPt] bf16
+  float* dW1;                        // [K][HD] f32 (stored)
+  float* dwc; float* dbc;            // [9][CC], [CC] (atomic +=)
+  int B, H, W;
+  long long* stamps;
+};
+
+// LDS carve (bytes)
+constexpr int kG = 0;                                   // bf16 [64][RSTR]
+constexpr int kW1 = kG + 64 * RSTR * 2;                 // bf16 [128][RSTR]
+constexpr int kPt = kW1 + 128 * RSTR * 2;               // bf16 [128][RSTR]
+constexpr int kGt = kPt + 128 * RSTR * 2;               // bf16 [64][RSTR]
+constexpr int kXs = kGt + 64 * RSTR * 2;                // f32  [PPW][64][16]
+constexpr int kAm = kXs + PPW * 64 * 16 * 4;            // u8   [PPW][64][CC]
+constexpr int kDp = kAm + PPW * 64 * CC;                // f32  [PPW][64][CC]  (reused as red [NW][16][CC])
+constexpr int kBwdLds = kDp + PPW * 64 * CC * 4;
+
+__global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16* Gs = reinterpret_cast<bf16*>(smem + kG);
+  bf16* W1s = reinterpret_cast<bf16*>(smem + kW1);
+  bf16* Pts = reinterpret_cast<bf16*>(smem + kPt);
+  bf16* Gts = reinterpret_cast<bf16*>(smem + kGt);
+  float* xs = reinterpret_cast<float*>(smem + kXs);
+  uint8_t* am = smem + kAm;
+  float* dps = reinterpret_cast<float*>(smem + kDp);
+  float* red = dps;
+  stamp(a.stamps, 0);
+  const int W = a.W, H = a.H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+  const int fr = lane & 15, fq = lane >> 4, fk = fq * 8;
+  const int Wp = (W - 2) / 2, Hp = (H - 2) / 2, P = Hp * Wp;
+  const int p0 = blockIdx.x * PPW;
+  const int nrow = min(PPW, P - p0) * CC;  // valid W1/Pt rows of this workgroup
+
+  f32x4 accw[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  f32x4 accr[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+
+  // W1 rows of the 4 positions: loaded once (independent of the image chunk)
+  {
+    const int r = tid >> 3, c = (tid & 7) * 8;  // 128 rows x 8 chunks of 16 B
+    bf16x8 v = r < nrow ? *reinterpret_cast<const bf16x8*>(a.W1r + (size_t)(p0 * CC + r) * a.ldw1r + c) : bf16x8{};
+    *reinterpret_cast<bf16x8*>(W1s + r * RSTR + c) = v;
+  }
+
+  for (int b0 = 0; b0 < a.B; b0 += 64) {
+    const int nb = min(64, a.B - b0);
+    // ---- prologue: coalesced loads of this chunk's operands
+    bf16x8 gv = {}, gtv = {}, ptv;
+    if (tid < 512) {
+      const int r = tid >> 3, c = (tid & 7) * 8;
+      if (r < nb) gv = *reinterpret_cast<const bf16x8*>(a.G + (size_t)(b0 + r) * a.ldg + c);
+      // Gt rows: unit r, images b0+c .. +8 (zero past B)
+      gtv = load_frag(a.Gt + (size_t)r * a.ldgt + b0 + c, b0 + c, a.B, true);
+    }
+    {
+      const int r = tid >> 3, c = (tid & 7) * 8;
+      ptv = r < nrow ? load_frag(a.Pt + (size_t)(p0 * CC + r) * a.ldPt + b0 + c, b0 + c, a.B, true) : bf16x8{};
+    }
+    float4 xv = {0.f, 0.f, 0.f, 0.f};
+    {
+      const int pp = tid >> 8, bl = (tid >> 2) & 63, r = tid & 3;
+      const int p = p0 + pp, b = b0 + bl;
+      if (p < P && b < a.B) {
+        const int py = p / Wp, px = p - py * Wp;
+        const float2* row = reinterpret_cast<const float2*>(a.x + (size_t)b * H * W + (2 * py + r) * W + 2 * px);
+        const float2 u = row[0], t = row[1];
+        xv = float4{u.x, u.y, t.x, t.y};
+      }
+    }
+    uint64_t amv = ~0ull;
+    {
+      const int pp = tid >> 8, cg = (tid >> 6) & 3, bl = tid & 63;
+      const int p = p0 + pp, b = b0 + bl;
+      if (p < P && b < a.B) amv = a.amax[((size_t)p * (CC / 8) + cg) * a.lda + b];
+    }
+    stamp(a.stamps, 1);
+    if (tid < 512) {
+      const int r = tid >> 3, c = (tid & 7) * 8;
+      *reinterpret_cast<bf16x8*>(Gs + r * RSTR + c) = gv;
+      *reinterpret_cast<bf16x8*>(Gts + r * RSTR + c) = gtv;
+    }
+    {
+      const int r = tid >> 3, c = (tid & 7) * 8;
+      *reinterpret_cast<bf16x8*>(Pts + r * RSTR + c) = ptv;
+    }
+    {
+      const int pp = tid >> 8, bl = (tid >> 2) & 63, r = tid & 3;
+      *reinterpret_cast<float4*>(xs + ((size_t)pp * 64 + bl) * 16 + r * 4) = xv;
+    }
+    {
+      const int pp = tid >> 8, cg = (tid >> 6) & 3, bl = tid & 63;
+      *reinterpret_cast<uint64_t*>(am + ((size_t)pp * 64 + bl) * CC + cg * 8) = amv;
+    }
+    lds_barrier();
+    stamp(a.stamps, 2);
+
+    // ---- dP[pp][b][c] = G[b] . W1[pp*32 + c]  (wave = position x 16 images)
+    {
+      const int pp = wave >> 2, mt = wave & 3;
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const bf16x8 av = *reinterpret_cast<const bf16x8*>(Gs + (mt * 16 + fr) * RSTR + ks * 32 + fk);
+          const bf16x8 bv = *reinterpret_cast<const bf16x8*>(W1s + (pp * CC + ct * 16 + fr) * RSTR + ks * 32 + fk);
+          acc = mfma16(av, bv, acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dps[((size_t)pp * 64 + mt * 16 + fq * 4 + r) * CC + ct * 16 + fr] = acc[r];
+      }
+    }
+    // ---- dW1 rows += P^T . G   (32 tiles of 16x16: t = wave, wave+16)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int t = wave + 16 * i;
+      const int nt = t & 3, rt = t >> 2;  // rt: 16-row block (of 8) within the 128 rows
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 av = *reinterpret_cast<const bf16x8*>(Pts + (rt * 16 + fr) * RSTR + ks * 32 + fk);
+        const bf16x8 bv = *reinterpret_cast<const bf16x8*>(Gts + (nt * 16 + fr) * RSTR + ks * 32 + fk);
+        accw[i] = mfma16(av, bv, accw[i]);
+      }
+    }
+    lds_barrier();
+    stamp(a.stamps, 3);
+
+    // ---- routing MFMA: k = ((pp*64 + b)*4 + q); 32 k-steps, wave takes ks = wave, wave+16
+    {
+      const int tap = fr, ky = tap / 3, kx = tap - ky * 3;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int ks = wave + 16 * h2;
+        const int kb = ks * 32 + fk;
+        const int pp = kb >> 8, bl = (kb >> 2) & 63;
+        bf16x8 av;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int bb = bl + (j >> 2), q = j & 3, qy = q >> 1, qx = q & 1;
+          float v;
+          if (tap < 9) v = xs[((size_t)pp * 64 + bb) * 16 + (qy + ky) * 4 + qx + kx];
+          else v = (tap == 9) ? 1.f : 0.f;
+          av[j] = f2bf(v);
+        }
+#pragma unroll
+        for (int ct = 0; ct < 2; ++ct) {
+          const int c = ct * 16 + fr;
+          bf16x8 bv;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const size_t idx = ((size_t)pp * 64 + bl + h) * CC + c;
+            const unsigned id = am[idx];
+            const float dv = dps[idx];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) bv[h * 4 + q] = f2bf(id == (unsigned)q ? dv : 0.f);
+          }
+          accr[ct] = mfma16(av, bv, accr[ct]);
+        }
+      }
+    }
+    lds_barrier();
+  }
+  stamp(a.stamps, 4);
+
+  // ---- store dW1 tiles (each row of dW1 belongs to exactly one workgroup)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int t = wave + 16 * i;
+    const int nt = t & 3, rt = t >> 2;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = rt * 16 + fq * 4 + r;
+      if (row < nrow) a.dW1[(size_t)(p0 * CC + row) * HD + nt * 16 + fr] = accw[i][r];
+    }
+  }
+  // ---- reduce routing accumulators over the 16 waves, then 10*CC atomics
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[((size_t)wave * 16 + fq * 4 + r) * CC + ct * 16 + fr] = accr[ct][r];
+  lds_barrier();
+  if (tid < 10 * CC) {
+    const int tap = tid / CC, c = tid - tap * CC;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) s += red[((size_t)w * 16 + tap) * CC + c];
+    if (tap < 9) atomicAdd(a.dwc + tap * CC + c, s);
+    else if (a.dbc) atomicAdd(a.dbc + c, s);
+  }
+  stamp(a.stamps, 5);
+}
+
+}  // namespace tde
+
+using namespace tde;
+
+// Specialised for Conv2D(32, 3x3, valid) on 1-channel input + MaxPool(2) + Dense(64).
+TDE_API int tde_convnet_fwd(const float* x, const float* wc, const float* bc, const void* W1c, int ldw1c,
+                            float* hpre, void* Pt, int ldPt, void* amax, int lda, int B, int H, int W,
+                            long long* stamps, hipStream_t stream) {
+  if ((W & 1) || (ldw1c & 7) || (Pt && (ldPt & 7)) || (amax && lda < B)) return -1;
+  if (((uintptr_t)wc | (uintptr_t)bc) & 15) return -2;
+  const int P = ((H - 2) / 2) * ((W - 2) / 2);
+  int by = (B + 63) / 64;
+  if (Pt) {
+    const int byp = (ldPt + 63) / 64;
+    if (byp > by) by = byp;
+  }
+  ConvNetFwdArgs a{x, wc, bc, (const bf16*)W1c, ldw1c, hpre, (bf16*)Pt, ldPt, (uint64_t*)amax, lda, B, H, W, stamps};
+  dim3 grid((P + PPW - 1) / PPW, by);
+  convnet_fwd_kernel<<<grid, 1024, 0, stream>>>(a);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+TDE_API int tde_convnet_bwd(const float* x, const void* amax, int lda, const void* G, int ldg, const void* Gt,
+                            int ldgt, const void* W1r, int ldw1r, const void* Pt, int ldPt, float* dW1, float* dwc,
+                            float* dbc, int B, int H, int W, long long* stamps, hipStream_t stream) {
+  if ((ldg & 7) || (ldgt & 7) || (ldw1r & 7) || (ldPt & 7) || ldgt < B || ldPt < B || lda < B) return -1;
+  const int P = ((H - 2) / 2) * ((W - 2) / 2);
+  ConvNetBwdArgs a{x, (const uint64_t*)amax, lda, (const bf16*)G, ldg, (const bf16*)Gt, ldgt, (const bf16*)W1r,
+                   ldw1r, (const bf16*)Pt, ldPt, dW1, dwc, dbc, B, H, W, stamps};
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)convnet_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kBwdLds);
+    attr_set = true;
+  }
+  convnet_bwd_kernel<<<dim3((P + PPW - 1) / PPW), 1024, kBwdLds, stream>>>(a);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+// Empty kernel: measures the launch/boundary floor of the device (microbenchmarks).
+__global__ void noop_kernel() {}
+TDE_API int tde_noop(int blocks, int threads, hipStream_t stream) {
+  noop_kernel<<<blocks, threads, 0, stream>>>();
+  TDE_LAUNCH_CHECK();
+  return 0;
+}

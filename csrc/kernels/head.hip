@@ -32,9 +32,12 @@ struct HeadArgs {
   float* metrics;                     // += {loss_sum, correct, count}
   float* probs; int probs_are_logits; // [B, C] out (nullable)
   float* row_loss;                    // [B] out (nullable)
+  float* zero_hin;                    // if set (== hin): rows consumed are zeroed for the next split-K accumulation
+  long long* iterations;              // if set: block 0 advances the step counter (Keras optimizer.iterations)
+  long long* stamps;                  // diagnostic phase stamps (nullable)
 };
 
-constexpr int kHeadRows = 16;
+constexpr int kHeadRows = 8;
 
 __global__ __launch_bounds__(256) void head_xent_kernel(HeadArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -46,7 +49,11 @@ __global__ __launch_bounds__(256) void head_xent_kernel(HeadArgs a) {
   float* dhs = dls + R * C;       // [R][H]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r0 = blockIdx.x * R;
-
+  stamp(a.stamps, 0);
+  if (a.iterations && blockIdx.x == 0 && tid == 0) atomicAdd((unsigned long long*)a.iterations, 1ull);
+  // Prefetch everything this block needs from global memory up front.
+  int label_pref = 0;
+  if (tid < R && r0 + tid < a.B) label_pref = a.labels[r0 + tid];
   for (int i = tid; i < R * H; i += 256) {
     const int r = i / H, j = i - r * H, row = r0 + r;
     float v = 0.f;
@@ -58,16 +65,36 @@ __global__ __launch_bounds__(256) void head_xent_kernel(HeadArgs a) {
     hs[i] = v;
   }
   for (int i = tid; i < H * C; i += 256) w2s[i] = a.W2[i];
-  __syncthreads();
+  float b2v = 0.f;
+  if (tid < C && a.b2) b2v = a.b2[tid];
+  int* labs = reinterpret_cast<int*>(dhs);  // scratch until dh is computed
+  if (tid < R) labs[tid] = label_pref;
+  __shared__ float b2sh[64];
+  if (tid < C) b2sh[tid] = b2v;
+  lds_barrier();
+  stamp(a.stamps, 1);
+  if (a.zero_hin) {
+    for (int i = tid; i < R * H; i += 256) {
+      const int r = i / H, j = i - r * H, row = r0 + r;
+      if (row < a.B) a.zero_hin[(size_t)row * a.ldh + j] = 0.f;
+    }
+  }
 
   for (int o = tid; o < R * C; o += 256) {
     const int r = o / C, c = o - r * C;
-    float s = a.b2 ? a.b2[c] : 0.f;
+    float s0 = b2sh[c], s1 = 0.f, s2 = 0.f, s3 = 0.f;
     const float* hr = hs + r * H;
-    for (int j = 0; j < H; ++j) s = fmaf(hr[j], w2s[j * C + c], s);
-    lg[o] = s;
+    int j = 0;
+    for (; j + 4 <= H; j += 4) {
+      s0 = fmaf(hr[j], w2s[j * C + c], s0);
+      s1 = fmaf(hr[j + 1], w2s[(j + 1) * C + c], s1);
+      s2 = fmaf(hr[j + 2], w2s[(j + 2) * C + c], s2);
+      s3 = fmaf(hr[j + 3], w2s[(j + 3) * C + c], s3);
+    }
+    for (; j < H; ++j) s0 = fmaf(hr[j], w2s[j * C + c], s0);
+    lg[o] = (s0 + s1) + (s2 + s3);
   }
-  __syncthreads();
+  lds_barrier();
 
   float loss_acc = 0.f, corr_acc = 0.f, cnt_acc = 0.f;
   for (int r = wave; r < R; r += 4) {
@@ -78,7 +105,7 @@ __global__ __launch_bounds__(256) void head_xent_kernel(HeadArgs a) {
     const float e = lane < C ? __expf(v - m) : 0.f;
     const float s = wave_sum(e);
     const float p = e / s;
-    const int label = valid ? a.labels[row] : 0;
+    const int label = valid ? labs[r] : 0;
     const float lse = __logf(s) + m;
     const unsigned long long mask = __ballot(lane < C && v == m);
     const int am = __ffsll((long long)mask) - 1;
@@ -93,20 +120,21 @@ __global__ __launch_bounds__(256) void head_xent_kernel(HeadArgs a) {
     }
     if (lane < C) dls[r * C + lane] = valid ? (p - (lane == label ? 1.f : 0.f)) * a.scale : 0.f;
   }
-  if (a.metrics && lane == 0) {
+  if (a.metrics && lane == 0 && cnt_acc > 0.f) {
     atomicAdd(a.metrics + 0, loss_acc);
     atomicAdd(a.metrics + 1, corr_acc);
     atomicAdd(a.metrics + 2, cnt_acc);
   }
+  stamp(a.stamps, 2);
   if (!a.compute_grad) return;
-  __syncthreads();
+  lds_barrier();
 
   // dW2 = h^T . dl ; db2 = sum dl
   if (a.dW2) {
     for (int o = tid; o < H * C; o += 256) {
       const int j = o / C, c = o - j * C;
       float s = 0.f;
-#pragma unroll 4
+#pragma unroll
       for (int r = 0; r < R; ++r) s = fmaf(hs[r * H + j], dls[r * C + c], s);
       atomicAdd(a.dW2 + o, s);
     }
@@ -130,7 +158,7 @@ __global__ __launch_bounds__(256) void head_xent_kernel(HeadArgs a) {
       if (a.Gf) a.Gf[(size_t)row * a.ldgf + j] = s;
     }
   }
-  __syncthreads();
+  lds_barrier();
   if (a.Gt) {
     // Transposed copy: consecutive threads walk rows -> coalesced along B.
     for (int o = tid; o < R * H; o += 256) {
@@ -145,6 +173,7 @@ __global__ __launch_bounds__(256) void head_xent_kernel(HeadArgs a) {
       atomicAdd(a.dpre_bias + j, s);
     }
   }
+  stamp(a.stamps, 3);
 }
 
 }  // namespace tde
@@ -156,11 +185,12 @@ TDE_API int tde_head_xent(const float* hin, int ldh, const float* pre_bias, int 
                           int C, float scale, int compute_grad, float* dW2, float* db2,
                           float* dpre_bias, void* G, int ldg, void* Gt, int ldgt, float* Gf,
                           int ldgf, float* metrics, float* probs, int probs_are_logits,
-                          float* row_loss, hipStream_t stream) {
+                          float* row_loss, int zero_hin, long long* iterations, long long* stamps,
+                          hipStream_t stream) {
   if (C > 64 || H * C > 16384 || H > 2048) return -1;
   HeadArgs a{hin, ldh, pre_bias, pre_relu, W2, b2, labels, B, H, C, scale, compute_grad,
              dW2, db2, dpre_bias, (bf16*)G, ldg, (bf16*)Gt, ldgt, Gf, ldgf, metrics, probs,
-             probs_are_logits, row_loss};
+             probs_are_logits, row_loss, zero_hin ? const_cast<float*>(hin) : nullptr, iterations, stamps};
   int rows = B;
   if (Gt && ldgt > rows) rows = ldgt;
   int grid = (rows + kHeadRows - 1) / kHeadRows;

@@ -5,11 +5,15 @@
 // tf2_mnist_distributed.py:137).
 //
 // The same pass (a) zeroes the gradient buffer for the next step's atomic /
-// split-K accumulation, (b) refreshes the bf16 compute copies ("shadows") of
+// split-K accumulation and (b) refreshes the bf16 compute copies ("shadows") of
 // the weights in the layouts the MFMA kernels read — row-major and, through an
-// LDS 64x64 transpose, column-major — and (c) advances the device-resident
-// `iterations` counter (Keras optimizer.iterations / Estimator global_step),
-// so a captured hipGraph replays whole training steps with no host work.
+// LDS 64x64 transpose, column-major.  The step counter (`iterations`, Keras
+// optimizer.iterations / Estimator global_step) lives on the device and is
+// advanced by the step's loss kernel before this launch, so Adam's bias
+// correction reads t = iterations with no host round trip and no in-kernel
+// cross-workgroup protocol.
+//
+// Vectorised: float4 loads/stores everywhere (segments are 256-byte aligned).
 #include "tde_common.h"
 
 namespace tde {
@@ -26,8 +30,7 @@ struct OptArgs {
   bf16* shadow;
   const OptSeg* segs;
   const int4* table;        // per block: {seg, kind(0=1d,1=tile), a, b}
-  long long* iterations;
-  unsigned* done;
+  const long long* iterations;
   int kind;                 // 0 sgd, 1 momentum, 2 nesterov, 3 adam
   float lr, mom, b1, b2, eps, grad_scale;
   int zero_grad;
@@ -36,77 +39,114 @@ struct OptArgs {
 
 constexpr int kChunk = 2048;
 
-__device__ __forceinline__ float opt_update(const OptArgs& a, size_t i, float t_b1, float t_b2,
-                                            float lr) {
-  float g = a.g[i] * a.grad_scale;
-  if (a.zero_grad) a.g[i] = 0.f;
-  float w = a.w[i];
-  if (a.kind == 0) {
-    w -= lr * g;
-  } else if (a.kind == 1 || a.kind == 2) {
-    float v = a.mom * a.m[i] - lr * g;  // Keras: v = m*v - lr*g ; w += v
-    a.m[i] = v;
-    w = (a.kind == 2) ? w + a.mom * v - lr * g : w + v;
-  } else {
-    float m = a.b1 * a.m[i] + (1.f - a.b1) * g;
-    float v = a.b2 * a.v[i] + (1.f - a.b2) * g * g;
-    a.m[i] = m;
-    a.v[i] = v;
-    const float lr_t = lr * sqrtf(1.f - t_b2) / (1.f - t_b1);
-    w -= lr_t * m / (sqrtf(v) + a.eps);
+struct Hyper {
+  float lr, lr_t;
+};
+
+__device__ __forceinline__ float upd1(const OptArgs& a, float w, float g, float& m, float& v, const Hyper& h) {
+  g *= a.grad_scale;
+  if (a.kind == 0) return w - h.lr * g;
+  if (a.kind == 1 || a.kind == 2) {
+    const float nv = a.mom * m - h.lr * g;  // Keras: v = m*v - lr*g ; w += v
+    m = nv;
+    return a.kind == 2 ? w + a.mom * nv - h.lr * g : w + nv;
   }
+  m = a.b1 * m + (1.f - a.b1) * g;
+  v = a.b2 * v + (1.f - a.b2) * g * g;
+  return w - h.lr_t * m / (sqrtf(v) + a.eps);
+}
+
+// Update 4 consecutive elements at flat index i (16-byte aligned).
+__device__ __forceinline__ float4 upd4(const OptArgs& a, size_t i, const Hyper& h) {
+  float4 w = *reinterpret_cast<float4*>(a.w + i);
+  const float4 g = *reinterpret_cast<float4*>(a.g + i);
+  float4 m = {0.f, 0.f, 0.f, 0.f}, v = {0.f, 0.f, 0.f, 0.f};
+  if (a.kind != 0) m = *reinterpret_cast<float4*>(a.m + i);
+  if (a.kind == 3) v = *reinterpret_cast<float4*>(a.v + i);
+  w.x = upd1(a, w.x, g.x, m.x, v.x, h);
+  w.y = upd1(a, w.y, g.y, m.y, v.y, h);
+  w.z = upd1(a, w.z, g.z, m.z, v.z, h);
+  w.w = upd1(a, w.w, g.w, m.w, v.w, h);
+  *reinterpret_cast<float4*>(a.w + i) = w;
+  if (a.zero_grad) *reinterpret_cast<float4*>(a.g + i) = float4{0.f, 0.f, 0.f, 0.f};
+  if (a.kind != 0) *reinterpret_cast<float4*>(a.m + i) = m;
+  if (a.kind == 3) *reinterpret_cast<float4*>(a.v + i) = v;
+  return w;
+}
+
+__device__ __forceinline__ float upds(const OptArgs& a, size_t i, const Hyper& h) {
+  float m = a.kind != 0 ? a.m[i] : 0.f, v = a.kind == 3 ? a.v[i] : 0.f;
+  const float w = upd1(a, a.w[i], a.g[i], m, v, h);
   a.w[i] = w;
+  if (a.zero_grad) a.g[i] = 0.f;
+  if (a.kind != 0) a.m[i] = m;
+  if (a.kind == 3) a.v[i] = v;
   return w;
 }
 
 __global__ __launch_bounds__(256) void optim_apply_kernel(OptArgs a) {
-  __shared__ bf16 tile[64][66];
+  __shared__ bf16 tile[64][72];
   const int4 ent = a.table[blockIdx.x];
   const OptSeg s = a.segs[ent.x];
-  const long long it = __hip_atomic_load(a.iterations, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const float t = (float)(it + 1);
-  const float t_b1 = a.kind == 3 ? __powf(a.b1, t) : 0.f;
-  const float t_b2 = a.kind == 3 ? __powf(a.b2, t) : 0.f;
-  const float lr = a.lr_ptr ? *a.lr_ptr : a.lr;
+  Hyper h;
+  h.lr = a.lr_ptr ? *a.lr_ptr : a.lr;
+  h.lr_t = h.lr;
+  if (a.kind == 3) {
+    const float t = (float)(*a.iterations > 0 ? *a.iterations : 1);
+    h.lr_t = h.lr * sqrtf(1.f - __powf(a.b2, t)) / (1.f - __powf(a.b1, t));
+  }
   const int tid = threadIdx.x;
 
   if (ent.y == 0) {
     const long long n = (long long)s.rows * s.cols;
     const long long beg = (long long)ent.z * kChunk;
     const long long end = beg + kChunk < n ? beg + kChunk : n;
-    for (long long e = beg + tid; e < end; e += 256) {
-      const float w = opt_update(a, (size_t)(s.off + e), t_b1, t_b2, lr);
-      if (s.sh_off >= 0) a.shadow[s.sh_off + e] = f2bf(w);
+#pragma unroll
+    for (int it = 0; it < kChunk / 1024; ++it) {
+      const long long e = beg + it * 1024 + tid * 4;
+      if (e + 4 <= end) {
+        const float4 w = upd4(a, (size_t)(s.off + e), h);
+        if (s.sh_off >= 0) {
+          bf16x4 hv = {f2bf(w.x), f2bf(w.y), f2bf(w.z), f2bf(w.w)};
+          *reinterpret_cast<bf16x4*>(a.shadow + s.sh_off + e) = hv;
+        }
+      } else {
+        for (long long q = e; q < end && q < e + 4; ++q) {
+          const float w = upds(a, (size_t)(s.off + q), h);
+          if (s.sh_off >= 0) a.shadow[s.sh_off + q] = f2bf(w);
+        }
+      }
     }
   } else {
     const int r0 = ent.z * 64, c0 = ent.w * 64;
-    for (int i = tid; i < 64 * 64; i += 256) {
-      const int r = i >> 6, c = i & 63;
+    const bool vec = (s.cols % 4) == 0;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int r = it * 16 + (tid >> 4), c = (tid & 15) * 4;
       const int gr = r0 + r, gc = c0 + c;
-      if (gr < s.rows && gc < s.cols) {
+      if (gr < s.rows) {
         const long long e = (long long)gr * s.cols + gc;
-        const float w = opt_update(a, (size_t)(s.off + e), t_b1, t_b2, lr);
-        const bf16 h = f2bf(w);
-        if (s.sh_off >= 0) a.shadow[s.sh_off + e] = h;
-        tile[r][c] = h;
+        if (vec && gc + 4 <= s.cols) {
+          const float4 w = upd4(a, (size_t)(s.off + e), h);
+          bf16x4 hv = {f2bf(w.x), f2bf(w.y), f2bf(w.z), f2bf(w.w)};
+          if (s.sh_off >= 0) *reinterpret_cast<bf16x4*>(a.shadow + s.sh_off + e) = hv;
+          *reinterpret_cast<bf16x4*>(&tile[r][c]) = hv;
+        } else {
+          for (int q = 0; q < 4 && gc + q < s.cols; ++q) {
+            const float w = upds(a, (size_t)(s.off + e + q), h);
+            const bf16 hv = f2bf(w);
+            if (s.sh_off >= 0) a.shadow[s.sh_off + e + q] = hv;
+            tile[r][c + q] = hv;
+          }
+        }
       }
     }
-    __syncthreads();
-    for (int i = tid; i < 64 * 64; i += 256) {
-      const int c = i >> 6, r = i & 63;
-      const int gr = r0 + r, gc = c0 + c;
+    lds_barrier();
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int i = it * 256 + tid;
+      const int c = i >> 6, r = i & 63, gr = r0 + r, gc = c0 + c;
       if (gr < s.rows && gc < s.cols) a.shadow[s.sht_off + (long long)gc * s.rows + gr] = tile[r][c];
-    }
-  }
-
-  // Last block advances the iteration counter.
-  __syncthreads();
-  if (tid == 0) {
-    __threadfence();
-    const unsigned ticket = atomicAdd(a.done, 1u);
-    if (ticket == gridDim.x - 1) {
-      atomicAdd((unsigned long long*)a.iterations, 1ull);
-      __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -180,12 +220,13 @@ TDE_API int tde_optim_build_table(const void* segs_host, int nseg, void* table_h
 
 TDE_API int tde_optim_apply(float* w, float* g, float* m, float* v, void* shadow,
                             const void* segs_dev, const void* table_dev, int nblocks,
-                            long long* iterations, unsigned* done, int kind, float lr,
-                            float mom, float b1, float b2, float eps, float grad_scale,
-                            int zero_grad, const float* lr_ptr, hipStream_t stream) {
+                            const long long* iterations, int kind, float lr, float mom, float b1,
+                            float b2, float eps, float grad_scale, int zero_grad,
+                            const float* lr_ptr, hipStream_t stream) {
   if (nblocks <= 0) return 0;
+  if (((uintptr_t)w | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) return -1;
   OptArgs a{w, g, m, v, (bf16*)shadow, (const OptSeg*)segs_dev, (const int4*)table_dev,
-            iterations, done, kind, lr, mom, b1, b2, eps, grad_scale, zero_grad, lr_ptr};
+            iterations, kind, lr, mom, b1, b2, eps, grad_scale, zero_grad, lr_ptr};
   optim_apply_kernel<<<nblocks, 256, 0, stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;

@@ -24,6 +24,9 @@ if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench 600 python bench.py --steps 2000 --warmup 200
   step bench_nograph 600 python bench.py --steps 400 --warmup 64 --no-graph
 fi
+if [ "$MODE" = all ] || [ "$MODE" = micro ]; then
+  step micro 300 python bench/micro.py
+fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 400 --warmup 64
 fi

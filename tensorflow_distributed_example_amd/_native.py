@@ -33,10 +33,13 @@ _HIP_PROTOS = {
     "tde_conv3x3c1_relu_pool_fwd": (i32, [p, p, p, p, p, i32, p, i32, i32, i32, i32, p, i32, p]),
     "tde_conv3x3c1_relu_pool_bwd": (i32, [p, p, p, i32, p, i32, i32, p, p, i32, i32, i32, i32, p]),
     "tde_head_xent": (i32, [p, i32, p, i32, p, p, p, i32, i32, i32, f32, i32, p, p, p, p, i32, p, i32,
-                            p, i32, p, p, i32, p, p]),
+                            p, i32, p, p, i32, p, i32, p, p, p]),
+    "tde_convnet_fwd": (i32, [p, p, p, p, i32, p, p, i32, p, i32, i32, i32, i32, p, p]),
+    "tde_convnet_bwd": (i32, [p, p, i32, p, i32, p, i32, p, i32, p, i32, p, p, p, i32, i32, i32, p, p]),
+    "tde_noop": (i32, [i32, i32, p]),
     "tde_optim_table_size": (i32, [p, i32]),
     "tde_optim_build_table": (i32, [p, i32, p]),
-    "tde_optim_apply": (i32, [p, p, p, p, p, p, p, i32, p, p, i32, f32, f32, f32, f32, f32, f32, i32, p, p]),
+    "tde_optim_apply": (i32, [p, p, p, p, p, p, p, i32, p, i32, f32, f32, f32, f32, f32, f32, i32, p, p]),
     "tde_shadow_refresh": (i32, [p, p, p, p, i32, p]),
     # RCCL
     "tde_nccl_version": (i32, []),

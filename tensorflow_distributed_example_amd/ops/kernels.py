@@ -79,7 +79,7 @@ def conv3x3c1_relu_pool_bwd(x, amax, G, W1, dw, db):
 
 def head_xent(hin, W2, b2, labels, *, B, scale, pre_bias=None, pre_relu=False, compute_grad=True,
               dW2=None, db2=None, dpre_bias=None, G=None, Gt=None, Gf=None, metrics=None,
-              probs=None, probs_are_logits=False, row_loss=None):
+              probs=None, probs_are_logits=False, row_loss=None, zero_hin=False, iterations=None, stamps=None):
     H, C = W2.shape
     _req(hin.dtype == torch.float32 and hin.shape[1] >= H, "head: input")
     _req(C <= 64 and H * C <= 16384, "head: too large for the fused head")
@@ -90,5 +90,46 @@ def head_xent(hin, W2, b2, labels, *, B, scale, pre_bias=None, pre_relu=False, c
     rc = N.hip().tde_head_xent(_P(hin), hin.stride(0), _P(pre_bias), int(pre_relu), _P(W2), _P(b2), _P(labels),
                                B, H, C, float(scale), int(compute_grad), _P(dW2), _P(db2), _P(dpre_bias),
                                _P(G), ldg, _P(Gt), ldgt, _P(Gf), ldgf, _P(metrics), _P(probs),
-                               int(probs_are_logits), _P(row_loss), _s())
+                               int(probs_are_logits), _P(row_loss), int(zero_hin), _P(iterations), _P(stamps), _s())
     N.check(rc, "tde_head_xent")
+
+
+def convnet_fwd(x, wc, bc, W1col, hpre, Pt=None, amax=None, stamps=None):
+    """Fused Conv2D(32,3x3,relu)+MaxPool(2)+Dense(64) matmul forward; hpre += (atomic).
+
+    amax: uint8 view of a [P, 4, lda] uint64 buffer (lane-contiguous pool argmax)."""
+    B, H, W = x.shape[0], x.shape[1], x.shape[2]
+    Kf = ((H - 2) // 2) * ((W - 2) // 2) * 32
+    _req(wc.shape == (3, 3, 1, 32) and bc is not None and bc.numel() == 32, "convnet_fwd: conv must be 3x3x1x32")
+    _req(W1col.shape == (64, Kf) and W1col.stride(0) % 8 == 0 and W1col.dtype == torch.bfloat16, "convnet_fwd: W1col")
+    _req(W % 2 == 0 and x.shape[3] == 1 and x.is_contiguous(), "convnet_fwd: input")
+    _req(hpre.shape[0] >= B and hpre.shape[1] == 64 and hpre.is_contiguous(), "convnet_fwd: hpre")
+    ldPt = 0
+    if Pt is not None:
+        ldPt = Pt.stride(0)
+        _req(Pt.shape[0] == Kf and ldPt >= B and ldPt % 8 == 0, "convnet_fwd: Pt")
+    lda = 0
+    if amax is not None:
+        lda = amax.shape[-1]
+        _req(amax.dtype == torch.int64 and amax.shape[:2] == (Kf // 32, 4) and lda >= B, "convnet_fwd: amax")
+    rc = N.hip().tde_convnet_fwd(_P(x), _P(wc), _P(bc), _P(W1col), W1col.stride(0), _P(hpre), _P(Pt), ldPt,
+                                 _P(amax), lda, B, H, W, _P(stamps), _s())
+    N.check(rc, "tde_convnet_fwd")
+
+
+def convnet_bwd(x, amax, G, Gt, W1row, Pt, dW1, dwc, dbc, B=None, stamps=None):
+    B = x.shape[0] if B is None else B
+    H, W = x.shape[1], x.shape[2]
+    Kf = ((H - 2) // 2) * ((W - 2) // 2) * 32
+    _req(dwc.shape == (3, 3, 1, 32) and G.shape[1] == 64, "convnet_bwd: specialised for Conv2D(32) + Dense(64)")
+    _req(W1row.shape == (Kf, 64) and dW1.shape == (Kf, 64) and Pt.shape[0] == Kf, "convnet_bwd: shapes")
+    _req(Gt.shape[0] == 64 and Gt.stride(0) >= B and Pt.stride(0) >= B, "convnet_bwd: ld")
+    _req(amax.dtype == torch.int64 and amax.shape[:2] == (Kf // 32, 4) and amax.shape[-1] >= B, "convnet_bwd: amax")
+    rc = N.hip().tde_convnet_bwd(_P(x), _P(amax), amax.shape[-1], _P(G), G.stride(0), _P(Gt), Gt.stride(0),
+                                 _P(W1row), W1row.stride(0), _P(Pt), Pt.stride(0), _P(dW1), _P(dwc), _P(dbc), B, H,
+                                 W, _P(stamps), _s())
+    N.check(rc, "tde_convnet_bwd")
+
+
+def noop(blocks=1, threads=64):
+    N.check(N.hip().tde_noop(blocks, threads, _s()), "tde_noop")

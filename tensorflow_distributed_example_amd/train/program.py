@@ -209,7 +209,6 @@ class OptimizerKernel:
         self.nblocks = nb
         self.segs_dev = torch.from_numpy(arr.view(np.uint8).copy()).to(store.device)
         self.table_dev = torch.from_numpy(table).to(store.device)
-        self.done = torch.zeros(1, dtype=torch.int32, device=store.device)
         self.refresh_shadows()
 
     def refresh_shadows(self):
@@ -229,7 +228,7 @@ class OptimizerKernel:
         v = st.slot(opt.slot_names()[1]) if len(opt.slot_names()) > 1 else None
         rc = N.hip().tde_optim_apply(st.w.data_ptr(), st.g.data_ptr(), N.ptr(m), N.ptr(v), self.shadow.data_ptr(),
                                      self.segs_dev.data_ptr(), self.table_dev.data_ptr(), self.nblocks,
-                                     self.iterations.data_ptr(), self.done.data_ptr(), opt.kind_id,
+                                     self.iterations.data_ptr(), opt.kind_id,
                                      float(opt.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"], 1.0,
                                      int(zero_grad), None, N.stream_ptr())
         N.check(rc, "tde_optim_apply")
@@ -256,8 +255,10 @@ def match_convnet(model, loss):
         return None
     if (d2.activation == "softmax") == bool(loss.from_logits):
         return None  # probabilities fed to from_logits=True (or logits w/o from_logits): not fusable
-    if d2.units > 64 or d1.units * d2.units > 16384 or d1.units % 32:
+    if d2.units > 64 or d1.units * d2.units > 16384 or d1.units % 32 or d1.units > 256:
         return None
+    if c.filters != 32 or d1.units != 64:
+        return None  # fused backward is specialised for the reference's Conv2D(32)/Dense(64)
     return dict(conv=c, pool=p, dense1=d1, dense2=d2)
 
 
@@ -280,9 +281,8 @@ class ConvNetPlan(ReplicaPlan):
         self.Bp = Bp
         dev = self.device
         bf = torch.bfloat16
-        self.Pb = torch.zeros(B, self.Kf, dtype=bf, device=dev)
         self.Pt = torch.zeros(self.Kf, Bp, dtype=bf, device=dev)
-        self.amax = torch.zeros(B, self.Kf, dtype=torch.uint8, device=dev)
+        self.amax = torch.zeros(self.Kf // 32, 4, Bp, dtype=torch.int64, device=dev)  # [P][C/8][B] argmax bytes
         self.hpre = torch.zeros(B, self.Hd, dtype=torch.float32, device=dev)
         self.G = torch.zeros(B, self.Hd, dtype=bf, device=dev)
         self.Gt = torch.zeros(self.Hd, Bp, dtype=bf, device=dev)
@@ -302,7 +302,6 @@ class ConvNetPlan(ReplicaPlan):
         ok = self.opt or self._shadow_only
         self.W1row = ok.shadow_views[(self.names["w1"], "row")]
         self.W1col = ok.shadow_views[(self.names["w1"], "col")]
-        self.splits = K.gemm_pick_splits(self.B, self.Hd, self.Kf)
 
     def on_weights_loaded(self):
         (self.opt or self._shadow_only).refresh_shadows()
@@ -316,36 +315,40 @@ class ConvNetPlan(ReplicaPlan):
         return None if nm is None else self.store.grad(nm)
 
     def _forward(self, x, B, with_pt):
-        K = self.K
-        K.conv3x3c1_relu_pool_fwd(x, self._v("wc"), self._v("bc"), self.Pb, self.Pt if with_pt else None, self.amax,
-                                  zbuf=self.hpre)
-        K.gemm_nt(self.Pb, self.W1col, self.hpre, M=B, N_=self.Hd, K=self.Kf, mode="atomic", splits=self.splits)
+        # kernel 1: conv+bias+ReLU+pool fused with the Dense(Hd) matmul (split-K atomics into hpre,
+        # which the previous head launch left zeroed)
+        self.K.convnet_fwd(x[:B], self._v("wc"), self._v("bc"), self.W1col, self.hpre,
+                           self.Pt if with_pt else None, self.amax)
 
     def train_step(self, x, y, B=None):
         K = self.K
         B = self.B if B is None else B
         self._forward(x, B, True)
+        # kernel 2: Dense bias+ReLU, Dense(10), softmax-CE, accuracy and the head backward
         K.head_xent(self.hpre, self._v("w2"), self._v("b2"), y, B=B, scale=self.scale, pre_bias=self._v("b1"),
                     pre_relu=self.pre_relu, compute_grad=True, dW2=self._g("w2"), db2=self._g("b2"),
-                    dpre_bias=self._g("b1"), G=self.G, Gt=self.Gt, metrics=self.metrics)
-        K.gemm_nt(self.Pt, self.Gt, self._g("w1"), M=self.Kf, N_=self.Hd, K=B, mode="store", splits=1)
-        K.conv3x3c1_relu_pool_bwd(x, self.amax, self.G, self.W1row, self._g("wc"), self._g("bc"))
+                    dpre_bias=self._g("b1"), G=self.G, Gt=self.Gt, metrics=self.metrics, zero_hin=True,
+                    iterations=self.iterations)
+        # kernel 3: Dense weight-grad + Dense input-grad + pool/ReLU routing + conv weight/bias grads
+        K.convnet_bwd(x, self.amax, self.G, self.Gt, self.W1row, self.Pt, self._g("w1"), self._g("wc"),
+                      self._g("bc"), B=B)
 
     def apply(self):
+        # kernel 4: multi-tensor optimizer (+ grad zeroing + bf16 shadow refresh)
         self.opt.apply()
 
     def eval_step(self, x, y, B=None):
         B = self.B if B is None else B
         self._forward(x, B, False)
         self.K.head_xent(self.hpre, self._v("w2"), self._v("b2"), y, B=B, scale=self.scale, pre_bias=self._v("b1"),
-                         pre_relu=self.pre_relu, compute_grad=False, metrics=self.metrics)
+                         pre_relu=self.pre_relu, compute_grad=False, metrics=self.metrics, zero_hin=True)
 
     def predict(self, x, B=None):
         B = self.B if B is None else B
         self._forward(x, B, False)
         self.K.head_xent(self.hpre, self._v("w2"), self._v("b2"), self._dummy_labels(B), B=B, scale=1.0,
                          pre_bias=self._v("b1"), pre_relu=self.pre_relu, compute_grad=False, probs=self.probs,
-                         probs_are_logits=self.logits_out)
+                         probs_are_logits=self.logits_out, zero_hin=True)
         return self.probs[:B]
 
     def _dummy_labels(self, B):

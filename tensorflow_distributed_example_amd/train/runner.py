@@ -84,6 +84,7 @@ class Program:
         cuda = all(d.type == "cuda" for d in self.devices)
         env = os.environ.get("TDE_GRAPH", "1") != "0"
         self.use_graph = bool(training and cuda and env and len(self.devices) == 1 and
+                              self.plans[0].kind != "reference" and
                               (self.comm is None or self.comm.capturable))
         self._comm_warm = False
 

@@ -1,0 +1,112 @@
+"""T3/T4 on CPU: MirroredStrategy (in-process replicas) and
+MultiWorkerMirroredStrategy (2 processes, gloo) — the DP invariants:
+replicas stay identical, and R replicas at global batch G match 1 replica at G."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
+import numpy as np
+import pytest
+
+import tensorflow_distributed_example_amd as tde
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _data(n=256, seed=0):
+    rng = np.random.default_rng(seed)
+    return rng.random((n, 28, 28, 1), dtype=np.float32), rng.integers(0, 10, size=n)
+
+
+def _train(strategy, x, y, w0, gb=64, epochs=1):
+    with strategy.scope():
+        m = tde.zoo.mnist_cnn()
+        m.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True), optimizer=tde.optimizers.SGD(0.1),
+                  metrics=["accuracy"])
+    m.set_weights(w0)
+    ds = tde.data.Dataset.from_tensor_slices((x, y)).batch(gb)
+    h = m.fit(ds, epochs=epochs, verbose=0)
+    return m, h
+
+
+def test_mirrored_two_cpu_replicas_match_single():
+    x, y = _data()
+    w0 = tde.zoo.mnist_cnn().get_weights()
+    tde.backend.clear_session()
+    m1, h1 = _train(tde.distribute.OneDeviceStrategy("cpu"), x, y, w0)
+    tde.backend.clear_session()
+    st = tde.distribute.MirroredStrategy(devices=["/cpu:0", "/cpu:0"])
+    assert st.num_replicas_in_sync == 2
+    m2, h2 = _train(st, x, y, w0)
+    stores = m2._replica_stores(st)
+    assert len(stores) == 2
+    assert np.array_equal(stores[0].w.numpy(), stores[1].w.numpy())   # replicas identical
+    for a, b in zip(m1.get_weights(), m2.get_weights()):
+        assert np.allclose(a, b, atol=2e-5, rtol=1e-4)
+    assert abs(h1.history["loss"][0] - h2.history["loss"][0]) < 1e-4
+
+
+WORKER = textwrap.dedent("""
+    import json, os, sys, numpy as np
+    sys.path.insert(0, {root!r})
+    import tensorflow_distributed_example_amd as tde
+    tde.backend.set_random_seed(0)
+    strategy = tde.distribute.MultiWorkerMirroredStrategy()
+    rng = np.random.default_rng(0)
+    x = rng.random((256, 28, 28, 1), dtype=np.float32); y = rng.integers(0, 10, size=256)
+    with strategy.scope():
+        m = tde.zoo.mnist_cnn()
+        m.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True),
+                  optimizer=tde.optimizers.SGD(0.1), metrics=['accuracy'])
+    w0 = np.load({w0!r}, allow_pickle=False)
+    m.set_weights([w0['arr_%d' % i] for i in range(6)])
+    opts = tde.data.Options(); opts.experimental_distribute.auto_shard_policy = tde.data.AutoShardPolicy.OFF
+    ds = tde.data.Dataset.from_tensor_slices((x, y)).batch(64).with_options(opts)
+    h = m.fit(ds, epochs=1, verbose=0)
+    out = {{"rank": strategy.worker_index, "replicas": strategy.num_replicas_in_sync,
+           "loss": h.history["loss"][0], "w": [float(np.abs(a).sum()) for a in m.get_weights()]}}
+    np.savez({outp!r} + str(strategy.worker_index) + ".npz", *m.get_weights())
+    print("RESULT" + json.dumps(out), flush=True)
+""")
+
+
+def test_multi_worker_mirrored_gloo_two_processes(tmp_path):
+    x, y = _data()
+    w0 = tde.zoo.mnist_cnn().get_weights()
+    np.savez(tmp_path / "w0.npz", *w0)
+    port = _free_port()
+    cluster = {"worker": [f"127.0.0.1:{port}", f"127.0.0.1:{_free_port()}"]}
+    script = WORKER.format(root=ROOT, w0=str(tmp_path / "w0.npz"), outp=str(tmp_path / "out"))
+    procs = []
+    for i in range(2):
+        env = dict(os.environ, TF_CONFIG=json.dumps({"cluster": cluster, "task": {"type": "worker", "index": i}}),
+                   CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+        procs.append(subprocess.Popen([sys.executable, "-c", script], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        o, _ = p.communicate(timeout=240)
+        assert p.returncode == 0, o
+        outs.append(json.loads(o.split("RESULT")[1].strip()))
+    assert outs[0]["replicas"] == 2
+    wa = np.load(tmp_path / "out0.npz")
+    wb = np.load(tmp_path / "out1.npz")
+    for k in wa.files:
+        assert np.array_equal(wa[k], wb[k])      # workers hold identical variables
+    # 2 workers x per-replica 32 at global 64, AutoShard OFF == 1 replica at global 64
+    tde.backend.clear_session()
+    m1, h1 = _train(tde.distribute.OneDeviceStrategy("cpu"), x, y, w0)
+    for k, a in zip(wa.files, m1.get_weights()):
+        assert np.allclose(wa[k], a, atol=2e-5, rtol=1e-4)
+    assert abs(outs[0]["loss"] - h1.history["loss"][0]) < 1e-4

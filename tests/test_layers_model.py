@@ -1,0 +1,121 @@
+"""T1: layer/model fidelity (param counts, names, shapes, summary, initializers)."""
+import io
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import tensorflow_distributed_example_amd as tde
+from tensorflow_distributed_example_amd.models import layers as L
+
+
+def test_model_a_params_and_names():
+    m = tde.zoo.mnist_cnn()
+    m.build()
+    assert m.count_params() == 347146
+    assert m.variable_names() == ["conv2d/kernel", "conv2d/bias", "dense/kernel", "dense/bias", "dense_1/kernel",
+                                  "dense_1/bias"]
+    assert [w.shape for w in m.get_weights()] == [(3, 3, 1, 32), (32,), (5408, 64), (64,), (64, 10), (10,)]
+    assert m.output_shape == (None, 10)
+
+
+def test_model_b_params_and_names():
+    m = tde.zoo.mnist_bn_cnn()
+    m.build()
+    tr = sum(int(np.prod(w.shape)) for w in m.trainable_weights)
+    ntr = sum(int(np.prod(w.shape)) for w in m.non_trainable_weights)
+    assert (tr, ntr) == (250466, 484)
+    names = m.variable_names()
+    assert names[:4] == ["conv2d/kernel", "batch_normalization/beta", "batch_normalization/moving_mean",
+                         "batch_normalization/moving_variance"]
+    assert "dense_1/bias" in names and "dense/bias" not in names
+
+
+def test_summary_text():
+    m = tde.zoo.mnist_cnn()
+    buf = []
+    m.summary(print_fn=buf.append)
+    text = "\n".join(buf)
+    assert 'Model: "sequential"' in text
+    assert "conv2d (Conv2D)" in text and "(None, 26, 26, 32)" in text
+    assert "Total params: 347,146" in text and "Non-trainable params: 0" in text
+
+
+def test_glorot_uniform_statistics():
+    m = tde.zoo.mnist_cnn()
+    w = m.get_weights()[2]
+    limit = math.sqrt(6 / (5408 + 64))
+    assert np.abs(w).max() <= limit + 1e-7
+    assert abs(w.std() - limit / math.sqrt(3)) < 0.02 * limit
+    assert np.all(m.get_weights()[3] == 0)
+
+
+def test_tf_same_padding_is_asymmetric():
+    assert L.tf_same_pads(28, 3, 1) == (1, 1)
+    assert L.tf_same_pads(28, 6, 2) == (2, 2)
+    assert L.tf_same_pads(224, 7, 2) == (2, 3)   # ResNet stem: TF pads (2,3), torch would use 3/3
+    c = L.Conv2D(12, 6, strides=2, padding="same")
+    assert c.compute_output_shape((28, 28, 6)) == (14, 14, 12)
+
+
+def test_flatten_order_is_hwc():
+    x = torch.arange(2 * 2 * 3 * 2).reshape(2, 2, 3, 2).float()
+    f = L.Flatten()
+    out = f.ref_call(x, {}, False)
+    assert torch.equal(out[0], x[0].reshape(-1))
+
+
+def test_batchnorm_keras_defaults_and_moving_update():
+    bn = L.BatchNormalization(scale=False, center=True)
+    assert bn.momentum == 0.99 and bn.epsilon == 1e-3
+    bn._build_shapes((4, 4, 3))
+    x = torch.randn(8, 4, 4, 3)
+    W = {"beta": torch.zeros(3), "moving_mean": torch.zeros(3), "moving_variance": torch.ones(3)}
+    upd = []
+    y = bn.ref_call(x, W, True, None, upd)
+    mean = x.mean(dim=(0, 1, 2))
+    var = x.var(dim=(0, 1, 2), unbiased=False)
+    assert torch.allclose(y, (x - mean) / torch.sqrt(var + 1e-3), atol=1e-5)
+    d = dict(upd)
+    n = 8 * 16
+    assert torch.allclose(d[f"{bn.name}/moving_mean"], 0.01 * mean, atol=1e-6)
+    assert torch.allclose(d[f"{bn.name}/moving_variance"], 0.99 + 0.01 * var * n / (n - 1), atol=1e-6)
+
+
+def test_dropout_scale_and_learning_phase():
+    d = L.Dropout(0.5)
+    x = torch.ones(1000, 20)
+    g = torch.Generator().manual_seed(0)
+    y = d.ref_call(x, {}, True, g)
+    vals = set(torch.unique(y).tolist())
+    assert vals <= {0.0, 2.0}
+    assert 0.4 < (y == 0).float().mean().item() < 0.6
+    assert torch.equal(d.ref_call(x, {}, False, g), x)
+    tde.backend.set_learning_phase(True)   # Q4: global training phase forces dropout on in eval
+    try:
+        y2 = d.ref_call(x, {}, False, g)
+        assert (y2 == 0).any()
+    finally:
+        tde.backend.set_learning_phase(None)
+
+
+def test_get_set_weights_roundtrip_and_config():
+    m = tde.zoo.mnist_cnn()
+    w = m.get_weights()
+    w2 = [a + 1 for a in w]
+    m.set_weights(w2)
+    for a, b in zip(m.get_weights(), w2):
+        assert np.array_equal(a, b)
+    cfg = m.get_config()
+    tde.backend.clear_session()
+    m2 = tde.Sequential.from_config(cfg)
+    m2.build()
+    assert m2.count_params() == m.count_params()
+
+
+def test_reference_forward_call_shapes():
+    m = tde.zoo.mnist_bn_cnn()
+    out = m(np.random.rand(3, 784).astype(np.float32))
+    assert out.shape == (3, 10)
+    assert torch.allclose(out.sum(1), torch.ones(3), atol=1e-5)  # softmax output
