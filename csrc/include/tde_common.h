@@ -53,6 +53,45 @@ __device__ __forceinline__ bf16x8 load_frag(const bf16* p, int k0, int K, bool r
   return r;
 }
 
+// Reductions over the 16 lanes of a DPP row with DPP modifiers (no LDS
+// round trip, unlike __shfl_xor which lowers to ds_bpermute): quad xor1, quad
+// xor2, row_half_mirror, row_mirror -> every lane of the row holds the result.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  v = fmaxf(v, dpp_f<0x140>(v));
+  return v;
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  v += dpp_f<0x140>(v);
+  return v;
+}
+__device__ __forceinline__ int row16_min(int v) {
+  v = min(v, dpp_i<0xB1>(v));
+  v = min(v, dpp_i<0x4E>(v));
+  v = min(v, dpp_i<0x141>(v));
+  v = min(v, dpp_i<0x140>(v));
+  return v;
+}
+// Sum over the 4 rows of a wave (lanes 0,16,32,48 after a row16 reduction).
+__device__ __forceinline__ float rows4_sum(float v) {
+  const int x = __float_as_int(v);
+  return (__int_as_float(__builtin_amdgcn_readlane(x, 0)) + __int_as_float(__builtin_amdgcn_readlane(x, 16))) +
+         (__int_as_float(__builtin_amdgcn_readlane(x, 32)) + __int_as_float(__builtin_amdgcn_readlane(x, 48)));
+}
+
 // Workgroup barrier that orders LDS only.  __syncthreads() also waits for every
 // outstanding global store/atomic of the wave (vmcnt(0)); at MNIST sizes those
 // scattered stores cost microseconds, and no wave reads them back in-kernel, so

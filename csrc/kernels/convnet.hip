@@ -45,8 +45,16 @@ struct ConvNetFwdArgs {
   long long* stamps;
 };
 
+// The input rows a workgroup's PPW positions touch (<= XR rows of <= XW floats per
+// image) are staged into LDS with coalesced float4 loads: gathering 4x4 patches
+// straight from HBM puts 64 distinct cache lines behind every load instruction.
+constexpr int XR = 6, XW = 32;
+constexpr int kFwdLds = PPW * 64 * PSTR * 2 + 64 * XR * XW * 4;
+
 __global__ __launch_bounds__(1024) void convnet_fwd_kernel(ConvNetFwdArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16 Ps[PPW * 64 * PSTR];
+  extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
+  bf16* Ps = reinterpret_cast<bf16*>(fsm);
+  float* xr = reinterpret_cast<float*>(fsm + PPW * 64 * PSTR * 2);  // [64][XR][W]
   stamp(a.stamps, 0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fk = (lane >> 4) * 8;
@@ -59,17 +67,19 @@ __global__ __launch_bounds__(1024) void convnet_fwd_kernel(ConvNetFwdArgs a) {
   const int pp = wave >> 2, cg = wave & 3, c0 = cg * 8;
   const int p = p0 + pp;
   const bool pok = p < P;
+  const int py0 = p0 / Wp;
+  const int nrows = min(XR, H - 2 * py0);
+  const int istride = XR * W;  // floats per staged image
 
   // ---- prologue: all global loads, independent, issued back to back
-  float patch[16];
-  if (bok && pok) {
-    const int py = p / Wp, px = p - py * Wp;
-    const float* xb = a.x + (size_t)b * H * W + (2 * py) * W + 2 * px;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float2* row = reinterpret_cast<const float2*>(xb + r * W);
-      const float2 u = row[0], v = row[1];
-      patch[r * 4 + 0] = u.x; patch[r * 4 + 1] = u.y; patch[r * 4 + 2] = v.x; patch[r * 4 + 3] = v.y;
+  {
+    const int n4 = nrows * W / 4;  // float4 per image
+    for (int i = threadIdx.x; i < 64 * n4; i += 1024) {
+      const int bl = i / n4, q = i - bl * n4;
+      float4 v = {0.f, 0.f, 0.f, 0.f};
+      if (b0 + bl < a.B)
+        v = *reinterpret_cast<const float4*>(a.x + (size_t)(b0 + bl) * H * W + (size_t)(2 * py0) * W + q * 4);
+      *reinterpret_cast<float4*>(xr + bl * istride + q * 4) = v;
     }
   }
   float4 wlo[9], whi[9];
@@ -90,10 +100,22 @@ __global__ __launch_bounds__(1024) void convnet_fwd_kernel(ConvNetFwdArgs a) {
                      : bf16x8{};
   }
   stamp(a.stamps, 1);
+  lds_barrier();
 
   // ---- phase 1: conv + bias + ReLU + 2x2 max-pool for 8 channels
   bf16x8 outv;
   if (bok && pok) {
+    float patch[16];
+    {
+      const int py = p / Wp, px = p - py * Wp;
+      const float* xb = xr + lane * istride + (2 * (py - py0)) * W + 2 * px;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float2 u = *reinterpret_cast<const float2*>(xb + r * W);
+        const float2 v = *reinterpret_cast<const float2*>(xb + r * W + 2);
+        patch[r * 4 + 0] = u.x; patch[r * 4 + 1] = u.y; patch[r * 4 + 2] = v.x; patch[r * 4 + 3] = v.y;
+      }
+    }
     uint64_t packed = 0;
 #pragma unroll
     for (int cc = 0; cc < 8; ++cc) {
@@ -363,7 +385,7 @@ using namespace tde;
 TDE_API int tde_convnet_fwd(const float* x, const float* wc, const float* bc, const void* W1c, int ldw1c,
                             float* hpre, void* Pt, int ldPt, void* amax, int lda, int B, int H, int W,
                             long long* stamps, hipStream_t stream) {
-  if ((W & 1) || (ldw1c & 7) || (Pt && (ldPt & 7)) || (amax && lda < B)) return -1;
+  if ((W & 3) || W > XW || ((W - 2) / 2) < PPW || (ldw1c & 7) || (Pt && (ldPt & 7)) || (amax && lda < B)) return -1;
   if (((uintptr_t)wc | (uintptr_t)bc) & 15) return -2;
   const int P = ((H - 2) / 2) * ((W - 2) / 2);
   int by = (B + 63) / 64;
@@ -373,7 +395,12 @@ TDE_API int tde_convnet_fwd(const float* x, const float* wc, const float* bc, co
   }
   ConvNetFwdArgs a{x, wc, bc, (const bf16*)W1c, ldw1c, hpre, (bf16*)Pt, ldPt, (uint64_t*)amax, lda, B, H, W, stamps};
   dim3 grid((P + PPW - 1) / PPW, by);
-  convnet_fwd_kernel<<<grid, 1024, 0, stream>>>(a);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)convnet_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kFwdLds);
+    attr_set = true;
+  }
+  convnet_fwd_kernel<<<grid, 1024, kFwdLds, stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;
 }

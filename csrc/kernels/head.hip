@@ -11,9 +11,15 @@
 //   * Dense(10, activation='softmax') + 'sparse_categorical_crossentropy' is
 //     computed from the pre-softmax logits (stable log-softmax, Q5).
 //   * 'accuracy' = argmax(first max) == label.
-// The gradient of the preceding Dense's bias+ReLU epilogue (dbias, ReLU mask) is
-// produced here too, and dH is emitted in bf16 both row-major and transposed so
-// the following MFMA GEMMs read K-contiguous fragments.
+//
+// One workgroup = 16 rows, 4 waves.  All three products run on the exact-f32
+// MFMA (v_mfma_f32_16x16x4_f32; no bf16 rounding in the loss path):
+//   logits[16 x 16]  = h[16 x H] . W2[H x C]          (wave 0, H/4 k-steps)
+//   softmax / CE / accuracy in registers on the MFMA C layout (16-lane groups)
+//   dW2[H x C]       = h^T . dl                       (wave w: 16-row tiles of H)
+//   dH[16 x H]       = dl . W2^T, ReLU mask           (wave w: 16-column tiles of H)
+// dH is emitted in bf16 row-major and transposed (K-contiguous for the next
+// MFMA GEMMs); bias grads by column sums; parameter grads are f32 atomics.
 #include "tde_common.h"
 
 namespace tde {
@@ -37,141 +43,164 @@ struct HeadArgs {
   long long* stamps;                  // diagnostic phase stamps (nullable)
 };
 
-constexpr int kHeadRows = 8;
+constexpr int HR = 16;          // rows per workgroup
+constexpr int HMAX = 256;       // max hidden width
+constexpr int HST = HMAX + 4;   // LDS row stride of h (floats; +4 breaks bank aliasing)
+
+__device__ __forceinline__ f32x4 mfma_f32(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// reductions over the 16 lanes of a lane-group (xor 8,4,2,1 stays inside the group)
+__device__ __forceinline__ float g16_max(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float g16_sum(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ int g16_min_i(int v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
 
 __global__ __launch_bounds__(256) void head_xent_kernel(HeadArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int H = a.H, C = a.C, R = kHeadRows;
-  float* hs = sm;                 // [R][H]
-  float* w2s = hs + R * H;        // [H][C]
-  float* lg = w2s + H * C;        // [R][C]
-  float* dls = lg + R * C;        // [R][C]
-  float* dhs = dls + R * C;       // [R][H]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r0 = blockIdx.x * R;
+  __shared__ __attribute__((aligned(16))) float hs[HR * HST];   // activated h, f32
+  __shared__ float w2s[HMAX * 16];                              // W2 padded to 16 classes
+  __shared__ float dls[HR * 16];                                // dlogits
+  __shared__ float b2s[16];
+  __shared__ int labs[HR];
   stamp(a.stamps, 0);
+  const int H = a.H, C = a.C;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int r0 = blockIdx.x * HR;
   if (a.iterations && blockIdx.x == 0 && tid == 0) atomicAdd((unsigned long long*)a.iterations, 1ull);
-  // Prefetch everything this block needs from global memory up front.
-  int label_pref = 0;
-  if (tid < R && r0 + tid < a.B) label_pref = a.labels[r0 + tid];
-  for (int i = tid; i < R * H; i += 256) {
-    const int r = i / H, j = i - r * H, row = r0 + r;
-    float v = 0.f;
-    if (row < a.B) {
-      v = a.hin[(size_t)row * a.ldh + j];
-      if (a.pre_bias) v += a.pre_bias[j];
-      if (a.pre_relu) v = fmaxf(v, 0.f);
+
+  // ---- prologue: every global load issued up front (H padded to Hp = 16k with zeros)
+  const int Hp = (H + 15) & ~15;
+  const int H4 = H / 4, Hp4 = Hp / 4;
+  for (int i = tid; i < HR * Hp4; i += 256) {
+    const int r = i / Hp4, j4 = (i - r * Hp4) * 4, row = r0 + r;
+    float4 v = {0.f, 0.f, 0.f, 0.f};
+    if (row < a.B && j4 < H) {
+      v = *reinterpret_cast<const float4*>(a.hin + (size_t)row * a.ldh + j4);
+      if (a.pre_bias) {
+        const float4 bb = *reinterpret_cast<const float4*>(a.pre_bias + j4);
+        v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
+      }
+      if (a.pre_relu) {
+        v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+      }
     }
-    hs[i] = v;
+    *reinterpret_cast<float4*>(hs + r * HST + j4) = v;
   }
-  for (int i = tid; i < H * C; i += 256) w2s[i] = a.W2[i];
-  float b2v = 0.f;
-  if (tid < C && a.b2) b2v = a.b2[tid];
-  int* labs = reinterpret_cast<int*>(dhs);  // scratch until dh is computed
-  if (tid < R) labs[tid] = label_pref;
-  __shared__ float b2sh[64];
-  if (tid < C) b2sh[tid] = b2v;
+  for (int i = tid; i < Hp * 16; i += 256) {
+    const int j = i >> 4, c = i & 15;
+    w2s[i] = (c < C && j < H) ? a.W2[j * C + c] : 0.f;
+  }
+  if (tid < 16) b2s[tid] = (a.b2 && tid < C) ? a.b2[tid] : 0.f;
+  if (tid < HR) labs[tid] = (r0 + tid < a.B) ? a.labels[r0 + tid] : 0;
   lds_barrier();
   stamp(a.stamps, 1);
   if (a.zero_hin) {
-    for (int i = tid; i < R * H; i += 256) {
-      const int r = i / H, j = i - r * H, row = r0 + r;
-      if (row < a.B) a.zero_hin[(size_t)row * a.ldh + j] = 0.f;
+    for (int i = tid; i < HR * H4; i += 256) {
+      const int r = i / H4, j4 = (i - r * H4) * 4, row = r0 + r;
+      if (row < a.B) *reinterpret_cast<float4*>(a.zero_hin + (size_t)row * a.ldh + j4) = float4{0.f, 0.f, 0.f, 0.f};
     }
   }
 
-  for (int o = tid; o < R * C; o += 256) {
-    const int r = o / C, c = o - r * C;
-    float s0 = b2sh[c], s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    const float* hr = hs + r * H;
-    int j = 0;
-    for (; j + 4 <= H; j += 4) {
-      s0 = fmaf(hr[j], w2s[j * C + c], s0);
-      s1 = fmaf(hr[j + 1], w2s[(j + 1) * C + c], s1);
-      s2 = fmaf(hr[j + 2], w2s[(j + 2) * C + c], s2);
-      s3 = fmaf(hr[j + 3], w2s[(j + 3) * C + c], s3);
+  // ---- logits + softmax-CE (wave 0): lane holds logits[4*fq + i][fr]
+  if (wave == 0) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < Hp; k += 4) acc = mfma_f32(hs[fr * HST + k + fq], w2s[(k + fq) * 16 + fr], acc);
+    float loss_acc = 0.f, corr_acc = 0.f, cnt_acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = fq * 4 + i, row = r0 + r;
+      const bool valid = row < a.B;
+      const bool cv = fr < C;
+      const float z = cv ? acc[i] + b2s[fr] : -3.0e38f;
+      const float m = row16_max(z);
+      const float e = cv ? __expf(z - m) : 0.f;
+      const float s = row16_sum(e);
+      const float p = e / s;
+      const int label = labs[r];
+      const int am = row16_min(cv && z == m ? fr : 64);
+      const float zl = __shfl(z, (lane & ~15) | (label & 15), 64);
+      if (valid) {
+        const float l = __logf(s) + m - zl;
+        if (fr == 0) {
+          loss_acc += l;
+          corr_acc += (am == label) ? 1.f : 0.f;
+          cnt_acc += 1.f;
+          if (a.row_loss) a.row_loss[row] = l;
+        }
+        if (a.probs && cv) a.probs[(size_t)row * C + fr] = a.probs_are_logits ? z : p;
+      }
+      dls[r * 16 + fr] = (valid && cv) ? (p - (fr == label ? 1.f : 0.f)) * a.scale : 0.f;
     }
-    for (; j < H; ++j) s0 = fmaf(hr[j], w2s[j * C + c], s0);
-    lg[o] = (s0 + s1) + (s2 + s3);
-  }
-  lds_barrier();
-
-  float loss_acc = 0.f, corr_acc = 0.f, cnt_acc = 0.f;
-  for (int r = wave; r < R; r += 4) {
-    const int row = r0 + r;
-    const bool valid = row < a.B;
-    const float v = lane < C ? lg[r * C + lane] : -3.0e38f;
-    const float m = wave_max(v);
-    const float e = lane < C ? __expf(v - m) : 0.f;
-    const float s = wave_sum(e);
-    const float p = e / s;
-    const int label = valid ? labs[r] : 0;
-    const float lse = __logf(s) + m;
-    const unsigned long long mask = __ballot(lane < C && v == m);
-    const int am = __ffsll((long long)mask) - 1;
-    const float lab_logit = lg[r * C + (label < C ? label : 0)];
-    if (valid) {
-      const float l = lse - lab_logit;
-      loss_acc += l;
-      corr_acc += (am == label) ? 1.f : 0.f;
-      cnt_acc += 1.f;
-      if (lane == 0 && a.row_loss) a.row_loss[row] = l;
-      if (a.probs && lane < C) a.probs[(size_t)row * C + lane] = a.probs_are_logits ? v : p;
+    if (a.metrics) {
+      loss_acc = rows4_sum(loss_acc);
+      corr_acc = rows4_sum(corr_acc);
+      cnt_acc = rows4_sum(cnt_acc);
+      if (lane == 0 && cnt_acc > 0.f) {
+        atomicAdd(a.metrics + 0, loss_acc);
+        atomicAdd(a.metrics + 1, corr_acc);
+        atomicAdd(a.metrics + 2, cnt_acc);
+      }
     }
-    if (lane < C) dls[r * C + lane] = valid ? (p - (lane == label ? 1.f : 0.f)) * a.scale : 0.f;
-  }
-  if (a.metrics && lane == 0 && cnt_acc > 0.f) {
-    atomicAdd(a.metrics + 0, loss_acc);
-    atomicAdd(a.metrics + 1, corr_acc);
-    atomicAdd(a.metrics + 2, cnt_acc);
   }
   stamp(a.stamps, 2);
   if (!a.compute_grad) return;
   lds_barrier();
 
-  // dW2 = h^T . dl ; db2 = sum dl
-  if (a.dW2) {
-    for (int o = tid; o < H * C; o += 256) {
-      const int j = o / C, c = o - j * C;
-      float s = 0.f;
+  // ---- per wave w: dW2 rows [16w, 16w+16) of H and dH columns [16w, 16w+16)
+  for (int t = wave; t < Hp / 16; t += 4) {
+    // dW2[j][c] = sum_r h[r][j] * dl[r][c]   (A = h^T tile, B = dl)
+    f32x4 gw = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < R; ++r) s = fmaf(hs[r * H + j], dls[r * C + c], s);
-      atomicAdd(a.dW2 + o, s);
+    for (int k = 0; k < HR; k += 4) gw = mfma_f32(hs[(k + fq) * HST + t * 16 + fr], dls[(k + fq) * 16 + fr], gw);
+    if (a.dW2 && fr < C) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (t * 16 + fq * 4 + i < H) atomicAdd(a.dW2 + (size_t)(t * 16 + fq * 4 + i) * C + fr, gw[i]);
     }
+    // dH[r][j] = sum_c dl[r][c] * W2[j][c]   (A = dl, B = W2^T)
+    f32x4 gh = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 16; k += 4) gh = mfma_f32(dls[fr * 16 + k + fq], w2s[(t * 16 + fr) * 16 + k + fq], gh);
+    // lane holds dH[4*fq + i][16t + fr]
+    float colsum = 0.f;
+    const int j = t * 16 + fr;
+    const bool jok = j < H;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = fq * 4 + i, row = r0 + r;
+      float v = gh[i];
+      if (a.pre_relu && !(hs[r * HST + j] > 0.f)) v = 0.f;
+      if (row >= a.B) v = 0.f;
+      colsum += v;
+      if (row < a.B && jok) {
+        if (a.G) a.G[(size_t)row * a.ldg + j] = f2bf(v);
+        if (a.Gf) a.Gf[(size_t)row * a.ldgf + j] = v;
+      }
+      if (a.Gt && jok && row < a.ldgt) a.Gt[(size_t)j * a.ldgt + row] = f2bf(v);
+    }
+    colsum += __shfl_xor(colsum, 16, 64);
+    colsum += __shfl_xor(colsum, 32, 64);
+    if (a.dpre_bias && fq == 0 && jok) atomicAdd(a.dpre_bias + j, colsum);
   }
-  if (a.db2) {
-    for (int c = tid; c < C; c += 256) {
-      float s = 0.f;
-      for (int r = 0; r < R; ++r) s += dls[r * C + c];
-      atomicAdd(a.db2 + c, s);
-    }
-  }
-  // dH = dl . W2^T, through the ReLU mask of the previous epilogue.
-  for (int o = tid; o < R * H; o += 256) {
-    const int r = o / H, j = o - r * H, row = r0 + r;
-    float s = 0.f;
-    for (int c = 0; c < C; ++c) s = fmaf(dls[r * C + c], w2s[j * C + c], s);
-    if (a.pre_relu && !(hs[o] > 0.f)) s = 0.f;
-    dhs[o] = s;
-    if (row < a.B) {
-      if (a.G) a.G[(size_t)row * a.ldg + j] = f2bf(s);
-      if (a.Gf) a.Gf[(size_t)row * a.ldgf + j] = s;
-    }
-  }
-  lds_barrier();
-  if (a.Gt) {
-    // Transposed copy: consecutive threads walk rows -> coalesced along B.
-    for (int o = tid; o < R * H; o += 256) {
-      const int j = o / R, r = o - j * R, row = r0 + r;
-      if (row < a.ldgt) a.Gt[(size_t)j * a.ldgt + row] = f2bf(row < a.B ? dhs[r * H + j] : 0.f);
-    }
-  }
-  if (a.dpre_bias) {
-    for (int j = tid; j < H; j += 256) {
-      float s = 0.f;
-      for (int r = 0; r < R; ++r) s += dhs[r * H + j];
-      atomicAdd(a.dpre_bias + j, s);
-    }
+  if (a.db2 && wave == 0) {
+    float s = dls[fq * 4 * 16 + fr] + dls[(fq * 4 + 1) * 16 + fr] + dls[(fq * 4 + 2) * 16 + fr] +
+              dls[(fq * 4 + 3) * 16 + fr];
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    if (fq == 0 && fr < C) atomicAdd(a.db2 + fr, s);
   }
   stamp(a.stamps, 3);
 }
@@ -187,15 +216,15 @@ TDE_API int tde_head_xent(const float* hin, int ldh, const float* pre_bias, int 
                           int ldgf, float* metrics, float* probs, int probs_are_logits,
                           float* row_loss, int zero_hin, long long* iterations, long long* stamps,
                           hipStream_t stream) {
-  if (C > 64 || H * C > 16384 || H > 2048) return -1;
+  if (C > 16 || H > HMAX || H % 4 || (ldh & 3)) return -1;
+  if (((uintptr_t)hin | (uintptr_t)pre_bias) & 15) return -2;
   HeadArgs a{hin, ldh, pre_bias, pre_relu, W2, b2, labels, B, H, C, scale, compute_grad,
              dW2, db2, dpre_bias, (bf16*)G, ldg, (bf16*)Gt, ldgt, Gf, ldgf, metrics, probs,
              probs_are_logits, row_loss, zero_hin ? const_cast<float*>(hin) : nullptr, iterations, stamps};
   int rows = B;
   if (Gt && ldgt > rows) rows = ldgt;
-  int grid = (rows + kHeadRows - 1) / kHeadRows;
-  size_t lds = (size_t)(2 * kHeadRows * H + H * C + 2 * kHeadRows * C) * sizeof(float);
-  head_xent_kernel<<<grid, 256, lds, stream>>>(a);
+  const int grid = (rows + HR - 1) / HR;
+  head_xent_kernel<<<grid, 256, 0, stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;
 }

@@ -332,12 +332,13 @@ class Sequential(Model):
         return json.dumps({"class_name": "Sequential", "config": self.get_config()})
 
     @classmethod
-    def from_config(cls, cfg):
-        m = cls(name=None)
+    def from_config(cls, cfg, keep_names=True):
+        m = cls(name=cfg.get("name") if keep_names else None)
         first = True
         for lc in cfg["layers"]:
             c = dict(lc["config"])
-            c.pop("name", None)
+            if not keep_names:
+                c.pop("name", None)
             if first and cfg.get("input_shape"):
                 c["input_shape"] = tuple(cfg["input_shape"])
             first = False

@@ -1,0 +1,655 @@
+"""Estimator framework (call stacks §3.2/§3.3).
+
+Reference usage (mnist_keras_distributed.py:240-283, tf2_mnist_distributed.py:205-241):
+
+    run_config = RunConfig(experimental_distribute=DistributeConfig(
+                               train_distribute=ParameterServerStrategy(),
+                               eval_distribute=MirroredStrategy()),
+                           session_config=..., model_dir=D, save_summary_steps=100,
+                           log_step_count_steps=100, save_checkpoints_steps=500)
+    estimator = model_to_estimator(keras_model=model, model_dir=D, config=run_config)
+    train_spec = TrainSpec(input_fn=..., max_steps=468.75)
+    eval_spec = EvalSpec(input_fn=..., steps=None, name='mnist-eval',
+                         exporters=[FinalExporter('exporter', serving_input_fn)],
+                         start_delay_secs=10, throttle_secs=10)
+    train_and_evaluate(estimator, train_spec, eval_spec)
+
+Role dispatch on TF_CONFIG.task.type: ``ps`` serves variables forever; ``chief`` /
+``master`` / ``worker`` train (PS: async pull/compute/push; Mirrored/MWMS: sync
+all-reduce through the same HIP plans as Keras fit); the chief owns checkpoints
+and summaries; ``master`` (TF1) and local mode also evaluate on every new
+checkpoint (throttled) and run the exporters at the end; ``evaluator`` polls
+``model_dir`` for new checkpoints (communication through the filesystem, C8).
+
+Quirks handled: max_steps floats are ceil'ed (Q3); local mode is a
+well-defined chief (Q1); ``set_learning_phase(True)`` is honoured globally (Q4).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import math
+import os
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+from .. import backend as Kb
+from ..data.dataset import Dataset
+from ..io import events as EV
+from ..metrics import logs_from
+from ..parallel import cluster as CL
+from ..parallel import strategy as DS
+from . import checkpoint as CK
+from . import hooks as HK
+
+log = logging.getLogger("tensorflow_distributed_example_amd")
+
+
+class ModeKeys:
+    TRAIN = "train"
+    EVAL = "eval"
+    PREDICT = "infer"
+
+
+class DistributeConfig:
+    def __init__(self, train_distribute=None, eval_distribute=None, remote_cluster=None):
+        self.train_distribute = train_distribute
+        self.eval_distribute = eval_distribute
+        self.remote_cluster = remote_cluster
+
+
+class SessionConfig:
+    """tf.ConfigProto stand-in: device_filters (+ gpu memory fraction hint, MKD:170-174)."""
+
+    def __init__(self, device_filters=None, per_process_gpu_memory_fraction=None, **kw):
+        self.device_filters = list(device_filters) if device_filters else None
+        self.per_process_gpu_memory_fraction = per_process_gpu_memory_fraction
+
+
+def session_config_from_env():
+    """Port of _get_session_config_from_env_var (mnist_keras_distributed.py:165-189)."""
+    f = CL.device_filters()
+    return SessionConfig(device_filters=f) if f is not None else None
+
+
+class RunConfig:
+    def __init__(self, model_dir=None, tf_random_seed=None, save_summary_steps=100, save_checkpoints_steps=None,
+                 save_checkpoints_secs=None, session_config=None, keep_checkpoint_max=5,
+                 log_step_count_steps=100, train_distribute=None, eval_distribute=None,
+                 experimental_distribute=None, device_fn=None, steps_per_execution=None):
+        if save_checkpoints_steps is not None and save_checkpoints_secs is not None:
+            raise ValueError("can not provide both save_checkpoints_steps and save_checkpoints_secs")
+        if save_checkpoints_steps is None and save_checkpoints_secs is None:
+            save_checkpoints_secs = 600  # Estimator default
+        self.model_dir = model_dir
+        self.tf_random_seed = tf_random_seed
+        self.save_summary_steps = save_summary_steps
+        self.save_checkpoints_steps = save_checkpoints_steps
+        self.save_checkpoints_secs = save_checkpoints_secs
+        self.session_config = session_config
+        self.keep_checkpoint_max = keep_checkpoint_max
+        self.log_step_count_steps = log_step_count_steps
+        self.train_distribute = train_distribute
+        self.eval_distribute = eval_distribute
+        if experimental_distribute is not None:
+            self.train_distribute = experimental_distribute.train_distribute or self.train_distribute
+            self.eval_distribute = experimental_distribute.eval_distribute or self.eval_distribute
+        self.steps_per_execution = steps_per_execution
+        res = CL.TFConfigClusterResolver()
+        self.cluster_spec = res.cluster_spec()
+        self.task_type = res.task_type or ("chief" if not self.cluster_spec else None)
+        self.task_id = res.task_id
+        self.is_chief = CL.is_chief()
+        self.num_ps_replicas = self.cluster_spec.num_tasks("ps")
+        self.num_worker_replicas = max(1, self.cluster_spec.num_tasks("worker") +
+                                       self.cluster_spec.num_tasks("chief") + self.cluster_spec.num_tasks("master"))
+        self.master = res.master()
+        if session_config is not None and getattr(session_config, "per_process_gpu_memory_fraction", None):
+            if torch.cuda.is_available():
+                torch.cuda.set_per_process_memory_fraction(session_config.per_process_gpu_memory_fraction)
+
+    def replace(self, **kw):
+        import copy
+        c = copy.copy(self)
+        for k, v in kw.items():
+            setattr(c, k, v)
+        return c
+
+
+class TrainSpec:
+    def __init__(self, input_fn, max_steps=None, hooks=None):
+        if max_steps is not None and max_steps <= 0:
+            raise ValueError("max_steps must be positive")
+        self.input_fn = input_fn
+        self.max_steps = None if max_steps is None else int(math.ceil(max_steps))  # Q3
+        self.hooks = list(hooks or [])
+
+
+class EvalSpec:
+    def __init__(self, input_fn, steps=100, name=None, hooks=None, exporters=None, start_delay_secs=120,
+                 throttle_secs=600):
+        self.input_fn = input_fn
+        self.steps = steps
+        self.name = name
+        self.hooks = list(hooks or [])
+        if exporters is None:
+            exporters = []
+        elif not isinstance(exporters, (list, tuple)):
+            exporters = [exporters]
+        self.exporters = list(exporters)
+        self.start_delay_secs = start_delay_secs
+        self.throttle_secs = throttle_secs
+
+
+class EstimatorSpec:
+    def __init__(self, mode, predictions=None, loss=None, train_op=None, eval_metric_ops=None, export_outputs=None,
+                 **kw):
+        if mode == ModeKeys.PREDICT and predictions is None:
+            raise ValueError("PREDICT mode requires predictions")
+        if mode == ModeKeys.TRAIN and (loss is None or train_op is None):
+            raise ValueError("TRAIN mode requires loss and train_op")
+        if kw:
+            raise TypeError(f"unexpected EstimatorSpec arguments {sorted(kw)} (Q9: PREDICT takes no labels)")
+        self.mode, self.predictions, self.loss, self.train_op = mode, predictions, loss, train_op
+        self.eval_metric_ops, self.export_outputs = eval_metric_ops or {}, export_outputs
+
+
+def _as_dataset(input_fn):
+    ds = input_fn()
+    if not isinstance(ds, Dataset):
+        raise TypeError("input_fn must return a tde.data.Dataset")
+    return ds
+
+
+def _split(elem):
+    if isinstance(elem, tuple):
+        x, y = elem[0], (elem[1] if len(elem) > 1 else None)
+    else:
+        x, y = elem, None
+    if isinstance(x, dict):
+        x = next(iter(x.values()))
+    return x, y
+
+
+class _Ctx:
+    def __init__(self, est, prog, start_step, manager):
+        self.est = est
+        self.model = est.model
+        self.prog = prog
+        self.global_step = start_step
+        self.prev_step = start_step
+        self.start_step = start_step
+        self.manager_latest = manager.latest if manager else None
+        self.last_steps_per_sec = None
+        self._m0 = None
+
+    def interval_metrics(self, reset=False):
+        acc = self.prog.local_metrics() if self.prog is not None else None
+        if acc is None:
+            return {}
+        base = self._m0 if self._m0 is not None else acc * 0
+        logs = logs_from(acc - base, self.est.model._metric_names)
+        if reset:
+            self._m0 = acc.clone()
+        return logs
+
+
+class Estimator:
+    """Estimator over a Keras-style model (model_to_estimator) — train/evaluate/predict/export."""
+
+    def __init__(self, model, model_dir=None, config=None, params=None):
+        self.model = model
+        self.config = config or RunConfig()
+        self._model_dir = model_dir or self.config.model_dir or _tmp_model_dir()
+        self.config.model_dir = self._model_dir
+        self.params = params or {}
+        self.manager = CK.CheckpointManager(self._model_dir, self.config.keep_checkpoint_max)
+        self._summary_writer = None
+        self._ps_client = None
+
+    @property
+    def model_dir(self):
+        return self._model_dir
+
+    # ------------------------------------------------------------------ helpers
+    def _train_strategy(self):
+        return self.config.train_distribute or DS.get_strategy()
+
+    def _eval_strategy(self):
+        st = self.config.eval_distribute
+        from ..parallel.ps import ParameterServerStrategy
+        if st is None or isinstance(st, ParameterServerStrategy):
+            return DS.OneDeviceStrategy(Kb.default_device())
+        return st
+
+    def _writer(self, sub=None):
+        d = Path(self._model_dir) / (sub or "")
+        return EV.EventFileWriter(d)
+
+    def _bind(self, strategy):
+        m = self.model
+        if m._strategy is not strategy:
+            m._strategy = strategy
+            m._programs = {}
+
+    def latest_checkpoint(self):
+        return self.manager.latest
+
+    def get_variable_names(self):
+        p = self.latest_checkpoint()
+        from ..io import tensor_bundle as TB
+        return [n for n, *_ in TB.list_variables(p)] if p else []
+
+    def get_variable_value(self, name):
+        from ..io import tensor_bundle as TB
+        return TB.read_bundle(self.latest_checkpoint())[name]
+
+    # ------------------------------------------------------------------ train
+    def train(self, input_fn, hooks=None, steps=None, max_steps=None, saving_listeners=None):
+        from ..parallel.ps import ParameterServerStrategy
+        if max_steps is not None:
+            max_steps = int(math.ceil(max_steps))
+        st = self._train_strategy()
+        if isinstance(st, ParameterServerStrategy) and st.is_distributed:
+            return self._train_ps(st, input_fn, hooks, steps, max_steps, saving_listeners)
+        return self._train_sync(st, input_fn, hooks, steps, max_steps, saving_listeners)
+
+    def _start_step(self):
+        r = self.manager.restore(self.model)
+        return 0 if r is None else r[0]
+
+    def _std_hooks(self, chief, prog, saving_listeners):
+        cfg = self.config
+        hooks = []
+        if chief:
+            self._summary_writer = self._summary_writer or self._writer()
+            hooks.append(HK.StepCounterHook(cfg.log_step_count_steps, self._summary_writer))
+            hooks.append(HK.LoggingHook(cfg.log_step_count_steps))
+            hooks.append(HK.SummarySaverHook(cfg.save_summary_steps, self._summary_writer))
+            saver = HK.CheckpointSaverHook(self.manager, cfg.save_checkpoints_steps, cfg.save_checkpoints_secs,
+                                           saver_fn=self._saver_fn)
+            saver.listeners += list(saving_listeners or [])
+            hooks.append(saver)
+        return hooks
+
+    def _saver_fn(self, step):
+        return self.manager.save(self.model, step)
+
+    def _spe(self, hooks_intervals):
+        cfg = self.config
+        if cfg.steps_per_execution:
+            return int(cfg.steps_per_execution)
+        s = 16
+        for iv in hooks_intervals:
+            if iv:
+                while s > 1 and iv % s:
+                    s //= 2
+        return s
+
+    def _train_sync(self, strategy, input_fn, hooks, steps, max_steps, saving_listeners):
+        m = self.model
+        self._bind(strategy)
+        start = self._start_step()
+        if max_steps is not None and start >= max_steps:
+            log.info("Skipping training since max_steps has already saved.")
+            return self
+        target = max_steps if max_steps is not None else (start + steps if steps else None)
+        ds = _as_dataset(input_fn)
+        from ..train.engine import _global_batch_of
+        per_replica = _global_batch_of(ds)
+        if per_replica is None:
+            raise ValueError("input_fn must return a batched dataset")
+        R = strategy.num_local_replicas
+        gb = per_replica * strategy.num_replicas_in_sync
+        cfg = self.config
+        spe = self._spe([cfg.log_step_count_steps, cfg.save_summary_steps, cfg.save_checkpoints_steps])
+        m.steps_per_execution = spe
+        prog = m._program("train", gb)
+        prog.reset_metrics()
+        chief = strategy.is_chief and (self.config.is_chief if self.config.cluster_spec else True)
+        all_hooks = self._std_hooks(chief, prog, saving_listeners) + list(hooks or [])
+        ctx = _Ctx(self, prog, start, self.manager if chief else None)
+        for h in all_hooks:
+            h.begin(ctx)
+        it = iter(ds)
+        in_shape = prog.x_shape
+        step = start
+        done = False
+        while not done and (target is None or step < target):
+            n = spe if target is None else min(spe, target - step)
+            group = []
+            for _ in range(n):
+                per = []
+                for _r in range(R):
+                    try:
+                        e = next(it)
+                    except StopIteration:
+                        done = True
+                        break
+                    x, y = _split(e)
+                    per.append((np.asarray(x).reshape((len(y),) + tuple(in_shape)), np.asarray(y).reshape(-1)))
+                if done or len(per) < R:
+                    done = True
+                    break
+                group.append(per)
+            if not group:
+                break
+            for h in all_hooks:
+                if hasattr(h, "before_step"):
+                    h.before_step(ctx, step + 1)
+            if len(group) == prog.S and all(len(r[1]) == prog.B for g in group for r in g):
+                from ..train.engine import _stack_steps
+                prog.stage(_stack_steps(group))
+                prog.run()
+            else:
+                for g in group:
+                    prog.run_single(g, sum(len(r[1]) for r in g) * strategy.num_workers)
+            ctx.prev_step = step
+            step += len(group)
+            ctx.global_step = step
+            for h in all_hooks:
+                h.after_step(ctx)
+        prog.sync()
+        for h in all_hooks:
+            h.end(ctx)
+        m.optimizer.iterations = step
+        return self
+
+    # ------------------------------------------------------------------ PS training (async)
+    def _ps_client(self, strategy):
+        if self._ps_client is None:
+            m = self.model
+            m._require_built()
+            shapes = {n: tuple(m._store.segments[n].shape) for n in m._store.order}
+            self._ps_client = strategy.client(shapes)
+            from ..optimizers import KIND
+            self._ps_client.set_optimizer(min(m.optimizer.kind_id, 2), getattr(m.optimizer, "momentum", 0.0))
+        return self._ps_client
+
+    def _train_ps(self, strategy, input_fn, hooks, steps, max_steps, saving_listeners):
+        """Between-graph async PS loop: pull -> fwd/bwd on the local GPU -> push; global_step on the PS."""
+        m = self.model
+        self._bind(DS.OneDeviceStrategy(Kb.default_device()))
+        client = self._ps_client(strategy)
+        chief = strategy.is_chief
+        if chief:
+            r = self.manager.restore(m)
+            client.initialize(m.state_dict(), is_chief=True)
+            if r is not None:
+                gs = client.global_step()
+                if gs < r[0]:
+                    client.step_add(r[0] - gs)
+        else:
+            client.initialize(None, is_chief=False)
+        ds = _as_dataset(input_fn)
+        from ..train.engine import _global_batch_of
+        B = _global_batch_of(ds)
+        m.steps_per_execution = 1
+        opt_saved = m.optimizer
+        prog = m._program("eval", B)           # buffers + kernels; the PS applies the update
+        prog.plans = [self._ps_plan(B)]
+        plan = prog.plans[0]
+        store = plan.store
+        target = max_steps
+        gstep = client.global_step()
+        ctx = _Ctx(self, prog, gstep, self.manager if chief else None)
+        all_hooks = (self._std_hooks(chief, prog, saving_listeners) if chief else []) + list(hooks or [])
+        if chief:
+            for h in all_hooks:
+                if isinstance(h, HK.CheckpointSaverHook):
+                    h.saver_fn = lambda step: self._ps_save(client, step)
+        for h in all_hooks:
+            h.begin(ctx)
+        it = iter(ds)
+        names_bn = [n for n in store.names(trainable=False)]
+        lr = float(opt_saved.learning_rate)
+        while target is None or gstep < target:
+            try:
+                e = next(it)
+            except StopIteration:
+                break
+            x, y = _split(e)
+            x = np.asarray(x, dtype=np.float32).reshape((len(y),) + tuple(prog.x_shape))
+            y = np.asarray(y).reshape(-1)
+            vals = client.pull()
+            old_state = {n: vals[n].copy() for n in names_bn}
+            m._store.load_dict(vals)
+            plan.on_weights_loaded()
+            n = len(y)
+            prog.x_stage[0].stage(x, prog.x_ring[0][0])
+            prog.y_stage[0].stage(y, prog.y_ring[0][0])
+            plan.scale = 1.0 / n
+            plan.train_step(prog.x_ring[0][0], prog.y_ring[0][0], n)
+            grads = {k: store.grad(k).detach().cpu().numpy() for k in store.names(trainable=True)}
+            store.g.zero_()
+            client.push(grads, lr)
+            if names_bn:
+                # the local step applied m*old + (1-m)*batch; recover the batch statistic and let the PS
+                # apply the moving average to ITS current value (no lost updates between async workers)
+                mom = {}
+                for n_ in names_bn:
+                    layer = n_.split("/")[0]
+                    mm = next(l.momentum for l in m.layers if l.name == layer)
+                    new = store.view(n_).detach().cpu().numpy()
+                    mom.setdefault(mm, {})[n_] = (new - mm * old_state[n_]) / (1.0 - mm)
+                for mm, dct in mom.items():
+                    client.moving_avg(dct, mm)
+            ctx.prev_step = gstep
+            gstep = client.step_add(1)
+            ctx.global_step = gstep
+            for h in all_hooks:
+                h.after_step(ctx)
+        if chief:
+            m._store.load_dict(client.pull())
+        for h in all_hooks:
+            h.end(ctx)
+        return self
+
+    def _ps_plan(self, B):
+        from . import program as PG
+        m = self.model
+        return PG.make_plan(m, m._store, m._store.device, B, B, None, m.loss)
+
+    def _ps_save(self, client, step):
+        self.model._store.load_dict(client.pull())
+        return self.manager.save(self.model, step)
+
+    # ------------------------------------------------------------------ evaluate / predict
+    def evaluate(self, input_fn, steps=None, hooks=None, checkpoint_path=None, name=None):
+        m = self.model
+        st = self._eval_strategy()
+        self._bind(st)
+        ck = checkpoint_path or self.latest_checkpoint()
+        step = 0
+        if ck is not None:
+            step = self.manager.restore(m, ck)[0]
+        ds = _as_dataset(input_fn)
+        from ..train.engine import _global_batch_of
+        per_replica = _global_batch_of(ds) or 32
+        R = st.num_local_replicas
+        prog = m._program("eval", per_replica * st.num_replicas_in_sync)
+        prog.on_weights_loaded()
+        prog.reset_metrics()
+        it = iter(ds)
+        n = 0
+        while steps is None or n < steps:
+            per = []
+            for _ in range(R):
+                try:
+                    e = next(it)
+                except StopIteration:
+                    break
+                x, y = _split(e)
+                per.append((np.asarray(x, dtype=np.float32).reshape((len(y),) + tuple(prog.x_shape)),
+                            np.asarray(y).reshape(-1)))
+            if not per:
+                break
+            while len(per) < R:
+                per.append((per[0][0][:0], per[0][1][:0]))
+            prog.eval_batch(per)
+            n += 1
+        logs = logs_from(prog.global_metrics(), m._metric_names)
+        logs["global_step"] = step
+        sub = f"eval_{name}" if name else "eval"
+        w = self._writer(sub)
+        w.add_scalars(step, {k: v for k, v in logs.items() if k != "global_step"})
+        w.close()
+        log.info("Saving dict for global step %d: %s", step,
+                 ", ".join(f"{k} = {v:g}" for k, v in logs.items()))
+        return logs
+
+    def predict(self, input_fn, predict_keys=None, checkpoint_path=None, yield_single_examples=True):
+        m = self.model
+        ck = checkpoint_path or self.latest_checkpoint()
+        if ck is not None:
+            self.manager.restore(m, ck)
+        for e in _as_dataset(input_fn):
+            x, _ = _split(e)
+            out = m.predict(np.asarray(x, dtype=np.float32), batch_size=len(x))
+            key = m.layers[-1].name
+            if yield_single_examples:
+                for row in out:
+                    yield {key: row}
+            else:
+                yield {key: out}
+
+    # ------------------------------------------------------------------ export
+    def export_saved_model(self, export_dir_base, serving_input_receiver_fn, checkpoint_path=None, **kw):
+        from ..io import export as EX
+        ck = checkpoint_path or self.latest_checkpoint()
+        if ck is not None:
+            self.manager.restore(self.model, ck)
+        return EX.export_saved_model(self.model, export_dir_base, serving_input_receiver_fn)
+
+    export_savedmodel = export_saved_model
+
+
+def _tmp_model_dir():
+    import tempfile
+    return tempfile.mkdtemp(prefix="tde_model_")
+
+
+def model_to_estimator(keras_model=None, keras_model_path=None, custom_objects=None, model_dir=None, config=None,
+                       checkpoint_format="checkpoint"):
+    """Wrap a compiled Keras-style model (mnist_keras_distributed.py:118-119).  Like TF, the
+    initial Keras weights are saved under model_dir/keras/ for warm start."""
+    if keras_model is None:
+        raise ValueError("keras_model is required")
+    if keras_model.optimizer is None:
+        raise ValueError("the model must be compiled before model_to_estimator")
+    keras_model._require_built()
+    est = Estimator(keras_model, model_dir=model_dir, config=config)
+    kdir = Path(est.model_dir) / "keras"
+    if est.config.is_chief:
+        kdir.mkdir(parents=True, exist_ok=True)
+        keras_model.save_weights(str(kdir / "keras_model.ckpt"))
+    return est
+
+
+# ---------------------------------------------------------------------------------------- train_and_evaluate
+def train_and_evaluate(estimator, train_spec, eval_spec):
+    cfg = estimator.config
+    role = cfg.task_type if cfg.cluster_spec else None
+    if role == "ps":
+        from ..parallel.ps import run_ps_server
+        addr = cfg.cluster_spec.task_address("ps", cfg.task_id)
+        run_ps_server(addr)
+        return None, None
+    if role == "evaluator":
+        return _run_evaluator(estimator, train_spec, eval_spec)
+    if role in (None, "master"):
+        return _run_local(estimator, train_spec, eval_spec)
+    # chief / worker: train only (evaluation belongs to the evaluator task)
+    estimator.train(train_spec.input_fn, hooks=train_spec.hooks, max_steps=train_spec.max_steps)
+    return None, None
+
+
+def _run_local(estimator, train_spec, eval_spec):
+    """Local / TF1-master mode: train, evaluate after each (throttled) checkpoint, export at the end."""
+    last_eval = [0.0]
+    results = [None]
+
+    def on_save(ctx, path):
+        now = time.time()
+        if ctx.global_step == 0:
+            return
+        if now - last_eval[0] >= eval_spec.throttle_secs:
+            last_eval[0] = now
+            results[0] = estimator.evaluate(eval_spec.input_fn, steps=eval_spec.steps, name=eval_spec.name,
+                                            checkpoint_path=path, hooks=eval_spec.hooks)
+            _rebind_train(estimator)
+
+    estimator.train(train_spec.input_fn, hooks=train_spec.hooks, max_steps=train_spec.max_steps,
+                    saving_listeners=[on_save])
+    final = estimator.evaluate(eval_spec.input_fn, steps=eval_spec.steps, name=eval_spec.name, hooks=eval_spec.hooks)
+    exports = [ex.export(estimator, os.path.join(estimator.model_dir, "export", ex.name),
+                         estimator.latest_checkpoint(), final, True) for ex in eval_spec.exporters]
+    return final, exports
+
+
+def _rebind_train(estimator):
+    estimator._bind(estimator._train_strategy() if not _is_ps(estimator) else DS.OneDeviceStrategy(Kb.default_device()))
+
+
+def _is_ps(estimator):
+    from ..parallel.ps import ParameterServerStrategy
+    return isinstance(estimator._train_strategy(), ParameterServerStrategy)
+
+
+def _run_evaluator(estimator, train_spec, eval_spec):
+    time.sleep(eval_spec.start_delay_secs)
+    last, result, exports = None, None, []
+    while True:
+        t0 = time.time()
+        ck = CK.wait_for_new_checkpoint(estimator.model_dir, last, timeout=None)
+        last = ck
+        result = estimator.evaluate(eval_spec.input_fn, steps=eval_spec.steps, name=eval_spec.name,
+                                    checkpoint_path=ck, hooks=eval_spec.hooks)
+        if train_spec.max_steps is not None and result["global_step"] >= train_spec.max_steps:
+            exports = [ex.export(estimator, os.path.join(estimator.model_dir, "export", ex.name), ck, result, True)
+                       for ex in eval_spec.exporters]
+            return result, exports
+        wait = eval_spec.throttle_secs - (time.time() - t0)
+        if wait > 0:
+            time.sleep(wait)
+
+
+# ---------------------------------------------------------------------------------------- exporters
+class Exporter:
+    name = "exporter"
+
+    def export(self, estimator, export_path, checkpoint_path, eval_result, is_the_final_export):
+        raise NotImplementedError
+
+
+class FinalExporter(Exporter):
+    """Exports once, after the final evaluation (mnist_keras_distributed.py:264)."""
+
+    def __init__(self, name, serving_input_receiver_fn, assets_extra=None, as_text=False):
+        self.name = name
+        self.serving_input_receiver_fn = serving_input_receiver_fn
+
+    def export(self, estimator, export_path, checkpoint_path, eval_result, is_the_final_export):
+        if not is_the_final_export:
+            return None
+        return estimator.export_saved_model(export_path, self.serving_input_receiver_fn,
+                                            checkpoint_path=checkpoint_path)
+
+
+class LatestExporter(FinalExporter):
+    def __init__(self, name, serving_input_receiver_fn, exports_to_keep=5, **kw):
+        super().__init__(name, serving_input_receiver_fn)
+        self.exports_to_keep = exports_to_keep
+
+    def export(self, estimator, export_path, checkpoint_path, eval_result, is_the_final_export):
+        out = estimator.export_saved_model(export_path, self.serving_input_receiver_fn,
+                                           checkpoint_path=checkpoint_path)
+        base = Path(export_path)
+        dirs = sorted([d for d in base.iterdir() if d.is_dir()], key=lambda d: d.name)
+        import shutil
+        for d in dirs[:-self.exports_to_keep]:
+            shutil.rmtree(d, ignore_errors=True)
+        return out

@@ -21,6 +21,32 @@ def _model(tde, lr=0.05, spe=1):
     return m
 
 
+def test_fused_step_gradients_match_reference():
+    """One training step: per-variable gradients of the fused HIP plan vs torch fp32 autograd."""
+    import torch
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.train import program as PG
+    x, y = _data(64, 5)
+    m = _model(tde)
+    m.build()
+    st = m._store
+    st_ref = st.clone_to("cuda")
+    fused = PG.make_plan(m, st, "cuda", 64, 64, m.optimizer, m.loss)
+    ref = PG.ReferencePlan(m, st_ref, "cuda", 64, 64, m.optimizer, m.loss)
+    assert fused.kind == "fused_convnet"
+    xt = torch.from_numpy(x).cuda()
+    yt = torch.from_numpy(y).int().cuda()
+    fused.train_step(xt, yt)
+    ref.train_step(xt, yt.long())
+    torch.cuda.synchronize()
+    for name in st.names(trainable=True):
+        gf, gr = st.grad(name).double(), st_ref.grad(name).double()
+        rel = ((gf - gr).norm() / (gr.norm() + 1e-12)).item()
+        assert rel < 0.03, (name, rel)
+    lf, lr_ = tde.metrics.logs_from(fused.metrics, ["accuracy"]), tde.metrics.logs_from(ref.metrics, ["accuracy"])
+    assert abs(lf["loss"] - lr_["loss"]) < 5e-3 and abs(lf["accuracy"] - lr_["accuracy"]) < 0.05
+
+
 def test_fused_plan_matches_reference(monkeypatch):
     import tensorflow_distributed_example_amd as tde
     x, y = _data(64 * 6)
@@ -35,9 +61,12 @@ def test_fused_plan_matches_reference(monkeypatch):
     monkeypatch.setenv("TDE_EXECUTOR", "reference")
     hr = mr.fit(x, y, batch_size=64, epochs=1, shuffle=False, verbose=0)
     assert mr._program("train", 64).plan_kind == "reference"
-    for a, b in zip(mf.get_weights(), mr.get_weights()):
-        scale = np.abs(b).max() + 1e-6
-        assert np.abs(a - b).max() / scale < 2e-2, np.abs(a - b).max()
+    # bf16 MFMA compute (mixed_bfloat16) vs an fp32 reference: compare the weight UPDATES by norm.
+    # Bias gradients are sums with heavy cancellation, so they get a looser bound than kernels.
+    for name, a, b, w in zip(mf.variable_names(), mf.get_weights(), mr.get_weights(), w0):
+        da, db = a - w, b - w
+        rel = np.linalg.norm(da - db) / (np.linalg.norm(db) + 1e-12)
+        assert rel < (0.05 if name.endswith("kernel") else 0.2), (name, rel)
     assert abs(hf.history["loss"][0] - hr.history["loss"][0]) < 2e-2
     assert abs(hf.history["accuracy"][0] - hr.history["accuracy"][0]) < 0.05
 
