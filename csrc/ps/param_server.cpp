@@ -35,7 +35,8 @@ struct PSServer {
   std::atomic<bool> stop{false};
   std::mutex mu;  // guards the map
   std::map<std::string, std::unique_ptr<Var>> vars;
-  std::atomic<int64_t> step{0};
+  std::atomic<int64_t> step{0};          // counter 0: global_step
+  std::atomic<int64_t> counters[3]{};     // counters 1..3: tickets etc.
   std::atomic<int64_t> pushes{0}, pulls{0};
   int kind = 0;  // 0 sgd, 1 momentum, 2 nesterov
   float momentum = 0.f;
@@ -163,8 +164,10 @@ struct PSServer {
           break;
         }
         case kStepAdd: {
+          const uint32_t idx = r.u32();
           int64_t d = r.i64();
-          int64_t nv = step.fetch_add(d) + d;
+          std::atomic<int64_t>& c = idx == 0 ? step : counters[(idx - 1) % 3];
+          int64_t nv = c.fetch_add(d) + d;
           w.u8(0);
           w.i64(nv);
           break;
@@ -353,9 +356,10 @@ TDE_API int tde_ps_assign(void* h, const char* name, const float* data, long lon
   return resp[0];
 }
 
-TDE_API long long tde_ps_step_add(void* h, long long d) {
+TDE_API long long tde_ps_counter_add(void* h, int idx, long long d) {
   tde_net::Writer w;
   w.u8(kStepAdd);
+  w.u32((uint32_t)idx);
   w.i64(d);
   std::string resp;
   if (!((PSClient*)h)->call(w.s, &resp)) return INT64_MIN;
@@ -363,6 +367,8 @@ TDE_API long long tde_ps_step_add(void* h, long long d) {
   r.u8();
   return r.i64();
 }
+
+TDE_API long long tde_ps_step_add(void* h, long long d) { return tde_ps_counter_add(h, 0, d); }
 
 TDE_API long long tde_ps_step_get(void* h) {
   tde_net::Writer w;

@@ -47,6 +47,7 @@ N.register_host({
     "tde_ps_assign": (C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_longlong]),
     "tde_ps_step_add": (C.c_longlong, [C.c_void_p, C.c_longlong]),
     "tde_ps_step_get": (C.c_longlong, [C.c_void_p]),
+    "tde_ps_counter_add": (C.c_longlong, [C.c_void_p, C.c_int, C.c_longlong]),
     "tde_ps_set_optimizer": (C.c_int, [C.c_void_p, C.c_int, C.c_float]),
     "tde_ps_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
 })
@@ -186,6 +187,11 @@ class PSClient:
     def step_add(self, d=1) -> int:
         c = self.conns[0]
         return int(c.lib.tde_ps_step_add(c.h, int(d)))
+
+    def counter_add(self, idx, d=1) -> int:
+        """Atomic add on PS counter ``idx`` (0 = global_step, 1 = step tickets); returns the new value."""
+        c = self.conns[0]
+        return int(c.lib.tde_ps_counter_add(c.h, int(idx), int(d)))
 
     def global_step(self) -> int:
         c = self.conns[0]

@@ -208,7 +208,7 @@ class Estimator:
         self.params = params or {}
         self.manager = CK.CheckpointManager(self._model_dir, self.config.keep_checkpoint_max)
         self._summary_writer = None
-        self._ps_client = None
+        self._psc = None
 
     @property
     def model_dir(self):
@@ -360,14 +360,14 @@ class Estimator:
 
     # ------------------------------------------------------------------ PS training (async)
     def _ps_client(self, strategy):
-        if self._ps_client is None:
+        if self._psc is None:
             m = self.model
             m._require_built()
             shapes = {n: tuple(m._store.segments[n].shape) for n in m._store.order}
-            self._ps_client = strategy.client(shapes)
+            self._psc = strategy.client(shapes)
             from ..optimizers import KIND
-            self._ps_client.set_optimizer(min(m.optimizer.kind_id, 2), getattr(m.optimizer, "momentum", 0.0))
-        return self._ps_client
+            self._psc.set_optimizer(min(m.optimizer.kind_id, 2), getattr(m.optimizer, "momentum", 0.0))
+        return self._psc
 
     def _train_ps(self, strategy, input_fn, hooks, steps, max_steps, saving_listeners):
         """Between-graph async PS loop: pull -> fwd/bwd on the local GPU -> push; global_step on the PS."""
@@ -377,11 +377,16 @@ class Estimator:
         chief = strategy.is_chief
         if chief:
             r = self.manager.restore(m)
-            client.initialize(m.state_dict(), is_chief=True)
             if r is not None:
                 gs = client.global_step()
                 if gs < r[0]:
                     client.step_add(r[0] - gs)
+            # step tickets (counter 1) start at the global step: a worker claims a ticket BEFORE computing a
+            # step and stops when the ticket passes max_steps, so async workers never overshoot
+            gs, t = client.global_step(), client.counter_add(1, 0)
+            if t < gs:
+                client.counter_add(1, gs - t)
+            client.initialize(m.state_dict(), is_chief=True)
         else:
             client.initialize(None, is_chief=False)
         ds = _as_dataset(input_fn)
@@ -393,8 +398,8 @@ class Estimator:
         prog.plans = [self._ps_plan(B)]
         plan = prog.plans[0]
         store = plan.store
-        target = max_steps
         gstep = client.global_step()
+        target = max_steps if max_steps is not None else (gstep + steps if steps is not None else None)
         ctx = _Ctx(self, prog, gstep, self.manager if chief else None)
         all_hooks = (self._std_hooks(chief, prog, saving_listeners) if chief else []) + list(hooks or [])
         if chief:
@@ -407,6 +412,8 @@ class Estimator:
         names_bn = [n for n in store.names(trainable=False)]
         lr = float(opt_saved.learning_rate)
         while target is None or gstep < target:
+            if max_steps is not None and client.counter_add(1, 1) > max_steps:
+                break
             try:
                 e = next(it)
             except StopIteration:
@@ -423,7 +430,7 @@ class Estimator:
             prog.y_stage[0].stage(y, prog.y_ring[0][0])
             plan.scale = 1.0 / n
             plan.train_step(prog.x_ring[0][0], prog.y_ring[0][0], n)
-            grads = {k: store.grad(k).detach().cpu().numpy() for k in store.names(trainable=True)}
+            grads = {k: store.grad(k).detach().cpu().numpy().copy() for k in store.names(trainable=True)}
             store.g.zero_()
             client.push(grads, lr)
             if names_bn:

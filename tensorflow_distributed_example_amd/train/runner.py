@@ -188,7 +188,7 @@ class Program:
         with _ctx(self.devices[0]):
             self.x_stage[0].stage(x, self.x_ring[0][0])
             out = self.plans[0].predict(self.x_ring[0][0], n)
-            return out[:n].float().cpu().numpy()
+            return out[:n].float().cpu().numpy().copy()
 
     # ------------------------------------------------------------------ metrics
     def reset_metrics(self):
