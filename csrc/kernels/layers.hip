@@ -1,0 +1,1122 @@
+// Layer-wise gfx950 kernel library: every Conv2D / Dense / BatchNormalization /
+// Activation / Dropout / MaxPooling2D / GlobalAveragePooling2D / ZeroPadding2D /
+// Add layer of a Keras model (Model B of mnist_keras_distributed.py:79-109 ==
+// tf2_mnist_distributed.py:105-135, the ResNet-18 stress config, and any other
+// Sequential / functional model built from those layers).
+//
+// * igemm: ONE implicit-GEMM MFMA kernel family for Conv2D fwd / bwd-data /
+//   bwd-filter and Dense fwd / bwd-data / bwd-weight.  C[M,N] = sum_k A(m,k) B(k,n)
+//   where A and B are *gathered* (im2col never materialised) straight from the
+//   NHWC bf16 activations / HWIO bf16 weight shadows into LDS:
+//       kind            A(m,k)                           B(k,n)
+//       dense fwd/dgrad X[m*lda+k]            (A_ROWK)   Wt[n*ldb+k]         (B_NK)
+//       conv fwd        X[b,oh*s-p+kh,..,ci]  (A_CONV)   Wt[co][kh,kw,ci]    (B_NK)
+//       conv dgrad      dY[b,(ih+p-kh)/s,..]  (A_DGRAD)  W[kh,kw,n,co]       (B_DGRADW)
+//       dense wgrad     X[k*lda+m]            (A_COLM)   dY[k*ldb+n]         (B_KN)
+//       conv wgrad      X[b,oh*s-p+kh,..,ci]  (A_WGRAD)  dY[p*Co+n]          (B_KN)
+//   Tiles are 64x64x32 (4 waves of 32x32 = 2x2 MFMA 16x16x32 bf16), operands are
+//   double-buffered through LDS (global loads of tile k+1 in flight while tile k
+//   feeds the matrix cores, one barrier per k-step).  K-contiguous operands move
+//   as 16-byte vectors; M/N-contiguous ones (weight grads) are loaded as 16-byte
+//   vectors along M/N and transposed on the LDS write.  The epilogue fuses bias,
+//   ReLU, bf16 store (or +=, for tensors with several consumers), f32 store /
+//   split-K atomics (weight grads), and the per-channel sum / sum-of-squares that
+//   the following BatchNormalization needs (DPP/shuffle column reduction + one
+//   atomic per column per wave) — the BN statistics never re-read the activation.
+// * bn_fwd: batch-stat (or moving-stat) affine + residual add + ReLU + Philox
+//   dropout in one pass; block 0 also updates the moving statistics (Keras
+//   momentum semantics, Bessel-corrected variance for 4-D input) and zeroes the
+//   backward accumulators of the same layer.  Dropout masks are never stored:
+//   the backward regenerates them from the counter-based Philox stream.
+// * bn_bwd_reduce / bn_bwd_apply: BN + ReLU + dropout backward (per-channel
+//   reductions in LDS, then the dx / residual-grad / dgamma / dbeta pass).
+// * maxpool (argmax bytes, gather backward), global average pool, zero-padding,
+//   bias/ReLU backward with the bias-grad column sum, and a general softmax
+//   cross-entropy (+accuracy, +dlogits, +probabilities) for any class count.
+#include "tde_common.h"
+
+namespace tde {
+
+struct Geo {  // NHWC input [B,H,W,C], HWIO kernel [KH,KW,C,Co], NHWC output [B,Ho,Wo,Co]
+  int B, H, W, C, Ho, Wo, Co, KH, KW, sh, sw, pt, pl;
+};
+
+enum AKind { A_ROWK = 0, A_CONV = 1, A_DGRAD = 2, A_COLM = 3, A_WGRAD = 4 };
+enum BKind { B_NK = 0, B_DGRADW = 1, B_KN = 2 };
+
+struct IGemmArgs {
+  const bf16* a;
+  long long lda;
+  const bf16* b;
+  long long ldb;
+  int M, N, K;
+  int ktiles_per_split;
+  Geo g;
+  int avec, bvec;
+  float* cf;
+  long long ldc;
+  int cf_mode;  // 0 none, 1 store, 2 atomic add
+  float alpha;
+  bf16* cb;
+  long long ldcb;
+  int cb_accum;
+  const float* bias;
+  int relu;
+  float* colstats;  // [2][N]
+};
+
+constexpr int TM = 64, TN = 64, TK = 32, LDK = TK + 8;
+
+__device__ __forceinline__ bf16x8 zero8() {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (bf16)0.0f;
+  return r;
+}
+
+// ---- A(m, k) for the K-vector kinds: the thread's row m is fixed for the whole K loop.
+struct ARow {
+  bool ok;
+  long long base;  // ROWK: m*lda
+  int b, y0, x0;   // CONV: b, oh*sh-pt, ow*sw-pl ; DGRAD: b, ih+pt, iw+pl
+};
+
+template <int AK>
+__device__ __forceinline__ ARow a_row(const IGemmArgs& p, int m) {
+  ARow r;
+  r.ok = m < p.M;
+  const int mm = r.ok ? m : 0;
+  r.base = 0;
+  r.b = r.y0 = r.x0 = 0;
+  if (AK == A_ROWK) {
+    r.base = (long long)mm * p.lda;
+  } else if (AK == A_CONV) {
+    const int hw = p.g.Ho * p.g.Wo;
+    const int b = mm / hw, rem = mm - b * hw;
+    const int oh = rem / p.g.Wo, ow = rem - oh * p.g.Wo;
+    r.b = b;
+    r.y0 = oh * p.g.sh - p.g.pt;
+    r.x0 = ow * p.g.sw - p.g.pl;
+  } else {  // A_DGRAD: m over input pixels
+    const int hw = p.g.H * p.g.W;
+    const int b = mm / hw, rem = mm - b * hw;
+    const int ih = rem / p.g.W, iw = rem - ih * p.g.W;
+    r.b = b;
+    r.y0 = ih + p.g.pt;
+    r.x0 = iw + p.g.pl;
+  }
+  return r;
+}
+
+// element index of A(m,k) (or -1 = zero) for the K-vector kinds
+template <int AK>
+__device__ __forceinline__ long long a_idx(const IGemmArgs& p, const ARow& r, int k) {
+  if (!r.ok || k >= p.K) return -1;
+  if (AK == A_ROWK) return r.base + k;
+  if (AK == A_CONV) {
+    const int C = p.g.C;
+    const int kc = k / C, ci = k - kc * C;
+    const int kh = kc / p.g.KW, kw = kc - kh * p.g.KW;
+    const int ih = r.y0 + kh, iw = r.x0 + kw;
+    if ((unsigned)ih >= (unsigned)p.g.H || (unsigned)iw >= (unsigned)p.g.W) return -1;
+    return (((long long)r.b * p.g.H + ih) * p.g.W + iw) * C + ci;
+  }
+  // A_DGRAD: k = (kh, kw, co) ; oh = (ih + pt - kh) / sh must be exact and in range
+  const int Co = p.g.Co;
+  const int kc = k / Co, co = k - kc * Co;
+  const int kh = kc / p.g.KW, kw = kc - kh * p.g.KW;
+  const int ty = r.y0 - kh, tx = r.x0 - kw;
+  if (ty < 0 || tx < 0) return -1;
+  const int oh = ty / p.g.sh, ow = tx / p.g.sw;
+  if (oh * p.g.sh != ty || ow * p.g.sw != tx || oh >= p.g.Ho || ow >= p.g.Wo) return -1;
+  return (((long long)r.b * p.g.Ho + oh) * p.g.Wo + ow) * Co + co;
+}
+
+template <int AK>
+__device__ __forceinline__ bf16x8 load_a_k8(const IGemmArgs& p, const ARow& r, int k) {
+  if (p.avec) {
+    const long long i = a_idx<AK>(p, r, k);  // 8 consecutive k share (kh,kw) when C%8==0
+    if (i < 0) return zero8();
+    return *reinterpret_cast<const bf16x8*>(p.a + i);
+  }
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const long long i = a_idx<AK>(p, r, k + j);
+    v[j] = i < 0 ? (bf16)0.0f : p.a[i];
+  }
+  return v;
+}
+
+// ---- B(k, n) for the K-vector kinds (row = n)
+__device__ __forceinline__ long long b_idx_k(const IGemmArgs& p, int BK_, int n, int k) {
+  if (n >= p.N || k >= p.K) return -1;
+  if (BK_ == B_NK) return (long long)n * p.ldb + k;
+  // B_DGRADW: k = (kh,kw,co), n = ci  ->  W[kh][kw][ci][co]
+  const int Co = p.g.Co;
+  const int kc = k / Co, co = k - kc * Co;
+  return ((long long)kc * p.g.C + n) * Co + co;
+}
+
+template <int BK_>
+__device__ __forceinline__ bf16x8 load_b_k8(const IGemmArgs& p, int n, int k) {
+  if (p.bvec) {
+    const long long i = b_idx_k(p, BK_, n, k);
+    if (i < 0) return zero8();
+    return *reinterpret_cast<const bf16x8*>(p.b + i);
+  }
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const long long i = b_idx_k(p, BK_, n, k + j);
+    v[j] = i < 0 ? (bf16)0.0f : p.b[i];
+  }
+  return v;
+}
+
+// ---- M-vector kinds: 8 consecutive rows m0..m0+7 at one k
+struct ACol {
+  int kh, kw, ci;  // WGRAD: decomposition of the first row
+};
+
+__device__ __forceinline__ long long wgrad_idx(const IGemmArgs& p, int m, int k) {
+  // A_WGRAD: m = (kh,kw,ci), k = pixel p = (b,oh,ow)
+  if (m >= p.M || k >= p.K) return -1;
+  const int C = p.g.C;
+  const int kc = m / C, ci = m - kc * C;
+  const int kh = kc / p.g.KW, kw = kc - kh * p.g.KW;
+  const int hw = p.g.Ho * p.g.Wo;
+  const int b = k / hw, rem = k - b * hw;
+  const int oh = rem / p.g.Wo, ow = rem - oh * p.g.Wo;
+  const int ih = oh * p.g.sh - p.g.pt + kh, iw = ow * p.g.sw - p.g.pl + kw;
+  if ((unsigned)ih >= (unsigned)p.g.H || (unsigned)iw >= (unsigned)p.g.W) return -1;
+  return (((long long)b * p.g.H + ih) * p.g.W + iw) * C + ci;
+}
+
+template <int AK>
+__device__ __forceinline__ bf16x8 load_a_m8(const IGemmArgs& p, int m, int k) {
+  if (AK == A_COLM) {
+    if (k >= p.K || m >= p.M) return zero8();
+    const long long i = (long long)k * p.lda + m;
+    if (p.avec) return *reinterpret_cast<const bf16x8*>(p.a + i);
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (m + j < p.M) ? p.a[i + j] : (bf16)0.0f;
+    return v;
+  }
+  if (p.avec) {
+    const long long i = wgrad_idx(p, m, k);
+    if (i < 0) return zero8();
+    return *reinterpret_cast<const bf16x8*>(p.a + i);
+  }
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const long long i = wgrad_idx(p, m + j, k);
+    v[j] = i < 0 ? (bf16)0.0f : p.a[i];
+  }
+  return v;
+}
+
+__device__ __forceinline__ bf16x8 load_b_n8(const IGemmArgs& p, int n, int k) {
+  // B_KN: B(k, n) = b[k*ldb + n]
+  if (k >= p.K || n >= p.N) return zero8();
+  const long long i = (long long)k * p.ldb + n;
+  if (p.bvec) return *reinterpret_cast<const bf16x8*>(p.b + i);
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (n + j < p.N) ? p.b[i + j] : (bf16)0.0f;
+  return v;
+}
+
+template <int AK, int BK_>
+__global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
+  __shared__ __attribute__((aligned(16))) bf16 As[2][TM][LDK];
+  __shared__ __attribute__((aligned(16))) bf16 Bs[2][TN][LDK];
+  constexpr bool AKV = (AK == A_ROWK || AK == A_CONV || AK == A_DGRAD);  // K-vector A
+  constexpr bool BKV = (BK_ == B_NK || BK_ == B_DGRADW);                 // K-vector B
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
+  const int kt0 = blockIdx.z * p.ktiles_per_split;
+  const int kt1 = min((p.K + TK - 1) / TK, kt0 + p.ktiles_per_split);
+
+  // loader coordinates
+  const int lr = tid >> 2, lk = (tid & 3) * 8;  // K-vector: row, k offset
+  const int vk = tid >> 3, vr = (tid & 7) * 8;  // M-vector: k, row offset
+  ARow ar;
+  if (AKV) ar = a_row<AK>(p, m0 + lr);
+
+  bf16x8 ra, rb;
+  auto gload = [&](int kt) {
+    const int k0 = kt * TK;
+    if (AKV) ra = load_a_k8<AK>(p, ar, k0 + lk);
+    else ra = load_a_m8<AK>(p, m0 + vr, k0 + vk);
+    if (BKV) rb = load_b_k8<BK_>(p, n0 + lr, k0 + lk);
+    else rb = load_b_n8(p, n0 + vr, k0 + vk);
+  };
+  auto sstore = [&](int buf) {
+    if (AKV) {
+      *reinterpret_cast<bf16x8*>(&As[buf][lr][lk]) = ra;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) As[buf][vr + j][vk] = ra[j];
+    }
+    if (BKV) {
+      *reinterpret_cast<bf16x8*>(&Bs[buf][lr][lk]) = rb;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Bs[buf][vr + j][vk] = rb[j];
+    }
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fk = (lane >> 4) * 8;
+  if (kt0 < kt1) {
+    gload(kt0);
+    sstore(0);
+    __syncthreads();
+    int buf = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const bool more = kt + 1 < kt1;
+      if (more) gload(kt + 1);
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&As[buf][wm * 32 + fr][fk]);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&As[buf][wm * 32 + 16 + fr][fk]);
+      const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(&Bs[buf][wn * 32 + fr][fk]);
+      const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(&Bs[buf][wn * 32 + 16 + fr][fk]);
+      acc[0][0] = mfma16(a0, b0, acc[0][0]);
+      acc[0][1] = mfma16(a0, b1, acc[0][1]);
+      acc[1][0] = mfma16(a1, b0, acc[1][0]);
+      acc[1][1] = mfma16(a1, b1, acc[1][1]);
+      if (more) {
+        sstore(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+      }
+    }
+  }
+
+  // ---- epilogue
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = n0 + wn * 32 + j * 16 + fr;
+    const bool cok = col < p.N;
+    const float bv = (p.bias && cok) ? p.bias[col] : 0.f;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+        if (!cok || row >= p.M) continue;
+        float v = p.alpha * acc[i][j][r] + bv;
+        if (p.colstats) {
+          s1 += v;
+          s2 += v * v;
+        }
+        if (p.relu) v = fmaxf(v, 0.f);
+        if (p.cf_mode == 1) p.cf[(long long)row * p.ldc + col] = v;
+        else if (p.cf_mode == 2) atomicAdd(&p.cf[(long long)row * p.ldc + col], v);
+        if (p.cb) {
+          bf16* q = &p.cb[(long long)row * p.ldcb + col];
+          if (p.cb_accum) v += bf2f(*q);
+          *q = f2bf(v);
+        }
+      }
+    }
+    if (p.colstats) {
+      s1 += __shfl_xor(s1, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (lane < 16 && cok) {
+        atomicAdd(&p.colstats[col], s1);
+        atomicAdd(&p.colstats[p.N + col], s2);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Philox4x32-10 (counter-based: dropout masks are regenerated, never stored)
+__device__ __forceinline__ uint4 philox(uint4 c, uint2 k) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const unsigned lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const unsigned lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = uint4{hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0};
+    k.x += 0x9E3779B9u;
+    k.y += 0xBB67AE85u;
+  }
+  return c;
+}
+
+struct Drop {
+  float rate;  // 0 = off
+  unsigned long long seed;
+  const long long* iter;
+  int iter_offset;
+  int layer_id;
+};
+
+// keep-scale (0 or 1/(1-rate)) of the 8 consecutive elements e0..e0+7 (e0 % 8 == 0)
+__device__ __forceinline__ void drop8(const Drop& d, long long e0, float* ks) {
+  const long long it = (d.iter ? *d.iter : 0) + d.iter_offset;
+  const uint2 key{(unsigned)d.seed, (unsigned)(d.seed >> 32)};
+  const float keep = 1.f - d.rate, inv = 1.f / keep;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const unsigned long long c = (unsigned long long)(e0 >> 2) + h;
+    const uint4 r = philox(uint4{(unsigned)c, (unsigned)(c >> 32), (unsigned)it, (unsigned)d.layer_id}, key);
+    const unsigned w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ks[h * 4 + q] = ((w[q] >> 8) * (1.f / 16777216.f) < keep) ? inv : 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// BatchNormalization (+ residual + ReLU + dropout) forward
+struct BnFwdArgs {
+  const bf16* y;
+  bf16* out;
+  const bf16* res;
+  long long R;  // rows (= elements / C)
+  int C;
+  int mode;  // 0 identity (ReLU/dropout/add only), 1 batch statistics, 2 moving statistics
+  const float* stats;  // [2][C] sum, sumsq (mode 1)
+  float* saved;        // [2][C] mean, rstd (mode 1, written by block 0)
+  const float* gamma;
+  const float* beta;
+  float eps;
+  float* mmean;
+  float* mvar;
+  float momentum, bessel;
+  float* zero_buf;  // [2][C] backward accumulators of this layer (zeroed by block 0)
+  int relu;
+  Drop drop;
+};
+
+constexpr int kMaxC = 2048;
+
+__global__ __launch_bounds__(256) void bn_fwd_kernel(BnFwdArgs a) {
+  __shared__ float sc[kMaxC], sf[kMaxC];
+  const int C = a.C;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float scale = 1.f, shift = 0.f;
+    if (a.mode != 0) {
+      float mean, var;
+      if (a.mode == 1) {
+        mean = a.stats[c] / (float)a.R;
+        var = fmaxf(a.stats[C + c] / (float)a.R - mean * mean, 0.f);
+      } else {
+        mean = a.mmean[c];
+        var = a.mvar[c];
+      }
+      const float rstd = rsqrtf(var + a.eps);
+      const float g = a.gamma ? a.gamma[c] : 1.f;
+      scale = g * rstd;
+      shift = (a.beta ? a.beta[c] : 0.f) - mean * scale;
+      if (blockIdx.x == 0 && a.mode == 1) {
+        a.saved[c] = mean;
+        a.saved[C + c] = rstd;
+        if (a.mmean) {
+          a.mmean[c] = a.mmean[c] * a.momentum + mean * (1.f - a.momentum);
+          a.mvar[c] = a.mvar[c] * a.momentum + var * a.bessel * (1.f - a.momentum);
+        }
+      }
+    }
+    if (blockIdx.x == 0 && a.zero_buf) {
+      a.zero_buf[c] = 0.f;
+      a.zero_buf[C + c] = 0.f;
+    }
+    sc[c] = scale;
+    sf[c] = shift;
+  }
+  __syncthreads();
+  const long long n = a.R * C;
+  const long long nchunk = (n + 7) / 8;
+  const bool vec = (n % 8) == 0;
+  for (long long q = blockIdx.x * (long long)blockDim.x + threadIdx.x; q < nchunk;
+       q += (long long)gridDim.x * blockDim.x) {
+    const long long e0 = q * 8;
+    float v[8], r[8], ks[8];
+    if (vec) {
+      const bf16x8 yv = *reinterpret_cast<const bf16x8*>(a.y + e0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = bf2f(yv[j]);
+      if (a.res) {
+        const bf16x8 rv = *reinterpret_cast<const bf16x8*>(a.res + e0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] = bf2f(rv[j]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[j] = e0 + j < n ? bf2f(a.y[e0 + j]) : 0.f;
+        r[j] = (a.res && e0 + j < n) ? bf2f(a.res[e0 + j]) : 0.f;
+      }
+    }
+    if (a.drop.rate > 0.f) drop8(a.drop, e0, ks);
+    int c = (int)(e0 % C);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float z = v[j] * sc[c] + sf[c];
+      if (a.res) z += r[j];
+      if (a.relu) z = fmaxf(z, 0.f);
+      if (a.drop.rate > 0.f) z *= ks[j];
+      o[j] = f2bf(z);
+      if (++c == C) c = 0;
+    }
+    if (vec) {
+      *reinterpret_cast<bf16x8*>(a.out + e0) = o;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (e0 + j < n) a.out[e0 + j] = o[j];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// BN (+ residual + ReLU + dropout) backward.  dz = dout * keep * (z > 0) where z is the
+// pre-ReLU value recomputed from y (and the residual); xhat = (y - mean) * rstd.
+struct BnBwdArgs {
+  const bf16* dout;
+  const bf16* y;
+  const bf16* res;
+  long long R;
+  int C;
+  int mode;  // 0 identity, 1 batch statistics
+  const float* saved;  // [2][C] mean, rstd
+  const float* gamma;
+  const float* beta;
+  int relu;
+  Drop drop;
+  float* dstats;  // [2][C] sum dz, sum dz*xhat
+  bf16* dx;
+  int dx_accum;
+  bf16* dres;
+  int dres_accum;
+  float* dgamma;
+  float* dbeta;
+  float* zero_fwd;  // [2][C] forward statistics of this layer (zeroed by block 0 of the apply pass)
+};
+
+struct BnPre {
+  float sc, sf, mean, rstd;
+};
+
+__device__ __forceinline__ void bn_dz8(const BnBwdArgs& a, const float* sc, const float* sf, const float* mu,
+                                       const float* rs, long long e0, long long n, bool vec, float* dz,
+                                       float* xh) {
+  float v[8], r[8], d[8], ks[8];
+  if (vec) {
+    const bf16x8 yv = *reinterpret_cast<const bf16x8*>(a.y + e0);
+    const bf16x8 dv = *reinterpret_cast<const bf16x8*>(a.dout + e0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      v[j] = bf2f(yv[j]);
+      d[j] = bf2f(dv[j]);
+      r[j] = 0.f;
+    }
+    if (a.res) {
+      const bf16x8 rv = *reinterpret_cast<const bf16x8*>(a.res + e0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = bf2f(rv[j]);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool ok = e0 + j < n;
+      v[j] = ok ? bf2f(a.y[e0 + j]) : 0.f;
+      d[j] = ok ? bf2f(a.dout[e0 + j]) : 0.f;
+      r[j] = (ok && a.res) ? bf2f(a.res[e0 + j]) : 0.f;
+    }
+  }
+  if (a.drop.rate > 0.f) drop8(a.drop, e0, ks);
+  int c = (int)(e0 % a.C);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float z = v[j] * sc[c] + sf[c] + r[j];
+    float g = d[j];
+    if (a.drop.rate > 0.f) g *= ks[j];
+    if (a.relu && !(z > 0.f)) g = 0.f;
+    dz[j] = (e0 + j < n) ? g : 0.f;
+    xh[j] = (v[j] - mu[c]) * rs[c];
+    if (++c == a.C) c = 0;
+  }
+}
+
+__device__ __forceinline__ void bn_bwd_prologue(const BnBwdArgs& a, float* sc, float* sf, float* mu, float* rs) {
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    if (a.mode == 1) {
+      const float mean = a.saved[c], rstd = a.saved[a.C + c];
+      const float g = a.gamma ? a.gamma[c] : 1.f;
+      sc[c] = g * rstd;
+      sf[c] = (a.beta ? a.beta[c] : 0.f) - mean * g * rstd;
+      mu[c] = mean;
+      rs[c] = rstd;
+    } else {
+      sc[c] = 1.f;
+      sf[c] = 0.f;
+      mu[c] = 0.f;
+      rs[c] = 1.f;
+    }
+  }
+}
+
+constexpr int kMaxCB = 1024;
+
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdArgs a) {
+  __shared__ float sc[kMaxCB], sf[kMaxCB], mu[kMaxCB], rs[kMaxCB], s1[kMaxCB], s2[kMaxCB];
+  bn_bwd_prologue(a, sc, sf, mu, rs);
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) s1[c] = s2[c] = 0.f;
+  __syncthreads();
+  const long long n = a.R * a.C;
+  const long long nchunk = (n + 7) / 8;
+  const bool vec = (n % 8) == 0;
+  // When the grid stride is a multiple of C (host picks such grids) every thread always sees the
+  // same 8 channels: accumulate in registers and touch LDS once at the end.
+  const long long first = (blockIdx.x * (long long)blockDim.x + threadIdx.x) * 8;
+  const bool fixed = ((long long)gridDim.x * blockDim.x * 8) % a.C == 0;
+  float r1[8], r2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r1[j] = r2[j] = 0.f;
+  for (long long q = blockIdx.x * (long long)blockDim.x + threadIdx.x; q < nchunk;
+       q += (long long)gridDim.x * blockDim.x) {
+    const long long e0 = q * 8;
+    float dz[8], xh[8];
+    bn_dz8(a, sc, sf, mu, rs, e0, n, vec, dz, xh);
+    if (fixed) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        r1[j] += dz[j];
+        r2[j] += dz[j] * xh[j];
+      }
+    } else {
+      int c = (int)(e0 % a.C);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        atomicAdd(&s1[c], dz[j]);
+        atomicAdd(&s2[c], dz[j] * xh[j]);
+        if (++c == a.C) c = 0;
+      }
+    }
+  }
+  if (fixed && first < n) {
+    int c = (int)(first % a.C);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      atomicAdd(&s1[c], r1[j]);
+      atomicAdd(&s2[c], r2[j]);
+      if (++c == a.C) c = 0;
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    atomicAdd(&a.dstats[c], s1[c]);
+    atomicAdd(&a.dstats[a.C + c], s2[c]);
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a) {
+  __shared__ float sc[kMaxCB], sf[kMaxCB], mu[kMaxCB], rs[kMaxCB], k1[kMaxCB], k2[kMaxCB];
+  bn_bwd_prologue(a, sc, sf, mu, rs);
+  const float invR = 1.f / (float)a.R;
+  for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+    if (a.mode == 1) {
+      const float sdz = a.dstats[c], sdx = a.dstats[a.C + c];
+      k1[c] = sdz * invR;
+      k2[c] = sdx * invR;
+      if (blockIdx.x == 0) {
+        if (a.dbeta) a.dbeta[c] += sdz;
+        if (a.dgamma) a.dgamma[c] += sdx;
+      }
+    } else {
+      k1[c] = k2[c] = 0.f;
+    }
+    if (blockIdx.x == 0 && a.zero_fwd) {
+      a.zero_fwd[c] = 0.f;
+      a.zero_fwd[a.C + c] = 0.f;
+    }
+  }
+  __syncthreads();
+  const long long n = a.R * a.C;
+  const long long nchunk = (n + 7) / 8;
+  const bool vec = (n % 8) == 0;
+  for (long long q = blockIdx.x * (long long)blockDim.x + threadIdx.x; q < nchunk;
+       q += (long long)gridDim.x * blockDim.x) {
+    const long long e0 = q * 8;
+    float dz[8], xh[8];
+    bn_dz8(a, sc, sf, mu, rs, e0, n, vec, dz, xh);
+    int c = (int)(e0 % a.C);
+    float dx[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      // mode 0: dx = dz (sc = 1); mode 1: dx = gamma*rstd*(dz - mean(dz) - xhat*mean(dz*xhat))
+      dx[j] = sc[c] * (dz[j] - k1[c] - xh[j] * k2[c]);
+      if (a.mode == 0) dx[j] = dz[j];
+      if (++c == a.C) c = 0;
+    }
+    if (a.dx) {
+      bf16x8 o;
+      if (a.dx_accum) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(dx[j] + (e0 + j < n ? bf2f(a.dx[e0 + j]) : 0.f));
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(dx[j]);
+      }
+      if (vec) {
+        *reinterpret_cast<bf16x8*>(a.dx + e0) = o;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (e0 + j < n) a.dx[e0 + j] = o[j];
+      }
+    }
+    if (a.dres) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (e0 + j >= n) break;
+        const float v = dz[j] + (a.dres_accum ? bf2f(a.dres[e0 + j]) : 0.f);
+        a.dres[e0 + j] = f2bf(v);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// bias / ReLU backward of a Conv2D/Dense with a fused activation: dz = dout*(out>0),
+// dbias[c] += sum_rows dz.
+__global__ __launch_bounds__(256) void act_bwd_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ out,
+                                                      long long R, int C, int relu, bf16* __restrict__ dz,
+                                                      float* __restrict__ dbias) {
+  __shared__ float s1[kMaxCB];
+  for (int c = threadIdx.x; c < C; c += blockDim.x) s1[c] = 0.f;
+  __syncthreads();
+  const long long n = R * C;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    float g = bf2f(dout[e]);
+    if (relu && !(bf2f(out[e]) > 0.f)) g = 0.f;
+    if (dz) dz[e] = f2bf(g);
+    if (dbias) atomicAdd(&s1[(int)(e % C)], g);
+  }
+  if (!dbias) return;
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) atomicAdd(&dbias[c], s1[c]);
+}
+
+// ---------------------------------------------------------------------------------------
+// Max pooling (NHWC) with the window argmax stored as one byte per output.
+struct PoolArgs {
+  const bf16* x;
+  bf16* y;
+  unsigned char* idx;
+  const bf16* dy;
+  bf16* dx;
+  int dx_accum;
+  Geo g;  // C = channels, Co unused, KH/KW window, sh/sw strides, pt/pl pads
+};
+
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(PoolArgs a) {
+  const Geo& g = a.g;
+  const long long n = (long long)g.B * g.Ho * g.Wo * g.C;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % g.C);
+    long long t = e / g.C;
+    const int ow = (int)(t % g.Wo);
+    t /= g.Wo;
+    const int oh = (int)(t % g.Ho);
+    const int b = (int)(t / g.Ho);
+    float best = -INFINITY;
+    int bi = 0;
+    for (int i = 0; i < g.KH; ++i) {
+      const int ih = oh * g.sh - g.pt + i;
+      if ((unsigned)ih >= (unsigned)g.H) continue;
+      for (int j = 0; j < g.KW; ++j) {
+        const int iw = ow * g.sw - g.pl + j;
+        if ((unsigned)iw >= (unsigned)g.W) continue;
+        const float v = bf2f(a.x[(((long long)b * g.H + ih) * g.W + iw) * g.C + c]);
+        if (v > best) {
+          best = v;
+          bi = i * g.KW + j;
+        }
+      }
+    }
+    a.y[e] = f2bf(best);
+    if (a.idx) a.idx[e] = (unsigned char)bi;
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(PoolArgs a) {
+  const Geo& g = a.g;
+  const long long n = (long long)g.B * g.H * g.W * g.C;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % g.C);
+    long long t = e / g.C;
+    const int iw = (int)(t % g.W);
+    t /= g.W;
+    const int ih = (int)(t % g.H);
+    const int b = (int)(t / g.H);
+    float s = 0.f;
+    const int ty = ih + g.pt, tx = iw + g.pl;
+    const int oh_lo = ty >= g.KH ? (ty - g.KH) / g.sh + 1 : 0, oh_hi = min(g.Ho - 1, ty / g.sh);
+    const int ow_lo = tx >= g.KW ? (tx - g.KW) / g.sw + 1 : 0, ow_hi = min(g.Wo - 1, tx / g.sw);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int i = ty - oh * g.sh;
+      if (i < 0 || i >= g.KH) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int j = tx - ow * g.sw;
+        if (j < 0 || j >= g.KW) continue;
+        const long long o = (((long long)b * g.Ho + oh) * g.Wo + ow) * g.C + c;
+        if (a.idx[o] == (unsigned char)(i * g.KW + j)) s += bf2f(a.dy[o]);
+      }
+    }
+    if (a.dx_accum) s += bf2f(a.dx[e]);
+    a.dx[e] = f2bf(s);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Global average pooling [B,HW,C] -> [B,C] and its backward; zero padding / its crop.
+__global__ __launch_bounds__(256) void gap_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int B, int HW,
+                                                      int C) {
+  const long long n = (long long)B * C;
+  const float inv = 1.f / (float)HW;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    const long long b = e / C;
+    const bf16* p = x + b * HW * C + c;
+    float s = 0.f;
+    for (int i = 0; i < HW; ++i) s += bf2f(p[(long long)i * C]);
+    y[e] = f2bf(s * inv);
+  }
+}
+
+__global__ __launch_bounds__(256) void gap_bwd_kernel(const bf16* __restrict__ dy, bf16* __restrict__ dx, int B,
+                                                      int HW, int C, int accum) {
+  const long long n = (long long)B * HW * C;
+  const float inv = 1.f / (float)HW;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    const long long b = e / ((long long)HW * C);
+    float v = bf2f(dy[b * C + c]) * inv;
+    if (accum) v += bf2f(dx[e]);
+    dx[e] = f2bf(v);
+  }
+}
+
+// dir 0: y[B,H+t+b,W+l+r,C] = pad(x);  dir 1: dx = crop(dy) (+= when accum)
+__global__ __launch_bounds__(256) void pad_kernel(const bf16* __restrict__ src, bf16* __restrict__ dst, Geo g, int dir,
+                                                  int accum) {
+  // g: H,W input dims; Ho,Wo padded dims; pt,pl offsets
+  const long long n = (long long)g.B * g.Ho * g.Wo * g.C;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % g.C);
+    long long t = e / g.C;
+    const int ow = (int)(t % g.Wo);
+    t /= g.Wo;
+    const int oh = (int)(t % g.Ho);
+    const int b = (int)(t / g.Ho);
+    const int ih = oh - g.pt, iw = ow - g.pl;
+    const bool in = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+    const long long ie = (((long long)b * g.H + ih) * g.W + iw) * g.C + c;
+    if (dir == 0) {
+      dst[e] = in ? src[ie] : (bf16)0.0f;
+    } else if (in) {
+      float v = bf2f(src[e]);
+      if (accum) v += bf2f(dst[ie]);
+      dst[ie] = f2bf(v);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Softmax cross-entropy over C classes, one wave per row (any C).
+struct XentArgs {
+  const float* logits;
+  long long ldl;
+  const int* labels;
+  int B, C;
+  float scale;
+  bf16* dlogits;  // [B][ldd] (softmax - onehot) * scale, or null
+  long long ldd;
+  float* metrics;  // [4] loss sum, correct, count, 0
+  float* probs;    // [B][C] softmax (or logits copy when probs_are_logits)
+  int probs_are_logits;
+  long long* iterations;
+};
+
+__global__ __launch_bounds__(256) void xent_kernel(XentArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ float part[4][2];
+  float loss = 0.f, corr = 0.f;
+  const bool ok = row < a.B;
+  if (ok) {
+    const float* l = a.logits + (long long)row * a.ldl;
+    float mx = -INFINITY;
+    int am = 0x7fffffff;
+    for (int c = lane; c < a.C; c += 64) {
+      const float v = l[c];
+      if (v > mx) {
+        mx = v;
+        am = c;
+      }
+    }
+    // wave argmax (first index of the max)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float om = __shfl_xor(mx, o, 64);
+      const int oi = __shfl_xor(am, o, 64);
+      if (om > mx || (om == mx && oi < am)) {
+        mx = om;
+        am = oi;
+      }
+    }
+    float se = 0.f;
+    for (int c = lane; c < a.C; c += 64) se += __expf(l[c] - mx);
+    se = wave_sum(se);
+    const int y = a.labels[row];
+    const float lse = mx + __logf(se);
+    const float ly = (y >= 0 && y < a.C) ? l[y] : mx;
+    loss = lse - ly;
+    corr = (am == y) ? 1.f : 0.f;
+    const float inv = 1.f / se;
+    for (int c = lane; c < a.C; c += 64) {
+      const float p = __expf(l[c] - mx) * inv;
+      if (a.dlogits) a.dlogits[(long long)row * a.ldd + c] = f2bf((p - (c == y ? 1.f : 0.f)) * a.scale);
+      if (a.probs) a.probs[(long long)row * a.C + c] = a.probs_are_logits ? l[c] : p;
+    }
+  }
+  if (lane == 0) {
+    part[threadIdx.x >> 6][0] = ok ? loss : 0.f;
+    part[threadIdx.x >> 6][1] = ok ? corr : 0.f;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float ls = part[0][0] + part[1][0] + part[2][0] + part[3][0];
+    const float cs = part[0][1] + part[1][1] + part[2][1] + part[3][1];
+    const int cnt = min(4, a.B - (int)blockIdx.x * 4);
+    if (a.metrics) {
+      atomicAdd(&a.metrics[0], ls);
+      atomicAdd(&a.metrics[1], cs);
+      atomicAdd(&a.metrics[2], (float)cnt);
+    }
+    if (a.iterations && blockIdx.x == 0) *a.iterations += 1;
+  }
+}
+
+// per-channel sum / sum of squares of a [R][C] bf16 tensor (BN after a non-GEMM producer)
+__global__ __launch_bounds__(256) void colstats_kernel(const bf16* __restrict__ x, long long R, int C,
+                                                       float* __restrict__ stats) {
+  __shared__ float s1[kMaxCB], s2[kMaxCB];
+  for (int c = threadIdx.x; c < C; c += blockDim.x) s1[c] = s2[c] = 0.f;
+  __syncthreads();
+  const long long n = R * C;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const float v = bf2f(x[e]);
+    const int c = (int)(e % C);
+    atomicAdd(&s1[c], v);
+    atomicAdd(&s2[c], v * v);
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    atomicAdd(&stats[c], s1[c]);
+    atomicAdd(&stats[C + c], s2[c]);
+  }
+}
+
+__global__ __launch_bounds__(256) void cast_kernel(const float* __restrict__ x, bf16* __restrict__ y, long long n) {
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e * 4 < n; e += (long long)gridDim.x * blockDim.x) {
+    const long long i = e * 4;
+    if (i + 4 <= n) {
+      const float4 v = *reinterpret_cast<const float4*>(x + i);
+      y[i] = f2bf(v.x);
+      y[i + 1] = f2bf(v.y);
+      y[i + 2] = f2bf(v.z);
+      y[i + 3] = f2bf(v.w);
+    } else {
+      for (long long j = i; j < n; ++j) y[j] = f2bf(x[j]);
+    }
+  }
+}
+
+static int grid_for(long long n, int per_thread = 1) {
+  const long long t = (n + per_thread - 1) / per_thread;
+  long long b = (t + 255) / 256;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace tde
+
+using namespace tde;
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, long long ldb, int bkind, int M, int N,
+                      int K, const int* geo, int splits, float* cf, long long ldc, int cf_mode, float alpha, bf16* cb,
+                      long long ldcb, int cb_accum, const float* bias, int relu, float* colstats, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  IGemmArgs p{};
+  p.a = a;
+  p.lda = lda;
+  p.b = b;
+  p.ldb = ldb;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  if (geo) {
+    Geo g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9], geo[10], geo[11], geo[12]};
+    p.g = g;
+  }
+  const int ktiles = (K + TK - 1) / TK;
+  if (splits < 1) splits = 1;
+  if (splits > ktiles) splits = ktiles > 0 ? ktiles : 1;
+  if (splits > 1 && (cb || colstats || cf_mode != 2 || bias || relu)) return -2;  // split-K only into f32 atomics
+  p.ktiles_per_split = (ktiles + splits - 1) / splits;
+  splits = ktiles > 0 ? (ktiles + p.ktiles_per_split - 1) / p.ktiles_per_split : 1;
+  const bool al = aligned16(a), bl = aligned16(b);
+  switch (akind) {
+    case A_ROWK: p.avec = al && lda % 8 == 0 && K % 8 == 0; break;
+    case A_CONV: p.avec = al && p.g.C % 8 == 0; break;
+    case A_DGRAD: p.avec = al && p.g.Co % 8 == 0; break;
+    case A_COLM: p.avec = al && lda % 8 == 0 && M % 8 == 0; break;
+    case A_WGRAD: p.avec = al && p.g.C % 8 == 0; break;
+    default: return -1;
+  }
+  switch (bkind) {
+    case B_NK: p.bvec = bl && ldb % 8 == 0 && K % 8 == 0; break;
+    case B_DGRADW: p.bvec = bl && p.g.Co % 8 == 0; break;
+    case B_KN: p.bvec = bl && ldb % 8 == 0 && N % 8 == 0; break;
+    default: return -1;
+  }
+  p.cf = cf;
+  p.ldc = ldc;
+  p.cf_mode = cf ? cf_mode : 0;
+  p.alpha = alpha;
+  p.cb = cb;
+  p.ldcb = ldcb;
+  p.cb_accum = cb_accum;
+  p.bias = bias;
+  p.relu = relu;
+  p.colstats = colstats;
+  dim3 grid((N + TN - 1) / TN, (M + TM - 1) / TM, splits);
+  if (grid.y > 65535) return -3;
+  if (akind == A_ROWK && bkind == B_NK) igemm_kernel<A_ROWK, B_NK><<<grid, 256, 0, stream>>>(p);
+  else if (akind == A_CONV && bkind == B_NK) igemm_kernel<A_CONV, B_NK><<<grid, 256, 0, stream>>>(p);
+  else if (akind == A_DGRAD && bkind == B_DGRADW) igemm_kernel<A_DGRAD, B_DGRADW><<<grid, 256, 0, stream>>>(p);
+  else if (akind == A_COLM && bkind == B_KN) igemm_kernel<A_COLM, B_KN><<<grid, 256, 0, stream>>>(p);
+  else if (akind == A_WGRAD && bkind == B_KN) igemm_kernel<A_WGRAD, B_KN><<<grid, 256, 0, stream>>>(p);
+  else return -1;
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+// drop: rate, seed, iter ptr, iter_offset, layer_id
+TDE_API int tde_bn_fwd(const bf16* y, bf16* out, const bf16* res, long long R, int C, int mode, const float* stats,
+                       float* saved, const float* gamma, const float* beta, float eps, float* mmean, float* mvar,
+                       float momentum, float bessel, float* zero_buf, int relu, float drop_rate,
+                       unsigned long long seed, const long long* iter, int iter_offset, int layer_id,
+                       hipStream_t stream) {
+  if (C > kMaxC) return -1;
+  BnFwdArgs a{y, out, res, R, C, mode, stats, saved, gamma, beta, eps, mmean, mvar, momentum, bessel, zero_buf, relu,
+              Drop{drop_rate, seed, iter, iter_offset, layer_id}};
+  bn_fwd_kernel<<<grid_for(R * C, 8), 256, 0, stream>>>(a);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+TDE_API int tde_bn_bwd(const bf16* dout, const bf16* y, const bf16* res, long long R, int C, int mode,
+                       const float* saved, const float* gamma, const float* beta, int relu, float drop_rate,
+                       unsigned long long seed, const long long* iter, int iter_offset, int layer_id, float* dstats,
+                       bf16* dx, int dx_accum, bf16* dres, int dres_accum, float* dgamma, float* dbeta,
+                       float* zero_fwd, hipStream_t stream) {
+  if (C > kMaxCB) return -1;
+  BnBwdArgs a{dout, y, res, R, C, mode, saved, gamma, beta, relu, Drop{drop_rate, seed, iter, iter_offset, layer_id},
+              dstats, dx, dx_accum, dres, dres_accum, dgamma, dbeta, zero_fwd};
+  int g = grid_for(R * C, 8);
+  if (mode == 1) {
+    // round the grid to a multiple of C / gcd(2048, C) so the grid stride is a multiple of C
+    int gc = C, t = 2048;
+    while (t) {
+      const int r = gc % t;
+      gc = t;
+      t = r;
+    }
+    const int mult = C / gc;
+    g = ((g + mult - 1) / mult) * mult;
+    bn_bwd_reduce_kernel<<<g, 256, 0, stream>>>(a);
+    TDE_LAUNCH_CHECK();
+  }
+  bn_bwd_apply_kernel<<<g, 256, 0, stream>>>(a);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+TDE_API int tde_act_bwd(const bf16* dout, const bf16* out, long long R, int C, int relu, bf16* dz, float* dbias,
+                        hipStream_t stream) {
+  if (C > kMaxCB) return -1;
+  act_bwd_kernel<<<grid_for(R * C, 8), 256, 0, stream>>>(dout, out, R, C, relu, dz, dbias);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+TDE_API int tde_maxpool(const bf16* x, bf16* y, unsigned char* idx, const bf16* dy, bf16* dx, int dx_accum,
+                        const int* geo, int backward, hipStream_t stream) {
+  Geo g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9], geo[10], geo[11], geo[12]};
+  if (g.KH * g.KW > 256) return -1;
+  PoolArgs a{x, y, idx, dy, dx, dx_accum, g};
+  if (!backward) maxpool_fwd_kernel<<<grid_for((long long)g.B * g.Ho * g.Wo * g.C), 256, 0, stream>>>(a);
+  else maxpool_bwd_kernel<<<grid_for((long long)g.B * g.H * g.W * g.C), 256, 0, stream>>>(a);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+TDE_API int tde_gap(const bf16* x, bf16* y, int B, int HW, int C, int backward, int accum, hipStream_t stream) {
+  if (!backward) gap_fwd_kernel<<<grid_for((long long)B * C), 256, 0, stream>>>(x, y, B, HW, C);
+  else gap_bwd_kernel<<<grid_for((long long)B * HW * C), 256, 0, stream>>>(x, y, B, HW, C, accum);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+TDE_API int tde_pad(const bf16* src, bf16* dst, const int* geo, int backward, int accum, hipStream_t stream) {
+  Geo g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9], geo[10], geo[11], geo[12]};
+  pad_kernel<<<grid_for((long long)g.B * g.Ho * g.Wo * g.C), 256, 0, stream>>>(src, dst, g, backward, accum);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+TDE_API int tde_xent(const float* logits, long long ldl, const int* labels, int B, int C, float scale, bf16* dlogits,
+                     long long ldd, float* metrics, float* probs, int probs_are_logits, long long* iterations,
+                     hipStream_t stream) {
+  if (B <= 0) return 0;
+  XentArgs a{logits, ldl, labels, B, C, scale, dlogits, ldd, metrics, probs, probs_are_logits, iterations};
+  xent_kernel<<<(B + 3) / 4, 256, 0, stream>>>(a);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+TDE_API int tde_colstats(const bf16* x, long long R, int C, float* stats, hipStream_t stream) {
+  if (C > kMaxCB) return -1;
+  colstats_kernel<<<grid_for(R * C, 8), 256, 0, stream>>>(x, R, C, stats);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+TDE_API int tde_cast_f32_bf16(const float* x, bf16* y, long long n, hipStream_t stream) {
+  if (((uintptr_t)x & 15) != 0) return -1;
+  cast_kernel<<<grid_for(n, 4), 256, 0, stream>>>(x, y, n);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}

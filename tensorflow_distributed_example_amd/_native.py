@@ -41,6 +41,20 @@ _HIP_PROTOS = {
     "tde_optim_build_table": (i32, [p, i32, p]),
     "tde_optim_apply": (i32, [p, p, p, p, p, p, p, i32, p, i32, f32, f32, f32, f32, f32, f32, i32, p, p]),
     "tde_shadow_refresh": (i32, [p, p, p, p, i32, p]),
+    # layer-wise kernel library (csrc/kernels/layers.hip)
+    "tde_igemm": (i32, [p, i64, i32, p, i64, i32, i32, i32, i32, p, i32, p, i64, i32, f32, p, i64, i32, p, i32,
+                        p, p]),
+    "tde_bn_fwd": (i32, [p, p, p, i64, i32, i32, p, p, p, p, f32, p, p, f32, f32, p, i32, f32, C.c_ulonglong,
+                         p, i32, i32, p]),
+    "tde_bn_bwd": (i32, [p, p, p, i64, i32, i32, p, p, p, i32, f32, C.c_ulonglong, p, i32, i32, p, p, i32, p,
+                         i32, p, p, p, p]),
+    "tde_act_bwd": (i32, [p, p, i64, i32, i32, p, p, p]),
+    "tde_maxpool": (i32, [p, p, p, p, p, i32, p, i32, p]),
+    "tde_gap": (i32, [p, p, i32, i32, i32, i32, i32, p]),
+    "tde_pad": (i32, [p, p, p, i32, i32, p]),
+    "tde_xent": (i32, [p, i64, p, i32, i32, f32, p, i64, p, p, i32, p, p]),
+    "tde_colstats": (i32, [p, i64, i32, p, p]),
+    "tde_cast_f32_bf16": (i32, [p, p, i64, p]),
     # RCCL
     "tde_nccl_version": (i32, []),
     "tde_nccl_error_string": (C.c_char_p, [i32]),

@@ -98,11 +98,12 @@ class Loaded:
 
 
 def load(path):
-    from ..models.model import Sequential
+    from ..models.model import Functional, Sequential
     from . import tensor_bundle as TB
     p = Path(path.decode() if isinstance(path, bytes) else path)
     spec = json.loads((p / "saved_model.json").read_text())
-    m = Sequential.from_config(spec["model"]["config"])
+    cls = Functional if spec["model"]["class_name"] == "Functional" else Sequential
+    m = cls.from_config(spec["model"]["config"])
     m.build()
     vals = TB.read_bundle(str(p / spec["variables"]))
     m._store.load_dict({k: v for k, v in vals.items() if k in m._store.segments})

@@ -78,8 +78,30 @@ def tf_same_pads(n, k, s):
     return total // 2, total - total // 2
 
 
+class KerasTensor:
+    """Symbolic tensor of the functional API: a shape plus the layer call that produces it."""
+
+    def __init__(self, shape, producer=None, inputs=(), name=None):
+        self.shape = (None,) + tuple(int(d) for d in shape)
+        self.producer = producer
+        self.inputs = list(inputs)
+        self.name = name
+
+    def __repr__(self):
+        who = self.producer.name if self.producer is not None else self.name
+        return f"<KerasTensor shape={self.shape} from {who}>"
+
+
+def Input(shape=None, batch_size=None, name=None, dtype=None, batch_shape=None):
+    """``keras.Input``: the symbolic model input (channels_last image or feature vector)."""
+    if shape is None and batch_shape is not None:
+        shape = tuple(batch_shape[1:])
+    return KerasTensor(tuple(shape), name=name or K.unique_name("input"))
+
+
 class Layer:
     _prefix = "layer"
+    multi_input = False
 
     def __init__(self, name: Optional[str] = None, input_shape=None, trainable=True, **kwargs):
         for k in kwargs:
@@ -110,12 +132,28 @@ class Layer:
         return input_shape
 
     def _build_shapes(self, input_shape):
+        if self.multi_input:
+            self.input_shape = [tuple(x) for x in input_shape]
+            self.built = True
+            self.output_shape = tuple(self.compute_output_shape(self.input_shape))
+            return self.output_shape
         self.input_shape = tuple(input_shape)
         if not self.built:
             self.build(self.input_shape)
             self.built = True
         self.output_shape = tuple(self.compute_output_shape(self.input_shape))
         return self.output_shape
+
+    # ---- functional API: calling a layer on symbolic tensors records a graph node
+    def __call__(self, inputs, **kw):
+        multi = isinstance(inputs, (list, tuple))
+        ins = list(inputs) if multi else [inputs]
+        if not all(isinstance(t, KerasTensor) for t in ins):
+            raise TypeError(f"{self.name}: layers are called on symbolic tensors from Input(); "
+                            "use model.predict()/model(x) for eager execution")
+        shapes = [t.shape[1:] for t in ins]
+        out = self._build_shapes(shapes if multi else shapes[0])
+        return KerasTensor(out, producer=self, inputs=ins)
 
     # ---- weights (views into the owning model's ParamStore)
     def w(self, name):
@@ -300,6 +338,9 @@ class ZeroPadding2D(Layer):
         (t, b), (l, r) = self.padding
         return F.pad(x, (0, 0, l, r, t, b))
 
+    def get_config(self):
+        return dict(name=self.name, padding=self.padding)
+
 
 class Flatten(Layer):
     _prefix = "flatten"
@@ -349,6 +390,9 @@ class ReLU(Activation):
 
     def __init__(self, **kw):
         super().__init__("relu", **kw)
+
+    def get_config(self):
+        return dict(name=self.name)
 
 
 class Dropout(Layer):
@@ -429,9 +473,27 @@ class BatchNormalization(Layer):
                     scale=self.scale)
 
 
+class Add(Layer):
+    """Element-wise sum of same-shaped inputs (ResNet shortcut join)."""
+    _prefix = "add"
+    multi_input = True
+
+    def compute_output_shape(self, shapes):
+        for s_ in shapes[1:]:
+            if tuple(s_) != tuple(shapes[0]):
+                raise ValueError(f"{self.name}: shape mismatch {shapes}")
+        return tuple(shapes[0])
+
+    def ref_call(self, xs, W, training, rng=None, state_updates=None):
+        out = xs[0]
+        for x in xs[1:]:
+            out = out + x
+        return out
+
+
 LAYER_CLASSES = {c.__name__: c for c in [InputLayer, Conv2D, Dense, MaxPooling2D, GlobalAveragePooling2D,
                                          ZeroPadding2D, Flatten, Reshape, Activation, ReLU, Dropout,
-                                         BatchNormalization]}
+                                         BatchNormalization, Add]}
 
 
 def from_config(cls_name, cfg):

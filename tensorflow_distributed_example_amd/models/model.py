@@ -31,6 +31,12 @@ class _SingleReplica(DS.Strategy):
 
 
 class Model:
+    def __new__(cls, *args, **kw):
+        # keras.Model(inputs, outputs) builds a functional (DAG) model
+        if cls is Model and (len(args) >= 2 or "inputs" in kw or "outputs" in kw):
+            return object.__new__(Functional)
+        return object.__new__(cls)
+
     def __init__(self, name: Optional[str] = None):
         self.name = name or K.unique_name(self._prefix)
         self._store: Optional[P.ParamStore] = None
@@ -49,6 +55,11 @@ class Model:
     @property
     def built(self):
         return self._store is not None
+
+    def _nodes(self):
+        """Execution graph: [(layer, input tensor ids, output tensor id)] in topological order;
+        tensor 0 is the model input, the last node's output is the model output."""
+        raise NotImplementedError
 
     def _create_store(self):
         st = DS.get_strategy()
@@ -241,6 +252,9 @@ class Sequential(Model):
     def layers(self):
         return [l for l in self._layers if not isinstance(l, L.InputLayer)]
 
+    def _nodes(self):
+        return [(l, [i], i + 1) for i, l in enumerate(self.layers)]
+
     def add(self, layer):
         if self.built:
             raise RuntimeError("cannot add layers to a built model")
@@ -344,3 +358,118 @@ class Sequential(Model):
             first = False
             m.add(L.from_config(lc["class_name"], c))
         return m
+
+
+class Functional(Model):
+    """Functional-API model: ``Model(inputs=Input(...), outputs=...)`` over a DAG of layer
+    calls (multi-consumer tensors, ``Add`` joins) — used by the ResNet-18 stress config."""
+    _prefix = "model"
+
+    def __init__(self, inputs=None, outputs=None, name=None):
+        super().__init__(name)
+        if isinstance(inputs, (list, tuple)):
+            if len(inputs) != 1:
+                raise ValueError("only single-input models are supported")
+            inputs = inputs[0]
+        if isinstance(outputs, (list, tuple)):
+            if len(outputs) != 1:
+                raise ValueError("only single-output models are supported")
+            outputs = outputs[0]
+        self._input = inputs
+        self._output = outputs
+        order, seen = [], set()
+
+        def visit(t):
+            if id(t) in seen:
+                return
+            seen.add(id(t))
+            for u in t.inputs:
+                visit(u)
+            order.append(t)
+
+        visit(outputs)
+        if inputs not in order:
+            raise ValueError("outputs are not connected to inputs")
+        ids = {id(inputs): 0}
+        self._graph = []
+        for t in order:
+            if t is inputs:
+                continue
+            if t.producer is None:
+                raise ValueError(f"disconnected input {t}")
+            ids[id(t)] = len(ids)
+            self._graph.append((t.producer, [ids[id(u)] for u in t.inputs], ids[id(t)]))
+        used = [l for l, _, _ in self._graph]
+        if len(set(map(id, used))) != len(used):
+            raise ValueError("a layer is called more than once (shared layers are not supported)")
+        self._input_shape = tuple(inputs.shape[1:])
+        self._output_shape = tuple(outputs.shape[1:])
+
+    @property
+    def layers(self):
+        return [l for l, _, _ in self._graph]
+
+    def _nodes(self):
+        return list(self._graph)
+
+    def build(self, input_shape=None):
+        if self._store is None:
+            self._create_store()
+
+    @property
+    def built(self):
+        return self._store is not None
+
+    def _require_built(self):
+        if self._store is None:
+            self._create_store()
+
+    @property
+    def input_shape(self):
+        return (None,) + tuple(self._input_shape)
+
+    @property
+    def output_shape(self):
+        return (None,) + tuple(self._output_shape)
+
+    def summary(self, line_length=98, print_fn=None):
+        self._require_built()
+        pf = print_fn or print
+        producers = {0: "input"}
+        for l, _, o in self._graph:
+            producers[o] = l.name
+        pf(f'Model: "{self.name}"')
+        pf("_" * line_length)
+        pf(f"{' Layer (type)':<34}{'Output Shape':<24}{'Param #':<10}Connected to")
+        pf("=" * line_length)
+        for l, ins, _ in self._graph:
+            pf(f"{(' ' + l.name + ' (' + type(l).__name__ + ')')[:33]:<34}"
+               f"{str((None,) + tuple(l.output_shape)):<24}{l.count_params():<10}"
+               f"{', '.join(producers[i] for i in ins)}")
+        pf("=" * line_length)
+        tot = self.count_params()
+        tr = sum(int(np.prod(s.shape)) for s in self._spec_list() if s.trainable)
+        pf(f"Total params: {tot:,}")
+        pf(f"Trainable params: {tr:,}")
+        pf(f"Non-trainable params: {tot - tr:,}")
+        pf("_" * line_length)
+
+    def get_config(self):
+        return {"name": self.name, "input_shape": list(self._input_shape),
+                "layers": [{"class_name": type(l).__name__, "config": l.get_config(), "inbound": ins}
+                           for l, ins, _ in self._graph]}
+
+    def to_json(self):
+        return json.dumps({"class_name": "Functional", "config": self.get_config()})
+
+    @classmethod
+    def from_config(cls, cfg, keep_names=True):
+        t = {0: L.Input(tuple(cfg["input_shape"]))}
+        for i, lc in enumerate(cfg["layers"]):
+            c = dict(lc["config"])
+            if not keep_names:
+                c.pop("name", None)
+            layer = L.from_config(lc["class_name"], c)
+            ins = [t[j] for j in lc["inbound"]]
+            t[i + 1] = layer(ins if layer.multi_input else ins[0])
+        return cls(t[0], t[len(cfg["layers"])], name=cfg.get("name") if keep_names else None)

@@ -40,3 +40,39 @@ def mnist_bn_cnn(name=None):
         L.Dropout(0.5),
         L.Dense(10, activation="softmax"),
     ], name=name)
+
+
+def _basic_block(x, filters, stride, name):
+    """ResNet v1 BasicBlock: 3x3(s) - BN - ReLU - 3x3 - BN, + (projection) shortcut, ReLU."""
+    y = L.Conv2D(filters, 3, strides=stride, padding="same", use_bias=False, kernel_initializer="he_normal",
+                 name=f"{name}_conv1")(x)
+    y = L.BatchNormalization(epsilon=1e-5, momentum=0.9, name=f"{name}_bn1")(y)
+    y = L.Activation("relu", name=f"{name}_relu1")(y)
+    y = L.Conv2D(filters, 3, padding="same", use_bias=False, kernel_initializer="he_normal", name=f"{name}_conv2")(y)
+    y = L.BatchNormalization(epsilon=1e-5, momentum=0.9, name=f"{name}_bn2")(y)
+    if stride != 1 or x.shape[-1] != filters:
+        s = L.Conv2D(filters, 1, strides=stride, use_bias=False, kernel_initializer="he_normal",
+                     name=f"{name}_proj")(x)
+        s = L.BatchNormalization(epsilon=1e-5, momentum=0.9, name=f"{name}_proj_bn")(s)
+    else:
+        s = x
+    y = L.Add(name=f"{name}_add")([y, s])
+    return L.Activation("relu", name=f"{name}_out")(y)
+
+
+def resnet18(input_shape=(224, 224, 3), classes=1000, name="resnet18"):
+    """ResNet-18 (BASELINE.json stress config; not in the reference): functional-API model with
+    TF-'SAME' padding (asymmetric (2,3) for the 7x7/2 stem at 224), 11.69M parameters."""
+    from .model import Model
+    inp = L.Input(input_shape)
+    x = L.Conv2D(64, 7, strides=2, padding="same", use_bias=False, kernel_initializer="he_normal",
+                 name="conv1")(inp)
+    x = L.BatchNormalization(epsilon=1e-5, momentum=0.9, name="conv1_bn")(x)
+    x = L.Activation("relu", name="conv1_relu")(x)
+    x = L.MaxPooling2D(3, strides=2, padding="same", name="pool1")(x)
+    for i, (f, s) in enumerate([(64, 1), (128, 2), (256, 2), (512, 2)]):
+        x = _basic_block(x, f, s, f"stage{i + 1}_block1")
+        x = _basic_block(x, f, 1, f"stage{i + 1}_block2")
+    x = L.GlobalAveragePooling2D(name="avg_pool")(x)
+    out = L.Dense(classes, name="fc")(x)
+    return Model(inputs=inp, outputs=out, name=name)

@@ -1,0 +1,292 @@
+"""Host wrappers for the layer-wise kernel library (csrc/kernels/layers.hip).
+
+All activations are NHWC bf16 (Keras ``mixed_bfloat16``: bf16 compute/activations,
+fp32 variables, fp32 BN statistics), weight grads accumulate in the fp32 flat
+gradient bucket.  Every wrapper validates operand sizes on the host against the
+geometry it hands the kernel, so a kernel never indexes outside its buffers.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import torch
+
+from .. import _native as N
+
+_P = N.ptr
+A_ROWK, A_CONV, A_DGRAD, A_COLM, A_WGRAD = range(5)
+B_NK, B_DGRADW, B_KN = range(3)
+bf16 = torch.bfloat16
+
+
+def _s():
+    return N.stream_ptr()
+
+
+def _req(cond, msg):
+    if not cond:
+        raise ValueError(msg)
+
+
+def _bf(t, n, what):
+    _req(t is not None and t.dtype == bf16 and t.is_contiguous() and t.numel() >= n, f"{what}: bf16 [{n}] expected")
+
+
+def _f32(t, n, what):
+    _req(t is not None and t.dtype == torch.float32 and t.is_contiguous() and t.numel() >= n,
+         f"{what}: f32 [{n}] expected")
+
+
+@dataclass(frozen=True)
+class ConvGeom:
+    B: int
+    H: int
+    W: int
+    C: int
+    Ho: int
+    Wo: int
+    Co: int
+    KH: int
+    KW: int
+    sh: int
+    sw: int
+    pt: int
+    pl: int
+
+    def carray(self):
+        return (C.c_int * 13)(self.B, self.H, self.W, self.C, self.Ho, self.Wo, self.Co, self.KH, self.KW,
+                              self.sh, self.sw, self.pt, self.pl)
+
+    @property
+    def K(self):
+        return self.KH * self.KW * self.C
+
+    def with_batch(self, B):
+        return ConvGeom(B, *[getattr(self, f) for f in ("H", "W", "C", "Ho", "Wo", "Co", "KH", "KW", "sh", "sw",
+                                                        "pt", "pl")])
+
+
+def pick_splits(M, N_, K, target=512):
+    tiles = -(-M // 64) * -(-N_ // 64)
+    ktiles = -(-K // 32)
+    s = max(1, min(-(-target // tiles), ktiles // 4))
+    return s
+
+
+def _igemm(a, lda, ak, b, ldb, bk, M, N_, K, geo=None, splits=1, cf=None, ldc=0, cf_mode=0, alpha=1.0,
+           cb=None, ldcb=0, cb_accum=False, bias=None, relu=False, colstats=None):
+    g = geo.carray() if geo is not None else None
+    rc = N.hip().tde_igemm(_P(a), int(lda), ak, _P(b), int(ldb), bk, int(M), int(N_), int(K), g, int(splits),
+                           _P(cf), int(ldc), int(cf_mode), float(alpha), _P(cb), int(ldcb), int(cb_accum), _P(bias),
+                           int(relu), _P(colstats), _s())
+    N.check(rc, "tde_igemm")
+
+
+# ---------------------------------------------------------------- Conv2D
+def conv_fwd(x, Wt, y, g: ConvGeom, bias=None, relu=False, colstats=None):
+    """y[B,Ho,Wo,Co] = conv(x[B,H,W,C], W) (+bias, ReLU); Wt = [Co, KH*KW*C] bf16 (transposed shadow)."""
+    _bf(x, g.B * g.H * g.W * g.C, "conv_fwd x")
+    _req(Wt.dtype == bf16 and tuple(Wt.shape) == (g.Co, g.K) and Wt.is_contiguous(), "conv_fwd Wt")
+    _bf(y, g.B * g.Ho * g.Wo * g.Co, "conv_fwd y")
+    if bias is not None:
+        _f32(bias, g.Co, "conv_fwd bias")
+    if colstats is not None:
+        _f32(colstats, 2 * g.Co, "conv_fwd colstats")
+    _igemm(x, 0, A_CONV, Wt, g.K, B_NK, g.B * g.Ho * g.Wo, g.Co, g.K, g, cb=y, ldcb=g.Co, bias=bias, relu=relu,
+           colstats=colstats)
+
+
+def conv_dgrad(dy, Wrow, dx, g: ConvGeom, accum=False):
+    """dx[B,H,W,C] (=|+=) conv_transpose(dy[B,Ho,Wo,Co], W); Wrow = HWIO bf16."""
+    _bf(dy, g.B * g.Ho * g.Wo * g.Co, "conv_dgrad dy")
+    _bf(Wrow, g.K * g.Co, "conv_dgrad W")
+    _bf(dx, g.B * g.H * g.W * g.C, "conv_dgrad dx")
+    _igemm(dy, 0, A_DGRAD, Wrow, 0, B_DGRADW, g.B * g.H * g.W, g.C, g.KH * g.KW * g.Co, g, cb=dx, ldcb=g.C,
+           cb_accum=accum)
+
+
+def conv_wgrad(x, dy, dW, g: ConvGeom, splits=None):
+    """dW[KH,KW,C,Co] (f32) += sum_pixels x (x) dy."""
+    _bf(x, g.B * g.H * g.W * g.C, "conv_wgrad x")
+    _bf(dy, g.B * g.Ho * g.Wo * g.Co, "conv_wgrad dy")
+    _f32(dW, g.K * g.Co, "conv_wgrad dW")
+    M, N_, K = g.K, g.Co, g.B * g.Ho * g.Wo
+    s = pick_splits(M, N_, K) if splits is None else splits
+    _igemm(x, 0, A_WGRAD, dy, g.Co, B_KN, M, N_, K, g, splits=s, cf=dW, ldc=g.Co, cf_mode=2)
+
+
+# ---------------------------------------------------------------- Dense
+def dense_fwd(x, Wt, B, *, y=None, logits=None, bias=None, relu=False, colstats=None):
+    """[B,out] = x[B,in] @ W (+bias, ReLU) -> bf16 ``y`` and/or f32 ``logits``; Wt = [out, in] bf16."""
+    out, fin = Wt.shape
+    _bf(x, B * fin, "dense_fwd x")
+    _req(Wt.dtype == bf16 and Wt.is_contiguous(), "dense_fwd Wt")
+    if y is not None:
+        _bf(y, B * out, "dense_fwd y")
+    if logits is not None:
+        _f32(logits, B * out, "dense_fwd logits")
+    if bias is not None:
+        _f32(bias, out, "dense_fwd bias")
+    if colstats is not None:
+        _f32(colstats, 2 * out, "dense_fwd colstats")
+    _igemm(x, fin, A_ROWK, Wt, fin, B_NK, B, out, fin, cf=logits, ldc=out, cf_mode=1 if logits is not None else 0,
+           cb=y, ldcb=out, bias=bias, relu=relu, colstats=colstats)
+
+
+def dense_dgrad(dy, Wrow, dx, B, accum=False):
+    """dx[B,in] (=|+=) dy[B,out] @ W^T; Wrow = [in, out] bf16."""
+    fin, out = Wrow.shape
+    _bf(dy, B * out, "dense_dgrad dy")
+    _req(Wrow.dtype == bf16 and Wrow.is_contiguous(), "dense_dgrad W")
+    _bf(dx, B * fin, "dense_dgrad dx")
+    _igemm(dy, out, A_ROWK, Wrow, out, B_NK, B, fin, out, cb=dx, ldcb=fin, cb_accum=accum)
+
+
+def dense_wgrad(x, dy, dW, B, splits=None):
+    """dW[in,out] (f32) += x[B,in]^T @ dy[B,out]."""
+    fin, out = dW.shape
+    _bf(x, B * fin, "dense_wgrad x")
+    _bf(dy, B * out, "dense_wgrad dy")
+    _f32(dW, fin * out, "dense_wgrad dW")
+    s = pick_splits(fin, out, B) if splits is None else splits
+    _igemm(x, fin, A_COLM, dy, out, B_KN, fin, out, B, splits=s, cf=dW, ldc=out, cf_mode=2)
+
+
+# ---------------------------------------------------------------- BN / activation / dropout
+@dataclass
+class DropSpec:
+    rate: float = 0.0
+    seed: int = 0
+    iterations: torch.Tensor = None
+    layer_id: int = 0
+
+
+_NODROP = DropSpec()
+
+
+def bn_fwd(y, out, R, Cc, *, mode, stats=None, saved=None, gamma=None, beta=None, eps=1e-3, mmean=None, mvar=None,
+           momentum=0.99, bessel=1.0, zero_buf=None, res=None, relu=False, drop: DropSpec = _NODROP, iter_offset=0):
+    """out = dropout(relu(bn(y) + res)); mode 0 identity, 1 batch stats (from ``stats``), 2 moving stats."""
+    n = R * Cc
+    _bf(y, n, "bn_fwd y")
+    _bf(out, n, "bn_fwd out")
+    _req(Cc <= 2048, "bn_fwd: at most 2048 channels")
+    if res is not None:
+        _bf(res, n, "bn_fwd res")
+    if mode == 1:
+        _f32(stats, 2 * Cc, "bn_fwd stats")
+        _f32(saved, 2 * Cc, "bn_fwd saved")
+    if mode == 2:
+        _f32(mmean, Cc, "bn_fwd moving_mean")
+        _f32(mvar, Cc, "bn_fwd moving_variance")
+    if zero_buf is not None:
+        _f32(zero_buf, 2 * Cc, "bn_fwd zero_buf")
+    rc = N.hip().tde_bn_fwd(_P(y), _P(out), _P(res), int(R), int(Cc), int(mode), _P(stats), _P(saved), _P(gamma),
+                            _P(beta), float(eps), _P(mmean), _P(mvar), float(momentum), float(bessel), _P(zero_buf),
+                            int(relu), float(drop.rate), int(drop.seed) & (2 ** 64 - 1), _P(drop.iterations),
+                            int(iter_offset), int(drop.layer_id), _s())
+    N.check(rc, "tde_bn_fwd")
+
+
+def bn_bwd(dout, y, R, Cc, *, mode, saved=None, gamma=None, beta=None, res=None, relu=False,
+           drop: DropSpec = _NODROP, iter_offset=-1, dstats=None, dx=None, dx_accum=False, dres=None,
+           dres_accum=False, dgamma=None, dbeta=None, zero_fwd=None):
+    n = R * Cc
+    _bf(dout, n, "bn_bwd dout")
+    _bf(y, n, "bn_bwd y")
+    _req(Cc <= 1024, "bn_bwd: at most 1024 channels")
+    if mode == 1:
+        _f32(saved, 2 * Cc, "bn_bwd saved")
+        _f32(dstats, 2 * Cc, "bn_bwd dstats")
+    if dx is not None:
+        _bf(dx, n, "bn_bwd dx")
+    if dres is not None:
+        _bf(dres, n, "bn_bwd dres")
+    if res is not None:
+        _bf(res, n, "bn_bwd res")
+    rc = N.hip().tde_bn_bwd(_P(dout), _P(y), _P(res), int(R), int(Cc), int(mode), _P(saved), _P(gamma), _P(beta),
+                            int(relu), float(drop.rate), int(drop.seed) & (2 ** 64 - 1), _P(drop.iterations),
+                            int(iter_offset), int(drop.layer_id), _P(dstats), _P(dx), int(dx_accum), _P(dres),
+                            int(dres_accum), _P(dgamma), _P(dbeta), _P(zero_fwd), _s())
+    N.check(rc, "tde_bn_bwd")
+
+
+def act_bwd(dout, out, R, Cc, *, relu, dz=None, dbias=None):
+    n = R * Cc
+    _bf(dout, n, "act_bwd dout")
+    if relu:
+        _bf(out, n, "act_bwd out")
+    if dz is not None:
+        _bf(dz, n, "act_bwd dz")
+    if dbias is not None:
+        _f32(dbias, Cc, "act_bwd dbias")
+    _req(Cc <= 1024, "act_bwd: at most 1024 channels")
+    rc = N.hip().tde_act_bwd(_P(dout), _P(out), int(R), int(Cc), int(relu), _P(dz), _P(dbias), _s())
+    N.check(rc, "tde_act_bwd")
+
+
+def colstats(x, R, Cc, stats):
+    _bf(x, R * Cc, "colstats x")
+    _f32(stats, 2 * Cc, "colstats stats")
+    N.check(N.hip().tde_colstats(_P(x), int(R), int(Cc), _P(stats), _s()), "tde_colstats")
+
+
+# ---------------------------------------------------------------- pooling / padding / casts
+def maxpool_fwd(x, y, idx, g: ConvGeom):
+    _bf(x, g.B * g.H * g.W * g.C, "maxpool x")
+    _bf(y, g.B * g.Ho * g.Wo * g.C, "maxpool y")
+    if idx is not None:
+        _req(idx.dtype == torch.uint8 and idx.numel() >= g.B * g.Ho * g.Wo * g.C, "maxpool idx")
+    N.check(N.hip().tde_maxpool(_P(x), _P(y), _P(idx), None, None, 0, g.carray(), 0, _s()), "tde_maxpool")
+
+
+def maxpool_bwd(dy, idx, dx, g: ConvGeom, accum=False):
+    _bf(dy, g.B * g.Ho * g.Wo * g.C, "maxpool dy")
+    _req(idx.dtype == torch.uint8 and idx.numel() >= g.B * g.Ho * g.Wo * g.C, "maxpool idx")
+    _bf(dx, g.B * g.H * g.W * g.C, "maxpool dx")
+    N.check(N.hip().tde_maxpool(None, None, _P(idx), _P(dy), _P(dx), int(accum), g.carray(), 1, _s()),
+            "tde_maxpool")
+
+
+def gap_fwd(x, y, B, HW, Cc):
+    _bf(x, B * HW * Cc, "gap x")
+    _bf(y, B * Cc, "gap y")
+    N.check(N.hip().tde_gap(_P(x), _P(y), B, HW, Cc, 0, 0, _s()), "tde_gap")
+
+
+def gap_bwd(dy, dx, B, HW, Cc, accum=False):
+    _bf(dy, B * Cc, "gap dy")
+    _bf(dx, B * HW * Cc, "gap dx")
+    N.check(N.hip().tde_gap(_P(dy), _P(dx), B, HW, Cc, 1, int(accum), _s()), "tde_gap")
+
+
+def pad_fwd(x, y, g: ConvGeom):
+    _bf(x, g.B * g.H * g.W * g.C, "pad x")
+    _bf(y, g.B * g.Ho * g.Wo * g.C, "pad y")
+    N.check(N.hip().tde_pad(_P(x), _P(y), g.carray(), 0, 0, _s()), "tde_pad")
+
+
+def pad_bwd(dy, dx, g: ConvGeom, accum=False):
+    _bf(dy, g.B * g.Ho * g.Wo * g.C, "pad dy")
+    _bf(dx, g.B * g.H * g.W * g.C, "pad dx")
+    N.check(N.hip().tde_pad(_P(dy), _P(dx), g.carray(), 1, int(accum), _s()), "tde_pad")
+
+
+def cast_bf16(x, y):
+    _req(x.dtype == torch.float32 and x.is_contiguous(), "cast x")
+    _bf(y, x.numel(), "cast y")
+    N.check(N.hip().tde_cast_f32_bf16(_P(x), _P(y), x.numel(), _s()), "tde_cast_f32_bf16")
+
+
+def xent(logits, labels, B, Cc, *, scale=1.0, dlogits=None, metrics=None, probs=None, probs_are_logits=False,
+         iterations=None):
+    _f32(logits, B * Cc, "xent logits")
+    _req(labels.dtype == torch.int32 and labels.numel() >= B, "xent labels")
+    if dlogits is not None:
+        _bf(dlogits, B * Cc, "xent dlogits")
+    if probs is not None:
+        _f32(probs, B * Cc, "xent probs")
+    rc = N.hip().tde_xent(_P(logits), Cc, _P(labels), int(B), int(Cc), float(scale), _P(dlogits), Cc, _P(metrics),
+                          _P(probs), int(probs_are_logits), _P(iterations), _s())
+    N.check(rc, "tde_xent")

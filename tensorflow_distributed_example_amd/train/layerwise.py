@@ -1,6 +1,610 @@
-"""Per-layer HIP kernel plans (Model B, ResNet-18): filled in by ops/layerwise kernels."""
+"""Layer-wise HIP execution plan: any Sequential / functional model built from the
+supported layers (Model B of mnist_keras_distributed.py:79-109 == tf2_mnist_distributed.py
+:105-135, the ResNet-18 stress config, ...) runs its whole training step on the
+gfx950 kernels of csrc/kernels/layers.hip — no torch compute op on the hot path.
+
+The plan compiler walks the model's execution graph once and fuses layer chains
+into *stages* (SURVEY.md §2.5 B1-B17):
+
+    Conv2D/Dense  ->  implicit-GEMM MFMA (+bias, +ReLU, +BN batch statistics in the epilogue)
+    BatchNormalization [-> Add(residual)] [-> ReLU] [-> Dropout]  ->  one bn_fwd pass
+    standalone ReLU / Dropout / Add(+ReLU)  ->  bn_fwd in identity mode
+    MaxPooling2D / GlobalAveragePooling2D / ZeroPadding2D  ->  dedicated kernels
+    Flatten / Reshape  ->  buffer aliases (no kernel)
+    last Dense (+softmax) + SparseCategoricalCrossentropy  ->  GEMM to f32 logits + fused
+        softmax-CE / accuracy / dlogits kernel (probability-space loss on a softmax output
+        is computed from the logits, Q5)
+
+The backward replays the stages in reverse; tensors with several consumers (ResNet
+shortcuts) accumulate their gradients in place (the first writer stores, later ones
+add), BN+ReLU+dropout backward regenerates the dropout mask from the Philox counter
+instead of storing it.  Weight gradients land in the replica's flat fp32 bucket (one
+RCCL all-reduce) and one multi-tensor optimizer kernel applies them and refreshes the
+bf16 weight shadows the GEMMs read.
+"""
 from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .. import backend as Kb
+from ..models import layers as L
+from ..ops import layer_ops as O
+from . import program as PG
+
+bf16 = torch.bfloat16
+
+
+class Unsupported(Exception):
+    pass
+
+
+class _T:
+    """One tensor of the execution graph (per-sample ``shape``)."""
+
+    def __init__(self, tid, shape):
+        self.id = tid
+        self.shape = tuple(shape)
+        self.numel = int(np.prod(self.shape)) if self.shape else 1
+        self.alias = None          # Flatten/Reshape: same storage as another tensor
+        self.consumers = []
+        self.producer = None
+        self.buf = None
+        self.grad = None
+
+    def root(self):
+        t = self
+        while t.alias is not None:
+            t = t.alias
+        return t
+
+    @property
+    def C(self):
+        return self.shape[-1]
+
+    def rows(self, B):
+        return B * (self.numel // self.C)
+
+
+class _Stage:
+    inputs: list
+    out: _T
+
+    def fwd(self, p, B, training):
+        raise NotImplementedError
+
+    def bwd(self, p, B):
+        raise NotImplementedError
+
+
+class LayerwisePlan(PG.ReplicaPlan):
+    kind = "layerwise"
+
+    def __init__(self, model, store, device, batch, global_batch, optimizer, loss):
+        super().__init__(model, store, device, batch, global_batch, optimizer)
+        self.loss = loss
+        self.model = model
+        self._compile()
+        self._alloc()
+        shadows = {}
+        for st in self.stages:
+            for name, want in getattr(st, "shadows", {}).items():
+                shadows[name] = want
+        self.shadows = shadows
+        if optimizer is not None:
+            self.opt = PG.OptimizerKernel(store, optimizer, shadows, self.iterations)
+            self._sh = self.opt
+        else:
+            from ..optimizers import SGD
+            self.opt = None
+            self._sh = PG.OptimizerKernel(store, SGD(0.0), shadows, self.iterations)
+        for st in self.stages:
+            if hasattr(st, "bind_shadows"):
+                st.bind_shadows(self._sh)
+
+    # ------------------------------------------------------------------ compile
+    def _compile(self):
+        m = self.model
+        nodes = m._nodes()
+        T = {0: _T(0, m.input_shape[1:])}
+        for i, (layer, ins, out) in enumerate(nodes):
+            T[out] = _T(out, layer.output_shape)
+            T[out].producer = i
+            for j in ins:
+                T[j].consumers.append(i)
+        self.T = T
+        self.nodes = nodes
+        n_nodes = len(nodes)
+
+        def single(t):
+            return nodes[t.consumers[0]] if len(t.consumers) == 1 else None
+
+        def is_relu(layer):
+            return isinstance(layer, L.Activation) and layer.activation == "relu"
+
+        fused = set()        # node indices absorbed into another stage
+        deferred = {}        # Add node index -> BN stage emitted at that position
+        stages = []
+        bn_fed = {}          # BN node index -> GEMM stage that computes its statistics
+
+        # pass 1: decide GEMM -> BN statistics fusion
+        for i, (layer, ins, out) in enumerate(nodes):
+            if isinstance(layer, (L.Conv2D, L.Dense)) and i != n_nodes - 1 and layer.activation is None:
+                c = single(T[out])
+                if c is not None and isinstance(c[0], L.BatchNormalization):
+                    bn_fed[nodes.index(c)] = i
+
+        last_layer = nodes[-1][0]
+        if not isinstance(last_layer, L.Dense):
+            raise Unsupported(f"last layer {last_layer.name} must be Dense (logits / softmax) for the fused head")
+        strip = PG._last_softmax(m, self.loss)
+        if last_layer.activation not in (None, "softmax") or (last_layer.activation == "softmax") != strip:
+            raise Unsupported("head must be Dense logits with from_logits=True or Dense(softmax) with probabilities")
+        from ..losses import SparseCategoricalCrossentropy
+        if not isinstance(self.loss, SparseCategoricalCrossentropy):
+            raise Unsupported(f"loss {type(self.loss).__name__} has no fused HIP kernel")
+
+        lid = 0
+        for i, (layer, ins, out) in enumerate(nodes):
+            if i in fused:
+                continue
+            tin = [T[j] for j in ins]
+            tout = T[out]
+            if isinstance(layer, (L.Flatten, L.Reshape, L.InputLayer)):
+                tout.alias = tin[0]
+                continue
+            if i == n_nodes - 1:
+                stages.append(_Head(self, layer, tin[0], tout, logits_out=not strip))
+                continue
+            if isinstance(layer, (L.Conv2D, L.Dense)):
+                if layer.activation not in (None, "relu"):
+                    raise Unsupported(f"{layer.name}: activation {layer.activation!r}")
+                stats = i in {v: k for k, v in bn_fed.items()}
+                stages.append(_Gemm(self, layer, tin[0], tout, stats))
+                continue
+            if isinstance(layer, (L.BatchNormalization, L.Activation, L.Dropout, L.Add)):
+                if isinstance(layer, L.Activation) and layer.activation != "relu":
+                    raise Unsupported(f"{layer.name}: activation {layer.activation!r} inside the network")
+                st = _Elementwise(self, layer, tin, tout, lid)
+                lid += 1
+                # absorb the chain that follows: [Add] [ReLU] [Dropout]
+                cur = tout
+                chain = [tout]
+                if isinstance(layer, L.BatchNormalization):
+                    st.stats_from_gemm = i in bn_fed
+                    c = single(cur)
+                    if c is not None and isinstance(c[0], L.Add) and len(c[1]) == 2 and nodes.index(c) not in fused:
+                        k = nodes.index(c)
+                        other = [T[j] for j in c[1] if j != out]
+                        if len(other) == 1:
+                            st.res = other[0]
+                            fused.add(k)
+                            cur = T[c[2]]
+                            chain.append(cur)
+                            st.defer_to = k
+                if not isinstance(layer, L.Dropout) and not (isinstance(layer, L.Activation)):
+                    c = single(cur)
+                    if c is not None and is_relu(c[0]):
+                        st.relu = True
+                        fused.add(nodes.index(c))
+                        cur = T[c[2]]
+                        chain.append(cur)
+                if not isinstance(layer, L.Dropout):
+                    c = single(cur)
+                    if c is not None and isinstance(c[0], L.Dropout):
+                        st.set_dropout(c[0])
+                        fused.add(nodes.index(c))
+                        cur = T[c[2]]
+                        chain.append(cur)
+                st.out = cur
+                for t in chain[:-1]:
+                    t.alias = cur
+                if st.defer_to is not None:
+                    deferred.setdefault(st.defer_to, []).append(st)
+                else:
+                    stages.append(st)
+                continue
+            if isinstance(layer, L.MaxPooling2D):
+                stages.append(_MaxPool(self, layer, tin[0], tout))
+                continue
+            if isinstance(layer, L.GlobalAveragePooling2D):
+                stages.append(_GAP(self, layer, tin[0], tout))
+                continue
+            if isinstance(layer, L.ZeroPadding2D):
+                stages.append(_Pad(self, layer, tin[0], tout))
+                continue
+            raise Unsupported(f"layer {layer.name} ({type(layer).__name__}) has no HIP kernel path")
+        # emit deferred BN+Add stages at the Add's position (after both branches exist)
+        if deferred:
+            out_stages = []
+            pending = sorted(deferred.items())
+            for st in stages:
+                while pending and st.node_index > pending[0][0]:
+                    out_stages += pending.pop(0)[1]
+                out_stages.append(st)
+            for _, lst in pending:
+                out_stages += lst
+            stages = out_stages
+        self.stages = stages
+        # gradient accumulation flags: reverse order, first writer stores
+        written = set()
+        for st in reversed(stages):
+            st.accum = {}
+            for t in st.grad_inputs():
+                r = t.root()
+                st.accum[r.id] = r.id in written
+                written.add(r.id)
+
+    def _alloc(self):
+        B, dev = self.B, self.device
+        self.x_bf = torch.zeros(B * self.T[0].numel, dtype=bf16, device=dev)
+        self.T[0].buf = self.x_bf
+        for t in self.T.values():
+            if t.id == 0 or t.alias is not None:
+                continue
+            t.buf = torch.zeros(B * t.numel, dtype=bf16, device=dev)
+            t.grad = torch.zeros(B * t.numel, dtype=bf16, device=dev)
+        for t in self.T.values():
+            if t.alias is not None:
+                t.buf, t.grad = t.root().buf, t.root().grad
+        for st in self.stages:
+            st.alloc(B, dev)
+
+    # ------------------------------------------------------------------ plan interface
+    def on_weights_loaded(self):
+        self._sh.refresh_shadows()
+
+    def _input(self, x, B):
+        O.cast_bf16(x[:B].reshape(-1), self.x_bf[: B * self.T[0].numel])
+
+    def train_step(self, x, y, B=None):
+        B = self.B if B is None else B
+        self._input(x, B)
+        self._labels = y
+        for st in self.stages:
+            st.fwd(self, B, True)
+        for st in reversed(self.stages):
+            st.bwd(self, B)
+
+    def apply(self):
+        self.opt.apply()
+
+    def eval_step(self, x, y, B=None):
+        B = self.B if B is None else B
+        self._input(x, B)
+        self._labels = y
+        tr = Kb.resolve_training(False)
+        for st in self.stages:
+            st.fwd(self, B, tr, mode="eval")
+        if tr:
+            self._reset_stats()
+
+    def predict(self, x, B=None):
+        B = self.B if B is None else B
+        self._input(x, B)
+        self._labels = self._zero_labels(B)
+        tr = Kb.resolve_training(False)
+        for st in self.stages:
+            st.fwd(self, B, tr, mode="predict")
+        if tr:
+            self._reset_stats()
+        return self.stages[-1].probs[: B * self.stages[-1].C].view(B, -1)
+
+    def _reset_stats(self):
+        for st in self.stages:
+            if getattr(st, "colstats", None) is not None:
+                st.colstats.zero_()
+
+    def _zero_labels(self, B):
+        if not hasattr(self, "_zl") or self._zl.shape[0] < B:
+            self._zl = torch.zeros(max(B, self.B), dtype=torch.int32, device=self.device)
+        return self._zl
+
+
+# ---------------------------------------------------------------------------------------
+class _Gemm(_Stage):
+    def __init__(self, plan, layer, tin, tout, stats):
+        self.layer, self.inp, self.out = layer, tin, tout
+        self.node_index = tout.producer
+        self.stats = stats
+        self.relu = layer.activation == "relu"
+        st = plan.store
+        self.wname = f"{layer.name}/kernel"
+        self.bname = f"{layer.name}/bias" if layer.use_bias else None
+        self.W = st.view(self.wname)
+        self.gW = st.grad(self.wname)
+        self.b = st.view(self.bname) if self.bname else None
+        self.gb = st.grad(self.bname) if self.bname else None
+        self.conv = isinstance(layer, L.Conv2D)
+        need_dgrad = tin.root().id != 0
+        self.need_dgrad = need_dgrad
+        self.shadows = {self.wname: ("row", "col") if need_dgrad else ("col",)}
+        if self.conv:
+            H, W_, C = tin.shape
+            Ho, Wo, Co = tout.shape
+            (pt, _), (pl, _) = layer.pads(tin.shape)
+            self.geo = O.ConvGeom(plan.B, H, W_, C, Ho, Wo, Co, layer.kernel_size[0], layer.kernel_size[1],
+                                  layer.strides[0], layer.strides[1], pt, pl)
+        self.colstats = None
+        self.dz = None
+
+    def alloc(self, B, dev):
+        if self.stats:
+            self.colstats = torch.zeros(2 * self.out.C, dtype=torch.float32, device=dev)
+        if self.relu or self.gb is not None:
+            self.dz = torch.zeros(B * self.out.numel, dtype=bf16, device=dev)
+
+    def bind_shadows(self, sh):
+        self.Wt = sh.shadow_views[(self.wname, "col")]
+        self.Wrow = sh.shadow_views.get((self.wname, "row"))
+
+    def grad_inputs(self):
+        return [self.inp] if self.need_dgrad else []
+
+    def fwd(self, p, B, training, mode="train"):
+        cs = self.colstats if (self.stats and training) else None
+        if self.conv:
+            O.conv_fwd(self.inp.buf, self.Wt, self.out.root().buf, self.geo.with_batch(B), bias=self.b,
+                       relu=self.relu, colstats=cs)
+        else:
+            rows = self.inp.rows(B)
+            O.dense_fwd(self.inp.buf, self.Wt, rows, y=self.out.root().buf, bias=self.b, relu=self.relu,
+                        colstats=cs)
+
+    def bwd(self, p, B):
+        dout = self.out.root().grad
+        if self.dz is not None:
+            O.act_bwd(dout, self.out.root().buf, self.out.rows(B), self.out.C, relu=self.relu, dz=self.dz,
+                      dbias=self.gb)
+            dout = self.dz
+        if self.conv:
+            g = self.geo.with_batch(B)
+            O.conv_wgrad(self.inp.buf, dout, self.gW, g)
+            if self.need_dgrad:
+                O.conv_dgrad(dout, self.Wrow, self.inp.root().grad, g, accum=self.accum[self.inp.root().id])
+        else:
+            rows = self.inp.rows(B)
+            O.dense_wgrad(self.inp.buf, dout, self.gW.view(self.W.shape[0], -1), rows)
+            if self.need_dgrad:
+                O.dense_dgrad(dout, self.Wrow, self.inp.root().grad, rows, accum=self.accum[self.inp.root().id])
+
+
+class _Elementwise(_Stage):
+    """BatchNormalization / Activation(relu) / Dropout / Add, each optionally followed by the
+    fused [Add] [ReLU] [Dropout] chain: out = dropout(relu(affine(y) + res))."""
+
+    def __init__(self, plan, layer, tin, tout, lid):
+        self.plan = plan
+        self.layer = layer
+        self.node_index = tout.producer
+        self.bn = isinstance(layer, L.BatchNormalization)
+        self.add = isinstance(layer, L.Add)
+        if self.add and len(tin) != 2:
+            raise Unsupported(f"{layer.name}: Add of {len(tin)} inputs")
+        self.inp = tin[0]
+        self.res = tin[1] if self.add else None
+        self.out = tout
+        self.relu = isinstance(layer, L.Activation)
+        self.drop = O.DropSpec()
+        self.lid = lid
+        self.defer_to = None
+        self.stats_from_gemm = False
+        if isinstance(layer, L.Dropout):
+            self.set_dropout(layer)
+        st = plan.store
+        self.colstats = None
+        if self.bn:
+            n = layer.name
+            self.gamma = st.view(f"{n}/gamma") if layer.scale else None
+            self.beta = st.view(f"{n}/beta") if layer.center else None
+            self.ggamma = st.grad(f"{n}/gamma") if layer.scale and st.segments[f"{n}/gamma"].trainable else None
+            self.gbeta = st.grad(f"{n}/beta") if layer.center and st.segments[f"{n}/beta"].trainable else None
+            self.mmean = st.view(f"{n}/moving_mean")
+            self.mvar = st.view(f"{n}/moving_variance")
+
+    def set_dropout(self, layer):
+        g = Kb.make_generator(7919 + self.lid)
+        seed = int(torch.randint(0, 2 ** 62, (1,), generator=g).item()) if layer.seed is None else int(layer.seed)
+        self.drop = O.DropSpec(layer.rate, seed, self.plan.iterations, self.lid)
+
+    def alloc(self, B, dev):
+        C = self.inp.C
+        if self.bn:
+            self.saved = torch.zeros(2 * C, dtype=torch.float32, device=dev)
+            self.dstats = torch.zeros(2 * C, dtype=torch.float32, device=dev)
+            if self.stats_from_gemm:
+                self.colstats = None   # bound below to the producing GEMM's buffer
+            else:
+                self.colstats = torch.zeros(2 * C, dtype=torch.float32, device=dev)
+        if self.bn and self.stats_from_gemm:
+            for st in self.plan.stages:
+                if isinstance(st, _Gemm) and st.out.root() is self.inp.root():
+                    self._gemm = st
+                    break
+
+    def _stats(self):
+        if self.stats_from_gemm:
+            return self._gemm.colstats
+        return self.colstats
+
+    def grad_inputs(self):
+        out = []
+        if self.inp.root().id != 0:
+            out.append(self.inp)
+        if self.res is not None and self.res.root().id != 0:
+            out.append(self.res)
+        return out
+
+    def fwd(self, p, B, training, mode="train"):
+        R, C = self.inp.rows(B), self.inp.C
+        drop = self.drop if (training and self.drop.rate > 0) else O.DropSpec()
+        kw = dict(res=self.res.root().buf if self.res is not None else None, relu=self.relu, drop=drop,
+                  iter_offset=0)
+        if not self.bn:
+            O.bn_fwd(self.inp.root().buf, self.out.root().buf, R, C, mode=0, **kw)
+            return
+        L_ = self.layer
+        if training:
+            stats = self._stats()
+            if not self.stats_from_gemm:
+                O.colstats(self.inp.root().buf, R, C, stats)
+            upd = mode == "train"
+            bessel = (R / max(R - 1, 1)) if L_.fused else 1.0
+            O.bn_fwd(self.inp.root().buf, self.out.root().buf, R, C, mode=1, stats=stats, saved=self.saved,
+                     gamma=self.gamma, beta=self.beta, eps=L_.epsilon, mmean=self.mmean if upd else None,
+                     mvar=self.mvar if upd else None, momentum=L_.momentum, bessel=bessel,
+                     zero_buf=self.dstats if upd else None, **kw)
+        else:
+            O.bn_fwd(self.inp.root().buf, self.out.root().buf, R, C, mode=2, gamma=self.gamma, beta=self.beta,
+                     eps=L_.epsilon, mmean=self.mmean, mvar=self.mvar, **kw)
+
+    def bwd(self, p, B):
+        R, C = self.inp.rows(B), self.inp.C
+        ir = self.inp.root()
+        rr = self.res.root() if self.res is not None else None
+        dx = ir.grad if ir.id != 0 else None
+        dres = rr.grad if (rr is not None and rr.id != 0) else None
+        O.bn_bwd(self.out.root().grad, ir.buf, R, C, mode=1 if self.bn else 0,
+                 saved=self.saved if self.bn else None, gamma=self.gamma if self.bn else None,
+                 beta=self.beta if self.bn else None, res=rr.buf if rr is not None else None, relu=self.relu,
+                 drop=self.drop, iter_offset=-1, dstats=self.dstats if self.bn else None,
+                 dx=dx, dx_accum=self.accum.get(ir.id, False), dres=dres,
+                 dres_accum=self.accum.get(rr.id, False) if rr is not None else False,
+                 dgamma=self.ggamma if self.bn else None, dbeta=self.gbeta if self.bn else None,
+                 zero_fwd=self._stats() if self.bn else None)
+
+
+class _MaxPool(_Stage):
+    def __init__(self, plan, layer, tin, tout):
+        self.inp, self.out = tin, tout
+        self.node_index = tout.producer
+        H, W_, C = tin.shape
+        Ho, Wo, _ = tout.shape
+        if layer.padding == "same":
+            pt = L.tf_same_pads(H, layer.pool_size[0], layer.strides[0])[0]
+            pl = L.tf_same_pads(W_, layer.pool_size[1], layer.strides[1])[0]
+        else:
+            pt = pl = 0
+        self.geo = O.ConvGeom(plan.B, H, W_, C, Ho, Wo, C, layer.pool_size[0], layer.pool_size[1],
+                              layer.strides[0], layer.strides[1], pt, pl)
+
+    def alloc(self, B, dev):
+        self.idx = torch.zeros(B * self.out.numel, dtype=torch.uint8, device=dev)
+
+    def grad_inputs(self):
+        return [self.inp] if self.inp.root().id != 0 else []
+
+    def fwd(self, p, B, training, mode="train"):
+        O.maxpool_fwd(self.inp.root().buf, self.out.root().buf, self.idx, self.geo.with_batch(B))
+
+    def bwd(self, p, B):
+        if self.inp.root().id == 0:
+            return
+        O.maxpool_bwd(self.out.root().grad, self.idx, self.inp.root().grad, self.geo.with_batch(B),
+                      accum=self.accum[self.inp.root().id])
+
+
+class _GAP(_Stage):
+    def __init__(self, plan, layer, tin, tout):
+        self.inp, self.out = tin, tout
+        self.node_index = tout.producer
+        self.HW = tin.shape[0] * tin.shape[1]
+        self.C = tin.shape[2]
+
+    def alloc(self, B, dev):
+        pass
+
+    def grad_inputs(self):
+        return [self.inp] if self.inp.root().id != 0 else []
+
+    def fwd(self, p, B, training, mode="train"):
+        O.gap_fwd(self.inp.root().buf, self.out.root().buf, B, self.HW, self.C)
+
+    def bwd(self, p, B):
+        if self.inp.root().id == 0:
+            return
+        O.gap_bwd(self.out.root().grad, self.inp.root().grad, B, self.HW, self.C,
+                  accum=self.accum[self.inp.root().id])
+
+
+class _Pad(_Stage):
+    def __init__(self, plan, layer, tin, tout):
+        self.inp, self.out = tin, tout
+        self.node_index = tout.producer
+        H, W_, C = tin.shape
+        Ho, Wo, _ = tout.shape
+        (t, _), (l, _) = layer.padding
+        self.geo = O.ConvGeom(plan.B, H, W_, C, Ho, Wo, C, 1, 1, 1, 1, t, l)
+
+    def alloc(self, B, dev):
+        pass
+
+    def grad_inputs(self):
+        return [self.inp] if self.inp.root().id != 0 else []
+
+    def fwd(self, p, B, training, mode="train"):
+        O.pad_fwd(self.inp.root().buf, self.out.root().buf, self.geo.with_batch(B))
+
+    def bwd(self, p, B):
+        if self.inp.root().id == 0:
+            return
+        O.pad_bwd(self.out.root().grad, self.inp.root().grad, self.geo.with_batch(B),
+                  accum=self.accum[self.inp.root().id])
+
+
+class _Head(_Stage):
+    """Last Dense -> f32 logits (+bias) -> softmax cross-entropy / accuracy / dlogits."""
+
+    def __init__(self, plan, layer, tin, tout, logits_out):
+        if len(tin.shape) != 1:
+            raise Unsupported("the head Dense must see a flat [B, features] input")
+        self.plan = plan
+        self.inp, self.out = tin, tout
+        self.node_index = tout.producer
+        self.layer = layer
+        self.logits_out = logits_out
+        st = plan.store
+        self.wname = f"{layer.name}/kernel"
+        self.bname = f"{layer.name}/bias" if layer.use_bias else None
+        self.b = st.view(self.bname) if self.bname else None
+        self.gb = st.grad(self.bname) if self.bname else None
+        self.gW = st.grad(self.wname)
+        self.need_dgrad = tin.root().id != 0
+        self.shadows = {self.wname: ("row", "col") if self.need_dgrad else ("col",)}
+        self.C = layer.units
+
+    def alloc(self, B, dev):
+        self.logits = torch.zeros(B * self.C, dtype=torch.float32, device=dev)
+        self.dlogits = torch.zeros(B * self.C, dtype=bf16, device=dev)
+        self.probs = torch.zeros(B * self.C, dtype=torch.float32, device=dev)
+
+    def bind_shadows(self, sh):
+        self.Wt = sh.shadow_views[(self.wname, "col")]
+        self.Wrow = sh.shadow_views.get((self.wname, "row"))
+
+    def grad_inputs(self):
+        return [self.inp] if self.need_dgrad else []
+
+    def fwd(self, p, B, training, mode="train"):
+        O.dense_fwd(self.inp.root().buf, self.Wt, B, logits=self.logits, bias=self.b)
+        if mode == "train":
+            O.xent(self.logits, p._labels, B, self.C, scale=p.scale, dlogits=self.dlogits, metrics=p.metrics,
+                   iterations=p.iterations)
+        elif mode == "eval":
+            O.xent(self.logits, p._labels, B, self.C, scale=p.scale, metrics=p.metrics)
+        else:
+            O.xent(self.logits, p._labels, B, self.C, probs=self.probs, probs_are_logits=self.logits_out)
+
+    def bwd(self, p, B):
+        if self.gb is not None:
+            O.act_bwd(self.dlogits, None, B, self.C, relu=False, dbias=self.gb)
+        O.dense_wgrad(self.inp.root().buf, self.dlogits, self.gW, B)
+        if self.need_dgrad:
+            O.dense_dgrad(self.dlogits, self.Wrow, self.inp.root().grad, B, accum=self.accum[self.inp.root().id])
 
 
 def try_make(model, store, device, batch, global_batch, optimizer, loss):
-    return None
+    try:
+        return LayerwisePlan(model, store, device, batch, global_batch, optimizer, loss)
+    except Unsupported:
+        return None

@@ -106,19 +106,20 @@ class ReferencePlan(ReplicaPlan):
         return W
 
     def _forward(self, x, W, training, updates=None):
-        h = x.float()
-        layers = self.model.layers
-        for i, layer in enumerate(layers):
-            if i == len(layers) - 1 and self.strip_softmax:
+        t = {0: x.float()}
+        nodes = self.model._nodes()
+        for i, (layer, ins, out) in enumerate(nodes):
+            h = [t[j] for j in ins] if layer.multi_input else t[ins[0]]
+            if i == len(nodes) - 1 and self.strip_softmax:
                 act = layer.activation
                 layer.activation = None
                 try:
-                    h = layer.ref_call(h, W[layer.name], training, self.rng, updates)
+                    t[out] = layer.ref_call(h, W[layer.name], training, self.rng, updates)
                 finally:
                     layer.activation = act
             else:
-                h = layer.ref_call(h, W[layer.name], training, self.rng, updates)
-        return h
+                t[out] = layer.ref_call(h, W[layer.name], training, self.rng, updates)
+        return t[nodes[-1][2]]
 
     def train_step(self, x, y, B=None):
         B = x.shape[0] if B is None else B
@@ -181,7 +182,9 @@ class OptimizerKernel:
         layout = []
         for name in store.names(trainable=True):
             seg = store.segments[name]
-            rows, cols = (seg.shape[0], int(np.prod(seg.shape[1:]))) if len(seg.shape) >= 2 else (1, seg.numel)
+            # 2-D view [prod(shape[:-1]), shape[-1]]: Dense [in, out] and conv HWIO as [KH*KW*Cin, Cout],
+            # so the transposed ("col") shadow is the K-contiguous [out, K] operand of the forward GEMM
+            rows, cols = (int(np.prod(seg.shape[:-1])), seg.shape[-1]) if len(seg.shape) >= 2 else (1, seg.numel)
             sh = sht = -1
             if name in shadows:
                 want = shadows[name]

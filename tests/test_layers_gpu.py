@@ -1,0 +1,319 @@
+"""T0/T1 for the layer-wise kernel library (csrc/kernels/layers.hip): every kernel vs a
+plain PyTorch fp32 reference of the same op on bf16-rounded operands, then whole-model
+gradients of the layer-wise plan (Model B, a small ResNet) vs the torch autograd plan."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+bf = torch.bfloat16
+
+
+def _r(*shape, seed=0, scale=1.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(bf).to(DEV)
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _tf_same(n, k, s):
+    out = -(-n // s)
+    tot = max((out - 1) * s + k - n, 0)
+    return tot // 2, tot - tot // 2
+
+
+CONV_CASES = [
+    # B, H, W, C, Co, k, s, padding
+    (4, 28, 28, 1, 6, 3, 1, "same"),     # Model B conv1
+    (4, 28, 28, 6, 12, 6, 2, "same"),    # Model B conv2
+    (4, 14, 14, 12, 24, 6, 2, "same"),   # Model B conv3
+    (2, 16, 16, 16, 64, 3, 1, "same"),   # vector paths
+    (2, 17, 15, 8, 24, 3, 2, "same"),    # odd sizes, stride 2, asymmetric pads
+    (2, 15, 15, 3, 64, 7, 2, "same"),    # ResNet stem shape family
+    (2, 8, 8, 64, 128, 1, 2, "valid"),   # projection shortcut
+    (3, 10, 9, 32, 40, 3, 1, "valid"),   # N tail
+]
+
+
+@pytest.mark.parametrize("B,H,W,C,Co,k,s,pad", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(B, H, W, C, Co, k, s, pad):
+    from tensorflow_distributed_example_amd.ops import layer_ops as O
+    if pad == "same":
+        (pt, pb), (pl, pr) = _tf_same(H, k, s), _tf_same(W, k, s)
+        Ho, Wo = -(-H // s), -(-W // s)
+    else:
+        pt = pb = pl = pr = 0
+        Ho, Wo = (H - k) // s + 1, (W - k) // s + 1
+    x = _r(B, H, W, C, seed=1)
+    w = _r(k, k, C, Co, seed=2, scale=0.2)
+    bias = torch.randn(Co, device=DEV)
+    g = O.ConvGeom(B, H, W, C, Ho, Wo, Co, k, k, s, s, pt, pl)
+    # forward (+bias, ReLU, column statistics)
+    y = torch.zeros(B, Ho, Wo, Co, dtype=bf, device=DEV)
+    stats = torch.zeros(2 * Co, device=DEV)
+    Wt = w.reshape(-1, Co).t().contiguous()
+    O.conv_fwd(x, Wt, y, g, bias=bias, relu=False, colstats=stats)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w.float().permute(3, 2, 0, 1).requires_grad_(True)
+    ref = F.conv2d(F.pad(xr, (pl, pr, pt, pb)), wr, bias, stride=s).permute(0, 2, 3, 1)
+    torch.cuda.synchronize()
+    assert _rel(y.float(), ref) < 1e-2
+    rs = ref.detach()
+    assert (stats[:Co] - rs.sum((0, 1, 2))).abs().max().item() <= 1e-4 * rs.abs().sum((0, 1, 2)).max().item() + 1e-3
+    assert _rel(stats[Co:], (rs ** 2).sum((0, 1, 2))) < 1e-3
+    # backward
+    dy = _r(B, Ho, Wo, Co, seed=3)
+    ref.backward(dy.float())
+    dx = torch.zeros(B, H, W, C, dtype=bf, device=DEV)
+    O.conv_dgrad(dy, w.contiguous(), dx, g)
+    dW = torch.zeros(k, k, C, Co, device=DEV)
+    O.conv_wgrad(x, dy, dW, g)
+    torch.cuda.synchronize()
+    assert _rel(dx.float(), xr.grad.permute(0, 2, 3, 1)) < 1e-2
+    assert _rel(dW, wr.grad.permute(2, 3, 1, 0)) < 1e-3
+    # accumulate mode
+    dx2 = dx.clone()
+    O.conv_dgrad(dy, w.contiguous(), dx2, g, accum=True)
+    torch.cuda.synchronize()
+    assert _rel(dx2.float(), 2 * dx.float()) < 1e-2
+
+
+@pytest.mark.parametrize("B,fin,out,relu", [(128, 1176, 200, False), (37, 64, 10, True), (256, 512, 1000, False),
+                                             (5, 13, 7, True)])
+def test_dense_fwd_dgrad_wgrad(B, fin, out, relu):
+    from tensorflow_distributed_example_amd.ops import layer_ops as O
+    x = _r(B, fin, seed=4)
+    w = _r(fin, out, seed=5, scale=0.1)
+    bias = torch.randn(out, device=DEV)
+    y = torch.zeros(B, out, dtype=bf, device=DEV)
+    logits = torch.zeros(B, out, device=DEV)
+    O.dense_fwd(x, w.t().contiguous(), B, y=y, logits=logits, bias=bias, relu=relu)
+    ref = x.float() @ w.float() + bias
+    if relu:
+        ref = F.relu(ref)
+    dy = _r(B, out, seed=6)
+    dx = torch.zeros(B, fin, dtype=bf, device=DEV)
+    O.dense_dgrad(dy, w.contiguous(), dx, B)
+    dW = torch.zeros(fin, out, device=DEV)
+    O.dense_wgrad(x, dy, dW, B)
+    torch.cuda.synchronize()
+    assert _rel(logits, ref) < 1e-4
+    assert _rel(y.float(), ref) < 1e-2
+    assert _rel(dx.float(), dy.float() @ w.float().t()) < 1e-2
+    assert _rel(dW, x.float().t() @ dy.float()) < 1e-4
+
+
+@pytest.mark.parametrize("R,C,relu,res,fused", [(4 * 784, 6, True, False, True), (128, 200, True, False, False),
+                                                (2 * 64, 64, True, True, True), (50, 24, False, False, True)])
+def test_batchnorm_fwd_bwd(R, C, relu, res, fused):
+    from tensorflow_distributed_example_amd.ops import layer_ops as O
+    y = _r(R, C, seed=7, scale=2.0) + 0.5
+    r = _r(R, C, seed=8) if res else None
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.1
+    stats = torch.zeros(2 * C, device=DEV)
+    O.colstats(y, R, C, stats)
+    saved = torch.zeros(2 * C, device=DEV)
+    mm, mv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    out = torch.zeros(R, C, dtype=bf, device=DEV)
+    dstats = torch.full((2 * C,), 7.0, device=DEV)
+    bessel = R / (R - 1) if fused else 1.0
+    O.bn_fwd(y, out, R, C, mode=1, stats=stats, saved=saved, gamma=gamma, beta=beta, eps=1e-3, mmean=mm, mvar=mv,
+             momentum=0.99, bessel=bessel, zero_buf=dstats, res=r, relu=relu)
+    yr = y.float().requires_grad_(True)
+    mean, var = yr.mean(0), yr.var(0, unbiased=False)
+    z = (yr - mean) * torch.rsqrt(var + 1e-3) * gamma + beta
+    if res:
+        z = z + r.float()
+    if relu:
+        z = F.relu(z)
+    torch.cuda.synchronize()
+    assert _rel(out.float(), z) < 1e-2
+    assert torch.allclose(mm, 0.01 * mean.detach(), atol=1e-5, rtol=1e-3)
+    assert torch.allclose(mv, 0.99 + 0.01 * var.detach() * bessel, atol=1e-5, rtol=1e-3)
+    assert dstats.abs().max().item() == 0.0   # zeroed for the backward
+    dout = _r(R, C, seed=9)
+    z.backward(dout.float())
+    dx = torch.zeros(R, C, dtype=bf, device=DEV)
+    dres = torch.zeros(R, C, dtype=bf, device=DEV) if res else None
+    dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    O.bn_bwd(dout, y, R, C, mode=1, saved=saved, gamma=gamma, beta=beta, res=r, relu=relu, dstats=dstats, dx=dx,
+             dres=dres, dgamma=dg, dbeta=db, zero_fwd=stats)
+    torch.cuda.synchronize()
+    zz = (yr.detach() - mean.detach()) * torch.rsqrt(var.detach() + 1e-3) * gamma + beta + (r.float() if res else 0)
+    dz = dout.float() * (zz > 0) if relu else dout.float()
+    assert _rel(dx.float(), yr.grad) < 2e-2
+    assert _rel(db, dz.sum(0)) < 1e-3
+    xhat = (yr.detach() - mean.detach()) * torch.rsqrt(var.detach() + 1e-3)
+    assert _rel(dg, (dz * xhat).sum(0)) < 1e-2
+    if res:
+        assert _rel(dres.float(), dz) < 1e-2
+    assert stats.abs().max().item() == 0.0
+
+
+def test_dropout_mask_regenerated_in_backward():
+    from tensorflow_distributed_example_amd.ops import layer_ops as O
+    R, C = 512, 200
+    y = _r(R, C, seed=10).abs() + 0.1
+    it = torch.tensor([5], dtype=torch.int64, device=DEV)
+    d = O.DropSpec(0.5, 1234, it, 3)
+    out = torch.zeros(R, C, dtype=bf, device=DEV)
+    O.bn_fwd(y, out, R, C, mode=0, relu=True, drop=d, iter_offset=0)
+    it += 1  # the loss kernel advances the step counter between forward and backward
+    dout = torch.ones(R, C, dtype=bf, device=DEV)
+    dx = torch.zeros(R, C, dtype=bf, device=DEV)
+    O.bn_bwd(dout, y, R, C, mode=0, relu=True, drop=d, iter_offset=-1, dx=dx)
+    torch.cuda.synchronize()
+    kept = out.float() != 0
+    frac = kept.float().mean().item()
+    assert 0.45 < frac < 0.55
+    assert torch.equal(kept, dx.float() != 0)
+    assert torch.allclose(dx.float()[kept], torch.full_like(dx.float()[kept], 2.0))
+    assert torch.allclose(out.float()[kept], 2 * y.float()[kept], rtol=1e-2)
+    # a different step gives a different mask
+    out2 = torch.zeros_like(out)
+    O.bn_fwd(y, out2, R, C, mode=0, relu=True, drop=d, iter_offset=0)
+    torch.cuda.synchronize()
+    assert not torch.equal(out2 != 0, kept)
+
+
+@pytest.mark.parametrize("H,W,k,s,pad", [(112, 112, 3, 2, "same"), (26, 26, 2, 2, "valid"), (9, 7, 3, 2, "same")])
+def test_maxpool(H, W, k, s, pad):
+    from tensorflow_distributed_example_amd.ops import layer_ops as O
+    B, C = 2, 16
+    if pad == "same":
+        (pt, pb), (pl, pr) = _tf_same(H, k, s), _tf_same(W, k, s)
+        Ho, Wo = -(-H // s), -(-W // s)
+    else:
+        pt = pb = pl = pr = 0
+        Ho, Wo = (H - k) // s + 1, (W - k) // s + 1
+    x = _r(B, H, W, C, seed=11)
+    g = O.ConvGeom(B, H, W, C, Ho, Wo, C, k, k, s, s, pt, pl)
+    y = torch.zeros(B, Ho, Wo, C, dtype=bf, device=DEV)
+    idx = torch.zeros(B * Ho * Wo * C, dtype=torch.uint8, device=DEV)
+    O.maxpool_fwd(x, y, idx, g)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    ref = F.max_pool2d(F.pad(xr, (pl, pr, pt, pb), value=float("-inf")), k, s).permute(0, 2, 3, 1)
+    dy = _r(B, Ho, Wo, C, seed=12)
+    ref.backward(dy.float())
+    dx = torch.zeros(B, H, W, C, dtype=bf, device=DEV)
+    O.maxpool_bwd(dy, idx, dx, g)
+    torch.cuda.synchronize()
+    assert torch.equal(y.float(), ref.detach())
+    assert _rel(dx.float(), xr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
+def test_gap_pad_xent():
+    from tensorflow_distributed_example_amd.ops import layer_ops as O
+    B, H, W, C = 3, 7, 7, 512
+    x = _r(B, H, W, C, seed=13)
+    y = torch.zeros(B, C, dtype=bf, device=DEV)
+    O.gap_fwd(x, y, B, H * W, C)
+    dy = _r(B, C, seed=14)
+    dx = torch.zeros(B, H, W, C, dtype=bf, device=DEV)
+    O.gap_bwd(dy, dx, B, H * W, C)
+    g = O.ConvGeom(B, H, W, C, H + 3, W + 1, C, 1, 1, 1, 1, 1, 0)
+    yp = torch.zeros(B, H + 3, W + 1, C, dtype=bf, device=DEV)
+    O.pad_fwd(x, yp, g)
+    dxp = torch.zeros(B, H, W, C, dtype=bf, device=DEV)
+    O.pad_bwd(yp, dxp, g)
+    Bx, Cx = 37, 1000
+    logits = torch.randn(Bx, Cx, device=DEV) * 3
+    labels = torch.randint(0, Cx, (Bx,), device=DEV, dtype=torch.int32)
+    labels[:5] = logits[:5].argmax(1).int()
+    dl = torch.zeros(Bx, Cx, dtype=bf, device=DEV)
+    met = torch.zeros(4, device=DEV)
+    it = torch.zeros(1, dtype=torch.int64, device=DEV)
+    O.xent(logits, labels, Bx, Cx, scale=0.5, dlogits=dl, metrics=met, iterations=it)
+    probs = torch.zeros(Bx, Cx, device=DEV)
+    O.xent(logits, labels, Bx, Cx, probs=probs)
+    torch.cuda.synchronize()
+    assert _rel(y.float(), x.float().mean((1, 2))) < 1e-2
+    assert _rel(dx.float(), dy.float()[:, None, None, :].expand(B, H, W, C) / (H * W)) < 1e-2
+    assert torch.equal(yp[:, 1:1 + H, :W].float(), x.float()) and yp[:, 0].abs().sum() == 0
+    assert torch.equal(dxp, x)
+    lr = logits.requires_grad_(True)
+    loss = F.cross_entropy(lr, labels.long(), reduction="sum")
+    (loss * 0.5).backward()
+    assert abs(met[0].item() - loss.item()) < 1e-3 * loss.item()
+    assert met[1].item() == (logits.argmax(1) == labels).sum().item() and met[2].item() == Bx
+    assert _rel(dl.float(), lr.grad) < 1e-2
+    assert _rel(probs, torch.softmax(logits.detach(), 1)) < 1e-5
+    assert it.item() == 1
+
+
+def _grad_compare(model, x, y, B, thresholds, default=0.05):
+    from tensorflow_distributed_example_amd.train import program as PG
+    from tensorflow_distributed_example_amd.train.layerwise import LayerwisePlan
+    st = model._store
+    st_ref = st.clone_to("cuda")
+    plan = PG.make_plan(model, st, "cuda", B, B, model.optimizer, model.loss)
+    assert isinstance(plan, LayerwisePlan)
+    ref = PG.ReferencePlan(model, st_ref, "cuda", B, B, model.optimizer, model.loss)
+    xt = torch.from_numpy(x).cuda()
+    yt = torch.from_numpy(y).int().cuda()
+    plan.train_step(xt, yt)
+    ref.train_step(xt, yt.long())
+    torch.cuda.synchronize()
+    errs = {}
+    for name in st.names(trainable=True):
+        errs[name] = _rel(st.grad(name), st_ref.grad(name))
+    for name in st.names(trainable=False):   # BN moving statistics after one update
+        errs[name] = _rel(st.view(name), st_ref.view(name))
+    print("layerwise vs reference rel err", errs)
+    for name, e in errs.items():
+        lim = next((v for k, v in thresholds.items() if k in name), default)
+        assert e < lim, (name, e)
+    return plan, ref
+
+
+def test_model_b_layerwise_gradients_match_reference():
+    import tensorflow_distributed_example_amd as tde
+    m = tde.zoo.mnist_bn_cnn()
+    for l in m.layers:
+        if isinstance(l, tde.keras.layers.Dropout):
+            l.rate = 0.0      # the reference plan draws its mask from torch's RNG
+    m.compile(loss="sparse_categorical_crossentropy", optimizer=tde.optimizers.SGD(0.01), metrics=["accuracy"])
+    m.build()
+    rng = np.random.default_rng(0)
+    x = rng.random((64, 784), dtype=np.float32)
+    y = rng.integers(0, 10, 64)
+    plan, ref = _grad_compare(m, x, y, 64, {"moving": 1e-2})
+    lf = tde.metrics.logs_from(plan.metrics, ["accuracy"])
+    lr = tde.metrics.logs_from(ref.metrics, ["accuracy"])
+    assert abs(lf["loss"] - lr["loss"]) < 1e-2 * lr["loss"]
+
+
+def test_small_resnet_layerwise_gradients_match_reference():
+    import tensorflow_distributed_example_amd as tde
+    m = tde.zoo.resnet18(input_shape=(32, 32, 3), classes=10)
+    m.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True), optimizer=tde.optimizers.SGD(0.01),
+              metrics=["accuracy"])
+    m.build()
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((16, 32, 32, 3), dtype=np.float32)
+    y = rng.integers(0, 10, 16)
+    _grad_compare(m, x, y, 16, {"moving": 2e-2}, default=0.08)
+
+
+def test_model_b_trains_with_dropout_and_graph():
+    import tensorflow_distributed_example_amd as tde
+    (xt, yt), _ = tde.data.mnist.load_data()
+    xt = (xt[:4096] / 255.0).astype(np.float32).reshape(-1, 784)
+    yt = yt[:4096]
+    m = tde.zoo.mnist_bn_cnn()
+    m.compile(loss="sparse_categorical_crossentropy", optimizer=tde.optimizers.SGD(0.05), metrics=["accuracy"],
+              steps_per_execution=8)
+    h = m.fit(xt, yt, batch_size=128, epochs=3, shuffle=False, verbose=0)
+    prog = m._program("train", 128)
+    assert prog.plan_kind == "layerwise" and prog.use_graph
+    assert h.history["loss"][-1] < h.history["loss"][0]
+    ev = m.evaluate(xt[:1024], yt[:1024], batch_size=128, verbose=0, return_dict=True)
+    assert ev["accuracy"] > 0.5
+    p = m.predict(xt[:200], batch_size=128)
+    assert p.shape == (200, 10) and np.allclose(p.sum(1), 1.0, atol=1e-3)
