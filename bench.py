@@ -26,15 +26,25 @@ import time
 METRIC = "images/sec (whole node) MNIST CNN at 1/2/4/8 MI355X; step time ms"
 
 
+# model -> (per-GPU batch, steps_per_execution, lr, from_logits, image shape, metric); batches follow the
+# reference: 64 per worker (distributed_with_keras.py:13), 128 per replica (mnist_keras_distributed.py:50-54)
+MODELS = {
+    "mnist_cnn": (64, 16, 0.001, True, (28, 28, 1), METRIC),
+    "mnist_bn_cnn": (128, 16, 0.01, False, (784,), METRIC),
+    "resnet18": (64, 1, 0.1, True, (224, 224, 3),
+                 "images/sec (whole node) synthetic 224x224x3 ResNet-18 bf16 at 1/2/4/8 MI355X; step time ms"),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=64)
-    ap.add_argument("--model", default="mnist_cnn", choices=["mnist_cnn", "mnist_bn_cnn"])
-    ap.add_argument("--batch-per-gpu", type=int, default=64)
-    ap.add_argument("--spe", type=int, default=16, help="steps_per_execution (steps per hipGraph replay)")
-    ap.add_argument("--lr", type=float, default=0.001)
+    ap.add_argument("--model", default="mnist_cnn", choices=sorted(MODELS))
+    ap.add_argument("--batch-per-gpu", type=int, default=None)
+    ap.add_argument("--spe", type=int, default=None, help="steps_per_execution (steps per hipGraph replay)")
+    ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--executor", default=None, help="fused|reference (default: fused on GPU)")
     ap.add_argument("--no-graph", action="store_true")
     return ap.parse_args()
@@ -61,17 +71,19 @@ def main():
     tde.backend.set_random_seed(1234)
     strategy = tde.distribute.MultiWorkerMirroredStrategy()
     n = strategy.num_replicas_in_sync
-    B = a.batch_per_gpu
+    dB, dspe, dlr, from_logits, img, metric = MODELS[a.model]
+    B = a.batch_per_gpu or dB
     GB = B * n
-    spe = a.spe
+    spe = a.spe or dspe
+    a.lr = a.lr if a.lr is not None else dlr
     while a.steps % spe:
         spe -= 1
     with strategy.scope():
-        model = tde.zoo.mnist_cnn() if a.model == "mnist_cnn" else tde.zoo.mnist_bn_cnn()
-        from_logits = a.model == "mnist_cnn"
+        model = getattr(tde.zoo, a.model)()
         model.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=from_logits),
                       optimizer=tde.optimizers.SGD(learning_rate=a.lr), metrics=["accuracy"],
                       steps_per_execution=spe)
+    ncls = model.output_shape[-1]
     prog = model._program("train", GB)
     dev = strategy.local_devices[0]
     in_shape = prog.x_shape
@@ -80,7 +92,7 @@ def main():
     pool_execs = 4
     g = torch.Generator(device="cpu").manual_seed(1000 + strategy.worker_index)
     xs = torch.rand((pool_execs, spe, B) + tuple(in_shape), generator=g).to(dev)
-    ys = torch.randint(0, 10, (pool_execs, spe, B), generator=g).to(torch.int32).to(dev)
+    ys = torch.randint(0, ncls, (pool_execs, spe, B), generator=g).to(torch.int32).to(dev)
 
     def run_exec(i):
         k = i % pool_execs
@@ -116,11 +128,11 @@ def main():
         print(f"[bench] plan={prog.plan_kind} graph={prog.use_graph} spe={spe} world={n} "
               f"loss={logs['loss']:.4f} acc={logs['accuracy']:.4f}", file=sys.stderr)
         print(json.dumps({
-            "metric": METRIC, "value": round(ips, 1), "unit": "images/sec", "n_gpus": n, "steps": a.steps,
+            "metric": metric, "value": round(ips, 1), "unit": "images/sec", "n_gpus": n, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16", "data": "synthetic (random 28x28x1 images, random labels; "
-            "random-init weights)",
-            "config": {"model": a.model, "global_batch": GB, "seq_len": None, "image_shape": [28, 28, 1],
+            "vs_baseline": None, "dtype": "bf16",
+            "data": f"synthetic (random {'x'.join(map(str, img))} images, random labels; random-init weights)",
+            "config": {"model": a.model, "global_batch": GB, "seq_len": None, "image_shape": list(img),
                        "per_gpu_batch": B, "parallelism": f"dp{n}", "strategy": "MultiWorkerMirroredStrategy",
                        "steps_per_execution": spe, "optimizer": f"SGD(lr={a.lr})", "plan": prog.plan_kind,
                        "hipgraph": prog.use_graph}}), flush=True)

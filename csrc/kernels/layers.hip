@@ -62,7 +62,7 @@ struct IGemmArgs {
   int cb_accum;
   const float* bias;
   int relu;
-  float* colstats;  // [2][N]
+  double* colstats;  // [2][N] sum / sum of squares of the STORED (bf16-rounded) values
 };
 
 constexpr int TM = 64, TN = 64, TK = 32, LDK = TK + 8;
@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
+  const int m0 = blockIdx.x * TM, n0 = blockIdx.y * TN;  // M-major: neighbours share the B tile in L2
   const int kt0 = blockIdx.z * p.ktiles_per_split;
   const int kt1 = min((p.K + TK - 1) / TK, kt0 + p.ktiles_per_split);
 
@@ -317,8 +317,10 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
         if (!cok || row >= p.M) continue;
         float v = p.alpha * acc[i][j][r] + bv;
         if (p.colstats) {
-          s1 += v;
-          s2 += v * v;
+          // statistics of exactly the tensor BN will normalise (the bf16 activation)
+          const float q = p.cb ? bf2f(f2bf(v)) : v;
+          s1 += q;
+          s2 += q * q;
         }
         if (p.relu) v = fmaxf(v, 0.f);
         if (p.cf_mode == 1) p.cf[(long long)row * p.ldc + col] = v;
@@ -336,8 +338,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
       s2 += __shfl_xor(s2, 16, 64);
       s2 += __shfl_xor(s2, 32, 64);
       if (lane < 16 && cok) {
-        atomicAdd(&p.colstats[col], s1);
-        atomicAdd(&p.colstats[p.N + col], s2);
+        atomicAdd(&p.colstats[col], (double)s1);
+        atomicAdd(&p.colstats[p.N + col], (double)s2);
       }
     }
   }
@@ -389,7 +391,7 @@ struct BnFwdArgs {
   long long R;  // rows (= elements / C)
   int C;
   int mode;  // 0 identity (ReLU/dropout/add only), 1 batch statistics, 2 moving statistics
-  const float* stats;  // [2][C] sum, sumsq (mode 1)
+  const double* stats;  // [2][C] sum, sumsq (mode 1; f64 so E[y^2]-E[y]^2 does not cancel)
   float* saved;        // [2][C] mean, rstd (mode 1, written by block 0)
   const float* gamma;
   const float* beta;
@@ -412,8 +414,9 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(BnFwdArgs a) {
     if (a.mode != 0) {
       float mean, var;
       if (a.mode == 1) {
-        mean = a.stats[c] / (float)a.R;
-        var = fmaxf(a.stats[C + c] / (float)a.R - mean * mean, 0.f);
+        const double md = a.stats[c] / (double)a.R;
+        mean = (float)md;
+        var = (float)fmax(a.stats[C + c] / (double)a.R - md * md, 0.0);
       } else {
         mean = a.mmean[c];
         var = a.mvar[c];
@@ -506,7 +509,7 @@ struct BnBwdArgs {
   int dres_accum;
   float* dgamma;
   float* dbeta;
-  float* zero_fwd;  // [2][C] forward statistics of this layer (zeroed by block 0 of the apply pass)
+  double* zero_fwd;  // [2][C] forward statistics of this layer (zeroed by block 0 of the apply pass)
 };
 
 struct BnPre {
@@ -643,8 +646,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a) {
       k1[c] = k2[c] = 0.f;
     }
     if (blockIdx.x == 0 && a.zero_fwd) {
-      a.zero_fwd[c] = 0.f;
-      a.zero_fwd[a.C + c] = 0.f;
+      a.zero_fwd[c] = 0.0;
+      a.zero_fwd[a.C + c] = 0.0;
     }
   }
   __syncthreads();
@@ -917,7 +920,7 @@ __global__ __launch_bounds__(256) void xent_kernel(XentArgs a) {
 
 // per-channel sum / sum of squares of a [R][C] bf16 tensor (BN after a non-GEMM producer)
 __global__ __launch_bounds__(256) void colstats_kernel(const bf16* __restrict__ x, long long R, int C,
-                                                       float* __restrict__ stats) {
+                                                       double* __restrict__ stats) {
   __shared__ float s1[kMaxCB], s2[kMaxCB];
   for (int c = threadIdx.x; c < C; c += blockDim.x) s1[c] = s2[c] = 0.f;
   __syncthreads();
@@ -930,8 +933,8 @@ __global__ __launch_bounds__(256) void colstats_kernel(const bf16* __restrict__ 
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    atomicAdd(&stats[c], s1[c]);
-    atomicAdd(&stats[C + c], s2[c]);
+    atomicAdd(&stats[c], (double)s1[c]);
+    atomicAdd(&stats[C + c], (double)s2[c]);
   }
 }
 
@@ -966,7 +969,7 @@ static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, long long ldb, int bkind, int M, int N,
                       int K, const int* geo, int splits, float* cf, long long ldc, int cf_mode, float alpha, bf16* cb,
-                      long long ldcb, int cb_accum, const float* bias, int relu, float* colstats, hipStream_t stream) {
+                      long long ldcb, int cb_accum, const float* bias, int relu, double* colstats, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   IGemmArgs p{};
   p.a = a;
@@ -1011,8 +1014,8 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   p.bias = bias;
   p.relu = relu;
   p.colstats = colstats;
-  dim3 grid((N + TN - 1) / TN, (M + TM - 1) / TM, splits);
-  if (grid.y > 65535) return -3;
+  dim3 grid((M + TM - 1) / TM, (N + TN - 1) / TN, splits);
+  if (grid.y > 65535 || splits > 65535) return -3;
   if (akind == A_ROWK && bkind == B_NK) igemm_kernel<A_ROWK, B_NK><<<grid, 256, 0, stream>>>(p);
   else if (akind == A_CONV && bkind == B_NK) igemm_kernel<A_CONV, B_NK><<<grid, 256, 0, stream>>>(p);
   else if (akind == A_DGRAD && bkind == B_DGRADW) igemm_kernel<A_DGRAD, B_DGRADW><<<grid, 256, 0, stream>>>(p);
@@ -1024,7 +1027,7 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
 }
 
 // drop: rate, seed, iter ptr, iter_offset, layer_id
-TDE_API int tde_bn_fwd(const bf16* y, bf16* out, const bf16* res, long long R, int C, int mode, const float* stats,
+TDE_API int tde_bn_fwd(const bf16* y, bf16* out, const bf16* res, long long R, int C, int mode, const double* stats,
                        float* saved, const float* gamma, const float* beta, float eps, float* mmean, float* mvar,
                        float momentum, float bessel, float* zero_buf, int relu, float drop_rate,
                        unsigned long long seed, const long long* iter, int iter_offset, int layer_id,
@@ -1041,7 +1044,7 @@ TDE_API int tde_bn_bwd(const bf16* dout, const bf16* y, const bf16* res, long lo
                        const float* saved, const float* gamma, const float* beta, int relu, float drop_rate,
                        unsigned long long seed, const long long* iter, int iter_offset, int layer_id, float* dstats,
                        bf16* dx, int dx_accum, bf16* dres, int dres_accum, float* dgamma, float* dbeta,
-                       float* zero_fwd, hipStream_t stream) {
+                       double* zero_fwd, hipStream_t stream) {
   if (C > kMaxCB) return -1;
   BnBwdArgs a{dout, y, res, R, C, mode, saved, gamma, beta, relu, Drop{drop_rate, seed, iter, iter_offset, layer_id},
               dstats, dx, dx_accum, dres, dres_accum, dgamma, dbeta, zero_fwd};
@@ -1107,7 +1110,7 @@ TDE_API int tde_xent(const float* logits, long long ldl, const int* labels, int 
   return 0;
 }
 
-TDE_API int tde_colstats(const bf16* x, long long R, int C, float* stats, hipStream_t stream) {
+TDE_API int tde_colstats(const bf16* x, long long R, int C, double* stats, hipStream_t stream) {
   if (C > kMaxCB) return -1;
   colstats_kernel<<<grid_for(R * C, 8), 256, 0, stream>>>(x, R, C, stats);
   TDE_LAUNCH_CHECK();

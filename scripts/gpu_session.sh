@@ -2,6 +2,7 @@
 # One GPU-box session: tests, smoke, bench, rocprof.  Stops at the first step
 # that ends in a fault/abort/timeout (exit codes other than 0/1).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export PYTHONPATH="$PWD${PYTHONPATH:+:$PYTHONPATH}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 OUT=gpurun_out
@@ -23,6 +24,16 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench 600 python bench.py --steps 2000 --warmup 200
   step bench_nograph 600 python bench.py --steps 400 --warmup 64 --no-graph
+fi
+if [ "$MODE" = all ] || [ "$MODE" = models ]; then
+  step bench_bn_cnn 600 python bench.py --model mnist_bn_cnn --steps 800 --warmup 64
+  step bench_resnet18 600 python bench.py --model resnet18 --steps 30 --warmup 5
+fi
+if [ "$MODE" = all ] || [ "$MODE" = baseline ]; then
+  step torch_cnn 600 python bench/torch_baseline.py --model mnist_cnn --steps 400 --warmup 64
+  step torch_cnn_graph 600 python bench/torch_baseline.py --model mnist_cnn --steps 2000 --warmup 64 --graph
+  step torch_bn_cnn_graph 600 python bench/torch_baseline.py --model mnist_bn_cnn --steps 800 --warmup 64 --graph
+  step torch_resnet18 600 python bench/torch_baseline.py --model resnet18 --steps 30 --warmup 5 --channels-last
 fi
 if [ "$MODE" = all ] || [ "$MODE" = micro ]; then
   step micro 300 python bench/micro.py

