@@ -74,12 +74,62 @@ __device__ __forceinline__ bf16x8 zero8() {
   return r;
 }
 
-// ---- A(m, k) for the K-vector kinds: the thread's row m is fixed for the whole K loop.
+// ---- LDS images.
+// K-contiguous operands: [rows][LDK] (32 k + 8 pad; 16-byte fragment rows are conflict-free).
+// Row-contiguous operands (weight grads: channels are contiguous, the reduction runs over pixels):
+// [k = 32][128] image with 256-byte rows and an XOR chunk swizzle, read back transposed with
+// ds_read_b64_tr_b16 (CDNA4 hardware transpose): conflict-free for the 16x16x32 operand.
+__device__ __forceinline__ int swz(int row, int ch) {
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+// 16x16x32 operand fragment (rows mb..mb+15 of the image's 128 columns, k 0..31) via two
+// transposed 4x16 reads per 16-lane group.
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* img, int mb, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+  const int ch = (mb >> 3) + (pp >> 1);
+  const char* base = reinterpret_cast<const char*>(img);
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + swz(8 * g + q, ch) + 8 * (pp & 1)));
+  const v4i16 hi =
+      __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + swz(8 * g + 4 + q, ch) + 8 * (pp & 1)));
+  // concatenate as 16-bit integers, then reinterpret the whole vector (element-wise bf16 casts of
+  // the intrinsic's result mis-assemble the fragment)
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+// ---- A(m, k), K-vector kinds: a thread's rows are fixed for the whole K loop; its k offset
+// advances by 32 per step, decomposed incrementally into (kh, kw, c) (no divisions in the loop).
 struct ARow {
   bool ok;
-  long long base;  // ROWK: m*lda
-  int b, y0, x0;   // CONV: b, oh*sh-pt, ow*sw-pl ; DGRAD: b, ih+pt, iw+pl
+  long long base;  // ROWK: m*lda ; CONV/DGRAD: pixel index of (b, y0, x0) in the gathered tensor
+  int y0, x0;      // CONV: oh*sh-pt, ow*sw-pl ; DGRAD: ih+pt, iw+pl
 };
+
+struct KPos {  // decomposition of k = (kh*KW + kw)*Cd + c
+  int kh, kw, c;
+};
+
+__device__ __forceinline__ void kpos_advance(KPos& s, int d, int Cd, int KW) {
+  s.c += d;
+  while (s.c >= Cd) {
+    s.c -= Cd;
+    if (++s.kw == KW) {
+      s.kw = 0;
+      ++s.kh;
+    }
+  }
+}
+
+__device__ __forceinline__ KPos kpos_of(int k, int Cd, int KW) {
+  const int kc = k / Cd;
+  const int kh = kc / KW;
+  return KPos{kh, kc - kh * KW, k - kc * Cd};
+}
 
 template <int AK>
 __device__ __forceinline__ ARow a_row(const IGemmArgs& p, int m) {
@@ -87,116 +137,129 @@ __device__ __forceinline__ ARow a_row(const IGemmArgs& p, int m) {
   r.ok = m < p.M;
   const int mm = r.ok ? m : 0;
   r.base = 0;
-  r.b = r.y0 = r.x0 = 0;
+  r.y0 = r.x0 = 0;
   if (AK == A_ROWK) {
     r.base = (long long)mm * p.lda;
   } else if (AK == A_CONV) {
     const int hw = p.g.Ho * p.g.Wo;
     const int b = mm / hw, rem = mm - b * hw;
     const int oh = rem / p.g.Wo, ow = rem - oh * p.g.Wo;
-    r.b = b;
     r.y0 = oh * p.g.sh - p.g.pt;
     r.x0 = ow * p.g.sw - p.g.pl;
-  } else {  // A_DGRAD: m over input pixels
+    r.base = (long long)b * p.g.H * p.g.W;
+  } else {  // A_DGRAD: m over input pixels, gathers dY
     const int hw = p.g.H * p.g.W;
     const int b = mm / hw, rem = mm - b * hw;
     const int ih = rem / p.g.W, iw = rem - ih * p.g.W;
-    r.b = b;
     r.y0 = ih + p.g.pt;
     r.x0 = iw + p.g.pl;
+    r.base = (long long)b * p.g.Ho * p.g.Wo;
   }
   return r;
 }
 
-// element index of A(m,k) (or -1 = zero) for the K-vector kinds
+// element index of A(m, k) at decomposition s (or -1 = zero); k < K checked by the caller
 template <int AK>
-__device__ __forceinline__ long long a_idx(const IGemmArgs& p, const ARow& r, int k) {
-  if (!r.ok || k >= p.K) return -1;
+__device__ __forceinline__ long long a_idx(const IGemmArgs& p, const ARow& r, const KPos& s, int k) {
   if (AK == A_ROWK) return r.base + k;
   if (AK == A_CONV) {
-    const int C = p.g.C;
-    const int kc = k / C, ci = k - kc * C;
-    const int kh = kc / p.g.KW, kw = kc - kh * p.g.KW;
-    const int ih = r.y0 + kh, iw = r.x0 + kw;
+    const int ih = r.y0 + s.kh, iw = r.x0 + s.kw;
     if ((unsigned)ih >= (unsigned)p.g.H || (unsigned)iw >= (unsigned)p.g.W) return -1;
-    return (((long long)r.b * p.g.H + ih) * p.g.W + iw) * C + ci;
+    return (r.base + (long long)ih * p.g.W + iw) * p.g.C + s.c;
   }
-  // A_DGRAD: k = (kh, kw, co) ; oh = (ih + pt - kh) / sh must be exact and in range
-  const int Co = p.g.Co;
-  const int kc = k / Co, co = k - kc * Co;
-  const int kh = kc / p.g.KW, kw = kc - kh * p.g.KW;
-  const int ty = r.y0 - kh, tx = r.x0 - kw;
-  if (ty < 0 || tx < 0) return -1;
-  const int oh = ty / p.g.sh, ow = tx / p.g.sw;
-  if (oh * p.g.sh != ty || ow * p.g.sw != tx || oh >= p.g.Ho || ow >= p.g.Wo) return -1;
-  return (((long long)r.b * p.g.Ho + oh) * p.g.Wo + ow) * Co + co;
+  // A_DGRAD: oh = (ih + pt - kh) / sh must be exact and in range
+  int oh = r.y0 - s.kh, ow = r.x0 - s.kw;
+  if (oh < 0 || ow < 0) return -1;
+  if (p.g.sh != 1) {
+    const int q = oh / p.g.sh;
+    if (q * p.g.sh != oh) return -1;
+    oh = q;
+  }
+  if (p.g.sw != 1) {
+    const int q = ow / p.g.sw;
+    if (q * p.g.sw != ow) return -1;
+    ow = q;
+  }
+  if (oh >= p.g.Ho || ow >= p.g.Wo) return -1;
+  return (r.base + (long long)oh * p.g.Wo + ow) * p.g.Co + s.c;
 }
 
 template <int AK>
-__device__ __forceinline__ bf16x8 load_a_k8(const IGemmArgs& p, const ARow& r, int k) {
-  if (p.avec) {
-    const long long i = a_idx<AK>(p, r, k);  // 8 consecutive k share (kh,kw) when C%8==0
+__device__ __forceinline__ bf16x8 load_a_k8(const IGemmArgs& p, const ARow& r, const KPos& s, int k, int Cd) {
+  if (!r.ok) return zero8();
+  if (p.avec) {  // 8 consecutive k share (kh, kw): one 16-byte load
+    if (k >= p.K) return zero8();
+    const long long i = a_idx<AK>(p, r, s, k);
     if (i < 0) return zero8();
     return *reinterpret_cast<const bf16x8*>(p.a + i);
   }
   bf16x8 v;
+  KPos t = s;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const long long i = a_idx<AK>(p, r, k + j);
+    const long long i = (k + j < p.K) ? a_idx<AK>(p, r, t, k + j) : -1;
     v[j] = i < 0 ? (bf16)0.0f : p.a[i];
+    if (AK != A_ROWK) kpos_advance(t, 1, Cd, p.g.KW);
   }
   return v;
 }
 
-// ---- B(k, n) for the K-vector kinds (row = n)
-__device__ __forceinline__ long long b_idx_k(const IGemmArgs& p, int BK_, int n, int k) {
-  if (n >= p.N || k >= p.K) return -1;
+// ---- B(k, n), K-vector kinds (image row = n)
+template <int BK_>
+__device__ __forceinline__ long long b_idx_k(const IGemmArgs& p, int n, const KPos& s, int k) {
   if (BK_ == B_NK) return (long long)n * p.ldb + k;
   // B_DGRADW: k = (kh,kw,co), n = ci  ->  W[kh][kw][ci][co]
-  const int Co = p.g.Co;
-  const int kc = k / Co, co = k - kc * Co;
-  return ((long long)kc * p.g.C + n) * Co + co;
+  return ((long long)(s.kh * p.g.KW + s.kw) * p.g.C + n) * p.g.Co + s.c;
 }
 
 template <int BK_>
-__device__ __forceinline__ bf16x8 load_b_k8(const IGemmArgs& p, int n, int k) {
+__device__ __forceinline__ bf16x8 load_b_k8(const IGemmArgs& p, int n, const KPos& s, int k) {
+  if (n >= p.N) return zero8();
   if (p.bvec) {
-    const long long i = b_idx_k(p, BK_, n, k);
-    if (i < 0) return zero8();
-    return *reinterpret_cast<const bf16x8*>(p.b + i);
+    if (k >= p.K) return zero8();
+    return *reinterpret_cast<const bf16x8*>(p.b + b_idx_k<BK_>(p, n, s, k));
   }
   bf16x8 v;
+  KPos t = s;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const long long i = b_idx_k(p, BK_, n, k + j);
-    v[j] = i < 0 ? (bf16)0.0f : p.b[i];
+    v[j] = (k + j < p.K) ? p.b[b_idx_k<BK_>(p, n, t, k + j)] : (bf16)0.0f;
+    if (BK_ == B_DGRADW) kpos_advance(t, 1, p.g.Co, p.g.KW);
   }
   return v;
 }
 
-// ---- M-vector kinds: 8 consecutive rows m0..m0+7 at one k
-struct ACol {
-  int kh, kw, ci;  // WGRAD: decomposition of the first row
+// ---- row-vector kinds: 8 consecutive rows m..m+7 at one k
+struct WRow {  // A_WGRAD: the decomposition of the slot's first row m = (kh, kw, ci)
+  int kh, kw, ci;
+  bool ok;
 };
 
-__device__ __forceinline__ long long wgrad_idx(const IGemmArgs& p, int m, int k) {
-  // A_WGRAD: m = (kh,kw,ci), k = pixel p = (b,oh,ow)
-  if (m >= p.M || k >= p.K) return -1;
-  const int C = p.g.C;
-  const int kc = m / C, ci = m - kc * C;
-  const int kh = kc / p.g.KW, kw = kc - kh * p.g.KW;
-  const int hw = p.g.Ho * p.g.Wo;
-  const int b = k / hw, rem = k - b * hw;
-  const int oh = rem / p.g.Wo, ow = rem - oh * p.g.Wo;
-  const int ih = oh * p.g.sh - p.g.pt + kh, iw = ow * p.g.sw - p.g.pl + kw;
+struct PixPos {  // pixel k = (b, oh, ow), advanced incrementally
+  int b, oh, ow;
+};
+
+__device__ __forceinline__ void pix_advance(PixPos& q, int d, int Ho, int Wo) {
+  q.ow += d;
+  while (q.ow >= Wo) {
+    q.ow -= Wo;
+    if (++q.oh == Ho) {
+      q.oh = 0;
+      ++q.b;
+    }
+  }
+}
+
+__device__ __forceinline__ long long wgrad_idx(const IGemmArgs& p, int kh, int kw, int ci, const PixPos& q) {
+  const int ih = q.oh * p.g.sh - p.g.pt + kh, iw = q.ow * p.g.sw - p.g.pl + kw;
   if ((unsigned)ih >= (unsigned)p.g.H || (unsigned)iw >= (unsigned)p.g.W) return -1;
-  return (((long long)b * p.g.H + ih) * p.g.W + iw) * C + ci;
+  return (((long long)q.b * p.g.H + ih) * p.g.W + iw) * p.g.C + ci;
 }
 
 template <int AK>
-__device__ __forceinline__ bf16x8 load_a_m8(const IGemmArgs& p, int m, int k) {
+__device__ __forceinline__ bf16x8 load_a_m8(const IGemmArgs& p, int m, const WRow& w, const PixPos& q, int k) {
+  if (k >= p.K || m >= p.M) return zero8();
   if (AK == A_COLM) {
-    if (k >= p.K || m >= p.M) return zero8();
     const long long i = (long long)k * p.lda + m;
     if (p.avec) return *reinterpret_cast<const bf16x8*>(p.a + i);
     bf16x8 v;
@@ -204,16 +267,25 @@ __device__ __forceinline__ bf16x8 load_a_m8(const IGemmArgs& p, int m, int k) {
     for (int j = 0; j < 8; ++j) v[j] = (m + j < p.M) ? p.a[i + j] : (bf16)0.0f;
     return v;
   }
-  if (p.avec) {
-    const long long i = wgrad_idx(p, m, k);
+  if (p.avec) {  // C % 8 == 0: the 8 rows are ci..ci+7 of one (kh, kw)
+    const long long i = wgrad_idx(p, w.kh, w.kw, w.ci, q);
     if (i < 0) return zero8();
     return *reinterpret_cast<const bf16x8*>(p.a + i);
   }
   bf16x8 v;
+  int kh = w.kh, kw = w.kw, ci = w.ci;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const long long i = wgrad_idx(p, m + j, k);
+    long long i = -1;
+    if (m + j < p.M) i = wgrad_idx(p, kh, kw, ci, q);
     v[j] = i < 0 ? (bf16)0.0f : p.a[i];
+    if (++ci == p.g.C) {
+      ci = 0;
+      if (++kw == p.g.KW) {
+        kw = 0;
+        ++kh;
+      }
+    }
   }
   return v;
 }
@@ -229,53 +301,114 @@ __device__ __forceinline__ bf16x8 load_b_n8(const IGemmArgs& p, int n, int k) {
   return v;
 }
 
-template <int AK, int BK_>
+template <int AK, int BK_, int BM, int BN>
 __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
-  __shared__ __attribute__((aligned(16))) bf16 As[2][TM][LDK];
-  __shared__ __attribute__((aligned(16))) bf16 Bs[2][TN][LDK];
   constexpr bool AKV = (AK == A_ROWK || AK == A_CONV || AK == A_DGRAD);  // K-vector A
   constexpr bool BKV = (BK_ == B_NK || BK_ == B_DGRADW);                 // K-vector B
+  static_assert(AKV || BM == 128, "row-contiguous A needs the 128-wide transposed image");
+  static_assert(BKV || BN == 128, "row-contiguous B needs the 128-wide transposed image");
+  constexpr int AIMG = AKV ? BM * LDK : TK * 128;  // elements per buffer
+  constexpr int BIMG = BKV ? BN * LDK : TK * 128;
+  constexpr int AS = AKV ? BM / 64 : 2;  // 16-byte slots per thread
+  constexpr int BS = BKV ? BN / 64 : 2;
+  constexpr int WTM = BM / 2, WTN = BN / 2, MI = WTM / 16, NI = WTN / 16;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (AIMG + BIMG)];
+  bf16* const As = smem;
+  bf16* const Bs = smem + 2 * AIMG;
+
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.x * TM, n0 = blockIdx.y * TN;  // M-major: neighbours share the B tile in L2
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;  // M-major: neighbours share the B tile in L2
   const int kt0 = blockIdx.z * p.ktiles_per_split;
   const int kt1 = min((p.K + TK - 1) / TK, kt0 + p.ktiles_per_split);
+  if (kt0 >= kt1 && p.cf_mode == 2) return;  // empty split contributes nothing
 
-  // loader coordinates
-  const int lr = tid >> 2, lk = (tid & 3) * 8;  // K-vector: row, k offset
-  const int vk = tid >> 3, vr = (tid & 7) * 8;  // M-vector: k, row offset
-  ARow ar;
-  if (AKV) ar = a_row<AK>(p, m0 + lr);
+  // ---- loader state
+  const int lk = (tid & 3) * 8;   // K-vector: k offset of every slot of this thread
+  const int vk = tid >> 4;        // row-vector slot s = tid + 256*i: k row = s >> 4, chunk = s & 15
+  const int vch = tid & 15;
+  ARow ar[AS];
+  WRow wr[AS];
+  KPos ka{0, 0, 0}, kb{0, 0, 0};
+  PixPos pa{0, 0, 0};
+  const int KW = p.g.KW;
+  const int Cda = (AK == A_CONV) ? p.g.C : p.g.Co;
+  if (AKV) {
+#pragma unroll
+    for (int i = 0; i < AS; ++i) ar[i] = a_row<AK>(p, m0 + ((tid + 256 * i) >> 2));
+    if (AK != A_ROWK) ka = kpos_of(kt0 * TK + lk, Cda, KW);
+  } else {
+#pragma unroll
+    for (int i = 0; i < AS; ++i) {
+      const int m = m0 + vch * 8;  // both slots share the chunk (rows vk and vk+16)
+      if (AK == A_WGRAD) {
+        const int mm = m < p.M ? m : 0;
+        const KPos t = kpos_of(mm, p.g.C, KW);
+        wr[i] = WRow{t.kh, t.kw, t.c, m < p.M};
+      }
+    }
+    if (AK == A_WGRAD) {
+      const int k = kt0 * TK + vk;
+      const int hw = p.g.Ho * p.g.Wo;
+      const int b = k / hw, rem = k - b * hw;
+      pa = PixPos{b, rem / p.g.Wo, rem - (rem / p.g.Wo) * p.g.Wo};
+    }
+  }
+  if (BK_ == B_DGRADW) kb = kpos_of(kt0 * TK + lk, p.g.Co, KW);
 
-  bf16x8 ra, rb;
+  bf16x8 ra[AS], rb[BS];
   auto gload = [&](int kt) {
     const int k0 = kt * TK;
-    if (AKV) ra = load_a_k8<AK>(p, ar, k0 + lk);
-    else ra = load_a_m8<AK>(p, m0 + vr, k0 + vk);
-    if (BKV) rb = load_b_k8<BK_>(p, n0 + lr, k0 + lk);
-    else rb = load_b_n8(p, n0 + vr, k0 + vk);
-  };
-  auto sstore = [&](int buf) {
     if (AKV) {
-      *reinterpret_cast<bf16x8*>(&As[buf][lr][lk]) = ra;
+#pragma unroll
+      for (int i = 0; i < AS; ++i) ra[i] = load_a_k8<AK>(p, ar[i], ka, k0 + lk, Cda);
     } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) As[buf][vr + j][vk] = ra[j];
+      for (int i = 0; i < AS; ++i) {
+        PixPos q = pa;
+        if (AK == A_WGRAD && i) pix_advance(q, 16, p.g.Ho, p.g.Wo);
+        ra[i] = load_a_m8<AK>(p, m0 + vch * 8, wr[i], q, k0 + vk + 16 * i);
+      }
     }
     if (BKV) {
-      *reinterpret_cast<bf16x8*>(&Bs[buf][lr][lk]) = rb;
+#pragma unroll
+      for (int i = 0; i < BS; ++i) rb[i] = load_b_k8<BK_>(p, n0 + ((tid + 256 * i) >> 2), kb, k0 + lk);
     } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) Bs[buf][vr + j][vk] = rb[j];
+      for (int i = 0; i < BS; ++i) rb[i] = load_b_n8(p, n0 + vch * 8, k0 + vk + 16 * i);
+    }
+    // advance the incremental decompositions to the next k-tile
+    if (AKV && AK != A_ROWK) kpos_advance(ka, TK, Cda, KW);
+    if (AK == A_WGRAD) pix_advance(pa, TK, p.g.Ho, p.g.Wo);
+    if (BK_ == B_DGRADW) kpos_advance(kb, TK, p.g.Co, KW);
+  };
+  auto sstore = [&](int buf) {
+    bf16* a = As + buf * AIMG;
+    bf16* b = Bs + buf * BIMG;
+    if (AKV) {
+#pragma unroll
+      for (int i = 0; i < AS; ++i) *reinterpret_cast<bf16x8*>(a + ((tid + 256 * i) >> 2) * LDK + lk) = ra[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < AS; ++i)
+        *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(a) + swz(vk + 16 * i, vch)) = ra[i];
+    }
+    if (BKV) {
+#pragma unroll
+      for (int i = 0; i < BS; ++i) *reinterpret_cast<bf16x8*>(b + ((tid + 256 * i) >> 2) * LDK + lk) = rb[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < BS; ++i)
+        *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(b) + swz(vk + 16 * i, vch)) = rb[i];
     }
   };
 
-  f32x4 acc[2][2];
+  f32x4 acc[MI][NI];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fk = (lane >> 4) * 8;
   if (kt0 < kt1) {
@@ -286,14 +419,25 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
     for (int kt = kt0; kt < kt1; ++kt) {
       const bool more = kt + 1 < kt1;
       if (more) gload(kt + 1);
-      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&As[buf][wm * 32 + fr][fk]);
-      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&As[buf][wm * 32 + 16 + fr][fk]);
-      const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(&Bs[buf][wn * 32 + fr][fk]);
-      const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(&Bs[buf][wn * 32 + 16 + fr][fk]);
-      acc[0][0] = mfma16(a0, b0, acc[0][0]);
-      acc[0][1] = mfma16(a0, b1, acc[0][1]);
-      acc[1][0] = mfma16(a1, b0, acc[1][0]);
-      acc[1][1] = mfma16(a1, b1, acc[1][1]);
+      const bf16* a = As + buf * AIMG;
+      const bf16* b = Bs + buf * BIMG;
+      bf16x8 af[MI], bfr[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int r = wm * WTM + i * 16;
+        if (AKV) af[i] = *reinterpret_cast<const bf16x8*>(a + (r + fr) * LDK + fk);
+        else af[i] = tr_frag(a, r, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int c = wn * WTN + j * 16;
+        if (BKV) bfr[j] = *reinterpret_cast<const bf16x8*>(b + (c + fr) * LDK + fk);
+        else bfr[j] = tr_frag(b, c, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
       if (more) {
         sstore(buf ^ 1);
         __syncthreads();
@@ -304,16 +448,16 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
 
   // ---- epilogue
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int col = n0 + wn * 32 + j * 16 + fr;
+  for (int j = 0; j < NI; ++j) {
+    const int col = n0 + wn * WTN + j * 16 + fr;
     const bool cok = col < p.N;
     const float bv = (p.bias && cok) ? p.bias[col] : 0.f;
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < MI; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 32 + i * 16 + (lane >> 4) * 4 + r;
+        const int row = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
         if (!cok || row >= p.M) continue;
         float v = p.alpha * acc[i][j][r] + bv;
         if (p.colstats) {
@@ -466,7 +610,7 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(BnFwdArgs a) {
       }
     }
     if (a.drop.rate > 0.f) drop8(a.drop, e0, ks);
-    int c = (int)(e0 % C);
+    int c = (int)((unsigned)e0 % (unsigned)C);
     bf16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -544,7 +688,7 @@ __device__ __forceinline__ void bn_dz8(const BnBwdArgs& a, const float* sc, cons
     }
   }
   if (a.drop.rate > 0.f) drop8(a.drop, e0, ks);
-  int c = (int)(e0 % a.C);
+  int c = (int)((unsigned)e0 % (unsigned)a.C);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const float z = v[j] * sc[c] + sf[c] + r[j];
@@ -604,7 +748,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdArgs a) {
         r2[j] += dz[j] * xh[j];
       }
     } else {
-      int c = (int)(e0 % a.C);
+      int c = (int)((unsigned)e0 % (unsigned)a.C);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         atomicAdd(&s1[c], dz[j]);
@@ -614,7 +758,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdArgs a) {
     }
   }
   if (fixed && first < n) {
-    int c = (int)(first % a.C);
+    int c = (int)((unsigned)first % (unsigned)a.C);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       atomicAdd(&s1[c], r1[j]);
@@ -659,7 +803,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a) {
     const long long e0 = q * 8;
     float dz[8], xh[8];
     bn_dz8(a, sc, sf, mu, rs, e0, n, vec, dz, xh);
-    int c = (int)(e0 % a.C);
+    int c = (int)((unsigned)e0 % (unsigned)a.C);
     float dx[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -710,7 +854,7 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(const bf16* __restrict__ d
     float g = bf2f(dout[e]);
     if (relu && !(bf2f(out[e]) > 0.f)) g = 0.f;
     if (dz) dz[e] = f2bf(g);
-    if (dbias) atomicAdd(&s1[(int)(e % C)], g);
+    if (dbias) atomicAdd(&s1[(int)((unsigned)e % (unsigned)C)], g);
   }
   if (!dbias) return;
   __syncthreads();
@@ -733,12 +877,13 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(PoolArgs a) {
   const Geo& g = a.g;
   const long long n = (long long)g.B * g.Ho * g.Wo * g.C;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(e % g.C);
-    long long t = e / g.C;
-    const int ow = (int)(t % g.Wo);
-    t /= g.Wo;
-    const int oh = (int)(t % g.Ho);
-    const int b = (int)(t / g.Ho);
+    const unsigned ue = (unsigned)e;
+    const int c = (int)(ue % (unsigned)g.C);
+    unsigned t = ue / (unsigned)g.C;
+    const int ow = (int)(t % (unsigned)g.Wo);
+    t /= (unsigned)g.Wo;
+    const int oh = (int)(t % (unsigned)g.Ho);
+    const int b = (int)(t / (unsigned)g.Ho);
     float best = -INFINITY;
     int bi = 0;
     for (int i = 0; i < g.KH; ++i) {
@@ -763,12 +908,13 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(PoolArgs a) {
   const Geo& g = a.g;
   const long long n = (long long)g.B * g.H * g.W * g.C;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(e % g.C);
-    long long t = e / g.C;
-    const int iw = (int)(t % g.W);
-    t /= g.W;
-    const int ih = (int)(t % g.H);
-    const int b = (int)(t / g.H);
+    const unsigned ue = (unsigned)e;
+    const int c = (int)(ue % (unsigned)g.C);
+    unsigned t = ue / (unsigned)g.C;
+    const int iw = (int)(t % (unsigned)g.W);
+    t /= (unsigned)g.W;
+    const int ih = (int)(t % (unsigned)g.H);
+    const int b = (int)(t / (unsigned)g.H);
     float s = 0.f;
     const int ty = ih + g.pt, tx = iw + g.pl;
     const int oh_lo = ty >= g.KH ? (ty - g.KH) / g.sh + 1 : 0, oh_hi = min(g.Ho - 1, ty / g.sh);
@@ -795,8 +941,8 @@ __global__ __launch_bounds__(256) void gap_fwd_kernel(const bf16* __restrict__ x
   const long long n = (long long)B * C;
   const float inv = 1.f / (float)HW;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(e % C);
-    const long long b = e / C;
+    const int c = (int)((unsigned)e % (unsigned)C);
+    const long long b = (unsigned)e / (unsigned)C;
     const bf16* p = x + b * HW * C + c;
     float s = 0.f;
     for (int i = 0; i < HW; ++i) s += bf2f(p[(long long)i * C]);
@@ -809,8 +955,8 @@ __global__ __launch_bounds__(256) void gap_bwd_kernel(const bf16* __restrict__ d
   const long long n = (long long)B * HW * C;
   const float inv = 1.f / (float)HW;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(e % C);
-    const long long b = e / ((long long)HW * C);
+    const int c = (int)((unsigned)e % (unsigned)C);
+    const long long b = (unsigned)e / ((unsigned)HW * (unsigned)C);
     float v = bf2f(dy[b * C + c]) * inv;
     if (accum) v += bf2f(dx[e]);
     dx[e] = f2bf(v);
@@ -823,12 +969,13 @@ __global__ __launch_bounds__(256) void pad_kernel(const bf16* __restrict__ src, 
   // g: H,W input dims; Ho,Wo padded dims; pt,pl offsets
   const long long n = (long long)g.B * g.Ho * g.Wo * g.C;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(e % g.C);
-    long long t = e / g.C;
-    const int ow = (int)(t % g.Wo);
-    t /= g.Wo;
-    const int oh = (int)(t % g.Ho);
-    const int b = (int)(t / g.Ho);
+    const unsigned ue = (unsigned)e;
+    const int c = (int)(ue % (unsigned)g.C);
+    unsigned t = ue / (unsigned)g.C;
+    const int ow = (int)(t % (unsigned)g.Wo);
+    t /= (unsigned)g.Wo;
+    const int oh = (int)(t % (unsigned)g.Ho);
+    const int b = (int)(t / (unsigned)g.Ho);
     const int ih = oh - g.pt, iw = ow - g.pl;
     const bool in = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
     const long long ie = (((long long)b * g.H + ih) * g.W + iw) * g.C + c;
@@ -927,7 +1074,7 @@ __global__ __launch_bounds__(256) void colstats_kernel(const bf16* __restrict__ 
   const long long n = R * C;
   for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
     const float v = bf2f(x[e]);
-    const int c = (int)(e % C);
+    const int c = (int)((unsigned)e % (unsigned)C);
     atomicAdd(&s1[c], v);
     atomicAdd(&s2[c], v * v);
   }
@@ -1014,14 +1161,41 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   p.bias = bias;
   p.relu = relu;
   p.colstats = colstats;
-  dim3 grid((M + TM - 1) / TM, (N + TN - 1) / TN, splits);
+  // tile: weight-grad kinds (row-contiguous operands) use the 128x128 transposed images; the others
+  // take the largest tile that still gives >= 2 workgroups per CU
+  int bm = 64, bn = 64;
+  const bool rowk = (akind == A_COLM || akind == A_WGRAD);
+  auto tiles = [&](int tm, int tn) { return (long long)((M + tm - 1) / tm) * ((N + tn - 1) / tn) * splits; };
+  if (rowk) {
+    bm = bn = 128;
+  } else if (N > 64 && tiles(128, 128) >= 512) {
+    bm = bn = 128;
+  } else if (tiles(128, 64) >= 512) {
+    bm = 128;
+  }
+  dim3 grid((M + bm - 1) / bm, (N + bn - 1) / bn, splits);
   if (grid.y > 65535 || splits > 65535) return -3;
-  if (akind == A_ROWK && bkind == B_NK) igemm_kernel<A_ROWK, B_NK><<<grid, 256, 0, stream>>>(p);
-  else if (akind == A_CONV && bkind == B_NK) igemm_kernel<A_CONV, B_NK><<<grid, 256, 0, stream>>>(p);
-  else if (akind == A_DGRAD && bkind == B_DGRADW) igemm_kernel<A_DGRAD, B_DGRADW><<<grid, 256, 0, stream>>>(p);
-  else if (akind == A_COLM && bkind == B_KN) igemm_kernel<A_COLM, B_KN><<<grid, 256, 0, stream>>>(p);
-  else if (akind == A_WGRAD && bkind == B_KN) igemm_kernel<A_WGRAD, B_KN><<<grid, 256, 0, stream>>>(p);
-  else return -1;
+#define TDE_IGEMM(AK_, BK__, BM_, BN_) igemm_kernel<AK_, BK__, BM_, BN_><<<grid, 256, 0, stream>>>(p)
+  if (akind == A_ROWK && bkind == B_NK) {
+    if (bm == 128 && bn == 128) TDE_IGEMM(A_ROWK, B_NK, 128, 128);
+    else if (bm == 128) TDE_IGEMM(A_ROWK, B_NK, 128, 64);
+    else TDE_IGEMM(A_ROWK, B_NK, 64, 64);
+  } else if (akind == A_CONV && bkind == B_NK) {
+    if (bm == 128 && bn == 128) TDE_IGEMM(A_CONV, B_NK, 128, 128);
+    else if (bm == 128) TDE_IGEMM(A_CONV, B_NK, 128, 64);
+    else TDE_IGEMM(A_CONV, B_NK, 64, 64);
+  } else if (akind == A_DGRAD && bkind == B_DGRADW) {
+    if (bm == 128 && bn == 128) TDE_IGEMM(A_DGRAD, B_DGRADW, 128, 128);
+    else if (bm == 128) TDE_IGEMM(A_DGRAD, B_DGRADW, 128, 64);
+    else TDE_IGEMM(A_DGRAD, B_DGRADW, 64, 64);
+  } else if (akind == A_COLM && bkind == B_KN) {
+    TDE_IGEMM(A_COLM, B_KN, 128, 128);
+  } else if (akind == A_WGRAD && bkind == B_KN) {
+    TDE_IGEMM(A_WGRAD, B_KN, 128, 128);
+  } else {
+    return -1;
+  }
+#undef TDE_IGEMM
   TDE_LAUNCH_CHECK();
   return 0;
 }
@@ -1033,6 +1207,7 @@ TDE_API int tde_bn_fwd(const bf16* y, bf16* out, const bf16* res, long long R, i
                        unsigned long long seed, const long long* iter, int iter_offset, int layer_id,
                        hipStream_t stream) {
   if (C > kMaxC) return -1;
+  if (R * C >= (1LL << 31)) return -4;
   BnFwdArgs a{y, out, res, R, C, mode, stats, saved, gamma, beta, eps, mmean, mvar, momentum, bessel, zero_buf, relu,
               Drop{drop_rate, seed, iter, iter_offset, layer_id}};
   bn_fwd_kernel<<<grid_for(R * C, 8), 256, 0, stream>>>(a);
@@ -1048,9 +1223,13 @@ TDE_API int tde_bn_bwd(const bf16* dout, const bf16* y, const bf16* res, long lo
   if (C > kMaxCB) return -1;
   BnBwdArgs a{dout, y, res, R, C, mode, saved, gamma, beta, relu, Drop{drop_rate, seed, iter, iter_offset, layer_id},
               dstats, dx, dx_accum, dres, dres_accum, dgamma, dbeta, zero_fwd};
-  int g = grid_for(R * C, 8);
+  if (R * C >= (1LL << 31)) return -4;
+  const int g = grid_for(R * C, 8);
   if (mode == 1) {
-    // round the grid to a multiple of C / gcd(2048, C) so the grid stride is a multiple of C
+    // Reduction grid: <= 2 blocks per CU (each block ends with 2*C global atomics, so more blocks only
+    // add contention), rounded to a multiple of C / gcd(2048, C) so the grid stride is a multiple of C
+    // and every thread accumulates fixed channels in registers.
+    int gr = g < 512 ? g : 512;
     int gc = C, t = 2048;
     while (t) {
       const int r = gc % t;
@@ -1058,8 +1237,8 @@ TDE_API int tde_bn_bwd(const bf16* dout, const bf16* y, const bf16* res, long lo
       t = r;
     }
     const int mult = C / gc;
-    g = ((g + mult - 1) / mult) * mult;
-    bn_bwd_reduce_kernel<<<g, 256, 0, stream>>>(a);
+    gr = ((gr + mult - 1) / mult) * mult;
+    bn_bwd_reduce_kernel<<<gr, 256, 0, stream>>>(a);
     TDE_LAUNCH_CHECK();
   }
   bn_bwd_apply_kernel<<<g, 256, 0, stream>>>(a);
@@ -1069,6 +1248,7 @@ TDE_API int tde_bn_bwd(const bf16* dout, const bf16* y, const bf16* res, long lo
 
 TDE_API int tde_act_bwd(const bf16* dout, const bf16* out, long long R, int C, int relu, bf16* dz, float* dbias,
                         hipStream_t stream) {
+  if (R * C >= (1LL << 31)) return -4;
   if (C > kMaxCB) return -1;
   act_bwd_kernel<<<grid_for(R * C, 8), 256, 0, stream>>>(dout, out, R, C, relu, dz, dbias);
   TDE_LAUNCH_CHECK();
@@ -1079,6 +1259,7 @@ TDE_API int tde_maxpool(const bf16* x, bf16* y, unsigned char* idx, const bf16* 
                         const int* geo, int backward, hipStream_t stream) {
   Geo g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9], geo[10], geo[11], geo[12]};
   if (g.KH * g.KW > 256) return -1;
+  if ((long long)g.B * g.H * g.W * g.C >= (1LL << 31) || (long long)g.B * g.Ho * g.Wo * g.C >= (1LL << 31)) return -4;
   PoolArgs a{x, y, idx, dy, dx, dx_accum, g};
   if (!backward) maxpool_fwd_kernel<<<grid_for((long long)g.B * g.Ho * g.Wo * g.C), 256, 0, stream>>>(a);
   else maxpool_bwd_kernel<<<grid_for((long long)g.B * g.H * g.W * g.C), 256, 0, stream>>>(a);
@@ -1087,6 +1268,7 @@ TDE_API int tde_maxpool(const bf16* x, bf16* y, unsigned char* idx, const bf16* 
 }
 
 TDE_API int tde_gap(const bf16* x, bf16* y, int B, int HW, int C, int backward, int accum, hipStream_t stream) {
+  if ((long long)B * HW * C >= (1LL << 31)) return -4;
   if (!backward) gap_fwd_kernel<<<grid_for((long long)B * C), 256, 0, stream>>>(x, y, B, HW, C);
   else gap_bwd_kernel<<<grid_for((long long)B * HW * C), 256, 0, stream>>>(x, y, B, HW, C, accum);
   TDE_LAUNCH_CHECK();
@@ -1095,6 +1277,7 @@ TDE_API int tde_gap(const bf16* x, bf16* y, int B, int HW, int C, int backward, 
 
 TDE_API int tde_pad(const bf16* src, bf16* dst, const int* geo, int backward, int accum, hipStream_t stream) {
   Geo g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9], geo[10], geo[11], geo[12]};
+  if ((long long)g.B * g.Ho * g.Wo * g.C >= (1LL << 31)) return -4;
   pad_kernel<<<grid_for((long long)g.B * g.Ho * g.Wo * g.C), 256, 0, stream>>>(src, dst, g, backward, accum);
   TDE_LAUNCH_CHECK();
   return 0;
@@ -1111,6 +1294,7 @@ TDE_API int tde_xent(const float* logits, long long ldl, const int* labels, int 
 }
 
 TDE_API int tde_colstats(const bf16* x, long long R, int C, double* stats, hipStream_t stream) {
+  if (R * C >= (1LL << 31)) return -4;
   if (C > kMaxCB) return -1;
   colstats_kernel<<<grid_for(R * C, 8), 256, 0, stream>>>(x, R, C, stats);
   TDE_LAUNCH_CHECK();

@@ -25,6 +25,7 @@ from .models.model import Model, Sequential  # noqa: F401
 from . import parallel as distribute  # noqa: F401
 from .parallel import cluster as _cluster
 from .train import estimator as _estimator
+from .train import callbacks as _callbacks
 from .train import hooks as _hooks
 from .utils import logging as _logging
 from .utils.tensorboard import start_tensorboard  # noqa: F401
@@ -91,6 +92,8 @@ keras = _Namespace(
     mixed_precision=_MixedPrecision(),
     datasets=_Namespace(mnist=_Namespace(load_data=_load_mnist)),
     estimator=_Namespace(model_to_estimator=_estimator.model_to_estimator),
+    callbacks=_callbacks,
+    Input=_layers.Input,
 )
 
 # tf.train.* names live on the real `train` subpackage (keeps `import ...train.estimator` working)

@@ -102,6 +102,14 @@ class Model:
             self._programs[key] = prog
         return prog
 
+    def _set_iterations(self, step: int):
+        """Restore the optimizer step counter (host and every plan's device counter)."""
+        if self.optimizer is not None:
+            self.optimizer.iterations = int(step)
+        for prog in self._programs.values():
+            for plan in prog.plans:
+                plan.iterations.fill_(int(step))
+
     def _weights_changed(self):
         """Propagate replica-0 values to every replica and refresh kernel caches."""
         st = self._strategy
@@ -115,7 +123,8 @@ class Model:
         """MEAN of the SyncOnRead (BN moving-stat) variables across replicas (C4)."""
         st = self._strategy
         lst = self._stores.get(id(st)) if st is not None else None
-        if not lst or st.num_replicas_in_sync == 1:
+        has_state = any(not seg.trainable for seg in self._store.segments.values())
+        if not lst or st.num_replicas_in_sync == 1 or not has_state:
             return self._store.state.detach().clone()
         bufs = [s.state.clone() for s in lst]
         st.comm.all_reduce_(bufs, op="mean")

@@ -130,7 +130,8 @@ class TCPStore:
             raise StoreError("barrier failed")
 
     def heartbeat(self, member_id: str):
-        self._lib.tde_store_heartbeat(self._h, member_id.encode())
+        if self._lib.tde_store_heartbeat(self._h, member_id.encode()) != 0:
+            raise StoreError("heartbeat failed: store unreachable")
 
     def dead_members(self, timeout: float) -> list:
         buf = C.create_string_buffer(1 << 16)

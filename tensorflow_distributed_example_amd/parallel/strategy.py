@@ -289,6 +289,9 @@ class MultiWorkerMirroredStrategy(Strategy):
             comm = CM.LocalCommunicator(n_local) if not use_gpu else CM.RcclCommunicator(devs)
         super().__init__(devs, comm, num_workers=world, worker_index=topo.rank, name="MultiWorkerMirroredStrategy")
         self.cluster_resolver = cluster_resolver or CL.TFConfigClusterResolver()
+        # peer failure detection: heartbeats to the chief's native store + watchdog
+        from . import health
+        self.health = health.maybe_start(topo.rank, world, comm)
 
     @staticmethod
     def _rccl(devs, topo, world, n_local):

@@ -105,7 +105,52 @@ class ModelCheckpoint(Callback):
 
     def on_epoch_end(self, epoch, logs=None):
         path = self.filepath.format(epoch=epoch + 1, **(logs or {}))
-        self.model.save_weights(path)
+        st = self.model._strategy
+        if st is None or st.is_chief:
+            self.model.save_weights(path)
+        else:
+            self.model.state_dict()              # take part in the SyncOnRead collective only
+
+
+class BackupAndRestore(Callback):
+    """``tf.keras.callbacks.BackupAndRestore``: fault-tolerant fit for MultiWorkerMirroredStrategy.
+
+    The chief backs up weights, optimizer slots, the step counter and the finished epoch into
+    ``backup_dir`` (TensorBundle, atomic state file) at the end of every epoch; when ``fit`` starts
+    and a backup exists, every worker restores it and training resumes with the next epoch — the
+    recovery half of the failure handling in SURVEY.md §5.3 (parallel/health.py detects the
+    failure and stops the job).  The backup is deleted when training finishes."""
+
+    def __init__(self, backup_dir, save_freq="epoch", delete_checkpoint=True):
+        super().__init__()
+        if save_freq != "epoch":
+            raise ValueError("BackupAndRestore: only save_freq='epoch' is supported")
+        self.backup_dir = backup_dir
+        self.delete_checkpoint = delete_checkpoint
+
+    def _mgr(self):
+        from .checkpoint import CheckpointManager
+        return CheckpointManager(self.backup_dir, max_to_keep=1, prefix="backup")
+
+    def on_train_begin(self, logs=None):
+        r = self._mgr().restore(self.model)
+        if r is None:
+            return
+        step, extras = r
+        self.model._set_iterations(step)
+        self.model._resume_epoch = int(extras.get("epoch", -1)) + 1
+
+    def on_epoch_end(self, epoch, logs=None):
+        st = self.model._strategy
+        state = self.model.state_dict()          # collective (SyncOnRead MEAN) on every worker
+        if st is None or st.is_chief:
+            self._mgr().save(self.model, self.model.optimizer.iterations, extra={"epoch": epoch}, state=state)
+
+    def on_train_end(self, logs=None):
+        st = self.model._strategy
+        if self.delete_checkpoint and (st is None or st.is_chief):
+            import shutil
+            shutil.rmtree(self.backup_dir, ignore_errors=True)
 
 
 class LambdaCallback(Callback):

@@ -34,9 +34,11 @@ class CheckpointManager:
     def latest(self):
         return TB.latest_checkpoint(self.dir)
 
-    def save(self, model, global_step: int, extra: dict | None = None) -> str:
+    def save(self, model, global_step: int, extra: dict | None = None, state: dict | None = None) -> str:
+        """``state``: a ``model.state_dict()`` taken on EVERY worker (its SyncOnRead reduction is a
+        collective) when only the chief writes."""
         self.dir.mkdir(parents=True, exist_ok=True)
-        tensors = {k: v.numpy() for k, v in model.state_dict().items()}
+        tensors = {k: v.numpy() for k, v in (state if state is not None else model.state_dict()).items()}
         tensors["global_step"] = np.array(int(global_step), dtype=np.int64)
         opt = model.optimizer
         if opt is not None and model._store is not None:

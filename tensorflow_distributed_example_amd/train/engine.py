@@ -18,6 +18,7 @@ from ..data.dataset import Dataset, _Batch
 from ..data.distributed import DistributedDataset
 from ..metrics import logs_from
 from . import callbacks as CB
+from ..utils import fault
 
 
 def _global_batch_of(ds):
@@ -90,7 +91,10 @@ def fit(model, x=None, y=None, batch_size=None, epochs=1, verbose="auto", callba
     cl = CB.CallbackList(cbs, model, {"epochs": epochs, "steps": steps_per_epoch, "verbose": verbose})
     model.history = hist
     model.stop_training = False
+    model._resume_epoch = None
     cl.on_train_begin()
+    if model._resume_epoch is not None:      # BackupAndRestore restored a finished epoch
+        initial_epoch = max(initial_epoch, model._resume_epoch)
     it = None
     persist = steps_per_epoch is not None
 
@@ -137,6 +141,7 @@ def fit(model, x=None, y=None, batch_size=None, epochs=1, verbose="auto", callba
                     glob = sum(len(r[1]) for r in g) * strategy.num_workers
                     prog.run_single(g, glob)
             step += len(group)
+            fault.maybe_inject(model.optimizer.iterations + step)
             if chief and verbose:
                 cl.on_train_batch_end(step - 1, logs_from(prog.local_metrics(), model._metric_names)
                                       if verbose == 1 and _due(prog) else None)
