@@ -13,7 +13,14 @@ with the capabilities of lowc1012/tensorflow-distributed-example:
     est = tde.keras.estimator.model_to_estimator(keras_model=model, model_dir=D, config=run_config)
     tde.estimator.train_and_evaluate(est, train_spec, eval_spec)
 """
-import torch  # noqa: F401  (first: our HIP library reuses torch's libamdhip64/librccl)
+import os as _os
+
+if _os.environ.get("TDE_DEBUG_SYNC", "0") not in ("", "0"):   # before any HIP call (utils/debug.py)
+    _os.environ.setdefault("AMD_SERIALIZE_KERNEL", "3")
+    _os.environ.setdefault("HIP_LAUNCH_BLOCKING", "1")
+    _os.environ["TDE_GRAPH"] = "0"
+
+import torch  # noqa: F401,E402  (first: our HIP library reuses torch's libamdhip64/librccl)
 
 from . import backend  # noqa: F401
 from . import data, losses, metrics, optimizers  # noqa: F401
@@ -93,6 +100,7 @@ keras = _Namespace(
     datasets=_Namespace(mnist=_Namespace(load_data=_load_mnist)),
     estimator=_Namespace(model_to_estimator=_estimator.model_to_estimator),
     callbacks=_callbacks,
+    # (ReplicaConsistencyCheck lives in utils.debug; exposed below)
     Input=_layers.Input,
 )
 
@@ -114,3 +122,7 @@ contrib = _Namespace(distribute=_Namespace(DistributeConfig=_estimator.Distribut
 
 saved_model = _Namespace(load=_export.load)
 ConfigProto = _estimator.SessionConfig
+
+from .utils import debug  # noqa: E402
+
+_callbacks.ReplicaConsistencyCheck = debug.ReplicaConsistencyCheck

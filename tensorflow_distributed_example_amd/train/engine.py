@@ -114,6 +114,9 @@ def fit(model, x=None, y=None, batch_size=None, epochs=1, verbose="auto", callba
         return per
 
     logs = {}
+    import os
+    check_every = int(os.environ.get("TDE_CHECK_REPLICAS", "0") or 0)   # utils/debug.py
+    n_exec = 0
     for epoch in range(initial_epoch, epochs):
         if not persist:
             it = None
@@ -141,6 +144,11 @@ def fit(model, x=None, y=None, batch_size=None, epochs=1, verbose="auto", callba
                     glob = sum(len(r[1]) for r in g) * strategy.num_workers
                     prog.run_single(g, glob)
             step += len(group)
+            n_exec += 1
+            if check_every and n_exec % check_every == 0:
+                from ..utils import debug
+                prog.sync()
+                debug.check_replicas(model, f"after step {model.optimizer.iterations + step}")
             fault.maybe_inject(model.optimizer.iterations + step)
             if chief and verbose:
                 cl.on_train_batch_end(step - 1, logs_from(prog.local_metrics(), model._metric_names)

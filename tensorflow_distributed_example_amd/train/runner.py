@@ -87,6 +87,7 @@ class Program:
                               self.plans[0].kind != "reference" and
                               (self.comm is None or self.comm.capturable))
         self._comm_warm = False
+        self._dbg = os.environ.get("TDE_DEBUG_SYNC", "0") not in ("", "0") and cuda
 
     @property
     def plan_kind(self):
@@ -106,11 +107,21 @@ class Program:
             for r, plan in enumerate(self.plans):
                 with _ctx(plan.device):
                     plan.train_step(self.x_ring[r][s], self.y_ring[r][s], B)
+                self._debug_sync("train_step")
             if self.comm is not None:
                 self.comm.all_reduce_([p.store.g for p in self.plans])
+                self._debug_sync("gradient all-reduce")
             for plan in self.plans:
                 with _ctx(plan.device):
                     plan.apply()
+                self._debug_sync("optimizer")
+
+    def _debug_sync(self, what):
+        if self._dbg:
+            try:
+                self.sync()
+            except RuntimeError as e:
+                raise RuntimeError(f"device fault surfaced after {what} (TDE_DEBUG_SYNC): {e}") from e
 
     def _warm_comm(self):
         if self.comm is not None and not self._comm_warm:

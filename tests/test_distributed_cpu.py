@@ -110,3 +110,25 @@ def test_multi_worker_mirrored_gloo_two_processes(tmp_path):
     for k, a in zip(wa.files, m1.get_weights()):
         assert np.allclose(wa[k], a, atol=2e-5, rtol=1e-4)
     assert abs(outs[0]["loss"] - h1.history["loss"][0]) < 1e-4
+
+
+def test_replica_consistency_checker_detects_divergence():
+    """all replicas bit-identical after training; a perturbed replica is reported."""
+    from tensorflow_distributed_example_amd.utils import debug
+    x, y = _data(128)
+    w0 = tde.zoo.mnist_cnn().get_weights()
+    tde.backend.clear_session()
+    st = tde.distribute.MirroredStrategy(["cpu", "cpu"])
+    with st.scope():
+        m = tde.zoo.mnist_cnn()
+        m.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True),
+                  optimizer=tde.optimizers.SGD(0.1), metrics=["accuracy"])
+    m.set_weights(w0)
+    ds = tde.data.Dataset.from_tensor_slices((x, y)).batch(64)
+    m.fit(ds, epochs=2, verbose=0, callbacks=[tde.keras.callbacks.ReplicaConsistencyCheck(1)])
+    fps = debug.check_replicas(m)
+    assert len(fps) == 2 and fps[0][2] == fps[1][2]
+    stores = m._stores[id(st)]
+    stores[1].w.view(-1)[123] += 1e-6          # one flipped low bit is enough
+    with pytest.raises(debug.ReplicaDivergence, match="replica 1"):
+        debug.check_replicas(m)
