@@ -1114,10 +1114,66 @@ using namespace tde;
 
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+// Split-K epilogue: the GEMM accumulated into the f32 scratch with atomics; apply bias / statistics /
+// ReLU / bf16 (+=) store / f32 store here, and re-zero the scratch for its next use.
+__global__ __launch_bounds__(256) void gemm_finalize_kernel(float* __restrict__ scr, int M, int N, float alpha,
+                                                            const float* __restrict__ bias, int relu,
+                                                            float* __restrict__ cf, long long ldc,
+                                                            bf16* __restrict__ cb, long long ldcb, int cb_accum,
+                                                            double* __restrict__ colstats) {
+  __shared__ float s1[kMaxCB], s2[kMaxCB];
+  if (colstats) {
+    for (int c = threadIdx.x; c < N; c += blockDim.x) s1[c] = s2[c] = 0.f;
+    __syncthreads();
+  }
+  const long long n = (long long)M * N;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x) {
+    const int col = (int)((unsigned long long)e % (unsigned)N);
+    const long long row = e / N;
+    float v = alpha * scr[e] + (bias ? bias[col] : 0.f);
+    scr[e] = 0.f;
+    if (colstats) {
+      const float q = cb ? bf2f(f2bf(v)) : v;
+      atomicAdd(&s1[col], q);
+      atomicAdd(&s2[col], q * q);
+    }
+    if (relu) v = fmaxf(v, 0.f);
+    if (cf) cf[row * ldc + col] = v;
+    if (cb) {
+      bf16* q = &cb[row * ldcb + col];
+      if (cb_accum) v += bf2f(*q);
+      *q = f2bf(v);
+    }
+  }
+  if (colstats) {
+    __syncthreads();
+    for (int c = threadIdx.x; c < N; c += blockDim.x) {
+      atomicAdd(&colstats[c], (double)s1[c]);
+      atomicAdd(&colstats[N + c], (double)s2[c]);
+    }
+  }
+}
+
 TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, long long ldb, int bkind, int M, int N,
                       int K, const int* geo, int splits, float* cf, long long ldc, int cf_mode, float alpha, bf16* cb,
-                      long long ldcb, int cb_accum, const float* bias, int relu, double* colstats, hipStream_t stream) {
+                      long long ldcb, int cb_accum, const float* bias, int relu, double* colstats, float* scratch,
+                      hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
+  const bool fused_epi = cb || colstats || bias || relu || cf_mode == 1;
+  if (splits > 1 && fused_epi) {
+    // split-K into the zeroed f32 scratch, then the epilogue pass
+    if (!scratch || (colstats && N > kMaxCB)) return -2;
+    int rc = tde_igemm(a, lda, akind, b, ldb, bkind, M, N, K, geo, splits, scratch, N, 2, 1.f, nullptr, 0, 0,
+                       nullptr, 0, nullptr, nullptr, stream);
+    if (rc) return rc;
+    const long long n = (long long)M * N;
+    int g = (int)((n + 255) / 256);
+    if (g > 1024) g = 1024;
+    gemm_finalize_kernel<<<g, 256, 0, stream>>>(scratch, M, N, alpha, bias, relu, cf_mode == 1 ? cf : nullptr, ldc,
+                                                 cb, ldcb, cb_accum, colstats);
+    TDE_LAUNCH_CHECK();
+    return 0;
+  }
   IGemmArgs p{};
   p.a = a;
   p.lda = lda;

@@ -79,17 +79,41 @@ def pick_splits(M, N_, K, target=512):
     return s
 
 
+def fwd_splits(M, N_, K):
+    """Split-K factor for an activation-producing GEMM (fwd / dgrad): only when the output tiles
+    alone cannot fill the 256 CUs and the K loop is long (latency-bound); the partial sums go
+    through the f32 scratch + finalize pass."""
+    tiles = -(-M // 64) * -(-N_ // 64)
+    ktiles = -(-K // 32)
+    if tiles >= 256 or ktiles < 8:
+        return 1
+    return max(1, min(-(-512 // tiles), ktiles // 4))
+
+
+def scratch_elems(M, N_, K):
+    return M * N_ if fwd_splits(M, N_, K) > 1 else 0
+
+
 def _igemm(a, lda, ak, b, ldb, bk, M, N_, K, geo=None, splits=1, cf=None, ldc=0, cf_mode=0, alpha=1.0,
-           cb=None, ldcb=0, cb_accum=False, bias=None, relu=False, colstats=None):
+           cb=None, ldcb=0, cb_accum=False, bias=None, relu=False, colstats=None, scratch=None):
     g = geo.carray() if geo is not None else None
+    if splits > 1 and scratch is not None:
+        _f32(scratch, M * N_, "igemm split-K scratch")
     rc = N.hip().tde_igemm(_P(a), int(lda), ak, _P(b), int(ldb), bk, int(M), int(N_), int(K), g, int(splits),
                            _P(cf), int(ldc), int(cf_mode), float(alpha), _P(cb), int(ldcb), int(cb_accum), _P(bias),
-                           int(relu), _P(colstats), _s())
+                           int(relu), _P(colstats), _P(scratch), _s())
     N.check(rc, "tde_igemm")
 
 
+def _fs(M, N_, K, scratch):
+    if scratch is None:
+        return 1
+    s = fwd_splits(M, N_, K)
+    return s if s > 1 and scratch.numel() >= M * N_ else 1
+
+
 # ---------------------------------------------------------------- Conv2D
-def conv_fwd(x, Wt, y, g: ConvGeom, bias=None, relu=False, colstats=None):
+def conv_fwd(x, Wt, y, g: ConvGeom, bias=None, relu=False, colstats=None, scratch=None):
     """y[B,Ho,Wo,Co] = conv(x[B,H,W,C], W) (+bias, ReLU); Wt = [Co, KH*KW*C] bf16 (transposed shadow)."""
     _bf(x, g.B * g.H * g.W * g.C, "conv_fwd x")
     _req(Wt.dtype == bf16 and tuple(Wt.shape) == (g.Co, g.K) and Wt.is_contiguous(), "conv_fwd Wt")
@@ -98,17 +122,19 @@ def conv_fwd(x, Wt, y, g: ConvGeom, bias=None, relu=False, colstats=None):
         _f32(bias, g.Co, "conv_fwd bias")
     if colstats is not None:
         _f64(colstats, 2 * g.Co, "conv_fwd colstats")
-    _igemm(x, 0, A_CONV, Wt, g.K, B_NK, g.B * g.Ho * g.Wo, g.Co, g.K, g, cb=y, ldcb=g.Co, bias=bias, relu=relu,
-           colstats=colstats)
+    M = g.B * g.Ho * g.Wo
+    _igemm(x, 0, A_CONV, Wt, g.K, B_NK, M, g.Co, g.K, g, splits=_fs(M, g.Co, g.K, scratch), cb=y, ldcb=g.Co,
+           bias=bias, relu=relu, colstats=colstats, scratch=scratch)
 
 
-def conv_dgrad(dy, Wrow, dx, g: ConvGeom, accum=False):
+def conv_dgrad(dy, Wrow, dx, g: ConvGeom, accum=False, scratch=None):
     """dx[B,H,W,C] (=|+=) conv_transpose(dy[B,Ho,Wo,Co], W); Wrow = HWIO bf16."""
     _bf(dy, g.B * g.Ho * g.Wo * g.Co, "conv_dgrad dy")
     _bf(Wrow, g.K * g.Co, "conv_dgrad W")
     _bf(dx, g.B * g.H * g.W * g.C, "conv_dgrad dx")
-    _igemm(dy, 0, A_DGRAD, Wrow, 0, B_DGRADW, g.B * g.H * g.W, g.C, g.KH * g.KW * g.Co, g, cb=dx, ldcb=g.C,
-           cb_accum=accum)
+    M, K = g.B * g.H * g.W, g.KH * g.KW * g.Co
+    _igemm(dy, 0, A_DGRAD, Wrow, 0, B_DGRADW, M, g.C, K, g, splits=_fs(M, g.C, K, scratch), cb=dx, ldcb=g.C,
+           cb_accum=accum, scratch=scratch)
 
 
 def conv_wgrad(x, dy, dW, g: ConvGeom, splits=None):
@@ -122,7 +148,7 @@ def conv_wgrad(x, dy, dW, g: ConvGeom, splits=None):
 
 
 # ---------------------------------------------------------------- Dense
-def dense_fwd(x, Wt, B, *, y=None, logits=None, bias=None, relu=False, colstats=None):
+def dense_fwd(x, Wt, B, *, y=None, logits=None, bias=None, relu=False, colstats=None, scratch=None):
     """[B,out] = x[B,in] @ W (+bias, ReLU) -> bf16 ``y`` and/or f32 ``logits``; Wt = [out, in] bf16."""
     out, fin = Wt.shape
     _bf(x, B * fin, "dense_fwd x")
@@ -135,17 +161,19 @@ def dense_fwd(x, Wt, B, *, y=None, logits=None, bias=None, relu=False, colstats=
         _f32(bias, out, "dense_fwd bias")
     if colstats is not None:
         _f64(colstats, 2 * out, "dense_fwd colstats")
-    _igemm(x, fin, A_ROWK, Wt, fin, B_NK, B, out, fin, cf=logits, ldc=out, cf_mode=1 if logits is not None else 0,
-           cb=y, ldcb=out, bias=bias, relu=relu, colstats=colstats)
+    _igemm(x, fin, A_ROWK, Wt, fin, B_NK, B, out, fin, splits=_fs(B, out, fin, scratch), cf=logits, ldc=out,
+           cf_mode=1 if logits is not None else 0, cb=y, ldcb=out, bias=bias, relu=relu, colstats=colstats,
+           scratch=scratch)
 
 
-def dense_dgrad(dy, Wrow, dx, B, accum=False):
+def dense_dgrad(dy, Wrow, dx, B, accum=False, scratch=None):
     """dx[B,in] (=|+=) dy[B,out] @ W^T; Wrow = [in, out] bf16."""
     fin, out = Wrow.shape
     _bf(dy, B * out, "dense_dgrad dy")
     _req(Wrow.dtype == bf16 and Wrow.is_contiguous(), "dense_dgrad W")
     _bf(dx, B * fin, "dense_dgrad dx")
-    _igemm(dy, out, A_ROWK, Wrow, out, B_NK, B, fin, out, cb=dx, ldcb=fin, cb_accum=accum)
+    _igemm(dy, out, A_ROWK, Wrow, out, B_NK, B, fin, out, splits=_fs(B, fin, out, scratch), cb=dx, ldcb=fin,
+           cb_accum=accum, scratch=scratch)
 
 
 def dense_wgrad(x, dy, dW, B, splits=None):

@@ -249,6 +249,9 @@ class LayerwisePlan(PG.ReplicaPlan):
                 t.buf, t.grad = t.root().buf, t.root().grad
         for st in self.stages:
             st.alloc(B, dev)
+        # one shared f32 split-K scratch (stages run in order on one stream; finalize re-zeroes it)
+        need = max([st.scratch_need(B) for st in self.stages if hasattr(st, "scratch_need")] + [0])
+        self.scratch = torch.zeros(max(need, 1), dtype=torch.float32, device=dev) if need else None
 
     # ------------------------------------------------------------------ plan interface
     def on_weights_loaded(self):
@@ -328,6 +331,14 @@ class _Gemm(_Stage):
         self.colstats = None
         self.dz = None
 
+    def scratch_need(self, B):
+        if self.conv:
+            g = self.geo.with_batch(B)
+            return max(O.scratch_elems(g.B * g.Ho * g.Wo, g.Co, g.K),
+                       O.scratch_elems(g.B * g.H * g.W, g.C, g.KH * g.KW * g.Co) if self.need_dgrad else 0)
+        rows, fin, out = self.inp.rows(B), self.W.shape[0], self.W.shape[1]
+        return max(O.scratch_elems(rows, out, fin), O.scratch_elems(rows, fin, out) if self.need_dgrad else 0)
+
     def alloc(self, B, dev):
         if self.stats:
             self.colstats = torch.zeros(2 * self.out.C, dtype=torch.float64, device=dev)
@@ -345,11 +356,11 @@ class _Gemm(_Stage):
         cs = self.colstats if (self.stats and training) else None
         if self.conv:
             O.conv_fwd(self.inp.buf, self.Wt, self.out.root().buf, self.geo.with_batch(B), bias=self.b,
-                       relu=self.relu, colstats=cs)
+                       relu=self.relu, colstats=cs, scratch=p.scratch)
         else:
             rows = self.inp.rows(B)
             O.dense_fwd(self.inp.buf, self.Wt, rows, y=self.out.root().buf, bias=self.b, relu=self.relu,
-                        colstats=cs)
+                        colstats=cs, scratch=p.scratch)
 
     def bwd(self, p, B):
         dout = self.out.root().grad
@@ -361,12 +372,14 @@ class _Gemm(_Stage):
             g = self.geo.with_batch(B)
             O.conv_wgrad(self.inp.buf, dout, self.gW, g)
             if self.need_dgrad:
-                O.conv_dgrad(dout, self.Wrow, self.inp.root().grad, g, accum=self.accum[self.inp.root().id])
+                O.conv_dgrad(dout, self.Wrow, self.inp.root().grad, g, accum=self.accum[self.inp.root().id],
+                             scratch=p.scratch)
         else:
             rows = self.inp.rows(B)
             O.dense_wgrad(self.inp.buf, dout, self.gW.view(self.W.shape[0], -1), rows)
             if self.need_dgrad:
-                O.dense_dgrad(dout, self.Wrow, self.inp.root().grad, rows, accum=self.accum[self.inp.root().id])
+                O.dense_dgrad(dout, self.Wrow, self.inp.root().grad, rows, accum=self.accum[self.inp.root().id],
+                              scratch=p.scratch)
 
 
 class _Elementwise(_Stage):
