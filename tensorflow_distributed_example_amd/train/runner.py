@@ -150,7 +150,18 @@ class Program:
     def run(self):
         if self.use_graph:
             if self.graph is None or self._graph_key != self._key():
-                self.capture()
+                try:
+                    self.capture()
+                except RuntimeError as e:
+                    # e.g. a collective implementation that refuses stream capture: keep training
+                    # with eager launches (same kernels, one host launch each) instead of failing
+                    import warnings
+                    warnings.warn(f"hipGraph capture of the training step failed ({e}); running eagerly")
+                    self.use_graph = False
+                    self.graph = None
+                    torch.cuda.synchronize(self.devices[0])
+                    self._steps(self.S)
+                    return
             with torch.cuda.device(self.devices[0]):
                 self.graph.replay()
         else:
