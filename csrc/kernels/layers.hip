@@ -79,8 +79,13 @@ __device__ __forceinline__ bf16x8 zero8() {
 // Row-contiguous operands (weight grads: channels are contiguous, the reduction runs over pixels):
 // [k = 32][128] image with 256-byte rows and an XOR chunk swizzle, read back transposed with
 // ds_read_b64_tr_b16 (CDNA4 hardware transpose): conflict-free for the 16x16x32 operand.
+// RW = 128: 256-byte rows, XOR of the 16-byte chunk index with ((row&3)<<2)|((row>>2)&3).
+// RW = 64: 128-byte rows (2 rows per 64 banks); the chunk pair is XORed with (row bit 1, row bit 3)
+// so the 8 rows one 32-lane half of a transposed read touches land in 8 distinct bank groups.
+template <int RW>
 __device__ __forceinline__ int swz(int row, int ch) {
-  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+  if (RW == 128) return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+  return 128 * row + 16 * (ch ^ ((((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1));
 }
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
@@ -88,13 +93,14 @@ typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
 // 16x16x32 operand fragment (rows mb..mb+15 of the image's 128 columns, k 0..31) via two
 // transposed 4x16 reads per 16-lane group.
+template <int RW>
 __device__ __forceinline__ bf16x8 tr_frag(const bf16* img, int mb, int lane) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
   const int ch = (mb >> 3) + (pp >> 1);
   const char* base = reinterpret_cast<const char*>(img);
-  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + swz(8 * g + q, ch) + 8 * (pp & 1)));
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + swz<RW>(8 * g + q, ch) + 8 * (pp & 1)));
   const v4i16 hi =
-      __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + swz(8 * g + 4 + q, ch) + 8 * (pp & 1)));
+      __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + swz<RW>(8 * g + 4 + q, ch) + 8 * (pp & 1)));
   // concatenate as 16-bit integers, then reinterpret the whole vector (element-wise bf16 casts of
   // the intrinsic's result mis-assemble the fragment)
   typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -305,12 +311,12 @@ template <int AK, int BK_, int BM, int BN>
 __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   constexpr bool AKV = (AK == A_ROWK || AK == A_CONV || AK == A_DGRAD);  // K-vector A
   constexpr bool BKV = (BK_ == B_NK || BK_ == B_DGRADW);                 // K-vector B
-  static_assert(AKV || BM == 128, "row-contiguous A needs the 128-wide transposed image");
-  static_assert(BKV || BN == 128, "row-contiguous B needs the 128-wide transposed image");
-  constexpr int AIMG = AKV ? BM * LDK : TK * 128;  // elements per buffer
-  constexpr int BIMG = BKV ? BN * LDK : TK * 128;
-  constexpr int AS = AKV ? BM / 64 : 2;  // 16-byte slots per thread
-  constexpr int BS = BKV ? BN / 64 : 2;
+  constexpr int AIMG = AKV ? BM * LDK : TK * BM;  // elements per buffer
+  constexpr int BIMG = BKV ? BN * LDK : TK * BN;
+  constexpr int AS = BM / 64;  // 16-byte slots per thread (either image kind)
+  constexpr int BS = BN / 64;
+  // row-vector images: CH 16-byte chunks per k row, a slot step covers 256/CH k rows
+  constexpr int CHA = BM / 8, RSA = 256 / CHA, CHB = BN / 8, RSB = 256 / CHB;
   constexpr int WTM = BM / 2, WTN = BN / 2, MI = WTM / 16, NI = WTN / 16;
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * (AIMG + BIMG)];
   bf16* const As = smem;
@@ -326,8 +332,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
 
   // ---- loader state
   const int lk = (tid & 3) * 8;   // K-vector: k offset of every slot of this thread
-  const int vk = tid >> 4;        // row-vector slot s = tid + 256*i: k row = s >> 4, chunk = s & 15
-  const int vch = tid & 15;
+  const int vka = tid / CHA, vca = tid % CHA;  // row-vector A: k row (+RSA per slot), m chunk
+  const int vkb = tid / CHB, vcb = tid % CHB;
   ARow ar[AS];
   WRow wr[AS];
   KPos ka{0, 0, 0}, kb{0, 0, 0};
@@ -341,7 +347,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   } else {
 #pragma unroll
     for (int i = 0; i < AS; ++i) {
-      const int m = m0 + vch * 8;  // both slots share the chunk (rows vk and vk+16)
+      const int m = m0 + vca * 8;  // every slot shares the chunk (k rows vka + RSA*i)
       if (AK == A_WGRAD) {
         const int mm = m < p.M ? m : 0;
         const KPos t = kpos_of(mm, p.g.C, KW);
@@ -349,7 +355,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
       }
     }
     if (AK == A_WGRAD) {
-      const int k = kt0 * TK + vk;
+      const int k = kt0 * TK + vka;
       const int hw = p.g.Ho * p.g.Wo;
       const int b = k / hw, rem = k - b * hw;
       pa = PixPos{b, rem / p.g.Wo, rem - (rem / p.g.Wo) * p.g.Wo};
@@ -367,8 +373,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
 #pragma unroll
       for (int i = 0; i < AS; ++i) {
         PixPos q = pa;
-        if (AK == A_WGRAD && i) pix_advance(q, 16, p.g.Ho, p.g.Wo);
-        ra[i] = load_a_m8<AK>(p, m0 + vch * 8, wr[i], q, k0 + vk + 16 * i);
+        if (AK == A_WGRAD && i) pix_advance(q, RSA * i, p.g.Ho, p.g.Wo);
+        ra[i] = load_a_m8<AK>(p, m0 + vca * 8, wr[i], q, k0 + vka + RSA * i);
       }
     }
     if (BKV) {
@@ -376,7 +382,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
       for (int i = 0; i < BS; ++i) rb[i] = load_b_k8<BK_>(p, n0 + ((tid + 256 * i) >> 2), kb, k0 + lk);
     } else {
 #pragma unroll
-      for (int i = 0; i < BS; ++i) rb[i] = load_b_n8(p, n0 + vch * 8, k0 + vk + 16 * i);
+      for (int i = 0; i < BS; ++i) rb[i] = load_b_n8(p, n0 + vcb * 8, k0 + vkb + RSB * i);
     }
     // advance the incremental decompositions to the next k-tile
     if (AKV && AK != A_ROWK) kpos_advance(ka, TK, Cda, KW);
@@ -392,7 +398,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
     } else {
 #pragma unroll
       for (int i = 0; i < AS; ++i)
-        *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(a) + swz(vk + 16 * i, vch)) = ra[i];
+        *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(a) + swz<BM>(vka + RSA * i, vca)) = ra[i];
     }
     if (BKV) {
 #pragma unroll
@@ -400,7 +406,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
     } else {
 #pragma unroll
       for (int i = 0; i < BS; ++i)
-        *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(b) + swz(vk + 16 * i, vch)) = rb[i];
+        *reinterpret_cast<bf16x8*>(reinterpret_cast<char*>(b) + swz<BN>(vkb + RSB * i, vcb)) = rb[i];
     }
   };
 
@@ -426,13 +432,13 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
       for (int i = 0; i < MI; ++i) {
         const int r = wm * WTM + i * 16;
         if (AKV) af[i] = *reinterpret_cast<const bf16x8*>(a + (r + fr) * LDK + fk);
-        else af[i] = tr_frag(a, r, lane);
+        else af[i] = tr_frag<BM>(a, r, lane);
       }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int c = wn * WTN + j * 16;
         if (BKV) bfr[j] = *reinterpret_cast<const bf16x8*>(b + (c + fr) * LDK + fk);
-        else bfr[j] = tr_frag(b, c, lane);
+        else bfr[j] = tr_frag<BN>(b, c, lane);
       }
 #pragma unroll
       for (int i = 0; i < MI; ++i)
@@ -934,6 +940,102 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(PoolArgs a) {
   }
 }
 
+// Channel-vectorised max pooling (C % 8 == 0): one thread per (pixel, 8 channels); index math
+// once per thread, 16-byte loads/stores, the 8 argmax bytes as one 8-byte word.
+__global__ __launch_bounds__(256) void maxpool_fwd8_kernel(PoolArgs a) {
+  const Geo& g = a.g;
+  const int C8 = g.C >> 3;
+  const int n = g.B * g.Ho * g.Wo * C8;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const int c8 = e % C8;
+    int t = e / C8;
+    const int ow = t % g.Wo;
+    t /= g.Wo;
+    const int oh = t % g.Ho;
+    const int b = t / g.Ho;
+    float best[8];
+    unsigned char bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      best[j] = -INFINITY;
+      bi[j] = 0;
+    }
+    for (int i = 0; i < g.KH; ++i) {
+      const int ih = oh * g.sh - g.pt + i;
+      if ((unsigned)ih >= (unsigned)g.H) continue;
+      for (int jj = 0; jj < g.KW; ++jj) {
+        const int iw = ow * g.sw - g.pl + jj;
+        if ((unsigned)iw >= (unsigned)g.W) continue;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(a.x + ((((long long)b * g.H + ih) * g.W + iw) * g.C + c8 * 8));
+        const unsigned char w = (unsigned char)(i * g.KW + jj);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = bf2f(v[j]);
+          if (f > best[j]) {
+            best[j] = f;
+            bi[j] = w;
+          }
+        }
+      }
+    }
+    bf16x8 o;
+    unsigned long long packed = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o[j] = f2bf(best[j]);
+      packed |= (unsigned long long)bi[j] << (8 * j);
+    }
+    *reinterpret_cast<bf16x8*>(a.y + (long long)e * 8) = o;
+    if (a.idx) *reinterpret_cast<unsigned long long*>(a.idx + (long long)e * 8) = packed;
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool_bwd8_kernel(PoolArgs a) {
+  const Geo& g = a.g;
+  const int C8 = g.C >> 3;
+  const int n = g.B * g.H * g.W * C8;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const int c8 = e % C8;
+    int t = e / C8;
+    const int iw = t % g.W;
+    t /= g.W;
+    const int ih = t % g.H;
+    const int b = t / g.H;
+    float s[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] = 0.f;
+    const int ty = ih + g.pt, tx = iw + g.pl;
+    const int oh_lo = ty >= g.KH ? (ty - g.KH) / g.sh + 1 : 0, oh_hi = min(g.Ho - 1, ty / g.sh);
+    const int ow_lo = tx >= g.KW ? (tx - g.KW) / g.sw + 1 : 0, ow_hi = min(g.Wo - 1, tx / g.sw);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int i = ty - oh * g.sh;
+      if (i < 0 || i >= g.KH) continue;
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int jj = tx - ow * g.sw;
+        if (jj < 0 || jj >= g.KW) continue;
+        const long long o = ((((long long)b * g.Ho + oh) * g.Wo + ow) * g.C + c8 * 8);
+        const unsigned long long id = *reinterpret_cast<const unsigned long long*>(a.idx + o);
+        const bf16x8 d = *reinterpret_cast<const bf16x8*>(a.dy + o);
+        const unsigned w = (unsigned)(i * g.KW + jj);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (((id >> (8 * j)) & 0xFF) == w) s[j] += bf2f(d[j]);
+      }
+    }
+    bf16x8* q = reinterpret_cast<bf16x8*>(a.dx + (long long)e * 8);
+    bf16x8 o;
+    if (a.dx_accum) {
+      const bf16x8 prev = *q;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(s[j] + bf2f(prev[j]));
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(s[j]);
+    }
+    *q = o;
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Global average pooling [B,HW,C] -> [B,C] and its backward; zero padding / its crop.
 __global__ __launch_bounds__(256) void gap_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int B, int HW,
@@ -1187,6 +1289,7 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     p.g = g;
   }
   const int ktiles = (K + TK - 1) / TK;
+  const bool auto_splits = splits == 0;
   if (splits < 1) splits = 1;
   if (splits > ktiles) splits = ktiles > 0 ? ktiles : 1;
   if (splits > 1 && (cb || colstats || cf_mode != 2 || bias || relu)) return -2;  // split-K only into f32 atomics
@@ -1223,7 +1326,17 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   const bool rowk = (akind == A_COLM || akind == A_WGRAD);
   auto tiles = [&](int tm, int tn) { return (long long)((M + tm - 1) / tm) * ((N + tn - 1) / tn) * splits; };
   if (rowk) {
-    bm = bn = 128;
+    bm = M > 64 ? 128 : 64;
+    bn = N > 64 ? 128 : 64;
+    if (auto_splits) {  // weight grads: f32 atomics, fill the chip with >= ~4 workgroups per CU
+      const long long t = (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+      long long sp = (1024 + t - 1) / t;
+      const long long maxs = ktiles / 4 > 0 ? ktiles / 4 : 1;
+      splits = (int)(sp < maxs ? sp : maxs);
+      if (splits < 1) splits = 1;
+      p.ktiles_per_split = (ktiles + splits - 1) / splits;
+      splits = (ktiles + p.ktiles_per_split - 1) / p.ktiles_per_split;
+    }
   } else if (N > 64 && tiles(128, 128) >= 512) {
     bm = bn = 128;
   } else if (tiles(128, 64) >= 512) {
@@ -1245,9 +1358,15 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     else if (bm == 128) TDE_IGEMM(A_DGRAD, B_DGRADW, 128, 64);
     else TDE_IGEMM(A_DGRAD, B_DGRADW, 64, 64);
   } else if (akind == A_COLM && bkind == B_KN) {
-    TDE_IGEMM(A_COLM, B_KN, 128, 128);
+    if (bm == 128 && bn == 128) TDE_IGEMM(A_COLM, B_KN, 128, 128);
+    else if (bm == 128) TDE_IGEMM(A_COLM, B_KN, 128, 64);
+    else if (bn == 128) TDE_IGEMM(A_COLM, B_KN, 64, 128);
+    else TDE_IGEMM(A_COLM, B_KN, 64, 64);
   } else if (akind == A_WGRAD && bkind == B_KN) {
-    TDE_IGEMM(A_WGRAD, B_KN, 128, 128);
+    if (bm == 128 && bn == 128) TDE_IGEMM(A_WGRAD, B_KN, 128, 128);
+    else if (bm == 128) TDE_IGEMM(A_WGRAD, B_KN, 128, 64);
+    else if (bn == 128) TDE_IGEMM(A_WGRAD, B_KN, 64, 128);
+    else TDE_IGEMM(A_WGRAD, B_KN, 64, 64);
   } else {
     return -1;
   }
@@ -1317,6 +1436,13 @@ TDE_API int tde_maxpool(const bf16* x, bf16* y, unsigned char* idx, const bf16* 
   if (g.KH * g.KW > 256) return -1;
   if ((long long)g.B * g.H * g.W * g.C >= (1LL << 31) || (long long)g.B * g.Ho * g.Wo * g.C >= (1LL << 31)) return -4;
   PoolArgs a{x, y, idx, dy, dx, dx_accum, g};
+  const bool vec = g.C % 8 == 0 && ((uintptr_t)(backward ? (const void*)dy : (const void*)x) & 15) == 0;
+  if (vec) {
+    if (!backward) maxpool_fwd8_kernel<<<grid_for((long long)g.B * g.Ho * g.Wo * g.C, 8), 256, 0, stream>>>(a);
+    else maxpool_bwd8_kernel<<<grid_for((long long)g.B * g.H * g.W * g.C, 8), 256, 0, stream>>>(a);
+    TDE_LAUNCH_CHECK();
+    return 0;
+  }
   if (!backward) maxpool_fwd_kernel<<<grid_for((long long)g.B * g.Ho * g.Wo * g.C), 256, 0, stream>>>(a);
   else maxpool_bwd_kernel<<<grid_for((long long)g.B * g.H * g.W * g.C), 256, 0, stream>>>(a);
   TDE_LAUNCH_CHECK();

@@ -73,10 +73,8 @@ class ConvGeom:
 
 
 def pick_splits(M, N_, K, target=512):
-    tiles = -(-M // 64) * -(-N_ // 64)
-    ktiles = -(-K // 32)
-    s = max(1, min(-(-target // tiles), ktiles // 4))
-    return s
+    """0 = let the kernel pick (weight-grad GEMMs size their split-K from the tile they run)."""
+    return 0
 
 
 def fwd_splits(M, N_, K):

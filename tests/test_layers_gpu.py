@@ -182,10 +182,11 @@ def test_dropout_mask_regenerated_in_backward():
     assert not torch.equal(out2 != 0, kept)
 
 
-@pytest.mark.parametrize("H,W,k,s,pad", [(112, 112, 3, 2, "same"), (26, 26, 2, 2, "valid"), (9, 7, 3, 2, "same")])
-def test_maxpool(H, W, k, s, pad):
+@pytest.mark.parametrize("H,W,k,s,pad,C", [(112, 112, 3, 2, "same", 16), (26, 26, 2, 2, "valid", 32),
+                                           (9, 7, 3, 2, "same", 16), (9, 7, 3, 2, "same", 6)])
+def test_maxpool(H, W, k, s, pad, C):
     from tensorflow_distributed_example_amd.ops import layer_ops as O
-    B, C = 2, 16
+    B = 2
     if pad == "same":
         (pt, pb), (pl, pr) = _tf_same(H, k, s), _tf_same(W, k, s)
         Ho, Wo = -(-H // s), -(-W // s)
