@@ -65,7 +65,7 @@ struct IGemmArgs {
   double* colstats;  // [2][N] sum / sum of squares of the STORED (bf16-rounded) values
 };
 
-constexpr int TM = 64, TN = 64, TK = 32, LDK = TK + 8;
+constexpr int TK = 32;  // MFMA k-slice
 
 __device__ __forceinline__ bf16x8 zero8() {
   bf16x8 r;
@@ -75,7 +75,7 @@ __device__ __forceinline__ bf16x8 zero8() {
 }
 
 // ---- LDS images.
-// K-contiguous operands: [rows][LDK] (32 k + 8 pad; 16-byte fragment rows are conflict-free).
+// K-contiguous operands: [rows][KB + 8] (8-element pad: the 16-byte fragment reads are conflict-free).
 // Row-contiguous operands (weight grads: channels are contiguous, the reduction runs over pixels):
 // [k = 32][128] image with 256-byte rows and an XOR chunk swizzle, read back transposed with
 // ds_read_b64_tr_b16 (CDNA4 hardware transpose): conflict-free for the 16x16x32 operand.
@@ -94,8 +94,8 @@ typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 // 16x16x32 operand fragment (rows mb..mb+15 of the image's 128 columns, k 0..31) via two
 // transposed 4x16 reads per 16-lane group.
 template <int RW>
-__device__ __forceinline__ bf16x8 tr_frag(const bf16* img, int mb, int lane) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* img, int mb, int lane, int k0) {
+  const int g = k0 / 8 + (lane >> 4), i = lane & 15, q = i >> 2, pp = i & 3;
   const int ch = (mb >> 3) + (pp >> 1);
   const char* base = reinterpret_cast<const char*>(img);
   const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + swz<RW>(8 * g + q, ch) + 8 * (pp & 1)));
@@ -307,14 +307,16 @@ __device__ __forceinline__ bf16x8 load_b_n8(const IGemmArgs& p, int n, int k) {
   return v;
 }
 
-template <int AK, int BK_, int BM, int BN>
+template <int AK, int BK_, int BM, int BN, int KB>
 __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   constexpr bool AKV = (AK == A_ROWK || AK == A_CONV || AK == A_DGRAD);  // K-vector A
   constexpr bool BKV = (BK_ == B_NK || BK_ == B_DGRADW);                 // K-vector B
-  constexpr int AIMG = AKV ? BM * LDK : TK * BM;  // elements per buffer
-  constexpr int BIMG = BKV ? BN * LDK : TK * BN;
-  constexpr int AS = BM / 64;  // 16-byte slots per thread (either image kind)
-  constexpr int BS = BN / 64;
+  constexpr int LDKB = KB + 8;                     // K-vector image row: KB k + 8 pad
+  constexpr int AIMG = AKV ? BM * LDKB : KB * BM;  // elements per buffer
+  constexpr int BIMG = BKV ? BN * LDKB : KB * BN;
+  constexpr int AS = BM * KB / 2048;  // 16-byte slots per thread (either image kind)
+  constexpr int BS = BN * KB / 2048;
+  constexpr int KV = KB / 8, RSK = 256 / KV;  // K-vector: vectors per row, rows per slot step
   // row-vector images: CH 16-byte chunks per k row, a slot step covers 256/CH k rows
   constexpr int CHA = BM / 8, RSA = 256 / CHA, CHB = BN / 8, RSB = 256 / CHB;
   constexpr int WTM = BM / 2, WTN = BN / 2, MI = WTM / 16, NI = WTN / 16;
@@ -327,11 +329,12 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   const int wm = wave >> 1, wn = wave & 1;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;  // M-major: neighbours share the B tile in L2
   const int kt0 = blockIdx.z * p.ktiles_per_split;
-  const int kt1 = min((p.K + TK - 1) / TK, kt0 + p.ktiles_per_split);
+  const int kt1 = min((p.K + KB - 1) / KB, kt0 + p.ktiles_per_split);
   if (kt0 >= kt1 && p.cf_mode == 2) return;  // empty split contributes nothing
 
   // ---- loader state
-  const int lk = (tid & 3) * 8;   // K-vector: k offset of every slot of this thread
+  const int lk = (tid % KV) * 8;  // K-vector: k offset of every slot of this thread
+  const int lr = tid / KV;        // K-vector: row of slot 0 (slot i: lr + RSK*i)
   const int vka = tid / CHA, vca = tid % CHA;  // row-vector A: k row (+RSA per slot), m chunk
   const int vkb = tid / CHB, vcb = tid % CHB;
   ARow ar[AS];
@@ -342,8 +345,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   const int Cda = (AK == A_CONV) ? p.g.C : p.g.Co;
   if (AKV) {
 #pragma unroll
-    for (int i = 0; i < AS; ++i) ar[i] = a_row<AK>(p, m0 + ((tid + 256 * i) >> 2));
-    if (AK != A_ROWK) ka = kpos_of(kt0 * TK + lk, Cda, KW);
+    for (int i = 0; i < AS; ++i) ar[i] = a_row<AK>(p, m0 + lr + RSK * i);
+    if (AK != A_ROWK) ka = kpos_of(kt0 * KB + lk, Cda, KW);
   } else {
 #pragma unroll
     for (int i = 0; i < AS; ++i) {
@@ -355,17 +358,17 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
       }
     }
     if (AK == A_WGRAD) {
-      const int k = kt0 * TK + vka;
+      const int k = kt0 * KB + vka;
       const int hw = p.g.Ho * p.g.Wo;
       const int b = k / hw, rem = k - b * hw;
       pa = PixPos{b, rem / p.g.Wo, rem - (rem / p.g.Wo) * p.g.Wo};
     }
   }
-  if (BK_ == B_DGRADW) kb = kpos_of(kt0 * TK + lk, p.g.Co, KW);
+  if (BK_ == B_DGRADW) kb = kpos_of(kt0 * KB + lk, p.g.Co, KW);
 
   bf16x8 ra[AS], rb[BS];
   auto gload = [&](int kt) {
-    const int k0 = kt * TK;
+    const int k0 = kt * KB;
     if (AKV) {
 #pragma unroll
       for (int i = 0; i < AS; ++i) ra[i] = load_a_k8<AK>(p, ar[i], ka, k0 + lk, Cda);
@@ -379,22 +382,22 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
     }
     if (BKV) {
 #pragma unroll
-      for (int i = 0; i < BS; ++i) rb[i] = load_b_k8<BK_>(p, n0 + ((tid + 256 * i) >> 2), kb, k0 + lk);
+      for (int i = 0; i < BS; ++i) rb[i] = load_b_k8<BK_>(p, n0 + lr + RSK * i, kb, k0 + lk);
     } else {
 #pragma unroll
       for (int i = 0; i < BS; ++i) rb[i] = load_b_n8(p, n0 + vcb * 8, k0 + vkb + RSB * i);
     }
     // advance the incremental decompositions to the next k-tile
-    if (AKV && AK != A_ROWK) kpos_advance(ka, TK, Cda, KW);
-    if (AK == A_WGRAD) pix_advance(pa, TK, p.g.Ho, p.g.Wo);
-    if (BK_ == B_DGRADW) kpos_advance(kb, TK, p.g.Co, KW);
+    if (AKV && AK != A_ROWK) kpos_advance(ka, KB, Cda, KW);
+    if (AK == A_WGRAD) pix_advance(pa, KB, p.g.Ho, p.g.Wo);
+    if (BK_ == B_DGRADW) kpos_advance(kb, KB, p.g.Co, KW);
   };
   auto sstore = [&](int buf) {
     bf16* a = As + buf * AIMG;
     bf16* b = Bs + buf * BIMG;
     if (AKV) {
 #pragma unroll
-      for (int i = 0; i < AS; ++i) *reinterpret_cast<bf16x8*>(a + ((tid + 256 * i) >> 2) * LDK + lk) = ra[i];
+      for (int i = 0; i < AS; ++i) *reinterpret_cast<bf16x8*>(a + (lr + RSK * i) * LDKB + lk) = ra[i];
     } else {
 #pragma unroll
       for (int i = 0; i < AS; ++i)
@@ -402,7 +405,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
     }
     if (BKV) {
 #pragma unroll
-      for (int i = 0; i < BS; ++i) *reinterpret_cast<bf16x8*>(b + ((tid + 256 * i) >> 2) * LDK + lk) = rb[i];
+      for (int i = 0; i < BS; ++i) *reinterpret_cast<bf16x8*>(b + (lr + RSK * i) * LDKB + lk) = rb[i];
     } else {
 #pragma unroll
       for (int i = 0; i < BS; ++i)
@@ -427,23 +430,26 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
       if (more) gload(kt + 1);
       const bf16* a = As + buf * AIMG;
       const bf16* b = Bs + buf * BIMG;
-      bf16x8 af[MI], bfr[NI];
 #pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int r = wm * WTM + i * 16;
-        if (AKV) af[i] = *reinterpret_cast<const bf16x8*>(a + (r + fr) * LDK + fk);
-        else af[i] = tr_frag<BM>(a, r, lane);
+      for (int kk = 0; kk < KB; kk += 32) {
+        bf16x8 af[MI], bfr[NI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int r = wm * WTM + i * 16;
+          if (AKV) af[i] = *reinterpret_cast<const bf16x8*>(a + (r + fr) * LDKB + kk + fk);
+          else af[i] = tr_frag<BM>(a, r, lane, kk);
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int c = wn * WTN + j * 16;
+          if (BKV) bfr[j] = *reinterpret_cast<const bf16x8*>(b + (c + fr) * LDKB + kk + fk);
+          else bfr[j] = tr_frag<BN>(b, c, lane, kk);
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
       }
-#pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const int c = wn * WTN + j * 16;
-        if (BKV) bfr[j] = *reinterpret_cast<const bf16x8*>(b + (c + fr) * LDK + fk);
-        else bfr[j] = tr_frag<BN>(b, c, lane);
-      }
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
       if (more) {
         sstore(buf ^ 1);
         __syncthreads();
@@ -1288,7 +1294,9 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     Geo g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9], geo[10], geo[11], geo[12]};
     p.g = g;
   }
-  const int ktiles = (K + TK - 1) / TK;
+  // K step: 64 (two MFMA k-slices per barrier) unless K is short
+  const int KB = K >= 256 ? 64 : 32;
+  const int ktiles = (K + KB - 1) / KB;
   const bool auto_splits = splits == 0;
   if (splits < 1) splits = 1;
   if (splits > ktiles) splits = ktiles > 0 ? ktiles : 1;
@@ -1331,7 +1339,7 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     if (auto_splits) {  // weight grads: f32 atomics, fill the chip with >= ~4 workgroups per CU
       const long long t = (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
       long long sp = (1024 + t - 1) / t;
-      const long long maxs = ktiles / 4 > 0 ? ktiles / 4 : 1;
+      const long long maxs = ktiles / 2 > 0 ? ktiles / 2 : 1;
       splits = (int)(sp < maxs ? sp : maxs);
       if (splits < 1) splits = 1;
       p.ktiles_per_split = (ktiles + splits - 1) / splits;
@@ -1344,7 +1352,11 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   }
   dim3 grid((M + bm - 1) / bm, (N + bn - 1) / bn, splits);
   if (grid.y > 65535 || splits > 65535) return -3;
-#define TDE_IGEMM(AK_, BK__, BM_, BN_) igemm_kernel<AK_, BK__, BM_, BN_><<<grid, 256, 0, stream>>>(p)
+#define TDE_IGEMM(AK_, BK__, BM_, BN_)                                         \
+  do {                                                                         \
+    if (KB == 64) igemm_kernel<AK_, BK__, BM_, BN_, 64><<<grid, 256, 0, stream>>>(p); \
+    else igemm_kernel<AK_, BK__, BM_, BN_, 32><<<grid, 256, 0, stream>>>(p);          \
+  } while (0)
   if (akind == A_ROWK && bkind == B_NK) {
     if (bm == 128 && bn == 128) TDE_IGEMM(A_ROWK, B_NK, 128, 128);
     else if (bm == 128) TDE_IGEMM(A_ROWK, B_NK, 128, 64);

@@ -1,0 +1,203 @@
+// Direct (VALU) convolution for narrow layers — Model B's Conv2D(1->6, 3x3), Conv2D(6->12, 6x6/2),
+// Conv2D(12->24, 6x6/2) (mnist_keras_distributed.py:83-98).
+//
+// With C_out <= 32 a 16x16 MFMA tile is mostly padding and the implicit-GEMM gathers of 1-12 channel
+// pixels are scalar, so the matrix-core path is latency-bound on index math.  Here one thread owns
+// one pixel and ALL its channels in registers (template CO/CI = channel count rounded up to 8):
+//  * fwd:   out[p][0..Co) = sum_k x[p,k] * W[k][0..Co)      (bf16 W, broadcast from LDS as f32)
+//           + the per-channel BN statistics of the stored bf16 values (wave shuffles -> LDS -> f64 atomics)
+//  * dgrad: dx[p][0..C) = sum over the taps that hit p (stride phase computed, no zero taps)
+//           of dy[o][co] * W[kh][kw][0..C)[co]
+// Weight gradients stay on the MFMA implicit GEMM (long pixel reductions suit split-K there).
+#include "tde_common.h"
+
+namespace tde {
+
+struct SGeo {
+  int B, H, W, C, Ho, Wo, Co, KH, KW, sh, sw, pt, pl;
+};
+
+constexpr int kSmallLds = 16384;  // f32 weight elements staged in LDS (64 KiB)
+
+template <int CO>
+__global__ __launch_bounds__(256) void smallconv_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w,
+                                                            const float* __restrict__ bias, int relu,
+                                                            bf16* __restrict__ y, double* __restrict__ colstats,
+                                                            SGeo g) {
+  __shared__ float ws[kSmallLds];
+  __shared__ float st[2][CO];
+  const int K = g.KH * g.KW * g.C;
+  for (int i = threadIdx.x; i < K * CO; i += blockDim.x) {
+    const int k = i / CO, co = i - k * CO;
+    ws[i] = co < g.Co ? bf2f(w[k * g.Co + co]) : 0.f;
+  }
+  if (threadIdx.x < 2 * CO) (&st[0][0])[threadIdx.x] = 0.f;
+  __syncthreads();
+  const int npix = g.B * g.Ho * g.Wo;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  float acc[CO];
+#pragma unroll
+  for (int c = 0; c < CO; ++c) acc[c] = 0.f;
+  const bool ok = p < npix;
+  if (ok) {
+    const int hw = g.Ho * g.Wo;
+    const int b = p / hw, r = p - b * hw;
+    const int oh = r / g.Wo, ow = r - oh * g.Wo;
+    const int y0 = oh * g.sh - g.pt, x0 = ow * g.sw - g.pl;
+    for (int kh = 0; kh < g.KH; ++kh) {
+      const int ih = y0 + kh;
+      if ((unsigned)ih >= (unsigned)g.H) continue;
+      for (int kw = 0; kw < g.KW; ++kw) {
+        const int iw = x0 + kw;
+        if ((unsigned)iw >= (unsigned)g.W) continue;
+        const bf16* xp = x + (((long long)b * g.H + ih) * g.W + iw) * g.C;
+        const float* wp = ws + ((kh * g.KW + kw) * g.C) * CO;
+        for (int ci = 0; ci < g.C; ++ci) {
+          const float xv = bf2f(xp[ci]);
+#pragma unroll
+          for (int c = 0; c < CO; ++c) acc[c] = fmaf(xv, wp[ci * CO + c], acc[c]);
+        }
+      }
+    }
+  }
+  float s1[CO], s2[CO];
+#pragma unroll
+  for (int c = 0; c < CO; ++c) {
+    float v = acc[c] + ((bias && c < g.Co) ? bias[c] : 0.f);
+    const float q = bf2f(f2bf(v));
+    s1[c] = ok ? q : 0.f;
+    s2[c] = ok ? q * q : 0.f;
+    if (relu) v = fmaxf(v, 0.f);
+    acc[c] = v;
+  }
+  if (ok) {
+    bf16* yp = y + (long long)p * g.Co;
+    if (g.Co == CO && (CO % 8) == 0) {
+#pragma unroll
+      for (int c = 0; c < CO; c += 8) {
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[c + j]);
+        *reinterpret_cast<bf16x8*>(yp + c) = o;
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < CO; ++c)
+        if (c < g.Co) yp[c] = f2bf(acc[c]);
+    }
+  }
+  if (!colstats) return;
+#pragma unroll
+  for (int c = 0; c < CO; ++c) {
+    const float a = wave_sum(s1[c]), b2 = wave_sum(s2[c]);
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(&st[0][c], a);
+      atomicAdd(&st[1][c], b2);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < g.Co) {
+    atomicAdd(&colstats[threadIdx.x], (double)st[0][threadIdx.x]);
+    atomicAdd(&colstats[g.Co + threadIdx.x], (double)st[1][threadIdx.x]);
+  }
+}
+
+template <int CI>
+__global__ __launch_bounds__(256) void smallconv_dgrad_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ w,
+                                                              bf16* __restrict__ dx, int accum, SGeo g) {
+  __shared__ float ws[kSmallLds];  // [kh][kw][co][ci] so the inner ci loop reads a broadcast row
+  const int taps = g.KH * g.KW;
+  for (int i = threadIdx.x; i < taps * g.Co * CI; i += blockDim.x) {
+    const int ci = i % CI;
+    const int t = i / CI;
+    const int co = t % g.Co, tap = t / g.Co;
+    ws[i] = ci < g.C ? bf2f(w[(tap * g.C + ci) * g.Co + co]) : 0.f;
+  }
+  __syncthreads();
+  const int npix = g.B * g.H * g.W;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npix) return;
+  const int hw = g.H * g.W;
+  const int b = p / hw, r = p - b * hw;
+  const int ih = r / g.W, iw = r - ih * g.W;
+  float acc[CI];
+#pragma unroll
+  for (int c = 0; c < CI; ++c) acc[c] = 0.f;
+  const int ty = ih + g.pt, tx = iw + g.pl;
+  // taps with (ty - kh) % sh == 0: start at the matching phase, step by the stride
+  for (int kh = ty % g.sh; kh < g.KH; kh += g.sh) {
+    const int oh = (ty - kh) / g.sh;
+    if (ty - kh < 0 || oh >= g.Ho) continue;
+    for (int kw = tx % g.sw; kw < g.KW; kw += g.sw) {
+      const int ow = (tx - kw) / g.sw;
+      if (tx - kw < 0 || ow >= g.Wo) continue;
+      const bf16* dp = dy + (((long long)b * g.Ho + oh) * g.Wo + ow) * g.Co;
+      const float* wp = ws + (kh * g.KW + kw) * g.Co * CI;
+      for (int co = 0; co < g.Co; ++co) {
+        const float gv = bf2f(dp[co]);
+#pragma unroll
+        for (int c = 0; c < CI; ++c) acc[c] = fmaf(gv, wp[co * CI + c], acc[c]);
+      }
+    }
+  }
+  bf16* xp = dx + (long long)p * g.C;
+#pragma unroll
+  for (int c = 0; c < CI; ++c) {
+    if (c >= g.C) break;
+    float v = acc[c];
+    if (accum) v += bf2f(xp[c]);
+    xp[c] = f2bf(v);
+  }
+}
+
+}  // namespace tde
+
+using namespace tde;
+
+static SGeo sgeo(const int* geo) {
+  return SGeo{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9], geo[10], geo[11], geo[12]};
+}
+
+static int round8(int c) { return (c + 7) / 8 * 8; }
+
+// w: bf16 HWIO weight shadow (what the MFMA path reads too), widened to f32 in LDS
+TDE_API int tde_smallconv_fwd(const bf16* x, const bf16* w, const float* bias, int relu, bf16* y, double* colstats,
+                              const int* geo, hipStream_t stream) {
+  const SGeo g = sgeo(geo);
+  const int co = round8(g.Co);
+  if (co > 32 || g.KH * g.KW * g.C * co > kSmallLds) return -1;
+  if ((long long)g.B * g.H * g.W * g.C >= (1LL << 31) || (long long)g.B * g.Ho * g.Wo * g.Co >= (1LL << 31)) return -4;
+  const int npix = g.B * g.Ho * g.Wo;
+  const int grid = (npix + 255) / 256;
+  switch (co) {
+    case 8: smallconv_fwd_kernel<8><<<grid, 256, 0, stream>>>(x, w, bias, relu, y, colstats, g); break;
+    case 16: smallconv_fwd_kernel<16><<<grid, 256, 0, stream>>>(x, w, bias, relu, y, colstats, g); break;
+    case 24: smallconv_fwd_kernel<24><<<grid, 256, 0, stream>>>(x, w, bias, relu, y, colstats, g); break;
+    default: smallconv_fwd_kernel<32><<<grid, 256, 0, stream>>>(x, w, bias, relu, y, colstats, g); break;
+  }
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+TDE_API int tde_smallconv_dgrad(const bf16* dy, const bf16* w, bf16* dx, int accum, const int* geo,
+                                hipStream_t stream) {
+  const SGeo g = sgeo(geo);
+  const int ci = round8(g.C);
+  if (ci > 32 || g.KH * g.KW * g.Co * ci > kSmallLds) return -1;
+  if ((long long)g.B * g.H * g.W * g.C >= (1LL << 31) || (long long)g.B * g.Ho * g.Wo * g.Co >= (1LL << 31)) return -4;
+  const int npix = g.B * g.H * g.W;
+  const int grid = (npix + 255) / 256;
+  switch (ci) {
+    case 8: smallconv_dgrad_kernel<8><<<grid, 256, 0, stream>>>(dy, w, dx, accum, g); break;
+    case 16: smallconv_dgrad_kernel<16><<<grid, 256, 0, stream>>>(dy, w, dx, accum, g); break;
+    case 24: smallconv_dgrad_kernel<24><<<grid, 256, 0, stream>>>(dy, w, dx, accum, g); break;
+    default: smallconv_dgrad_kernel<32><<<grid, 256, 0, stream>>>(dy, w, dx, accum, g); break;
+  }
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+TDE_API int tde_smallconv_ok(int C, int Co, int KH, int KW, int dgrad) {
+  if (dgrad) return round8(C) <= 32 && KH * KW * Co * round8(C) <= kSmallLds;
+  return round8(Co) <= 32 && KH * KW * C * round8(Co) <= kSmallLds;
+}

@@ -55,6 +55,9 @@ _HIP_PROTOS = {
     "tde_xent": (i32, [p, i64, p, i32, i32, f32, p, i64, p, p, i32, p, p]),
     "tde_colstats": (i32, [p, i64, i32, p, p]),
     "tde_cast_f32_bf16": (i32, [p, p, i64, p]),
+    "tde_smallconv_fwd": (i32, [p, p, p, i32, p, p, p, p]),
+    "tde_smallconv_dgrad": (i32, [p, p, p, i32, p, p]),
+    "tde_smallconv_ok": (i32, [i32, i32, i32, i32, i32]),
     # RCCL
     "tde_nccl_version": (i32, []),
     "tde_nccl_error_string": (C.c_char_p, [i32]),

@@ -135,6 +135,34 @@ def conv_dgrad(dy, Wrow, dx, g: ConvGeom, accum=False, scratch=None):
            cb_accum=accum, scratch=scratch)
 
 
+# ---------------------------------------------------------------- narrow convolutions (direct, VALU)
+def smallconv_ok(g: ConvGeom, dgrad=False):
+    return bool(N.hip().tde_smallconv_ok(g.C, g.Co, g.KH, g.KW, int(dgrad)))
+
+
+def smallconv_fwd(x, Wrow, y, g: ConvGeom, bias=None, relu=False, colstats=None):
+    """Direct convolution for C_out <= 32: one thread per output pixel, all channels in registers."""
+    _bf(x, g.B * g.H * g.W * g.C, "smallconv_fwd x")
+    _bf(Wrow, g.K * g.Co, "smallconv_fwd W")
+    _bf(y, g.B * g.Ho * g.Wo * g.Co, "smallconv_fwd y")
+    if bias is not None:
+        _f32(bias, g.Co, "smallconv_fwd bias")
+    if colstats is not None:
+        _f64(colstats, 2 * g.Co, "smallconv_fwd colstats")
+    _req(smallconv_ok(g), "smallconv_fwd: layer too wide for the direct kernel")
+    N.check(N.hip().tde_smallconv_fwd(_P(x), _P(Wrow), _P(bias), int(relu), _P(y), _P(colstats), g.carray(), _s()),
+            "tde_smallconv_fwd")
+
+
+def smallconv_dgrad(dy, Wrow, dx, g: ConvGeom, accum=False):
+    """Direct input-gradient for C_in <= 32 (only the taps of each pixel's stride phase)."""
+    _bf(dy, g.B * g.Ho * g.Wo * g.Co, "smallconv_dgrad dy")
+    _bf(Wrow, g.K * g.Co, "smallconv_dgrad W")
+    _bf(dx, g.B * g.H * g.W * g.C, "smallconv_dgrad dx")
+    _req(smallconv_ok(g, True), "smallconv_dgrad: layer too wide for the direct kernel")
+    N.check(N.hip().tde_smallconv_dgrad(_P(dy), _P(Wrow), _P(dx), int(accum), g.carray(), _s()), "tde_smallconv_dgrad")
+
+
 def conv_wgrad(x, dy, dW, g: ConvGeom, splits=None):
     """dW[KH,KW,C,Co] (f32) += sum_pixels x (x) dy."""
     _bf(x, g.B * g.H * g.W * g.C, "conv_wgrad x")

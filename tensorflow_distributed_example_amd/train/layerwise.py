@@ -24,6 +24,8 @@ bf16 weight shadows the GEMMs read.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -322,12 +324,19 @@ class _Gemm(_Stage):
         need_dgrad = tin.root().id != 0
         self.need_dgrad = need_dgrad
         self.shadows = {self.wname: ("row", "col") if need_dgrad else ("col",)}
+        self.small_fwd = self.small_dgrad = False
         if self.conv:
             H, W_, C = tin.shape
             Ho, Wo, Co = tout.shape
             (pt, _), (pl, _) = layer.pads(tin.shape)
             self.geo = O.ConvGeom(plan.B, H, W_, C, Ho, Wo, Co, layer.kernel_size[0], layer.kernel_size[1],
                                   layer.strides[0], layer.strides[1], pt, pl)
+            # narrow layers (C_out / C_in <= 32, e.g. Model B) take the direct VALU kernels
+            narrow = os.environ.get("TDE_SMALLCONV", "1") != "0"
+            self.small_fwd = narrow and Co <= 32 and O.smallconv_ok(self.geo)
+            self.small_dgrad = narrow and need_dgrad and C <= 32 and O.smallconv_ok(self.geo, True)
+            if self.small_fwd:
+                self.shadows = {self.wname: ("row", "col")}
         self.colstats = None
         self.dz = None
 
@@ -354,7 +363,10 @@ class _Gemm(_Stage):
 
     def fwd(self, p, B, training, mode="train"):
         cs = self.colstats if (self.stats and training) else None
-        if self.conv:
+        if self.conv and self.small_fwd:
+            O.smallconv_fwd(self.inp.buf, self.Wrow, self.out.root().buf, self.geo.with_batch(B), bias=self.b,
+                            relu=self.relu, colstats=cs)
+        elif self.conv:
             O.conv_fwd(self.inp.buf, self.Wt, self.out.root().buf, self.geo.with_batch(B), bias=self.b,
                        relu=self.relu, colstats=cs, scratch=p.scratch)
         else:
@@ -371,7 +383,9 @@ class _Gemm(_Stage):
         if self.conv:
             g = self.geo.with_batch(B)
             O.conv_wgrad(self.inp.buf, dout, self.gW, g)
-            if self.need_dgrad:
+            if self.need_dgrad and self.small_dgrad:
+                O.smallconv_dgrad(dout, self.Wrow, self.inp.root().grad, g, accum=self.accum[self.inp.root().id])
+            elif self.need_dgrad:
                 O.conv_dgrad(dout, self.Wrow, self.inp.root().grad, g, accum=self.accum[self.inp.root().id],
                              scratch=p.scratch)
         else:

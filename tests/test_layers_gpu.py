@@ -403,3 +403,36 @@ def test_split_k_epilogue_matches_single_pass(monkeypatch, relu, accum):
     assert _rel(y2.float(), y1.float()) < 1e-2
     assert _rel(s2, s1) < 1e-4
     assert scratch.abs().max().item() == 0.0      # finalize re-zeroed it
+
+
+@pytest.mark.parametrize("B,H,W,C,Co,k,s,pad", [c for c in CONV_CASES if c[4] <= 32])
+def test_smallconv_direct_kernels(B, H, W, C, Co, k, s, pad):
+    """Direct VALU conv (narrow layers) vs the torch fp32 reference: forward (+bias, ReLU, BN stats) and dgrad."""
+    from tensorflow_distributed_example_amd.ops import layer_ops as O
+    if pad == "same":
+        (pt, pb), (pl, pr) = _tf_same(H, k, s), _tf_same(W, k, s)
+        Ho, Wo = -(-H // s), -(-W // s)
+    else:
+        pt = pb = pl = pr = 0
+        Ho, Wo = (H - k) // s + 1, (W - k) // s + 1
+    g = O.ConvGeom(B, H, W, C, Ho, Wo, Co, k, k, s, s, pt, pl)
+    if not O.smallconv_ok(g):
+        pytest.skip("too wide for the direct kernel")
+    x = _r(B, H, W, C, seed=31)
+    w = _r(k, k, C, Co, seed=32, scale=0.2)
+    bias = torch.randn(Co, device=DEV)
+    y = torch.zeros(B, Ho, Wo, Co, dtype=bf, device=DEV)
+    st = torch.zeros(2 * Co, dtype=torch.float64, device=DEV)
+    O.smallconv_fwd(x, w.contiguous(), y, g, bias=bias, relu=False, colstats=st)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    ref = F.conv2d(F.pad(xr, (pl, pr, pt, pb)), w.float().permute(3, 2, 0, 1), bias, stride=s).permute(0, 2, 3, 1)
+    dy = _r(B, Ho, Wo, Co, seed=33)
+    ref.backward(dy.float())
+    dx = torch.zeros(B, H, W, C, dtype=bf, device=DEV)
+    O.smallconv_dgrad(dy, w.contiguous(), dx, g)
+    torch.cuda.synchronize()
+    rs = ref.detach().to(bf).double()
+    assert _rel(y.float(), ref) < 1e-2
+    assert (st[:Co] - rs.sum((0, 1, 2))).abs().max().item() <= 1e-4 * rs.abs().sum((0, 1, 2)).max().item() + 1e-3
+    assert _rel(st[Co:], (rs ** 2).sum((0, 1, 2))) < 1e-3
+    assert _rel(dx.float(), xr.grad.permute(0, 2, 3, 1)) < 1e-2
