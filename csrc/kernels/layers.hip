@@ -63,6 +63,9 @@ struct IGemmArgs {
   const float* bias;
   int relu;
   double* colstats;  // [2][N] sum / sum of squares of the STORED (bf16-rounded) values
+  // strided-conv dgrad, one stride phase (ih % sh, iw % sw) per launch: rows are that phase's
+  // pixels and K runs over only the taps kh = kh0 + i*sh, kw = kw0 + j*sw that reach them
+  int ph_on, ph_h, ph_w, Hp, Wp, kh0, kw0, KHp, KWp;
 };
 
 constexpr int TK = 32;  // MFMA k-slice
@@ -153,12 +156,19 @@ __device__ __forceinline__ ARow a_row(const IGemmArgs& p, int m) {
     r.y0 = oh * p.g.sh - p.g.pt;
     r.x0 = ow * p.g.sw - p.g.pl;
     r.base = (long long)b * p.g.H * p.g.W;
-  } else {  // A_DGRAD: m over input pixels, gathers dY
+  } else if (!p.ph_on) {  // A_DGRAD: m over input pixels, gathers dY
     const int hw = p.g.H * p.g.W;
     const int b = mm / hw, rem = mm - b * hw;
     const int ih = rem / p.g.W, iw = rem - ih * p.g.W;
     r.y0 = ih + p.g.pt;
     r.x0 = iw + p.g.pl;
+    r.base = (long long)b * p.g.Ho * p.g.Wo;
+  } else {  // A_DGRAD, one stride phase: y0/x0 = the output row/col hit by tap (kh0, kw0)
+    const int hw = p.Hp * p.Wp;
+    const int b = mm / hw, rem = mm - b * hw;
+    const int ihp = rem / p.Wp, iwp = rem - ihp * p.Wp;
+    r.y0 = (ihp * p.g.sh + p.ph_h + p.g.pt - p.kh0) / p.g.sh;
+    r.x0 = (iwp * p.g.sw + p.ph_w + p.g.pl - p.kw0) / p.g.sw;
     r.base = (long long)b * p.g.Ho * p.g.Wo;
   }
   return r;
@@ -172,6 +182,11 @@ __device__ __forceinline__ long long a_idx(const IGemmArgs& p, const ARow& r, co
     const int ih = r.y0 + s.kh, iw = r.x0 + s.kw;
     if ((unsigned)ih >= (unsigned)p.g.H || (unsigned)iw >= (unsigned)p.g.W) return -1;
     return (r.base + (long long)ih * p.g.W + iw) * p.g.C + s.c;
+  }
+  if (p.ph_on) {  // phased: tap (kh0 + kh'*sh) reaches output row y0 - kh' exactly
+    const int oh = r.y0 - s.kh, ow = r.x0 - s.kw;
+    if ((unsigned)oh >= (unsigned)p.g.Ho || (unsigned)ow >= (unsigned)p.g.Wo) return -1;
+    return (r.base + (long long)oh * p.g.Wo + ow) * p.g.Co + s.c;
   }
   // A_DGRAD: oh = (ih + pt - kh) / sh must be exact and in range
   int oh = r.y0 - s.kh, ow = r.x0 - s.kw;
@@ -215,6 +230,8 @@ template <int BK_>
 __device__ __forceinline__ long long b_idx_k(const IGemmArgs& p, int n, const KPos& s, int k) {
   if (BK_ == B_NK) return (long long)n * p.ldb + k;
   // B_DGRADW: k = (kh,kw,co), n = ci  ->  W[kh][kw][ci][co]
+  if (p.ph_on)
+    return ((long long)((p.kh0 + s.kh * p.g.sh) * p.g.KW + p.kw0 + s.kw * p.g.sw) * p.g.C + n) * p.g.Co + s.c;
   return ((long long)(s.kh * p.g.KW + s.kw) * p.g.C + n) * p.g.Co + s.c;
 }
 
@@ -230,7 +247,7 @@ __device__ __forceinline__ bf16x8 load_b_k8(const IGemmArgs& p, int n, const KPo
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     v[j] = (k + j < p.K) ? p.b[b_idx_k<BK_>(p, n, t, k + j)] : (bf16)0.0f;
-    if (BK_ == B_DGRADW) kpos_advance(t, 1, p.g.Co, p.g.KW);
+    if (BK_ == B_DGRADW) kpos_advance(t, 1, p.g.Co, p.ph_on ? p.KWp : p.g.KW);
   }
   return v;
 }
@@ -341,7 +358,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   WRow wr[AS];
   KPos ka{0, 0, 0}, kb{0, 0, 0};
   PixPos pa{0, 0, 0};
-  const int KW = p.g.KW;
+  const int KW = (AK == A_DGRAD && p.ph_on) ? p.KWp : p.g.KW;  // taps per kernel row of this K
   const int Cda = (AK == A_CONV) ? p.g.C : p.g.Co;
   if (AKV) {
 #pragma unroll
@@ -469,8 +486,15 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
     for (int i = 0; i < MI; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
-        if (!cok || row >= p.M) continue;
+        const int mrow = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+        if (!cok || mrow >= p.M) continue;
+        int row = mrow;
+        if (AK == A_DGRAD && p.ph_on) {  // phase row -> input pixel
+          const int hw = p.Hp * p.Wp;
+          const int b = mrow / hw, rem = mrow - b * hw;
+          const int ihp = rem / p.Wp, iwp = rem - ihp * p.Wp;
+          row = (b * p.g.H + ihp * p.g.sh + p.ph_h) * p.g.W + iwp * p.g.sw + p.ph_w;
+        }
         float v = p.alpha * acc[i][j][r] + bv;
         if (p.colstats) {
           // statistics of exactly the tensor BN will normalise (the bf16 activation)
@@ -1265,14 +1289,15 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(float* __restrict__ 
 TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, long long ldb, int bkind, int M, int N,
                       int K, const int* geo, int splits, float* cf, long long ldc, int cf_mode, float alpha, bf16* cb,
                       long long ldcb, int cb_accum, const float* bias, int relu, double* colstats, float* scratch,
-                      hipStream_t stream) {
+                      const int* phase, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
+  if (phase && (akind != A_DGRAD || splits > 1 || colstats)) return -5;
   const bool fused_epi = cb || colstats || bias || relu || cf_mode == 1;
   if (splits > 1 && fused_epi) {
     // split-K into the zeroed f32 scratch, then the epilogue pass
     if (!scratch || (colstats && N > kMaxCB)) return -2;
     int rc = tde_igemm(a, lda, akind, b, ldb, bkind, M, N, K, geo, splits, scratch, N, 2, 1.f, nullptr, 0, 0,
-                       nullptr, 0, nullptr, nullptr, stream);
+                       nullptr, 0, nullptr, nullptr, nullptr, stream);
     if (rc) return rc;
     const long long n = (long long)M * N;
     int g = (int)((n + 255) / 256);
@@ -1293,6 +1318,17 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   if (geo) {
     Geo g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9], geo[10], geo[11], geo[12]};
     p.g = g;
+  }
+  if (phase) {
+    p.ph_on = 1;
+    p.ph_h = phase[0];
+    p.ph_w = phase[1];
+    p.Hp = phase[2];
+    p.Wp = phase[3];
+    p.kh0 = phase[4];
+    p.kw0 = phase[5];
+    p.KHp = phase[6];
+    p.KWp = phase[7];
   }
   // K step: 64 (two MFMA k-slices per barrier) unless K is short
   const int KB = K >= 256 ? 64 : 32;
@@ -1413,10 +1449,10 @@ TDE_API int tde_bn_bwd(const bf16* dout, const bf16* y, const bf16* res, long lo
   if (R * C >= (1LL << 31)) return -4;
   const int g = grid_for(R * C, 8);
   if (mode == 1) {
-    // Reduction grid: <= 2 blocks per CU (each block ends with 2*C global atomics, so more blocks only
+    // Reduction grid: <= 8 blocks per CU (each block ends with 2*C global atomics, so more blocks only
     // add contention), rounded to a multiple of C / gcd(2048, C) so the grid stride is a multiple of C
     // and every thread accumulates fixed channels in registers.
-    int gr = g < 512 ? g : 512;
+    int gr = g < 2048 ? g : 2048;
     int gc = C, t = 2048;
     while (t) {
       const int r = gc % t;

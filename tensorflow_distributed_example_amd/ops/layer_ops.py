@@ -93,14 +93,33 @@ def scratch_elems(M, N_, K):
 
 
 def _igemm(a, lda, ak, b, ldb, bk, M, N_, K, geo=None, splits=1, cf=None, ldc=0, cf_mode=0, alpha=1.0,
-           cb=None, ldcb=0, cb_accum=False, bias=None, relu=False, colstats=None, scratch=None):
+           cb=None, ldcb=0, cb_accum=False, bias=None, relu=False, colstats=None, scratch=None, phase=None):
     g = geo.carray() if geo is not None else None
     if splits > 1 and scratch is not None:
         _f32(scratch, M * N_, "igemm split-K scratch")
+    ph = (C.c_int * 8)(*phase) if phase is not None else None
     rc = N.hip().tde_igemm(_P(a), int(lda), ak, _P(b), int(ldb), bk, int(M), int(N_), int(K), g, int(splits),
                            _P(cf), int(ldc), int(cf_mode), float(alpha), _P(cb), int(ldcb), int(cb_accum), _P(bias),
-                           int(relu), _P(colstats), _P(scratch), _s())
+                           int(relu), _P(colstats), _P(scratch), ph, _s())
     N.check(rc, "tde_igemm")
+
+
+def dgrad_phases(g: ConvGeom):
+    """Stride phases of a strided conv's input gradient: (ph_h, ph_w, Hp, Wp, kh0, kw0, KHp, KWp) per phase —
+    the phase's pixel grid and the only taps that reach it (the other (s^2-1)/s^2 of the implicit-GEMM K
+    would multiply zeros)."""
+    out = []
+    for ph in range(g.sh):
+        Hp = -(-(g.H - ph) // g.sh) if g.H > ph else 0
+        kh0 = (ph + g.pt) % g.sh
+        KHp = -(-(g.KH - kh0) // g.sh) if g.KH > kh0 else 0
+        for pw in range(g.sw):
+            Wp = -(-(g.W - pw) // g.sw) if g.W > pw else 0
+            kw0 = (pw + g.pl) % g.sw
+            KWp = -(-(g.KW - kw0) // g.sw) if g.KW > kw0 else 0
+            if Hp and Wp:
+                out.append((ph, pw, Hp, Wp, kh0, kw0, KHp, KWp))
+    return out
 
 
 def _fs(M, N_, K, scratch):
@@ -130,6 +149,11 @@ def conv_dgrad(dy, Wrow, dx, g: ConvGeom, accum=False, scratch=None):
     _bf(dy, g.B * g.Ho * g.Wo * g.Co, "conv_dgrad dy")
     _bf(Wrow, g.K * g.Co, "conv_dgrad W")
     _bf(dx, g.B * g.H * g.W * g.C, "conv_dgrad dx")
+    if g.sh > 1 or g.sw > 1:
+        for ph in dgrad_phases(g):
+            _igemm(dy, 0, A_DGRAD, Wrow, 0, B_DGRADW, g.B * ph[2] * ph[3], g.C, ph[6] * ph[7] * g.Co, g,
+                   cb=dx, ldcb=g.C, cb_accum=accum, phase=ph)
+        return
     M, K = g.B * g.H * g.W, g.KH * g.KW * g.Co
     _igemm(dy, 0, A_DGRAD, Wrow, 0, B_DGRADW, M, g.C, K, g, splits=_fs(M, g.C, K, scratch), cb=dx, ldcb=g.C,
            cb_accum=accum, scratch=scratch)

@@ -332,9 +332,16 @@ class _Gemm(_Stage):
             self.geo = O.ConvGeom(plan.B, H, W_, C, Ho, Wo, Co, layer.kernel_size[0], layer.kernel_size[1],
                                   layer.strides[0], layer.strides[1], pt, pl)
             # narrow layers (C_out / C_in <= 32, e.g. Model B) take the direct VALU kernels
+            # (per-thread FMA count bounds: above ~1k a thread's serial chain loses to the MFMA GEMM)
             narrow = os.environ.get("TDE_SMALLCONV", "1") != "0"
-            self.small_fwd = narrow and Co <= 32 and O.smallconv_ok(self.geo)
-            self.small_dgrad = narrow and need_dgrad and C <= 32 and O.smallconv_ok(self.geo, True)
+            r8 = lambda c: -(-c // 8) * 8  # noqa: E731
+            kh, kw = layer.kernel_size
+            sh, sw = layer.strides
+            fwd_work = kh * kw * C * r8(Co)
+            dgrad_work = -(-kh // sh) * -(-kw // sw) * Co * r8(C)
+            self.small_fwd = narrow and Co <= 32 and fwd_work <= 1024 and O.smallconv_ok(self.geo)
+            self.small_dgrad = (narrow and need_dgrad and C <= 32 and dgrad_work <= 1024
+                                and O.smallconv_ok(self.geo, True))
             if self.small_fwd:
                 self.shadows = {self.wname: ("row", "col")}
         self.colstats = None
