@@ -205,10 +205,10 @@ __device__ __forceinline__ long long a_idx(const IGemmArgs& p, const ARow& r, co
   return (r.base + (long long)oh * p.g.Wo + ow) * p.g.Co + s.c;
 }
 
-template <int AK>
+template <int AK, int VEC>
 __device__ __forceinline__ bf16x8 load_a_k8(const IGemmArgs& p, const ARow& r, const KPos& s, int k, int Cd) {
   if (!r.ok) return zero8();
-  if (p.avec) {  // 8 consecutive k share (kh, kw): one 16-byte load
+  if (VEC || p.avec) {  // 8 consecutive k share (kh, kw): one 16-byte load
     if (k >= p.K) return zero8();
     const long long i = a_idx<AK>(p, r, s, k);
     if (i < 0) return zero8();
@@ -220,7 +220,7 @@ __device__ __forceinline__ bf16x8 load_a_k8(const IGemmArgs& p, const ARow& r, c
   for (int j = 0; j < 8; ++j) {
     const long long i = (k + j < p.K) ? a_idx<AK>(p, r, t, k + j) : -1;
     v[j] = i < 0 ? (bf16)0.0f : p.a[i];
-    if (AK != A_ROWK) kpos_advance(t, 1, Cd, p.g.KW);
+    if (AK != A_ROWK) kpos_advance(t, 1, Cd, (AK == A_DGRAD && p.ph_on) ? p.KWp : p.g.KW);
   }
   return v;
 }
@@ -235,10 +235,10 @@ __device__ __forceinline__ long long b_idx_k(const IGemmArgs& p, int n, const KP
   return ((long long)(s.kh * p.g.KW + s.kw) * p.g.C + n) * p.g.Co + s.c;
 }
 
-template <int BK_>
+template <int BK_, int VEC>
 __device__ __forceinline__ bf16x8 load_b_k8(const IGemmArgs& p, int n, const KPos& s, int k) {
   if (n >= p.N) return zero8();
-  if (p.bvec) {
+  if (VEC || p.bvec) {
     if (k >= p.K) return zero8();
     return *reinterpret_cast<const bf16x8*>(p.b + b_idx_k<BK_>(p, n, s, k));
   }
@@ -279,18 +279,18 @@ __device__ __forceinline__ long long wgrad_idx(const IGemmArgs& p, int kh, int k
   return (((long long)q.b * p.g.H + ih) * p.g.W + iw) * p.g.C + ci;
 }
 
-template <int AK>
+template <int AK, int VEC>
 __device__ __forceinline__ bf16x8 load_a_m8(const IGemmArgs& p, int m, const WRow& w, const PixPos& q, int k) {
   if (k >= p.K || m >= p.M) return zero8();
   if (AK == A_COLM) {
     const long long i = (long long)k * p.lda + m;
-    if (p.avec) return *reinterpret_cast<const bf16x8*>(p.a + i);
+    if (VEC || p.avec) return *reinterpret_cast<const bf16x8*>(p.a + i);
     bf16x8 v;
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = (m + j < p.M) ? p.a[i + j] : (bf16)0.0f;
     return v;
   }
-  if (p.avec) {  // C % 8 == 0: the 8 rows are ci..ci+7 of one (kh, kw)
+  if (VEC || p.avec) {  // C % 8 == 0: the 8 rows are ci..ci+7 of one (kh, kw)
     const long long i = wgrad_idx(p, w.kh, w.kw, w.ci, q);
     if (i < 0) return zero8();
     return *reinterpret_cast<const bf16x8*>(p.a + i);
@@ -313,18 +313,21 @@ __device__ __forceinline__ bf16x8 load_a_m8(const IGemmArgs& p, int m, const WRo
   return v;
 }
 
+template <int VEC>
 __device__ __forceinline__ bf16x8 load_b_n8(const IGemmArgs& p, int n, int k) {
   // B_KN: B(k, n) = b[k*ldb + n]
   if (k >= p.K || n >= p.N) return zero8();
   const long long i = (long long)k * p.ldb + n;
-  if (p.bvec) return *reinterpret_cast<const bf16x8*>(p.b + i);
+  if (VEC || p.bvec) return *reinterpret_cast<const bf16x8*>(p.b + i);
   bf16x8 v;
 #pragma unroll
   for (int j = 0; j < 8; ++j) v[j] = (n + j < p.N) ? p.b[i + j] : (bf16)0.0f;
   return v;
 }
 
-template <int AK, int BK_, int BM, int BN, int KB>
+// VEC = 1: both operands are 16-byte gatherable (channel counts % 8 == 0, aligned) — the scalar
+// fallbacks are compiled out of the hot loop.
+template <int AK, int BK_, int BM, int BN, int KB, int VEC>
 __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   constexpr bool AKV = (AK == A_ROWK || AK == A_CONV || AK == A_DGRAD);  // K-vector A
   constexpr bool BKV = (BK_ == B_NK || BK_ == B_DGRADW);                 // K-vector B
@@ -388,21 +391,21 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
     const int k0 = kt * KB;
     if (AKV) {
 #pragma unroll
-      for (int i = 0; i < AS; ++i) ra[i] = load_a_k8<AK>(p, ar[i], ka, k0 + lk, Cda);
+      for (int i = 0; i < AS; ++i) ra[i] = load_a_k8<AK, VEC>(p, ar[i], ka, k0 + lk, Cda);
     } else {
 #pragma unroll
       for (int i = 0; i < AS; ++i) {
         PixPos q = pa;
         if (AK == A_WGRAD && i) pix_advance(q, RSA * i, p.g.Ho, p.g.Wo);
-        ra[i] = load_a_m8<AK>(p, m0 + vca * 8, wr[i], q, k0 + vka + RSA * i);
+        ra[i] = load_a_m8<AK, VEC>(p, m0 + vca * 8, wr[i], q, k0 + vka + RSA * i);
       }
     }
     if (BKV) {
 #pragma unroll
-      for (int i = 0; i < BS; ++i) rb[i] = load_b_k8<BK_>(p, n0 + lr + RSK * i, kb, k0 + lk);
+      for (int i = 0; i < BS; ++i) rb[i] = load_b_k8<BK_, VEC>(p, n0 + lr + RSK * i, kb, k0 + lk);
     } else {
 #pragma unroll
-      for (int i = 0; i < BS; ++i) rb[i] = load_b_n8(p, n0 + vcb * 8, k0 + vkb + RSB * i);
+      for (int i = 0; i < BS; ++i) rb[i] = load_b_n8<VEC>(p, n0 + vcb * 8, k0 + vkb + RSB * i);
     }
     // advance the incremental decompositions to the next k-tile
     if (AKV && AK != A_ROWK) kpos_advance(ka, KB, Cda, KW);
@@ -1388,10 +1391,16 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   }
   dim3 grid((M + bm - 1) / bm, (N + bn - 1) / bn, splits);
   if (grid.y > 65535 || splits > 65535) return -3;
-#define TDE_IGEMM(AK_, BK__, BM_, BN_)                                         \
-  do {                                                                         \
-    if (KB == 64) igemm_kernel<AK_, BK__, BM_, BN_, 64><<<grid, 256, 0, stream>>>(p); \
-    else igemm_kernel<AK_, BK__, BM_, BN_, 32><<<grid, 256, 0, stream>>>(p);          \
+  const bool vec = p.avec && p.bvec;
+#define TDE_IGEMM(AK_, BK__, BM_, BN_)                                                   \
+  do {                                                                                   \
+    if (vec) {                                                                           \
+      if (KB == 64) igemm_kernel<AK_, BK__, BM_, BN_, 64, 1><<<grid, 256, 0, stream>>>(p); \
+      else igemm_kernel<AK_, BK__, BM_, BN_, 32, 1><<<grid, 256, 0, stream>>>(p);          \
+    } else {                                                                             \
+      if (KB == 64) igemm_kernel<AK_, BK__, BM_, BN_, 64, 0><<<grid, 256, 0, stream>>>(p); \
+      else igemm_kernel<AK_, BK__, BM_, BN_, 32, 0><<<grid, 256, 0, stream>>>(p);          \
+    }                                                                                    \
   } while (0)
   if (akind == A_ROWK && bkind == B_NK) {
     if (bm == 128 && bn == 128) TDE_IGEMM(A_ROWK, B_NK, 128, 128);
@@ -1449,10 +1458,10 @@ TDE_API int tde_bn_bwd(const bf16* dout, const bf16* y, const bf16* res, long lo
   if (R * C >= (1LL << 31)) return -4;
   const int g = grid_for(R * C, 8);
   if (mode == 1) {
-    // Reduction grid: <= 8 blocks per CU (each block ends with 2*C global atomics, so more blocks only
+    // Reduction grid: <= 2 blocks per CU (each block ends with 2*C global atomics, so more blocks only
     // add contention), rounded to a multiple of C / gcd(2048, C) so the grid stride is a multiple of C
     // and every thread accumulates fixed channels in registers.
-    int gr = g < 2048 ? g : 2048;
+    int gr = g < 512 ? g : 512;
     int gc = C, t = 2048;
     while (t) {
       const int r = gc % t;
