@@ -1235,6 +1235,55 @@ __global__ __launch_bounds__(256) void cast_kernel(const float* __restrict__ x, 
   }
 }
 
+// Explicit im2col for convolutions whose input channel count is not a multiple of 8 (the ResNet
+// stem, C = 3): out[m][k] = x[b, oh*s-p+kh, ow*s-p+kw, ci] for k = (kh*KW+kw)*C+ci < K, 0 up to Kp
+// (Kp = K rounded up to 8), so the GEMM that follows runs the 16-byte vector path on both operands.
+// Blocks past the pixel range copy the [Co][K] weight shadow into a [Co][Kp] zero-padded copy.
+__global__ __launch_bounds__(256) void im2col_kernel(const bf16* __restrict__ x, Geo g, int Kp,
+                                                     bf16* __restrict__ out, const bf16* __restrict__ w_in,
+                                                     bf16* __restrict__ w_out, int pix_blocks) {
+  const int K = g.KH * g.KW * g.C;
+  if ((int)blockIdx.x >= pix_blocks) {  // weight padding blocks
+    const int n = g.Co * Kp;
+    for (int e = (blockIdx.x - pix_blocks) * blockDim.x + threadIdx.x; e < n;
+         e += (gridDim.x - pix_blocks) * blockDim.x) {
+      const int co = e / Kp, k = e - co * Kp;
+      w_out[e] = k < K ? w_in[co * K + k] : (bf16)0.0f;
+    }
+    return;
+  }
+  const int K8 = Kp >> 3;
+  const long long n = (long long)g.B * g.Ho * g.Wo * K8;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)pix_blocks * blockDim.x) {
+    const int k8 = (int)(e % K8);
+    const long long m = e / K8;
+    const int hw = g.Ho * g.Wo;
+    const int b = (int)(m / hw), rem = (int)(m - (long long)b * hw);
+    const int oh = rem / g.Wo, ow = rem - oh * g.Wo;
+    const int y0 = oh * g.sh - g.pt, x0 = ow * g.sw - g.pl;
+    int k = k8 * 8;
+    int kc = k / g.C, ci = k - kc * g.C;
+    int kh = kc / g.KW, kw = kc - kh * g.KW;
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float val = 0.f;
+      const int ih = y0 + kh, iw = x0 + kw;
+      if (k + j < K && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
+        val = bf2f(x[(((long long)b * g.H + ih) * g.W + iw) * g.C + ci]);
+      v[j] = f2bf(val);
+      if (++ci == g.C) {
+        ci = 0;
+        if (++kw == g.KW) {
+          kw = 0;
+          ++kh;
+        }
+      }
+    }
+    *reinterpret_cast<bf16x8*>(out + m * Kp + k) = v;
+  }
+}
+
 static int grid_for(long long n, int per_thread = 1) {
   const long long t = (n + per_thread - 1) / per_thread;
   long long b = (t + 255) / 256;
@@ -1347,7 +1396,7 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     case A_ROWK: p.avec = al && lda % 8 == 0 && K % 8 == 0; break;
     case A_CONV: p.avec = al && p.g.C % 8 == 0; break;
     case A_DGRAD: p.avec = al && p.g.Co % 8 == 0; break;
-    case A_COLM: p.avec = al && lda % 8 == 0 && M % 8 == 0; break;
+    case A_COLM: p.avec = al && lda % 8 == 0 && (M + 7) / 8 * 8 <= lda; break;  // padded rows read, never stored
     case A_WGRAD: p.avec = al && p.g.C % 8 == 0; break;
     default: return -1;
   }
@@ -1543,6 +1592,17 @@ TDE_API int tde_colstats(const bf16* x, long long R, int C, double* stats, hipSt
 TDE_API int tde_cast_f32_bf16(const float* x, bf16* y, long long n, hipStream_t stream) {
   if (((uintptr_t)x & 15) != 0) return -1;
   cast_kernel<<<grid_for(n, 4), 256, 0, stream>>>(x, y, n);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+TDE_API int tde_im2col(const bf16* x, const int* geo, int Kp, bf16* out, const bf16* w_in, bf16* w_out,
+                       hipStream_t stream) {
+  Geo g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9], geo[10], geo[11], geo[12]};
+  if (Kp % 8 || Kp < g.KH * g.KW * g.C || ((uintptr_t)out & 15)) return -1;
+  const int pix = grid_for((long long)g.B * g.Ho * g.Wo * (Kp / 8));
+  const int wb = w_in ? 8 : 0;
+  im2col_kernel<<<pix + wb, 256, 0, stream>>>(x, g, Kp, out, w_in, w_out, pix);
   TDE_LAUNCH_CHECK();
   return 0;
 }

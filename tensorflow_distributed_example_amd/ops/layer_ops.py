@@ -159,6 +159,35 @@ def conv_dgrad(dy, Wrow, dx, g: ConvGeom, accum=False, scratch=None):
            cb_accum=accum, scratch=scratch)
 
 
+# ---------------------------------------------------------------- explicit im2col (C % 8 != 0, e.g. the RGB stem)
+def im2col(x, g: ConvGeom, xcol, Wt=None, Wt_pad=None):
+    """xcol[B*Ho*Wo, Kp] = patches of x (Kp = K rounded up to 8, zero tail); optionally Wt [Co, K] ->
+    Wt_pad [Co, Kp].  Lets the conv GEMMs run the 16-byte vector path."""
+    Kp = -(-g.K // 8) * 8
+    _bf(x, g.B * g.H * g.W * g.C, "im2col x")
+    _bf(xcol, g.B * g.Ho * g.Wo * Kp, "im2col out")
+    if Wt is not None:
+        _req(tuple(Wt.shape) == (g.Co, g.K) and Wt.dtype == bf16 and Wt.is_contiguous(), "im2col Wt")
+        _bf(Wt_pad, g.Co * Kp, "im2col Wt_pad")
+    N.check(N.hip().tde_im2col(_P(x), g.carray(), Kp, _P(xcol), _P(Wt), _P(Wt_pad), _s()), "tde_im2col")
+    return Kp
+
+
+def conv_fwd_im2col(xcol, Wt_pad, y, g: ConvGeom, Kp, bias=None, relu=False, colstats=None, scratch=None):
+    M = g.B * g.Ho * g.Wo
+    _bf(y, M * g.Co, "conv_fwd_im2col y")
+    _igemm(xcol, Kp, A_ROWK, Wt_pad, Kp, B_NK, M, g.Co, Kp, splits=_fs(M, g.Co, Kp, scratch), cb=y, ldcb=g.Co,
+           bias=bias, relu=relu, colstats=colstats, scratch=scratch)
+
+
+def conv_wgrad_im2col(xcol, dy, dW, g: ConvGeom, Kp):
+    """dW[K, Co] += xcol[:, :K]^T @ dy (the padded columns are read, never written)."""
+    M = g.B * g.Ho * g.Wo
+    _bf(dy, M * g.Co, "conv_wgrad_im2col dy")
+    _f32(dW, g.K * g.Co, "conv_wgrad_im2col dW")
+    _igemm(xcol, Kp, A_COLM, dy, g.Co, B_KN, g.K, g.Co, M, splits=0, cf=dW, ldc=g.Co, cf_mode=2)
+
+
 # ---------------------------------------------------------------- narrow convolutions (direct, VALU)
 def smallconv_ok(g: ConvGeom, dgrad=False):
     return bool(N.hip().tde_smallconv_ok(g.C, g.Co, g.KH, g.KW, int(dgrad)))

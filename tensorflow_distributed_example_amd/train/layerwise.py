@@ -344,6 +344,8 @@ class _Gemm(_Stage):
                                 and O.smallconv_ok(self.geo, True))
             if self.small_fwd:
                 self.shadows = {self.wname: ("row", "col")}
+            # channel counts that defeat 16-byte gathers (RGB stem): explicit im2col + vector GEMMs
+            self.use_im2col = (not self.small_fwd and C % 8 != 0 and os.environ.get("TDE_IM2COL", "1") != "0")
         self.colstats = None
         self.dz = None
 
@@ -356,6 +358,11 @@ class _Gemm(_Stage):
         return max(O.scratch_elems(rows, out, fin), O.scratch_elems(rows, fin, out) if self.need_dgrad else 0)
 
     def alloc(self, B, dev):
+        if self.conv and self.use_im2col:
+            g = self.geo.with_batch(B)
+            self.Kp = -(-g.K // 8) * 8
+            self.xcol = torch.zeros(B * g.Ho * g.Wo * self.Kp, dtype=bf16, device=dev)
+            self.Wt_pad = torch.zeros(g.Co * self.Kp, dtype=bf16, device=dev)
         if self.stats:
             self.colstats = torch.zeros(2 * self.out.C, dtype=torch.float64, device=dev)
         if self.relu or self.gb is not None:
@@ -370,7 +377,12 @@ class _Gemm(_Stage):
 
     def fwd(self, p, B, training, mode="train"):
         cs = self.colstats if (self.stats and training) else None
-        if self.conv and self.small_fwd:
+        if self.conv and self.use_im2col:
+            g = self.geo.with_batch(B)
+            O.im2col(self.inp.buf, g, self.xcol, self.Wt, self.Wt_pad)
+            O.conv_fwd_im2col(self.xcol, self.Wt_pad, self.out.root().buf, g, self.Kp, bias=self.b, relu=self.relu,
+                              colstats=cs, scratch=p.scratch)
+        elif self.conv and self.small_fwd:
             O.smallconv_fwd(self.inp.buf, self.Wrow, self.out.root().buf, self.geo.with_batch(B), bias=self.b,
                             relu=self.relu, colstats=cs)
         elif self.conv:
@@ -389,7 +401,10 @@ class _Gemm(_Stage):
             dout = self.dz
         if self.conv:
             g = self.geo.with_batch(B)
-            O.conv_wgrad(self.inp.buf, dout, self.gW, g)
+            if self.use_im2col:
+                O.conv_wgrad_im2col(self.xcol, dout, self.gW, g, self.Kp)
+            else:
+                O.conv_wgrad(self.inp.buf, dout, self.gW, g)
             if self.need_dgrad and self.small_dgrad:
                 O.smallconv_dgrad(dout, self.Wrow, self.inp.root().grad, g, accum=self.accum[self.inp.root().id])
             elif self.need_dgrad:

@@ -436,3 +436,33 @@ def test_smallconv_direct_kernels(B, H, W, C, Co, k, s, pad):
     assert (st[:Co] - rs.sum((0, 1, 2))).abs().max().item() <= 1e-4 * rs.abs().sum((0, 1, 2)).max().item() + 1e-3
     assert _rel(st[Co:], (rs ** 2).sum((0, 1, 2))) < 1e-3
     assert _rel(dx.float(), xr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
+@pytest.mark.parametrize("B,H,W,C,Co,k,s,pad", [(2, 15, 15, 3, 64, 7, 2, "same"), (4, 28, 28, 6, 12, 6, 2, "same"),
+                                                (2, 14, 14, 12, 24, 6, 2, "same")])
+def test_im2col_conv_path(B, H, W, C, Co, k, s, pad):
+    """Explicit im2col (C % 8 != 0) + vector GEMMs: forward with BN statistics and weight gradient."""
+    from tensorflow_distributed_example_amd.ops import layer_ops as O
+    (pt, pb), (pl, pr) = _tf_same(H, k, s), _tf_same(W, k, s)
+    Ho, Wo = -(-H // s), -(-W // s)
+    g = O.ConvGeom(B, H, W, C, Ho, Wo, Co, k, k, s, s, pt, pl)
+    x = _r(B, H, W, C, seed=41)
+    w = _r(k, k, C, Co, seed=42, scale=0.2)
+    Kp = -(-g.K // 8) * 8
+    xcol = torch.zeros(B * Ho * Wo * Kp, dtype=bf, device=DEV)
+    Wt_pad = torch.zeros(Co * Kp, dtype=bf, device=DEV)
+    O.im2col(x, g, xcol, w.reshape(-1, Co).t().contiguous(), Wt_pad)
+    y = torch.zeros(B, Ho, Wo, Co, dtype=bf, device=DEV)
+    st = torch.zeros(2 * Co, dtype=torch.float64, device=DEV)
+    O.conv_fwd_im2col(xcol, Wt_pad, y, g, Kp, colstats=st)
+    dy = _r(B, Ho, Wo, Co, seed=43)
+    dW = torch.zeros(k, k, C, Co, device=DEV)
+    O.conv_wgrad_im2col(xcol, dy, dW, g, Kp)
+    xr = x.float().permute(0, 3, 1, 2)
+    wr = w.float().permute(3, 2, 0, 1).requires_grad_(True)
+    ref = F.conv2d(F.pad(xr, (pl, pr, pt, pb)), wr, stride=s).permute(0, 2, 3, 1)
+    ref.backward(dy.float())
+    torch.cuda.synchronize()
+    assert _rel(y.float(), ref) < 1e-2
+    assert _rel(st[Co:], (ref.detach().to(bf).double() ** 2).sum((0, 1, 2))) < 1e-3
+    assert _rel(dW, wr.grad.permute(2, 3, 1, 0)) < 1e-3
