@@ -69,6 +69,9 @@ struct IGemmArgs {
 };
 
 constexpr int TK = 32;  // MFMA k-slice
+// BN statistics accumulate into kStatSlots interleaved copies ([slot][2][C] f64, slot = block % slots)
+// so thousands of producer workgroups do not serialise on the same 2*C addresses; readers sum slots.
+constexpr int kStatSlots = 8;
 
 __device__ __forceinline__ bf16x8 zero8() {
   bf16x8 r;
@@ -479,6 +482,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   }
 
   // ---- epilogue
+  float sp1[NI], sp2[NI];  // per-column statistics of this wave (valid in lanes 0..15)
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     const int col = n0 + wn * WTN + j * 16 + fr;
@@ -520,9 +524,30 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
       s1 += __shfl_xor(s1, 32, 64);
       s2 += __shfl_xor(s2, 16, 64);
       s2 += __shfl_xor(s2, 32, 64);
-      if (lane < 16 && cok) {
-        atomicAdd(&p.colstats[col], (double)s1);
-        atomicAdd(&p.colstats[p.N + col], (double)s2);
+    }
+    sp1[j] = s1;
+    sp2[j] = s2;
+  }
+  if (p.colstats) {
+    // the two waves sharing a column range (wm = 0, 1) combine through LDS: one atomic per column per block
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [2 wn][NI][2][16]
+    if (wm == 1 && lane < 16) {
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        red[((wn * NI + j) * 2 + 0) * 16 + lane] = sp1[j];
+        red[((wn * NI + j) * 2 + 1) * 16 + lane] = sp2[j];
+      }
+    }
+    __syncthreads();
+    if (wm == 0 && lane < 16) {
+      double* st = p.colstats + (size_t)(blockIdx.x % kStatSlots) * 2 * p.N;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int col = n0 + wn * WTN + j * 16 + lane;
+        if (col >= p.N) continue;
+        atomicAdd(&st[col], (double)(sp1[j] + red[((wn * NI + j) * 2 + 0) * 16 + lane]));
+        atomicAdd(&st[p.N + col], (double)(sp2[j] + red[((wn * NI + j) * 2 + 1) * 16 + lane]));
       }
     }
   }
@@ -597,9 +622,14 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(BnFwdArgs a) {
     if (a.mode != 0) {
       float mean, var;
       if (a.mode == 1) {
-        const double md = a.stats[c] / (double)a.R;
+        double s1 = 0.0, s2 = 0.0;
+        for (int sl = 0; sl < kStatSlots; ++sl) {
+          s1 += a.stats[sl * 2 * C + c];
+          s2 += a.stats[sl * 2 * C + C + c];
+        }
+        const double md = s1 / (double)a.R;
         mean = (float)md;
-        var = (float)fmax(a.stats[C + c] / (double)a.R - md * md, 0.0);
+        var = (float)fmax(s2 / (double)a.R - md * md, 0.0);
       } else {
         mean = a.mmean[c];
         var = a.mvar[c];
@@ -829,8 +859,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a) {
       k1[c] = k2[c] = 0.f;
     }
     if (blockIdx.x == 0 && a.zero_fwd) {
-      a.zero_fwd[c] = 0.0;
-      a.zero_fwd[a.C + c] = 0.0;
+      for (int sl = 0; sl < kStatSlots; ++sl) {
+        a.zero_fwd[sl * 2 * a.C + c] = 0.0;
+        a.zero_fwd[sl * 2 * a.C + a.C + c] = 0.0;
+      }
     }
   }
   __syncthreads();
@@ -1214,9 +1246,10 @@ __global__ __launch_bounds__(256) void colstats_kernel(const bf16* __restrict__ 
     atomicAdd(&s2[c], v * v);
   }
   __syncthreads();
+  double* st = stats + (size_t)(blockIdx.x % kStatSlots) * 2 * C;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    atomicAdd(&stats[c], (double)s1[c]);
-    atomicAdd(&stats[C + c], (double)s2[c]);
+    atomicAdd(&st[c], (double)s1[c]);
+    atomicAdd(&st[C + c], (double)s2[c]);
   }
 }
 
@@ -1331,9 +1364,10 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(float* __restrict__ 
   }
   if (colstats) {
     __syncthreads();
+    double* st = colstats + (size_t)(blockIdx.x % kStatSlots) * 2 * N;
     for (int c = threadIdx.x; c < N; c += blockDim.x) {
-      atomicAdd(&colstats[c], (double)s1[c]);
-      atomicAdd(&colstats[N + c], (double)s2[c]);
+      atomicAdd(&st[c], (double)s1[c]);
+      atomicAdd(&st[N + c], (double)s2[c]);
     }
   }
 }

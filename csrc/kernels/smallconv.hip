@@ -96,9 +96,10 @@ __global__ __launch_bounds__(256) void smallconv_fwd_kernel(const bf16* __restri
     }
   }
   __syncthreads();
-  if (threadIdx.x < g.Co) {
-    atomicAdd(&colstats[threadIdx.x], (double)st[0][threadIdx.x]);
-    atomicAdd(&colstats[g.Co + threadIdx.x], (double)st[1][threadIdx.x]);
+  if (threadIdx.x < g.Co) {  // slotted statistics (layers.hip kStatSlots = 8)
+    double* cs = colstats + (size_t)(blockIdx.x % 8) * 2 * g.Co;
+    atomicAdd(&cs[threadIdx.x], (double)st[0][threadIdx.x]);
+    atomicAdd(&cs[g.Co + threadIdx.x], (double)st[1][threadIdx.x]);
   }
 }
 

@@ -16,6 +16,7 @@ from .. import _native as N
 
 _P = N.ptr
 A_ROWK, A_CONV, A_DGRAD, A_COLM, A_WGRAD = range(5)
+STAT_SLOTS = 8   # BN statistics buffers are [STAT_SLOTS][2][C] f64 (layers.hip kStatSlots)
 B_NK, B_DGRADW, B_KN = range(3)
 bf16 = torch.bfloat16
 
@@ -138,7 +139,7 @@ def conv_fwd(x, Wt, y, g: ConvGeom, bias=None, relu=False, colstats=None, scratc
     if bias is not None:
         _f32(bias, g.Co, "conv_fwd bias")
     if colstats is not None:
-        _f64(colstats, 2 * g.Co, "conv_fwd colstats")
+        _f64(colstats, 2 * STAT_SLOTS * g.Co, "conv_fwd colstats")
     M = g.B * g.Ho * g.Wo
     _igemm(x, 0, A_CONV, Wt, g.K, B_NK, M, g.Co, g.K, g, splits=_fs(M, g.Co, g.K, scratch), cb=y, ldcb=g.Co,
            bias=bias, relu=relu, colstats=colstats, scratch=scratch)
@@ -201,7 +202,7 @@ def smallconv_fwd(x, Wrow, y, g: ConvGeom, bias=None, relu=False, colstats=None)
     if bias is not None:
         _f32(bias, g.Co, "smallconv_fwd bias")
     if colstats is not None:
-        _f64(colstats, 2 * g.Co, "smallconv_fwd colstats")
+        _f64(colstats, 2 * STAT_SLOTS * g.Co, "smallconv_fwd colstats")
     _req(smallconv_ok(g), "smallconv_fwd: layer too wide for the direct kernel")
     N.check(N.hip().tde_smallconv_fwd(_P(x), _P(Wrow), _P(bias), int(relu), _P(y), _P(colstats), g.carray(), _s()),
             "tde_smallconv_fwd")
@@ -239,7 +240,7 @@ def dense_fwd(x, Wt, B, *, y=None, logits=None, bias=None, relu=False, colstats=
     if bias is not None:
         _f32(bias, out, "dense_fwd bias")
     if colstats is not None:
-        _f64(colstats, 2 * out, "dense_fwd colstats")
+        _f64(colstats, 2 * STAT_SLOTS * out, "dense_fwd colstats")
     _igemm(x, fin, A_ROWK, Wt, fin, B_NK, B, out, fin, splits=_fs(B, out, fin, scratch), cf=logits, ldc=out,
            cf_mode=1 if logits is not None else 0, cb=y, ldcb=out, bias=bias, relu=relu, colstats=colstats,
            scratch=scratch)
@@ -287,7 +288,7 @@ def bn_fwd(y, out, R, Cc, *, mode, stats=None, saved=None, gamma=None, beta=None
     if res is not None:
         _bf(res, n, "bn_fwd res")
     if mode == 1:
-        _f64(stats, 2 * Cc, "bn_fwd stats")
+        _f64(stats, 2 * STAT_SLOTS * Cc, "bn_fwd stats")
         _f32(saved, 2 * Cc, "bn_fwd saved")
     if mode == 2:
         _f32(mmean, Cc, "bn_fwd moving_mean")
@@ -312,7 +313,7 @@ def bn_bwd(dout, y, R, Cc, *, mode, saved=None, gamma=None, beta=None, res=None,
         _f32(saved, 2 * Cc, "bn_bwd saved")
         _f32(dstats, 2 * Cc, "bn_bwd dstats")
     if zero_fwd is not None:
-        _f64(zero_fwd, 2 * Cc, "bn_bwd zero_fwd")
+        _f64(zero_fwd, 2 * STAT_SLOTS * Cc, "bn_bwd zero_fwd")
     if dx is not None:
         _bf(dx, n, "bn_bwd dx")
     if dres is not None:
@@ -342,7 +343,7 @@ def act_bwd(dout, out, R, Cc, *, relu, dz=None, dbias=None):
 
 def colstats(x, R, Cc, stats):
     _bf(x, R * Cc, "colstats x")
-    _f64(stats, 2 * Cc, "colstats stats")
+    _f64(stats, 2 * STAT_SLOTS * Cc, "colstats stats")
     N.check(N.hip().tde_colstats(_P(x), int(R), int(Cc), _P(stats), _s()), "tde_colstats")
 
 

@@ -364,7 +364,7 @@ class _Gemm(_Stage):
             self.xcol = torch.zeros(B * g.Ho * g.Wo * self.Kp, dtype=bf16, device=dev)
             self.Wt_pad = torch.zeros(g.Co * self.Kp, dtype=bf16, device=dev)
         if self.stats:
-            self.colstats = torch.zeros(2 * self.out.C, dtype=torch.float64, device=dev)
+            self.colstats = torch.zeros(2 * O.STAT_SLOTS * self.out.C, dtype=torch.float64, device=dev)
         if self.relu or self.gb is not None:
             self.dz = torch.zeros(B * self.out.numel, dtype=bf16, device=dev)
 
@@ -464,7 +464,7 @@ class _Elementwise(_Stage):
             if self.stats_from_gemm:
                 self.colstats = None   # bound below to the producing GEMM's buffer
             else:
-                self.colstats = torch.zeros(2 * C, dtype=torch.float64, device=dev)
+                self.colstats = torch.zeros(2 * O.STAT_SLOTS * C, dtype=torch.float64, device=dev)
         if self.bn and self.stats_from_gemm:
             for st in self.plan.stages:
                 if isinstance(st, _Gemm) and st.out.root() is self.inp.root():
