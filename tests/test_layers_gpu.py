@@ -33,6 +33,15 @@ def _sum_slots(st, C):
     return st.view(SLOTS, 2, C).sum(0).reshape(-1)
 
 
+def _cpu64(t):
+    """float64 CPU copy: the torch oracles run on the host, so no vendor GPU kernel is part of a check."""
+    return t.detach().double().cpu()
+
+
+def _dev(t):
+    return t.to(DEV)
+
+
 def _tf_same(n, k, s):
     out = -(-n // s)
     tot = max((out - 1) * s + k - n, 0)
@@ -71,24 +80,24 @@ def test_conv_fwd_dgrad_wgrad(B, H, W, C, Co, k, s, pad):
     Wt = w.reshape(-1, Co).t().contiguous()
     O.conv_fwd(x, Wt, y, g, bias=bias, relu=False, colstats=stats_raw)
     stats = _sum_slots(stats_raw, Co)
-    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
-    wr = w.float().permute(3, 2, 0, 1).requires_grad_(True)
-    ref = F.conv2d(F.pad(xr, (pl, pr, pt, pb)), wr, bias, stride=s).permute(0, 2, 3, 1)
+    xr = _cpu64(x).permute(0, 3, 1, 2).requires_grad_(True)
+    wr = _cpu64(w).permute(3, 2, 0, 1).requires_grad_(True)
+    ref = F.conv2d(F.pad(xr, (pl, pr, pt, pb)), wr, _cpu64(bias), stride=s).permute(0, 2, 3, 1)
+    dy = _r(B, Ho, Wo, Co, seed=3)
+    ref.backward(_cpu64(dy))
+    ref, xr_grad, wr_grad = _dev(ref.detach()), _dev(xr.grad), _dev(wr.grad)
     torch.cuda.synchronize()
     assert _rel(y.float(), ref) < 1e-2
-    rs = ref.detach().to(bf).double()   # statistics are of the stored bf16 activation
+    rs = ref.to(bf).double()   # statistics are of the stored bf16 activation
     assert (stats[:Co] - rs.sum((0, 1, 2))).abs().max().item() <= 1e-4 * rs.abs().sum((0, 1, 2)).max().item() + 1e-3
     assert _rel(stats[Co:], (rs ** 2).sum((0, 1, 2))) < 1e-3
-    # backward
-    dy = _r(B, Ho, Wo, Co, seed=3)
-    ref.backward(dy.float())
     dx = torch.zeros(B, H, W, C, dtype=bf, device=DEV)
     O.conv_dgrad(dy, w.contiguous(), dx, g)
     dW = torch.zeros(k, k, C, Co, device=DEV)
     O.conv_wgrad(x, dy, dW, g)
     torch.cuda.synchronize()
-    assert _rel(dx.float(), xr.grad.permute(0, 2, 3, 1)) < 1e-2
-    assert _rel(dW, wr.grad.permute(2, 3, 1, 0)) < 1e-3
+    assert _rel(dx.float(), xr_grad.permute(0, 2, 3, 1)) < 1e-2
+    assert _rel(dW, wr_grad.permute(2, 3, 1, 0)) < 1e-3
     # accumulate mode
     dx2 = dx.clone()
     O.conv_dgrad(dy, w.contiguous(), dx2, g, accum=True)
@@ -438,10 +447,12 @@ def test_smallconv_direct_kernels(B, H, W, C, Co, k, s, pad):
     st_raw = _stats_buf(Co)
     O.smallconv_fwd(x, w.contiguous(), y, g, bias=bias, relu=False, colstats=st_raw)
     st = _sum_slots(st_raw, Co)
-    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
-    ref = F.conv2d(F.pad(xr, (pl, pr, pt, pb)), w.float().permute(3, 2, 0, 1), bias, stride=s).permute(0, 2, 3, 1)
+    xr = _cpu64(x).permute(0, 3, 1, 2).requires_grad_(True)
+    ref = F.conv2d(F.pad(xr, (pl, pr, pt, pb)), _cpu64(w).permute(3, 2, 0, 1), _cpu64(bias), stride=s)
+    ref = ref.permute(0, 2, 3, 1)
     dy = _r(B, Ho, Wo, Co, seed=33)
-    ref.backward(dy.float())
+    ref.backward(_cpu64(dy))
+    ref, xgrad = _dev(ref.detach()), _dev(xr.grad)
     dx = torch.zeros(B, H, W, C, dtype=bf, device=DEV)
     O.smallconv_dgrad(dy, w.contiguous(), dx, g)
     torch.cuda.synchronize()
@@ -449,7 +460,7 @@ def test_smallconv_direct_kernels(B, H, W, C, Co, k, s, pad):
     assert _rel(y.float(), ref) < 1e-2
     assert (st[:Co] - rs.sum((0, 1, 2))).abs().max().item() <= 1e-4 * rs.abs().sum((0, 1, 2)).max().item() + 1e-3
     assert _rel(st[Co:], (rs ** 2).sum((0, 1, 2))) < 1e-3
-    assert _rel(dx.float(), xr.grad.permute(0, 2, 3, 1)) < 1e-2
+    assert _rel(dx.float(), xgrad.permute(0, 2, 3, 1)) < 1e-2
 
 
 @pytest.mark.parametrize("B,H,W,C,Co,k,s,pad", [(2, 15, 15, 3, 64, 7, 2, "same"), (4, 28, 28, 6, 12, 6, 2, "same"),
@@ -473,11 +484,12 @@ def test_im2col_conv_path(B, H, W, C, Co, k, s, pad):
     dy = _r(B, Ho, Wo, Co, seed=43)
     dW = torch.zeros(k, k, C, Co, device=DEV)
     O.conv_wgrad_im2col(xcol, dy, dW, g, Kp)
-    xr = x.float().permute(0, 3, 1, 2)
-    wr = w.float().permute(3, 2, 0, 1).requires_grad_(True)
+    xr = _cpu64(x).permute(0, 3, 1, 2)
+    wr = _cpu64(w).permute(3, 2, 0, 1).requires_grad_(True)
     ref = F.conv2d(F.pad(xr, (pl, pr, pt, pb)), wr, stride=s).permute(0, 2, 3, 1)
-    ref.backward(dy.float())
+    ref.backward(_cpu64(dy))
+    ref, wgrad = _dev(ref.detach()), _dev(wr.grad)
     torch.cuda.synchronize()
     assert _rel(y.float(), ref) < 1e-2
     assert _rel(st[Co:], (ref.detach().to(bf).double() ** 2).sum((0, 1, 2))) < 1e-3
-    assert _rel(dW, wr.grad.permute(2, 3, 1, 0)) < 1e-3
+    assert _rel(dW, wgrad.permute(2, 3, 1, 0)) < 1e-3
