@@ -305,7 +305,12 @@ class Estimator:
         R = strategy.num_local_replicas
         gb = per_replica * strategy.num_replicas_in_sync
         cfg = self.config
+        # steps per hipGraph replay: the standard hooks fire on multiples of their intervals, so the group
+        # size divides them; user SessionRunHooks see every step (TF after_run semantics) unless the
+        # RunConfig asks for grouped execution explicitly
         spe = self._spe([cfg.log_step_count_steps, cfg.save_summary_steps, cfg.save_checkpoints_steps])
+        if hooks and not cfg.steps_per_execution:
+            spe = 1
         m.steps_per_execution = spe
         prog = m._program("train", gb)
         prog.reset_metrics()
