@@ -454,6 +454,14 @@ class Estimator:
             ctx.global_step = gstep
             for h in all_hooks:
                 h.after_step(ctx)
+        if chief and max_steps is not None:
+            # tickets are exhausted, but other workers may still be finishing steps they claimed: the
+            # final checkpoint/export of the chief must see all max_steps global updates
+            t0 = time.time()
+            while gstep < max_steps and time.time() - t0 < 120:
+                time.sleep(0.01)
+                gstep = client.global_step()
+            ctx.prev_step, ctx.global_step = ctx.global_step, gstep
         if chief:
             m._store.load_dict(client.pull())
         for h in all_hooks:
