@@ -607,7 +607,7 @@ struct BnFwdArgs {
   float* mmean;
   float* mvar;
   float momentum, bessel;
-  float* zero_buf;  // [2][C] backward accumulators of this layer (zeroed by block 0)
+  float* zero_buf;  // [kStatSlots][2][C] backward accumulators of this layer (zeroed by block 0)
   int relu;
   Drop drop;
 };
@@ -648,8 +648,10 @@ __global__ __launch_bounds__(256) void bn_fwd_kernel(BnFwdArgs a) {
       }
     }
     if (blockIdx.x == 0 && a.zero_buf) {
-      a.zero_buf[c] = 0.f;
-      a.zero_buf[C + c] = 0.f;
+      for (int sl = 0; sl < kStatSlots; ++sl) {
+        a.zero_buf[sl * 2 * C + c] = 0.f;
+        a.zero_buf[sl * 2 * C + C + c] = 0.f;
+      }
     }
     sc[c] = scale;
     sf[c] = shift;
@@ -715,7 +717,7 @@ struct BnBwdArgs {
   const float* beta;
   int relu;
   Drop drop;
-  float* dstats;  // [2][C] sum dz, sum dz*xhat
+  float* dstats;  // [kStatSlots][2][C] sum dz, sum dz*xhat (slot = block % kStatSlots)
   bf16* dx;
   int dx_accum;
   bf16* dres;
@@ -837,8 +839,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdArgs a) {
   }
   __syncthreads();
   for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-    atomicAdd(&a.dstats[c], s1[c]);
-    atomicAdd(&a.dstats[a.C + c], s2[c]);
+    float* ds = a.dstats + (size_t)(blockIdx.x % kStatSlots) * 2 * a.C;
+    atomicAdd(&ds[c], s1[c]);
+    atomicAdd(&ds[a.C + c], s2[c]);
   }
 }
 
@@ -848,7 +851,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a) {
   const float invR = 1.f / (float)a.R;
   for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
     if (a.mode == 1) {
-      const float sdz = a.dstats[c], sdx = a.dstats[a.C + c];
+      float sdz = 0.f, sdx = 0.f;
+      for (int sl = 0; sl < kStatSlots; ++sl) {
+        sdz += a.dstats[sl * 2 * a.C + c];
+        sdx += a.dstats[sl * 2 * a.C + a.C + c];
+      }
       k1[c] = sdz * invR;
       k2[c] = sdx * invR;
       if (blockIdx.x == 0) {

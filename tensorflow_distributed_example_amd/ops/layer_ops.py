@@ -294,7 +294,7 @@ def bn_fwd(y, out, R, Cc, *, mode, stats=None, saved=None, gamma=None, beta=None
         _f32(mmean, Cc, "bn_fwd moving_mean")
         _f32(mvar, Cc, "bn_fwd moving_variance")
     if zero_buf is not None:
-        _f32(zero_buf, 2 * Cc, "bn_fwd zero_buf")
+        _f32(zero_buf, 2 * STAT_SLOTS * Cc, "bn_fwd zero_buf")
     rc = N.hip().tde_bn_fwd(_P(y), _P(out), _P(res), int(R), int(Cc), int(mode), _P(stats), _P(saved), _P(gamma),
                             _P(beta), float(eps), _P(mmean), _P(mvar), float(momentum), float(bessel), _P(zero_buf),
                             int(relu), float(drop.rate), int(drop.seed) & (2 ** 64 - 1), _P(drop.iterations),
@@ -311,7 +311,7 @@ def bn_bwd(dout, y, R, Cc, *, mode, saved=None, gamma=None, beta=None, res=None,
     _req(Cc <= 1024, "bn_bwd: at most 1024 channels")
     if mode == 1:
         _f32(saved, 2 * Cc, "bn_bwd saved")
-        _f32(dstats, 2 * Cc, "bn_bwd dstats")
+        _f32(dstats, 2 * STAT_SLOTS * Cc, "bn_bwd dstats")
     if zero_fwd is not None:
         _f64(zero_fwd, 2 * STAT_SLOTS * Cc, "bn_bwd zero_fwd")
     if dx is not None:

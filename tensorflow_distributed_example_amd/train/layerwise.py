@@ -460,7 +460,7 @@ class _Elementwise(_Stage):
         C = self.inp.C
         if self.bn:
             self.saved = torch.zeros(2 * C, dtype=torch.float32, device=dev)
-            self.dstats = torch.zeros(2 * C, dtype=torch.float32, device=dev)
+            self.dstats = torch.zeros(2 * O.STAT_SLOTS * C, dtype=torch.float32, device=dev)
             if self.stats_from_gemm:
                 self.colstats = None   # bound below to the producing GEMM's buffer
             else:

@@ -143,7 +143,7 @@ def test_batchnorm_fwd_bwd(R, C, relu, res, fused):
     saved = torch.zeros(2 * C, device=DEV)
     mm, mv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
     out = torch.zeros(R, C, dtype=bf, device=DEV)
-    dstats = torch.full((2 * C,), 7.0, device=DEV)
+    dstats = torch.full((2 * SLOTS * C,), 7.0, device=DEV)
     bessel = R / (R - 1) if fused else 1.0
     O.bn_fwd(y, out, R, C, mode=1, stats=stats, saved=saved, gamma=gamma, beta=beta, eps=1e-3, mmean=mm, mvar=mv,
              momentum=0.99, bessel=bessel, zero_buf=dstats, res=r, relu=relu)
