@@ -35,6 +35,8 @@
 //   cross-entropy (+accuracy, +dlogits, +probabilities) for any class count.
 #include "tde_common.h"
 
+#include <initializer_list>
+
 namespace tde {
 
 struct Geo {  // NHWC input [B,H,W,C], HWIO kernel [KH,KW,C,Co], NHWC output [B,Ho,Wo,Co]
@@ -919,6 +921,367 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Channel-tiled BN kernels (C % 8 == 0 and C <= 64 or C % 64 == 0; 16-byte aligned tensors).
+// A block owns CG = min(C, 64) channels and a strided set of rows: each thread keeps its 8
+// channels' coefficients in registers (no per-element LDS lookups), the per-channel prologue
+// touches only CG channels (not all C: the 8 f64 statistic slots of a C=512 layer are 64 KB per
+// block otherwise), the reduction ends with 2*CG atomics per block, and U=4 rows are loaded
+// before any is used so enough bytes are in flight to cover HBM latency with few blocks.
+struct BnTile {
+  int cg, tpr, rp, g, c0;  // channels per group, threads per row, rows per pass, group, first channel
+  long long row, stride;   // first row of this thread, row stride
+  bool active;
+};
+
+__device__ __forceinline__ BnTile bn_tile(int C) {
+  BnTile t;
+  t.cg = C < 64 ? C : 64;
+  t.tpr = t.cg >> 3;
+  t.rp = blockDim.x / t.tpr;
+  const int ng = C / t.cg;
+  t.g = blockIdx.x % ng;
+  const int rb = blockIdx.x / ng, nrb = gridDim.x / ng;
+  const int tid = threadIdx.x;
+  t.active = tid < t.rp * t.tpr;
+  t.c0 = t.g * t.cg + (tid % t.tpr) * 8;
+  t.row = (long long)rb * t.rp + tid / t.tpr;
+  t.stride = (long long)nrb * t.rp;
+  return t;
+}
+
+__device__ __forceinline__ void ld8(const bf16* p, float* v) {
+  const bf16x8 x = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = bf2f(x[j]);
+}
+
+__device__ __forceinline__ void st8(bf16* p, const float* v) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
+  *reinterpret_cast<bf16x8*>(p) = o;
+}
+
+constexpr int kBnU = 4;
+
+__global__ __launch_bounds__(256) void bn_fwd_tiled_kernel(BnFwdArgs a) {
+  __shared__ float lsc[64], lsf[64];
+  const int C = a.C;
+  const BnTile t = bn_tile(C);
+  if (threadIdx.x < t.cg) {
+    const int c = t.g * t.cg + threadIdx.x;
+    const bool first = blockIdx.x < C / t.cg;  // row-block 0 of this channel group
+    float scale = 1.f, shift = 0.f;
+    if (a.mode != 0) {
+      float mean, var;
+      if (a.mode == 1) {
+        double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+        for (int sl = 0; sl < kStatSlots; ++sl) {
+          s1 += a.stats[sl * 2 * C + c];
+          s2 += a.stats[sl * 2 * C + C + c];
+        }
+        const double md = s1 / (double)a.R;
+        mean = (float)md;
+        var = (float)fmax(s2 / (double)a.R - md * md, 0.0);
+      } else {
+        mean = a.mmean[c];
+        var = a.mvar[c];
+      }
+      const float rstd = rsqrtf(var + a.eps);
+      const float g = a.gamma ? a.gamma[c] : 1.f;
+      scale = g * rstd;
+      shift = (a.beta ? a.beta[c] : 0.f) - mean * scale;
+      if (first && a.mode == 1) {
+        a.saved[c] = mean;
+        a.saved[C + c] = rstd;
+        if (a.mmean) {
+          a.mmean[c] = a.mmean[c] * a.momentum + mean * (1.f - a.momentum);
+          a.mvar[c] = a.mvar[c] * a.momentum + var * a.bessel * (1.f - a.momentum);
+        }
+      }
+    }
+    if (first && a.zero_buf) {
+#pragma unroll
+      for (int sl = 0; sl < kStatSlots; ++sl) {
+        a.zero_buf[sl * 2 * C + c] = 0.f;
+        a.zero_buf[sl * 2 * C + C + c] = 0.f;
+      }
+    }
+    lsc[threadIdx.x] = scale;
+    lsf[threadIdx.x] = shift;
+  }
+  __syncthreads();
+  if (!t.active) return;
+  const int lc = t.c0 - t.g * t.cg;
+  float sc[8], sf[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = lsc[lc + j];
+    sf[j] = lsf[lc + j];
+  }
+  const long long nr = t.row < a.R ? (a.R - t.row + t.stride - 1) / t.stride : 0;
+  for (long long i = 0; i < nr; i += kBnU) {
+    bf16x8 v[kBnU], r[kBnU];
+#pragma unroll
+    for (int u = 0; u < kBnU; ++u) {
+      if (i + u < nr) {
+        const long long e = (t.row + (i + u) * t.stride) * C + t.c0;
+        v[u] = *reinterpret_cast<const bf16x8*>(a.y + e);
+        if (a.res) r[u] = *reinterpret_cast<const bf16x8*>(a.res + e);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kBnU; ++u) {
+      if (i + u < nr) {
+        const long long e = (t.row + (i + u) * t.stride) * C + t.c0;
+        float ks[8];
+        if (a.drop.rate > 0.f) drop8(a.drop, e, ks);
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float z = bf2f(v[u][j]) * sc[j] + sf[j];
+          if (a.res) z += bf2f(r[u][j]);
+          if (a.relu) z = fmaxf(z, 0.f);
+          if (a.drop.rate > 0.f) z *= ks[j];
+          o[j] = z;
+        }
+        st8(a.out + e, o);
+      }
+    }
+  }
+}
+
+// per-thread coefficients of the tiled backward: sc/sf rebuild z, mu/rs give xhat
+struct BnBwdRegs {
+  float sc[8], sf[8], mu[8], rs[8];
+};
+
+__device__ __forceinline__ void bn_dz8_regs(const BnBwdArgs& a, const BnBwdRegs& k, const bf16x8& yv,
+                                            const bf16x8& dv, const bf16x8& rv, long long e, float* dz, float* xh) {
+  float ks[8];
+  if (a.drop.rate > 0.f) drop8(a.drop, e, ks);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float v = bf2f(yv[j]);
+    const float z = v * k.sc[j] + k.sf[j] + bf2f(rv[j]);
+    float g = bf2f(dv[j]);
+    if (a.drop.rate > 0.f) g *= ks[j];
+    if (a.relu && !(z > 0.f)) g = 0.f;
+    dz[j] = g;
+    xh[j] = (v - k.mu[j]) * k.rs[j];
+  }
+}
+
+__device__ __forceinline__ void bn_bwd_tiled_prologue(const BnBwdArgs& a, const BnTile& t, float* l) {
+  // l: [4][64] sc, sf, mu, rs of the block's channel group
+  if (threadIdx.x < t.cg) {
+    const int c = t.g * t.cg + threadIdx.x;
+    float sc = 1.f, sf = 0.f, mu = 0.f, rs = 1.f;
+    if (a.mode == 1) {
+      mu = a.saved[c];
+      rs = a.saved[a.C + c];
+      const float g = a.gamma ? a.gamma[c] : 1.f;
+      sc = g * rs;
+      sf = (a.beta ? a.beta[c] : 0.f) - mu * sc;
+    }
+    l[threadIdx.x] = sc;
+    l[64 + threadIdx.x] = sf;
+    l[128 + threadIdx.x] = mu;
+    l[192 + threadIdx.x] = rs;
+  }
+}
+
+__device__ __forceinline__ void bn_bwd_regs(const BnTile& t, const float* l, BnBwdRegs& k) {
+  const int lc = t.c0 - t.g * t.cg;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    k.sc[j] = l[lc + j];
+    k.sf[j] = l[64 + lc + j];
+    k.mu[j] = l[128 + lc + j];
+    k.rs[j] = l[192 + lc + j];
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_reduce_tiled_kernel(BnBwdArgs a) {
+  __shared__ float l[256];
+  __shared__ float red[2][2048];  // [rp][cg] partials (rp * cg = 256 / tpr * 8 * tpr = 2048)
+  const BnTile t = bn_tile(a.C);
+  bn_bwd_tiled_prologue(a, t, l);
+  __syncthreads();
+  float r1[8], r2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r1[j] = r2[j] = 0.f;
+  if (t.active) {
+    BnBwdRegs k;
+    bn_bwd_regs(t, l, k);
+    const long long nr = t.row < a.R ? (a.R - t.row + t.stride - 1) / t.stride : 0;
+    for (long long i = 0; i < nr; i += kBnU) {
+      bf16x8 v[kBnU], d[kBnU], r[kBnU];
+#pragma unroll
+      for (int u = 0; u < kBnU; ++u) {
+        if (i + u < nr) {
+          const long long e = (t.row + (i + u) * t.stride) * a.C + t.c0;
+          v[u] = *reinterpret_cast<const bf16x8*>(a.y + e);
+          d[u] = *reinterpret_cast<const bf16x8*>(a.dout + e);
+          if (a.res) {
+            r[u] = *reinterpret_cast<const bf16x8*>(a.res + e);
+          } else {
+            r[u] = zero8();
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kBnU; ++u) {
+        if (i + u < nr) {
+          const long long e = (t.row + (i + u) * t.stride) * a.C + t.c0;
+          float dz[8], xh[8];
+          bn_dz8_regs(a, k, v[u], d[u], r[u], e, dz, xh);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            r1[j] += dz[j];
+            r2[j] += dz[j] * xh[j];
+          }
+        }
+      }
+    }
+    const int slot = (int)(threadIdx.x / t.tpr) * t.cg + (t.c0 - t.g * t.cg);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[0][slot + j] = r1[j];
+      red[1][slot + j] = r2[j];
+    }
+  }
+  __syncthreads();
+  // 256 threads fold the rp rows: thread -> (channel tid % cg, part tid / cg)
+  const int nparts = blockDim.x / t.cg;
+  const int c = threadIdx.x % t.cg, part = threadIdx.x / t.cg;
+  float s1 = 0.f, s2 = 0.f;
+  if (part < nparts)
+    for (int row = part; row < t.rp; row += nparts) {
+      s1 += red[0][row * t.cg + c];
+      s2 += red[1][row * t.cg + c];
+    }
+  __syncthreads();
+  float* fold = &red[0][0];  // reuse: [2][256]
+  fold[threadIdx.x] = part < nparts ? s1 : 0.f;
+  fold[256 + threadIdx.x] = part < nparts ? s2 : 0.f;
+  __syncthreads();
+  if (threadIdx.x < t.cg) {
+    float a1 = 0.f, a2 = 0.f;
+    for (int p = 0; p < nparts; ++p) {
+      a1 += fold[p * t.cg + threadIdx.x];
+      a2 += fold[256 + p * t.cg + threadIdx.x];
+    }
+    float* ds = a.dstats + (size_t)(blockIdx.x % kStatSlots) * 2 * a.C;
+    const int cc = t.g * t.cg + threadIdx.x;
+    atomicAdd(&ds[cc], a1);
+    atomicAdd(&ds[a.C + cc], a2);
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_tiled_kernel(BnBwdArgs a) {
+  __shared__ float l[384];  // sc, sf, mu, rs, k1, k2
+  const BnTile t = bn_tile(a.C);
+  bn_bwd_tiled_prologue(a, t, l);
+  if (threadIdx.x < t.cg) {
+    const int c = t.g * t.cg + threadIdx.x;
+    const bool first = blockIdx.x < a.C / t.cg;
+    float k1 = 0.f, k2 = 0.f;
+    if (a.mode == 1) {
+      float sdz = 0.f, sdx = 0.f;
+#pragma unroll
+      for (int sl = 0; sl < kStatSlots; ++sl) {
+        sdz += a.dstats[sl * 2 * a.C + c];
+        sdx += a.dstats[sl * 2 * a.C + a.C + c];
+      }
+      k1 = sdz / (float)a.R;
+      k2 = sdx / (float)a.R;
+      if (first) {
+        if (a.dbeta) a.dbeta[c] += sdz;
+        if (a.dgamma) a.dgamma[c] += sdx;
+      }
+    }
+    if (first && a.zero_fwd) {
+#pragma unroll
+      for (int sl = 0; sl < kStatSlots; ++sl) {
+        a.zero_fwd[sl * 2 * a.C + c] = 0.0;
+        a.zero_fwd[sl * 2 * a.C + a.C + c] = 0.0;
+      }
+    }
+    l[256 + threadIdx.x] = k1;
+    l[320 + threadIdx.x] = k2;
+  }
+  __syncthreads();
+  if (!t.active) return;
+  BnBwdRegs k;
+  bn_bwd_regs(t, l, k);
+  const int lc = t.c0 - t.g * t.cg;
+  float k1[8], k2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    k1[j] = l[256 + lc + j];
+    k2[j] = l[320 + lc + j];
+  }
+  const long long nr = t.row < a.R ? (a.R - t.row + t.stride - 1) / t.stride : 0;
+  constexpr int U = 2;  // 3-5 streams per row: fewer rows in flight keep the VGPR count low
+  for (long long i = 0; i < nr; i += U) {
+    bf16x8 v[U], d[U], r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (i + u < nr) {
+        const long long e = (t.row + (i + u) * t.stride) * a.C + t.c0;
+        v[u] = *reinterpret_cast<const bf16x8*>(a.y + e);
+        d[u] = *reinterpret_cast<const bf16x8*>(a.dout + e);
+        if (a.res) {
+          r[u] = *reinterpret_cast<const bf16x8*>(a.res + e);
+        } else {
+          r[u] = zero8();
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (i + u < nr) {
+        const long long e = (t.row + (i + u) * t.stride) * a.C + t.c0;
+        float dz[8], xh[8], dx[8];
+        bn_dz8_regs(a, k, v[u], d[u], r[u], e, dz, xh);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dx[j] = a.mode == 1 ? k.sc[j] * (dz[j] - k1[j] - xh[j] * k2[j]) : dz[j];
+        if (a.dx) {
+          if (a.dx_accum) {
+            float o[8];
+            ld8(a.dx + e, o);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dx[j] += o[j];
+          }
+          st8(a.dx + e, dx);
+        }
+        if (a.dres) {
+          if (a.dres_accum) {
+            float o[8];
+            ld8(a.dres + e, o);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dz[j] += o[j];
+          }
+          st8(a.dres + e, dz);
+        }
+      }
+    }
+  }
+}
+
+// rows per block: target `blocks` blocks in total, at least kBnU rows per thread when there is work
+static inline int bn_tiled_grid(long long R, int C, int blocks) {
+  const int cg = C < 64 ? C : 64, tpr = cg / 8, rp = 256 / tpr, ng = C / cg;
+  long long nrb = (R + rp - 1) / rp;            // one row per thread
+  long long want = (blocks + ng - 1) / ng;
+  if (nrb > want) nrb = want;
+  if (nrb < 1) nrb = 1;
+  return (int)(nrb * ng);
+}
+
+// ---------------------------------------------------------------------------------------
 // bias / ReLU backward of a Conv2D/Dense with a fused activation: dz = dout*(out>0),
 // dbias[c] += sum_rows dz.
 __global__ __launch_bounds__(256) void act_bwd_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ out,
@@ -1523,6 +1886,20 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
 }
 
 // drop: rate, seed, iter ptr, iter_offset, layer_id
+// channel-tiled BN path: 8-channel vectors with whole channel groups of <= 64, 16-byte aligned tensors
+static bool bn_tiled_ok(int C, std::initializer_list<const void*> ptrs) {
+  if (C % 8 != 0 || (C > 64 && C % 64 != 0)) return false;
+  for (const void* p : ptrs)
+    if (((uintptr_t)p & 15) != 0) return false;
+  return true;
+}
+
+// streaming grid: ~16K elements per block (prologue amortised), 512..4096 blocks
+static int bn_stream_blocks(long long n) {
+  long long b = n / 16384;
+  return (int)(b < 512 ? 512 : (b > 4096 ? 4096 : b));
+}
+
 TDE_API int tde_bn_fwd(const bf16* y, bf16* out, const bf16* res, long long R, int C, int mode, const double* stats,
                        float* saved, const float* gamma, const float* beta, float eps, float* mmean, float* mvar,
                        float momentum, float bessel, float* zero_buf, int relu, float drop_rate,
@@ -1532,7 +1909,11 @@ TDE_API int tde_bn_fwd(const bf16* y, bf16* out, const bf16* res, long long R, i
   if (R * C >= (1LL << 31)) return -4;
   BnFwdArgs a{y, out, res, R, C, mode, stats, saved, gamma, beta, eps, mmean, mvar, momentum, bessel, zero_buf, relu,
               Drop{drop_rate, seed, iter, iter_offset, layer_id}};
-  bn_fwd_kernel<<<grid_for(R * C, 8), 256, 0, stream>>>(a);
+  if (bn_tiled_ok(C, {y, out, res})) {
+    bn_fwd_tiled_kernel<<<bn_tiled_grid(R, C, bn_stream_blocks(R * C)), 256, 0, stream>>>(a);
+  } else {
+    bn_fwd_kernel<<<grid_for(R * C, 8), 256, 0, stream>>>(a);
+  }
   TDE_LAUNCH_CHECK();
   return 0;
 }
@@ -1546,6 +1927,18 @@ TDE_API int tde_bn_bwd(const bf16* dout, const bf16* y, const bf16* res, long lo
   BnBwdArgs a{dout, y, res, R, C, mode, saved, gamma, beta, relu, Drop{drop_rate, seed, iter, iter_offset, layer_id},
               dstats, dx, dx_accum, dres, dres_accum, dgamma, dbeta, zero_fwd};
   if (R * C >= (1LL << 31)) return -4;
+  if (bn_tiled_ok(C, {dout, y, res, dx, dres})) {
+    if (mode == 1) {
+      // each block ends with 2*min(C,64) global atomics: a moderate grid, deep per-thread ILP
+      long long want = R * C / 32768;
+      want = want < 256 ? 256 : (want > 1024 ? 1024 : want);
+      bn_bwd_reduce_tiled_kernel<<<bn_tiled_grid(R, C, (int)want), 256, 0, stream>>>(a);
+      TDE_LAUNCH_CHECK();
+    }
+    bn_bwd_apply_tiled_kernel<<<bn_tiled_grid(R, C, bn_stream_blocks(R * C)), 256, 0, stream>>>(a);
+    TDE_LAUNCH_CHECK();
+    return 0;
+  }
   const int g = grid_for(R * C, 8);
   if (mode == 1) {
     // Reduction grid: <= 2 blocks per CU (each block ends with 2*C global atomics, so more blocks only

@@ -131,7 +131,9 @@ def test_dense_fwd_dgrad_wgrad(B, fin, out, relu):
 
 
 @pytest.mark.parametrize("R,C,relu,res,fused", [(4 * 784, 6, True, False, True), (128, 200, True, False, False),
-                                                (2 * 64, 64, True, True, True), (50, 24, False, False, True)])
+                                                (2 * 64, 64, True, True, True), (50, 24, False, False, True),
+                                                (3136, 512, True, True, True), (1000, 128, False, True, False),
+                                                (300, 8, True, False, True)])
 def test_batchnorm_fwd_bwd(R, C, relu, res, fused):
     from tensorflow_distributed_example_amd.ops import layer_ops as O
     y = _r(R, C, seed=7, scale=2.0) + 0.5
@@ -178,9 +180,10 @@ def test_batchnorm_fwd_bwd(R, C, relu, res, fused):
     assert stats.abs().max().item() == 0.0
 
 
-def test_dropout_mask_regenerated_in_backward():
+@pytest.mark.parametrize("C", [200, 64])   # flat and channel-tiled kernels
+def test_dropout_mask_regenerated_in_backward(C):
     from tensorflow_distributed_example_amd.ops import layer_ops as O
-    R, C = 512, 200
+    R = 512
     y = _r(R, C, seed=10).abs() + 0.1
     it = torch.tensor([5], dtype=torch.int64, device=DEV)
     d = O.DropSpec(0.5, 1234, it, 3)
@@ -202,6 +205,32 @@ def test_dropout_mask_regenerated_in_backward():
     O.bn_fwd(y, out2, R, C, mode=0, relu=True, drop=d, iter_offset=0)
     torch.cuda.synchronize()
     assert not torch.equal(out2 != 0, kept)
+
+
+@pytest.mark.parametrize("C", [200, 64, 256])   # flat and channel-tiled kernels
+def test_bn_bwd_accumulates(C):
+    """dx_accum / dres_accum add into the existing gradient buffers (multi-consumer tensors)."""
+    from tensorflow_distributed_example_amd.ops import layer_ops as O
+    R = 384
+    y, r, dout = _r(R, C, seed=20) + 0.3, _r(R, C, seed=21), _r(R, C, seed=22)
+    gamma, beta = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.1
+    stats = _stats_buf(C)
+    O.colstats(y, R, C, stats)
+    saved = torch.zeros(2 * C, device=DEV)
+    dstats = torch.zeros(2 * SLOTS * C, device=DEV)
+    out = torch.zeros(R, C, dtype=bf, device=DEV)
+    O.bn_fwd(y, out, R, C, mode=1, stats=stats, saved=saved, gamma=gamma, beta=beta, eps=1e-3, zero_buf=dstats,
+             res=r, relu=True)
+    fresh = [torch.zeros(R, C, dtype=bf, device=DEV) for _ in range(2)]
+    base = [_r(R, C, seed=23), _r(R, C, seed=24)]
+    acc = [b.clone() for b in base]
+    for (dx, dres, accum) in ((fresh[0], fresh[1], False), (acc[0], acc[1], True)):
+        dstats.zero_()
+        O.bn_bwd(dout, y, R, C, mode=1, saved=saved, gamma=gamma, beta=beta, res=r, relu=True, dstats=dstats,
+                 dx=dx, dx_accum=accum, dres=dres, dres_accum=accum)
+    torch.cuda.synchronize()
+    for f, b, a in zip(fresh, base, acc):
+        assert _rel(a.float(), f.float() + b.float()) < 1e-2
 
 
 @pytest.mark.parametrize("H,W,k,s,pad,C", [(112, 112, 3, 2, "same", 16), (26, 26, 2, 2, "valid", 32),
