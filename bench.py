@@ -67,7 +67,7 @@ def main():
             raise SystemExit("--gpus N>1 must be launched with torchrun --nproc-per-node N")
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if torch.cuda.is_available():
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(local_rank % torch.cuda.device_count())  # ranks > GPUs only in rehearsals
     tde.backend.set_random_seed(1234)
     strategy = tde.distribute.MultiWorkerMirroredStrategy()
     n = strategy.num_replicas_in_sync
@@ -122,6 +122,15 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     logs = tde.metrics.logs_from(prog.global_metrics(), ["accuracy"])
+    comm = strategy.comm
+    ar = {"XgmiCommunicator": "xgmi", "RcclCommunicator": "rccl", "TorchDistCommunicator": "gloo"}.get(
+        type(comm).__name__, "none")
+    if world > 1:  # data-parallel invariant (outside the timed region): every replica bit-identical
+        from tensorflow_distributed_example_amd.utils import debug
+        fps = debug.replica_fingerprints(model)
+        same = all(f[2:] == fps[0][2:] for f in fps)
+        if strategy.worker_index == 0:
+            print(f"[bench] replicas_identical={same}", file=sys.stderr, flush=True)
     ms = elapsed / a.steps * 1e3
     ips = GB * a.steps / elapsed
     if strategy.worker_index == 0:
@@ -135,6 +144,7 @@ def main():
             "config": {"model": a.model, "global_batch": GB, "seq_len": None, "image_shape": list(img),
                        "per_gpu_batch": B, "parallelism": f"dp{n}", "strategy": "MultiWorkerMirroredStrategy",
                        "steps_per_execution": spe, "optimizer": f"SGD(lr={a.lr})", "plan": prog.plan_kind,
+                       "allreduce": ar,
                        "hipgraph": prog.use_graph}}), flush=True)
 
 

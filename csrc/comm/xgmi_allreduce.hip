@@ -1,0 +1,292 @@
+// Single-node gradient all-reduce over xGMI peer memory (one process per GPU).
+//
+// MI355X nodes are a full xGMI mesh: every GPU has a point-to-point link to each of
+// its 7 peers.  A ring all-reduce keeps one outgoing link busy per step and pays
+// 2(N-1) latency hops; at the MNIST bucket sizes of the reference models
+// (1.0-1.4 MB fp32) that latency, not bandwidth, is the
+// step-time cost.  This is the "optional one-shot xGMI P2P all-reduce for small
+// buckets" of SURVEY.md §7.1/§7.6, in its two-shot (reduce-scatter + all-gather)
+// push form, so every phase drives all N-1 links at once and crosses the fabric
+// exactly once:
+//
+//   phase 1  block c of rank r stores chunk c of every slice s of its gradient
+//            straight into rank s's receive area   in[p][r][c]   (remote stores)
+//            and raises flag1[p][r][c] on rank s.
+//   phase 2  block c of rank s waits for flag1[p][*][c], sums the N contributions
+//            of its own slice in rank order 0..N-1 (all reads are LOCAL HBM), and
+//            stores the reduced chunk into out[p][s][c] of every rank, raising
+//            flag2[p][s][c] there.
+//   phase 3  block c of every rank waits for flag2[p][*][c] and copies the reduced
+//            chunks back into the gradient bucket.
+//
+// Block c only ever waits for block c of its peers, so there is no grid-wide
+// barrier; the grid (<= kXgMaxBlocks workgroups) is resident on the 256 CUs at once.
+// Every slice is reduced by exactly one rank in a fixed order, so all replicas end
+// bit-identical (the DP invariant checked by utils/debug.ReplicaConsistencyCheck).
+//
+// The shared window of each rank is one IPC-exported allocation:
+//   [flags: 2 parities x 2 phases x kXgMaxRanks x kXgMaxBlocks u32] [in: 2 x cap] [out: 2 x cap]
+// Flags carry the call's epoch (a device-side counter bumped on the stream after the
+// kernel, so hipGraph replays advance it without the host), never need resetting,
+// and the parity double-buffers the areas so call k+1 can start writing while a slow
+// peer still copies out call k (a rank can only reach call k+2 after every peer has
+// signalled phase 1 of call k+1, i.e. finished call k).  Waits are bounded: a peer
+// that never arrives (dead process, broken link) sets the error word (host-mapped
+// memory, read by the host with no HIP call) after `timeout_ticks` of the 100 MHz
+// wall clock instead of hanging the GPU; check_health() polls it and aborts, like
+// ncclCommGetAsyncError.
+//
+// Memory ordering (MI355X_MICROARCH.md § inter-workgroup visibility, applied at
+// system scope).  Producer: payload stores -> every storing wave `s_waitcnt
+// vmcnt(0)` -> workgroup barrier -> (cached window only: one system-scope release
+// = L2 writeback) -> relaxed system-scope flag store.  The default window is
+// fine-grained uncached memory (MTYPE UC), whose stores do not stay in any L2, so
+// the release is skipped.  Consumer: ONE lane polls the flags relaxed (with
+// s_sleep), then ONE system-scope acquire (L1/L2 invalidate), `s_waitcnt
+// vmcnt(0)`, workgroup barrier, plain loads.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "tde_common.h"
+
+namespace tde {
+
+constexpr int kXgMaxRanks = 8;
+constexpr int kXgMaxBlocks = 128;
+constexpr int kXgThreads = 256;
+constexpr size_t kXgFlagWords = 2 * 2 * kXgMaxRanks * kXgMaxBlocks;
+constexpr size_t kXgFlagBytes = kXgFlagWords * 4;
+
+struct XgArgs {
+  float* grad;                    // local gradient bucket (in/out), M floats
+  char* peer[kXgMaxRanks];        // every rank's window base, mapped in this process
+  uint32_t* epoch;                // local device word: calls completed
+  uint32_t* err;                  // host-mapped error word (bit0 phase-1 wait, bit1 phase-2 wait timed out)
+  int rank, nranks;
+  long long M;                    // elements
+  long long L;                    // slice length (multiple of 4 * gridDim.x)
+  long long chunk;                // chunk length within a slice (multiple of 4)
+  long long cap;                  // elements per area (>= nranks * L)
+  long long timeout_ticks;
+};
+
+__device__ __forceinline__ uint32_t* flag_ptr(char* base, int parity, int phase, int src, int blk) {
+  return reinterpret_cast<uint32_t*>(base) + (((parity * 2 + phase) * kXgMaxRanks + src) * kXgMaxBlocks + blk);
+}
+// which 0 = in (contributions), 1 = out (reduced slices)
+__device__ __forceinline__ float* area(char* base, int which, int parity, long long cap) {
+  return reinterpret_cast<float*>(base + kXgFlagBytes) + ((size_t)which * 2 + parity) * (size_t)cap;
+}
+
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Makes this block's stores of the phase visible, then raises the phase flag of block
+// `blk` on every rank (threads 0..N-1, one flag each).
+template <bool UNCACHED>
+__device__ __forceinline__ void publish(char* const* peer, int nranks, int parity, int phase, int src, int blk,
+                                        uint32_t epoch) {
+  drain_stores();
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < nranks) {
+    if (!UNCACHED) {
+      __atomic_thread_fence(__ATOMIC_RELEASE);   // system scope: L2 writeback
+      drain_stores();
+    }
+    __hip_atomic_store(flag_ptr(peer[t], parity, phase, src, blk), epoch, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// Thread 0 waits until every rank's flag of (parity, phase, blk) equals `epoch`.
+__device__ __forceinline__ void await(char* base, int parity, int phase, int nranks, int blk, uint32_t epoch,
+                                      long long timeout, uint32_t* err, uint32_t bit) {
+  if (threadIdx.x == 0) {
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    bool ok = true;
+    for (int s = 0; s < nranks && ok; ++s) {
+      uint32_t* f = flag_ptr(base, parity, phase, s, blk);
+      while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+        __builtin_amdgcn_s_sleep(2);
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+          ok = false;
+          break;
+        }
+      }
+    }
+    if (!ok) __hip_atomic_fetch_or(err, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);   // system scope: drop stale L1/L2 lines
+    drain_stores();
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void copy_chunk(float* dst, const float* src, long long n, bool vec) {
+  const int tid = threadIdx.x;
+  if (vec) {
+    const long long nv = n >> 2;
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    for (long long i = tid; i < nv; i += kXgThreads) d4[i] = s4[i];
+    for (long long i = (nv << 2) + tid; i < n; i += kXgThreads) dst[i] = src[i];
+  } else {
+    for (long long i = tid; i < n; i += kXgThreads) dst[i] = src[i];
+  }
+}
+
+template <bool UNCACHED>
+__global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgArgs a) {
+  const int blk = blockIdx.x, tid = threadIdx.x;
+  const uint32_t epoch = a.epoch[0] + 1;
+  const int parity = epoch & 1;
+  const int N = a.nranks, r = a.rank;
+  const long long M = a.M, L = a.L, CH = a.chunk, cap = a.cap;
+  const long long c0 = (long long)blk * CH;
+
+  // ---- phase 1: push chunk `blk` of every slice s to rank s
+  for (int s = 0; s < N; ++s) {
+    const long long g0 = (long long)s * L + c0;
+    const long long n = max(0LL, min(CH, M - g0));
+    copy_chunk(area(a.peer[s], 0, parity, cap) + (size_t)r * L + c0, a.grad + g0, n, (g0 & 3) == 0);
+  }
+  publish<UNCACHED>(a.peer, N, parity, 0, r, blk, epoch);
+
+  // ---- phase 2: reduce own slice chunk from local HBM, push the result to every rank
+  await(a.peer[r], parity, 0, N, blk, epoch, a.timeout_ticks, a.err, 1u);
+  {
+    const long long g0 = (long long)r * L + c0;
+    const long long n = max(0LL, min(CH, M - g0));
+    const float* in = area(a.peer[r], 0, parity, cap) + c0;
+    const long long nv = n >> 2;   // area offsets are multiples of 4 elements
+    for (long long i = tid; i < nv; i += kXgThreads) {
+      float4 acc = reinterpret_cast<const float4*>(in)[i];
+      for (int s = 1; s < N; ++s) {
+        const float4 v = reinterpret_cast<const float4*>(in + (size_t)s * L)[i];
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+      for (int p = 0; p < N; ++p)
+        reinterpret_cast<float4*>(area(a.peer[p], 1, parity, cap) + (size_t)r * L + c0)[i] = acc;
+    }
+    for (long long i = (nv << 2) + tid; i < n; i += kXgThreads) {
+      float acc = in[i];
+      for (int s = 1; s < N; ++s) acc += in[(size_t)s * L + i];
+      for (int p = 0; p < N; ++p) area(a.peer[p], 1, parity, cap)[(size_t)r * L + c0 + i] = acc;
+    }
+  }
+  publish<UNCACHED>(a.peer, N, parity, 1, r, blk, epoch);
+
+  // ---- phase 3: gather every reduced slice chunk back into the bucket
+  await(a.peer[r], parity, 1, N, blk, epoch, a.timeout_ticks, a.err, 2u);
+  const float* out = area(a.peer[r], 1, parity, cap);
+  for (int s = 0; s < N; ++s) {
+    const long long g0 = (long long)s * L + c0;
+    const long long n = max(0LL, min(CH, M - g0));
+    copy_chunk(a.grad + g0, out + (size_t)s * L + c0, n, (g0 & 3) == 0);
+  }
+}
+
+// Advances the epoch after every block of the all-reduce kernel finished (stream order).
+__global__ void xgmi_epoch_bump_kernel(uint32_t* epoch) {
+  if (threadIdx.x == 0) epoch[0] += 1;
+}
+
+// Slice length for M elements over `nranks` ranks and `nblocks` chunks.
+inline long long xg_slice(long long M, int nranks, int nblocks) {
+  const long long q = 4LL * nblocks;
+  return ((M + nranks - 1) / nranks + q - 1) / q * q;
+}
+
+}  // namespace tde
+
+using namespace tde;
+
+// Area capacity (elements) for buckets of up to max_elems elements: nranks * L <=
+// max_elems + nranks * 4 * nblocks for every admissible nranks/nblocks.
+static long long xg_cap(long long max_elems) {
+  return max_elems + (long long)kXgMaxRanks * 4 * kXgMaxBlocks;
+}
+
+TDE_API size_t tde_xgmi_window_bytes(long long max_elems) {
+  return kXgFlagBytes + 4 * (size_t)xg_cap(max_elems) * sizeof(float);
+}
+TDE_API int tde_xgmi_max_ranks() { return kXgMaxRanks; }
+TDE_API int tde_xgmi_max_blocks() { return kXgMaxBlocks; }
+TDE_API int tde_xgmi_ipc_handle_bytes() { return (int)sizeof(hipIpcMemHandle_t); }
+
+// Allocates this rank's window (fine-grained / uncached unless `uncached`=0), the
+// local epoch word and the host-mapped error word, and returns the window's IPC handle.
+TDE_API int tde_xgmi_alloc(int device, long long max_elems, int uncached, void** window, void** epoch, void** err,
+                           char* handle_out) {
+  if (hipSetDevice(device) != hipSuccess) return -100;
+  const size_t bytes = tde_xgmi_window_bytes(max_elems);
+  hipError_t e = uncached ? hipExtMallocWithFlags(window, bytes, hipDeviceMallocUncached) : hipMalloc(window, bytes);
+  if (e != hipSuccess) return (int)e;
+  if ((e = hipMemset(*window, 0, bytes)) != hipSuccess) return (int)e;
+  if ((e = hipMalloc(epoch, sizeof(uint32_t))) != hipSuccess) return (int)e;
+  if ((e = hipMemset(*epoch, 0, sizeof(uint32_t))) != hipSuccess) return (int)e;
+  if ((e = hipHostMalloc(err, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+    return (int)e;
+  *(volatile uint32_t*)*err = 0;
+  hipIpcMemHandle_t h;
+  if ((e = hipIpcGetMemHandle(&h, *window)) != hipSuccess) return (int)e;
+  memcpy(handle_out, &h, sizeof(h));
+  return (int)hipDeviceSynchronize();
+}
+
+TDE_API int tde_xgmi_open(int device, const char* handle, void** mapped) {
+  if (hipSetDevice(device) != hipSuccess) return -100;
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof(h));
+  return (int)hipIpcOpenMemHandle(mapped, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+TDE_API int tde_xgmi_close(void* mapped) { return (int)hipIpcCloseMemHandle(mapped); }
+
+TDE_API int tde_xgmi_free(void* window, void* epoch, void* err) {
+  hipError_t e1 = window ? hipFree(window) : hipSuccess;
+  hipError_t e2 = epoch ? hipFree(epoch) : hipSuccess;
+  hipError_t e3 = err ? hipHostFree(err) : hipSuccess;
+  return e1 != hipSuccess ? (int)e1 : e2 != hipSuccess ? (int)e2 : (int)e3;
+}
+
+// Error bits of this rank (host read of the mapped word; no HIP call, never blocks).
+TDE_API int tde_xgmi_error(void* err) { return (int)*(volatile uint32_t*)err; }
+
+// Calls completed (synchronous device read; tests/diagnostics only).
+TDE_API long long tde_xgmi_epoch(void* epoch) {
+  uint32_t h = 0;
+  if (hipMemcpy(&h, epoch, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return (long long)h;
+}
+
+// In-place SUM all-reduce of `grad` (M fp32 elements, M <= the window's max_elems).
+TDE_API int tde_xgmi_all_reduce(float* grad, long long M, long long max_elems, void* const* peers, void* epoch,
+                                void* err, int rank, int nranks, int nblocks, int uncached, long long timeout_ticks,
+                                hipStream_t stream) {
+  if (nranks < 1 || nranks > kXgMaxRanks || rank < 0 || rank >= nranks) return -1;
+  if (M < 0 || M > max_elems) return -2;
+  if (((uintptr_t)grad & 15) != 0) return -4;
+  if (nblocks < 1) nblocks = 1;
+  if (nblocks > kXgMaxBlocks) nblocks = kXgMaxBlocks;
+  XgArgs a;
+  memset(&a, 0, sizeof(a));
+  a.grad = grad;
+  for (int i = 0; i < nranks; ++i) a.peer[i] = (char*)peers[i];
+  a.epoch = (uint32_t*)epoch;
+  a.err = (uint32_t*)err;
+  a.rank = rank;
+  a.nranks = nranks;
+  a.M = M;
+  a.L = xg_slice(M, nranks, nblocks);
+  a.chunk = a.L / nblocks;
+  a.cap = xg_cap(max_elems);
+  a.timeout_ticks = timeout_ticks;
+  if (a.L * nranks > a.cap) return -3;   // areas hold nranks slices
+  if (uncached) hipLaunchKernelGGL(xgmi_allreduce_kernel<true>, dim3(nblocks), dim3(kXgThreads), 0, stream, a);
+  else hipLaunchKernelGGL(xgmi_allreduce_kernel<false>, dim3(nblocks), dim3(kXgThreads), 0, stream, a);
+  TDE_LAUNCH_CHECK();
+  hipLaunchKernelGGL(xgmi_epoch_bump_kernel, dim3(1), dim3(64), 0, stream, a.epoch);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}

@@ -27,7 +27,8 @@ CSRC = ROOT / "csrc"
 LIBDIR = PKG / "_lib"
 OBJDIR = ROOT / "build" / "obj"
 
-HIP_SOURCES = sorted((CSRC / "kernels").glob("*.hip")) + [CSRC / "comm" / "rccl_comm.cpp"]
+HIP_SOURCES = sorted((CSRC / "kernels").glob("*.hip")) + [CSRC / "comm" / "rccl_comm.cpp",
+                                                           CSRC / "comm" / "xgmi_allreduce.hip"]
 HOST_DIRS = ["host", "io", "ps"]
 
 

@@ -78,6 +78,18 @@ _HIP_PROTOS = {
     "tde_nccl_reduce_scatter": (i32, [p, p, sz, i32, i32, p, p]),
     "tde_nccl_send": (i32, [p, sz, i32, i32, p, p]),
     "tde_nccl_recv": (i32, [p, sz, i32, i32, p, p]),
+    # single-node xGMI peer-memory all-reduce (csrc/comm/xgmi_allreduce.hip)
+    "tde_xgmi_window_bytes": (sz, [i64]),
+    "tde_xgmi_max_ranks": (i32, []),
+    "tde_xgmi_max_blocks": (i32, []),
+    "tde_xgmi_ipc_handle_bytes": (i32, []),
+    "tde_xgmi_alloc": (i32, [i32, i64, i32, C.POINTER(p), C.POINTER(p), C.POINTER(p), C.c_char_p]),
+    "tde_xgmi_open": (i32, [i32, C.c_char_p, C.POINTER(p)]),
+    "tde_xgmi_close": (i32, [p]),
+    "tde_xgmi_free": (i32, [p, p, p]),
+    "tde_xgmi_error": (i32, [p]),
+    "tde_xgmi_epoch": (i64, [p]),
+    "tde_xgmi_all_reduce": (i32, [p, i64, i64, p, p, p, i32, i32, i32, i32, i64, p]),
 }
 
 _EXTRA_HIP_PROTOS: dict = {}

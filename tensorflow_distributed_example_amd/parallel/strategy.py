@@ -297,10 +297,19 @@ class MultiWorkerMirroredStrategy(Strategy):
     def _rccl(devs, topo, world, n_local):
         if world == 1:
             return CM.RcclCommunicator(devs)
-        import torch.distributed as dist
-        obj = [CM.RcclCommunicator.unique_id() if topo.rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        return CM.RcclCommunicator(devs, rank0=topo.rank * n_local, nranks=world * n_local, unique_id=obj[0])
+        if os.environ.get("TDE_RCCL", "1") == "0":
+            # no RCCL clique (e.g. several ranks sharing one GPU in a rehearsal): gloo carries the
+            # non-gradient collectives, the xGMI kernel the gradient bucket
+            base = CM.TorchDistCommunicator(n_local)
+        else:
+            import torch.distributed as dist
+            obj = [CM.RcclCommunicator.unique_id() if topo.rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            base = CM.RcclCommunicator(devs, rank0=topo.rank * n_local, nranks=world * n_local, unique_id=obj[0])
+        if n_local == 1:
+            # one GPU per process on one xGMI node: the gradient bucket takes the peer-memory kernel
+            return CM.maybe_xgmi(base, devs[0], topo.rank, world)
+        return base
 
     def barrier(self):
         if self.num_workers > 1:

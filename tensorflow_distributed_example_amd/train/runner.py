@@ -228,6 +228,7 @@ class Program:
         """SUM of the metric accumulators over ALL replicas (SyncOnRead SUM, C3/C5)."""
         if self.comm is None:
             return self.local_metrics()
+        self.comm.check_health()   # surfaces a timed-out peer wait of the xGMI all-reduce
         bufs = [p.metrics.clone() for p in self.plans]
         self.comm.all_reduce_(bufs)
         for d in self.devices:
