@@ -26,8 +26,8 @@
 //
 // The shared window of each rank is one IPC-exported allocation:
 //   [flags: 2 parities x 2 phases x kXgMaxRanks x kXgMaxBlocks u32] [in: 2 x cap] [out: 2 x cap]
-// Flags carry the call's epoch (a device-side counter bumped on the stream after the
-// kernel, so hipGraph replays advance it without the host), never need resetting,
+// Flags carry the call's epoch (a device-side counter the call's last finishing block
+// advances, so hipGraph replays advance it without the host), never need resetting,
 // and the parity double-buffers the areas so call k+1 can start writing while a slow
 // peer still copies out call k (a rank can only reach call k+2 after every peer has
 // signalled phase 1 of call k+1, i.e. finished call k).  Waits are bounded: a peer
@@ -61,7 +61,7 @@ constexpr size_t kXgFlagBytes = kXgFlagWords * 4;
 struct XgArgs {
   float* grad;                    // local gradient bucket (in/out), M floats
   char* peer[kXgMaxRanks];        // every rank's window base, mapped in this process
-  uint32_t* epoch;                // local device word: calls completed
+  uint32_t* epoch;                // local device words: [0] calls completed, [1] blocks finished (this call)
   uint32_t* err;                  // host-mapped error word (bit0 phase-1 wait, bit1 phase-2 wait timed out)
   int rank, nranks;
   long long M;                    // elements
@@ -184,11 +184,15 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgArgs a) {
     const long long n = max(0LL, min(CH, M - g0));
     copy_chunk(a.grad + g0, out + (size_t)s * L + c0, n, (g0 & 3) == 0);
   }
-}
-
-// Advances the epoch after every block of the all-reduce kernel finished (stream order).
-__global__ void xgmi_epoch_bump_kernel(uint32_t* epoch) {
-  if (threadIdx.x == 0) epoch[0] += 1;
+  // the last block to finish advances the epoch (every block read it at its start) and re-arms
+  // the arrival counter epoch[1] for the next call
+  if (tid == 0) {
+    const uint32_t arrived = __hip_atomic_fetch_add(&a.epoch[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (arrived == gridDim.x - 1) {
+      __hip_atomic_store(&a.epoch[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&a.epoch[0], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // Slice length for M elements over `nranks` ranks and `nblocks` chunks.
@@ -223,8 +227,8 @@ TDE_API int tde_xgmi_alloc(int device, long long max_elems, int uncached, void**
   hipError_t e = uncached ? hipExtMallocWithFlags(window, bytes, hipDeviceMallocUncached) : hipMalloc(window, bytes);
   if (e != hipSuccess) return (int)e;
   if ((e = hipMemset(*window, 0, bytes)) != hipSuccess) return (int)e;
-  if ((e = hipMalloc(epoch, sizeof(uint32_t))) != hipSuccess) return (int)e;
-  if ((e = hipMemset(*epoch, 0, sizeof(uint32_t))) != hipSuccess) return (int)e;
+  if ((e = hipMalloc(epoch, 2 * sizeof(uint32_t))) != hipSuccess) return (int)e;
+  if ((e = hipMemset(*epoch, 0, 2 * sizeof(uint32_t))) != hipSuccess) return (int)e;
   if ((e = hipHostMalloc(err, sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
     return (int)e;
   *(volatile uint32_t*)*err = 0;
@@ -285,8 +289,6 @@ TDE_API int tde_xgmi_all_reduce(float* grad, long long M, long long max_elems, v
   if (a.L * nranks > a.cap) return -3;   // areas hold nranks slices
   if (uncached) hipLaunchKernelGGL(xgmi_allreduce_kernel<true>, dim3(nblocks), dim3(kXgThreads), 0, stream, a);
   else hipLaunchKernelGGL(xgmi_allreduce_kernel<false>, dim3(nblocks), dim3(kXgThreads), 0, stream, a);
-  TDE_LAUNCH_CHECK();
-  hipLaunchKernelGGL(xgmi_epoch_bump_kernel, dim3(1), dim3(64), 0, stream, a.epoch);
   TDE_LAUNCH_CHECK();
   return 0;
 }

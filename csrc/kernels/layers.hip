@@ -1831,7 +1831,9 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     if (auto_splits) {  // weight grads: f32 atomics, fill the chip with >= ~4 workgroups per CU
       const long long t = (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
       long long sp = (1024 + t - 1) / t;
-      const long long maxs = ktiles / 2 > 0 ? ktiles / 2 : 1;
+      // >= 8 k-tiles per split: every split ends in BM x BN f32 atomics, and with the skinny weight
+      // grads of narrow layers (N = 12, 24) hundreds of 2-k-tile splits spend their time in atomics
+      const long long maxs = ktiles / 8 > 0 ? ktiles / 8 : 1;
       splits = (int)(sp < maxs ? sp : maxs);
       if (splits < 1) splits = 1;
       p.ktiles_per_split = (ktiles + splits - 1) / splits;

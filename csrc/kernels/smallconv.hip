@@ -8,7 +8,8 @@
 //           + the per-channel BN statistics of the stored bf16 values (wave shuffles -> LDS -> f64 atomics)
 //  * dgrad: dx[p][0..C) = sum over the taps that hit p (stride phase computed, no zero taps)
 //           of dy[o][co] * W[kh][kw][0..C)[co]
-// Weight gradients stay on the MFMA implicit GEMM (long pixel reductions suit split-K there).
+//  * wgrad: filters small enough for registers (K*Co <= 128, Model B's first conv) reduce over all
+//           pixels per thread; wider weight gradients stay on the MFMA implicit GEMM (split-K).
 #include "tde_common.h"
 
 namespace tde {
@@ -151,6 +152,65 @@ __global__ __launch_bounds__(256) void smallconv_dgrad_kernel(const bf16* __rest
   }
 }
 
+
+// Weight gradient of a layer whose whole filter fits in registers (K = KH*KW*C <= 128/CO, e.g. Model B's
+// Conv2D(1->6, 3x3): K = 9): dW[k][co] += sum_p x_patch(p)[k] * dy[p][co].  The implicit GEMM would run
+// M = K rows of a 64-row MFMA tile with scalar C = 1 gathers over a 100k-pixel reduction; here each thread
+// keeps all K x CO partial sums in registers over a grid-stride run of pixels, the block folds them with
+// DPP row reductions + LDS, and one f32 atomic per (k, co) per block lands in the gradient bucket.
+template <int CO>
+__global__ __launch_bounds__(256) void smallconv_wgrad_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                              float* __restrict__ dw, SGeo g) {
+  constexpr int KMAX = 128 / CO;
+  __shared__ float red[4][KMAX * CO];
+  const int K = g.KH * g.KW * g.C;
+  float acc[KMAX][CO];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+#pragma unroll
+    for (int c = 0; c < CO; ++c) acc[k][c] = 0.f;
+  const int npix = g.B * g.Ho * g.Wo;
+  const int hw = g.Ho * g.Wo;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += gridDim.x * blockDim.x) {
+    const int b = p / hw, r = p - b * hw;
+    const int oh = r / g.Wo, ow = r - oh * g.Wo;
+    const int y0 = oh * g.sh - g.pt, x0 = ow * g.sw - g.pl;
+    float d[CO];
+    const bf16* dp = dy + (long long)p * g.Co;
+#pragma unroll
+    for (int c = 0; c < CO; ++c) d[c] = c < g.Co ? bf2f(dp[c]) : 0.f;
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      if (k < K) {
+        const int ci = k % g.C, t = k / g.C;
+        const int kw = t % g.KW, kh = t / g.KW;
+        const int ih = y0 + kh, iw = x0 + kw;
+        float xv = 0.f;
+        if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
+          xv = bf2f(x[(((long long)b * g.H + ih) * g.W + iw) * g.C + ci]);
+#pragma unroll
+        for (int c = 0; c < CO; ++c) acc[k][c] = fmaf(xv, d[c], acc[k][c]);
+      }
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    if (k < K) {
+#pragma unroll
+      for (int c = 0; c < CO; ++c) {
+        const float v = rows4_sum(row16_sum(acc[k][c]));
+        if (lane == 0) red[wave][k * CO + c] = v;
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < K * CO; i += blockDim.x) {
+    const int k = i / CO, c = i - k * CO;
+    if (c < g.Co) atomicAdd(&dw[k * g.Co + c], (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]));
+  }
+}
+
 }  // namespace tde
 
 using namespace tde;
@@ -196,6 +256,29 @@ TDE_API int tde_smallconv_dgrad(const bf16* dy, const bf16* w, bf16* dx, int acc
   }
   TDE_LAUNCH_CHECK();
   return 0;
+}
+
+// dw: f32 [KH*KW*C][Co] slice of the gradient bucket (accumulated with atomics)
+TDE_API int tde_smallconv_wgrad(const bf16* x, const bf16* dy, float* dw, const int* geo, hipStream_t stream) {
+  const SGeo g = sgeo(geo);
+  const int co = round8(g.Co);
+  const int K = g.KH * g.KW * g.C;
+  if (co > 32 || K * co > 128) return -1;
+  if ((long long)g.B * g.H * g.W * g.C >= (1LL << 31) || (long long)g.B * g.Ho * g.Wo * g.Co >= (1LL << 31)) return -4;
+  const int npix = g.B * g.Ho * g.Wo;
+  int grid = (npix + 256 * 2 - 1) / (256 * 2);   // ~2 pixels per thread, <= one block per CU
+  grid = grid < 1 ? 1 : (grid > 256 ? 256 : grid);
+  switch (co) {
+    case 8: smallconv_wgrad_kernel<8><<<grid, 256, 0, stream>>>(x, dy, dw, g); break;
+    case 16: smallconv_wgrad_kernel<16><<<grid, 256, 0, stream>>>(x, dy, dw, g); break;
+    default: smallconv_wgrad_kernel<32><<<grid, 256, 0, stream>>>(x, dy, dw, g); break;
+  }
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+TDE_API int tde_smallconv_wgrad_ok(int C, int Co, int KH, int KW) {
+  return round8(Co) <= 32 && KH * KW * C * round8(Co) <= 128;
 }
 
 TDE_API int tde_smallconv_ok(int C, int Co, int KH, int KW, int dgrad) {

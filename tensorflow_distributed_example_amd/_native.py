@@ -58,6 +58,8 @@ _HIP_PROTOS = {
     "tde_smallconv_fwd": (i32, [p, p, p, i32, p, p, p, p]),
     "tde_smallconv_dgrad": (i32, [p, p, p, i32, p, p]),
     "tde_smallconv_ok": (i32, [i32, i32, i32, i32, i32]),
+    "tde_smallconv_wgrad": (i32, [p, p, p, p, p]),
+    "tde_smallconv_wgrad_ok": (i32, [i32, i32, i32, i32]),
     "tde_im2col": (i32, [p, p, i32, p, p, p, p]),
     # RCCL
     "tde_nccl_version": (i32, []),

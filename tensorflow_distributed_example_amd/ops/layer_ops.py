@@ -217,6 +217,19 @@ def smallconv_dgrad(dy, Wrow, dx, g: ConvGeom, accum=False):
     N.check(N.hip().tde_smallconv_dgrad(_P(dy), _P(Wrow), _P(dx), int(accum), g.carray(), _s()), "tde_smallconv_dgrad")
 
 
+def smallconv_wgrad_ok(g: ConvGeom):
+    return bool(N.hip().tde_smallconv_wgrad_ok(g.C, g.Co, g.KH, g.KW))
+
+
+def smallconv_wgrad(x, dy, dW, g: ConvGeom):
+    """dW[KH,KW,C,Co] (f32) += sum_pixels x (x) dy for filters whose K*Co partial sums fit in registers."""
+    _bf(x, g.B * g.H * g.W * g.C, "smallconv_wgrad x")
+    _bf(dy, g.B * g.Ho * g.Wo * g.Co, "smallconv_wgrad dy")
+    _f32(dW, g.K * g.Co, "smallconv_wgrad dW")
+    _req(smallconv_wgrad_ok(g), "smallconv_wgrad: filter too large for the register kernel")
+    N.check(N.hip().tde_smallconv_wgrad(_P(x), _P(dy), _P(dW), g.carray(), _s()), "tde_smallconv_wgrad")
+
+
 def conv_wgrad(x, dy, dW, g: ConvGeom, splits=None):
     """dW[KH,KW,C,Co] (f32) += sum_pixels x (x) dy."""
     _bf(x, g.B * g.H * g.W * g.C, "conv_wgrad x")

@@ -324,7 +324,7 @@ class _Gemm(_Stage):
         need_dgrad = tin.root().id != 0
         self.need_dgrad = need_dgrad
         self.shadows = {self.wname: ("row", "col") if need_dgrad else ("col",)}
-        self.small_fwd = self.small_dgrad = False
+        self.small_fwd = self.small_dgrad = self.small_wgrad = False
         if self.conv:
             H, W_, C = tin.shape
             Ho, Wo, Co = tout.shape
@@ -346,6 +346,8 @@ class _Gemm(_Stage):
                 self.shadows = {self.wname: ("row", "col")}
             # channel counts that defeat 16-byte gathers (RGB stem): explicit im2col + vector GEMMs
             self.use_im2col = (not self.small_fwd and C % 8 != 0 and os.environ.get("TDE_IM2COL", "1") != "0")
+            # filters whose K*Co partial sums fit in registers (Model B conv1: 3x3x1 -> 6)
+            self.small_wgrad = narrow and not self.use_im2col and O.smallconv_wgrad_ok(self.geo)
         self.colstats = None
         self.dz = None
 
@@ -403,6 +405,8 @@ class _Gemm(_Stage):
             g = self.geo.with_batch(B)
             if self.use_im2col:
                 O.conv_wgrad_im2col(self.xcol, dout, self.gW, g, self.Kp)
+            elif self.small_wgrad:
+                O.smallconv_wgrad(self.inp.buf, dout, self.gW, g)
             else:
                 O.conv_wgrad(self.inp.buf, dout, self.gW, g)
             if self.need_dgrad and self.small_dgrad:

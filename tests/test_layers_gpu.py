@@ -522,3 +522,29 @@ def test_im2col_conv_path(B, H, W, C, Co, k, s, pad):
     assert _rel(y.float(), ref) < 1e-2
     assert _rel(st[Co:], (ref.detach().to(bf).double() ** 2).sum((0, 1, 2))) < 1e-3
     assert _rel(dW, wgrad.permute(2, 3, 1, 0)) < 1e-3
+
+
+@pytest.mark.parametrize("B,H,W,C,Co,k,s,pad", [(128, 28, 28, 1, 6, 3, 1, "same"), (7, 13, 11, 1, 16, 2, 2, "same"),
+                                                (3, 9, 9, 2, 5, 2, 1, "valid"), (5, 12, 12, 1, 32, 2, 1, "same")])
+def test_smallconv_wgrad(B, H, W, C, Co, k, s, pad):
+    """Register-resident weight gradient (Model B conv1: 3x3x1 -> 6 over B*784 pixels) vs the fp64 oracle."""
+    from tensorflow_distributed_example_amd.ops import layer_ops as O
+    if pad == "same":
+        (pt, pb), (pl, pr) = _tf_same(H, k, s), _tf_same(W, k, s)
+        Ho, Wo = -(-H // s), -(-W // s)
+    else:
+        pt = pb = pl = pr = 0
+        Ho, Wo = (H - k) // s + 1, (W - k) // s + 1
+    g = O.ConvGeom(B, H, W, C, Ho, Wo, Co, k, k, s, s, pt, pl)
+    assert O.smallconv_wgrad_ok(g)
+    x = _r(B, H, W, C, seed=41)
+    dy = _r(B, Ho, Wo, Co, seed=42)
+    dW0 = torch.randn(k, k, C, Co, device=DEV)
+    dW = dW0.clone()
+    O.smallconv_wgrad(x, dy, dW, g)
+    wr = torch.zeros(Co, C, k, k, dtype=torch.float64, requires_grad=True)
+    out = F.conv2d(F.pad(_cpu64(x).permute(0, 3, 1, 2), (pl, pr, pt, pb)), wr, stride=s)
+    out.backward(_cpu64(dy).permute(0, 3, 1, 2))
+    ref = _dev(wr.grad.permute(2, 3, 1, 0)) + dW0.double()
+    torch.cuda.synchronize()
+    assert _rel(dW.double(), ref) < 1e-5
