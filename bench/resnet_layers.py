@@ -1,0 +1,99 @@
+#!/usr/bin/env python
+"""Per-layer GEMM timings of the ResNet-18 layer-wise plan on one MI355X (B = 64, bf16).
+
+For every Conv2D stage of the compiled plan: forward (implicit GEMM + BN-statistics epilogue),
+input gradient and weight gradient, each replayed in a hipGraph; prints µs and TFLOP/s per op and
+the totals.  ``--sweep`` re-times the weight gradients under the split-K / K-step knobs of
+``tde_igemm_tune`` (csrc/kernels/layers.hip) to pick the defaults.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "bench"))
+import torch  # noqa: E402
+
+from micro import graph_time  # noqa: E402
+
+
+def _convs(plan, LW):
+    return [st for st in plan.stages if isinstance(st, LW._Gemm) and st.conv and not st.use_im2col]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--sweep", action="store_true")
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd import _native as N
+    from tensorflow_distributed_example_amd.ops import layer_ops as O
+    from tensorflow_distributed_example_amd.train import layerwise as LW
+    torch.cuda.set_device(0)
+    tde.backend.set_random_seed(0)
+    m = tde.zoo.resnet18()
+    m.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True), optimizer=tde.optimizers.SGD(0.1))
+    B = a.batch
+    prog = m._program("train", B)
+    plan = prog.plans[0]
+    x = torch.rand((1, B, 224, 224, 3)).cuda()
+    y = torch.randint(0, 1000, (1, B)).to(torch.int32).cuda()
+    prog.stage([(x, y)])
+    prog.run()
+    torch.cuda.synchronize()
+    rows = []
+    for st in _convs(plan, LW):
+        g = st.geo.with_batch(B)
+        dout = st.out.root().grad
+        flop = 2.0 * g.B * g.Ho * g.Wo * g.Co * g.K
+        t_f = graph_time(lambda: st.fwd(plan, B, True), a.reps)
+        t_w = graph_time(lambda: O.conv_wgrad(st.inp.buf, dout, st.gW, g), a.reps)
+        t_d = graph_time(lambda: O.conv_dgrad(dout, st.Wrow, st.inp.root().grad, g, scratch=plan.scratch),
+                         a.reps) if st.need_dgrad else 0.0
+        rows.append(dict(layer=st.layer.name, shape=f"{g.H}x{g.W}x{g.C}->{g.Ho}x{g.Wo}x{g.Co} k{g.KH}s{g.sh}",
+                         fwd_us=t_f, dgrad_us=t_d, wgrad_us=t_w, gflop=flop / 1e9))
+    tot = {k: round(sum(r[k] for r in rows), 1) for k in ("fwd_us", "dgrad_us", "wgrad_us")}
+    for r in rows:
+        def tf(us):
+            return r["gflop"] / us * 1e3 if us else 0.0
+        print(f"{r['layer']:<14} {r['shape']:<28} fwd {r['fwd_us']:7.1f} us {tf(r['fwd_us']):5.0f} TF | dgrad "
+              f"{r['dgrad_us']:7.1f} us {tf(r['dgrad_us']):5.0f} TF | wgrad {r['wgrad_us']:7.1f} us "
+              f"{tf(r['wgrad_us']):5.0f} TF", flush=True)
+    print("TOTAL", json.dumps(tot), flush=True)
+    if a.sweep:
+        lib = N.hip()
+        for target, mkt, kb in [(1024, 8, 0), (512, 8, 0), (256, 8, 0), (512, 16, 0), (256, 16, 0), (2048, 4, 0),
+                                (1024, 8, 32), (512, 8, 32), (2048, 4, 32)]:
+            lib.tde_igemm_tune(target, mkt, kb, -1, -1, 0)
+            tw = 0.0
+            for st in _convs(plan, LW):
+                g = st.geo.with_batch(B)
+                tw += graph_time(lambda: O.conv_wgrad(st.inp.buf, st.out.root().grad, st.gW, g), a.reps)
+            print(f"SWEEP wgrad target={target} min_kt={mkt} kb={kb}: {tw:.1f} us", flush=True)
+        for glds, kb, big, bmin in ((1, 0, 0, 0), (1, 0, 1, 64), (1, 0, 1, 128), (1, 0, 1, 192), (1, 0, 1, 256),
+                                    (0, 0, 0, 0)):
+            lib.tde_igemm_tune(512, 16, kb, glds, big, bmin)
+            tf_ = sum(graph_time(lambda: st.fwd(plan, B, True), a.reps) for st in _convs(plan, LW))
+            td_ = sum(graph_time(lambda: O.conv_dgrad(st.out.root().grad, st.Wrow, st.inp.root().grad,
+                                                      st.geo.with_batch(B), scratch=plan.scratch), a.reps)
+                      for st in _convs(plan, LW) if st.need_dgrad)
+            print(f"SWEEP glds={glds} kb={kb} big={big} min={bmin}: fwd {tf_:.1f} us dgrad {td_:.1f} us", flush=True)
+        lib.tde_igemm_tune(512, 16, 0, 1, 0, 192)
+        for kb in ():
+            lib.tde_igemm_tune(512, 16, kb, -1)
+            tf_ = sum(graph_time(lambda: st.fwd(plan, B, True), a.reps) for st in _convs(plan, LW))
+            td_ = sum(graph_time(lambda: O.conv_dgrad(st.out.root().grad, st.Wrow, st.inp.root().grad,
+                                                      st.geo.with_batch(B), scratch=plan.scratch), a.reps)
+                      for st in _convs(plan, LW) if st.need_dgrad)
+            print(f"SWEEP kb={kb}: fwd {tf_:.1f} us dgrad {td_:.1f} us", flush=True)
+        lib.tde_igemm_tune(512, 16, 0, 1, 0, 192)
+
+
+if __name__ == "__main__":
+    main()

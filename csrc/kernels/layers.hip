@@ -330,28 +330,50 @@ __device__ __forceinline__ bf16x8 load_b_n8(const IGemmArgs& p, int n, int k) {
   return v;
 }
 
+// 16 zero bytes: the global_load_lds source of every padding / out-of-range slot.
+__device__ __attribute__((aligned(16))) bf16 g_zero16[8];
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // VEC = 1: both operands are 16-byte gatherable (channel counts % 8 == 0, aligned) — the scalar
 // fallbacks are compiled out of the hot loop.
-template <int AK, int BK_, int BM, int BN, int KB, int VEC>
+// S > 0 (K-vector A and B, VEC only): the operands go global -> LDS directly (global_load_lds
+// dwordx4 into lane-linear images whose 16-byte chunks are XOR-swizzled on the SOURCE address), S
+// LDS stages with S-1 k-tiles in flight across the per-step barrier (counted vmcnt, raw s_barrier),
+// instead of the register-staged double buffer.
+// WGM: waves along M (4 / WGM along N); the register-staged path is 2 x 2.
+template <int AK, int BK_, int BM, int BN, int KB, int VEC, int S = 0, int WGM = 2>
 __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   constexpr bool AKV = (AK == A_ROWK || AK == A_CONV || AK == A_DGRAD);  // K-vector A
   constexpr bool BKV = (BK_ == B_NK || BK_ == B_DGRADW);                 // K-vector B
-  constexpr int LDKB = KB + 8;                     // K-vector image row: KB k + 8 pad
+  constexpr bool GLDS = S > 0;
+  static_assert(!GLDS || (AKV && BKV && VEC), "global_load_lds staging needs 16-byte K-vector operands");
+  constexpr int LDKB = GLDS ? KB : KB + 8;         // K-vector image row: KB k (+ 8 pad unless swizzled)
   constexpr int AIMG = AKV ? BM * LDKB : KB * BM;  // elements per buffer
   constexpr int BIMG = BKV ? BN * LDKB : KB * BN;
+  constexpr int NBUF = GLDS ? S : 2;
   constexpr int AS = BM * KB / 2048;  // 16-byte slots per thread (either image kind)
   constexpr int BS = BN * KB / 2048;
   constexpr int KV = KB / 8, RSK = 256 / KV;  // K-vector: vectors per row, rows per slot step
   // row-vector images: CH 16-byte chunks per k row, a slot step covers 256/CH k rows
   constexpr int CHA = BM / 8, RSA = 256 / CHA, CHB = BN / 8, RSB = 256 / CHB;
-  constexpr int WTM = BM / 2, WTN = BN / 2, MI = WTM / 16, NI = WTN / 16;
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (AIMG + BIMG)];
+  constexpr int WGN = 4 / WGM;
+  static_assert(GLDS || WGM == 2, "wave layouts other than 2 x 2 are built for the glds path only");
+  constexpr int WTM = BM / WGM, WTN = BN / WGN, MI = WTM / 16, NI = WTN / 16;
+  // glds images: a wave instruction fills 1024 B = RPI rows of KV chunks; rows are read 16 at a time
+  // (one per lane of a 16-lane group) at one logical chunk, so the physical chunk is XORed with
+  // (row / rows-per-256B-bank-row) to land the 16 reads in 16 distinct bank slots
+  constexpr int RPI = 64 / KV, RPB = 128 / KB;
+  __shared__ __attribute__((aligned(16))) bf16 smem[NBUF * (AIMG + BIMG)];
   bf16* const As = smem;
-  bf16* const Bs = smem + 2 * AIMG;
+  bf16* const Bs = smem + NBUF * AIMG;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WGN, wn = wave % WGN;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;  // M-major: neighbours share the B tile in L2
   const int kt0 = blockIdx.z * p.ktiles_per_split;
   const int kt1 = min((p.K + KB - 1) / KB, kt0 + p.ktiles_per_split);
@@ -445,7 +467,117 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fk = (lane >> 4) * 8;
-  if (kt0 < kt1) {
+  if constexpr (GLDS) {
+    // per-slot loader state: instruction j = wave*AS + i fills rows j*RPI + lane/KV, physical chunk
+    // lane%KV, which holds logical chunk (lane%KV) ^ swz(row).  The host only takes this path when
+    // every k-tile lies inside ONE filter tap (C, resp. Co, a multiple of KB): the tap and channel
+    // offset of a k-tile are block-uniform scalars, and a slot's source address is its row's pixel
+    // base plus one bounds-checked offset (no per-element index decomposition in the loop).
+    ARow gar[AS];
+    int gla[AS], glb[BS], gnb[BS];
+#pragma unroll
+    for (int i = 0; i < AS; ++i) {
+      const int row = (wave * AS + i) * RPI + lane / KV;
+      gla[i] = (lane % KV) ^ ((row / RPB) & (KV - 1));
+      gar[i] = a_row<AK>(p, m0 + row);
+    }
+#pragma unroll
+    for (int i = 0; i < BS; ++i) {
+      const int row = (wave * BS + i) * RPI + lane / KV;
+      glb[i] = (lane % KV) ^ ((row / RPB) & (KV - 1));
+      gnb[i] = n0 + row;
+    }
+    const int KWd = (AK == A_DGRAD && p.ph_on) ? p.KWp : p.g.KW;  // taps per kernel row of this K
+    auto issue = [&](int stage, int kt) {
+      const int k0 = kt * KB;
+      char* ab = reinterpret_cast<char*>(As + stage * AIMG);
+      char* bb = reinterpret_cast<char*>(Bs + stage * BIMG);
+      // block-uniform tap of this k-tile
+      int th = 0, tw = 0, c0 = k0;
+      if (AK != A_ROWK || BK_ == B_DGRADW) {
+        const int Cd = (AK == A_CONV) ? p.g.C : p.g.Co;
+        const int t = k0 / Cd;
+        c0 = k0 - t * Cd;
+        th = t / KWd;
+        tw = t - th * KWd;
+      }
+#pragma unroll
+      for (int i = 0; i < AS; ++i) {
+        const bf16* src = g_zero16;
+        const ARow& r = gar[i];
+        if (AK == A_ROWK) {
+          const int k = k0 + gla[i] * 8;
+          if (r.ok && k < p.K) src = p.a + r.base + k;
+        } else if (AK == A_CONV) {
+          const int ih = r.y0 + th, iw = r.x0 + tw;
+          if (r.ok && (unsigned)ih < (unsigned)p.g.H && (unsigned)iw < (unsigned)p.g.W)
+            src = p.a + ((r.base + (long long)ih * p.g.W + iw) * p.g.C + c0 + gla[i] * 8);
+        } else {  // A_DGRAD (stride 1 or one stride phase): output pixel (y0 - th, x0 - tw)
+          const int oh = r.y0 - th, ow = r.x0 - tw;
+          if (r.ok && (unsigned)oh < (unsigned)p.g.Ho && (unsigned)ow < (unsigned)p.g.Wo)
+            src = p.a + ((r.base + (long long)oh * p.g.Wo + ow) * p.g.Co + c0 + gla[i] * 8);
+        }
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(ab + (wave * AS + i) * 1024), 16,
+                                         0, 0);
+      }
+      int tap = 0;
+      if (BK_ == B_DGRADW) {
+        const int kh = p.ph_on ? p.kh0 + th * p.g.sh : th, kw = p.ph_on ? p.kw0 + tw * p.g.sw : tw;
+        tap = kh * p.g.KW + kw;
+      }
+#pragma unroll
+      for (int i = 0; i < BS; ++i) {
+        const bf16* src = g_zero16;
+        const int n = gnb[i];
+        if (BK_ == B_NK) {
+          const int k = k0 + glb[i] * 8;
+          if (n < p.N && k < p.K) src = p.b + (long long)n * p.ldb + k;
+        } else {  // W[kh][kw][n][co]
+          if (n < p.N) src = p.b + ((long long)(tap * p.g.C + n) * p.g.Co + c0 + glb[i] * 8);
+        }
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(bb + (wave * BS + i) * 1024), 16,
+                                         0, 0);
+      }
+    };
+    if (kt0 < kt1) {
+#pragma unroll
+      for (int st = 0; st < S - 1; ++st)
+        if (kt0 + st < kt1) issue(st, kt0 + st);
+      for (int kt = kt0; kt < kt1; ++kt) {
+        const int rel = kt - kt0;
+        const int after = min(S - 2, kt1 - 1 - kt);  // stages already issued behind this one
+        if (after >= 2) vm_wait<2 * (AS + BS)>();
+        else if (after == 1) vm_wait<AS + BS>();
+        else vm_wait<0>();
+        __builtin_amdgcn_s_barrier();  // stage rel%S visible to all waves; stage (rel-1)%S free
+        if (kt + S - 1 < kt1) issue((rel + S - 1) % S, kt + S - 1);
+        const bf16* a = As + (rel % S) * AIMG;
+        const bf16* b = Bs + (rel % S) * BIMG;
+#pragma unroll
+        for (int kk = 0; kk < KB; kk += 32) {
+          const int c = kk / 8 + (lane >> 4);
+          bf16x8 af[MI], bfr[NI];
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            const int r = wm * WTM + i * 16 + fr;
+            af[i] = *reinterpret_cast<const bf16x8*>(a + r * KB + ((c ^ ((r / RPB) & (KV - 1))) << 3));
+          }
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            const int r = wn * WTN + j * 16 + fr;
+            bfr[j] = *reinterpret_cast<const bf16x8*>(b + r * KB + ((c ^ ((r / RPB) & (KV - 1))) << 3));
+          }
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+        }
+      }
+      vm_wait<0>();
+    }
+  } else if (kt0 < kt1) {
     gload(kt0);
     sstore(0);
     __syncthreads();
@@ -531,14 +663,14 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
     sp2[j] = s2;
   }
   if (p.colstats) {
-    // the two waves sharing a column range (wm = 0, 1) combine through LDS: one atomic per column per block
+    // the WGM waves sharing a column range combine through LDS: one atomic per column per block
     __syncthreads();
-    float* red = reinterpret_cast<float*>(smem);  // [2 wn][NI][2][16]
-    if (wm == 1 && lane < 16) {
+    float* red = reinterpret_cast<float*>(smem);  // [WGM][WGN][NI][2][16]
+    if (wm > 0 && lane < 16) {
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        red[((wn * NI + j) * 2 + 0) * 16 + lane] = sp1[j];
-        red[((wn * NI + j) * 2 + 1) * 16 + lane] = sp2[j];
+        red[(((wm * WGN + wn) * NI + j) * 2 + 0) * 16 + lane] = sp1[j];
+        red[(((wm * WGN + wn) * NI + j) * 2 + 1) * 16 + lane] = sp2[j];
       }
     }
     __syncthreads();
@@ -548,8 +680,14 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
       for (int j = 0; j < NI; ++j) {
         const int col = n0 + wn * WTN + j * 16 + lane;
         if (col >= p.N) continue;
-        atomicAdd(&st[col], (double)(sp1[j] + red[((wn * NI + j) * 2 + 0) * 16 + lane]));
-        atomicAdd(&st[p.N + col], (double)(sp2[j] + red[((wn * NI + j) * 2 + 1) * 16 + lane]));
+        float a1 = sp1[j], a2 = sp2[j];
+#pragma unroll
+        for (int w = 1; w < WGM; ++w) {
+          a1 += red[(((w * WGN + wn) * NI + j) * 2 + 0) * 16 + lane];
+          a2 += red[(((w * WGN + wn) * NI + j) * 2 + 1) * 16 + lane];
+        }
+        atomicAdd(&st[col], (double)a1);
+        atomicAdd(&st[p.N + col], (double)a2);
       }
     }
   }
@@ -1742,6 +1880,21 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(float* __restrict__ 
   }
 }
 
+// Tile-selection knobs (bench/resnet_layers.py sweeps them; the defaults are the measured choice):
+// weight-grad split-K targets ~g_wg_target workgroups with >= g_wg_min_kt k-tiles per split, and
+// g_kb_force (32/64) overrides the K step.
+// g_glds selects the global_load_lds pipeline for the K-vector kinds (fwd / dgrad / dense).
+static int g_wg_target = 512, g_wg_min_kt = 16, g_kb_force = 0, g_glds = 1, g_big = 0, g_big_min = 192;
+
+TDE_API void tde_igemm_tune(int wg_target, int wg_min_kt, int kb_force, int glds, int big, int big_min) {
+  if (wg_target > 0) g_wg_target = wg_target;
+  if (wg_min_kt > 0) g_wg_min_kt = wg_min_kt;
+  g_kb_force = (kb_force == 32 || kb_force == 64) ? kb_force : 0;
+  if (glds >= 0) g_glds = glds;
+  if (big >= 0) g_big = big;
+  if (big_min > 0) g_big_min = big_min;
+}
+
 TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, long long ldb, int bkind, int M, int N,
                       int K, const int* geo, int splits, float* cf, long long ldc, int cf_mode, float alpha, bf16* cb,
                       long long ldcb, int cb_accum, const float* bias, int relu, double* colstats, float* scratch,
@@ -1786,8 +1939,9 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     p.KHp = phase[6];
     p.KWp = phase[7];
   }
-  // K step: 64 (two MFMA k-slices per barrier) unless K is short
-  const int KB = K >= 256 ? 64 : 32;
+  // K step: 64 (two MFMA k-slices per barrier) for long reductions; the gathered input gradient
+  // measures faster at 32 (ResNet-18 sweep, bench/resnet_layers.py)
+  const int KB = g_kb_force ? g_kb_force : ((akind == A_DGRAD || K < 256) ? 32 : 64);
   const int ktiles = (K + KB - 1) / KB;
   const bool auto_splits = splits == 0;
   if (splits < 1) splits = 1;
@@ -1830,10 +1984,10 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     bn = N > 64 ? 128 : 64;
     if (auto_splits) {  // weight grads: f32 atomics, fill the chip with >= ~4 workgroups per CU
       const long long t = (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
-      long long sp = (1024 + t - 1) / t;
-      // >= 8 k-tiles per split: every split ends in BM x BN f32 atomics, and with the skinny weight
-      // grads of narrow layers (N = 12, 24) hundreds of 2-k-tile splits spend their time in atomics
-      const long long maxs = ktiles / 8 > 0 ? ktiles / 8 : 1;
+      long long sp = (g_wg_target + t - 1) / t;
+      // >= g_wg_min_kt k-tiles per split: every split ends in BM x BN f32 atomics (executed at the
+      // memory side), and hundreds of short splits spend their time in atomics
+      const long long maxs = ktiles / g_wg_min_kt > 0 ? ktiles / g_wg_min_kt : 1;
       splits = (int)(sp < maxs ? sp : maxs);
       if (splits < 1) splits = 1;
       p.ktiles_per_split = (ktiles + splits - 1) / splits;
@@ -1847,6 +2001,14 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   dim3 grid((M + bm - 1) / bm, (N + bn - 1) / bn, splits);
   if (grid.y > 65535 || splits > 65535) return -3;
   const bool vec = p.avec && p.bvec;
+  // global_load_lds path: every k-tile inside one filter tap (see igemm_kernel)
+  bool ut = true;
+  if (akind == A_CONV) ut = p.g.C % KB == 0;
+  if (akind == A_DGRAD) ut = p.g.Co % KB == 0 && (p.ph_on || (p.g.sh == 1 && p.g.sw == 1));
+  // big tiles (256 x 64 with 64 x 64 per wave, or 256 x 128 with 128 x 64 per wave): LDS reads per
+  // MFMA flop within the CU's LDS bandwidth; only when they still give >= g_big_min workgroups
+  const long long big_tiles = (long long)((M + 255) / 256) * ((N + (N <= 64 ? 63 : 127)) / (N <= 64 ? 64 : 128));
+  const bool big = g_big && KB == 64 && splits == 1 && !rowk && (N <= 64 || N % 128 == 0) && big_tiles >= g_big_min;
 #define TDE_IGEMM(AK_, BK__, BM_, BN_)                                                   \
   do {                                                                                   \
     if (vec) {                                                                           \
@@ -1857,18 +2019,37 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
       else igemm_kernel<AK_, BK__, BM_, BN_, 32, 0><<<grid, 256, 0, stream>>>(p);          \
     }                                                                                    \
   } while (0)
+  // K-vector kinds: global_load_lds pipeline, 3 stages at KB = 64 (<= 96 KiB LDS), 4 at KB = 32
+#define TDE_IGEMM_KV(AK_, BK__, BM_, BN_)                                                           \
+  do {                                                                                              \
+    if (vec && g_glds && ut) {                                                                      \
+      if (big && N <= 64) {                                                                         \
+        grid = dim3((M + 255) / 256, (N + 63) / 64, splits);                                        \
+        igemm_kernel<AK_, BK__, 256, 64, 64, 1, 3, 4><<<grid, 256, 0, stream>>>(p);                 \
+      } else if (big) {                                                                             \
+        grid = dim3((M + 255) / 256, (N + 127) / 128, splits);                                      \
+        igemm_kernel<AK_, BK__, 256, 128, 64, 1, 3, 2><<<grid, 256, 0, stream>>>(p);                \
+      } else if (KB == 64) {                                                                        \
+        igemm_kernel<AK_, BK__, BM_, BN_, 64, 1, 3><<<grid, 256, 0, stream>>>(p);                   \
+      } else {                                                                                      \
+        igemm_kernel<AK_, BK__, BM_, BN_, 32, 1, 4><<<grid, 256, 0, stream>>>(p);                   \
+      }                                                                                             \
+    } else {                                                                                        \
+      TDE_IGEMM(AK_, BK__, BM_, BN_);                                                               \
+    }                                                                                               \
+  } while (0)
   if (akind == A_ROWK && bkind == B_NK) {
-    if (bm == 128 && bn == 128) TDE_IGEMM(A_ROWK, B_NK, 128, 128);
-    else if (bm == 128) TDE_IGEMM(A_ROWK, B_NK, 128, 64);
-    else TDE_IGEMM(A_ROWK, B_NK, 64, 64);
+    if (bm == 128 && bn == 128) TDE_IGEMM_KV(A_ROWK, B_NK, 128, 128);
+    else if (bm == 128) TDE_IGEMM_KV(A_ROWK, B_NK, 128, 64);
+    else TDE_IGEMM_KV(A_ROWK, B_NK, 64, 64);
   } else if (akind == A_CONV && bkind == B_NK) {
-    if (bm == 128 && bn == 128) TDE_IGEMM(A_CONV, B_NK, 128, 128);
-    else if (bm == 128) TDE_IGEMM(A_CONV, B_NK, 128, 64);
-    else TDE_IGEMM(A_CONV, B_NK, 64, 64);
+    if (bm == 128 && bn == 128) TDE_IGEMM_KV(A_CONV, B_NK, 128, 128);
+    else if (bm == 128) TDE_IGEMM_KV(A_CONV, B_NK, 128, 64);
+    else TDE_IGEMM_KV(A_CONV, B_NK, 64, 64);
   } else if (akind == A_DGRAD && bkind == B_DGRADW) {
-    if (bm == 128 && bn == 128) TDE_IGEMM(A_DGRAD, B_DGRADW, 128, 128);
-    else if (bm == 128) TDE_IGEMM(A_DGRAD, B_DGRADW, 128, 64);
-    else TDE_IGEMM(A_DGRAD, B_DGRADW, 64, 64);
+    if (bm == 128 && bn == 128) TDE_IGEMM_KV(A_DGRAD, B_DGRADW, 128, 128);
+    else if (bm == 128) TDE_IGEMM_KV(A_DGRAD, B_DGRADW, 128, 64);
+    else TDE_IGEMM_KV(A_DGRAD, B_DGRADW, 64, 64);
   } else if (akind == A_COLM && bkind == B_KN) {
     if (bm == 128 && bn == 128) TDE_IGEMM(A_COLM, B_KN, 128, 128);
     else if (bm == 128) TDE_IGEMM(A_COLM, B_KN, 128, 64);
@@ -1882,6 +2063,7 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   } else {
     return -1;
   }
+#undef TDE_IGEMM_KV
 #undef TDE_IGEMM
   TDE_LAUNCH_CHECK();
   return 0;
