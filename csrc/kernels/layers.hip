@@ -1987,7 +1987,13 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
       long long sp = (g_wg_target + t - 1) / t;
       // >= g_wg_min_kt k-tiles per split: every split ends in BM x BN f32 atomics (executed at the
       // memory side), and hundreds of short splits spend their time in atomics
-      const long long maxs = ktiles / g_wg_min_kt > 0 ? ktiles / g_wg_min_kt : 1;
+      long long maxs = ktiles / g_wg_min_kt > 0 ? ktiles / g_wg_min_kt : 1;
+      // ... but never starve the chip: few output tiles over a short K (1x1 projections of the
+      // deep layers) still get ~256 workgroups, down to 2 k-tiles per split
+      if (t * maxs < 256) {
+        const long long want = (256 + t - 1) / t, cap = ktiles / 2 > 0 ? ktiles / 2 : 1;
+        maxs = want < cap ? want : cap;
+      }
       splits = (int)(sp < maxs ? sp : maxs);
       if (splits < 1) splits = 1;
       p.ktiles_per_split = (ktiles + splits - 1) / splits;

@@ -151,7 +151,15 @@ def conv_dgrad(dy, Wrow, dx, g: ConvGeom, accum=False, scratch=None):
     _bf(Wrow, g.K * g.Co, "conv_dgrad W")
     _bf(dx, g.B * g.H * g.W * g.C, "conv_dgrad dx")
     if g.sh > 1 or g.sw > 1:
-        for ph in dgrad_phases(g):
+        phases = dgrad_phases(g)
+        if not accum and any(ph[6] * ph[7] == 0 for ph in phases):
+            # phases no tap reaches (3 of the 4 of a 1x1 stride-2 projection) are zero: one fill of dx,
+            # then the tapped phases accumulate, instead of K = 0 GEMM launches that store zeros
+            dx[: g.B * g.H * g.W * g.C].zero_()
+            accum = True
+        for ph in phases:
+            if ph[6] * ph[7] == 0 and accum:
+                continue
             _igemm(dy, 0, A_DGRAD, Wrow, 0, B_DGRADW, g.B * ph[2] * ph[3], g.C, ph[6] * ph[7] * g.Co, g,
                    cb=dx, ldcb=g.C, cb_accum=accum, phase=ph)
         return

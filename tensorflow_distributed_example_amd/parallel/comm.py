@@ -430,8 +430,9 @@ def maybe_xgmi(fallback, device, rank, world, bucket_hint=None, group=None):
         dec = [tx <= tr]
         dist.broadcast_object_list(dec, src=0, group=group)
         if rank == 0:
+            import sys
             print(f"[tde.comm] all-reduce of {t.numel()} fp32: xGMI {tx * 1e6:.1f} us, RCCL {tr * 1e6:.1f} us "
-                  f"-> {'xGMI' if dec[0] else 'RCCL'}", flush=True)
+                  f"-> {'xGMI' if dec[0] else 'RCCL'}", file=sys.stderr, flush=True)
         if not dec[0]:
             xg.fallback = None
             xg.close()
