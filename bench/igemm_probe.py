@@ -18,7 +18,10 @@ def main():
     from tensorflow_distributed_example_amd.ops import layer_ops as O
     torch.cuda.set_device(0)
     bf = torch.bfloat16
-    for (B, H, C, Co) in [(64, 56, 64, 64), (64, 28, 128, 128), (64, 7, 512, 512)]:
+    cfgs = [(64, 56, 64, 64), (64, 28, 128, 128), (64, 7, 512, 512)]
+    if len(sys.argv) > 1:
+        cfgs = [cfgs[int(sys.argv[1])]]
+    for (B, H, C, Co) in cfgs:
         g = O.ConvGeom(B, H, H, C, H, H, Co, 3, 3, 1, 1, 1, 1)
         M, K = B * H * H, 9 * C
         x = torch.randn(B * H * H * C, device="cuda").to(bf)
@@ -37,6 +40,9 @@ def main():
                                                                ldcb=Co), 20)
         res["conv K/9 bf16"] = graph_time(lambda: O._igemm(x, 0, O.A_CONV, Wt, K, O.B_NK, M, Co, C, g, cb=y,
                                                           ldcb=Co), 20)
+        dW = torch.zeros(K * Co, device="cuda")
+        dy = torch.randn(M * Co, device="cuda").to(bf)
+        res["wgrad atomics"] = graph_time(lambda: O.conv_wgrad(x, dy, dW, g), 20)
         print(f"B{B} {H}x{H}x{C}->{Co}: " + " | ".join(f"{k} {v:.1f}us ({fl / v * 1e-6 if 'K/9' not in k else fl / 9 / v * 1e-6:.0f}TF)"
                                                       for k, v in res.items()), flush=True)
 

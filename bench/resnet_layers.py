@@ -53,7 +53,7 @@ def main():
         dout = st.out.root().grad
         flop = 2.0 * g.B * g.Ho * g.Wo * g.Co * g.K
         t_f = graph_time(lambda: st.fwd(plan, B, True), a.reps)
-        t_w = graph_time(lambda: O.conv_wgrad(st.inp.buf, dout, st.gW, g), a.reps)
+        t_w = graph_time(lambda: O.conv_wgrad(st.inp.buf, dout, st.gW, g, scratch=plan.wscratch), a.reps)
         t_d = graph_time(lambda: O.conv_dgrad(dout, st.Wrow, st.inp.root().grad, g, scratch=plan.scratch),
                          a.reps) if st.need_dgrad else 0.0
         rows.append(dict(layer=st.layer.name, shape=f"{g.H}x{g.W}x{g.C}->{g.Ho}x{g.Wo}x{g.Co} k{g.KH}s{g.sh}",
@@ -74,7 +74,7 @@ def main():
             tw = 0.0
             for st in _convs(plan, LW):
                 g = st.geo.with_batch(B)
-                tw += graph_time(lambda: O.conv_wgrad(st.inp.buf, st.out.root().grad, st.gW, g), a.reps)
+                tw += graph_time(lambda: O.conv_wgrad(st.inp.buf, st.out.root().grad, st.gW, g, scratch=plan.wscratch), a.reps)
             print(f"SWEEP wgrad target={target} min_kt={mkt} kb={kb}: {tw:.1f} us", flush=True)
         for glds, kb, big, bmin in ((1, 0, 0, 0), (1, 0, 1, 64), (1, 0, 1, 128), (1, 0, 1, 192), (1, 0, 1, 256),
                                     (0, 0, 0, 0)):

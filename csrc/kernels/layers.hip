@@ -377,7 +377,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;  // M-major: neighbours share the B tile in L2
   const int kt0 = blockIdx.z * p.ktiles_per_split;
   const int kt1 = min((p.K + KB - 1) / KB, kt0 + p.ktiles_per_split);
-  if (kt0 >= kt1 && p.cf_mode == 2) return;  // empty split contributes nothing
+  if (kt0 >= kt1 && p.cf_mode == 2) return;  // empty split contributes nothing (mode 3 stores its zeros)
 
   // ---- loader state
   const int lk = (tid % KV) * 8;  // K-vector: k offset of every slot of this thread
@@ -488,18 +488,30 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
       gnb[i] = n0 + row;
     }
     const int KWd = (AK == A_DGRAD && p.ph_on) ? p.KWp : p.g.KW;  // taps per kernel row of this K
+    // block-uniform tap (th, tw) and channel offset c0 of the next k-tile to issue: decomposed once,
+    // then advanced by KB per issue (issues run in k order)
+    const int Cd = (AK == A_CONV) ? p.g.C : p.g.Co;
+    int nth = 0, ntw = 0, nc0 = kt0 * KB;
+    if (AK != A_ROWK || BK_ == B_DGRADW) {
+      const int t = (kt0 * KB) / Cd;
+      nc0 = kt0 * KB - t * Cd;
+      nth = t / KWd;
+      ntw = t - nth * KWd;
+    }
     auto issue = [&](int stage, int kt) {
       const int k0 = kt * KB;
       char* ab = reinterpret_cast<char*>(As + stage * AIMG);
       char* bb = reinterpret_cast<char*>(Bs + stage * BIMG);
-      // block-uniform tap of this k-tile
-      int th = 0, tw = 0, c0 = k0;
+      const int th = nth, tw = ntw, c0 = (AK != A_ROWK || BK_ == B_DGRADW) ? nc0 : k0;
       if (AK != A_ROWK || BK_ == B_DGRADW) {
-        const int Cd = (AK == A_CONV) ? p.g.C : p.g.Co;
-        const int t = k0 / Cd;
-        c0 = k0 - t * Cd;
-        th = t / KWd;
-        tw = t - th * KWd;
+        nc0 += KB;
+        if (nc0 >= Cd) {
+          nc0 -= Cd;
+          if (++ntw == KWd) {
+            ntw = 0;
+            ++nth;
+          }
+        }
       }
 #pragma unroll
       for (int i = 0; i < AS; ++i) {
@@ -615,7 +627,106 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
     }
   }
 
-  // ---- epilogue
+  // ---- epilogue, bf16 activation outputs of the glds kernels: the accumulator tile goes through
+  // LDS (f32, MFMA layout in, row-contiguous out) so the global stores are 16-byte row chunks, not
+  // 2-byte scattered per-lane stores; per-column BN statistics are still taken in the MFMA layout.
+  constexpr int TLD = BN + 16;  // f32 row stride: the 4 row groups of a 16-lane MFMA column hit 4 bank quarters
+  constexpr bool LDS_EPI = GLDS && (size_t)BM * TLD * 4 + 4 * 16 * 2 * 4 * 8 <= sizeof(smem);
+  if constexpr (LDS_EPI) {
+    if (p.cb && p.cf_mode == 0) {
+      float* T = reinterpret_cast<float*>(smem);
+      float* red = T + BM * TLD;  // [WGM][WGN][NI][2][16] statistics partials
+      __syncthreads();            // every wave is done reading the last stage
+      float e1[NI], e2[NI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int lc = wn * WTN + j * 16 + fr, col = n0 + lc;
+        const bool cok = col < p.N;
+        const float bv = (p.bias && cok) ? p.bias[col] : 0.f;
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int lr = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+            float v = p.alpha * acc[i][j][r] + bv;
+            if (p.colstats && cok && m0 + lr < p.M) {
+              const float q = bf2f(f2bf(v));
+              s1 += q;
+              s2 += q * q;
+            }
+            if (p.relu) v = fmaxf(v, 0.f);
+            T[lr * TLD + lc] = v;
+          }
+        }
+        if (p.colstats) {
+          s1 += __shfl_xor(s1, 16, 64);
+          s1 += __shfl_xor(s1, 32, 64);
+          s2 += __shfl_xor(s2, 16, 64);
+          s2 += __shfl_xor(s2, 32, 64);
+        }
+        e1[j] = s1;
+        e2[j] = s2;
+      }
+      if (p.colstats && lane < 16) {
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          red[(((wm * WGN + wn) * NI + j) * 2 + 0) * 16 + lane] = e1[j];
+          red[(((wm * WGN + wn) * NI + j) * 2 + 1) * 16 + lane] = e2[j];
+        }
+      }
+      __syncthreads();
+      if (p.colstats && wm == 0 && lane < 16) {
+        double* st = p.colstats + (size_t)(blockIdx.x % kStatSlots) * 2 * p.N;
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int col = n0 + wn * WTN + j * 16 + lane;
+          if (col >= p.N) continue;
+          float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+          for (int w = 0; w < WGM; ++w) {
+            a1 += red[(((w * WGN + wn) * NI + j) * 2 + 0) * 16 + lane];
+            a2 += red[(((w * WGN + wn) * NI + j) * 2 + 1) * 16 + lane];
+          }
+          atomicAdd(&st[col], (double)a1);
+          atomicAdd(&st[p.N + col], (double)a2);
+        }
+      }
+      // row-contiguous 8-column chunks: 16-byte bf16 stores (read-add-store for accumulated outputs)
+      constexpr int CPRW = BN / 8;
+      const bool vst = (p.ldcb % 8) == 0 && ((uintptr_t)p.cb & 15) == 0;
+      for (int c = tid; c < BM * CPRW; c += 256) {
+        const int lr = c / CPRW, ch = c - lr * CPRW;
+        const int mrow = m0 + lr, col0 = n0 + ch * 8;
+        if (mrow >= p.M || col0 >= p.N) continue;
+        long long row = mrow;
+        if (AK == A_DGRAD && p.ph_on) {  // phase row -> input pixel
+          const int hw = p.Hp * p.Wp;
+          const int b = mrow / hw, rem = mrow - b * hw;
+          const int ihp = rem / p.Wp, iwp = rem - ihp * p.Wp;
+          row = ((long long)b * p.g.H + ihp * p.g.sh + p.ph_h) * p.g.W + iwp * p.g.sw + p.ph_w;
+        }
+        const float4 lo = *reinterpret_cast<const float4*>(T + lr * TLD + ch * 8);
+        const float4 hi = *reinterpret_cast<const float4*>(T + lr * TLD + ch * 8 + 4);
+        float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        bf16* q = p.cb + row * p.ldcb + col0;
+        if (vst && col0 + 8 <= p.N) {
+          if (p.cb_accum) {
+            const bf16x8 o = *reinterpret_cast<const bf16x8*>(q);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += bf2f(o[e]);
+          }
+          bf16x8 o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e]);
+          *reinterpret_cast<bf16x8*>(q) = o;
+        } else {
+          for (int e = 0; e < 8 && col0 + e < p.N; ++e) q[e] = f2bf(v[e] + (p.cb_accum ? bf2f(q[e]) : 0.f));
+        }
+      }
+      return;
+    }
+  }
   float sp1[NI], sp2[NI];  // per-column statistics of this wave (valid in lanes 0..15)
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
@@ -646,6 +757,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
         if (p.relu) v = fmaxf(v, 0.f);
         if (p.cf_mode == 1) p.cf[(long long)row * p.ldc + col] = v;
         else if (p.cf_mode == 2) atomicAdd(&p.cf[(long long)row * p.ldc + col], v);
+        else if (p.cf_mode == 3) p.cf[(long long)blockIdx.z * p.M * p.ldc + (long long)row * p.ldc + col] = v;
         if (p.cb) {
           bf16* q = &p.cb[(long long)row * p.ldcb + col];
           if (p.cb_accum) v += bf2f(*q);
@@ -1885,6 +1997,8 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(float* __restrict__ 
 // g_kb_force (32/64) overrides the K step.
 // g_glds selects the global_load_lds pipeline for the K-vector kinds (fwd / dgrad / dense).
 static int g_wg_target = 512, g_wg_min_kt = 16, g_kb_force = 0, g_glds = 1, g_big = 0, g_big_min = 192;
+// split-K weight gradients with at most this many splits store partials + reduce; more splits use atomics
+static int g_wg_scratch_max = 16;
 
 TDE_API void tde_igemm_tune(int wg_target, int wg_min_kt, int kb_force, int glds, int big, int big_min) {
   if (wg_target > 0) g_wg_target = wg_target;
@@ -1893,6 +2007,55 @@ TDE_API void tde_igemm_tune(int wg_target, int wg_min_kt, int kb_force, int glds
   if (glds >= 0) g_glds = glds;
   if (big >= 0) g_big = big;
   if (big_min > 0) g_big_min = big_min;
+}
+
+// Split-K factor of a weight-gradient GEMM (row-contiguous operands, 128/64 tiles): fill the chip with
+// ~g_wg_target workgroups, >= g_wg_min_kt k-tiles per split (every split ends in a BM x BN partial
+// sum), but never fewer than ~256 workgroups while K allows 2 k-tiles per split (1x1 projections).
+static int wgrad_splits(int M, int N, int K, int KB, int* ktiles_per_split) {
+  const int bm = M > 64 ? 128 : 64, bn = N > 64 ? 128 : 64;
+  const int ktiles = (K + KB - 1) / KB;
+  const long long t = (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  long long sp = (g_wg_target + t - 1) / t;
+  long long maxs = ktiles / g_wg_min_kt > 0 ? ktiles / g_wg_min_kt : 1;
+  if (t * maxs < 256) {
+    const long long want = (256 + t - 1) / t, cap = ktiles / 2 > 0 ? ktiles / 2 : 1;
+    maxs = want < cap ? want : cap;
+  }
+  int splits = (int)(sp < maxs ? sp : maxs);
+  if (splits < 1) splits = 1;
+  const int per = (ktiles + splits - 1) / splits;
+  if (ktiles_per_split) *ktiles_per_split = per;
+  return ktiles > 0 ? (ktiles + per - 1) / per : 1;
+}
+
+// f32 elements of split-K scratch a weight gradient of this shape uses (0: no split)
+TDE_API long long tde_igemm_wgrad_scratch_elems(int M, int N, int K) {
+  const int KB = g_kb_force ? g_kb_force : (K < 256 ? 32 : 64);
+  const int sp = wgrad_splits(M, N, K, KB, nullptr);
+  return (sp > 1 && sp <= g_wg_scratch_max) ? (long long)sp * M * N : 0;
+}
+
+// dst[i] += sum_s part[s][i] over contiguous [M*N] (the split-K partials of a weight gradient)
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int splits, long long n,
+                                                            float* __restrict__ dst) {
+  const long long n4 = n >> 2;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    float4 acc = reinterpret_cast<const float4*>(part)[i];
+    for (int s = 1; s < splits; ++s) {
+      const float4 v = reinterpret_cast<const float4*>(part + (size_t)s * n)[i];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    float4 d = reinterpret_cast<float4*>(dst)[i];
+    d.x += acc.x; d.y += acc.y; d.z += acc.z; d.w += acc.w;
+    reinterpret_cast<float4*>(dst)[i] = d;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const long long e = (n4 << 2) + threadIdx.x;
+    float acc = 0.f;
+    for (int s = 0; s < splits; ++s) acc += part[(size_t)s * n + e];
+    dst[e] += acc;
+  }
 }
 
 TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, long long ldb, int bkind, int M, int N,
@@ -1982,22 +2145,8 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   if (rowk) {
     bm = M > 64 ? 128 : 64;
     bn = N > 64 ? 128 : 64;
-    if (auto_splits) {  // weight grads: f32 atomics, fill the chip with >= ~4 workgroups per CU
-      const long long t = (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
-      long long sp = (g_wg_target + t - 1) / t;
-      // >= g_wg_min_kt k-tiles per split: every split ends in BM x BN f32 atomics (executed at the
-      // memory side), and hundreds of short splits spend their time in atomics
-      long long maxs = ktiles / g_wg_min_kt > 0 ? ktiles / g_wg_min_kt : 1;
-      // ... but never starve the chip: few output tiles over a short K (1x1 projections of the
-      // deep layers) still get ~256 workgroups, down to 2 k-tiles per split
-      if (t * maxs < 256) {
-        const long long want = (256 + t - 1) / t, cap = ktiles / 2 > 0 ? ktiles / 2 : 1;
-        maxs = want < cap ? want : cap;
-      }
-      splits = (int)(sp < maxs ? sp : maxs);
-      if (splits < 1) splits = 1;
-      p.ktiles_per_split = (ktiles + splits - 1) / splits;
-      splits = (ktiles + p.ktiles_per_split - 1) / p.ktiles_per_split;
+    if (auto_splits) {
+      splits = wgrad_splits(M, N, K, KB, &p.ktiles_per_split);
     }
   } else if (N > 64 && tiles(128, 128) >= 512) {
     bm = bn = 128;
@@ -2006,6 +2155,17 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   }
   dim3 grid((M + bm - 1) / bm, (N + bn - 1) / bn, splits);
   if (grid.y > 65535 || splits > 65535) return -3;
+  // weight-grad split-K with a scratch: every split stores its partial tile (plain stores) and one
+  // reduction pass adds them to the gradient, instead of BM x BN memory-side f32 atomics per split
+  float* const wg_dst = p.cf;
+  const long long wg_ldc = p.ldc;
+  const bool wg_scratch = rowk && auto_splits && splits > 1 && splits <= g_wg_scratch_max && scratch &&
+                          p.cf_mode == 2 && p.ldc == N && p.cf &&
+                          ((uintptr_t)p.cf & 15) == 0 && ((uintptr_t)scratch & 15) == 0;
+  if (wg_scratch) {
+    p.cf = scratch;
+    p.cf_mode = 3;
+  }
   const bool vec = p.avec && p.bvec;
   // global_load_lds path: every k-tile inside one filter tap (see igemm_kernel)
   bool ut = true;
@@ -2072,6 +2232,14 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
 #undef TDE_IGEMM_KV
 #undef TDE_IGEMM
   TDE_LAUNCH_CHECK();
+  if (wg_scratch) {
+    const long long n = (long long)M * N;
+    long long g = (n / 4 + 255) / 256;
+    g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
+    (void)wg_ldc;
+    splitk_reduce_kernel<<<(int)g, 256, 0, stream>>>(scratch, splits, n, wg_dst);
+    TDE_LAUNCH_CHECK();
+  }
   return 0;
 }
 

@@ -238,14 +238,27 @@ def smallconv_wgrad(x, dy, dW, g: ConvGeom):
     N.check(N.hip().tde_smallconv_wgrad(_P(x), _P(dy), _P(dW), g.carray(), _s()), "tde_smallconv_wgrad")
 
 
-def conv_wgrad(x, dy, dW, g: ConvGeom, splits=None):
-    """dW[KH,KW,C,Co] (f32) += sum_pixels x (x) dy."""
+def wgrad_scratch_elems(M, N_, K):
+    """f32 scratch the split-K weight gradient of an [M, N] x K GEMM stores its partials in (0: no split)."""
+    return int(N.hip().tde_igemm_wgrad_scratch_elems(int(M), int(N_), int(K)))
+
+
+def _wscratch(M, N_, K, scratch):
+    if scratch is None:
+        return None
+    need = wgrad_scratch_elems(M, N_, K)
+    return scratch if need and scratch.numel() >= need else None
+
+
+def conv_wgrad(x, dy, dW, g: ConvGeom, splits=None, scratch=None):
+    """dW[KH,KW,C,Co] (f32) += sum_pixels x (x) dy  (split-K partials through ``scratch`` when given)."""
     _bf(x, g.B * g.H * g.W * g.C, "conv_wgrad x")
     _bf(dy, g.B * g.Ho * g.Wo * g.Co, "conv_wgrad dy")
     _f32(dW, g.K * g.Co, "conv_wgrad dW")
     M, N_, K = g.K, g.Co, g.B * g.Ho * g.Wo
     s = pick_splits(M, N_, K) if splits is None else splits
-    _igemm(x, 0, A_WGRAD, dy, g.Co, B_KN, M, N_, K, g, splits=s, cf=dW, ldc=g.Co, cf_mode=2)
+    _igemm(x, 0, A_WGRAD, dy, g.Co, B_KN, M, N_, K, g, splits=s, cf=dW, ldc=g.Co, cf_mode=2,
+           scratch=_wscratch(M, N_, K, scratch) if s == 0 else None)
 
 
 # ---------------------------------------------------------------- Dense
@@ -277,14 +290,15 @@ def dense_dgrad(dy, Wrow, dx, B, accum=False, scratch=None):
            cb_accum=accum, scratch=scratch)
 
 
-def dense_wgrad(x, dy, dW, B, splits=None):
+def dense_wgrad(x, dy, dW, B, splits=None, scratch=None):
     """dW[in,out] (f32) += x[B,in]^T @ dy[B,out]."""
     fin, out = dW.shape
     _bf(x, B * fin, "dense_wgrad x")
     _bf(dy, B * out, "dense_wgrad dy")
     _f32(dW, fin * out, "dense_wgrad dW")
     s = pick_splits(fin, out, B) if splits is None else splits
-    _igemm(x, fin, A_COLM, dy, out, B_KN, fin, out, B, splits=s, cf=dW, ldc=out, cf_mode=2)
+    _igemm(x, fin, A_COLM, dy, out, B_KN, fin, out, B, splits=s, cf=dW, ldc=out, cf_mode=2,
+           scratch=_wscratch(fin, out, B, scratch) if s == 0 else None)
 
 
 # ---------------------------------------------------------------- BN / activation / dropout

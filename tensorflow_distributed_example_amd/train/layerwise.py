@@ -254,6 +254,9 @@ class LayerwisePlan(PG.ReplicaPlan):
         # one shared f32 split-K scratch (stages run in order on one stream; finalize re-zeroes it)
         need = max([st.scratch_need(B) for st in self.stages if hasattr(st, "scratch_need")] + [0])
         self.scratch = torch.zeros(max(need, 1), dtype=torch.float32, device=dev) if need else None
+        # split-K weight gradients store per-split partials here and reduce them in one pass
+        wneed = max([st.wscratch_need(B) for st in self.stages if hasattr(st, "wscratch_need")] + [0])
+        self.wscratch = torch.empty(wneed, dtype=torch.float32, device=dev) if wneed else None
 
     # ------------------------------------------------------------------ plan interface
     def on_weights_loaded(self):
@@ -359,6 +362,14 @@ class _Gemm(_Stage):
         rows, fin, out = self.inp.rows(B), self.W.shape[0], self.W.shape[1]
         return max(O.scratch_elems(rows, out, fin), O.scratch_elems(rows, fin, out) if self.need_dgrad else 0)
 
+    def wscratch_need(self, B):
+        if self.conv:
+            g = self.geo.with_batch(B)
+            if self.use_im2col or self.small_wgrad:
+                return 0
+            return O.wgrad_scratch_elems(g.K, g.Co, g.B * g.Ho * g.Wo)
+        return O.wgrad_scratch_elems(self.W.shape[0], self.W.shape[1], self.inp.rows(B))
+
     def alloc(self, B, dev):
         if self.conv and self.use_im2col:
             g = self.geo.with_batch(B)
@@ -408,7 +419,7 @@ class _Gemm(_Stage):
             elif self.small_wgrad:
                 O.smallconv_wgrad(self.inp.buf, dout, self.gW, g)
             else:
-                O.conv_wgrad(self.inp.buf, dout, self.gW, g)
+                O.conv_wgrad(self.inp.buf, dout, self.gW, g, scratch=p.wscratch)
             if self.need_dgrad and self.small_dgrad:
                 O.smallconv_dgrad(dout, self.Wrow, self.inp.root().grad, g, accum=self.accum[self.inp.root().id])
             elif self.need_dgrad:
@@ -416,7 +427,7 @@ class _Gemm(_Stage):
                              scratch=p.scratch)
         else:
             rows = self.inp.rows(B)
-            O.dense_wgrad(self.inp.buf, dout, self.gW.view(self.W.shape[0], -1), rows)
+            O.dense_wgrad(self.inp.buf, dout, self.gW.view(self.W.shape[0], -1), rows, scratch=p.wscratch)
             if self.need_dgrad:
                 O.dense_dgrad(dout, self.Wrow, self.inp.root().grad, rows, accum=self.accum[self.inp.root().id],
                               scratch=p.scratch)
@@ -651,7 +662,7 @@ class _Head(_Stage):
     def bwd(self, p, B):
         if self.gb is not None:
             O.act_bwd(self.dlogits, None, B, self.C, relu=False, dbias=self.gb)
-        O.dense_wgrad(self.inp.root().buf, self.dlogits, self.gW, B)
+        O.dense_wgrad(self.inp.root().buf, self.dlogits, self.gW, B, scratch=p.wscratch)
         if self.need_dgrad:
             O.dense_dgrad(self.dlogits, self.Wrow, self.inp.root().grad, B, accum=self.accum[self.inp.root().id])
 

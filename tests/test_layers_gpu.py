@@ -98,6 +98,14 @@ def test_conv_fwd_dgrad_wgrad(B, H, W, C, Co, k, s, pad):
     torch.cuda.synchronize()
     assert _rel(dx.float(), xr_grad.permute(0, 2, 3, 1)) < 1e-2
     assert _rel(dW, wr_grad.permute(2, 3, 1, 0)) < 1e-3
+    # split-K partials through a scratch + reduction pass (added onto an existing gradient)
+    need = O.wgrad_scratch_elems(g.K, Co, B * Ho * Wo)
+    if need:
+        dW0 = torch.randn(k, k, C, Co, device=DEV)
+        dW2 = dW0.clone()
+        O.conv_wgrad(x, dy, dW2, g, scratch=torch.full((need,), float("nan"), device=DEV))
+        torch.cuda.synchronize()
+        assert _rel(dW2 - dW0, wr_grad.permute(2, 3, 1, 0)) < 1e-3
     # accumulate mode
     dx2 = dx.clone()
     O.conv_dgrad(dy, w.contiguous(), dx2, g, accum=True)
@@ -128,6 +136,12 @@ def test_dense_fwd_dgrad_wgrad(B, fin, out, relu):
     assert _rel(y.float(), ref) < 1e-2
     assert _rel(dx.float(), dy.float() @ w.float().t()) < 1e-2
     assert _rel(dW, x.float().t() @ dy.float()) < 1e-4
+    need = O.wgrad_scratch_elems(fin, out, B)
+    if need:
+        dW2 = torch.zeros(fin, out, device=DEV)
+        O.dense_wgrad(x, dy, dW2, B, scratch=torch.full((need,), float("nan"), device=DEV))
+        torch.cuda.synchronize()
+        assert _rel(dW2, x.float().t() @ dy.float()) < 1e-4
 
 
 @pytest.mark.parametrize("R,C,relu,res,fused", [(4 * 784, 6, True, False, True), (128, 200, True, False, False),
