@@ -413,12 +413,78 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   }
   if (BK_ == B_DGRADW) kb = kpos_of(kt0 * KB + lk, p.g.Co, KW);
 
+  // Weight-gradient VEC fast path (the host guarantees 32-bit offsets): every thread's 8 rows are
+  // one tap (kh, kw) and 8 channels; each slot walks its pixel forward by KB per k-step with
+  // incremental offsets (adds and a rare wrap), no per-step index multiplications.
+  constexpr bool WFAST = (AK == A_WGRAD && VEC);
+  constexpr bool BFAST = (BK_ == B_KN && VEC);
+  struct WSlot {
+    int ow, oh, ih, iw, rowoff, coloff, bo;
+  };
+  WSlot ws[WFAST ? AS : 1];
+  int wci = 0, wHWC = 0, wBHWC = 0;
+  bool wok = false;
+  if constexpr (WFAST) {
+    const int m = m0 + vca * 8;
+    wok = m < p.M;
+    const KPos t = kpos_of(wok ? m : 0, p.g.C, p.g.KW);
+    const int WC = p.g.W * p.g.C;
+    wHWC = p.g.H * WC;
+    wBHWC = p.g.B * wHWC;
+    wci = t.c;
+    const int hw = p.g.Ho * p.g.Wo;
+#pragma unroll
+    for (int i = 0; i < AS; ++i) {
+      const int k = kt0 * KB + vka + RSA * i;
+      const int b = k / hw, rem = k - b * hw, oh = rem / p.g.Wo, ow = rem - oh * p.g.Wo;
+      const int ih = oh * p.g.sh - p.g.pt + t.kh, iw = ow * p.g.sw - p.g.pl + t.kw;
+      ws[i] = WSlot{ow, oh, ih, iw, ih * WC, iw * p.g.C, b * wHWC};
+    }
+  }
+  int bo_off[BFAST ? BS : 1];
+  if constexpr (BFAST) {
+#pragma unroll
+    for (int i = 0; i < BS; ++i) bo_off[i] = (kt0 * KB + vkb + RSB * i) * (int)p.ldb + n0 + vcb * 8;
+  }
+
   bf16x8 ra[AS], rb[BS];
   auto gload = [&](int kt) {
     const int k0 = kt * KB;
     if (AKV) {
 #pragma unroll
       for (int i = 0; i < AS; ++i) ra[i] = load_a_k8<AK, VEC>(p, ar[i], ka, k0 + lk, Cda);
+    } else if constexpr (WFAST) {
+      // KB pixels = qW output rows + rW columns (block-uniform)
+      const int qW = KB / p.g.Wo, rW = KB - qW * p.g.Wo;
+      const int WC = p.g.W * p.g.C, drow = p.g.sh * WC, wrapr = p.g.Ho * p.g.sh * WC;
+      const int wrapc = p.g.Wo * p.g.sw * p.g.C, dcol = rW * p.g.sw * p.g.C, drowq = qW * drow;
+#pragma unroll
+      for (int i = 0; i < AS; ++i) {
+        WSlot& w = ws[i];
+        const bool ok = wok && w.bo < wBHWC && (unsigned)w.ih < (unsigned)p.g.H && (unsigned)w.iw < (unsigned)p.g.W;
+        ra[i] = ok ? *reinterpret_cast<const bf16x8*>(p.a + (w.bo + w.rowoff + w.coloff + wci)) : zero8();
+        // next k-tile: KB pixels further
+        w.ow += rW;
+        w.iw += rW * p.g.sw;
+        w.coloff += dcol;
+        w.oh += qW;
+        w.ih += qW * p.g.sh;
+        w.rowoff += drowq;
+        if (w.ow >= p.g.Wo) {
+          w.ow -= p.g.Wo;
+          w.iw -= p.g.Wo * p.g.sw;
+          w.coloff -= wrapc;
+          ++w.oh;
+          w.ih += p.g.sh;
+          w.rowoff += drow;
+        }
+        while (w.oh >= p.g.Ho) {
+          w.oh -= p.g.Ho;
+          w.ih -= p.g.Ho * p.g.sh;
+          w.rowoff -= wrapr;
+          w.bo += wHWC;
+        }
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < AS; ++i) {
@@ -430,13 +496,20 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
     if (BKV) {
 #pragma unroll
       for (int i = 0; i < BS; ++i) rb[i] = load_b_k8<BK_, VEC>(p, n0 + lr + RSK * i, kb, k0 + lk);
+    } else if constexpr (BFAST) {
+      const bool nok = n0 + vcb * 8 < p.N;
+#pragma unroll
+      for (int i = 0; i < BS; ++i) {
+        rb[i] = (nok && k0 + vkb + RSB * i < p.K) ? *reinterpret_cast<const bf16x8*>(p.b + bo_off[i]) : zero8();
+        bo_off[i] += KB * (int)p.ldb;
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < BS; ++i) rb[i] = load_b_n8<VEC>(p, n0 + vcb * 8, k0 + vkb + RSB * i);
     }
     // advance the incremental decompositions to the next k-tile
     if (AKV && AK != A_ROWK) kpos_advance(ka, KB, Cda, KW);
-    if (AK == A_WGRAD) pix_advance(pa, KB, p.g.Ho, p.g.Wo);
+    if (AK == A_WGRAD && !WFAST) pix_advance(pa, KB, p.g.Ho, p.g.Wo);
     if (BK_ == B_DGRADW) kpos_advance(kb, KB, p.g.Co, KW);
   };
   auto sstore = [&](int buf) {
@@ -755,9 +828,18 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
           s2 += q * q;
         }
         if (p.relu) v = fmaxf(v, 0.f);
-        if (p.cf_mode == 1) p.cf[(long long)row * p.ldc + col] = v;
-        else if (p.cf_mode == 2) atomicAdd(&p.cf[(long long)row * p.ldc + col], v);
-        else if (p.cf_mode == 3) p.cf[(long long)blockIdx.z * p.M * p.ldc + (long long)row * p.ldc + col] = v;
+        if (AK == A_WGRAD || AK == A_COLM) {  // weight gradients: M * ldc < 2^31
+          const int e = row * (int)p.ldc + col;
+          if (p.cf_mode == 2) atomicAdd(&p.cf[e], v);
+          else if (p.cf_mode == 3) p.cf[(long long)blockIdx.z * p.M * p.ldc + e] = v;
+          else if (p.cf_mode == 1) p.cf[e] = v;
+        } else if (p.cf_mode == 1) {
+          p.cf[(long long)row * p.ldc + col] = v;
+        } else if (p.cf_mode == 2) {
+          atomicAdd(&p.cf[(long long)row * p.ldc + col], v);
+        } else if (p.cf_mode == 3) {
+          p.cf[(long long)blockIdx.z * p.M * p.ldc + (long long)row * p.ldc + col] = v;
+        }
         if (p.cb) {
           bf16* q = &p.cb[(long long)row * p.ldcb + col];
           if (p.cb_accum) v += bf2f(*q);
@@ -2167,6 +2249,10 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     p.cf_mode = 3;
   }
   const bool vec = p.avec && p.bvec;
+  if (rowk && vec) {  // the weight-gradient fast loaders index with 32-bit offsets
+    const long long asz = akind == A_WGRAD ? (long long)p.g.B * p.g.H * p.g.W * p.g.C : (long long)K * lda;
+    if (asz >= (1LL << 31) || (long long)K * ldb >= (1LL << 31) || (long long)M * N >= (1LL << 31)) return -6;
+  }
   // global_load_lds path: every k-tile inside one filter tap (see igemm_kernel)
   bool ut = true;
   if (akind == A_CONV) ut = p.g.C % KB == 0;
