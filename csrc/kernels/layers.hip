@@ -1987,26 +1987,33 @@ __global__ __launch_bounds__(256) void im2col_kernel(const bf16* __restrict__ x,
     }
     return;
   }
+  // (kh, kw, ci) of the first element of every 8-element chunk, once per block (K8 <= 256 chunks)
+  __shared__ int tap[256];
   const int K8 = Kp >> 3;
-  const long long n = (long long)g.B * g.Ho * g.Wo * K8;
-  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < n; e += (long long)pix_blocks * blockDim.x) {
-    const int k8 = (int)(e % K8);
-    const long long m = e / K8;
-    const int hw = g.Ho * g.Wo;
-    const int b = (int)(m / hw), rem = (int)(m - (long long)b * hw);
+  for (int c = threadIdx.x; c < K8; c += blockDim.x) {
+    const int k = c * 8, kc = k / g.C;
+    tap[c] = ((kc / g.KW) << 20) | ((kc % g.KW) << 10) | (k - kc * g.C);
+  }
+  __syncthreads();
+  // consecutive threads fill consecutive 16-byte chunks of a patch row (coalesced stores); 32-bit
+  // index math throughout (the host checks the sizes)
+  const int n = g.B * g.Ho * g.Wo * K8;
+  const int hw = g.Ho * g.Wo;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += pix_blocks * blockDim.x) {
+    const int m = e / K8, k8 = e - m * K8;
+    const int b = m / hw, rem = m - b * hw;
     const int oh = rem / g.Wo, ow = rem - oh * g.Wo;
     const int y0 = oh * g.sh - g.pt, x0 = ow * g.sw - g.pl;
-    int k = k8 * 8;
-    int kc = k / g.C, ci = k - kc * g.C;
-    int kh = kc / g.KW, kw = kc - kh * g.KW;
+    const int t = tap[k8];
+    int kh = t >> 20, kw = (t >> 10) & 1023, ci = t & 1023;
+    const int k = k8 * 8;
+    const bf16* xb = x + b * g.H * g.W * g.C;
     bf16x8 v;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      float val = 0.f;
       const int ih = y0 + kh, iw = x0 + kw;
-      if (k + j < K && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
-        val = bf2f(x[(((long long)b * g.H + ih) * g.W + iw) * g.C + ci]);
-      v[j] = f2bf(val);
+      v[j] = (k + j < K && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W) ? xb[(ih * g.W + iw) * g.C + ci]
+                                                                                      : (bf16)0.0f;
       if (++ci == g.C) {
         ci = 0;
         if (++kw == g.KW) {
@@ -2015,7 +2022,7 @@ __global__ __launch_bounds__(256) void im2col_kernel(const bf16* __restrict__ x,
         }
       }
     }
-    *reinterpret_cast<bf16x8*>(out + m * Kp + k) = v;
+    *reinterpret_cast<bf16x8*>(out + (long long)m * Kp + k) = v;
   }
 }
 
@@ -2478,6 +2485,9 @@ TDE_API int tde_im2col(const bf16* x, const int* geo, int Kp, bf16* out, const b
                        hipStream_t stream) {
   Geo g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9], geo[10], geo[11], geo[12]};
   if (Kp % 8 || Kp < g.KH * g.KW * g.C || ((uintptr_t)out & 15)) return -1;
+  if (Kp / 8 > 256 || g.C >= 1024 || g.KW >= 1024) return -2;  // per-block tap table / packing
+  if ((long long)g.B * g.Ho * g.Wo * (Kp / 8) >= (1LL << 31) || (long long)g.B * g.H * g.W * g.C >= (1LL << 31))
+    return -4;
   const int pix = grid_for((long long)g.B * g.Ho * g.Wo * (Kp / 8));
   const int wb = w_in ? 8 : 0;
   im2col_kernel<<<pix + wb, 256, 0, stream>>>(x, g, Kp, out, w_in, w_out, pix);
