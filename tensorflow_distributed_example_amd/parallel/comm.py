@@ -273,31 +273,38 @@ class XgmiCommunicator(Communicator):
         timeout_s = float(timeout_s or os.environ.get("TDE_XGMI_TIMEOUT", 300))
         self.timeout_ticks = int(timeout_s * 1e8)   # s_memrealtime: 100 MHz
         self.window, self.epoch, self.err = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        self._opened = []
+        # every step below that can fail on one rank is followed by an agreement among all ranks, so a
+        # failure anywhere makes EVERY rank raise (no rank is left waiting in a collective)
         hb = C.create_string_buffer(self.lib.tde_xgmi_ipc_handle_bytes())
         rc = self.lib.tde_xgmi_alloc(self.device.index, self.max_elems, self.uncached, C.byref(self.window),
                                      C.byref(self.epoch), C.byref(self.err), hb)
-        if rc != 0:
-            raise RuntimeError(f"xGMI window allocation failed ({rc})")
+        if os.environ.get("TDE_XGMI_FAIL_RANK") == str(self.rank):   # fault injection (tests)
+            rc = -999
         handles = [None] * self.world
-        dist.all_gather_object(handles, hb.raw, group=group)
-        self._opened = []
-        peers = []
-        try:
-            for r, h in enumerate(handles):
-                if r == self.rank:
-                    peers.append(self.window.value)
-                    continue
-                m = C.c_void_p()
-                rc = self.lib.tde_xgmi_open(self.device.index, h, C.byref(m))
-                if rc != 0:
-                    raise RuntimeError(f"hipIpcOpenMemHandle of rank {r}'s window failed ({rc})")
-                self._opened.append(m.value)
-                peers.append(m.value)
-        except Exception:
-            self.close()
-            raise
+        dist.all_gather_object(handles, hb.raw if rc == 0 else None, group=group)
+        if any(h is None for h in handles):
+            self._free()
+            raise RuntimeError(f"xGMI window allocation failed on rank(s) "
+                               f"{[r for r, h in enumerate(handles) if h is None]} (local rc {rc})")
+        peers, err = [], None
+        for r, h in enumerate(handles):
+            if r == self.rank:
+                peers.append(self.window.value)
+                continue
+            m = C.c_void_p()
+            rc = self.lib.tde_xgmi_open(self.device.index, h, C.byref(m))
+            if rc != 0:
+                err = f"hipIpcOpenMemHandle of rank {r}'s window failed ({rc})"
+                break
+            self._opened.append(m.value)
+            peers.append(m.value)
+        oks = [None] * self.world
+        dist.all_gather_object(oks, err, group=group)
+        if any(o is not None for o in oks):
+            self._free()
+            raise RuntimeError(f"xGMI peer mapping failed: {[o for o in oks if o]}")
         self.peers = (C.c_void_p * self.world)(*peers)
-        dist.barrier(group=group)
 
     def nblocks(self, M):
         if self.nblocks_override:
@@ -344,13 +351,16 @@ class XgmiCommunicator(Communicator):
         if hasattr(self.fallback, "abort"):
             self.fallback.abort()
 
-    def close(self):
+    def _free(self):
         for m in getattr(self, "_opened", []):
             self.lib.tde_xgmi_close(m)
         self._opened = []
         if self.window:
             self.lib.tde_xgmi_free(self.window, self.epoch, self.err)
-            self.window = self.epoch = self.err = C.c_void_p()
+        self.window = self.epoch = self.err = C.c_void_p()
+
+    def close(self):
+        self._free()
         if self.fallback is not None:
             self.fallback.close()
 
@@ -360,6 +370,8 @@ class XgmiCommunicator(Communicator):
         n = n or min(self.max_elems, 347_146 + 37)
         idx = torch.arange(n, device=self.device, dtype=torch.float32)
         ok = True
+        # a broken fabric path must not park the test for the production timeout: 10 s per wait here
+        saved, self.timeout_ticks = self.timeout_ticks, int(10 * 1e8)
         for it in range(3):
             parts = [((idx * 0.37 + r * 1.91 + it) % 7.0) - 3.0 for r in range(self.world)]
             want = parts[0].clone()
@@ -370,6 +382,7 @@ class XgmiCommunicator(Communicator):
             torch.cuda.synchronize(self.device)
             ok = ok and bool(torch.equal(t, want))
         ok = ok and self.lib.tde_xgmi_error(self.err) == 0
+        self.timeout_ticks = saved
         return ok
 
 
@@ -410,9 +423,14 @@ def maybe_xgmi(fallback, device, rank, world, bucket_hint=None, group=None):
     xg = None
     try:
         xg = XgmiCommunicator(device, rank, world, fallback, group=group)
-        ok = xg.self_test()
-    except Exception as e:  # noqa: BLE001 - any failure keeps RCCL
-        ok, err = False, e
+    except Exception as e:  # noqa: BLE001 - raised consistently on every rank; keeps RCCL
+        xg, err = None, e
+    ok = False
+    if xg is not None:
+        try:
+            ok = xg.self_test()
+        except Exception as e:  # noqa: BLE001
+            ok, err = False, e
     flags = [None] * world
     dist.all_gather_object(flags, bool(ok), group=group)
     if not all(flags):

@@ -140,3 +140,37 @@ def test_mwms_bench_two_ranks_on_xgmi(tmp_path):
     assert res["config"]["allreduce"] == "xgmi", res
     assert res["config"]["hipgraph"] is True, res
     assert "replicas_identical=True" in r.stdout, r.stdout[-3000:]
+
+
+FALLBACK = r"""
+import json, os, sys
+sys.path.insert(0, {root!r})
+import torch, torch.distributed as dist
+from tensorflow_distributed_example_amd.parallel import comm as CM
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+torch.cuda.set_device(0)
+dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+fb = CM.TorchDistCommunicator(1)
+c = CM.maybe_xgmi(fb, torch.device("cuda:0"), rank, world)
+t = torch.full((1000,), float(rank + 1), device="cuda")
+c.all_reduce_([t])
+torch.cuda.synchronize()
+print("RESULT" + json.dumps({{"kind": type(c).__name__, "sum": float(t[0])}}), flush=True)
+"""
+
+
+def test_xgmi_setup_failure_on_one_rank_falls_back_everywhere():
+    """A window that fails on ONE rank must make every rank keep the fallback (no rank left waiting)."""
+    port = _free_port()
+    script = FALLBACK.format(root=ROOT, port=port)
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", OMP_NUM_THREADS="2", TDE_ALLREDUCE="xgmi",
+                   TDE_XGMI_FAIL_RANK="1")
+        procs.append(subprocess.Popen([sys.executable, "-c", script], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    for p in procs:
+        o, _ = p.communicate(timeout=180)
+        assert p.returncode == 0, o[-3000:]
+        res = json.loads(o.split("RESULT")[1].strip())
+        assert res["kind"] == "TorchDistCommunicator" and res["sum"] == 3.0, res
