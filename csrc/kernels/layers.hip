@@ -1179,6 +1179,59 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdArgs a) {
   }
 }
 
+// Narrow layers (C <= CM, C % 8 != 0: Model B's 6 / 12 channel BNs): one thread per ROW keeps all
+// C channels' partial sums in registers (no per-element channel arithmetic, no LDS atomics); the
+// block folds them with DPP row reductions and lands 2C global atomics.  Batch-statistics mode
+// without dropout only (the general kernel covers the rest).
+template <int CM>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_rows_kernel(BnBwdArgs a) {
+  __shared__ float red[4][2 * CM];
+  const int C = a.C;
+  float sc[CM], sf[CM], mu[CM], rs[CM], r1[CM], r2[CM];
+#pragma unroll
+  for (int c = 0; c < CM; ++c) {
+    const bool ok = c < C;
+    mu[c] = ok ? a.saved[c] : 0.f;
+    rs[c] = ok ? a.saved[C + c] : 0.f;
+    const float g = (ok && a.gamma) ? a.gamma[c] : 1.f;
+    sc[c] = g * rs[c];
+    sf[c] = ((ok && a.beta) ? a.beta[c] : 0.f) - mu[c] * sc[c];
+    r1[c] = r2[c] = 0.f;
+  }
+  for (long long row = blockIdx.x * (long long)blockDim.x + threadIdx.x; row < a.R;
+       row += (long long)gridDim.x * blockDim.x) {
+    const long long e = row * C;
+#pragma unroll
+    for (int c = 0; c < CM; ++c) {
+      if (c < C) {
+        const float v = bf2f(a.y[e + c]);
+        const float z = v * sc[c] + sf[c] + (a.res ? bf2f(a.res[e + c]) : 0.f);
+        float g = bf2f(a.dout[e + c]);
+        if (a.relu && !(z > 0.f)) g = 0.f;
+        r1[c] += g;
+        r2[c] += g * (v - mu[c]) * rs[c];
+      }
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < CM; ++c) {
+    if (c < C) {
+      const float t1 = rows4_sum(row16_sum(r1[c])), t2 = rows4_sum(row16_sum(r2[c]));
+      if (lane == 0) {
+        red[wave][c] = t1;
+        red[wave][CM + c] = t2;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * C) {
+    const int c = threadIdx.x % C, w = threadIdx.x / C;
+    const float v = (red[0][w * CM + c] + red[1][w * CM + c]) + (red[2][w * CM + c] + red[3][w * CM + c]);
+    atomicAdd(a.dstats + (size_t)(blockIdx.x % kStatSlots) * 2 * C + w * C + c, v);
+  }
+}
+
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(BnBwdArgs a) {
   __shared__ float sc[kMaxCB], sf[kMaxCB], mu[kMaxCB], rs[kMaxCB], k1[kMaxCB], k2[kMaxCB];
   bn_bwd_prologue(a, sc, sf, mu, rs);
@@ -2391,7 +2444,14 @@ TDE_API int tde_bn_bwd(const bf16* dout, const bf16* y, const bf16* res, long lo
     return 0;
   }
   const int g = grid_for(R * C, 8);
-  if (mode == 1) {
+  if (mode == 1 && C <= 16 && drop_rate == 0.f) {
+    // narrow layers: row-per-thread reduction (~2 rows per thread, <= 256 blocks)
+    long long gr = (R + 511) / 512;
+    gr = gr < 1 ? 1 : (gr > 256 ? 256 : gr);
+    if (C <= 8) bn_bwd_reduce_rows_kernel<8><<<(int)gr, 256, 0, stream>>>(a);
+    else bn_bwd_reduce_rows_kernel<16><<<(int)gr, 256, 0, stream>>>(a);
+    TDE_LAUNCH_CHECK();
+  } else if (mode == 1) {
     // Reduction grid: <= 2 blocks per CU (each block ends with 2*C global atomics, so more blocks only
     // add contention), rounded to a multiple of C / gcd(2048, C) so the grid stride is a multiple of C
     // and every thread accumulates fixed channels in registers.
