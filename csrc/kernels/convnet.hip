@@ -64,7 +64,9 @@ __global__ __launch_bounds__(1024) void convnet_fwd_kernel(ConvNetFwdArgs a) {
   const int b0 = blockIdx.y * 64;
   const int b = b0 + lane;
   const bool bok = b < a.B;
-  const int pp = wave >> 2, cg = wave & 3, c0 = cg * 8;
+  // wave-uniform: the conv weights of this wave's 8 channels are scalar loads (SGPRs), not 72 VGPRs
+  const int pp = __builtin_amdgcn_readfirstlane(wave >> 2), cg = __builtin_amdgcn_readfirstlane(wave & 3),
+            c0 = cg * 8;
   const int p = p0 + pp;
   const bool pok = p < P;
   const int py0 = p0 / Wp;
