@@ -29,7 +29,7 @@ OBJDIR = ROOT / "build" / "obj"
 
 HIP_SOURCES = sorted((CSRC / "kernels").glob("*.hip")) + [CSRC / "comm" / "rccl_comm.cpp",
                                                            CSRC / "comm" / "xgmi_allreduce.hip"]
-HOST_DIRS = ["host", "io", "ps"]
+HOST_DIRS = ["host", "io", "ps", "data"]
 
 
 def _host_sources():

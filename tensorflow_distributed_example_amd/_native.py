@@ -103,6 +103,13 @@ _HOST_PROTOS: dict = {
     "tde_crc32c_masked": (u32, [p, sz]),
     "tde_crc32c_mask": (u32, [u32]),
     "tde_crc32c_unmask": (u32, [u32]),
+    # tf.data pipeline engine (csrc/data/pipeline.cpp)
+    "tde_shuffle_new": (p, [i64, C.c_ulonglong]),
+    "tde_shuffle_free": (None, [p]),
+    "tde_shuffle_feed": (i64, [p, p, i64, p]),
+    "tde_shuffle_drain": (i64, [p, p]),
+    "tde_shuffle_size": (i64, [p]),
+    "tde_gather_rows": (i32, [p, i64, i64, p, i64, p, i32]),
 }
 
 

@@ -15,6 +15,7 @@ those indices.  ``prefetch`` runs the upstream iterator in a background thread.
 from __future__ import annotations
 
 import enum
+import os
 import queue
 import threading
 
@@ -76,6 +77,39 @@ def _np(a):
     except Exception:  # pragma: no cover
         pass
     return np.asarray(a)
+
+
+_CHUNK = 8192
+
+
+def _chunked(it):
+    buf = []
+    for i in it:
+        buf.append(i)
+        if len(buf) == _CHUNK:
+            yield np.asarray(buf, dtype=np.int64)
+            buf = []
+    if buf:
+        yield np.asarray(buf, dtype=np.int64)
+
+
+_HOST = []
+
+
+def _host_lib():
+    """libtde_host.so with the pipeline engine, or None (then numpy / Python paths are used)."""
+    if not _HOST:
+        lib = None
+        if os.environ.get("TDE_NATIVE_DATA", "1") != "0":
+            try:
+                from .. import _native as N
+                lib = N.host()
+                if not hasattr(lib, "tde_shuffle_new"):
+                    lib = None
+            except Exception:  # no compiler / library: the pipeline still works
+                lib = None
+        _HOST.append(lib)
+    return _HOST[0]
 
 
 class Dataset:
@@ -172,8 +206,14 @@ class Dataset:
     def _columns(self):
         raise NotImplementedError
 
-    def _index_stream(self, epoch_seed):
+    def _index_chunks(self, epoch_seed):
+        """The element indices this op produces, as a stream of int64 numpy arrays (chunked so the
+        per-element work — shuffling, sharding, batch gathers — runs in numpy / native code)."""
         raise NotImplementedError
+
+    def _index_stream(self, epoch_seed):
+        for c in self._index_chunks(epoch_seed):
+            yield from c.tolist()
 
     @property
     def _structure(self):
@@ -211,8 +251,9 @@ class _Source(Dataset):
     def _columns(self):
         return self._cols
 
-    def _index_stream(self, epoch_seed):
-        return iter(range(self._n))
+    def _index_chunks(self, epoch_seed):
+        for a in range(0, self._n, _CHUNK):
+            yield np.arange(a, min(a + _CHUNK, self._n), dtype=np.int64)
 
     def _element(self, i):
         if self._keys is not None:
@@ -280,8 +321,8 @@ class _Cache(_Unary):
     def _columns(self):
         return self._fill()._columns()
 
-    def _index_stream(self, epoch_seed):
-        return self._fill()._index_stream(epoch_seed)
+    def _index_chunks(self, epoch_seed):
+        return self._fill()._index_chunks(epoch_seed)
 
     def _element(self, i):
         return self._fill()._element(i)
@@ -346,13 +387,33 @@ class _Shuffle(_Unary):
     def _element(self, i):
         return self._parent._element(i)
 
-    def _index_stream(self, epoch_seed):
-        return self._shuffle_stream(self._parent._index_stream(epoch_seed), self._buf, self._rng())
+    def _index_chunks(self, epoch_seed):
+        rng = self._rng()
+        parent = self._parent._index_chunks(epoch_seed)
+        lib = _host_lib()
+        if lib is None:   # pure-Python shuffle buffer (same semantics, numpy RNG)
+            yield from _chunked(self._shuffle_stream((i for c in parent for i in c.tolist()), self._buf, rng))
+            return
+        h = lib.tde_shuffle_new(self._buf, int(rng.integers(0, 2 ** 63 - 1)))
+        try:
+            for c in parent:
+                c = np.ascontiguousarray(c, dtype=np.int64)
+                out = np.empty(len(c), np.int64)
+                m = lib.tde_shuffle_feed(h, c.ctypes.data, len(c), out.ctypes.data)
+                if m:
+                    yield out[:m]
+            out = np.empty(max(1, lib.tde_shuffle_size(h)), np.int64)
+            m = lib.tde_shuffle_drain(h, out.ctypes.data)
+            if m:
+                yield out[:m]
+        finally:
+            lib.tde_shuffle_free(h)
 
     def __iter__(self):
         if self._indexable():
-            for i in self._index_stream(None):
-                yield self._element(i)
+            for c in self._index_chunks(None):
+                for i in c.tolist():
+                    yield self._element(i)
         else:
             yield from self._shuffle_stream(iter(self._parent), self._buf, self._rng())
 
@@ -374,10 +435,15 @@ class _Repeat(_Unary):
     def _element(self, i):
         return self._parent._element(i)
 
-    def _index_stream(self, epoch_seed):
+    def _index_chunks(self, epoch_seed):
         k = 0
         while self._count is None or k < self._count:
-            yield from self._parent._index_stream(epoch_seed)
+            empty = True
+            for c in self._parent._index_chunks(epoch_seed):
+                empty = empty and len(c) == 0
+                yield c
+            if empty:
+                return
             k += 1
 
     def __iter__(self):
@@ -415,11 +481,19 @@ class _Take(_Unary):
     def _element(self, i):
         return self._parent._element(i)
 
-    def _index_stream(self, epoch_seed):
-        for k, i in enumerate(self._parent._index_stream(epoch_seed)):
-            if self._n >= 0 and k >= self._n:
+    def _index_chunks(self, epoch_seed):
+        if self._n < 0:
+            yield from self._parent._index_chunks(epoch_seed)
+            return
+        left = self._n
+        if left == 0:
+            return
+        for c in self._parent._index_chunks(epoch_seed):
+            if len(c) >= left:
+                yield c[:left]
                 return
-            yield i
+            left -= len(c)
+            yield c
 
     def __iter__(self):
         for k, e in enumerate(self._parent):
@@ -438,10 +512,15 @@ class _Take(_Unary):
 
 
 class _Skip(_Take):
-    def _index_stream(self, epoch_seed):
-        for k, i in enumerate(self._parent._index_stream(epoch_seed)):
-            if k >= self._n:
-                yield i
+    def _index_chunks(self, epoch_seed):
+        left = max(self._n, 0)
+        for c in self._parent._index_chunks(epoch_seed):
+            if left:
+                if len(c) <= left:
+                    left -= len(c)
+                    continue
+                c, left = c[left:], 0
+            yield c
 
     def __iter__(self):
         for k, e in enumerate(self._parent):
@@ -472,10 +551,13 @@ class _Shard(_Unary):
     def _element(self, i):
         return self._parent._element(i)
 
-    def _index_stream(self, epoch_seed):
-        for k, i in enumerate(self._parent._index_stream(epoch_seed)):
-            if k % self._k == self._i:
-                yield i
+    def _index_chunks(self, epoch_seed):
+        pos = 0   # position of c[0] in the parent stream: keep positions == index (mod k)
+        for c in self._parent._index_chunks(epoch_seed):
+            sel = c[(self._i - pos) % self._k::self._k]
+            pos += len(c)
+            if len(sel):
+                yield sel
 
     def __iter__(self):
         for k, e in enumerate(self._parent):
@@ -502,18 +584,26 @@ class _Batch(_Unary):
         if p._indexable():
             cols = p._columns()
             tup = p._structure
-            buf = []
-            for i in p._index_stream(None):
-                buf.append(i)
-                if len(buf) == bs:
-                    idx = np.asarray(buf)
-                    out = tuple(np.take(c, idx, axis=0) for c in cols)
-                    yield out if tup else out[0]
-                    buf = []
-            if buf and not self.drop_remainder:
-                idx = np.asarray(buf)
-                out = tuple(np.take(c, idx, axis=0) for c in cols)
-                yield out if tup else out[0]
+            lib = _host_lib()
+
+            def emit(idx):
+                out = _gather(cols, idx, lib)
+                return out if tup else out[0]
+
+            pend, npend = [], 0
+            for c in p._index_chunks(None):
+                pend.append(c)
+                npend += len(c)
+                if npend < bs:
+                    continue
+                cur = np.concatenate(pend) if len(pend) > 1 else pend[0]
+                nfull = len(cur) // bs
+                for k in range(nfull):
+                    yield emit(cur[k * bs:(k + 1) * bs])
+                rest = cur[nfull * bs:]
+                pend, npend = ([rest] if len(rest) else []), len(rest)
+            if npend and not self.drop_remainder:
+                yield emit(np.concatenate(pend))
             return
         buf = []
         for e in p:
@@ -532,6 +622,24 @@ class _Batch(_Unary):
 
     def _rebuild(self, p):
         return _Batch(p, self.batch_size, self.drop_remainder)
+
+
+def _gather(cols, idx, lib):
+    """Rows ``idx`` of every column: native multi-threaded row gather (csrc/data/pipeline.cpp) for
+    plain contiguous arrays, numpy ``take`` otherwise."""
+    idx = np.ascontiguousarray(idx, dtype=np.int64)
+    out = []
+    for c in cols:
+        if lib is not None and isinstance(c, np.ndarray) and c.flags.c_contiguous and c.dtype != object and len(c):
+            dst = np.empty((len(idx),) + c.shape[1:], c.dtype)
+            rc = lib.tde_gather_rows(c.ctypes.data, c.itemsize * (c.size // len(c)), len(c), idx.ctypes.data,
+                                     len(idx), dst.ctypes.data, 8)
+            if rc != 0:
+                raise IndexError("dataset index out of range")
+            out.append(dst)
+        else:
+            out.append(np.take(c, idx, axis=0))
+    return tuple(out)
 
 
 def _stack(buf):
@@ -622,8 +730,8 @@ class _WithOptions(_Unary):
     def _element(self, i):
         return self._parent._element(i)
 
-    def _index_stream(self, epoch_seed):
-        return self._parent._index_stream(epoch_seed)
+    def _index_chunks(self, epoch_seed):
+        return self._parent._index_chunks(epoch_seed)
 
     def __iter__(self):
         return iter(self._parent)

@@ -75,3 +75,69 @@ def test_mnist_synthetic_shapes():
     assert xt.shape == (60000, 28, 28) and xt.dtype == np.uint8
     assert xe.shape == (10000, 28, 28) and yt.shape == (60000,)
     assert set(np.unique(yt)) == set(range(10))
+
+
+def _ref_ops(n, ops):
+    """Plain-Python model of take/skip/shard/repeat over range(n)."""
+    v = list(range(n))
+    for op, *a in ops:
+        if op == "shard":
+            v = v[a[1]::a[0]]
+        elif op == "skip":
+            v = v[a[0]:]
+        elif op == "take":
+            v = v[:a[0]]
+        elif op == "repeat":
+            v = v * a[0]
+    return v
+
+
+@pytest.mark.parametrize("native", ["1", "0"])
+def test_chunked_index_ops_across_chunk_boundaries(native, monkeypatch):
+    """The index protocol runs in numpy chunks of 8192 (data/dataset.py _CHUNK): take/skip/shard/
+    repeat and batching must not depend on where the chunk boundaries fall."""
+    from tensorflow_distributed_example_amd.data import dataset as D
+    monkeypatch.setattr(D, "_HOST", [])
+    monkeypatch.setenv("TDE_NATIVE_DATA", native)
+    n = 20011
+    x = np.arange(n, dtype=np.int64)
+    cases = [[("shard", 3, 1), ("skip", 5000), ("take", 4099)],
+             [("skip", 8191), ("take", 8194)],
+             [("repeat", 3), ("shard", 5, 4), ("skip", 7), ("take", 9000)],
+             [("take", 0)], [("skip", 30000)]]
+    for ops in cases:
+        ds = Dataset.from_tensor_slices(x)
+        for op, *a in ops:
+            ds = getattr(ds, op)(*a)
+        want = _ref_ops(n, ops)
+        got = np.concatenate(list(ds.batch(1000))).tolist() if want else list(ds.batch(1000))
+        assert got == want, ops
+
+
+def test_native_shuffle_buffer_semantics_large():
+    """Native shuffle buffer (csrc/data/pipeline.cpp): a permutation per epoch, seeded replay,
+    reshuffled across repeat() epochs, and TF's locality bound (out position >= in position - buffer)."""
+    from tensorflow_distributed_example_amd.data import dataset as D
+    assert D._host_lib() is not None, "libtde_host.so pipeline engine missing"
+    n, buf = 30000, 1000
+    x = np.arange(n)
+    ds = Dataset.from_tensor_slices(x).shuffle(buf, seed=7).repeat(2).batch(512)
+    out = np.concatenate(list(ds))
+    e0, e1 = out[:n], out[n:]
+    assert sorted(e0.tolist()) == list(range(n)) and sorted(e1.tolist()) == list(range(n))
+    assert not np.array_equal(e0, e1)
+    pos = np.empty(n, np.int64)
+    pos[e0] = np.arange(n)
+    assert np.all(pos >= np.arange(n) - buf)
+    again = np.concatenate(list(Dataset.from_tensor_slices(x).shuffle(buf, seed=7).repeat(2).batch(512)))
+    assert np.array_equal(out, again)
+
+
+def test_native_gather_matches_numpy_for_all_column_kinds():
+    imgs = np.random.default_rng(0).random((3000, 28, 28, 1)).astype(np.float32)
+    lab = np.arange(3000, dtype=np.int64)
+    strided = np.arange(6000, dtype=np.int32)[::2]          # not contiguous: numpy take path
+    ds = Dataset.from_tensor_slices((imgs, lab, strided)).shuffle(500, seed=3).batch(128)
+    for bi, bl, bs in ds:
+        assert np.array_equal(bi, imgs[bl]) and np.array_equal(bs, strided[bl])
+        assert bi.dtype == np.float32 and bs.dtype == np.int32
