@@ -58,7 +58,8 @@ def _split_xy(elem):
 
 
 def _stack_steps(batches):
-    """list over steps of per-replica [(x,y)] -> per-replica (x[S,...], y[S,...])."""
+    """list over steps of per-replica [(x,y)] -> per-replica (x[S,...], y[S,...]); numpy steps stay
+    lists (the stager packs them straight into its pinned buffer)."""
     R = len(batches[0])
     out = []
     for r in range(R):
@@ -67,7 +68,7 @@ def _stack_steps(batches):
         if torch.is_tensor(xs[0]):
             out.append((torch.stack(xs), torch.stack(ys)))
         else:
-            out.append((np.stack(xs), np.stack(ys)))
+            out.append((xs, ys))
     return out
 
 

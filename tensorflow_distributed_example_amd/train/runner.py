@@ -35,21 +35,39 @@ class _Stager:
         self.k = 0
 
     def stage(self, arr, dst):
-        """Copy numpy/torch ``arr`` into device tensor ``dst`` (same numel)."""
+        """Copy numpy/torch ``arr`` into device tensor ``dst`` (same numel).  ``arr`` may also be a
+        list of per-step numpy arrays: they are packed straight into the pinned buffer (no stack)."""
+        if isinstance(arr, (list, tuple)):
+            buf = self._next_buf()
+            flat = buf.view(-1).numpy()
+            n = 0
+            for part in arr:
+                part = np.asarray(part)
+                np.copyto(flat[n: n + part.size], part.reshape(-1), casting="unsafe")
+                n += part.size
+            self._launch(flat_t=buf.view(-1), n=n, dst=dst)
+            return
         if torch.is_tensor(arr) and arr.device == dst.device:
             dst.view(-1)[: arr.numel()].copy_(arr.reshape(-1).to(dst.dtype), non_blocking=True)
             return
         if torch.is_tensor(arr):
             arr = arr.detach().cpu().numpy()
         arr = np.asarray(arr)
-        buf = self.bufs[self.k]
-        ev = self.events[self.k]
-        if ev is not None:
-            ev.synchronize()
+        buf = self._next_buf()
         flat = buf.view(-1)
         n = arr.size
         np.copyto(flat[:n].numpy(), arr.reshape(-1), casting="unsafe")
-        dst.view(-1)[:n].copy_(flat[:n], non_blocking=self.cuda)
+        self._launch(flat_t=flat, n=n, dst=dst)
+
+    def _next_buf(self):
+        buf = self.bufs[self.k]
+        ev = self.events[self.k]
+        if ev is not None:
+            ev.synchronize()   # the H2D copy that last read this buffer is done
+        return buf
+
+    def _launch(self, flat_t, n, dst):
+        dst.view(-1)[:n].copy_(flat_t[:n], non_blocking=self.cuda)
         if self.cuda:
             e = torch.cuda.Event()
             e.record(torch.cuda.current_stream(self.device))
