@@ -31,6 +31,8 @@ METRIC = "images/sec (whole node) MNIST CNN at 1/2/4/8 MI355X; step time ms"
 MODELS = {
     "mnist_cnn": (64, 16, 0.001, True, (28, 28, 1), METRIC),
     "mnist_bn_cnn": (128, 16, 0.01, False, (784,), METRIC),
+    "lenet5": (128, 16, 0.01, True, (28, 28, 1), "images/sec (whole node) MNIST LeNet-5 CNN bf16 at 1/2/4/8 MI355X; step time ms"),
+    "mnist_mlp": (128, 16, 0.01, True, (28, 28, 1), "images/sec (whole node) MNIST dense MLP at 1/2/4/8 MI355X; step time ms"),
     "resnet18": (64, 1, 0.1, True, (224, 224, 3),
                  "images/sec (whole node) synthetic 224x224x3 ResNet-18 bf16 at 1/2/4/8 MI355X; step time ms"),
 }
@@ -139,7 +141,7 @@ def main():
         print(json.dumps({
             "metric": metric, "value": round(ips, 1), "unit": "images/sec", "n_gpus": n, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16",
+            "vs_baseline": None, "dtype": "bf16" if prog.plan_kind != "reference" else "fp32",
             "data": f"synthetic (random {'x'.join(map(str, img))} images, random labels; random-init weights)",
             "config": {"model": a.model, "global_batch": GB, "seq_len": None, "image_shape": list(img),
                        "per_gpu_batch": B, "parallelism": f"dp{n}", "strategy": "MultiWorkerMirroredStrategy",

@@ -26,7 +26,34 @@ MODELS = {  # per-GPU batch, lr, image shape (NHWC), classes
     "mnist_cnn": (64, 0.001, (28, 28, 1), 10),
     "mnist_bn_cnn": (128, 0.01, (28, 28, 1), 10),
     "resnet18": (64, 0.1, (224, 224, 3), 1000),
+    "lenet5": (128, 0.01, (28, 28, 1), 10),
+    "mnist_mlp": (128, 0.01, (28, 28, 1), 10),
 }
+
+
+class LeNet5(nn.Module):  # models/zoo.py lenet5
+    def __init__(self):
+        super().__init__()
+        self.c1 = nn.Conv2d(1, 6, 5, padding=2)
+        self.c2 = nn.Conv2d(6, 16, 5)
+        self.f1 = nn.Linear(400, 120)
+        self.f2 = nn.Linear(120, 84)
+        self.f3 = nn.Linear(84, 10)
+
+    def forward(self, x):
+        x = F.max_pool2d(F.relu(self.c1(x)), 2)
+        x = F.max_pool2d(F.relu(self.c2(x)), 2)
+        return self.f3(F.relu(self.f2(F.relu(self.f1(x.flatten(1))))))
+
+
+class MLP(nn.Module):  # models/zoo.py mnist_mlp
+    def __init__(self):
+        super().__init__()
+        self.f1 = nn.Linear(784, 128)
+        self.f2 = nn.Linear(128, 10)
+
+    def forward(self, x):
+        return self.f2(F.relu(self.f1(x.flatten(1))))
 
 
 class MnistCNN(nn.Module):  # distributed_with_keras.py:33-39
@@ -114,7 +141,8 @@ def main():
     if world > 1:
         torch.distributed.init_process_group("nccl", device_id=dev)
     torch.manual_seed(1234)
-    model = {"mnist_cnn": MnistCNN, "mnist_bn_cnn": MnistBNCNN, "resnet18": lambda: ResNet18(ncls)}[a.model]()
+    model = {"mnist_cnn": MnistCNN, "mnist_bn_cnn": MnistBNCNN, "resnet18": lambda: ResNet18(ncls),
+             "lenet5": LeNet5, "mnist_mlp": MLP}[a.model]()
     model = model.to(dev)
     mf = torch.channels_last if a.channels_last else torch.contiguous_format
     model = model.to(memory_format=mf)

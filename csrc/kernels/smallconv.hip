@@ -158,12 +158,14 @@ __global__ __launch_bounds__(256) void smallconv_dgrad_kernel(const bf16* __rest
 // M = K rows of a 64-row MFMA tile with scalar C = 1 gathers over a 100k-pixel reduction; here each thread
 // keeps all K x CO partial sums in registers over a grid-stride run of pixels, the block folds them with
 // DPP row reductions + LDS, and one f32 atomic per (k, co) per block lands in the gradient bucket.
+// Filters with more than KMAX taps (LeNet-5 conv1: 5x5x1 -> 6, K = 25) split the taps over blockIdx.y.
 template <int CO>
 __global__ __launch_bounds__(256) void smallconv_wgrad_kernel(const bf16* __restrict__ x, const bf16* __restrict__ dy,
                                                               float* __restrict__ dw, SGeo g) {
   constexpr int KMAX = 128 / CO;
   __shared__ float red[4][KMAX * CO];
-  const int K = g.KH * g.KW * g.C;
+  const int kbase = blockIdx.y * KMAX;
+  const int K = min(KMAX, g.KH * g.KW * g.C - kbase);   // taps [kbase, kbase + K) of this block
   float acc[KMAX][CO];
 #pragma unroll
   for (int k = 0; k < KMAX; ++k)
@@ -182,7 +184,7 @@ __global__ __launch_bounds__(256) void smallconv_wgrad_kernel(const bf16* __rest
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
       if (k < K) {
-        const int ci = k % g.C, t = k / g.C;
+        const int ci = (kbase + k) % g.C, t = (kbase + k) / g.C;
         const int kw = t % g.KW, kh = t / g.KW;
         const int ih = y0 + kh, iw = x0 + kw;
         float xv = 0.f;
@@ -207,7 +209,7 @@ __global__ __launch_bounds__(256) void smallconv_wgrad_kernel(const bf16* __rest
   __syncthreads();
   for (int i = threadIdx.x; i < K * CO; i += blockDim.x) {
     const int k = i / CO, c = i - k * CO;
-    if (c < g.Co) atomicAdd(&dw[k * g.Co + c], (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]));
+    if (c < g.Co) atomicAdd(&dw[(kbase + k) * g.Co + c], (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]));
   }
 }
 
@@ -263,22 +265,25 @@ TDE_API int tde_smallconv_wgrad(const bf16* x, const bf16* dy, float* dw, const 
   const SGeo g = sgeo(geo);
   const int co = round8(g.Co);
   const int K = g.KH * g.KW * g.C;
-  if (co > 32 || K * co > 128) return -1;
+  const int cot = co == 24 ? 32 : co;   // the kernel instance the switch below picks
+  if (co > 32 || K * co > 1024) return -1;
   if ((long long)g.B * g.H * g.W * g.C >= (1LL << 31) || (long long)g.B * g.Ho * g.Wo * g.Co >= (1LL << 31)) return -4;
   const int npix = g.B * g.Ho * g.Wo;
   int grid = (npix + 256 * 2 - 1) / (256 * 2);   // ~2 pixels per thread, <= one block per CU
   grid = grid < 1 ? 1 : (grid > 256 ? 256 : grid);
+  const int kchunks = (K + 128 / cot - 1) / (128 / cot);
+  const dim3 gr(grid, kchunks);
   switch (co) {
-    case 8: smallconv_wgrad_kernel<8><<<grid, 256, 0, stream>>>(x, dy, dw, g); break;
-    case 16: smallconv_wgrad_kernel<16><<<grid, 256, 0, stream>>>(x, dy, dw, g); break;
-    default: smallconv_wgrad_kernel<32><<<grid, 256, 0, stream>>>(x, dy, dw, g); break;
+    case 8: smallconv_wgrad_kernel<8><<<gr, 256, 0, stream>>>(x, dy, dw, g); break;
+    case 16: smallconv_wgrad_kernel<16><<<gr, 256, 0, stream>>>(x, dy, dw, g); break;
+    default: smallconv_wgrad_kernel<32><<<gr, 256, 0, stream>>>(x, dy, dw, g); break;
   }
   TDE_LAUNCH_CHECK();
   return 0;
 }
 
 TDE_API int tde_smallconv_wgrad_ok(int C, int Co, int KH, int KW) {
-  return round8(Co) <= 32 && KH * KW * C * round8(Co) <= 128;
+  return round8(Co) <= 32 && KH * KW * C * round8(Co) <= 1024;   // <= 8 tap chunks of 128 partial sums
 }
 
 TDE_API int tde_smallconv_ok(int C, int Co, int KH, int KW, int dgrad) {

@@ -4,6 +4,14 @@
   347,146 trainable params.
 * ``mnist_bn_cnn()`` — Model B, mnist_keras_distributed.py:79-109 (== tf2_mnist_distributed.py:105-135):
   250,466 trainable + 484 non-trainable params.
+
+Models for the remaining BASELINE.json configs (not in the reference):
+
+* ``lenet5()``    — "MNIST LeNet-5 CNN bf16, MirroredStrategy on 1 MI355X": LeNet-5 with ReLU and max
+  pooling, 61,706 trainable params.
+* ``mnist_mlp()`` — "tf2_mnist_distributed.py dense MLP on CPU, MirroredStrategy devices=1":
+  Flatten · Dense(128, relu) · Dense(10), 101,770 trainable params.
+* ``resnet18()``  — "Synthetic 224x224x3 ResNet-18 bf16 on 8xMI355X".
 """
 from __future__ import annotations
 
@@ -39,6 +47,27 @@ def mnist_bn_cnn(name=None):
         L.Activation("relu"),
         L.Dropout(0.5),
         L.Dense(10, activation="softmax"),
+    ], name=name)
+
+
+def lenet5(name=None):
+    return Sequential([
+        L.Conv2D(6, 5, padding="same", activation="relu", input_shape=(28, 28, 1)),
+        L.MaxPooling2D(),
+        L.Conv2D(16, 5, activation="relu"),
+        L.MaxPooling2D(),
+        L.Flatten(),
+        L.Dense(120, activation="relu"),
+        L.Dense(84, activation="relu"),
+        L.Dense(10),
+    ], name=name)
+
+
+def mnist_mlp(name=None):
+    return Sequential([
+        L.Flatten(input_shape=(28, 28, 1)),
+        L.Dense(128, activation="relu"),
+        L.Dense(10),
     ], name=name)
 
 

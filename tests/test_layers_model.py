@@ -32,6 +32,35 @@ def test_model_b_params_and_names():
     assert "dense_1/bias" in names and "dense/bias" not in names
 
 
+def test_baseline_config_models_lenet5_and_mlp():
+    """BASELINE.json configs beyond the reference's two models."""
+    m = tde.zoo.lenet5()
+    m.build()
+    assert m.count_params() == 61706
+    assert [w.shape for w in m.get_weights()][:4] == [(5, 5, 1, 6), (6,), (5, 5, 6, 16), (16,)]
+    assert m.output_shape == (None, 10)
+    m = tde.zoo.mnist_mlp()
+    m.build()
+    assert m.count_params() == 101770 and m.output_shape == (None, 10)
+
+
+def test_mlp_plumbing_config_on_cpu_mirrored_one_device():
+    """'tf2_mnist_distributed.py dense MLP on CPU, MirroredStrategy devices=1 (plumbing, no GPU)'."""
+    tde.backend.set_random_seed(0)
+    st = tde.distribute.MirroredStrategy(devices=["/cpu:0"])
+    assert st.num_replicas_in_sync == 1
+    with st.scope():
+        m = tde.zoo.mnist_mlp()
+        m.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True),
+                  optimizer=tde.optimizers.SGD(0.1), metrics=["accuracy"])
+    rng = np.random.default_rng(0)
+    x = rng.random((512, 28, 28, 1), dtype=np.float32)
+    y = (x.reshape(512, -1)[:, :10].argmax(1)).astype(np.int64)     # learnable synthetic labels
+    h = m.fit(tde.data.Dataset.from_tensor_slices((x, y)).shuffle(512, seed=1).repeat().batch(64), epochs=4,
+              steps_per_epoch=16, verbose=0)
+    assert h.history["loss"][-1] < h.history["loss"][0]
+
+
 def test_summary_text():
     m = tde.zoo.mnist_cnn()
     buf = []
