@@ -145,3 +145,18 @@ def test_evaluator_polls_new_checkpoints(tmp_path):
     est.train(_input_fn(x, y), max_steps=10)
     t.join(timeout=90)
     assert len(seen) == 2 and seen[0] != seen[1]
+
+
+def test_profiler_hook_writes_chrome_timelines(tmp_path):
+    """ProfilerHook(save_steps, output_dir, show_memory) (mnist_keras_distributed.py:235-237): one
+    profiled step per save_steps window, written as timeline-<step>.json Chrome traces."""
+    import json
+    x, y = _data(seed=4)
+    est = _estimator(tmp_path / "m", save_checkpoints_steps=100)
+    hook = tde.estimator.ProfilerHook(save_steps=4, output_dir=str(tmp_path / "prof"), show_memory=True)
+    est.train(_input_fn(x, y), hooks=[hook], max_steps=9)
+    names = sorted(p.split("/")[-1] for p in hook.written)
+    assert names == ["timeline-1.json", "timeline-4.json", "timeline-8.json"], names
+    for p in hook.written:
+        doc = json.loads(open(p).read())
+        assert "traceEvents" in doc
