@@ -130,7 +130,7 @@ def main():
     if world > 1:  # data-parallel invariant (outside the timed region): every replica bit-identical
         from tensorflow_distributed_example_amd.utils import debug
         fps = debug.replica_fingerprints(model)
-        same = all(f[2:] == fps[0][2:] for f in fps)
+        same = all(f[2] == fps[0][2] for f in fps)   # trainable weights (BN moving stats are per replica)
         if strategy.worker_index == 0:
             print(f"[bench] replicas_identical={same}", file=sys.stderr, flush=True)
     ms = elapsed / a.steps * 1e3
@@ -147,7 +147,7 @@ def main():
                        "per_gpu_batch": B, "parallelism": f"dp{n}", "strategy": "MultiWorkerMirroredStrategy",
                        "steps_per_execution": spe, "optimizer": f"SGD(lr={a.lr})", "plan": prog.plan_kind,
                        "allreduce": ar,
-                       "hipgraph": prog.use_graph}}), flush=True)
+                       "hipgraph": prog.use_graph, "grad_buckets": len(prog.buckets or []) or 1}}), flush=True)
 
 
 if __name__ == "__main__":

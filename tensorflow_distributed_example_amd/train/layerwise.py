@@ -68,6 +68,31 @@ class _T:
         return B * (self.numel // self.C)
 
 
+def plan_grad_buckets(stage_params, segments, total, target_elems):
+    """Bucket cuts for ``LayerwisePlan.grad_buckets``: ``stage_params[i]`` = variables written by the
+    i-th backward stage, ``segments`` = (name, flat offset) of every trainable variable, ``total`` =
+    bucket length.  Returns [(i, lo, hi)] covering [0, total) exactly, highest offsets first."""
+    last = len(stage_params) - 1
+    owner = {}
+    for i, names in enumerate(stage_params):
+        for n in names:
+            owner.setdefault(n, i)
+    segs = sorted(segments, key=lambda g: g[1], reverse=True)
+    out = []
+    hi = front = total
+    k = 0
+    for i in range(len(stage_params)):
+        while k < len(segs) and owner.get(segs[k][0], last) <= i:
+            front = segs[k][1]
+            k += 1
+        if k == len(segs):
+            front = 0
+        if front < hi and (hi - front >= target_elems or front == 0):
+            out.append((i, front, hi))
+            hi = front
+    return out
+
+
 class _Stage:
     inputs: list
     out: _T
@@ -77,6 +102,10 @@ class _Stage:
 
     def bwd(self, p, B):
         raise NotImplementedError
+
+    def param_names(self):
+        """Trainable variables whose gradients this stage's backward writes (all of them, once)."""
+        return [n for n in (getattr(self, "wname", None), getattr(self, "bname", None)) if n]
 
 
 class LayerwisePlan(PG.ReplicaPlan):
@@ -265,14 +294,29 @@ class LayerwisePlan(PG.ReplicaPlan):
     def _input(self, x, B):
         O.cast_bf16(x[:B].reshape(-1), self.x_bf[: B * self.T[0].numel])
 
-    def train_step(self, x, y, B=None):
+    def train_step(self, x, y, B=None, after_bwd=None):
+        """Forward + backward.  ``after_bwd(i)`` (optional) runs after the i-th backward stage (reverse
+        order) has been enqueued — the hook the Program uses to start gradient-bucket all-reduces
+        while the rest of the backward is still running (see ``grad_buckets``)."""
         B = self.B if B is None else B
         self._input(x, B)
         self._labels = y
         for st in self.stages:
             st.fwd(self, B, True)
-        for st in reversed(self.stages):
+        for i, st in enumerate(reversed(self.stages)):
             st.bwd(self, B)
+            if after_bwd is not None:
+                after_bwd(i)
+
+    def grad_buckets(self, target_elems):
+        """Reverse-order gradient buckets: [(i, lo, hi)] = once backward stage i (reverse order) is
+        enqueued, the flat gradient range [lo, hi) is final (every variable in it has had its only
+        writer run).  Variables sit in the flat bucket in layer order and backward visits layers in
+        reverse, so the final region grows from the end of the bucket; a bucket is cut whenever it
+        reaches ``target_elems`` (4-8 MB buckets issued as backward produces them)."""
+        st = self.store
+        segs = [(n, st.segments[n].offset) for n in st.names(trainable=True)]
+        return plan_grad_buckets([s.param_names() for s in reversed(self.stages)], segs, st.g.numel(), target_elems)
 
     def apply(self):
         self.opt.apply()
@@ -465,6 +509,13 @@ class _Elementwise(_Stage):
             self.gbeta = st.grad(f"{n}/beta") if layer.center and st.segments[f"{n}/beta"].trainable else None
             self.mmean = st.view(f"{n}/moving_mean")
             self.mvar = st.view(f"{n}/moving_variance")
+        self._pnames = []
+        if self.bn:
+            self._pnames = [f"{layer.name}/{v}" for v, g in (("gamma", self.ggamma), ("beta", self.gbeta))
+                            if g is not None]
+
+    def param_names(self):
+        return self._pnames
 
     def set_dropout(self, layer):
         g = Kb.make_generator(7919 + self.lid)

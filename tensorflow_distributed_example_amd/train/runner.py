@@ -106,6 +106,23 @@ class Program:
                               (self.comm is None or self.comm.capturable))
         self._comm_warm = False
         self._dbg = os.environ.get("TDE_DEBUG_SYNC", "0") not in ("", "0") and cuda
+        self.buckets = self._plan_buckets() if training else None
+        self._comm_stream = torch.cuda.Stream(self.devices[0]) if self.buckets else None
+
+    def _plan_buckets(self):
+        """Reverse-order gradient buckets all-reduced on a comm stream while backward still runs
+        (one local replica, a stream-ordered collective, a plan that exposes its backward order).
+        ``TDE_OVERLAP=0`` keeps the single post-backward all-reduce; ``TDE_BUCKET_MB`` sizes buckets."""
+        if self.comm is None or len(self.plans) != 1 or self.devices[0].type != "cuda":
+            return None
+        if not getattr(self.comm, "capturable", False) or os.environ.get("TDE_OVERLAP", "1") == "0":
+            return None
+        plan = self.plans[0]
+        if not hasattr(plan, "grad_buckets"):
+            return None
+        mb = float(os.environ.get("TDE_BUCKET_MB", "8"))
+        bk = plan.grad_buckets(max(1, int(mb * 2 ** 20 / 4)))
+        return bk if len(bk) > 1 else None
 
     @property
     def plan_kind(self):
@@ -122,6 +139,9 @@ class Program:
     # ------------------------------------------------------------------ training
     def _steps(self, S, B=None):
         for s in range(S):
+            if self.buckets:
+                self._overlapped_step(s, B)
+                continue
             for r, plan in enumerate(self.plans):
                 with _ctx(plan.device):
                     plan.train_step(self.x_ring[r][s], self.y_ring[r][s], B)
@@ -133,6 +153,31 @@ class Program:
                 with _ctx(plan.device):
                     plan.apply()
                 self._debug_sync("optimizer")
+
+    def _overlapped_step(self, s, B):
+        """fwd + bwd on the compute stream; each gradient bucket's all-reduce is enqueued on the comm
+        stream right after the backward stage that finalises it (event dependency), so it overlaps
+        the remaining backward; the optimizer waits for the comm stream."""
+        plan = self.plans[0]
+        main = torch.cuda.current_stream(plan.device)
+        cs = self._comm_stream
+        g = plan.store.g
+        ready = {}
+        for i, lo, hi in self.buckets:
+            ready.setdefault(i, []).append((lo, hi))
+
+        def after_bwd(i):
+            for lo, hi in ready.get(i, ()):
+                cs.wait_stream(main)
+                with torch.cuda.stream(cs):
+                    self.comm.all_reduce_([g[lo:hi]])
+
+        with _ctx(plan.device):
+            plan.train_step(self.x_ring[0][s], self.y_ring[0][s], B, after_bwd=after_bwd)
+            main.wait_stream(cs)
+            self._debug_sync("train_step + bucketed gradient all-reduce")
+            plan.apply()
+            self._debug_sync("optimizer")
 
     def _debug_sync(self, what):
         if self._dbg:
@@ -198,6 +243,17 @@ class Program:
         for p in self.plans:
             p.scale = 1.0 / float(global_actual)
         try:
+            if self.buckets:   # every rank issues the same bucket collectives, with or without data
+                n = len(per_replica[0][1])
+                if n > 0:
+                    self._overlapped_step(0, n)
+                else:
+                    plan = self.plans[0]
+                    with _ctx(plan.device):
+                        for _, lo, hi in self.buckets:
+                            self.comm.all_reduce_([plan.store.g[lo:hi]])
+                        plan.apply()
+                return
             for r, plan in enumerate(self.plans):
                 n = len(per_replica[r][1])
                 with _ctx(plan.device):

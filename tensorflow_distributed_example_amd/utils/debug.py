@@ -58,9 +58,12 @@ def replica_fingerprints(model) -> list:
 
 
 def check_replicas(model, what="weights"):
+    """Raise unless every replica holds bit-identical trainable variables.  BN moving statistics are
+    not compared: they are SyncOnRead (MEAN) variables that each replica updates from its own slice of
+    the batch (mnist_keras_distributed.py:86 under a strategy), so they legitimately differ."""
     fps = replica_fingerprints(model)
     ref = fps[0]
-    bad = [f for f in fps if f[2] != ref[2] or f[3] != ref[3]]
+    bad = [f for f in fps if f[2] != ref[2]]
     if bad:
         raise ReplicaDivergence(
             f"replicas diverged ({what}): reference worker {ref[0]}/replica {ref[1]} "

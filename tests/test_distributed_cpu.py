@@ -132,3 +132,34 @@ def test_replica_consistency_checker_detects_divergence():
     stores[1].w.view(-1)[123] += 1e-6          # one flipped low bit is enough
     with pytest.raises(debug.ReplicaDivergence, match="replica 1"):
         debug.check_replicas(m)
+
+
+def test_reverse_order_gradient_buckets_cover_bucket_exactly():
+    """plan_grad_buckets: buckets tile [0, total) from the end, each is emitted only after every
+    variable inside it has had its backward stage, and they respect the size target."""
+    from tensorflow_distributed_example_amd.train.layerwise import plan_grad_buckets
+    m = tde.zoo.resnet18()
+    m.build()
+    st = m._store
+    names = st.names(trainable=True)
+    segs = [(n, st.segments[n].offset) for n in names]
+    # stages in reverse layer order, one per layer (what the layer-wise plan's backward visits)
+    by_layer = {}
+    for n in names:
+        by_layer.setdefault(n.rsplit("/", 1)[0], []).append(n)
+    stage_params = list(reversed(list(by_layer.values())))
+    total = st.g.numel()
+    target = 2 * 2 ** 20
+    bk = plan_grad_buckets(stage_params, segs, total, target)
+    assert len(bk) >= 4
+    assert bk[0][2] == total and bk[-1][1] == 0
+    assert all(a[1] == b[2] for a, b in zip(bk, bk[1:]))            # contiguous, descending
+    assert [b[0] for b in bk] == sorted(b[0] for b in bk)             # in backward order
+    done_at = {n: i for i, lst in enumerate(stage_params) for n in lst}
+    for i, lo, hi in bk:
+        inside = [n for n, off in segs if lo <= off < hi]
+        assert inside and all(done_at[n] <= i for n in inside)
+        assert hi - lo >= target or lo == 0 or any(done_at[n] == i and st.segments[n].numel >= target
+                                                   for n in inside)
+    # one bucket when the target exceeds the model
+    assert plan_grad_buckets(stage_params, segs, total, total + 1) == [(len(stage_params) - 1, 0, total)]

@@ -174,3 +174,25 @@ def test_xgmi_setup_failure_on_one_rank_falls_back_everywhere():
         assert p.returncode == 0, o[-3000:]
         res = json.loads(o.split("RESULT")[1].strip())
         assert res["kind"] == "TorchDistCommunicator" and res["sum"] == 3.0, res
+
+
+def test_bucketed_overlapped_allreduce_two_ranks():
+    """Layer-wise plan under MWMS with small reverse-order buckets: each bucket's xGMI all-reduce is
+    enqueued on the comm stream behind the backward stage that finalises it (captured in the step's
+    hipGraph); replicas stay bit-identical and training matches the single post-backward all-reduce."""
+    losses = {}
+    for overlap in ("1", "0"):
+        env = dict(os.environ, TDE_RCCL="0", TDE_ALLREDUCE="xgmi", TDE_HEARTBEAT="0", OMP_NUM_THREADS="2",
+                   TDE_OVERLAP=overlap, TDE_BUCKET_MB="0.2")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+               "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
+               "--gpus", "2", "--model", "mnist_bn_cnn", "--steps", "48", "--warmup", "16"]
+        r = subprocess.run(cmd, env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stdout[-4000:]
+        res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+        assert res["config"]["allreduce"] == "xgmi" and res["config"]["hipgraph"] is True, res
+        assert (res["config"]["grad_buckets"] > 1) == (overlap == "1"), res
+        assert "replicas_identical=True" in r.stdout, r.stdout[-3000:]
+        losses[overlap] = float(r.stdout.split("loss=")[1].split()[0])
+    assert abs(losses["1"] - losses["0"]) < 0.05 * max(1.0, abs(losses["0"])), losses
