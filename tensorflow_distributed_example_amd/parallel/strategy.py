@@ -302,10 +302,25 @@ class MultiWorkerMirroredStrategy(Strategy):
             # non-gradient collectives, the xGMI kernel the gradient bucket
             base = CM.TorchDistCommunicator(n_local)
         else:
+            import sys
             import torch.distributed as dist
             obj = [CM.RcclCommunicator.unique_id() if topo.rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
-            base = CM.RcclCommunicator(devs, rank0=topo.rank * n_local, nranks=world * n_local, unique_id=obj[0])
+            base, err = None, None
+            try:
+                base = CM.RcclCommunicator(devs, rank0=topo.rank * n_local, nranks=world * n_local,
+                                           unique_id=obj[0])
+            except Exception as e:  # keep every rank on the same backend: agree before using it
+                err = f"rank {topo.rank}: {e}"
+            errs = [None] * world
+            dist.all_gather_object(errs, err)
+            errs = [e for e in errs if e]
+            if errs:
+                if base is not None:
+                    base.abort()
+                print(f"[tde] RCCL communicator init failed ({'; '.join(errs)}); collectives fall back to "
+                      "gloo", file=sys.stderr, flush=True)
+                base = CM.TorchDistCommunicator(n_local)
         if n_local == 1:
             # one GPU per process on one xGMI node: the gradient bucket takes the peer-memory kernel
             return CM.maybe_xgmi(base, devs[0], topo.rank, world)

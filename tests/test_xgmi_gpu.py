@@ -196,3 +196,20 @@ def test_bucketed_overlapped_allreduce_two_ranks():
         assert "replicas_identical=True" in r.stdout, r.stdout[-3000:]
         losses[overlap] = float(r.stdout.split("loss=")[1].split()[0])
     assert abs(losses["1"] - losses["0"]) < 0.05 * max(1.0, abs(losses["0"])), losses
+
+
+def test_rccl_init_failure_falls_back_on_every_rank():
+    """Two ranks on one GPU make ncclCommInitRank fail on both (duplicate GPU): the strategy agrees on
+    the failure, keeps gloo for the control collectives and the xGMI kernel for the gradient bucket."""
+    env = dict(os.environ, TDE_ALLREDUCE="xgmi", TDE_HEARTBEAT="0", OMP_NUM_THREADS="2")
+    env.pop("TDE_RCCL", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "32", "--warmup", "8"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout[-4000:]
+    assert "RCCL communicator init failed" in r.stdout, r.stdout[-3000:]
+    res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert res["config"]["allreduce"] == "xgmi", res
+    assert "replicas_identical=True" in r.stdout
