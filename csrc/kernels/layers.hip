@@ -68,6 +68,7 @@ struct IGemmArgs {
   // strided-conv dgrad, one stride phase (ih % sh, iw % sw) per launch: rows are that phase's
   // pixels and K runs over only the taps kh = kh0 + i*sh, kw = kw0 + j*sw that reach them
   int ph_on, ph_h, ph_w, Hp, Wp, kh0, kw0, KHp, KWp;
+  int xcd;  // 1: XCD-aware tile order (consecutive tiles share an XCD's L2)
 };
 
 constexpr int TK = 32;  // MFMA k-slice
@@ -374,8 +375,23 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;  // M-major: neighbours share the B tile in L2
-  const int kt0 = blockIdx.z * p.ktiles_per_split;
+  // Workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share an L2): remap the
+  // linear id so every XCD owns a contiguous run of tiles — M-major neighbours then share the B
+  // tile (and the A rows of the next N column) in one L2.  Bijective for any grid size.
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (p.xcd) {
+    const int gx = gridDim.x, gy = gridDim.y, nwg = gx * gy * gridDim.z;
+    if (nwg > 8) {
+      const int bid = bx + gx * (by + gy * bz);
+      const int q = nwg >> 3, r = nwg & 7, x8 = bid & 7;
+      const int L = (x8 < r ? x8 * (q + 1) : r * (q + 1) + (x8 - r) * q) + (bid >> 3);
+      bx = L % gx;
+      by = (L / gx) % gy;
+      bz = L / (gx * gy);
+    }
+  }
+  const int m0 = bx * BM, n0 = by * BN;  // M-major: neighbours share the B tile in L2
+  const int kt0 = bz * p.ktiles_per_split;
   const int kt1 = min((p.K + KB - 1) / KB, kt0 + p.ktiles_per_split);
   if (kt0 >= kt1 && p.cf_mode == 2) return;  // empty split contributes nothing (mode 3 stores its zeros)
 
@@ -750,7 +766,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
       }
       __syncthreads();
       if (p.colstats && wm == 0 && lane < 16) {
-        double* st = p.colstats + (size_t)(blockIdx.x % kStatSlots) * 2 * p.N;
+        double* st = p.colstats + (size_t)(bx % kStatSlots) * 2 * p.N;
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
           const int col = n0 + wn * WTN + j * 16 + lane;
@@ -831,14 +847,14 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
         if (AK == A_WGRAD || AK == A_COLM) {  // weight gradients: M * ldc < 2^31
           const int e = row * (int)p.ldc + col;
           if (p.cf_mode == 2) atomicAdd(&p.cf[e], v);
-          else if (p.cf_mode == 3) p.cf[(long long)blockIdx.z * p.M * p.ldc + e] = v;
+          else if (p.cf_mode == 3) p.cf[(long long)bz * p.M * p.ldc + e] = v;
           else if (p.cf_mode == 1) p.cf[e] = v;
         } else if (p.cf_mode == 1) {
           p.cf[(long long)row * p.ldc + col] = v;
         } else if (p.cf_mode == 2) {
           atomicAdd(&p.cf[(long long)row * p.ldc + col], v);
         } else if (p.cf_mode == 3) {
-          p.cf[(long long)blockIdx.z * p.M * p.ldc + (long long)row * p.ldc + col] = v;
+          p.cf[(long long)bz * p.M * p.ldc + (long long)row * p.ldc + col] = v;
         }
         if (p.cb) {
           bf16* q = &p.cb[(long long)row * p.ldcb + col];
@@ -869,7 +885,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
     }
     __syncthreads();
     if (wm == 0 && lane < 16) {
-      double* st = p.colstats + (size_t)(blockIdx.x % kStatSlots) * 2 * p.N;
+      double* st = p.colstats + (size_t)(bx % kStatSlots) * 2 * p.N;
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int col = n0 + wn * WTN + j * 16 + lane;
@@ -2139,6 +2155,10 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(float* __restrict__ 
 // g_kb_force (32/64) overrides the K step.
 // g_glds selects the global_load_lds pipeline for the K-vector kinds (fwd / dgrad / dense).
 static int g_wg_target = 512, g_wg_min_kt = 16, g_kb_force = 0, g_glds = 1, g_big = 0, g_big_min = 192;
+// XCD-aware tile order (TDE_XCD_SWIZZLE=1).  Off by default: on ResNet-18 / Model B at their batch
+// sizes the GEMMs are not HBM-bound (working sets sit in L2/MALL) and the remap measured within noise
+// (fwd 681 -> 692 us, dgrad 837 -> 847, wgrad 916 -> 911 per step; bench/resnet_layers.py).
+static int g_xcd = -1;
 // split-K weight gradients with at most this many splits store partials + reduce; more splits use atomics
 static int g_wg_scratch_max = 16;
 
@@ -2222,6 +2242,11 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     return 0;
   }
   IGemmArgs p{};
+  if (g_xcd < 0) {
+    const char* e = getenv("TDE_XCD_SWIZZLE");
+    g_xcd = e ? atoi(e) != 0 : 0;
+  }
+  p.xcd = g_xcd;
   p.a = a;
   p.lda = lda;
   p.b = b;
