@@ -1872,6 +1872,58 @@ __global__ __launch_bounds__(256) void maxpool_bwd8_kernel(PoolArgs a) {
   }
 }
 
+// MaxPool backward when every input pixel is covered by at most 2 x 2 windows (3x3/2, 2x2/2, ...):
+// one grid row per input row (b, ih) so the output-row candidates are block-uniform scalars, and a
+// thread issues all (up to 4) argmax-byte + dy loads before using any of them.
+__global__ __launch_bounds__(256) void maxpool_bwd8_w2_kernel(PoolArgs a) {
+  const Geo& g = a.g;
+  const int C8 = g.C >> 3;
+  const int row = blockIdx.y;
+  const int b = row / g.H, ih = row - b * g.H;
+  const int ty = ih + g.pt;
+  const int oh_lo = ty >= g.KH ? (ty - g.KH) / g.sh + 1 : 0, oh_hi = min(g.Ho - 1, ty / g.sh);
+  const int n = g.W * C8;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const int iw = e / C8, c8 = e - iw * C8;
+    const int tx = iw + g.pl;
+    const int ow_lo = tx >= g.KW ? (tx - g.KW) / g.sw + 1 : 0, ow_hi = min(g.Wo - 1, tx / g.sw);
+    unsigned long long id[4];
+    bf16x8 d[4];
+    unsigned wi[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int oh = oh_lo + (q >> 1), ow = ow_lo + (q & 1);
+      id[q] = ~0ull;  // byte 0xFF never equals a window index (host: KH*KW < 255)
+      wi[q] = 0;
+      if (oh <= oh_hi && ow <= ow_hi) {
+        const long long o = (((long long)b * g.Ho + oh) * g.Wo + ow) * g.C + c8 * 8;
+        id[q] = *reinterpret_cast<const unsigned long long*>(a.idx + o);
+        d[q] = *reinterpret_cast<const bf16x8*>(a.dy + o);
+        wi[q] = (unsigned)((ty - oh * g.sh) * g.KW + (tx - ow * g.sw));
+      }
+    }
+    float s[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (((id[q] >> (8 * j)) & 0xFF) == wi[q]) s[j] += bf2f(d[q][j]);
+    bf16x8* out = reinterpret_cast<bf16x8*>(a.dx + (((long long)row * g.W + iw) * g.C + c8 * 8));
+    bf16x8 o;
+    if (a.dx_accum) {
+      const bf16x8 prev = *out;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(s[j] + bf2f(prev[j]));
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(s[j]);
+    }
+    *out = o;
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Global average pooling [B,HW,C] -> [B,C] and its backward; zero padding / its crop.
 __global__ __launch_bounds__(256) void gap_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int B, int HW,
@@ -2092,6 +2144,84 @@ __global__ __launch_bounds__(256) void im2col_kernel(const bf16* __restrict__ x,
       }
     }
     *reinterpret_cast<bf16x8*>(out + (long long)m * Kp + k) = v;
+  }
+}
+
+// Row-staged im2col (the stem: C = 3, 7x7/2): one block per output row (b, oh).  The KH input
+// rows that row reads are staged once into LDS with coalesced loads (zero rows / columns for the
+// padding), then every output 16-byte chunk is assembled from LDS: element k = (kh, kw, ci) of
+// pixel ow sits at LDS offset k + kh*(LROW - KW*C) + PAD + ow*sw*C, so a thread keeps its chunk's 8
+// offsets in registers and walks ow with one add: no global gathers, no per-element bounds tests.
+// (The gather kernel above issues 8 bounds-checked 2-byte global loads per chunk: issue-bound.)
+constexpr int kI2cLds = 16384;  // bf16 elements (32 KB)
+// LDS row kh starts at kh*LROW (LROW % 8 == 0); input column iw of it at PAD + (iw + pl)*C, with PAD
+// chosen so that column 0 is 16-byte aligned: whole input rows are then staged with 16-byte copies
+// (VROW) into a zeroed image.
+__global__ __launch_bounds__(256) void im2col_rows_kernel(const bf16* __restrict__ x, Geo g, int Kp, int LROW, int PAD,
+                                                          int VROW, bf16* __restrict__ out,
+                                                          const bf16* __restrict__ w_in, bf16* __restrict__ w_out,
+                                                          int pix_blocks) {
+  const int K = g.KH * g.KW * g.C;
+  if ((int)blockIdx.x >= pix_blocks) {  // weight padding blocks
+    const int n = g.Co * Kp;
+    for (int e = (blockIdx.x - pix_blocks) * blockDim.x + threadIdx.x; e < n;
+         e += (gridDim.x - pix_blocks) * blockDim.x) {
+      const int co = e / Kp, k = e - co * Kp;
+      w_out[e] = k < K ? w_in[co * K + k] : (bf16)0.0f;
+    }
+    return;
+  }
+  __shared__ __attribute__((aligned(16))) bf16 rows[kI2cLds];
+  const int b = blockIdx.x / g.Ho, oh = blockIdx.x - b * g.Ho;
+  const int y0 = oh * g.sh - g.pt;
+  const bf16* xb = x + (long long)b * g.H * g.W * g.C;
+  const int WC = g.W * g.C, span = LROW - PAD;  // span: elements of columns -pl .. (LROW-PAD)/C - pl - 1
+  if (VROW) {
+    for (int e = threadIdx.x; e < g.KH * LROW / 8; e += blockDim.x)
+      *reinterpret_cast<bf16x8*>(rows + e * 8) = zero8();
+    __syncthreads();
+    const int c8 = WC / 8, col0 = PAD + g.pl * g.C;
+    for (int e = threadIdx.x; e < g.KH * c8; e += blockDim.x) {
+      const int kh = e / c8, j = e - kh * c8;
+      const int ih = y0 + kh;
+      if ((unsigned)ih < (unsigned)g.H)
+        *reinterpret_cast<bf16x8*>(rows + kh * LROW + col0 + j * 8) =
+            *reinterpret_cast<const bf16x8*>(xb + ih * WC + j * 8);
+    }
+  } else {
+    for (int e = threadIdx.x; e < g.KH * span; e += blockDim.x) {
+      const int kh = e / span, j = e - kh * span;
+      const int ih = y0 + kh;
+      const int col = j / g.C, ci = j - col * g.C;
+      const int iw = col - g.pl;
+      bf16 v = (bf16)0.0f;
+      if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W) v = xb[(ih * g.W + iw) * g.C + ci];
+      rows[kh * LROW + PAD + j] = v;
+    }
+  }
+  __syncthreads();
+  const int K8 = Kp >> 3, P = blockDim.x / K8;
+  const int t = threadIdx.x;
+  if (t >= P * K8) return;
+  const int k8 = t % K8;
+  int off[8];
+  bool ok[8];
+  const int KWC = g.KW * g.C;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = k8 * 8 + j;
+    ok[j] = k < K;
+    const int kh = k / KWC;
+    off[j] = ok[j] ? k + kh * (LROW - KWC) + PAD : 0;
+  }
+  const int dstep = g.sw * g.C;
+  bf16* orow = out + (long long)blockIdx.x * g.Wo * Kp + k8 * 8;
+  for (int ow = t / K8; ow < g.Wo; ow += P) {
+    const int base = ow * dstep;
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = ok[j] ? rows[off[j] + base] : (bf16)0.0f;
+    *reinterpret_cast<bf16x8*>(orow + (long long)ow * Kp) = v;
   }
 }
 
@@ -2515,7 +2645,11 @@ TDE_API int tde_maxpool(const bf16* x, bf16* y, unsigned char* idx, const bf16* 
   const bool vec = g.C % 8 == 0 && ((uintptr_t)(backward ? (const void*)dy : (const void*)x) & 15) == 0;
   if (vec) {
     if (!backward) maxpool_fwd8_kernel<<<grid_for((long long)g.B * g.Ho * g.Wo * g.C, 8), 256, 0, stream>>>(a);
-    else maxpool_bwd8_kernel<<<grid_for((long long)g.B * g.H * g.W * g.C, 8), 256, 0, stream>>>(a);
+    else if ((g.KH + g.sh - 1) / g.sh <= 2 && (g.KW + g.sw - 1) / g.sw <= 2 && g.KH * g.KW < 255 &&
+             (long long)g.B * g.H <= 65535) {
+      const int per_row = g.W * (g.C / 8);
+      maxpool_bwd8_w2_kernel<<<dim3((per_row + 255) / 256, g.B * g.H), 256, 0, stream>>>(a);
+    } else maxpool_bwd8_kernel<<<grid_for((long long)g.B * g.H * g.W * g.C, 8), 256, 0, stream>>>(a);
     TDE_LAUNCH_CHECK();
     return 0;
   }
@@ -2573,8 +2707,21 @@ TDE_API int tde_im2col(const bf16* x, const int* geo, int Kp, bf16* out, const b
   if (Kp / 8 > 256 || g.C >= 1024 || g.KW >= 1024) return -2;  // per-block tap table / packing
   if ((long long)g.B * g.Ho * g.Wo * (Kp / 8) >= (1LL << 31) || (long long)g.B * g.H * g.W * g.C >= (1LL << 31))
     return -4;
-  const int pix = grid_for((long long)g.B * g.Ho * g.Wo * (Kp / 8));
   const int wb = w_in ? 8 : 0;
+  // row-staged path: the KH input rows of one output row fit the LDS buffer
+  const int SPAN = ((g.Wo - 1) * g.sw + g.KW) * g.C;  // elements of one staged row
+  const int PAD = (8 - (g.pl * g.C) % 8) % 8;
+  const int LROW = (PAD + SPAN + 7) / 8 * 8;
+  const int VROW = (g.W * g.C) % 8 == 0 && ((uintptr_t)x & 15) == 0 && g.pl * g.C + g.W * g.C <= SPAN;
+  static const bool rows_off = getenv("TDE_IM2COL_GATHER") != nullptr;
+  if (!rows_off && g.KH * LROW <= kI2cLds && Kp / 8 <= 256 && (long long)g.B * g.Ho < (1LL << 30) &&
+      (long long)g.B * g.Ho * g.Wo * Kp < (1LL << 40)) {
+    const int pix = g.B * g.Ho;
+    im2col_rows_kernel<<<pix + wb, 256, 0, stream>>>(x, g, Kp, LROW, PAD, VROW, out, w_in, w_out, pix);
+    TDE_LAUNCH_CHECK();
+    return 0;
+  }
+  const int pix = grid_for((long long)g.B * g.Ho * g.Wo * (Kp / 8));
   im2col_kernel<<<pix + wb, 256, 0, stream>>>(x, g, Kp, out, w_in, w_out, pix);
   TDE_LAUNCH_CHECK();
   return 0;

@@ -247,7 +247,8 @@ def test_bn_bwd_accumulates(C):
         assert _rel(a.float(), f.float() + b.float()) < 1e-2
 
 
-@pytest.mark.parametrize("H,W,k,s,pad,C", [(112, 112, 3, 2, "same", 16), (26, 26, 2, 2, "valid", 32),
+@pytest.mark.parametrize("H,W,k,s,pad,C", [(112, 112, 3, 2, "same", 16), (112, 112, 3, 2, "same", 64),
+                                           (26, 26, 2, 2, "valid", 32), (11, 11, 3, 1, "same", 8),
                                            (9, 7, 3, 2, "same", 16), (9, 7, 3, 2, "same", 6)])
 def test_maxpool(H, W, k, s, pad, C):
     from tensorflow_distributed_example_amd.ops import layer_ops as O
@@ -516,6 +517,31 @@ def test_smallconv_direct_kernels(B, H, W, C, Co, k, s, pad):
     assert (st[:Co] - rs.sum((0, 1, 2))).abs().max().item() <= 1e-4 * rs.abs().sum((0, 1, 2)).max().item() + 1e-3
     assert _rel(st[Co:], (rs ** 2).sum((0, 1, 2))) < 1e-3
     assert _rel(dx.float(), xgrad.permute(0, 2, 3, 1)) < 1e-2
+
+
+@pytest.mark.parametrize("B,H,W,C,Co,k,s", [(3, 224, 224, 3, 64, 7, 2), (2, 15, 17, 3, 8, 7, 2), (2, 28, 28, 6, 12, 6, 2),
+                                            (1, 9, 9, 5, 4, 3, 1)])
+def test_im2col_exact(B, H, W, C, Co, k, s):
+    """im2col is a pure copy: bitwise equal to a torch-built patch matrix (row-staged LDS kernel for
+    the ResNet stem, zero columns up to Kp) and the zero-padded weight copy."""
+    from tensorflow_distributed_example_amd.ops import layer_ops as O
+    (pt, pb), (pl, pr) = _tf_same(H, k, s), _tf_same(W, k, s)
+    Ho, Wo = -(-H // s), -(-W // s)
+    g = O.ConvGeom(B, H, W, C, Ho, Wo, Co, k, k, s, s, pt, pl)
+    x = _r(B, H, W, C, seed=44)
+    w = _r(k, k, C, Co, seed=45)
+    Kp = -(-g.K // 8) * 8
+    xcol = torch.full((B * Ho * Wo * Kp,), 7.0, dtype=bf, device=DEV)
+    Wt_pad = torch.full((Co * Kp,), 7.0, dtype=bf, device=DEV)
+    wt = w.reshape(-1, Co).t().contiguous()
+    O.im2col(x, g, xcol, wt, Wt_pad)
+    xp = F.pad(x, (0, 0, pl, pr + s, pt, pb + s))
+    taps = [xp[:, i:i + s * (Ho - 1) + 1:s, j:j + s * (Wo - 1) + 1:s, :] for i in range(k) for j in range(k)]
+    ref = torch.stack(taps, 3).reshape(B * Ho * Wo, g.K)
+    ref = F.pad(ref, (0, Kp - g.K)).reshape(-1)
+    torch.cuda.synchronize()
+    assert torch.equal(xcol, ref)
+    assert torch.equal(Wt_pad, F.pad(wt, (0, Kp - g.K)).reshape(-1))
 
 
 @pytest.mark.parametrize("B,H,W,C,Co,k,s,pad", [(2, 15, 15, 3, 64, 7, 2, "same"), (4, 28, 28, 6, 12, 6, 2, "same"),
