@@ -7,7 +7,7 @@
 // The same pass (a) zeroes the gradient buffer for the next step's atomic /
 // split-K accumulation and (b) refreshes the bf16 compute copies ("shadows") of
 // the weights in the layouts the MFMA kernels read — row-major and, through an
-// LDS 64x64 transpose, column-major.  The step counter (`iterations`, Keras
+// LDS 16x64 transpose, column-major.  The step counter (`iterations`, Keras
 // optimizer.iterations / Estimator global_step) lives on the device and is
 // advanced by the step's loss kernel before this launch, so Adam's bias
 // correction reads t = iterations with no host round trip and no in-kernel
@@ -38,6 +38,7 @@ struct OptArgs {
 };
 
 constexpr int kChunk = 2048;
+constexpr int kTileR = 16;  // rows per transposed-shadow tile (tile = kTileR x 64)
 
 struct Hyper {
   float lr, lr_t;
@@ -85,7 +86,7 @@ __device__ __forceinline__ float upds(const OptArgs& a, size_t i, const Hyper& h
 }
 
 __global__ __launch_bounds__(256) void optim_apply_kernel(OptArgs a) {
-  __shared__ bf16 tile[64][72];
+  __shared__ bf16 tile[kTileR][72];
   const int4 ent = a.table[blockIdx.x];
   const OptSeg s = a.segs[ent.x];
   Hyper h;
@@ -118,11 +119,12 @@ __global__ __launch_bounds__(256) void optim_apply_kernel(OptArgs a) {
       }
     }
   } else {
-    const int r0 = ent.z * 64, c0 = ent.w * 64;
+    // 16x64 tiles (one float4 per thread): ~4x more workgroups than 64x64 tiles, so
+    // a 5408x64 Dense kernel spreads over 338 workgroups instead of 85 CUs.
+    const int r0 = ent.z * kTileR, c0 = ent.w * 64;
     const bool vec = (s.cols % 4) == 0;
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int r = it * 16 + (tid >> 4), c = (tid & 15) * 4;
+    {
+      const int r = tid >> 4, c = (tid & 15) * 4;
       const int gr = r0 + r, gc = c0 + c;
       if (gr < s.rows) {
         const long long e = (long long)gr * s.cols + gc;
@@ -143,9 +145,9 @@ __global__ __launch_bounds__(256) void optim_apply_kernel(OptArgs a) {
     }
     lds_barrier();
 #pragma unroll
-    for (int it = 0; it < 16; ++it) {
+    for (int it = 0; it < kTileR * 64 / 256; ++it) {
       const int i = it * 256 + tid;
-      const int c = i >> 6, r = i & 63, gr = r0 + r, gc = c0 + c;
+      const int c = i / kTileR, r = i % kTileR, gr = r0 + r, gc = c0 + c;
       if (gr < s.rows && gc < s.cols) a.shadow[s.sht_off + (long long)gc * s.rows + gr] = tile[r][c];
     }
   }
@@ -155,7 +157,7 @@ __global__ __launch_bounds__(256) void optim_apply_kernel(OptArgs a) {
 __global__ __launch_bounds__(256) void shadow_refresh_kernel(const float* w, bf16* shadow,
                                                              const OptSeg* segs,
                                                              const int4* table) {
-  __shared__ bf16 tile[64][66];
+  __shared__ bf16 tile[kTileR][66];
   const int4 ent = table[blockIdx.x];
   const OptSeg s = segs[ent.x];
   const int tid = threadIdx.x;
@@ -166,8 +168,8 @@ __global__ __launch_bounds__(256) void shadow_refresh_kernel(const float* w, bf1
     if (s.sh_off >= 0)
       for (long long e = beg + tid; e < end; e += 256) shadow[s.sh_off + e] = f2bf(w[s.off + e]);
   } else {
-    const int r0 = ent.z * 64, c0 = ent.w * 64;
-    for (int i = tid; i < 64 * 64; i += 256) {
+    const int r0 = ent.z * kTileR, c0 = ent.w * 64;
+    for (int i = tid; i < kTileR * 64; i += 256) {
       const int r = i >> 6, c = i & 63, gr = r0 + r, gc = c0 + c;
       if (gr < s.rows && gc < s.cols) {
         const long long e = (long long)gr * s.cols + gc;
@@ -177,8 +179,8 @@ __global__ __launch_bounds__(256) void shadow_refresh_kernel(const float* w, bf1
       }
     }
     __syncthreads();
-    for (int i = tid; i < 64 * 64; i += 256) {
-      const int c = i >> 6, r = i & 63, gr = r0 + r, gc = c0 + c;
+    for (int i = tid; i < kTileR * 64; i += 256) {
+      const int c = i / kTileR, r = i % kTileR, gr = r0 + r, gc = c0 + c;
       if (gr < s.rows && gc < s.cols) shadow[s.sht_off + (long long)gc * s.rows + gr] = tile[r][c];
     }
   }
@@ -194,7 +196,7 @@ TDE_API int tde_optim_table_size(const void* segs_host, int nseg) {
   int n = 0;
   for (int i = 0; i < nseg; ++i) {
     if (s[i].sht_off >= 0)
-      n += ((s[i].rows + 63) / 64) * ((s[i].cols + 63) / 64);
+      n += ((s[i].rows + kTileR - 1) / kTileR) * ((s[i].cols + 63) / 64);
     else
       n += (int)(((long long)s[i].rows * s[i].cols + kChunk - 1) / kChunk);
   }
@@ -208,7 +210,7 @@ TDE_API int tde_optim_build_table(const void* segs_host, int nseg, void* table_h
   int n = 0;
   for (int i = 0; i < nseg; ++i) {
     if (s[i].sht_off >= 0) {
-      for (int r = 0; r < (s[i].rows + 63) / 64; ++r)
+      for (int r = 0; r < (s[i].rows + kTileR - 1) / kTileR; ++r)
         for (int c = 0; c < (s[i].cols + 63) / 64; ++c) t[n++] = int4{i, 1, r, c};
     } else {
       int nb = (int)(((long long)s[i].rows * s[i].cols + kChunk - 1) / kChunk);
