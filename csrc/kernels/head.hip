@@ -14,7 +14,7 @@
 //
 // One workgroup = 16 rows, 4 waves.  All three products run on the exact-f32
 // MFMA (v_mfma_f32_16x16x4_f32; no bf16 rounding in the loss path):
-//   logits[16 x 16]  = h[16 x H] . W2[H x C]          (wave 0, H/4 k-steps)
+//   logits[16 x 16]  = h[16 x H] . W2[H x C]          (4 waves x H/16 k-steps, LDS sum)
 //   softmax / CE / accuracy in registers on the MFMA C layout (16-lane groups)
 //   dW2[H x C]       = h^T . dl                       (wave w: 16-row tiles of H)
 //   dH[16 x H]       = dl . W2^T, ReLU mask           (wave w: 16-column tiles of H)
@@ -74,6 +74,7 @@ __global__ __launch_bounds__(256) void head_xent_kernel(HeadArgs a) {
   __shared__ float dls[HR * 16];                                // dlogits
   __shared__ float b2s[16];
   __shared__ int labs[HR];
+  __shared__ __attribute__((aligned(16))) float lgp[3 * 64 * 4];  // logits partials of waves 1..3
   stamp(a.stamps, 0);
   const int H = a.H, C = a.C;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -114,10 +115,22 @@ __global__ __launch_bounds__(256) void head_xent_kernel(HeadArgs a) {
     }
   }
 
-  // ---- logits + softmax-CE (wave 0): lane holds logits[4*fq + i][fr]
+  // ---- logits: the Hp/4 k-steps split over the 4 waves (Hp is a multiple of 16), the
+  // partial 16x16 tiles summed through LDS -- a 4x shorter dependent MFMA/LDS chain.
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  {
+    const int kq = Hp / 4, kb = wave * kq;
+    for (int k = kb; k < kb + kq; k += 4) acc = mfma_f32(hs[fr * HST + k + fq], w2s[(k + fq) * 16 + fr], acc);
+    if (wave > 0) *reinterpret_cast<f32x4*>(lgp + ((wave - 1) * 64 + lane) * 4) = acc;
+  }
+  lds_barrier();
+  // ---- softmax-CE (wave 0): lane holds logits[4*fq + i][fr]
   if (wave == 0) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < Hp; k += 4) acc = mfma_f32(hs[fr * HST + k + fq], w2s[(k + fq) * 16 + fr], acc);
+#pragma unroll
+    for (int w = 0; w < 3; ++w) {
+      const f32x4 p = *reinterpret_cast<const f32x4*>(lgp + (w * 64 + lane) * 4);
+      acc[0] += p[0]; acc[1] += p[1]; acc[2] += p[2]; acc[3] += p[3];
+    }
     float loss_acc = 0.f, corr_acc = 0.f, cnt_acc = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
