@@ -49,18 +49,24 @@ struct ConvNetFwdArgs {
 // image) are staged into LDS with coalesced float4 loads: gathering 4x4 patches
 // straight from HBM puts 64 distinct cache lines behind every load instruction.
 constexpr int XR = 6, XW = 32;
-constexpr int kFwdLds = PPW * 64 * PSTR * 2 + 64 * XR * XW * 4;
+constexpr int fwd_lds(int fpw) { return fpw * 64 * PSTR * 2 + 64 * XR * XW * 4; }
 
-__global__ __launch_bounds__(1024) void convnet_fwd_kernel(ConvNetFwdArgs a) {
+// FPW pooled positions x 64 images per workgroup, 4*FPW waves (wave = position x 8-channel
+// group).  Phase 1 is VALU-bound: fewer positions per workgroup spread the conv over more CUs
+// (FPW=4: 43 workgroups x 16 waves for MNIST; FPW=2: 85 x 8) at the price of more split-K
+// atomics in phase 2.
+template <int FPW>
+__global__ __launch_bounds__(FPW * 256) void convnet_fwd_kernel(ConvNetFwdArgs a) {
+  constexpr int NT = FPW * 256;
   extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
   bf16* Ps = reinterpret_cast<bf16*>(fsm);
-  float* xr = reinterpret_cast<float*>(fsm + PPW * 64 * PSTR * 2);  // [64][XR][W]
+  float* xr = reinterpret_cast<float*>(fsm + FPW * 64 * PSTR * 2);  // [64][XR][W]
   stamp(a.stamps, 0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fk = (lane >> 4) * 8;
   const int W = a.W, H = a.H;
   const int Wp = (W - 2) / 2, Hp = (H - 2) / 2, P = Hp * Wp;
-  const int p0 = blockIdx.x * PPW;
+  const int p0 = blockIdx.x * FPW;
   const int b0 = blockIdx.y * 64;
   const int b = b0 + lane;
   const bool bok = b < a.B;
@@ -76,7 +82,7 @@ __global__ __launch_bounds__(1024) void convnet_fwd_kernel(ConvNetFwdArgs a) {
   // ---- prologue: all global loads, independent, issued back to back
   {
     const int n4 = nrows * W / 4;  // float4 per image
-    for (int i = threadIdx.x; i < 64 * n4; i += 1024) {
+    for (int i = threadIdx.x; i < 64 * n4; i += NT) {
       const int bl = i / n4, q = i - bl * n4;
       float4 v = {0.f, 0.f, 0.f, 0.f};
       if (b0 + bl < a.B)
@@ -92,11 +98,12 @@ __global__ __launch_bounds__(1024) void convnet_fwd_kernel(ConvNetFwdArgs a) {
   }
   const float4 blo = *reinterpret_cast<const float4*>(a.bc + c0);
   const float4 bhi = *reinterpret_cast<const float4*>(a.bc + c0 + 4);
-  // W1^T fragments of this wave's output tile: mt = wave>>2 (image rows), nt = wave&3 (units)
-  const int mt = wave >> 2, nt = wave & 3;
-  bf16x8 wfr[PPW];
+  // W1^T fragments of this wave's output tiles: tile t = wave + 4*FPW*j (j < 4/FPW),
+  // mt = t>>2 (image rows), nt = t&3 = wave&3 (units) for every j
+  const int nt = wave & 3;
+  bf16x8 wfr[FPW];
 #pragma unroll
-  for (int ks = 0; ks < PPW; ++ks) {
+  for (int ks = 0; ks < FPW; ++ks) {
     const int kp = p0 + ks;
     wfr[ks] = kp < P ? *reinterpret_cast<const bf16x8*>(a.W1c + (size_t)(nt * 16 + fr) * a.ldw1c + (size_t)kp * CC + fk)
                      : bf16x8{};
@@ -164,19 +171,23 @@ __global__ __launch_bounds__(1024) void convnet_fwd_kernel(ConvNetFwdArgs a) {
   lds_barrier();
   stamp(a.stamps, 3);
 
-  // ---- phase 2: hpre[64 x 64] += Ps(64 x 4*32) . W1^T(4*32 x 64); one 16x16 tile per wave
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  // ---- phase 2: hpre[64 x 64] += Ps(64 x FPW*32) . W1^T(FPW*32 x 64); 16x16 tiles over the waves
 #pragma unroll
-  for (int ks = 0; ks < PPW; ++ks) {
-    if (p0 + ks < P) {
-      const bf16x8 av = *reinterpret_cast<const bf16x8*>(Ps + ((size_t)ks * 64 + mt * 16 + fr) * PSTR + fk);
-      acc = mfma16(av, wfr[ks], acc);
+  for (int j = 0; j < 4 / FPW; ++j) {
+    const int mt = (wave >> 2) + FPW * j;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < FPW; ++ks) {
+      if (p0 + ks < P) {
+        const bf16x8 av = *reinterpret_cast<const bf16x8*>(Ps + ((size_t)ks * 64 + mt * 16 + fr) * PSTR + fk);
+        acc = mfma16(av, wfr[ks], acc);
+      }
     }
-  }
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = b0 + mt * 16 + (lane >> 4) * 4 + r;
-    if (row < a.B) atomicAdd(a.hpre + (size_t)row * HD + nt * 16 + fr, acc[r]);
+    for (int r = 0; r < 4; ++r) {
+      const int row = b0 + mt * 16 + (lane >> 4) * 4 + r;
+      if (row < a.B) atomicAdd(a.hpre + (size_t)row * HD + nt * 16 + fr, acc[r]);
+    }
   }
   stamp(a.stamps, 4);
 }
@@ -387,7 +398,7 @@ using namespace tde;
 TDE_API int tde_convnet_fwd(const float* x, const float* wc, const float* bc, const void* W1c, int ldw1c,
                             float* hpre, void* Pt, int ldPt, void* amax, int lda, int B, int H, int W,
                             long long* stamps, hipStream_t stream) {
-  if ((W & 3) || W > XW || ((W - 2) / 2) < PPW || (ldw1c & 7) || (Pt && (ldPt & 7)) || (amax && lda < B)) return -1;
+  if ((W & 3) || W > XW || ((W - 2) / 2) < 4 || (ldw1c & 7) || (Pt && (ldPt & 7)) || (amax && lda < B)) return -1;
   if (((uintptr_t)wc | (uintptr_t)bc) & 15) return -2;
   const int P = ((H - 2) / 2) * ((W - 2) / 2);
   int by = (B + 63) / 64;
@@ -396,13 +407,23 @@ TDE_API int tde_convnet_fwd(const float* x, const float* wc, const float* bc, co
     if (byp > by) by = byp;
   }
   ConvNetFwdArgs a{x, wc, bc, (const bf16*)W1c, ldw1c, hpre, (bf16*)Pt, ldPt, (uint64_t*)amax, lda, B, H, W, stamps};
-  dim3 grid((P + PPW - 1) / PPW, by);
+  // positions per workgroup (TDE_CONVNET_FPW = 1|2|4, default 2)
+  static const int fpw = [] {
+    const char* e = getenv("TDE_CONVNET_FPW");
+    const int v = e ? atoi(e) : 2;
+    return (v == 1 || v == 4) ? v : 2;
+  }();
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)convnet_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kFwdLds);
+    hipFuncSetAttribute((const void*)convnet_fwd_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, fwd_lds(1));
+    hipFuncSetAttribute((const void*)convnet_fwd_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, fwd_lds(2));
+    hipFuncSetAttribute((const void*)convnet_fwd_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, fwd_lds(4));
     attr_set = true;
   }
-  convnet_fwd_kernel<<<grid, 1024, kFwdLds, stream>>>(a);
+  const dim3 grid((P + fpw - 1) / fpw, by);
+  if (fpw == 1) convnet_fwd_kernel<1><<<grid, 256, fwd_lds(1), stream>>>(a);
+  else if (fpw == 2) convnet_fwd_kernel<2><<<grid, 512, fwd_lds(2), stream>>>(a);
+  else convnet_fwd_kernel<4><<<grid, 1024, fwd_lds(4), stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;
 }
