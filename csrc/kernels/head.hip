@@ -82,30 +82,50 @@ __global__ __launch_bounds__(256) void head_xent_kernel(HeadArgs a) {
   const int r0 = blockIdx.x * HR;
   if (a.iterations && blockIdx.x == 0 && tid == 0) atomicAdd((unsigned long long*)a.iterations, 1ull);
 
-  // ---- prologue: every global load issued up front (H padded to Hp = 16k with zeros)
+  // ---- prologue: every global load issued up front into registers (one memory latency,
+  // not one per loop trip), then the LDS images (H padded to Hp = 16k with zeros)
   const int Hp = (H + 15) & ~15;
   const int H4 = H / 4, Hp4 = Hp / 4;
-  for (int i = tid; i < HR * Hp4; i += 256) {
-    const int r = i / Hp4, j4 = (i - r * Hp4) * 4, row = r0 + r;
-    float4 v = {0.f, 0.f, 0.f, 0.f};
-    if (row < a.B && j4 < H) {
-      v = *reinterpret_cast<const float4*>(a.hin + (size_t)row * a.ldh + j4);
-      if (a.pre_bias) {
-        const float4 bb = *reinterpret_cast<const float4*>(a.pre_bias + j4);
-        v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
-      }
+  constexpr int NH4 = HR * (HMAX / 4) / 256;  // float4 of h per thread (max)
+  constexpr int NW2 = HMAX * 16 / 256;        // W2 elements per thread (max)
+  float4 hv[NH4], pb[NH4];
+  float wv[NW2];
+#pragma unroll
+  for (int u = 0; u < NH4; ++u) {
+    const int i = tid + u * 256, r = i / Hp4, j4 = (i - r * Hp4) * 4, row = r0 + r;
+    hv[u] = float4{0.f, 0.f, 0.f, 0.f};
+    pb[u] = float4{0.f, 0.f, 0.f, 0.f};
+    if (i < HR * Hp4 && row < a.B && j4 < H) {
+      hv[u] = *reinterpret_cast<const float4*>(a.hin + (size_t)row * a.ldh + j4);
+      if (a.pre_bias) pb[u] = *reinterpret_cast<const float4*>(a.pre_bias + j4);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NW2; ++u) {
+    const int i = tid + u * 256, j = i >> 4, c = i & 15;
+    wv[u] = (i < Hp * 16 && c < C && j < H) ? a.W2[j * C + c] : 0.f;
+  }
+  const float bv = (tid < 16 && a.b2 && tid < C) ? a.b2[tid] : 0.f;
+  const int lv = (tid < HR && r0 + tid < a.B) ? a.labels[r0 + tid] : 0;
+#pragma unroll
+  for (int u = 0; u < NH4; ++u) {
+    const int i = tid + u * 256, r = i / Hp4, j4 = (i - r * Hp4) * 4;
+    if (i < HR * Hp4) {
+      float4 v = hv[u];
+      v.x += pb[u].x; v.y += pb[u].y; v.z += pb[u].z; v.w += pb[u].w;
       if (a.pre_relu) {
         v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
       }
+      *reinterpret_cast<float4*>(hs + r * HST + j4) = v;
     }
-    *reinterpret_cast<float4*>(hs + r * HST + j4) = v;
   }
-  for (int i = tid; i < Hp * 16; i += 256) {
-    const int j = i >> 4, c = i & 15;
-    w2s[i] = (c < C && j < H) ? a.W2[j * C + c] : 0.f;
+#pragma unroll
+  for (int u = 0; u < NW2; ++u) {
+    const int i = tid + u * 256;
+    if (i < Hp * 16) w2s[i] = wv[u];
   }
-  if (tid < 16) b2s[tid] = (a.b2 && tid < C) ? a.b2[tid] : 0.f;
-  if (tid < HR) labs[tid] = (r0 + tid < a.B) ? a.labels[r0 + tid] : 0;
+  if (tid < 16) b2s[tid] = bv;
+  if (tid < HR) labs[tid] = lv;
   lds_barrier();
   stamp(a.stamps, 1);
   if (a.zero_hin) {
