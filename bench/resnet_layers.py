@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--sweep", action="store_true")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--sweep-tile", action="store_true", help="sweep the fwd/dgrad tile-size threshold only")
     a = ap.parse_args()
     import tensorflow_distributed_example_amd as tde
     from tensorflow_distributed_example_amd import _native as N
@@ -66,6 +67,16 @@ def main():
               f"{r['dgrad_us']:7.1f} us {tf(r['dgrad_us']):5.0f} TF | wgrad {r['wgrad_us']:7.1f} us "
               f"{tf(r['wgrad_us']):5.0f} TF", flush=True)
     print("TOTAL", json.dumps(tot), flush=True)
+    if a.sweep_tile:
+        lib = N.hip()
+        for tmin in (512, 1024, 1536, 2048, 3072, 4096, 100000):
+            lib.tde_igemm_tile_min(tmin)
+            tf_ = sum(graph_time(lambda: st.fwd(plan, B, True), a.reps) for st in _convs(plan, LW))
+            td_ = sum(graph_time(lambda: O.conv_dgrad(st.out.root().grad, st.Wrow, st.inp.root().grad,
+                                                      st.geo.with_batch(B), scratch=plan.scratch), a.reps)
+                      for st in _convs(plan, LW) if st.need_dgrad)
+            print(f"SWEEP tile_min={tmin}: fwd {tf_:.1f} us dgrad {td_:.1f} us", flush=True)
+        lib.tde_igemm_tile_min(512)
     if a.sweep:
         lib = N.hip()
         for target, mkt, kb in [(1024, 8, 0), (512, 8, 0), (256, 8, 0), (512, 16, 0), (256, 16, 0), (2048, 4, 0),

@@ -2291,6 +2291,17 @@ static int g_wg_target = 512, g_wg_min_kt = 16, g_kb_force = 0, g_glds = 1, g_bi
 static int g_xcd = -1;
 // split-K weight gradients with at most this many splits store partials + reduce; more splits use atomics
 static int g_wg_scratch_max = 16;
+// fwd / dgrad / dense tile choice: the largest of 128x128, 128x64, 64x64 with >= g_tile_min workgroups.
+// 2048 (~8 per CU) measured best on ResNet-18 at batch 64 (bench/resnet_layers.py --sweep-tile: fwd
+// 671 -> 637 us, dgrad 832 -> 825 us per step vs 512); TDE_IGEMM_TILE_MIN overrides.
+static int g_tile_min = [] {
+  const char* e = getenv("TDE_IGEMM_TILE_MIN");
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? v : 2048;
+}();
+TDE_API void tde_igemm_tile_min(int v) {
+  if (v > 0) g_tile_min = v;
+}
 
 TDE_API void tde_igemm_tune(int wg_target, int wg_min_kt, int kb_force, int glds, int big, int big_min) {
   if (wg_target > 0) g_wg_target = wg_target;
@@ -2445,9 +2456,9 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     if (auto_splits) {
       splits = wgrad_splits(M, N, K, KB, &p.ktiles_per_split);
     }
-  } else if (N > 64 && tiles(128, 128) >= 512) {
+  } else if (N > 64 && tiles(128, 128) >= g_tile_min) {
     bm = bn = 128;
-  } else if (tiles(128, 64) >= 512) {
+  } else if (tiles(128, 64) >= g_tile_min) {
     bm = 128;
   }
   dim3 grid((M + bm - 1) / bm, (N + bn - 1) / bn, splits);

@@ -46,6 +46,7 @@ _HIP_PROTOS = {
                         p, p, p, p]),
     "tde_igemm_wgrad_scratch_elems": (i64, [i32, i32, i32]),
     "tde_igemm_tune": (None, [i32, i32, i32, i32, i32, i32]),
+    "tde_igemm_tile_min": (None, [i32]),
     "tde_bn_fwd": (i32, [p, p, p, i64, i32, i32, p, p, p, p, f32, p, p, f32, f32, p, i32, f32, C.c_ulonglong,
                          p, i32, i32, p]),
     "tde_bn_bwd": (i32, [p, p, p, i64, i32, i32, p, p, p, i32, f32, C.c_ulonglong, p, i32, i32, p, p, i32, p,
