@@ -1924,6 +1924,72 @@ __global__ __launch_bounds__(256) void maxpool_bwd8_w2_kernel(PoolArgs a) {
   }
 }
 
+// Pair variant of the above for windows where two horizontally adjacent input pixels see at most
+// 2 output columns together ((KW + sw) / sw <= 2: 3x3/2, 2x2/2): a thread owns input columns
+// (2t, 2t+1), so the <= 4 argmax + dy loads serve two outputs (half the load instructions).
+__global__ __launch_bounds__(256) void maxpool_bwd8_w2p_kernel(PoolArgs a) {
+  const Geo& g = a.g;
+  const int C8 = g.C >> 3;
+  const int row = blockIdx.y;
+  const int b = row / g.H, ih = row - b * g.H;
+  const int ty = ih + g.pt;
+  const int oh_lo = ty >= g.KH ? (ty - g.KH) / g.sh + 1 : 0, oh_hi = min(g.Ho - 1, ty / g.sh);
+  const int W2 = (g.W + 1) >> 1;
+  const int n = W2 * C8;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const int iw2 = e / C8, c8 = e - iw2 * C8;
+    const int iw0 = 2 * iw2;
+    const int tx0 = iw0 + g.pl;
+    const int ow_lo = tx0 >= g.KW ? (tx0 - g.KW) / g.sw + 1 : 0, ow_hi = min(g.Wo - 1, (tx0 + 1) / g.sw);
+    unsigned long long id[4];
+    bf16x8 d[4];
+    unsigned wi0[4], wi1[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int oh = oh_lo + (q >> 1), ow = ow_lo + (q & 1);
+      id[q] = ~0ull;  // byte 0xFF never equals a window index (host: KH*KW < 255)
+      wi0[q] = wi1[q] = 0xFFu;
+      if (oh <= oh_hi && ow <= ow_hi) {
+        const long long o = (((long long)b * g.Ho + oh) * g.Wo + ow) * g.C + c8 * 8;
+        id[q] = *reinterpret_cast<const unsigned long long*>(a.idx + o);
+        d[q] = *reinterpret_cast<const bf16x8*>(a.dy + o);
+        const int i = ty - oh * g.sh, j0 = tx0 - ow * g.sw;
+        if (j0 >= 0 && j0 < g.KW) wi0[q] = (unsigned)(i * g.KW + j0);
+        if (j0 + 1 >= 0 && j0 + 1 < g.KW) wi1[q] = (unsigned)(i * g.KW + j0 + 1);
+      }
+    }
+    float s0[8], s1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s0[j] = s1[j] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const unsigned w = (unsigned)((id[q] >> (8 * j)) & 0xFF);
+        const float v = bf2f(d[q][j]);
+        if (w == wi0[q]) s0[j] += v;
+        if (w == wi1[q]) s1[j] += v;
+      }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int iw = iw0 + h;
+      if (iw >= g.W) break;
+      const float* sv = h ? s1 : s0;
+      bf16x8* out = reinterpret_cast<bf16x8*>(a.dx + (((long long)row * g.W + iw) * g.C + c8 * 8));
+      bf16x8 o;
+      if (a.dx_accum) {
+        const bf16x8 prev = *out;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(sv[j] + bf2f(prev[j]));
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(sv[j]);
+      }
+      *out = o;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Global average pooling [B,HW,C] -> [B,C] and its backward; zero padding / its crop.
 __global__ __launch_bounds__(256) void gap_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int B, int HW,
@@ -2658,8 +2724,14 @@ TDE_API int tde_maxpool(const bf16* x, bf16* y, unsigned char* idx, const bf16* 
     if (!backward) maxpool_fwd8_kernel<<<grid_for((long long)g.B * g.Ho * g.Wo * g.C, 8), 256, 0, stream>>>(a);
     else if ((g.KH + g.sh - 1) / g.sh <= 2 && (g.KW + g.sw - 1) / g.sw <= 2 && g.KH * g.KW < 255 &&
              (long long)g.B * g.H <= 65535) {
-      const int per_row = g.W * (g.C / 8);
-      maxpool_bwd8_w2_kernel<<<dim3((per_row + 255) / 256, g.B * g.H), 256, 0, stream>>>(a);
+      static const bool pair_off = getenv("TDE_MAXPOOL_BWD_SINGLE") != nullptr;
+      if (!pair_off && (g.KW + g.sw) / g.sw <= 2) {
+        const int per_row = ((g.W + 1) / 2) * (g.C / 8);
+        maxpool_bwd8_w2p_kernel<<<dim3((per_row + 255) / 256, g.B * g.H), 256, 0, stream>>>(a);
+      } else {
+        const int per_row = g.W * (g.C / 8);
+        maxpool_bwd8_w2_kernel<<<dim3((per_row + 255) / 256, g.B * g.H), 256, 0, stream>>>(a);
+      }
     } else maxpool_bwd8_kernel<<<grid_for((long long)g.B * g.H * g.W * g.C, 8), 256, 0, stream>>>(a);
     TDE_LAUNCH_CHECK();
     return 0;
