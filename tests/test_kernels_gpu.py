@@ -241,3 +241,20 @@ def test_optimizer_kernel_matches_reference(kind):
     W = st2.view("dense/kernel")
     assert torch.equal(ok.shadow_views[("dense/kernel", "row")], W.to(torch.bfloat16))
     assert torch.equal(ok.shadow_views[("dense/kernel", "col")], W.T.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("fpw", [1, 4])
+def test_convnet_fwd_geometries(fpw):
+    """The non-default forward geometries (TDE_CONVNET_FPW = 1 / 4 pooled positions per workgroup; the
+    library reads the knob once per process) against the same fp32 reference, in a child process."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = ("import sys; sys.path.insert(0, %r); import test_kernels_gpu as t\n"
+            "for B in (64, 37, 130): t.test_convnet_fwd_fused(B)\n"
+            "t.test_convnet_bwd_fused(64)\nprint('ok')\n" % here)
+    env = dict(os.environ, TDE_CONVNET_FPW=str(fpw))
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=os.path.dirname(here), capture_output=True,
+                       text=True, timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

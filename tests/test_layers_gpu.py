@@ -603,3 +603,20 @@ def test_smallconv_wgrad(B, H, W, C, Co, k, s, pad):
     ref = _dev(wr.grad.permute(2, 3, 1, 0)) + dW0.double()
     torch.cuda.synchronize()
     assert _rel(dW.double(), ref) < 1e-5
+
+
+def test_conv_and_dense_with_largest_tiles():
+    """TDE_IGEMM_TILE_MIN=1 makes every fwd/dgrad/dense GEMM take the largest tile (128x128 / 128x64)
+    that the 2048-workgroup default now rarely picks; same fp32 references, in a child process (the
+    library reads the knob once)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = ("import sys; sys.path.insert(0, %r); import test_layers_gpu as t\n"
+            "for c in t.CONV_CASES: t.test_conv_fwd_dgrad_wgrad(*c)\n"
+            "t.test_dense_fwd_dgrad_wgrad(256, 512, 1000, False)\nprint('ok')\n" % here)
+    env = dict(os.environ, TDE_IGEMM_TILE_MIN="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=os.path.dirname(here), capture_output=True,
+                       text=True, timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
