@@ -49,7 +49,10 @@ struct ConvNetFwdArgs {
 // image) are staged into LDS with coalesced float4 loads: gathering 4x4 patches
 // straight from HBM puts 64 distinct cache lines behind every load instruction.
 constexpr int XR = 6, XW = 32;
-constexpr int fwd_lds(int fpw) { return fpw * 64 * PSTR * 2 + 64 * XR * XW * 4; }
+// per-image stride of the staged rows padded to 2 (mod 64) floats: the per-lane (= per-image) float2
+// patch reads then hit distinct bank pairs (168 = 40 mod 64 for MNIST made them 8-way conflicts)
+__host__ __device__ constexpr int fwd_istride(int W) { return XR * W + ((2 - (XR * W) % 64) + 64) % 64; }
+constexpr int fwd_lds(int fpw) { return fpw * 64 * PSTR * 2 + 64 * (XR * XW + 64) * 4; }
 
 // FPW pooled positions x 64 images per workgroup, 4*FPW waves (wave = position x 8-channel
 // group).  Phase 1 is VALU-bound: fewer positions per workgroup spread the conv over more CUs
@@ -77,7 +80,7 @@ __global__ __launch_bounds__(FPW * 256) void convnet_fwd_kernel(ConvNetFwdArgs a
   const bool pok = p < P;
   const int py0 = p0 / Wp;
   const int nrows = min(XR, H - 2 * py0);
-  const int istride = XR * W;  // floats per staged image
+  const int istride = fwd_istride(W);  // floats per staged image (bank-padded)
 
   // ---- prologue: all global loads, independent, issued back to back
   {
@@ -87,7 +90,10 @@ __global__ __launch_bounds__(FPW * 256) void convnet_fwd_kernel(ConvNetFwdArgs a
       float4 v = {0.f, 0.f, 0.f, 0.f};
       if (b0 + bl < a.B)
         v = *reinterpret_cast<const float4*>(a.x + (size_t)(b0 + bl) * H * W + (size_t)(2 * py0) * W + q * 4);
-      *reinterpret_cast<float4*>(xr + bl * istride + q * 4) = v;
+      // istride is only 8-byte aligned (bank padding): two 8-byte LDS writes
+      float2* d2 = reinterpret_cast<float2*>(xr + bl * istride + q * 4);
+      d2[0] = float2{v.x, v.y};
+      d2[1] = float2{v.z, v.w};
     }
   }
   float4 wlo[9], whi[9];
@@ -211,8 +217,11 @@ constexpr int kPt = kW1 + 128 * RSTR * 2;               // bf16 [128][RSTR]
 constexpr int kGt = kPt + 128 * RSTR * 2;               // bf16 [64][RSTR]
 constexpr int kXs = kGt + 64 * RSTR * 2;                // f32  [PPW][64][16]
 constexpr int kAm = kXs + PPW * 64 * 16 * 4;            // u8   [PPW][64][CC]
-constexpr int kDp = kAm + PPW * 64 * CC;                // f32  [PPW][64][CC]  (reused as red [NW][16][CC])
-constexpr int kBwdLds = kDp + PPW * 64 * CC * 4;
+constexpr int kDp = kAm + PPW * 64 * CC;                // f32  [PPW][64][DPS] (reused as red [NW][16][CC])
+// dP row stride: 40 floats puts the 4 lane groups of the routing reads (rows 2 apart) on disjoint
+// bank quarters (stride 32 made them 4-way LDS bank conflicts)
+constexpr int DPS = 40;
+constexpr int kBwdLds = kDp + PPW * 64 * DPS * 4;
 
 __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -307,7 +316,7 @@ __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
           acc = mfma16(av, bv, acc);
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) dps[((size_t)pp * 64 + mt * 16 + fq * 4 + r) * CC + ct * 16 + fr] = acc[r];
+        for (int r = 0; r < 4; ++r) dps[((size_t)pp * 64 + mt * 16 + fq * 4 + r) * DPS + ct * 16 + fr] = acc[r];
       }
     }
     // ---- dW1 rows += P^T . G   (32 tiles of 16x16: t = wave, wave+16)
@@ -350,7 +359,7 @@ __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
           for (int h = 0; h < 2; ++h) {
             const size_t idx = ((size_t)pp * 64 + bl + h) * CC + c;
             const unsigned id = am[idx];
-            const float dv = dps[idx];
+            const float dv = dps[((size_t)pp * 64 + bl + h) * DPS + c];
 #pragma unroll
             for (int q = 0; q < 4; ++q) bv[h * 4 + q] = f2bf(id == (unsigned)q ? dv : 0.f);
           }
