@@ -2552,7 +2552,14 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   // big tiles (256 x 64 with 64 x 64 per wave, or 256 x 128 with 128 x 64 per wave): LDS reads per
   // MFMA flop within the CU's LDS bandwidth; only when they still give >= g_big_min workgroups
   const long long big_tiles = (long long)((M + 255) / 256) * ((N + (N <= 64 ? 63 : 127)) / (N <= 64 ? 64 : 128));
-  const bool big = g_big && KB == 64 && splits == 1 && !rowk && (N <= 64 || N % 128 == 0) && big_tiles >= g_big_min;
+  // dgrad takes them by default (ResNet-18 sweep: dgrad 841 -> 824 us/step); fwd only when tuned on
+  // (fwd 641 -> 840 us with them).  TDE_IGEMM_BIG_DGRAD=0 turns the dgrad default off.
+  static const bool big_dgrad = [] {
+    const char* e = getenv("TDE_IGEMM_BIG_DGRAD");
+    return !(e && e[0] == '0');
+  }();
+  const bool big = (g_big || (big_dgrad && akind == A_DGRAD)) && KB == 64 && splits == 1 && !rowk &&
+                   (N <= 64 || N % 128 == 0) && big_tiles >= g_big_min;
 #define TDE_IGEMM(AK_, BK__, BM_, BN_)                                                   \
   do {                                                                                   \
     if (vec) {                                                                           \

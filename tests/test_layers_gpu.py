@@ -620,3 +620,18 @@ def test_conv_and_dense_with_largest_tiles():
     r = subprocess.run([sys.executable, "-c", code], env=env, cwd=os.path.dirname(here), capture_output=True,
                        text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_conv_big_tiles_forced():
+    """The 256-row "big" implicit-GEMM tiles (default for dgrad on large layers, opt-in for fwd) forced on
+    every eligible conv case (big_min = 1) against the same fp32 references; defaults restored after."""
+    from tensorflow_distributed_example_amd import _native as N
+    lib = N.hip()
+    lib.tde_igemm_tune(512, 16, 0, 1, 1, 1)
+    try:
+        for c in CONV_CASES:
+            test_conv_fwd_dgrad_wgrad(*c)
+        test_conv_fwd_dgrad_wgrad(4, 20, 20, 64, 128, 3, 1, "same")
+        test_conv_fwd_dgrad_wgrad(2, 14, 14, 128, 64, 3, 2, "same")
+    finally:
+        lib.tde_igemm_tune(512, 16, 0, 1, 0, 192)
