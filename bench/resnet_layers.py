@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--sweep", action="store_true")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--sweep-tile", action="store_true", help="sweep the fwd/dgrad tile-size threshold only")
+    ap.add_argument("--sweep-big-dgrad", action="store_true", help="A/B the dgrad big tiles only")
     a = ap.parse_args()
     import tensorflow_distributed_example_amd as tde
     from tensorflow_distributed_example_amd import _native as N
@@ -77,6 +78,15 @@ def main():
                       for st in _convs(plan, LW) if st.need_dgrad)
             print(f"SWEEP tile_min={tmin}: fwd {tf_:.1f} us dgrad {td_:.1f} us", flush=True)
         lib.tde_igemm_tile_min(512)
+    if a.sweep_big_dgrad:
+        lib = N.hip()
+        for bd in (0, 1, 0, 1):
+            lib.tde_igemm_big_dgrad(bd)
+            td_ = sum(graph_time(lambda: O.conv_dgrad(st.out.root().grad, st.Wrow, st.inp.root().grad,
+                                                      st.geo.with_batch(B), scratch=plan.scratch), a.reps)
+                      for st in _convs(plan, LW) if st.need_dgrad)
+            print(f"SWEEP big_dgrad={bd}: dgrad {td_:.1f} us", flush=True)
+        lib.tde_igemm_big_dgrad(0)
     if a.sweep:
         lib = N.hip()
         for target, mkt, kb in [(1024, 8, 0), (512, 8, 0), (256, 8, 0), (512, 16, 0), (256, 16, 0), (2048, 4, 0),
@@ -96,14 +106,14 @@ def main():
                       for st in _convs(plan, LW) if st.need_dgrad)
             print(f"SWEEP glds={glds} kb={kb} big={big} min={bmin}: fwd {tf_:.1f} us dgrad {td_:.1f} us", flush=True)
         lib.tde_igemm_tune(512, 16, 0, 1, 0, 192)
-        for kb in ():
-            lib.tde_igemm_tune(512, 16, kb, -1)
-            tf_ = sum(graph_time(lambda: st.fwd(plan, B, True), a.reps) for st in _convs(plan, LW))
+        # dgrad on the 256-row big tiles (KB = 64) vs the default KB = 32 tiles, A/B/A/B
+        for bd in (0, 1, 0, 1):
+            lib.tde_igemm_big_dgrad(bd)
             td_ = sum(graph_time(lambda: O.conv_dgrad(st.out.root().grad, st.Wrow, st.inp.root().grad,
                                                       st.geo.with_batch(B), scratch=plan.scratch), a.reps)
                       for st in _convs(plan, LW) if st.need_dgrad)
-            print(f"SWEEP kb={kb}: fwd {tf_:.1f} us dgrad {td_:.1f} us", flush=True)
-        lib.tde_igemm_tune(512, 16, 0, 1, 0, 192)
+            print(f"SWEEP big_dgrad={bd}: dgrad {td_:.1f} us", flush=True)
+        lib.tde_igemm_big_dgrad(0)
 
 
 if __name__ == "__main__":

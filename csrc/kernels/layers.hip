@@ -2351,6 +2351,13 @@ __global__ __launch_bounds__(256) void gemm_finalize_kernel(float* __restrict__ 
 // g_kb_force (32/64) overrides the K step.
 // g_glds selects the global_load_lds pipeline for the K-vector kinds (fwd / dgrad / dense).
 static int g_wg_target = 512, g_wg_min_kt = 16, g_kb_force = 0, g_glds = 1, g_big = 0, g_big_min = 192;
+// dgrad on 256-row big tiles (which need the KB = 64 step): TDE_IGEMM_BIG_DGRAD=1 / tde_igemm_big_dgrad()
+static int g_big_dgrad = [] {
+  const char* e = getenv("TDE_IGEMM_BIG_DGRAD");
+  return e && e[0] == '1' ? 1 : 0;
+}();
+// number of big-tile launches since load (tests assert the path ran)
+static unsigned long long g_big_launches = 0;
 // XCD-aware tile order (TDE_XCD_SWIZZLE=1).  Off by default: on ResNet-18 / Model B at their batch
 // sizes the GEMMs are not HBM-bound (working sets sit in L2/MALL) and the remap measured within noise
 // (fwd 681 -> 692 us, dgrad 837 -> 847, wgrad 916 -> 911 per step; bench/resnet_layers.py).
@@ -2368,6 +2375,9 @@ static int g_tile_min = [] {
 TDE_API void tde_igemm_tile_min(int v) {
   if (v > 0) g_tile_min = v;
 }
+
+TDE_API void tde_igemm_big_dgrad(int on) { g_big_dgrad = on ? 1 : 0; }
+TDE_API unsigned long long tde_igemm_big_launches() { return g_big_launches; }
 
 TDE_API void tde_igemm_tune(int wg_target, int wg_min_kt, int kb_force, int glds, int big, int big_min) {
   if (wg_target > 0) g_wg_target = wg_target;
@@ -2478,7 +2488,13 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   }
   // K step: 64 (two MFMA k-slices per barrier) for long reductions; the gathered input gradient
   // measures faster at 32 (ResNet-18 sweep, bench/resnet_layers.py)
-  const int KB = g_kb_force ? g_kb_force : ((akind == A_DGRAD || K < 256) ? 32 : 64);
+  // 256-row big tiles: LDS reads per MFMA flop within the CU's LDS bandwidth; only when they still give
+  // >= g_big_min workgroups (tile count independent of the K step)
+  const long long big_tiles = (long long)((M + 255) / 256) * ((N + (N <= 64 ? 63 : 127)) / (N <= 64 ? 64 : 128));
+  const bool big_shape = splits <= 1 && (N <= 64 || N % 128 == 0) && big_tiles >= g_big_min;
+  // dgrad big tiles run at KB = 64 (their only instantiation), so enabling them moves dgrad to KB = 64
+  const bool dgrad_big = akind == A_DGRAD && g_big_dgrad && big_shape && p.g.Co % 64 == 0;
+  const int KB = g_kb_force ? g_kb_force : (dgrad_big ? 64 : ((akind == A_DGRAD || K < 256) ? 32 : 64));
   const int ktiles = (K + KB - 1) / KB;
   const bool auto_splits = splits == 0;
   if (splits < 1) splits = 1;
@@ -2549,17 +2565,9 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   bool ut = true;
   if (akind == A_CONV) ut = p.g.C % KB == 0;
   if (akind == A_DGRAD) ut = p.g.Co % KB == 0 && (p.ph_on || (p.g.sh == 1 && p.g.sw == 1));
-  // big tiles (256 x 64 with 64 x 64 per wave, or 256 x 128 with 128 x 64 per wave): LDS reads per
-  // MFMA flop within the CU's LDS bandwidth; only when they still give >= g_big_min workgroups
-  const long long big_tiles = (long long)((M + 255) / 256) * ((N + (N <= 64 ? 63 : 127)) / (N <= 64 ? 64 : 128));
-  // dgrad takes them by default (ResNet-18 sweep: dgrad 841 -> 824 us/step); fwd only when tuned on
-  // (fwd 641 -> 840 us with them).  TDE_IGEMM_BIG_DGRAD=0 turns the dgrad default off.
-  static const bool big_dgrad = [] {
-    const char* e = getenv("TDE_IGEMM_BIG_DGRAD");
-    return !(e && e[0] == '0');
-  }();
-  const bool big = (g_big || (big_dgrad && akind == A_DGRAD)) && KB == 64 && splits == 1 && !rowk &&
-                   (N <= 64 || N % 128 == 0) && big_tiles >= g_big_min;
+  // big tiles (256 x 64 with 64 x 64 per wave, or 256 x 128 with 128 x 64 per wave): fwd/dense when
+  // tuned on (fwd 641 -> 840 us on ResNet-18 with them), dgrad when g_big_dgrad
+  const bool big = (g_big || (g_big_dgrad && akind == A_DGRAD)) && KB == 64 && splits == 1 && !rowk && big_shape;
 #define TDE_IGEMM(AK_, BK__, BM_, BN_)                                                   \
   do {                                                                                   \
     if (vec) {                                                                           \
@@ -2574,6 +2582,7 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
 #define TDE_IGEMM_KV(AK_, BK__, BM_, BN_)                                                           \
   do {                                                                                              \
     if (vec && g_glds && ut) {                                                                      \
+      if (big) ++g_big_launches;                                                                    \
       if (big && N <= 64) {                                                                         \
         grid = dim3((M + 255) / 256, (N + 63) / 64, splits);                                        \
         igemm_kernel<AK_, BK__, 256, 64, 64, 1, 3, 4><<<grid, 256, 0, stream>>>(p);                 \

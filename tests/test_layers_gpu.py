@@ -623,15 +623,29 @@ def test_conv_and_dense_with_largest_tiles():
 
 
 def test_conv_big_tiles_forced():
-    """The 256-row "big" implicit-GEMM tiles (default for dgrad on large layers, opt-in for fwd) forced on
-    every eligible conv case (big_min = 1) against the same fp32 references; defaults restored after."""
+    """The 256-row "big" implicit-GEMM tiles forced on every eligible conv case (big_min = 1) against the
+    same fp32 references: fwd through g_big (KB = 64 forced so the K < 256 layers qualify too), dgrad
+    through the dgrad toggle (which moves dgrad to KB = 64).  The launch counter proves the big kernels
+    ran for both; defaults restored after."""
     from tensorflow_distributed_example_amd import _native as N
     lib = N.hip()
-    lib.tde_igemm_tune(512, 16, 0, 1, 1, 1)
+    cases = list(CONV_CASES) + [(4, 20, 20, 64, 128, 3, 1, "same"), (2, 14, 14, 128, 64, 3, 2, "same"),
+                                (2, 16, 16, 64, 64, 3, 1, "same")]
     try:
-        for c in CONV_CASES:
+        for kb in (0, 64):
+            lib.tde_igemm_tune(512, 16, kb, 1, 1, 1)
+            lib.tde_igemm_big_dgrad(1)
+            n0 = lib.tde_igemm_big_launches()
+            for c in cases:
+                test_conv_fwd_dgrad_wgrad(*c)
+            assert lib.tde_igemm_big_launches() > n0
+        # dgrad alone (fwd big tiles off): the 64-channel stride-1 and stride-2 (phase) cases must go big
+        lib.tde_igemm_tune(512, 16, 0, 1, 0, 1)
+        lib.tde_igemm_big_dgrad(1)
+        for c in [(2, 16, 16, 64, 64, 3, 1, "same"), (2, 14, 14, 128, 64, 3, 2, "same")]:
+            n0 = lib.tde_igemm_big_launches()
             test_conv_fwd_dgrad_wgrad(*c)
-        test_conv_fwd_dgrad_wgrad(4, 20, 20, 64, 128, 3, 1, "same")
-        test_conv_fwd_dgrad_wgrad(2, 14, 14, 128, 64, 3, 2, "same")
+            assert lib.tde_igemm_big_launches() > n0, c
     finally:
         lib.tde_igemm_tune(512, 16, 0, 1, 0, 192)
+        lib.tde_igemm_big_dgrad(0)
