@@ -133,6 +133,9 @@ def main():
         same = all(f[2] == fps[0][2] for f in fps)   # trainable weights (BN moving stats are per replica)
         if strategy.worker_index == 0:
             print(f"[bench] replicas_identical={same}", file=sys.stderr, flush=True)
+    # where the optimizer update runs: fused into the step's kernels (1 replica), into the xGMI
+    # gradient all-reduce (one replica per process), or its own multi-tensor launch
+    placement = {"local": "in_step_kernels", "xgmi": "allreduce"}.get(prog.plans[0].step_mode, "separate")
     ms = elapsed / a.steps * 1e3
     ips = GB * a.steps / elapsed
     if strategy.worker_index == 0:
@@ -147,7 +150,8 @@ def main():
                        "per_gpu_batch": B, "parallelism": f"dp{n}", "strategy": "MultiWorkerMirroredStrategy",
                        "steps_per_execution": spe, "optimizer": f"SGD(lr={a.lr})", "plan": prog.plan_kind,
                        "allreduce": ar,
-                       "hipgraph": prog.use_graph, "grad_buckets": len(prog.buckets or []) or 1}}), flush=True)
+                       "hipgraph": prog.use_graph, "grad_buckets": len(prog.buckets or []) or 1,
+                       "optimizer_placement": placement}}), flush=True)
 
 
 if __name__ == "__main__":

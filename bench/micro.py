@@ -89,17 +89,21 @@ def main():
     y = torch.randint(0, 10, (64,), device="cuda", dtype=torch.int32)
 
     def k_fwd(stamps=None):
-        K.convnet_fwd(x, plan._v("wc"), plan._v("bc"), plan.W1col, plan.hpre, plan.Pt, plan.amax, stamps=stamps)
+        plan._forward(x, 64, True, plan._sopt if plan.step_mode == "local" else None) if stamps is None else \
+            K.convnet_fwd(x, plan._v("wc"), plan._v("bc"), plan.W1fwd, plan.hpre, plan.Pt, plan.amax, stamps=stamps)
 
     def k_head(stamps=None):
         K.head_xent(plan.hpre, plan._v("w2"), plan._v("b2"), y, B=64, scale=plan.scale, pre_bias=plan._v("b1"),
                     pre_relu=True, compute_grad=True, dW2=plan._g("w2"), db2=plan._g("b2"), dpre_bias=plan._g("b1"),
                     G=plan.G, Gt=plan.Gt, metrics=plan.metrics, zero_hin=True, iterations=plan.iterations,
-                    stamps=stamps)
+                    stamps=stamps, commit=plan._commit if plan.step_mode == "local" else None)
 
     def k_bwd(stamps=None):
+        local = plan.step_mode == "local"
         K.convnet_bwd(x, plan.amax, plan.G, plan.Gt, plan.W1row, plan.Pt, plan._g("w1"), plan._g("wc"),
-                      plan._g("bc"), B=64, stamps=stamps)
+                      plan._g("bc"), B=64, stamps=stamps, opt=plan._sopt if local else None,
+                      off_w1=plan.store.segments[plan.names["w1"]].offset, W1col=plan.W1col,
+                      head_ranges=plan._head_ranges if local else ())
 
     def k_opt():
         plan.opt.apply()
@@ -107,10 +111,23 @@ def main():
     def step():
         k_fwd(); k_head(); k_bwd(); k_opt()
 
+    def step_local():
+        k_fwd(); k_head(); k_bwd()
+
+    plan.set_step_mode("plain")
+    out["w1_source"] = "rows" if plan.w1_rows else "col"
     out["kernel_graph_us"] = {n: graph_time(f) for n, f in
                               [("convnet_fwd", k_fwd), ("head", k_head), ("convnet_bwd", k_bwd), ("optim", k_opt)]}
     out["step_graph_us"] = graph_time(step, reps=100)
     out["step_eager_us"] = eager_time(step, reps=200)
+    # fused single-replica step: the optimizer inside fwd / head / bwd, one flush per execution
+    plan.set_step_mode("local")
+    out["local_kernel_graph_us"] = {n: graph_time(f) for n, f in
+                                    [("convnet_fwd", k_fwd), ("head", k_head), ("convnet_bwd", k_bwd),
+                                     ("flush", plan.finish)]}
+    out["local_step_graph_us"] = graph_time(step_local, reps=100)
+    plan.finish()
+    plan.set_step_mode("plain")
     st = torch.zeros(4096 * 8, dtype=torch.int64, device="cuda")
     for name, f, ns in [("convnet_fwd", k_fwd, 5), ("head", k_head, 4), ("convnet_bwd", k_bwd, 6)]:
         st.zero_()

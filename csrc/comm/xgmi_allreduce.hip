@@ -17,7 +17,11 @@
 //            stores the reduced chunk into out[p][s][c] of every rank, raising
 //            flag2[p][s][c] there.
 //   phase 3  block c of every rank waits for flag2[p][*][c] and copies the reduced
-//            chunks back into the gradient bucket.
+//            chunks back into the gradient bucket — or, in the fused form
+//            (tde_xgmi_all_reduce_apply), applies the optimizer to them: every rank
+//            updates its fp32 weights (+ slots, + bf16 shadow) from the same reduced
+//            sums in the same order and zeroes its gradient, so the separate
+//            optimizer launch disappears from the data-parallel step.
 //
 // Block c only ever waits for block c of its peers, so there is no grid-wide
 // barrier; the grid (<= kXgMaxBlocks workgroups) is resident on the 256 CUs at once.
@@ -48,7 +52,7 @@
 #include <stdint.h>
 #include <string.h>
 
-#include "tde_common.h"
+#include "tde_optim.h"
 
 namespace tde {
 
@@ -69,6 +73,15 @@ struct XgArgs {
   long long chunk;                // chunk length within a slice (multiple of 4)
   long long cap;                  // elements per area (>= nranks * L)
   long long timeout_ticks;
+  // fused optimizer (phase 3): w/m/v flat like grad; shadow[e - sh_lo] = bf16(w[e]) for e in
+  // [sh_lo, sh_hi) (sh_lo a multiple of 4), and, when sht != null, sht[c * sht_ld + r] with
+  // (r, c) = divmod(e - sh_lo, sh_cols)
+  int apply;
+  float *w, *m, *v;
+  bf16* sh; long long sh_lo, sh_hi;
+  bf16* sht; int sh_cols; long long sht_ld;
+  const long long* iterations;
+  OptHyper h;
 };
 
 __device__ __forceinline__ uint32_t* flag_ptr(char* base, int parity, int phase, int src, int blk) {
@@ -135,6 +148,59 @@ __device__ __forceinline__ void copy_chunk(float* dst, const float* src, long lo
   }
 }
 
+__device__ __forceinline__ void shadow_store(const XgArgs& a, long long e, float w) {
+  if (e < a.sh_lo || e >= a.sh_hi) return;
+  const long long q = e - a.sh_lo;
+  const bf16 h = f2bf(w);
+  a.sh[q] = h;
+  if (a.sht) a.sht[(q % a.sh_cols) * a.sht_ld + q / a.sh_cols] = h;
+}
+
+// Optimizer step on n reduced elements (global index g0..): w, slots, shadows; grad zeroed.
+__device__ __forceinline__ void apply_chunk(const XgArgs& a, float lr_t, long long g0, const float* red, long long n) {
+  const int tid = threadIdx.x;
+  const bool mom = a.h.kind != kOptSGD, adam = a.h.kind == kOptAdam;
+  long long nv = 0;
+  if ((g0 & 3) == 0) {   // area offsets are multiples of 4 elements
+    nv = n >> 2;
+    for (long long i = tid; i < nv; i += kXgThreads) {
+      const long long e = g0 + 4 * i;
+      const float4 gs = reinterpret_cast<const float4*>(red)[i];
+      float4 w = *reinterpret_cast<const float4*>(a.w + e);
+      float4 m = {0.f, 0.f, 0.f, 0.f}, v = {0.f, 0.f, 0.f, 0.f};
+      if (mom) m = *reinterpret_cast<const float4*>(a.m + e);
+      if (adam) v = *reinterpret_cast<const float4*>(a.v + e);
+      w.x = opt_step(a.h, lr_t, w.x, gs.x, m.x, v.x);
+      w.y = opt_step(a.h, lr_t, w.y, gs.y, m.y, v.y);
+      w.z = opt_step(a.h, lr_t, w.z, gs.z, m.z, v.z);
+      w.w = opt_step(a.h, lr_t, w.w, gs.w, m.w, v.w);
+      *reinterpret_cast<float4*>(a.w + e) = w;
+      if (mom) *reinterpret_cast<float4*>(a.m + e) = m;
+      if (adam) *reinterpret_cast<float4*>(a.v + e) = v;
+      *reinterpret_cast<float4*>(a.grad + e) = float4{0.f, 0.f, 0.f, 0.f};
+      if (e >= a.sh_lo && e + 4 <= a.sh_hi && !a.sht) {
+        *reinterpret_cast<bf16x4*>(a.sh + (e - a.sh_lo)) = bf16x4{f2bf(w.x), f2bf(w.y), f2bf(w.z), f2bf(w.w)};
+      } else {
+        shadow_store(a, e, w.x);
+        shadow_store(a, e + 1, w.y);
+        shadow_store(a, e + 2, w.z);
+        shadow_store(a, e + 3, w.w);
+      }
+    }
+    nv <<= 2;
+  }
+  for (long long i = nv + tid; i < n; i += kXgThreads) {
+    const long long e = g0 + i;
+    float m = mom ? a.m[e] : 0.f, v = adam ? a.v[e] : 0.f;
+    const float w = opt_step(a.h, lr_t, a.w[e], red[i], m, v);
+    a.w[e] = w;
+    if (mom) a.m[e] = m;
+    if (adam) a.v[e] = v;
+    a.grad[e] = 0.f;
+    shadow_store(a, e, w);
+  }
+}
+
 template <bool UNCACHED>
 __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgArgs a) {
   const int blk = blockIdx.x, tid = threadIdx.x;
@@ -176,13 +242,16 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgArgs a) {
   }
   publish<UNCACHED>(a.peer, N, parity, 1, r, blk, epoch);
 
-  // ---- phase 3: gather every reduced slice chunk back into the bucket
+  // ---- phase 3: gather every reduced slice chunk back into the bucket (or apply the update)
+  float lr_t = 0.f;
+  if (a.apply) lr_t = opt_lr_t(a.h, a.h.kind == kOptAdam ? *a.iterations : 0);
   await(a.peer[r], parity, 1, N, blk, epoch, a.timeout_ticks, a.err, 2u);
   const float* out = area(a.peer[r], 1, parity, cap);
   for (int s = 0; s < N; ++s) {
     const long long g0 = (long long)s * L + c0;
     const long long n = max(0LL, min(CH, M - g0));
-    copy_chunk(a.grad + g0, out + (size_t)s * L + c0, n, (g0 & 3) == 0);
+    if (a.apply) apply_chunk(a, lr_t, g0, out + (size_t)s * L + c0, n);
+    else copy_chunk(a.grad + g0, out + (size_t)s * L + c0, n, (g0 & 3) == 0);
   }
   // the last block to finish advances the epoch (every block read it at its start) and re-arms
   // the arrival counter epoch[1] for the next call
@@ -265,16 +334,61 @@ TDE_API long long tde_xgmi_epoch(void* epoch) {
 }
 
 // In-place SUM all-reduce of `grad` (M fp32 elements, M <= the window's max_elems).
+static int xg_launch(XgArgs& a, float* grad, long long M, long long max_elems, void* const* peers, void* epoch,
+                     void* err, int rank, int nranks, int nblocks, int uncached, long long timeout_ticks,
+                     hipStream_t stream);
+
 TDE_API int tde_xgmi_all_reduce(float* grad, long long M, long long max_elems, void* const* peers, void* epoch,
                                 void* err, int rank, int nranks, int nblocks, int uncached, long long timeout_ticks,
                                 hipStream_t stream) {
+  XgArgs a;
+  memset(&a, 0, sizeof(a));
+  return xg_launch(a, grad, M, max_elems, peers, epoch, err, rank, nranks, nblocks, uncached, timeout_ticks, stream);
+}
+
+// Fused form: SUM all-reduce of `grad` and the optimizer step of every element on every rank
+// (w/m/v flat like grad; shadows as in XgArgs); grad is left zeroed.
+struct TdeXgApply {
+  int kind;
+  float lr, mom, b1, b2, eps;
+  float *w, *m, *v;
+  const long long* iterations;
+  void* sh; long long sh_lo, sh_hi;
+  void* sht; int sh_cols; long long sht_ld;
+};
+
+TDE_API int tde_xgmi_all_reduce_apply(float* grad, long long M, long long max_elems, void* const* peers,
+                                      void* epoch, void* err, int rank, int nranks, int nblocks, int uncached,
+                                      long long timeout_ticks, const TdeXgApply* o, hipStream_t stream) {
+  if (!o || !o->w || (o->kind != kOptSGD && !o->m) || (o->kind == kOptAdam && (!o->v || !o->iterations))) return -7;
+  if ((((uintptr_t)o->w | (uintptr_t)o->m | (uintptr_t)o->v) & 15) || (o->sh && ((o->sh_lo & 3) || ((uintptr_t)o->sh & 7))))
+    return -8;
+  if (o->sht && (o->sh_cols <= 0 || !o->sh)) return -9;
+  XgArgs a;
+  memset(&a, 0, sizeof(a));
+  a.apply = 1;
+  a.w = o->w;
+  a.m = o->m;
+  a.v = o->v;
+  a.sh = (bf16*)o->sh;
+  a.sh_lo = o->sh ? o->sh_lo : 0;
+  a.sh_hi = o->sh ? o->sh_hi : 0;
+  a.sht = (bf16*)o->sht;
+  a.sh_cols = o->sh_cols;
+  a.sht_ld = o->sht_ld;
+  a.iterations = o->iterations;
+  a.h = OptHyper{o->kind, o->lr, o->mom, o->b1, o->b2, o->eps};
+  return xg_launch(a, grad, M, max_elems, peers, epoch, err, rank, nranks, nblocks, uncached, timeout_ticks, stream);
+}
+
+static int xg_launch(XgArgs& a, float* grad, long long M, long long max_elems, void* const* peers, void* epoch,
+                     void* err, int rank, int nranks, int nblocks, int uncached, long long timeout_ticks,
+                     hipStream_t stream) {
   if (nranks < 1 || nranks > kXgMaxRanks || rank < 0 || rank >= nranks) return -1;
   if (M < 0 || M > max_elems) return -2;
   if (((uintptr_t)grad & 15) != 0) return -4;
   if (nblocks < 1) nblocks = 1;
   if (nblocks > kXgMaxBlocks) nblocks = kXgMaxBlocks;
-  XgArgs a;
-  memset(&a, 0, sizeof(a));
   a.grad = grad;
   for (int i = 0; i < nranks; ++i) a.peer[i] = (char*)peers[i];
   a.epoch = (uint32_t*)epoch;

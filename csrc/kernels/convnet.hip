@@ -24,7 +24,20 @@
 //   route dP through the pool argmax and ReLU mask and reduce over (image, window
 //   slot) with MFMA: dWc[tap][c] = sum_k X[tap][k] D[k][c], k=(pos,b,q) — the
 //   bias gradient is the extra all-ones tap row.
-#include "tde_common.h"
+//
+// Fused single-replica step (no gradient all-reduce between backward and update):
+// the optimizer runs where each gradient is finished, with no extra launch and no
+// cross-workgroup hand-off inside a kernel (on gfx950 an in-kernel release/acquire
+// costs about as much as a kernel boundary):
+//   * Dense(64) kernel rows: each backward workgroup owns its rows' dW1 completely,
+//     so it updates the fp32 rows and rewrites their bf16 shadow in place;
+//   * Dense(64) bias, Dense(10) kernel + bias (finished by the head launch): the
+//     last backward workgroup updates them;
+//   * Conv2D kernel + bias (finished by the backward's atomics): deferred — the next
+//     forward computes the updated values on the fly from (w, g, slots) while *pend,
+//     and the next head launch (which does not read them) commits them and clears
+//     *pend; a flush launch commits them at the end of each execution.
+#include "tde_optim.h"
 
 namespace tde {
 
@@ -43,6 +56,13 @@ struct ConvNetFwdArgs {
   uint64_t* amax; int lda;          // [P][CC/8][lda] (nullable)
   int B, H, W;
   long long* stamps;
+  int w1_rows;                      // 1: W1c is the row-major [K][HD] shadow (ldw1c = HD)
+  // deferred conv update (fused step): while *pend the conv weights used are the optimizer
+  // step of (wc, bc) with the previous backward's gradients (nullable: use wc, bc as stored)
+  const int* pend;
+  const float *gwc, *gbc, *mwc, *mbc, *vwc, *vbc;
+  const long long* iterations;
+  OptHyper h;
 };
 
 // The input rows a workgroup's PPW positions touch (<= XR rows of <= XW floats per
@@ -52,7 +72,8 @@ constexpr int XR = 6, XW = 32;
 // per-image stride of the staged rows padded to 2 (mod 64) floats: the per-lane (= per-image) float2
 // patch reads then hit distinct bank pairs (168 = 40 mod 64 for MNIST made them 8-way conflicts)
 __host__ __device__ constexpr int fwd_istride(int W) { return XR * W + ((2 - (XR * W) % 64) + 64) % 64; }
-constexpr int fwd_lds(int fpw) { return fpw * 64 * PSTR * 2 + 64 * (XR * XW + 64) * 4; }
+constexpr int kConvW = CC * 10;   // conv taps [9][CC] + bias [CC] (floats), staged in LDS
+constexpr int fwd_lds(int fpw) { return fpw * 64 * PSTR * 2 + 64 * (XR * XW + 64) * 4 + kConvW * 4; }
 
 // FPW pooled positions x 64 images per workgroup, 4*FPW waves (wave = position x 8-channel
 // group).  Phase 1 is VALU-bound: fewer positions per workgroup spread the conv over more CUs
@@ -64,6 +85,7 @@ __global__ __launch_bounds__(FPW * 256) void convnet_fwd_kernel(ConvNetFwdArgs a
   extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
   bf16* Ps = reinterpret_cast<bf16*>(fsm);
   float* xr = reinterpret_cast<float*>(fsm + FPW * 64 * PSTR * 2);  // [64][XR][W]
+  float* wcs = reinterpret_cast<float*>(fsm + FPW * 64 * PSTR * 2 + 64 * (XR * XW + 64) * 4);  // [10][CC]
   stamp(a.stamps, 0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fk = (lane >> 4) * 8;
@@ -96,14 +118,21 @@ __global__ __launch_bounds__(FPW * 256) void convnet_fwd_kernel(ConvNetFwdArgs a
       d2[1] = float2{v.z, v.w};
     }
   }
-  float4 wlo[9], whi[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    wlo[t] = *reinterpret_cast<const float4*>(a.wc + t * CC + c0);
-    whi[t] = *reinterpret_cast<const float4*>(a.wc + t * CC + c0 + 4);
+  // conv weights in effect for this step -> LDS (with the deferred update applied while *pend)
+  for (int i = threadIdx.x; i < kConvW; i += NT) {
+    const bool isb = i >= 9 * CC;
+    const int j = isb ? i - 9 * CC : i;
+    float w = isb ? a.bc[j] : a.wc[j];
+    if (a.pend) {
+      const float g = isb ? a.gbc[j] : a.gwc[j];
+      float m = 0.f, v = 0.f;
+      if (a.h.kind != kOptSGD) m = isb ? a.mbc[j] : a.mwc[j];
+      if (a.h.kind == kOptAdam) v = isb ? a.vbc[j] : a.vwc[j];
+      const long long t = a.h.kind == kOptAdam ? *a.iterations : 0;
+      if (*a.pend) w = opt_step(a.h, opt_lr_t(a.h, t), w, g, m, v);
+    }
+    wcs[i] = w;
   }
-  const float4 blo = *reinterpret_cast<const float4*>(a.bc + c0);
-  const float4 bhi = *reinterpret_cast<const float4*>(a.bc + c0 + 4);
   // W1^T fragments of this wave's output tiles: tile t = wave + 4*FPW*j (j < 4/FPW),
   // mt = t>>2 (image rows), nt = t&3 = wave&3 (units) for every j
   const int nt = wave & 3;
@@ -111,11 +140,36 @@ __global__ __launch_bounds__(FPW * 256) void convnet_fwd_kernel(ConvNetFwdArgs a
 #pragma unroll
   for (int ks = 0; ks < FPW; ++ks) {
     const int kp = p0 + ks;
-    wfr[ks] = kp < P ? *reinterpret_cast<const bf16x8*>(a.W1c + (size_t)(nt * 16 + fr) * a.ldw1c + (size_t)kp * CC + fk)
-                     : bf16x8{};
+    if (kp >= P) {
+      wfr[ks] = bf16x8{};
+    } else if (a.w1_rows) {
+      // row-major shadow [K][HD]: 8 K-consecutive elements of column nt*16+fr (16 lanes read
+      // 32 contiguous bytes per element row)
+      const bf16* src = a.W1c + (size_t)(kp * CC + fk) * a.ldw1c + nt * 16 + fr;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) wfr[ks][j] = src[(size_t)j * a.ldw1c];
+    } else {
+      wfr[ks] = *reinterpret_cast<const bf16x8*>(a.W1c + (size_t)(nt * 16 + fr) * a.ldw1c + (size_t)kp * CC + fk);
+    }
   }
   stamp(a.stamps, 1);
   lds_barrier();
+  // this wave's 8 channels (wave-uniform LDS broadcast reads)
+  float4 wlo[9], whi[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const float4 lo = *reinterpret_cast<const float4*>(wcs + t * CC + c0);
+    const float4 hi = *reinterpret_cast<const float4*>(wcs + t * CC + c0 + 4);
+    wlo[t] = lo;
+    whi[t] = hi;
+  }
+  float4 blo, bhi;
+  {
+    const float4 lo = *reinterpret_cast<const float4*>(wcs + 9 * CC + c0);
+    const float4 hi = *reinterpret_cast<const float4*>(wcs + 9 * CC + c0 + 4);
+    blo = lo;
+    bhi = hi;
+  }
 
   // ---- phase 1: conv + bias + ReLU + 2x2 max-pool for 8 channels
   bf16x8 outv;
@@ -204,11 +258,82 @@ struct ConvNetBwdArgs {
   const bf16* Gt; int ldgt;          // [HD][ldgt] bf16
   const bf16* W1r; int ldw1r;        // [K][HD] bf16 (row-major shadow)
   const bf16* Pt; int ldPt;          // [K][ldPt] bf16
-  float* dW1;                        // [K][HD] f32 (stored)
+  float* dW1;                        // [K][HD] f32 (stored; unused when apply)
   float* dwc; float* dbc;            // [9][CC], [CC] (atomic +=)
   int B, H, W;
   long long* stamps;
+  // fused step: update the Dense(64) kernel rows here instead of storing dW1
+  int apply;
+  float *w1, *m1, *v1;               // fp32 master [K][HD] (+ slots), updated in place
+  bf16* w1r_out;                     // row-major bf16 shadow (== W1r), rewritten
+  bf16* w1c_out; int ldw1c;          // transposed bf16 shadow [HD][ldw1c] (nullable)
+  const long long* iterations;
+  OptHyper h;
+  FlatApply head;                    // applied by the last workgroup (head variables), nr = 0: none
+  int* pend;                         // set to 1: the conv update is pending (nullable)
 };
+
+// Up to NPER elements per thread of a FlatApply's ranges, loaded early into registers and
+// updated later (the loads' latency hides behind the caller's work).
+template <int NPER>
+struct FlatPrefetch {
+  int e[NPER];
+  float w[NPER], g[NPER], m[NPER], v[NPER];
+  __device__ __forceinline__ void load(const FlatApply& f, int tid, int nt) {
+#pragma unroll
+    for (int k = 0; k < NPER; ++k) {
+      int idx = tid + k * nt;
+      e[k] = -1;
+      for (int r = 0; r < f.nr; ++r) {
+        if (idx < f.n[r]) {
+          e[k] = f.lo[r] + idx;
+          break;
+        }
+        idx -= f.n[r];
+      }
+      w[k] = g[k] = m[k] = v[k] = 0.f;
+      if (e[k] >= 0) {
+        w[k] = f.w[e[k]];
+        g[k] = f.g[e[k]];
+        if (f.h.kind != kOptSGD) m[k] = f.m[e[k]];
+        if (f.h.kind == kOptAdam) v[k] = f.v[e[k]];
+      }
+    }
+  }
+  __device__ __forceinline__ void apply(const FlatApply& f, long long t) {
+    const float lr_t = opt_lr_t(f.h, t);
+#pragma unroll
+    for (int k = 0; k < NPER; ++k) {
+      if (e[k] < 0) continue;
+      f.w[e[k]] = opt_step(f.h, lr_t, w[k], g[k], m[k], v[k]);
+      f.g[e[k]] = 0.f;
+      if (f.h.kind != kOptSGD) f.m[e[k]] = m[k];
+      if (f.h.kind == kOptAdam) f.v[e[k]] = v[k];
+    }
+  }
+};
+
+// Elements [start, total) of a FlatApply's ranges, threads tid, tid + nt, ... (no prefetch).
+__device__ __forceinline__ void flat_apply_from(const FlatApply& f, long long t, int start, int tid, int nt) {
+  int total = 0;
+  for (int r = 0; r < f.nr; ++r) total += f.n[r];
+  const float lr_t = opt_lr_t(f.h, t);
+  for (int idx0 = start + tid; idx0 < total; idx0 += nt) {
+    int idx = idx0, e = -1;
+    for (int r = 0; r < f.nr; ++r) {
+      if (idx < f.n[r]) {
+        e = f.lo[r] + idx;
+        break;
+      }
+      idx -= f.n[r];
+    }
+    float m = f.h.kind != kOptSGD ? f.m[e] : 0.f, v = f.h.kind == kOptAdam ? f.v[e] : 0.f;
+    f.w[e] = opt_step(f.h, lr_t, f.w[e], f.g[e], m, v);
+    f.g[e] = 0.f;
+    if (f.h.kind != kOptSGD) f.m[e] = m;
+    if (f.h.kind == kOptAdam) f.v[e] = v;
+  }
+}
 
 // LDS carve (bytes)
 constexpr int kG = 0;                                   // bf16 [64][RSTR]
@@ -223,6 +348,8 @@ constexpr int kDp = kAm + PPW * 64 * CC;                // f32  [PPW][64][DPS] (
 constexpr int DPS = 40;
 constexpr int kBwdLds = kDp + PPW * 64 * DPS * 4;
 
+// MODE 0: store dW1; 1: fused step, SGD; 2: fused step, optimizer with slots (momentum / Adam)
+template <int MODE>
 __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16* Gs = reinterpret_cast<bf16*>(smem + kG);
@@ -243,6 +370,33 @@ __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
 
   f32x4 accw[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   f32x4 accr[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+
+  // fused step: this workgroup's fp32 master rows (and slots) and the head variables, loaded
+  // now, updated after the chunk loop
+  constexpr int NS = MODE == 2 ? 2 : 1;   // slot registers (dummies unless MODE 2)
+  f32x4 wp[2], mp[NS], vp[NS];
+  long long t_it = 0;
+  const bool head_wg = a.head.nr > 0 && blockIdx.x == gridDim.x - 1;
+  FlatPrefetch<1> hp;
+  if (MODE != 0) {
+    if (a.h.kind == kOptAdam || a.head.h.kind == kOptAdam) t_it = *a.iterations;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int t = wave + 16 * i;
+      const int nt = t & 3, rt = t >> 2;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rt * 16 + fq * 4 + r;
+        const size_t e = (size_t)(p0 * CC + row) * HD + nt * 16 + fr;
+        wp[i][r] = row < nrow ? a.w1[e] : 0.f;
+        if (MODE == 2) {
+          mp[i % NS][r] = (row < nrow && a.h.kind != kOptSGD) ? a.m1[e] : 0.f;
+          vp[i % NS][r] = (row < nrow && a.h.kind == kOptAdam) ? a.v1[e] : 0.f;
+        }
+      }
+    }
+    if (head_wg) hp.load(a.head, tid, 1024);
+  }
 
   // W1 rows of the 4 positions: loaded once (independent of the image chunk)
   {
@@ -371,15 +525,46 @@ __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
   }
   stamp(a.stamps, 4);
 
-  // ---- store dW1 tiles (each row of dW1 belongs to exactly one workgroup)
+  if (MODE != 0) {
+    // ---- update this workgroup's Dense(64) rows (complete dW1: rows belong to one workgroup) and
+    // rewrite their bf16 shadows; its W1 rows were read into LDS before the chunk loop
+    const float lr_t = opt_lr_t(a.h, t_it);
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int t = wave + 16 * i;
-    const int nt = t & 3, rt = t >> 2;
+    for (int i = 0; i < 2; ++i) {
+      const int t = wave + 16 * i;
+      const int nt = t & 3, rt = t >> 2;
+      const int col = nt * 16 + fr, row0 = rt * 16 + fq * 4;
+      if (row0 >= nrow) continue;   // nrow is a multiple of 32: all 4 rows valid or none
+      bf16x4 hv;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = rt * 16 + fq * 4 + r;
-      if (row < nrow) a.dW1[(size_t)(p0 * CC + row) * HD + nt * 16 + fr] = accw[i][r];
+      for (int r = 0; r < 4; ++r) {
+        const size_t e = (size_t)(p0 * CC + row0 + r) * HD + col;
+        float m = MODE == 2 ? mp[i % NS][r] : 0.f, v = MODE == 2 ? vp[i % NS][r] : 0.f;
+        const float w = opt_step(a.h, lr_t, wp[i][r], accw[i][r], m, v);
+        a.w1[e] = w;
+        if (MODE == 2 && a.h.kind != kOptSGD) a.m1[e] = m;
+        if (MODE == 2 && a.h.kind == kOptAdam) a.v1[e] = v;
+        hv[r] = f2bf(w);
+        a.w1r_out[e] = hv[r];
+      }
+      if (a.w1c_out) *reinterpret_cast<bf16x4*>(a.w1c_out + (size_t)col * a.ldw1c + p0 * CC + row0) = hv;
+    }
+    if (head_wg) {
+      hp.apply(a.head, t_it);
+      flat_apply_from(a.head, t_it, 1024, tid, 1024);   // elements beyond one per thread (none for MNIST)
+    }
+    if (a.pend && blockIdx.x == 0 && tid == 0) *a.pend = 1;
+  } else {
+    // ---- store dW1 tiles (each row of dW1 belongs to exactly one workgroup)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int t = wave + 16 * i;
+      const int nt = t & 3, rt = t >> 2;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rt * 16 + fq * 4 + r;
+        if (row < nrow) a.dW1[(size_t)(p0 * CC + row) * HD + nt * 16 + fr] = accw[i][r];
+      }
     }
   }
   // ---- reduce routing accumulators over the 16 waves, then 10*CC atomics
@@ -404,11 +589,31 @@ __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
 using namespace tde;
 
 // Specialised for Conv2D(32, 3x3, valid) on 1-channel input + MaxPool(2) + Dense(64).
+// Fused-step optimizer description shared by the convnet entry points (ctypes struct):
+// slots m/v flat like w; iterations = the device step counter.
+struct TdeStepOpt {
+  int kind;
+  float lr, mom, b1, b2, eps;
+  float *w, *g, *m, *v;
+  const long long* iterations;
+  int* pend;
+};
+
+static OptHyper hyper_of(const TdeStepOpt* o) { return OptHyper{o->kind, o->lr, o->mom, o->b1, o->b2, o->eps}; }
+static bool opt_ok(const TdeStepOpt* o) {
+  return o->w && o->g && o->iterations && (o->kind == kOptSGD || o->m) && (o->kind != kOptAdam || o->v);
+}
+
+// w1_rows: W1c is the row-major [K][HD] shadow (ldw1c == HD) instead of [HD][K].
+// opt (nullable): deferred conv update {w, g, m, v, pend} with wc/bc at offsets off_wc/off_bc.
 TDE_API int tde_convnet_fwd(const float* x, const float* wc, const float* bc, const void* W1c, int ldw1c,
                             float* hpre, void* Pt, int ldPt, void* amax, int lda, int B, int H, int W,
-                            long long* stamps, hipStream_t stream) {
+                            long long* stamps, int w1_rows, const TdeStepOpt* opt, long long off_wc,
+                            long long off_bc, hipStream_t stream) {
   if ((W & 3) || W > XW || ((W - 2) / 2) < 4 || (ldw1c & 7) || (Pt && (ldPt & 7)) || (amax && lda < B)) return -1;
   if (((uintptr_t)wc | (uintptr_t)bc) & 15) return -2;
+  if (w1_rows && ldw1c != HD) return -3;
+  if (opt && (!opt_ok(opt) || !opt->pend)) return -4;
   const int P = ((H - 2) / 2) * ((W - 2) / 2);
   int by = (B + 63) / 64;
   if (Pt) {
@@ -416,6 +621,18 @@ TDE_API int tde_convnet_fwd(const float* x, const float* wc, const float* bc, co
     if (byp > by) by = byp;
   }
   ConvNetFwdArgs a{x, wc, bc, (const bf16*)W1c, ldw1c, hpre, (bf16*)Pt, ldPt, (uint64_t*)amax, lda, B, H, W, stamps};
+  a.w1_rows = w1_rows;
+  if (opt) {
+    a.pend = opt->pend;
+    a.gwc = opt->g + off_wc;
+    a.gbc = opt->g + off_bc;
+    a.mwc = opt->m ? opt->m + off_wc : nullptr;
+    a.mbc = opt->m ? opt->m + off_bc : nullptr;
+    a.vwc = opt->v ? opt->v + off_wc : nullptr;
+    a.vbc = opt->v ? opt->v + off_bc : nullptr;
+    a.iterations = opt->iterations;
+    a.h = hyper_of(opt);
+  }
   // positions per workgroup (TDE_CONVNET_FPW = 1|2|4, default 2)
   static const int fpw = [] {
     const char* e = getenv("TDE_CONVNET_FPW");
@@ -437,19 +654,50 @@ TDE_API int tde_convnet_fwd(const float* x, const float* wc, const float* bc, co
   return 0;
 }
 
+// opt (nullable): fused step — Dense(64) rows at off_w1 updated in place (W1r rewritten; W1c [HD][ldw1c]
+// too when non-null), the head variables (ranges = {lo, n} x nr, nr <= kFlatRanges) updated by
+// the last workgroup, and *opt->pend set (deferred conv update).
 TDE_API int tde_convnet_bwd(const float* x, const void* amax, int lda, const void* G, int ldg, const void* Gt,
                             int ldgt, const void* W1r, int ldw1r, const void* Pt, int ldPt, float* dW1, float* dwc,
-                            float* dbc, int B, int H, int W, long long* stamps, hipStream_t stream) {
+                            float* dbc, int B, int H, int W, long long* stamps, const TdeStepOpt* opt,
+                            long long off_w1, void* W1c, int ldw1c, const int* ranges, int nr,
+                            hipStream_t stream) {
   if ((ldg & 7) || (ldgt & 7) || (ldw1r & 7) || (ldPt & 7) || ldgt < B || ldPt < B || lda < B) return -1;
+  if (opt && (!opt_ok(opt) || ldw1r != HD || (W1c && (ldw1c & 3)) || (off_w1 & 3) || nr < 0 || nr > kFlatRanges))
+    return -4;
   const int P = ((H - 2) / 2) * ((W - 2) / 2);
   ConvNetBwdArgs a{x, (const uint64_t*)amax, lda, (const bf16*)G, ldg, (const bf16*)Gt, ldgt, (const bf16*)W1r,
                    ldw1r, (const bf16*)Pt, ldPt, dW1, dwc, dbc, B, H, W, stamps};
+  if (opt) {
+    int total = 0;
+    for (int i = 0; i < nr; ++i) total += ranges[2 * i + 1];
+    a.apply = 1;
+    a.w1 = opt->w + off_w1;
+    a.m1 = opt->m ? opt->m + off_w1 : nullptr;
+    a.v1 = opt->v ? opt->v + off_w1 : nullptr;
+    a.w1r_out = (bf16*)W1r;
+    a.w1c_out = (bf16*)W1c;
+    a.ldw1c = ldw1c;
+    a.iterations = opt->iterations;
+    a.h = hyper_of(opt);
+    a.head = FlatApply{opt->w, opt->g, opt->m, opt->v, opt->iterations, nullptr, a.h, nr, {0}, {0}};
+    for (int i = 0; i < nr; ++i) {
+      a.head.lo[i] = ranges[2 * i];
+      a.head.n[i] = ranges[2 * i + 1];
+    }
+    a.pend = opt->pend;
+  }
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)convnet_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kBwdLds);
+    hipFuncSetAttribute((const void*)convnet_bwd_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, kBwdLds);
+    hipFuncSetAttribute((const void*)convnet_bwd_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, kBwdLds);
+    hipFuncSetAttribute((const void*)convnet_bwd_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, kBwdLds);
     attr_set = true;
   }
-  convnet_bwd_kernel<<<dim3((P + PPW - 1) / PPW), 1024, kBwdLds, stream>>>(a);
+  const dim3 grid((P + PPW - 1) / PPW);
+  if (!a.apply) convnet_bwd_kernel<0><<<grid, 1024, kBwdLds, stream>>>(a);
+  else if (a.h.kind == kOptSGD) convnet_bwd_kernel<1><<<grid, 1024, kBwdLds, stream>>>(a);
+  else convnet_bwd_kernel<2><<<grid, 1024, kBwdLds, stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;
 }

@@ -14,7 +14,7 @@
 // cross-workgroup protocol.
 //
 // Vectorised: float4 loads/stores everywhere (segments are 256-byte aligned).
-#include "tde_common.h"
+#include "tde_optim.h"
 
 namespace tde {
 
@@ -45,16 +45,8 @@ struct Hyper {
 };
 
 __device__ __forceinline__ float upd1(const OptArgs& a, float w, float g, float& m, float& v, const Hyper& h) {
-  g *= a.grad_scale;
-  if (a.kind == 0) return w - h.lr * g;
-  if (a.kind == 1 || a.kind == 2) {
-    const float nv = a.mom * m - h.lr * g;  // Keras: v = m*v - lr*g ; w += v
-    m = nv;
-    return a.kind == 2 ? w + a.mom * nv - h.lr * g : w + nv;
-  }
-  m = a.b1 * m + (1.f - a.b1) * g;
-  v = a.b2 * v + (1.f - a.b2) * g * g;
-  return w - h.lr_t * m / (sqrtf(v) + a.eps);
+  const OptHyper oh{a.kind, h.lr, a.mom, a.b1, a.b2, a.eps};
+  return opt_step(oh, h.lr_t, w, g * a.grad_scale, m, v);
 }
 
 // Update 4 consecutive elements at flat index i (16-byte aligned).
@@ -91,11 +83,7 @@ __global__ __launch_bounds__(256) void optim_apply_kernel(OptArgs a) {
   const OptSeg s = a.segs[ent.x];
   Hyper h;
   h.lr = a.lr_ptr ? *a.lr_ptr : a.lr;
-  h.lr_t = h.lr;
-  if (a.kind == 3) {
-    const float t = (float)(*a.iterations > 0 ? *a.iterations : 1);
-    h.lr_t = h.lr * sqrtf(1.f - __powf(a.b2, t)) / (1.f - __powf(a.b1, t));
-  }
+  h.lr_t = opt_lr_t(OptHyper{a.kind, h.lr, a.mom, a.b1, a.b2, a.eps}, a.kind == kOptAdam ? *a.iterations : 0);
   const int tid = threadIdx.x;
 
   if (ent.y == 0) {
@@ -186,9 +174,37 @@ __global__ __launch_bounds__(256) void shadow_refresh_kernel(const float* w, bf1
   }
 }
 
+// Deferred-update flush (one workgroup): applies the ranges if *pend (or always when
+// pend is null) with t = *iterations, then clears *pend.
+__global__ __launch_bounds__(256) void flat_apply_kernel(FlatApply f) {
+  __shared__ int go;
+  if (threadIdx.x == 0) go = f.pend ? *f.pend : 1;
+  __syncthreads();
+  if (!go) return;
+  flat_apply(f, f.h.kind == kOptAdam ? *f.iterations : 0, threadIdx.x, 256);
+  __syncthreads();
+  if (threadIdx.x == 0 && f.pend) *f.pend = 0;
+}
+
 }  // namespace tde
 
 using namespace tde;
+
+// ranges: int[2*nr] = {lo0, n0, lo1, n1, ...}
+TDE_API int tde_flat_apply(float* w, float* g, float* m, float* v, const long long* iterations, int* pend,
+                           int kind, float lr, float mom, float b1, float b2, float eps, const int* ranges,
+                           int nr, hipStream_t stream) {
+  if (nr < 0 || nr > kFlatRanges || (kind != kOptSGD && !m) || (kind == kOptAdam && (!v || !iterations)))
+    return -1;
+  FlatApply f{w, g, m, v, iterations, pend, OptHyper{kind, lr, mom, b1, b2, eps}, nr, {0}, {0}};
+  for (int i = 0; i < nr; ++i) {
+    f.lo[i] = ranges[2 * i];
+    f.n[i] = ranges[2 * i + 1];
+  }
+  flat_apply_kernel<<<1, 256, 0, stream>>>(f);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
 
 // Host helper: number of table entries for a segment list (for sizing).
 TDE_API int tde_optim_table_size(const void* segs_host, int nseg) {

@@ -7,11 +7,73 @@ operand shape it does not support (a faulting kernel can reset the node).
 """
 from __future__ import annotations
 
+import ctypes as _ct
+
 import torch
 
 from .. import _native as N
 
 _P = N.ptr
+
+_FLAT_RANGES = 4
+
+
+class OptHyper(_ct.Structure):
+    _fields_ = [("kind", _ct.c_int), ("lr", _ct.c_float), ("mom", _ct.c_float), ("b1", _ct.c_float), ("b2", _ct.c_float),
+                ("eps", _ct.c_float)]
+
+
+class StepOpt(_ct.Structure):
+    """``TdeStepOpt`` (csrc/kernels/convnet.hip): the optimizer of a fused training step."""
+    _fields_ = [("kind", _ct.c_int), ("lr", _ct.c_float), ("mom", _ct.c_float), ("b1", _ct.c_float), ("b2", _ct.c_float),
+                ("eps", _ct.c_float), ("w", _ct.c_void_p), ("g", _ct.c_void_p), ("m", _ct.c_void_p), ("v", _ct.c_void_p),
+                ("iterations", _ct.c_void_p), ("pend", _ct.c_void_p)]
+
+
+class FlatApply(_ct.Structure):
+    """``FlatApply`` (csrc/include/tde_optim.h): an update of element ranges of the flat buffers."""
+    _fields_ = [("w", _ct.c_void_p), ("g", _ct.c_void_p), ("m", _ct.c_void_p), ("v", _ct.c_void_p),
+                ("iterations", _ct.c_void_p), ("pend", _ct.c_void_p), ("h", OptHyper), ("nr", _ct.c_int),
+                ("lo", _ct.c_int * _FLAT_RANGES), ("n", _ct.c_int * _FLAT_RANGES)]
+
+
+class XgApply(_ct.Structure):
+    """``TdeXgApply`` (csrc/comm/xgmi_allreduce.hip): the optimizer fused into the all-reduce."""
+    _fields_ = [("kind", _ct.c_int), ("lr", _ct.c_float), ("mom", _ct.c_float), ("b1", _ct.c_float), ("b2", _ct.c_float),
+                ("eps", _ct.c_float), ("w", _ct.c_void_p), ("m", _ct.c_void_p), ("v", _ct.c_void_p),
+                ("iterations", _ct.c_void_p), ("sh", _ct.c_void_p), ("sh_lo", _ct.c_longlong), ("sh_hi", _ct.c_longlong),
+                ("sht", _ct.c_void_p), ("sh_cols", _ct.c_int), ("sht_ld", _ct.c_longlong)]
+
+
+def step_opt(optimizer, w, g, m, v, iterations, pend):
+    hp = optimizer.hparams()
+    return StepOpt(optimizer.kind_id, float(optimizer.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"],
+                   _P(w), _P(g), _P(m), _P(v), _P(iterations), _P(pend))
+
+
+def flat_apply_spec(optimizer, w, g, m, v, iterations, pend, ranges):
+    """ranges: [(lo, n), ...] element ranges of the flat buffers (<= 4)."""
+    _req(len(ranges) <= _FLAT_RANGES, "flat_apply: at most 4 ranges")
+    hp = optimizer.hparams()
+    f = FlatApply()
+    f.w, f.g, f.m, f.v = _P(w), _P(g), _P(m), _P(v)
+    f.iterations, f.pend = _P(iterations), _P(pend)
+    f.h = OptHyper(optimizer.kind_id, float(optimizer.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"])
+    f.nr = len(ranges)
+    for i, (lo, n) in enumerate(ranges):
+        f.lo[i], f.n[i] = int(lo), int(n)
+    return f
+
+
+def flat_apply(spec: FlatApply):
+    """One-workgroup update of ``spec``'s ranges (skipped while ``*pend == 0``; clears ``*pend``)."""
+    rng = (_ct.c_int * (2 * _FLAT_RANGES))()
+    for i in range(spec.nr):
+        rng[2 * i], rng[2 * i + 1] = spec.lo[i], spec.n[i]
+    h = spec.h
+    rc = N.hip().tde_flat_apply(spec.w, spec.g, spec.m, spec.v, spec.iterations, spec.pend, h.kind, h.lr, h.mom,
+                                h.b1, h.b2, h.eps, rng, spec.nr, _s())
+    N.check(rc, "tde_flat_apply")
 
 
 def _s():
@@ -79,7 +141,9 @@ def conv3x3c1_relu_pool_bwd(x, amax, G, W1, dw, db):
 
 def head_xent(hin, W2, b2, labels, *, B, scale, pre_bias=None, pre_relu=False, compute_grad=True,
               dW2=None, db2=None, dpre_bias=None, G=None, Gt=None, Gf=None, metrics=None,
-              probs=None, probs_are_logits=False, row_loss=None, zero_hin=False, iterations=None, stamps=None):
+              probs=None, probs_are_logits=False, row_loss=None, zero_hin=False, iterations=None, stamps=None,
+              commit: FlatApply | None = None):
+    """Fused head launch; ``commit`` (fused step): block 0 commits that deferred update while ``*pend``."""
     H, C = W2.shape
     _req(hin.dtype == torch.float32 and hin.shape[1] >= H, "head: input")
     _req(C <= 64 and H * C <= 16384, "head: too large for the fused head")
@@ -90,18 +154,26 @@ def head_xent(hin, W2, b2, labels, *, B, scale, pre_bias=None, pre_relu=False, c
     rc = N.hip().tde_head_xent(_P(hin), hin.stride(0), _P(pre_bias), int(pre_relu), _P(W2), _P(b2), _P(labels),
                                B, H, C, float(scale), int(compute_grad), _P(dW2), _P(db2), _P(dpre_bias),
                                _P(G), ldg, _P(Gt), ldgt, _P(Gf), ldgf, _P(metrics), _P(probs),
-                               int(probs_are_logits), _P(row_loss), int(zero_hin), _P(iterations), _P(stamps), _s())
+                               int(probs_are_logits), _P(row_loss), int(zero_hin), _P(iterations), _P(stamps),
+                               _ct.byref(commit) if commit is not None else None, _s())
     N.check(rc, "tde_head_xent")
 
 
-def convnet_fwd(x, wc, bc, W1col, hpre, Pt=None, amax=None, stamps=None):
+def convnet_fwd(x, wc, bc, W1, hpre, Pt=None, amax=None, stamps=None, *, opt: StepOpt | None = None,
+                off_wc=0, off_bc=0):
     """Fused Conv2D(32,3x3,relu)+MaxPool(2)+Dense(64) matmul forward; hpre += (atomic).
 
-    amax: uint8 view of a [P, 4, lda] uint64 buffer (lane-contiguous pool argmax)."""
+    W1: the bf16 Dense(64) kernel shadow, row-major [K, 64] or transposed [64, K].
+    amax: uint8 view of a [P, 4, lda] uint64 buffer (lane-contiguous pool argmax).
+    opt (fused step): while ``*opt.pend`` the conv weights used are the optimizer step of
+    (w, g) at offsets off_wc / off_bc of the flat buffers (the deferred update)."""
     B, H, W = x.shape[0], x.shape[1], x.shape[2]
     Kf = ((H - 2) // 2) * ((W - 2) // 2) * 32
     _req(wc.shape == (3, 3, 1, 32) and bc is not None and bc.numel() == 32, "convnet_fwd: conv must be 3x3x1x32")
-    _req(W1col.shape == (64, Kf) and W1col.stride(0) % 8 == 0 and W1col.dtype == torch.bfloat16, "convnet_fwd: W1col")
+    _req(W1.dtype == torch.bfloat16 and W1.stride(-1) == 1, "convnet_fwd: W1 bf16")
+    rows = tuple(W1.shape) == (Kf, 64)
+    _req(rows and W1.stride(0) == 64 or tuple(W1.shape) == (64, Kf) and W1.stride(0) % 8 == 0,
+         "convnet_fwd: W1 must be [K,64] or [64,K]")
     _req(W % 2 == 0 and x.shape[3] == 1 and x.is_contiguous(), "convnet_fwd: input")
     _req(hpre.shape[0] >= B and hpre.shape[1] == 64 and hpre.is_contiguous(), "convnet_fwd: hpre")
     ldPt = 0
@@ -112,12 +184,17 @@ def convnet_fwd(x, wc, bc, W1col, hpre, Pt=None, amax=None, stamps=None):
     if amax is not None:
         lda = amax.shape[-1]
         _req(amax.dtype == torch.int64 and amax.shape[:2] == (Kf // 32, 4) and lda >= B, "convnet_fwd: amax")
-    rc = N.hip().tde_convnet_fwd(_P(x), _P(wc), _P(bc), _P(W1col), W1col.stride(0), _P(hpre), _P(Pt), ldPt,
-                                 _P(amax), lda, B, H, W, _P(stamps), _s())
+    rc = N.hip().tde_convnet_fwd(_P(x), _P(wc), _P(bc), _P(W1), W1.stride(0), _P(hpre), _P(Pt), ldPt,
+                                 _P(amax), lda, B, H, W, _P(stamps), int(rows),
+                                 _ct.byref(opt) if opt is not None else None, int(off_wc), int(off_bc), _s())
     N.check(rc, "tde_convnet_fwd")
 
 
-def convnet_bwd(x, amax, G, Gt, W1row, Pt, dW1, dwc, dbc, B=None, stamps=None):
+def convnet_bwd(x, amax, G, Gt, W1row, Pt, dW1, dwc, dbc, B=None, stamps=None, *, opt: StepOpt | None = None,
+                off_w1=0, W1col=None, head_ranges=()):
+    """Fused trunk backward.  opt (fused step): instead of storing dW1, the Dense(64) rows at off_w1 of
+    the flat buffers are updated and their bf16 shadows (W1row, and W1col [64, K] if given) rewritten;
+    the last workgroup updates ``head_ranges`` [(lo, n)] and ``*opt.pend`` is set."""
     B = x.shape[0] if B is None else B
     H, W = x.shape[1], x.shape[2]
     Kf = ((H - 2) // 2) * ((W - 2) // 2) * 32
@@ -125,9 +202,17 @@ def convnet_bwd(x, amax, G, Gt, W1row, Pt, dW1, dwc, dbc, B=None, stamps=None):
     _req(W1row.shape == (Kf, 64) and dW1.shape == (Kf, 64) and Pt.shape[0] == Kf, "convnet_bwd: shapes")
     _req(Gt.shape[0] == 64 and Gt.stride(0) >= B and Pt.stride(0) >= B, "convnet_bwd: ld")
     _req(amax.dtype == torch.int64 and amax.shape[:2] == (Kf // 32, 4) and amax.shape[-1] >= B, "convnet_bwd: amax")
+    rng = (_ct.c_int * (2 * _FLAT_RANGES))()
+    if opt is not None:
+        _req(len(head_ranges) <= _FLAT_RANGES and off_w1 % 4 == 0, "convnet_bwd: head ranges / offset")
+        _req(W1col is None or (tuple(W1col.shape) == (64, Kf) and W1col.stride(0) % 4 == 0), "convnet_bwd: W1col")
+        for i, (lo, n) in enumerate(head_ranges):
+            rng[2 * i], rng[2 * i + 1] = int(lo), int(n)
     rc = N.hip().tde_convnet_bwd(_P(x), _P(amax), amax.shape[-1], _P(G), G.stride(0), _P(Gt), Gt.stride(0),
                                  _P(W1row), W1row.stride(0), _P(Pt), Pt.stride(0), _P(dW1), _P(dwc), _P(dbc), B, H,
-                                 W, _P(stamps), _s())
+                                 W, _P(stamps), _ct.byref(opt) if opt is not None else None, int(off_w1),
+                                 _P(W1col), W1col.stride(0) if W1col is not None else 0, rng,
+                                 len(head_ranges) if opt is not None else 0, _s())
     N.check(rc, "tde_convnet_bwd")
 
 

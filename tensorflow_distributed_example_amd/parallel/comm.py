@@ -329,6 +329,22 @@ class XgmiCommunicator(Communicator):
         if rc != 0:
             raise RuntimeError(f"tde_xgmi_all_reduce failed ({rc})")
 
+    def all_reduce_apply_(self, grad, spec):
+        """SUM all-reduce of the flat gradient bucket fused with the optimizer step on every rank
+        (``spec``: ``ops.kernels.XgApply``): weights, slots and the bf16 shadow are updated from the
+        reduced sums and the bucket is left zeroed."""
+        if not self.handles(grad, "sum"):
+            raise ValueError("xGMI fused all-reduce: fp32 contiguous bucket within the window required")
+        import ctypes as C
+        M = grad.numel()
+        with torch.cuda.device(self.device):
+            s = torch.cuda.current_stream(self.device).cuda_stream
+            rc = self.lib.tde_xgmi_all_reduce_apply(grad.data_ptr(), M, self.max_elems, self.peers, self.epoch,
+                                                    self.err, self.rank, self.world, self.nblocks(M), self.uncached,
+                                                    self.timeout_ticks, C.byref(spec), s)
+        if rc != 0:
+            raise RuntimeError(f"tde_xgmi_all_reduce_apply failed ({rc})")
+
     def broadcast_(self, tensors, root=0):
         return self.fallback.broadcast_(tensors, root)
 

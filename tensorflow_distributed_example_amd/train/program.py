@@ -72,6 +72,30 @@ class ReplicaPlan:
     def on_weights_loaded(self):
         pass
 
+    # How the optimizer runs (set by the Program): "plain" — gradients land in the flat bucket and
+    # ``apply()`` runs the multi-tensor optimizer; fused plans may also support "local" (the update
+    # happens inside the step's own kernels; ``finish()`` flushes what is deferred) and "xgmi" (the
+    # communicator's fused all-reduce applies it).
+    step_mode = "plain"
+
+    def supports_step_mode(self, mode):
+        return mode == "plain"
+
+    def set_step_mode(self, mode):
+        if not self.supports_step_mode(mode):
+            raise ValueError(f"{self.kind} plan does not support step mode {mode!r}")
+        self.step_mode = mode
+
+    @property
+    def applies_in_step(self):
+        return self.step_mode == "local"
+
+    def finish(self):
+        """End of an execution (a run of steps): commit deferred updates."""
+
+    def refresh(self):
+        """Before an execution is launched or captured: pick up optimizer hyper-parameter changes."""
+
 
 # ---------------------------------------------------------------------------------------
 def _last_softmax(model, loss):
@@ -295,19 +319,79 @@ class ConvNetPlan(ReplicaPlan):
         n = lambda l, w: f"{l.name}/{w}"  # noqa: E731
         self.names = dict(wc=n(c, "kernel"), bc=n(c, "bias"), w1=n(d1, "kernel"),
                           b1=n(d1, "bias") if d1.use_bias else None, w2=n(d2, "kernel"), b2=n(d2, "bias"))
-        self.opt = OptimizerKernel(store, optimizer, {self.names["w1"]: ("row", "col")}, self.iterations) \
-            if optimizer is not None else None
+        # the forward reads the Dense(64) kernel from the row-major bf16 shadow (the one the backward
+        # reads and the fused updates rewrite); TDE_CONVNET_W1=col keeps a transposed [64, K] copy for it
+        self.w1_rows = os.environ.get("TDE_CONVNET_W1", "rows") != "col"
+        shadows = {self.names["w1"]: ("row",) if self.w1_rows else ("row", "col")}
+        self.opt = OptimizerKernel(store, optimizer, shadows, self.iterations) if optimizer is not None else None
         self._shadow_only = None
         if self.opt is None:
             # eval/predict-only plan still needs the bf16 weight copies
             from ..optimizers import SGD
-            self._shadow_only = OptimizerKernel(store, SGD(0.0), {self.names["w1"]: ("row", "col")}, self.iterations)
+            self._shadow_only = OptimizerKernel(store, SGD(0.0), shadows, self.iterations)
         ok = self.opt or self._shadow_only
         self.W1row = ok.shadow_views[(self.names["w1"], "row")]
-        self.W1col = ok.shadow_views[(self.names["w1"], "col")]
+        self.W1col = None if self.w1_rows else ok.shadow_views[(self.names["w1"], "col")]
+        self.W1fwd = self.W1row if self.w1_rows else self.W1col
+        self.pend = torch.zeros(1, dtype=torch.int32, device=dev)   # deferred conv update outstanding
+        self._sopt = self._commit = None
+
+    # ------------------------------------------------------------------ fused step modes
+    def supports_step_mode(self, mode):
+        if mode == "plain":
+            return True
+        return self.optimizer is not None and self.device.type == "cuda" and mode in ("local", "xgmi")
+
+    def set_step_mode(self, mode):
+        super().set_step_mode(mode)
+        if mode == "plain":
+            self._sopt = self._commit = None
+            return
+        st, opt = self.store, self.optimizer
+        sl = opt.slot_names()
+        m = st.slot(sl[0]) if sl else None
+        v = st.slot(sl[1]) if len(sl) > 1 else None
+        self._slots = (m, v)
+        self._sopt = self.K.step_opt(opt, st.w, st.g, m, v, self.iterations, self.pend)
+        seg = st.segments
+        conv = [(seg[self.names["wc"]].offset, seg[self.names["wc"]].numel),
+                (seg[self.names["bc"]].offset, seg[self.names["bc"]].numel)]
+        # deferred conv update: committed by the next head launch, flushed at the end of an execution
+        self._commit = self.K.flat_apply_spec(opt, st.w, st.g, m, v, self.iterations, self.pend, conv)
+        head = [self.names[k] for k in ("w2", "b2", "b1") if self.names[k] is not None]
+        self._head_ranges = [(seg[h].offset, seg[h].numel) for h in head]
+        self._sopt_key = self._opt_key()
+
+    def _opt_key(self):
+        o = self.optimizer
+        return (o.kind_id, float(o.learning_rate), tuple(sorted(o.hparams().items())))
+
+    def refresh(self):
+        # the kernel argument structs carry lr / hyper-parameters by value
+        if self._sopt is not None and self._sopt_key != self._opt_key():
+            self.set_step_mode(self.step_mode)
+
+    def xg_apply_spec(self):
+        """``XgApply`` for the communicator's fused all-reduce (step mode "xgmi")."""
+        st, opt = self.store, self.optimizer
+        m, v = self._slots
+        hp = opt.hparams()
+        seg = st.segments[self.names["w1"]]
+        K = self.K
+        return K.XgApply(opt.kind_id, float(opt.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"],
+                         K._P(st.w), K._P(m), K._P(v), K._P(self.iterations), K._P(self.W1row), seg.offset,
+                         seg.offset + seg.numel, K._P(self.W1col), self.Hd,
+                         self.W1col.stride(0) if self.W1col is not None else 0)
+
+    def finish(self):
+        if self.step_mode == "local":
+            self.K.flat_apply(self._commit)
 
     def on_weights_loaded(self):
         (self.opt or self._shadow_only).refresh_shadows()
+        # loaded weights replace whatever update was outstanding
+        self.pend.zero_()
+        self.store.g.zero_()
 
     def _v(self, key):
         nm = self.names[key]
@@ -317,27 +401,34 @@ class ConvNetPlan(ReplicaPlan):
         nm = self.names[key]
         return None if nm is None else self.store.grad(nm)
 
-    def _forward(self, x, B, with_pt):
+    def _forward(self, x, B, with_pt, opt=None):
         # kernel 1: conv+bias+ReLU+pool fused with the Dense(Hd) matmul (split-K atomics into hpre,
         # which the previous head launch left zeroed)
-        self.K.convnet_fwd(x[:B], self._v("wc"), self._v("bc"), self.W1col, self.hpre,
-                           self.Pt if with_pt else None, self.amax)
+        seg = self.store.segments
+        self.K.convnet_fwd(x[:B], self._v("wc"), self._v("bc"), self.W1fwd, self.hpre,
+                           self.Pt if with_pt else None, self.amax, opt=opt,
+                           off_wc=seg[self.names["wc"]].offset, off_bc=seg[self.names["bc"]].offset)
 
     def train_step(self, x, y, B=None):
         K = self.K
         B = self.B if B is None else B
-        self._forward(x, B, True)
-        # kernel 2: Dense bias+ReLU, Dense(10), softmax-CE, accuracy and the head backward
+        local = self.step_mode == "local"
+        opt = self._sopt if local else None
+        self._forward(x, B, True, opt)
+        # kernel 2: Dense bias+ReLU, Dense(10), softmax-CE, accuracy and the head backward (fused step:
+        # also commits the previous step's deferred conv update)
         K.head_xent(self.hpre, self._v("w2"), self._v("b2"), y, B=B, scale=self.scale, pre_bias=self._v("b1"),
                     pre_relu=self.pre_relu, compute_grad=True, dW2=self._g("w2"), db2=self._g("b2"),
                     dpre_bias=self._g("b1"), G=self.G, Gt=self.Gt, metrics=self.metrics, zero_hin=True,
-                    iterations=self.iterations)
+                    iterations=self.iterations, commit=self._commit if local else None)
         # kernel 3: Dense weight-grad + Dense input-grad + pool/ReLU routing + conv weight/bias grads
+        # (fused step: the Dense(64) rows and the head variables are updated here)
         K.convnet_bwd(x, self.amax, self.G, self.Gt, self.W1row, self.Pt, self._g("w1"), self._g("wc"),
-                      self._g("bc"), B=B)
+                      self._g("bc"), B=B, opt=opt, off_w1=self.store.segments[self.names["w1"]].offset,
+                      W1col=self.W1col, head_ranges=self._head_ranges if local else ())
 
     def apply(self):
-        # kernel 4: multi-tensor optimizer (+ grad zeroing + bf16 shadow refresh)
+        # kernel 4 (step mode "plain"): multi-tensor optimizer (+ grad zeroing + bf16 shadow refresh)
         self.opt.apply()
 
     def eval_step(self, x, y, B=None):

@@ -108,6 +108,23 @@ class Program:
         self._dbg = os.environ.get("TDE_DEBUG_SYNC", "0") not in ("", "0") and cuda
         self.buckets = self._plan_buckets() if training else None
         self._comm_stream = torch.cuda.Stream(self.devices[0]) if self.buckets else None
+        self.comm_applies = False
+        if training:
+            self._pick_step_mode()
+
+    def _pick_step_mode(self):
+        """Fused optimizer placement (TDE_FUSED_STEP=0 keeps the separate optimizer launch): with one
+        replica the update runs inside the step's own kernels ("local"); with one replica per process
+        under the xGMI communicator it runs inside the gradient all-reduce ("xgmi")."""
+        if os.environ.get("TDE_FUSED_STEP", "1") == "0" or len(self.plans) != 1 or self.buckets:
+            return
+        plan = self.plans[0]
+        from ..parallel.comm import XgmiCommunicator
+        if self.comm is None and plan.supports_step_mode("local"):
+            plan.set_step_mode("local")
+        elif isinstance(self.comm, XgmiCommunicator) and plan.supports_step_mode("xgmi"):
+            plan.set_step_mode("xgmi")
+            self.comm_applies = True
 
     def _plan_buckets(self):
         """Reverse-order gradient buckets all-reduced on a comm stream while backward still runs
@@ -137,6 +154,29 @@ class Program:
                 self.y_stage[r].stage(y, self.y_ring[r])
 
     # ------------------------------------------------------------------ training
+    def _reduce_and_apply(self):
+        """Gradient all-reduce + optimizer of every local replica (after their backward)."""
+        if self.comm_applies:
+            plan = self.plans[0]
+            with _ctx(plan.device):
+                self.comm.all_reduce_apply_(plan.store.g, plan.xg_apply_spec())
+            self._debug_sync("gradient all-reduce + optimizer")
+            return
+        if self.comm is not None:
+            self.comm.all_reduce_([p.store.g for p in self.plans])
+            self._debug_sync("gradient all-reduce")
+        for plan in self.plans:
+            if plan.applies_in_step:
+                continue
+            with _ctx(plan.device):
+                plan.apply()
+            self._debug_sync("optimizer")
+
+    def _finish(self):
+        for plan in self.plans:
+            with _ctx(plan.device):
+                plan.finish()
+
     def _steps(self, S, B=None):
         for s in range(S):
             if self.buckets:
@@ -146,13 +186,8 @@ class Program:
                 with _ctx(plan.device):
                     plan.train_step(self.x_ring[r][s], self.y_ring[r][s], B)
                 self._debug_sync("train_step")
-            if self.comm is not None:
-                self.comm.all_reduce_([p.store.g for p in self.plans])
-                self._debug_sync("gradient all-reduce")
-            for plan in self.plans:
-                with _ctx(plan.device):
-                    plan.apply()
-                self._debug_sync("optimizer")
+            self._reduce_and_apply()
+        self._finish()
 
     def _overlapped_step(self, s, B):
         """fwd + bwd on the compute stream; each gradient bucket's all-reduce is enqueued on the comm
@@ -199,13 +234,23 @@ class Program:
         return (float(self.model.optimizer.learning_rate), self.model.optimizer.kind)
 
     def capture(self):
+        import gc
         self._warm_comm()
+        for p in self.plans:
+            p.refresh()
         dev = self.devices[0]
         with torch.cuda.device(dev):
             torch.cuda.synchronize(dev)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._steps(self.S)
+            # no garbage collection while capturing: finalizers of unrelated dead objects (graphs,
+            # events, device buffers of earlier programs) must not run inside the capture
+            gc.collect()
+            gc.disable()
+            try:
+                with torch.cuda.graph(g):
+                    self._steps(self.S)
+            finally:
+                gc.enable()
             torch.cuda.synchronize(dev)
         self.graph = g
         self._graph_key = self._key()
@@ -229,6 +274,8 @@ class Program:
                 self.graph.replay()
         else:
             self._warm_comm()
+            for p in self.plans:
+                p.refresh()
             self._steps(self.S)
 
     def run_single(self, per_replica, global_actual):
@@ -239,6 +286,8 @@ class Program:
                 n = len(y)
                 self.x_stage[r].stage(x, self.x_ring[r][0])
                 self.y_stage[r].stage(y, self.y_ring[r][0])
+        for p in self.plans:
+            p.refresh()
         scales = [p.scale for p in self.plans]
         for p in self.plans:
             p.scale = 1.0 / float(global_actual)
@@ -259,11 +308,10 @@ class Program:
                 with _ctx(plan.device):
                     if n > 0:
                         plan.train_step(self.x_ring[r][0], self.y_ring[r][0], n)
-            if self.comm is not None:
-                self.comm.all_reduce_([p.store.g for p in self.plans])
-            for plan in self.plans:
-                with _ctx(plan.device):
-                    plan.apply()
+                    elif plan.applies_in_step:
+                        continue   # no data, nothing to reduce: the fused step has no update to make
+            self._reduce_and_apply()
+            self._finish()
         finally:
             for p, s in zip(self.plans, scales):
                 p.scale = s

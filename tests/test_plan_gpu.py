@@ -154,3 +154,78 @@ def test_loss_decreases_and_eval_predict():
     assert p.shape == (37, 10)
     torch_logits = m(xe[:37]).cpu().numpy()
     assert np.allclose(p, torch_logits, atol=5e-2, rtol=5e-2)
+
+
+def _opt(tde, kind):
+    O = tde.optimizers
+    return {"sgd": lambda: O.SGD(0.05), "momentum": lambda: O.SGD(0.05, momentum=0.9),
+            "nesterov": lambda: O.SGD(0.05, momentum=0.9, nesterov=True), "adam": lambda: O.Adam(2e-3)}[kind]()
+
+
+@pytest.mark.parametrize("kind,w1", [("sgd", "rows"), ("momentum", "rows"), ("nesterov", "rows"), ("adam", "rows"),
+                                     ("sgd", "col"), ("adam", "col")])
+def test_fused_local_step_matches_plain(kind, w1, monkeypatch):
+    """Step mode "local" (the optimizer inside fwd / head / bwd, the conv update deferred to the next
+    forward + head and flushed at the end) vs the separate optimizer launch, over three steps from the
+    same weights: every variable's update and the optimizer slots agree (bf16 shadow roundings aside)."""
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.train import program as PG
+    monkeypatch.setenv("TDE_CONVNET_W1", w1)
+    m = tde.zoo.mnist_cnn()
+    m.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True), optimizer=_opt(tde, kind),
+              metrics=["accuracy"])
+    m.build()
+    st = m._store
+    st2 = st.clone_to("cuda")
+    w0 = {n: st.view(n).detach().clone() for n in st.names(trainable=True)}
+    plain = PG.make_plan(m, st2, "cuda", 64, 64, m.optimizer, m.loss)
+    local = PG.make_plan(m, st, "cuda", 64, 64, m.optimizer, m.loss)
+    local.set_step_mode("local")
+    assert local.applies_in_step and not plain.applies_in_step
+    for s in range(3):
+        x, y = _data(64, 10 + s)
+        xt, yt = torch.from_numpy(x).cuda(), torch.from_numpy(y).int().cuda()
+        plain.train_step(xt, yt)
+        plain.apply()
+        local.train_step(xt, yt)
+    local.finish()
+    torch.cuda.synchronize()
+    assert int(local.pend.item()) == 0 and float(st.g.abs().max()) == 0.0
+    for n in st.names(trainable=True):
+        da, db = st.view(n).double() - w0[n].double(), st2.view(n).double() - w0[n].double()
+        rel = ((da - db).norm() / (db.norm() + 1e-12)).item()
+        assert rel < 2e-2, (kind, n, rel)
+    for sname in m.optimizer.slot_names():
+        a, b = st.slot(sname).double(), st2.slot(sname).double()
+        assert ((a - b).norm() / (b.norm() + 1e-12)).item() < 2e-2, sname
+    # the shadow the forward reads is the bf16 of the updated fp32 weights
+    w1 = st.view(local.names["w1"])
+    assert torch.equal(local.W1row, w1.to(torch.bfloat16))
+    if local.W1col is not None:
+        assert torch.equal(local.W1col, w1.t().to(torch.bfloat16))
+
+
+def test_fused_local_fit_matches_plain(monkeypatch):
+    """fit() with hipGraph executions of 3 steps and a final partial batch (eager run_single): the fused
+    single-replica step vs TDE_FUSED_STEP=0."""
+    import tensorflow_distributed_example_amd as tde
+    x, y = _data(64 * 6 + 17, 2)
+    tde.backend.set_random_seed(5)
+    ma = tde.zoo.mnist_cnn()
+    ma.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True),
+               optimizer=tde.optimizers.SGD(0.05, momentum=0.9), metrics=["accuracy"], steps_per_execution=3)
+    w0 = ma.get_weights()
+    ha = ma.fit(x, y, batch_size=64, epochs=1, shuffle=False, verbose=0)
+    assert ma._program("train", 64).plans[0].step_mode == "local"
+    tde.backend.clear_session()
+    monkeypatch.setenv("TDE_FUSED_STEP", "0")
+    mb = tde.zoo.mnist_cnn()
+    mb.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True),
+               optimizer=tde.optimizers.SGD(0.05, momentum=0.9), metrics=["accuracy"], steps_per_execution=3)
+    mb.set_weights(w0)
+    hb = mb.fit(x, y, batch_size=64, epochs=1, shuffle=False, verbose=0)
+    assert mb._program("train", 64).plans[0].step_mode == "plain"
+    for a, b, w in zip(ma.get_weights(), mb.get_weights(), w0):
+        rel = np.linalg.norm((a - w) - (b - w)) / (np.linalg.norm(b - w) + 1e-12)
+        assert rel < 5e-2, rel
+    assert abs(ha.history["loss"][0] - hb.history["loss"][0]) < 1e-2

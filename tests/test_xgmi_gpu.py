@@ -213,3 +213,107 @@ def test_rccl_init_failure_falls_back_on_every_rank():
     res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert res["config"]["allreduce"] == "xgmi", res
     assert "replicas_identical=True" in r.stdout
+
+
+APPLY = r"""
+import json, os, sys
+sys.path.insert(0, {root!r})
+import torch, torch.distributed as dist
+from tensorflow_distributed_example_amd.parallel import comm as CM
+from tensorflow_distributed_example_amd.ops import kernels as K
+from tensorflow_distributed_example_amd import optimizers as O
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+torch.cuda.set_device(0)
+dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+xg = CM.XgmiCommunicator("cuda:0", rank, world, CM.TorchDistCommunicator(1), max_elems=1 << 20, timeout_s=30)
+out = {{}}
+n, lo, rows, cols = 347146 + 58, 64, 5408, 64
+opts = {{"sgd": O.SGD(0.05), "momentum": O.SGD(0.05, momentum=0.9),
+         "nesterov": O.SGD(0.05, momentum=0.9, nesterov=True), "adam": O.Adam(1e-3)}}
+for name, opt in opts.items():
+    g = torch.Generator(device="cpu").manual_seed(7)
+    w = torch.randn(n, generator=g).cuda()
+    m = torch.randn(n, generator=g).cuda() if opt.kind != "sgd" else None
+    v = torch.rand(n, generator=g).cuda() if opt.kind == "adam" else None
+    it = torch.full((1,), 3, dtype=torch.int64, device="cuda")
+    grads = [torch.randn(n, generator=torch.Generator().manual_seed(100 + r)).cuda() for r in range(world)]
+    gsum = grads[0].clone()
+    for q in grads[1:]:
+        gsum += q
+    rw, rm, rv = w.clone(), None if m is None else m.clone(), None if v is None else v.clone()
+    slots = {{}}
+    if opt.kind in ("momentum", "nesterov"):
+        slots["momentum"] = rm
+    if opt.kind == "adam":
+        slots["m"], slots["v"] = rm, rv
+    opt.apply_reference(rw, gsum, slots, 2)   # Adam t = step + 1 = 3 = iterations
+    sh = torch.zeros(rows * cols, dtype=torch.bfloat16, device="cuda")
+    sht = torch.zeros(cols, rows, dtype=torch.bfloat16, device="cuda")
+    hp = opt.hparams()
+    spec = K.XgApply(opt.kind_id, opt.learning_rate, hp["mom"], hp["b1"], hp["b2"], hp["eps"], w.data_ptr(),
+                     K._P(m), K._P(v), it.data_ptr(), sh.data_ptr(), lo, lo + rows * cols, sht.data_ptr(), cols,
+                     rows)
+    gb = grads[rank].clone()
+    xg.all_reduce_apply_(gb, spec)
+    torch.cuda.synchronize()
+    rel = float((w - rw).norm() / (rw.norm()))
+    res = {{"w_rel": rel, "w_max": float((w - rw).abs().max()), "grad_zero": bool((gb == 0).all()),
+           "sh_ok": bool(torch.equal(sh, w[lo:lo + rows * cols].to(torch.bfloat16))),
+           "sht_ok": bool(torch.equal(sht, w[lo:lo + rows * cols].view(rows, cols).t().to(torch.bfloat16)))}}
+    if m is not None:
+        res["m_max"] = float((m - rm).abs().max())
+    if v is not None:
+        res["v_max"] = float((v - rv).abs().max())
+    # every rank must hold bit-identical weights
+    allw = [torch.zeros_like(w).cpu() for _ in range(world)]
+    dist.all_gather(allw, w.cpu())
+    res["identical"] = all(torch.equal(allw[0], q) for q in allw[1:])
+    out[name] = res
+out["err"] = int(xg.lib.tde_xgmi_error(xg.err))
+dist.barrier()
+xg.close()
+print("RESULT" + json.dumps(out), flush=True)
+"""
+
+
+def test_xgmi_allreduce_apply_matches_reference():
+    """The fused all-reduce + optimizer (every kind) against the fp32 torch update of the rank-ordered
+    gradient sum: weights, slots, bf16 shadows (row-major and transposed), zeroed bucket, and all ranks
+    bit-identical."""
+    world = 2
+    port = _free_port()
+    script = APPLY.format(root=ROOT, port=port)
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), OMP_NUM_THREADS="2")
+        procs.append(subprocess.Popen([sys.executable, "-c", script], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    for p in procs:
+        o, _ = p.communicate(timeout=240)
+        assert p.returncode == 0, o[-4000:]
+        res = json.loads(o.split("RESULT")[1].strip())
+        assert res.pop("err") == 0, res
+        for name, r in res.items():
+            assert r["w_max"] < 1e-5 and r["grad_zero"] and r["sh_ok"] and r["sht_ok"] and r["identical"], (name, r)
+            assert r.get("m_max", 0.0) < 1e-5 and r.get("v_max", 0.0) < 1e-5, (name, r)
+
+
+def test_mwms_fused_allreduce_apply_matches_unfused():
+    """bench.py with 2 ranks: the optimizer fused into the xGMI all-reduce (default) vs the separate
+    optimizer launch (TDE_FUSED_STEP=0): replicas bit-identical in both, same training trajectory."""
+    losses = {}
+    for fused in ("1", "0"):
+        env = dict(os.environ, TDE_RCCL="0", TDE_ALLREDUCE="xgmi", TDE_HEARTBEAT="0", OMP_NUM_THREADS="2",
+                   TDE_FUSED_STEP=fused)
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+               "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
+               "--gpus", "2", "--steps", "48", "--warmup", "16", "--lr", "0.05"]
+        r = subprocess.run(cmd, env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stdout[-4000:]
+        res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+        assert res["config"]["allreduce"] == "xgmi" and res["config"]["hipgraph"] is True, res
+        assert res["config"]["optimizer_placement"] == ("allreduce" if fused == "1" else "separate"), res
+        assert "replicas_identical=True" in r.stdout, r.stdout[-3000:]
+        losses[fused] = float(r.stdout.split("loss=")[1].split()[0])
+    assert abs(losses["1"] - losses["0"]) < 0.02 * max(1.0, abs(losses["0"])), losses
