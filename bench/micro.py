@@ -89,47 +89,47 @@ def main():
     y = torch.randint(0, 10, (64,), device="cuda", dtype=torch.int32)
 
     def k_fwd(stamps=None):
-        plan._forward(x, 64, True, plan._sopt if plan.step_mode == "local" else None) if stamps is None else \
-            K.convnet_fwd(x, plan._v("wc"), plan._v("bc"), plan.W1fwd, plan.hpre, plan.Pt, plan.amax, stamps=stamps)
-
-    def k_head(stamps=None):
-        K.head_xent(plan.hpre, plan._v("w2"), plan._v("b2"), y, B=64, scale=plan.scale, pre_bias=plan._v("b1"),
-                    pre_relu=True, compute_grad=True, dW2=plan._g("w2"), db2=plan._g("b2"), dpre_bias=plan._g("b1"),
-                    G=plan.G, Gt=plan.Gt, metrics=plan.metrics, zero_hin=True, iterations=plan.iterations,
-                    stamps=stamps, commit=plan._commit if plan.step_mode == "local" else None)
+        q = plan.parity
+        local = plan.step_mode == "local"
+        K.convnet_fwd(x, plan._v("wc"), plan._v("bc"), plan.W1fwd, plan.hpre2[q], plan.Pt, plan.amax, stamps=stamps,
+                      opt=plan._fopt[q] if local else None,
+                      off_wc=plan.store.segments[plan.names["wc"]].offset,
+                      off_bc=plan.store.segments[plan.names["bc"]].offset, inc_iter=plan.iterations)
 
     def k_bwd(stamps=None):
+        q = plan.parity
         local = plan.step_mode == "local"
-        K.convnet_bwd(x, plan.amax, plan.G, plan.Gt, plan.W1row, plan.Pt, plan._g("w1"), plan._g("wc"),
-                      plan._g("bc"), B=64, stamps=stamps, opt=plan._sopt if local else None,
-                      off_w1=plan.store.segments[plan.names["w1"]].offset, W1col=plan.W1col,
-                      head_ranges=plan._head_ranges if local else ())
+        dwc, dbc = plan._gconv_views(q) if local else (plan._g("wc"), plan._g("bc"))
+        K.convnet_bwd(x, plan.amax, plan.hpre2[q], plan.hpre2[1 - q], plan._v("b1"), plan._v("w2"), plan._v("b2"), y,
+                      scale=plan.scale, pre_relu=True, metrics=plan.metrics, W1row=plan.W1row, Pt=plan.Pt,
+                      dW1=plan._g("w1"), dwc=dwc, dbc=dbc, dW2=plan._g("w2"), db2=plan._g("b2"), db1=plan._g("b1"),
+                      B=64, stamps=stamps, opt=plan._bopt[q] if local else None)
 
     def k_opt():
         plan.opt.apply()
 
     def step():
-        k_fwd(); k_head(); k_bwd(); k_opt()
+        plan.train_step(x, y)
+        plan.apply()
 
     def step_local():
-        k_fwd(); k_head(); k_bwd()
+        plan.train_step(x, y)
 
     plan.set_step_mode("plain")
     out["w1_source"] = "rows" if plan.w1_rows else "col"
     out["kernel_graph_us"] = {n: graph_time(f) for n, f in
-                              [("convnet_fwd", k_fwd), ("head", k_head), ("convnet_bwd", k_bwd), ("optim", k_opt)]}
+                              [("convnet_fwd", k_fwd), ("convnet_bwd_head", k_bwd), ("optim", k_opt)]}
     out["step_graph_us"] = graph_time(step, reps=100)
     out["step_eager_us"] = eager_time(step, reps=200)
-    # fused single-replica step: the optimizer inside fwd / head / bwd, one flush per execution
+    # fused single-replica step: the optimizer inside the two launches, one flush per execution
     plan.set_step_mode("local")
     out["local_kernel_graph_us"] = {n: graph_time(f) for n, f in
-                                    [("convnet_fwd", k_fwd), ("head", k_head), ("convnet_bwd", k_bwd),
-                                     ("flush", plan.finish)]}
+                                    [("convnet_fwd", k_fwd), ("convnet_bwd_head", k_bwd), ("flush", plan.finish)]}
     out["local_step_graph_us"] = graph_time(step_local, reps=100)
     plan.finish()
     plan.set_step_mode("plain")
     st = torch.zeros(4096 * 8, dtype=torch.int64, device="cuda")
-    for name, f, ns in [("convnet_fwd", k_fwd, 5), ("head", k_head, 4), ("convnet_bwd", k_bwd, 6)]:
+    for name, f, ns in [("convnet_fwd", k_fwd, 5), ("convnet_bwd_head", k_bwd, 6)]:
         st.zero_()
         f()
         torch.cuda.synchronize()

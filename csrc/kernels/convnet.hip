@@ -63,6 +63,7 @@ struct ConvNetFwdArgs {
   const float *gwc, *gbc, *mwc, *mbc, *vwc, *vbc;
   const long long* iterations;
   OptHyper h;
+  unsigned long long* inc_iter;      // training: block 0 advances the step counter (nullable)
 };
 
 // The input rows a workgroup's PPW positions touch (<= XR rows of <= XW floats per
@@ -87,6 +88,8 @@ __global__ __launch_bounds__(FPW * 256) void convnet_fwd_kernel(ConvNetFwdArgs a
   float* xr = reinterpret_cast<float*>(fsm + FPW * 64 * PSTR * 2);  // [64][XR][W]
   float* wcs = reinterpret_cast<float*>(fsm + FPW * 64 * PSTR * 2 + 64 * (XR * XW + 64) * 4);  // [10][CC]
   stamp(a.stamps, 0);
+  // Keras optimizer.iterations: advanced here, read (stable) by this step's backward / optimizer
+  if (a.inc_iter && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicAdd(a.inc_iter, 1ull);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fk = (lane >> 4) * 8;
   const int W = a.W, H = a.H;
@@ -252,25 +255,43 @@ __global__ __launch_bounds__(FPW * 256) void convnet_fwd_kernel(ConvNetFwdArgs a
   stamp(a.stamps, 4);
 }
 
+// Backward of the trunk with the classifier head fused in (the head is
+// the same math as head.hip):  per 64-image chunk every workgroup recomputes the head from the
+// Dense(64) pre-activation (16 KB f32): h = ReLU(hpre + b1) -> logits = h . W2 + b2 (exact f32
+// MFMA) -> softmax-CE -> dl = (p - onehot) * scale -> G = dl . W2^T masked by h > 0, straight into
+// LDS — the Dense(64) input gradient every workgroup needs anyway.  The recompute costs about a
+// microsecond of MFMA/LDS work per workgroup and removes a launch and its boundary.  ONE workgroup
+// (the last: it owns a single pooled position) also produces the head's side outputs — loss and
+// accuracy, dW2 = h^T . dl, db2, db1 (complete sums, no atomics) — and stores them or, in the fused
+// step, applies the update to them.
+// hpre is double-buffered by step parity: this launch reads hpre[p] and zeroes hpre[1-p] (read by
+// the previous step's backward, accumulated into by the next forward): no in-kernel hand-off.
 struct ConvNetBwdArgs {
   const float* x; const uint64_t* amax; int lda;
-  const bf16* G; int ldg;            // [B][HD] bf16 (dHpre)
-  const bf16* Gt; int ldgt;          // [HD][ldgt] bf16
+  const float* hpre;                 // [B][HD] f32 Dense(64) pre-activation (this step's parity)
+  float* hzero;                      // [B][HD] the other parity buffer, zeroed here
+  const float* b1; const float* W2; const float* b2; int C; int pre_relu;
+  const int* labels;
+  float scale;                       // 1 / global batch (Keras AUTO reduction under a strategy)
+  float* metrics;                    // += {loss_sum, correct, count}
   const bf16* W1r; int ldw1r;        // [K][HD] bf16 (row-major shadow)
   const bf16* Pt; int ldPt;          // [K][ldPt] bf16
-  float* dW1;                        // [K][HD] f32 (stored; unused when apply)
+  float* dW1;                        // [K][HD] f32 (MODE 0: stored)
   float* dwc; float* dbc;            // [9][CC], [CC] (atomic +=)
+  float *dW2, *db2, *db1;            // MODE 0: head gradients (+= by the head workgroup)
   int B, H, W;
   long long* stamps;
-  // fused step: update the Dense(64) kernel rows here instead of storing dW1
-  int apply;
+  // fused step (MODE != 0)
   float *w1, *m1, *v1;               // fp32 master [K][HD] (+ slots), updated in place
   bf16* w1r_out;                     // row-major bf16 shadow (== W1r), rewritten
   bf16* w1c_out; int ldw1c;          // transposed bf16 shadow [HD][ldw1c] (nullable)
-  const long long* iterations;
+  float *hw, *hm, *hv;               // flat weight / slot buffers (head variables at the offsets below)
+  long long off_w2, off_b2, off_b1;  // off_b1 < 0: the Dense(64) has no bias
+  const long long* iterations;       // t of this step (advanced by this step's forward)
+  long long* iter_prev;              // := t by the head workgroup (read by the next forward)
   OptHyper h;
-  FlatApply head;                    // applied by the last workgroup (head variables), nr = 0: none
-  int* pend;                         // set to 1: the conv update is pending (nullable)
+  FlatApply commit;                  // the previous step's deferred conv update (workgroup 0, while *pend)
+  int* pend_set;                     // := 1: this step's conv update is deferred
 };
 
 // Up to NPER elements per thread of a FlatApply's ranges, loaded early into registers and
@@ -313,28 +334,6 @@ struct FlatPrefetch {
   }
 };
 
-// Elements [start, total) of a FlatApply's ranges, threads tid, tid + nt, ... (no prefetch).
-__device__ __forceinline__ void flat_apply_from(const FlatApply& f, long long t, int start, int tid, int nt) {
-  int total = 0;
-  for (int r = 0; r < f.nr; ++r) total += f.n[r];
-  const float lr_t = opt_lr_t(f.h, t);
-  for (int idx0 = start + tid; idx0 < total; idx0 += nt) {
-    int idx = idx0, e = -1;
-    for (int r = 0; r < f.nr; ++r) {
-      if (idx < f.n[r]) {
-        e = f.lo[r] + idx;
-        break;
-      }
-      idx -= f.n[r];
-    }
-    float m = f.h.kind != kOptSGD ? f.m[e] : 0.f, v = f.h.kind == kOptAdam ? f.v[e] : 0.f;
-    f.w[e] = opt_step(f.h, lr_t, f.w[e], f.g[e], m, v);
-    f.g[e] = 0.f;
-    if (f.h.kind != kOptSGD) f.m[e] = m;
-    if (f.h.kind == kOptAdam) f.v[e] = v;
-  }
-}
-
 // LDS carve (bytes)
 constexpr int kG = 0;                                   // bf16 [64][RSTR]
 constexpr int kW1 = kG + 64 * RSTR * 2;                 // bf16 [128][RSTR]
@@ -342,13 +341,226 @@ constexpr int kPt = kW1 + 128 * RSTR * 2;               // bf16 [128][RSTR]
 constexpr int kGt = kPt + 128 * RSTR * 2;               // bf16 [64][RSTR]
 constexpr int kXs = kGt + 64 * RSTR * 2;                // f32  [PPW][64][16]
 constexpr int kAm = kXs + PPW * 64 * 16 * 4;            // u8   [PPW][64][CC]
-constexpr int kDp = kAm + PPW * 64 * CC;                // f32  [PPW][64][DPS] (reused as red [NW][16][CC])
+constexpr int kDp = kAm + PPW * 64 * CC;                // f32  [PPW][64][DPS] (head scratch; red [NW][16][CC])
 // dP row stride: 40 floats puts the 4 lane groups of the routing reads (rows 2 apart) on disjoint
 // bank quarters (stride 32 made them 4-way LDS bank conflicts)
 constexpr int DPS = 40;
-constexpr int kBwdLds = kDp + PPW * 64 * DPS * 4;
+constexpr int kW2s = kDp + PPW * 64 * DPS * 4;          // f32  [HD][16] W2, classes padded to 16
+constexpr int kB2s = kW2s + HD * 16 * 4;                // f32  [16]
+constexpr int kLab = kB2s + 16 * 4;                     // i32  [64]
+constexpr int kBwdLds = kLab + 64 * 4;
+// head scratch inside the dP area (dead during the head phase of a chunk)
+constexpr int HS = HD + 4;                              // f32 row stride of h
+constexpr int kHs = 0, kPart = kHs + 64 * HS * 4, kDl = kPart + 12 * 64 * 4 * 4;
+static_assert(kDl + 64 * 16 * 4 <= PPW * 64 * DPS * 4, "head scratch exceeds the dP area");
 
-// MODE 0: store dW1; 1: fused step, SGD; 2: fused step, optimizer with slots (momentum / Adam)
+__device__ __forceinline__ f32x4 mfma_f32x4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// ---- head pieces shared by the trunk workgroups and the head workgroup (16 waves, 64 rows)
+
+// h = act(hpre + b1) of this thread's row / 4 units into LDS (rows past nb zeroed)
+__device__ __forceinline__ void head_stage(const ConvNetBwdArgs& a, float4 hv, float4 b1v, int hr, int hc4, int nb,
+                                           float* hs) {
+  float4 h = float4{hv.x + b1v.x, hv.y + b1v.y, hv.z + b1v.z, hv.w + b1v.w};
+  if (a.pre_relu) h = float4{fmaxf(h.x, 0.f), fmaxf(h.y, 0.f), fmaxf(h.z, 0.f), fmaxf(h.w, 0.f)};
+  if (hr >= nb) h = float4{0.f, 0.f, 0.f, 0.f};
+  *reinterpret_cast<float4*>(hs + hr * HS + hc4) = h;
+}
+
+// logits = h . W2 + b2 (exact f32 MFMA; wave = 16-row tile x K quarter), softmax-CE on waves 0..3
+// -> dls = dlogits [64][16]; loss / correct / count accumulated into la / ca / na (lanes fr == 0).
+// Entered after a barrier that published hs / labs; ends with a barrier that publishes dls.
+__device__ __forceinline__ void head_logits_ce(const ConvNetBwdArgs& a, int nb, const float* hs, float* part,
+                                               float* dls, const float* w2s, const float* b2s, const int* labs,
+                                               int lane, int wave, float& la, float& ca, float& na) {
+  const int fr = lane & 15, fq = lane >> 4, C = a.C;
+  f32x4 lg = {0.f, 0.f, 0.f, 0.f};
+  {
+    const int rt = wave & 3, kq = wave >> 2;
+#pragma unroll
+    for (int k = kq * 16; k < kq * 16 + 16; k += 4)
+      lg = mfma_f32x4(hs[(rt * 16 + fr) * HS + k + fq], w2s[(k + fq) * 16 + fr], lg);
+    if (kq > 0) *reinterpret_cast<f32x4*>(part + (((kq - 1) * 4 + rt) * 64 + lane) * 4) = lg;
+  }
+  lds_barrier();
+  if (wave < 4) {
+    const int rt = wave;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const f32x4 pv = *reinterpret_cast<const f32x4*>(part + ((q * 4 + rt) * 64 + lane) * 4);
+      lg[0] += pv[0]; lg[1] += pv[1]; lg[2] += pv[2]; lg[3] += pv[3];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = rt * 16 + fq * 4 + i;
+      const bool valid = r < nb;
+      const bool cv = fr < C;
+      const float z = cv ? lg[i] + b2s[fr] : -3.0e38f;
+      const float m = row16_max(z);
+      const float e = cv ? __expf(z - m) : 0.f;
+      const float s = row16_sum(e);
+      const float pr = e / s;
+      const int label = labs[r];
+      const int amx = row16_min(cv && z == m ? fr : 64);
+      const float zl = __shfl(z, (lane & ~15) | (label & 15), 64);
+      if (valid && fr == 0) {
+        la += __logf(s) + m - zl;
+        ca += (amx == label) ? 1.f : 0.f;
+        na += 1.f;
+      }
+      dls[r * 16 + fr] = (valid && cv) ? (pr - (fr == label ? 1.f : 0.f)) * a.scale : 0.f;
+    }
+  }
+  lds_barrier();
+}
+
+// dH tile of this wave (rows rt*16.., units ut*16.., rt = wave>>2, ut = wave&3) = dl . W2^T, masked
+// by h > 0 and rows < nb.  Lane holds dH[rt*16 + 4fq + i][ut*16 + fr].
+__device__ __forceinline__ f32x4 head_dh(const ConvNetBwdArgs& a, int nb, const float* hs, const float* dls,
+                                         const float* w2s, int lane, int wave) {
+  const int fr = lane & 15, fq = lane >> 4, rt = wave >> 2, ut = wave & 3;
+  f32x4 gh = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 16; k += 4)
+    gh = mfma_f32x4(dls[(rt * 16 + fr) * 16 + k + fq], w2s[(ut * 16 + fr) * 16 + k + fq], gh);
+  const int j = ut * 16 + fr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = rt * 16 + fq * 4 + i;
+    if ((a.pre_relu && !(hs[r * HS + j] > 0.f)) || r >= nb) gh[i] = 0.f;
+  }
+  return gh;
+}
+
+// The head workgroup: loss / accuracy, dW2 = h^T . dl, db2, db1 over all chunks, then stored (MODE 0)
+// or updated (fused step; with the previous step's deferred conv update and the flags).
+template <int MODE>
+__device__ __forceinline__ void head_workgroup(const ConvNetBwdArgs& a, unsigned char* smem) {
+  float* hs = reinterpret_cast<float*>(smem + kDp + kHs);
+  float* part = reinterpret_cast<float*>(smem + kDp + kPart);
+  float* dls = reinterpret_cast<float*>(smem + kDp + kDl);
+  float* w2s = reinterpret_cast<float*>(smem + kW2s);
+  float* b2s = reinterpret_cast<float*>(smem + kB2s);
+  int* labs = reinterpret_cast<int*>(smem + kLab);
+  float* db1p = reinterpret_cast<float*>(smem + kG);   // [4][64] (the trunk's G area is unused here)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+  const int fr = lane & 15, fq = lane >> 4, C = a.C;
+  const int hr = tid >> 4, hc4 = (tid & 15) * 4;
+  const float4 b1v = a.b1 ? *reinterpret_cast<const float4*>(a.b1 + hc4) : float4{0.f, 0.f, 0.f, 0.f};
+
+  // fused step: the variables this workgroup updates, loaded now.  waves 0..3: W2[wave*16 + 4fq + i][fr]
+  // (the dW2 tile layout); wave 4: b2[fr]; wave 5: b1[lane]
+  long long e[4] = {-1, -1, -1, -1};
+  if (wave < 4 && fr < C) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) e[i] = a.off_w2 + (long long)(wave * 16 + fq * 4 + i) * C + fr;
+  } else if (wave == 4 && fq == 0 && fr < C) {
+    e[0] = a.off_b2 + fr;
+  } else if (wave == 5 && a.off_b1 >= 0) {
+    e[0] = a.off_b1 + lane;
+  }
+  float hwv[4] = {0.f, 0.f, 0.f, 0.f}, hmv[4] = {0.f, 0.f, 0.f, 0.f}, hvv[4] = {0.f, 0.f, 0.f, 0.f};
+  long long t_it = 0;
+  FlatPrefetch<1> cp;
+  int cpend = 0;
+  if (MODE != 0) {
+    t_it = *a.iterations;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (e[i] < 0) continue;
+      hwv[i] = a.hw[e[i]];
+      if (MODE == 2 && a.h.kind != kOptSGD) hmv[i] = a.hm[e[i]];
+      if (MODE == 2 && a.h.kind == kOptAdam) hvv[i] = a.hv[e[i]];
+    }
+    if (a.commit.nr > 0) {
+      cpend = *a.commit.pend;
+      cp.load(a.commit, tid, 1024);
+    }
+  }
+
+  f32x4 gw = {0.f, 0.f, 0.f, 0.f};
+  float db1acc = 0.f, db2acc = 0.f, la = 0.f, ca = 0.f, na = 0.f;
+  for (int b0 = 0; b0 < a.B; b0 += 64) {
+    const int nb = min(64, a.B - b0);
+    float4 hv = {0.f, 0.f, 0.f, 0.f};
+    if (hr < nb) hv = *reinterpret_cast<const float4*>(a.hpre + (size_t)(b0 + hr) * HD + hc4);
+    const int lab = (tid < nb) ? a.labels[b0 + tid] : 0;
+    head_stage(a, hv, b1v, hr, hc4, nb, hs);
+    if (tid < 64) labs[tid] = lab;
+    lds_barrier();
+    head_logits_ce(a, nb, hs, part, dls, w2s, b2s, labs, lane, wave, la, ca, na);
+    const f32x4 gh = head_dh(a, nb, hs, dls, w2s, lane, wave);
+    db1acc += (gh[0] + gh[1]) + (gh[2] + gh[3]);
+    if (wave < 4) {
+#pragma unroll
+      for (int k = 0; k < 64; k += 4) gw = mfma_f32x4(hs[(k + fq) * HS + wave * 16 + fr], dls[(k + fq) * 16 + fr], gw);
+    } else if (wave == 4) {
+#pragma unroll 4
+      for (int r = fq * 16; r < fq * 16 + 16; ++r) db2acc += dls[r * 16 + fr];
+    }
+    lds_barrier();
+  }
+  // db1: over the 4 lane groups, then the 4 row-tile waves of each unit tile; db2: over the lane groups
+  db1acc += __shfl_xor(db1acc, 16, 64);
+  db1acc += __shfl_xor(db1acc, 32, 64);
+  if (fq == 0) db1p[(wave >> 2) * 64 + (wave & 3) * 16 + fr] = db1acc;
+  db2acc += __shfl_xor(db2acc, 16, 64);
+  db2acc += __shfl_xor(db2acc, 32, 64);
+  if (wave < 4) {
+    la = rows4_sum(la);
+    ca = rows4_sum(ca);
+    na = rows4_sum(na);
+    if (a.metrics && lane == 0 && na > 0.f) {
+      atomicAdd(a.metrics + 0, la);
+      atomicAdd(a.metrics + 1, ca);
+      atomicAdd(a.metrics + 2, na);
+    }
+  }
+  lds_barrier();
+  float gv[4] = {0.f, 0.f, 0.f, 0.f};
+  float* gdst[4] = {nullptr, nullptr, nullptr, nullptr};
+  if (wave < 4 && fr < C) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      gv[i] = gw[i];
+      gdst[i] = a.dW2 ? a.dW2 + (size_t)(wave * 16 + fq * 4 + i) * C + fr : nullptr;
+    }
+  } else if (wave == 4 && fq == 0 && fr < C) {
+    gv[0] = db2acc;
+    gdst[0] = a.db2 ? a.db2 + fr : nullptr;
+  } else if (wave == 5 && a.b1) {
+    gv[0] = (db1p[lane] + db1p[64 + lane]) + (db1p[128 + lane] + db1p[192 + lane]);
+    gdst[0] = a.db1 ? a.db1 + lane : nullptr;
+  }
+  if (MODE == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (gdst[i]) *gdst[i] += gv[i];
+    return;
+  }
+  const float lr_t = opt_lr_t(a.h, t_it);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (e[i] < 0) continue;
+    float m = hmv[i], v = hvv[i];
+    a.hw[e[i]] = opt_step(a.h, lr_t, hwv[i], gv[i], m, v);
+    if (MODE == 2 && a.h.kind != kOptSGD) a.hm[e[i]] = m;
+    if (MODE == 2 && a.h.kind == kOptAdam) a.hv[e[i]] = v;
+  }
+  // the previous step's conv update (its forward used it on the fly; this launch does not read the
+  // conv weights): commit it, clear its flag; flag this step's update (the trunk's atomics)
+  if (cpend) cp.apply(a.commit, t_it - 1);
+  if (tid == 0) {
+    if (cpend) *a.commit.pend = 0;
+    if (a.pend_set) *a.pend_set = 1;
+    if (a.iter_prev) *a.iter_prev = t_it;
+  }
+}
+
+// MODE 0: store gradients; 1: fused step, SGD; 2: fused step, optimizer with slots (momentum / Adam).
+// Grid: one workgroup per PPW pooled positions + the head workgroup (last).
 template <int MODE>
 __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -360,26 +572,49 @@ __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
   uint8_t* am = smem + kAm;
   float* dps = reinterpret_cast<float*>(smem + kDp);
   float* red = dps;
+  float* hs = reinterpret_cast<float*>(smem + kDp + kHs);
+  float* part = reinterpret_cast<float*>(smem + kDp + kPart);
+  float* dls = reinterpret_cast<float*>(smem + kDp + kDl);
+  float* w2s = reinterpret_cast<float*>(smem + kW2s);
+  float* b2s = reinterpret_cast<float*>(smem + kB2s);
+  int* labs = reinterpret_cast<int*>(smem + kLab);
   stamp(a.stamps, 0);
-  const int W = a.W, H = a.H;
+  const int W = a.W, H = a.H, C = a.C;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
   const int fr = lane & 15, fq = lane >> 4, fk = fq * 8;
+
+  // ---- every workgroup: W2 image (classes padded to 16) and b2 in LDS; its slice of the other
+  // parity buffer of hpre zeroed for the next forward's atomics
+  {
+    const int u = tid >> 4, c = tid & 15;   // 64 x 16
+    w2s[u * 16 + c] = c < C ? a.W2[u * C + c] : 0.f;
+    if (tid < 16) b2s[tid] = tid < C ? a.b2[tid] : 0.f;
+  }
+  {
+    const int n4 = a.B * HD / 4, per = (n4 + gridDim.x - 1) / gridDim.x, beg = blockIdx.x * per;
+    const int end = min(n4, beg + per);
+    for (int i = beg + tid; i < end; i += 1024) reinterpret_cast<float4*>(a.hzero)[i] = float4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (blockIdx.x == gridDim.x - 1) {
+    head_workgroup<MODE>(a, smem);
+    return;
+  }
+
   const int Wp = (W - 2) / 2, Hp = (H - 2) / 2, P = Hp * Wp;
   const int p0 = blockIdx.x * PPW;
   const int nrow = min(PPW, P - p0) * CC;  // valid W1/Pt rows of this workgroup
+  const int hr = tid >> 4, hc4 = (tid & 15) * 4;   // hpre element group of this thread: row, 4 units
+  const float4 b1v = a.b1 ? *reinterpret_cast<const float4*>(a.b1 + hc4) : float4{0.f, 0.f, 0.f, 0.f};
 
   f32x4 accw[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   f32x4 accr[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 
-  // fused step: this workgroup's fp32 master rows (and slots) and the head variables, loaded
-  // now, updated after the chunk loop
+  // ---- fused step: this workgroup's fp32 master rows (and slots), loaded now, updated after the loop
   constexpr int NS = MODE == 2 ? 2 : 1;   // slot registers (dummies unless MODE 2)
   f32x4 wp[2], mp[NS], vp[NS];
   long long t_it = 0;
-  const bool head_wg = a.head.nr > 0 && blockIdx.x == gridDim.x - 1;
-  FlatPrefetch<1> hp;
   if (MODE != 0) {
-    if (a.h.kind == kOptAdam || a.head.h.kind == kOptAdam) t_it = *a.iterations;
+    t_it = *a.iterations;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int t = wave + 16 * i;
@@ -395,7 +630,6 @@ __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
         }
       }
     }
-    if (head_wg) hp.load(a.head, tid, 1024);
   }
 
   // W1 rows of the 4 positions: loaded once (independent of the image chunk)
@@ -408,13 +642,10 @@ __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
   for (int b0 = 0; b0 < a.B; b0 += 64) {
     const int nb = min(64, a.B - b0);
     // ---- prologue: coalesced loads of this chunk's operands
-    bf16x8 gv = {}, gtv = {}, ptv;
-    if (tid < 512) {
-      const int r = tid >> 3, c = (tid & 7) * 8;
-      if (r < nb) gv = *reinterpret_cast<const bf16x8*>(a.G + (size_t)(b0 + r) * a.ldg + c);
-      // Gt rows: unit r, images b0+c .. +8 (zero past B)
-      gtv = load_frag(a.Gt + (size_t)r * a.ldgt + b0 + c, b0 + c, a.B, true);
-    }
+    float4 hv = {0.f, 0.f, 0.f, 0.f};
+    if (hr < nb) hv = *reinterpret_cast<const float4*>(a.hpre + (size_t)(b0 + hr) * HD + hc4);
+    const int lab = (tid < nb) ? a.labels[b0 + tid] : 0;
+    bf16x8 ptv;
     {
       const int r = tid >> 3, c = (tid & 7) * 8;
       ptv = r < nrow ? load_frag(a.Pt + (size_t)(p0 * CC + r) * a.ldPt + b0 + c, b0 + c, a.B, true) : bf16x8{};
@@ -437,11 +668,8 @@ __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
       if (p < P && b < a.B) amv = a.amax[((size_t)p * (CC / 8) + cg) * a.lda + b];
     }
     stamp(a.stamps, 1);
-    if (tid < 512) {
-      const int r = tid >> 3, c = (tid & 7) * 8;
-      *reinterpret_cast<bf16x8*>(Gs + r * RSTR + c) = gv;
-      *reinterpret_cast<bf16x8*>(Gts + r * RSTR + c) = gtv;
-    }
+    head_stage(a, hv, b1v, hr, hc4, nb, hs);
+    if (tid < 64) labs[tid] = lab;
     {
       const int r = tid >> 3, c = (tid & 7) * 8;
       *reinterpret_cast<bf16x8*>(Pts + r * RSTR + c) = ptv;
@@ -453,6 +681,21 @@ __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
     {
       const int pp = tid >> 8, cg = (tid >> 6) & 3, bl = tid & 63;
       *reinterpret_cast<uint64_t*>(am + ((size_t)pp * 64 + bl) * CC + cg * 8) = amv;
+    }
+    lds_barrier();
+    // ---- the head recomputed: G = dH (bf16) into LDS, row-major and transposed
+    {
+      float la = 0.f, ca = 0.f, na = 0.f;   // the head workgroup keeps these
+      head_logits_ce(a, nb, hs, part, dls, w2s, b2s, labs, lane, wave, la, ca, na);
+      const f32x4 gh = head_dh(a, nb, hs, dls, w2s, lane, wave);
+      const int rt = wave >> 2, j = (wave & 3) * 16 + fr;
+      bf16x4 gt;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        gt[i] = f2bf(gh[i]);
+        Gs[(rt * 16 + fq * 4 + i) * RSTR + j] = gt[i];
+      }
+      *reinterpret_cast<bf16x4*>(Gts + j * RSTR + rt * 16 + fq * 4) = gt;
     }
     lds_barrier();
     stamp(a.stamps, 2);
@@ -535,7 +778,7 @@ __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
       const int nt = t & 3, rt = t >> 2;
       const int col = nt * 16 + fr, row0 = rt * 16 + fq * 4;
       if (row0 >= nrow) continue;   // nrow is a multiple of 32: all 4 rows valid or none
-      bf16x4 hv;
+      bf16x4 hv4;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const size_t e = (size_t)(p0 * CC + row0 + r) * HD + col;
@@ -544,16 +787,11 @@ __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
         a.w1[e] = w;
         if (MODE == 2 && a.h.kind != kOptSGD) a.m1[e] = m;
         if (MODE == 2 && a.h.kind == kOptAdam) a.v1[e] = v;
-        hv[r] = f2bf(w);
-        a.w1r_out[e] = hv[r];
+        hv4[r] = f2bf(w);
+        a.w1r_out[e] = hv4[r];
       }
-      if (a.w1c_out) *reinterpret_cast<bf16x4*>(a.w1c_out + (size_t)col * a.ldw1c + p0 * CC + row0) = hv;
+      if (a.w1c_out) *reinterpret_cast<bf16x4*>(a.w1c_out + (size_t)col * a.ldw1c + p0 * CC + row0) = hv4;
     }
-    if (head_wg) {
-      hp.apply(a.head, t_it);
-      flat_apply_from(a.head, t_it, 1024, tid, 1024);   // elements beyond one per thread (none for MNIST)
-    }
-    if (a.pend && blockIdx.x == 0 && tid == 0) *a.pend = 1;
   } else {
     // ---- store dW1 tiles (each row of dW1 belongs to exactly one workgroup)
 #pragma unroll
@@ -609,7 +847,7 @@ static bool opt_ok(const TdeStepOpt* o) {
 TDE_API int tde_convnet_fwd(const float* x, const float* wc, const float* bc, const void* W1c, int ldw1c,
                             float* hpre, void* Pt, int ldPt, void* amax, int lda, int B, int H, int W,
                             long long* stamps, int w1_rows, const TdeStepOpt* opt, long long off_wc,
-                            long long off_bc, hipStream_t stream) {
+                            long long off_bc, long long* inc_iter, hipStream_t stream) {
   if ((W & 3) || W > XW || ((W - 2) / 2) < 4 || (ldw1c & 7) || (Pt && (ldPt & 7)) || (amax && lda < B)) return -1;
   if (((uintptr_t)wc | (uintptr_t)bc) & 15) return -2;
   if (w1_rows && ldw1c != HD) return -3;
@@ -622,6 +860,7 @@ TDE_API int tde_convnet_fwd(const float* x, const float* wc, const float* bc, co
   }
   ConvNetFwdArgs a{x, wc, bc, (const bf16*)W1c, ldw1c, hpre, (bf16*)Pt, ldPt, (uint64_t*)amax, lda, B, H, W, stamps};
   a.w1_rows = w1_rows;
+  a.inc_iter = (unsigned long long*)inc_iter;
   if (opt) {
     a.pend = opt->pend;
     a.gwc = opt->g + off_wc;
@@ -654,49 +893,98 @@ TDE_API int tde_convnet_fwd(const float* x, const float* wc, const float* bc, co
   return 0;
 }
 
-// opt (nullable): fused step — Dense(64) rows at off_w1 updated in place (W1r rewritten; W1c [HD][ldw1c]
-// too when non-null), the head variables (ranges = {lo, n} x nr, nr <= kFlatRanges) updated by
-// the last workgroup, and *opt->pend set (deferred conv update).
-TDE_API int tde_convnet_bwd(const float* x, const void* amax, int lda, const void* G, int ldg, const void* Gt,
-                            int ldgt, const void* W1r, int ldw1r, const void* Pt, int ldPt, float* dW1, float* dwc,
-                            float* dbc, int B, int H, int W, long long* stamps, const TdeStepOpt* opt,
-                            long long off_w1, void* W1c, int ldw1c, const int* ranges, int nr,
+// Fused-step description of the backward (ctypes struct).
+struct TdeBwdOpt {
+  int kind;
+  float lr, mom, b1, b2, eps;
+  float *w, *m, *v;                   // flat buffers
+  long long off_w1, off_w2, off_b2, off_b1;
+  void* W1c; int ldw1c;               // transposed bf16 shadow (nullable)
+  const long long* iterations;
+  long long* iter_prev;
+  FlatApply commit;                   // previous step's deferred conv update (nr = 0: none)
+  int* pend_set;
+};
+
+// hpre: this step's Dense(64) pre-activation [B][64] f32; hzero: the other parity buffer (zeroed).
+// MODE 0 (opt == null): dW1 stored, conv grads atomically added, head grads (dW2 [64][C], db2, db1)
+// added by one workgroup.  opt: fused step (see ConvNetBwdArgs).
+TDE_API int tde_convnet_bwd(const float* x, const void* amax, int lda, const float* hpre, float* hzero,
+                            const float* b1, const float* W2, const float* b2, int C, int pre_relu,
+                            const int* labels, float scale, float* metrics, const void* W1r, int ldw1r,
+                            const void* Pt, int ldPt, float* dW1, float* dwc, float* dbc, float* dW2, float* db2,
+                            float* db1, int B, int H, int W, long long* stamps, const TdeBwdOpt* opt,
                             hipStream_t stream) {
-  if ((ldg & 7) || (ldgt & 7) || (ldw1r & 7) || (ldPt & 7) || ldgt < B || ldPt < B || lda < B) return -1;
-  if (opt && (!opt_ok(opt) || ldw1r != HD || (W1c && (ldw1c & 3)) || (off_w1 & 3) || nr < 0 || nr > kFlatRanges))
+  if ((ldw1r & 7) || (ldPt & 7) || ldPt < B || lda < B || C < 1 || C > 16 || !hpre || !hzero || !labels) return -1;
+  if ((((uintptr_t)hpre | (uintptr_t)hzero | (uintptr_t)b1) & 15)) return -2;
+  if (opt && (!opt->w || !opt->iterations || (opt->kind != kOptSGD && !opt->m) || (opt->kind == kOptAdam && !opt->v) ||
+              ldw1r != HD || (opt->W1c && (opt->ldw1c & 3)) || (opt->off_w1 & 3) || opt->commit.nr > kFlatRanges ||
+              (opt->commit.nr > 0 && !opt->commit.pend) || (b1 != nullptr) != (opt->off_b1 >= 0)))
     return -4;
-  const int P = ((H - 2) / 2) * ((W - 2) / 2);
-  ConvNetBwdArgs a{x, (const uint64_t*)amax, lda, (const bf16*)G, ldg, (const bf16*)Gt, ldgt, (const bf16*)W1r,
-                   ldw1r, (const bf16*)Pt, ldPt, dW1, dwc, dbc, B, H, W, stamps};
-  if (opt) {
+  if (opt && opt->commit.nr > 0) {
     int total = 0;
-    for (int i = 0; i < nr; ++i) total += ranges[2 * i + 1];
-    a.apply = 1;
-    a.w1 = opt->w + off_w1;
-    a.m1 = opt->m ? opt->m + off_w1 : nullptr;
-    a.v1 = opt->v ? opt->v + off_w1 : nullptr;
+    for (int i = 0; i < opt->commit.nr; ++i) total += opt->commit.n[i];
+    if (total > 1024) return -5;
+  }
+  const int P = ((H - 2) / 2) * ((W - 2) / 2);
+  ConvNetBwdArgs a{};
+  a.x = x;
+  a.amax = (const uint64_t*)amax;
+  a.lda = lda;
+  a.hpre = hpre;
+  a.hzero = hzero;
+  a.b1 = b1;
+  a.W2 = W2;
+  a.b2 = b2;
+  a.C = C;
+  a.pre_relu = pre_relu;
+  a.labels = labels;
+  a.scale = scale;
+  a.metrics = metrics;
+  a.W1r = (const bf16*)W1r;
+  a.ldw1r = ldw1r;
+  a.Pt = (const bf16*)Pt;
+  a.ldPt = ldPt;
+  a.dW1 = dW1;
+  a.dwc = dwc;
+  a.dbc = dbc;
+  a.dW2 = dW2;
+  a.db2 = db2;
+  a.db1 = db1;
+  a.B = B;
+  a.H = H;
+  a.W = W;
+  a.stamps = stamps;
+  a.off_b1 = -1;
+  if (opt) {
+    a.w1 = opt->w + opt->off_w1;
+    a.m1 = opt->m ? opt->m + opt->off_w1 : nullptr;
+    a.v1 = opt->v ? opt->v + opt->off_w1 : nullptr;
     a.w1r_out = (bf16*)W1r;
-    a.w1c_out = (bf16*)W1c;
-    a.ldw1c = ldw1c;
+    a.w1c_out = (bf16*)opt->W1c;
+    a.ldw1c = opt->ldw1c;
+    a.hw = opt->w;
+    a.hm = opt->m;
+    a.hv = opt->v;
+    a.off_w2 = opt->off_w2;
+    a.off_b2 = opt->off_b2;
+    a.off_b1 = opt->off_b1;
     a.iterations = opt->iterations;
-    a.h = hyper_of(opt);
-    a.head = FlatApply{opt->w, opt->g, opt->m, opt->v, opt->iterations, nullptr, a.h, nr, {0}, {0}};
-    for (int i = 0; i < nr; ++i) {
-      a.head.lo[i] = ranges[2 * i];
-      a.head.n[i] = ranges[2 * i + 1];
-    }
-    a.pend = opt->pend;
+    a.iter_prev = opt->iter_prev;
+    a.h = OptHyper{opt->kind, opt->lr, opt->mom, opt->b1, opt->b2, opt->eps};
+    a.commit = opt->commit;
+    a.pend_set = opt->pend_set;
   }
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)convnet_bwd_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, kBwdLds);
-    hipFuncSetAttribute((const void*)convnet_bwd_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, kBwdLds);
-    hipFuncSetAttribute((const void*)convnet_bwd_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, kBwdLds);
+    (void)hipFuncSetAttribute((const void*)convnet_bwd_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, kBwdLds);
+    (void)hipFuncSetAttribute((const void*)convnet_bwd_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, kBwdLds);
+    (void)hipFuncSetAttribute((const void*)convnet_bwd_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, kBwdLds);
     attr_set = true;
   }
-  const dim3 grid((P + PPW - 1) / PPW);
-  if (!a.apply) convnet_bwd_kernel<0><<<grid, 1024, kBwdLds, stream>>>(a);
-  else if (a.h.kind == kOptSGD) convnet_bwd_kernel<1><<<grid, 1024, kBwdLds, stream>>>(a);
+  const dim3 grid((P + PPW - 1) / PPW + 1);   // + the head workgroup
+  if (!opt) convnet_bwd_kernel<0><<<grid, 1024, kBwdLds, stream>>>(a);
+  else if (opt->kind == kOptSGD) convnet_bwd_kernel<1><<<grid, 1024, kBwdLds, stream>>>(a);
   else convnet_bwd_kernel<2><<<grid, 1024, kBwdLds, stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;

@@ -20,7 +20,7 @@
 //   dH[16 x H]       = dl . W2^T, ReLU mask           (wave w: 16-column tiles of H)
 // dH is emitted in bf16 row-major and transposed (K-contiguous for the next
 // MFMA GEMMs); bias grads by column sums; parameter grads are f32 atomics.
-#include "tde_optim.h"
+#include "tde_common.h"
 
 namespace tde {
 
@@ -41,11 +41,7 @@ struct HeadArgs {
   float* zero_hin;                    // if set (== hin): rows consumed are zeroed for the next split-K accumulation
   long long* iterations;              // if set: block 0 advances the step counter (Keras optimizer.iterations)
   long long* stamps;                  // diagnostic phase stamps (nullable)
-  // fused step: block 0 commits the deferred conv update of the previous step while *commit.pend
-  // (this launch does not read those variables; the forward before it used them on the fly)
-  FlatApply commit;                   // nr = 0: none
 };
-constexpr int kCommitPer = 2;         // <= 512 committed elements (Conv2D(32) 3x3x1 kernel + bias = 320)
 
 constexpr int HR = 16;          // rows per workgroup
 constexpr int HMAX = 256;       // max hidden width
@@ -84,37 +80,7 @@ __global__ __launch_bounds__(256) void head_xent_kernel(HeadArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int r0 = blockIdx.x * HR;
-  __shared__ long long it_old;
-  if (a.iterations && blockIdx.x == 0 && tid == 0)
-    it_old = (long long)atomicAdd((unsigned long long*)a.iterations, 1ull);
-  // deferred conv update: operands loaded now, committed at the end (t = the counter before
-  // this launch's increment, the step that produced the gradient)
-  const bool committer = a.commit.nr > 0 && blockIdx.x == 0;
-  int pend = 0;
-  float cw[kCommitPer], cg[kCommitPer], cm[kCommitPer], cv[kCommitPer];
-  int ce[kCommitPer];
-  if (committer) {
-    pend = *a.commit.pend;
-#pragma unroll
-    for (int k = 0; k < kCommitPer; ++k) {
-      int idx = tid + k * 256;
-      ce[k] = -1;
-      for (int r = 0; r < a.commit.nr; ++r) {
-        if (idx < a.commit.n[r]) {
-          ce[k] = a.commit.lo[r] + idx;
-          break;
-        }
-        idx -= a.commit.n[r];
-      }
-      cw[k] = cg[k] = cm[k] = cv[k] = 0.f;
-      if (ce[k] >= 0) {
-        cw[k] = a.commit.w[ce[k]];
-        cg[k] = a.commit.g[ce[k]];
-        if (a.commit.h.kind != kOptSGD) cm[k] = a.commit.m[ce[k]];
-        if (a.commit.h.kind == kOptAdam) cv[k] = a.commit.v[ce[k]];
-      }
-    }
-  }
+  if (a.iterations && blockIdx.x == 0 && tid == 0) atomicAdd((unsigned long long*)a.iterations, 1ull);
 
   // ---- prologue: every global load issued up front into registers (one memory latency,
   // not one per loop trip), then the LDS images (H padded to Hp = 16k with zeros)
@@ -223,20 +189,6 @@ __global__ __launch_bounds__(256) void head_xent_kernel(HeadArgs a) {
     }
   }
   stamp(a.stamps, 2);
-  if (committer) {
-    if (pend) {   // block-uniform
-      const float lr_t = opt_lr_t(a.commit.h, a.commit.h.kind == kOptAdam ? it_old : 0);
-#pragma unroll
-      for (int k = 0; k < kCommitPer; ++k) {
-        if (ce[k] < 0) continue;
-        a.commit.w[ce[k]] = opt_step(a.commit.h, lr_t, cw[k], cg[k], cm[k], cv[k]);
-        a.commit.g[ce[k]] = 0.f;
-        if (a.commit.h.kind != kOptSGD) a.commit.m[ce[k]] = cm[k];
-        if (a.commit.h.kind == kOptAdam) a.commit.v[ce[k]] = cv[k];
-      }
-      if (tid == 0) *a.commit.pend = 0;
-    }
-  }
   if (!a.compute_grad) return;
   lds_barrier();
 
@@ -296,18 +248,12 @@ TDE_API int tde_head_xent(const float* hin, int ldh, const float* pre_bias, int 
                           float* dpre_bias, void* G, int ldg, void* Gt, int ldgt, float* Gf,
                           int ldgf, float* metrics, float* probs, int probs_are_logits,
                           float* row_loss, int zero_hin, long long* iterations, long long* stamps,
-                          const FlatApply* commit, hipStream_t stream) {
+                          hipStream_t stream) {
   if (C > 16 || H > HMAX || H % 4 || (ldh & 3)) return -1;
   if (((uintptr_t)hin | (uintptr_t)pre_bias) & 15) return -2;
   HeadArgs a{hin, ldh, pre_bias, pre_relu, W2, b2, labels, B, H, C, scale, compute_grad,
              dW2, db2, dpre_bias, (bf16*)G, ldg, (bf16*)Gt, ldgt, Gf, ldgf, metrics, probs,
-             probs_are_logits, row_loss, zero_hin ? const_cast<float*>(hin) : nullptr, iterations, stamps, {}};
-  if (commit && commit->nr > 0) {
-    int total = 0;
-    for (int i = 0; i < commit->nr; ++i) total += commit->n[i];
-    if (commit->nr > kFlatRanges || total > kCommitPer * 256 || !commit->pend || !iterations) return -3;
-    a.commit = *commit;
-  }
+             probs_are_logits, row_loss, zero_hin ? const_cast<float*>(hin) : nullptr, iterations, stamps};
   int rows = B;
   if (Gt && ldgt > rows) rows = ldgt;
   const int grid = (rows + HR - 1) / HR;

@@ -45,6 +45,16 @@ class XgApply(_ct.Structure):
                 ("sht", _ct.c_void_p), ("sh_cols", _ct.c_int), ("sht_ld", _ct.c_longlong)]
 
 
+class BwdOpt(_ct.Structure):
+    """``TdeBwdOpt`` (csrc/kernels/convnet.hip): the fused-step part of the trunk backward."""
+    _fields_ = [("kind", _ct.c_int), ("lr", _ct.c_float), ("mom", _ct.c_float), ("b1", _ct.c_float),
+                ("b2", _ct.c_float), ("eps", _ct.c_float), ("w", _ct.c_void_p), ("m", _ct.c_void_p),
+                ("v", _ct.c_void_p), ("off_w1", _ct.c_longlong), ("off_w2", _ct.c_longlong),
+                ("off_b2", _ct.c_longlong), ("off_b1", _ct.c_longlong), ("W1c", _ct.c_void_p),
+                ("ldw1c", _ct.c_int), ("iterations", _ct.c_void_p), ("iter_prev", _ct.c_void_p),
+                ("commit", FlatApply), ("pend_set", _ct.c_void_p)]
+
+
 def step_opt(optimizer, w, g, m, v, iterations, pend):
     hp = optimizer.hparams()
     return StepOpt(optimizer.kind_id, float(optimizer.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"],
@@ -141,9 +151,7 @@ def conv3x3c1_relu_pool_bwd(x, amax, G, W1, dw, db):
 
 def head_xent(hin, W2, b2, labels, *, B, scale, pre_bias=None, pre_relu=False, compute_grad=True,
               dW2=None, db2=None, dpre_bias=None, G=None, Gt=None, Gf=None, metrics=None,
-              probs=None, probs_are_logits=False, row_loss=None, zero_hin=False, iterations=None, stamps=None,
-              commit: FlatApply | None = None):
-    """Fused head launch; ``commit`` (fused step): block 0 commits that deferred update while ``*pend``."""
+              probs=None, probs_are_logits=False, row_loss=None, zero_hin=False, iterations=None, stamps=None):
     H, C = W2.shape
     _req(hin.dtype == torch.float32 and hin.shape[1] >= H, "head: input")
     _req(C <= 64 and H * C <= 16384, "head: too large for the fused head")
@@ -154,19 +162,19 @@ def head_xent(hin, W2, b2, labels, *, B, scale, pre_bias=None, pre_relu=False, c
     rc = N.hip().tde_head_xent(_P(hin), hin.stride(0), _P(pre_bias), int(pre_relu), _P(W2), _P(b2), _P(labels),
                                B, H, C, float(scale), int(compute_grad), _P(dW2), _P(db2), _P(dpre_bias),
                                _P(G), ldg, _P(Gt), ldgt, _P(Gf), ldgf, _P(metrics), _P(probs),
-                               int(probs_are_logits), _P(row_loss), int(zero_hin), _P(iterations), _P(stamps),
-                               _ct.byref(commit) if commit is not None else None, _s())
+                               int(probs_are_logits), _P(row_loss), int(zero_hin), _P(iterations), _P(stamps), _s())
     N.check(rc, "tde_head_xent")
 
 
 def convnet_fwd(x, wc, bc, W1, hpre, Pt=None, amax=None, stamps=None, *, opt: StepOpt | None = None,
-                off_wc=0, off_bc=0):
+                off_wc=0, off_bc=0, inc_iter=None):
     """Fused Conv2D(32,3x3,relu)+MaxPool(2)+Dense(64) matmul forward; hpre += (atomic).
 
     W1: the bf16 Dense(64) kernel shadow, row-major [K, 64] or transposed [64, K].
     amax: uint8 view of a [P, 4, lda] uint64 buffer (lane-contiguous pool argmax).
     opt (fused step): while ``*opt.pend`` the conv weights used are the optimizer step of
-    (w, g) at offsets off_wc / off_bc of the flat buffers (the deferred update)."""
+    (w, g) at offsets off_wc / off_bc of the flat buffers (the deferred update).
+    inc_iter (training): the int64 step counter, advanced by one."""
     B, H, W = x.shape[0], x.shape[1], x.shape[2]
     Kf = ((H - 2) // 2) * ((W - 2) // 2) * 32
     _req(wc.shape == (3, 3, 1, 32) and bc is not None and bc.numel() == 32, "convnet_fwd: conv must be 3x3x1x32")
@@ -176,6 +184,7 @@ def convnet_fwd(x, wc, bc, W1, hpre, Pt=None, amax=None, stamps=None, *, opt: St
          "convnet_fwd: W1 must be [K,64] or [64,K]")
     _req(W % 2 == 0 and x.shape[3] == 1 and x.is_contiguous(), "convnet_fwd: input")
     _req(hpre.shape[0] >= B and hpre.shape[1] == 64 and hpre.is_contiguous(), "convnet_fwd: hpre")
+    _req(inc_iter is None or inc_iter.dtype == torch.int64, "convnet_fwd: int64 step counter")
     ldPt = 0
     if Pt is not None:
         ldPt = Pt.stride(0)
@@ -186,33 +195,35 @@ def convnet_fwd(x, wc, bc, W1, hpre, Pt=None, amax=None, stamps=None, *, opt: St
         _req(amax.dtype == torch.int64 and amax.shape[:2] == (Kf // 32, 4) and lda >= B, "convnet_fwd: amax")
     rc = N.hip().tde_convnet_fwd(_P(x), _P(wc), _P(bc), _P(W1), W1.stride(0), _P(hpre), _P(Pt), ldPt,
                                  _P(amax), lda, B, H, W, _P(stamps), int(rows),
-                                 _ct.byref(opt) if opt is not None else None, int(off_wc), int(off_bc), _s())
+                                 _ct.byref(opt) if opt is not None else None, int(off_wc), int(off_bc),
+                                 _P(inc_iter), _s())
     N.check(rc, "tde_convnet_fwd")
 
 
-def convnet_bwd(x, amax, G, Gt, W1row, Pt, dW1, dwc, dbc, B=None, stamps=None, *, opt: StepOpt | None = None,
-                off_w1=0, W1col=None, head_ranges=()):
-    """Fused trunk backward.  opt (fused step): instead of storing dW1, the Dense(64) rows at off_w1 of
-    the flat buffers are updated and their bf16 shadows (W1row, and W1col [64, K] if given) rewritten;
-    the last workgroup updates ``head_ranges`` [(lo, n)] and ``*opt.pend`` is set."""
+def convnet_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, metrics, W1row, Pt, dW1, dwc, dbc,
+                dW2=None, db2=None, db1=None, B=None, stamps=None, opt: BwdOpt | None = None):
+    """Trunk backward with the classifier head fused in: from this step's Dense(64) pre-activation
+    ``hpre`` [B, 64] (f32) every workgroup recomputes the head (loss, dlogits, Dense(64) input gradient)
+    and runs the trunk backward; ``hzero`` (the other parity buffer) is zeroed for the next forward.
+    Plain (``opt`` None): dW1 stored, conv grads atomically added, dW2 / db2 / db1 added, metrics
+    accumulated.  ``opt`` (fused step): the updates are applied instead (see ``BwdOpt``)."""
     B = x.shape[0] if B is None else B
     H, W = x.shape[1], x.shape[2]
     Kf = ((H - 2) // 2) * ((W - 2) // 2) * 32
-    _req(dwc.shape == (3, 3, 1, 32) and G.shape[1] == 64, "convnet_bwd: specialised for Conv2D(32) + Dense(64)")
-    _req(W1row.shape == (Kf, 64) and dW1.shape == (Kf, 64) and Pt.shape[0] == Kf, "convnet_bwd: shapes")
-    _req(Gt.shape[0] == 64 and Gt.stride(0) >= B and Pt.stride(0) >= B, "convnet_bwd: ld")
+    Hd, C = W2.shape
+    _req(dwc.shape == (3, 3, 1, 32) and Hd == 64 and C <= 16, "convnet_bwd: specialised for Conv2D(32) + Dense(64)")
+    _req(W1row.shape == (Kf, 64) and W1row.stride(0) == 64 and dW1.shape == (Kf, 64) and Pt.shape[0] == Kf,
+         "convnet_bwd: shapes")
+    _req(Pt.stride(0) >= B and Pt.stride(0) % 8 == 0, "convnet_bwd: Pt ld")
     _req(amax.dtype == torch.int64 and amax.shape[:2] == (Kf // 32, 4) and amax.shape[-1] >= B, "convnet_bwd: amax")
-    rng = (_ct.c_int * (2 * _FLAT_RANGES))()
-    if opt is not None:
-        _req(len(head_ranges) <= _FLAT_RANGES and off_w1 % 4 == 0, "convnet_bwd: head ranges / offset")
-        _req(W1col is None or (tuple(W1col.shape) == (64, Kf) and W1col.stride(0) % 4 == 0), "convnet_bwd: W1col")
-        for i, (lo, n) in enumerate(head_ranges):
-            rng[2 * i], rng[2 * i + 1] = int(lo), int(n)
-    rc = N.hip().tde_convnet_bwd(_P(x), _P(amax), amax.shape[-1], _P(G), G.stride(0), _P(Gt), Gt.stride(0),
-                                 _P(W1row), W1row.stride(0), _P(Pt), Pt.stride(0), _P(dW1), _P(dwc), _P(dbc), B, H,
-                                 W, _P(stamps), _ct.byref(opt) if opt is not None else None, int(off_w1),
-                                 _P(W1col), W1col.stride(0) if W1col is not None else 0, rng,
-                                 len(head_ranges) if opt is not None else 0, _s())
+    _req(hpre.shape[0] >= B and hpre.shape[1] == 64 and hpre.is_contiguous() and hzero.shape == hpre.shape
+         and hzero.is_contiguous(), "convnet_bwd: hpre / hzero")
+    _req(labels.dtype == torch.int32 and labels.numel() >= B, "convnet_bwd: int32 labels")
+    _req(W2.is_contiguous() and b2.numel() == C and (b1 is None or b1.numel() == 64), "convnet_bwd: head variables")
+    rc = N.hip().tde_convnet_bwd(_P(x), _P(amax), amax.shape[-1], _P(hpre), _P(hzero), _P(b1), _P(W2), _P(b2), C,
+                                 int(pre_relu), _P(labels), float(scale), _P(metrics), _P(W1row), W1row.stride(0),
+                                 _P(Pt), Pt.stride(0), _P(dW1), _P(dwc), _P(dbc), _P(dW2), _P(db2), _P(db1), B, H,
+                                 W, _P(stamps), _ct.byref(opt) if opt is not None else None, _s())
     N.check(rc, "tde_convnet_bwd")
 
 

@@ -77,6 +77,7 @@ class ReplicaPlan:
     # happens inside the step's own kernels; ``finish()`` flushes what is deferred) and "xgmi" (the
     # communicator's fused all-reduce applies it).
     step_mode = "plain"
+    parity = 0   # step parity of plans that double-buffer across steps (one hipGraph per start parity)
 
     def supports_step_mode(self, mode):
         return mode == "plain"
@@ -290,6 +291,18 @@ def match_convnet(model, loss):
 
 
 class ConvNetPlan(ReplicaPlan):
+    """The DWK/TF2M small CNN as two HIP launches per training step (csrc/kernels/convnet.hip):
+
+      forward   conv+bias+ReLU+pool fused with the Dense(64) matmul (split-K atomics into hpre[p])
+      backward  the head recomputed from hpre[p] in every workgroup (softmax-CE, dlogits, Dense(64)
+                input gradient), Dense(64) weight / input gradients, pool / ReLU routing and conv
+                gradients; one extra workgroup makes the head's own gradients and the metrics; the
+                other parity buffer hpre[1-p] is zeroed for the next forward
+
+    followed, by step mode, by the multi-tensor optimizer ("plain"), nothing ("local": the update
+    runs inside the two launches, the conv update deferred to the next step and flushed by
+    ``finish()``), or the xGMI all-reduce that applies it ("xgmi").  ``parity`` alternates per step;
+    the Program captures one hipGraph per starting parity."""
     kind = "fused_convnet"
 
     def __init__(self, model, store, device, batch, global_batch, optimizer, loss, pattern):
@@ -310,9 +323,10 @@ class ConvNetPlan(ReplicaPlan):
         bf = torch.bfloat16
         self.Pt = torch.zeros(self.Kf, Bp, dtype=bf, device=dev)
         self.amax = torch.zeros(self.Kf // 32, 4, Bp, dtype=torch.int64, device=dev)  # [P][C/8][B] argmax bytes
+        # Dense(64) pre-activation: two training buffers by step parity + one for eval / predict
+        self.hpre2 = torch.zeros(2, B, self.Hd, dtype=torch.float32, device=dev)
         self.hpre = torch.zeros(B, self.Hd, dtype=torch.float32, device=dev)
-        self.G = torch.zeros(B, self.Hd, dtype=bf, device=dev)
-        self.Gt = torch.zeros(self.Hd, Bp, dtype=bf, device=dev)
+        self.parity = 0
         self.probs = torch.zeros(B, self.Cls, dtype=torch.float32, device=dev)
         self.pre_relu = d1.activation == "relu"
         self.logits_out = d2.activation is None
@@ -333,8 +347,17 @@ class ConvNetPlan(ReplicaPlan):
         self.W1row = ok.shadow_views[(self.names["w1"], "row")]
         self.W1col = None if self.w1_rows else ok.shadow_views[(self.names["w1"], "col")]
         self.W1fwd = self.W1row if self.w1_rows else self.W1col
-        self.pend = torch.zeros(1, dtype=torch.int32, device=dev)   # deferred conv update outstanding
-        self._sopt = self._commit = None
+        # fused step ("local"): conv gradients by step parity (the deferred update of step t is read by
+        # forward t+1 while backward t+1 accumulates the next), their pending flags, and the step count
+        # the deferred update belongs to
+        seg = store.segments
+        sw, sb = seg[self.names["wc"]], seg[self.names["bc"]]
+        self._conv_lo = min(sw.offset, sb.offset)
+        span = max(sw.offset + sw.numel, sb.offset + sb.numel) - self._conv_lo
+        self.gconv = torch.zeros(2, span, dtype=torch.float32, device=dev)
+        self.pend = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.iter_prev = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._fopt = self._bopt = self._flush = None
 
     # ------------------------------------------------------------------ fused step modes
     def supports_step_mode(self, mode):
@@ -342,25 +365,54 @@ class ConvNetPlan(ReplicaPlan):
             return True
         return self.optimizer is not None and self.device.type == "cuda" and mode in ("local", "xgmi")
 
+    def _gconv(self, q):
+        """Pointer that indexes parity q's conv gradients with the flat-buffer offsets."""
+        return self.gconv[q].data_ptr() - 4 * self._conv_lo
+
+    def _gconv_views(self, q):
+        seg = self.store.segments
+        sw, sb = seg[self.names["wc"]], seg[self.names["bc"]]
+        lo = self._conv_lo
+        return (self.gconv[q, sw.offset - lo: sw.offset - lo + sw.numel].view(sw.shape),
+                self.gconv[q, sb.offset - lo: sb.offset - lo + sb.numel].view(sb.shape))
+
     def set_step_mode(self, mode):
         super().set_step_mode(mode)
+        self._fopt = self._bopt = self._flush = None
+        self._slots = (None, None)
         if mode == "plain":
-            self._sopt = self._commit = None
             return
-        st, opt = self.store, self.optimizer
+        K, st, opt = self.K, self.store, self.optimizer
         sl = opt.slot_names()
         m = st.slot(sl[0]) if sl else None
         v = st.slot(sl[1]) if len(sl) > 1 else None
         self._slots = (m, v)
-        self._sopt = self.K.step_opt(opt, st.w, st.g, m, v, self.iterations, self.pend)
+        self._opt_key_set = self._opt_key()
+        if mode != "local":
+            return
         seg = st.segments
         conv = [(seg[self.names["wc"]].offset, seg[self.names["wc"]].numel),
                 (seg[self.names["bc"]].offset, seg[self.names["bc"]].numel)]
-        # deferred conv update: committed by the next head launch, flushed at the end of an execution
-        self._commit = self.K.flat_apply_spec(opt, st.w, st.g, m, v, self.iterations, self.pend, conv)
-        head = [self.names[k] for k in ("w2", "b2", "b1") if self.names[k] is not None]
-        self._head_ranges = [(seg[h].offset, seg[h].numel) for h in head]
-        self._sopt_key = self._opt_key()
+        hp = opt.hparams()
+        P_ = K._P
+        self._fopt, self._bopt, self._flush = [], [], []
+        for q in (0, 1):
+            # forward of parity q: the deferred update of the previous step (parity 1-q), t = iter_prev
+            f = K.step_opt(opt, st.w, None, m, v, self.iter_prev, self.pend[1 - q])
+            f.g = self._gconv(1 - q)
+            self._fopt.append(f)
+            commit = K.flat_apply_spec(opt, st.w, None, m, v, self.iterations, self.pend[1 - q], conv)
+            commit.g = self._gconv(1 - q)
+            b1 = self.names["b1"]
+            self._bopt.append(K.BwdOpt(
+                opt.kind_id, float(opt.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"], P_(st.w), P_(m),
+                P_(v), seg[self.names["w1"]].offset, seg[self.names["w2"]].offset, seg[self.names["b2"]].offset,
+                seg[b1].offset if b1 is not None else -1, P_(self.W1col),
+                self.W1col.stride(0) if self.W1col is not None else 0, P_(self.iterations), P_(self.iter_prev),
+                commit, self.pend[q].data_ptr()))
+            fl = K.flat_apply_spec(opt, st.w, None, m, v, self.iterations, self.pend[q], conv)
+            fl.g = self._gconv(q)
+            self._flush.append(fl)
 
     def _opt_key(self):
         o = self.optimizer
@@ -368,7 +420,7 @@ class ConvNetPlan(ReplicaPlan):
 
     def refresh(self):
         # the kernel argument structs carry lr / hyper-parameters by value
-        if self._sopt is not None and self._sopt_key != self._opt_key():
+        if self.step_mode != "plain" and self._opt_key_set != self._opt_key():
             self.set_step_mode(self.step_mode)
 
     def xg_apply_spec(self):
@@ -385,12 +437,14 @@ class ConvNetPlan(ReplicaPlan):
 
     def finish(self):
         if self.step_mode == "local":
-            self.K.flat_apply(self._commit)
+            for q in (0, 1):   # at most one parity is pending
+                self.K.flat_apply(self._flush[q])
 
     def on_weights_loaded(self):
         (self.opt or self._shadow_only).refresh_shadows()
         # loaded weights replace whatever update was outstanding
         self.pend.zero_()
+        self.gconv.zero_()
         self.store.g.zero_()
 
     def _v(self, key):
@@ -401,45 +455,42 @@ class ConvNetPlan(ReplicaPlan):
         nm = self.names[key]
         return None if nm is None else self.store.grad(nm)
 
-    def _forward(self, x, B, with_pt, opt=None):
-        # kernel 1: conv+bias+ReLU+pool fused with the Dense(Hd) matmul (split-K atomics into hpre,
-        # which the previous head launch left zeroed)
+    def _forward(self, x, B, hpre, with_pt, opt=None, train=False):
+        # launch 1: conv+bias+ReLU+pool fused with the Dense(Hd) matmul (split-K atomics into hpre,
+        # which the previous backward / head launch left zeroed)
         seg = self.store.segments
-        self.K.convnet_fwd(x[:B], self._v("wc"), self._v("bc"), self.W1fwd, self.hpre,
+        self.K.convnet_fwd(x[:B], self._v("wc"), self._v("bc"), self.W1fwd, hpre,
                            self.Pt if with_pt else None, self.amax, opt=opt,
-                           off_wc=seg[self.names["wc"]].offset, off_bc=seg[self.names["bc"]].offset)
+                           off_wc=seg[self.names["wc"]].offset, off_bc=seg[self.names["bc"]].offset,
+                           inc_iter=self.iterations if train else None)
 
     def train_step(self, x, y, B=None):
         K = self.K
         B = self.B if B is None else B
+        q = self.parity
         local = self.step_mode == "local"
-        opt = self._sopt if local else None
-        self._forward(x, B, True, opt)
-        # kernel 2: Dense bias+ReLU, Dense(10), softmax-CE, accuracy and the head backward (fused step:
-        # also commits the previous step's deferred conv update)
-        K.head_xent(self.hpre, self._v("w2"), self._v("b2"), y, B=B, scale=self.scale, pre_bias=self._v("b1"),
-                    pre_relu=self.pre_relu, compute_grad=True, dW2=self._g("w2"), db2=self._g("b2"),
-                    dpre_bias=self._g("b1"), G=self.G, Gt=self.Gt, metrics=self.metrics, zero_hin=True,
-                    iterations=self.iterations, commit=self._commit if local else None)
-        # kernel 3: Dense weight-grad + Dense input-grad + pool/ReLU routing + conv weight/bias grads
-        # (fused step: the Dense(64) rows and the head variables are updated here)
-        K.convnet_bwd(x, self.amax, self.G, self.Gt, self.W1row, self.Pt, self._g("w1"), self._g("wc"),
-                      self._g("bc"), B=B, opt=opt, off_w1=self.store.segments[self.names["w1"]].offset,
-                      W1col=self.W1col, head_ranges=self._head_ranges if local else ())
+        self._forward(x, B, self.hpre2[q], True, self._fopt[q] if local else None, train=True)
+        # launch 2: head + trunk backward (fused step: the updates too)
+        dwc, dbc = self._gconv_views(q) if local else (self._g("wc"), self._g("bc"))
+        K.convnet_bwd(x, self.amax, self.hpre2[q], self.hpre2[1 - q], self._v("b1"), self._v("w2"), self._v("b2"), y,
+                      scale=self.scale, pre_relu=self.pre_relu, metrics=self.metrics, W1row=self.W1row, Pt=self.Pt,
+                      dW1=self._g("w1"), dwc=dwc, dbc=dbc, dW2=self._g("w2"), db2=self._g("b2"), db1=self._g("b1"),
+                      B=B, opt=self._bopt[q] if local else None)
+        self.parity = 1 - q
 
     def apply(self):
-        # kernel 4 (step mode "plain"): multi-tensor optimizer (+ grad zeroing + bf16 shadow refresh)
+        # step mode "plain": multi-tensor optimizer (+ grad zeroing + bf16 shadow refresh)
         self.opt.apply()
 
     def eval_step(self, x, y, B=None):
         B = self.B if B is None else B
-        self._forward(x, B, False)
+        self._forward(x, B, self.hpre, False)
         self.K.head_xent(self.hpre, self._v("w2"), self._v("b2"), y, B=B, scale=self.scale, pre_bias=self._v("b1"),
                          pre_relu=self.pre_relu, compute_grad=False, metrics=self.metrics, zero_hin=True)
 
     def predict(self, x, B=None):
         B = self.B if B is None else B
-        self._forward(x, B, False)
+        self._forward(x, B, self.hpre, False)
         self.K.head_xent(self.hpre, self._v("w2"), self._v("b2"), self._dummy_labels(B), B=B, scale=1.0,
                          pre_bias=self._v("b1"), pre_relu=self.pre_relu, compute_grad=False, probs=self.probs,
                          probs_are_logits=self.logits_out, zero_hin=True)

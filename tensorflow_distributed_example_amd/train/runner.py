@@ -97,7 +97,8 @@ class Program:
         self.y_ring = [torch.zeros((self.S, self.B), dtype=torch.int32, device=d) for d in self.devices]
         self.x_stage = [_Stager((self.S, self.B) + xs, torch.float32, d) for d in self.devices]
         self.y_stage = [_Stager((self.S, self.B), torch.int32, d) for d in self.devices]
-        self.graph = None
+        self.graph = None          # the last captured graph (diagnostics)
+        self.graphs = {}           # start parities -> (hipGraph of one execution, end parities)
         self._graph_key = None
         cuda = all(d.type == "cuda" for d in self.devices)
         env = os.environ.get("TDE_GRAPH", "1") != "0"
@@ -231,13 +232,20 @@ class Program:
             self._comm_warm = True
 
     def _key(self):
-        return (float(self.model.optimizer.learning_rate), self.model.optimizer.kind)
+        o = self.model.optimizer
+        return (float(o.learning_rate), o.kind, tuple(sorted(o.hparams().items())))
+
+    def _parities(self):
+        return tuple(p.parity for p in self.plans)
 
     def capture(self):
+        """Capture one execution (S steps) as a hipGraph for the plans' current step parities; the
+        parities are restored afterwards (capturing launches nothing)."""
         import gc
         self._warm_comm()
         for p in self.plans:
             p.refresh()
+        start = self._parities()
         dev = self.devices[0]
         with torch.cuda.device(dev):
             torch.cuda.synchronize(dev)
@@ -251,13 +259,19 @@ class Program:
                     self._steps(self.S)
             finally:
                 gc.enable()
+                self._end = self._parities()
+                for p, q in zip(self.plans, start):
+                    p.parity = q
             torch.cuda.synchronize(dev)
-        self.graph = g
+        self.graphs[start] = (g, self._end)
         self._graph_key = self._key()
+        self.graph = g
 
     def run(self):
         if self.use_graph:
-            if self.graph is None or self._graph_key != self._key():
+            if self._graph_key != self._key():
+                self.graphs = {}
+            if self._parities() not in self.graphs:
                 try:
                     self.capture()
                 except RuntimeError as e:
@@ -267,11 +281,15 @@ class Program:
                     warnings.warn(f"hipGraph capture of the training step failed ({e}); running eagerly")
                     self.use_graph = False
                     self.graph = None
+                    self.graphs = {}
                     torch.cuda.synchronize(self.devices[0])
                     self._steps(self.S)
                     return
+            g, end = self.graphs[self._parities()]
             with torch.cuda.device(self.devices[0]):
-                self.graph.replay()
+                g.replay()
+            for p, q in zip(self.plans, end):
+                p.parity = q
         else:
             self._warm_comm()
             for p in self.plans:

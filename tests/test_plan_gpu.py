@@ -190,7 +190,7 @@ def test_fused_local_step_matches_plain(kind, w1, monkeypatch):
         local.train_step(xt, yt)
     local.finish()
     torch.cuda.synchronize()
-    assert int(local.pend.item()) == 0 and float(st.g.abs().max()) == 0.0
+    assert int(local.pend.sum()) == 0 and float(st.g.abs().max()) == 0.0 and float(local.gconv.abs().max()) == 0.0
     for n in st.names(trainable=True):
         da, db = st.view(n).double() - w0[n].double(), st2.view(n).double() - w0[n].double()
         rel = ((da - db).norm() / (db.norm() + 1e-12)).item()
