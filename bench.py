@@ -77,6 +77,8 @@ def main():
     B = a.batch_per_gpu or dB
     GB = B * n
     spe = a.spe or dspe
+    if a.spe is None and dspe > 1 and a.steps <= 128:
+        spe = a.steps   # short runs (the driver's --steps 20): the whole timed region is one graph replay
     a.lr = a.lr if a.lr is not None else dlr
     while a.steps % spe:
         spe -= 1
@@ -148,7 +150,8 @@ def main():
             "data": f"synthetic (random {'x'.join(map(str, img))} images, random labels; random-init weights)",
             "config": {"model": a.model, "global_batch": GB, "seq_len": None, "image_shape": list(img),
                        "per_gpu_batch": B, "parallelism": f"dp{n}", "strategy": "MultiWorkerMirroredStrategy",
-                       "steps_per_execution": spe, "optimizer": f"SGD(lr={a.lr})", "plan": prog.plan_kind,
+                       "steps_per_execution": spe, "warmup_steps_run": n_warm * spe,
+                       "optimizer": f"SGD(lr={a.lr})", "plan": prog.plan_kind,
                        "allreduce": ar,
                        "hipgraph": prog.use_graph, "grad_buckets": len(prog.buckets or []) or 1,
                        "optimizer_placement": placement}}), flush=True)

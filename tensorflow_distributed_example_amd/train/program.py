@@ -437,8 +437,8 @@ class ConvNetPlan(ReplicaPlan):
 
     def finish(self):
         if self.step_mode == "local":
-            for q in (0, 1):   # at most one parity is pending
-                self.K.flat_apply(self._flush[q])
+            # only the last step's conv update can be pending (each backward commits the previous one)
+            self.K.flat_apply(self._flush[1 - self.parity])
 
     def on_weights_loaded(self):
         (self.opt or self._shadow_only).refresh_shadows()
