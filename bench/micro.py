@@ -94,7 +94,8 @@ def main():
         K.convnet_fwd(x, plan._v("wc"), plan._v("bc"), plan.W1fwd, plan.hpre2[q], plan.Pt, plan.amax, stamps=stamps,
                       opt=plan._fopt[q] if local else None,
                       off_wc=plan.store.segments[plan.names["wc"]].offset,
-                      off_bc=plan.store.segments[plan.names["bc"]].offset, inc_iter=plan.iterations)
+                      off_bc=plan.store.segments[plan.names["bc"]].offset, inc_iter=plan.iterations,
+                      hrep=plan.hrep)
 
     def k_bwd(stamps=None):
         q = plan.parity

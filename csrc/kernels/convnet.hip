@@ -64,6 +64,7 @@ struct ConvNetFwdArgs {
   const long long* iterations;
   OptHyper h;
   unsigned long long* inc_iter;      // training: block 0 advances the step counter (nullable)
+  int hrep; long long hrep_stride;   // hpre replicas: workgroup x adds into replica x % hrep
 };
 
 // The input rows a workgroup's PPW positions touch (<= XR rows of <= XW floats per
@@ -234,7 +235,10 @@ __global__ __launch_bounds__(FPW * 256) void convnet_fwd_kernel(ConvNetFwdArgs a
   lds_barrier();
   stamp(a.stamps, 3);
 
-  // ---- phase 2: hpre[64 x 64] += Ps(64 x FPW*32) . W1^T(FPW*32 x 64); 16x16 tiles over the waves
+  // ---- phase 2: hpre[64 x 64] += Ps(64 x FPW*32) . W1^T(FPW*32 x 64); 16x16 tiles over the waves.
+  // The ~85 workgroups' partial sums land on the same 16 KB: spread over hrep replicas (summed by the
+  // consumer) so each address sees ~85/hrep memory-side adds instead of 85
+  float* const hrow = a.hpre + (size_t)(blockIdx.x % a.hrep) * a.hrep_stride;
 #pragma unroll
   for (int j = 0; j < 4 / FPW; ++j) {
     const int mt = (wave >> 2) + FPW * j;
@@ -249,7 +253,7 @@ __global__ __launch_bounds__(FPW * 256) void convnet_fwd_kernel(ConvNetFwdArgs a
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int row = b0 + mt * 16 + (lane >> 4) * 4 + r;
-      if (row < a.B) atomicAdd(a.hpre + (size_t)row * HD + nt * 16 + fr, acc[r]);
+      if (row < a.B) atomicAdd(hrow + (size_t)row * HD + nt * 16 + fr, acc[r]);
     }
   }
   stamp(a.stamps, 4);
@@ -270,6 +274,7 @@ struct ConvNetBwdArgs {
   const float* x; const uint64_t* amax; int lda;
   const float* hpre;                 // [B][HD] f32 Dense(64) pre-activation (this step's parity)
   float* hzero;                      // [B][HD] the other parity buffer, zeroed here
+  int hrep; long long hrep_stride;   // hpre replicas (summed on load; all zeroed)
   const float* b1; const float* W2; const float* b2; int C; int pre_relu;
   const int* labels;
   float scale;                       // 1 / global batch (Keras AUTO reduction under a strategy)
@@ -359,6 +364,22 @@ __device__ __forceinline__ f32x4 mfma_f32x4(float a, float b, f32x4 c) {
 }
 
 // ---- head pieces shared by the trunk workgroups and the head workgroup (16 waves, 64 rows)
+
+// hpre[row][c4..c4+3] summed over the replicas (loads issued together)
+__device__ __forceinline__ float4 load_hpre(const ConvNetBwdArgs& a, int row, int c4) {
+  constexpr int kMaxRep = 4;
+  float4 v[kMaxRep];
+#pragma unroll
+  for (int r = 0; r < kMaxRep; ++r)
+    v[r] = r < a.hrep ? *reinterpret_cast<const float4*>(a.hpre + (size_t)r * a.hrep_stride + (size_t)row * HD + c4)
+                      : float4{0.f, 0.f, 0.f, 0.f};
+  float4 s = v[0];
+#pragma unroll
+  for (int r = 1; r < kMaxRep; ++r) {
+    s.x += v[r].x; s.y += v[r].y; s.z += v[r].z; s.w += v[r].w;
+  }
+  return s;
+}
 
 // h = act(hpre + b1) of this thread's row / 4 units into LDS (rows past nb zeroed)
 __device__ __forceinline__ void head_stage(const ConvNetBwdArgs& a, float4 hv, float4 b1v, int hr, int hc4, int nb,
@@ -485,7 +506,7 @@ __device__ __forceinline__ void head_workgroup(const ConvNetBwdArgs& a, unsigned
   for (int b0 = 0; b0 < a.B; b0 += 64) {
     const int nb = min(64, a.B - b0);
     float4 hv = {0.f, 0.f, 0.f, 0.f};
-    if (hr < nb) hv = *reinterpret_cast<const float4*>(a.hpre + (size_t)(b0 + hr) * HD + hc4);
+    if (hr < nb) hv = load_hpre(a, b0 + hr, hc4);
     const int lab = (tid < nb) ? a.labels[b0 + tid] : 0;
     head_stage(a, hv, b1v, hr, hc4, nb, hs);
     if (tid < 64) labs[tid] = lab;
@@ -591,7 +612,8 @@ __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
     if (tid < 16) b2s[tid] = tid < C ? a.b2[tid] : 0.f;
   }
   {
-    const int n4 = a.B * HD / 4, per = (n4 + gridDim.x - 1) / gridDim.x, beg = blockIdx.x * per;
+    const int n4 = (int)(((a.hrep - 1) * a.hrep_stride + (long long)a.B * HD) / 4);
+    const int per = (n4 + gridDim.x - 1) / gridDim.x, beg = blockIdx.x * per;
     const int end = min(n4, beg + per);
     for (int i = beg + tid; i < end; i += 1024) reinterpret_cast<float4*>(a.hzero)[i] = float4{0.f, 0.f, 0.f, 0.f};
   }
@@ -643,7 +665,7 @@ __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
     const int nb = min(64, a.B - b0);
     // ---- prologue: coalesced loads of this chunk's operands
     float4 hv = {0.f, 0.f, 0.f, 0.f};
-    if (hr < nb) hv = *reinterpret_cast<const float4*>(a.hpre + (size_t)(b0 + hr) * HD + hc4);
+    if (hr < nb) hv = load_hpre(a, b0 + hr, hc4);
     const int lab = (tid < nb) ? a.labels[b0 + tid] : 0;
     bf16x8 ptv;
     {
@@ -847,7 +869,8 @@ static bool opt_ok(const TdeStepOpt* o) {
 TDE_API int tde_convnet_fwd(const float* x, const float* wc, const float* bc, const void* W1c, int ldw1c,
                             float* hpre, void* Pt, int ldPt, void* amax, int lda, int B, int H, int W,
                             long long* stamps, int w1_rows, const TdeStepOpt* opt, long long off_wc,
-                            long long off_bc, long long* inc_iter, hipStream_t stream) {
+                            long long off_bc, long long* inc_iter, int hrep, long long hrep_stride,
+                            hipStream_t stream) {
   if ((W & 3) || W > XW || ((W - 2) / 2) < 4 || (ldw1c & 7) || (Pt && (ldPt & 7)) || (amax && lda < B)) return -1;
   if (((uintptr_t)wc | (uintptr_t)bc) & 15) return -2;
   if (w1_rows && ldw1c != HD) return -3;
@@ -861,6 +884,8 @@ TDE_API int tde_convnet_fwd(const float* x, const float* wc, const float* bc, co
   ConvNetFwdArgs a{x, wc, bc, (const bf16*)W1c, ldw1c, hpre, (bf16*)Pt, ldPt, (uint64_t*)amax, lda, B, H, W, stamps};
   a.w1_rows = w1_rows;
   a.inc_iter = (unsigned long long*)inc_iter;
+  a.hrep = hrep > 0 ? hrep : 1;
+  a.hrep_stride = hrep_stride;
   if (opt) {
     a.pend = opt->pend;
     a.gwc = opt->g + off_wc;
@@ -910,7 +935,7 @@ struct TdeBwdOpt {
 // MODE 0 (opt == null): dW1 stored, conv grads atomically added, head grads (dW2 [64][C], db2, db1)
 // added by one workgroup.  opt: fused step (see ConvNetBwdArgs).
 TDE_API int tde_convnet_bwd(const float* x, const void* amax, int lda, const float* hpre, float* hzero,
-                            const float* b1, const float* W2, const float* b2, int C, int pre_relu,
+                            int hrep, long long hrep_stride, const float* b1, const float* W2, const float* b2, int C, int pre_relu,
                             const int* labels, float scale, float* metrics, const void* W1r, int ldw1r,
                             const void* Pt, int ldPt, float* dW1, float* dwc, float* dbc, float* dW2, float* db2,
                             float* db1, int B, int H, int W, long long* stamps, const TdeBwdOpt* opt,
@@ -933,6 +958,9 @@ TDE_API int tde_convnet_bwd(const float* x, const void* amax, int lda, const flo
   a.lda = lda;
   a.hpre = hpre;
   a.hzero = hzero;
+  if (hrep < 1 || hrep > 4 || (hrep > 1 && (hrep_stride < (long long)B * HD || (hrep_stride & 3)))) return -6;
+  a.hrep = hrep;
+  a.hrep_stride = hrep_stride;
   a.b1 = b1;
   a.W2 = W2;
   a.b2 = b2;

@@ -167,14 +167,15 @@ def head_xent(hin, W2, b2, labels, *, B, scale, pre_bias=None, pre_relu=False, c
 
 
 def convnet_fwd(x, wc, bc, W1, hpre, Pt=None, amax=None, stamps=None, *, opt: StepOpt | None = None,
-                off_wc=0, off_bc=0, inc_iter=None):
+                off_wc=0, off_bc=0, inc_iter=None, hrep=1):
     """Fused Conv2D(32,3x3,relu)+MaxPool(2)+Dense(64) matmul forward; hpre += (atomic).
 
     W1: the bf16 Dense(64) kernel shadow, row-major [K, 64] or transposed [64, K].
     amax: uint8 view of a [P, 4, lda] uint64 buffer (lane-contiguous pool argmax).
     opt (fused step): while ``*opt.pend`` the conv weights used are the optimizer step of
     (w, g) at offsets off_wc / off_bc of the flat buffers (the deferred update).
-    inc_iter (training): the int64 step counter, advanced by one."""
+    inc_iter (training): the int64 step counter, advanced by one.
+    hrep: hpre is [hrep, >=B, 64] replicas (workgroup i adds into replica i % hrep) or [>=B, 64]."""
     B, H, W = x.shape[0], x.shape[1], x.shape[2]
     Kf = ((H - 2) // 2) * ((W - 2) // 2) * 32
     _req(wc.shape == (3, 3, 1, 32) and bc is not None and bc.numel() == 32, "convnet_fwd: conv must be 3x3x1x32")
@@ -183,7 +184,9 @@ def convnet_fwd(x, wc, bc, W1, hpre, Pt=None, amax=None, stamps=None, *, opt: St
     _req(rows and W1.stride(0) == 64 or tuple(W1.shape) == (64, Kf) and W1.stride(0) % 8 == 0,
          "convnet_fwd: W1 must be [K,64] or [64,K]")
     _req(W % 2 == 0 and x.shape[3] == 1 and x.is_contiguous(), "convnet_fwd: input")
-    _req(hpre.shape[0] >= B and hpre.shape[1] == 64 and hpre.is_contiguous(), "convnet_fwd: hpre")
+    hp = hpre if hrep == 1 and hpre.dim() == 2 else hpre.reshape(-1, *hpre.shape[-2:])
+    _req(hp.shape[0] == hrep and hpre.is_contiguous() if hp.dim() == 3 else hrep == 1, "convnet_fwd: hpre replicas")
+    _req(hp.shape[-2] >= B and hp.shape[-1] == 64 and hpre.is_contiguous(), "convnet_fwd: hpre")
     _req(inc_iter is None or inc_iter.dtype == torch.int64, "convnet_fwd: int64 step counter")
     ldPt = 0
     if Pt is not None:
@@ -196,7 +199,7 @@ def convnet_fwd(x, wc, bc, W1, hpre, Pt=None, amax=None, stamps=None, *, opt: St
     rc = N.hip().tde_convnet_fwd(_P(x), _P(wc), _P(bc), _P(W1), W1.stride(0), _P(hpre), _P(Pt), ldPt,
                                  _P(amax), lda, B, H, W, _P(stamps), int(rows),
                                  _ct.byref(opt) if opt is not None else None, int(off_wc), int(off_bc),
-                                 _P(inc_iter), _s())
+                                 _P(inc_iter), int(hrep), hp.stride(0) if hp.dim() == 3 else 0, _s())
     N.check(rc, "tde_convnet_fwd")
 
 
@@ -205,6 +208,7 @@ def convnet_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, me
     """Trunk backward with the classifier head fused in: from this step's Dense(64) pre-activation
     ``hpre`` [B, 64] (f32) every workgroup recomputes the head (loss, dlogits, Dense(64) input gradient)
     and runs the trunk backward; ``hzero`` (the other parity buffer) is zeroed for the next forward.
+    ``hpre`` / ``hzero`` may be [R, B, 64] replica stacks (summed on load; all zeroed).
     Plain (``opt`` None): dW1 stored, conv grads atomically added, dW2 / db2 / db1 added, metrics
     accumulated.  ``opt`` (fused step): the updates are applied instead (see ``BwdOpt``)."""
     B = x.shape[0] if B is None else B
@@ -216,11 +220,13 @@ def convnet_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, me
          "convnet_bwd: shapes")
     _req(Pt.stride(0) >= B and Pt.stride(0) % 8 == 0, "convnet_bwd: Pt ld")
     _req(amax.dtype == torch.int64 and amax.shape[:2] == (Kf // 32, 4) and amax.shape[-1] >= B, "convnet_bwd: amax")
-    _req(hpre.shape[0] >= B and hpre.shape[1] == 64 and hpre.is_contiguous() and hzero.shape == hpre.shape
-         and hzero.is_contiguous(), "convnet_bwd: hpre / hzero")
+    hp = hpre if hpre.dim() == 3 else hpre.unsqueeze(0)
+    _req(hp.shape[0] <= 4 and hp.shape[1] >= B and hp.shape[2] == 64 and hpre.is_contiguous()
+         and hzero.shape == hpre.shape and hzero.is_contiguous(), "convnet_bwd: hpre / hzero")
     _req(labels.dtype == torch.int32 and labels.numel() >= B, "convnet_bwd: int32 labels")
     _req(W2.is_contiguous() and b2.numel() == C and (b1 is None or b1.numel() == 64), "convnet_bwd: head variables")
-    rc = N.hip().tde_convnet_bwd(_P(x), _P(amax), amax.shape[-1], _P(hpre), _P(hzero), _P(b1), _P(W2), _P(b2), C,
+    rc = N.hip().tde_convnet_bwd(_P(x), _P(amax), amax.shape[-1], _P(hpre), _P(hzero), hp.shape[0], hp.stride(0),
+                                 _P(b1), _P(W2), _P(b2), C,
                                  int(pre_relu), _P(labels), float(scale), _P(metrics), _P(W1row), W1row.stride(0),
                                  _P(Pt), Pt.stride(0), _P(dW1), _P(dwc), _P(dbc), _P(dW2), _P(db2), _P(db1), B, H,
                                  W, _P(stamps), _ct.byref(opt) if opt is not None else None, _s())

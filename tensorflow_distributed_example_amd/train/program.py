@@ -324,7 +324,9 @@ class ConvNetPlan(ReplicaPlan):
         self.Pt = torch.zeros(self.Kf, Bp, dtype=bf, device=dev)
         self.amax = torch.zeros(self.Kf // 32, 4, Bp, dtype=torch.int64, device=dev)  # [P][C/8][B] argmax bytes
         # Dense(64) pre-activation: two training buffers by step parity + one for eval / predict
-        self.hpre2 = torch.zeros(2, B, self.Hd, dtype=torch.float32, device=dev)
+        # (training buffers: hrep replicas each, so the forward's ~85 split-K adders per address spread out)
+        self.hrep = max(1, min(4, int(os.environ.get("TDE_CONVNET_HREP", "4"))))
+        self.hpre2 = torch.zeros(2, self.hrep, B, self.Hd, dtype=torch.float32, device=dev)
         self.hpre = torch.zeros(B, self.Hd, dtype=torch.float32, device=dev)
         self.parity = 0
         self.probs = torch.zeros(B, self.Cls, dtype=torch.float32, device=dev)
@@ -455,21 +457,21 @@ class ConvNetPlan(ReplicaPlan):
         nm = self.names[key]
         return None if nm is None else self.store.grad(nm)
 
-    def _forward(self, x, B, hpre, with_pt, opt=None, train=False):
+    def _forward(self, x, B, hpre, with_pt, opt=None, train=False, hrep=1):
         # launch 1: conv+bias+ReLU+pool fused with the Dense(Hd) matmul (split-K atomics into hpre,
         # which the previous backward / head launch left zeroed)
         seg = self.store.segments
         self.K.convnet_fwd(x[:B], self._v("wc"), self._v("bc"), self.W1fwd, hpre,
                            self.Pt if with_pt else None, self.amax, opt=opt,
                            off_wc=seg[self.names["wc"]].offset, off_bc=seg[self.names["bc"]].offset,
-                           inc_iter=self.iterations if train else None)
+                           inc_iter=self.iterations if train else None, hrep=hrep)
 
     def train_step(self, x, y, B=None):
         K = self.K
         B = self.B if B is None else B
         q = self.parity
         local = self.step_mode == "local"
-        self._forward(x, B, self.hpre2[q], True, self._fopt[q] if local else None, train=True)
+        self._forward(x, B, self.hpre2[q], True, self._fopt[q] if local else None, train=True, hrep=self.hrep)
         # launch 2: head + trunk backward (fused step: the updates too)
         dwc, dbc = self._gconv_views(q) if local else (self._g("wc"), self._g("bc"))
         K.convnet_bwd(x, self.amax, self.hpre2[q], self.hpre2[1 - q], self._v("b1"), self._v("w2"), self._v("b2"), y,
