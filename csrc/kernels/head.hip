@@ -26,6 +26,7 @@ namespace tde {
 
 struct HeadArgs {
   const float* hin; int ldh;          // [B, H] pre-activation input (f32)
+  const bf16* hin_b;                  // ... or a bf16 input (the layer-wise plan's activations)
   const float* pre_bias;              // [H] or null
   int pre_relu;
   const float* W2; const float* b2;   // [H, C], [C]
@@ -96,7 +97,12 @@ __global__ __launch_bounds__(256) void head_xent_kernel(HeadArgs a) {
     hv[u] = float4{0.f, 0.f, 0.f, 0.f};
     pb[u] = float4{0.f, 0.f, 0.f, 0.f};
     if (i < HR * Hp4 && row < a.B && j4 < H) {
-      hv[u] = *reinterpret_cast<const float4*>(a.hin + (size_t)row * a.ldh + j4);
+      if (a.hin_b) {
+        const bf16x4 v = *reinterpret_cast<const bf16x4*>(a.hin_b + (size_t)row * a.ldh + j4);
+        hv[u] = float4{bf2f(v[0]), bf2f(v[1]), bf2f(v[2]), bf2f(v[3])};
+      } else {
+        hv[u] = *reinterpret_cast<const float4*>(a.hin + (size_t)row * a.ldh + j4);
+      }
       if (a.pre_bias) pb[u] = *reinterpret_cast<const float4*>(a.pre_bias + j4);
     }
   }
@@ -248,12 +254,13 @@ TDE_API int tde_head_xent(const float* hin, int ldh, const float* pre_bias, int 
                           float* dpre_bias, void* G, int ldg, void* Gt, int ldgt, float* Gf,
                           int ldgf, float* metrics, float* probs, int probs_are_logits,
                           float* row_loss, int zero_hin, long long* iterations, long long* stamps,
-                          hipStream_t stream) {
+                          int hin_bf16, hipStream_t stream) {
   if (C > 16 || H > HMAX || H % 4 || (ldh & 3)) return -1;
-  if (((uintptr_t)hin | (uintptr_t)pre_bias) & 15) return -2;
-  HeadArgs a{hin, ldh, pre_bias, pre_relu, W2, b2, labels, B, H, C, scale, compute_grad,
-             dW2, db2, dpre_bias, (bf16*)G, ldg, (bf16*)Gt, ldgt, Gf, ldgf, metrics, probs,
-             probs_are_logits, row_loss, zero_hin ? const_cast<float*>(hin) : nullptr, iterations, stamps};
+  if (hin_bf16 ? (((uintptr_t)hin & 7) || zero_hin) : (((uintptr_t)hin | (uintptr_t)pre_bias) & 15)) return -2;
+  HeadArgs a{hin_bf16 ? nullptr : hin, ldh, hin_bf16 ? (const bf16*)hin : nullptr, pre_bias, pre_relu, W2, b2,
+             labels, B, H, C, scale, compute_grad, dW2, db2, dpre_bias, (bf16*)G, ldg, (bf16*)Gt, ldgt, Gf, ldgf,
+             metrics, probs, probs_are_logits, row_loss, zero_hin ? const_cast<float*>(hin) : nullptr, iterations,
+             stamps};
   int rows = B;
   if (Gt && ldgt > rows) rows = ldgt;
   const int grid = (rows + HR - 1) / HR;

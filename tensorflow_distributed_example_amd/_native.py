@@ -33,7 +33,7 @@ _HIP_PROTOS = {
     "tde_conv3x3c1_relu_pool_fwd": (i32, [p, p, p, p, p, i32, p, i32, i32, i32, i32, p, i32, p]),
     "tde_conv3x3c1_relu_pool_bwd": (i32, [p, p, p, i32, p, i32, i32, p, p, i32, i32, i32, i32, p]),
     "tde_head_xent": (i32, [p, i32, p, i32, p, p, p, i32, i32, i32, f32, i32, p, p, p, p, i32, p, i32,
-                            p, i32, p, p, i32, p, i32, p, p, p]),
+                            p, i32, p, p, i32, p, i32, p, p, i32, p]),
     "tde_convnet_fwd": (i32, [p, p, p, p, i32, p, p, i32, p, i32, i32, i32, i32, p, i32, p, i64, i64, p, i32, i64,
                               p]),
     "tde_convnet_bwd": (i32, [p, p, i32, p, p, i32, i64, p, p, p, i32, i32, p, f32, p, p, i32, p, i32, p, p, p, p,

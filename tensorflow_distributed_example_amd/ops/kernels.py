@@ -153,7 +153,9 @@ def head_xent(hin, W2, b2, labels, *, B, scale, pre_bias=None, pre_relu=False, c
               dW2=None, db2=None, dpre_bias=None, G=None, Gt=None, Gf=None, metrics=None,
               probs=None, probs_are_logits=False, row_loss=None, zero_hin=False, iterations=None, stamps=None):
     H, C = W2.shape
-    _req(hin.dtype == torch.float32 and hin.shape[1] >= H, "head: input")
+    hb = hin.dtype == torch.bfloat16
+    _req((hin.dtype == torch.float32 or hb and not zero_hin) and hin.dim() == 2 and hin.shape[1] >= H
+         and hin.stride(1) == 1, "head: f32 or bf16 [B, H] input")
     _req(C <= 64 and H * C <= 16384, "head: too large for the fused head")
     _req(labels.dtype == torch.int32, "head: int32 labels")
     ldg = G.stride(0) if G is not None else 0
@@ -162,7 +164,8 @@ def head_xent(hin, W2, b2, labels, *, B, scale, pre_bias=None, pre_relu=False, c
     rc = N.hip().tde_head_xent(_P(hin), hin.stride(0), _P(pre_bias), int(pre_relu), _P(W2), _P(b2), _P(labels),
                                B, H, C, float(scale), int(compute_grad), _P(dW2), _P(db2), _P(dpre_bias),
                                _P(G), ldg, _P(Gt), ldgt, _P(Gf), ldgf, _P(metrics), _P(probs),
-                               int(probs_are_logits), _P(row_loss), int(zero_hin), _P(iterations), _P(stamps), _s())
+                               int(probs_are_logits), _P(row_loss), int(zero_hin), _P(iterations), _P(stamps),
+                               int(hb), _s())
     N.check(rc, "tde_head_xent")
 
 

@@ -668,7 +668,13 @@ class _Pad(_Stage):
 
 
 class _Head(_Stage):
-    """Last Dense -> f32 logits (+bias) -> softmax cross-entropy / accuracy / dlogits."""
+    """Last Dense -> f32 logits (+bias) -> softmax cross-entropy / accuracy / dlogits.
+
+    Fused (<= 16 classes, <= 256 input features, the usual MNIST heads): ONE launch of the head
+    kernel (csrc/kernels/head.hip) at the head's forward position does the Dense on the bf16 input with
+    exact f32 MFMA, softmax-CE, accuracy, dW / db and the input gradient — the five launches of the
+    general path (logits GEMM, xent, bias-grad, wgrad GEMM, dgrad GEMM) become one.  Otherwise: GEMM to
+    f32 logits, the fused softmax-CE kernel, and the backward GEMMs."""
 
     def __init__(self, plan, layer, tin, tout, logits_out):
         if len(tin.shape) != 1:
@@ -685,8 +691,12 @@ class _Head(_Stage):
         self.gb = st.grad(self.bname) if self.bname else None
         self.gW = st.grad(self.wname)
         self.need_dgrad = tin.root().id != 0
-        self.shadows = {self.wname: ("row", "col") if self.need_dgrad else ("col",)}
         self.C = layer.units
+        self.H = tin.shape[0]
+        self.W = st.view(self.wname)
+        self.fused = (self.C <= 16 and self.H <= 256 and self.H % 4 == 0
+                      and os.environ.get("TDE_FUSED_HEAD", "1") != "0")
+        self.shadows = {} if self.fused else {self.wname: ("row", "col") if self.need_dgrad else ("col",)}
 
     def alloc(self, B, dev):
         self.logits = torch.zeros(B * self.C, dtype=torch.float32, device=dev)
@@ -694,13 +704,33 @@ class _Head(_Stage):
         self.probs = torch.zeros(B * self.C, dtype=torch.float32, device=dev)
 
     def bind_shadows(self, sh):
+        if self.fused:
+            return
         self.Wt = sh.shadow_views[(self.wname, "col")]
         self.Wrow = sh.shadow_views.get((self.wname, "row"))
 
     def grad_inputs(self):
         return [self.inp] if self.need_dgrad else []
 
+    def _fused_fwd(self, p, B, mode):
+        from ..ops import kernels as K
+        h = self.inp.root().buf[: B * self.H].view(B, self.H)
+        if mode == "train":
+            G = self.inp.root().grad[: B * self.H].view(B, self.H) if self.need_dgrad else None
+            # the input gradient is stored, never accumulated: the head is the first backward writer
+            assert not self.need_dgrad or not self.accum[self.inp.root().id]
+            K.head_xent(h, self.W, self.b, p._labels, B=B, scale=p.scale, compute_grad=True, dW2=self.gW.view(self.H, -1),
+                        db2=self.gb, G=G, metrics=p.metrics, iterations=p.iterations)
+        elif mode == "eval":
+            K.head_xent(h, self.W, self.b, p._labels, B=B, scale=p.scale, compute_grad=False, metrics=p.metrics)
+        else:
+            K.head_xent(h, self.W, self.b, p._labels, B=B, scale=1.0, compute_grad=False,
+                        probs=self.probs[: B * self.C].view(B, self.C), probs_are_logits=self.logits_out)
+
     def fwd(self, p, B, training, mode="train"):
+        if self.fused:
+            self._fused_fwd(p, B, mode)
+            return
         O.dense_fwd(self.inp.root().buf, self.Wt, B, logits=self.logits, bias=self.b)
         if mode == "train":
             O.xent(self.logits, p._labels, B, self.C, scale=p.scale, dlogits=self.dlogits, metrics=p.metrics,
@@ -711,6 +741,8 @@ class _Head(_Stage):
             O.xent(self.logits, p._labels, B, self.C, probs=self.probs, probs_are_logits=self.logits_out)
 
     def bwd(self, p, B):
+        if self.fused:
+            return   # done by the forward's launch
         if self.gb is not None:
             O.act_bwd(self.dlogits, None, B, self.C, relu=False, dbias=self.gb)
         O.dense_wgrad(self.inp.root().buf, self.dlogits, self.gW, B, scratch=p.wscratch)
@@ -830,10 +862,14 @@ def emulate_step(plan: LayerwisePlan, x, y, B=None):
             vals[stg.out.root().id] = o.reshape(B, -1)
         elif isinstance(stg, _Head):
             a = get(stg.inp)
-            logits = a @ qw(stg.wname)
+            if stg.fused:   # f32 weights, f32 dlogits (the input gradient is rounded where it is stored)
+                logits = a @ W[stg.wname]
+            else:
+                logits = a @ qw(stg.wname)
             if stg.bname:
                 logits = logits + W[stg.bname]
-            logits = _QGrad.apply(logits)
+            if not stg.fused:
+                logits = _QGrad.apply(logits)
             loss = F.cross_entropy(logits, y[:B].long(), reduction="sum") * plan.scale
     loss.backward()
     out = {n: W[n].grad for n in st.names(trainable=True)}
