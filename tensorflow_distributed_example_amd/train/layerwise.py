@@ -110,6 +110,9 @@ class _Stage:
 
 class LayerwisePlan(PG.ReplicaPlan):
     kind = "layerwise"
+    # inputs staged as bf16 (Keras mixed_bfloat16 casts them at the first layer anyway): no per-step
+    # cast launch; TDE_BF16_INPUT=0 keeps f32 staging + the cast kernel
+    input_dtype = bf16 if os.environ.get("TDE_BF16_INPUT", "1") != "0" else torch.float32
 
     def __init__(self, model, store, device, batch, global_batch, optimizer, loss):
         super().__init__(model, store, device, batch, global_batch, optimizer)
@@ -257,6 +260,13 @@ class LayerwisePlan(PG.ReplicaPlan):
                 out_stages += lst
             stages = out_stages
         self.stages = stages
+        # the fused head also takes over the ReLU mask and bias gradient of a Dense that feeds only it
+        head = stages[-1]
+        if isinstance(head, _Head) and head.fused and len(stages) > 1:
+            prev = stages[-2]
+            if (isinstance(prev, _Gemm) and not prev.conv and prev.out.root() is head.inp.root()
+                    and len(T[prev.out.id].consumers) == 1 and not prev.stats):
+                head.absorb(prev)
         # gradient accumulation flags: reverse order, first writer stores
         written = set()
         for st in reversed(stages):
@@ -292,7 +302,21 @@ class LayerwisePlan(PG.ReplicaPlan):
         self._sh.refresh_shadows()
 
     def _input(self, x, B):
-        O.cast_bf16(x[:B].reshape(-1), self.x_bf[: B * self.T[0].numel])
+        n = B * self.T[0].numel
+        if x.dtype == bf16:
+            # the Program's input ring already holds bf16 (cast once per execution at staging): the
+            # first layer reads the ring slot directly
+            self._bind_input(x.reshape(-1)[:n])
+        else:
+            self._bind_input(self.x_bf)
+            O.cast_bf16(x[:B].reshape(-1), self.x_bf[:n])
+
+    def _bind_input(self, buf):
+        if self.T[0].buf is buf:
+            return
+        for t in self.T.values():
+            if t.root() is self.T[0]:
+                t.buf = buf
 
     def train_step(self, x, y, B=None, after_bwd=None):
         """Forward + backward.  ``after_bwd(i)`` (optional) runs after the i-th backward stage (reverse
@@ -397,6 +421,7 @@ class _Gemm(_Stage):
             self.small_wgrad = narrow and not self.use_im2col and O.smallconv_wgrad_ok(self.geo)
         self.colstats = None
         self.dz = None
+        self.act_done = False   # the consumer's launch already applied the ReLU mask / bias gradient
 
     def scratch_need(self, B):
         if self.conv:
@@ -422,7 +447,7 @@ class _Gemm(_Stage):
             self.Wt_pad = torch.zeros(g.Co * self.Kp, dtype=bf16, device=dev)
         if self.stats:
             self.colstats = torch.zeros(2 * O.STAT_SLOTS * self.out.C, dtype=torch.float64, device=dev)
-        if self.relu or self.gb is not None:
+        if (self.relu or self.gb is not None) and not self.act_done:
             self.dz = torch.zeros(B * self.out.numel, dtype=bf16, device=dev)
 
     def bind_shadows(self, sh):
@@ -697,6 +722,11 @@ class _Head(_Stage):
         self.fused = (self.C <= 16 and self.H <= 256 and self.H % 4 == 0
                       and os.environ.get("TDE_FUSED_HEAD", "1") != "0")
         self.shadows = {} if self.fused else {self.wname: ("row", "col") if self.need_dgrad else ("col",)}
+        self.pre = None   # absorbed Dense: its ReLU mask and bias gradient are applied by the head launch
+
+    def absorb(self, gemm):
+        self.pre = gemm
+        gemm.act_done = True
 
     def alloc(self, B, dev):
         self.logits = torch.zeros(B * self.C, dtype=torch.float32, device=dev)
@@ -719,8 +749,11 @@ class _Head(_Stage):
             G = self.inp.root().grad[: B * self.H].view(B, self.H) if self.need_dgrad else None
             # the input gradient is stored, never accumulated: the head is the first backward writer
             assert not self.need_dgrad or not self.accum[self.inp.root().id]
-            K.head_xent(h, self.W, self.b, p._labels, B=B, scale=p.scale, compute_grad=True, dW2=self.gW.view(self.H, -1),
-                        db2=self.gb, G=G, metrics=p.metrics, iterations=p.iterations)
+            pre = self.pre
+            # (with an absorbed Dense: h is its ReLU output, so h > 0 is its ReLU mask)
+            K.head_xent(h, self.W, self.b, p._labels, B=B, scale=p.scale, compute_grad=True,
+                        dW2=self.gW.view(self.H, -1), db2=self.gb, G=G, metrics=p.metrics, iterations=p.iterations,
+                        pre_relu=pre is not None and pre.relu, dpre_bias=pre.gb if pre is not None else None)
         elif mode == "eval":
             K.head_xent(h, self.W, self.b, p._labels, B=B, scale=p.scale, compute_grad=False, metrics=p.metrics)
         else:

@@ -77,6 +77,7 @@ class ReplicaPlan:
     # happens inside the step's own kernels; ``finish()`` flushes what is deferred) and "xgmi" (the
     # communicator's fused all-reduce applies it).
     step_mode = "plain"
+    input_dtype = torch.float32   # dtype of the Program's input ring for this plan
     parity = 0   # step parity of plans that double-buffer across steps (one hipGraph per start parity)
 
     def supports_step_mode(self, mode):

@@ -67,7 +67,14 @@ class _Stager:
         return buf
 
     def _launch(self, flat_t, n, dst):
-        dst.view(-1)[:n].copy_(flat_t[:n], non_blocking=self.cuda)
+        if dst.dtype != flat_t.dtype:
+            # e.g. a bf16 input ring: async H2D of the f32 staging, then one on-device cast
+            if getattr(self, "dev_tmp", None) is None or self.dev_tmp.numel() < flat_t.numel():
+                self.dev_tmp = torch.empty(flat_t.numel(), dtype=flat_t.dtype, device=dst.device)
+            self.dev_tmp[:n].copy_(flat_t[:n], non_blocking=self.cuda)
+            dst.view(-1)[:n].copy_(self.dev_tmp[:n])
+        else:
+            dst.view(-1)[:n].copy_(flat_t[:n], non_blocking=self.cuda)
         if self.cuda:
             e = torch.cuda.Event()
             e.record(torch.cuda.current_stream(self.device))
@@ -93,7 +100,8 @@ class Program:
         self.comm = strategy.comm if self.world > 1 else None
         xs = tuple(model.input_shape[1:])
         self.x_shape = xs
-        self.x_ring = [torch.zeros((self.S, self.B) + xs, dtype=torch.float32, device=d) for d in self.devices]
+        xdt = self.plans[0].input_dtype
+        self.x_ring = [torch.zeros((self.S, self.B) + xs, dtype=xdt, device=d) for d in self.devices]
         self.y_ring = [torch.zeros((self.S, self.B), dtype=torch.int32, device=d) for d in self.devices]
         self.x_stage = [_Stager((self.S, self.B) + xs, torch.float32, d) for d in self.devices]
         self.y_stage = [_Stager((self.S, self.B), torch.int32, d) for d in self.devices]
@@ -274,6 +282,16 @@ class Program:
             if self._parities() not in self.graphs:
                 try:
                     self.capture()
+                    end = self.graphs[self._parities()][1]
+                    if end not in self.graphs:
+                        # an odd number of steps per execution alternates the start parity: capture the
+                        # other graph now too, so no later execution pays a capture
+                        cur = self._parities()
+                        for p, q in zip(self.plans, end):
+                            p.parity = q
+                        self.capture()
+                        for p, q in zip(self.plans, cur):
+                            p.parity = q
                 except RuntimeError as e:
                     # e.g. a collective implementation that refuses stream capture: keep training
                     # with eager launches (same kernels, one host launch each) instead of failing

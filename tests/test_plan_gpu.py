@@ -216,7 +216,9 @@ def test_fused_local_fit_matches_plain(monkeypatch):
                optimizer=tde.optimizers.SGD(0.05, momentum=0.9), metrics=["accuracy"], steps_per_execution=3)
     w0 = ma.get_weights()
     ha = ma.fit(x, y, batch_size=64, epochs=1, shuffle=False, verbose=0)
-    assert ma._program("train", 64).plans[0].step_mode == "local"
+    pa = ma._program("train", 64)
+    assert pa.plans[0].step_mode == "local"
+    assert len(pa.graphs) == 2   # odd steps per execution: both start parities captured up front
     tde.backend.clear_session()
     monkeypatch.setenv("TDE_FUSED_STEP", "0")
     mb = tde.zoo.mnist_cnn()
