@@ -155,7 +155,8 @@ def hip():
     if _hip is None:
         with _lock:
             if _hip is None:
-                path = lib_path("libtde_hip.so")
+                # TDE_HIP_LIB: another in-tree build of the kernel library (A/B timing of kernel variants)
+                path = lib_path(os.environ.get("TDE_HIP_LIB", "libtde_hip.so"))
                 if not path.exists():
                     raise RuntimeError(
                         f"native HIP library missing: {path}. Build it with "
