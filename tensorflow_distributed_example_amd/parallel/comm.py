@@ -461,7 +461,10 @@ def maybe_xgmi(fallback, device, rank, world, bucket_hint=None, group=None):
         t = torch.zeros(min(n, xg.max_elems), device=device)
         tx = _time_allreduce(xg, t, 20, group)
         tr = _time_allreduce(fallback, t, 20, group)
-        dec = [tx <= tr]
+        # the xGMI kernel can also carry the optimizer update (one launch fewer per step, see
+        # XgmiCommunicator.all_reduce_apply_): it keeps the bucket unless RCCL is faster by more than that
+        margin = float(os.environ.get("TDE_XGMI_MARGIN_US", "3")) * 1e-6
+        dec = [tx <= tr + margin]
         dist.broadcast_object_list(dec, src=0, group=group)
         if rank == 0:
             import sys
