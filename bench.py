@@ -107,11 +107,30 @@ def main():
         if world > 1:
             torch.distributed.barrier()
 
-    # at least W warmup steps and at least 2 executions: the first replay follows the capture and
-    # the second still runs ~12% slow (GPU leaving idle; bench/exec_overhead.py "fresh_sequence_us")
+    # warm-up: at least W steps, at least 2 executions (the first replay follows the capture) and at
+    # least TDE_BENCH_WARM_MS of back-to-back work.  A GPU that idled runs the next ~0.5 ms of work
+    # 25-35% slower (bench/short_run.py: 20-step device time 585-629 us after a 50 ms idle gap vs
+    # 467-480 us after >= 1 ms of warm-up; profiles/r2_short_run.json), which alone decided the
+    # driver's 20-step number (1.5-2.4 M img/s across boxes at 2 executions of warm-up).
+    # Every rank runs the same number of executions (each holds collectives): the count is fixed from
+    # the timed first two and agreed as the max over ranks.
     n_warm = max(2, math.ceil(a.warmup / spe))
-    for i in range(n_warm):
+    warm_s = float(os.environ.get("TDE_BENCH_WARM_MS", "200")) * 1e-3
+    run_exec(0)
+    prog.sync()
+    tw = time.perf_counter()
+    run_exec(1)
+    prog.sync()
+    per_exec = max(time.perf_counter() - tw, 1e-6)
+    n_warm = max(n_warm, 2 + math.ceil(warm_s / per_exec))
+    if world > 1:
+        t = torch.tensor([n_warm], dtype=torch.int64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        n_warm = int(t.item())
+    for i in range(2, n_warm):
         run_exec(i)
+        if i % 8 == 0:
+            prog.sync()   # bounded queue depth; the GPU never idles for long
     prog.sync()
     barrier()
     prog.sync()
