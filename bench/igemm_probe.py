@@ -40,6 +40,9 @@ def main():
                                                                ldcb=Co), 20)
         res["conv K/9 bf16"] = graph_time(lambda: O._igemm(x, 0, O.A_CONV, Wt, K, O.B_NK, M, Co, C, g, cb=y,
                                                           ldcb=Co), 20)
+        if os.environ.get("PROBE_TORCH", "1") == "1":   # library reference point (hipBLASLt), same GEMM
+            xm, wm = xcol.view(M, K), Wt.t()
+            res["torch.mm(im2col) bf16"] = graph_time(lambda: torch.mm(xm, wm, out=y.view(M, Co)), 20)
         dW = torch.zeros(K * Co, device="cuda")
         dy = torch.randn(M * Co, device="cuda").to(bf)
         res["wgrad atomics"] = graph_time(lambda: O.conv_wgrad(x, dy, dW, g), 20)

@@ -69,6 +69,7 @@ struct IGemmArgs {
   // pixels and K runs over only the taps kh = kh0 + i*sh, kw = kw0 + j*sw that reach them
   int ph_on, ph_h, ph_w, Hp, Wp, kh0, kw0, KHp, KWp;
   int xcd;  // 1: XCD-aware tile order (consecutive tiles share an XCD's L2)
+  int a_bytes, b_bytes;  // operand sizes for the buffer-resource range checks of the LDS-DMA path (< 2^31)
 };
 
 constexpr int TK = 32;  // MFMA k-slice
@@ -334,6 +335,27 @@ __device__ __forceinline__ bf16x8 load_b_n8(const IGemmArgs& p, int n, int k) {
 // 16 zero bytes: the global_load_lds source of every padding / out-of-range slot.
 __device__ __attribute__((aligned(16))) bf16 g_zero16[8];
 
+// Raw buffer resource (base, byte range) and its 16-byte LDS-DMA load (buffer_load_dwordx4 ... lds:
+// lane i lands at lds + 16 i; offsets at or beyond the range read zeros).  The resource type exists
+// for the device target only, so the host pass of the kernels sees empty stand-ins.
+struct BufRes {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __amdgpu_buffer_rsrc_t r;
+#endif
+};
+__device__ __forceinline__ BufRes buf_res(const void* base, int bytes) {
+  BufRes b;
+#if defined(__HIP_DEVICE_COMPILE__)
+  b.r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+#endif
+  return b;
+}
+__device__ __forceinline__ void buf_lds16(const BufRes& b, char* lds, int voff, int soff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(b.r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+#endif
+}
+
 template <int N>
 __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -557,29 +579,63 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
 
   const int fr = lane & 15, fk = (lane >> 4) * 8;
   if constexpr (GLDS) {
-    // per-slot loader state: instruction j = wave*AS + i fills rows j*RPI + lane/KV, physical chunk
-    // lane%KV, which holds logical chunk (lane%KV) ^ swz(row).  The host only takes this path when
-    // every k-tile lies inside ONE filter tap (C, resp. Co, a multiple of KB): the tap and channel
-    // offset of a k-tile are block-uniform scalars, and a slot's source address is its row's pixel
-    // base plus one bounds-checked offset (no per-element index decomposition in the loop).
-    ARow gar[AS];
-    int gla[AS], glb[BS], gnb[BS];
+    // LDS-DMA staging (buffer_load_dwordx4 ... lds over raw buffer resources of A and B).
+    // Instruction j = wave*AS + i fills rows j*RPI + lane/KV, physical chunk lane%KV, which holds
+    // logical chunk (lane%KV) ^ swz(row).  The host only takes this path when every k-tile lies inside
+    // ONE filter tap (C, resp. Co, a multiple of KB) and both operands are < 2 GiB.  A slot's 32-bit
+    // byte offset (VGPR) is fixed for the whole loop (B, dense A) or recomputed only when the k-tile
+    // enters a new filter tap (conv A: two range compares and a select per slot); the k-tile's
+    // channel / k / tap offset is the block-uniform soffset (SGPR); padding and out-of-range slots
+    // read zeros through the buffer range check (offset 2^31).  The loop is unrolled by the stage
+    // count, so stage bases are immediates and no per-k-tile VALU address math remains.
+    constexpr int kOOB = (int)0x80000000u;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const BufRes rsa = buf_res(p.a, p.a_bytes), rsb = buf_res(p.b, p.b_bytes);
+    int arow[AS], ay0[AS], ax0[AS], avo[AS], bvo[BS], alch[AS], blch[BS];
 #pragma unroll
     for (int i = 0; i < AS; ++i) {
-      const int row = (wave * AS + i) * RPI + lane / KV;
-      gla[i] = (lane % KV) ^ ((row / RPB) & (KV - 1));
-      gar[i] = a_row<AK>(p, m0 + row);
+      const int row = (wv * AS + i) * RPI + lane / KV;
+      const int lch = (lane % KV) ^ ((row / RPB) & (KV - 1));
+      const int m = m0 + row;
+      const bool ok = m < p.M;
+      alch[i] = lch;
+      if (AK == A_ROWK) {
+        avo[i] = ok ? (int)(((long long)m * p.lda + lch * 8) * 2) : kOOB;
+        arow[i] = ay0[i] = ax0[i] = 0;
+      } else {
+        const ARow r = a_row<AK>(p, m);
+        const int Wd = AK == A_CONV ? p.g.W : p.g.Wo, Cd0 = AK == A_CONV ? p.g.C : p.g.Co;
+        arow[i] = (int)((r.base + (long long)r.y0 * Wd + r.x0) * Cd0) + lch * 8;   // may be < 0 (padding)
+        ay0[i] = r.ok ? r.y0 : -(1 << 28);   // an invalid row never passes the range check
+        ax0[i] = r.x0;
+        avo[i] = kOOB;
+      }
     }
 #pragma unroll
-    for (int i = 0; i < BS; ++i) {
-      const int row = (wave * BS + i) * RPI + lane / KV;
-      glb[i] = (lane % KV) ^ ((row / RPB) & (KV - 1));
-      gnb[i] = n0 + row;
+    for (int j = 0; j < BS; ++j) {
+      const int row = (wv * BS + j) * RPI + lane / KV;
+      const int lch = (lane % KV) ^ ((row / RPB) & (KV - 1));
+      const int n = n0 + row;
+      blch[j] = lch;
+      if (BK_ == B_NK) bvo[j] = n < p.N ? (int)(((long long)n * p.ldb + lch * 8) * 2) : kOOB;
+      else bvo[j] = n < p.N ? (n * p.g.Co + lch * 8) * 2 : kOOB;   // W[kh][kw][n][co]
+    }
+    // per-lane LDS fragment offsets (bytes) of row i = 0 / column j = 0 at each 32-wide k slice: the
+    // XOR swizzle of a row does not change over the 16-row steps of i / j (16 / RPB is a multiple of KV)
+    int offa[KB / 32], offb[KB / 32];
+#pragma unroll
+    for (int kk = 0; kk < KB; kk += 32) {
+      const int c = kk / 8 + (lane >> 4);
+      const int ra0 = wm * WTM + fr, rb0 = wn * WTN + fr;
+      offa[kk / 32] = (ra0 * KB + ((c ^ ((ra0 / RPB) & (KV - 1))) << 3)) * 2;
+      offb[kk / 32] = (rb0 * KB + ((c ^ ((rb0 / RPB) & (KV - 1))) << 3)) * 2;
     }
     const int KWd = (AK == A_DGRAD && p.ph_on) ? p.KWp : p.g.KW;  // taps per kernel row of this K
     // block-uniform tap (th, tw) and channel offset c0 of the next k-tile to issue: decomposed once,
     // then advanced by KB per issue (issues run in k order)
     const int Cd = (AK == A_CONV) ? p.g.C : p.g.Co;
+    const int Hl = AK == A_CONV ? p.g.H : p.g.Ho, Wl = AK == A_CONV ? p.g.W : p.g.Wo;
+    const int tsgn = AK == A_CONV ? 1 : -1;   // conv reads pixel (y0 + th, x0 + tw), dgrad (y0 - th, x0 - tw)
     int nth = 0, ntw = 0, nc0 = kt0 * KB;
     if (AK != A_ROWK || BK_ == B_DGRADW) {
       const int t = (kt0 * KB) / Cd;
@@ -587,14 +643,16 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
       nth = t / KWd;
       ntw = t - nth * KWd;
     }
+    bool newtap = true;   // the first issue of the block computes its tap's slot offsets
+    char* const lds = reinterpret_cast<char*>(smem);
     auto issue = [&](int stage, int kt) {
       const int k0 = kt * KB;
-      char* ab = reinterpret_cast<char*>(As + stage * AIMG);
-      char* bb = reinterpret_cast<char*>(Bs + stage * BIMG);
       const int th = nth, tw = ntw, c0 = (AK != A_ROWK || BK_ == B_DGRADW) ? nc0 : k0;
+      const bool fresh = newtap;
       if (AK != A_ROWK || BK_ == B_DGRADW) {
         nc0 += KB;
-        if (nc0 >= Cd) {
+        newtap = nc0 >= Cd;
+        if (newtap) {
           nc0 -= Cd;
           if (++ntw == KWd) {
             ntw = 0;
@@ -602,79 +660,72 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
           }
         }
       }
+      if (AK != A_ROWK && fresh) {
+        const int tapoff = tsgn * (th * Wl + tw) * Cd;
 #pragma unroll
-      for (int i = 0; i < AS; ++i) {
-        const bf16* src = g_zero16;
-        const ARow& r = gar[i];
-        if (AK == A_ROWK) {
-          const int k = k0 + gla[i] * 8;
-          if (r.ok && k < p.K) src = p.a + r.base + k;
-        } else if (AK == A_CONV) {
-          const int ih = r.y0 + th, iw = r.x0 + tw;
-          if (r.ok && (unsigned)ih < (unsigned)p.g.H && (unsigned)iw < (unsigned)p.g.W)
-            src = p.a + ((r.base + (long long)ih * p.g.W + iw) * p.g.C + c0 + gla[i] * 8);
-        } else {  // A_DGRAD (stride 1 or one stride phase): output pixel (y0 - th, x0 - tw)
-          const int oh = r.y0 - th, ow = r.x0 - tw;
-          if (r.ok && (unsigned)oh < (unsigned)p.g.Ho && (unsigned)ow < (unsigned)p.g.Wo)
-            src = p.a + ((r.base + (long long)oh * p.g.Wo + ow) * p.g.Co + c0 + gla[i] * 8);
+        for (int i = 0; i < AS; ++i) {
+          const bool v = (unsigned)(ay0[i] + tsgn * th) < (unsigned)Hl && (unsigned)(ax0[i] + tsgn * tw) < (unsigned)Wl;
+          avo[i] = v ? (arow[i] + tapoff) * 2 : kOOB;
         }
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)(ab + (wave * AS + i) * 1024), 16,
-                                         0, 0);
       }
-      int tap = 0;
+      const int soa = (AK == A_ROWK ? k0 : c0) * 2;
+      int sob = k0 * 2;
       if (BK_ == B_DGRADW) {
         const int kh = p.ph_on ? p.kh0 + th * p.g.sh : th, kw = p.ph_on ? p.kw0 + tw * p.g.sw : tw;
-        tap = kh * p.g.KW + kw;
+        sob = ((kh * p.g.KW + kw) * p.g.C * p.g.Co + c0) * 2;
       }
+      char* ab = lds + stage * AIMG * 2 + wv * AS * 1024;
+      char* bb = lds + NBUF * AIMG * 2 + stage * BIMG * 2 + wv * BS * 1024;
+      if (k0 + KB > p.K) {   // partial last k-tile (dense K % KB != 0; K % 8 == 0): chunks past K read zeros
 #pragma unroll
-      for (int i = 0; i < BS; ++i) {
-        const bf16* src = g_zero16;
-        const int n = gnb[i];
-        if (BK_ == B_NK) {
-          const int k = k0 + glb[i] * 8;
-          if (n < p.N && k < p.K) src = p.b + (long long)n * p.ldb + k;
-        } else {  // W[kh][kw][n][co]
-          if (n < p.N) src = p.b + ((long long)(tap * p.g.C + n) * p.g.Co + c0 + glb[i] * 8);
-        }
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)(bb + (wave * BS + i) * 1024), 16,
-                                         0, 0);
+        for (int i = 0; i < AS; ++i)
+          buf_lds16(rsa, ab + i * 1024, k0 + alch[i] * 8 < p.K ? avo[i] : kOOB, soa);
+#pragma unroll
+        for (int j = 0; j < BS; ++j)
+          buf_lds16(rsb, bb + j * 1024, k0 + blch[j] * 8 < p.K ? bvo[j] : kOOB, sob);
+      } else {
+#pragma unroll
+        for (int i = 0; i < AS; ++i)
+          buf_lds16(rsa, ab + i * 1024, avo[i], soa);
+#pragma unroll
+        for (int j = 0; j < BS; ++j)
+          buf_lds16(rsb, bb + j * 1024, bvo[j], sob);
       }
     };
-    if (kt0 < kt1) {
+    auto compute = [&](int stage) {   // stage: block-uniform; 4 VALU adds form the k-tile's read bases
+      const char* a = lds + stage * AIMG * 2;
+      const char* b = lds + NBUF * AIMG * 2 + stage * BIMG * 2;
+#pragma unroll
+      for (int kk = 0; kk < KB; kk += 32) {
+        bf16x8 af[MI], bfr[NI];
+        const char* ak = a + offa[kk / 32];
+        const char* bk = b + offb[kk / 32];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) af[i] = *reinterpret_cast<const bf16x8*>(ak + i * 16 * KB * 2);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(bk + j * 16 * KB * 2);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      }
+    };
+    const int nk = kt1 - kt0;
+    if (nk > 0) {
 #pragma unroll
       for (int st = 0; st < S - 1; ++st)
-        if (kt0 + st < kt1) issue(st, kt0 + st);
-      for (int kt = kt0; kt < kt1; ++kt) {
-        const int rel = kt - kt0;
-        const int after = min(S - 2, kt1 - 1 - kt);  // stages already issued behind this one
+        if (st < nk) issue(st, kt0 + st);
+      int cst = 0, ist = S - 1;   // compute / issue stage (scalar rotation, no modulo)
+      for (int rel = 0; rel < nk; ++rel) {
+        const int after = min(S - 2, nk - 1 - rel);  // k-tiles already issued behind this one
         if (after >= 2) vm_wait<2 * (AS + BS)>();
         else if (after == 1) vm_wait<AS + BS>();
         else vm_wait<0>();
-        __builtin_amdgcn_s_barrier();  // stage rel%S visible to all waves; stage (rel-1)%S free
-        if (kt + S - 1 < kt1) issue((rel + S - 1) % S, kt + S - 1);
-        const bf16* a = As + (rel % S) * AIMG;
-        const bf16* b = Bs + (rel % S) * BIMG;
-#pragma unroll
-        for (int kk = 0; kk < KB; kk += 32) {
-          const int c = kk / 8 + (lane >> 4);
-          bf16x8 af[MI], bfr[NI];
-#pragma unroll
-          for (int i = 0; i < MI; ++i) {
-            const int r = wm * WTM + i * 16 + fr;
-            af[i] = *reinterpret_cast<const bf16x8*>(a + r * KB + ((c ^ ((r / RPB) & (KV - 1))) << 3));
-          }
-#pragma unroll
-          for (int j = 0; j < NI; ++j) {
-            const int r = wn * WTN + j * 16 + fr;
-            bfr[j] = *reinterpret_cast<const bf16x8*>(b + r * KB + ((c ^ ((r / RPB) & (KV - 1))) << 3));
-          }
-#pragma unroll
-          for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
-        }
+        __builtin_amdgcn_s_barrier();  // stage cst visible to all waves; stage ist free
+        if (rel + S - 1 < nk) issue(ist, kt0 + rel + S - 1);
+        compute(cst);
+        cst = cst == S - 1 ? 0 : cst + 1;
+        ist = ist == S - 1 ? 0 : ist + 1;
       }
       vm_wait<0>();
     }
@@ -2565,6 +2616,18 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   bool ut = true;
   if (akind == A_CONV) ut = p.g.C % KB == 0;
   if (akind == A_DGRAD) ut = p.g.Co % KB == 0 && (p.ph_on || (p.g.sh == 1 && p.g.sw == 1));
+  {
+    // LDS-DMA loads address both operands with 32-bit byte offsets under buffer range checks
+    long long ae = 0, be = 0;
+    if (akind == A_ROWK) ae = (long long)(M - 1) * lda + K;
+    else if (akind == A_CONV) ae = (long long)p.g.B * p.g.H * p.g.W * p.g.C;
+    else if (akind == A_DGRAD) ae = (long long)p.g.B * p.g.Ho * p.g.Wo * p.g.Co;
+    if (bkind == B_NK) be = (long long)(N - 1) * ldb + K;
+    else if (bkind == B_DGRADW) be = (long long)p.g.KH * p.g.KW * p.g.C * p.g.Co;
+    if (ae * 2 >= (1LL << 31) - 16 || be * 2 >= (1LL << 31) - 16) ut = false;
+    p.a_bytes = (int)(ae * 2 < (1LL << 31) ? ae * 2 : 0);
+    p.b_bytes = (int)(be * 2 < (1LL << 31) ? be * 2 : 0);
+  }
   // big tiles (256 x 64 with 64 x 64 per wave, or 256 x 128 with 128 x 64 per wave): fwd/dense when
   // tuned on (fwd 641 -> 840 us on ResNet-18 with them), dgrad when g_big_dgrad
   const bool big = (g_big || (g_big_dgrad && akind == A_DGRAD)) && KB == 64 && splits == 1 && !rowk && big_shape;

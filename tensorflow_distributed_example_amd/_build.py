@@ -97,7 +97,8 @@ def build_hip(force=False, jobs=8) -> Path:
     if force or _deps_newer(out, objs):
         rocm = _rocm()
         _run([_hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", *map(str, objs), "-o", str(out),
-              f"-L{rocm}/lib", "-lrccl", "-lamdhip64", f"-Wl,-rpath,{rocm}/lib"])
+              f"-L{rocm}/lib", "-lrccl", "-lamdhip64", f"-Wl,-rpath,{rocm}/lib",
+              "-Wl,-z,defs"])   # an unresolved symbol (e.g. a kernel stub the host pass dropped) fails the build
     return out
 
 
