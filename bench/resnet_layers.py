@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--sweep-tile", action="store_true", help="sweep the fwd/dgrad tile-size threshold only")
     ap.add_argument("--sweep-big-dgrad", action="store_true", help="A/B the dgrad big tiles only")
+    ap.add_argument("--sweep-fd", action="store_true", help="fwd / dgrad per layer over tile threshold x K step")
     a = ap.parse_args()
     import tensorflow_distributed_example_amd as tde
     from tensorflow_distributed_example_amd import _native as N
@@ -77,7 +78,26 @@ def main():
                                                       st.geo.with_batch(B), scratch=plan.scratch), a.reps)
                       for st in _convs(plan, LW) if st.need_dgrad)
             print(f"SWEEP tile_min={tmin}: fwd {tf_:.1f} us dgrad {td_:.1f} us", flush=True)
-        lib.tde_igemm_tile_min(512)
+        lib.tde_igemm_tile_min(2048)
+    if a.sweep_fd:
+        # fwd / dgrad per layer under (tile_min, K step): picks the per-shape defaults
+        lib = N.hip()
+        cfgs = [(tm, kb, 0) for kb in (32, 64) for tm in (256, 1024, 2048, 4096)] + [(2048, 64, 1)]
+        for st in _convs(plan, LW):
+            g = st.geo.with_batch(B)
+            res = []
+            for tm, kb, big in cfgs:
+                lib.tde_igemm_tile_min(tm)
+                lib.tde_igemm_tune(512, 16, kb, -1, big, 64)
+                lib.tde_igemm_big_dgrad(big)
+                tf_ = graph_time(lambda: st.fwd(plan, B, True), a.reps)
+                td_ = graph_time(lambda: O.conv_dgrad(st.out.root().grad, st.Wrow, st.inp.root().grad, g,
+                                                      scratch=plan.scratch), a.reps) if st.need_dgrad else 0.0
+                res.append(f"t{tm}/k{kb}{'/big' if big else ''}: {tf_:.1f}/{td_:.1f}")
+            print(f"SWEEPFD {st.layer.name} {g.H}x{g.W}x{g.C}->{g.Co} s{g.sh} | " + " | ".join(res), flush=True)
+        lib.tde_igemm_tile_min(2048)
+        lib.tde_igemm_tune(512, 16, 0, -1, 0, 192)
+        lib.tde_igemm_big_dgrad(0)
     if a.sweep_big_dgrad:
         lib = N.hip()
         for bd in (0, 1, 0, 1):

@@ -2545,7 +2545,10 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   const bool big_shape = splits <= 1 && (N <= 64 || N % 128 == 0) && big_tiles >= g_big_min;
   // dgrad big tiles run at KB = 64 (their only instantiation), so enabling them moves dgrad to KB = 64
   const bool dgrad_big = akind == A_DGRAD && g_big_dgrad && big_shape && p.g.Co % 64 == 0;
-  const int KB = g_kb_force ? g_kb_force : (dgrad_big ? 64 : ((akind == A_DGRAD || K < 256) ? 32 : 64));
+  // (the LDS-DMA dgrad runs best at 64 too since its loop lost the per-k-tile address math:
+  // profiles/r2_sweep_fd.txt, 18 ResNet-18 dgrads 834 -> ~640 us)
+  const int KB = g_kb_force ? g_kb_force
+                            : (dgrad_big ? 64 : (akind == A_DGRAD ? (p.g.Co % 64 == 0 ? 64 : 32) : (K < 256 ? 32 : 64)));
   const int ktiles = (K + KB - 1) / KB;
   const bool auto_splits = splits == 0;
   if (splits < 1) splits = 1;
@@ -2591,7 +2594,9 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     }
   } else if (N > 64 && tiles(128, 128) >= g_tile_min) {
     bm = bn = 128;
-  } else if (tiles(128, 64) >= g_tile_min) {
+  } else if (tiles(128, 64) >= g_tile_min || (ktiles >= 16 && tiles(128, 64) >= 256)) {
+    // 128x64 also for long K loops that still give >= one workgroup per CU: half the operand re-reads
+    // of 64x64 (ResNet-18 14x14x256 convs 34.7 -> 27.1 us; profiles/r2_sweep_fd.txt)
     bm = 128;
   }
   dim3 grid((M + bm - 1) / bm, (N + bn - 1) / bn, splits);
