@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--sweep-tile", action="store_true", help="sweep the fwd/dgrad tile-size threshold only")
     ap.add_argument("--sweep-big-dgrad", action="store_true", help="A/B the dgrad big tiles only")
     ap.add_argument("--sweep-fd", action="store_true", help="fwd / dgrad per layer over tile threshold x K step")
+    ap.add_argument("--sweep-wgrad", action="store_true", help="weight-gradient path x stages x tile cap x split target")
     a = ap.parse_args()
     import tensorflow_distributed_example_amd as tde
     from tensorflow_distributed_example_amd import _native as N
@@ -98,6 +99,23 @@ def main():
         lib.tde_igemm_tile_min(2048)
         lib.tde_igemm_tune(512, 16, 0, -1, 0, 192)
         lib.tde_igemm_big_dgrad(0)
+    if a.sweep_wgrad:
+        lib = N.hip()
+        for mode, cap, target in [(0, 0, 512), (3, 0, 512), (1, 0, 512), (2, 0, 512), (1, 1, 512), (2, 1, 512),
+                                  (3, 0, 256), (3, 0, 1024), (0, 0, 512), (3, 0, 512)]:
+            lib.tde_igemm_wgrad_dma(mode)
+            lib.tde_igemm_wgrad_tile_cap(cap)
+            lib.tde_igemm_tune(target, 16, 0, -1, -1, 0)
+            per = []
+            for st in _convs(plan, LW):
+                g = st.geo.with_batch(B)
+                per.append(graph_time(lambda: O.conv_wgrad(st.inp.buf, st.out.root().grad, st.gW, g,
+                                                           scratch=plan.wscratch), a.reps))
+            print(f"SWEEPWG dma={mode} cap={cap} target={target}: {sum(per):.1f} us | "
+                  + " ".join(f"{t:.1f}" for t in per), flush=True)
+        lib.tde_igemm_wgrad_dma(3)
+        lib.tde_igemm_wgrad_tile_cap(0)
+        lib.tde_igemm_tune(512, 16, 0, -1, -1, 0)
     if a.sweep_big_dgrad:
         lib = N.hip()
         for bd in (0, 1, 0, 1):

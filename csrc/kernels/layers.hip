@@ -70,6 +70,9 @@ struct IGemmArgs {
   int ph_on, ph_h, ph_w, Hp, Wp, kh0, kw0, KHp, KWp;
   int xcd;  // 1: XCD-aware tile order (consecutive tiles share an XCD's L2)
   int a_bytes, b_bytes;  // operand sizes for the buffer-resource range checks of the LDS-DMA path (< 2^31)
+  // LDS-DMA weight gradient: pixels in row-padded order k = (oh * B + b) * 2^wp_log + ow (K = Ho*B*2^wp_log;
+  // the padding columns ow >= Wo read zeros); a_shift = (pt*W + pl)*C elements below X for the A resource
+  int wp_log, a_shift;
 };
 
 constexpr int TK = 32;  // MFMA k-slice
@@ -93,9 +96,13 @@ __device__ __forceinline__ bf16x8 zero8() {
 // RW = 64: 128-byte rows (2 rows per 64 banks); the chunk pair is XORed with (row bit 1, row bit 3)
 // so the 8 rows one 32-lane half of a transposed read touches land in 8 distinct bank groups.
 template <int RW>
+__device__ __forceinline__ int swzc(int row) {  // XOR applied to the 16-byte chunk index of image row `row`
+  if (RW == 128) return ((row & 3) << 2) | ((row >> 2) & 3);
+  return (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1;
+}
+template <int RW>
 __device__ __forceinline__ int swz(int row, int ch) {
-  if (RW == 128) return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
-  return 128 * row + 16 * (ch ^ ((((row >> 1) & 1) | (((row >> 3) & 1) << 1)) << 1));
+  return 2 * RW * row + 16 * (ch ^ swzc<RW>(row));
 }
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
@@ -373,7 +380,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   constexpr bool AKV = (AK == A_ROWK || AK == A_CONV || AK == A_DGRAD);  // K-vector A
   constexpr bool BKV = (BK_ == B_NK || BK_ == B_DGRADW);                 // K-vector B
   constexpr bool GLDS = S > 0;
-  static_assert(!GLDS || (AKV && BKV && VEC), "global_load_lds staging needs 16-byte K-vector operands");
+  static_assert(!GLDS || (AKV && BKV && VEC) || (AK == A_WGRAD && BK_ == B_KN && VEC),
+                "LDS-DMA staging: 16-byte K-vector operands, or the row-padded weight gradient");
   constexpr int LDKB = GLDS ? KB : KB + 8;         // K-vector image row: KB k (+ 8 pad unless swizzled)
   constexpr int AIMG = AKV ? BM * LDKB : KB * BM;  // elements per buffer
   constexpr int BIMG = BKV ? BN * LDKB : KB * BN;
@@ -578,7 +586,106 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fk = (lane >> 4) * 8;
-  if constexpr (GLDS) {
+  if constexpr (GLDS && !AKV) {
+    // Weight gradient dW[(kh,kw,ci), co] = sum over pixels of X(pixel shifted by the tap)[ci] * dY[pixel][co],
+    // both operands row-vector images [k][BM|BN] (XOR-swizzled 16-byte chunks, read back transposed), filled
+    // by LDS-DMA.  The pixel (K) order is row-padded and batch-inner: k = (oh * B + b) * Wp + ow with Wp a
+    // power of two >= Wo dividing KB, so a k-tile covers RT = KB / Wp whole output rows (oh fixed, b0..b0+RT-1;
+    // the host guarantees B % RT == 0).  Every slot's byte offset is then fixed for the whole loop except
+    // for the kernel-row bounds check of A, redone when oh changes (every B / RT k-tiles); the k-tile's
+    // (b0, oh) position is the scalar soffset; padding columns, padding pixels and rows past M / N read zeros.
+    constexpr int kOOB = (int)0x80000000u;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const Geo& g = p.g;
+    const int Wp = 1 << p.wp_log, RT = KB >> p.wp_log;
+    const int HWC = g.H * g.W * g.C, HoWoCo = g.Ho * g.Wo * g.Co;
+    const BufRes rsa = buf_res(reinterpret_cast<const char*>(p.a) - 2 * (long long)p.a_shift, p.a_bytes);
+    const BufRes rsb = buf_res(p.b, p.b_bytes);
+    constexpr int RPA = 1024 / (BM * 2), RPB_ = 1024 / (BN * 2);  // k rows per 1 KiB LDS-DMA instruction
+    int afix[AS], akh[AS], avo[AS], bvo[BS];
+    bool aok[AS];
+#pragma unroll
+    for (int i = 0; i < AS; ++i) {
+      const int row = (wv * AS + i) * RPA + lane / CHA;
+      const int m = m0 + ((lane % CHA) ^ swzc<BM>(row)) * 8;
+      const int rr = row >> p.wp_log, ow = row & (Wp - 1);
+      const KPos t = kpos_of(m < p.M ? m : 0, g.C, g.KW);
+      const int iw = ow * g.sw - g.pl + t.kw;
+      aok[i] = m < p.M && ow < g.Wo && (unsigned)iw < (unsigned)g.W;
+      afix[i] = rr * HWC + (t.kh * g.W + ow * g.sw + t.kw) * g.C + t.c;  // >= 0 relative to X - a_shift
+      akh[i] = t.kh - g.pt;
+      avo[i] = kOOB;
+    }
+#pragma unroll
+    for (int j = 0; j < BS; ++j) {
+      const int row = (wv * BS + j) * RPB_ + lane / CHB;
+      const int n = n0 + ((lane % CHB) ^ swzc<BN>(row)) * 8;
+      const int rr = row >> p.wp_log, ow = row & (Wp - 1);
+      bvo[j] = (n < p.N && ow < g.Wo) ? (rr * HoWoCo + ow * g.Co + n) * 2 : kOOB;
+    }
+    const int R0 = kt0 * RT;  // pixel row (oh * B + b) of the next k-tile to issue
+    int noh = R0 / g.B, nb0 = R0 - noh * g.B;
+    bool newoh = true;
+    char* const lds = reinterpret_cast<char*>(smem);
+    auto issue = [&](int stage) {
+      const int oh = noh, b0 = nb0;
+      const bool fresh = newoh;
+      nb0 += RT;
+      newoh = nb0 >= g.B;
+      if (newoh) {
+        nb0 -= g.B;
+        ++noh;
+      }
+      if (fresh) {
+#pragma unroll
+        for (int i = 0; i < AS; ++i)
+          avo[i] = (aok[i] && (unsigned)(oh * g.sh + akh[i]) < (unsigned)g.H) ? afix[i] * 2 : kOOB;
+      }
+      const int soa = (b0 * HWC + oh * g.sh * g.W * g.C) * 2;
+      const int sob = (b0 * HoWoCo + oh * g.Wo * g.Co) * 2;
+      char* ab = lds + stage * AIMG * 2 + wv * AS * 1024;
+      char* bb = lds + NBUF * AIMG * 2 + stage * BIMG * 2 + wv * BS * 1024;
+#pragma unroll
+      for (int i = 0; i < AS; ++i) buf_lds16(rsa, ab + i * 1024, avo[i], soa);
+#pragma unroll
+      for (int j = 0; j < BS; ++j) buf_lds16(rsb, bb + j * 1024, bvo[j], sob);
+    };
+    auto compute = [&](int stage) {
+      const bf16* a = As + stage * AIMG;
+      const bf16* b = Bs + stage * BIMG;
+#pragma unroll
+      for (int kk = 0; kk < KB; kk += 32) {
+        bf16x8 af[MI], bfr[NI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) af[i] = tr_frag<BM>(a, wm * WTM + i * 16, lane, kk);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) bfr[j] = tr_frag<BN>(b, wn * WTN + j * 16, lane, kk);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+      }
+    };
+    const int nk = kt1 - kt0;
+    if (nk > 0) {
+#pragma unroll
+      for (int st = 0; st < S - 1; ++st)
+        if (st < nk) issue(st);
+      int cst = 0, ist = S - 1;
+      for (int rel = 0; rel < nk; ++rel) {
+        const int after = min(S - 2, nk - 1 - rel);
+        if (after >= 2) vm_wait<2 * (AS + BS)>();
+        else if (after == 1) vm_wait<AS + BS>();
+        else vm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        if (rel + S - 1 < nk) issue(ist);
+        compute(cst);
+        cst = cst == S - 1 ? 0 : cst + 1;
+        ist = ist == S - 1 ? 0 : ist + 1;
+      }
+      vm_wait<0>();
+    }
+  } else if constexpr (GLDS) {
     // LDS-DMA staging (buffer_load_dwordx4 ... lds over raw buffer resources of A and B).
     // Instruction j = wave*AS + i fills rows j*RPI + lane/KV, physical chunk lane%KV, which holds
     // logical chunk (lane%KV) ^ swz(row).  The host only takes this path when every k-tile lies inside
@@ -2415,6 +2522,19 @@ static unsigned long long g_big_launches = 0;
 static int g_xcd = -1;
 // split-K weight gradients with at most this many splits store partials + reduce; more splits use atomics
 static int g_wg_scratch_max = 16;
+// weight gradients through the row-padded LDS-DMA path (TDE_WGRAD_DMA=0: the register-staged loaders)
+// 0 = off, 1 = 3 LDS stages, 2 = 2 stages, 3 = per shape (default; bench/resnet_layers.py --sweep-wgrad,
+// profiles/r2_sweep_wgrad.txt): Co <= 64 (ResNet stage 1) keeps the register-staged loaders (the row padding
+// costs more than it saves), strided / 1x1 convs take 128 x 64 tiles at 3 stages (twice the workgroups of
+// their short pixel loops), the other convs 128 x 128 at 2 stages (two workgroups per CU)
+static int g_wg_dma = [] {
+  const char* e = getenv("TDE_WGRAD_DMA");
+  return e ? atoi(e) : 3;
+}();
+TDE_API void tde_igemm_wgrad_dma(int mode) { g_wg_dma = mode; }
+// weight-gradient tile cap under a forced g_wg_dma mode (sweeps): 1 = 128 x 64 / 64 x 128 at most
+static int g_wg_tile_cap = 0;
+TDE_API void tde_igemm_wgrad_tile_cap(int v) { g_wg_tile_cap = v; }
 // fwd / dgrad / dense tile choice: the largest of 128x128, 128x64, 64x64 with >= g_tile_min workgroups.
 // 2048 (~8 per CU) measured best on ResNet-18 at batch 64 (bench/resnet_layers.py --sweep-tile: fwd
 // 671 -> 637 us, dgrad 832 -> 825 us per step vs 512); TDE_IGEMM_TILE_MIN overrides.
@@ -2442,8 +2562,8 @@ TDE_API void tde_igemm_tune(int wg_target, int wg_min_kt, int kb_force, int glds
 // Split-K factor of a weight-gradient GEMM (row-contiguous operands, 128/64 tiles): fill the chip with
 // ~g_wg_target workgroups, >= g_wg_min_kt k-tiles per split (every split ends in a BM x BN partial
 // sum), but never fewer than ~256 workgroups while K allows 2 k-tiles per split (1x1 projections).
-static int wgrad_splits(int M, int N, int K, int KB, int* ktiles_per_split) {
-  const int bm = M > 64 ? 128 : 64, bn = N > 64 ? 128 : 64;
+static int wgrad_splits(int M, int N, int K, int KB, int* ktiles_per_split, bool cap = false) {
+  const int bm = M > 64 ? 128 : 64, bn = (N > 64 && !(cap && bm == 128)) ? 128 : 64;
   const int ktiles = (K + KB - 1) / KB;
   const long long t = (long long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   long long sp = (g_wg_target + t - 1) / t;
@@ -2462,7 +2582,8 @@ static int wgrad_splits(int M, int N, int K, int KB, int* ktiles_per_split) {
 // f32 elements of split-K scratch a weight gradient of this shape uses (0: no split)
 TDE_API long long tde_igemm_wgrad_scratch_elems(int M, int N, int K) {
   const int KB = g_kb_force ? g_kb_force : (K < 256 ? 32 : 64);
-  const int sp = wgrad_splits(M, N, K, KB, nullptr);
+  // the LDS-DMA weight gradient runs over a row-padded pixel count < 2 K: size for that bound (splits grow with K)
+  const int sp = wgrad_splits(M, N, K < (1 << 29) ? 2 * K : K, KB, nullptr);
   return (sp > 1 && sp <= g_wg_scratch_max) ? (long long)sp * M * N : 0;
 }
 
@@ -2549,6 +2670,38 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   // profiles/r2_sweep_fd.txt, 18 ResNet-18 dgrads 834 -> ~640 us)
   const int KB = g_kb_force ? g_kb_force
                             : (dgrad_big ? 64 : (akind == A_DGRAD ? (p.g.Co % 64 == 0 ? 64 : 32) : (K < 256 ? 32 : 64)));
+  // LDS-DMA weight gradient: pixels in the row-padded order of the kernel's row-vector LDS-DMA path
+  // (Wp = pow2 >= Wo dividing KB; B a multiple of the output rows per k-tile; 32-bit operand offsets)
+  bool wg_dma = false, wg_cap = false;
+  int wg_stages = 3;
+  if (akind == A_WGRAD && bkind == B_KN && g_glds && g_wg_dma && KB == 64 && !phase && aligned16(a) && aligned16(b) &&
+      (g_wg_dma != 3 || N > 64) &&
+      p.g.C % 8 == 0 && p.g.Co % 8 == 0 && ldb == p.g.Co && N == p.g.Co && M == p.g.KH * p.g.KW * p.g.C &&
+      K == p.g.B * p.g.Ho * p.g.Wo) {
+    int wl = 0;
+    while ((1 << wl) < p.g.Wo) ++wl;
+    const int RT = wl <= 6 ? 64 >> wl : 0;
+    const long long shift = ((long long)p.g.pt * p.g.W + p.g.pl) * p.g.C;
+    const long long ae = (long long)p.g.B * p.g.H * p.g.W * p.g.C + shift;
+    const long long be = (long long)p.g.B * p.g.Ho * p.g.Wo * p.g.Co;
+    const long long kp = (long long)p.g.Ho * p.g.B * (1LL << wl);
+    if (RT >= 1 && p.g.B % RT == 0 && ae * 2 < (1LL << 31) - 16 && be * 2 < (1LL << 31) - 16 && kp < (1LL << 30)) {
+      wg_dma = true;
+      if (g_wg_dma == 3) {
+        wg_cap = p.g.sh > 1 || p.g.sw > 1 || (p.g.KH == 1 && p.g.KW == 1);
+        wg_stages = wg_cap ? 3 : 2;
+      } else {
+        wg_cap = g_wg_tile_cap != 0;
+        wg_stages = g_wg_dma == 2 ? 2 : 3;
+      }
+      p.wp_log = wl;
+      p.a_shift = (int)shift;
+      p.a_bytes = (int)(ae * 2);
+      p.b_bytes = (int)(be * 2);
+      K = (int)kp;
+      p.K = K;
+    }
+  }
   const int ktiles = (K + KB - 1) / KB;
   const bool auto_splits = splits == 0;
   if (splits < 1) splits = 1;
@@ -2589,8 +2742,9 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   if (rowk) {
     bm = M > 64 ? 128 : 64;
     bn = N > 64 ? 128 : 64;
+    if (wg_cap && bm == 128 && bn == 128) bn = 64;
     if (auto_splits) {
-      splits = wgrad_splits(M, N, K, KB, &p.ktiles_per_split);
+      splits = wgrad_splits(M, N, K, KB, &p.ktiles_per_split, wg_cap);
     }
   } else if (N > 64 && tiles(128, 128) >= g_tile_min) {
     bm = bn = 128;
@@ -2613,7 +2767,7 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     p.cf_mode = 3;
   }
   const bool vec = p.avec && p.bvec;
-  if (rowk && vec) {  // the weight-gradient fast loaders index with 32-bit offsets
+  if (rowk && vec && !wg_dma) {  // the weight-gradient fast loaders index with 32-bit offsets
     const long long asz = akind == A_WGRAD ? (long long)p.g.B * p.g.H * p.g.W * p.g.C : (long long)K * lda;
     if (asz >= (1LL << 31) || (long long)K * ldb >= (1LL << 31) || (long long)M * N >= (1LL << 31)) return -6;
   }
@@ -2630,8 +2784,10 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     if (bkind == B_NK) be = (long long)(N - 1) * ldb + K;
     else if (bkind == B_DGRADW) be = (long long)p.g.KH * p.g.KW * p.g.C * p.g.Co;
     if (ae * 2 >= (1LL << 31) - 16 || be * 2 >= (1LL << 31) - 16) ut = false;
-    p.a_bytes = (int)(ae * 2 < (1LL << 31) ? ae * 2 : 0);
-    p.b_bytes = (int)(be * 2 < (1LL << 31) ? be * 2 : 0);
+    if (!wg_dma) {
+      p.a_bytes = (int)(ae * 2 < (1LL << 31) ? ae * 2 : 0);
+      p.b_bytes = (int)(be * 2 < (1LL << 31) ? be * 2 : 0);
+    }
   }
   // big tiles (256 x 64 with 64 x 64 per wave, or 256 x 128 with 128 x 64 per wave): fwd/dense when
   // tuned on (fwd 641 -> 840 us on ResNet-18 with them), dgrad when g_big_dgrad
@@ -2683,6 +2839,12 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     else if (bm == 128) TDE_IGEMM(A_COLM, B_KN, 128, 64);
     else if (bn == 128) TDE_IGEMM(A_COLM, B_KN, 64, 128);
     else TDE_IGEMM(A_COLM, B_KN, 64, 64);
+  } else if (akind == A_WGRAD && bkind == B_KN && wg_dma) {
+    if (bm == 128 && bn == 128 && wg_stages == 2) igemm_kernel<A_WGRAD, B_KN, 128, 128, 64, 1, 2><<<grid, 256, 0, stream>>>(p);
+    else if (bm == 128 && bn == 128) igemm_kernel<A_WGRAD, B_KN, 128, 128, 64, 1, 3><<<grid, 256, 0, stream>>>(p);
+    else if (bm == 128) igemm_kernel<A_WGRAD, B_KN, 128, 64, 64, 1, 3><<<grid, 256, 0, stream>>>(p);
+    else if (bn == 128) igemm_kernel<A_WGRAD, B_KN, 64, 128, 64, 1, 3><<<grid, 256, 0, stream>>>(p);
+    else igemm_kernel<A_WGRAD, B_KN, 64, 64, 64, 1, 3><<<grid, 256, 0, stream>>>(p);
   } else if (akind == A_WGRAD && bkind == B_KN) {
     if (bm == 128 && bn == 128) TDE_IGEMM(A_WGRAD, B_KN, 128, 128);
     else if (bm == 128) TDE_IGEMM(A_WGRAD, B_KN, 128, 64);
