@@ -2532,6 +2532,8 @@ static int g_wg_dma = [] {
   return e ? atoi(e) : 3;
 }();
 TDE_API void tde_igemm_wgrad_dma(int mode) { g_wg_dma = mode; }
+static unsigned long long g_wg_dma_launches = 0;   // tests assert the path ran
+TDE_API unsigned long long tde_igemm_wgrad_dma_launches() { return g_wg_dma_launches; }
 // weight-gradient tile cap under a forced g_wg_dma mode (sweeps): 1 = 128 x 64 / 64 x 128 at most
 static int g_wg_tile_cap = 0;
 TDE_API void tde_igemm_wgrad_tile_cap(int v) { g_wg_tile_cap = v; }
@@ -2840,6 +2842,7 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     else if (bn == 128) TDE_IGEMM(A_COLM, B_KN, 64, 128);
     else TDE_IGEMM(A_COLM, B_KN, 64, 64);
   } else if (akind == A_WGRAD && bkind == B_KN && wg_dma) {
+    ++g_wg_dma_launches;
     if (bm == 128 && bn == 128 && wg_stages == 2) igemm_kernel<A_WGRAD, B_KN, 128, 128, 64, 1, 2><<<grid, 256, 0, stream>>>(p);
     else if (bm == 128 && bn == 128) igemm_kernel<A_WGRAD, B_KN, 128, 128, 64, 1, 3><<<grid, 256, 0, stream>>>(p);
     else if (bm == 128) igemm_kernel<A_WGRAD, B_KN, 128, 64, 64, 1, 3><<<grid, 256, 0, stream>>>(p);

@@ -53,6 +53,7 @@ _HIP_PROTOS = {
     "tde_igemm_big_dgrad": (None, [i32]),
     "tde_igemm_wgrad_dma": (None, [i32]),
     "tde_igemm_wgrad_tile_cap": (None, [i32]),
+    "tde_igemm_wgrad_dma_launches": (C.c_ulonglong, []),
     "tde_igemm_big_launches": (C.c_ulonglong, []),
     "tde_bn_fwd": (i32, [p, p, p, i64, i32, i32, p, p, p, p, f32, p, p, f32, f32, p, i32, f32, C.c_ulonglong,
                          p, i32, i32, p]),

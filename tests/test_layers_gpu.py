@@ -649,3 +649,31 @@ def test_conv_big_tiles_forced():
     finally:
         lib.tde_igemm_tune(512, 16, 0, 1, 0, 192)
         lib.tde_igemm_big_dgrad(0)
+
+
+# shapes that reach the LDS-DMA weight gradient (row-padded, batch-inner pixel order): Co > 64, C and Co
+# multiples of 8, Wo <= 64 and B a multiple of the output rows per k-tile (64 / pow2(Wo))
+WGRAD_DMA_CASES = [
+    (8, 14, 14, 64, 128, 3, 1, "same"),    # stride 1 -> 128x128 tiles at 2 stages (Wo 14 -> 16-wide rows)
+    (8, 15, 15, 64, 128, 3, 2, "same"),    # stride 2 -> 128x64 at 3 stages, asymmetric TF pads
+    (8, 16, 16, 64, 128, 1, 2, "valid"),   # 1x1 stride-2 projection
+    (8, 7, 7, 128, 96, 3, 1, "same"),      # Wo 7 (8-wide rows, 8 batch rows per k-tile), N tail of 96
+    (4, 28, 28, 24, 96, 3, 1, "same"),     # M = 216: partial M tile, C = 24 (three 8-channel chunks per tap)
+]
+
+
+@pytest.mark.parametrize("mode", [3, 1, 2])
+def test_conv_wgrad_lds_dma_paths(mode):
+    """Every conv case above through the LDS-DMA weight gradient (auto per-shape choice, forced 3 stages,
+    forced 2 stages) against the float64 references of test_conv_fwd_dgrad_wgrad; the launch counter
+    proves the path ran; the default (3 = per shape) is restored after."""
+    from tensorflow_distributed_example_amd import _native as N
+    lib = N.hip()
+    try:
+        lib.tde_igemm_wgrad_dma(mode)
+        for c in WGRAD_DMA_CASES:
+            n0 = lib.tde_igemm_wgrad_dma_launches()
+            test_conv_fwd_dgrad_wgrad(*c)
+            assert lib.tde_igemm_wgrad_dma_launches() > n0, c
+    finally:
+        lib.tde_igemm_wgrad_dma(3)
