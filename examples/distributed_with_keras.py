@@ -20,6 +20,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import tensorflow_distributed_example_amd as tde  # noqa: E402
 
+from tensorflow_distributed_example_amd.utils import flags as fw  # noqa: E402
+
+# framework flags (--devices/--dtype/--synthetic/--profile-steps) take effect before the
+# strategy below is built, as the reference builds it at import time (DWK:16)
+FW_ARGS = fw.apply_framework_flags(fw.add_framework_flags(argparse.ArgumentParser(add_help=False))
+                                   .parse_known_args()[0])
+
 tfds = tde.tfds
 tfds.disable_progress_bar()
 
@@ -63,6 +70,8 @@ def main(argv=None):
     ap.add_argument("--epochs", type=int, default=3)
     ap.add_argument("--steps-per-epoch", type=int, default=5)
     ap.add_argument("--verbose", type=int, default=1)
+    ap.add_argument("--profile-dir", default="/tmp/dwk_profile", help="where --profile-steps timelines go")
+    fw.add_framework_flags(ap)
     args, _ = ap.parse_known_args(argv)
     with strategy.scope():
         # Creation of dataset, and model building/compiling need to be within `strategy.scope()`.
@@ -74,7 +83,8 @@ def main(argv=None):
     # Keras' `model.fit()` trains the model with specified number of epochs and number of steps per epoch.
     history = multi_worker_model.fit(x=train_datasets_no_auto_shard, epochs=args.epochs,
                                      steps_per_epoch=args.steps_per_epoch,
-                                     verbose=args.verbose if strategy.is_chief else 0)
+                                     verbose=args.verbose if strategy.is_chief else 0,
+                                     callbacks=fw.profiler_callbacks(args, args.profile_dir))
     return history
 
 

@@ -43,6 +43,7 @@ def get_args(argv=None):
     parser.add_argument("--reference-steps", action="store_true",
                         help="reproduce the reference's one-epoch max_steps = len(train)/batch_size (Q2)")
     parser.add_argument("--no-tensorboard", action="store_true")
+    tde.utils.flags.add_framework_flags(parser)
     args, _ = parser.parse_known_args(argv)
     return args
 
@@ -135,7 +136,7 @@ def train_and_evaluate(args):
     estimator = create_model(model_dir=args.working_dir, config=run_config, learning_rate=args.learning_rate)
     train_spec = tde.estimator.TrainSpec(
         input_fn=lambda: input_fn(train_images, train_labels, args.batch_size, mode=tde.estimator.ModeKeys.TRAIN),
-        max_steps=train_steps)
+        max_steps=train_steps, hooks=tde.utils.flags.profiler_hooks(args, args.working_dir))
     exporter = tde.estimator.FinalExporter("exporter", serving_input_fn)
     eval_spec = tde.estimator.EvalSpec(
         input_fn=lambda: input_fn(test_images, test_labels, args.batch_size, mode=tde.estimator.ModeKeys.EVAL),
@@ -153,7 +154,7 @@ def train_and_evaluate(args):
 
 
 if __name__ == "__main__":
-    args = get_args()
+    args = tde.utils.flags.apply_framework_flags(get_args())
     logger = tde.get_logger()
     logger.setLevel(args.verbosity)
     out = train_and_evaluate(args)

@@ -10,6 +10,7 @@ train_and_evaluate.  The reference's unused custom ``model_fn`` (TF2M:65-91) is
 kept, fixed (Q9), as an example of a custom Estimator model_fn.
 TF_CONFIG must be set externally for distributed runs (no CLUSTER_SPEC translation).
 """
+import argparse
 import logging
 import math
 import os
@@ -88,7 +89,11 @@ def serving_input_fn():
     return tde.estimator.export.TensorServingInputReceiver(feature_placeholder, feature_placeholder)
 
 
-def main():
+def main(argv=None):
+    # the reference has no CLI (its parser is commented out, TF2M:28-31): only the framework flags
+    ap = tde.utils.flags.add_framework_flags(argparse.ArgumentParser())
+    args, _ = ap.parse_known_args(argv)
+    tde.utils.flags.apply_framework_flags(args)
     logging.getLogger().setLevel(logging.INFO)
     tde.get_logger().setLevel(logging.INFO)
     strategy = tde.distribute.experimental.ParameterServerStrategy()
@@ -103,7 +108,7 @@ def main():
     classifier = create_model(model_dir=MODEL_DIR, config=config, learning_rate=LEARNING_RATE)
     train_spec = tde.estimator.TrainSpec(
         input_fn=lambda: input_fn(train_images, train_labels, BATCH_SIZE, mode=tde.estimator.ModeKeys.TRAIN),
-        max_steps=train_steps)
+        max_steps=train_steps, hooks=tde.utils.flags.profiler_hooks(args, MODEL_DIR))
     exporter = tde.estimator.FinalExporter("exporter", serving_input_fn)
     eval_spec = tde.estimator.EvalSpec(
         input_fn=lambda: input_fn(test_images, test_labels, BATCH_SIZE, mode=tde.estimator.ModeKeys.EVAL),

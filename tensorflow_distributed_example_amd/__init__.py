@@ -126,3 +126,5 @@ ConfigProto = _estimator.SessionConfig
 from .utils import debug  # noqa: E402
 
 _callbacks.ReplicaConsistencyCheck = debug.ReplicaConsistencyCheck
+from . import utils  # noqa: E402
+from .utils import flags as _flags  # noqa: E402,F401  (tde.utils.flags: the examples' framework flags)

@@ -65,7 +65,25 @@ def local_rank() -> int:
     return int(os.environ.get("LOCAL_RANK", "0"))
 
 
+_default_devices = None   # --devices: what a strategy built without devices uses
+
+
+def set_default_devices(devices):
+    """Devices strategies use when constructed without an explicit list (``--devices``): a list of
+    ``"cpu"`` / ``"gpu:N"`` / ``"cuda:N"`` strings or torch devices, or None for all local GPUs (else CPU)."""
+    global _default_devices
+    _default_devices = None if devices is None else [str(d).strip() for d in devices if str(d).strip()]
+
+
+def default_devices():
+    return _default_devices
+
+
 def default_device() -> torch.device:
+    if _default_devices:
+        d = _default_devices[0].lower()
+        if d.startswith("/cpu") or d.startswith("cpu"):
+            return torch.device("cpu")
     if gpu_available():
         n = torch.cuda.device_count()
         return torch.device("cuda", local_rank() % max(n, 1))

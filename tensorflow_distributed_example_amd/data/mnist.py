@@ -57,6 +57,8 @@ def _find(path):
 
 
 def load_data(path=None, synthetic_data=None, seed=0):
+    if synthetic_data is None:
+        synthetic_data = os.environ.get("TDE_SYNTHETIC_MNIST", "0") not in ("", "0")   # --synthetic
     f = None if synthetic_data else _find(path)
     if f is not None:
         with np.load(f, allow_pickle=False) as d:

@@ -195,6 +195,8 @@ class Strategy:
 
 
 def _parse_devices(devices):
+    if devices is None and Kb.default_devices():
+        devices = Kb.default_devices()
     if devices is None:
         if torch.cuda.is_available():
             return [torch.device("cuda", i) for i in range(torch.cuda.device_count())]
@@ -263,7 +265,9 @@ class MultiWorkerMirroredStrategy(Strategy):
         self.topology = topo
         gpw = gpus_per_worker or int(os.environ.get("TDE_GPUS_PER_WORKER", "1"))
         use_gpu = torch.cuda.is_available()
-        if use_gpu:
+        if Kb.default_devices() and gpus_per_worker is None and "TDE_GPUS_PER_WORKER" not in os.environ:
+            devs = _parse_devices(None)   # --devices: this worker's local replicas
+        elif use_gpu:
             ndev = torch.cuda.device_count()
             if topo.world == 1 and topo.source == "local" and gpus_per_worker is None and \
                     "TDE_GPUS_PER_WORKER" not in os.environ:

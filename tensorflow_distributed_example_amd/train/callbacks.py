@@ -153,6 +153,32 @@ class BackupAndRestore(Callback):
             shutil.rmtree(self.backup_dir, ignore_errors=True)
 
 
+class ProfilerCallback(Callback):
+    """Keras-side counterpart of the Estimator ProfilerHook (MKD:235-237; TF's TensorBoard
+    ``profile_batch``): every ``every_n_steps`` training steps (and the first), one step is recorded with
+    torch.profiler (host + ROCm activity) into ``<log_dir>/timeline-<step>.json`` (Chrome trace)."""
+
+    def __init__(self, log_dir, every_n_steps=100, show_memory=True):
+        super().__init__()
+        from .hooks import ProfilerHook
+        self._hook = ProfilerHook(save_steps=every_n_steps, output_dir=log_dir, show_memory=show_memory)
+        self._step = 0
+
+    @property
+    def written(self):
+        return self._hook.written
+
+    def on_train_batch_begin(self, batch, logs=None):
+        self._hook.before_step(None, self._step + 1)
+
+    def on_train_batch_end(self, batch, logs=None):
+        self._step += 1
+
+        class _Ctx:
+            global_step = self._step
+        self._hook.after_step(_Ctx)
+
+
 class LambdaCallback(Callback):
     def __init__(self, on_epoch_end=None, on_train_batch_end=None, **kw):
         super().__init__()

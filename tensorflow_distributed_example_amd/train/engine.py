@@ -137,6 +137,7 @@ def fit(model, x=None, y=None, batch_size=None, epochs=1, verbose="auto", callba
             if not group:
                 break
             full = [all(len(r[1]) == prog.B for r in g) for g in group]
+            cl.on_train_batch_begin(step)
             if len(group) == S and all(full):
                 prog.stage(_stack_steps(group))
                 prog.run()
@@ -151,9 +152,8 @@ def fit(model, x=None, y=None, batch_size=None, epochs=1, verbose="auto", callba
                 prog.sync()
                 debug.check_replicas(model, f"after step {model.optimizer.iterations + step}")
             fault.maybe_inject(model.optimizer.iterations + step)
-            if chief and verbose:
-                cl.on_train_batch_end(step - 1, logs_from(prog.local_metrics(), model._metric_names)
-                                      if verbose == 1 and _due(prog) else None)
+            cl.on_train_batch_end(step - 1, logs_from(prog.local_metrics(), model._metric_names)
+                                  if chief and verbose == 1 and _due(prog) else None)
         if steps_per_epoch is not None and step < steps_per_epoch and exhausted:
             print("WARNING: your input ran out of data; interrupting training. Make sure that your dataset can "
                   f"generate at least `steps_per_epoch * epochs` batches ({steps_per_epoch * epochs}).")

@@ -85,3 +85,39 @@ def test_tf2_mnist_distributed_local(tmp_path):
                    _env(TDE_MODEL_DIR=str(tmp_path / "mode"), TDE_MAX_STEPS="20"))
     assert rc == 0, out
     assert list((tmp_path / "mode").glob("model.ckpt-20.index")), out
+
+
+def test_framework_flags_devices_dtype_synthetic_profile(tmp_path, monkeypatch):
+    """SURVEY.md §5.6 framework flags: --devices / --dtype / --synthetic set the global state strategies and
+    loaders read; --profile-steps yields a ProfilerCallback (Keras) that writes Chrome-trace timelines."""
+    import argparse
+
+    import numpy as np
+
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd import backend as Kb
+    from tensorflow_distributed_example_amd.utils import flags as fw
+    monkeypatch.delenv("TDE_SYNTHETIC_MNIST", raising=False)
+    ap = fw.add_framework_flags(argparse.ArgumentParser())
+    args = ap.parse_args(["--devices", "cpu,cpu", "--dtype", "fp32", "--synthetic", "--profile-steps", "2"])
+    try:
+        fw.apply_framework_flags(args)
+        assert Kb.global_policy().name == "float32"
+        assert tde.keras.datasets.mnist.load_data()[0][0].shape == (60000, 28, 28)
+        strategy = tde.distribute.MirroredStrategy()
+        assert strategy.num_replicas_in_sync == 2 and all(d.type == "cpu" for d in strategy.local_devices)
+        cbs = fw.profiler_callbacks(args, str(tmp_path))
+        with strategy.scope():
+            m = tde.zoo.mnist_cnn()
+            m.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True),
+                      optimizer=tde.optimizers.SGD(0.01), metrics=["accuracy"])
+        x = np.random.default_rng(0).random((8 * 16, 28, 28, 1), dtype=np.float32)
+        y = np.random.default_rng(1).integers(0, 10, 8 * 16)
+        m.fit(x, y, batch_size=16, epochs=1, verbose=0, callbacks=cbs)
+        assert cbs[0].written and all((tmp_path / p.split("/")[-1]).exists() for p in cbs[0].written)
+        assert len(fw.profiler_hooks(args, str(tmp_path))) == 1
+    finally:
+        Kb.set_default_devices(None)
+        Kb.set_global_policy(None)
+        monkeypatch.delenv("TDE_SYNTHETIC_MNIST", raising=False)
+        monkeypatch.delenv("TDE_EXECUTOR", raising=False)
