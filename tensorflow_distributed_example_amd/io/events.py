@@ -102,7 +102,7 @@ def _fields(b):
 
 
 def parse_event(rec: bytes) -> dict:
-    ev = {"scalars": {}}
+    ev = {"scalars": {}, "step": 0}   # proto3: a zero step is not on the wire
     for f, wt, v in _fields(rec):
         if f == 1 and wt == 1:
             ev["wall_time"] = struct.unpack("<d", v)[0]

@@ -677,3 +677,26 @@ def test_conv_wgrad_lds_dma_paths(mode):
             assert lib.tde_igemm_wgrad_dma_launches() > n0, c
     finally:
         lib.tde_igemm_wgrad_dma(3)
+
+
+def _hyp():
+    from hypothesis import HealthCheck, given, settings
+    from hypothesis import strategies as st
+    return HealthCheck, given, settings, st
+
+
+_HC, _given, _settings, _st = _hyp()
+
+
+@_settings(max_examples=30, deadline=None, suppress_health_check=[_HC.too_slow], derandomize=True)
+@_given(B=_st.integers(1, 4), H=_st.integers(3, 20), W=_st.integers(3, 20), C=_st.sampled_from([1, 3, 8, 16, 24, 64]),
+        Co=_st.sampled_from([6, 8, 16, 40, 64, 96, 128]), k=_st.integers(1, 5), s=_st.integers(1, 3),
+        pad=_st.sampled_from(["same", "valid"]))
+def test_conv_kernels_random_geometries(B, H, W, C, Co, k, s, pad):
+    """Property test: random (B, H, W, C, Co, k, s, padding) — TF-SAME asymmetric pads,
+    strides 1-3, channel counts on and off the 16-byte vector paths — through the HIP implicit-GEMM fwd /
+    dgrad (stride-phase) / wgrad against the float64 references of test_conv_fwd_dgrad_wgrad.  Derandomized
+    so a GPU run is reproducible."""
+    if pad == "valid" and (k > H or k > W):
+        return
+    test_conv_fwd_dgrad_wgrad(B, H, W, C, Co, k, s, pad)
