@@ -72,6 +72,8 @@ _HIP_PROTOS = {
     "tde_smallconv_wgrad": (i32, [p, p, p, p, p]),
     "tde_smallconv_wgrad_ok": (i32, [i32, i32, i32, i32]),
     "tde_im2col": (i32, [p, p, i32, p, p, p, p]),
+    "tde_stem_pack": (i32, [p, p, p, p, p, p]),
+    "tde_stem_unpack_wgrad": (i32, [p, p, p, p]),
     # RCCL
     "tde_nccl_version": (i32, []),
     "tde_nccl_error_string": (C.c_char_p, [i32]),

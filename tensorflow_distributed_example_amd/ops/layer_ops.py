@@ -182,6 +182,38 @@ def im2col(x, g: ConvGeom, xcol, Wt=None, Wt_pad=None):
     return Kp
 
 
+# ---------------------------------------------------------------- packed stem (C <= 4, stride 2 along W)
+def stem_geometry(g: ConvGeom):
+    """The packed stem's virtual conv (csrc/kernels/layers.hip tde_stem_pack): input [B, Hp, Wv, 8] (two
+    real pixels x 4 channels per virtual pixel), KW' = ceil(KW/2) taps, stride (sh, 1), valid."""
+    kwv = -(-g.KW // 2)
+    hp, wv = (g.Ho - 1) * g.sh + g.KH, g.Wo + kwv - 1
+    return ConvGeom(g.B, hp, wv, 8, g.Ho, g.Wo, g.Co, g.KH, kwv, g.sh, 1, 0, 0)
+
+
+def stem_pack_ok(g: ConvGeom):
+    """Eligible: C <= 4, stride 2 along W, and the virtual conv's kernel row is one 32-wide k-tile (KW in
+    7..8) or the 16-byte vector path (any KW)."""
+    return g.C <= 4 and g.sw == 2 and g.KW >= 2
+
+
+def stem_pack(x, g: ConvGeom, xp, Wt=None, Wv=None):
+    gv = stem_geometry(g)
+    _bf(x, g.B * g.H * g.W * g.C, "stem_pack x")
+    _bf(xp, gv.B * gv.H * gv.W * 8, "stem_pack xp")
+    if Wt is not None:
+        _req(tuple(Wt.shape) == (g.Co, g.K) and Wt.dtype == bf16 and Wt.is_contiguous(), "stem_pack Wt")
+        _bf(Wv, g.Co * gv.K, "stem_pack Wv")
+    N.check(N.hip().tde_stem_pack(_P(x), g.carray(), _P(xp), _P(Wt), _P(Wv), _s()), "tde_stem_pack")
+
+
+def stem_unpack_wgrad(gWv, g: ConvGeom, gW):
+    gv = stem_geometry(g)
+    _f32(gWv, gv.K * g.Co, "stem_unpack gWv")
+    _f32(gW, g.K * g.Co, "stem_unpack gW")
+    N.check(N.hip().tde_stem_unpack_wgrad(_P(gWv), g.carray(), _P(gW), _s()), "tde_stem_unpack_wgrad")
+
+
 def conv_fwd_im2col(xcol, Wt_pad, y, g: ConvGeom, Kp, bias=None, relu=False, colstats=None, scratch=None):
     M = g.B * g.Ho * g.Wo
     _bf(y, M * g.Co, "conv_fwd_im2col y")

@@ -396,6 +396,7 @@ class _Gemm(_Stage):
         self.need_dgrad = need_dgrad
         self.shadows = {self.wname: ("row", "col") if need_dgrad else ("col",)}
         self.small_fwd = self.small_dgrad = self.small_wgrad = False
+        self.use_im2col = self.use_stem_pack = False
         if self.conv:
             H, W_, C = tin.shape
             Ho, Wo, Co = tout.shape
@@ -417,6 +418,12 @@ class _Gemm(_Stage):
                 self.shadows = {self.wname: ("row", "col")}
             # channel counts that defeat 16-byte gathers (RGB stem): explicit im2col + vector GEMMs
             self.use_im2col = (not self.small_fwd and C % 8 != 0 and os.environ.get("TDE_IM2COL", "1") != "0")
+            # the RGB stem as a packed virtual conv through the LDS-DMA implicit GEMM (no im2col matrix);
+            # input layer only (no input gradient in the packed layout)
+            self.use_stem_pack = (self.use_im2col and not need_dgrad and O.stem_pack_ok(self.geo)
+                                  and os.environ.get("TDE_STEM_PACK", "1") != "0")
+            if self.use_stem_pack:
+                self.use_im2col = False
             # filters whose K*Co partial sums fit in registers (Model B conv1: 3x3x1 -> 6)
             self.small_wgrad = narrow and not self.use_im2col and O.smallconv_wgrad_ok(self.geo)
         self.colstats = None
@@ -436,10 +443,18 @@ class _Gemm(_Stage):
             g = self.geo.with_batch(B)
             if self.use_im2col or self.small_wgrad:
                 return 0
+            if self.use_stem_pack:
+                gv = O.stem_geometry(g)
+                return O.wgrad_scratch_elems(gv.K, gv.Co, gv.B * gv.Ho * gv.Wo)
             return O.wgrad_scratch_elems(g.K, g.Co, g.B * g.Ho * g.Wo)
         return O.wgrad_scratch_elems(self.W.shape[0], self.W.shape[1], self.inp.rows(B))
 
     def alloc(self, B, dev):
+        if self.conv and self.use_stem_pack:
+            gv = O.stem_geometry(self.geo.with_batch(B))
+            self.xp = torch.zeros(gv.B * gv.H * gv.W * 8, dtype=bf16, device=dev)
+            self.Wv = torch.zeros(gv.Co * gv.K, dtype=bf16, device=dev)
+            self.gWv = torch.zeros(gv.K * gv.Co, dtype=torch.float32, device=dev)
         if self.conv and self.use_im2col:
             g = self.geo.with_batch(B)
             self.Kp = -(-g.K // 8) * 8
@@ -459,7 +474,12 @@ class _Gemm(_Stage):
 
     def fwd(self, p, B, training, mode="train"):
         cs = self.colstats if (self.stats and training) else None
-        if self.conv and self.use_im2col:
+        if self.conv and self.use_stem_pack:
+            g = self.geo.with_batch(B)
+            O.stem_pack(self.inp.buf, g, self.xp, self.Wt, self.Wv)
+            O.conv_fwd(self.xp, self.Wv.view(g.Co, -1), self.out.root().buf, O.stem_geometry(g), bias=self.b,
+                       relu=self.relu, colstats=cs, scratch=p.scratch)
+        elif self.conv and self.use_im2col:
             g = self.geo.with_batch(B)
             O.im2col(self.inp.buf, g, self.xcol, self.Wt, self.Wt_pad)
             O.conv_fwd_im2col(self.xcol, self.Wt_pad, self.out.root().buf, g, self.Kp, bias=self.b, relu=self.relu,
@@ -483,7 +503,10 @@ class _Gemm(_Stage):
             dout = self.dz
         if self.conv:
             g = self.geo.with_batch(B)
-            if self.use_im2col:
+            if self.use_stem_pack:
+                O.conv_wgrad(self.xp, dout, self.gWv, O.stem_geometry(g), scratch=p.wscratch)
+                O.stem_unpack_wgrad(self.gWv, g, self.gW)
+            elif self.use_im2col:
                 O.conv_wgrad_im2col(self.xcol, dout, self.gW, g, self.Kp)
             elif self.small_wgrad:
                 O.smallconv_wgrad(self.inp.buf, dout, self.gW, g)

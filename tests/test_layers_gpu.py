@@ -700,3 +700,39 @@ def test_conv_kernels_random_geometries(B, H, W, C, Co, k, s, pad):
     if pad == "valid" and (k > H or k > W):
         return
     test_conv_fwd_dgrad_wgrad(B, H, W, C, Co, k, s, pad)
+
+
+@pytest.mark.parametrize("B,H,W,C,Co,k,s", [(2, 32, 32, 3, 64, 7, 2), (3, 29, 23, 3, 16, 7, 2), (2, 20, 20, 1, 8, 3, 2),
+                                            (2, 17, 18, 4, 64, 5, 2)])
+def test_stem_pack_conv_fwd_wgrad(B, H, W, C, Co, k, s):
+    """The packed stem (tde_stem_pack: two pixels x 4 channels per virtual pixel, a valid stride-(s, 1) conv
+    with ceil(k/2) taps, row-tile LDS-DMA when that row is one 32-wide k-tile) against the float64 conv of
+    the real layer with TF-SAME pads; its weight gradient unpacked into the real [k, k, C, Co] layout."""
+    from tensorflow_distributed_example_amd.ops import layer_ops as O
+    (pt, pb), (pl, pr) = _tf_same(H, k, s), _tf_same(W, k, s)
+    Ho, Wo = -(-H // s), -(-W // s)
+    g = O.ConvGeom(B, H, W, C, Ho, Wo, Co, k, k, s, s, pt, pl)
+    gv = O.stem_geometry(g)
+    x = _r(B, H, W, C, seed=11)
+    w = _r(k, k, C, Co, seed=12, scale=0.2)
+    bias = torch.randn(Co, device=DEV)
+    xp = torch.full((gv.B * gv.H * gv.W * 8,), float("nan"), device=DEV).to(bf)
+    Wv = torch.full((Co * gv.K,), float("nan"), device=DEV).to(bf)
+    O.stem_pack(x, g, xp, w.reshape(-1, Co).t().contiguous(), Wv)
+    y = torch.zeros(B, Ho, Wo, Co, dtype=bf, device=DEV)
+    O.conv_fwd(xp, Wv.view(Co, -1), y, gv, bias=bias)
+    xr = _cpu64(x).permute(0, 3, 1, 2).requires_grad_(True)
+    wr = _cpu64(w).permute(3, 2, 0, 1).requires_grad_(True)
+    ref = F.conv2d(F.pad(xr, (pl, pr, pt, pb)), wr, _cpu64(bias), stride=s).permute(0, 2, 3, 1)
+    dy = _r(B, Ho, Wo, Co, seed=13)
+    ref.backward(_cpu64(dy))
+    torch.cuda.synchronize()
+    assert _rel(y.float(), _dev(ref.detach())) < 1e-2
+    gWv = torch.zeros(gv.K * Co, device=DEV)
+    gW = torch.randn(k, k, C, Co, device=DEV)
+    gW0 = gW.clone()
+    O.conv_wgrad(xp, dy, gWv, gv)
+    O.stem_unpack_wgrad(gWv, g, gW)
+    torch.cuda.synchronize()
+    assert _rel(gW - gW0, _dev(wr.grad.permute(2, 3, 1, 0))) < 1e-3
+    assert float(gWv.abs().max()) == 0.0   # re-armed for the next step's accumulation
