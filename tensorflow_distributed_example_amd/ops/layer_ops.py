@@ -152,13 +152,16 @@ def conv_dgrad(dy, Wrow, dx, g: ConvGeom, accum=False, scratch=None):
     _bf(dx, g.B * g.H * g.W * g.C, "conv_dgrad dx")
     if g.sh > 1 or g.sw > 1:
         phases = dgrad_phases(g)
-        if not accum and any(ph[6] * ph[7] == 0 for ph in phases):
-            # phases no tap reaches (3 of the 4 of a 1x1 stride-2 projection) are zero: one fill of dx,
-            # then the tapped phases accumulate, instead of K = 0 GEMM launches that store zeros
-            dx[: g.B * g.H * g.W * g.C].zero_()
-            accum = True
+        untapped = [ph for ph in phases if ph[6] * ph[7] == 0]
+        skip_untapped = bool(untapped) and (accum or g.C % 8 == 0)
+        if untapped and not accum:
+            # phases no tap reaches (3 of the 4 of a 1x1 stride-2 projection) are zero: one HIP pass zeroes
+            # exactly their pixels and the tapped phases store theirs, instead of K = 0 GEMM launches
+            if g.C % 8 == 0:
+                mask = sum(1 << (ph[0] * g.sw + ph[1]) for ph in untapped)
+                N.check(N.hip().tde_dgrad_phase_zero(_P(dx), g.carray(), mask, _s()), "tde_dgrad_phase_zero")
         for ph in phases:
-            if ph[6] * ph[7] == 0 and accum:
+            if ph[6] * ph[7] == 0 and skip_untapped:
                 continue
             _igemm(dy, 0, A_DGRAD, Wrow, 0, B_DGRADW, g.B * ph[2] * ph[3], g.C, ph[6] * ph[7] * g.Co, g,
                    cb=dx, ldcb=g.C, cb_accum=accum, phase=ph)

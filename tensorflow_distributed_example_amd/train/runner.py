@@ -24,6 +24,11 @@ def _ctx(dev):
     return torch.cuda.device(dev) if dev.type == "cuda" else contextlib.nullcontext()
 
 
+def _cast_bf16(src, dst):
+    from ..ops import layer_ops as O
+    O.cast_bf16(src, dst)
+
+
 class _Stager:
     """Double-buffered pinned host staging for async H2D copies into a ring."""
 
@@ -48,7 +53,10 @@ class _Stager:
             self._launch(flat_t=buf.view(-1), n=n, dst=dst)
             return
         if torch.is_tensor(arr) and arr.device == dst.device:
-            dst.view(-1)[: arr.numel()].copy_(arr.reshape(-1).to(dst.dtype), non_blocking=True)
+            if self.cuda and arr.dtype == torch.float32 and dst.dtype == torch.bfloat16:
+                _cast_bf16(arr.reshape(-1).contiguous(), dst.view(-1)[: arr.numel()])   # HIP cast kernel
+            else:
+                dst.view(-1)[: arr.numel()].copy_(arr.reshape(-1).to(dst.dtype), non_blocking=True)
             return
         if torch.is_tensor(arr):
             arr = arr.detach().cpu().numpy()
@@ -72,7 +80,10 @@ class _Stager:
             if getattr(self, "dev_tmp", None) is None or self.dev_tmp.numel() < flat_t.numel():
                 self.dev_tmp = torch.empty(flat_t.numel(), dtype=flat_t.dtype, device=dst.device)
             self.dev_tmp[:n].copy_(flat_t[:n], non_blocking=self.cuda)
-            dst.view(-1)[:n].copy_(self.dev_tmp[:n])
+            if self.cuda and self.dev_tmp.dtype == torch.float32 and dst.dtype == torch.bfloat16:
+                _cast_bf16(self.dev_tmp[:n], dst.view(-1)[:n])
+            else:
+                dst.view(-1)[:n].copy_(self.dev_tmp[:n])
         else:
             dst.view(-1)[:n].copy_(flat_t[:n], non_blocking=self.cuda)
         if self.cuda:
