@@ -76,6 +76,10 @@ struct IGemmArgs {
   // A_CONV LDS-DMA with whole-kernel-row k-tiles (C * KW == KB, no padding, valid geometry): the packed
   // stem (tde_stem_pack) runs through this
   int rowtile;
+  // strided dgrad, all stride phases in ONE launch (grid z = phase; splits must be 1): per phase
+  // {ph_h, ph_w, Hp, Wp, kh0, kw0, KHp, KWp}; M and K follow per phase, grid x covers the largest M
+  int nph;
+  int phs[4][8];
 };
 
 constexpr int TK = 32;  // MFMA k-slice
@@ -379,7 +383,24 @@ __device__ __forceinline__ void vm_wait() {
 // instead of the register-staged double buffer.
 // WGM: waves along M (4 / WGM along N); the register-staged path is 2 x 2.
 template <int AK, int BK_, int BM, int BN, int KB, int VEC, int S = 0, int WGM = 2>
-__global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
+__global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p_) {
+  IGemmArgs p = p_;
+  if (AK == A_DGRAD && p_.nph > 0) {  // multi-phase strided dgrad: this block's phase is blockIdx.z
+    const int* ph = p_.phs[blockIdx.z];
+    p.ph_on = 1;
+    p.ph_h = ph[0];
+    p.ph_w = ph[1];
+    p.Hp = ph[2];
+    p.Wp = ph[3];
+    p.kh0 = ph[4];
+    p.kw0 = ph[5];
+    p.KHp = ph[6];
+    p.KWp = ph[7];
+    p.M = p.g.B * p.Hp * p.Wp;
+    p.K = p.KHp * p.KWp * p.g.Co;
+    p.ktiles_per_split = (p.K + KB - 1) / KB;
+    if ((int)blockIdx.x * BM >= p.M) return;  // grid x covers the largest phase
+  }
   constexpr bool AKV = (AK == A_ROWK || AK == A_CONV || AK == A_DGRAD);  // K-vector A
   constexpr bool BKV = (BK_ == B_NK || BK_ == B_DGRADW);                 // K-vector B
   constexpr bool GLDS = S > 0;
@@ -411,8 +432,8 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p) {
   // Workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share an L2): remap the
   // linear id so every XCD owns a contiguous run of tiles — M-major neighbours then share the B
   // tile (and the A rows of the next N column) in one L2.  Bijective for any grid size.
-  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-  if (p.xcd) {
+  int bx = blockIdx.x, by = blockIdx.y, bz = (AK == A_DGRAD && p.nph > 0) ? 0 : (int)blockIdx.z;
+  if (p.xcd && !(AK == A_DGRAD && p.nph > 0)) {
     const int gx = gridDim.x, gy = gridDim.y, nwg = gx * gy * gridDim.z;
     if (nwg > 8) {
       const int bid = bx + gx * (by + gy * bz);
@@ -2656,7 +2677,21 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     Geo g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9], geo[10], geo[11], geo[12]};
     p.g = g;
   }
-  if (phase) {
+  int nph = 0;
+  if (phase && phase[0] == -1) {
+    // multi-phase table {-1, n, n x {ph_h, ph_w, Hp, Wp, kh0, kw0, KHp, KWp}}: one launch, grid z = phase;
+    // M / K passed in are the largest over the phases (grid and K-step sizing)
+    nph = phase[1];
+    if (nph < 1 || nph > 4 || splits > 1) return -5;
+    p.nph = nph;
+    for (int i = 0; i < nph; ++i)
+      for (int j = 0; j < 8; ++j) p.phs[i][j] = phase[2 + 8 * i + j];
+    p.ph_on = 1;
+    p.Hp = p.phs[0][2];   // host-side checks only; the kernel takes each block's phase from the table
+    p.Wp = p.phs[0][3];
+    p.KHp = p.phs[0][6];
+    p.KWp = p.phs[0][7];
+  } else if (phase) {
     p.ph_on = 1;
     p.ph_h = phase[0];
     p.ph_w = phase[1];
@@ -2762,7 +2797,7 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     // of 64x64 (ResNet-18 14x14x256 convs 34.7 -> 27.1 us; profiles/r2_sweep_fd.txt)
     bm = 128;
   }
-  dim3 grid((M + bm - 1) / bm, (N + bn - 1) / bn, splits);
+  dim3 grid((M + bm - 1) / bm, (N + bn - 1) / bn, nph > 0 ? nph : splits);
   if (grid.y > 65535 || splits > 65535) return -3;
   // weight-grad split-K with a scratch: every split stores its partial tile (plain stores) and one
   // reduction pass adds them to the gradient, instead of BM x BN memory-side f32 atomics per split
@@ -2824,10 +2859,10 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     if (vec && g_glds && ut) {                                                                      \
       if (big) ++g_big_launches;                                                                    \
       if (big && N <= 64) {                                                                         \
-        grid = dim3((M + 255) / 256, (N + 63) / 64, splits);                                        \
+        grid = dim3((M + 255) / 256, (N + 63) / 64, grid.z);                                        \
         igemm_kernel<AK_, BK__, 256, 64, 64, 1, 3, 4><<<grid, 256, 0, stream>>>(p);                 \
       } else if (big) {                                                                             \
-        grid = dim3((M + 255) / 256, (N + 127) / 128, splits);                                      \
+        grid = dim3((M + 255) / 256, (N + 127) / 128, grid.z);                                      \
         igemm_kernel<AK_, BK__, 256, 128, 64, 1, 3, 2><<<grid, 256, 0, stream>>>(p);                \
       } else if (KB == 64) {                                                                        \
         igemm_kernel<AK_, BK__, BM_, BN_, 64, 1, 3><<<grid, 256, 0, stream>>>(p);                   \

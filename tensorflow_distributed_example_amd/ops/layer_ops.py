@@ -8,6 +8,7 @@ geometry it hands the kernel, so a kernel never indexes outside its buffers.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 
 import torch
@@ -98,7 +99,7 @@ def _igemm(a, lda, ak, b, ldb, bk, M, N_, K, geo=None, splits=1, cf=None, ldc=0,
     g = geo.carray() if geo is not None else None
     if splits > 1 and scratch is not None:
         _f32(scratch, M * N_, "igemm split-K scratch")
-    ph = (C.c_int * 8)(*phase) if phase is not None else None
+    ph = (C.c_int * len(phase))(*phase) if phase is not None else None
     rc = N.hip().tde_igemm(_P(a), int(lda), ak, _P(b), int(ldb), bk, int(M), int(N_), int(K), g, int(splits),
                            _P(cf), int(ldc), int(cf_mode), float(alpha), _P(cb), int(ldcb), int(cb_accum), _P(bias),
                            int(relu), _P(colstats), _P(scratch), ph, _s())
@@ -160,9 +161,16 @@ def conv_dgrad(dy, Wrow, dx, g: ConvGeom, accum=False, scratch=None):
             if g.C % 8 == 0:
                 mask = sum(1 << (ph[0] * g.sw + ph[1]) for ph in untapped)
                 N.check(N.hip().tde_dgrad_phase_zero(_P(dx), g.carray(), mask, _s()), "tde_dgrad_phase_zero")
-        for ph in phases:
-            if ph[6] * ph[7] == 0 and skip_untapped:
-                continue
+        run = [ph for ph in phases if not (ph[6] * ph[7] == 0 and skip_untapped)]
+        if 1 < len(run) <= 4 and os.environ.get("TDE_DGRAD_MULTIPHASE", "1") != "0":
+            # every stride phase in one launch (grid z = phase): M / K of the largest phase size the grid
+            table = [-1, len(run)] + [v for ph in run for v in ph]
+            Mx = max(g.B * ph[2] * ph[3] for ph in run)
+            Kx = max(ph[6] * ph[7] * g.Co for ph in run)
+            _igemm(dy, 0, A_DGRAD, Wrow, 0, B_DGRADW, Mx, g.C, Kx, g, cb=dx, ldcb=g.C, cb_accum=accum,
+                   phase=table)
+            return
+        for ph in run:
             _igemm(dy, 0, A_DGRAD, Wrow, 0, B_DGRADW, g.B * ph[2] * ph[3], g.C, ph[6] * ph[7] * g.Co, g,
                    cb=dx, ldcb=g.C, cb_accum=accum, phase=ph)
         return

@@ -736,3 +736,27 @@ def test_stem_pack_conv_fwd_wgrad(B, H, W, C, Co, k, s):
     torch.cuda.synchronize()
     assert _rel(gW - gW0, _dev(wr.grad.permute(2, 3, 1, 0))) < 1e-3
     assert float(gWv.abs().max()) == 0.0   # re-armed for the next step's accumulation
+
+
+@pytest.mark.parametrize("B,H,W,C,Co,k,s,pad", [(4, 14, 14, 16, 24, 6, 2, "same"), (2, 17, 15, 8, 24, 3, 2, "same"),
+                                                (2, 15, 15, 64, 128, 3, 2, "same")])
+def test_strided_dgrad_single_launch_matches_per_phase(B, H, W, C, Co, k, s, pad, monkeypatch):
+    """All stride phases of a strided conv's input gradient in ONE launch (grid z = phase, per-phase M / K
+    from the kernel's phase table) equals the per-phase launches bit for bit, store and accumulate modes."""
+    from tensorflow_distributed_example_amd.ops import layer_ops as O
+    (pt, _), (pl, _) = _tf_same(H, k, s), _tf_same(W, k, s)
+    Ho, Wo = -(-H // s), -(-W // s)
+    g = O.ConvGeom(B, H, W, C, Ho, Wo, Co, k, k, s, s, pt, pl)
+    w = _r(k, k, C, Co, seed=21, scale=0.2)
+    dy = _r(B, Ho, Wo, Co, seed=22)
+    outs = []
+    for multi in ("1", "0"):
+        monkeypatch.setenv("TDE_DGRAD_MULTIPHASE", multi)
+        dx = torch.full((B, H, W, C), float("nan"), device=DEV).to(bf)
+        O.conv_dgrad(dy, w.contiguous(), dx, g)
+        dx2 = _r(B, H, W, C, seed=23)
+        O.conv_dgrad(dy, w.contiguous(), dx2, g, accum=True)
+        outs.append((dx, dx2))
+    torch.cuda.synchronize()
+    assert not torch.isnan(outs[0][0].float()).any()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
