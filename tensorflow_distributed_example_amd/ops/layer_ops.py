@@ -83,11 +83,19 @@ def fwd_splits(M, N_, K):
     """Split-K factor for an activation-producing GEMM (fwd / dgrad): only when the output tiles
     alone cannot fill the 256 CUs and the K loop is long (latency-bound); the partial sums go
     through the f32 scratch + finalize pass."""
+    target = _FWD_SPLIT_TARGET
     tiles = -(-M // 64) * -(-N_ // 64)
     ktiles = -(-K // 32)
-    if tiles >= 256 or ktiles < 8:
+    if target <= 0 or tiles >= 256 or ktiles < 8:
         return 1
-    return max(1, min(-(-512 // tiles), ktiles // 4))
+    return max(1, min(-(-target // tiles), ktiles // 4))
+
+
+# workgroups a split-K fwd/dgrad GEMM aims for (TDE_FWD_SPLIT_TARGET; 0 = never split, the default since the
+# LDS-DMA k loop: the split's extra finalize launch costs more than the parallelism it buys —
+# scripts/split_sweep.sh, profiles/r2_split_sweep.txt: Model B 489k -> 512k, LeNet-5 676k -> 697k,
+# MLP 3.17M -> 3.53M img/s, ResNet-18 neutral)
+_FWD_SPLIT_TARGET = int(os.environ.get("TDE_FWD_SPLIT_TARGET", "0"))
 
 
 def scratch_elems(M, N_, K):
