@@ -22,7 +22,9 @@ from micro import graph_time  # noqa: E402
 
 
 def _convs(plan, LW):
-    return [st for st in plan.stages if isinstance(st, LW._Gemm) and st.conv and not st.use_im2col]
+    # the stem (im2col or packed-stem path) has its own kernels: timed by the model bench, not here
+    return [st for st in plan.stages if isinstance(st, LW._Gemm) and st.conv and not st.use_im2col
+            and not st.use_stem_pack]
 
 
 def main():

@@ -2544,9 +2544,8 @@ static int g_big_dgrad = [] {
 }();
 // number of big-tile launches since load (tests assert the path ran)
 static unsigned long long g_big_launches = 0;
-// XCD-aware tile order (TDE_XCD_SWIZZLE=1).  Off by default: on ResNet-18 / Model B at their batch
-// sizes the GEMMs are not HBM-bound (working sets sit in L2/MALL) and the remap measured within noise
-// (fwd 681 -> 692 us, dgrad 837 -> 847, wgrad 916 -> 911 per step; bench/resnet_layers.py).
+// XCD-aware tile order (TDE_XCD_SWIZZLE = bit mask by GEMM kind, see tde_igemm).  Round 1 (VALU-bound
+// loop) measured it neutral; with the LDS-DMA loop it pays for the weight gradients only.
 static int g_xcd = -1;
 // split-K weight gradients with at most this many splits store partials + reduce; more splits use atomics
 static int g_wg_scratch_max = 16;
@@ -2662,10 +2661,16 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   }
   IGemmArgs p{};
   if (g_xcd < 0) {
+    // bit mask by GEMM kind: 1 = fwd / dense (A_ROWK, A_CONV), 2 = dgrad, 4 = weight gradients
     const char* e = getenv("TDE_XCD_SWIZZLE");
-    g_xcd = e ? atoi(e) != 0 : 0;
+    // default 4: weight gradients only (ResNet-18 wgrad 840 -> 798 us/step; fwd / dgrad 1-3 % slower with it,
+    // profiles/r2_xcd_ab.txt)
+    g_xcd = e ? atoi(e) : 4;
   }
-  p.xcd = g_xcd;
+  {
+    const int kind_bit = (akind == A_ROWK || akind == A_CONV) ? 1 : akind == A_DGRAD ? 2 : 4;
+    p.xcd = (g_xcd & kind_bit) ? 1 : 0;
+  }
   p.a = a;
   p.lda = lda;
   p.b = b;
