@@ -125,7 +125,7 @@ def test_xgmi_allreduce_bitwise(world, tmp_path):
 def test_mwms_bench_two_ranks_on_xgmi(tmp_path):
     """bench.py under torchrun with 2 ranks sharing cuda:0: the gradient bucket goes through the
     xGMI kernel (captured in the step's hipGraph) and the run reports one JSON line."""
-    env = dict(os.environ, TDE_RCCL="0", TDE_ALLREDUCE="xgmi", TDE_HEARTBEAT="0", OMP_NUM_THREADS="2",
+    env = dict(os.environ, TDE_RCCL="0", TDE_ALLREDUCE="xgmi", TDE_HEARTBEAT="0", OMP_NUM_THREADS="2", TDE_BENCH_WARM_MS="0",
                TDE_CHECK_XGMI="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
@@ -182,7 +182,7 @@ def test_bucketed_overlapped_allreduce_two_ranks():
     hipGraph); replicas stay bit-identical and training matches the single post-backward all-reduce."""
     losses = {}
     for overlap in ("1", "0"):
-        env = dict(os.environ, TDE_RCCL="0", TDE_ALLREDUCE="xgmi", TDE_HEARTBEAT="0", OMP_NUM_THREADS="2",
+        env = dict(os.environ, TDE_RCCL="0", TDE_ALLREDUCE="xgmi", TDE_HEARTBEAT="0", OMP_NUM_THREADS="2", TDE_BENCH_WARM_MS="0",
                    TDE_OVERLAP=overlap, TDE_BUCKET_MB="0.2")
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
                "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
@@ -201,7 +201,7 @@ def test_bucketed_overlapped_allreduce_two_ranks():
 def test_rccl_init_failure_falls_back_on_every_rank():
     """Two ranks on one GPU make ncclCommInitRank fail on both (duplicate GPU): the strategy agrees on
     the failure, keeps gloo for the control collectives and the xGMI kernel for the gradient bucket."""
-    env = dict(os.environ, TDE_ALLREDUCE="xgmi", TDE_HEARTBEAT="0", OMP_NUM_THREADS="2")
+    env = dict(os.environ, TDE_ALLREDUCE="xgmi", TDE_HEARTBEAT="0", OMP_NUM_THREADS="2", TDE_BENCH_WARM_MS="0")
     env.pop("TDE_RCCL", None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
@@ -303,7 +303,7 @@ def test_mwms_fused_allreduce_apply_matches_unfused():
     optimizer launch (TDE_FUSED_STEP=0): replicas bit-identical in both, same training trajectory."""
     losses = {}
     for fused in ("1", "0"):
-        env = dict(os.environ, TDE_RCCL="0", TDE_ALLREDUCE="xgmi", TDE_HEARTBEAT="0", OMP_NUM_THREADS="2",
+        env = dict(os.environ, TDE_RCCL="0", TDE_ALLREDUCE="xgmi", TDE_HEARTBEAT="0", OMP_NUM_THREADS="2", TDE_BENCH_WARM_MS="0",
                    TDE_FUSED_STEP=fused)
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
                "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
