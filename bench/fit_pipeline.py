@@ -36,8 +36,9 @@ def main():
     def scale(img, lab):
         return img.astype(np.float32) / 255.0, lab
 
-    for native in ("1", "0"):
+    for native, device in (("1", "1"), ("1", "0"), ("0", "0")):
         os.environ["TDE_NATIVE_DATA"] = native
+        os.environ["TDE_DEVICE_DATA"] = device
         from tensorflow_distributed_example_amd.data import dataset as DS
         DS._HOST.clear()
         tde.backend.set_random_seed(0)
@@ -52,6 +53,7 @@ def main():
         m.fit(ds, epochs=1, steps_per_epoch=a.steps, verbose=0)
         dt = time.perf_counter() - t
         print(json.dumps({"what": "fit() img/s, DWK pipeline", "native_pipeline": native == "1",
+                          "device_feed": bool(m._device_feed),
                           "img_per_s": round(128 * a.steps / dt), "ms_per_step": round(dt / a.steps * 1e3, 4),
                           "steps_per_execution": a.spe, "prefetch": a.prefetch}), flush=True)
 

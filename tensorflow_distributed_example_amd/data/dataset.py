@@ -167,6 +167,18 @@ class Dataset:
     def unbatch(self):
         return _Unbatch(self)
 
+    def device_source(self):
+        """(columns, structured, batch node) when this pipeline is batches of rows of in-memory columns
+        (source [-> map -> cache] -> shuffle/repeat/shard/take/skip -> batch [-> prefetch / options]), so
+        a trainer may keep the columns resident on the device and gather batches there from the index
+        stream; None otherwise."""
+        d = self
+        while isinstance(d, (_Prefetch, _WithOptions)):
+            d = d._parent
+        if not isinstance(d, _Batch) or not d._parent._indexable():
+            return None
+        return d._parent._columns(), d._parent._structure, d
+
     def with_options(self, options: Options):
         d = _WithOptions(self, options)
         return d
@@ -578,37 +590,39 @@ class _Batch(_Unary):
         self.batch_size = batch_size
         self.drop_remainder = drop_remainder
 
-    def __iter__(self):
+    def index_batches(self):
+        """Row indices of every batch of an indexable parent (the shuffle / repeat / shard / take / skip
+        algebra runs on index streams; no row is gathered)."""
         bs = self.batch_size
+        pend, npend = [], 0
+        for c in self._parent._index_chunks(None):
+            pend.append(c)
+            npend += len(c)
+            if npend < bs:
+                continue
+            cur = np.concatenate(pend) if len(pend) > 1 else pend[0]
+            nfull = len(cur) // bs
+            for k in range(nfull):
+                yield cur[k * bs:(k + 1) * bs]
+            rest = cur[nfull * bs:]
+            pend, npend = ([rest] if len(rest) else []), len(rest)
+        if npend and not self.drop_remainder:
+            yield np.concatenate(pend)
+
+    def __iter__(self):
         p = self._parent
         if p._indexable():
             cols = p._columns()
             tup = p._structure
             lib = _host_lib()
-
-            def emit(idx):
+            for idx in self.index_batches():
                 out = _gather(cols, idx, lib)
-                return out if tup else out[0]
-
-            pend, npend = [], 0
-            for c in p._index_chunks(None):
-                pend.append(c)
-                npend += len(c)
-                if npend < bs:
-                    continue
-                cur = np.concatenate(pend) if len(pend) > 1 else pend[0]
-                nfull = len(cur) // bs
-                for k in range(nfull):
-                    yield emit(cur[k * bs:(k + 1) * bs])
-                rest = cur[nfull * bs:]
-                pend, npend = ([rest] if len(rest) else []), len(rest)
-            if npend and not self.drop_remainder:
-                yield emit(np.concatenate(pend))
+                yield out if tup else out[0]
             return
         buf = []
         for e in p:
             buf.append(e)
-            if len(buf) == bs:
+            if len(buf) == self.batch_size:
                 yield _stack(buf)
                 buf = []
         if buf and not self.drop_remainder:

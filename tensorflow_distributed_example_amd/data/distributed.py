@@ -78,3 +78,17 @@ class DistributedDataset:
     def __iter__(self):
         for b in self._ds:
             yield self._split(b)
+
+    def device_source(self):
+        """(columns, structured, per-replica index-batch iterator factory) for trainers that keep the
+        columns resident on the device (MI355X: a cached MNIST is 188 MB of 288 GB HBM) and gather each
+        replica's rows there; the same shard / rebatch / split semantics as iterating the dataset."""
+        src = self._ds.device_source()
+        if src is None:
+            return None
+        cols, tup, batch = src
+
+        def index_iter():
+            for idx in batch.index_batches():
+                yield self._split(idx)
+        return cols, tup, index_iter

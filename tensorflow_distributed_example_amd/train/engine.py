@@ -117,10 +117,16 @@ def fit(model, x=None, y=None, batch_size=None, epochs=1, verbose="auto", callba
     logs = {}
     import os
     check_every = int(os.environ.get("TDE_CHECK_REPLICAS", "0") or 0)   # utils/debug.py
+    # in-memory (x, y) datasets on GPU replicas: HBM-resident cache + on-device gather (train/device_feed.py)
+    from .device_feed import DeviceFeed
+    feed = DeviceFeed.try_make(dds, prog)
+    model._device_feed = feed is not None
     n_exec = 0
     for epoch in range(initial_epoch, epochs):
         if not persist:
             it = None
+            if feed is not None:
+                feed.reset()
         prog.reset_metrics()
         cl.on_epoch_begin(epoch)
         step = 0
@@ -129,20 +135,28 @@ def fit(model, x=None, y=None, batch_size=None, epochs=1, verbose="auto", callba
             want = S if steps_per_epoch is None else min(S, steps_per_epoch - step)
             group = []
             while len(group) < want:
-                b = next_batch()
+                b = next_batch() if feed is None else feed.next()
                 if b is None:
                     exhausted = True
                     break
                 group.append(b)
             if not group:
                 break
-            full = [all(len(r[1]) == prog.B for r in g) for g in group]
+            if feed is not None:   # per-replica row-index arrays
+                full = [all(len(r) == prog.B for r in g) for g in group]
+            else:
+                full = [all(len(r[1]) == prog.B for r in g) for g in group]
             cl.on_train_batch_begin(step)
             if len(group) == S and all(full):
-                prog.stage(_stack_steps(group))
+                if feed is not None:
+                    feed.stage(group)
+                else:
+                    prog.stage(_stack_steps(group))
                 prog.run()
             else:
                 for g in group:
+                    if feed is not None:
+                        g = feed.host_batch(g)
                     glob = sum(len(r[1]) for r in g) * strategy.num_workers
                     prog.run_single(g, glob)
             step += len(group)
@@ -170,6 +184,8 @@ def fit(model, x=None, y=None, batch_size=None, epochs=1, verbose="auto", callba
         if exhausted and persist:
             break
     prog.sync()
+    if feed is not None:
+        feed.check()
     cl.on_train_end(logs)
     return hist
 

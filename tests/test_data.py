@@ -141,3 +141,36 @@ def test_native_gather_matches_numpy_for_all_column_kinds():
     for bi, bl, bs in ds:
         assert np.array_equal(bi, imgs[bl]) and np.array_equal(bs, strided[bl])
         assert bi.dtype == np.float32 and bs.dtype == np.int32
+
+
+@pytest.mark.parametrize("policy,workers,widx", [(None, 1, 0), (AutoShardPolicy.OFF, 2, 1),
+                                                 (AutoShardPolicy.DATA, 2, 1)])
+def test_device_source_index_stream_matches_iteration(policy, workers, widx):
+    """The device feed (train/device_feed.py) gathers rows on the GPU from DistributedDataset.device_source's
+    per-replica index stream: it must select exactly the rows iterating the dataset yields."""
+    from types import SimpleNamespace
+    from tensorflow_distributed_example_amd.data.distributed import DistributedDataset
+    n = 203
+    x = np.arange(n * 6, dtype=np.float32).reshape(n, 2, 3)
+    y = np.arange(n) % 10
+
+    def make():
+        ds = Dataset.from_tensor_slices((x, y)).map(lambda a, b: (a * 0.5, b)).cache() \
+            .shuffle(50, seed=3).repeat(2).batch(16).prefetch(2)
+        if policy is not None:
+            o = Options()
+            o.experimental_distribute.auto_shard_policy = policy
+            ds = ds.with_options(o)
+        return ds
+    st = SimpleNamespace(num_workers=workers, worker_index=widx, num_local_replicas=2,
+                         num_replicas_in_sync=2 * workers, global_replica_id=lambda i: widx * 2 + i)
+    ref = list(DistributedDataset(make(), st))
+    cols, tup, index_iter = DistributedDataset(make(), st).device_source()
+    got = list(index_iter())
+    assert tup and len(got) == len(ref) and len(ref) > 10
+    for rb, ib in zip(ref, got):
+        assert len(rb) == len(ib) == 2
+        for (rx, ry), idx in zip(rb, ib):
+            assert np.array_equal(cols[0][idx], rx) and np.array_equal(cols[1][idx], ry)
+    # pipelines that are not batches of in-memory rows have no device source
+    assert Dataset.from_tensor_slices(x).batch(4).unbatch().batch(4).device_source() is None

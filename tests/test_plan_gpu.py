@@ -231,3 +231,76 @@ def test_fused_local_fit_matches_plain(monkeypatch):
         rel = np.linalg.norm((a - w) - (b - w)) / (np.linalg.norm(b - w) + 1e-12)
         assert rel < 5e-2, rel
     assert abs(ha.history["loss"][0] - hb.history["loss"][0]) < 1e-2
+
+
+
+def _feed_model(tde, zoo, spe=3):
+    # a small plain-SGD step: random labels at lr 0.05 + momentum make 28 steps chaotic enough that
+    # atomic-order rounding alone moves LeNet-5 weights by ~30% run to run (bench/feed_det.py)
+    m = getattr(tde.zoo, zoo)()
+    m.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True),
+              optimizer=tde.optimizers.SGD(0.005), metrics=["accuracy"], steps_per_execution=spe)
+    return m
+
+
+@pytest.mark.parametrize("zoo", ["mnist_cnn", "lenet5"])
+def test_device_feed_stages_the_host_rows(zoo):
+    """The HBM-resident cache + HIP row gather (train/device_feed.py) writes exactly the ring the host gather
+    + pinned staging path writes (fp32 ring of the fused plan, bf16 ring of the layer-wise plan), for
+    the rows iterating the distributed dataset yields."""
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.train.device_feed import DeviceFeed
+    from tensorflow_distributed_example_amd.train.engine import _stack_steps
+    tde.backend.clear_session()
+    x, y = _data(500, 4)
+    m = _feed_model(tde, zoo)
+    prog = m._program("train", 64)
+    assert prog.x_ring[0].dtype == (torch.float32 if zoo == "mnist_cnn" else torch.bfloat16)
+
+    def dds():
+        ds = tde.data.Dataset.from_tensor_slices((x, y)).cache().shuffle(100, seed=11).repeat(2).batch(64)
+        return m._strategy.experimental_distribute_dataset(ds)
+    feed = DeviceFeed.try_make(dds(), prog)
+    assert feed is not None
+    ref = iter(dds())
+    for _ in range(4):
+        group = [feed.next() for _ in range(prog.S)]
+        feed.stage(group)
+        got_x, got_y = prog.x_ring[0].clone(), prog.y_ring[0].clone()
+        host = [next(ref) for _ in range(prog.S)]
+        for g, h in zip(group, host):
+            (hx, hy), = h
+            (fx, fy), = feed.host_batch(g)
+            assert np.array_equal(fx, hx) and np.array_equal(fy, hy)
+        prog.stage(_stack_steps([[(np.asarray(hx), np.asarray(hy).reshape(-1))] for (hx, hy), in host]))
+        assert torch.equal(got_x, prog.x_ring[0]) and torch.equal(got_y, prog.y_ring[0])
+    feed.check()
+
+
+@pytest.mark.parametrize("zoo", ["mnist_cnn", "lenet5"])
+def test_device_feed_fit_matches_host_path(zoo, monkeypatch):
+    """fit() over a cached / shuffled / repeated pipeline with the device feed vs TDE_DEVICE_DATA=0 (host
+    gather + pinned staging); the last global batch is partial (eager run_single from host rows).  The
+    rings match bitwise (test above); the tolerance covers the kernels' atomic-order rounding."""
+    import tensorflow_distributed_example_amd as tde
+    x, y = _data(64 * 7 + 23, 4)
+
+    def run(device_data, w0=None):
+        monkeypatch.setenv("TDE_DEVICE_DATA", "1" if device_data else "0")
+        tde.backend.clear_session()
+        tde.backend.set_random_seed(9)
+        m = _feed_model(tde, zoo)
+        if w0 is not None:
+            m.set_weights(w0)
+        w = m.get_weights()
+        ds = tde.data.Dataset.from_tensor_slices((x, y)).cache().shuffle(100, seed=11).repeat(2).batch(64)
+        h = m.fit(ds, epochs=2, verbose=0)
+        assert m._device_feed == device_data
+        return m.get_weights(), h.history["loss"], w
+
+    wa, la, w0 = run(True)
+    wb, lb, _ = run(False, w0)
+    for a, b, w in zip(wa, wb, w0):
+        rel = np.linalg.norm((a - w) - (b - w)) / (np.linalg.norm(b - w) + 1e-12)
+        assert rel < 2e-2, rel
+    np.testing.assert_allclose(la, lb, rtol=1e-3)
