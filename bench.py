@@ -167,7 +167,7 @@ def main():
         print(json.dumps({
             "metric": metric, "value": round(ips, 1), "unit": "images/sec", "n_gpus": n, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16" if prog.plan_kind != "reference" else "fp32",
+            "vs_baseline": None, "dtype": "fp32" if prog.plan_kind in ("reference", "fused_smallnet") else "bf16",
             "data": f"synthetic (random {'x'.join(map(str, img))} images, random labels; random-init weights)",
             "config": {"model": a.model, "global_batch": GB, "seq_len": None, "image_shape": list(img),
                        "per_gpu_batch": B, "parallelism": f"dp{n}", "strategy": "MultiWorkerMirroredStrategy",

@@ -346,9 +346,11 @@ def test_model_b_layerwise_matches_bf16_oracle():
 
 
 @pytest.mark.parametrize("name", ["lenet5", "mnist_mlp"])
-def test_baseline_config_models_layerwise_match_bf16_oracle(name):
-    """LeNet-5 (5x5 narrow convs, two pools, three Dense) and the dense MLP on the layer-wise plan."""
+def test_baseline_config_models_layerwise_match_bf16_oracle(name, monkeypatch):
+    """LeNet-5 (5x5 narrow convs, two pools, three Dense) and the dense MLP on the layer-wise plan (the
+    default plan for them is the fused small-net plan: tests/test_smallnet_gpu.py)."""
     import tensorflow_distributed_example_amd as tde
+    monkeypatch.setenv("TDE_SMALLNET", "0")
     tde.backend.set_random_seed(0)
     m = getattr(tde.zoo, name)()
     m.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True), optimizer=tde.optimizers.SGD(0.01))

@@ -148,3 +148,19 @@ def test_reference_forward_call_shapes():
     out = m(np.random.rand(3, 784).astype(np.float32))
     assert out.shape == (3, 10)
     assert torch.allclose(out.sum(1), torch.ones(3), atol=1e-5)  # softmax output
+
+
+def test_smallnet_matcher():
+    """Which models the fused per-image plan (train/smallnet.py) takes: LeNet-5 and the MLP (BASELINE
+    configs 2 and 1), not Model B (BatchNorm, Dropout, strided convs) nor ResNet."""
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.train.smallnet import CONV, DENSE, POOL, match_smallnet
+    logits = tde.losses.SparseCategoricalCrossentropy(from_logits=True)
+    probs = tde.losses.SparseCategoricalCrossentropy(from_logits=False)
+    spec = match_smallnet(tde.zoo.lenet5(), logits)
+    assert [s["kind"] for s in spec] == [CONV, POOL, CONV, POOL, DENSE, DENSE, DENSE]
+    assert spec[0]["pt"] == 2 and spec[2]["inp"] == (14, 14, 6) and spec[4]["inp"] == (1, 1, 400)
+    assert [s["kind"] for s in match_smallnet(tde.zoo.mnist_mlp(), logits)] == [DENSE, DENSE]
+    assert match_smallnet(tde.zoo.mnist_bn_cnn(), probs) is None
+    assert match_smallnet(tde.zoo.lenet5(), probs) is None        # logits head fed to the probability loss
+    assert match_smallnet(tde.zoo.resnet((1, 1), (16, 32), input_shape=(32, 32, 3), classes=10), logits) is None

@@ -244,13 +244,14 @@ def _feed_model(tde, zoo, spe=3):
 
 
 @pytest.mark.parametrize("zoo", ["mnist_cnn", "lenet5"])
-def test_device_feed_stages_the_host_rows(zoo):
+def test_device_feed_stages_the_host_rows(zoo, monkeypatch):
     """The HBM-resident cache + HIP row gather (train/device_feed.py) writes exactly the ring the host gather
     + pinned staging path writes (fp32 ring of the fused plan, bf16 ring of the layer-wise plan), for
     the rows iterating the distributed dataset yields."""
     import tensorflow_distributed_example_amd as tde
     from tensorflow_distributed_example_amd.train.device_feed import DeviceFeed
     from tensorflow_distributed_example_amd.train.engine import _stack_steps
+    monkeypatch.setenv("TDE_SMALLNET", "0")   # LeNet-5 on the layer-wise plan: a bf16 input ring
     tde.backend.clear_session()
     x, y = _data(500, 4)
     m = _feed_model(tde, zoo)
@@ -284,6 +285,7 @@ def test_device_feed_fit_matches_host_path(zoo, monkeypatch):
     rings match bitwise (test above); the tolerance covers the kernels' atomic-order rounding."""
     import tensorflow_distributed_example_amd as tde
     x, y = _data(64 * 7 + 23, 4)
+    monkeypatch.setenv("TDE_SMALLNET", "0")
 
     def run(device_data, w0=None):
         monkeypatch.setenv("TDE_DEVICE_DATA", "1" if device_data else "0")
