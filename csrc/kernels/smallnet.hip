@@ -30,7 +30,7 @@ namespace tde {
 
 constexpr int kSnMaxLayers = 12;
 constexpr int kSnLds = 28 * 1024;  // floats of LDS per workgroup (112 KiB)
-constexpr int kSnThreads = 1024;
+constexpr int kSnThreads = 512;
 enum { kSnConv = 0, kSnPool = 1, kSnDense = 2 };
 
 // All offsets in floats.  Buffers: `in` / `out` are the layer's input / output activations in LDS;
@@ -49,6 +49,7 @@ constexpr int kSnLayerInts = sizeof(SnLayer) / sizeof(int);
 struct SnArgs {
   SnLayer L[kSnMaxLayers];
   int nl, mode, B, x_stride, in0, n_in0;  // mode 0 train, 1 eval, 2 predict
+  int img_H, img_W, img_C, pad_t, pad_l, img_Wp, img_Hp;  // the image lands zero-padded for a same-padded first conv
   const float* w;
   const float* x;
   const int* y;
@@ -93,7 +94,7 @@ __device__ __forceinline__ void st_cg(float* p, const float* v) {
 // threads and folded with LDS float atomics.
 constexpr int kSnScratch = 4096;  // floats of LDS scratch at offset 0 of the layout
 constexpr int kSnUnroll = 8;
-constexpr int kSnItemsTarget = 2048;
+constexpr int kSnItemsTarget = 1024;
 
 // conv forward: item = (output pixel p, channel group g); pixels fastest, so a wave shares g and its
 // kernel reads are LDS broadcasts
@@ -289,6 +290,184 @@ __device__ void sn_conv_dgrad(const SnLayer L, float* s) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Compile-time-geometry conv phases for the shapes of the zoo models (valid convs; a same-padded first
+// conv reads the zero-padded image).  Constant trip counts let every tap / channel loop unroll with
+// immediate LDS offsets, so the VALU work is the FMAs instead of runtime-stride address arithmetic
+// (the generic phases above spend ~5 VALU instructions per FMA).
+constexpr int sn_slices(int Ho, int items) {
+  int best = 1;
+  for (int d = 1; d <= Ho; ++d)
+    if (Ho % d == 0 && items * d <= kSnItemsTarget) best = d;
+  return best;
+}
+
+template <int CG, int KH, int KW, int C, int Co, int Win, int Ho, int Wo>
+__device__ void sn_conv_fwd_c(const SnLayer L, float* s) {
+  constexpr int P = Ho * Wo, NG = Co / CG;
+  const float* in = s + L.in;
+  const float* wl = s + L.wl;
+  float* out = s + L.out;
+  for (int it = threadIdx.x; it < P * NG; it += kSnThreads) {
+    const int p = it % P, g = it / P;
+    const int oh = p / Wo, ow = p % Wo;
+    const float* ip = in + (oh * Win + ow) * C;
+    const float* wp = wl + g * CG;
+    float acc[CG], acc2[CG];
+    if (L.b_off >= 0) {
+      ld_cg<CG>(wl + KH * KW * C * Co + g * CG, acc);
+    } else {
+#pragma unroll
+      for (int k = 0; k < CG; ++k) acc[k] = 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < CG; ++k) acc2[k] = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < KH; ++kh) {
+#pragma unroll
+      for (int r = 0; r < KW * C; ++r) {
+        const float a = ip[kh * Win * C + r];
+        float w[CG];
+        ld_cg<CG>(wp + (kh * KW * C + r) * Co, w);
+#pragma unroll
+        for (int k = 0; k < CG; ++k) {
+          if (r & 1) acc2[k] = fmaf(a, w[k], acc2[k]);
+          else acc[k] = fmaf(a, w[k], acc[k]);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < CG; ++k) {
+      acc[k] += acc2[k];
+      if (L.relu) acc[k] = fmaxf(acc[k], 0.f);
+    }
+    st_cg<CG>(out + p * Co + g * CG, acc);
+  }
+}
+
+template <int CG, int KH, int KW, int C, int Co, int Win, int Ho, int Wo>
+__device__ void sn_conv_wgrad_c(const SnLayer L, float* s, float* part) {
+  constexpr int T = KH * KW * C, NG = Co / CG;
+  constexpr int S = sn_slices(Ho, T * NG), R = Ho / S;
+  static_assert(T * Co + Co <= kSnScratch, "scratch");
+  const float* in = s + L.in;
+  const float* dz = s + L.out;
+  float* red = s;
+  constexpr int n = T * Co + Co;
+  for (int i = threadIdx.x; i < n; i += kSnThreads) red[i] = 0.f;
+  __syncthreads();
+  for (int it = threadIdx.x; it < T * NG * S; it += kSnThreads) {
+    const int t = it % T, g = (it / T) % NG, sl = it / (T * NG);
+    const int ci = t % C, kk = t / C;
+    const int kh = kk / KW, kw = kk % KW;
+    const float* ip = in + ((sl * R + kh) * Win + kw) * C + ci;
+    const float* dp = dz + sl * R * Wo * Co + g * CG;
+    float acc[CG], acc2[CG];
+#pragma unroll
+    for (int k = 0; k < CG; ++k) acc[k] = acc2[k] = 0.f;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+#pragma unroll
+      for (int ow = 0; ow < Wo; ++ow) {
+        const float a = ip[(r * Win + ow) * C];
+        float d[CG];
+        ld_cg<CG>(dp + (r * Wo + ow) * Co, d);
+#pragma unroll
+        for (int k = 0; k < CG; ++k) {
+          if (ow & 1) acc2[k] = fmaf(a, d[k], acc2[k]);
+          else acc[k] = fmaf(a, d[k], acc[k]);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < CG; ++k) atomicAdd(&red[t * Co + g * CG + k], acc[k] + acc2[k]);
+  }
+  if (L.b_off >= 0) {  // bias: column sums of the output gradient, sliced over rows
+    for (int it = threadIdx.x; it < NG * Ho; it += kSnThreads) {
+      const int g = it % NG, oh = it / NG;
+      float acc[CG];
+#pragma unroll
+      for (int k = 0; k < CG; ++k) acc[k] = 0.f;
+#pragma unroll
+      for (int ow = 0; ow < Wo; ++ow) {
+        float d[CG];
+        ld_cg<CG>(dz + (oh * Wo + ow) * Co + g * CG, d);
+#pragma unroll
+        for (int k = 0; k < CG; ++k) acc[k] += d[k];
+      }
+#pragma unroll
+      for (int k = 0; k < CG; ++k) atomicAdd(&red[T * Co + g * CG + k], acc[k]);
+    }
+  }
+  __syncthreads();
+  const int nw = L.b_off >= 0 ? n : T * Co;
+  for (int i = threadIdx.x; i < nw; i += kSnThreads) part[L.part + i] = red[i];
+}
+
+template <int CG, int KH, int KW, int C, int Co, int Win, int Hin, int Ho, int Wo>
+__device__ void sn_conv_dgrad_c(const SnLayer L, float* s) {
+  constexpr int Q = Hin * Win;
+  float* in = s + L.in;
+  const float* dz = s + L.out;
+  const float* wl = s + L.wl;
+  for (int it = threadIdx.x; it < Q * C; it += kSnThreads) {
+    const int q = it % Q, ci = it / Q;
+    const int ih = q / Win, iw = q % Win;
+    float acc = 0.f, acc2 = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < KH; ++kh) {
+      const int oh = ih - kh;
+#pragma unroll
+      for (int kw = 0; kw < KW; ++kw) {
+        const int ow = iw - kw;
+        if ((unsigned)oh < (unsigned)Ho && (unsigned)ow < (unsigned)Wo) {
+          const float* dp = dz + (oh * Wo + ow) * Co;
+          const float* wp = wl + ((kh * KW + kw) * C + ci) * Co;
+#pragma unroll
+          for (int co = 0; co < Co; co += CG) {
+            float d[CG], w[CG];
+            ld_cg<CG>(dp + co, d);
+            ld_cg<CG>(wp + co, w);
+#pragma unroll
+            for (int k = 0; k < CG; ++k) {
+              if ((co / CG) & 1) acc2 = fmaf(d[k], w[k], acc2);
+              else acc = fmaf(d[k], w[k], acc);
+            }
+          }
+        }
+      }
+    }
+    acc += acc2;
+    const int e = q * C + ci;
+    if (L.mask_in && !(in[e] > 0.f)) acc = 0.f;
+    in[e] = acc;
+  }
+}
+
+// (KH, KW, C, Co, input H, input W): LeNet-5's two convs (the first on the 32x32 zero-padded image)
+// and the DWK small CNN's conv
+#define SN_FAST_GEOS(X) \
+  X(5, 5, 1, 6, 32, 32)   \
+  X(5, 5, 6, 16, 14, 14)  \
+  X(3, 3, 1, 32, 28, 28)
+
+// phase 0 forward, 1 weight gradient, 2 input gradient; false when the geometry is not compiled in
+__device__ __forceinline__ bool sn_conv_fast(int phase, const SnLayer L, float* s, float* part) {
+  if (L.pt != 0 || L.pl != 0) return false;
+#define SN_FAST_CASE(KH_, KW_, C_, CO_, H_, W_)                                                              \
+  if (L.kh == KH_ && L.kw == KW_ && L.C == C_ && L.Co == CO_ && L.H == H_ && L.W == W_) {                    \
+    constexpr int CG = (CO_ % 4 == 0) ? 4 : ((CO_ % 2 == 0) ? 2 : 1);                                        \
+    constexpr int HO = H_ - KH_ + 1, WO = W_ - KW_ + 1;                                                      \
+    if (phase == 0) sn_conv_fwd_c<CG, KH_, KW_, C_, CO_, W_, HO, WO>(L, s);                                  \
+    else if (phase == 1) sn_conv_wgrad_c<CG, KH_, KW_, C_, CO_, W_, HO, WO>(L, s, part);                     \
+    else sn_conv_dgrad_c<CG, KH_, KW_, C_, CO_, W_, H_, HO, WO>(L, s);                                       \
+    return true;                                                                                             \
+  }
+  SN_FAST_GEOS(SN_FAST_CASE)
+#undef SN_FAST_CASE
+  return false;
+}
+
+// ---------------------------------------------------------------------------------------
 __device__ void sn_pool_fwd(const SnLayer L, float* s) {
   const float* in = s + L.in;
   float* out = s + L.out;
@@ -460,7 +639,16 @@ __global__ __launch_bounds__(kSnThreads) void smallnet_step_kernel(SnArgs a) {
   float* scratch = s;  // [kSnScratch] dense slice partials
   // the image and every conv kernel (+ bias) into LDS
   const float* xb = a.x + (long long)b * a.x_stride;
-  for (int i = threadIdx.x; i < a.n_in0; i += kSnThreads) s[a.in0 + i] = xb[i];
+  if (a.img_Hp == a.img_H && a.img_Wp == a.img_W) {
+    for (int i = threadIdx.x; i < a.n_in0; i += kSnThreads) s[a.in0 + i] = xb[i];
+  } else {
+    const int n = a.img_Hp * a.img_Wp * a.img_C;
+    for (int i = threadIdx.x; i < n; i += kSnThreads) {
+      const int c = i % a.img_C, q = i / a.img_C;
+      const int h = q / a.img_Wp - a.pad_t, w = q % a.img_Wp - a.pad_l;
+      s[a.in0 + i] = (h >= 0 && h < a.img_H && w >= 0 && w < a.img_W) ? xb[(h * a.img_W + w) * a.img_C + c] : 0.f;
+    }
+  }
   for (int l = 0; l < a.nl; ++l) {
     const SnLayer L = a.L[l];
     if (L.kind != kSnConv) continue;
@@ -481,7 +669,7 @@ __global__ __launch_bounds__(kSnThreads) void smallnet_step_kernel(SnArgs a) {
   for (int l = 0; l < a.nl; ++l) {
     const SnLayer L = a.L[l];
     if (L.kind == kSnConv) {
-      sn_by_cg(L.Co, [&](auto cg) { sn_conv_fwd<decltype(cg)::value>(L, s); });
+      if (!sn_conv_fast(0, L, s, nullptr)) sn_by_cg(L.Co, [&](auto cg) { sn_conv_fwd<decltype(cg)::value>(L, s); });
     } else if (L.kind == kSnPool) {
       sn_pool_fwd(L, s);
     } else {
@@ -546,10 +734,12 @@ __global__ __launch_bounds__(kSnThreads) void smallnet_step_kernel(SnArgs a) {
   for (int l = a.nl - 1; l >= 0; --l) {
     const SnLayer L = a.L[l];
     if (L.kind == kSnConv) {
-      sn_by_cg(L.Co, [&](auto cg) { sn_conv_wgrad<decltype(cg)::value>(L, s, part); });
+      if (!sn_conv_fast(1, L, s, part))
+        sn_by_cg(L.Co, [&](auto cg) { sn_conv_wgrad<decltype(cg)::value>(L, s, part); });
       __syncthreads();  // the weight gradient reads the input the input gradient overwrites
       stamp();
-      if (L.need_gin) sn_by_cg(L.Co, [&](auto cg) { sn_conv_dgrad<decltype(cg)::value>(L, s); });
+      if (L.need_gin && !sn_conv_fast(2, L, s, nullptr))
+        sn_by_cg(L.Co, [&](auto cg) { sn_conv_dgrad<decltype(cg)::value>(L, s); });
     } else if (L.kind == kSnPool) {
       sn_pool_bwd(L, s);
     } else {
@@ -702,7 +892,8 @@ TDE_API int tde_smallnet_limits(int* out) {
 // layers: nl x kSnLayerInts int32 (SnLayer field order).  mode 0 train (part / rec written,
 // iterations += 1), 1 eval (metrics += loss, correct, count), 2 predict (probs).
 TDE_API int tde_smallnet_step(const int* layers, int nl, int mode, int B, const float* w, const float* x,
-                              int x_stride, int in0, int n_in0, const int* y, float* part, int npart, float* rec,
+                              int x_stride, int in0, int n_in0, const int* img, const int* y, float* part, int npart,
+                              float* rec,
                               int nrec, float* metrics, long long* iterations, float scale, float* probs,
                               int probs_softmax, long long* stamps, hipStream_t stream) {
   if (nl < 1 || nl > kSnMaxLayers || B <= 0) return -1;
@@ -722,6 +913,15 @@ TDE_API int tde_smallnet_step(const int* layers, int nl, int mode, int B, const 
   a.x_stride = x_stride;
   a.in0 = in0;
   a.n_in0 = n_in0;
+  a.img_H = img[0];
+  a.img_W = img[1];
+  a.img_C = img[2];
+  a.pad_t = img[3];
+  a.pad_l = img[4];
+  a.img_Hp = img[5];
+  a.img_Wp = img[6];
+  if ((long long)a.img_Hp * a.img_Wp * a.img_C > kSnLds || a.img_Hp < a.img_H + a.pad_t || a.img_Wp < a.img_W + a.pad_l)
+    return -6;
   a.w = w;
   a.x = x;
   a.y = y;

@@ -90,12 +90,12 @@ def match_smallnet(model, loss):
             if layer.strides != (1, 1) or layer.activation not in (None, "linear", "relu"):
                 return None
             H, W, C = shape
-            (pt, _), (pl, _) = layer.pads((H, W, C))
+            (pt, pb), (pl, pr) = layer.pads((H, W, C))
             Ho, Wo, Co = layer.compute_output_shape((H, W, C))
             if Ho < 1 or Wo < 1:
                 return None
             spec.append(dict(kind=CONV, layer=layer, inp=(H, W, C), outp=(Ho, Wo, Co),
-                             relu=int(layer.activation == "relu"), pt=pt, pl=pl))
+                             relu=int(layer.activation == "relu"), pt=pt, pl=pl, pb=pb, pr=pr))
             shape = (Ho, Wo, Co)
             continue
         if isinstance(layer, L.MaxPooling2D):
@@ -143,8 +143,18 @@ class SmallNetPlan(ReplicaPlan):
         self.lib = N.hip()
         seg = store.segments
         H0, W0, C0 = spec[0]["inp"]
+        self.x_stride = H0 * W0 * C0
+        # a same-padded first conv reads the image from a zero-padded LDS copy (then it is a valid conv)
+        pad = spec[0]["kind"] == CONV and any(spec[0][k] for k in ("pt", "pb", "pl", "pr"))
+        if pad:
+            s0 = spec[0]
+            Hp, Wp = H0 + s0["pt"] + s0["pb"], W0 + s0["pl"] + s0["pr"]
+            self.img = np.array([H0, W0, C0, s0["pt"], s0["pl"], Hp, Wp], dtype=np.int32)
+            spec = [dict(spec[0], inp=(Hp, Wp, C0), pt=0, pl=0, pb=0, pr=0)] + list(spec[1:])
+        else:
+            self.img = np.array([H0, W0, C0, 0, 0, H0, W0], dtype=np.int32)
         off = lim["scratch"]                      # [0, scratch): dense slice partials
-        self.in0, self.n_in0 = off, H0 * W0 * C0
+        self.in0, self.n_in0 = off, int(self.img[5] * self.img[6] * C0)
         off = _a4(off + self.n_in0)
         rows = []
         part = 0
@@ -203,7 +213,6 @@ class SmallNetPlan(ReplicaPlan):
         self.dense = np.ascontiguousarray(np.array(dense, dtype=np.int32))
         self.ncls = spec[-1]["outp"][2]
         self.probs_softmax = int(spec[-1]["layer"].activation == "softmax")
-        self.x_stride = self.n_in0
         dev = self.device
         B = self.B
         self.part = torch.zeros(B, self.npart, dtype=torch.float32, device=dev)
@@ -228,7 +237,8 @@ class SmallNetPlan(ReplicaPlan):
         train = mode == 0
         rc = self.lib.tde_smallnet_step(
             self.layers.ctypes.data, len(self.layers), mode, B, self.store.w.data_ptr(), x.data_ptr(),
-            self.x_stride, self.in0, self.n_in0, N.ptr(y), self.part.data_ptr() if train else None, self.npart,
+            self.x_stride, self.in0, self.n_in0, self.img.ctypes.data, N.ptr(y),
+            self.part.data_ptr() if train else None, self.npart,
             self.rec.data_ptr() if train else None, self.nrec, self.metrics.data_ptr(),
             self.iterations.data_ptr(), float(self.scale), N.ptr(probs), self.probs_softmax, N.ptr(self.stamps),
             N.stream_ptr())
