@@ -2177,6 +2177,100 @@ __global__ __launch_bounds__(256) void maxpool_bwd8_w2p_kernel(PoolArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
+// BatchNorm + ReLU + MaxPool forward in one pass (the ResNet stem: conv1_bn -> conv1_relu -> pool1).
+// The BN output (the largest activation of the network, 112x112x64 per image) is never stored: each
+// pooled output reads its window of the conv output y, normalises + rectifies every element exactly
+// as bn_fwd would store it (bf16-rounded), and keeps the max and its window index for the pool's
+// backward.  The BN backward recomputes z from y, so nothing downstream needs the BN output.
+__global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(BnFwdArgs a, PoolArgs pa) {
+  __shared__ float sc[kMaxC], sf[kMaxC];
+  const int C = a.C;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float mean, var;
+    if (a.mode == 1) {
+      double s1 = 0.0, s2 = 0.0;
+      for (int sl = 0; sl < kStatSlots; ++sl) {
+        s1 += a.stats[sl * 2 * C + c];
+        s2 += a.stats[sl * 2 * C + C + c];
+      }
+      const double md = s1 / (double)a.R;
+      mean = (float)md;
+      var = (float)fmax(s2 / (double)a.R - md * md, 0.0);
+    } else {
+      mean = a.mmean[c];
+      var = a.mvar[c];
+    }
+    const float rstd = rsqrtf(var + a.eps);
+    const float scale = (a.gamma ? a.gamma[c] : 1.f) * rstd;
+    if (blockIdx.x == 0 && a.mode == 1) {
+      a.saved[c] = mean;
+      a.saved[C + c] = rstd;
+      if (a.mmean) {
+        a.mmean[c] = a.mmean[c] * a.momentum + mean * (1.f - a.momentum);
+        a.mvar[c] = a.mvar[c] * a.momentum + var * a.bessel * (1.f - a.momentum);
+      }
+    }
+    if (blockIdx.x == 0 && a.zero_buf) {
+      for (int sl = 0; sl < kStatSlots; ++sl) {
+        a.zero_buf[sl * 2 * C + c] = 0.f;
+        a.zero_buf[sl * 2 * C + C + c] = 0.f;
+      }
+    }
+    sc[c] = scale;
+    sf[c] = (a.beta ? a.beta[c] : 0.f) - mean * scale;
+  }
+  __syncthreads();
+  const Geo& g = pa.g;
+  const int C8 = C >> 3;
+  const int n = g.B * g.Ho * g.Wo * C8;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+    const int c8 = e % C8;
+    int t = e / C8;
+    const int ow = t % g.Wo;
+    t /= g.Wo;
+    const int oh = t % g.Ho;
+    const int b = t / g.Ho;
+    float k[8], s[8], best[8];
+    unsigned char bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      k[j] = sc[c8 * 8 + j];
+      s[j] = sf[c8 * 8 + j];
+      best[j] = -INFINITY;
+      bi[j] = 0;
+    }
+    for (int i = 0; i < g.KH; ++i) {
+      const int ih = oh * g.sh - g.pt + i;
+      if ((unsigned)ih >= (unsigned)g.H) continue;
+      for (int jj = 0; jj < g.KW; ++jj) {
+        const int iw = ow * g.sw - g.pl + jj;
+        if ((unsigned)iw >= (unsigned)g.W) continue;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(a.y + ((((long long)b * g.H + ih) * g.W + iw) * C + c8 * 8));
+        const unsigned char w = (unsigned char)(i * g.KW + jj);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          // the value bn_fwd would store: bf16(relu(y * scale + shift))
+          const float f = bf2f(f2bf(fmaxf(fmaf(bf2f(v[j]), k[j], s[j]), 0.f)));
+          if (f > best[j]) {
+            best[j] = f;
+            bi[j] = w;
+          }
+        }
+      }
+    }
+    bf16x8 o;
+    unsigned long long packed = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o[j] = f2bf(best[j]);
+      packed |= (unsigned long long)bi[j] << (8 * j);
+    }
+    *reinterpret_cast<bf16x8*>(pa.y + (long long)e * 8) = o;
+    if (pa.idx) *reinterpret_cast<unsigned long long*>(pa.idx + (long long)e * 8) = packed;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Global average pooling [B,HW,C] -> [B,C] and its backward; zero padding / its crop.
 __global__ __launch_bounds__(256) void gap_fwd_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int B, int HW,
                                                       int C) {
@@ -3041,6 +3135,25 @@ TDE_API int tde_maxpool(const bf16* x, bf16* y, unsigned char* idx, const bf16* 
   }
   if (!backward) maxpool_fwd_kernel<<<grid_for((long long)g.B * g.Ho * g.Wo * g.C), 256, 0, stream>>>(a);
   else maxpool_bwd_kernel<<<grid_for((long long)g.B * g.H * g.W * g.C), 256, 0, stream>>>(a);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+// BatchNorm (mode 1 batch statistics / 2 moving statistics) + ReLU + MaxPool forward (bn_relu_maxpool_fwd_kernel):
+// y [R = B*H*W, C] conv output -> pooled [B, Ho, Wo, C] + argmax bytes; geo = the pool geometry
+TDE_API int tde_bn_relu_maxpool_fwd(const bf16* y, long long R, int C, int mode, const double* stats, float* saved,
+                                    const float* gamma, const float* beta, float eps, float* mmean, float* mvar,
+                                    float momentum, float bessel, float* zero_buf, bf16* pooled, unsigned char* idx,
+                                    const int* geo, hipStream_t stream) {
+  Geo g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9], geo[10], geo[11], geo[12]};
+  if (C > kMaxC || C % 8 != 0 || g.C != C || (long long)g.B * g.H * g.W != R) return -1;
+  if (mode != 1 && mode != 2) return -1;
+  if (g.KH * g.KW > 255 || ((uintptr_t)y & 15) != 0 || ((uintptr_t)pooled & 15) != 0) return -1;
+  if (R * C >= (1LL << 31)) return -4;
+  BnFwdArgs a{y, nullptr, nullptr, R, C, mode, stats, saved, gamma, beta, eps, mmean, mvar, momentum, bessel, zero_buf, 1,
+              Drop{0.f, 0, nullptr, 0, 0}};
+  PoolArgs pa{y, pooled, idx, nullptr, nullptr, 0, g};
+  bn_relu_maxpool_fwd_kernel<<<grid_for((long long)g.B * g.Ho * g.Wo * C, 8), 256, 0, stream>>>(a, pa);
   TDE_LAUNCH_CHECK();
   return 0;
 }

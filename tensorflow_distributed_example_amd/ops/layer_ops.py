@@ -442,6 +442,29 @@ def maxpool_fwd(x, y, idx, g: ConvGeom):
     N.check(N.hip().tde_maxpool(_P(x), _P(y), _P(idx), None, None, 0, g.carray(), 0, _s()), "tde_maxpool")
 
 
+def bn_relu_maxpool_fwd(y, R, Cc, pooled, idx, g: ConvGeom, *, mode, stats=None, saved=None, gamma=None, beta=None,
+                        eps=1e-3, mmean=None, mvar=None, momentum=0.99, bessel=1.0, zero_buf=None):
+    """pooled, idx = maxpool(relu(bn(y))) without storing the BN output (the ResNet stem; see
+    csrc/kernels/layers.hip bn_relu_maxpool_fwd_kernel).  mode 1 batch statistics from ``stats`` (+ saved
+    mean/rstd, moving averages, zeroed backward accumulators as bn_fwd), 2 moving statistics."""
+    _bf(y, R * Cc, "bn_pool y")
+    _req(g.C == Cc and g.B * g.H * g.W == R, "bn_pool geometry")
+    _bf(pooled, g.B * g.Ho * g.Wo * Cc, "bn_pool pooled")
+    _req(idx.dtype == torch.uint8 and idx.numel() >= g.B * g.Ho * g.Wo * Cc, "bn_pool idx")
+    if mode == 1:
+        _f64(stats, 2 * STAT_SLOTS * Cc, "bn_pool stats")
+        _f32(saved, 2 * Cc, "bn_pool saved")
+    else:
+        _f32(mmean, Cc, "bn_pool mmean")
+        _f32(mvar, Cc, "bn_pool mvar")
+    if zero_buf is not None:
+        _f32(zero_buf, 2 * STAT_SLOTS * Cc, "bn_pool zero_buf")
+    rc = N.hip().tde_bn_relu_maxpool_fwd(_P(y), int(R), int(Cc), int(mode), _P(stats), _P(saved), _P(gamma),
+                                         _P(beta), float(eps), _P(mmean), _P(mvar), float(momentum), float(bessel),
+                                         _P(zero_buf), _P(pooled), _P(idx), g.carray(), _s())
+    N.check(rc, "tde_bn_relu_maxpool_fwd")
+
+
 def maxpool_bwd(dy, idx, dx, g: ConvGeom, accum=False):
     _bf(dy, g.B * g.Ho * g.Wo * g.C, "maxpool dy")
     _req(idx.dtype == torch.uint8 and idx.numel() >= g.B * g.Ho * g.Wo * g.C, "maxpool idx")

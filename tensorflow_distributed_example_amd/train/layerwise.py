@@ -267,6 +267,16 @@ class LayerwisePlan(PG.ReplicaPlan):
             if (isinstance(prev, _Gemm) and not prev.conv and prev.out.root() is head.inp.root()
                     and len(T[prev.out.id].consumers) == 1 and not prev.stats):
                 head.absorb(prev)
+        # BatchNorm + ReLU whose only consumer is a MaxPool (the ResNet stem): one pass reads the conv output
+        # and writes the pooled output + argmax; the BN output itself is never stored (its backward recomputes
+        # z from the conv output).  TDE_BN_POOL=0 keeps the two launches.
+        if os.environ.get("TDE_BN_POOL", "1") != "0":
+            for i, st in enumerate(stages[:-1]):
+                nxt = stages[i + 1]
+                if (isinstance(st, _Elementwise) and st.bn and st.relu and st.res is None and st.drop.rate == 0
+                        and isinstance(nxt, _MaxPool) and nxt.inp.root() is st.out.root()
+                        and len(T[st.out.id].consumers) == 1 and st.inp.C % 8 == 0):
+                    st.pool, nxt.fused = nxt, True
         # gradient accumulation flags: reverse order, first writer stores
         written = set()
         for st in reversed(stages):
@@ -545,6 +555,7 @@ class _Elementwise(_Stage):
         self.lid = lid
         self.defer_to = None
         self.stats_from_gemm = False
+        self.pool = None  # _MaxPool whose forward this BN+ReLU stage runs in the same pass
         if isinstance(layer, L.Dropout):
             self.set_dropout(layer)
         st = plan.store
@@ -613,10 +624,21 @@ class _Elementwise(_Stage):
                 O.colstats(self.inp.root().buf, R, C, stats)
             upd = mode == "train"
             bessel = (R / max(R - 1, 1)) if L_.fused else 1.0
+            if self.pool is not None:
+                O.bn_relu_maxpool_fwd(self.inp.root().buf, R, C, self.pool.out.root().buf, self.pool.idx,
+                                      self.pool.geo.with_batch(B), mode=1, stats=stats, saved=self.saved,
+                                      gamma=self.gamma, beta=self.beta, eps=L_.epsilon,
+                                      mmean=self.mmean if upd else None, mvar=self.mvar if upd else None,
+                                      momentum=L_.momentum, bessel=bessel, zero_buf=self.dstats if upd else None)
+                return
             O.bn_fwd(self.inp.root().buf, self.out.root().buf, R, C, mode=1, stats=stats, saved=self.saved,
                      gamma=self.gamma, beta=self.beta, eps=L_.epsilon, mmean=self.mmean if upd else None,
                      mvar=self.mvar if upd else None, momentum=L_.momentum, bessel=bessel,
                      zero_buf=self.dstats if upd else None, **kw)
+        elif self.pool is not None:
+            O.bn_relu_maxpool_fwd(self.inp.root().buf, R, C, self.pool.out.root().buf, self.pool.idx,
+                                  self.pool.geo.with_batch(B), mode=2, gamma=self.gamma, beta=self.beta,
+                                  eps=L_.epsilon, mmean=self.mmean, mvar=self.mvar)
         else:
             O.bn_fwd(self.inp.root().buf, self.out.root().buf, R, C, mode=2, gamma=self.gamma, beta=self.beta,
                      eps=L_.epsilon, mmean=self.mmean, mvar=self.mvar, **kw)
@@ -650,6 +672,7 @@ class _MaxPool(_Stage):
             pt = pl = 0
         self.geo = O.ConvGeom(plan.B, H, W_, C, Ho, Wo, C, layer.pool_size[0], layer.pool_size[1],
                               layer.strides[0], layer.strides[1], pt, pl)
+        self.fused = False  # the producing BN+ReLU stage runs this pool's forward (bn_relu_maxpool_fwd)
 
     def alloc(self, B, dev):
         self.idx = torch.zeros(B * self.out.numel, dtype=torch.uint8, device=dev)
@@ -658,6 +681,8 @@ class _MaxPool(_Stage):
         return [self.inp] if self.inp.root().id != 0 else []
 
     def fwd(self, p, B, training, mode="train"):
+        if self.fused:
+            return
         O.maxpool_fwd(self.inp.root().buf, self.out.root().buf, self.idx, self.geo.with_batch(B))
 
     def bwd(self, p, B):

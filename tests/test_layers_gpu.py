@@ -762,3 +762,61 @@ def test_strided_dgrad_single_launch_matches_per_phase(B, H, W, C, Co, k, s, pad
     torch.cuda.synchronize()
     assert not torch.isnan(outs[0][0].float()).any()
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("B,H,W,C,mode", [(2, 112, 112, 64, 1), (3, 15, 13, 16, 1), (2, 16, 16, 64, 2)])
+def test_bn_relu_maxpool_fused_matches_two_passes(B, H, W, C, mode):
+    """The stem's BN + ReLU + MaxPool(3, 2, same) in one pass (tde_bn_relu_maxpool_fwd) gives the pooled
+    output, argmax bytes, saved statistics, moving averages and zeroed accumulators of bn_fwd + maxpool_fwd
+    bit for bit (the BN output is never stored)."""
+    from tensorflow_distributed_example_amd.ops import layer_ops as O
+    R = B * H * W
+    Ho, Wo = -(-H // 2), -(-W // 2)
+    (pt, _), (pl, _) = _tf_same(H, 3, 2), _tf_same(W, 3, 2)
+    g = O.ConvGeom(B, H, W, C, Ho, Wo, C, 3, 3, 2, 2, pt, pl)
+    y = _r(R, C, seed=41, scale=2.0) + 0.2
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.3
+    stats = _stats_buf(C)
+    O.colstats(y, R, C, stats)
+    outs = []
+    for fused in (False, True):
+        saved = torch.zeros(2 * C, device=DEV)
+        mm, mv = torch.full((C,), 0.1, device=DEV), torch.full((C,), 0.9, device=DEV)
+        zb = torch.full((2 * SLOTS * C,), 3.0, device=DEV)
+        pooled = torch.full((B * Ho * Wo * C,), float("nan"), device=DEV).to(bf)
+        idx = torch.full((B * Ho * Wo * C,), 77, dtype=torch.uint8, device=DEV)
+        kw = dict(mode=mode, stats=stats if mode == 1 else None, saved=saved if mode == 1 else None, gamma=gamma,
+                  beta=beta, eps=1e-5, mmean=mm, mvar=mv, momentum=0.9, bessel=R / (R - 1),
+                  zero_buf=zb if mode == 1 else None)
+        if fused:
+            O.bn_relu_maxpool_fwd(y, R, C, pooled, idx, g, **kw)
+        else:
+            out = torch.zeros(R, C, dtype=bf, device=DEV)
+            O.bn_fwd(y, out, R, C, relu=True, **kw)
+            O.maxpool_fwd(out, pooled, idx, g)
+        outs.append((pooled, idx, saved, mm, mv, zb))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert not torch.isnan(outs[1][0].float()).any()
+    # and against fp64 torch: relu(bn(y)) then max_pool2d with TF-SAME padding (-inf pads)
+    mean, var = _cpu64(y).mean(0), _cpu64(y).var(0, unbiased=False)
+    if mode == 2:
+        mean, var = torch.full((C,), 0.1, dtype=torch.float64), torch.full((C,), 0.9, dtype=torch.float64)
+    z = torch.relu((_cpu64(y) - mean) / torch.sqrt(var + 1e-5) * _cpu64(gamma) + _cpu64(beta))
+    z = z.view(B, H, W, C).permute(0, 3, 1, 2)
+    (_, pb), (_, pr) = _tf_same(H, 3, 2), _tf_same(W, 3, 2)
+    ref = F.max_pool2d(F.pad(z, (pl, pr, pt, pb), value=float("-inf")), 3, 2).permute(0, 2, 3, 1).reshape(-1)
+    assert _rel(outs[1][0].float().cpu(), ref) < 1e-2
+
+
+def test_resnet18_plan_fuses_stem_bn_pool():
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.train import layerwise as LW
+    m = tde.zoo.resnet18()
+    m.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True), optimizer=tde.optimizers.SGD(0.1))
+    plan = m._program("train", 8).plans[0]
+    fused = [st for st in plan.stages if isinstance(st, LW._Elementwise) and st.pool is not None]
+    assert [st.layer.name for st in fused] == ["conv1_bn"]
+    assert fused[0].pool.fused
