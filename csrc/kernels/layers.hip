@@ -2134,7 +2134,8 @@ __global__ __launch_bounds__(256) void maxpool_bwd8_w2p_kernel(PoolArgs a) {
     for (int q = 0; q < 4; ++q) {
       const int oh = oh_lo + (q >> 1), ow = ow_lo + (q & 1);
       id[q] = ~0ull;  // byte 0xFF never equals a window index (host: KH*KW < 255)
-      wi0[q] = wi1[q] = 0xFFu;
+      wi0[q] = wi1[q] = 0x100u;  // matches no argmax byte (0xFF included: id[q] of a missing window)
+      d[q] = zero8();
       if (oh <= oh_hi && ow <= ow_hi) {
         const long long o = (((long long)b * g.Ho + oh) * g.Wo + ow) * g.C + c8 * 8;
         id[q] = *reinterpret_cast<const unsigned long long*>(a.idx + o);
@@ -2267,6 +2268,164 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(BnFwdArgs a, P
     }
     *reinterpret_cast<bf16x8*>(pa.y + (long long)e * 8) = o;
     if (pa.idx) *reinterpret_cast<unsigned long long*>(pa.idx + (long long)e * 8) = packed;
+  }
+}
+
+// Backward of the fused stem: BN backward whose output gradient is the MaxPool's input gradient,
+// gathered on the fly from the pooled gradient + argmax bytes (as maxpool_bwd8_w2p_kernel does, <= 2 x 2
+// windows per pixel) instead of being stored and re-read.  PASS 0: per-channel sums of dz and dz * xhat
+// (dz = gathered gradient, bf16-rounded as the pool backward would store it, masked by the ReLU) into
+// dstats; PASS 1: dx = scale * (dz - mean(dz) - xhat * mean(dz * xhat)) (+ dbeta / dgamma, zero the
+// forward statistics), as bn_bwd_apply_tiled_kernel.  A thread owns input pixels (2t, 2t+1) of one row
+// and 8 channels; 256 % (C / 8) == 0 keeps its channels fixed over the grid stride.
+constexpr int kBnPoolRow = 4096;  // elements of one staged pooled row (Wo * C)
+template <int PASS>
+__global__ __launch_bounds__(256) void bn_pool_bwd_kernel(BnBwdArgs a, PoolArgs pa) {
+  __shared__ float l[6][512];  // sc, sf, mu, rs, k1, k2 per channel
+  // PASS 0's fold [256][16] f32, and (aliased, per row) two staged pooled rows: dy bf16 + argmax bytes
+  __shared__ __attribute__((aligned(16))) float fold[(2 * kBnPoolRow * 3 + 3) / 4 > 4096 ? (2 * kBnPoolRow * 3 + 3) / 4 : 4096];
+  const int C = a.C;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float mu = a.saved[c], rs = a.saved[C + c];
+    const float sc = (a.gamma ? a.gamma[c] : 1.f) * rs;
+    l[0][c] = sc;
+    l[1][c] = (a.beta ? a.beta[c] : 0.f) - mu * sc;
+    l[2][c] = mu;
+    l[3][c] = rs;
+    if (PASS == 1) {
+      float sdz = 0.f, sdx = 0.f;
+#pragma unroll
+      for (int sl = 0; sl < kStatSlots; ++sl) {
+        sdz += a.dstats[sl * 2 * C + c];
+        sdx += a.dstats[sl * 2 * C + C + c];
+      }
+      l[4][c] = sdz / (float)a.R;
+      l[5][c] = sdx / (float)a.R;
+      if (blockIdx.x == 0) {
+        if (a.dbeta) a.dbeta[c] += sdz;
+        if (a.dgamma) a.dgamma[c] += sdx;
+        if (a.zero_fwd)
+          for (int sl = 0; sl < kStatSlots; ++sl) {
+            a.zero_fwd[sl * 2 * C + c] = 0.0;
+            a.zero_fwd[sl * 2 * C + C + c] = 0.0;
+          }
+      }
+    }
+  }
+  const Geo& g = pa.g;
+  const int C8 = C >> 3, W2 = (g.W + 1) >> 1;
+  const int c8 = threadIdx.x % C8;
+  float k[6][8];
+  float r1[8], r2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r1[j] = r2[j] = 0.f;
+  const int rowlen = g.Wo * C;  // elements of one pooled row (host: <= kBnPoolRow)
+  bf16* const sdy = reinterpret_cast<bf16*>(fold);                              // [2][rowlen]
+  unsigned char* const sid = reinterpret_cast<unsigned char*>(sdy + 2 * kBnPoolRow);  // [2][rowlen]
+  for (int row = blockIdx.x; row < g.B * g.H; row += gridDim.x) {
+    const int b = row / g.H, ih = row - b * g.H;
+    const int ty = ih + g.pt;
+    const int oh_lo = ty >= g.KH ? (ty - g.KH) / g.sh + 1 : 0, oh_hi = min(g.Ho - 1, ty / g.sh);
+    __syncthreads();  // coefficients written (first row) / the previous row's gathers done
+    if (row == (int)blockIdx.x) {
+#pragma unroll
+      for (int q = 0; q < 6; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) k[q][j] = (PASS == 1 || q < 4) ? l[q][c8 * 8 + j] : 0.f;
+    }
+    // the <= 2 pooled rows this input row reads: 16-byte coalesced loads of dy and the argmax bytes into LDS
+    for (int r = 0; r <= oh_hi - oh_lo; ++r) {
+      const long long o = ((long long)b * g.Ho + oh_lo + r) * rowlen;
+      for (int i = threadIdx.x; i < rowlen / 8; i += blockDim.x)
+        *reinterpret_cast<bf16x8*>(sdy + r * kBnPoolRow + i * 8) = *reinterpret_cast<const bf16x8*>(pa.dy + o + i * 8);
+      for (int i = threadIdx.x; i < rowlen / 16; i += blockDim.x)
+        *reinterpret_cast<uint4*>(sid + r * kBnPoolRow + i * 16) = *reinterpret_cast<const uint4*>(pa.idx + o + i * 16);
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < W2 * C8; e += blockDim.x) {
+      const int iw2 = e / C8;
+      const int iw0 = 2 * iw2, tx0 = iw0 + g.pl;
+      const int ow_lo = tx0 >= g.KW ? (tx0 - g.KW) / g.sw + 1 : 0, ow_hi = min(g.Wo - 1, (tx0 + 1) / g.sw);
+      const long long px0 = (long long)row * g.W + iw0;
+      bf16x8 yv[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        yv[h] = iw0 + h < g.W ? *reinterpret_cast<const bf16x8*>(a.y + (px0 + h) * C + c8 * 8) : zero8();
+      float s0[8], s1[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s0[j] = s1[j] = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int oh = oh_lo + (q >> 1), ow = ow_lo + (q & 1);
+        if (oh > oh_hi || ow > ow_hi) continue;
+        const int lo = (q >> 1) * kBnPoolRow + ow * C + c8 * 8;
+        const unsigned long long id = *reinterpret_cast<const unsigned long long*>(sid + lo);
+        const bf16x8 d = *reinterpret_cast<const bf16x8*>(sdy + lo);
+        const int i = ty - oh * g.sh, j0 = tx0 - ow * g.sw;
+        const unsigned w0 = (j0 >= 0 && j0 < g.KW) ? (unsigned)(i * g.KW + j0) : 0x100u;
+        const unsigned w1 = (j0 + 1 >= 0 && j0 + 1 < g.KW) ? (unsigned)(i * g.KW + j0 + 1) : 0x100u;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const unsigned w = (unsigned)((id >> (8 * j)) & 0xFF);
+          const float v = bf2f(d[j]);
+          if (w == w0) s0[j] += v;
+          if (w == w1) s1[j] += v;
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (iw0 + h >= g.W) break;
+        const float* sv = h ? s1 : s0;
+        float dx[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = bf2f(yv[h][j]);
+          const float z = v * k[0][j] + k[1][j];
+          const float dz = (a.relu && !(z > 0.f)) ? 0.f : bf2f(f2bf(sv[j]));  // the pool backward's stored value
+          const float xh = (v - k[2][j]) * k[3][j];
+          if (PASS == 0) {
+            r1[j] += dz;
+            r2[j] += dz * xh;
+          } else {
+            dx[j] = k[0][j] * (dz - k[4][j] - xh * k[5][j]);
+          }
+        }
+        if (PASS == 1) {
+          bf16x8* out = reinterpret_cast<bf16x8*>(a.dx + (px0 + h) * C + c8 * 8);
+          bf16x8 o;
+          if (a.dx_accum) {
+            const bf16x8 prev = *out;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = f2bf(dx[j] + bf2f(prev[j]));
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = f2bf(dx[j]);
+          }
+          *out = o;
+        }
+      }
+    }
+  }
+  if (PASS == 0) {
+    // fold the 256 / C8 threads of each channel octet, then one atomic pair per channel per block
+    __syncthreads();  // the staged pooled rows share this LDS
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      fold[threadIdx.x * 16 + j] = r1[j];
+      fold[threadIdx.x * 16 + 8 + j] = r2[j];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      const int o8 = c >> 3, j = c & 7;
+      float a1 = 0.f, a2 = 0.f;
+      for (int t = o8; t < 256; t += C8) {
+        a1 += fold[t * 16 + j];
+        a2 += fold[t * 16 + 8 + j];
+      }
+      float* ds = a.dstats + (size_t)(blockIdx.x % kStatSlots) * 2 * C;
+      atomicAdd(&ds[c], a1);
+      atomicAdd(&ds[C + c], a2);
+    }
   }
 }
 
@@ -3154,6 +3313,32 @@ TDE_API int tde_bn_relu_maxpool_fwd(const bf16* y, long long R, int C, int mode,
               Drop{0.f, 0, nullptr, 0, 0}};
   PoolArgs pa{y, pooled, idx, nullptr, nullptr, 0, g};
   bn_relu_maxpool_fwd_kernel<<<grid_for((long long)g.B * g.Ho * g.Wo * C, 8), 256, 0, stream>>>(a, pa);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+// Backward of tde_bn_relu_maxpool_fwd (bn_pool_bwd_kernel): pooled gradient dpool [B, Ho, Wo, C] + argmax bytes
+// -> the BN input gradient dx [R, C] (dstats: [slots][2][C] f32, zeroed by the forward)
+TDE_API int tde_bn_pool_bwd(const bf16* dpool, const unsigned char* idx, const bf16* y, long long R, int C,
+                            const float* saved, const float* gamma, const float* beta, int relu, float* dstats, bf16* dx,
+                            int dx_accum, float* dgamma, float* dbeta, double* zero_fwd, const int* geo,
+                            hipStream_t stream) {
+  Geo g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9], geo[10], geo[11], geo[12]};
+  if (C > 512 || C % 8 != 0 || 256 % (C / 8) != 0 || g.C != C || (long long)g.B * g.H * g.W != R) return -1;
+  if ((g.KH + g.sh - 1) / g.sh > 2 || (g.KW + g.sw) / g.sw > 2 || g.KH * g.KW >= 255) return -1;
+  if (((uintptr_t)y & 15) != 0 || ((uintptr_t)dx & 15) != 0 || ((uintptr_t)dpool & 15) != 0 || !saved || !dstats)
+    return -1;
+  if (R * C >= (1LL << 31)) return -4;
+  BnBwdArgs a{nullptr, y, nullptr, R, C, 1, saved, gamma, beta, relu, Drop{0.f, 0, nullptr, 0, 0}, dstats, dx,
+              dx_accum, nullptr, 0, dgamma, dbeta, zero_fwd};
+  PoolArgs pa{nullptr, nullptr, const_cast<unsigned char*>(idx), dpool, dx, dx_accum, g};
+  if ((long long)g.Wo * C > kBnPoolRow || (g.Wo * C) % 16 != 0 || ((uintptr_t)idx & 15) != 0) return -1;
+  // one input row per block iteration (its <= 2 pooled rows staged in LDS); the reduction ends with 2*C
+  // atomics per block, so it takes a moderate grid, the apply pass one block per row
+  const int rows = g.B * g.H;
+  bn_pool_bwd_kernel<0><<<rows < 1024 ? rows : 1024, 256, 0, stream>>>(a, pa);
+  TDE_LAUNCH_CHECK();
+  bn_pool_bwd_kernel<1><<<rows < 16384 ? rows : 16384, 256, 0, stream>>>(a, pa);
   TDE_LAUNCH_CHECK();
   return 0;
 }

@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/stem
 mkdir -p $OUT
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_layers_gpu.py \
-  -k "bn_relu_maxpool or fuses_stem or small_resnet or maxpool or batchnorm" > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
+  -k "bn_relu_maxpool or fuses_stem or small_resnet or maxpool or batchnorm or resnet" > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
 tail -3 $OUT/pytest.log
 for i in 1 2; do
   for e in 0 1; do

@@ -62,6 +62,7 @@ _HIP_PROTOS = {
     "tde_act_bwd": (i32, [p, p, i64, i32, i32, p, p, p]),
     "tde_maxpool": (i32, [p, p, p, p, p, i32, p, i32, p]),
     "tde_bn_relu_maxpool_fwd": (i32, [p, i64, i32, i32, p, p, p, p, f32, p, p, f32, f32, p, p, p, p, p]),
+    "tde_bn_pool_bwd": (i32, [p, p, p, i64, i32, p, p, p, i32, p, p, i32, p, p, p, p, p]),
     "tde_gap": (i32, [p, p, i32, i32, i32, i32, i32, p]),
     "tde_pad": (i32, [p, p, p, i32, i32, p]),
     "tde_xent": (i32, [p, i64, p, i32, i32, f32, p, i64, p, p, i32, p, p]),

@@ -465,6 +465,24 @@ def bn_relu_maxpool_fwd(y, R, Cc, pooled, idx, g: ConvGeom, *, mode, stats=None,
     N.check(rc, "tde_bn_relu_maxpool_fwd")
 
 
+def bn_pool_bwd(dpool, idx, y, R, Cc, g: ConvGeom, *, saved, dstats, dx, gamma=None, beta=None, relu=True,
+                dx_accum=False, dgamma=None, dbeta=None, zero_fwd=None):
+    """Backward of bn_relu_maxpool_fwd: the BN input gradient ``dx`` from the POOLED gradient + argmax bytes (the
+    pool's input gradient is gathered per element, never stored); two passes (sums, apply) as bn_bwd."""
+    _bf(dpool, g.B * g.Ho * g.Wo * Cc, "bn_pool_bwd dpool")
+    _req(idx.dtype == torch.uint8 and idx.numel() >= g.B * g.Ho * g.Wo * Cc, "bn_pool_bwd idx")
+    _bf(y, R * Cc, "bn_pool_bwd y")
+    _bf(dx, R * Cc, "bn_pool_bwd dx")
+    _f32(saved, 2 * Cc, "bn_pool_bwd saved")
+    _f32(dstats, 2 * STAT_SLOTS * Cc, "bn_pool_bwd dstats")
+    if zero_fwd is not None:
+        _f64(zero_fwd, 2 * STAT_SLOTS * Cc, "bn_pool_bwd zero_fwd")
+    rc = N.hip().tde_bn_pool_bwd(_P(dpool), _P(idx), _P(y), int(R), int(Cc), _P(saved), _P(gamma), _P(beta), int(relu),
+                                 _P(dstats), _P(dx), int(dx_accum), _P(dgamma), _P(dbeta), _P(zero_fwd), g.carray(),
+                                 _s())
+    N.check(rc, "tde_bn_pool_bwd")
+
+
 def maxpool_bwd(dy, idx, dx, g: ConvGeom, accum=False):
     _bf(dy, g.B * g.Ho * g.Wo * g.C, "maxpool dy")
     _req(idx.dtype == torch.uint8 and idx.numel() >= g.B * g.Ho * g.Wo * g.C, "maxpool idx")

@@ -275,7 +275,8 @@ class LayerwisePlan(PG.ReplicaPlan):
                 nxt = stages[i + 1]
                 if (isinstance(st, _Elementwise) and st.bn and st.relu and st.res is None and st.drop.rate == 0
                         and isinstance(nxt, _MaxPool) and nxt.inp.root() is st.out.root()
-                        and len(T[st.out.id].consumers) == 1 and st.inp.C % 8 == 0):
+                        and len(T[st.out.id].consumers) == 1 and st.inp.C % 8 == 0 and 256 % (st.inp.C // 8) == 0
+                        and st.inp.root().id != 0):
                     st.pool, nxt.fused = nxt, True
         # gradient accumulation flags: reverse order, first writer stores
         written = set()
@@ -649,6 +650,12 @@ class _Elementwise(_Stage):
         rr = self.res.root() if self.res is not None else None
         dx = ir.grad if ir.id != 0 else None
         dres = rr.grad if (rr is not None and rr.id != 0) else None
+        if self.pool is not None:
+            O.bn_pool_bwd(self.pool.out.root().grad, self.pool.idx, ir.buf, R, C, self.pool.geo.with_batch(B),
+                          saved=self.saved, dstats=self.dstats, dx=dx, gamma=self.gamma, beta=self.beta, relu=True,
+                          dx_accum=self.accum.get(ir.id, False), dgamma=self.ggamma, dbeta=self.gbeta,
+                          zero_fwd=self._stats())
+            return
         O.bn_bwd(self.out.root().grad, ir.buf, R, C, mode=1 if self.bn else 0,
                  saved=self.saved if self.bn else None, gamma=self.gamma if self.bn else None,
                  beta=self.beta if self.bn else None, res=rr.buf if rr is not None else None, relu=self.relu,
@@ -686,7 +693,7 @@ class _MaxPool(_Stage):
         O.maxpool_fwd(self.inp.root().buf, self.out.root().buf, self.idx, self.geo.with_batch(B))
 
     def bwd(self, p, B):
-        if self.inp.root().id == 0:
+        if self.inp.root().id == 0 or self.fused:
             return
         O.maxpool_bwd(self.out.root().grad, self.idx, self.inp.root().grad, self.geo.with_batch(B),
                       accum=self.accum[self.inp.root().id])

@@ -809,6 +809,32 @@ def test_bn_relu_maxpool_fused_matches_two_passes(B, H, W, C, mode):
     (_, pb), (_, pr) = _tf_same(H, 3, 2), _tf_same(W, 3, 2)
     ref = F.max_pool2d(F.pad(z, (pl, pr, pt, pb), value=float("-inf")), 3, 2).permute(0, 2, 3, 1).reshape(-1)
     assert _rel(outs[1][0].float().cpu(), ref) < 1e-2
+    if mode != 1:
+        return
+    # backward: pool backward + two-pass BN backward vs the fused gather (the pool's input gradient never stored)
+    idx, saved = outs[1][1], outs[1][2]
+    dpool = _r(B * Ho * Wo * C, seed=42)
+    grads = []
+    for fused in (False, True):
+        dst = torch.zeros(2 * SLOTS * C, device=DEV)
+        dx = torch.full((R, C), float("nan"), device=DEV).to(bf)
+        dg, db = torch.ones(C, device=DEV), torch.ones(C, device=DEV)
+        zf = _stats_buf(C).fill_(1.0)
+        if fused:
+            O.bn_pool_bwd(dpool, idx, y, R, C, g, saved=saved, dstats=dst, dx=dx, gamma=gamma, beta=beta, relu=True,
+                          dgamma=dg, dbeta=db, zero_fwd=zf)
+        else:
+            dout = torch.full((R, C), float("nan"), device=DEV).to(bf)
+            O.maxpool_bwd(dpool, idx, dout, g)
+            O.bn_bwd(dout, y, R, C, mode=1, saved=saved, gamma=gamma, beta=beta, relu=True, dstats=dst, dx=dx,
+                     dgamma=dg, dbeta=db, zero_fwd=zf)
+        grads.append((dx, dg, db, zf))
+    torch.cuda.synchronize()
+    (dx0, dg0, db0, zf0), (dx1, dg1, db1, zf1) = grads
+    assert not torch.isnan(dx1.float()).any()
+    assert _rel(dx1.float(), dx0.float()) < 2e-3
+    assert _rel(dg1, dg0) < 1e-4 and _rel(db1, db0) < 1e-4
+    assert zf1.abs().max().item() == 0.0 and zf0.abs().max().item() == 0.0
 
 
 def test_resnet18_plan_fuses_stem_bn_pool():
