@@ -2801,7 +2801,10 @@ static unsigned long long g_big_launches = 0;
 // loop) measured it neutral; with the LDS-DMA loop it pays for the weight gradients only.
 static int g_xcd = -1;
 // split-K weight gradients with at most this many splits store partials + reduce; more splits use atomics
-static int g_wg_scratch_max = 16;
+static int g_wg_scratch_max = [] {
+  const char* e = getenv("TDE_WG_SCRATCH_MAX");
+  return e ? atoi(e) : 16;
+}();
 // weight gradients through the row-padded LDS-DMA path (TDE_WGRAD_DMA=0: the register-staged loaders)
 // 0 = off, 1 = 3 LDS stages, 2 = 2 stages, 3 = per shape (default; bench/resnet_layers.py --sweep-wgrad,
 // profiles/r2_sweep_wgrad.txt): Co <= 64 (ResNet stage 1) keeps the register-staged loaders (the row padding
