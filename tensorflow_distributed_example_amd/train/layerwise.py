@@ -120,6 +120,12 @@ class LayerwisePlan(PG.ReplicaPlan):
         self.model = model
         self._compile()
         self._alloc()
+        # TDE_WGRAD_STREAM=1: weight gradients on a side stream, concurrent with the input-gradient chain
+        # (joined at the end of the backward).  Off by default: measured slower in the captured step
+        # (ResNet-18 20.7k -> 20.0k, Model B 511k -> 457k img/s; profiles/r2_ab_notes.md).
+        self.side_stream = None
+        if torch.device(device).type == "cuda" and os.environ.get("TDE_WGRAD_STREAM", "0") == "1":
+            self.side_stream = torch.cuda.Stream(device=device)
         shadows = {}
         for st in self.stages:
             for name, want in getattr(st, "shadows", {}).items():
@@ -342,6 +348,8 @@ class LayerwisePlan(PG.ReplicaPlan):
             st.bwd(self, B)
             if after_bwd is not None:
                 after_bwd(i)
+        if self.side_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.side_stream)
 
     def grad_buckets(self, target_elems):
         """Reverse-order gradient buckets: [(i, lo, hi)] = once backward stage i (reverse order) is
@@ -512,6 +520,28 @@ class _Gemm(_Stage):
             O.act_bwd(dout, self.out.root().buf, self.out.rows(B), self.out.C, relu=self.relu, dz=self.dz,
                       dbias=self.gb)
             dout = self.dz
+        side = p.side_stream
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream(p.device))
+            with torch.cuda.stream(side):
+                self._wgrad(p, B, dout)
+        else:
+            self._wgrad(p, B, dout)
+        if not self.need_dgrad:
+            return
+        if self.conv:
+            g = self.geo.with_batch(B)
+            if self.small_dgrad:
+                O.smallconv_dgrad(dout, self.Wrow, self.inp.root().grad, g, accum=self.accum[self.inp.root().id])
+            else:
+                O.conv_dgrad(dout, self.Wrow, self.inp.root().grad, g, accum=self.accum[self.inp.root().id],
+                             scratch=p.scratch)
+        else:
+            O.dense_dgrad(dout, self.Wrow, self.inp.root().grad, self.inp.rows(B),
+                          accum=self.accum[self.inp.root().id], scratch=p.scratch)
+
+    def _wgrad(self, p, B, dout):
+        """This layer's weight gradient (all of it on the plan's side stream when there is one)."""
         if self.conv:
             g = self.geo.with_batch(B)
             if self.use_stem_pack:
@@ -523,17 +553,9 @@ class _Gemm(_Stage):
                 O.smallconv_wgrad(self.inp.buf, dout, self.gW, g)
             else:
                 O.conv_wgrad(self.inp.buf, dout, self.gW, g, scratch=p.wscratch)
-            if self.need_dgrad and self.small_dgrad:
-                O.smallconv_dgrad(dout, self.Wrow, self.inp.root().grad, g, accum=self.accum[self.inp.root().id])
-            elif self.need_dgrad:
-                O.conv_dgrad(dout, self.Wrow, self.inp.root().grad, g, accum=self.accum[self.inp.root().id],
-                             scratch=p.scratch)
         else:
-            rows = self.inp.rows(B)
-            O.dense_wgrad(self.inp.buf, dout, self.gW.view(self.W.shape[0], -1), rows, scratch=p.wscratch)
-            if self.need_dgrad:
-                O.dense_dgrad(dout, self.Wrow, self.inp.root().grad, rows, accum=self.accum[self.inp.root().id],
-                              scratch=p.scratch)
+            O.dense_wgrad(self.inp.buf, dout, self.gW.view(self.W.shape[0], -1), self.inp.rows(B),
+                          scratch=p.wscratch)
 
 
 class _Elementwise(_Stage):

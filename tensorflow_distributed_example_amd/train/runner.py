@@ -221,9 +221,13 @@ class Program:
         for i, lo, hi in self.buckets:
             ready.setdefault(i, []).append((lo, hi))
 
+        side = getattr(plan, "side_stream", None)   # weight gradients of the layer-wise plan
+
         def after_bwd(i):
             for lo, hi in ready.get(i, ()):
                 cs.wait_stream(main)
+                if side is not None:
+                    cs.wait_stream(side)
                 with torch.cuda.stream(cs):
                     self.comm.all_reduce_([g[lo:hi]])
 
