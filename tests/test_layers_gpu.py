@@ -846,3 +846,36 @@ def test_resnet18_plan_fuses_stem_bn_pool():
     fused = [st for st in plan.stages if isinstance(st, LW._Elementwise) and st.pool is not None]
     assert [st.layer.name for st in fused] == ["conv1_bn"]
     assert fused[0].pool.fused
+
+
+def test_fused_stem_fit_evaluate_predict_match_unfused(monkeypatch):
+    """A mini ResNet trained, evaluated and used for prediction with the fused stem (BN + ReLU + MaxPool,
+    TDE_BN_POOL=1) and without it: same losses, metrics, moving statistics and predictions (the forward is
+    bit-identical; the backward differs only in the BN sums' summation order)."""
+    import tensorflow_distributed_example_amd as tde
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((32, 32, 32, 3), dtype=np.float32)
+    y = rng.integers(0, 10, 32)
+    runs = []
+    init = None
+    for fused in ("0", "1"):
+        monkeypatch.setenv("TDE_BN_POOL", fused)
+        tde.backend.set_random_seed(3)
+        m = _mini_resnet(tde)
+        m.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True), optimizer=tde.optimizers.SGD(0.01),
+                  metrics=["accuracy"])
+        m.build()
+        if init is None:
+            init = m.get_weights()
+        else:
+            m.set_weights(init)
+        h = m.fit(x, y, batch_size=16, epochs=1, verbose=0, shuffle=False)
+        ev = m.evaluate(x, y, batch_size=16, verbose=0, return_dict=True)
+        pr = m.predict(x, batch_size=16)
+        runs.append((h.history["loss"][0], ev, np.asarray(pr), m.get_weights()))
+    (l0, e0, p0, w0), (l1, e1, p1, w1) = runs
+    assert abs(l0 - l1) <= 1e-3 * abs(l0)
+    assert abs(e0["loss"] - e1["loss"]) <= 1e-2 * abs(e0["loss"])
+    assert np.abs(p0 - p1).max() <= 1e-2 * (np.abs(p0).max() + 1e-6)
+    for a, b in zip(w0, w1):
+        assert np.abs(a - b).max() <= 1e-2 * (np.abs(a).max() + 1e-3)
