@@ -2279,19 +2279,26 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(BnFwdArgs a, P
 // forward statistics), as bn_bwd_apply_tiled_kernel.  A thread owns input pixels (2t, 2t+1) of one row
 // and 8 channels; 256 % (C / 8) == 0 keeps its channels fixed over the grid stride.
 constexpr int kBnPoolRow = 4096;  // elements of one staged pooled row (Wo * C)
+// dynamic LDS of bn_pool_bwd_kernel: [6][C] coefficients, then PASS 0's fold [256][16] f32 aliased with the
+// two staged pooled rows (dy bf16 + argmax bytes) — sized per launch so small layers keep more blocks per CU
+static size_t bn_pool_bwd_lds(int C, int rowlen) {
+  const size_t stage = (size_t)2 * rowlen * 3, fold = 256 * 16 * 4;
+  return (size_t)6 * C * 4 + ((stage > fold ? stage : fold) + 15) / 16 * 16;
+}
 template <int PASS>
 __global__ __launch_bounds__(256) void bn_pool_bwd_kernel(BnBwdArgs a, PoolArgs pa) {
-  __shared__ float l[6][512];  // sc, sf, mu, rs, k1, k2 per channel
-  // PASS 0's fold [256][16] f32, and (aliased, per row) two staged pooled rows: dy bf16 + argmax bytes
-  __shared__ __attribute__((aligned(16))) float fold[(2 * kBnPoolRow * 3 + 3) / 4 > 4096 ? (2 * kBnPoolRow * 3 + 3) / 4 : 4096];
+  extern __shared__ __attribute__((aligned(16))) float bn_pool_dyn[];
   const int C = a.C;
+  float* const l0 = bn_pool_dyn;  // [6][C]: sc, sf, mu, rs, k1, k2
+  float* const fold = bn_pool_dyn + ((6 * C + 3) & ~3);
+  auto l = [&](int q, int c) -> float& { return l0[q * C + c]; };
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     const float mu = a.saved[c], rs = a.saved[C + c];
     const float sc = (a.gamma ? a.gamma[c] : 1.f) * rs;
-    l[0][c] = sc;
-    l[1][c] = (a.beta ? a.beta[c] : 0.f) - mu * sc;
-    l[2][c] = mu;
-    l[3][c] = rs;
+    l(0, c) = sc;
+    l(1, c) = (a.beta ? a.beta[c] : 0.f) - mu * sc;
+    l(2, c) = mu;
+    l(3, c) = rs;
     if (PASS == 1) {
       float sdz = 0.f, sdx = 0.f;
 #pragma unroll
@@ -2299,8 +2306,8 @@ __global__ __launch_bounds__(256) void bn_pool_bwd_kernel(BnBwdArgs a, PoolArgs 
         sdz += a.dstats[sl * 2 * C + c];
         sdx += a.dstats[sl * 2 * C + C + c];
       }
-      l[4][c] = sdz / (float)a.R;
-      l[5][c] = sdx / (float)a.R;
+      l(4, c) = sdz / (float)a.R;
+      l(5, c) = sdx / (float)a.R;
       if (blockIdx.x == 0) {
         if (a.dbeta) a.dbeta[c] += sdz;
         if (a.dgamma) a.dgamma[c] += sdx;
@@ -2321,7 +2328,7 @@ __global__ __launch_bounds__(256) void bn_pool_bwd_kernel(BnBwdArgs a, PoolArgs 
   for (int j = 0; j < 8; ++j) r1[j] = r2[j] = 0.f;
   const int rowlen = g.Wo * C;  // elements of one pooled row (host: <= kBnPoolRow)
   bf16* const sdy = reinterpret_cast<bf16*>(fold);                              // [2][rowlen]
-  unsigned char* const sid = reinterpret_cast<unsigned char*>(sdy + 2 * kBnPoolRow);  // [2][rowlen]
+  unsigned char* const sid = reinterpret_cast<unsigned char*>(sdy + 2 * rowlen);  // [2][rowlen]
   for (int row = blockIdx.x; row < g.B * g.H; row += gridDim.x) {
     const int b = row / g.H, ih = row - b * g.H;
     const int ty = ih + g.pt;
@@ -2331,15 +2338,35 @@ __global__ __launch_bounds__(256) void bn_pool_bwd_kernel(BnBwdArgs a, PoolArgs 
 #pragma unroll
       for (int q = 0; q < 6; ++q)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) k[q][j] = (PASS == 1 || q < 4) ? l[q][c8 * 8 + j] : 0.f;
+        for (int j = 0; j < 8; ++j) k[q][j] = (PASS == 1 || q < 4) ? l(q, c8 * 8 + j) : 0.f;
     }
     // the <= 2 pooled rows this input row reads: 16-byte coalesced loads of dy and the argmax bytes into LDS
-    for (int r = 0; r <= oh_hi - oh_lo; ++r) {
-      const long long o = ((long long)b * g.Ho + oh_lo + r) * rowlen;
-      for (int i = threadIdx.x; i < rowlen / 8; i += blockDim.x)
-        *reinterpret_cast<bf16x8*>(sdy + r * kBnPoolRow + i * 8) = *reinterpret_cast<const bf16x8*>(pa.dy + o + i * 8);
-      for (int i = threadIdx.x; i < rowlen / 16; i += blockDim.x)
-        *reinterpret_cast<uint4*>(sid + r * kBnPoolRow + i * 16) = *reinterpret_cast<const uint4*>(pa.idx + o + i * 16);
+    // (all of a thread's loads issued before any LDS write: one memory latency per row, not one per chunk;
+    // rowlen <= kBnPoolRow = 4096 gives <= 2 dy chunks and 1 argmax chunk per thread per pooled row)
+    {
+      const int nr = oh_hi - oh_lo + 1;
+      bf16x8 sv[4];
+      uint4 si[2];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int r = t >> 1, i = threadIdx.x + (t & 1) * 256;
+        const long long o = ((long long)b * g.Ho + oh_lo + r) * rowlen;
+        sv[t] = (r < nr && i < rowlen / 8) ? *reinterpret_cast<const bf16x8*>(pa.dy + o + i * 8) : zero8();
+      }
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const long long o = ((long long)b * g.Ho + oh_lo + r) * rowlen;
+        si[r] = (r < nr && (int)threadIdx.x < rowlen / 16) ? *reinterpret_cast<const uint4*>(pa.idx + o + threadIdx.x * 16)
+                                                           : uint4{0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int r = t >> 1, i = threadIdx.x + (t & 1) * 256;
+        if (r < nr && i < rowlen / 8) *reinterpret_cast<bf16x8*>(sdy + r * rowlen + i * 8) = sv[t];
+      }
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+        if (r < nr && (int)threadIdx.x < rowlen / 16) *reinterpret_cast<uint4*>(sid + r * rowlen + threadIdx.x * 16) = si[r];
     }
     __syncthreads();
     for (int e = threadIdx.x; e < W2 * C8; e += blockDim.x) {
@@ -2358,7 +2385,7 @@ __global__ __launch_bounds__(256) void bn_pool_bwd_kernel(BnBwdArgs a, PoolArgs 
       for (int q = 0; q < 4; ++q) {
         const int oh = oh_lo + (q >> 1), ow = ow_lo + (q & 1);
         if (oh > oh_hi || ow > ow_hi) continue;
-        const int lo = (q >> 1) * kBnPoolRow + ow * C + c8 * 8;
+        const int lo = (q >> 1) * rowlen + ow * C + c8 * 8;
         const unsigned long long id = *reinterpret_cast<const unsigned long long*>(sid + lo);
         const bf16x8 d = *reinterpret_cast<const bf16x8*>(sdy + lo);
         const int i = ty - oh * g.sh, j0 = tx0 - ow * g.sw;
@@ -3335,13 +3362,16 @@ TDE_API int tde_bn_pool_bwd(const bf16* dpool, const unsigned char* idx, const b
   BnBwdArgs a{nullptr, y, nullptr, R, C, 1, saved, gamma, beta, relu, Drop{0.f, 0, nullptr, 0, 0}, dstats, dx,
               dx_accum, nullptr, 0, dgamma, dbeta, zero_fwd};
   PoolArgs pa{nullptr, nullptr, const_cast<unsigned char*>(idx), dpool, dx, dx_accum, g};
+  // the staging loads of bn_pool_bwd_kernel cover <= 2 x 256 dy chunks and 256 argmax chunks per pooled row
   if ((long long)g.Wo * C > kBnPoolRow || (g.Wo * C) % 16 != 0 || ((uintptr_t)idx & 15) != 0) return -1;
+  if (kBnPoolRow / 8 > 2 * 256 || kBnPoolRow / 16 > 256) return -1;
   // one input row per block iteration (its <= 2 pooled rows staged in LDS); the reduction ends with 2*C
   // atomics per block, so it takes a moderate grid, the apply pass one block per row
   const int rows = g.B * g.H;
-  bn_pool_bwd_kernel<0><<<rows < 1024 ? rows : 1024, 256, 0, stream>>>(a, pa);
+  const size_t lds = bn_pool_bwd_lds(C, g.Wo * C);
+  bn_pool_bwd_kernel<0><<<rows < 1024 ? rows : 1024, 256, lds, stream>>>(a, pa);
   TDE_LAUNCH_CHECK();
-  bn_pool_bwd_kernel<1><<<rows < 16384 ? rows : 16384, 256, 0, stream>>>(a, pa);
+  bn_pool_bwd_kernel<1><<<rows < 16384 ? rows : 16384, 256, lds, stream>>>(a, pa);
   TDE_LAUNCH_CHECK();
   return 0;
 }
