@@ -2828,6 +2828,11 @@ static unsigned long long g_big_launches = 0;
 // loop) measured it neutral; with the LDS-DMA loop it pays for the weight gradients only.
 static int g_xcd = -1;
 // split-K weight gradients with at most this many splits store partials + reduce; more splits use atomics
+// weight gradients with too few workgroups for 128-wide tiles drop to 64 (TDE_WG_SMALL_TILES=0: off)
+static int g_wg_small_tiles = [] {
+  const char* e = getenv("TDE_WG_SMALL_TILES");
+  return e ? atoi(e) : 1;
+}();
 static int g_wg_scratch_max = [] {
   const char* e = getenv("TDE_WG_SCRATCH_MAX");
   return e ? atoi(e) : 16;
@@ -3077,6 +3082,12 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     if (wg_cap && bm == 128 && bn == 128) bn = 64;
     if (auto_splits) {
       splits = wgrad_splits(M, N, K, KB, &p.ktiles_per_split, wg_cap);
+    }
+    // short reductions (K = a small batch, e.g. a Dense weight gradient at batch 128: 2 splits at most) cannot
+    // reach a chip-filling grid by splitting K: take narrower tiles while that still leaves < 256 workgroups
+    if (!wg_dma && g_wg_small_tiles) {
+      if (bm == 128 && tiles(bm, bn) < 256) bm = 64;
+      if (bn == 128 && tiles(bm, bn) < 256) bn = 64;
     }
   } else if (N > 64 && tiles(128, 128) >= g_tile_min) {
     bm = bn = 128;
