@@ -153,6 +153,77 @@ __global__ __launch_bounds__(256) void smallconv_dgrad_kernel(const bf16* __rest
 }
 
 
+// The same input gradient with the filter's output-channel count and the taps per kernel row reaching a
+// pixel (KWP = ceil(KW / sw)) known at compile time (Model B's Conv2D(6 -> 12, 6x6, stride 2)): the KWP
+// taps of a kernel row load their CO-channel dy vectors (8-byte loads) together before any FMA, so a
+// pixel waits ceil(KH / sh) memory latencies instead of one per tap and channel.
+template <int CI, int CO, int KWP>
+__global__ __launch_bounds__(256) void smallconv_dgrad_c_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ w,
+                                                                bf16* __restrict__ dx, int accum, SGeo g) {
+  static_assert(CO % 4 == 0, "8-byte dy vectors");
+  __shared__ float ws[kSmallLds];  // [kh][kw][co][ci]
+  const int taps = g.KH * g.KW;
+  for (int i = threadIdx.x; i < taps * CO * CI; i += blockDim.x) {
+    const int ci = i % CI;
+    const int t = i / CI;
+    const int co = t % CO, tap = t / CO;
+    ws[i] = ci < g.C ? bf2f(w[(tap * g.C + ci) * CO + co]) : 0.f;
+  }
+  __syncthreads();
+  const int npix = g.B * g.H * g.W;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npix) return;
+  const int hw = g.H * g.W;
+  const int b = p / hw, r = p - b * hw;
+  const int ih = r / g.W, iw = r - ih * g.W;
+  float acc[CI];
+#pragma unroll
+  for (int c = 0; c < CI; ++c) acc[c] = 0.f;
+  const int ty = ih + g.pt, tx = iw + g.pl;
+  const int kw0 = tx % g.sw;
+  for (int kh = ty % g.sh; kh < g.KH; kh += g.sh) {
+    const int oh = (ty - kh) / g.sh;
+    if (ty - kh < 0 || oh >= g.Ho) continue;
+    bf16x4 d[KWP][CO / 4];
+    bool ok[KWP];
+#pragma unroll
+    for (int j = 0; j < KWP; ++j) {
+      const int kw = kw0 + j * g.sw;
+      const int ow = (tx - kw) / g.sw;
+      ok[j] = kw < g.KW && tx - kw >= 0 && ow < g.Wo;
+      const bf16* dp = dy + (((long long)b * g.Ho + oh) * g.Wo + (ok[j] ? ow : 0)) * CO;
+#pragma unroll
+      for (int q = 0; q < CO / 4; ++q) {
+        if (ok[j]) {
+          d[j][q] = *reinterpret_cast<const bf16x4*>(dp + 4 * q);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) d[j][q][e] = (bf16)0.0f;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < KWP; ++j) {
+      if (!ok[j]) continue;
+      const float* wp = ws + (kh * g.KW + kw0 + j * g.sw) * CO * CI;
+#pragma unroll
+      for (int co = 0; co < CO; ++co) {
+        const float gv = bf2f(d[j][co / 4][co % 4]);
+#pragma unroll
+        for (int c = 0; c < CI; ++c) acc[c] = fmaf(gv, wp[co * CI + c], acc[c]);
+      }
+    }
+  }
+  bf16* xp = dx + (long long)p * g.C;
+#pragma unroll
+  for (int c = 0; c < CI; ++c) {
+    if (c >= g.C) break;
+    float v = acc[c];
+    if (accum) v += bf2f(xp[c]);
+    xp[c] = f2bf(v);
+  }
+}
+
 // Weight gradient of a layer whose whole filter fits in registers (K = KH*KW*C <= 128/CO, e.g. Model B's
 // Conv2D(1->6, 3x3): K = 9): dW[k][co] += sum_p x_patch(p)[k] * dy[p][co].  The implicit GEMM would run
 // M = K rows of a 64-row MFMA tile with scalar C = 1 gathers over a 100k-pixel reduction; here each thread
@@ -250,6 +321,12 @@ TDE_API int tde_smallconv_dgrad(const bf16* dy, const bf16* w, bf16* dx, int acc
   if ((long long)g.B * g.H * g.W * g.C >= (1LL << 31) || (long long)g.B * g.Ho * g.Wo * g.Co >= (1LL << 31)) return -4;
   const int npix = g.B * g.H * g.W;
   const int grid = (npix + 255) / 256;
+  static const bool generic_only = getenv("TDE_SMALLCONV_DGRAD_GENERIC") != nullptr;
+  if (!generic_only && ci == 8 && g.Co == 12 && (g.KW + g.sw - 1) / g.sw == 3 && ((uintptr_t)dy & 7) == 0) {
+    smallconv_dgrad_c_kernel<8, 12, 3><<<grid, 256, 0, stream>>>(dy, w, dx, accum, g);  // Model B conv2
+    TDE_LAUNCH_CHECK();
+    return 0;
+  }
   switch (ci) {
     case 8: smallconv_dgrad_kernel<8><<<grid, 256, 0, stream>>>(dy, w, dx, accum, g); break;
     case 16: smallconv_dgrad_kernel<16><<<grid, 256, 0, stream>>>(dy, w, dx, accum, g); break;
@@ -269,8 +346,17 @@ TDE_API int tde_smallconv_wgrad(const bf16* x, const bf16* dy, float* dw, const 
   if (co > 32 || K * co > 1024) return -1;
   if ((long long)g.B * g.H * g.W * g.C >= (1LL << 31) || (long long)g.B * g.Ho * g.Wo * g.Co >= (1LL << 31)) return -4;
   const int npix = g.B * g.Ho * g.Wo;
-  int grid = (npix + 256 * 2 - 1) / (256 * 2);   // ~2 pixels per thread, <= one block per CU
-  grid = grid < 1 ? 1 : (grid > 256 ? 256 : grid);
+  // ~2 pixels per thread, at most g_wg_grid_max blocks (every block ends in K x Co same-address atomics)
+  static const int gmax = [] {
+    const char* e = getenv("TDE_SMALLCONV_WGRAD_GRID");
+    return e ? atoi(e) : 256;
+  }();
+  static const int ppt = [] {
+    const char* e = getenv("TDE_SMALLCONV_WGRAD_PPT");
+    return e ? atoi(e) : 2;
+  }();
+  int grid = (npix + 256 * ppt - 1) / (256 * ppt);
+  grid = grid < 1 ? 1 : (grid > gmax ? gmax : grid);
   const int kchunks = (K + 128 / cot - 1) / (128 / cot);
   const dim3 gr(grid, kchunks);
   switch (co) {
