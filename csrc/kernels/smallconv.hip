@@ -337,13 +337,18 @@ TDE_API int tde_smallconv_dgrad(const bf16* dy, const bf16* w, bf16* dx, int acc
   return 0;
 }
 
+// <= g_sw_max / 128 tap chunks of 128 partial sums (TDE_SMALLCONV_WGRAD_MAX, default 1024 = 8 chunks)
+static int g_sw_max = [] {
+  const char* e = getenv("TDE_SMALLCONV_WGRAD_MAX");
+  return e ? atoi(e) : 1024;
+}();
 // dw: f32 [KH*KW*C][Co] slice of the gradient bucket (accumulated with atomics)
 TDE_API int tde_smallconv_wgrad(const bf16* x, const bf16* dy, float* dw, const int* geo, hipStream_t stream) {
   const SGeo g = sgeo(geo);
   const int co = round8(g.Co);
   const int K = g.KH * g.KW * g.C;
   const int cot = co == 24 ? 32 : co;   // the kernel instance the switch below picks
-  if (co > 32 || K * co > 1024) return -1;
+  if (co > 32 || K * co > g_sw_max) return -1;
   if ((long long)g.B * g.H * g.W * g.C >= (1LL << 31) || (long long)g.B * g.Ho * g.Wo * g.Co >= (1LL << 31)) return -4;
   const int npix = g.B * g.Ho * g.Wo;
   // ~2 pixels per thread, at most g_wg_grid_max blocks (every block ends in K x Co same-address atomics)
@@ -369,7 +374,7 @@ TDE_API int tde_smallconv_wgrad(const bf16* x, const bf16* dy, float* dw, const 
 }
 
 TDE_API int tde_smallconv_wgrad_ok(int C, int Co, int KH, int KW) {
-  return round8(Co) <= 32 && KH * KW * C * round8(Co) <= 1024;   // <= 8 tap chunks of 128 partial sums
+  return round8(Co) <= 32 && KH * KW * C * round8(Co) <= g_sw_max;
 }
 
 TDE_API int tde_smallconv_ok(int C, int Co, int KH, int KW, int dgrad) {

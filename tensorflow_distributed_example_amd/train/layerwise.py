@@ -444,7 +444,9 @@ class _Gemm(_Stage):
             if self.use_stem_pack:
                 self.use_im2col = False
             # filters whose K*Co partial sums fit in registers (Model B conv1: 3x3x1 -> 6)
-            self.small_wgrad = narrow and not self.use_im2col and O.smallconv_wgrad_ok(self.geo)
+            # (TDE_SMALLWG_IM2COL=1: also for layers whose forward runs on an explicit im2col matrix)
+            self.small_wgrad = (narrow and O.smallconv_wgrad_ok(self.geo)
+                                and (not self.use_im2col or os.environ.get("TDE_SMALLWG_IM2COL", "0") == "1"))
         self.colstats = None
         self.dz = None
         self.act_done = False   # the consumer's launch already applied the ReLU mask / bias gradient
@@ -547,10 +549,10 @@ class _Gemm(_Stage):
             if self.use_stem_pack:
                 O.conv_wgrad(self.xp, dout, self.gWv, O.stem_geometry(g), scratch=p.wscratch)
                 O.stem_unpack_wgrad(self.gWv, g, self.gW)
-            elif self.use_im2col:
-                O.conv_wgrad_im2col(self.xcol, dout, self.gW, g, self.Kp)
             elif self.small_wgrad:
                 O.smallconv_wgrad(self.inp.buf, dout, self.gW, g)
+            elif self.use_im2col:
+                O.conv_wgrad_im2col(self.xcol, dout, self.gW, g, self.Kp)
             else:
                 O.conv_wgrad(self.inp.buf, dout, self.gW, g, scratch=p.wscratch)
         else:
