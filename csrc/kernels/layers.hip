@@ -2183,9 +2183,6 @@ __global__ __launch_bounds__(256) void maxpool_bwd8_w2p_kernel(PoolArgs a) {
 // pooled output reads its window of the conv output y, normalises + rectifies every element exactly
 // as bn_fwd would store it (bf16-rounded), and keeps the max and its window index for the pool's
 // backward.  The BN backward recomputes z from y, so nothing downstream needs the BN output.
-// KH_ / KW_: the pool window at compile time (0 = runtime): the 3x3 stem window's nine 16-byte loads are then
-// all issued before the first max.
-template <int KH_, int KW_>
 __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(BnFwdArgs a, PoolArgs pa) {
   __shared__ float sc[kMaxC], sf[kMaxC];
   const int C = a.C;
@@ -2243,17 +2240,14 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(BnFwdArgs a, P
       best[j] = -INFINITY;
       bi[j] = 0;
     }
-    const int KH = KH_ ? KH_ : g.KH, KW = KW_ ? KW_ : g.KW;
-#pragma unroll
-    for (int i = 0; i < KH; ++i) {
+    for (int i = 0; i < g.KH; ++i) {
       const int ih = oh * g.sh - g.pt + i;
       if ((unsigned)ih >= (unsigned)g.H) continue;
-#pragma unroll
-      for (int jj = 0; jj < KW; ++jj) {
+      for (int jj = 0; jj < g.KW; ++jj) {
         const int iw = ow * g.sw - g.pl + jj;
         if ((unsigned)iw >= (unsigned)g.W) continue;
         const bf16x8 v = *reinterpret_cast<const bf16x8*>(a.y + ((((long long)b * g.H + ih) * g.W + iw) * C + c8 * 8));
-        const unsigned char w = (unsigned char)(i * KW + jj);
+        const unsigned char w = (unsigned char)(i * g.KW + jj);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           // the value bn_fwd would store: bf16(relu(y * scale + shift))
@@ -3359,9 +3353,7 @@ TDE_API int tde_bn_relu_maxpool_fwd(const bf16* y, long long R, int C, int mode,
   BnFwdArgs a{y, nullptr, nullptr, R, C, mode, stats, saved, gamma, beta, eps, mmean, mvar, momentum, bessel, zero_buf, 1,
               Drop{0.f, 0, nullptr, 0, 0}};
   PoolArgs pa{y, pooled, idx, nullptr, nullptr, 0, g};
-  const int grid = grid_for((long long)g.B * g.Ho * g.Wo * C, 8);
-  if (g.KH == 3 && g.KW == 3) bn_relu_maxpool_fwd_kernel<3, 3><<<grid, 256, 0, stream>>>(a, pa);
-  else bn_relu_maxpool_fwd_kernel<0, 0><<<grid, 256, 0, stream>>>(a, pa);
+  bn_relu_maxpool_fwd_kernel<<<grid_for((long long)g.B * g.Ho * g.Wo * C, 8), 256, 0, stream>>>(a, pa);
   TDE_LAUNCH_CHECK();
   return 0;
 }
