@@ -1112,6 +1112,18 @@ struct Drop {
 };
 
 // keep-scale (0 or 1/(1-rate)) of the 8 consecutive elements e0..e0+7 (e0 % 8 == 0)
+// the keep-scale of one element (the same Philox stream drop8 draws: counter e / 4, word e % 4)
+__device__ __forceinline__ float drop1(const Drop& d, long long e) {
+  const long long it = (d.iter ? *d.iter : 0) + d.iter_offset;
+  const uint2 key{(unsigned)d.seed, (unsigned)(d.seed >> 32)};
+  const float keep = 1.f - d.rate;
+  const unsigned long long c = (unsigned long long)(e >> 2);
+  const uint4 r = philox(uint4{(unsigned)c, (unsigned)(c >> 32), (unsigned)it, (unsigned)d.layer_id}, key);
+  const int q = (int)(e & 3);
+  const unsigned w = q == 0 ? r.x : q == 1 ? r.y : q == 2 ? r.z : r.w;
+  return ((w >> 8) * (1.f / 16777216.f) < keep) ? 1.f / keep : 0.f;
+}
+
 __device__ __forceinline__ void drop8(const Drop& d, long long e0, float* ks) {
   const long long it = (d.iter ? *d.iter : 0) + d.iter_offset;
   const uint2 key{(unsigned)d.seed, (unsigned)(d.seed >> 32)};
@@ -1431,6 +1443,43 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_rows_kernel(BnBwdArgs a) {
     const int c = threadIdx.x % C, w = threadIdx.x / C;
     const float v = (red[0][w * CM + c] + red[1][w * CM + c]) + (red[2][w * CM + c] + red[3][w * CM + c]);
     atomicAdd(a.dstats + (size_t)(blockIdx.x % kStatSlots) * 2 * C + w * C + c, v);
+  }
+}
+
+// Few rows (a Dense layer's BN: R = batch, e.g. Model B's BatchNormalization after Dense(200) at batch 128):
+// one block per 64 channels, a wave per row quarter walking its rows with 128-byte coalesced loads, the four
+// partials folded in LDS and ONE atomic pair per channel (the generic kernel runs 25 blocks with per-element
+// LDS atomics).  Batch statistics; dropout masks regenerated per element (drop1).
+constexpr int kBnColsRows = 16;  // rows per block (grid y): 4 per wave
+__global__ __launch_bounds__(256) void bn_bwd_reduce_cols_kernel(BnBwdArgs a) {
+  __shared__ float red[2][4][64];
+  const int lane = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int C = a.C;
+  float r1 = 0.f, r2 = 0.f;
+  if (c < C) {
+    const float mu = a.saved[c], rs = a.saved[C + c];
+    const float sc = (a.gamma ? a.gamma[c] : 1.f) * rs;
+    const float sf = (a.beta ? a.beta[c] : 0.f) - mu * sc;
+    const long long r1e = min((long long)(blockIdx.y + 1) * kBnColsRows, a.R);
+#pragma unroll
+    for (long long row = (long long)blockIdx.y * kBnColsRows + rg; row < r1e; row += 4) {
+      const long long e = row * C + c;
+      const float v = bf2f(a.y[e]);
+      const float z = v * sc + sf + (a.res ? bf2f(a.res[e]) : 0.f);
+      float g = bf2f(a.dout[e]);
+      if (a.drop.rate > 0.f) g *= drop1(a.drop, e);
+      if (a.relu && !(z > 0.f)) g = 0.f;
+      r1 += g;
+      r2 += g * (v - mu) * rs;
+    }
+  }
+  red[0][rg][lane] = r1;
+  red[1][rg][lane] = r2;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    atomicAdd(&a.dstats[c], (red[0][0][lane] + red[0][1][lane]) + (red[0][2][lane] + red[0][3][lane]));
+    atomicAdd(&a.dstats[C + c], (red[1][0][lane] + red[1][1][lane]) + (red[1][2][lane] + red[1][3][lane]));
   }
 }
 
@@ -3273,7 +3322,11 @@ TDE_API int tde_bn_bwd(const bf16* dout, const bf16* y, const bf16* res, long lo
     return 0;
   }
   const int g = grid_for(R * C, 8);
-  if (mode == 1 && C <= 16 && drop_rate == 0.f) {
+  static const bool cols_off = getenv("TDE_BN_COLS_OFF") != nullptr;
+  if (mode == 1 && C > 16 && R <= 1024 && !cols_off) {
+    bn_bwd_reduce_cols_kernel<<<dim3((C + 63) / 64, (unsigned)((R + kBnColsRows - 1) / kBnColsRows)), 256, 0, stream>>>(a);
+    TDE_LAUNCH_CHECK();
+  } else if (mode == 1 && C <= 16 && drop_rate == 0.f) {
     // narrow layers: row-per-thread reduction (~2 rows per thread, <= 256 blocks)
     long long gr = (R + 511) / 512;
     gr = gr < 1 ? 1 : (gr > 256 ? 256 : gr);

@@ -879,3 +879,54 @@ def test_fused_stem_fit_evaluate_predict_match_unfused(monkeypatch):
     assert np.abs(p0 - p1).max() <= 1e-2 * (np.abs(p0).max() + 1e-6)
     for a, b in zip(w0, w1):
         assert np.abs(a - b).max() <= 1e-2 * (np.abs(a).max() + 1e-3)
+
+
+@pytest.mark.parametrize("R,C,drop", [(128, 200, 0.5), (128, 200, 0.0), (1000, 72, 0.3)])
+def test_bn_bwd_few_rows_with_dropout(R, C, drop):
+    """BN + ReLU + dropout backward over few rows (a Dense layer's BN; bn_bwd_reduce_cols_kernel): the
+    regenerated per-element dropout masks match the forward's, and dgamma / dbeta / dx match torch."""
+    from tensorflow_distributed_example_amd.ops import layer_ops as O
+    y = _r(R, C, seed=51, scale=1.5) + 0.2
+    gamma = torch.rand(C, device=DEV) + 0.5
+    beta = torch.randn(C, device=DEV) * 0.1
+    stats = _stats_buf(C)
+    O.colstats(y, R, C, stats)
+    saved = torch.zeros(2 * C, device=DEV)
+    dstats = torch.zeros(2 * SLOTS * C, device=DEV)
+    out = torch.zeros(R, C, dtype=bf, device=DEV)
+    it = torch.zeros(1, dtype=torch.int64, device=DEV)
+    d = O.DropSpec(drop, 1234, it, 3) if drop else O.DropSpec()
+    O.bn_fwd(y, out, R, C, mode=1, stats=stats, saved=saved, gamma=gamma, beta=beta, eps=1e-3, zero_buf=dstats,
+             relu=True, drop=d, iter_offset=0)
+    dout = _r(R, C, seed=52)
+    dx = torch.zeros(R, C, dtype=bf, device=DEV)
+    dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    O.bn_bwd(dout, y, R, C, mode=1, saved=saved, gamma=gamma, beta=beta, relu=True, drop=d, iter_offset=0,
+             dstats=dstats, dx=dx, dgamma=dg, dbeta=db)
+    torch.cuda.synchronize()
+    yd = _cpu64(y)
+    mean, var = yd.mean(0), yd.var(0, unbiased=False)
+    xhat = (yd - mean) / torch.sqrt(var + 1e-3)
+    zr = torch.relu(xhat * _cpu64(gamma) + _cpu64(beta))
+    o = _cpu64(out)
+    if drop:
+        # the mask the kernels draw for this (seed, step, layer): the same dropout over an all-ones input
+        # normalised by moving statistics (0, 1) reads it out exactly
+        ones = torch.ones(R, C, dtype=bf, device=DEV)
+        out2 = torch.zeros(R, C, dtype=bf, device=DEV)
+        O.bn_fwd(ones, out2, R, C, mode=2, eps=0.0, mmean=torch.zeros(C, device=DEV), mvar=torch.ones(C, device=DEV),
+                 relu=True, drop=d, iter_offset=0)
+        torch.cuda.synchronize()
+        inv = torch.tensor(1.0 / (1 - drop)).to(torch.bfloat16).item()
+        ks = _cpu64(out2)
+        assert set(torch.unique(ks).tolist()) <= {0.0, inv}
+        ks = (ks > 0).double() / (1 - drop)
+        assert 0.3 < (ks > 0).double().mean().item() < 0.9
+        assert torch.allclose(o, (zr * ks).to(torch.bfloat16).double(), rtol=2e-2, atol=2e-2)   # the forward's mask
+    else:
+        ks = torch.ones_like(zr)
+    dz = _cpu64(dout) * ks * (zr > 0)
+    assert _rel(db.cpu(), dz.sum(0)) < 1e-2
+    assert _rel(dg.cpu(), (dz * xhat).sum(0)) < 1e-2
+    dxr = _cpu64(gamma) / torch.sqrt(var + 1e-3) * (dz - dz.mean(0) - xhat * (dz * xhat).mean(0))
+    assert _rel(dx.float().cpu(), dxr) < 3e-2
