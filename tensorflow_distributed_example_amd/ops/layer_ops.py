@@ -465,6 +465,15 @@ def bn_relu_maxpool_fwd(y, R, Cc, pooled, idx, g: ConvGeom, *, mode, stats=None,
     N.check(rc, "tde_bn_relu_maxpool_fwd")
 
 
+def bn_pool_ok(g: ConvGeom):
+    """Geometries the fused BN + ReLU + MaxPool pair runs (tde_bn_pool_bwd's host checks): 8-channel vectors with
+    256 % (C / 8) == 0, C <= 512, windows covering each pixel at most 2 x 2 times, one pooled row <= 4096
+    elements in LDS."""
+    C8 = g.C // 8
+    return (g.C % 8 == 0 and g.C <= 512 and 256 % C8 == 0 and -(-g.KH // g.sh) <= 2 and (g.KW + g.sw) // g.sw <= 2
+            and g.KH * g.KW < 255 and g.Wo * g.C <= 4096 and (g.Wo * g.C) % 16 == 0)
+
+
 def bn_pool_bwd(dpool, idx, y, R, Cc, g: ConvGeom, *, saved, dstats, dx, gamma=None, beta=None, relu=True,
                 dx_accum=False, dgamma=None, dbeta=None, zero_fwd=None):
     """Backward of bn_relu_maxpool_fwd: the BN input gradient ``dx`` from the POOLED gradient + argmax bytes (the

@@ -281,7 +281,7 @@ class LayerwisePlan(PG.ReplicaPlan):
                 nxt = stages[i + 1]
                 if (isinstance(st, _Elementwise) and st.bn and st.relu and st.res is None and st.drop.rate == 0
                         and isinstance(nxt, _MaxPool) and nxt.inp.root() is st.out.root()
-                        and len(T[st.out.id].consumers) == 1 and st.inp.C % 8 == 0 and 256 % (st.inp.C // 8) == 0
+                        and len(T[st.out.id].consumers) == 1 and O.bn_pool_ok(nxt.geo)
                         and st.inp.root().id != 0):
                     st.pool, nxt.fused = nxt, True
         # gradient accumulation flags: reverse order, first writer stores
