@@ -3328,8 +3328,14 @@ TDE_API int tde_bn_bwd(const bf16* dout, const bf16* y, const bf16* res, long lo
     TDE_LAUNCH_CHECK();
   } else if (mode == 1 && C <= 16 && drop_rate == 0.f) {
     // narrow layers: row-per-thread reduction (~2 rows per thread, <= 256 blocks)
-    long long gr = (R + 511) / 512;
-    gr = gr < 1 ? 1 : (gr > 256 ? 256 : gr);
+    // rows per block (TDE_BN_ROWS_PER_BLOCK, default 256 = one row per thread; Model B 588k / 593k vs 587k / 590k
+    // img/s at 512), at most 1024 blocks
+    static const int rpb = [] {
+      const char* e = getenv("TDE_BN_ROWS_PER_BLOCK");
+      return e && atoi(e) > 0 ? atoi(e) : 256;
+    }();
+    long long gr = (R + rpb - 1) / rpb;
+    gr = gr < 1 ? 1 : (gr > 1024 ? 1024 : gr);
     if (C <= 8) bn_bwd_reduce_rows_kernel<8><<<(int)gr, 256, 0, stream>>>(a);
     else bn_bwd_reduce_rows_kernel<16><<<(int)gr, 256, 0, stream>>>(a);
     TDE_LAUNCH_CHECK();
