@@ -9,7 +9,9 @@ synthetic 28x28x1 inputs, per-GPU batch 64 (the reference's BATCH_SIZE per
 worker, distributed_with_keras.py:13) -> weak scaling, global batch 64*N.
 Distribution: MultiWorkerMirroredStrategy, one process per GPU, RCCL gradient
 all-reduce over xGMI.  Every timed step runs the full forward, backward, gradient
-all-reduce and SGD update (bf16 MFMA compute, fp32 master weights).
+all-reduce and SGD update.  Precision: float32 by default — the reference's
+(distributed_with_keras.py:21), exact-f32 MFMA kernels over the f32 weights;
+``--dtype bf16`` runs the mixed_bfloat16 kernel forms (bf16 MFMA, fp32 master weights).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
@@ -33,7 +35,7 @@ MODELS = {
     "mnist_bn_cnn": (128, 16, 0.01, False, (784,), METRIC),
     "lenet5": (128, 16, 0.01, True, (28, 28, 1), "images/sec (whole node) MNIST LeNet-5 CNN bf16 at 1/2/4/8 MI355X; step time ms"),
     "mnist_mlp": (128, 16, 0.01, True, (28, 28, 1), "images/sec (whole node) MNIST dense MLP at 1/2/4/8 MI355X; step time ms"),
-    "resnet18": (64, 1, 0.1, True, (224, 224, 3),
+    "resnet18": (64, 1, 0.1, True, (224, 224, 3),   # BASELINE.json names this config bf16
                  "images/sec (whole node) synthetic 224x224x3 ResNet-18 bf16 at 1/2/4/8 MI355X; step time ms"),
 }
 
@@ -49,6 +51,8 @@ def parse():
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--executor", default=None, help="fused|reference (default: fused on GPU)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--dtype", choices=("fp32", "bf16"), default=None,
+                    help="compute precision (default fp32; resnet18: bf16, as its BASELINE config)")
     return ap.parse_args()
 
 
@@ -71,6 +75,8 @@ def main():
     if torch.cuda.is_available():
         torch.cuda.set_device(local_rank % torch.cuda.device_count())  # ranks > GPUs only in rehearsals
     tde.backend.set_random_seed(1234)
+    dtype = a.dtype or ("bf16" if a.model == "resnet18" else "fp32")
+    tde.backend.set_global_policy("float32" if dtype == "fp32" else "mixed_bfloat16")
     strategy = tde.distribute.MultiWorkerMirroredStrategy()
     n = strategy.num_replicas_in_sync
     dB, dspe, dlr, from_logits, img, metric = MODELS[a.model]
@@ -127,7 +133,7 @@ def main():
     run_exec(0)
     prog.sync()
     tw = time.perf_counter()
-    run_exec(1)
+    run_exec(1, prefetch=False)
     prog.sync()
     per_exec = max(time.perf_counter() - tw, 1e-6)
     n_warm = max(n_warm, 2 + math.ceil(warm_s / per_exec))
@@ -135,8 +141,10 @@ def main():
         t = torch.tensor([n_warm], dtype=torch.int64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         n_warm = int(t.item())
+    if n_warm > 2:
+        stage(2)
     for i in range(2, n_warm):
-        run_exec(i)
+        run_exec(i, prefetch=i + 1 < n_warm)
         if i % 8 == 0:
             prog.sync()   # bounded queue depth; the GPU never idles for long
     prog.sync()
@@ -144,6 +152,9 @@ def main():
     prog.sync()
     t0 = time.perf_counter()
     n_exec = a.steps // spe
+    # the first timed execution's input group is staged inside the timed region (short and long runs
+    # count the same input work per execution); later ones overlap the previous replay
+    stage(n_warm)
     for i in range(n_exec):
         run_exec(n_warm + i, prefetch=i + 1 < n_exec)
     prog.sync()
@@ -175,11 +186,12 @@ def main():
         print(json.dumps({
             "metric": metric, "value": round(ips, 1), "unit": "images/sec", "n_gpus": n, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "fp32" if prog.plan_kind in ("reference", "fused_smallnet") else "bf16",
+            "vs_baseline": None, "dtype": prog.plans[0].compute_dtype,
             "data": f"synthetic (random {'x'.join(map(str, img))} images, random labels; random-init weights)",
             "config": {"model": a.model, "global_batch": GB, "seq_len": None, "image_shape": list(img),
                        "per_gpu_batch": B, "parallelism": f"dp{n}", "strategy": "MultiWorkerMirroredStrategy",
                        "steps_per_execution": spe, "warmup_steps_run": n_warm * spe,
+                       "input_staged_in_timed_region": True,
                        "optimizer": f"SGD(lr={a.lr})", "plan": prog.plan_kind,
                        "allreduce": ar,
                        "hipgraph": prog.use_graph, "grad_buckets": len(prog.buckets or []) or 1,

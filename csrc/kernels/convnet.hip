@@ -1,4 +1,5 @@
-// Fused forward and backward of the DWK/TF2M small CNN trunk
+// Fused forward and backward of the DWK/TF2M small CNN trunk — bf16 MFMA form (Keras
+// mixed_bfloat16 policy; the float32 form is convnet_f32.hip, shared pieces in tde_convnet.h)
 //   Conv2D(32,3x3,VALID,bias,ReLU) · MaxPooling2D(2) · Flatten · Dense(64)  (matmul part)
 // (distributed_with_keras.py:34-37, tf2_mnist_distributed.py:67-70;
 //  SURVEY.md §2.5 A1-A4 forward, A10-A13 backward).
@@ -12,11 +13,11 @@
 //    drain in the background instead of stalling the barrier;
 //  * the pool-argmax side output is stored lane-contiguous ([P][C/8][ldA] u64).
 //
-// Forward: a workgroup owns PPW=4 pooled positions x 64 images.
+// Forward: a workgroup owns FPW pooled positions x 64 images.
 //   phase 1 (VALU; wave = (position, 8-channel group), lane = image): 3x3 conv of
 //           the 2x2 pool window from a 4x4 register patch, bias, ReLU, max ->
 //           bf16 pooled tile in LDS, argmax bytes, P^T (for the weight grad);
-//   phase 2 (MFMA; wave = 16x16 output tile): tile . W1^T rows of the 4 positions
+//   phase 2 (MFMA; wave = 16x16 output tile): tile . W1^T rows of the positions
 //           -> split-K partial of the Dense pre-activation, f32 atomics into hpre.
 // Backward, per workgroup of 4 positions, looping 64-image chunks:
 //   dP   = G . W1[p*32:(p+1)*32]^T      (MFMA; Dense input-gradient, in-kernel)
@@ -31,63 +32,34 @@
 // costs about as much as a kernel boundary):
 //   * Dense(64) kernel rows: each backward workgroup owns its rows' dW1 completely,
 //     so it updates the fp32 rows and rewrites their bf16 shadow in place;
-//   * Dense(64) bias, Dense(10) kernel + bias (finished by the head launch): the
-//     last backward workgroup updates them;
+//   * Dense(64) bias, Dense(10) kernel + bias (finished by the head workgroup):
+//     the last backward workgroup updates them;
 //   * Conv2D kernel + bias (finished by the backward's atomics): deferred — the next
 //     forward computes the updated values on the fly from (w, g, slots) while *pend,
-//     and the next head launch (which does not read them) commits them and clears
+//     and the next head workgroup (which does not read them) commits them and clears
 //     *pend; a flush launch commits them at the end of each execution.
-#include "tde_optim.h"
+#include "tde_convnet.h"
 
 namespace tde {
+using namespace cnet;
 
-constexpr int PPW = 4;   // pooled positions per workgroup
-constexpr int NW = 16;   // waves per workgroup
-constexpr int CC = 32;   // conv filters
-constexpr int HD = 64;   // Dense units
+constexpr int PPW = 4;   // pooled positions per backward workgroup
 constexpr int PSTR = 40; // padded LDS row stride (bf16) of the pooled tile
 constexpr int RSTR = 72; // padded LDS row stride (bf16) of 64-wide operand rows
 
-struct ConvNetFwdArgs {
-  const float* x; const float* wc; const float* bc;
-  const bf16* W1c; int ldw1c;       // [HD][K] bf16 (W1^T shadow)
-  float* hpre;                      // [B][HD] f32, += (pre-zeroed by the previous head launch)
-  bf16* Pt; int ldPt;               // [K][ldPt] (nullable)
-  uint64_t* amax; int lda;          // [P][CC/8][lda] (nullable)
-  int B, H, W;
-  long long* stamps;
-  int w1_rows;                      // 1: W1c is the row-major [K][HD] shadow (ldw1c = HD)
-  // deferred conv update (fused step): while *pend the conv weights used are the optimizer
-  // step of (wc, bc) with the previous backward's gradients (nullable: use wc, bc as stored)
-  const int* pend;
-  const float *gwc, *gbc, *mwc, *mbc, *vwc, *vbc;
-  const long long* iterations;
-  OptHyper h;
-  unsigned long long* inc_iter;      // training: block 0 advances the step counter (nullable)
-  int hrep; long long hrep_stride;   // hpre replicas: workgroup x adds into replica x % hrep
-};
-
-// The input rows a workgroup's PPW positions touch (<= XR rows of <= XW floats per
-// image) are staged into LDS with coalesced float4 loads: gathering 4x4 patches
-// straight from HBM puts 64 distinct cache lines behind every load instruction.
-constexpr int XR = 6, XW = 32;
-// per-image stride of the staged rows padded to 2 (mod 64) floats: the per-lane (= per-image) float2
-// patch reads then hit distinct bank pairs (168 = 40 mod 64 for MNIST made them 8-way conflicts)
-__host__ __device__ constexpr int fwd_istride(int W) { return XR * W + ((2 - (XR * W) % 64) + 64) % 64; }
-constexpr int kConvW = CC * 10;   // conv taps [9][CC] + bias [CC] (floats), staged in LDS
-constexpr int fwd_lds(int fpw) { return fpw * 64 * PSTR * 2 + 64 * (XR * XW + 64) * 4 + kConvW * 4; }
+constexpr int fwd_lds(int fpw) { return fpw * 64 * PSTR * 2 + kXrBytes + kConvW * 4; }
 
 // FPW pooled positions x 64 images per workgroup, 4*FPW waves (wave = position x 8-channel
 // group).  Phase 1 is VALU-bound: fewer positions per workgroup spread the conv over more CUs
 // (FPW=4: 43 workgroups x 16 waves for MNIST; FPW=2: 85 x 8) at the price of more split-K
 // atomics in phase 2.
 template <int FPW>
-__global__ __launch_bounds__(FPW * 256) void convnet_fwd_kernel(ConvNetFwdArgs a) {
+__global__ __launch_bounds__(FPW * 256) void convnet_fwd_kernel(FwdArgs a) {
   constexpr int NT = FPW * 256;
   extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
   bf16* Ps = reinterpret_cast<bf16*>(fsm);
   float* xr = reinterpret_cast<float*>(fsm + FPW * 64 * PSTR * 2);  // [64][XR][W]
-  float* wcs = reinterpret_cast<float*>(fsm + FPW * 64 * PSTR * 2 + 64 * (XR * XW + 64) * 4);  // [10][CC]
+  float* wcs = reinterpret_cast<float*>(fsm + FPW * 64 * PSTR * 2 + kXrBytes);  // [10][CC]
   stamp(a.stamps, 0);
   // Keras optimizer.iterations: advanced here, read (stable) by this step's backward / optimizer
   if (a.inc_iter && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicAdd(a.inc_iter, 1ull);
@@ -106,37 +78,12 @@ __global__ __launch_bounds__(FPW * 256) void convnet_fwd_kernel(ConvNetFwdArgs a
   const bool pok = p < P;
   const int py0 = p0 / Wp;
   const int nrows = min(XR, H - 2 * py0);
-  const int istride = fwd_istride(W);  // floats per staged image (bank-padded)
+  const bf16* W1c = reinterpret_cast<const bf16*>(a.W1);
+  bf16* Pt = reinterpret_cast<bf16*>(a.Pt);
 
   // ---- prologue: all global loads, independent, issued back to back
-  {
-    const int n4 = nrows * W / 4;  // float4 per image
-    for (int i = threadIdx.x; i < 64 * n4; i += NT) {
-      const int bl = i / n4, q = i - bl * n4;
-      float4 v = {0.f, 0.f, 0.f, 0.f};
-      if (b0 + bl < a.B)
-        v = *reinterpret_cast<const float4*>(a.x + (size_t)(b0 + bl) * H * W + (size_t)(2 * py0) * W + q * 4);
-      // istride is only 8-byte aligned (bank padding): two 8-byte LDS writes
-      float2* d2 = reinterpret_cast<float2*>(xr + bl * istride + q * 4);
-      d2[0] = float2{v.x, v.y};
-      d2[1] = float2{v.z, v.w};
-    }
-  }
-  // conv weights in effect for this step -> LDS (with the deferred update applied while *pend)
-  for (int i = threadIdx.x; i < kConvW; i += NT) {
-    const bool isb = i >= 9 * CC;
-    const int j = isb ? i - 9 * CC : i;
-    float w = isb ? a.bc[j] : a.wc[j];
-    if (a.pend) {
-      const float g = isb ? a.gbc[j] : a.gwc[j];
-      float m = 0.f, v = 0.f;
-      if (a.h.kind != kOptSGD) m = isb ? a.mbc[j] : a.mwc[j];
-      if (a.h.kind == kOptAdam) v = isb ? a.vbc[j] : a.vwc[j];
-      const long long t = a.h.kind == kOptAdam ? *a.iterations : 0;
-      if (*a.pend) w = opt_step(a.h, opt_lr_t(a.h, t), w, g, m, v);
-    }
-    wcs[i] = w;
-  }
+  fwd_stage_x(a, xr, b0, py0, nrows, NT);
+  fwd_stage_conv(a, wcs, NT);
   // W1^T fragments of this wave's output tiles: tile t = wave + 4*FPW*j (j < 4/FPW),
   // mt = t>>2 (image rows), nt = t&3 = wave&3 (units) for every j
   const int nt = wave & 3;
@@ -149,85 +96,38 @@ __global__ __launch_bounds__(FPW * 256) void convnet_fwd_kernel(ConvNetFwdArgs a
     } else if (a.w1_rows) {
       // row-major shadow [K][HD]: 8 K-consecutive elements of column nt*16+fr (16 lanes read
       // 32 contiguous bytes per element row)
-      const bf16* src = a.W1c + (size_t)(kp * CC + fk) * a.ldw1c + nt * 16 + fr;
+      const bf16* src = W1c + (size_t)(kp * CC + fk) * a.ldw1 + nt * 16 + fr;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) wfr[ks][j] = src[(size_t)j * a.ldw1c];
+      for (int j = 0; j < 8; ++j) wfr[ks][j] = src[(size_t)j * a.ldw1];
     } else {
-      wfr[ks] = *reinterpret_cast<const bf16x8*>(a.W1c + (size_t)(nt * 16 + fr) * a.ldw1c + (size_t)kp * CC + fk);
+      wfr[ks] = *reinterpret_cast<const bf16x8*>(W1c + (size_t)(nt * 16 + fr) * a.ldw1 + (size_t)kp * CC + fk);
     }
   }
   stamp(a.stamps, 1);
   lds_barrier();
-  // this wave's 8 channels (wave-uniform LDS broadcast reads)
-  float4 wlo[9], whi[9];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const float4 lo = *reinterpret_cast<const float4*>(wcs + t * CC + c0);
-    const float4 hi = *reinterpret_cast<const float4*>(wcs + t * CC + c0 + 4);
-    wlo[t] = lo;
-    whi[t] = hi;
-  }
-  float4 blo, bhi;
-  {
-    const float4 lo = *reinterpret_cast<const float4*>(wcs + 9 * CC + c0);
-    const float4 hi = *reinterpret_cast<const float4*>(wcs + 9 * CC + c0 + 4);
-    blo = lo;
-    bhi = hi;
-  }
+  ConvW8 cw;
+  cw.load(wcs, c0);
 
   // ---- phase 1: conv + bias + ReLU + 2x2 max-pool for 8 channels
   bf16x8 outv;
   if (bok && pok) {
-    float patch[16];
-    {
-      const int py = p / Wp, px = p - py * Wp;
-      const float* xb = xr + lane * istride + (2 * (py - py0)) * W + 2 * px;
+    const int py = p / Wp, px = p - py * Wp;
+    float out[8];
+    uint64_t packed;
+    conv_pool8(xr + lane * fwd_istride(W) + (2 * (py - py0)) * W + 2 * px, W, cw, out, packed);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float2 u = *reinterpret_cast<const float2*>(xb + r * W);
-        const float2 v = *reinterpret_cast<const float2*>(xb + r * W + 2);
-        patch[r * 4 + 0] = u.x; patch[r * 4 + 1] = u.y; patch[r * 4 + 2] = v.x; patch[r * 4 + 3] = v.y;
-      }
-    }
-    uint64_t packed = 0;
-#pragma unroll
-    for (int cc = 0; cc < 8; ++cc) {
-      float wt[9];
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const float4 q = cc < 4 ? wlo[t] : whi[t];
-        const int k = cc & 3;
-        wt[t] = k == 0 ? q.x : (k == 1 ? q.y : (k == 2 ? q.z : q.w));
-      }
-      const float4 bq = cc < 4 ? blo : bhi;
-      const int kb = cc & 3;
-      const float bcv = kb == 0 ? bq.x : (kb == 1 ? bq.y : (kb == 2 ? bq.z : bq.w));
-      float best = -3.0e38f;
-      int bi = 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int dy = q >> 1, dx = q & 1;
-        float z = bcv;
-#pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-          for (int kx = 0; kx < 3; ++kx) z = fmaf(patch[(dy + ky) * 4 + dx + kx], wt[ky * 3 + kx], z);
-        if (z > best) { best = z; bi = q; }
-      }
-      outv[cc] = f2bf(fmaxf(best, 0.f));
-      packed |= (uint64_t)(best > 0.f ? (unsigned)bi : 0xFFu) << (8 * cc);
-    }
+    for (int cc = 0; cc < 8; ++cc) outv[cc] = f2bf(out[cc]);
     if (a.amax) a.amax[((size_t)p * (CC / 8) + cg) * a.lda + b] = packed;
-    if (a.Pt) {
+    if (Pt) {
 #pragma unroll
-      for (int cc = 0; cc < 8; ++cc) a.Pt[(size_t)(p * CC + c0 + cc) * a.ldPt + b] = outv[cc];
+      for (int cc = 0; cc < 8; ++cc) Pt[(size_t)(p * CC + c0 + cc) * a.ldPt + b] = outv[cc];
     }
   } else {
 #pragma unroll
     for (int cc = 0; cc < 8; ++cc) outv[cc] = f2bf(0.f);
-    if (pok && a.Pt && b < a.ldPt) {
+    if (pok && Pt && b < a.ldPt) {
 #pragma unroll
-      for (int cc = 0; cc < 8; ++cc) a.Pt[(size_t)(p * CC + c0 + cc) * a.ldPt + b] = outv[cc];
+      for (int cc = 0; cc < 8; ++cc) Pt[(size_t)(p * CC + c0 + cc) * a.ldPt + b] = outv[cc];
     }
   }
   *reinterpret_cast<bf16x8*>(Ps + ((size_t)pp * 64 + lane) * PSTR + c0) = outv;
@@ -259,87 +159,7 @@ __global__ __launch_bounds__(FPW * 256) void convnet_fwd_kernel(ConvNetFwdArgs a
   stamp(a.stamps, 4);
 }
 
-// Backward of the trunk with the classifier head fused in (the head is
-// the same math as head.hip):  per 64-image chunk every workgroup recomputes the head from the
-// Dense(64) pre-activation (16 KB f32): h = ReLU(hpre + b1) -> logits = h . W2 + b2 (exact f32
-// MFMA) -> softmax-CE -> dl = (p - onehot) * scale -> G = dl . W2^T masked by h > 0, straight into
-// LDS — the Dense(64) input gradient every workgroup needs anyway.  The recompute costs about a
-// microsecond of MFMA/LDS work per workgroup and removes a launch and its boundary.  ONE workgroup
-// (the last: it owns a single pooled position) also produces the head's side outputs — loss and
-// accuracy, dW2 = h^T . dl, db2, db1 (complete sums, no atomics) — and stores them or, in the fused
-// step, applies the update to them.
-// hpre is double-buffered by step parity: this launch reads hpre[p] and zeroes hpre[1-p] (read by
-// the previous step's backward, accumulated into by the next forward): no in-kernel hand-off.
-struct ConvNetBwdArgs {
-  const float* x; const uint64_t* amax; int lda;
-  const float* hpre;                 // [B][HD] f32 Dense(64) pre-activation (this step's parity)
-  float* hzero;                      // [B][HD] the other parity buffer, zeroed here
-  int hrep; long long hrep_stride;   // hpre replicas (summed on load; all zeroed)
-  const float* b1; const float* W2; const float* b2; int C; int pre_relu;
-  const int* labels;
-  float scale;                       // 1 / global batch (Keras AUTO reduction under a strategy)
-  float* metrics;                    // += {loss_sum, correct, count}
-  const bf16* W1r; int ldw1r;        // [K][HD] bf16 (row-major shadow)
-  const bf16* Pt; int ldPt;          // [K][ldPt] bf16
-  float* dW1;                        // [K][HD] f32 (MODE 0: stored)
-  float* dwc; float* dbc;            // [9][CC], [CC] (atomic +=)
-  float *dW2, *db2, *db1;            // MODE 0: head gradients (+= by the head workgroup)
-  int B, H, W;
-  long long* stamps;
-  // fused step (MODE != 0)
-  float *w1, *m1, *v1;               // fp32 master [K][HD] (+ slots), updated in place
-  bf16* w1r_out;                     // row-major bf16 shadow (== W1r), rewritten
-  bf16* w1c_out; int ldw1c;          // transposed bf16 shadow [HD][ldw1c] (nullable)
-  float *hw, *hm, *hv;               // flat weight / slot buffers (head variables at the offsets below)
-  long long off_w2, off_b2, off_b1;  // off_b1 < 0: the Dense(64) has no bias
-  const long long* iterations;       // t of this step (advanced by this step's forward)
-  long long* iter_prev;              // := t by the head workgroup (read by the next forward)
-  OptHyper h;
-  FlatApply commit;                  // the previous step's deferred conv update (workgroup 0, while *pend)
-  int* pend_set;                     // := 1: this step's conv update is deferred
-};
-
-// Up to NPER elements per thread of a FlatApply's ranges, loaded early into registers and
-// updated later (the loads' latency hides behind the caller's work).
-template <int NPER>
-struct FlatPrefetch {
-  int e[NPER];
-  float w[NPER], g[NPER], m[NPER], v[NPER];
-  __device__ __forceinline__ void load(const FlatApply& f, int tid, int nt) {
-#pragma unroll
-    for (int k = 0; k < NPER; ++k) {
-      int idx = tid + k * nt;
-      e[k] = -1;
-      for (int r = 0; r < f.nr; ++r) {
-        if (idx < f.n[r]) {
-          e[k] = f.lo[r] + idx;
-          break;
-        }
-        idx -= f.n[r];
-      }
-      w[k] = g[k] = m[k] = v[k] = 0.f;
-      if (e[k] >= 0) {
-        w[k] = f.w[e[k]];
-        g[k] = f.g[e[k]];
-        if (f.h.kind != kOptSGD) m[k] = f.m[e[k]];
-        if (f.h.kind == kOptAdam) v[k] = f.v[e[k]];
-      }
-    }
-  }
-  __device__ __forceinline__ void apply(const FlatApply& f, long long t) {
-    const float lr_t = opt_lr_t(f.h, t);
-#pragma unroll
-    for (int k = 0; k < NPER; ++k) {
-      if (e[k] < 0) continue;
-      f.w[e[k]] = opt_step(f.h, lr_t, w[k], g[k], m[k], v[k]);
-      f.g[e[k]] = 0.f;
-      if (f.h.kind != kOptSGD) f.m[e[k]] = m[k];
-      if (f.h.kind == kOptAdam) f.v[e[k]] = v[k];
-    }
-  }
-};
-
-// LDS carve (bytes)
+// LDS carve of the backward (bytes)
 constexpr int kG = 0;                                   // bf16 [64][RSTR]
 constexpr int kW1 = kG + 64 * RSTR * 2;                 // bf16 [128][RSTR]
 constexpr int kPt = kW1 + 128 * RSTR * 2;               // bf16 [128][RSTR]
@@ -351,239 +171,15 @@ constexpr int kDp = kAm + PPW * 64 * CC;                // f32  [PPW][64][DPS] (
 // bank quarters (stride 32 made them 4-way LDS bank conflicts)
 constexpr int DPS = 40;
 constexpr int kW2s = kDp + PPW * 64 * DPS * 4;          // f32  [HD][16] W2, classes padded to 16
-constexpr int kB2s = kW2s + HD * 16 * 4;                // f32  [16]
-constexpr int kLab = kB2s + 16 * 4;                     // i32  [64]
-constexpr int kBwdLds = kLab + 64 * 4;
-// head scratch inside the dP area (dead during the head phase of a chunk)
-constexpr int HS = HD + 4;                              // f32 row stride of h
-constexpr int kHs = 0, kPart = kHs + 64 * HS * 4, kDl = kPart + 12 * 64 * 4 * 4;
-static_assert(kDl + 64 * 16 * 4 <= PPW * 64 * DPS * 4, "head scratch exceeds the dP area");
-
-__device__ __forceinline__ f32x4 mfma_f32x4(float a, float b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
-// ---- head pieces shared by the trunk workgroups and the head workgroup (16 waves, 64 rows)
-
-// hpre[row][c4..c4+3] summed over the replicas (loads issued together)
-__device__ __forceinline__ float4 load_hpre(const ConvNetBwdArgs& a, int row, int c4) {
-  constexpr int kMaxRep = 4;
-  float4 v[kMaxRep];
-#pragma unroll
-  for (int r = 0; r < kMaxRep; ++r)
-    v[r] = r < a.hrep ? *reinterpret_cast<const float4*>(a.hpre + (size_t)r * a.hrep_stride + (size_t)row * HD + c4)
-                      : float4{0.f, 0.f, 0.f, 0.f};
-  float4 s = v[0];
-#pragma unroll
-  for (int r = 1; r < kMaxRep; ++r) {
-    s.x += v[r].x; s.y += v[r].y; s.z += v[r].z; s.w += v[r].w;
-  }
-  return s;
-}
-
-// h = act(hpre + b1) of this thread's row / 4 units into LDS (rows past nb zeroed)
-__device__ __forceinline__ void head_stage(const ConvNetBwdArgs& a, float4 hv, float4 b1v, int hr, int hc4, int nb,
-                                           float* hs) {
-  float4 h = float4{hv.x + b1v.x, hv.y + b1v.y, hv.z + b1v.z, hv.w + b1v.w};
-  if (a.pre_relu) h = float4{fmaxf(h.x, 0.f), fmaxf(h.y, 0.f), fmaxf(h.z, 0.f), fmaxf(h.w, 0.f)};
-  if (hr >= nb) h = float4{0.f, 0.f, 0.f, 0.f};
-  *reinterpret_cast<float4*>(hs + hr * HS + hc4) = h;
-}
-
-// logits = h . W2 + b2 (exact f32 MFMA; wave = 16-row tile x K quarter), softmax-CE on waves 0..3
-// -> dls = dlogits [64][16]; loss / correct / count accumulated into la / ca / na (lanes fr == 0).
-// Entered after a barrier that published hs / labs; ends with a barrier that publishes dls.
-__device__ __forceinline__ void head_logits_ce(const ConvNetBwdArgs& a, int nb, const float* hs, float* part,
-                                               float* dls, const float* w2s, const float* b2s, const int* labs,
-                                               int lane, int wave, float& la, float& ca, float& na) {
-  const int fr = lane & 15, fq = lane >> 4, C = a.C;
-  f32x4 lg = {0.f, 0.f, 0.f, 0.f};
-  {
-    const int rt = wave & 3, kq = wave >> 2;
-#pragma unroll
-    for (int k = kq * 16; k < kq * 16 + 16; k += 4)
-      lg = mfma_f32x4(hs[(rt * 16 + fr) * HS + k + fq], w2s[(k + fq) * 16 + fr], lg);
-    if (kq > 0) *reinterpret_cast<f32x4*>(part + (((kq - 1) * 4 + rt) * 64 + lane) * 4) = lg;
-  }
-  lds_barrier();
-  if (wave < 4) {
-    const int rt = wave;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const f32x4 pv = *reinterpret_cast<const f32x4*>(part + ((q * 4 + rt) * 64 + lane) * 4);
-      lg[0] += pv[0]; lg[1] += pv[1]; lg[2] += pv[2]; lg[3] += pv[3];
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = rt * 16 + fq * 4 + i;
-      const bool valid = r < nb;
-      const bool cv = fr < C;
-      const float z = cv ? lg[i] + b2s[fr] : -3.0e38f;
-      const float m = row16_max(z);
-      const float e = cv ? __expf(z - m) : 0.f;
-      const float s = row16_sum(e);
-      const float pr = e / s;
-      const int label = labs[r];
-      const int amx = row16_min(cv && z == m ? fr : 64);
-      const float zl = __shfl(z, (lane & ~15) | (label & 15), 64);
-      if (valid && fr == 0) {
-        la += __logf(s) + m - zl;
-        ca += (amx == label) ? 1.f : 0.f;
-        na += 1.f;
-      }
-      dls[r * 16 + fr] = (valid && cv) ? (pr - (fr == label ? 1.f : 0.f)) * a.scale : 0.f;
-    }
-  }
-  lds_barrier();
-}
-
-// dH tile of this wave (rows rt*16.., units ut*16.., rt = wave>>2, ut = wave&3) = dl . W2^T, masked
-// by h > 0 and rows < nb.  Lane holds dH[rt*16 + 4fq + i][ut*16 + fr].
-__device__ __forceinline__ f32x4 head_dh(const ConvNetBwdArgs& a, int nb, const float* hs, const float* dls,
-                                         const float* w2s, int lane, int wave) {
-  const int fr = lane & 15, fq = lane >> 4, rt = wave >> 2, ut = wave & 3;
-  f32x4 gh = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int k = 0; k < 16; k += 4)
-    gh = mfma_f32x4(dls[(rt * 16 + fr) * 16 + k + fq], w2s[(ut * 16 + fr) * 16 + k + fq], gh);
-  const int j = ut * 16 + fr;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = rt * 16 + fq * 4 + i;
-    if ((a.pre_relu && !(hs[r * HS + j] > 0.f)) || r >= nb) gh[i] = 0.f;
-  }
-  return gh;
-}
-
-// The head workgroup: loss / accuracy, dW2 = h^T . dl, db2, db1 over all chunks, then stored (MODE 0)
-// or updated (fused step; with the previous step's deferred conv update and the flags).
-template <int MODE>
-__device__ __forceinline__ void head_workgroup(const ConvNetBwdArgs& a, unsigned char* smem) {
-  float* hs = reinterpret_cast<float*>(smem + kDp + kHs);
-  float* part = reinterpret_cast<float*>(smem + kDp + kPart);
-  float* dls = reinterpret_cast<float*>(smem + kDp + kDl);
-  float* w2s = reinterpret_cast<float*>(smem + kW2s);
-  float* b2s = reinterpret_cast<float*>(smem + kB2s);
-  int* labs = reinterpret_cast<int*>(smem + kLab);
-  float* db1p = reinterpret_cast<float*>(smem + kG);   // [4][64] (the trunk's G area is unused here)
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
-  const int fr = lane & 15, fq = lane >> 4, C = a.C;
-  const int hr = tid >> 4, hc4 = (tid & 15) * 4;
-  const float4 b1v = a.b1 ? *reinterpret_cast<const float4*>(a.b1 + hc4) : float4{0.f, 0.f, 0.f, 0.f};
-
-  // fused step: the variables this workgroup updates, loaded now.  waves 0..3: W2[wave*16 + 4fq + i][fr]
-  // (the dW2 tile layout); wave 4: b2[fr]; wave 5: b1[lane]
-  long long e[4] = {-1, -1, -1, -1};
-  if (wave < 4 && fr < C) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) e[i] = a.off_w2 + (long long)(wave * 16 + fq * 4 + i) * C + fr;
-  } else if (wave == 4 && fq == 0 && fr < C) {
-    e[0] = a.off_b2 + fr;
-  } else if (wave == 5 && a.off_b1 >= 0) {
-    e[0] = a.off_b1 + lane;
-  }
-  float hwv[4] = {0.f, 0.f, 0.f, 0.f}, hmv[4] = {0.f, 0.f, 0.f, 0.f}, hvv[4] = {0.f, 0.f, 0.f, 0.f};
-  long long t_it = 0;
-  FlatPrefetch<1> cp;
-  int cpend = 0;
-  if (MODE != 0) {
-    t_it = *a.iterations;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (e[i] < 0) continue;
-      hwv[i] = a.hw[e[i]];
-      if (MODE == 2 && a.h.kind != kOptSGD) hmv[i] = a.hm[e[i]];
-      if (MODE == 2 && a.h.kind == kOptAdam) hvv[i] = a.hv[e[i]];
-    }
-    if (a.commit.nr > 0) {
-      cpend = *a.commit.pend;
-      cp.load(a.commit, tid, 1024);
-    }
-  }
-
-  f32x4 gw = {0.f, 0.f, 0.f, 0.f};
-  float db1acc = 0.f, db2acc = 0.f, la = 0.f, ca = 0.f, na = 0.f;
-  for (int b0 = 0; b0 < a.B; b0 += 64) {
-    const int nb = min(64, a.B - b0);
-    float4 hv = {0.f, 0.f, 0.f, 0.f};
-    if (hr < nb) hv = load_hpre(a, b0 + hr, hc4);
-    const int lab = (tid < nb) ? a.labels[b0 + tid] : 0;
-    head_stage(a, hv, b1v, hr, hc4, nb, hs);
-    if (tid < 64) labs[tid] = lab;
-    lds_barrier();
-    head_logits_ce(a, nb, hs, part, dls, w2s, b2s, labs, lane, wave, la, ca, na);
-    const f32x4 gh = head_dh(a, nb, hs, dls, w2s, lane, wave);
-    db1acc += (gh[0] + gh[1]) + (gh[2] + gh[3]);
-    if (wave < 4) {
-#pragma unroll
-      for (int k = 0; k < 64; k += 4) gw = mfma_f32x4(hs[(k + fq) * HS + wave * 16 + fr], dls[(k + fq) * 16 + fr], gw);
-    } else if (wave == 4) {
-#pragma unroll 4
-      for (int r = fq * 16; r < fq * 16 + 16; ++r) db2acc += dls[r * 16 + fr];
-    }
-    lds_barrier();
-  }
-  // db1: over the 4 lane groups, then the 4 row-tile waves of each unit tile; db2: over the lane groups
-  db1acc += __shfl_xor(db1acc, 16, 64);
-  db1acc += __shfl_xor(db1acc, 32, 64);
-  if (fq == 0) db1p[(wave >> 2) * 64 + (wave & 3) * 16 + fr] = db1acc;
-  db2acc += __shfl_xor(db2acc, 16, 64);
-  db2acc += __shfl_xor(db2acc, 32, 64);
-  if (wave < 4) {
-    la = rows4_sum(la);
-    ca = rows4_sum(ca);
-    na = rows4_sum(na);
-    if (a.metrics && lane == 0 && na > 0.f) {
-      atomicAdd(a.metrics + 0, la);
-      atomicAdd(a.metrics + 1, ca);
-      atomicAdd(a.metrics + 2, na);
-    }
-  }
-  lds_barrier();
-  float gv[4] = {0.f, 0.f, 0.f, 0.f};
-  float* gdst[4] = {nullptr, nullptr, nullptr, nullptr};
-  if (wave < 4 && fr < C) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      gv[i] = gw[i];
-      gdst[i] = a.dW2 ? a.dW2 + (size_t)(wave * 16 + fq * 4 + i) * C + fr : nullptr;
-    }
-  } else if (wave == 4 && fq == 0 && fr < C) {
-    gv[0] = db2acc;
-    gdst[0] = a.db2 ? a.db2 + fr : nullptr;
-  } else if (wave == 5 && a.b1) {
-    gv[0] = (db1p[lane] + db1p[64 + lane]) + (db1p[128 + lane] + db1p[192 + lane]);
-    gdst[0] = a.db1 ? a.db1 + lane : nullptr;
-  }
-  if (MODE == 0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (gdst[i]) *gdst[i] += gv[i];
-    return;
-  }
-  const float lr_t = opt_lr_t(a.h, t_it);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if (e[i] < 0) continue;
-    float m = hmv[i], v = hvv[i];
-    a.hw[e[i]] = opt_step(a.h, lr_t, hwv[i], gv[i], m, v);
-    if (MODE == 2 && a.h.kind != kOptSGD) a.hm[e[i]] = m;
-    if (MODE == 2 && a.h.kind == kOptAdam) a.hv[e[i]] = v;
-  }
-  // the previous step's conv update (its forward used it on the fly; this launch does not read the
-  // conv weights): commit it, clear its flag; flag this step's update (the trunk's atomics)
-  if (cpend) cp.apply(a.commit, t_it - 1);
-  if (tid == 0) {
-    if (cpend) *a.commit.pend = 0;
-    if (a.pend_set) *a.pend_set = 1;
-    if (a.iter_prev) *a.iter_prev = t_it;
-  }
-}
+constexpr int kB2s = kW2s + kW2Bytes;                   // f32  [16]
+constexpr int kLab = kB2s + kB2Bytes;                   // i32  [64]
+constexpr int kBwdLds = kLab + kLabBytes;
+static_assert(kHeadScratch <= PPW * 64 * DPS * 4, "head scratch exceeds the dP area");
 
 // MODE 0: store gradients; 1: fused step, SGD; 2: fused step, optimizer with slots (momentum / Adam).
 // Grid: one workgroup per PPW pooled positions + the head workgroup (last).
 template <int MODE>
-__global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
+__global__ __launch_bounds__(1024) void convnet_bwd_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16* Gs = reinterpret_cast<bf16*>(smem + kG);
   bf16* W1s = reinterpret_cast<bf16*>(smem + kW1);
@@ -592,33 +188,19 @@ __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
   float* xs = reinterpret_cast<float*>(smem + kXs);
   uint8_t* am = smem + kAm;
   float* dps = reinterpret_cast<float*>(smem + kDp);
-  float* red = dps;
-  float* hs = reinterpret_cast<float*>(smem + kDp + kHs);
-  float* part = reinterpret_cast<float*>(smem + kDp + kPart);
-  float* dls = reinterpret_cast<float*>(smem + kDp + kDl);
-  float* w2s = reinterpret_cast<float*>(smem + kW2s);
-  float* b2s = reinterpret_cast<float*>(smem + kB2s);
-  int* labs = reinterpret_cast<int*>(smem + kLab);
+  const HeadLds hl = HeadLds::carve(smem + kDp, smem + kW2s, smem + kB2s, smem + kLab);
   stamp(a.stamps, 0);
-  const int W = a.W, H = a.H, C = a.C;
+  const int W = a.W, H = a.H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
   const int fr = lane & 15, fq = lane >> 4, fk = fq * 8;
+  const bf16* W1r = reinterpret_cast<const bf16*>(a.W1);
+  const bf16* Pt = reinterpret_cast<const bf16*>(a.Pt);
 
-  // ---- every workgroup: W2 image (classes padded to 16) and b2 in LDS; its slice of the other
-  // parity buffer of hpre zeroed for the next forward's atomics
-  {
-    const int u = tid >> 4, c = tid & 15;   // 64 x 16
-    w2s[u * 16 + c] = c < C ? a.W2[u * C + c] : 0.f;
-    if (tid < 16) b2s[tid] = tid < C ? a.b2[tid] : 0.f;
-  }
-  {
-    const int n4 = (int)(((a.hrep - 1) * a.hrep_stride + (long long)a.B * HD) / 4);
-    const int per = (n4 + gridDim.x - 1) / gridDim.x, beg = blockIdx.x * per;
-    const int end = min(n4, beg + per);
-    for (int i = beg + tid; i < end; i += 1024) reinterpret_cast<float4*>(a.hzero)[i] = float4{0.f, 0.f, 0.f, 0.f};
-  }
+  // ---- every workgroup: W2 image and b2 in LDS; its slice of the other parity buffer of hpre zeroed
+  head_load_w2(a, hl, tid);
+  zero_other_parity(a, tid);
   if (blockIdx.x == gridDim.x - 1) {
-    head_workgroup<MODE>(a, smem);
+    head_workgroup<MODE>(a, hl, reinterpret_cast<float*>(smem + kG));   // the G area is unused there
     return;
   }
 
@@ -657,7 +239,7 @@ __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
   // W1 rows of the 4 positions: loaded once (independent of the image chunk)
   {
     const int r = tid >> 3, c = (tid & 7) * 8;  // 128 rows x 8 chunks of 16 B
-    bf16x8 v = r < nrow ? *reinterpret_cast<const bf16x8*>(a.W1r + (size_t)(p0 * CC + r) * a.ldw1r + c) : bf16x8{};
+    bf16x8 v = r < nrow ? *reinterpret_cast<const bf16x8*>(W1r + (size_t)(p0 * CC + r) * a.ldw1 + c) : bf16x8{};
     *reinterpret_cast<bf16x8*>(W1s + r * RSTR + c) = v;
   }
 
@@ -670,7 +252,7 @@ __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
     bf16x8 ptv;
     {
       const int r = tid >> 3, c = (tid & 7) * 8;
-      ptv = r < nrow ? load_frag(a.Pt + (size_t)(p0 * CC + r) * a.ldPt + b0 + c, b0 + c, a.B, true) : bf16x8{};
+      ptv = r < nrow ? load_frag(Pt + (size_t)(p0 * CC + r) * a.ldPt + b0 + c, b0 + c, a.B, true) : bf16x8{};
     }
     float4 xv = {0.f, 0.f, 0.f, 0.f};
     {
@@ -690,8 +272,8 @@ __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
       if (p < P && b < a.B) amv = a.amax[((size_t)p * (CC / 8) + cg) * a.lda + b];
     }
     stamp(a.stamps, 1);
-    head_stage(a, hv, b1v, hr, hc4, nb, hs);
-    if (tid < 64) labs[tid] = lab;
+    head_stage(a, hv, b1v, hr, hc4, nb, hl.hs);
+    if (tid < 64) hl.labs[tid] = lab;
     {
       const int r = tid >> 3, c = (tid & 7) * 8;
       *reinterpret_cast<bf16x8*>(Pts + r * RSTR + c) = ptv;
@@ -708,8 +290,8 @@ __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
     // ---- the head recomputed: G = dH (bf16) into LDS, row-major and transposed
     {
       float la = 0.f, ca = 0.f, na = 0.f;   // the head workgroup keeps these
-      head_logits_ce(a, nb, hs, part, dls, w2s, b2s, labs, lane, wave, la, ca, na);
-      const f32x4 gh = head_dh(a, nb, hs, dls, w2s, lane, wave);
+      head_logits_ce(a, nb, hl, lane, wave, la, ca, na);
+      const f32x4 gh = head_dh(a, nb, hl, lane, wave);
       const int rt = wave >> 2, j = (wave & 3) * 16 + fr;
       bf16x4 gt;
 #pragma unroll
@@ -828,42 +410,16 @@ __global__ __launch_bounds__(1024) void convnet_bwd_kernel(ConvNetBwdArgs a) {
     }
   }
   // ---- reduce routing accumulators over the 16 waves, then 10*CC atomics
-#pragma unroll
-  for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) red[((size_t)wave * 16 + fq * 4 + r) * CC + ct * 16 + fr] = accr[ct][r];
-  lds_barrier();
-  if (tid < 10 * CC) {
-    const int tap = tid / CC, c = tid - tap * CC;
-    float s = 0.f;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) s += red[((size_t)w * 16 + tap) * CC + c];
-    if (tap < 9) atomicAdd(a.dwc + tap * CC + c, s);
-    else if (a.dbc) atomicAdd(a.dbc + c, s);
-  }
+  conv_grad_reduce(a, accr, dps, lane, wave);
   stamp(a.stamps, 5);
 }
 
 }  // namespace tde
 
 using namespace tde;
+using namespace tde::cnet;
 
 // Specialised for Conv2D(32, 3x3, valid) on 1-channel input + MaxPool(2) + Dense(64).
-// Fused-step optimizer description shared by the convnet entry points (ctypes struct):
-// slots m/v flat like w; iterations = the device step counter.
-struct TdeStepOpt {
-  int kind;
-  float lr, mom, b1, b2, eps;
-  float *w, *g, *m, *v;
-  const long long* iterations;
-  int* pend;
-};
-
-static OptHyper hyper_of(const TdeStepOpt* o) { return OptHyper{o->kind, o->lr, o->mom, o->b1, o->b2, o->eps}; }
-static bool opt_ok(const TdeStepOpt* o) {
-  return o->w && o->g && o->iterations && (o->kind == kOptSGD || o->m) && (o->kind != kOptAdam || o->v);
-}
-
 // w1_rows: W1c is the row-major [K][HD] shadow (ldw1c == HD) instead of [HD][K].
 // opt (nullable): deferred conv update {w, g, m, v, pend} with wc/bc at offsets off_wc/off_bc.
 TDE_API int tde_convnet_fwd(const float* x, const float* wc, const float* bc, const void* W1c, int ldw1c,
@@ -881,22 +437,9 @@ TDE_API int tde_convnet_fwd(const float* x, const float* wc, const float* bc, co
     const int byp = (ldPt + 63) / 64;
     if (byp > by) by = byp;
   }
-  ConvNetFwdArgs a{x, wc, bc, (const bf16*)W1c, ldw1c, hpre, (bf16*)Pt, ldPt, (uint64_t*)amax, lda, B, H, W, stamps};
+  FwdArgs a{x, wc, bc, W1c, ldw1c, hpre, Pt, ldPt, (uint64_t*)amax, lda, B, H, W, stamps};
   a.w1_rows = w1_rows;
-  a.inc_iter = (unsigned long long*)inc_iter;
-  a.hrep = hrep > 0 ? hrep : 1;
-  a.hrep_stride = hrep_stride;
-  if (opt) {
-    a.pend = opt->pend;
-    a.gwc = opt->g + off_wc;
-    a.gbc = opt->g + off_bc;
-    a.mwc = opt->m ? opt->m + off_wc : nullptr;
-    a.mbc = opt->m ? opt->m + off_bc : nullptr;
-    a.vwc = opt->v ? opt->v + off_wc : nullptr;
-    a.vbc = opt->v ? opt->v + off_bc : nullptr;
-    a.iterations = opt->iterations;
-    a.h = hyper_of(opt);
-  }
+  fill_fwd_opt(a, opt, off_wc, off_bc, inc_iter, hrep, hrep_stride);
   // positions per workgroup (TDE_CONVNET_FPW = 1|2|4, default 2)
   static const int fpw = [] {
     const char* e = getenv("TDE_CONVNET_FPW");
@@ -918,91 +461,20 @@ TDE_API int tde_convnet_fwd(const float* x, const float* wc, const float* bc, co
   return 0;
 }
 
-// Fused-step description of the backward (ctypes struct).
-struct TdeBwdOpt {
-  int kind;
-  float lr, mom, b1, b2, eps;
-  float *w, *m, *v;                   // flat buffers
-  long long off_w1, off_w2, off_b2, off_b1;
-  void* W1c; int ldw1c;               // transposed bf16 shadow (nullable)
-  const long long* iterations;
-  long long* iter_prev;
-  FlatApply commit;                   // previous step's deferred conv update (nr = 0: none)
-  int* pend_set;
-};
-
 // hpre: this step's Dense(64) pre-activation [B][64] f32; hzero: the other parity buffer (zeroed).
 // MODE 0 (opt == null): dW1 stored, conv grads atomically added, head grads (dW2 [64][C], db2, db1)
-// added by one workgroup.  opt: fused step (see ConvNetBwdArgs).
+// added by one workgroup.  opt: fused step (see BwdArgs).
 TDE_API int tde_convnet_bwd(const float* x, const void* amax, int lda, const float* hpre, float* hzero,
                             int hrep, long long hrep_stride, const float* b1, const float* W2, const float* b2, int C, int pre_relu,
                             const int* labels, float scale, float* metrics, const void* W1r, int ldw1r,
                             const void* Pt, int ldPt, float* dW1, float* dwc, float* dbc, float* dW2, float* db2,
                             float* db1, int B, int H, int W, long long* stamps, const TdeBwdOpt* opt,
                             hipStream_t stream) {
-  if ((ldw1r & 7) || (ldPt & 7) || ldPt < B || lda < B || C < 1 || C > 16 || !hpre || !hzero || !labels) return -1;
-  if ((((uintptr_t)hpre | (uintptr_t)hzero | (uintptr_t)b1) & 15)) return -2;
-  if (opt && (!opt->w || !opt->iterations || (opt->kind != kOptSGD && !opt->m) || (opt->kind == kOptAdam && !opt->v) ||
-              ldw1r != HD || (opt->W1c && (opt->ldw1c & 3)) || (opt->off_w1 & 3) || opt->commit.nr > kFlatRanges ||
-              (opt->commit.nr > 0 && !opt->commit.pend) || (b1 != nullptr) != (opt->off_b1 >= 0)))
-    return -4;
-  if (opt && opt->commit.nr > 0) {
-    int total = 0;
-    for (int i = 0; i < opt->commit.nr; ++i) total += opt->commit.n[i];
-    if (total > 1024) return -5;
-  }
+  BwdArgs a;
+  const int rc = fill_bwd(a, x, amax, lda, hpre, hzero, hrep, hrep_stride, b1, W2, b2, C, pre_relu, labels, scale,
+                          metrics, W1r, ldw1r, Pt, ldPt, dW1, dwc, dbc, dW2, db2, db1, B, H, W, stamps, opt);
+  if (rc) return rc;
   const int P = ((H - 2) / 2) * ((W - 2) / 2);
-  ConvNetBwdArgs a{};
-  a.x = x;
-  a.amax = (const uint64_t*)amax;
-  a.lda = lda;
-  a.hpre = hpre;
-  a.hzero = hzero;
-  if (hrep < 1 || hrep > 4 || (hrep > 1 && (hrep_stride < (long long)B * HD || (hrep_stride & 3)))) return -6;
-  a.hrep = hrep;
-  a.hrep_stride = hrep_stride;
-  a.b1 = b1;
-  a.W2 = W2;
-  a.b2 = b2;
-  a.C = C;
-  a.pre_relu = pre_relu;
-  a.labels = labels;
-  a.scale = scale;
-  a.metrics = metrics;
-  a.W1r = (const bf16*)W1r;
-  a.ldw1r = ldw1r;
-  a.Pt = (const bf16*)Pt;
-  a.ldPt = ldPt;
-  a.dW1 = dW1;
-  a.dwc = dwc;
-  a.dbc = dbc;
-  a.dW2 = dW2;
-  a.db2 = db2;
-  a.db1 = db1;
-  a.B = B;
-  a.H = H;
-  a.W = W;
-  a.stamps = stamps;
-  a.off_b1 = -1;
-  if (opt) {
-    a.w1 = opt->w + opt->off_w1;
-    a.m1 = opt->m ? opt->m + opt->off_w1 : nullptr;
-    a.v1 = opt->v ? opt->v + opt->off_w1 : nullptr;
-    a.w1r_out = (bf16*)W1r;
-    a.w1c_out = (bf16*)opt->W1c;
-    a.ldw1c = opt->ldw1c;
-    a.hw = opt->w;
-    a.hm = opt->m;
-    a.hv = opt->v;
-    a.off_w2 = opt->off_w2;
-    a.off_b2 = opt->off_b2;
-    a.off_b1 = opt->off_b1;
-    a.iterations = opt->iterations;
-    a.iter_prev = opt->iter_prev;
-    a.h = OptHyper{opt->kind, opt->lr, opt->mom, opt->b1, opt->b2, opt->eps};
-    a.commit = opt->commit;
-    a.pend_set = opt->pend_set;
-  }
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)convnet_bwd_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, kBwdLds);

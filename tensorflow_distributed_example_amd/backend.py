@@ -4,9 +4,10 @@ Keras-backend equivalents used by the reference:
   * ``set_learning_phase`` — mnist_keras_distributed.py:116, tf2_mnist_distributed.py:142
     (quirk Q4: a global training-phase override that also affects eval/export).
   * layer auto-naming (``conv2d``, ``conv2d_1``, ...) — used for checkpoint keys.
-  * dtype policy: reference is float32; the MI355X build defaults to
-    ``mixed_bfloat16`` on GPU (fp32 master weights, bf16 MFMA compute) as the
-    BASELINE configs ask for bf16.
+  * dtype policy: ``float32`` by default, the reference's precision (Keras default;
+    distributed_with_keras.py:21 casts the images to float32): the fused GPU plans then
+    run their exact-f32 MFMA kernel forms.  ``mixed_bfloat16`` (fp32 master weights,
+    bf16 MFMA compute) is the opt-in fast path the bf16 BASELINE configs ask for.
 """
 from __future__ import annotations
 
@@ -79,11 +80,24 @@ def default_devices():
     return _default_devices
 
 
+def parse_device(spec: str) -> torch.device:
+    """``cpu`` / ``/cpu:0`` / ``gpu:N`` / ``/gpu:N`` / ``cuda:N`` (``--devices`` entries) -> torch device."""
+    d = str(spec).strip().lower().lstrip("/")
+    if d.startswith("device:"):
+        d = d[len("device:"):]
+    if d.startswith("cpu"):
+        return torch.device("cpu")
+    for pre in ("gpu", "cuda"):
+        if d.startswith(pre):
+            rest = d[len(pre):].lstrip(":")
+            return torch.device("cuda", int(rest) if rest else 0)
+    raise ValueError(f"unknown device {spec!r} (cpu, gpu:N, cuda:N)")
+
+
 def default_device() -> torch.device:
     if _default_devices:
-        d = _default_devices[0].lower()
-        if d.startswith("/cpu") or d.startswith("cpu"):
-            return torch.device("cpu")
+        # the first --devices entry (the Estimator paths build OneDeviceStrategy(default_device()))
+        return parse_device(_default_devices[0])
     if gpu_available():
         n = torch.cuda.device_count()
         return torch.device("cuda", local_rank() % max(n, 1))
@@ -103,14 +117,15 @@ class Policy:
         return f"<Policy {self.name}>"
 
 
-def set_global_policy(name: str):
+def set_global_policy(name):
+    """``"float32"`` | ``"mixed_bfloat16"`` | a Policy | None (back to the default, float32)."""
     global _policy
     _policy = Policy(name) if isinstance(name, str) else name
 
 
 def global_policy() -> Policy:
     if _policy is None:
-        return Policy("mixed_bfloat16" if gpu_available() else "float32")
+        return Policy(os.environ.get("TDE_POLICY", "float32"))
     return _policy
 
 

@@ -173,7 +173,9 @@ def convnet_fwd(x, wc, bc, W1, hpre, Pt=None, amax=None, stamps=None, *, opt: St
                 off_wc=0, off_bc=0, inc_iter=None, hrep=1):
     """Fused Conv2D(32,3x3,relu)+MaxPool(2)+Dense(64) matmul forward; hpre += (atomic).
 
-    W1: the bf16 Dense(64) kernel shadow, row-major [K, 64] or transposed [64, K].
+    Precision follows W1: a bf16 Dense(64) kernel shadow, row-major [K, 64] or transposed [64, K],
+    runs the bf16 MFMA form (csrc/kernels/convnet.hip); the f32 master kernel [K, 64] runs the
+    float32 form (csrc/kernels/convnet_f32.hip, exact-f32 MFMA), whose Pt must then be f32 too.
     amax: uint8 view of a [P, 4, lda] uint64 buffer (lane-contiguous pool argmax).
     opt (fused step): while ``*opt.pend`` the conv weights used are the optimizer step of
     (w, g) at offsets off_wc / off_bc of the flat buffers (the deferred update).
@@ -182,11 +184,15 @@ def convnet_fwd(x, wc, bc, W1, hpre, Pt=None, amax=None, stamps=None, *, opt: St
     B, H, W = x.shape[0], x.shape[1], x.shape[2]
     Kf = ((H - 2) // 2) * ((W - 2) // 2) * 32
     _req(wc.shape == (3, 3, 1, 32) and bc is not None and bc.numel() == 32, "convnet_fwd: conv must be 3x3x1x32")
-    _req(W1.dtype == torch.bfloat16 and W1.stride(-1) == 1, "convnet_fwd: W1 bf16")
+    f32 = W1.dtype == torch.float32
+    _req((f32 or W1.dtype == torch.bfloat16) and W1.stride(-1) == 1, "convnet_fwd: W1 bf16 or f32")
     rows = tuple(W1.shape) == (Kf, 64)
-    _req(rows and W1.stride(0) == 64 or tuple(W1.shape) == (64, Kf) and W1.stride(0) % 8 == 0,
-         "convnet_fwd: W1 must be [K,64] or [64,K]")
-    _req(W % 2 == 0 and x.shape[3] == 1 and x.is_contiguous(), "convnet_fwd: input")
+    if f32:
+        _req(rows and W1.stride(0) == 64, "convnet_fwd: f32 W1 must be the [K,64] master kernel")
+    else:
+        _req(rows and W1.stride(0) == 64 or tuple(W1.shape) == (64, Kf) and W1.stride(0) % 8 == 0,
+             "convnet_fwd: W1 must be [K,64] or [64,K]")
+    _req(W % 2 == 0 and x.shape[3] == 1 and x.is_contiguous() and x.dtype == torch.float32, "convnet_fwd: input")
     hp = hpre if hrep == 1 and hpre.dim() == 2 else hpre.reshape(-1, *hpre.shape[-2:])
     _req(hp.shape[0] == hrep and hpre.is_contiguous() if hp.dim() == 3 else hrep == 1, "convnet_fwd: hpre replicas")
     _req(hp.shape[-2] >= B and hp.shape[-1] == 64 and hpre.is_contiguous(), "convnet_fwd: hpre")
@@ -194,15 +200,22 @@ def convnet_fwd(x, wc, bc, W1, hpre, Pt=None, amax=None, stamps=None, *, opt: St
     ldPt = 0
     if Pt is not None:
         ldPt = Pt.stride(0)
-        _req(Pt.shape[0] == Kf and ldPt >= B and ldPt % 8 == 0, "convnet_fwd: Pt")
+        _req(Pt.shape[0] == Kf and ldPt >= B and ldPt % 8 == 0 and Pt.dtype == W1.dtype, "convnet_fwd: Pt")
     lda = 0
     if amax is not None:
         lda = amax.shape[-1]
         _req(amax.dtype == torch.int64 and amax.shape[:2] == (Kf // 32, 4) and lda >= B, "convnet_fwd: amax")
+    optp = _ct.byref(opt) if opt is not None else None
+    hstride = hp.stride(0) if hp.dim() == 3 else 0
+    if f32:
+        rc = N.hip().tde_convnet_fwd_f32(_P(x), _P(wc), _P(bc), _P(W1), W1.stride(0), _P(hpre), _P(Pt), ldPt,
+                                         _P(amax), lda, B, H, W, _P(stamps), optp, int(off_wc), int(off_bc),
+                                         _P(inc_iter), int(hrep), hstride, _s())
+        N.check(rc, "tde_convnet_fwd_f32")
+        return
     rc = N.hip().tde_convnet_fwd(_P(x), _P(wc), _P(bc), _P(W1), W1.stride(0), _P(hpre), _P(Pt), ldPt,
-                                 _P(amax), lda, B, H, W, _P(stamps), int(rows),
-                                 _ct.byref(opt) if opt is not None else None, int(off_wc), int(off_bc),
-                                 _P(inc_iter), int(hrep), hp.stride(0) if hp.dim() == 3 else 0, _s())
+                                 _P(amax), lda, B, H, W, _P(stamps), int(rows), optp, int(off_wc), int(off_bc),
+                                 _P(inc_iter), int(hrep), hstride, _s())
     N.check(rc, "tde_convnet_fwd")
 
 
@@ -212,15 +225,19 @@ def convnet_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, me
     ``hpre`` [B, 64] (f32) every workgroup recomputes the head (loss, dlogits, Dense(64) input gradient)
     and runs the trunk backward; ``hzero`` (the other parity buffer) is zeroed for the next forward.
     ``hpre`` / ``hzero`` may be [R, B, 64] replica stacks (summed on load; all zeroed).
+    Precision follows ``W1row``: the bf16 row-major shadow (bf16 form) or the f32 master kernel
+    (float32 form; ``Pt`` f32, and in the fused step ``W1row`` is the memory ``opt`` updates).
     Plain (``opt`` None): dW1 stored, conv grads atomically added, dW2 / db2 / db1 added, metrics
     accumulated.  ``opt`` (fused step): the updates are applied instead (see ``BwdOpt``)."""
     B = x.shape[0] if B is None else B
     H, W = x.shape[1], x.shape[2]
     Kf = ((H - 2) // 2) * ((W - 2) // 2) * 32
     Hd, C = W2.shape
+    f32 = W1row.dtype == torch.float32
     _req(dwc.shape == (3, 3, 1, 32) and Hd == 64 and C <= 16, "convnet_bwd: specialised for Conv2D(32) + Dense(64)")
     _req(W1row.shape == (Kf, 64) and W1row.stride(0) == 64 and dW1.shape == (Kf, 64) and Pt.shape[0] == Kf,
          "convnet_bwd: shapes")
+    _req(Pt.dtype == W1row.dtype and (f32 or W1row.dtype == torch.bfloat16), "convnet_bwd: W1 / Pt dtypes")
     _req(Pt.stride(0) >= B and Pt.stride(0) % 8 == 0, "convnet_bwd: Pt ld")
     _req(amax.dtype == torch.int64 and amax.shape[:2] == (Kf // 32, 4) and amax.shape[-1] >= B, "convnet_bwd: amax")
     hp = hpre if hpre.dim() == 3 else hpre.unsqueeze(0)
@@ -228,12 +245,13 @@ def convnet_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, me
          and hzero.shape == hpre.shape and hzero.is_contiguous(), "convnet_bwd: hpre / hzero")
     _req(labels.dtype == torch.int32 and labels.numel() >= B, "convnet_bwd: int32 labels")
     _req(W2.is_contiguous() and b2.numel() == C and (b1 is None or b1.numel() == 64), "convnet_bwd: head variables")
-    rc = N.hip().tde_convnet_bwd(_P(x), _P(amax), amax.shape[-1], _P(hpre), _P(hzero), hp.shape[0], hp.stride(0),
-                                 _P(b1), _P(W2), _P(b2), C,
-                                 int(pre_relu), _P(labels), float(scale), _P(metrics), _P(W1row), W1row.stride(0),
-                                 _P(Pt), Pt.stride(0), _P(dW1), _P(dwc), _P(dbc), _P(dW2), _P(db2), _P(db1), B, H,
-                                 W, _P(stamps), _ct.byref(opt) if opt is not None else None, _s())
-    N.check(rc, "tde_convnet_bwd")
+    fn = N.hip().tde_convnet_bwd_f32 if f32 else N.hip().tde_convnet_bwd
+    rc = fn(_P(x), _P(amax), amax.shape[-1], _P(hpre), _P(hzero), hp.shape[0], hp.stride(0),
+            _P(b1), _P(W2), _P(b2), C,
+            int(pre_relu), _P(labels), float(scale), _P(metrics), _P(W1row), W1row.stride(0),
+            _P(Pt), Pt.stride(0), _P(dW1), _P(dwc), _P(dbc), _P(dW2), _P(db2), _P(db1), B, H,
+            W, _P(stamps), _ct.byref(opt) if opt is not None else None, _s())
+    N.check(rc, "tde_convnet_bwd_f32" if f32 else "tde_convnet_bwd")
 
 
 def noop(blocks=1, threads=64):

@@ -254,6 +254,7 @@ class XgmiCommunicator(Communicator):
     """
 
     capturable = True
+    plain_ok = True   # False: the fallback measured faster for a plain (unfused) gradient all-reduce
 
     def __init__(self, device, rank, world, fallback, max_elems=None, uncached=None, nblocks=None,
                  timeout_s=None, group=None):
@@ -463,9 +464,12 @@ def maybe_xgmi(fallback, device, rank, world, bucket_hint=None, group=None):
         tr = _time_allreduce(fallback, t, 20, group)
         # the xGMI kernel can also carry the optimizer update (one launch fewer per step, see
         # XgmiCommunicator.all_reduce_apply_): it keeps the bucket unless RCCL is faster by more than that
+        # (the margin only applies to plans that fuse the update into it: Program re-decides the plain
+        # all-reduce with plain_ok)
         margin = float(os.environ.get("TDE_XGMI_MARGIN_US", "3")) * 1e-6
-        dec = [tx <= tr + margin]
+        dec = [tx <= tr + margin, tx <= tr]
         dist.broadcast_object_list(dec, src=0, group=group)
+        xg.plain_ok = bool(dec[1])
         if rank == 0:
             import sys
             print(f"[tde.comm] all-reduce of {t.numel()} fp32: xGMI {tx * 1e6:.1f} us, RCCL {tr * 1e6:.1f} us "

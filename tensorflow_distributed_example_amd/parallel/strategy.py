@@ -206,13 +206,7 @@ def _parse_devices(devices):
         if isinstance(d, torch.device):
             out.append(d)
             continue
-        s = str(d).lower()
-        if s.startswith("/gpu:") or s.startswith("gpu:") or s.startswith("/device:gpu:"):
-            out.append(torch.device("cuda", int(s.rsplit(":", 1)[1])))
-        elif s.startswith("/cpu") or s.startswith("cpu"):
-            out.append(torch.device("cpu"))
-        else:
-            out.append(torch.device(s))
+        out.append(Kb.parse_device(d))
     return out
 
 

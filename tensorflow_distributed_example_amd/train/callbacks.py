@@ -169,10 +169,13 @@ class ProfilerCallback(Callback):
         return self._hook.written
 
     def on_train_batch_begin(self, batch, logs=None):
+        self._first = batch
         self._hook.before_step(None, self._step + 1)
 
     def on_train_batch_end(self, batch, logs=None):
-        self._step += 1
+        # fit() calls begin / end once per execution (steps_per_execution steps): batch is the index of
+        # the execution's last step, so the global step advances by the execution's length
+        self._step += batch - getattr(self, "_first", batch) + 1
 
         class _Ctx:
             global_step = self._step

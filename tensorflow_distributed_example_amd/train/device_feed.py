@@ -43,7 +43,16 @@ class DeviceFeed:
         per = int(np.prod(prog.x_shape))
         if len(y) != n or x.size != n * per or y.size != n or n >= 2 ** 31:
             return None
+        if not DeviceFeed.row_ok(per, prog.x_ring[0].dtype):
+            return None
         return DeviceFeed(prog, x, y, index_iter)
+
+    @staticmethod
+    def row_ok(per, ring_dtype):
+        """The HIP row gather moves whole 4-byte words (gather.hip): a row of ``per`` elements of the ring
+        dtype must be a multiple of 4 bytes (an odd feature count in a bf16 ring is not), else the
+        host gather + pinned staging path feeds the program."""
+        return (per * torch.empty((), dtype=ring_dtype).element_size()) % 4 == 0
 
     def __init__(self, prog, x, y, index_iter):
         from .. import _native as N

@@ -108,8 +108,12 @@ class _Stage:
         return [n for n in (getattr(self, "wname", None), getattr(self, "bname", None)) if n]
 
 
+_warned_bf16 = set()
+
+
 class LayerwisePlan(PG.ReplicaPlan):
     kind = "layerwise"
+    compute_dtype = "bf16"   # the layer-wise kernel library computes in bf16 (fp32 master weights)
     # inputs staged as bf16 (Keras mixed_bfloat16 casts them at the first layer anyway): no per-step
     # cast launch; TDE_BF16_INPUT=0 keeps f32 staging + the cast kernel
     input_dtype = bf16 if os.environ.get("TDE_BF16_INPUT", "1") != "0" else torch.float32
@@ -119,6 +123,12 @@ class LayerwisePlan(PG.ReplicaPlan):
         self.loss = loss
         self.model = model
         self._compile()
+        if Kb.global_policy().compute_dtype == torch.float32 and model.name not in _warned_bf16:
+            # never silent: the float32 policy asked for exact f32, this plan computes in bf16
+            _warned_bf16.add(model.name)
+            import warnings
+            warnings.warn(f"model {model.name!r}: the layer-wise HIP plan computes in bf16 (mixed_bfloat16) under "
+                          "the float32 policy; set_global_policy('mixed_bfloat16') states that explicitly")
         self._alloc()
         # TDE_WGRAD_STREAM=1: weight gradients on a side stream, concurrent with the input-gradient chain
         # (joined at the end of the backward).  Off by default: measured slower in the captured step

@@ -78,6 +78,7 @@ class ReplicaPlan:
     # communicator's fused all-reduce applies it).
     step_mode = "plain"
     input_dtype = torch.float32   # dtype of the Program's input ring for this plan
+    compute_dtype = "fp32"        # what the plan's kernels compute in ("fp32" | "bf16"; bench / logs)
     parity = 0   # step parity of plans that double-buffer across steps (one hipGraph per start parity)
 
     def supports_step_mode(self, mode):
@@ -287,12 +288,19 @@ def match_convnet(model, loss):
     if d2.units > 64 or d1.units * d2.units > 16384 or d1.units % 32 or d1.units > 256:
         return None
     if c.filters != 32 or d1.units != 64:
-        return None  # fused backward is specialised for the reference's Conv2D(32)/Dense(64)
+        # the fused step is specialised for the reference's Conv2D(32)/Dense(64) (distributed_with_keras.py
+        # :34,37): say so instead of silently dropping a near-miss to the slower per-layer plan
+        import warnings
+        warnings.warn(f"model {model.name!r}: the fused small-CNN step supports Conv2D(32) + Dense(64) only "
+                      f"(got Conv2D({c.filters}) + Dense({d1.units})); running the per-layer kernel plan")
+        return None
     return dict(conv=c, pool=p, dense1=d1, dense2=d2)
 
 
 class ConvNetPlan(ReplicaPlan):
-    """The DWK/TF2M small CNN as two HIP launches per training step (csrc/kernels/convnet.hip):
+    """The DWK/TF2M small CNN as two HIP launches per training step, in the precision of the global
+    policy: float32 (the reference's; csrc/kernels/convnet_f32.hip, exact-f32 MFMA over the f32 master
+    weights) or mixed_bfloat16 (csrc/kernels/convnet.hip, bf16 MFMA over bf16 weight shadows):
 
       forward   conv+bias+ReLU+pool fused with the Dense(64) matmul (split-K atomics into hpre[p])
       backward  the head recomputed from hpre[p] in every workgroup (softmax-CE, dlogits, Dense(64)
@@ -313,6 +321,8 @@ class ConvNetPlan(ReplicaPlan):
         self.loss = loss
         c, d1, d2 = pattern["conv"], pattern["dense1"], pattern["dense2"]
         self.c, self.d1, self.d2 = c, d1, d2
+        self.f32 = Kb.global_policy().compute_dtype == torch.float32
+        self.compute_dtype = "fp32" if self.f32 else "bf16"
         H, W = c.input_shape[0], c.input_shape[1]
         self.H, self.W, self.C = H, W, c.filters
         Hp, Wp = (H - 2) // 2, (W - 2) // 2
@@ -321,8 +331,7 @@ class ConvNetPlan(ReplicaPlan):
         B, Bp = self.B, _round8(self.B)
         self.Bp = Bp
         dev = self.device
-        bf = torch.bfloat16
-        self.Pt = torch.zeros(self.Kf, Bp, dtype=bf, device=dev)
+        self.Pt = torch.zeros(self.Kf, Bp, dtype=torch.float32 if self.f32 else torch.bfloat16, device=dev)
         self.amax = torch.zeros(self.Kf // 32, 4, Bp, dtype=torch.int64, device=dev)  # [P][C/8][B] argmax bytes
         # Dense(64) pre-activation: two training buffers by step parity + one for eval / predict
         # (training buffers: hrep replicas each, so the forward's ~85 split-K adders per address spread out)
@@ -336,19 +345,27 @@ class ConvNetPlan(ReplicaPlan):
         n = lambda l, w: f"{l.name}/{w}"  # noqa: E731
         self.names = dict(wc=n(c, "kernel"), bc=n(c, "bias"), w1=n(d1, "kernel"),
                           b1=n(d1, "bias") if d1.use_bias else None, w2=n(d2, "kernel"), b2=n(d2, "bias"))
-        # the forward reads the Dense(64) kernel from the row-major bf16 shadow (the one the backward
-        # reads and the fused updates rewrite); TDE_CONVNET_W1=col keeps a transposed [64, K] copy for it
-        self.w1_rows = os.environ.get("TDE_CONVNET_W1", "rows") != "col"
-        shadows = {self.names["w1"]: ("row",) if self.w1_rows else ("row", "col")}
+        # bf16: the forward reads the Dense(64) kernel from the row-major bf16 shadow (the one the
+        # backward reads and the fused updates rewrite); TDE_CONVNET_W1=col keeps a transposed [64, K]
+        # copy for it.  f32: both read the f32 master kernel itself (no shadow exists).
+        self.w1_rows = self.f32 or os.environ.get("TDE_CONVNET_W1", "rows") != "col"
+        if self.f32:
+            shadows = {}
+        else:
+            shadows = {self.names["w1"]: ("row",) if self.w1_rows else ("row", "col")}
         self.opt = OptimizerKernel(store, optimizer, shadows, self.iterations) if optimizer is not None else None
         self._shadow_only = None
-        if self.opt is None:
+        if self.opt is None and shadows:
             # eval/predict-only plan still needs the bf16 weight copies
             from ..optimizers import SGD
             self._shadow_only = OptimizerKernel(store, SGD(0.0), shadows, self.iterations)
-        ok = self.opt or self._shadow_only
-        self.W1row = ok.shadow_views[(self.names["w1"], "row")]
-        self.W1col = None if self.w1_rows else ok.shadow_views[(self.names["w1"], "col")]
+        if self.f32:
+            self.W1row = store.view(self.names["w1"])
+            self.W1col = None
+        else:
+            ok = self.opt or self._shadow_only
+            self.W1row = ok.shadow_views[(self.names["w1"], "row")]
+            self.W1col = None if self.w1_rows else ok.shadow_views[(self.names["w1"], "col")]
         self.W1fwd = self.W1row if self.w1_rows else self.W1col
         # fused step ("local"): conv gradients by step parity (the deferred update of step t is read by
         # forward t+1 while backward t+1 accumulates the next), their pending flags, and the step count
@@ -433,6 +450,9 @@ class ConvNetPlan(ReplicaPlan):
         hp = opt.hparams()
         seg = st.segments[self.names["w1"]]
         K = self.K
+        if self.f32:   # no shadow: the all-reduce updates the f32 master weights only
+            return K.XgApply(opt.kind_id, float(opt.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"],
+                             K._P(st.w), K._P(m), K._P(v), K._P(self.iterations), None, 0, 0, None, 0, 0)
         return K.XgApply(opt.kind_id, float(opt.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"],
                          K._P(st.w), K._P(m), K._P(v), K._P(self.iterations), K._P(self.W1row), seg.offset,
                          seg.offset + seg.numel, K._P(self.W1col), self.Hd,
@@ -444,7 +464,8 @@ class ConvNetPlan(ReplicaPlan):
             self.K.flat_apply(self._flush[1 - self.parity])
 
     def on_weights_loaded(self):
-        (self.opt or self._shadow_only).refresh_shadows()
+        if not self.f32:
+            (self.opt or self._shadow_only).refresh_shadows()
         # loaded weights replace whatever update was outstanding
         self.pend.zero_()
         self.gconv.zero_()

@@ -109,6 +109,7 @@ class Program:
         self.plans = [PG.make_plan(model, st, dev, self.B, global_batch, opt, model.loss)
                       for st, dev in zip(self.stores, self.devices)]
         self.comm = strategy.comm if self.world > 1 else None
+        self.grad_comm = self.comm   # carries the gradient bucket (may differ from self.comm: _pick_step_mode)
         xs = tuple(model.input_shape[1:])
         self.x_shape = xs
         xdt = self.plans[0].input_dtype
@@ -136,15 +137,24 @@ class Program:
         """Fused optimizer placement (TDE_FUSED_STEP=0 keeps the separate optimizer launch): with one
         replica the update runs inside the step's own kernels ("local"); with one replica per process
         under the xGMI communicator it runs inside the gradient all-reduce ("xgmi")."""
+        from ..parallel.comm import XgmiCommunicator
+        self._route_grads()
         if os.environ.get("TDE_FUSED_STEP", "1") == "0" or len(self.plans) != 1 or self.buckets:
             return
         plan = self.plans[0]
-        from ..parallel.comm import XgmiCommunicator
         if self.comm is None and plan.supports_step_mode("local"):
             plan.set_step_mode("local")
         elif isinstance(self.comm, XgmiCommunicator) and plan.supports_step_mode("xgmi"):
             plan.set_step_mode("xgmi")
             self.comm_applies = True
+            self.grad_comm = self.comm
+
+    def _route_grads(self):
+        """The xGMI kernel keeps the bucket over a slightly faster RCCL only because it can also apply the
+        update; a plan that cannot fuse it sends a plain all-reduce to whichever measured faster."""
+        from ..parallel.comm import XgmiCommunicator
+        if isinstance(self.comm, XgmiCommunicator) and not self.comm.plain_ok and self.comm.fallback is not None:
+            self.grad_comm = self.comm.fallback
 
     def _plan_buckets(self):
         """Reverse-order gradient buckets all-reduced on a comm stream while backward still runs
@@ -183,7 +193,7 @@ class Program:
             self._debug_sync("gradient all-reduce + optimizer")
             return
         if self.comm is not None:
-            self.comm.all_reduce_([p.store.g for p in self.plans])
+            self.grad_comm.all_reduce_([p.store.g for p in self.plans])
             self._debug_sync("gradient all-reduce")
         for plan in self.plans:
             if plan.applies_in_step:
@@ -229,7 +239,7 @@ class Program:
                 if side is not None:
                     cs.wait_stream(side)
                 with torch.cuda.stream(cs):
-                    self.comm.all_reduce_([g[lo:hi]])
+                    self.grad_comm.all_reduce_([g[lo:hi]])
 
         with _ctx(plan.device):
             plan.train_step(self.x_ring[0][s], self.y_ring[0][s], B, after_bwd=after_bwd)
@@ -351,7 +361,7 @@ class Program:
                     plan = self.plans[0]
                     with _ctx(plan.device):
                         for _, lo, hi in self.buckets:
-                            self.comm.all_reduce_([plan.store.g[lo:hi]])
+                            self.grad_comm.all_reduce_([plan.store.g[lo:hi]])
                         plan.apply()
                 return
             for r, plan in enumerate(self.plans):

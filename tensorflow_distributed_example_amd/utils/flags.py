@@ -4,7 +4,8 @@ The reference scripts keep their own flags (``mnist_keras_distributed.py:33-65``
 framework additions every example accepts on top of them:
 
     --devices cpu | gpu:0,gpu:1 | cuda:0   replicas a strategy built without devices uses
-    --dtype fp32 | bf16                    compute policy (float32 / mixed_bfloat16)
+    --dtype fp32 | bf16                    compute policy: float32 (default; the reference's precision,
+                                           exact-f32 MFMA kernel forms) / mixed_bfloat16 (bf16 MFMA)
     --synthetic                            synthetic MNIST even when a local mnist.npz exists
     --profile-steps N                      Chrome-trace timeline of one step every N steps
                                            (Estimator ProfilerHook, MKD:235-237; Keras ProfilerCallback)
@@ -23,8 +24,8 @@ def add_framework_flags(parser):
     g.add_argument("--devices", default=None,
                    help="comma-separated replica devices (cpu, gpu:N, cuda:N); default: every local GPU, else CPU")
     g.add_argument("--dtype", choices=sorted(DTYPES), default=None,
-                   help="compute dtype: bf16 (mixed_bfloat16, the GPU kernels) or fp32 (CPU backend / torch "
-                        "reference executor on GPU)")
+                   help="compute dtype: fp32 (float32, the default and the reference's precision: exact-f32 "
+                        "MFMA kernels) or bf16 (mixed_bfloat16: bf16 MFMA kernels, fp32 master weights)")
     g.add_argument("--synthetic", action="store_true", help="use synthetic MNIST even if a local mnist.npz exists")
     g.add_argument("--profile-steps", type=int, default=0,
                    help="write a Chrome-trace timeline of one step every N steps (0: off)")
@@ -38,15 +39,8 @@ def apply_framework_flags(args):
         Kb.set_default_devices(devices.split(","))
     dtype = getattr(args, "dtype", None)
     if dtype:
+        # the GPU plans pick their kernel form from the policy (train/program.py make_plan)
         Kb.set_global_policy(DTYPES[dtype])
-        gpu = Kb.gpu_available() and not (devices and all(d.strip().lower().startswith(("cpu", "/cpu"))
-                                                           for d in devices.split(",")))
-        if dtype == "fp32" and gpu:
-            # the gfx950 kernel library computes in bf16 (fp32 master weights); exact fp32 on a GPU runs
-            # the torch reference executor (the numerics oracle), never silently
-            os.environ["TDE_EXECUTOR"] = "reference"
-            import warnings
-            warnings.warn("--dtype fp32 on a GPU: the torch reference executor runs (the HIP kernels are bf16)")
     if getattr(args, "synthetic", False):
         os.environ["TDE_SYNTHETIC_MNIST"] = "1"
     return args

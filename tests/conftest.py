@@ -19,6 +19,24 @@ def _fresh_session():
     tde.backend.clear_session()
     tde.backend.set_random_seed(0)
     yield
+    tde.backend.set_global_policy(None)
+
+
+@pytest.fixture
+def bf16_policy():
+    """Run the test under the mixed_bfloat16 policy (the bf16 MFMA kernel forms)."""
+    import tensorflow_distributed_example_amd as tde
+    tde.backend.set_global_policy("mixed_bfloat16")
+    yield
+    tde.backend.set_global_policy(None)
+
+
+@pytest.fixture
+def fp32_policy():
+    import tensorflow_distributed_example_amd as tde
+    tde.backend.set_global_policy("float32")
+    yield
+    tde.backend.set_global_policy(None)
 
 
 def pytest_collection_modifyitems(config, items):

@@ -174,3 +174,11 @@ def test_device_source_index_stream_matches_iteration(policy, workers, widx):
             assert np.array_equal(cols[0][idx], rx) and np.array_equal(cols[1][idx], ry)
     # pipelines that are not batches of in-memory rows have no device source
     assert Dataset.from_tensor_slices(x).batch(4).unbatch().batch(4).device_source() is None
+
+
+def test_device_feed_row_eligibility():
+    """the HIP row gather moves 4-byte words; an odd bf16 row must fall back to host staging."""
+    import torch
+    from tensorflow_distributed_example_amd.train.device_feed import DeviceFeed
+    assert DeviceFeed.row_ok(784, torch.bfloat16) and DeviceFeed.row_ok(785, torch.float32)
+    assert not DeviceFeed.row_ok(785, torch.bfloat16) and not DeviceFeed.row_ok(3, torch.bfloat16)

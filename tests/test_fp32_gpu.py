@@ -1,0 +1,261 @@
+"""Float32 (the reference's precision, distributed_with_keras.py:21) kernel forms vs float64 oracles.
+
+The fused MNIST-CNN step in its float32 form (csrc/kernels/convnet_f32.hip: exact-f32 MFMA over the
+f32 master weights) must match float64 autograd to fp32 accuracy: <= 1e-5 relative (norm-wise) on
+every gradient.  Inputs and conv weights are quantized so the conv pre-activations are exact in f32:
+the max-pool argmax / ReLU routing is then the same decision in both precisions (a near-tie decided
+differently by one ulp would move a whole pooled gradient), and the comparison measures the GEMMs,
+the head and the reductions."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("fp32_policy")]
+
+DEV = "cuda"
+TOL = 1e-5
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def _qdata(B, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randint(0, 17, (B, 28, 28, 1), generator=g).float() / 16.0
+    y = torch.randint(0, 10, (B,), generator=g).int()
+    return x.to(DEV), y.to(DEV)
+
+
+def _quantize_conv(st, name):
+    w = st.view(name)
+    w.copy_(torch.round(w * 64) / 64)
+
+
+def _ref_convpool(x, w, b):
+    y = F.conv2d(x.permute(0, 3, 1, 2), w.permute(3, 2, 0, 1), b)
+    return F.max_pool2d(F.relu(y), 2).permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize("B", [64, 37, 130])
+def test_convnet_fwd_f32(B):
+    from tensorflow_distributed_example_amd.ops import kernels as Kk
+    g = torch.Generator(device="cpu").manual_seed(21)
+    Kf, Hd = 13 * 13 * 32, 64
+    x, _ = _qdata(B, 3)
+    w = (torch.randint(-32, 33, (3, 3, 1, 32), generator=g).float() / 64).to(DEV)
+    b = (torch.randint(-8, 9, (32,), generator=g).float() / 64).to(DEV)
+    W1 = (torch.randn(Kf, Hd, generator=g) * 0.02).to(DEV)
+    Bp = (B + 7) // 8 * 8
+    hpre = torch.zeros(B, Hd, device=DEV)
+    Pt = torch.full((Kf, Bp), 5.0, device=DEV)
+    amax = torch.zeros(Kf // 32, 4, Bp, dtype=torch.int64, device=DEV)
+    Kk.convnet_fwd(x, w, b, W1, hpre, Pt, amax)
+    pooled = _ref_convpool(x.double(), w.double(), b.double()).reshape(B, Kf)
+    ref = pooled @ W1.double()
+    torch.cuda.synchronize()
+    assert torch.equal(Pt[:, :B].double().T, pooled)          # exact conv (quantized operands)
+    assert torch.all(Pt[:, B:] == 0)
+    assert _rel(hpre, ref) < TOL, _rel(hpre, ref)
+    amax_b = amax.view(torch.uint8).view(Kf // 32, 4, Bp, 8).permute(2, 0, 1, 3).reshape(Bp, Kf)[:B]
+    assert torch.equal(amax_b != 255, pooled > 0)
+
+
+@pytest.mark.parametrize("B,relu", [(64, True), (50, True), (128, False)])
+def test_convnet_bwd_f32(B, relu):
+    """Trunk backward with the head fused in, float32 form, vs float64 torch at fp32 tolerance."""
+    from tensorflow_distributed_example_amd.ops import kernels as Kk
+    g = torch.Generator(device="cpu").manual_seed(23)
+    C, Hd, NC = 32, 64, 10
+    Kf = 13 * 13 * C
+    Bp = (B + 7) // 8 * 8
+    x, lab = _qdata(B, 4)
+    w = (torch.randint(-32, 33, (3, 3, 1, C), generator=g).float() / 64).to(DEV)
+    b = (torch.randint(-8, 9, (C,), generator=g).float() / 64).to(DEV)
+    W1 = (torch.randn(Kf, Hd, generator=g) * 0.05).to(DEV)
+    hpre = (torch.randn(B, Hd, generator=g) * 0.5).to(DEV)
+    hzero = torch.full((B, Hd), 7.0, device=DEV)
+    b1 = (torch.randn(Hd, generator=g) * 0.1).to(DEV)
+    W2 = (torch.randn(Hd, NC, generator=g) * 0.3).to(DEV)
+    b2 = (torch.randn(NC, generator=g) * 0.1).to(DEV)
+    scale = 1.0 / 256
+    Pt = torch.zeros(Kf, Bp, device=DEV)
+    amax = torch.zeros(Kf // 32, 4, Bp, dtype=torch.int64, device=DEV)
+    Kk.convnet_fwd(x, w, b, W1, torch.zeros(B, Hd, device=DEV), Pt, amax)
+    dW1 = torch.full((Kf, Hd), 9.0, device=DEV)
+    dw = torch.zeros(3, 3, 1, C, device=DEV)
+    db = torch.zeros(C, device=DEV)
+    dW2, db2, db1 = torch.zeros(Hd, NC, device=DEV), torch.zeros(NC, device=DEV), torch.zeros(Hd, device=DEV)
+    met = torch.zeros(4, device=DEV)
+    hkeep = hpre.clone()
+    Kk.convnet_bwd(x, amax, hpre, hzero, b1, W2, b2, lab, scale=scale, pre_relu=relu, metrics=met, W1row=W1, Pt=Pt,
+                   dW1=dW1, dwc=dw, dbc=db, dW2=dW2, db2=db2, db1=db1)
+    d = torch.float64
+    h = hpre.to(d) + b1.to(d)
+    if relu:
+        h = h.clamp_min(0)
+    logits = h @ W2.to(d) + b2.to(d)
+    pr = torch.softmax(logits, 1)
+    onehot = F.one_hot(lab.long(), NC).to(d)
+    dl = (pr - onehot) * scale
+    dH = dl @ W2.to(d).T
+    if relu:
+        dH = dH * (h > 0)
+    wr, br = w.double().clone().requires_grad_(), b.double().clone().requires_grad_()
+    out = _ref_convpool(x.double(), wr, br).reshape(B, Kf)
+    (out * (dH @ W1.double().T)).sum().backward()
+    dW1_ref = out.detach().T @ dH
+    torch.cuda.synchronize()
+    assert torch.equal(hpre, hkeep) and torch.all(hzero == 0)
+    for name, got, ref in [("dW1", dW1, dW1_ref), ("dconv_w", dw, wr.grad), ("dconv_b", db, br.grad),
+                           ("dW2", dW2, h.T @ dl), ("db2", db2, dl.sum(0)), ("db1", db1, dH.sum(0))]:
+        assert _rel(got, ref) < TOL, (name, _rel(got, ref))
+    loss = -(torch.log(pr) * onehot).sum()
+    assert abs(met[0].item() - loss.item()) < 1e-5 * abs(loss.item())
+    assert met[1].item() == (logits.argmax(1) == lab.long()).sum().item() and met[2].item() == B
+
+
+def _model(tde, opt=None, spe=1):
+    m = tde.zoo.mnist_cnn()
+    m.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True), optimizer=opt or tde.optimizers.SGD(0.05),
+              metrics=["accuracy"], steps_per_execution=spe)
+    m.build()
+    _quantize_conv(m._store, f"{m.layers[0].name}/kernel")
+    _quantize_conv(m._store, f"{m.layers[0].name}/bias")
+    return m
+
+
+def _oracle_grads(m, x, y, B):
+    """float64 autograd of the DWK model at the store's current weights."""
+    st = m._store
+    dd = torch.float64
+    W = {n: st.view(n).detach().to(dd).clone().requires_grad_(True) for n in st.names(trainable=True)}
+    c, d1, d2 = m.layers[0].name, m.layers[3].name, m.layers[4].name
+    P = _ref_convpool(x.to(dd), W[f"{c}/kernel"], W[f"{c}/bias"]).reshape(B, -1)
+    h = F.relu(P @ W[f"{d1}/kernel"] + W[f"{d1}/bias"])
+    logits = h @ W[f"{d2}/kernel"] + W[f"{d2}/bias"]
+    loss = F.cross_entropy(logits, y.long(), reduction="sum") / B
+    loss.backward()
+    return {n: w.grad for n, w in W.items()}, loss.item()
+
+
+def test_fp32_plan_step_gradients_match_float64():
+    """One training step of the fused plan in its float32 form: every variable's gradient vs float64."""
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.train import program as PG
+    m = _model(tde)
+    st = m._store
+    plan = PG.make_plan(m, st, DEV, 64, 64, m.optimizer, m.loss)
+    assert plan.kind == "fused_convnet" and plan.compute_dtype == "fp32" and plan.Pt.dtype == torch.float32
+    x, y = _qdata(64, 7)
+    ref, loss = _oracle_grads(m, x, y, 64)
+    plan.train_step(x, y)
+    torch.cuda.synchronize()
+    for n, gr in ref.items():
+        assert _rel(st.grad(n), gr) < TOL, (n, _rel(st.grad(n), gr))
+    assert abs(plan.metrics[0].item() / 64 - loss) < 1e-5 * abs(loss)
+
+
+@pytest.mark.parametrize("kind", ["sgd", "momentum", "adam"])
+def test_fp32_fused_local_step_matches_float64_sgd(kind):
+    """Three steps of the float32 fused step ("local": the optimizer inside the step's kernels, the conv
+    update deferred and flushed) vs three float64 steps of the same optimizer math (Keras forms)."""
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.train import program as PG
+    O = tde.optimizers
+    opt = {"sgd": lambda: O.SGD(0.05), "momentum": lambda: O.SGD(0.05, momentum=0.9),
+           "adam": lambda: O.Adam(2e-3)}[kind]()
+    m = _model(tde, opt)
+    st = m._store
+    names = st.names(trainable=True)
+    w = {n: st.view(n).detach().double().clone() for n in names}
+    slots = {n: [torch.zeros_like(w[n]), torch.zeros_like(w[n])] for n in names}
+    plan = PG.make_plan(m, st, DEV, 64, 64, m.optimizer, m.loss)
+    plan.set_step_mode("local")
+    for s in range(3):
+        x, y = _qdata(64, 30 + s)
+        # float64 oracle step from the oracle weights (copied into a scratch store view for the forward)
+        saved = {n: st.view(n).detach().clone() for n in names}
+        for n in names:
+            st.view(n).copy_(w[n])
+        g, _ = _oracle_grads(m, x, y, 64)
+        for n in names:
+            st.view(n).copy_(saved[n])
+        t = s + 1
+        for n in names:
+            if kind == "sgd":
+                w[n] = w[n] - 0.05 * g[n]
+            elif kind == "momentum":
+                slots[n][0] = 0.9 * slots[n][0] - 0.05 * g[n]
+                w[n] = w[n] + slots[n][0]
+            else:
+                b1, b2, eps = 0.9, 0.999, 1e-7
+                slots[n][0] = b1 * slots[n][0] + (1 - b1) * g[n]
+                slots[n][1] = b2 * slots[n][1] + (1 - b2) * g[n] ** 2
+                lr_t = 2e-3 * (1 - b2 ** t) ** 0.5 / (1 - b1 ** t)
+                w[n] = w[n] - lr_t * slots[n][0] / (slots[n][1].sqrt() + eps)
+        plan.train_step(x, y)
+    plan.finish()
+    torch.cuda.synchronize()
+    assert int(plan.pend.sum()) == 0
+    for n in names:
+        w0 = st.view(n).detach().double()
+        # the oracle's forward ran on the f32-rounded oracle weights: compare the weights themselves
+        # (SGD / momentum updates of 3 steps are ~1e-3 of |w|, so this is a tight check on the step;
+        # Adam's normalised steps are as large as the small bias weights: fp32-level relative error
+        # of the update shows up ~1:1 there)
+        tol = 5e-6 if kind == "adam" else 1e-6
+        assert _rel(w0, w[n]) < tol, (kind, n, _rel(w0, w[n]))
+
+
+def test_fp32_fit_graph_matches_eager(monkeypatch):
+    """fit() with hipGraph executions (fp32 form) vs eager launches: identical up to atomic order."""
+    import tensorflow_distributed_example_amd as tde
+    rng = np.random.default_rng(1)
+    x = rng.random((64 * 8, 28, 28, 1), dtype=np.float32)
+    y = rng.integers(0, 10, 64 * 8)
+    tde.backend.set_random_seed(3)
+    mg = tde.zoo.mnist_cnn()
+    mg.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True), optimizer=tde.optimizers.SGD(0.05),
+               metrics=["accuracy"], steps_per_execution=4)
+    w0 = mg.get_weights()
+    mg.fit(x, y, batch_size=64, epochs=1, shuffle=False, verbose=0)
+    prog = mg._program("train", 64)
+    assert prog.use_graph and prog.plans[0].compute_dtype == "fp32"
+    tde.backend.clear_session()
+    monkeypatch.setenv("TDE_GRAPH", "0")
+    me = tde.zoo.mnist_cnn()
+    me.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True), optimizer=tde.optimizers.SGD(0.05),
+               metrics=["accuracy"], steps_per_execution=1)
+    me.set_weights(w0)
+    me.fit(x, y, batch_size=64, epochs=1, shuffle=False, verbose=0)
+    for a, b, w in zip(mg.get_weights(), me.get_weights(), w0):
+        rel = np.linalg.norm((a - w) - (b - w)) / (np.linalg.norm(b - w) + 1e-12)
+        assert rel < 1e-4, rel
+
+
+def test_fp32_fit_matches_reference_executor(monkeypatch):
+    """The float32 HIP plan vs the torch fp32 reference executor over 4 fit steps: the accumulated
+    updates agree to fp32 accuracy (no bf16 anywhere in the HIP path)."""
+    import tensorflow_distributed_example_amd as tde
+    rng = np.random.default_rng(2)
+    x = (rng.integers(0, 17, (64 * 4, 28, 28, 1)) / 16.0).astype(np.float32)
+    y = rng.integers(0, 10, 64 * 4)
+    tde.backend.set_random_seed(7)
+    mf = _model(tde, tde.optimizers.SGD(0.02))
+    w0 = mf.get_weights()
+    hf = mf.fit(x, y, batch_size=64, epochs=1, shuffle=False, verbose=0)
+    assert mf._program("train", 64).plan_kind == "fused_convnet"
+    tde.backend.clear_session()
+    monkeypatch.setenv("TDE_EXECUTOR", "reference")
+    mr = tde.zoo.mnist_cnn()
+    mr.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True), optimizer=tde.optimizers.SGD(0.02),
+               metrics=["accuracy"])
+    mr.set_weights(w0)
+    hr = mr.fit(x, y, batch_size=64, epochs=1, shuffle=False, verbose=0)
+    for name, a, b, w in zip(mf.variable_names(), mf.get_weights(), mr.get_weights(), w0):
+        rel = np.linalg.norm((a - w) - (b - w)) / (np.linalg.norm(b - w) + 1e-12)
+        assert rel < 1e-4, (name, rel)
+    assert abs(hf.history["loss"][0] - hr.history["loss"][0]) < 1e-5

@@ -1,12 +1,13 @@
-"""T1/T4: the fused HIP training plan vs the torch reference plan, step by step,
-and hipGraph multi-step execution vs eager execution."""
+"""T1/T4: the fused HIP training plan (its bf16 form: mixed_bfloat16 policy) vs the torch reference
+plan, step by step, and hipGraph multi-step execution vs eager execution.  The float32 form is pinned
+against float64 oracles in test_fp32_gpu.py."""
 import copy
 
 import numpy as np
 import pytest
 import torch
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("bf16_policy")]
 
 
 def _data(n, seed=0):
