@@ -117,8 +117,7 @@ def main():
             stage(i + 1)
 
     def barrier():
-        if world > 1:
-            torch.distributed.barrier()
+        strategy.barrier()   # the native control plane (parallel/control.py); no-op at 1 worker
 
     # warm-up: at least W steps, at least 2 executions (the first replay follows the capture) and at
     # least TDE_BENCH_WARM_MS of back-to-back work.  A GPU that idled runs the next ~0.5 ms of work
@@ -138,9 +137,7 @@ def main():
     per_exec = max(time.perf_counter() - tw, 1e-6)
     n_warm = max(n_warm, 2 + math.ceil(warm_s / per_exec))
     if world > 1:
-        t = torch.tensor([n_warm], dtype=torch.int64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        n_warm = int(t.item())
+        n_warm = int(strategy.control.all_reduce_max(n_warm))
     if n_warm > 2:
         stage(2)
     for i in range(2, n_warm):
@@ -162,12 +159,10 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = strategy.control.all_reduce_max(elapsed)
     logs = tde.metrics.logs_from(prog.global_metrics(), ["accuracy"])
     comm = strategy.comm
-    ar = {"XgmiCommunicator": "xgmi", "RcclCommunicator": "rccl", "TorchDistCommunicator": "gloo"}.get(
+    ar = {"XgmiCommunicator": "xgmi", "RcclCommunicator": "rccl", "StoreCommunicator": "store"}.get(
         type(comm).__name__, "none")
     if world > 1:  # data-parallel invariant (outside the timed region): every replica bit-identical
         from tensorflow_distributed_example_amd.utils import debug

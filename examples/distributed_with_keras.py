@@ -92,3 +92,5 @@ if __name__ == "__main__":
     h = main()
     if strategy.is_chief:
         print("history:", {k: [round(v, 4) for v in vs] for k, vs in h.history.items()})
+    print(f"worker {strategy.worker_index}/{strategy.num_workers} done: {strategy.num_replicas_in_sync} replicas "
+          f"in sync, {len(h.history.get('loss', []))} epochs", flush=True)

@@ -5,8 +5,10 @@
                        GPUs per process, grouped init) or in-process
                        (ncclCommInitAll).  Collectives are enqueued on each device's
                        current stream and are hipGraph-capturable.
-``TorchDistCommunicator`` torch.distributed (gloo on CPU — the CPU plumbing
-                       config's collective path; also a GPU fallback).
+``StoreCommunicator``  CPU collectives over the native control-plane store
+                       (parallel/control.py; the CPU plumbing config's collective
+                       path across worker processes; also the fallback when no RCCL
+                       clique exists).
 ``LocalCommunicator``  several replicas in one process without RCCL (CPU).
 ``NullCommunicator``   a single replica.
 
@@ -89,45 +91,47 @@ def _combine(a, b, op):
     raise ValueError(op)
 
 
-class TorchDistCommunicator(Communicator):
-    """torch.distributed process group (one or more local replicas per process)."""
+class StoreCommunicator(Communicator):
+    """Collectives of one or more local replicas per process through the native control-plane store
+    (``parallel/control.ControlPlane``): every rank publishes its (locally reduced) tensor and reduces
+    all of them in rank order, so every rank ends with bit-identical results.  Host-staged: the CPU
+    plumbing path and the non-gradient collectives of GPU jobs that have no RCCL clique."""
 
-    def __init__(self, n_local, group=None):
-        import torch.distributed as dist
-        self.dist = dist
-        self.group = group
+    def __init__(self, control, n_local):
+        self.cp = control
         self.n_local = n_local
-        self.world_size = dist.get_world_size(group) * n_local
+        self.world_size = control.world * n_local
 
     def all_reduce_(self, tensors, op="sum"):
-        d = self.dist
         t0 = tensors[0]
-        if len(tensors) > 1:
-            acc = t0.clone()
-            for t in tensors[1:]:
-                acc = _combine(acc, t.to(acc.device), op)
-        else:
-            acc = t0
-        dop = {"sum": d.ReduceOp.SUM, "mean": d.ReduceOp.SUM, "max": d.ReduceOp.MAX, "min": d.ReduceOp.MIN,
-               "prod": d.ReduceOp.PRODUCT}[op]
-        d.all_reduce(acc, op=dop, group=self.group)
+        acc = t0.detach().clone()
+        for t in tensors[1:]:
+            acc = _combine(acc, t.to(acc.device), op)
+        host = acc.cpu()
+        wide = host.dtype in (torch.bfloat16, torch.float16)
+        arr = (host.float() if wide else host).numpy()
+        red = self.cp.all_reduce_array(arr, "sum" if op == "mean" else op)
+        out = torch.from_numpy(red)
         if op == "mean":
-            acc /= self.world_size
+            out = out / self.world_size
         for t in tensors:
-            if t is not acc:
-                t.copy_(acc.to(t.device))
+            t.copy_(out.to(device=t.device, dtype=t.dtype).view_as(t))
 
     def broadcast_(self, tensors, root=0):
-        d = self.dist
         src_rank, local = divmod(root, self.n_local)
-        t0 = tensors[local] if d.get_rank(self.group) == src_rank else tensors[0]
-        d.broadcast(t0, src=src_rank, group=self.group)
+        src = tensors[local] if self.cp.rank == src_rank else None
+        data = None
+        if src is not None:
+            data = src.detach().cpu().contiguous().view(torch.uint8).numpy().tobytes()
+        raw = self.cp.broadcast_bytes(data, src_rank)
+        t0 = tensors[0]
+        val = torch.frombuffer(bytearray(raw), dtype=torch.uint8).view(t0.dtype).view(t0.shape)
         for t in tensors:
-            if t is not t0:
-                t.copy_(t0.to(t.device))
+            if t is not src:
+                t.copy_(val.to(t.device))
 
     def barrier(self):
-        self.dist.barrier(group=self.group)
+        self.cp.barrier()
 
 
 class RcclError(RuntimeError):
@@ -250,22 +254,22 @@ class XgmiCommunicator(Communicator):
     larger than the window) goes to ``fallback`` (RCCL).  Stream-ordered and hipGraph-capturable:
     the call epoch lives on the device, so graph replays need no host bookkeeping.
 
-    ``control`` is the torch.distributed (gloo) group used once, to exchange the IPC handles.
+    ``control`` is the native control plane (parallel/control.py) that exchanges the IPC handles and
+    agrees on the setup outcome across ranks.
     """
 
     capturable = True
     plain_ok = True   # False: the fallback measured faster for a plain (unfused) gradient all-reduce
 
-    def __init__(self, device, rank, world, fallback, max_elems=None, uncached=None, nblocks=None,
-                 timeout_s=None, group=None):
-        import torch.distributed as dist
+    def __init__(self, device, rank, world, fallback, control, max_elems=None, uncached=None, nblocks=None,
+                 timeout_s=None):
         from .. import _native as N
         self.lib = N.hip()
         self.device = torch.device(device)
         self.rank, self.world = int(rank), int(world)
         self.world_size = self.world
         self.fallback = fallback
-        self.group = group
+        self.cp = control
         if self.world > self.lib.tde_xgmi_max_ranks():
             raise ValueError(f"xGMI all-reduce supports at most {self.lib.tde_xgmi_max_ranks()} ranks")
         self.max_elems = int(max_elems or os.environ.get("TDE_XGMI_MAX_ELEMS", 8 << 20))
@@ -282,8 +286,7 @@ class XgmiCommunicator(Communicator):
                                      C.byref(self.epoch), C.byref(self.err), hb)
         if os.environ.get("TDE_XGMI_FAIL_RANK") == str(self.rank):   # fault injection (tests)
             rc = -999
-        handles = [None] * self.world
-        dist.all_gather_object(handles, hb.raw if rc == 0 else None, group=group)
+        handles = [h if h else None for h in control.all_gather_bytes(hb.raw if rc == 0 else b"", "xgmi_handles")]
         if any(h is None for h in handles):
             self._free()
             raise RuntimeError(f"xGMI window allocation failed on rank(s) "
@@ -300,11 +303,10 @@ class XgmiCommunicator(Communicator):
                 break
             self._opened.append(m.value)
             peers.append(m.value)
-        oks = [None] * self.world
-        dist.all_gather_object(oks, err, group=group)
-        if any(o is not None for o in oks):
+        errs = control.agree(err, "xgmi_open")
+        if errs:
             self._free()
-            raise RuntimeError(f"xGMI peer mapping failed: {[o for o in oks if o]}")
+            raise RuntimeError(f"xGMI peer mapping failed: {errs}")
         self.peers = (C.c_void_p * self.world)(*peers)
 
     def nblocks(self, M):
@@ -403,14 +405,12 @@ class XgmiCommunicator(Communicator):
         return ok
 
 
-def _time_allreduce(comm, t, iters, group=None):
+def _time_allreduce(comm, t, iters, control):
     import time
-
-    import torch.distributed as dist
     for _ in range(3):
         comm.all_reduce_([t])
     torch.cuda.synchronize(t.device)
-    dist.barrier(group=group)
+    control.barrier()
     t0 = time.perf_counter()
     for _ in range(iters):
         comm.all_reduce_([t])
@@ -418,7 +418,7 @@ def _time_allreduce(comm, t, iters, group=None):
     return (time.perf_counter() - t0) / iters
 
 
-def maybe_xgmi(fallback, device, rank, world, bucket_hint=None, group=None):
+def maybe_xgmi(fallback, device, rank, world, control, bucket_hint=None):
     """Wrap ``fallback`` with the xGMI peer-memory all-reduce when every rank is one GPU of this node.
 
     ``TDE_ALLREDUCE`` = ``auto`` (default: self-test, then keep whichever of xGMI / RCCL is faster on
@@ -426,20 +426,16 @@ def maybe_xgmi(fallback, device, rank, world, bucket_hint=None, group=None):
     only) or ``rccl`` (never wrap)."""
     import socket
     import warnings
-
-    import torch.distributed as dist
     mode = os.environ.get("TDE_ALLREDUCE", "auto").lower()
     if mode == "rccl" or world < 2 or not torch.cuda.is_available():
         return fallback
-    me = (socket.gethostname(), _boot_id())
-    hosts = [None] * world
-    dist.all_gather_object(hosts, me, group=group)
+    hosts = control.all_gather_json([socket.gethostname(), _boot_id()], "hosts")
     if any(h != hosts[0] for h in hosts):
         return fallback   # multi-node: RCCL handles the inter-node path
     err = None
     xg = None
     try:
-        xg = XgmiCommunicator(device, rank, world, fallback, group=group)
+        xg = XgmiCommunicator(device, rank, world, fallback, control)
     except Exception as e:  # noqa: BLE001 - raised consistently on every rank; keeps RCCL
         xg, err = None, e
     ok = False
@@ -448,8 +444,7 @@ def maybe_xgmi(fallback, device, rank, world, bucket_hint=None, group=None):
             ok = xg.self_test()
         except Exception as e:  # noqa: BLE001
             ok, err = False, e
-    flags = [None] * world
-    dist.all_gather_object(flags, bool(ok), group=group)
+    flags = control.all_gather_json(bool(ok), "xgmi_selftest")
     if not all(flags):
         if xg is not None:
             xg.fallback = None
@@ -460,15 +455,14 @@ def maybe_xgmi(fallback, device, rank, world, bucket_hint=None, group=None):
     if mode == "auto":
         n = int(bucket_hint or 347_146)
         t = torch.zeros(min(n, xg.max_elems), device=device)
-        tx = _time_allreduce(xg, t, 20, group)
-        tr = _time_allreduce(fallback, t, 20, group)
+        tx = _time_allreduce(xg, t, 20, control)
+        tr = _time_allreduce(fallback, t, 20, control)
         # the xGMI kernel can also carry the optimizer update (one launch fewer per step, see
         # XgmiCommunicator.all_reduce_apply_): it keeps the bucket unless RCCL is faster by more than that
         # (the margin only applies to plans that fuse the update into it: Program re-decides the plain
         # all-reduce with plain_ok)
         margin = float(os.environ.get("TDE_XGMI_MARGIN_US", "3")) * 1e-6
-        dec = [tx <= tr + margin, tx <= tr]
-        dist.broadcast_object_list(dec, src=0, group=group)
+        dec = control.broadcast_json([tx <= tr + margin, tx <= tr], src=0, tag="xgmi_pick")
         xg.plain_ok = bool(dec[1])
         if rank == 0:
             import sys

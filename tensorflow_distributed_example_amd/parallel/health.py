@@ -23,8 +23,9 @@ EXIT_PEER_FAILURE = 75
 
 
 class HealthMonitor:
-    def __init__(self, rank, world, comm=None, timeout=None, interval=None, on_failure=None):
+    def __init__(self, rank, world, comm=None, timeout=None, interval=None, on_failure=None, control=None):
         self.rank, self.world, self.comm = rank, world, comm
+        self.control = control
         self.timeout = float(timeout if timeout is not None else os.environ.get("TDE_HEARTBEAT_TIMEOUT", 60))
         self.interval = float(interval if interval is not None else os.environ.get("TDE_HEARTBEAT_INTERVAL", 0.5))
         self.on_failure = on_failure or self._default_failure
@@ -36,22 +37,18 @@ class HealthMonitor:
 
     # ------------------------------------------------------------------ bootstrap
     def start(self):
-        import torch.distributed as dist
-
         from .store import TCPStore, TCPStoreServer
-        addr = [None]
-        if self.rank == 0:
+        if self.control is not None:
+            # the job's control-plane store (hosted by the chief) also keeps the heartbeats
+            host, port = self.control.host, self.control.port
+        else:
             self.server = TCPStoreServer("0.0.0.0", 0)
-            host = os.environ.get("MASTER_ADDR", "127.0.0.1")
-            addr = [(host if host not in ("localhost",) else "127.0.0.1", self.server.port)]
-        if dist.is_initialized():
-            dist.broadcast_object_list(addr, src=0)
-        host, port = addr[0]
+            host, port = "127.0.0.1", self.server.port
         self.store = TCPStore(host, port, timeout=max(self.timeout, 10.0))
         self._beat_store = TCPStore(host, port, timeout=max(self.timeout, 10.0))
         self._beat()
-        if dist.is_initialized():
-            dist.barrier()
+        if self.control is not None:
+            self.control.barrier("health")
         for fn in (self._heartbeat_loop, self._watch_loop):
             t = threading.Thread(target=fn, daemon=True, name=f"tde-health-{fn.__name__}")
             t.start()
@@ -113,7 +110,7 @@ class HealthMonitor:
         self._stop.set()
 
 
-def maybe_start(rank, world, comm):
+def maybe_start(rank, world, comm, control=None):
     if world <= 1 or os.environ.get("TDE_HEARTBEAT", "1") == "0":
         return None
-    return HealthMonitor(rank, world, comm).start()
+    return HealthMonitor(rank, world, comm, control=control).start()

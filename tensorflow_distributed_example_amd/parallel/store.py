@@ -88,7 +88,9 @@ class TCPStore:
             raise StoreError("set failed")
 
     def get(self, key: str, timeout=60.0) -> bytes:
-        cap = 1 << 16
+        # the value is fetched whole into a buffer of the last size seen (large control-plane values,
+        # e.g. CPU all-reduce parts, repeat their size: one round trip each)
+        cap = getattr(self, "_cap", 1 << 16)
         while True:
             buf = C.create_string_buffer(cap)
             n = self._lib.tde_store_get(self._h, key.encode(), buf, cap, int(timeout * 1000) if timeout else -1)
@@ -98,7 +100,7 @@ class TCPStore:
                 raise StoreError("get failed")
             if n <= cap:
                 return buf.raw[:n]
-            cap = n
+            cap = self._cap = n
 
     def wait(self, key: str, timeout=60.0):
         rc = self._lib.tde_store_wait(self._h, key.encode(), int(timeout * 1000))

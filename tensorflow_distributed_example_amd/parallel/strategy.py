@@ -5,11 +5,12 @@
   with it).  In-process RCCL clique (ncclCommInitAll) over xGMI.
 * ``MultiWorkerMirroredStrategy()`` — synchronous DP over worker processes
   (distributed_with_keras.py:16).  Reads TF_CONFIG (or torchrun env) at
-  construction, bootstraps a control-plane process group, distributes the RCCL
-  unique id from the chief and builds one clique over ALL replicas of ALL
-  workers (``TDE_GPUS_PER_WORKER`` GPUs per process; default 1 = one process per
-  GPU, the MI355X-preferred layout).  Initial variables are broadcast from
-  replica 0 (C1).
+  construction, starts the native control plane (the chief hosts the C++ TCP store
+  at its cluster address: parallel/control.py), distributes the RCCL unique id from
+  the chief through it and builds one clique over ALL replicas of ALL workers
+  (``TDE_GPUS_PER_WORKER`` GPUs per process; default 1 = one process per GPU, the
+  MI355X-preferred layout).  Initial variables are broadcast from replica 0 (C1).
+  torch.distributed is not used.
 * the default strategy — one replica on the default device.
 
 Replicated variables (MirroredVariable) are realised as one flat ParamStore per
@@ -97,6 +98,8 @@ class _Extended:
 
 
 class Strategy:
+    control = None   # the native control plane of a multi-worker strategy (parallel/control.py)
+
     def __init__(self, local_devices, communicator, num_workers=1, worker_index=0, name=None):
         self.local_devices = [torch.device(d) for d in local_devices]
         self.comm = communicator
@@ -120,6 +123,9 @@ class Strategy:
     @property
     def is_chief(self):
         return self.worker_index == 0
+
+    def barrier(self):
+        """All workers of the strategy (a no-op for one process)."""
 
     # ------------------------------------------------------------------ scope
     @contextlib.contextmanager
@@ -230,24 +236,6 @@ class OneDeviceStrategy(Strategy):
         super().__init__(_parse_devices([device]), CM.NullCommunicator(), name="OneDeviceStrategy")
 
 
-_pg_initialized = False
-
-
-def _init_control_plane(topo, timeout_s=300):
-    """torch.distributed gloo group = control plane (barriers, id exchange, CPU all-reduce)."""
-    global _pg_initialized
-    import datetime
-
-    import torch.distributed as dist
-    if dist.is_initialized():
-        _pg_initialized = True
-        return
-    init = f"tcp://{topo.master_addr}:{topo.master_port}"
-    dist.init_process_group("gloo", init_method=init, rank=topo.rank, world_size=topo.world,
-                            timeout=datetime.timedelta(seconds=timeout_s))
-    _pg_initialized = True
-
-
 class MultiWorkerMirroredStrategy(Strategy):
     """Synchronous DP across worker processes; must be created first (DWK:16)."""
 
@@ -273,61 +261,60 @@ class MultiWorkerMirroredStrategy(Strategy):
             devs = [torch.device("cpu")]
         n_local = len(devs)
         world = topo.world
+        self.control = None
         if world > 1:
-            _init_control_plane(topo)
+            from . import control as CP
+            self.control = CP.ControlPlane.for_topology(topo)
+            CP.set_current(self.control)
         impl = communication if isinstance(communication, CommunicationImplementation) else \
             CommunicationImplementation(str(communication))
         if world * n_local == 1:
             comm = CM.NullCommunicator()
         elif use_gpu and impl in (CommunicationImplementation.AUTO, CommunicationImplementation.NCCL):
-            comm = self._rccl(devs, topo, world, n_local)
+            comm = self._rccl(devs, topo, world, n_local, self.control)
         elif world > 1:
-            comm = CM.TorchDistCommunicator(n_local)
+            comm = CM.StoreCommunicator(self.control, n_local)
         else:
             comm = CM.LocalCommunicator(n_local) if not use_gpu else CM.RcclCommunicator(devs)
         super().__init__(devs, comm, num_workers=world, worker_index=topo.rank, name="MultiWorkerMirroredStrategy")
         self.cluster_resolver = cluster_resolver or CL.TFConfigClusterResolver()
         # peer failure detection: heartbeats to the chief's native store + watchdog
         from . import health
-        self.health = health.maybe_start(topo.rank, world, comm)
+        self.health = health.maybe_start(topo.rank, world, comm, self.control)
 
     @staticmethod
-    def _rccl(devs, topo, world, n_local):
+    def _rccl(devs, topo, world, n_local, control):
         if world == 1:
             return CM.RcclCommunicator(devs)
         if os.environ.get("TDE_RCCL", "1") == "0":
-            # no RCCL clique (e.g. several ranks sharing one GPU in a rehearsal): gloo carries the
-            # non-gradient collectives, the xGMI kernel the gradient bucket
-            base = CM.TorchDistCommunicator(n_local)
+            # no RCCL clique (e.g. several ranks sharing one GPU in a rehearsal): the control-plane store
+            # carries the non-gradient collectives, the xGMI kernel the gradient bucket
+            base = CM.StoreCommunicator(control, n_local)
         else:
             import sys
-            import torch.distributed as dist
-            obj = [CM.RcclCommunicator.unique_id() if topo.rank == 0 else None]
-            dist.broadcast_object_list(obj, src=0)
+            # the chief's ncclUniqueId travels through the native store
+            uid = control.broadcast_bytes(CM.RcclCommunicator.unique_id() if topo.rank == 0 else None, 0,
+                                          "rccl_uid")
             base, err = None, None
             try:
-                base = CM.RcclCommunicator(devs, rank0=topo.rank * n_local, nranks=world * n_local,
-                                           unique_id=obj[0])
+                base = CM.RcclCommunicator(devs, rank0=topo.rank * n_local, nranks=world * n_local, unique_id=uid)
             except Exception as e:  # keep every rank on the same backend: agree before using it
                 err = f"rank {topo.rank}: {e}"
-            errs = [None] * world
-            dist.all_gather_object(errs, err)
-            errs = [e for e in errs if e]
+            errs = control.agree(err, "rccl_init")
             if errs:
                 if base is not None:
                     base.abort()
                 print(f"[tde] RCCL communicator init failed ({'; '.join(errs)}); collectives fall back to "
-                      "gloo", file=sys.stderr, flush=True)
-                base = CM.TorchDistCommunicator(n_local)
+                      "the control-plane store", file=sys.stderr, flush=True)
+                base = CM.StoreCommunicator(control, n_local)
         if n_local == 1:
             # one GPU per process on one xGMI node: the gradient bucket takes the peer-memory kernel
-            return CM.maybe_xgmi(base, devs[0], topo.rank, world)
+            return CM.maybe_xgmi(base, devs[0], topo.rank, world, control)
         return base
 
     def barrier(self):
         if self.num_workers > 1:
-            import torch.distributed as dist
-            dist.barrier()
+            self.control.barrier()
 
 
 class _Experimental:

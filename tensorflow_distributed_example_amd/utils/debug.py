@@ -51,9 +51,7 @@ def replica_fingerprints(model) -> list:
     local = [(_fold(s.w), _fold(s.state)) for s in stores]
     if st is None or st.num_workers == 1:
         return [(0, i, w, b) for i, (w, b) in enumerate(local)]
-    import torch.distributed as dist
-    allv = [None] * st.num_workers
-    dist.all_gather_object(allv, local)
+    allv = st.control.all_gather_json(local, "fingerprints")
     return [(r, i, w, b) for r, lst in enumerate(allv) for i, (w, b) in enumerate(lst)]
 
 

@@ -1,6 +1,7 @@
 """T3/T4 on CPU: MirroredStrategy (in-process replicas) and
-MultiWorkerMirroredStrategy (2 processes, gloo) — the DP invariants:
-replicas stay identical, and R replicas at global batch G match 1 replica at G."""
+MultiWorkerMirroredStrategy (2 processes over the native control plane: the chief's C++ TCP store,
+torch.distributed never initialised) — the DP invariants: replicas stay identical, and R replicas at
+global batch G match 1 replica at G."""
 import json
 import os
 import socket
@@ -77,11 +78,14 @@ WORKER = textwrap.dedent("""
     out = {{"rank": strategy.worker_index, "replicas": strategy.num_replicas_in_sync,
            "loss": h.history["loss"][0], "w": [float(np.abs(a).sum()) for a in m.get_weights()]}}
     np.savez({outp!r} + str(strategy.worker_index) + ".npz", *m.get_weights())
+    import torch.distributed as dist
+    out["torch_dist"] = dist.is_initialized()
+    out["comm"] = type(strategy.comm).__name__
     print("RESULT" + json.dumps(out), flush=True)
 """)
 
 
-def test_multi_worker_mirrored_gloo_two_processes(tmp_path):
+def test_multi_worker_mirrored_native_control_plane_two_processes(tmp_path):
     x, y = _data()
     w0 = tde.zoo.mnist_cnn().get_weights()
     np.savez(tmp_path / "w0.npz", *w0)
@@ -100,6 +104,7 @@ def test_multi_worker_mirrored_gloo_two_processes(tmp_path):
         assert p.returncode == 0, o
         outs.append(json.loads(o.split("RESULT")[1].strip()))
     assert outs[0]["replicas"] == 2
+    assert not any(o["torch_dist"] for o in outs) and all(o["comm"] == "StoreCommunicator" for o in outs)
     wa = np.load(tmp_path / "out0.npz")
     wb = np.load(tmp_path / "out1.npz")
     for k in wa.files:
@@ -163,3 +168,46 @@ def test_reverse_order_gradient_buckets_cover_bucket_exactly():
                                                    for n in inside)
     # one bucket when the target exceeds the model
     assert plan_grad_buckets(stage_params, segs, total, total + 1) == [(len(stage_params) - 1, 0, total)]
+
+
+AGREE = textwrap.dedent("""
+    import json, os, sys
+    sys.path.insert(0, {root!r})
+    from tensorflow_distributed_example_amd.parallel import cluster as CL, control as CP
+    cp = CP.ControlPlane.for_topology(CL.worker_topology(), timeout=60)
+    fail = os.environ.get("FAIL_RANK") == str(cp.rank)
+    errs = cp.agree("rank %d: injected setup failure" % cp.rank if fail else None)
+    uid = cp.broadcast_bytes(b"\\x01uid-bytes" if cp.rank == 0 else None)
+    got = cp.all_gather_bytes(bytes([cp.rank]) * 3)
+    s = cp.all_reduce_array(__import__("numpy").full(5, cp.rank + 1.0))
+    cp.barrier()
+    import torch.distributed as dist
+    print("RESULT" + json.dumps({{"errs": errs, "uid": uid.hex(), "got": [g.hex() for g in got],
+                                  "sum": s.tolist(), "keys": cp.store.num_keys(), "dist": dist.is_initialized()}}),
+          flush=True)
+    cp.shutdown()
+""")
+
+
+def test_native_control_plane_agreement_two_processes():
+    """The MWMS control plane (parallel/control.py) over the chief's native store: a failure injected on ONE
+    rank is seen by every rank (the rank-agreed fallback), the chief's broadcast (the ncclUniqueId path),
+    all-gather and rank-ordered host reductions, and no torch.distributed group anywhere."""
+    port = _free_port()
+    cluster = {"worker": [f"127.0.0.1:{port}", f"127.0.0.1:{_free_port()}"]}
+    script = AGREE.format(root=ROOT)
+    procs = []
+    for i in range(2):
+        env = dict(os.environ, TF_CONFIG=json.dumps({"cluster": cluster, "task": {"type": "worker", "index": i}}),
+                   FAIL_RANK="1", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+        procs.append(subprocess.Popen([sys.executable, "-c", script], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        o, _ = p.communicate(timeout=120)
+        assert p.returncode == 0, o
+        outs.append(json.loads(o.split("RESULT")[1].strip()))
+    for o in outs:
+        assert o["errs"] == ["rank 1: injected setup failure"], o
+        assert bytes.fromhex(o["uid"]) == b"\x01uid-bytes" and o["got"] == ["000000", "010101"], o
+        assert o["sum"] == [3.0] * 5 and not o["dist"], o

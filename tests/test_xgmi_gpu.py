@@ -30,13 +30,13 @@ def _free_port():
 WORKER = r"""
 import json, os, sys
 sys.path.insert(0, {root!r})
-import torch, torch.distributed as dist
-from tensorflow_distributed_example_amd.parallel import comm as CM
+import torch
+from tensorflow_distributed_example_amd.parallel import comm as CM, control as CP
 rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
 torch.cuda.set_device(0)
-dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-fb = CM.TorchDistCommunicator(1)
-xg = CM.XgmiCommunicator("cuda:0", rank, world, fb, max_elems=1 << 20, timeout_s=30)
+cp = CP.ControlPlane(rank, world, "127.0.0.1", {port}, timeout=120)
+fb = CM.StoreCommunicator(cp, 1)
+xg = CM.XgmiCommunicator("cuda:0", rank, world, fb, cp, max_elems=1 << 20, timeout_s=30)
 out = {{"self_test": xg.self_test()}}
 bad = []
 g = torch.Generator(device="cpu")
@@ -64,7 +64,7 @@ with torch.cuda.stream(s):
     xg.all_reduce_([buf])      # warm-up outside capture
 torch.cuda.current_stream().wait_stream(s)
 torch.cuda.synchronize()
-dist.barrier()
+cp.barrier()
 graph = torch.cuda.CUDAGraph()
 with torch.cuda.graph(graph):
     for k in range(5):
@@ -78,7 +78,7 @@ for rep in range(3):
     base = [torch.rand(n) for _ in range(world)]
     src.copy_(base[rank].cuda())
     torch.cuda.synchronize()
-    dist.barrier()
+    cp.barrier()
     graph.replay()
     torch.cuda.synchronize()
     # reference: x_r <- sum_r(x_r * (k+1)) five times, all ranks identical after the first
@@ -94,9 +94,10 @@ for rep in range(3):
 out["graph_bad"] = gbad
 out["calls"] = xg.calls()
 out["err"] = int(xg.lib.tde_xgmi_error(xg.err))
-dist.barrier()
+cp.barrier()
 xg.close()
 print("RESULT" + json.dumps(out), flush=True)
+cp.shutdown()
 """
 
 
@@ -145,17 +146,18 @@ def test_mwms_bench_two_ranks_on_xgmi(tmp_path):
 FALLBACK = r"""
 import json, os, sys
 sys.path.insert(0, {root!r})
-import torch, torch.distributed as dist
-from tensorflow_distributed_example_amd.parallel import comm as CM
+import torch
+from tensorflow_distributed_example_amd.parallel import comm as CM, control as CP
 rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
 torch.cuda.set_device(0)
-dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-fb = CM.TorchDistCommunicator(1)
-c = CM.maybe_xgmi(fb, torch.device("cuda:0"), rank, world)
+cp = CP.ControlPlane(rank, world, "127.0.0.1", {port}, timeout=120)
+fb = CM.StoreCommunicator(cp, 1)
+c = CM.maybe_xgmi(fb, torch.device("cuda:0"), rank, world, cp)
 t = torch.full((1000,), float(rank + 1), device="cuda")
 c.all_reduce_([t])
 torch.cuda.synchronize()
 print("RESULT" + json.dumps({{"kind": type(c).__name__, "sum": float(t[0])}}), flush=True)
+cp.shutdown()
 """
 
 
@@ -173,7 +175,7 @@ def test_xgmi_setup_failure_on_one_rank_falls_back_everywhere():
         o, _ = p.communicate(timeout=180)
         assert p.returncode == 0, o[-3000:]
         res = json.loads(o.split("RESULT")[1].strip())
-        assert res["kind"] == "TorchDistCommunicator" and res["sum"] == 3.0, res
+        assert res["kind"] == "StoreCommunicator" and res["sum"] == 3.0, res
 
 
 def test_bucketed_overlapped_allreduce_two_ranks():
@@ -200,7 +202,8 @@ def test_bucketed_overlapped_allreduce_two_ranks():
 
 def test_rccl_init_failure_falls_back_on_every_rank():
     """Two ranks on one GPU make ncclCommInitRank fail on both (duplicate GPU): the strategy agrees on
-    the failure, keeps gloo for the control collectives and the xGMI kernel for the gradient bucket."""
+    the failure (through the native control plane), keeps the store for the control collectives and the
+    xGMI kernel for the gradient bucket."""
     env = dict(os.environ, TDE_ALLREDUCE="xgmi", TDE_HEARTBEAT="0", OMP_NUM_THREADS="2", TDE_BENCH_WARM_MS="0")
     env.pop("TDE_RCCL", None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
@@ -218,14 +221,14 @@ def test_rccl_init_failure_falls_back_on_every_rank():
 APPLY = r"""
 import json, os, sys
 sys.path.insert(0, {root!r})
-import torch, torch.distributed as dist
-from tensorflow_distributed_example_amd.parallel import comm as CM
+import torch
+from tensorflow_distributed_example_amd.parallel import comm as CM, control as CP
 from tensorflow_distributed_example_amd.ops import kernels as K
 from tensorflow_distributed_example_amd import optimizers as O
 rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
 torch.cuda.set_device(0)
-dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-xg = CM.XgmiCommunicator("cuda:0", rank, world, CM.TorchDistCommunicator(1), max_elems=1 << 20, timeout_s=30)
+cp = CP.ControlPlane(rank, world, "127.0.0.1", {port}, timeout=120)
+xg = CM.XgmiCommunicator("cuda:0", rank, world, CM.StoreCommunicator(cp, 1), cp, max_elems=1 << 20, timeout_s=30)
 out = {{}}
 n, lo, rows, cols = 347146 + 58, 64, 5408, 64
 opts = {{"sgd": O.SGD(0.05), "momentum": O.SGD(0.05, momentum=0.9),
@@ -265,14 +268,14 @@ for name, opt in opts.items():
     if v is not None:
         res["v_max"] = float((v - rv).abs().max())
     # every rank must hold bit-identical weights
-    allw = [torch.zeros_like(w).cpu() for _ in range(world)]
-    dist.all_gather(allw, w.cpu())
-    res["identical"] = all(torch.equal(allw[0], q) for q in allw[1:])
+    allw = cp.all_gather_bytes(w.cpu().numpy().tobytes())
+    res["identical"] = all(q == allw[0] for q in allw[1:])
     out[name] = res
 out["err"] = int(xg.lib.tde_xgmi_error(xg.err))
-dist.barrier()
+cp.barrier()
 xg.close()
 print("RESULT" + json.dumps(out), flush=True)
+cp.shutdown()
 """
 
 
