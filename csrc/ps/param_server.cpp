@@ -38,8 +38,9 @@ struct PSServer {
   std::atomic<int64_t> step{0};          // counter 0: global_step
   std::atomic<int64_t> counters[3]{};     // counters 1..3: tickets etc.
   std::atomic<int64_t> pushes{0}, pulls{0};
-  int kind = 0;  // 0 sgd, 1 momentum, 2 nesterov
-  float momentum = 0.f;
+  // set by a kSetOpt request on one connection's thread, read by every push handler
+  std::atomic<int> kind{0};  // 0 sgd, 1 momentum, 2 nesterov
+  std::atomic<float> momentum{0.f};
   std::thread acceptor;
   std::mutex cmu;
   std::set<int> clients;
@@ -51,17 +52,28 @@ struct PSServer {
     return it == vars.end() ? nullptr : it->second.get();
   }
 
-  void apply(Var* v, const float* g, size_t n, float lr) {
+  // Wire payloads sit at arbitrary byte offsets of the request frame: floats are read with memcpy
+  // (an unaligned float load is undefined behaviour; found by the UBSan stress run).
+  static float wire_f32(const char* p, size_t i) {
+    float v;
+    memcpy(&v, p + 4 * i, 4);
+    return v;
+  }
+
+  void apply(Var* v, const char* g, size_t n, float lr) {
+    const int k = kind.load();
+    const float mom = momentum.load();
     std::lock_guard<std::mutex> lk(v->mu);
     if (n != v->w.size()) return;
-    if (kind == 0) {
-      for (size_t i = 0; i < n; ++i) v->w[i] -= lr * g[i];
+    if (k == 0) {
+      for (size_t i = 0; i < n; ++i) v->w[i] -= lr * wire_f32(g, i);
     } else {
       if (v->slot.size() != n) v->slot.assign(n, 0.f);
       for (size_t i = 0; i < n; ++i) {
-        const float nv = momentum * v->slot[i] - lr * g[i];
+        const float gi = wire_f32(g, i);
+        const float nv = mom * v->slot[i] - lr * gi;
         v->slot[i] = nv;
-        v->w[i] += (kind == 2) ? momentum * nv - lr * g[i] : nv;
+        v->w[i] += (k == 2) ? mom * nv - lr * gi : nv;
       }
     }
     v->version++;
@@ -124,7 +136,7 @@ struct PSServer {
               w.s[0] = 2;
               continue;
             }
-            apply(v, (const float*)g, nb / 4, lr);
+            apply(v, g, nb / 4, lr);
           }
           pushes++;
           break;
@@ -136,14 +148,14 @@ struct PSServer {
           for (uint32_t i = 0; i < k && r.ok; ++i) {
             std::string name = r.str();
             uint32_t nb = 0;
-            const float* val = (const float*)r.view(&nb);
+            const char* val = r.view(&nb);
             Var* v = find(name);
             if (!v || !val || nb / 4 != v->w.size()) {
               w.s[0] = 2;
               continue;
             }
             std::lock_guard<std::mutex> lk(v->mu);
-            for (size_t j = 0; j < v->w.size(); ++j) v->w[j] = v->w[j] * m + val[j] * (1.f - m);
+            for (size_t j = 0; j < v->w.size(); ++j) v->w[j] = v->w[j] * m + wire_f32(val, j) * (1.f - m);
             v->version++;
           }
           break;
@@ -188,8 +200,8 @@ struct PSServer {
           break;
         }
         case kSetOpt: {
-          kind = (int)r.u32();
-          momentum = r.f32();
+          kind.store((int)r.u32());
+          momentum.store(r.f32());
           w.u8(0);
           break;
         }

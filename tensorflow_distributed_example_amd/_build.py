@@ -79,10 +79,10 @@ def _compile_hip(src: Path, force: bool) -> Path:
     return obj
 
 
-def _compile_host(src: Path, force: bool, extra=(), objdir: Path | None = None) -> Path:
+def _compile_host(src: Path, force: bool, extra=(), objdir: Path | None = None, cxx="g++") -> Path:
     obj = (objdir or OBJDIR) / (src.parent.name + "_" + src.stem + ".host.o")
     if force or _deps_newer(obj, [src]):
-        cmd = ["g++", "-O2", "-fPIC", "-std=c++17", "-Wall", "-I", str(CSRC / "include"),
+        cmd = [cxx, "-O2", "-fPIC", "-std=c++17", "-Wall", "-I", str(CSRC / "include"),
                *extra, "-c", str(src), "-o", str(obj)]
         _run(cmd)
     return obj
@@ -115,6 +115,35 @@ def build_host(force=False, jobs=8, sanitize: str | None = None) -> Path:
         objs = list(ex.map(lambda s: _compile_host(s, force, extra, objdir), srcs))
     if force or _deps_newer(out, objs):
         _run(["g++", "-shared", "-fPIC", *map(str, objs), "-o", str(out), "-lpthread", *extra])
+    return out
+
+
+SANITIZERS = {"address": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
+              "thread": ["-fsanitize=thread"]}
+
+
+def _sanitizer_cxx():
+    # ROCm's LLVM ships the compiler-rt ASan / UBSan / TSan runtimes; its TSan also intercepts
+    # pthread_cond_clockwait (libstdc++'s steady-clock waits), which gcc 11's libtsan misses
+    # (false "double lock" reports on every timed condition-variable wait)
+    c = os.path.join(_rocm(), "lib", "llvm", "bin", "clang++")
+    return c if os.path.exists(c) else "g++"
+
+
+def build_host_stress(sanitize: str, force=False, jobs=8) -> Path:
+    """The host-runtime stress driver (csrc/tests/host_stress.cpp) linked with every host source under
+    ``-fsanitize=<address|thread>``: an executable, so no sanitizer runtime has to be
+    preloaded into a Python process."""
+    flags = SANITIZERS[sanitize] + ["-g", "-O1", "-fno-omit-frame-pointer"]
+    cxx = _sanitizer_cxx()
+    objdir = OBJDIR / f"stress_{sanitize}"
+    objdir.mkdir(parents=True, exist_ok=True)
+    srcs = _host_sources() + [CSRC / "tests" / "host_stress.cpp"]
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: _compile_host(s, force, flags, objdir, cxx), srcs))
+    out = objdir / "host_stress"
+    if force or _deps_newer(out, objs):
+        _run([cxx, *flags, *map(str, objs), "-o", str(out), "-lpthread"])
     return out
 
 
