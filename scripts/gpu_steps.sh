@@ -31,6 +31,7 @@ prof() {  # name timeout cmd... : rocprofv3 kernel statistics of a command
 for s in "$@"; do
   case "$s" in
     t_fp32) step t_fp32 300 $PYT tests/test_fp32_gpu.py ;;
+    t_bncnn) step t_bncnn 300 $PYT tests/test_bncnn_gpu.py ;;
     t_convnet) step t_convnet 400 $PYT tests/test_kernels_gpu.py tests/test_plan_gpu.py ;;
     t_all) step t_all 1000 $PYT tests -m gpu ;;
     t_xgmi) step t_xgmi 400 $PYT tests/test_xgmi_gpu.py ;;

@@ -534,6 +534,11 @@ def make_plan(model, store, device, batch, global_batch, optimizer, loss, prefer
         pat = match_convnet(model, loss)
         if pat is not None and prefer in (None, "fused"):
             return ConvNetPlan(model, store, device, batch, global_batch, optimizer, loss, pat)
+        if prefer in (None, "fused", "bncnn"):
+            from . import bncnn
+            plan = bncnn.try_make(model, store, device, batch, global_batch, optimizer, loss)
+            if plan is not None:
+                return plan
         if prefer in (None, "fused", "smallnet"):
             from . import smallnet
             plan = smallnet.try_make(model, store, device, batch, global_batch, optimizer, loss)

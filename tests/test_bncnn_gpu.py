@@ -1,0 +1,205 @@
+"""Model B (mnist_keras_distributed.py:79-109) on the fused float32 BN-CNN plan (csrc/kernels/bncnn.hip)
+vs float64 autograd oracles: every gradient <= 1e-5 relative (norm-wise), BN moving statistics, the
+loss / accuracy metrics, evaluation with moving statistics and prediction.
+
+The oracle takes each ReLU decision from the plan's own f32 pre-activations (its stored raw conv /
+dense outputs and saved batch statistics): a pre-activation within one f32 ulp of zero may be decided
+differently in f64, and a flipped ReLU moves a whole gradient element; everything else is f64."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("fp32_policy")]
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def _model_b(tde, rate=0.0, opt=None):
+    L = tde.layers if hasattr(tde, "layers") else tde.keras.layers
+    m = tde.Sequential([
+        L.Reshape(input_shape=(28 * 28,), target_shape=(28, 28, 1)),
+        L.Conv2D(filters=6, kernel_size=3, padding="same", use_bias=False),
+        L.BatchNormalization(scale=False, center=True),
+        L.Activation("relu"),
+        L.Conv2D(filters=12, kernel_size=6, padding="same", use_bias=False, strides=2),
+        L.BatchNormalization(scale=False, center=True),
+        L.Activation("relu"),
+        L.Conv2D(filters=24, kernel_size=6, padding="same", use_bias=False, strides=2),
+        L.BatchNormalization(scale=False, center=True),
+        L.Activation("relu"),
+        L.Flatten(),
+        L.Dense(200, use_bias=False),
+        L.BatchNormalization(scale=False, center=True),
+        L.Activation("relu"),
+        L.Dropout(rate),
+        L.Dense(10, activation="softmax"),
+    ])
+    m.compile(loss="sparse_categorical_crossentropy", optimizer=opt or tde.optimizers.SGD(0.01), metrics=["accuracy"])
+    m.build()
+    # non-trivial BN betas / moving statistics
+    g = torch.Generator(device="cpu").manual_seed(3)
+    for n in m._store.names():
+        if n.endswith("/beta"):
+            v = m._store.view(n)
+            v.copy_((torch.rand(v.shape, generator=g) - 0.5).to(v.device) * 0.2)
+    return m
+
+
+def _data(B, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.rand(B, 784, generator=g).to(DEV)
+    y = torch.randint(0, 10, (B,), generator=g).int().to(DEV)
+    return x, y
+
+
+def _oracle(plan, x, y, B):
+    """float64 autograd of the plan's model at the store's weights; ReLU decisions from the plan's f32
+    pre-activations (after plan.train_step).  Returns ({var: grad}, {moving var: new value}, loss)."""
+    st = plan.store
+    dd = torch.float64
+    W = {n: st.view(n).detach().to(dd).clone().requires_grad_(st.segments[n].trainable) for n in st.order}
+    a = x[:B].to(dd).view(B, 28, 28, 1)
+    moving = {}
+    for blk in plan.blocks:
+        conv, bn = blk["conv"], blk["bn"]
+        (pt, pb), (pl, pr) = conv.pads(conv.input_shape)
+        z = F.conv2d(F.pad(a.permute(0, 3, 1, 2), (pl, pr, pt, pb)), W[f"{conv.name}/kernel"].permute(3, 2, 0, 1),
+                     stride=conv.strides).permute(0, 2, 3, 1)
+        mean, var = z.mean((0, 1, 2)), z.var((0, 1, 2), unbiased=False)
+        pre = (z - mean) / torch.sqrt(var + bn.epsilon) + W[f"{bn.name}/beta"]
+        g = blk["geo"]
+        z32 = blk["z"][: B * g.Ho * g.Wo * g.Co].view(B, g.Ho, g.Wo, g.Co)
+        s = blk["saved"]
+        mask = ((z32 - s[: g.Co]) * s[g.Co:] + st.view(f"{bn.name}/beta")) > 0
+        a = pre * mask
+        R = B * g.Ho * g.Wo
+        moving[f"{bn.name}/moving_mean"] = W[f"{bn.name}/moving_mean"] * bn.momentum + mean.detach() * (1 - bn.momentum)
+        moving[f"{bn.name}/moving_variance"] = (W[f"{bn.name}/moving_variance"] * bn.momentum
+                                                + var.detach() * R / (R - 1) * (1 - bn.momentum))
+    h = a.reshape(B, -1) @ W[f"{plan.dense.name}/kernel"]
+    bnl = plan.bnd["layer"]
+    mean, var = h.mean(0), h.var(0, unbiased=False)
+    pre = (h - mean) / torch.sqrt(var + bnl.epsilon) + W[f"{bnl.name}/beta"]
+    h32 = plan.h[: B * plan.Dp].view(B, plan.Dp)[:, : plan.D]
+    sv = plan.bnd["saved"]
+    mask = ((h32 - sv[: plan.D]) * sv[plan.D:] + st.view(f"{bnl.name}/beta")) > 0
+    a = pre * mask
+    moving[f"{bnl.name}/moving_mean"] = W[f"{bnl.name}/moving_mean"] * bnl.momentum + mean.detach() * (1 - bnl.momentum)
+    moving[f"{bnl.name}/moving_variance"] = W[f"{bnl.name}/moving_variance"] * bnl.momentum + var.detach() * (
+        1 - bnl.momentum)
+    logits = a @ W[f"{plan.head.name}/kernel"] + W[f"{plan.head.name}/bias"]
+    loss = F.cross_entropy(logits, y[:B].long(), reduction="sum") * plan.scale
+    loss.backward()
+    return {n: W[n].grad for n in st.names(trainable=True)}, moving, loss.item() / plan.scale / B, logits.detach()
+
+
+@pytest.mark.parametrize("B", [128, 50])
+def test_bncnn_step_gradients_match_float64(B):
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.train import program as PG
+    m = _model_b(tde)
+    st = m._store
+    plan = PG.make_plan(m, st, DEV, 128, 128, m.optimizer, m.loss)
+    assert plan.kind == "fused_bncnn" and plan.compute_dtype == "fp32"
+    before = {n: st.view(n).detach().double().clone() for n in st.order}
+    x, y = _data(128, 11)
+    plan.train_step(x, y, B)
+    torch.cuda.synchronize()
+    # the oracle from the pre-step weights / moving statistics
+    after = {n: st.view(n).detach().clone() for n in st.order}
+    for n in st.order:
+        st.view(n).copy_(before[n])
+    grads, moving, loss, _ = _oracle(plan, x, y, B)
+    for n in st.order:
+        st.view(n).copy_(after[n])
+    for n, gr in grads.items():
+        assert _rel(st.grad(n), gr) < 1e-5, (n, _rel(st.grad(n), gr))
+    for n, v in moving.items():
+        assert _rel(st.view(n), v) < 1e-6, (n, _rel(st.view(n), v))
+    met = plan.metrics.double().cpu()
+    assert met[2].item() == B and abs(met[0].item() / B - loss) < 1e-5 * abs(loss)
+
+
+def test_bncnn_eval_and_predict_use_moving_statistics():
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.train import program as PG
+    m = _model_b(tde)
+    st = m._store
+    g = torch.Generator(device="cpu").manual_seed(5)
+    for n in st.order:
+        if "moving" in n:
+            v = st.view(n)
+            v.copy_((torch.rand(v.shape, generator=g) + (0.5 if "variance" in n else -0.5)).to(v.device))
+    plan = PG.make_plan(m, st, DEV, 64, 64, None, m.loss)
+    x, y = _data(64, 12)
+    probs = plan.predict(x, 64).clone()
+    plan.eval_step(x, y, 64)
+    torch.cuda.synchronize()
+    m.layers  # noqa: B018
+    ref = m(x.cpu().numpy())   # the torch reference forward (inference: moving statistics, no dropout)
+    ref = (ref if torch.is_tensor(ref) else torch.as_tensor(np.asarray(ref))).to(DEV, torch.float64)
+    assert _rel(probs, ref) < 1e-5, _rel(probs, ref)
+    met = plan.metrics.double().cpu()
+    want = F.nll_loss(torch.log(ref), y.long(), reduction="sum").item()
+    assert abs(met[0].item() - want) < 1e-4 * abs(want) and met[2].item() == 64
+    assert met[1].item() == (ref.argmax(1) == y.long()).sum().item()
+
+
+def test_bncnn_fit_matches_reference_executor(monkeypatch):
+    """fit() over 4 steps (hipGraph executions) on the fused plan vs the torch fp32 reference executor
+    (dropout off so both are deterministic): same weights, moving statistics and loss to fp32 accuracy."""
+    import tensorflow_distributed_example_amd as tde
+    rng = np.random.default_rng(0)
+    x = rng.random((128 * 4, 784), dtype=np.float32)
+    y = rng.integers(0, 10, 128 * 4)
+    mf = _model_b(tde)
+    w0 = mf.get_weights()
+    hf = mf.fit(x, y, batch_size=128, epochs=1, shuffle=False, verbose=0)
+    prog = mf._program("train", 128)
+    assert prog.plan_kind == "fused_bncnn"
+    tde.backend.clear_session()
+    monkeypatch.setenv("TDE_EXECUTOR", "reference")
+    mr = _model_b(tde)
+    mr.set_weights(w0)
+    hr = mr.fit(x, y, batch_size=128, epochs=1, shuffle=False, verbose=0)
+    for name, a, b, w in zip(mf.variable_names(), mf.get_weights(), mr.get_weights(), w0):
+        rel = np.linalg.norm(a - b) / (np.linalg.norm(b - w) + np.linalg.norm(b) * 1e-6 + 1e-12)
+        assert rel < 1e-3, (name, rel)
+    assert abs(hf.history["loss"][0] - hr.history["loss"][0]) < 1e-4
+
+
+def test_bncnn_dropout_is_active_in_training_only():
+    """Dropout(0.5) of Model B: training steps differ from the dropout-free step; evaluation without the
+    forced learning phase is deterministic; set_learning_phase(1) (quirk Q4) keeps dropout and batch
+    statistics in prediction (two predictions at different steps differ)."""
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.train import program as PG
+    m = _model_b(tde, rate=0.5)
+    st = m._store
+    plan = PG.make_plan(m, st, DEV, 128, 128, m.optimizer, m.loss)
+    x, y = _data(128, 13)
+    plan.train_step(x, y)
+    g_drop = st.grad(f"{plan.head.name}/kernel").clone()
+    st.g.zero_()
+    plan.iterations += 1
+    plan.train_step(x, y)
+    g_drop2 = st.grad(f"{plan.head.name}/kernel").clone()
+    torch.cuda.synchronize()
+    assert torch.isfinite(g_drop).all() and not torch.equal(g_drop, g_drop2)   # new mask per step
+    p1 = plan.predict(x, 128).clone()
+    p2 = plan.predict(x, 128).clone()
+    assert torch.equal(p1, p2)
+    tde.backend.set_learning_phase(1)
+    try:
+        q1 = plan.predict(x, 128).clone()
+        plan.iterations += 1
+        q2 = plan.predict(x, 128).clone()
+    finally:
+        tde.backend.set_learning_phase(None)
+    assert not torch.equal(q1, q2)

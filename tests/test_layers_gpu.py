@@ -6,7 +6,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("bf16_policy")]   # the layer-wise kernel library: bf16
 DEV = "cuda"
 bf = torch.bfloat16
 

@@ -179,7 +179,7 @@ def test_xgmi_setup_failure_on_one_rank_falls_back_everywhere():
 
 
 def test_bucketed_overlapped_allreduce_two_ranks():
-    """Layer-wise plan under MWMS with small reverse-order buckets: each bucket's xGMI all-reduce is
+    """Layer-wise plan (bf16 policy) under MWMS with small reverse-order buckets: each bucket's xGMI all-reduce is
     enqueued on the comm stream behind the backward stage that finalises it (captured in the step's
     hipGraph); replicas stay bit-identical and training matches the single post-backward all-reduce."""
     losses = {}
@@ -188,7 +188,7 @@ def test_bucketed_overlapped_allreduce_two_ranks():
                    TDE_OVERLAP=overlap, TDE_BUCKET_MB="0.2")
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
                "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
-               "--gpus", "2", "--model", "mnist_bn_cnn", "--steps", "48", "--warmup", "16"]
+               "--gpus", "2", "--model", "mnist_bn_cnn", "--steps", "48", "--warmup", "16", "--dtype", "bf16"]
         r = subprocess.run(cmd, env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
                            timeout=300)
         assert r.returncode == 0, r.stdout[-4000:]
