@@ -3,26 +3,29 @@
 //   [Reshape] · (Conv2D(no bias) · BatchNormalization · ReLU) x L · Flatten ·
 //   Dense(no bias) · BatchNormalization · ReLU · [Dropout] · Dense(+bias)[softmax] + SCCE
 // in the reference's precision: every GEMM-shaped product on the exact-f32 MFMA
-// (v_mfma_f32_16x16x4_f32), statistics in f32/f64, no bf16 anywhere.
+// (v_mfma_f32_16x16x4_f32), batch statistics accumulated in f64, no bf16 anywhere.
 //
-// BatchNormalization needs batch-wide statistics between layers, so the step is a short chain of
-// launches whose boundaries ARE the statistics exchanges (one per BN, forward and backward); each
-// launch applies the previous layer's BN + ReLU while it stages its input, so no activation is
-// ever written in normalised form:
-//   conv_fwd x L   stage relu(BN(z_prev)) (the BN finalised from the producer's per-workgroup
-//                  (mean, M2) partials, Chan-combined in f64) -> implicit-GEMM conv -> raw z,
-//                  this layer's statistics partials
-//   dense_fwd      relu(BN(z_L)) flattened . W_dense -> h (split-K f32 atomics)
-//   head           ONE workgroup: the dense BN statistics over the batch, ReLU, Philox dropout,
-//                  Dense head (MFMA), softmax-CE / accuracy, and the head + dropout + ReLU + BN
-//                  backward down to dL/dh; head / BN gradients
-//   dense_bwd      dW_dense = A^T . dh and dA = dh . W^T -> g_L = dA * relu mask, BN_L backward
-//                  partial sums (sum g, sum g*xhat)
-//   conv_bwd x L   dZ = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) on load; roles per image:
+// BatchNormalization needs batch-wide statistics between layers, so the step is a chain of launches
+// whose boundaries ARE the statistics exchanges (one per BN each way); every launch applies the
+// previous layer's BN + ReLU while it stages its input, so no normalised activation is stored:
+//   conv_fwd x L   one image per workgroup: relu(BN(z_prev)) and the weights staged in LDS ->
+//                  implicit-GEMM conv -> raw z + this BN's sums (sum, sum of squares: f64)
+//   dense_fwd      relu(BN(z_L)) . W_dense -> per-K-chunk partials of h (summed in a fixed order)
+//   head_fwd/bwd   per 16-feature tile: the dense BN statistics, ReLU, Philox dropout, the Dense head,
+//                  softmax-CE / accuracy, and the head + dropout + ReLU + BN backward down to dL/dh
+//   dense_bwd      per 32-feature K tile: dW_dense = A^T . dh and dA = dh . W^T -> g_L (ReLU mask) and
+//                  BN_L's backward sums (sum g, sum g*xhat)
+//   conv_bwd x L   one image per workgroup: dZ = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) in LDS;
 //                  input gradient per stride class (only the taps that hit that class) -> g of the
-//                  previous layer + its partial sums; weight gradient partials per image
-//   reduce         per-image weight-gradient partials -> the flat gradient bucket (fixed order:
-//                  deterministic, no atomics)
+//                  previous layer + its BN backward sums; the image's weight-gradient partial
+//   reduce         per-image weight-gradient partials -> the flat gradient bucket in image order
+// Statistics sums are consumed by the next launch and re-zeroed by the one after it (each launch
+// zeroes a buffer two steps back in the chain), so a step needs no memset.
+//
+// Latency is the budget at MNIST sizes: a dependent round trip to data another XCD just wrote costs
+// ~2 us, an MFMA pass over a whole image well under that.  So the conv / dense launches run 1024-thread
+// workgroups (one per CU) that issue EVERY global load they need in one batch into registers (the
+// statistics sums included), then work out of LDS: one round trip per launch.
 // Gradients land in the replica's flat fp32 bucket (one all-reduce for data parallelism), then the
 // multi-tensor optimizer kernel applies them.
 #include "tde_common.h"
@@ -30,245 +33,228 @@
 namespace tde {
 namespace bncnn {
 
-constexpr int NTH = 256;   // threads of every workgroup except the head's
+constexpr int NTH = 256;    // head / reduce workgroups
+constexpr int NTB = 1024;   // conv / dense workgroups: 16 waves
+constexpr int kUAct = 5, kUW = 11, kUImg = 5;   // prefetch registers per thread (x NTB elements)
+constexpr int kMaxCls = 4;                       // stride classes of the input gradient (strides <= 2)
 
 struct Geo {   // NHWC input [B][H][W][C], HWIO kernel [kh][kw][C][Co], NHWC output [B][Ho][Wo][Co]
   int H, W, C, Ho, Wo, Co, kh, kw, sh, sw, pt, pl;
 };
 
-// The BatchNormalization (+ ReLU) that follows a layer, C channels.
+// The BatchNormalization (+ ReLU) after a layer, C channels.
 enum { kBnNone = 0, kBnTrain = 1, kBnMoving = 2, kBnBatch = 3, kBnSaved = 4 };
 struct Bn {
   int mode;        // kBnNone: raw values (the image); kBnTrain: batch statistics + saved + moving update;
                    // kBnMoving: moving statistics; kBnBatch: batch statistics, no update (learning phase 1
                    // in evaluation, Q4); kBnSaved: the statistics the forward saved (backward)
   int C;
-  const float* pmean; const float* pm2; const float* pn; int npart;   // statistics partials [npart][C], [npart]
+  const double* acc; double count;   // batch statistics: [kSlots][2][C] sums, sums of squares
   const float* gamma; const float* beta;
   float eps, momentum, bessel;
   float* mmean; float* mvar;
   float* saved;    // [2][C] mean, rstd
 };
 
-// Backward partial sums of a BN: g = dL/d(BN output, pre-ReLU); sums of g and g*xhat per channel.
+// Backward sums of a BN: g = dL/d(BN output, pre-ReLU); acc = [kSlots][2][C] sum g, sum g*xhat.
 struct BnBwd {
-  const float* psg; const float* psgx; int npart;   // [npart][C]
-  float* dbeta; float* dgamma;                        // flat gradient bucket views (nullable)
+  const double* acc;
+  float* dbeta; float* dgamma;   // flat gradient bucket views (nullable)
 };
-
-// Per-channel scale / shift of the forward BN (y = x*sc + sh, then ReLU) and mean / rstd, into LDS
-// (st: 4*C floats: sc, sh, mean, rstd).  red: 2*NTH doubles of LDS.  Block `writer` stores the
-// saved statistics and the moving-average update (training).  Ends with a barrier.
-__device__ void bn_prepare(const Bn& bn, float* st, double* red, bool writer) {
-  const int C = bn.C, t = threadIdx.x;
-  float* sc = st;
-  float* sh = st + C;
-  float* mu = st + 2 * C;
-  float* rs = st + 3 * C;
-  if (bn.mode == kBnNone) {
-    for (int c = t; c < C; c += NTH) {
-      sc[c] = 1.f; sh[c] = 0.f; mu[c] = 0.f; rs[c] = 1.f;
-    }
-    __syncthreads();
-    return;
-  }
-  if (bn.mode == kBnMoving || bn.mode == kBnSaved) {
-    for (int c = t; c < C; c += NTH) {
-      float mean, rstd;
-      if (bn.mode == kBnMoving) {
-        mean = bn.mmean[c];
-        rstd = rsqrtf(bn.mvar[c] + bn.eps);
-      } else {
-        mean = bn.saved[c];
-        rstd = bn.saved[C + c];
-      }
-      const float g = bn.gamma ? bn.gamma[c] : 1.f;
-      sc[c] = g * rstd;
-      sh[c] = (bn.beta ? bn.beta[c] : 0.f) - mean * g * rstd;
-      mu[c] = mean;
-      rs[c] = rstd;
-    }
-    __syncthreads();
-    return;
-  }
-  // batch statistics from the producer's per-workgroup (count, mean, M2): Chan's parallel combination
-  // in two f64 passes (total mean; then sum of M2_w + n_w (mean_w - mean)^2), NTH/C threads per channel
-  const int G = NTH / C, c = t % C, j = t / C;
-  double s = 0.0, n = 0.0;
-  if (j < G) {
-    for (int w = j; w < bn.npart; w += G) {
-      const double nw = bn.pn[w];
-      s += nw * (double)bn.pmean[(size_t)w * C + c];
-      n += nw;
-    }
-  }
-  red[t] = s;
-  red[NTH + t] = n;
-  __syncthreads();
-  double S = 0.0, N = 0.0;
-  if (j < G) {
-    for (int q = 0; q < G; ++q) {
-      S += red[q * C + c];
-      N += red[NTH + q * C + c];
-    }
-  }
-  const double mean = N > 0.0 ? S / N : 0.0;
-  __syncthreads();
-  double m2 = 0.0;
-  if (j < G) {
-    for (int w = j; w < bn.npart; w += G) {
-      const double d = (double)bn.pmean[(size_t)w * C + c] - mean;
-      m2 += (double)bn.pm2[(size_t)w * C + c] + (double)bn.pn[w] * d * d;
-    }
-  }
-  red[t] = m2;
-  __syncthreads();
-  if (t < C) {
-    double M2 = 0.0;
-    for (int q = 0; q < G; ++q) M2 += red[q * C + t];
-    const float var = N > 0.0 ? (float)(M2 / N) : 0.f;
-    const float rstd = (float)(1.0 / sqrt((double)var + (double)bn.eps));
-    const float g = bn.gamma ? bn.gamma[t] : 1.f;
-    sc[t] = g * rstd;
-    sh[t] = (bn.beta ? bn.beta[t] : 0.f) - (float)mean * g * rstd;
-    mu[t] = (float)mean;
-    rs[t] = rstd;
-    if (writer && bn.mode == kBnTrain) {
-      bn.saved[t] = (float)mean;
-      bn.saved[C + t] = rstd;
-      if (bn.mmean) {
-        bn.mmean[t] = bn.mmean[t] * bn.momentum + (float)mean * (1.f - bn.momentum);
-        bn.mvar[t] = bn.mvar[t] * bn.momentum + var * bn.bessel * (1.f - bn.momentum);
-      }
-    }
-  }
-  __syncthreads();
-}
-
-// Sums of a BN's backward partials -> k[c] = sum g, k[C + c] = sum g*xhat (LDS, 2*C floats);
-// block `writer` stores dbeta / dgamma.  Ends with a barrier.
-__device__ void bnbwd_prepare(const BnBwd& bb, int C, float* k, double* red, bool writer) {
-  const int t = threadIdx.x, G = NTH / C, c = t % C, j = t / C;
-  double s1 = 0.0, s2 = 0.0;
-  if (j < G) {
-    for (int w = j; w < bb.npart; w += G) {
-      s1 += bb.psg[(size_t)w * C + c];
-      s2 += bb.psgx[(size_t)w * C + c];
-    }
-  }
-  red[t] = s1;
-  red[NTH + t] = s2;
-  __syncthreads();
-  if (t < C) {
-    double a = 0.0, b = 0.0;
-    for (int q = 0; q < G; ++q) {
-      a += red[q * C + t];
-      b += red[NTH + q * C + t];
-    }
-    k[t] = (float)a;
-    k[C + t] = (float)b;
-    if (writer) {
-      if (bb.dbeta) bb.dbeta[t] = (float)a;
-      if (bb.dgamma) bb.dgamma[t] = (float)b;
-    }
-  }
-  __syncthreads();
-}
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// Input image of one sample, BN + ReLU applied (st from bn_prepare; bn_mode kBnNone: raw), into the
-// zero-padded LDS image Xs [(Hp)][(Wp)][C] (the image at offset (pt, pl)); only padded rows
-// [r0, r1) are written (the rows a workgroup's output pixels read).
-__device__ void stage_image(const Geo& g, const float* in, int b, int bn_mode, const float* st, float* Xs, int Wp,
-                            int r0, int r1) {
-  const int C = g.C;
-  const float* sc = st;
-  const float* sh = st + C;
-  const int n = (r1 - r0) * Wp * C;
-  const float* img = in + (size_t)b * g.H * g.W * C;
-  for (int e = threadIdx.x; e < n; e += NTH) {
-    const int c = e % C, pix = e / C;
-    const int y = r0 + pix / Wp, x = pix % Wp;
-    const int iy = y - g.pt, ix = x - g.pl;
-    float v = 0.f;
-    if (iy >= 0 && iy < g.H && ix >= 0 && ix < g.W) {
-      v = img[((size_t)iy * g.W + ix) * C + c];
-      if (bn_mode != kBnNone) v = fmaxf(fmaf(v, sc[c], sh[c]), 0.f);
+// ---- one-batch prefetch: element i = tid + u * NTB of an n-element source into registers (clamped
+// addresses, so every load of the batch is issued without a branch), stored to LDS later
+template <int U>
+struct Pf {
+  float v[U];
+};
+template <int U, typename LD>
+__device__ __forceinline__ void pf_load(Pf<U>& p, int n, LD ld) {
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (u * NTB < n) p.v[u] = ld(min((int)threadIdx.x + u * NTB, n - 1));
+}
+template <int U, typename ST>
+__device__ __forceinline__ void pf_store(const Pf<U>& p, int n, ST st) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = threadIdx.x + u * NTB;
+    if (i < n) st(i, p.v[u]);
+  }
+}
+
+// Statistics accumulators are spread over kSlots copies ([kSlots][2][C] doubles; a producer
+// workgroup adds into slot (its linear id % kSlots)): hundreds of workgroups adding into the same few
+// addresses serialise at the L2 atomic unit, 64 slots keep that contention a few deep.
+constexpr int kSlots = 64;
+__device__ __forceinline__ int my_slot() {
+  return ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) & (kSlots - 1);
+}
+
+// red[q] = sum over the slots of acc[slot][q], q < Q (Q <= blockDim); red: blockDim doubles of LDS.
+// Ends with a barrier.
+__device__ void slot_sums(const double* acc, int Q, double* red) {
+  const int t = threadIdx.x, np = blockDim.x / Q, q = t % Q, part = t / Q;
+  double s = 0.0;
+  if (part < np) {
+    for (int j0 = part; j0 < kSlots; j0 += 8 * np) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = j0 + u * np;
+        v[u] = j < kSlots ? acc[j * Q + q] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
     }
-    Xs[(size_t)y * Wp * C + (size_t)x * C + c] = v;
+    red[t] = s;
+  }
+  lds_barrier();
+  double S = 0.0;
+  if (t < Q)
+    for (int p = 0; p < np; ++p) S += red[p * Q + t];
+  lds_barrier();
+  if (t < Q) red[t] = S;
+  lds_barrier();
+}
+
+// Per-channel scale / shift of the forward BN (y = x*sc + sh, then ReLU) and mean / rstd into LDS
+// (st: 4*C floats: sc, sh, mean, rstd).  Block `writer` stores the saved statistics and the
+// moving-average update (training).  red: blockDim doubles of LDS (batch modes).  Ends with a barrier.
+__device__ void bn_prepare(const Bn& bn, float* st, bool writer, double* red) {
+  const int C = bn.C;
+  const bool batch = bn.mode == kBnTrain || bn.mode == kBnBatch;
+  if (batch) slot_sums(bn.acc, 2 * C, red);
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float mean = 0.f, rstd = 1.f, var = 0.f;
+    if (bn.mode == kBnMoving) {
+      mean = bn.mmean[c];
+      rstd = rsqrtf(bn.mvar[c] + bn.eps);
+    } else if (bn.mode == kBnSaved) {
+      mean = bn.saved[c];
+      rstd = bn.saved[C + c];
+    } else if (batch) {
+      // E[x^2] - E[x]^2 over f64 sums of f32 values: ~1e-16 * (mean/std)^2 relative on the variance
+      const double m = red[c] / bn.count;
+      const double v = fmax(red[C + c] / bn.count - m * m, 0.0);
+      mean = (float)m;
+      var = (float)v;
+      rstd = (float)(1.0 / sqrt(v + (double)bn.eps));
+    }
+    float sc = 1.f, sh = 0.f;
+    if (bn.mode != kBnNone) {
+      const float g = bn.gamma ? bn.gamma[c] : 1.f;
+      sc = g * rstd;
+      sh = (bn.beta ? bn.beta[c] : 0.f) - mean * sc;
+    }
+    st[c] = sc;
+    st[C + c] = sh;
+    st[2 * C + c] = mean;
+    st[3 * C + c] = rstd;
+    if (writer && bn.mode == kBnTrain) {
+      bn.saved[c] = mean;
+      bn.saved[C + c] = rstd;
+      if (bn.mmean) {
+        bn.mmean[c] = bn.mmean[c] * bn.momentum + mean * (1.f - bn.momentum);
+        bn.mvar[c] = bn.mvar[c] * bn.momentum + var * bn.bessel * (1.f - bn.momentum);
+      }
+    }
+  }
+  lds_barrier();
+}
+
+// Zeroes n doubles cooperatively over the grid (a statistics buffer two launches back in the chain).
+__device__ __forceinline__ void zero_share(double* p, int n) {
+  if (!p) return;
+  const int nb = gridDim.x * gridDim.y * gridDim.z;
+  const int me = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  for (int i = me * (int)blockDim.x + threadIdx.x; i < n; i += nb * (int)blockDim.x) p[i] = 0.0;
+}
+
+// Per-wave column statistics (lanes fq == 0 after the cross-fq shuffles hold column fr of N tile n)
+// -> cs[wave][stat][32] -> one f64 atomic per (stat, channel) into this workgroup's slot, the 16
+// waves summed in a fixed order.
+__device__ __forceinline__ void wave_cols_to_slot(const double (&s1)[2], const double (&s2)[2], double* cs,
+                                                  double* acc, int C) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    double x1 = s1[n], x2 = s2[n];
+    x1 += __shfl_xor(x1, 16, 64);
+    x1 += __shfl_xor(x1, 32, 64);
+    x2 += __shfl_xor(x2, 16, 64);
+    x2 += __shfl_xor(x2, 32, 64);
+    if (fq == 0) {
+      cs[(wave * 2 + 0) * 32 + n * 16 + fr] = x1;
+      cs[(wave * 2 + 1) * 32 + n * 16 + fr] = x2;
+    }
+  }
+  lds_barrier();
+  if (tid < 2 * C) {
+    const int j = tid / C, c = tid - j * C;
+    double S = 0.0;
+    for (int w = 0; w < 16; ++w) S += cs[(w * 2 + j) * 32 + c];
+    atomicAdd(acc + my_slot() * 2 * C + j * C + c, S);
   }
 }
 
 // ------------------------------------------------------------------------------------------------
-// Forward conv: grid (B, nchunk); each workgroup = one image x a chunk of 16-pixel output tiles.
-// Wave w: K part kp = w % KS (of KS), tile group tg = w / KS owning TPW consecutive tiles; NT tiles of
-// 16 output channels.  Partial sums of the KS K parts are combined through LDS.
-struct ConvFwdArgs {
+// Forward conv: grid B (one image per workgroup).  Work items (16-pixel output tile, 16-channel N
+// tile, K part) over the 16 waves; K parts (strided K steps) summed through LDS in a fixed order.
+struct ConvFwdP {
   Geo g;
+  int K, M, Hp, Wp, nct, ks, spp, Kpad, mt, nitems;
+  int o_red, o_cs, o_st, o_xs, o_ws, o_koff, o_part, lds;
+};
+struct ConvFwdArgs {
+  ConvFwdP p;
   int B;
   const float* in;
   Bn bn;                     // BN + ReLU of the input (kBnNone for the image)
   const float* w;
   float* z;
-  float *pmean, *pm2, *pn;   // this layer's statistics partials (nullable: no statistics needed)
-  int nchunk, Hp, Wp, Kp;
-  float* zero; long long nzero;   // a buffer zeroed cooperatively by the grid (the dense accumulator)
+  double* acc;               // this layer's BN sums [kSlots][2][Co] (nullable: no statistics)
+  double* zero; int nzero;   // the statistics buffer two launches back, zeroed by the grid
+  long long* stamps;         // diagnostic phase clock (tde_bncnn_stamps), nullable
 };
 
-struct ConvFwdLds {
-  int xs, ws, koff, st, red, acc, sts, total;
-};
-template <int TPW, int NT, int KS>
-__host__ __device__ ConvFwdLds conv_fwd_lds(int Hp, int Wp, int C, int Kp) {
-  ConvFwdLds L;
-  int o = 0;
-  L.red = o; o += 2 * NTH * 8;
-  L.xs = o; o += ((Hp * Wp * C + 3) & ~3) * 4;
-  L.ws = o; o += Kp * NT * 16 * 4;
-  L.koff = o; o += Kp * 4;
-  L.st = o; o += 4 * ((C + 3) & ~3) * 4;
-  L.acc = o; o += (KS - 1) * (4 / KS) * TPW * NT * 256 * 4;
-  L.sts = o; o += (4 + 1) * NT * 16 * 4;
-  L.total = o;
-  return L;
-}
-
-template <int TPW, int NT, int KS>
-__global__ __launch_bounds__(NTH) void conv_fwd_kernel(ConvFwdArgs a) {
+__global__ __launch_bounds__(NTB) void conv_fwd_kernel(ConvFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
-  const Geo g = a.g;
-  const ConvFwdLds L = conv_fwd_lds<TPW, NT, KS>(a.Hp, a.Wp, g.C, a.Kp);
-  double* red = reinterpret_cast<double*>(sm + L.red);
-  float* Xs = reinterpret_cast<float*>(sm + L.xs);
-  float* Ws = reinterpret_cast<float*>(sm + L.ws);
-  int* koff = reinterpret_cast<int*>(sm + L.koff);
-  float* st = reinterpret_cast<float*>(sm + L.st);
-  float* accs = reinterpret_cast<float*>(sm + L.acc);
-  float* sts = reinterpret_cast<float*>(sm + L.sts);
-  constexpr int NTP = NT * 16, MTW = (4 / KS) * TPW;
+  const ConvFwdP& P = a.p;
+  const Geo& g = P.g;
+  double* red = reinterpret_cast<double*>(sm + P.o_red);
+  double* cs = reinterpret_cast<double*>(sm + P.o_cs);
+  float* st = reinterpret_cast<float*>(sm + P.o_st);
+  float* Xs = reinterpret_cast<float*>(sm + P.o_xs);
+  float* Ws = reinterpret_cast<float*>(sm + P.o_ws);
+  int* koff = reinterpret_cast<int*>(sm + P.o_koff);
+  float* part = reinterpret_cast<float*>(sm + P.o_part);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
-  const int b = blockIdx.x, chunk = blockIdx.y;
-  const int Wp = a.Wp, C = g.C, Co = g.Co, K = g.kh * g.kw * C, Kp = a.Kp;
-  const int M = g.Ho * g.Wo;
-
-  if (a.zero) {
-    const long long nb = (long long)gridDim.x * gridDim.y, me = (long long)blockIdx.y * gridDim.x + blockIdx.x;
-    const long long per = (a.nzero + nb - 1) / nb;
-    for (long long i = me * per + tid; i < min(a.nzero, (me + 1) * per); i += NTH) a.zero[i] = 0.f;
+  const int b = blockIdx.x, C = g.C, Co = g.Co, K = P.K, M = P.M, NTP = P.nct * 16, Wp = P.Wp;
+  stamp(a.stamps, 0);
+  // ---- one batch of global loads: the image and the weights (the BN sums join in bn_prepare)
+  const int nimg = g.H * g.W * C, nw = K * Co;
+  const float* img = a.in + (size_t)b * nimg;
+  Pf<kUImg> pi;
+  Pf<kUW> pw;
+  pf_load(pi, nimg, [&](int i) { return img[i]; });
+  pf_load(pw, nw, [&](int i) { return a.w[i]; });
+  zero_share(a.zero, a.nzero);
+  // LDS the registers do not cover: image border, weight padding, im2col offsets
+  for (int i = tid; i < P.Hp * Wp; i += NTB) {
+    const int y = i / Wp, x = i - y * Wp, iy = y - g.pt, ix = x - g.pl;
+    if (iy < 0 || iy >= g.H || ix < 0 || ix >= g.W)
+      for (int c = 0; c < C; ++c) Xs[i * C + c] = 0.f;
   }
-  bn_prepare(a.bn, st, red, b == 0 && chunk == 0);
-  // padded input rows of this chunk's output pixels
-  const int m0 = chunk * MTW * 16, m1 = min(M, m0 + MTW * 16);
-  const int r0 = (m0 / g.Wo) * g.sh, r1 = ((m1 - 1) / g.Wo) * g.sh + g.kh;
-  stage_image(g, a.in, b, a.bn.mode, st, Xs, Wp, r0, r1);
-  for (int e = tid; e < Kp * NTP; e += NTH) {
-    const int k = e / NTP, n = e - k * NTP;
-    Ws[e] = (k < K && n < Co) ? a.w[(size_t)k * Co + n] : 0.f;
+  for (int i = tid; i < P.Kpad * NTP; i += NTB) {
+    const int k = i / NTP, col = i - k * NTP;
+    if (k >= K || col >= Co) Ws[i] = 0.f;
   }
-  for (int k = tid; k < Kp; k += NTH) {
+  for (int k = tid; k < P.Kpad; k += NTB) {
     int off = 0;
     if (k < K) {
       const int ci = k % C, t = k / C, kx = t % g.kw, ky = t / g.kw;
@@ -276,171 +262,152 @@ __global__ __launch_bounds__(NTH) void conv_fwd_kernel(ConvFwdArgs a) {
     }
     koff[k] = off;
   }
-  __syncthreads();
-
-  const int kp = wave % KS, tg = wave / KS;
-  const int tile0 = chunk * MTW + tg * TPW;
-  int pb[TPW];
-#pragma unroll
-  for (int j = 0; j < TPW; ++j) {
-    const int m = (tile0 + j) * 16 + fr;
+  bn_prepare(a.bn, st, b == 0, red);
+  stamp(a.stamps, 1);
+  {
+    const float* sc = st;
+    const float* sh = st + C;
+    const bool raw = a.bn.mode == kBnNone;
+    pf_store(pi, nimg, [&](int i, float v) {
+      const int c = i % C, pix = i / C, y = pix / g.W, x = pix - y * g.W;
+      Xs[((y + g.pt) * Wp + x + g.pl) * C + c] = raw ? v : fmaxf(fmaf(v, sc[c], sh[c]), 0.f);
+    });
+    pf_store(pw, nw, [&](int i, float v) {
+      const int k = i / Co, co = i - k * Co;
+      Ws[k * NTP + co] = v;
+    });
+  }
+  lds_barrier();
+  stamp(a.stamps, 2);
+  // ---- MFMA work items
+  const int ntile = P.mt * P.nct;
+  for (int item = wave; item < P.nitems; item += 16) {
+    const int kp = item % P.ks, t = item / P.ks, n = t % P.nct, mtile = t / P.nct;
+    const int m = min(mtile * 16 + fr, M - 1);
     const int oh = m / g.Wo, ow = m - oh * g.Wo;
-    pb[j] = m < M ? (oh * g.sh * Wp + ow * g.sw) * C : r0 * Wp * C;
-  }
-  f32x4 acc[TPW][NT];
+    const int pb = (oh * g.sh * Wp + ow * g.sw) * C;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int i0 = 0; i0 < P.spp; i0 += 4) {
+      int ko[4];
+      float bv[4];
 #pragma unroll
-  for (int j = 0; j < TPW; ++j)
+      for (int u = 0; u < 4; ++u) {
+        const int k = 4 * (kp + (i0 + u) * P.ks) + fq;
+        ko[u] = koff[k];
+        bv[u] = Ws[k * NTP + n * 16 + fr];
+      }
 #pragma unroll
-    for (int n = 0; n < NT; ++n) acc[j][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int steps = Kp / 4;
-  for (int s = kp; s < steps; s += KS) {
-    const int k = 4 * s + fq;
-    const int off = koff[k];
-    float bv[NT];
-#pragma unroll
-    for (int n = 0; n < NT; ++n) bv[n] = Ws[k * NTP + n * 16 + fr];
-#pragma unroll
-    for (int j = 0; j < TPW; ++j) {
-      const float av = Xs[pb[j] + off];
-#pragma unroll
-      for (int n = 0; n < NT; ++n) acc[j][n] = mfma4(av, bv[n], acc[j][n]);
+      for (int u = 0; u < 4; ++u) acc = mfma4(Xs[pb + ko[u]], bv[u], acc);
     }
+    *reinterpret_cast<f32x4*>(part + ((size_t)(kp * ntile + t) * 64 + lane) * 4) = acc;
   }
-  if (KS > 1) {
-    if (kp > 0) {
-#pragma unroll
-      for (int j = 0; j < TPW; ++j)
-#pragma unroll
-        for (int n = 0; n < NT; ++n)
-          *reinterpret_cast<f32x4*>(accs + ((((kp - 1) * (4 / KS) + tg) * TPW + j) * NT + n) * 256 + lane * 4) =
-              acc[j][n];
-    }
-    __syncthreads();
-    if (kp == 0) {
-      for (int q = 1; q < KS; ++q)
-#pragma unroll
-        for (int j = 0; j < TPW; ++j)
-#pragma unroll
-          for (int n = 0; n < NT; ++n) {
-            const f32x4 v =
-                *reinterpret_cast<const f32x4*>(accs + ((((q - 1) * (4 / KS) + tg) * TPW + j) * NT + n) * 256 + lane * 4);
-            acc[j][n] += v;
-          }
-    }
-  }
-  // ---- epilogue: raw z, then this chunk's per-channel (mean, M2)
+  lds_barrier();
+  stamp(a.stamps, 3);
+  // ---- epilogue: the K parts summed in order; raw z; this layer's BN sums
   float* zb = a.z + (size_t)b * M * Co;
-  float csum[NT];
+  double s1[2] = {0.0, 0.0}, s2[2] = {0.0, 0.0};
+  for (int t = wave; t < ntile; t += 16) {
+    const int n = t % P.nct, mtile = t / P.nct;
+    f32x4 v = *reinterpret_cast<const f32x4*>(part + ((size_t)t * 64 + lane) * 4);
+    for (int kp = 1; kp < P.ks; ++kp) v += *reinterpret_cast<const f32x4*>(part + ((size_t)(kp * ntile + t) * 64 + lane) * 4);
+    const int co = n * 16 + fr;
+    double t1 = 0.0, t2 = 0.0;
 #pragma unroll
-  for (int n = 0; n < NT; ++n) csum[n] = 0.f;
-  if (kp == 0) {
-#pragma unroll
-    for (int j = 0; j < TPW; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = (tile0 + j) * 16 + fq * 4 + r;
-        if (m >= m1) continue;
-#pragma unroll
-        for (int n = 0; n < NT; ++n) {
-          const int co = n * 16 + fr;
-          if (co < Co) zb[(size_t)m * Co + co] = acc[j][n][r];
-          csum[n] += acc[j][n][r];
-        }
+    for (int i = 0; i < 4; ++i) {
+      const int m = mtile * 16 + fq * 4 + i;
+      if (m < M && co < Co) {
+        zb[(size_t)m * Co + co] = v[i];
+        t1 += v[i];
+        t2 += (double)v[i] * v[i];
       }
+    }
+    if (n == 0) {
+      s1[0] += t1;
+      s2[0] += t2;
+    } else {
+      s1[1] += t1;
+      s2[1] += t2;
+    }
   }
-  if (!a.pmean) return;
-  const int wg = b * a.nchunk + chunk;
-  const float cnt = (float)(m1 - m0);
-  float* mean_s = sts + 4 * NTP;
-#pragma unroll
-  for (int n = 0; n < NT; ++n) {
-    float v = csum[n];
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    if (fq == 0) sts[wave * NTP + n * 16 + fr] = kp == 0 ? v : 0.f;
-  }
-  __syncthreads();
-  if (tid < NTP) mean_s[tid] = (sts[tid] + sts[NTP + tid] + sts[2 * NTP + tid] + sts[3 * NTP + tid]) / cnt;
-  __syncthreads();
-#pragma unroll
-  for (int n = 0; n < NT; ++n) csum[n] = 0.f;
-  if (kp == 0) {
-#pragma unroll
-    for (int j = 0; j < TPW; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = (tile0 + j) * 16 + fq * 4 + r;
-        if (m >= m1) continue;
-#pragma unroll
-        for (int n = 0; n < NT; ++n) {
-          const float d = acc[j][n][r] - mean_s[n * 16 + fr];
-          csum[n] += d * d;
-        }
-      }
-  }
-#pragma unroll
-  for (int n = 0; n < NT; ++n) {
-    float v = csum[n];
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    if (fq == 0) sts[wave * NTP + n * 16 + fr] = kp == 0 ? v : 0.f;
-  }
-  __syncthreads();
-  if (tid < Co) {
-    a.pmean[(size_t)wg * Co + tid] = mean_s[tid];
-    a.pm2[(size_t)wg * Co + tid] = sts[tid] + sts[NTP + tid] + sts[2 * NTP + tid] + sts[3 * NTP + tid];
-  }
-  if (tid == 0) a.pn[wg] = cnt;
+  if (a.acc) wave_cols_to_slot(s1, s2, cs, a.acc, Co);
+  stamp(a.stamps, 4);
 }
 
 // ------------------------------------------------------------------------------------------------
-// Dense forward: h[B][Dp] += relu(BN(in))[B][K] . W[K][D]; grid (Dp/16, K chunks, row blocks of 64).
-// Wave w = 16-row tile w of the block; K chunk staged in LDS with the BN + ReLU applied.
+// Dense forward: hpart[kchunk][B][Dp] = relu(BN(in))[rows][chunk] . W[chunk][cols]; grid (column
+// groups of kDenseCols, K chunks <= kMaxKc, row blocks of 64).  The head sums the chunk partials in a
+// fixed order (deterministic h).
+constexpr int kMaxKc = 8;
+constexpr int kDenseCols = 112;
+constexpr int kUA = 10, kUB = 18;   // A: 64 x kc <= 10240, W: kc x 112 <= 18432 (kc <= 160)
 struct DenseFwdArgs {
-  int B, K, D, Dp, kc, lda;
+  int B, K, D, Dp, kc, lda, ldb;
   const float* in;           // [B][K], channel of feature k = k % bn.C
   Bn bn;
   const float* w;            // [K][D]
-  float* h;                  // [B][Dp] (+=)
+  float* hpart;              // [gridDim.y][B][Dp]
+  double* zero; int nzero;
+  long long* stamps;
 };
 
-__global__ __launch_bounds__(NTH) void dense_fwd_kernel(DenseFwdArgs a) {
+__global__ __launch_bounds__(NTB) void dense_fwd_kernel(DenseFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
-  double* red = reinterpret_cast<double*>(sm);
-  float* st = reinterpret_cast<float*>(sm + 2 * NTH * 8);
-  float* As = st + 4 * ((a.bn.C + 3) & ~3);          // [64][lda]
-  float* Bs = As + 64 * a.lda;                         // [kc][16]
+  const int C = a.bn.C;
+  double* red = reinterpret_cast<double*>(sm);  // [NTB]
+  float* st = reinterpret_cast<float*>(sm + NTB * 8);
+  float* As = st + 4 * 32;                      // [64][lda]
+  float* Bs = As + 64 * a.lda;                  // [kc][ldb]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
-  const int nt = blockIdx.x, k0 = blockIdx.y * a.kc, b0 = blockIdx.z * 64;
-  const int kn = min(a.kc, a.K - k0), C = a.bn.C;
-  bn_prepare(a.bn, st, red, nt == 0 && blockIdx.y == 0 && blockIdx.z == 0);
-  const float* sc = st;
-  const float* sh = st + C;
-  for (int e = tid; e < 64 * a.kc; e += NTH) {
-    const int r = e / a.kc, kk = e - r * a.kc;
-    float v = 0.f;
-    if (kk < kn && b0 + r < a.B) {
-      const int k = k0 + kk, c = k % C;
-      v = fmaxf(fmaf(a.in[(size_t)(b0 + r) * a.K + k], sc[c], sh[c]), 0.f);
-    }
-    As[r * a.lda + kk] = v;
+  const int c0 = blockIdx.x * kDenseCols, k0 = blockIdx.y * a.kc, b0 = blockIdx.z * 64;
+  const int kc = a.kc, kn = min(kc, a.K - k0);
+  stamp(a.stamps, 0);
+  Pf<kUA> pa;
+  Pf<kUB> pb;
+  pf_load(pa, 64 * kc, [&](int e) {
+    const int r = e / kc, kk = e - r * kc;
+    return a.in[(size_t)min(b0 + r, a.B - 1) * a.K + min(k0 + kk, a.K - 1)];
+  });
+  pf_load(pb, kc * kDenseCols, [&](int e) {
+    const int kk = e / kDenseCols, col = e - kk * kDenseCols;
+    return a.w[(size_t)min(k0 + kk, a.K - 1) * a.D + min(c0 + col, a.D - 1)];
+  });
+  zero_share(a.zero, a.nzero);
+  bn_prepare(a.bn, st, blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0, red);
+  stamp(a.stamps, 1);
+  {
+    const float* sc = st;
+    const float* sh = st + C;
+    pf_store(pa, 64 * kc, [&](int e, float v) {
+      const int r = e / kc, kk = e - r * kc, c = (k0 + kk) % C;
+      As[r * a.lda + kk] = (kk < kn && b0 + r < a.B) ? fmaxf(fmaf(v, sc[c], sh[c]), 0.f) : 0.f;
+    });
+    pf_store(pb, kc * kDenseCols, [&](int e, float v) {
+      const int kk = e / kDenseCols, col = e - kk * kDenseCols;
+      Bs[kk * a.ldb + col] = (kk < kn && c0 + col < a.D) ? v : 0.f;
+    });
   }
-  for (int e = tid; e < a.kc * 16; e += NTH) {
-    const int kk = e >> 4, n = e & 15, col = nt * 16 + n;
-    Bs[e] = (kk < kn && col < a.D) ? a.w[(size_t)(k0 + kk) * a.D + col] : 0.f;
-  }
-  __syncthreads();
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  const float* Ar = As + (wave * 16 + fr) * a.lda;
-  for (int s = 0; s < a.kc / 4; ++s) {
-    const int k = 4 * s + fq;
-    acc = mfma4(Ar[k], Bs[k * 16 + fr], acc);
-  }
+  lds_barrier();
+  stamp(a.stamps, 2);
+  // items: 4 row tiles x 7 column tiles
+  for (int item = wave; item < 4 * (kDenseCols / 16); item += 16) {
+    const int rt = item & 3, ct = item >> 2;
+    if (c0 + ct * 16 >= a.Dp) continue;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* Ar = As + (rt * 16 + fr) * a.lda;
+    for (int s0 = 0; s0 < kc / 4; s0 += 4) {   // kc % 16 == 0
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = b0 + wave * 16 + fq * 4 + r;
-    if (row < a.B) atomicAdd(a.h + (size_t)row * a.Dp + nt * 16 + fr, acc[r]);
+      for (int u = 0; u < 4; ++u) {
+        const int k = 4 * (s0 + u) + fq;
+        acc = mfma4(Ar[k], Bs[k * a.ldb + ct * 16 + fr], acc);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = b0 + rt * 16 + fq * 4 + i;
+      if (row < a.B) a.hpart[((size_t)blockIdx.y * a.B + row) * a.Dp + c0 + ct * 16 + fr] = acc[i];
+    }
   }
+  stamp(a.stamps, 3);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -467,530 +434,680 @@ __device__ __forceinline__ float keep_scale(float rate, unsigned long long seed,
 }
 
 // ------------------------------------------------------------------------------------------------
-// Head: ONE workgroup of 1024 threads.  h [B][Dp] -> BN (batch statistics over the B rows, or moving)
-// -> ReLU -> dropout -> Dense(D -> NC) + bias -> softmax-CE / accuracy; training: the head gradients,
-// and the dropout / ReLU / BN backward down to dL/dh.  Row blocks of 64.
+// Head, two launches over 16-feature tiles of the dense layer (grid Dp/16, so the per-feature
+// statistics never leave a workgroup):
+//   head_fwd   the dense BN statistics over the batch (or the moving ones), ReLU, Philox dropout, and
+//              this tile's share of the logits (act[:, tile] . Wh[tile, :]: f32 atomics into
+//              logits [B][16], zeroed by dense_fwd)
+//   head_bwd   softmax-CE / accuracy from the logits (every workgroup; workgroup 0 keeps the metrics,
+//              the bias gradient and the prediction output); training: dWh rows of the tile,
+//              g = dl . Wh^T through the dropout / ReLU masks, the BN backward sums of the tile, and
+//              dL/dh = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) for the tile.
+constexpr int kHeadMaxTiles = 16;   // Dp <= 256
 struct HeadArgs {
   int B, D, Dp, NC, mode;          // mode 0 train, 1 eval (metrics), 2 predict
-  const float* h;
-  Bn bn;                            // C = D (mode kBnTrain / kBnMoving / kBnBatch)
+  const float* hpart; int nkc;      // dense_fwd's K-chunk partials [nkc][B][Dp]
+  float* h;                         // [B][Dp]: their sum (written by head_fwd)
+  Bn bn;                            // C = D (mode kBnTrain / kBnMoving / kBnBatch; computed by head_fwd)
   float rate; unsigned long long seed; const long long* iter; int layer_id, drop_on;
   const float* wh; const float* bh;
+  float* logits;                    // [Dp/16][B][16] per-feature-tile partials (bias excluded)
   const int* labels; float scale;
   float* metrics;
   float* out; int out_softmax;      // predict: [B][NC] probabilities (softmax head) or logits
   float *dwh, *dbh, *dbeta, *dgamma;
   float* dh;                        // [B][Dp]: dL/dh (holds the pre-ReLU gradient g until the last pass)
+  double* zero; int nzero;
+  long long* stamps;   // diagnostic phase clock (tde_bncnn_stamps), nullable
 };
-constexpr int kHeadThreads = 1024;
-constexpr int kHeadMaxDp = 240;          // <= 15 feature tiles: wave 15 keeps the bias gradient
-constexpr int HLD = kHeadMaxDp + 4;   // LDS row stride of the row-block tile
-struct HeadLdsMap {
-  int mu, rs, sc, sh, sg, sgx, whs, bhs, as, part, dl, lab, red, total;
-};
-__host__ __device__ constexpr HeadLdsMap head_lds() {
-  HeadLdsMap L{};
-  int o = 0;
-  L.mu = o; o += kHeadMaxDp * 4;
-  L.rs = o; o += kHeadMaxDp * 4;
-  L.sc = o; o += kHeadMaxDp * 4;
-  L.sh = o; o += kHeadMaxDp * 4;
-  L.sg = o; o += kHeadMaxDp * 4;
-  L.sgx = o; o += kHeadMaxDp * 4;
-  L.whs = o; o += kHeadMaxDp * 16 * 4;     // [Dp][16]
-  L.bhs = o; o += 16 * 4;
-  L.as = o; o += 64 * HLD * 4;             // post-dropout activations of the row block
-  L.part = o; o += 12 * 64 * 4 * 4;        // logits partials
-  L.dl = o; o += 64 * 16 * 4;              // dlogits
-  L.lab = o; o += 64 * 4;
-  L.red = o; o += 4 * 256 * 8;             // f64 [4][256]: 4 threads per feature, f = tid & 255
-  L.total = o;
-  return L;
-}
 
-__global__ __launch_bounds__(kHeadThreads) void head_kernel(HeadArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
-  constexpr HeadLdsMap L = head_lds();
-  float* mu = reinterpret_cast<float*>(sm + L.mu);
-  float* rs = reinterpret_cast<float*>(sm + L.rs);
-  float* sc = reinterpret_cast<float*>(sm + L.sc);
-  float* sh = reinterpret_cast<float*>(sm + L.sh);
-  float* sg = reinterpret_cast<float*>(sm + L.sg);
-  float* sgx = reinterpret_cast<float*>(sm + L.sgx);
-  float* whs = reinterpret_cast<float*>(sm + L.whs);
-  float* bhs = reinterpret_cast<float*>(sm + L.bhs);
-  float* as = reinterpret_cast<float*>(sm + L.as);
-  float* part = reinterpret_cast<float*>(sm + L.part);
-  float* dls = reinterpret_cast<float*>(sm + L.dl);
-  int* labs = reinterpret_cast<int*>(sm + L.lab);
-  double* red = reinterpret_cast<double*>(sm + L.red);
+__global__ __launch_bounds__(NTH) void head_fwd_kernel(HeadArgs a) {
+  __shared__ float whs[16 * 16];           // [feature][class]
+  __shared__ float sc[16], sh[16];
+  __shared__ double red[2][16][16];
+  __shared__ float As[128 * 17];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  const int c = tid & 15, rg = tid >> 4;
+  const int f0 = blockIdx.x * 16, f = f0 + c;
   const int B = a.B, D = a.D, Dp = a.Dp, NC = a.NC;
-  const bool train = a.mode == 0;
+  const bool fok = f < D;
   const long long it = a.iter ? *a.iter : 0;
-
-  // ---- BN statistics of h over the batch (4 threads per feature, two f64 passes), or moving statistics
+  stamp(a.stamps, 0);
+  zero_share(a.zero, a.nzero);
   {
-    const int f = tid & 255, q = tid >> 8;
-    const bool batch = a.bn.mode == kBnTrain || a.bn.mode == kBnBatch;
-    if (batch) {
-      double s = 0.0;
-      if (f < D)
-        for (int b = q; b < B; b += 4) s += a.h[(size_t)b * Dp + f];
-      red[q * 256 + f] = s;
-      __syncthreads();
-      const double mean = (red[f] + red[256 + f] + red[512 + f] + red[768 + f]) / B;
-      __syncthreads();
-      double m2 = 0.0;
-      if (f < D)
-        for (int b = q; b < B; b += 4) {
-          const double d = a.h[(size_t)b * Dp + f] - mean;
-          m2 += d * d;
-        }
-      red[q * 256 + f] = m2;
-      __syncthreads();
-      if (q == 0 && f < D) {
-        const double M2 = red[f] + red[256 + f] + red[512 + f] + red[768 + f];
-        const float var = (float)(M2 / B);
-        const float rstd = (float)(1.0 / sqrt((double)var + (double)a.bn.eps));
-        mu[f] = (float)mean;
-        rs[f] = rstd;
-        if (a.bn.mode == kBnTrain) {
-          a.bn.saved[f] = (float)mean;
-          a.bn.saved[D + f] = rstd;
-          a.bn.mmean[f] = a.bn.mmean[f] * a.bn.momentum + (float)mean * (1.f - a.bn.momentum);
-          a.bn.mvar[f] = a.bn.mvar[f] * a.bn.momentum + var * a.bn.bessel * (1.f - a.bn.momentum);
-        }
-      }
-    } else if (q == 0 && f < D) {
-      mu[f] = a.bn.mmean[f];
-      rs[f] = rsqrtf(a.bn.mvar[f] + a.bn.eps);
-    }
-    __syncthreads();
-    if (q == 0 && f < Dp) {
-      const float g = (f < D && a.bn.gamma) ? a.bn.gamma[f] : 1.f;
-      sc[f] = f < D ? g * rs[f] : 0.f;
-      sh[f] = f < D ? (a.bn.beta ? a.bn.beta[f] : 0.f) - mu[f] * g * rs[f] : 0.f;
-      sg[f] = 0.f;
-      sgx[f] = 0.f;
-    }
+    const int ff = f0 + (tid >> 4), cc = tid & 15;
+    whs[tid] = (ff < D && cc < NC) ? a.wh[(size_t)ff * NC + cc] : 0.f;
   }
-  for (int e = tid; e < Dp * 16; e += kHeadThreads) {
-    const int f = e >> 4, c = e & 15;
-    whs[e] = (f < D && c < NC) ? a.wh[(size_t)f * NC + c] : 0.f;
-  }
-  if (tid < 16) bhs[tid] = tid < NC ? a.bh[tid] : 0.f;
-  __syncthreads();
-
-  const int ksteps = Dp / 16;   // per K quarter: Dp/4 features = Dp/16 steps of 4
-  f32x4 gw = {0.f, 0.f, 0.f, 0.f};   // dWh tile of waves 0..Dp/16-1
-  float gb = 0.f, la = 0.f, ca = 0.f, na = 0.f;
-  for (int b0 = 0; b0 < B; b0 += 64) {
-    const int nb = min(64, B - b0);
-    // ---- row block: post-dropout activation
-    for (int e = tid; e < 64 * Dp; e += kHeadThreads) {
-      const int r = e / Dp, f = e - r * Dp;
-      float v = 0.f;
-      if (r < nb && f < D) {
-        const float x = a.h[(size_t)(b0 + r) * Dp + f];
-        v = fmaxf(fmaf(x, sc[f], sh[f]), 0.f);
-        if (a.drop_on) v *= keep_scale(a.rate, a.seed, it, a.layer_id, (long long)(b0 + r) * D + f);
-      }
-      as[r * HLD + f] = v;
-    }
-    if (tid < 64) labs[tid] = (tid < nb && a.labels) ? a.labels[b0 + tid] : 0;
-    __syncthreads();
-    // ---- logits [64][16] = as . Wh: wave = (row tile rt = w & 3, K quarter kq = w >> 2)
-    f32x4 lg = {0.f, 0.f, 0.f, 0.f};
+  const bool batch = a.bn.mode == kBnTrain || a.bn.mode == kBnBatch;
+  // ---- pass 1: sums over the batch (rows rg + 16u of 128-row blocks); the first block stays in registers
+  float hv[8];
+  double s = 0.0, s2 = 0.0;
+  for (int b0 = 0; b0 < B; b0 += 128) {
+    float v[8];
     {
-      const int rt = wave & 3, kq = wave >> 2;
-      for (int s = 0; s < ksteps; ++s) {
-        const int k = kq * (Dp / 4) + 4 * s + fq;
-        lg = mfma4(as[(rt * 16 + fr) * HLD + k], whs[k * 16 + fr], lg);
-      }
-      if (kq > 0) *reinterpret_cast<f32x4*>(part + (((kq - 1) * 4 + rt) * 64 + lane) * 4) = lg;
-    }
-    __syncthreads();
-    if (wave < 4) {
-      const int rt = wave;
+      float pv[8][kMaxKc];   // every partial of the 8 rows in flight at once (clamped, branch-free)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        const f32x4 pv = *reinterpret_cast<const f32x4*>(part + ((q * 4 + rt) * 64 + lane) * 4);
-        lg += pv;
+      for (int u = 0; u < 8; ++u) {
+        const int r = min(b0 + rg + 16 * u, B - 1);
+#pragma unroll
+        for (int q = 0; q < kMaxKc; ++q)
+          pv[u][q] = a.hpart[((size_t)min(q, a.nkc - 1) * B + r) * Dp + f];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int r = b0 + rg + 16 * u;
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < kMaxKc; ++q) t += q < a.nkc ? pv[u][q] : 0.f;
+        v[u] = (r < B && fok) ? t : 0.f;
+        if (r < B && f < Dp) a.h[(size_t)r * Dp + f] = v[u];
+      }
+    }
+    if (b0 == 0) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) hv[u] = v[u];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      s += v[u];
+      s2 += (double)v[u] * v[u];
+    }
+  }
+  red[0][rg][c] = s;
+  red[1][rg][c] = s2;
+  __syncthreads();
+  if (tid < 16) {
+    const int ft = f0 + tid;
+    float mean = 0.f, rstd = 1.f;
+    if (ft < D) {
+      if (batch) {
+        double S = 0.0, S2 = 0.0;
+        for (int q = 0; q < 16; ++q) {
+          S += red[0][q][tid];
+          S2 += red[1][q][tid];
+        }
+        const double m = S / B, v = fmax(S2 / B - m * m, 0.0);
+        mean = (float)m;
+        rstd = (float)(1.0 / sqrt(v + (double)a.bn.eps));
+        if (a.bn.mode == kBnTrain) {
+          a.bn.saved[ft] = mean;
+          a.bn.saved[D + ft] = rstd;
+          a.bn.mmean[ft] = a.bn.mmean[ft] * a.bn.momentum + mean * (1.f - a.bn.momentum);
+          a.bn.mvar[ft] = a.bn.mvar[ft] * a.bn.momentum + (float)v * a.bn.bessel * (1.f - a.bn.momentum);
+        }
+      } else {
+        mean = a.bn.mmean[ft];
+        rstd = rsqrtf(a.bn.mvar[ft] + a.bn.eps);
+      }
+    }
+    const float g = (ft < D && a.bn.gamma) ? a.bn.gamma[ft] : 1.f;
+    sc[tid] = ft < D ? g * rstd : 0.f;
+    sh[tid] = ft < D ? (a.bn.beta ? a.bn.beta[ft] : 0.f) - mean * g * rstd : 0.f;
+  }
+  lds_barrier();
+  // ---- pass 2: activation of 128-row blocks -> LDS -> logits share (wave: row tiles wave, wave + 4)
+  for (int b0 = 0; b0 < B; b0 += 128) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = b0 + rg + 16 * u;
+      v[u] = b0 == 0 ? hv[u] : ((r < B && fok) ? a.h[(size_t)r * Dp + f] : 0.f);   // this thread's own stores
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = b0 + rg + 16 * u;
+      float act = 0.f;
+      if (r < B && fok) {
+        act = fmaxf(fmaf(v[u], sc[c], sh[c]), 0.f);
+        if (a.drop_on) act *= keep_scale(a.rate, a.seed, it, a.layer_id, (long long)r * D + f);
+      }
+      As[(rg + 16 * u) * 17 + c] = act;
+    }
+    lds_barrier();
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int rt = wave + 4 * j;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const int k = 4 * st + fq;
+        acc = mfma4(As[(rt * 16 + fr) * 17 + k], whs[k * 16 + fr], acc);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int r = rt * 16 + fq * 4 + i;
-        const bool valid = r < nb, cv = fr < NC;
-        const float z = cv ? lg[i] + bhs[fr] : -3.0e38f;
-        const float m = row16_max(z);
-        const float ex = cv ? __expf(z - m) : 0.f;
-        const float s = row16_sum(ex);
-        const float pr = ex / s;
-        const int label = labs[r];
-        const int amx = row16_min(cv && z == m ? fr : 64);
-        const float zl = __shfl(z, (lane & ~15) | (label & 15), 64);
-        if (valid && fr == 0) {
-          la += __logf(s) + m - zl;
-          ca += (amx == label) ? 1.f : 0.f;
-          na += 1.f;
-        }
-        if (a.mode == 2 && valid && cv) a.out[(size_t)(b0 + r) * NC + fr] = a.out_softmax ? pr : z;
-        dls[r * 16 + fr] = (train && valid && cv) ? (pr - (fr == label ? 1.f : 0.f)) * a.scale : 0.f;
+        const int r = b0 + rt * 16 + fq * 4 + i;
+        if (r < B) a.logits[((size_t)blockIdx.x * B + r) * 16 + fr] = acc[i];
       }
     }
-    __syncthreads();
-    if (train) {
-      // dWh tile (features w*16.., classes) += as^T . dl; wave ksteps*4..: dbh
-      if (wave < Dp / 16) {
-        for (int s = 0; s < 16; ++s) {
-          const int r = 4 * s + fq;
-          gw = mfma4(as[r * HLD + wave * 16 + fr], dls[r * 16 + fr], gw);
-        }
-      } else if (wave == 15) {
-        for (int r = fq; r < 64; r += 4) gb += dls[r * 16 + fr];
-      }
-      // g = dl . Wh^T, dropout, ReLU mask -> dh buffer (pre-BN-backward), sums of g and g*xhat
-      const int ntile = Dp / 16;
-      for (int t = wave; t < 4 * ntile; t += 16) {
-        const int mt = t / ntile, nt = t - mt * ntile;
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const int c = 4 * s + fq;
-          acc = mfma4(dls[(mt * 16 + fr) * 16 + c], whs[(nt * 16 + fr) * 16 + c], acc);
-        }
-        // lane holds g[row mt*16 + 4fq + i][feature nt*16 + fr]
-        const int f = nt * 16 + fr;
-        float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = mt * 16 + fq * 4 + i;
-          float gval = 0.f, xh = 0.f;
-          if (r < nb && f < D) {
-            const float act = as[r * HLD + f];
-            // act > 0 <=> ReLU passed AND dropout kept; the kept scale is 1/keep
-            if (act > 0.f) gval = a.drop_on ? acc[i] * (1.f / (1.f - a.rate)) : acc[i];
-            a.dh[(size_t)(b0 + r) * Dp + f] = gval;
-            xh = (a.h[(size_t)(b0 + r) * Dp + f] - mu[f]) * rs[f];
-          }
-          s1 += gval;
-          s2 += gval * xh;
-        }
-        s1 += __shfl_xor(s1, 16, 64);
-        s1 += __shfl_xor(s1, 32, 64);
-        s2 += __shfl_xor(s2, 16, 64);
-        s2 += __shfl_xor(s2, 32, 64);
-        if (fq == 0 && f < D) {
-          atomicAdd(sg + f, s1);
-          atomicAdd(sgx + f, s2);
-        }
-      }
-    }
-    __syncthreads();
+    lds_barrier();
   }
-  // ---- metrics
-  if (wave < 4) {
-    la = rows4_sum(la);
-    ca = rows4_sum(ca);
-    na = rows4_sum(na);
-    if (a.metrics && lane == 0 && na > 0.f) {
-      atomicAdd(a.metrics + 0, la);
-      atomicAdd(a.metrics + 1, ca);
-      atomicAdd(a.metrics + 2, na);
+  stamp(a.stamps, 3);
+}
+
+__global__ __launch_bounds__(NTH) void head_bwd_kernel(HeadArgs a) {
+  __shared__ float whs[16 * 16];           // [feature][class]
+  __shared__ float mu[16], rs[16], sc[16], sh[16], gm[16];
+  __shared__ float dls[64 * 16];
+  __shared__ float As[64 * 17], Xh[64 * 17];
+  __shared__ float sg[16], sgx[16];
+  __shared__ float part[4][256];
+  __shared__ float gbs[4][16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  const int c = tid & 15, rg = tid >> 4;
+  const int f0 = blockIdx.x * 16, f = f0 + c;
+  const int B = a.B, D = a.D, Dp = a.Dp, NC = a.NC;
+  const bool train = a.mode == 0, lead = blockIdx.x == 0, fok = f < D;
+  const long long it = a.iter ? *a.iter : 0;
+  stamp(a.stamps, 0);
+  if (train) {
+    const int ff = f0 + (tid >> 4), cc = tid & 15;
+    whs[tid] = (ff < D && cc < NC) ? a.wh[(size_t)ff * NC + cc] : 0.f;
+    if (tid < 16) {
+      const int ft = f0 + tid;
+      const float m = ft < D ? a.bn.saved[ft] : 0.f, r = ft < D ? a.bn.saved[D + ft] : 0.f;
+      const float g = (ft < D && a.bn.gamma) ? a.bn.gamma[ft] : 1.f;
+      mu[tid] = m;
+      rs[tid] = r;
+      gm[tid] = g;
+      sc[tid] = g * r;
+      sh[tid] = ft < D ? (a.bn.beta ? a.bn.beta[ft] : 0.f) - m * g * r : 0.f;
+      sg[tid] = 0.f;
+      sgx[tid] = 0.f;
+    }
+  }
+  const float bias = c < NC ? a.bh[c] : 0.f;
+  f32x4 gw = {0.f, 0.f, 0.f, 0.f};
+  float gb = 0.f, la = 0.f, ca = 0.f, na = 0.f, s1 = 0.f, s2 = 0.f;
+  lds_barrier();
+  for (int b0 = 0; b0 < B; b0 += 64) {
+    float hv[4], z[4];
+    int lab[4];
+    {
+      const int nlt = Dp / 16;
+      float lp[4][kHeadMaxTiles];   // the feature tiles' logits partials, all in flight (clamped)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = min(b0 + rg + 16 * u, B - 1);
+#pragma unroll
+        for (int q = 0; q < kHeadMaxTiles; ++q) lp[u][q] = a.logits[((size_t)min(q, nlt - 1) * B + r) * 16 + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = b0 + rg + 16 * u;
+        hv[u] = (train && r < B && fok) ? a.h[(size_t)r * Dp + f] : 0.f;
+        lab[u] = (r < B && a.labels) ? a.labels[r] : 0;
+        float t = 0.f;
+#pragma unroll
+        for (int q = 0; q < kHeadMaxTiles; ++q) t += q < nlt ? lp[u][q] : 0.f;
+        z[u] = t;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int rl = rg + 16 * u, r = b0 + rl;
+      const bool valid = r < B, cv = c < NC;
+      const float zz = cv ? z[u] + bias : -3.0e38f;
+      const float m = row16_max(zz);
+      const float ex = cv ? __expf(zz - m) : 0.f;
+      const float sum = row16_sum(ex);
+      const float pr = ex / sum;
+      const int label = lab[u];
+      const int amx = row16_min(cv && zz == m ? c : 64);
+      const float zl = __shfl(zz, (lane & ~15) | (label & 15), 64);
+      if (lead && valid && c == 0) {
+        la += __logf(sum) + m - zl;
+        ca += (amx == label) ? 1.f : 0.f;
+        na += 1.f;
+      }
+      if (a.mode == 2 && lead && valid && cv) a.out[(size_t)r * NC + c] = a.out_softmax ? pr : zz;
+      const float dl = (train && valid && cv) ? (pr - (c == label ? 1.f : 0.f)) * a.scale : 0.f;
+      dls[rl * 16 + c] = dl;
+      gb += dl;
+      if (train) {
+        float act = 0.f, xh = 0.f;
+        if (valid && fok) {
+          xh = (hv[u] - mu[c]) * rs[c];
+          act = fmaxf(fmaf(hv[u], sc[c], sh[c]), 0.f);
+          if (a.drop_on) act *= keep_scale(a.rate, a.seed, it, a.layer_id, (long long)r * D + f);
+        }
+        As[rl * 17 + c] = act;
+        Xh[rl * 17 + c] = xh;
+      }
+    }
+    if (!train) continue;
+    lds_barrier();
+    // dWh^T tile [feature][class] += act^T . dl over this wave's 16 rows
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const int r = wave * 16 + 4 * st + fq;
+      gw = mfma4(As[r * 17 + fr], dls[r * 16 + fr], gw);
+    }
+    // g [row][feature] = dl . Wh^T through the dropout / ReLU masks
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const int k = 4 * st + fq;
+      acc = mfma4(dls[(wave * 16 + fr) * 16 + k], whs[fr * 16 + k], acc);
+    }
+    const int fg = f0 + fr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rl = wave * 16 + fq * 4 + i, r = b0 + rl;
+      if (r < B && fg < D) {
+        const float act = As[rl * 17 + fr];
+        // act > 0 <=> ReLU passed AND dropout kept; the kept scale is 1/keep
+        const float gv = act > 0.f ? (a.drop_on ? acc[i] * (1.f / (1.f - a.rate)) : acc[i]) : 0.f;
+        a.dh[(size_t)r * Dp + fg] = gv;
+        s1 += gv;
+        s2 += gv * Xh[rl * 17 + fr];
+      }
+    }
+    lds_barrier();
+  }
+  // ---- metrics and the bias gradient (workgroup 0)
+  if (lead) {
+    float l = la, cc = ca, n = na;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      l += __shfl_xor(l, o, 64);
+      cc += __shfl_xor(cc, o, 64);
+      n += __shfl_xor(n, o, 64);
+    }
+    if (a.metrics && lane == 0 && n > 0.f) {
+      atomicAdd(a.metrics + 0, l);
+      atomicAdd(a.metrics + 1, cc);
+      atomicAdd(a.metrics + 2, n);
     }
   }
   if (!train) return;
-  // ---- head gradients
-  if (wave < Dp / 16) {
+  gb += __shfl_xor(gb, 16, 64);
+  gb += __shfl_xor(gb, 32, 64);
+  if (fq == 0) gbs[wave][fr] = gb;
+  s1 += __shfl_xor(s1, 16, 64);
+  s1 += __shfl_xor(s1, 32, 64);
+  s2 += __shfl_xor(s2, 16, 64);
+  s2 += __shfl_xor(s2, 32, 64);
+  if (fq == 0) {
+    atomicAdd(sg + fr, s1);
+    atomicAdd(sgx + fr, s2);
+  }
+  *reinterpret_cast<f32x4*>(&part[wave][lane * 4]) = gw;
+  __syncthreads();   // LDS partials, and the g stores of every wave visible to the workgroup
+  if (wave == 0) {
+    f32x4 t = gw;
+#pragma unroll
+    for (int w = 1; w < 4; ++w) t += *reinterpret_cast<const f32x4*>(&part[w][lane * 4]);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int f = wave * 16 + fq * 4 + i;
-      if (f < D && fr < NC) a.dwh[(size_t)f * NC + fr] = gw[i];
+      const int fi = f0 + fq * 4 + i;
+      if (fi < D && fr < NC) a.dwh[(size_t)fi * NC + fr] = t[i];
     }
-  } else if (wave == 15) {
-    gb += __shfl_xor(gb, 16, 64);
-    gb += __shfl_xor(gb, 32, 64);
-    if (fq == 0 && fr < NC) a.dbh[fr] = gb;
   }
-  __syncthreads();   // the g stores of every wave are complete and visible to the workgroup
-  if (tid < D) {
-    if (a.dbeta) a.dbeta[tid] = sg[tid];
-    if (a.dgamma) a.dgamma[tid] = sgx[tid];
+  if (lead && tid < 16 && tid < NC) a.dbh[tid] = (gbs[0][tid] + gbs[1][tid]) + (gbs[2][tid] + gbs[3][tid]);
+  if (tid < 16 && f0 + tid < D) {
+    if (a.dbeta) a.dbeta[f0 + tid] = sg[tid];
+    if (a.dgamma) a.dgamma[f0 + tid] = sgx[tid];
   }
-  // ---- dL/dh = gamma * rstd * (g - mean(g) - xhat * mean(g * xhat))
+  // ---- dL/dh for the tile, 8 rows in flight per thread
   const float invB = 1.f / (float)B;
-  for (int e = tid; e < B * D; e += kHeadThreads) {
-    const int r = e / D, f = e - r * D;
-    const float g = a.dh[(size_t)r * Dp + f];
-    const float xh = (a.h[(size_t)r * Dp + f] - mu[f]) * rs[f];
-    const float gm = a.bn.gamma ? a.bn.gamma[f] : 1.f;
-    a.dh[(size_t)r * Dp + f] = gm * rs[f] * (g - sg[f] * invB - xh * sgx[f] * invB);
+  const float k1 = sg[c] * invB, k2 = sgx[c] * invB, kk = gm[c] * rs[c];
+  for (int b0 = 0; b0 < B; b0 += 128) {
+    float gv[8], xv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = b0 + rg + 16 * u;
+      gv[u] = (r < B && fok) ? a.dh[(size_t)r * Dp + f] : 0.f;
+      xv[u] = (r < B && fok) ? a.h[(size_t)r * Dp + f] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = b0 + rg + 16 * u;
+      if (r < B && fok) {
+        const float xh = (xv[u] - mu[c]) * rs[c];
+        a.dh[(size_t)r * Dp + f] = kk * (gv[u] - k1 - xh * k2);
+      }
+    }
   }
+  stamp(a.stamps, 3);
 }
 
 // ------------------------------------------------------------------------------------------------
-// Dense backward: grid (ceil(K/16), 2).  role 0: dW[k-tile][0..D) = relu(BN(in))^T . dh;
-// role 1: dA = dh . W^T for the k-tile -> g = dA * relu mask of the input BN, the input BN's backward
-// partial sums (per k-tile workgroup, per channel).  Row blocks of 64 (dh staged per block).
+// Dense backward: grid (ceil(K/32), ceil(B/64)): one 32-feature K tile x one 64-row block per
+// workgroup, every load in one batch.
+//   waves 0-7   dA[64 rows][32] = dh . W^T (row tile w & 3, K half w >> 2) -> g = dA * ReLU mask of
+//               the input BN, and that BN's backward sums
+//   waves 8-15  the row block's dW partial [32][Dp] = A^T . dh (K half x 16-column tiles); the reduce
+//               launch sums the row blocks in order
+constexpr int kUDh = 16, kUWk = 8;   // dh block 64 x Dp <= 16384, W rows 32 x D <= 8192
 struct DenseBwdArgs {
   int B, K, D, Dp, ldh;
   const float* in; Bn bn;           // the input layer's raw output and its BN (kBnSaved)
   const float* w;                   // [K][D]
   const float* dh;                  // [B][Dp]
-  float* dw;                        // [K][D] (gradient bucket)
+  float* dwpart;                    // [ceil(B/64)][K][D]
   float* g;                         // [B][K]
-  float *psg, *psgx;                // [gridDim.x][C]
+  double* acc;                      // [kSlots][2][C] BN backward sums of the input layer
+  long long* stamps;
 };
 
-__global__ __launch_bounds__(NTH) void dense_bwd_kernel(DenseBwdArgs a) {
+__global__ __launch_bounds__(NTB) void dense_bwd_kernel(DenseBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
-  const int C = a.bn.C, CP = (C + 3) & ~3;
-  double* red = reinterpret_cast<double*>(sm);
-  float* st = reinterpret_cast<float*>(sm + 2 * NTH * 8);
-  float* dhs = st + 4 * CP;                   // [64][ldh]
-  float* tile = dhs + 64 * a.ldh;             // role 0: A^T block [64][17]; role 1: W rows [16][ldh]
-  float* csum = tile + 16 * a.ldh;            // [2][CP]
+  const int C = a.bn.C, K = a.K, D = a.D, Dp = a.Dp, ldh = a.ldh;
+  double* cs = reinterpret_cast<double*>(sm);             // [8][2][32]
+  float* st = reinterpret_cast<float*>(sm + 16 * 2 * 32 * 8);
+  float* Wk = st + 4 * 32;                                 // [32][ldh]
+  float* dhs = Wk + 32 * ldh;                              // [64][ldh]
+  float* Ab = dhs + 64 * ldh;                              // [64][33] relu(BN(in))
+  float* Xb = Ab + 64 * 33;                                // [64][33] raw in
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
-  const int kt = blockIdx.x, role = blockIdx.y, K = a.K, D = a.D, Dp = a.Dp;
-  bn_prepare(a.bn, st, red, false);
+  const int kt0 = blockIdx.x * 32, b0 = blockIdx.y * 64, nb = min(64, a.B - b0);
+  stamp(a.stamps, 0);
+  Pf<kUWk> pw;
+  Pf<kUDh> pd;
+  Pf<2> px;
+  pf_load(pw, 32 * D, [&](int e) { return a.w[(size_t)min(kt0 + e / D, K - 1) * D + e % D]; });
+  pf_load(pd, 64 * Dp, [&](int e) { return a.dh[(size_t)min(b0 + e / Dp, a.B - 1) * Dp + e % Dp]; });
+  pf_load(px, 64 * 32, [&](int e) { return a.in[(size_t)min(b0 + (e >> 5), a.B - 1) * K + min(kt0 + (e & 31), K - 1)]; });
+  bn_prepare(a.bn, st, false, nullptr);
+  stamp(a.stamps, 1);
   const float* sc = st;
   const float* sh = st + C;
   const float* mu = st + 2 * C;
   const float* rs = st + 3 * C;
-  const int ntile = Dp / 16;
-  if (role == 0) {
-    f32x4 acc[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int b0 = 0; b0 < a.B; b0 += 64) {
-      const int nb = min(64, a.B - b0);
-      __syncthreads();
-      for (int e = tid; e < 64 * Dp; e += NTH) {
-        const int r = e / Dp, n = e - r * Dp;
-        dhs[r * a.ldh + n] = r < nb ? a.dh[(size_t)(b0 + r) * Dp + n] : 0.f;
-      }
-      for (int e = tid; e < 64 * 16; e += NTH) {
-        const int r = e >> 4, kk = e & 15, k = kt * 16 + kk;
-        float v = 0.f;
-        if (r < nb && k < K) {
-          const int c = k % C;
-          v = fmaxf(fmaf(a.in[(size_t)(b0 + r) * K + k], sc[c], sh[c]), 0.f);
-        }
-        tile[r * 17 + kk] = v;
-      }
-      __syncthreads();
-      for (int s = 0; s < 16; ++s) {
-        const int r = 4 * s + fq;
-        const float av = tile[r * 17 + fr];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int nt = wave + 4 * j;
-          if (nt < ntile) acc[j] = mfma4(av, dhs[r * a.ldh + nt * 16 + fr], acc[j]);
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int nt = wave + 4 * j;
-      if (nt >= ntile) continue;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int k = kt * 16 + fq * 4 + i, n = nt * 16 + fr;
-        if (k < K && n < D) a.dw[(size_t)k * D + n] = acc[j][i];
-      }
-    }
-    return;
-  }
-  // role 1
-  for (int e = tid; e < 16 * Dp; e += NTH) {
-    const int kk = e / Dp, n = e - kk * Dp, k = kt * 16 + kk;
-    tile[kk * a.ldh + n] = (k < K && n < D) ? a.w[(size_t)k * D + n] : 0.f;
-  }
-  for (int c = tid; c < 2 * CP; c += NTH) csum[c] = 0.f;
-  const int k = kt * 16 + fr;
-  const int ck = k % C;
-  float s1 = 0.f, s2 = 0.f;
-  for (int b0 = 0; b0 < a.B; b0 += 64) {
-    const int nb = min(64, a.B - b0);
-    __syncthreads();
-    for (int e = tid; e < 64 * Dp; e += NTH) {
-      const int r = e / Dp, n = e - r * Dp;
-      dhs[r * a.ldh + n] = r < nb ? a.dh[(size_t)(b0 + r) * Dp + n] : 0.f;
-    }
-    __syncthreads();
+  pf_store(pw, 32 * D, [&](int e, float v) {
+    const int kk = e / D, n = e - kk * D;
+    Wk[kk * ldh + n] = kt0 + kk < K ? v : 0.f;
+  });
+  for (int e = tid; e < 32 * (Dp - D); e += NTB) Wk[(e / (Dp - D)) * ldh + D + e % (Dp - D)] = 0.f;
+  pf_store(pd, 64 * Dp, [&](int e, float v) {
+    const int r = e / Dp, n = e - r * Dp;
+    dhs[r * ldh + n] = r < nb ? v : 0.f;
+  });
+  pf_store(px, 64 * 32, [&](int e, float v) {
+    const int r = e >> 5, kk = e & 31, c = (kt0 + kk) % C;
+    const bool ok = r < nb && kt0 + kk < K;
+    Xb[r * 33 + kk] = ok ? v : 0.f;
+    Ab[r * 33 + kk] = ok ? fmaxf(fmaf(v, sc[c], sh[c]), 0.f) : 0.f;
+  });
+  lds_barrier();
+  stamp(a.stamps, 2);
+  if (wave < 8) {
+    const int rt = wave & 3, kh = wave >> 2;
+    const int k_me = kt0 + kh * 16 + fr, c_me = k_me % C;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < Dp / 4; ++s) {
-      const int n = 4 * s + fq;
-      acc = mfma4(dhs[(wave * 16 + fr) * a.ldh + n], tile[fr * a.ldh + n], acc);
+    for (int s0 = 0; s0 < Dp / 4; s0 += 4) {   // Dp % 16 == 0
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int n = 4 * (s0 + u) + fq;
+        acc = mfma4(dhs[(rt * 16 + fr) * ldh + n], Wk[(kh * 16 + fr) * ldh + n], acc);
+      }
     }
-    // lane: dA[row wave*16 + 4fq + i][feature kt*16 + fr]
+    // lane: dA[row rt*16 + 4fq + i][feature k_me]
+    float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int r = wave * 16 + fq * 4 + i;
-      if (r < nb && k < K) {
-        const float x = a.in[(size_t)(b0 + r) * K + k];
-        const float pre = fmaf(x, sc[ck], sh[ck]);
-        const float gv = pre > 0.f ? acc[i] : 0.f;
-        a.g[(size_t)(b0 + r) * K + k] = gv;
+      const int r = rt * 16 + fq * 4 + i;
+      if (r < nb && k_me < K) {
+        const float x = Xb[r * 33 + kh * 16 + fr];
+        const float gv = fmaf(x, sc[c_me], sh[c_me]) > 0.f ? acc[i] : 0.f;
+        a.g[(size_t)(b0 + r) * K + k_me] = gv;
         s1 += gv;
-        s2 += gv * (x - mu[ck]) * rs[ck];
+        s2 += gv * (x - mu[c_me]) * rs[c_me];
+      }
+    }
+    s1 += __shfl_xor(s1, 16, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 16, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    if (fq == 0) {
+      cs[(wave * 2 + 0) * 32 + fr] = s1;
+      cs[(wave * 2 + 1) * 32 + fr] = s2;
+    }
+  } else {
+    const int ntd = Dp / 16;
+    float* dst = a.dwpart + (size_t)blockIdx.y * K * D;
+    for (int item = wave - 8; item < 2 * ntd; item += 8) {
+      const int kh = item & 1, dt = item >> 1;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int st4 = 0; st4 < 16; ++st4) {
+        const int r = 4 * st4 + fq;
+        acc = mfma4(Ab[r * 33 + kh * 16 + fr], dhs[r * ldh + dt * 16 + fr], acc);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = kt0 + kh * 16 + fq * 4 + i, n = dt * 16 + fr;
+        if (k < K && n < D) dst[(size_t)k * D + n] = acc[i];
       }
     }
   }
-  s1 += __shfl_xor(s1, 16, 64);
-  s1 += __shfl_xor(s1, 32, 64);
-  s2 += __shfl_xor(s2, 16, 64);
-  s2 += __shfl_xor(s2, 32, 64);
-  __syncthreads();
-  if (fq == 0 && k < K) {
-    atomicAdd(csum + ck, s1);
-    atomicAdd(csum + CP + ck, s2);
+  // BN backward sums: feature f of wave w -> channel (kt0 + (w >> 2) * 16 + f) % C
+  lds_barrier();
+  if (tid < 2 * C) {
+    const int j = tid / C, c = tid - j * C;
+    double S = 0.0;
+    for (int w = 0; w < 8; ++w)
+      for (int f = 0; f < 16; ++f) {
+        const int k = kt0 + (w >> 2) * 16 + f;
+        if (k < K && k % C == c) S += cs[(w * 2 + j) * 32 + f];
+      }
+    atomicAdd(a.acc + my_slot() * 2 * C + j * C + c, S);
   }
-  __syncthreads();
-  for (int c = tid; c < C; c += NTH) {
-    a.psg[(size_t)kt * C + c] = csum[c];
-    a.psgx[(size_t)kt * C + c] = csum[CP + c];
-  }
+  stamp(a.stamps, 3);
 }
 
 // ------------------------------------------------------------------------------------------------
-// Conv backward: grid (B, n_dg + n_wg).  Prologue of every role: this layer's BN backward sums
-// (from the consumer's partials) and dZ = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) of the image
-// into a zero-bordered LDS grid.
-//   dgrad role y < n_dg: stride class (ry, rx) = (y / dg_chunks) of the input pixels, chunk of its
-//     16-pixel tiles; K = the taps that hit that class x Co; -> g of the previous layer's BN output
-//     (ReLU mask applied) + that BN's backward partial sums (per workgroup, per channel)
-//   wgrad role: a chunk of 16-row tiles of dW (rows = (kh, kw, ci)); K = the image's output pixels;
-//     the input image staged with the previous BN + ReLU as in the forward -> per-image partial dW.
-struct ConvBwdArgs {
+// Conv backward: grid B (one image per workgroup).  dZ of the image in a zero-bordered LDS grid;
+// work items over the 16 waves:
+//   input gradient (when wanted): (stride class, 16-pixel tile of that class) -> K = the taps that hit
+//     the class x Co; -> g of the previous layer (its ReLU mask) + that BN's backward sums
+//   weight gradient: (16-row K tile, pixel split) -> K = the image's output pixels; split partials
+//     summed through LDS in a fixed order -> the image's partial dW
+struct ConvBwdP {
   Geo g;
+  int K, Mo, Hp, Wp, Hd, Wd, Ph, Pw, zslot, dgrad, nci, nco, CP16;
+  int ncls, cls_nth[kMaxCls], cls_ntw[kMaxCls], cls_Kc[kMaxCls], cls_Kc16[kMaxCls], cls_wc[kMaxCls],
+      cls_ko[kMaxCls], cls_Mc[kMaxCls], cls_W[kMaxCls], cls_ih0[kMaxCls], cls_iw0[kMaxCls], cls_item0[kMaxCls + 1];
+  int n_dg_items, wg_tiles, wg_split, wg_spp, Kw16, n_items;
+  int o_cs, o_st, o_stin, o_kk, o_dz, o_xs, o_xr, o_wc, o_kod, o_kow, o_ptab, o_part, o_red, lds;
+};
+struct ConvBwdArgs {
+  ConvBwdP p;
   int B;
   const float* z; Bn bn; BnBwd bb; const float* gout; float count;   // this layer (count = B*Ho*Wo)
   const float* w;
-  const float* in; Bn bn_in; float* gin; float *psg_in, *psgx_in;     // the input side
+  const float* in; Bn bn_in; float* gin; double* acc_in;             // the input side
   float* dwpart;                     // [B][K][Co]
-  int n_dg, n_wg, dg_chunks, Ph, Pw, Hd, Wd, Hp, Wp, TPW_dg, TPW_wg;
+  double* zero; int nzero;           // the backward sums of the layer after this one (consumed)
+  long long* stamps;
 };
 
-struct ConvBwdLds {
-  int red, st, stin, kk, dz, xs, wc, koff, ptab, csum, total;
-};
-__host__ __device__ inline ConvBwdLds conv_bwd_lds(const Geo& g, int Hd, int Wd, int Hp, int Wp) {
-  ConvBwdLds L{};
-  const int CoP = (g.Co + 3) & ~3, CP = (g.C + 3) & ~3;
-  const int K = g.kh * g.kw * g.C, Kp = (K + 15) & ~15;
-  const int ntah = (g.kh + g.sh - 1) / g.sh, ntaw = (g.kw + g.sw - 1) / g.sw;
-  const int Kc = ((ntah * ntaw * g.Co + 3) & ~3);
-  int o = 0;
-  L.red = o; o += 2 * NTH * 8;
-  L.st = o; o += 4 * CoP * 4;
-  L.stin = o; o += 4 * CP * 4;
-  L.kk = o; o += 2 * CoP * 4;
-  L.dz = o; o += (Hd * Wd * g.Co + 16) * 4;
-  L.xs = o; o += ((Hp * Wp * g.C + 3) & ~3) * 4;
-  L.wc = o; o += Kc * ((g.C + 15) & ~15) * 4;
-  L.koff = o; o += (Kp > Kc ? Kp : Kc) * 4;
-  L.ptab = o; o += 2 * ((g.Ho * g.Wo + 3) & ~3) * 4;
-  L.csum = o; o += 2 * CP * 4;
-  L.total = o;
-  return L;
-}
-
-__global__ __launch_bounds__(NTH) void conv_bwd_kernel(ConvBwdArgs a) {
+__global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
-  const Geo g = a.g;
-  const ConvBwdLds L = conv_bwd_lds(g, a.Hd, a.Wd, a.Hp, a.Wp);
-  double* red = reinterpret_cast<double*>(sm + L.red);
-  float* st = reinterpret_cast<float*>(sm + L.st);
-  float* stin = reinterpret_cast<float*>(sm + L.stin);
-  float* kks = reinterpret_cast<float*>(sm + L.kk);
-  float* dz = reinterpret_cast<float*>(sm + L.dz);
-  float* Xs = reinterpret_cast<float*>(sm + L.xs);
-  float* Wc = reinterpret_cast<float*>(sm + L.wc);
-  int* koff = reinterpret_cast<int*>(sm + L.koff);
-  int* ptab = reinterpret_cast<int*>(sm + L.ptab);
-  float* csum = reinterpret_cast<float*>(sm + L.csum);
+  const ConvBwdP& P = a.p;
+  const Geo& g = P.g;
+  double* cs = reinterpret_cast<double*>(sm + P.o_cs);
+  double* red = reinterpret_cast<double*>(sm + P.o_red);
+  float* st = reinterpret_cast<float*>(sm + P.o_st);       // this BN: mean, rstd, gamma*rstd
+  float* stin = reinterpret_cast<float*>(sm + P.o_stin);   // input BN: sc, sh, mean, rstd
+  float* kks = reinterpret_cast<float*>(sm + P.o_kk);      // sum g, sum g*xhat
+  float* dz = reinterpret_cast<float*>(sm + P.o_dz);
+  float* Xs = reinterpret_cast<float*>(sm + P.o_xs);
+  float* Xr = reinterpret_cast<float*>(sm + P.o_xr);
+  float* Wc = reinterpret_cast<float*>(sm + P.o_wc);
+  int* kod = reinterpret_cast<int*>(sm + P.o_kod);
+  int* kow = reinterpret_cast<int*>(sm + P.o_kow);
+  int2* ptab = reinterpret_cast<int2*>(sm + P.o_ptab);
+  float* part = reinterpret_cast<float*>(sm + P.o_part);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
-  const int b = blockIdx.x, y = blockIdx.y;
-  const int C = g.C, Co = g.Co, Mo = g.Ho * g.Wo, K = g.kh * g.kw * C;
-  const int Wd = a.Wd;
-  const bool writer = b == 0 && y == 0;
-
-  bn_prepare(a.bn, st, red, false);
-  bnbwd_prepare(a.bb, Co, kks, red, writer);
-  // dZ of this image into the bordered grid (borders stay zero)
+  const int b = blockIdx.x;
+  const int C = g.C, Co = g.Co, Mo = P.Mo, K = P.K, Wd = P.Wd, Wp = P.Wp, CP16 = P.CP16;
+  stamp(a.stamps, 0);
+  // ---- one batch of global loads
+  const int nact = Mo * Co, nimg = g.H * g.W * C, nw = K * Co;
+  Pf<kUAct> pg, pz;
+  Pf<kUW> pw;
+  Pf<kUImg> px;
   {
-    const float* mu = st + 2 * Co;
-    const float* rs = st + 3 * Co;
-    const float inv = 1.f / a.count;
-    const int nd = a.Hd * Wd * Co;
-    for (int e = tid; e < nd + 16; e += NTH) dz[e] = 0.f;
-    __syncthreads();
-    const float* gz = a.gout + (size_t)b * Mo * Co;
-    const float* zz = a.z + (size_t)b * Mo * Co;
-    for (int e = tid; e < Mo * Co; e += NTH) {
-      const int co = e % Co, p = e / Co, oh = p / g.Wo, ow = p - oh * g.Wo;
-      const float xh = (zz[e] - mu[co]) * rs[co];
-      const float gm = a.bn.gamma ? a.bn.gamma[co] : 1.f;
-      const float v = gm * rs[co] * (gz[e] - kks[co] * inv - xh * kks[Co + co] * inv);
-      dz[((oh + a.Ph) * Wd + ow + a.Pw) * Co + co] = v;
+    const float* gz = a.gout + (size_t)b * nact;
+    const float* zz = a.z + (size_t)b * nact;
+    const float* im = a.in + (size_t)b * nimg;
+    pf_load(pg, nact, [&](int i) { return gz[i]; });
+    pf_load(pz, nact, [&](int i) { return zz[i]; });
+    if (P.dgrad) pf_load(pw, nw, [&](int i) { return a.w[i]; });
+    pf_load(px, nimg, [&](int i) { return im[i]; });
+  }
+  // the per-channel constants: slot partials of this layer's backward sums, saved statistics
+  const int Q = 2 * Co, np = NTB / Q, qq = tid % Q, qpart = tid / Q;
+  double sv[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int j = qpart + u * np;
+    sv[u] = (qpart < np && j < kSlots) ? a.bb.acc[j * Q + qq] : 0.0;
+  }
+  float cmu = 0.f, crs = 0.f, cg = 1.f;
+  if (tid < Co) {
+    cmu = a.bn.saved[tid];
+    crs = a.bn.saved[Co + tid];
+    cg = a.bn.gamma ? a.bn.gamma[tid] : 1.f;
+  }
+  float imu = 0.f, irs = 1.f, ig = 1.f, ib = 0.f;
+  const int ti = tid - 64;
+  if (ti >= 0 && ti < C && a.bn_in.mode == kBnSaved) {
+    imu = a.bn_in.saved[ti];
+    irs = a.bn_in.saved[C + ti];
+    ig = a.bn_in.gamma ? a.bn_in.gamma[ti] : 1.f;
+    ib = a.bn_in.beta ? a.bn_in.beta[ti] : 0.f;
+  }
+  zero_share(a.zero, a.nzero);
+  // LDS the registers do not cover
+  for (int i = tid; i < P.Hd * Wd; i += NTB) {
+    const int y = i / Wd, x = i - y * Wd;
+    if (y < P.Ph || y >= P.Ph + g.Ho || x < P.Pw || x >= P.Pw + g.Wo)
+      for (int c = 0; c < Co; ++c) dz[i * Co + c] = 0.f;
+  }
+  if (tid < 32) dz[P.zslot + tid] = 0.f;
+  for (int i = tid; i < P.Hp * Wp; i += NTB) {
+    const int y = i / Wp, x = i - y * Wp, iy = y - g.pt, ix = x - g.pl;
+    if (iy < 0 || iy >= g.H || ix < 0 || ix >= g.W)
+      for (int c = 0; c < C; ++c) Xs[i * C + c] = 0.f;
+  }
+  if (P.dgrad) {
+    for (int cl = 0; cl < P.ncls; ++cl) {
+      const int Kc = P.cls_Kc[cl], Kc16 = P.cls_Kc16[cl], ntw = P.cls_ntw[cl];
+      float* wc = Wc + P.cls_wc[cl];
+      for (int i = tid; i < Kc16 * CP16; i += NTB) {
+        const int kk = i / CP16, ci = i - kk * CP16;
+        if (kk >= Kc || ci >= C) wc[i] = 0.f;
+      }
+      for (int kk = tid; kk < Kc16; kk += NTB) {
+        int off = 0;
+        if (kk < Kc) {
+          const int co = kk % Co, t = kk / Co, jw = t % ntw, jh = t / ntw;
+          off = (-jh * Wd - jw) * Co + co;
+        }
+        kod[P.cls_ko[cl] + kk] = off;
+      }
     }
   }
-  bn_prepare(a.bn_in, stin, red, false);   // (barrier: dz complete)
-
-  if (y < a.n_dg) {
-    // ---------------- input gradient of one stride class
-    const int cls = y / a.dg_chunks, chunk = y - cls * a.dg_chunks;
-    const int ry = cls / g.sw, rx = cls - ry * g.sw;
-    // input rows / cols of the class: (i + pt) % sh == ry
-    const int ih0 = ((ry - g.pt) % g.sh + g.sh) % g.sh, iw0 = ((rx - g.pl) % g.sw + g.sw) % g.sw;
-    const int Hc = ih0 < g.H ? (g.H - ih0 + g.sh - 1) / g.sh : 0;
-    const int Wc_ = iw0 < g.W ? (g.W - iw0 + g.sw - 1) / g.sw : 0;
-    const int Mc = Hc * Wc_;
-    const int nth = (g.kh - ry + g.sh - 1) / g.sh, ntw = (g.kw - rx + g.sw - 1) / g.sw;
-    const int Kc = nth * ntw * Co, Kcp = (Kc + 3) & ~3;
-    const int CP16 = (C + 15) & ~15;
-    for (int e = tid; e < Kcp * CP16; e += NTH) {
-      const int kk = e / CP16, ci = e - kk * CP16;
-      float v = 0.f;
-      if (kk < Kc && ci < C) {
-        const int co = kk % Co, t = kk / Co, jw = t % ntw, jh = t / ntw;
-        const int ky = ry + g.sh * jh, kx = rx + g.sw * jw;
-        v = a.w[(((size_t)ky * g.kw + kx) * C + ci) * Co + co];
-      }
-      Wc[e] = v;
+  for (int k = tid; k < P.Kw16; k += NTB) {
+    int off = 0;
+    if (k < K) {
+      const int ci = k % C, t = k / C, kx = t % g.kw, ky = t / g.kw;
+      off = (ky * Wp + kx) * C + ci;
     }
-    for (int kk = tid; kk < Kcp; kk += NTH) {
-      int off = 0;
-      if (kk < Kc) {
-        const int co = kk % Co, t = kk / Co, jw = t % ntw, jh = t / ntw;
-        off = (-jh * Wd - jw) * Co + co;
-      }
-      koff[kk] = off;
+    kow[k] = off;
+  }
+  for (int p = tid; p < P.wg_split * P.wg_spp * 4; p += NTB) {
+    int2 e{0, P.zslot};
+    if (p < Mo) {
+      const int oh = p / g.Wo, ow = p - oh * g.Wo;
+      e = int2{(oh * g.sh * Wp + ow * g.sw) * C, ((oh + P.Ph) * Wd + ow + P.Pw) * Co};
     }
-    for (int c = tid; c < 2 * ((C + 3) & ~3); c += NTH) csum[c] = 0.f;
-    __syncthreads();
-    const int TPW = a.TPW_dg;
-    const int NTc = CP16 / 16;
-    const int CPad = (C + 3) & ~3;
-    float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
-    for (int j = 0; j < TPW; ++j) {
-      const int tile = (chunk * 4 + wave) * TPW + j;
-      const int m = tile * 16 + fr;
-      const int mc = m < Mc ? m : 0;
-      const int ih = ih0 + (mc / Wc_) * g.sh, iw = iw0 + (mc % Wc_) * g.sw;
-      const int ohb = (ih + g.pt - ry) / g.sh, owb = (iw + g.pl - rx) / g.sw;
-      const int base = ((ohb + a.Ph) * Wd + owb + a.Pw) * Co;
-      f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-      for (int s = 0; s < Kcp / 4; ++s) {
-        const int kk = 4 * s + fq;
-        const float av = dz[base + koff[kk]];
+    ptab[p] = e;
+  }
+  if (qpart < np) red[tid] = (sv[0] + sv[1]) + (sv[2] + sv[3]);
+  if (tid < Co) {
+    st[tid] = cmu;
+    st[Co + tid] = crs;
+    st[2 * Co + tid] = cg * crs;
+  }
+  if (ti >= 0 && ti < C) {
+    const bool none = a.bn_in.mode == kBnNone;
+    stin[ti] = none ? 1.f : ig * irs;
+    stin[C + ti] = none ? 0.f : ib - imu * ig * irs;
+    stin[2 * C + ti] = imu;
+    stin[3 * C + ti] = irs;
+  }
+  lds_barrier();
+  if (tid < Q) {
+    double S = 0.0;
+    for (int p = 0; p < np; ++p) S += red[p * Q + tid];
+    kks[tid] = (float)S;
+    if (b == 0) {
+      if (tid < Co && a.bb.dbeta) a.bb.dbeta[tid] = (float)S;
+      if (tid >= Co && a.bb.dgamma) a.bb.dgamma[tid - Co] = (float)S;
+    }
+  }
+  lds_barrier();
+  stamp(a.stamps, 1);
+  // ---- registers -> LDS: dZ, the input (raw and BN + ReLU'd), the class-ordered weights
+  {
+    const float inv = 1.f / a.count;
 #pragma unroll
-        for (int n = 0; n < 2; ++n)
-          if (n < NTc) acc[n] = mfma4(av, Wc[kk * CP16 + n * 16 + fr], acc[n]);
+    for (int u = 0; u < kUAct; ++u) {
+      const int i = tid + u * NTB;
+      if (i < nact) {
+        const int co = i % Co, p = i / Co, oh = p / g.Wo, ow = p - oh * g.Wo;
+        const float xh = (pz.v[u] - st[co]) * st[Co + co];
+        dz[((oh + P.Ph) * Wd + ow + P.Pw) * Co + co] =
+            st[2 * Co + co] * (pg.v[u] - kks[co] * inv - xh * kks[Co + co] * inv);
       }
-      // lane: dA[class pixel tile*16 + 4fq + i][ci = n*16 + fr] -> g_in (ReLU mask of the input BN)
+    }
+    const bool raw = a.bn_in.mode == kBnNone;
+    pf_store(px, nimg, [&](int i, float v) {
+      const int c = i % C, pix = i / C, y = pix / g.W, x = pix - y * g.W;
+      Xs[((y + g.pt) * Wp + x + g.pl) * C + c] = raw ? v : fmaxf(fmaf(v, stin[c], stin[C + c]), 0.f);
+      Xr[i] = v;
+    });
+    if (P.dgrad)
+      pf_store(pw, nw, [&](int i, float v) {
+        const int co = i % Co, t = i / Co, ci = t % C, t2 = t / C, kx = t2 % g.kw, ky = t2 / g.kw;
+        const int cl = (ky % g.sh) * g.sw + (kx % g.sw), jh = ky / g.sh, jw = kx / g.sw;
+        const int kk = (jh * P.cls_ntw[cl] + jw) * Co + co;
+        Wc[P.cls_wc[cl] + kk * CP16 + ci] = v;
+      });
+  }
+  lds_barrier();
+  stamp(a.stamps, 2);
+  // ---- work items
+  double s1[2] = {0.0, 0.0}, s2[2] = {0.0, 0.0};
+  for (int item = wave; item < P.n_items; item += 16) {
+    if (item < P.n_dg_items) {
+      int cl = 0;
+      while (cl + 1 < P.ncls && item >= P.cls_item0[cl + 1]) ++cl;
+      const int tile = item - P.cls_item0[cl];
+      const int Mc = P.cls_Mc[cl], Wc_ = P.cls_W[cl], ih0 = P.cls_ih0[cl], iw0 = P.cls_iw0[cl];
+      const int ry = cl / g.sw, rx = cl - ry * g.sw;
+      const int m = min(tile * 16 + fr, Mc - 1);
+      const int ih = ih0 + (m / Wc_) * g.sh, iw = iw0 + (m % Wc_) * g.sw;
+      const int ohb = (ih + g.pt - ry) / g.sh, owb = (iw + g.pl - rx) / g.sw;
+      const int base = ((ohb + P.Ph) * Wd + owb + P.Pw) * Co;
+      const int* ko = kod + P.cls_ko[cl];
+      const float* wc = Wc + P.cls_wc[cl];
+      f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      for (int s0 = 0; s0 < P.cls_Kc16[cl] / 4; s0 += 4) {
+        int o[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[u] = ko[4 * (s0 + u) + fq];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int kk = 4 * (s0 + u) + fq;
+          const float av = dz[base + o[u]];
+          acc[0] = mfma4(av, wc[kk * CP16 + fr], acc[0]);
+          if (P.nci > 1) acc[1] = mfma4(av, wc[kk * CP16 + 16 + fr], acc[1]);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int mm = tile * 16 + fq * 4 + i;
@@ -999,110 +1116,108 @@ __global__ __launch_bounds__(NTH) void conv_bwd_kernel(ConvBwdArgs a) {
 #pragma unroll
         for (int n = 0; n < 2; ++n) {
           const int ci = n * 16 + fr;
-          if (n >= NTc || ci >= C) continue;
-          const size_t e = (((size_t)b * g.H + ih2) * g.W + iw2) * C + ci;
-          const float x = a.in[e];
-          const float pre = fmaf(x, stin[ci], stin[C + ci]);
-          const float gv = pre > 0.f ? acc[n][i] : 0.f;
-          a.gin[e] = gv;
+          if (n >= P.nci || ci >= C) continue;
+          const int e = (ih2 * g.W + iw2) * C + ci;
+          const float x = Xr[e];
+          const float gv = fmaf(x, stin[ci], stin[C + ci]) > 0.f ? acc[n][i] : 0.f;
+          a.gin[(size_t)b * nimg + e] = gv;
           s1[n] += gv;
-          s2[n] += gv * (x - stin[2 * C + ci]) * stin[3 * C + ci];
+          s2[n] += (double)(gv * (x - stin[2 * C + ci]) * stin[3 * C + ci]);
         }
       }
-    }
+    } else {
+      const int wi = item - P.n_dg_items, kt = wi % P.wg_tiles, sp = wi / P.wg_tiles;
+      const int off = kow[kt * 16 + fr];
+      f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      for (int s0 = 0; s0 < P.wg_spp; s0 += 4) {
+        int2 t[4];
 #pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      float v1 = s1[n], v2 = s2[n];
-      v1 += __shfl_xor(v1, 16, 64);
-      v1 += __shfl_xor(v1, 32, 64);
-      v2 += __shfl_xor(v2, 16, 64);
-      v2 += __shfl_xor(v2, 32, 64);
-      const int ci = n * 16 + fr;
-      if (fq == 0 && n < NTc && ci < C) {
-        atomicAdd(csum + ci, v1);
-        atomicAdd(csum + CPad + ci, v2);
+        for (int u = 0; u < 4; ++u) t[u] = ptab[4 * (sp * P.wg_spp + s0 + u) + fq];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float av = Xs[t[u].x + off];
+          acc[0] = mfma4(av, dz[t[u].y + fr], acc[0]);
+          if (P.nco > 1) acc[1] = mfma4(av, dz[t[u].y + 16 + fr], acc[1]);
+        }
+      }
+      if (P.wg_split == 1) {
+        float* dst = a.dwpart + (size_t)b * K * Co;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = kt * 16 + fq * 4 + i;
+#pragma unroll
+          for (int n = 0; n < 2; ++n) {
+            const int co = n * 16 + fr;
+            if (k < K && n < P.nco && co < Co) dst[(size_t)k * Co + co] = acc[n][i];
+          }
+        }
+      } else {
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+          if (n < P.nco)
+            *reinterpret_cast<f32x4*>(part + ((size_t)((sp * P.wg_tiles + kt) * P.nco + n) * 64 + lane) * 4) = acc[n];
       }
     }
-    __syncthreads();
-    const int wg = b * a.n_dg + y;
-    for (int c = tid; c < C; c += NTH) {
-      a.psg_in[(size_t)wg * C + c] = csum[c];
-      a.psgx_in[(size_t)wg * C + c] = csum[CPad + c];
-    }
-    return;
   }
-  // ---------------- weight gradient partial of this image: rows (kh, kw, ci) tiles of this chunk
-  const int chunk = y - a.n_dg;
-  const int TPW = a.TPW_wg;
-  const int Kp = (K + 15) & ~15;
-  const int Wp = a.Wp;
-  stage_image(g, a.in, b, a.bn_in.mode, stin, Xs, Wp, 0, a.Hp);
-  for (int k = tid; k < Kp; k += NTH) {
-    int off = 0;
-    if (k < K) {
-      const int ci = k % C, t = k / C, kx = t % g.kw, ky = t / g.kw;
-      off = (ky * Wp + kx) * C + ci;
-    }
-    koff[k] = off;
-  }
-  for (int p = tid; p < ((Mo + 3) & ~3); p += NTH) {
-    const int pc = p < Mo ? p : 0;
-    const int oh = pc / g.Wo, ow = pc - oh * g.Wo;
-    ptab[2 * p] = (oh * g.sh * Wp + ow * g.sw) * C;
-    ptab[2 * p + 1] = p < Mo ? ((oh + a.Ph) * Wd + ow + a.Pw) * Co : -1;
-  }
-  __syncthreads();
-  const int NTo = (Co + 15) / 16;
-  for (int j = 0; j < TPW; ++j) {
-    const int tile = (chunk * 4 + wave) * TPW + j;
-    if (tile * 16 >= K) break;
-    const int off = koff[tile * 16 + fr];
-    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    for (int s = 0; s < (Mo + 3) / 4; ++s) {
-      const int p = 4 * s + fq;
-      const int pb = ptab[2 * p], pz = ptab[2 * p + 1];
-      const float av = Xs[pb + off];
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        if (n >= NTo) continue;
-        const float bv = pz >= 0 ? dz[pz + n * 16 + fr] : 0.f;
-        acc[n] = mfma4(av, bv, acc[n]);
-      }
-    }
+  if (P.wg_split > 1) {
+    lds_barrier();
     float* dst = a.dwpart + (size_t)b * K * Co;
+    for (int t = wave; t < P.wg_tiles * P.nco; t += 16) {
+      const int kt = t / P.nco, n = t - kt * P.nco;
+      f32x4 v = *reinterpret_cast<const f32x4*>(part + ((size_t)(kt * P.nco + n) * 64 + lane) * 4);
+      for (int sp = 1; sp < P.wg_split; ++sp)
+        v += *reinterpret_cast<const f32x4*>(part + ((size_t)((sp * P.wg_tiles + kt) * P.nco + n) * 64 + lane) * 4);
+      const int co = n * 16 + fr;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int k = tile * 16 + fq * 4 + i;
-      if (k >= K) continue;
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        const int co = n * 16 + fr;
-        if (n < NTo && co < Co) dst[(size_t)k * Co + co] = acc[n][i];
+      for (int i = 0; i < 4; ++i) {
+        const int k = kt * 16 + fq * 4 + i;
+        if (k < K && co < Co) dst[(size_t)k * Co + co] = v[i];
       }
     }
   }
+  if (P.dgrad) wave_cols_to_slot(s1, s2, cs, a.acc_in, C);
+  stamp(a.stamps, 3);
 }
 
 // ------------------------------------------------------------------------------------------------
-// Per-image weight-gradient partials -> the flat gradient bucket, summed in image order.
+// Weight-gradient partials (per image for the convs, per row block for the dense layer) -> the flat
+// gradient bucket, summed in partial order.  Each workgroup owns 64 elements of one segment; its 4
+// waves take every 4th partial with up to 32 loads in flight per thread; fixed combine order.
 constexpr int kMaxRed = 4;
 struct ReduceArgs {
-  int n, B;
+  int n;
   const float* part[kMaxRed];
   float* out[kMaxRed];
   long long len[kMaxRed];
+  int cnt[kMaxRed];            // partials of the segment
+  int blk0[kMaxRed + 1];       // first workgroup of the segment
+  double* zero; int nzero;
+  long long* stamps;
 };
 __global__ __launch_bounds__(NTH) void reduce_kernel(ReduceArgs a) {
-  long long e = (long long)blockIdx.x * NTH + threadIdx.x;
-  for (int j = 0; j < a.n; ++j) {
-    if (e < a.len[j]) {
-      float s = 0.f;
-      for (int b = 0; b < a.B; ++b) s += a.part[j][(size_t)b * a.len[j] + e];
-      a.out[j][e] = s;
-      return;
-    }
-    e -= a.len[j];
+  __shared__ float red[4][64];
+  zero_share(a.zero, a.nzero);
+  const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
+  int j = 0;
+  while (j + 1 < a.n && (int)blockIdx.x >= a.blk0[j + 1]) ++j;
+  const long long len = a.len[j];
+  const long long e = (long long)(blockIdx.x - a.blk0[j]) * 64 + l;
+  const int cnt = a.cnt[j];
+  const float* p = a.part[j];
+  const long long ec = e < len ? e : len - 1;
+  float s = 0.f;
+  for (int b0 = q; b0 < cnt; b0 += 128) {
+    float v[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u)
+      if (b0 + 4 * u < cnt) v[u] = p[(size_t)(b0 + 4 * u) * len + ec];
+#pragma unroll
+    for (int u = 0; u < 32; ++u)
+      if (b0 + 4 * u < cnt) s += v[u];
   }
+  red[q][l] = s;
+  __syncthreads();
+  if (q == 0 && e < len) a.out[j][e] = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
 }
 
 }  // namespace bncnn
@@ -1115,207 +1230,302 @@ using namespace tde::bncnn;
 struct TdeBnGeo { int H, W, C, Ho, Wo, Co, kh, kw, sh, sw, pt, pl; };
 struct TdeBn {
   int mode, C;
-  const float *pmean, *pm2, *pn; int npart;
+  const double* acc; double count;
   const float *gamma, *beta;
   float eps, momentum, bessel;
   float *mmean, *mvar, *saved;
 };
+struct TdeBnBwd {
+  const double* acc;
+  float *dbeta, *dgamma;
+};
 static Geo geo_of(const TdeBnGeo* g) { return Geo{g->H, g->W, g->C, g->Ho, g->Wo, g->Co, g->kh, g->kw, g->sh, g->sw, g->pt, g->pl}; }
 static Bn bn_of(const TdeBn* b) {
-  return Bn{b->mode, b->C, b->pmean, b->pm2, b->pn, b->npart, b->gamma, b->beta, b->eps, b->momentum, b->bessel,
-            b->mmean, b->mvar, b->saved};
+  return Bn{b->mode, b->C, b->acc, b->count, b->gamma, b->beta, b->eps, b->momentum, b->bessel, b->mmean, b->mvar,
+            b->saved};
 }
 static bool bn_ok(const TdeBn* b) {
-  if (!b || b->C < 1 || b->C > NTH) return false;
-  if ((b->mode == kBnTrain || b->mode == kBnBatch) && (!b->pmean || !b->pm2 || !b->pn || b->npart < 1)) return false;
+  if (!b || b->C < 1 || b->C > 32) return false;
+  if ((b->mode == kBnTrain || b->mode == kBnBatch) && (!b->acc || !(b->count > 0))) return false;
   if (b->mode == kBnTrain && !b->saved) return false;
   if (b->mode == kBnMoving && (!b->mmean || !b->mvar)) return false;
   if (b->mode == kBnSaved && !b->saved) return false;
   return b->mode >= kBnNone && b->mode <= kBnSaved;
 }
 
+// Diagnostic phase clocks: after tde_bncnn_stamps(base, n), the next n launches record
+// stamps[launch][workgroup][slot] (s_memrealtime, 100 MHz) into base (kStampStride per launch).
+constexpr int kStampStride = 8192 * kMaxStamps;
+static long long* g_stamp_base = nullptr;
+static int g_stamp_next = 0, g_stamp_cap = 0;
+TDE_API void tde_bncnn_stamps(long long* base, int n) {
+  g_stamp_base = base;
+  g_stamp_next = 0;
+  g_stamp_cap = base ? n : 0;
+}
+static long long* next_stamps() {
+  if (!g_stamp_base || g_stamp_next >= g_stamp_cap) return nullptr;
+  return g_stamp_base + (size_t)(g_stamp_next++) * kStampStride;
+}
+
 template <typename F>
 static void set_lds(F* f, int bytes) {
   (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
+static int up(int x, int m) { return (x + m - 1) / m * m; }
+constexpr int kMaxLds = 160 * 1024;
 
-// tiles-per-wave / N tiles / K split of the forward conv, chosen by the host (see bncnn_conv_fwd)
-#define TDE_CONV_FWD_CFG(X) X(4, 1, 1) X(2, 1, 1) X(1, 1, 1) X(1, 2, 4) X(1, 1, 4) X(2, 2, 1) X(1, 2, 1)
+TDE_API int tde_bncnn_stat_slots() { return kSlots; }
 
-TDE_API int tde_bncnn_conv_fwd_lds(const TdeBnGeo* gg, int tpw, int nt, int ks) {
-  const Geo g = geo_of(gg);
-  const int Hp = (g.Ho - 1) * g.sh + g.kh, Wp = (g.Wo - 1) * g.sw + g.kw;
-  const int K = g.kh * g.kw * g.C, steps = (K + 3) / 4, Kp = ((steps + ks - 1) / ks) * ks * 4;
-#define X(T, N, S) if (tpw == T && nt == N && ks == S) return conv_fwd_lds<T, N, S>(Hp, Wp, g.C, Kp).total;
-  TDE_CONV_FWD_CFG(X)
-#undef X
-  return -1;
+// Forward conv launch geometry; 0 if it fits (LDS, prefetch registers), <0 otherwise.
+static int conv_fwd_plan(const Geo& g, ConvFwdP& P) {
+  P = ConvFwdP{};
+  P.g = g;
+  P.K = g.kh * g.kw * g.C;
+  P.M = g.Ho * g.Wo;
+  P.Hp = std::max((g.Ho - 1) * g.sh + g.kh, g.pt + g.H);
+  P.Wp = std::max((g.Wo - 1) * g.sw + g.kw, g.pl + g.W);
+  if (g.C < 1 || g.C > 32 || g.Co < 1 || g.Co > 32) return -1;
+  if (g.H * g.W * g.C > kUImg * NTB || P.K * g.Co > kUW * NTB) return -2;
+  P.nct = (g.Co + 15) / 16;
+  const int steps = (P.K + 3) / 4;
+  P.mt = (P.M + 15) / 16;
+  const int base = P.mt * P.nct;
+  P.ks = 1;
+  while (base * P.ks < 16 && P.ks < 8 && (steps + 2 * P.ks - 1) / (2 * P.ks) >= 8) P.ks *= 2;
+  P.spp = up((steps + P.ks - 1) / P.ks, 4);
+  P.Kpad = 4 * P.ks * P.spp;
+  P.nitems = base * P.ks;
+  int o = 0;
+  P.o_red = o; o += NTB * 8;
+  P.o_cs = o; o += 16 * 2 * 32 * 8;
+  P.o_st = o; o += 4 * 32 * 4;
+  P.o_xs = o; o += up(P.Hp * P.Wp * g.C, 4) * 4;
+  P.o_ws = o; o += P.Kpad * P.nct * 16 * 4;
+  P.o_koff = o; o += P.Kpad * 4;
+  P.o_part = o; o += P.ks * base * 256 * 4;
+  P.lds = o;
+  return o > kMaxLds ? -3 : 0;
 }
 
-// z = conv(relu(BN_in(in))); statistics partials of this layer (nullable).  zero/nzero: a buffer the
-// grid zeroes.  Returns <0 on an unsupported configuration.
+// out = {lds, ks, nitems}
+TDE_API int tde_bncnn_conv_fwd_cfg(const TdeBnGeo* gg, int* out) {
+  ConvFwdP P;
+  const int rc = conv_fwd_plan(geo_of(gg), P);
+  out[0] = P.lds;
+  out[1] = P.ks;
+  out[2] = P.nitems;
+  return rc;
+}
+
+// z = conv(relu(BN_in(in))); this layer's BN sums into acc (nullable).  zero/nzero: a statistics
+// buffer the grid zeroes.
 TDE_API int tde_bncnn_conv_fwd(const TdeBnGeo* gg, int B, const float* in, const TdeBn* bn_in, const float* w, float* z,
-                               float* pmean, float* pm2, float* pn, int tpw, int nt, int ks, float* zero,
-                               long long nzero, hipStream_t stream) {
-  const Geo g = geo_of(gg);
-  if (!bn_ok(bn_in) || bn_in->C != g.C || B < 1 || g.Co > nt * 16 || g.Co < 1) return -1;
-  if (bn_in->mode == kBnSaved) return -2;
-  const int Hp = (g.Ho - 1) * g.sh + g.kh, Wp = (g.Wo - 1) * g.sw + g.kw;
-  const int K = g.kh * g.kw * g.C, steps = (K + 3) / 4, Kp = ((steps + ks - 1) / ks) * ks * 4;
-  const int M = g.Ho * g.Wo, MTW = (4 / ks) * tpw, nchunk = ((M + 15) / 16 + MTW - 1) / MTW;
-  ConvFwdArgs a{g, B, in, bn_of(bn_in), w, z, pmean, pm2, pn, nchunk, Hp, Wp, Kp, zero, nzero};
-  const int lds = tde_bncnn_conv_fwd_lds(gg, tpw, nt, ks);
-  if (lds < 0 || lds > 160 * 1024) return -3;
-  const dim3 grid(B, nchunk);
-#define X(T, N, S)                                                          \
-  if (tpw == T && nt == N && ks == S) {                                    \
-    set_lds(conv_fwd_kernel<T, N, S>, lds);                                \
-    conv_fwd_kernel<T, N, S><<<grid, NTH, lds, stream>>>(a);               \
-    TDE_LAUNCH_CHECK();                                                    \
-    return nchunk;                                                         \
-  }
-  TDE_CONV_FWD_CFG(X)
-#undef X
-  return -4;
-}
-
-TDE_API int tde_bncnn_dense_fwd(int B, int K, int D, int Dp, int kc, const float* in, const TdeBn* bn, const float* w,
-                                float* h, hipStream_t stream) {
-  if (!bn_ok(bn) || bn->mode == kBnSaved || bn->mode == kBnNone || (kc & 3) || kc < 4 || (Dp & 15) || Dp < D)
-    return -1;
-  const int lda = kc + ((2 - kc % 32) + 32) % 32;   // lda = 2 (mod 32): the 32-lane halves hit 32 banks
-  const int lds = 2 * NTH * 8 + 4 * ((bn->C + 3) & ~3) * 4 + 64 * lda * 4 + kc * 16 * 4;
-  if (lds > 160 * 1024) return -3;
-  DenseFwdArgs a{B, K, D, Dp, kc, lda, in, bn_of(bn), w, h};
-  set_lds(dense_fwd_kernel, lds);
-  dense_fwd_kernel<<<dim3(Dp / 16, (K + kc - 1) / kc, (B + 63) / 64), NTH, lds, stream>>>(a);
+                               double* acc, double* zero, int nzero, hipStream_t stream) {
+  ConvFwdP P;
+  if (conv_fwd_plan(geo_of(gg), P) != 0) return -1;
+  if (!bn_ok(bn_in) || bn_in->C != P.g.C || B < 1 || bn_in->mode == kBnSaved) return -2;
+  ConvFwdArgs a{P, B, in, bn_of(bn_in), w, z, acc, zero, nzero, next_stamps()};
+  set_lds(conv_fwd_kernel, P.lds);
+  conv_fwd_kernel<<<B, NTB, P.lds, stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;
 }
 
-TDE_API int tde_bncnn_head(int B, int D, int Dp, int NC, int mode, const float* h, const TdeBn* bn, float rate,
+TDE_API int tde_bncnn_dense_fwd(int B, int K, int D, int Dp, int kc, const float* in, const TdeBn* bn, const float* w,
+                                float* hpart, double* zero, int nzero, hipStream_t stream) {
+  if (!bn_ok(bn) || bn->mode == kBnSaved || bn->mode == kBnNone || (kc & 15) || kc < 16 || (Dp & 15) || Dp < D)
+    return -1;
+  if ((K + kc - 1) / kc > kMaxKc || 64 * kc > kUA * NTB || kc * kDenseCols > kUB * NTB) return -2;
+  const int lda = kc + 4, ldb = kDenseCols + 4;
+  const int lds = NTB * 8 + 4 * 32 * 4 + 64 * lda * 4 + kc * ldb * 4;
+  if (lds > kMaxLds) return -3;
+  DenseFwdArgs a{B, K, D, Dp, kc, lda, ldb, in, bn_of(bn), w, hpart, zero, nzero, next_stamps()};
+  set_lds(dense_fwd_kernel, lds);
+  dense_fwd_kernel<<<dim3((Dp + kDenseCols - 1) / kDenseCols, (K + kc - 1) / kc, (B + 63) / 64), NTB, lds, stream>>>(a);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+// head_fwd + head_bwd (see HeadArgs).  logits: [Dp/16][B][16] feature-tile partials (written by head_fwd).
+TDE_API int tde_bncnn_head(int B, int D, int Dp, int NC, int mode, const float* hpart, int nkc, float* h,
+                           const TdeBn* bn, float rate,
                            unsigned long long seed, const long long* iter, int layer_id, int drop_on, const float* wh,
-                           const float* bh, const int* labels, float scale, float* metrics, float* out, int out_softmax,
-                           float* dwh, float* dbh, float* dbeta, float* dgamma, float* dh, hipStream_t stream) {
-  // the head computes its BN statistics itself (no partials): check the fields it uses
-  if (!bn || bn->C != D || D > kHeadMaxDp || Dp > kHeadMaxDp || (Dp & 15) || Dp < D || NC < 1 || NC > 16) return -1;
+                           const float* bh, float* logits, const int* labels, float scale, float* metrics, float* out,
+                           int out_softmax, float* dwh, float* dbh, float* dbeta, float* dgamma, float* dh, double* zero,
+                           int nzero, hipStream_t stream) {
+  // the head computes its BN statistics itself: check the fields it uses
+  if (!bn || bn->C != D || (Dp & 15) || Dp < D || Dp > 16 * kHeadMaxTiles || NC < 1 || NC > 16 || B < 1 || !logits ||
+      nkc < 1 || nkc > kMaxKc || !hpart || !h)
+    return -1;
   if (!(bn->mode == kBnTrain || bn->mode == kBnMoving || bn->mode == kBnBatch)) return -2;
   if ((bn->mode == kBnTrain && !bn->saved) || ((bn->mode == kBnTrain || bn->mode == kBnMoving) && (!bn->mmean || !bn->mvar)))
     return -2;
   if (mode == 0 && (!dwh || !dbh || !dh || !labels || bn->mode != kBnTrain)) return -3;
   if (mode == 2 && !out) return -4;
   if (drop_on && !(rate > 0.f && rate < 1.f)) return -5;
-  HeadArgs a{B, D, Dp, NC, mode, h, bn_of(bn), rate, seed, iter, layer_id, drop_on, wh, bh, labels, scale, metrics,
-             out, out_softmax, dwh, dbh, dbeta, dgamma, dh};
-  constexpr int lds = head_lds().total;
-  static_assert(lds <= 160 * 1024, "head LDS");
-  set_lds(head_kernel, lds);
-  head_kernel<<<1, kHeadThreads, lds, stream>>>(a);
+  HeadArgs a{B, D, Dp, NC, mode, hpart, nkc, h, bn_of(bn), rate, seed, iter, layer_id, drop_on, wh, bh, logits, labels, scale,
+             metrics, out, out_softmax, dwh, dbh, dbeta, dgamma, dh, zero, nzero, next_stamps()};
+  head_fwd_kernel<<<Dp / 16, NTH, 0, stream>>>(a);
+  TDE_LAUNCH_CHECK();
+  a.zero = nullptr;
+  a.nzero = 0;
+  a.stamps = next_stamps();
+  head_bwd_kernel<<<mode == 0 ? Dp / 16 : 1, NTH, 0, stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;
 }
 
 TDE_API int tde_bncnn_dense_bwd(int B, int K, int D, int Dp, const float* in, const TdeBn* bn, const float* w,
-                                const float* dh, float* dw, float* g, float* psg, float* psgx, hipStream_t stream) {
-  if (!bn_ok(bn) || bn->mode != kBnSaved || (Dp & 15) || Dp < D || Dp > 256) return -1;
+                                const float* dh, float* dwpart, float* g, double* acc, hipStream_t stream) {
+  if (!bn_ok(bn) || bn->mode != kBnSaved || (Dp & 15) || Dp < D || Dp > 256 || !acc) return -1;
+  if (32 * D > kUWk * NTB || 64 * Dp > kUDh * NTB || 2 * (Dp / 16) > 32) return -2;
   const int ldh = Dp + 4;
-  const int CP = (bn->C + 3) & ~3;
-  const int lds = 2 * NTH * 8 + 4 * CP * 4 + 64 * ldh * 4 + 16 * ldh * 4 + 2 * CP * 4;
-  if (64 * 17 > 16 * ldh || lds > 160 * 1024) return -3;
-  DenseBwdArgs a{B, K, D, Dp, ldh, in, bn_of(bn), w, dh, dw, g, psg, psgx};
+  const int lds = 16 * 2 * 32 * 8 + 4 * 32 * 4 + 32 * ldh * 4 + 64 * ldh * 4 + 2 * 64 * 33 * 4;
+  if (lds > kMaxLds) return -3;
+  DenseBwdArgs a{B, K, D, Dp, ldh, in, bn_of(bn), w, dh, dwpart, g, acc, next_stamps()};
   set_lds(dense_bwd_kernel, lds);
-  dense_bwd_kernel<<<dim3((K + 15) / 16, 2), NTH, lds, stream>>>(a);
+  dense_bwd_kernel<<<dim3((K + 31) / 32, (B + 63) / 64), NTB, lds, stream>>>(a);
   TDE_LAUNCH_CHECK();
-  return (K + 15) / 16;
+  return 0;
 }
 
-struct TdeBnBwd {
-  const float *psg, *psgx; int npart;
-  float *dbeta, *dgamma;
-};
-
-// Geometry of the backward grid (bordered dZ, dgrad roles) for the host to size buffers:
-// out = {n_dg, n_wg, dg_chunks, Ph, Pw, Hd, Wd, Hp, Wp, TPW_dg, TPW_wg, lds}
-TDE_API int tde_bncnn_conv_bwd_plan(const TdeBnGeo* gg, int dgrad, int* out) {
-  const Geo g = geo_of(gg);
-  const int K = g.kh * g.kw * g.C;
+// Backward conv launch geometry; 0 if it fits, <0 otherwise.
+static int conv_bwd_plan(const Geo& g, int dgrad, ConvBwdP& P) {
+  P = ConvBwdP{};
+  P.g = g;
+  P.dgrad = dgrad;
+  P.K = g.kh * g.kw * g.C;
+  P.Mo = g.Ho * g.Wo;
+  if (g.C < 1 || g.C > 32 || g.Co < 1 || g.Co > 32 || g.sh < 1 || g.sw < 1 || g.sh * g.sw > kMaxCls) return -1;
+  if (P.Mo * g.Co > kUAct * NTB || g.H * g.W * g.C > kUImg * NTB || (dgrad && P.K * g.Co > kUW * NTB)) return -2;
+  P.nci = (g.C + 15) / 16;
+  P.nco = (g.Co + 15) / 16;
+  P.CP16 = P.nci * 16;
   const int nth = (g.kh + g.sh - 1) / g.sh, ntw = (g.kw + g.sw - 1) / g.sw;
-  const int Ph = dgrad ? nth + 1 : 0, Pw = dgrad ? ntw + 1 : 0;
+  P.Ph = dgrad ? nth + 1 : 0;
+  P.Pw = dgrad ? ntw + 1 : 0;
   // bottom / right margin: the largest base row (H-1+pt)/sh must stay inside the bordered grid
-  const int Hd = g.Ho + 2 * Ph + (dgrad ? ((g.H - 1 + g.pt) / g.sh - (g.Ho - 1)) : 0);
-  const int Wd = g.Wo + 2 * Pw + (dgrad ? ((g.W - 1 + g.pl) / g.sw - (g.Wo - 1)) : 0);
-  const int Hp = (g.Ho - 1) * g.sh + g.kh, Wp = (g.Wo - 1) * g.sw + g.kw;
-  // dgrad: classes x chunks of 4 waves x TPW tiles
-  const int classes = g.sh * g.sw;
-  const int Mc_max = ((g.H + g.sh - 1) / g.sh) * ((g.W + g.sw - 1) / g.sw);
-  const int tiles_c = (Mc_max + 15) / 16;
-  const int TPW_dg = tiles_c >= 16 ? 2 : 1;
-  const int dg_chunks = (tiles_c + 4 * TPW_dg - 1) / (4 * TPW_dg);
-  const int n_dg = dgrad ? classes * dg_chunks : 0;
-  const int tiles_w = (K + 15) / 16;
-  const int TPW_wg = tiles_w >= 32 ? 2 : 1;
-  const int n_wg = (tiles_w + 4 * TPW_wg - 1) / (4 * TPW_wg);
-  const ConvBwdLds L = conv_bwd_lds(g, Hd, Wd, Hp, Wp);
-  const int v[12] = {n_dg, n_wg, dg_chunks, Ph, Pw, Hd, Wd, Hp, Wp, TPW_dg, TPW_wg, L.total};
-  for (int i = 0; i < 12; ++i) out[i] = v[i];
-  return (L.total > 160 * 1024 || g.Co > 32 || g.C > 32) ? -1 : 0;
+  P.Hd = g.Ho + 2 * P.Ph + (dgrad ? std::max((g.H - 1 + g.pt) / g.sh - (g.Ho - 1), 0) : 0);
+  P.Wd = g.Wo + 2 * P.Pw + (dgrad ? std::max((g.W - 1 + g.pl) / g.sw - (g.Wo - 1), 0) : 0);
+  P.Hp = std::max((g.Ho - 1) * g.sh + g.kh, g.pt + g.H);
+  P.Wp = std::max((g.Wo - 1) * g.sw + g.kw, g.pl + g.W);
+  P.zslot = P.Hd * P.Wd * g.Co;
+  // input-gradient classes
+  P.ncls = dgrad ? g.sh * g.sw : 0;
+  int wc = 0, ko = 0, items = 0;
+  for (int cl = 0; cl < P.ncls; ++cl) {
+    const int ry = cl / g.sw, rx = cl % g.sw;
+    const int ih0 = ((ry - g.pt) % g.sh + g.sh) % g.sh, iw0 = ((rx - g.pl) % g.sw + g.sw) % g.sw;
+    const int Hc = ih0 < g.H ? (g.H - ih0 + g.sh - 1) / g.sh : 0;
+    const int Wc = iw0 < g.W ? (g.W - iw0 + g.sw - 1) / g.sw : 0;
+    const int cnth = (g.kh - ry + g.sh - 1) / g.sh, cntw = (g.kw - rx + g.sw - 1) / g.sw;
+    P.cls_nth[cl] = cnth;
+    P.cls_ntw[cl] = cntw;
+    P.cls_Kc[cl] = cnth * cntw * g.Co;
+    P.cls_Kc16[cl] = up(std::max(P.cls_Kc[cl], 1), 16);
+    P.cls_wc[cl] = wc;
+    wc += P.cls_Kc16[cl] * P.CP16;
+    P.cls_ko[cl] = ko;
+    ko += P.cls_Kc16[cl];
+    P.cls_Mc[cl] = Hc * Wc;
+    P.cls_W[cl] = std::max(Wc, 1);
+    P.cls_ih0[cl] = ih0;
+    P.cls_iw0[cl] = iw0;
+    P.cls_item0[cl] = items;
+    items += (Hc * Wc + 15) / 16;
+  }
+  P.cls_item0[P.ncls] = items;
+  P.n_dg_items = items;
+  // weight gradient: K tiles x pixel splits (~32 items; >= 4 steps per split)
+  P.wg_tiles = (P.K + 15) / 16;
+  P.Kw16 = P.wg_tiles * 16;
+  const int wsteps = (P.Mo + 3) / 4;
+  P.wg_split = std::max(1, std::min(std::min(16, 32 / P.wg_tiles), wsteps / 4));
+  P.wg_spp = up((wsteps + P.wg_split - 1) / P.wg_split, 4);
+  P.n_items = items + P.wg_tiles * P.wg_split;
+  int o = 0;
+  P.o_red = o; o += NTB * 8;
+  P.o_cs = o; o += 16 * 2 * 32 * 8;
+  P.o_st = o; o += 4 * 32 * 4;
+  P.o_stin = o; o += 4 * 32 * 4;
+  P.o_kk = o; o += 2 * 32 * 4;
+  P.o_dz = o; o += up(P.zslot + 32, 4) * 4;
+  P.o_xs = o; o += up(P.Hp * P.Wp * g.C, 4) * 4;
+  P.o_xr = o; o += up(g.H * g.W * g.C, 4) * 4;
+  P.o_wc = o; o += wc * 4;
+  P.o_kod = o; o += up(ko, 4) * 4;
+  P.o_kow = o; o += P.Kw16 * 4;
+  P.o_ptab = o; o += P.wg_split * P.wg_spp * 4 * 8;
+  P.o_part = o; o += (P.wg_split > 1 ? P.wg_split * P.wg_tiles * P.nco * 256 : 0) * 4;
+  P.lds = o;
+  return o > kMaxLds ? -3 : 0;
+}
+
+// out = {lds, n_items, n_dg_items, wg_split}
+TDE_API int tde_bncnn_conv_bwd_plan(const TdeBnGeo* gg, int dgrad, int* out) {
+  ConvBwdP P;
+  const int rc = conv_bwd_plan(geo_of(gg), dgrad, P);
+  out[0] = P.lds;
+  out[1] = P.n_items;
+  out[2] = P.n_dg_items;
+  out[3] = P.wg_split;
+  return rc;
 }
 
 TDE_API int tde_bncnn_conv_bwd(const TdeBnGeo* gg, int B, const float* z, const TdeBn* bn, const TdeBnBwd* bb,
                                const float* gout, const float* w, const float* in, const TdeBn* bn_in, float* gin,
-                               float* psg_in, float* psgx_in, float* dwpart, int dgrad, hipStream_t stream) {
-  const Geo g = geo_of(gg);
-  int p[12];
-  if (tde_bncnn_conv_bwd_plan(gg, dgrad, p) != 0) return -1;
-  if (!bn_ok(bn) || bn->mode != kBnSaved || bn->C != g.Co || !bb || bb->npart < 1) return -2;
+                               double* acc_in, float* dwpart, int dgrad, double* zero, int nzero, hipStream_t stream) {
+  ConvBwdP P;
+  if (conv_bwd_plan(geo_of(gg), dgrad, P) != 0) return -1;
+  const Geo& g = P.g;
+  if (!bn_ok(bn) || bn->mode != kBnSaved || bn->C != g.Co || !bb || !bb->acc) return -2;
   if (!bn_ok(bn_in) || bn_in->C != g.C || !(bn_in->mode == kBnSaved || bn_in->mode == kBnNone)) return -3;
-  if (dgrad && (!gin || !psg_in || !psgx_in || bn_in->mode != kBnSaved)) return -4;
+  if (dgrad && (!gin || !acc_in || bn_in->mode != kBnSaved || !w)) return -4;
   ConvBwdArgs a{};
-  a.g = g;
+  a.p = P;
   a.B = B;
   a.z = z;
   a.bn = bn_of(bn);
-  a.bb = BnBwd{bb->psg, bb->psgx, bb->npart, bb->dbeta, bb->dgamma};
+  a.bb = BnBwd{bb->acc, bb->dbeta, bb->dgamma};
   a.gout = gout;
   a.count = (float)((double)B * g.Ho * g.Wo);
   a.w = w;
   a.in = in;
   a.bn_in = bn_of(bn_in);
   a.gin = gin;
-  a.psg_in = psg_in;
-  a.psgx_in = psgx_in;
+  a.acc_in = acc_in;
   a.dwpart = dwpart;
-  a.n_dg = p[0];
-  a.n_wg = p[1];
-  a.dg_chunks = p[2];
-  a.Ph = p[3];
-  a.Pw = p[4];
-  a.Hd = p[5];
-  a.Wd = p[6];
-  a.Hp = p[7];
-  a.Wp = p[8];
-  a.TPW_dg = p[9];
-  a.TPW_wg = p[10];
-  set_lds(conv_bwd_kernel, p[11]);
-  conv_bwd_kernel<<<dim3(B, a.n_dg + a.n_wg), NTH, p[11], stream>>>(a);
+  a.zero = zero;
+  a.nzero = nzero;
+  a.stamps = next_stamps();
+  set_lds(conv_bwd_kernel, P.lds);
+  conv_bwd_kernel<<<B, NTB, P.lds, stream>>>(a);
   TDE_LAUNCH_CHECK();
-  return a.n_dg;   // the number of input-BN partials per image
+  return 0;
 }
 
-TDE_API int tde_bncnn_reduce(int n, int B, const float* const* part, float* const* out, const long long* len,
-                             hipStream_t stream) {
-  if (n < 1 || n > kMaxRed || B < 1) return -1;
+// n segments: part[j] holds cnt[j] partials of len[j] floats, summed in order into out[j].
+TDE_API int tde_bncnn_reduce(int n, const int* cnt, const float* const* part, float* const* out, const long long* len,
+                             double* zero, int nzero, hipStream_t stream) {
+  if (n < 1 || n > kMaxRed) return -1;
   ReduceArgs a{};
   a.n = n;
-  a.B = B;
-  long long tot = 0;
+  a.zero = zero;
+  a.nzero = nzero;
+  a.stamps = next_stamps();
+  int blocks = 0;
   for (int j = 0; j < n; ++j) {
+    if (cnt[j] < 1 || len[j] < 1) return -1;
     a.part[j] = part[j];
     a.out[j] = out[j];
     a.len[j] = len[j];
-    tot += len[j];
+    a.cnt[j] = cnt[j];
+    a.blk0[j] = blocks;
+    blocks += (int)((len[j] + 63) / 64);
   }
-  reduce_kernel<<<(unsigned)((tot + NTH - 1) / NTH), NTH, 0, stream>>>(a);
+  a.blk0[n] = blocks;
+  reduce_kernel<<<blocks, NTH, 0, stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;
 }

@@ -32,24 +32,25 @@ from .program import OptimizerKernel, ReplicaPlan
 
 BN_NONE, BN_TRAIN, BN_MOVING, BN_BATCH, BN_SAVED = 0, 1, 2, 3, 4
 
+_vp, _i = C.c_void_p, C.c_int
 N.register_hip({
-    "tde_bncnn_conv_fwd_lds": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int]),
-    "tde_bncnn_conv_fwd": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
-                                     C.c_longlong, C.c_void_p]),
-    "tde_bncnn_dense_fwd": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
-                                      C.c_void_p, C.c_void_p, C.c_void_p]),
-    "tde_bncnn_head": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_float,
-                                 C.c_ulonglong, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
-                                 C.c_float, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
-                                 C.c_void_p, C.c_void_p, C.c_void_p]),
-    "tde_bncnn_dense_bwd": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
-                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
-    "tde_bncnn_conv_bwd_plan": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),
-    "tde_bncnn_conv_bwd": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
-                                     C.c_void_p, C.c_int, C.c_void_p]),
-    "tde_bncnn_reduce": (C.c_int, [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "tde_bncnn_conv_fwd_cfg": (_i, [_vp, _vp]),
+    # geo, B, in, bn_in, w, z, acc, zero, nzero, stream
+    "tde_bncnn_conv_fwd": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
+    # B, K, D, Dp, kc, in, bn, w, hpart, zero, nzero, stream
+    "tde_bncnn_dense_fwd": (_i, [_i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
+    "tde_bncnn_stat_slots": (_i, []),
+    # B, D, Dp, NC, mode, hpart, nkc, h, bn, rate, seed, iter, layer_id, drop_on, wh, bh, logits, labels, scale,
+    # metrics, out, out_softmax, dwh, dbh, dbeta, dgamma, dh, zero, nzero, stream
+    "tde_bncnn_head": (_i, [_i, _i, _i, _i, _i, _vp, _i, _vp, _vp, C.c_float, C.c_ulonglong, _vp, _i, _i, _vp, _vp,
+                            _vp, _vp, C.c_float, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
+    # B, K, D, Dp, in, bn, w, dh, dwpart, g, acc, stream
+    "tde_bncnn_dense_bwd": (_i, [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "tde_bncnn_conv_bwd_plan": (_i, [_vp, _i, _vp]),
+    # geo, B, z, bn, bb, gout, w, in, bn_in, gin, acc_in, dwpart, dgrad, zero, nzero, stream
+    "tde_bncnn_conv_bwd": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _i, _vp]),
+    # n, cnt, part, out, len, zero, nzero, stream
+    "tde_bncnn_reduce": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
 })
 
 
@@ -58,15 +59,15 @@ class Geo(C.Structure):
 
 
 class Bn(C.Structure):
-    _fields_ = [("mode", C.c_int), ("C", C.c_int), ("pmean", C.c_void_p), ("pm2", C.c_void_p), ("pn", C.c_void_p),
-                ("npart", C.c_int), ("gamma", C.c_void_p), ("beta", C.c_void_p), ("eps", C.c_float),
-                ("momentum", C.c_float), ("bessel", C.c_float), ("mmean", C.c_void_p), ("mvar", C.c_void_p),
-                ("saved", C.c_void_p)]
+    """acc: f64 [2][C] batch sums (sum, sum of squares) over `count` values."""
+    _fields_ = [("mode", C.c_int), ("C", C.c_int), ("acc", C.c_void_p), ("count", C.c_double),
+                ("gamma", C.c_void_p), ("beta", C.c_void_p), ("eps", C.c_float), ("momentum", C.c_float),
+                ("bessel", C.c_float), ("mmean", C.c_void_p), ("mvar", C.c_void_p), ("saved", C.c_void_p)]
 
 
 class BnBwd(C.Structure):
-    _fields_ = [("psg", C.c_void_p), ("psgx", C.c_void_p), ("npart", C.c_int), ("dbeta", C.c_void_p),
-                ("dgamma", C.c_void_p)]
+    """acc: f64 [2][C] backward sums (sum g, sum g*xhat)."""
+    _fields_ = [("acc", C.c_void_p), ("dbeta", C.c_void_p), ("dgamma", C.c_void_p)]
 
 
 _P = N.ptr
@@ -109,13 +110,13 @@ def match_bncnn(model, loss):
             return None
         convs.append((c, ls[i + 1]))
         i += 3
-    if not convs or i >= len(ls) or not isinstance(ls[i], L.Flatten):
+    if not convs or len(convs) > 3 or i >= len(ls) or not isinstance(ls[i], L.Flatten):
         return None
     i += 1
     if i >= len(ls) or not isinstance(ls[i], L.Dense):
         return None
     d = ls[i]
-    if d.use_bias or d.activation not in (None, "linear") or not bn_relu(i + 1) or d.units > 240:
+    if d.use_bias or d.activation not in (None, "linear") or not bn_relu(i + 1) or d.units > 256:
         return None
     bn_d = ls[i + 1]
     i += 3
@@ -133,17 +134,6 @@ def match_bncnn(model, loss):
     return dict(convs=convs, dense=(d, bn_d, drop), head=head)
 
 
-def _fwd_cfg(Co, K):
-    """(tiles per wave, N tiles, K split) of a forward conv: ~50 f32 MFMAs per wave, >= 4 waves per tile row."""
-    nt = 1 if Co <= 16 else 2
-    steps = (K + 3) // 4
-    if steps <= 8:
-        return (4, 1, 1) if nt == 1 else (2, 2, 1)
-    if nt == 2:
-        return (1, 2, 4) if steps >= 64 else (1, 2, 1)
-    return (1, 1, 4) if steps >= 96 else (1, 1, 1)
-
-
 class BnCnnPlan(ReplicaPlan):
     kind = "fused_bncnn"
     compute_dtype = "fp32"
@@ -157,6 +147,8 @@ class BnCnnPlan(ReplicaPlan):
         dev = self.device
         B = self.B
         f32 = dict(dtype=torch.float32, device=dev)
+        f64 = dict(dtype=torch.float64, device=dev)
+        slots = self.lib.tde_bncnn_stat_slots()   # statistics sums are spread over this many copies
         self.blocks = []
         for conv, bn in spec["convs"]:
             H, W_, Cin = conv.input_shape
@@ -165,47 +157,35 @@ class BnCnnPlan(ReplicaPlan):
             kh, kw = conv.kernel_size
             g = Geo(H, W_, Cin, Ho, Wo, Co, kh, kw, conv.strides[0], conv.strides[1], pt, pl)
             K = kh * kw * Cin
-            cfg = _fwd_cfg(Co, K)
             M = Ho * Wo
-            mtw = (4 // cfg[2]) * cfg[0]
-            nchunk = -(-(-(-M // 16)) // mtw)
-            lds = self.lib.tde_bncnn_conv_fwd_lds(C.byref(g), *cfg)
-            if lds < 0 or lds > 160 * 1024:
-                raise ValueError(f"{conv.name}: forward tile does not fit in LDS ({lds} B)")
-            blk = dict(conv=conv, bn=bn, geo=g, K=K, cfg=cfg, nchunk=nchunk,
+            cfg = (C.c_int * 4)()
+            rc = self.lib.tde_bncnn_conv_fwd_cfg(C.byref(g), cfg)
+            if rc != 0:
+                raise ValueError(f"{conv.name}: no forward tile configuration fits ({rc})")
+            blk = dict(conv=conv, bn=bn, geo=g, K=K, cfg=list(cfg),
                        w=st.view(f"{conv.name}/kernel"), gw=st.grad(f"{conv.name}/kernel"),
                        z=torch.zeros(B * M * Co, **f32), g=torch.zeros(B * M * Co, **f32),
-                       pmean=torch.zeros(B * nchunk * Co, **f32), pm2=torch.zeros(B * nchunk * Co, **f32),
-                       pn=torch.zeros(B * nchunk, **f32), saved=torch.zeros(2 * Co, **f32),
-                       dwpart=torch.zeros(B * K * Co, **f32))
+                       acc=torch.zeros(slots * 2 * Co, **f64), accb=torch.zeros(slots * 2 * Co, **f64),
+                       saved=torch.zeros(2 * Co, **f32), dwpart=torch.zeros(B * K * Co, **f32))
             blk.update(self._bn_vars(bn))
-            blk["bessel_R"] = M   # rows per image of this BN (Bessel factor uses B * M)
             self.blocks.append(blk)
-        # backward grids (input-gradient roles of layer l produce layer l-1's BN partial sums)
+        # backward grids (the input-gradient roles of layer l accumulate layer l-1's BN backward sums)
         for li, blk in enumerate(self.blocks):
             out = (C.c_int * 12)()
             if self.lib.tde_bncnn_conv_bwd_plan(C.byref(blk["geo"]), int(li > 0), out) != 0:
                 raise ValueError(f"{blk['conv'].name}: backward tiles do not fit")
             blk["bwd"] = list(out)
-        for li, blk in enumerate(self.blocks[:-1]):
-            n_dg = self.blocks[li + 1]["bwd"][0]
-            Co = blk["geo"].Co
-            blk["psg"] = torch.zeros(B * n_dg * Co, **f32)
-            blk["psgx"] = torch.zeros(B * n_dg * Co, **f32)
-            blk["npart_bwd"] = n_dg   # per image
         dense, bn_d, drop = spec["dense"]
         last = self.blocks[-1]
         self.K = last["geo"].Ho * last["geo"].Wo * last["geo"].Co
         self.D = dense.units
         self.Dp = -(-self.D // 16) * 16
-        self.kc = -(-(-(-self.K // 8)) // 4) * 4
-        nkt = -(-self.K // 16)
-        last["psg"] = torch.zeros(nkt * last["geo"].Co, **f32)
-        last["psgx"] = torch.zeros(nkt * last["geo"].Co, **f32)
-        last["npart_bwd"] = None   # fixed: one per dense k-tile
-        self.nkt = nkt
+        self.kc = -(-(-(-self.K // 8)) // 32) * 32   # <= 8 K chunks of a multiple of 32
+        self.nkc = -(-self.K // self.kc)
         self.dense = dense
         self.wd, self.gwd = st.view(f"{dense.name}/kernel"), st.grad(f"{dense.name}/kernel")
+        self.nrb = -(-B // 64)   # dense dW partials: one per 64-row block
+        self.dwd_part = torch.zeros(self.nrb * self.K * self.D, **f32)
         self.bnd = dict(layer=bn_d, saved=torch.zeros(2 * self.D, **f32), **self._bn_vars(bn_d))
         self.drop = drop
         self.drop_seed = 0
@@ -220,6 +200,8 @@ class BnCnnPlan(ReplicaPlan):
         self.wh, self.bh = st.view(f"{head.name}/kernel"), st.view(f"{head.name}/bias")
         self.gwh, self.gbh = st.grad(f"{head.name}/kernel"), st.grad(f"{head.name}/bias")
         self.h = torch.zeros(B * self.Dp, **f32)
+        self.hpart = torch.zeros(self.nkc * B * self.Dp, **f32)
+        self.logits = torch.zeros(self.Dp // 16 * B * 16, **f32)
         self.dh = torch.zeros(B * self.Dp, **f32)
         self.probs = torch.zeros(B, self.NC, **f32)
         H0, W0, C0 = self.blocks[0]["geo"].H, self.blocks[0]["geo"].W, self.blocks[0]["geo"].C
@@ -237,12 +219,19 @@ class BnCnnPlan(ReplicaPlan):
         return v
 
     # ------------------------------------------------------------------ descriptors
-    def _bn(self, blk, mode, B, C_=None, npart=None, pm=None, bessel=1.0):
-        Cc = C_ if C_ is not None else blk["geo"].Co
-        src = pm if pm is not None else blk
-        return Bn(mode, Cc, _P(src.get("pmean")), _P(src.get("pm2")), _P(src.get("pn")), int(npart or 0),
-                  _P(blk["gamma"]), _P(blk["beta"]), float(blk["eps"]), float(blk["momentum"]), float(bessel),
-                  _P(blk["mmean"]), _P(blk["mvar"]), _P(blk["saved"]))
+    def _bn(self, blk, mode, B):
+        g = blk["geo"]
+        R = B * g.Ho * g.Wo
+        return Bn(mode, g.Co, _P(blk["acc"]), float(R), _P(blk["gamma"]), _P(blk["beta"]), float(blk["eps"]),
+                  float(blk["momentum"]), float(R / max(R - 1, 1)), _P(blk["mmean"]), _P(blk["mvar"]),
+                  _P(blk["saved"]))
+
+    def _acc(self, i, key="acc"):
+        """(pointer, n) of block i's f64 statistics buffer, or (None, 0) outside the chain."""
+        if 0 <= i < len(self.blocks):
+            t = self.blocks[i][key]
+            return _P(t), t.numel()
+        return None, 0
 
     def _fwd_mode(self, training):
         if training == "train":
@@ -255,38 +244,39 @@ class BnCnnPlan(ReplicaPlan):
         lib, s = self.lib, N.stream_ptr()
         mode = self._fwd_mode(phase)
         batch_stats = mode in (BN_TRAIN, BN_BATCH)
+        # launch i of the chain [conv_1..conv_L, dense, head] zeroes block i-2's statistics sums (consumed
+        # by launch i-1), so every step starts from zero sums without a memset
         inp = x
         bn_in = Bn(BN_NONE, self.blocks[0]["geo"].C)
         for li, blk in enumerate(self.blocks):
-            tpw, nt, ks = blk["cfg"]
-            zero, nzero = (self.h, B * self.Dp) if li == 0 else (None, 0)
+            zp, zn = self._acc(li - 2)
             rc = lib.tde_bncnn_conv_fwd(C.byref(blk["geo"]), B, _P(inp), C.byref(bn_in), _P(blk["w"]), _P(blk["z"]),
-                                        _P(blk["pmean"]) if batch_stats else None,
-                                        _P(blk["pm2"]) if batch_stats else None,
-                                        _P(blk["pn"]) if batch_stats else None, tpw, nt, ks, _P(zero), nzero, s)
+                                        _P(blk["acc"]) if batch_stats else None, zp, zn, s)
             if rc < 0:
                 raise RuntimeError(f"tde_bncnn_conv_fwd({blk['conv'].name}) failed with {rc}")
-            R = B * blk["geo"].Ho * blk["geo"].Wo
-            bn_in = self._bn(blk, mode, B, npart=B * blk["nchunk"], bessel=R / max(R - 1, 1))
+            bn_in = self._bn(blk, mode, B)
             inp = blk["z"]
+        zp, zn = self._acc(len(self.blocks) - 2)
         rc = lib.tde_bncnn_dense_fwd(B, self.K, self.D, self.Dp, self.kc, _P(inp), C.byref(bn_in), _P(self.wd),
-                                     _P(self.h), s)
+                                     _P(self.hpart), zp, zn, s)
         N.check(rc, "tde_bncnn_dense_fwd")
         return bn_in
 
     def _head(self, B, hmode, phase, labels, scale, probs=None):
         mode = self._fwd_mode(phase)
         bnd = self.bnd
-        bn = Bn(mode, self.D, None, None, None, 0, _P(bnd["gamma"]), _P(bnd["beta"]), float(bnd["eps"]),
+        bn = Bn(mode, self.D, None, float(B), _P(bnd["gamma"]), _P(bnd["beta"]), float(bnd["eps"]),
                 float(bnd["momentum"]), 1.0, _P(bnd["mmean"]), _P(bnd["mvar"]), _P(bnd["saved"]))
+        zp, zn = self._acc(len(self.blocks) - 1)
         drop_on = int(self.drop is not None and self.drop.rate > 0 and phase is not False)
         train = hmode == 0
         rc = self.lib.tde_bncnn_head(
-            B, self.D, self.Dp, self.NC, hmode, _P(self.h), C.byref(bn), float(self.drop.rate if self.drop else 0.0),
-            self.drop_seed, _P(self.iterations), 0, drop_on, _P(self.wh), _P(self.bh), _P(labels), float(scale),
-            _P(self.metrics), _P(probs), int(self.softmax), _P(self.gwh) if train else None,
+            B, self.D, self.Dp, self.NC, hmode, _P(self.hpart), self.nkc, _P(self.h), C.byref(bn),
+            float(self.drop.rate if self.drop else 0.0),
+            self.drop_seed, _P(self.iterations), 0, drop_on, _P(self.wh), _P(self.bh), _P(self.logits), _P(labels),
+            float(scale), _P(self.metrics) if hmode != 2 else None, _P(probs), int(self.softmax), _P(self.gwh) if train else None,
             _P(self.gbh) if train else None, _P(bnd["dbeta"]) if train else None,
-            _P(bnd["dgamma"]) if train else None, _P(self.dh) if train else None, N.stream_ptr())
+            _P(bnd["dgamma"]) if train else None, _P(self.dh) if train else None, zp, zn, N.stream_ptr())
         N.check(rc, "tde_bncnn_head")
 
     # ------------------------------------------------------------------ plan interface
@@ -305,31 +295,34 @@ class BnCnnPlan(ReplicaPlan):
         last = self.blocks[-1]
         bn_last = self._bn(last, BN_SAVED, B)
         rc = lib.tde_bncnn_dense_bwd(B, self.K, self.D, self.Dp, _P(last["z"]), C.byref(bn_last), _P(self.wd),
-                                     _P(self.dh), _P(self.gwd), _P(last["g"]), _P(last["psg"]), _P(last["psgx"]), s)
-        if rc < 0:
-            raise RuntimeError(f"tde_bncnn_dense_bwd failed with {rc}")
-        npart = rc
+                                     _P(self.dh), _P(self.dwd_part), _P(last["g"]), _P(last["accb"]), s)
+        N.check(rc, "tde_bncnn_dense_bwd")
+        # conv_bwd of block li consumes accb[li] and zeroes accb[li + 1] (consumed by the launch before it);
+        # the reduce zeroes accb[0]
         for li in range(len(self.blocks) - 1, -1, -1):
             blk = self.blocks[li]
-            bb = BnBwd(_P(blk["psg"]), _P(blk["psgx"]), int(npart), _P(blk["dbeta"]), _P(blk["dgamma"]))
+            bb = BnBwd(_P(blk["accb"]), _P(blk["dbeta"]), _P(blk["dgamma"]))
             if li > 0:
                 prev = self.blocks[li - 1]
-                inp, bn_in = prev["z"], self._bn(prev, BN_SAVED, B)
-                gin, psg_in, psgx_in = prev["g"], prev["psg"], prev["psgx"]
+                inp, bn_in, gin, acc_in = prev["z"], self._bn(prev, BN_SAVED, B), prev["g"], prev["accb"]
             else:
-                inp, bn_in = x, Bn(BN_NONE, blk["geo"].C)
-                gin = psg_in = psgx_in = None
+                inp, bn_in, gin, acc_in = x, Bn(BN_NONE, blk["geo"].C), None, None
+            zp, zn = self._acc(li + 1, "accb")
             rc = lib.tde_bncnn_conv_bwd(C.byref(blk["geo"]), B, _P(blk["z"]), C.byref(self._bn(blk, BN_SAVED, B)),
                                         C.byref(bb), _P(blk["g"]), _P(blk["w"]), _P(inp), C.byref(bn_in), _P(gin),
-                                        _P(psg_in), _P(psgx_in), _P(blk["dwpart"]), int(li > 0), s)
+                                        _P(acc_in), _P(blk["dwpart"]), int(li > 0), zp, zn, s)
             if rc < 0:
                 raise RuntimeError(f"tde_bncnn_conv_bwd({blk['conv'].name}) failed with {rc}")
-            npart = B * rc
-        n = len(self.blocks)
-        parts = (C.c_void_p * n)(*[b["dwpart"].data_ptr() for b in self.blocks])
-        outs = (C.c_void_p * n)(*[b["gw"].data_ptr() for b in self.blocks])
-        lens = (C.c_longlong * n)(*[b["K"] * b["geo"].Co for b in self.blocks])
-        N.check(lib.tde_bncnn_reduce(n, B, parts, outs, lens, s), "tde_bncnn_reduce")
+        # weight-gradient partials -> the bucket: per image for the convs, per 64-row block for the dense
+        segs = [(b["dwpart"], b["gw"], b["K"] * b["geo"].Co, B) for b in self.blocks]
+        segs.append((self.dwd_part, self.gwd, self.K * self.D, -(-B // 64)))
+        n = len(segs)
+        cnt = (C.c_int * n)(*[sg[3] for sg in segs])
+        parts = (C.c_void_p * n)(*[sg[0].data_ptr() for sg in segs])
+        outs = (C.c_void_p * n)(*[sg[1].data_ptr() for sg in segs])
+        lens = (C.c_longlong * n)(*[sg[2] for sg in segs])
+        zp, zn = self._acc(0, "accb")
+        N.check(lib.tde_bncnn_reduce(n, cnt, parts, outs, lens, zp, zn, s), "tde_bncnn_reduce")
 
     def apply(self):
         self.opt.apply()
