@@ -19,8 +19,8 @@
 //                  input gradient per stride class (only the taps that hit that class) -> g of the
 //                  previous layer + its BN backward sums; the image's weight-gradient partial
 //   reduce         per-image weight-gradient partials -> the flat gradient bucket in image order
-// Statistics sums are consumed by the next launch and re-zeroed by the one after it (each launch
-// zeroes a buffer two steps back in the chain), so a step needs no memset.
+// Statistics sums travel as per-workgroup partials ([producer workgroup][2][C] f64, plain stores) that
+// the consumer sums in a fixed order: no atomics, no zeroing, and the whole step is deterministic.
 //
 // Latency is the budget at MNIST sizes: a dependent round trip to data another XCD just wrote costs
 // ~2 us, an MFMA pass over a whole image well under that.  So the conv / dense launches run 1024-thread
@@ -49,16 +49,16 @@ struct Bn {
                    // kBnMoving: moving statistics; kBnBatch: batch statistics, no update (learning phase 1
                    // in evaluation, Q4); kBnSaved: the statistics the forward saved (backward)
   int C;
-  const double* acc; double count;   // batch statistics: [kSlots][2][C] sums, sums of squares
+  const double* acc; int npart; double count;   // batch statistics: [npart][2][C] partial sums, sums of squares
   const float* gamma; const float* beta;
   float eps, momentum, bessel;
   float* mmean; float* mvar;
   float* saved;    // [2][C] mean, rstd
 };
 
-// Backward sums of a BN: g = dL/d(BN output, pre-ReLU); acc = [kSlots][2][C] sum g, sum g*xhat.
+// Backward sums of a BN: g = dL/d(BN output, pre-ReLU); acc = [npart][2][C] partial sum g, sum g*xhat.
 struct BnBwd {
-  const double* acc;
+  const double* acc; int npart;
   float* dbeta; float* dgamma;   // flat gradient bucket views (nullable)
 };
 
@@ -87,26 +87,24 @@ __device__ __forceinline__ void pf_store(const Pf<U>& p, int n, ST st) {
   }
 }
 
-// Statistics accumulators are spread over kSlots copies ([kSlots][2][C] doubles; a producer
-// workgroup adds into slot (its linear id % kSlots)): hundreds of workgroups adding into the same few
-// addresses serialise at the L2 atomic unit, 64 slots keep that contention a few deep.
-constexpr int kSlots = 64;
-__device__ __forceinline__ int my_slot() {
-  return ((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) & (kSlots - 1);
+// Linear id of this workgroup: its row in a [npart][2][C] partial-statistics buffer.
+__device__ __forceinline__ int wg_id() {
+  return (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
 }
 
-// red[q] = sum over the slots of acc[slot][q], q < Q (Q <= blockDim); red: blockDim doubles of LDS.
+// red[q] = sum over the npart partials acc[p][q], q < Q (Q <= blockDim), in a fixed order (thread
+// (part, q) sums p = part, part + np, ...; then the parts in order); red: blockDim doubles of LDS.
 // Ends with a barrier.
-__device__ void slot_sums(const double* acc, int Q, double* red) {
+__device__ void slot_sums(const double* acc, int npart, int Q, double* red) {
   const int t = threadIdx.x, np = blockDim.x / Q, q = t % Q, part = t / Q;
   double s = 0.0;
   if (part < np) {
-    for (int j0 = part; j0 < kSlots; j0 += 8 * np) {
+    for (int j0 = part; j0 < npart; j0 += 8 * np) {
       double v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int j = j0 + u * np;
-        v[u] = j < kSlots ? acc[j * Q + q] : 0.0;
+        v[u] = j < npart ? acc[j * Q + q] : 0.0;
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) s += v[u];
@@ -128,7 +126,7 @@ __device__ void slot_sums(const double* acc, int Q, double* red) {
 __device__ void bn_prepare(const Bn& bn, float* st, bool writer, double* red) {
   const int C = bn.C;
   const bool batch = bn.mode == kBnTrain || bn.mode == kBnBatch;
-  if (batch) slot_sums(bn.acc, 2 * C, red);
+  if (batch) slot_sums(bn.acc, bn.npart, 2 * C, red);
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float mean = 0.f, rstd = 1.f, var = 0.f;
     if (bn.mode == kBnMoving) {
@@ -167,17 +165,9 @@ __device__ void bn_prepare(const Bn& bn, float* st, bool writer, double* red) {
   lds_barrier();
 }
 
-// Zeroes n doubles cooperatively over the grid (a statistics buffer two launches back in the chain).
-__device__ __forceinline__ void zero_share(double* p, int n) {
-  if (!p) return;
-  const int nb = gridDim.x * gridDim.y * gridDim.z;
-  const int me = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-  for (int i = me * (int)blockDim.x + threadIdx.x; i < n; i += nb * (int)blockDim.x) p[i] = 0.0;
-}
-
 // Per-wave column statistics (lanes fq == 0 after the cross-fq shuffles hold column fr of N tile n)
-// -> cs[wave][stat][32] -> one f64 atomic per (stat, channel) into this workgroup's slot, the 16
-// waves summed in a fixed order.
+// -> cs[wave][stat][32] -> this workgroup's partial row acc[wg][stat][C], the 16 waves summed in a
+// fixed order.
 __device__ __forceinline__ void wave_cols_to_slot(const double (&s1)[2], const double (&s2)[2], double* cs,
                                                   double* acc, int C) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
@@ -198,16 +188,28 @@ __device__ __forceinline__ void wave_cols_to_slot(const double (&s1)[2], const d
     const int j = tid / C, c = tid - j * C;
     double S = 0.0;
     for (int w = 0; w < 16; ++w) S += cs[(w * 2 + j) * 32 + c];
-    atomicAdd(acc + my_slot() * 2 * C + j * C + c, S);
+    acc[(size_t)wg_id() * 2 * C + j * C + c] = S;
   }
 }
 
+// Fast integer division for the staging index math: q = floor(i / d) for 0 <= i < 2^21 from a
+// host-rounded reciprocal ((i + 0.5) / d lies >= 0.5 / d away from the next integer, far more than
+// the f32 rounding of the product).
+struct Dv {
+  int d;
+  float r;
+};
+__device__ __forceinline__ int dq(int i, Dv v) { return (int)(((float)i + 0.5f) * v.r); }
+
 // ------------------------------------------------------------------------------------------------
-// Forward conv: grid B (one image per workgroup).  Work items (16-pixel output tile, 16-channel N
-// tile, K part) over the 16 waves; K parts (strided K steps) summed through LDS in a fixed order.
+// Forward conv: grid (B, msplit): workgroup (b, h) = image b, output tiles [h * mtw, (h+1) * mtw)
+// (two workgroups per image keep all 256 CUs busy at B = 128).  Work items (16-pixel output tile,
+// 16-channel N tile, K part) over the 16 waves; K parts (strided K steps) summed through LDS in a fixed
+// order.
 struct ConvFwdP {
   Geo g;
-  int K, M, Hp, Wp, nct, ks, spp, Kpad, mt, nitems;
+  int K, M, Hp, Wp, nct, ks, spp, Kpad, mt, mtw, msplit;
+  Dv dC, dCo, dW, dWo, dWp, dkw, dNTP;
   int o_red, o_cs, o_st, o_xs, o_ws, o_koff, o_part, lds;
 };
 struct ConvFwdArgs {
@@ -217,8 +219,7 @@ struct ConvFwdArgs {
   Bn bn;                     // BN + ReLU of the input (kBnNone for the image)
   const float* w;
   float* z;
-  double* acc;               // this layer's BN sums [kSlots][2][Co] (nullable: no statistics)
-  double* zero; int nzero;   // the statistics buffer two launches back, zeroed by the grid
+  double* acc;               // this layer's BN partial sums [msplit * B][2][Co] (nullable: no statistics)
   long long* stamps;         // diagnostic phase clock (tde_bncnn_stamps), nullable
 };
 
@@ -243,48 +244,48 @@ __global__ __launch_bounds__(NTB) void conv_fwd_kernel(ConvFwdArgs a) {
   Pf<kUW> pw;
   pf_load(pi, nimg, [&](int i) { return img[i]; });
   pf_load(pw, nw, [&](int i) { return a.w[i]; });
-  zero_share(a.zero, a.nzero);
   // LDS the registers do not cover: image border, weight padding, im2col offsets
   for (int i = tid; i < P.Hp * Wp; i += NTB) {
-    const int y = i / Wp, x = i - y * Wp, iy = y - g.pt, ix = x - g.pl;
+    const int y = dq(i, P.dWp), x = i - y * Wp, iy = y - g.pt, ix = x - g.pl;
     if (iy < 0 || iy >= g.H || ix < 0 || ix >= g.W)
       for (int c = 0; c < C; ++c) Xs[i * C + c] = 0.f;
   }
   for (int i = tid; i < P.Kpad * NTP; i += NTB) {
-    const int k = i / NTP, col = i - k * NTP;
+    const int k = dq(i, P.dNTP), col = i - k * NTP;
     if (k >= K || col >= Co) Ws[i] = 0.f;
   }
   for (int k = tid; k < P.Kpad; k += NTB) {
     int off = 0;
     if (k < K) {
-      const int ci = k % C, t = k / C, kx = t % g.kw, ky = t / g.kw;
+      const int t = dq(k, P.dC), ci = k - t * C, ky = dq(t, P.dkw), kx = t - ky * g.kw;
       off = (ky * Wp + kx) * C + ci;
     }
     koff[k] = off;
   }
-  bn_prepare(a.bn, st, b == 0, red);
+  bn_prepare(a.bn, st, b == 0 && blockIdx.y == 0, red);
   stamp(a.stamps, 1);
   {
     const float* sc = st;
     const float* sh = st + C;
     const bool raw = a.bn.mode == kBnNone;
     pf_store(pi, nimg, [&](int i, float v) {
-      const int c = i % C, pix = i / C, y = pix / g.W, x = pix - y * g.W;
+      const int pix = dq(i, P.dC), c = i - pix * C, y = dq(pix, P.dW), x = pix - y * g.W;
       Xs[((y + g.pt) * Wp + x + g.pl) * C + c] = raw ? v : fmaxf(fmaf(v, sc[c], sh[c]), 0.f);
     });
     pf_store(pw, nw, [&](int i, float v) {
-      const int k = i / Co, co = i - k * Co;
+      const int k = dq(i, P.dCo), co = i - k * Co;
       Ws[k * NTP + co] = v;
     });
   }
   lds_barrier();
   stamp(a.stamps, 2);
-  // ---- MFMA work items
-  const int ntile = P.mt * P.nct;
-  for (int item = wave; item < P.nitems; item += 16) {
-    const int kp = item % P.ks, t = item / P.ks, n = t % P.nct, mtile = t / P.nct;
+  // ---- MFMA work items over this workgroup's output tiles
+  const int mt0 = blockIdx.y * P.mtw, mtn = min(P.mtw, P.mt - mt0);
+  const int ntile = mtn * P.nct, nitems = ntile * P.ks;
+  for (int item = wave; item < nitems; item += 16) {
+    const int kp = item % P.ks, t = item / P.ks, n = t % P.nct, mtile = mt0 + t / P.nct;
     const int m = min(mtile * 16 + fr, M - 1);
-    const int oh = m / g.Wo, ow = m - oh * g.Wo;
+    const int oh = dq(m, P.dWo), ow = m - oh * g.Wo;
     const int pb = (oh * g.sh * Wp + ow * g.sw) * C;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int i0 = 0; i0 < P.spp; i0 += 4) {
@@ -307,7 +308,7 @@ __global__ __launch_bounds__(NTB) void conv_fwd_kernel(ConvFwdArgs a) {
   float* zb = a.z + (size_t)b * M * Co;
   double s1[2] = {0.0, 0.0}, s2[2] = {0.0, 0.0};
   for (int t = wave; t < ntile; t += 16) {
-    const int n = t % P.nct, mtile = t / P.nct;
+    const int n = t % P.nct, mtile = mt0 + t / P.nct;
     f32x4 v = *reinterpret_cast<const f32x4*>(part + ((size_t)t * 64 + lane) * 4);
     for (int kp = 1; kp < P.ks; ++kp) v += *reinterpret_cast<const f32x4*>(part + ((size_t)(kp * ntile + t) * 64 + lane) * 4);
     const int co = n * 16 + fr;
@@ -346,7 +347,6 @@ struct DenseFwdArgs {
   Bn bn;
   const float* w;            // [K][D]
   float* hpart;              // [gridDim.y][B][Dp]
-  double* zero; int nzero;
   long long* stamps;
 };
 
@@ -371,7 +371,6 @@ __global__ __launch_bounds__(NTB) void dense_fwd_kernel(DenseFwdArgs a) {
     const int kk = e / kDenseCols, col = e - kk * kDenseCols;
     return a.w[(size_t)min(k0 + kk, a.K - 1) * a.D + min(c0 + col, a.D - 1)];
   });
-  zero_share(a.zero, a.nzero);
   bn_prepare(a.bn, st, blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0, red);
   stamp(a.stamps, 1);
   {
@@ -457,7 +456,6 @@ struct HeadArgs {
   float* out; int out_softmax;      // predict: [B][NC] probabilities (softmax head) or logits
   float *dwh, *dbh, *dbeta, *dgamma;
   float* dh;                        // [B][Dp]: dL/dh (holds the pre-ReLU gradient g until the last pass)
-  double* zero; int nzero;
   long long* stamps;   // diagnostic phase clock (tde_bncnn_stamps), nullable
 };
 
@@ -473,7 +471,6 @@ __global__ __launch_bounds__(NTH) void head_fwd_kernel(HeadArgs a) {
   const bool fok = f < D;
   const long long it = a.iter ? *a.iter : 0;
   stamp(a.stamps, 0);
-  zero_share(a.zero, a.nzero);
   {
     const int ff = f0 + (tid >> 4), cc = tid & 15;
     whs[tid] = (ff < D && cc < NC) ? a.wh[(size_t)ff * NC + cc] : 0.f;
@@ -589,7 +586,7 @@ __global__ __launch_bounds__(NTH) void head_bwd_kernel(HeadArgs a) {
   __shared__ float mu[16], rs[16], sc[16], sh[16], gm[16];
   __shared__ float dls[64 * 16];
   __shared__ float As[64 * 17], Xh[64 * 17];
-  __shared__ float sg[16], sgx[16];
+  __shared__ float sgp[4][16], sgxp[4][16];   // per-wave BN backward sums (summed in wave order)
   __shared__ float part[4][256];
   __shared__ float gbs[4][16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
@@ -611,8 +608,6 @@ __global__ __launch_bounds__(NTH) void head_bwd_kernel(HeadArgs a) {
       gm[tid] = g;
       sc[tid] = g * r;
       sh[tid] = ft < D ? (a.bn.beta ? a.bn.beta[ft] : 0.f) - m * g * r : 0.f;
-      sg[tid] = 0.f;
-      sgx[tid] = 0.f;
     }
   }
   const float bias = c < NC ? a.bh[c] : 0.f;
@@ -728,8 +723,8 @@ __global__ __launch_bounds__(NTH) void head_bwd_kernel(HeadArgs a) {
   s2 += __shfl_xor(s2, 16, 64);
   s2 += __shfl_xor(s2, 32, 64);
   if (fq == 0) {
-    atomicAdd(sg + fr, s1);
-    atomicAdd(sgx + fr, s2);
+    sgp[wave][fr] = s1;
+    sgxp[wave][fr] = s2;
   }
   *reinterpret_cast<f32x4*>(&part[wave][lane * 4]) = gw;
   __syncthreads();   // LDS partials, and the g stores of every wave visible to the workgroup
@@ -744,13 +739,15 @@ __global__ __launch_bounds__(NTH) void head_bwd_kernel(HeadArgs a) {
     }
   }
   if (lead && tid < 16 && tid < NC) a.dbh[tid] = (gbs[0][tid] + gbs[1][tid]) + (gbs[2][tid] + gbs[3][tid]);
+  const float sgc = (sgp[0][c] + sgp[1][c]) + (sgp[2][c] + sgp[3][c]);
+  const float sgxc = (sgxp[0][c] + sgxp[1][c]) + (sgxp[2][c] + sgxp[3][c]);
   if (tid < 16 && f0 + tid < D) {
-    if (a.dbeta) a.dbeta[f0 + tid] = sg[tid];
-    if (a.dgamma) a.dgamma[f0 + tid] = sgx[tid];
+    if (a.dbeta) a.dbeta[f0 + tid] = sgc;
+    if (a.dgamma) a.dgamma[f0 + tid] = sgxc;
   }
   // ---- dL/dh for the tile, 8 rows in flight per thread
   const float invB = 1.f / (float)B;
-  const float k1 = sg[c] * invB, k2 = sgx[c] * invB, kk = gm[c] * rs[c];
+  const float k1 = sgc * invB, k2 = sgxc * invB, kk = gm[c] * rs[c];
   for (int b0 = 0; b0 < B; b0 += 128) {
     float gv[8], xv[8];
 #pragma unroll
@@ -786,7 +783,7 @@ struct DenseBwdArgs {
   const float* dh;                  // [B][Dp]
   float* dwpart;                    // [ceil(B/64)][K][D]
   float* g;                         // [B][K]
-  double* acc;                      // [kSlots][2][C] BN backward sums of the input layer
+  double* acc;                      // [gridDim.x * gridDim.y][2][C] BN backward partial sums of the input layer
   long long* stamps;
 };
 
@@ -891,25 +888,37 @@ __global__ __launch_bounds__(NTB) void dense_bwd_kernel(DenseBwdArgs a) {
         const int k = kt0 + (w >> 2) * 16 + f;
         if (k < K && k % C == c) S += cs[(w * 2 + j) * 32 + f];
       }
-    atomicAdd(a.acc + my_slot() * 2 * C + j * C + c, S);
+    a.acc[(size_t)wg_id() * 2 * C + j * C + c] = S;
   }
   stamp(a.stamps, 3);
 }
 
 // ------------------------------------------------------------------------------------------------
-// Conv backward: grid B (one image per workgroup).  dZ of the image in a zero-bordered LDS grid;
-// work items over the 16 waves:
-//   input gradient (when wanted): (stride class, 16-pixel tile of that class) -> K = the taps that hit
-//     the class x Co; -> g of the previous layer (its ReLU mask) + that BN's backward sums
-//   weight gradient: (16-row K tile, pixel split) -> K = the image's output pixels; split partials
-//     summed through LDS in a fixed order -> the image's partial dW
+// ------------------------------------------------------------------------------------------------
+// Conv backward: grid (B, 1 + dgrad); blockIdx.y 0 = the weight gradient of image b, 1 = its input
+// gradient (two workgroups per image: all 256 CUs busy at B = 128).
+//   both roles: dZ = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) of the image in a zero-bordered LDS
+//     grid (this BN's backward sums from the fixed-order partials)
+//   weight gradient: items (16-row K tile, pixel split) -> K = the image's output pixels; the split
+//     partials summed through LDS in order -> the image's partial dW
+//   input gradient, the stride-s conv as a stride-1 "depth-to-space" product: every output-base block
+//     (ob_h, ob_w) gathers the same dZ window (taps jh < ceil(kh/sh), jw < ceil(kw/sw)) for all
+//     sh*sw sub-pixel classes, so A = that window [blocks x (jh, jw, co)] and B = the class-stacked
+//     weights [(jh, jw, co) x (class, ci)] -> dA of the whole sh x sw input block per output row;
+//     ReLU mask of the input BN -> g of the previous layer + that BN's backward partial sums
+constexpr int kMaxDgNT = 4;   // input-gradient N tiles: classes x C <= 64
 struct ConvBwdP {
   Geo g;
-  int K, Mo, Hp, Wp, Hd, Wd, Ph, Pw, zslot, dgrad, nci, nco, CP16;
-  int ncls, cls_nth[kMaxCls], cls_ntw[kMaxCls], cls_Kc[kMaxCls], cls_Kc16[kMaxCls], cls_wc[kMaxCls],
-      cls_ko[kMaxCls], cls_Mc[kMaxCls], cls_W[kMaxCls], cls_ih0[kMaxCls], cls_iw0[kMaxCls], cls_item0[kMaxCls + 1];
-  int n_dg_items, wg_tiles, wg_split, wg_spp, Kw16, n_items;
-  int o_cs, o_st, o_stin, o_kk, o_dz, o_xs, o_xr, o_wc, o_kod, o_kow, o_ptab, o_part, o_red, lds;
+  int K, Mo, Hp, Wp, Hd, Wd, Ph, Pw, zslot, dgrad, nco;
+  // input gradient (depth-to-space)
+  int nth, ntw, Kd, Kdp, ncls, NC, NP, nnt, obh0, obw0, Nbw, Md, mtd, ksd, spd, n_dg_items;
+  // weight gradient
+  int wg_tiles, wg_split, wg_spp, Kw16, n_wg_items;
+  Dv dC, dCo, dW, dWo, dWd, dWp, dkw, dntw, dNbw, dNP;
+  int o_red, o_cs, o_st, o_stin, o_kk, o_dz, o_role;
+  int o_xs, o_kow, o_ptab, o_part;           // weight-gradient role
+  int o_xr, o_wb, o_kod, o_partd;            // input-gradient role
+  int lds;
 };
 struct ConvBwdArgs {
   ConvBwdP p;
@@ -918,7 +927,6 @@ struct ConvBwdArgs {
   const float* w;
   const float* in; Bn bn_in; float* gin; double* acc_in;             // the input side
   float* dwpart;                     // [B][K][Co]
-  double* zero; int nzero;           // the backward sums of the layer after this one (consumed)
   long long* stamps;
 };
 
@@ -926,22 +934,16 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
   const ConvBwdP& P = a.p;
   const Geo& g = P.g;
-  double* cs = reinterpret_cast<double*>(sm + P.o_cs);
+  double* cs = reinterpret_cast<double*>(sm + P.o_cs);     // [16][2][64]
   double* red = reinterpret_cast<double*>(sm + P.o_red);
   float* st = reinterpret_cast<float*>(sm + P.o_st);       // this BN: mean, rstd, gamma*rstd
   float* stin = reinterpret_cast<float*>(sm + P.o_stin);   // input BN: sc, sh, mean, rstd
   float* kks = reinterpret_cast<float*>(sm + P.o_kk);      // sum g, sum g*xhat
   float* dz = reinterpret_cast<float*>(sm + P.o_dz);
-  float* Xs = reinterpret_cast<float*>(sm + P.o_xs);
-  float* Xr = reinterpret_cast<float*>(sm + P.o_xr);
-  float* Wc = reinterpret_cast<float*>(sm + P.o_wc);
-  int* kod = reinterpret_cast<int*>(sm + P.o_kod);
-  int* kow = reinterpret_cast<int*>(sm + P.o_kow);
-  int2* ptab = reinterpret_cast<int2*>(sm + P.o_ptab);
-  float* part = reinterpret_cast<float*>(sm + P.o_part);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
   const int b = blockIdx.x;
-  const int C = g.C, Co = g.Co, Mo = P.Mo, K = P.K, Wd = P.Wd, Wp = P.Wp, CP16 = P.CP16;
+  const bool dg = blockIdx.y == 1;
+  const int C = g.C, Co = g.Co, Mo = P.Mo, K = P.K, Wd = P.Wd, Wp = P.Wp;
   stamp(a.stamps, 0);
   // ---- one batch of global loads
   const int nact = Mo * Co, nimg = g.H * g.W * C, nw = K * Co;
@@ -954,16 +956,24 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
     const float* im = a.in + (size_t)b * nimg;
     pf_load(pg, nact, [&](int i) { return gz[i]; });
     pf_load(pz, nact, [&](int i) { return zz[i]; });
-    if (P.dgrad) pf_load(pw, nw, [&](int i) { return a.w[i]; });
+    if (dg) pf_load(pw, nw, [&](int i) { return a.w[i]; });
     pf_load(px, nimg, [&](int i) { return im[i]; });
   }
-  // the per-channel constants: slot partials of this layer's backward sums, saved statistics
+  // the per-channel constants: partials of this layer's backward sums (fixed-order sum), saved
+  // statistics
   const int Q = 2 * Co, np = NTB / Q, qq = tid % Q, qpart = tid / Q;
-  double sv[4];
+  double tsum = 0.0;
+  if (qpart < np) {
+    for (int j0 = qpart; j0 < a.bb.npart; j0 += 8 * np) {
+      double v[8];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int j = qpart + u * np;
-    sv[u] = (qpart < np && j < kSlots) ? a.bb.acc[j * Q + qq] : 0.0;
+      for (int u = 0; u < 8; ++u) {
+        const int j = j0 + u * np;
+        v[u] = j < a.bb.npart ? a.bb.acc[j * Q + qq] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) tsum += v[u];
+    }
   }
   float cmu = 0.f, crs = 0.f, cg = 1.f;
   if (tid < Co) {
@@ -979,54 +989,62 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
     ig = a.bn_in.gamma ? a.bn_in.gamma[ti] : 1.f;
     ib = a.bn_in.beta ? a.bn_in.beta[ti] : 0.f;
   }
-  zero_share(a.zero, a.nzero);
   // LDS the registers do not cover
   for (int i = tid; i < P.Hd * Wd; i += NTB) {
-    const int y = i / Wd, x = i - y * Wd;
+    const int y = dq(i, P.dWd), x = i - y * Wd;
     if (y < P.Ph || y >= P.Ph + g.Ho || x < P.Pw || x >= P.Pw + g.Wo)
       for (int c = 0; c < Co; ++c) dz[i * Co + c] = 0.f;
   }
   if (tid < 32) dz[P.zslot + tid] = 0.f;
-  for (int i = tid; i < P.Hp * Wp; i += NTB) {
-    const int y = i / Wp, x = i - y * Wp, iy = y - g.pt, ix = x - g.pl;
-    if (iy < 0 || iy >= g.H || ix < 0 || ix >= g.W)
-      for (int c = 0; c < C; ++c) Xs[i * C + c] = 0.f;
-  }
-  if (P.dgrad) {
-    for (int cl = 0; cl < P.ncls; ++cl) {
-      const int Kc = P.cls_Kc[cl], Kc16 = P.cls_Kc16[cl], ntw = P.cls_ntw[cl];
-      float* wc = Wc + P.cls_wc[cl];
-      for (int i = tid; i < Kc16 * CP16; i += NTB) {
-        const int kk = i / CP16, ci = i - kk * CP16;
-        if (kk >= Kc || ci >= C) wc[i] = 0.f;
+  if (!dg) {
+    float* Xs = reinterpret_cast<float*>(sm + P.o_xs);
+    int* kow = reinterpret_cast<int*>(sm + P.o_kow);
+    int2* ptab = reinterpret_cast<int2*>(sm + P.o_ptab);
+    for (int i = tid; i < P.Hp * Wp; i += NTB) {
+      const int y = dq(i, P.dWp), x = i - y * Wp, iy = y - g.pt, ix = x - g.pl;
+      if (iy < 0 || iy >= g.H || ix < 0 || ix >= g.W)
+        for (int c = 0; c < C; ++c) Xs[i * C + c] = 0.f;
+    }
+    for (int k = tid; k < P.Kw16; k += NTB) {
+      int off = 0;
+      if (k < K) {
+        const int t = dq(k, P.dC), ci = k - t * C, ky = dq(t, P.dkw), kx = t - ky * g.kw;
+        off = (ky * Wp + kx) * C + ci;
       }
-      for (int kk = tid; kk < Kc16; kk += NTB) {
-        int off = 0;
-        if (kk < Kc) {
-          const int co = kk % Co, t = kk / Co, jw = t % ntw, jh = t / ntw;
-          off = (-jh * Wd - jw) * Co + co;
-        }
-        kod[P.cls_ko[cl] + kk] = off;
+      kow[k] = off;
+    }
+    for (int p = tid; p < P.wg_split * P.wg_spp * 4; p += NTB) {
+      int2 e{0, P.zslot};
+      if (p < Mo) {
+        const int oh = dq(p, P.dWo), ow = p - oh * g.Wo;
+        e = int2{(oh * g.sh * Wp + ow * g.sw) * C, ((oh + P.Ph) * Wd + ow + P.Pw) * Co};
       }
+      ptab[p] = e;
+    }
+  } else {
+    float* Wb = reinterpret_cast<float*>(sm + P.o_wb);
+    int* kod = reinterpret_cast<int*>(sm + P.o_kod);
+    // class-stacked weights: zero where no weight lands (padding rows / columns, taps past the kernel)
+    for (int i = tid; i < P.Kdp * P.NP; i += NTB) {
+      const int kk = dq(i, P.dNP), n = i - kk * P.NP;
+      bool hole = kk >= P.Kd || n >= P.NC;
+      if (!hole) {
+        const int t = dq(kk, P.dCo), jh = dq(t, P.dntw), jw = t - jh * P.ntw;
+        const int cl = dq(n, P.dC), ry = cl / g.sw, rx = cl - ry * g.sw;
+        hole = ry + g.sh * jh >= g.kh || rx + g.sw * jw >= g.kw;
+      }
+      if (hole) Wb[i] = 0.f;
+    }
+    for (int kk = tid; kk < P.Kdp; kk += NTB) {
+      int off = 0;
+      if (kk < P.Kd) {
+        const int t = dq(kk, P.dCo), co = kk - t * Co, jh = dq(t, P.dntw), jw = t - jh * P.ntw;
+        off = (-jh * Wd - jw) * Co + co;
+      }
+      kod[kk] = off;
     }
   }
-  for (int k = tid; k < P.Kw16; k += NTB) {
-    int off = 0;
-    if (k < K) {
-      const int ci = k % C, t = k / C, kx = t % g.kw, ky = t / g.kw;
-      off = (ky * Wp + kx) * C + ci;
-    }
-    kow[k] = off;
-  }
-  for (int p = tid; p < P.wg_split * P.wg_spp * 4; p += NTB) {
-    int2 e{0, P.zslot};
-    if (p < Mo) {
-      const int oh = p / g.Wo, ow = p - oh * g.Wo;
-      e = int2{(oh * g.sh * Wp + ow * g.sw) * C, ((oh + P.Ph) * Wd + ow + P.Pw) * Co};
-    }
-    ptab[p] = e;
-  }
-  if (qpart < np) red[tid] = (sv[0] + sv[1]) + (sv[2] + sv[3]);
+  if (qpart < np) red[tid] = tsum;
   if (tid < Co) {
     st[tid] = cmu;
     st[Co + tid] = crs;
@@ -1034,8 +1052,9 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
   }
   if (ti >= 0 && ti < C) {
     const bool none = a.bn_in.mode == kBnNone;
-    stin[ti] = none ? 1.f : ig * irs;
-    stin[C + ti] = none ? 0.f : ib - imu * ig * irs;
+    const float sc = ig * irs;
+    stin[ti] = none ? 1.f : sc;
+    stin[C + ti] = none ? 0.f : ib - imu * sc;
     stin[2 * C + ti] = imu;
     stin[3 * C + ti] = irs;
   }
@@ -1044,89 +1063,57 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
     double S = 0.0;
     for (int p = 0; p < np; ++p) S += red[p * Q + tid];
     kks[tid] = (float)S;
-    if (b == 0) {
+    if (b == 0 && !dg) {
       if (tid < Co && a.bb.dbeta) a.bb.dbeta[tid] = (float)S;
       if (tid >= Co && a.bb.dgamma) a.bb.dgamma[tid - Co] = (float)S;
     }
   }
   lds_barrier();
   stamp(a.stamps, 1);
-  // ---- registers -> LDS: dZ, the input (raw and BN + ReLU'd), the class-ordered weights
+  // ---- registers -> LDS: dZ, the input (BN + ReLU'd for the weight gradient, raw for the input
+  // gradient's mask), the class-stacked weights
   {
     const float inv = 1.f / a.count;
 #pragma unroll
     for (int u = 0; u < kUAct; ++u) {
       const int i = tid + u * NTB;
       if (i < nact) {
-        const int co = i % Co, p = i / Co, oh = p / g.Wo, ow = p - oh * g.Wo;
+        const int p = dq(i, P.dCo), co = i - p * Co, oh = dq(p, P.dWo), ow = p - oh * g.Wo;
         const float xh = (pz.v[u] - st[co]) * st[Co + co];
         dz[((oh + P.Ph) * Wd + ow + P.Pw) * Co + co] =
             st[2 * Co + co] * (pg.v[u] - kks[co] * inv - xh * kks[Co + co] * inv);
       }
     }
-    const bool raw = a.bn_in.mode == kBnNone;
-    pf_store(px, nimg, [&](int i, float v) {
-      const int c = i % C, pix = i / C, y = pix / g.W, x = pix - y * g.W;
-      Xs[((y + g.pt) * Wp + x + g.pl) * C + c] = raw ? v : fmaxf(fmaf(v, stin[c], stin[C + c]), 0.f);
-      Xr[i] = v;
-    });
-    if (P.dgrad)
-      pf_store(pw, nw, [&](int i, float v) {
-        const int co = i % Co, t = i / Co, ci = t % C, t2 = t / C, kx = t2 % g.kw, ky = t2 / g.kw;
-        const int cl = (ky % g.sh) * g.sw + (kx % g.sw), jh = ky / g.sh, jw = kx / g.sw;
-        const int kk = (jh * P.cls_ntw[cl] + jw) * Co + co;
-        Wc[P.cls_wc[cl] + kk * CP16 + ci] = v;
+    if (!dg) {
+      float* Xs = reinterpret_cast<float*>(sm + P.o_xs);
+      const bool raw = a.bn_in.mode == kBnNone;
+      pf_store(px, nimg, [&](int i, float v) {
+        const int pix = dq(i, P.dC), c = i - pix * C, y = dq(pix, P.dW), x = pix - y * g.W;
+        Xs[((y + g.pt) * Wp + x + g.pl) * C + c] = raw ? v : fmaxf(fmaf(v, stin[c], stin[C + c]), 0.f);
       });
+    } else {
+      float* Xr = reinterpret_cast<float*>(sm + P.o_xr);
+      float* Wb = reinterpret_cast<float*>(sm + P.o_wb);
+      pf_store(px, nimg, [&](int i, float v) { Xr[i] = v; });
+      pf_store(pw, nw, [&](int i, float v) {
+        const int t = dq(i, P.dCo), co = i - t * Co, t2 = dq(t, P.dC), ci = t - t2 * C;
+        const int ky = dq(t2, P.dkw), kx = t2 - ky * g.kw;
+        const int cl = (ky % g.sh) * g.sw + (kx % g.sw), jh = ky / g.sh, jw = kx / g.sw;
+        Wb[((jh * P.ntw + jw) * Co + co) * P.NP + cl * C + ci] = v;
+      });
+    }
   }
   lds_barrier();
   stamp(a.stamps, 2);
-  // ---- work items
-  double s1[2] = {0.0, 0.0}, s2[2] = {0.0, 0.0};
-  for (int item = wave; item < P.n_items; item += 16) {
-    if (item < P.n_dg_items) {
-      int cl = 0;
-      while (cl + 1 < P.ncls && item >= P.cls_item0[cl + 1]) ++cl;
-      const int tile = item - P.cls_item0[cl];
-      const int Mc = P.cls_Mc[cl], Wc_ = P.cls_W[cl], ih0 = P.cls_ih0[cl], iw0 = P.cls_iw0[cl];
-      const int ry = cl / g.sw, rx = cl - ry * g.sw;
-      const int m = min(tile * 16 + fr, Mc - 1);
-      const int ih = ih0 + (m / Wc_) * g.sh, iw = iw0 + (m % Wc_) * g.sw;
-      const int ohb = (ih + g.pt - ry) / g.sh, owb = (iw + g.pl - rx) / g.sw;
-      const int base = ((ohb + P.Ph) * Wd + owb + P.Pw) * Co;
-      const int* ko = kod + P.cls_ko[cl];
-      const float* wc = Wc + P.cls_wc[cl];
-      f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-      for (int s0 = 0; s0 < P.cls_Kc16[cl] / 4; s0 += 4) {
-        int o[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) o[u] = ko[4 * (s0 + u) + fq];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int kk = 4 * (s0 + u) + fq;
-          const float av = dz[base + o[u]];
-          acc[0] = mfma4(av, wc[kk * CP16 + fr], acc[0]);
-          if (P.nci > 1) acc[1] = mfma4(av, wc[kk * CP16 + 16 + fr], acc[1]);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int mm = tile * 16 + fq * 4 + i;
-        if (mm >= Mc) continue;
-        const int ih2 = ih0 + (mm / Wc_) * g.sh, iw2 = iw0 + (mm % Wc_) * g.sw;
-#pragma unroll
-        for (int n = 0; n < 2; ++n) {
-          const int ci = n * 16 + fr;
-          if (n >= P.nci || ci >= C) continue;
-          const int e = (ih2 * g.W + iw2) * C + ci;
-          const float x = Xr[e];
-          const float gv = fmaf(x, stin[ci], stin[C + ci]) > 0.f ? acc[n][i] : 0.f;
-          a.gin[(size_t)b * nimg + e] = gv;
-          s1[n] += gv;
-          s2[n] += (double)(gv * (x - stin[2 * C + ci]) * stin[3 * C + ci]);
-        }
-      }
-    } else {
-      const int wi = item - P.n_dg_items, kt = wi % P.wg_tiles, sp = wi / P.wg_tiles;
+  if (!dg) {
+    // ---------------- weight gradient
+    const float* Xs = reinterpret_cast<const float*>(sm + P.o_xs);
+    const int* kow = reinterpret_cast<const int*>(sm + P.o_kow);
+    const int2* ptab = reinterpret_cast<const int2*>(sm + P.o_ptab);
+    float* part = reinterpret_cast<float*>(sm + P.o_part);
+    float* dst = a.dwpart + (size_t)b * K * Co;
+    for (int item = wave; item < P.n_wg_items; item += 16) {
+      const int kt = item % P.wg_tiles, sp = item / P.wg_tiles;
       const int off = kow[kt * 16 + fr];
       f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
       for (int s0 = 0; s0 < P.wg_spp; s0 += 4) {
@@ -1141,7 +1128,6 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
         }
       }
       if (P.wg_split == 1) {
-        float* dst = a.dwpart + (size_t)b * K * Co;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int k = kt * 16 + fq * 4 + i;
@@ -1158,25 +1144,108 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
             *reinterpret_cast<f32x4*>(part + ((size_t)((sp * P.wg_tiles + kt) * P.nco + n) * 64 + lane) * 4) = acc[n];
       }
     }
-  }
-  if (P.wg_split > 1) {
-    lds_barrier();
-    float* dst = a.dwpart + (size_t)b * K * Co;
-    for (int t = wave; t < P.wg_tiles * P.nco; t += 16) {
-      const int kt = t / P.nco, n = t - kt * P.nco;
-      f32x4 v = *reinterpret_cast<const f32x4*>(part + ((size_t)(kt * P.nco + n) * 64 + lane) * 4);
-      for (int sp = 1; sp < P.wg_split; ++sp)
-        v += *reinterpret_cast<const f32x4*>(part + ((size_t)((sp * P.wg_tiles + kt) * P.nco + n) * 64 + lane) * 4);
-      const int co = n * 16 + fr;
+    if (P.wg_split > 1) {
+      lds_barrier();
+      for (int t = wave; t < P.wg_tiles * P.nco; t += 16) {
+        const int kt = t / P.nco, n = t - kt * P.nco;
+        f32x4 v = *reinterpret_cast<const f32x4*>(part + ((size_t)(kt * P.nco + n) * 64 + lane) * 4);
+        for (int sp = 1; sp < P.wg_split; ++sp)
+          v += *reinterpret_cast<const f32x4*>(part + ((size_t)((sp * P.wg_tiles + kt) * P.nco + n) * 64 + lane) * 4);
+        const int co = n * 16 + fr;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int k = kt * 16 + fq * 4 + i;
-        if (k < K && co < Co) dst[(size_t)k * Co + co] = v[i];
+        for (int i = 0; i < 4; ++i) {
+          const int k = kt * 16 + fq * 4 + i;
+          if (k < K && co < Co) dst[(size_t)k * Co + co] = v[i];
+        }
       }
     }
+    stamp(a.stamps, 3);
+    return;
   }
-  if (P.dgrad) wave_cols_to_slot(s1, s2, cs, a.acc_in, C);
+  // ---------------- input gradient (depth-to-space)
+  const float* Xr = reinterpret_cast<const float*>(sm + P.o_xr);
+  const float* Wb = reinterpret_cast<const float*>(sm + P.o_wb);
+  const int* kod = reinterpret_cast<const int*>(sm + P.o_kod);
+  float* partd = reinterpret_cast<float*>(sm + P.o_partd);
+  const int ntile = P.mtd * P.nnt;
+  for (int item = wave; item < P.n_dg_items; item += 16) {
+    const int kp = item % P.ksd, t = item / P.ksd, nt = t % P.nnt, mtile = t / P.nnt;
+    const int m = min(mtile * 16 + fr, P.Md - 1);
+    const int obh = dq(m, P.dNbw), obw = m - obh * P.Nbw;
+    const int base = ((P.obh0 + obh + P.Ph) * Wd + P.obw0 + obw + P.Pw) * Co;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int i0 = 0; i0 < P.spd; i0 += 4) {
+      int o[4];
+      float bv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = 4 * (kp + (i0 + u) * P.ksd) + fq;
+        o[u] = kod[k];
+        bv[u] = Wb[k * P.NP + nt * 16 + fr];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = mfma4(dz[base + o[u]], bv[u], acc);
+    }
+    *reinterpret_cast<f32x4*>(partd + ((size_t)(kp * ntile + t) * 64 + lane) * 4) = acc;
+  }
+  lds_barrier();
   stamp(a.stamps, 3);
+  double s1[kMaxDgNT], s2[kMaxDgNT];
+#pragma unroll
+  for (int n = 0; n < kMaxDgNT; ++n) s1[n] = s2[n] = 0.0;
+  float* gin = a.gin + (size_t)b * nimg;
+  for (int t = wave; t < ntile; t += 16) {
+    const int nt = t % P.nnt, mtile = t / P.nnt;
+    f32x4 v = *reinterpret_cast<const f32x4*>(partd + ((size_t)t * 64 + lane) * 4);
+    for (int kp = 1; kp < P.ksd; ++kp) v += *reinterpret_cast<const f32x4*>(partd + ((size_t)(kp * ntile + t) * 64 + lane) * 4);
+    const int n = nt * 16 + fr;
+    if (n >= P.NC) continue;
+    const int cl = dq(n, P.dC), ci = n - cl * C, ry = cl / g.sw, rx = cl - ry * g.sw;
+    double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = mtile * 16 + fq * 4 + i;
+      if (m >= P.Md) continue;
+      const int obh = dq(m, P.dNbw), obw = m - obh * P.Nbw;
+      const int ih = (P.obh0 + obh) * g.sh + ry - g.pt, iw = (P.obw0 + obw) * g.sw + rx - g.pl;
+      if (ih < 0 || ih >= g.H || iw < 0 || iw >= g.W) continue;
+      const int e = (ih * g.W + iw) * C + ci;
+      const float x = Xr[e];
+      const float gv = fmaf(x, stin[ci], stin[C + ci]) > 0.f ? v[i] : 0.f;
+      gin[e] = gv;
+      t1 += gv;
+      t2 += (double)(gv * (x - stin[2 * C + ci]) * stin[3 * C + ci]);
+    }
+#pragma unroll
+    for (int q = 0; q < kMaxDgNT; ++q)
+      if (q == nt) {
+        s1[q] += t1;
+        s2[q] += t2;
+      }
+  }
+  // the input BN's backward partial sums: per-wave column sums -> cs[wave][stat][64 columns] -> per
+  // channel (columns n with n % C == ci), waves and columns in a fixed order
+#pragma unroll
+  for (int q = 0; q < kMaxDgNT; ++q) {
+    double x1 = s1[q], x2 = s2[q];
+    x1 += __shfl_xor(x1, 16, 64);
+    x1 += __shfl_xor(x1, 32, 64);
+    x2 += __shfl_xor(x2, 16, 64);
+    x2 += __shfl_xor(x2, 32, 64);
+    if (fq == 0) {
+      cs[(wave * 2 + 0) * 64 + q * 16 + fr] = x1;
+      cs[(wave * 2 + 1) * 64 + q * 16 + fr] = x2;
+    }
+  }
+  lds_barrier();
+  if (tid < 2 * C) {
+    const int j = tid / C, c = tid - j * C;
+    double S = 0.0;
+    for (int w = 0; w < 16; ++w)
+      for (int n = c; n < P.NC; n += C) S += cs[(w * 2 + j) * 64 + n];
+    a.acc_in[(size_t)b * 2 * C + j * C + c] = S;
+  }
+  stamp(a.stamps, 4);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1191,12 +1260,10 @@ struct ReduceArgs {
   long long len[kMaxRed];
   int cnt[kMaxRed];            // partials of the segment
   int blk0[kMaxRed + 1];       // first workgroup of the segment
-  double* zero; int nzero;
   long long* stamps;
 };
 __global__ __launch_bounds__(NTH) void reduce_kernel(ReduceArgs a) {
   __shared__ float red[4][64];
-  zero_share(a.zero, a.nzero);
   const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
   int j = 0;
   while (j + 1 < a.n && (int)blockIdx.x >= a.blk0[j + 1]) ++j;
@@ -1230,23 +1297,23 @@ using namespace tde::bncnn;
 struct TdeBnGeo { int H, W, C, Ho, Wo, Co, kh, kw, sh, sw, pt, pl; };
 struct TdeBn {
   int mode, C;
-  const double* acc; double count;
+  const double* acc; int npart; double count;
   const float *gamma, *beta;
   float eps, momentum, bessel;
   float *mmean, *mvar, *saved;
 };
 struct TdeBnBwd {
-  const double* acc;
+  const double* acc; int npart;
   float *dbeta, *dgamma;
 };
 static Geo geo_of(const TdeBnGeo* g) { return Geo{g->H, g->W, g->C, g->Ho, g->Wo, g->Co, g->kh, g->kw, g->sh, g->sw, g->pt, g->pl}; }
 static Bn bn_of(const TdeBn* b) {
-  return Bn{b->mode, b->C, b->acc, b->count, b->gamma, b->beta, b->eps, b->momentum, b->bessel, b->mmean, b->mvar,
+  return Bn{b->mode, b->C, b->acc, b->npart, b->count, b->gamma, b->beta, b->eps, b->momentum, b->bessel, b->mmean, b->mvar,
             b->saved};
 }
 static bool bn_ok(const TdeBn* b) {
   if (!b || b->C < 1 || b->C > 32) return false;
-  if ((b->mode == kBnTrain || b->mode == kBnBatch) && (!b->acc || !(b->count > 0))) return false;
+  if ((b->mode == kBnTrain || b->mode == kBnBatch) && (!b->acc || b->npart < 1 || !(b->count > 0))) return false;
   if (b->mode == kBnTrain && !b->saved) return false;
   if (b->mode == kBnMoving && (!b->mmean || !b->mvar)) return false;
   if (b->mode == kBnSaved && !b->saved) return false;
@@ -1275,7 +1342,8 @@ static void set_lds(F* f, int bytes) {
 static int up(int x, int m) { return (x + m - 1) / m * m; }
 constexpr int kMaxLds = 160 * 1024;
 
-TDE_API int tde_bncnn_stat_slots() { return kSlots; }
+
+static Dv dv(int d) { return Dv{d, 1.0f / (float)d}; }
 
 // Forward conv launch geometry; 0 if it fits (LDS, prefetch registers), <0 otherwise.
 static int conv_fwd_plan(const Geo& g, ConvFwdP& P) {
@@ -1290,12 +1358,21 @@ static int conv_fwd_plan(const Geo& g, ConvFwdP& P) {
   P.nct = (g.Co + 15) / 16;
   const int steps = (P.K + 3) / 4;
   P.mt = (P.M + 15) / 16;
-  const int base = P.mt * P.nct;
+  P.msplit = P.mt >= 2 ? 2 : 1;
+  P.mtw = (P.mt + P.msplit - 1) / P.msplit;
+  P.msplit = (P.mt + P.mtw - 1) / P.mtw;
+  const int base = P.mtw * P.nct;
   P.ks = 1;
   while (base * P.ks < 16 && P.ks < 8 && (steps + 2 * P.ks - 1) / (2 * P.ks) >= 8) P.ks *= 2;
   P.spp = up((steps + P.ks - 1) / P.ks, 4);
   P.Kpad = 4 * P.ks * P.spp;
-  P.nitems = base * P.ks;
+  P.dC = dv(g.C);
+  P.dCo = dv(g.Co);
+  P.dW = dv(g.W);
+  P.dWo = dv(g.Wo);
+  P.dWp = dv(P.Wp);
+  P.dkw = dv(g.kw);
+  P.dNTP = dv(P.nct * 16);
   int o = 0;
   P.o_red = o; o += NTB * 8;
   P.o_cs = o; o += 16 * 2 * 32 * 8;
@@ -1308,39 +1385,38 @@ static int conv_fwd_plan(const Geo& g, ConvFwdP& P) {
   return o > kMaxLds ? -3 : 0;
 }
 
-// out = {lds, ks, nitems}
+// out = {lds, ks, msplit (workgroups per image = statistics partials per image)}
 TDE_API int tde_bncnn_conv_fwd_cfg(const TdeBnGeo* gg, int* out) {
   ConvFwdP P;
   const int rc = conv_fwd_plan(geo_of(gg), P);
   out[0] = P.lds;
   out[1] = P.ks;
-  out[2] = P.nitems;
+  out[2] = P.msplit;
   return rc;
 }
 
-// z = conv(relu(BN_in(in))); this layer's BN sums into acc (nullable).  zero/nzero: a statistics
-// buffer the grid zeroes.
+// z = conv(relu(BN_in(in))); this layer's BN partial sums into acc [B][2][Co] (nullable).
 TDE_API int tde_bncnn_conv_fwd(const TdeBnGeo* gg, int B, const float* in, const TdeBn* bn_in, const float* w, float* z,
-                               double* acc, double* zero, int nzero, hipStream_t stream) {
+                               double* acc, hipStream_t stream) {
   ConvFwdP P;
   if (conv_fwd_plan(geo_of(gg), P) != 0) return -1;
   if (!bn_ok(bn_in) || bn_in->C != P.g.C || B < 1 || bn_in->mode == kBnSaved) return -2;
-  ConvFwdArgs a{P, B, in, bn_of(bn_in), w, z, acc, zero, nzero, next_stamps()};
+  ConvFwdArgs a{P, B, in, bn_of(bn_in), w, z, acc, next_stamps()};
   set_lds(conv_fwd_kernel, P.lds);
-  conv_fwd_kernel<<<B, NTB, P.lds, stream>>>(a);
+  conv_fwd_kernel<<<dim3(B, P.msplit), NTB, P.lds, stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;
 }
 
 TDE_API int tde_bncnn_dense_fwd(int B, int K, int D, int Dp, int kc, const float* in, const TdeBn* bn, const float* w,
-                                float* hpart, double* zero, int nzero, hipStream_t stream) {
+                                float* hpart, hipStream_t stream) {
   if (!bn_ok(bn) || bn->mode == kBnSaved || bn->mode == kBnNone || (kc & 15) || kc < 16 || (Dp & 15) || Dp < D)
     return -1;
   if ((K + kc - 1) / kc > kMaxKc || 64 * kc > kUA * NTB || kc * kDenseCols > kUB * NTB) return -2;
   const int lda = kc + 4, ldb = kDenseCols + 4;
   const int lds = NTB * 8 + 4 * 32 * 4 + 64 * lda * 4 + kc * ldb * 4;
   if (lds > kMaxLds) return -3;
-  DenseFwdArgs a{B, K, D, Dp, kc, lda, ldb, in, bn_of(bn), w, hpart, zero, nzero, next_stamps()};
+  DenseFwdArgs a{B, K, D, Dp, kc, lda, ldb, in, bn_of(bn), w, hpart, next_stamps()};
   set_lds(dense_fwd_kernel, lds);
   dense_fwd_kernel<<<dim3((Dp + kDenseCols - 1) / kDenseCols, (K + kc - 1) / kc, (B + 63) / 64), NTB, lds, stream>>>(a);
   TDE_LAUNCH_CHECK();
@@ -1352,8 +1428,8 @@ TDE_API int tde_bncnn_head(int B, int D, int Dp, int NC, int mode, const float* 
                            const TdeBn* bn, float rate,
                            unsigned long long seed, const long long* iter, int layer_id, int drop_on, const float* wh,
                            const float* bh, float* logits, const int* labels, float scale, float* metrics, float* out,
-                           int out_softmax, float* dwh, float* dbh, float* dbeta, float* dgamma, float* dh, double* zero,
-                           int nzero, hipStream_t stream) {
+                           int out_softmax, float* dwh, float* dbh, float* dbeta, float* dgamma, float* dh,
+                           hipStream_t stream) {
   // the head computes its BN statistics itself: check the fields it uses
   if (!bn || bn->C != D || (Dp & 15) || Dp < D || Dp > 16 * kHeadMaxTiles || NC < 1 || NC > 16 || B < 1 || !logits ||
       nkc < 1 || nkc > kMaxKc || !hpart || !h)
@@ -1365,11 +1441,9 @@ TDE_API int tde_bncnn_head(int B, int D, int Dp, int NC, int mode, const float* 
   if (mode == 2 && !out) return -4;
   if (drop_on && !(rate > 0.f && rate < 1.f)) return -5;
   HeadArgs a{B, D, Dp, NC, mode, hpart, nkc, h, bn_of(bn), rate, seed, iter, layer_id, drop_on, wh, bh, logits, labels, scale,
-             metrics, out, out_softmax, dwh, dbh, dbeta, dgamma, dh, zero, nzero, next_stamps()};
+             metrics, out, out_softmax, dwh, dbh, dbeta, dgamma, dh, next_stamps()};
   head_fwd_kernel<<<Dp / 16, NTH, 0, stream>>>(a);
   TDE_LAUNCH_CHECK();
-  a.zero = nullptr;
-  a.nzero = 0;
   a.stamps = next_stamps();
   head_bwd_kernel<<<mode == 0 ? Dp / 16 : 1, NTH, 0, stream>>>(a);
   TDE_LAUNCH_CHECK();
@@ -1399,87 +1473,97 @@ static int conv_bwd_plan(const Geo& g, int dgrad, ConvBwdP& P) {
   P.Mo = g.Ho * g.Wo;
   if (g.C < 1 || g.C > 32 || g.Co < 1 || g.Co > 32 || g.sh < 1 || g.sw < 1 || g.sh * g.sw > kMaxCls) return -1;
   if (P.Mo * g.Co > kUAct * NTB || g.H * g.W * g.C > kUImg * NTB || (dgrad && P.K * g.Co > kUW * NTB)) return -2;
-  P.nci = (g.C + 15) / 16;
   P.nco = (g.Co + 15) / 16;
-  P.CP16 = P.nci * 16;
-  const int nth = (g.kh + g.sh - 1) / g.sh, ntw = (g.kw + g.sw - 1) / g.sw;
-  P.Ph = dgrad ? nth + 1 : 0;
-  P.Pw = dgrad ? ntw + 1 : 0;
-  // bottom / right margin: the largest base row (H-1+pt)/sh must stay inside the bordered grid
+  P.nth = (g.kh + g.sh - 1) / g.sh;
+  P.ntw = (g.kw + g.sw - 1) / g.sw;
+  P.Ph = dgrad ? P.nth + 1 : 0;
+  P.Pw = dgrad ? P.ntw + 1 : 0;
+  // bottom / right margin: the largest output-base row (H-1+pt)/sh must stay inside the bordered grid
   P.Hd = g.Ho + 2 * P.Ph + (dgrad ? std::max((g.H - 1 + g.pt) / g.sh - (g.Ho - 1), 0) : 0);
   P.Wd = g.Wo + 2 * P.Pw + (dgrad ? std::max((g.W - 1 + g.pl) / g.sw - (g.Wo - 1), 0) : 0);
   P.Hp = std::max((g.Ho - 1) * g.sh + g.kh, g.pt + g.H);
   P.Wp = std::max((g.Wo - 1) * g.sw + g.kw, g.pl + g.W);
   P.zslot = P.Hd * P.Wd * g.Co;
-  // input-gradient classes
-  P.ncls = dgrad ? g.sh * g.sw : 0;
-  int wc = 0, ko = 0, items = 0;
-  for (int cl = 0; cl < P.ncls; ++cl) {
-    const int ry = cl / g.sw, rx = cl % g.sw;
-    const int ih0 = ((ry - g.pt) % g.sh + g.sh) % g.sh, iw0 = ((rx - g.pl) % g.sw + g.sw) % g.sw;
-    const int Hc = ih0 < g.H ? (g.H - ih0 + g.sh - 1) / g.sh : 0;
-    const int Wc = iw0 < g.W ? (g.W - iw0 + g.sw - 1) / g.sw : 0;
-    const int cnth = (g.kh - ry + g.sh - 1) / g.sh, cntw = (g.kw - rx + g.sw - 1) / g.sw;
-    P.cls_nth[cl] = cnth;
-    P.cls_ntw[cl] = cntw;
-    P.cls_Kc[cl] = cnth * cntw * g.Co;
-    P.cls_Kc16[cl] = up(std::max(P.cls_Kc[cl], 1), 16);
-    P.cls_wc[cl] = wc;
-    wc += P.cls_Kc16[cl] * P.CP16;
-    P.cls_ko[cl] = ko;
-    ko += P.cls_Kc16[cl];
-    P.cls_Mc[cl] = Hc * Wc;
-    P.cls_W[cl] = std::max(Wc, 1);
-    P.cls_ih0[cl] = ih0;
-    P.cls_iw0[cl] = iw0;
-    P.cls_item0[cl] = items;
-    items += (Hc * Wc + 15) / 16;
-  }
-  P.cls_item0[P.ncls] = items;
-  P.n_dg_items = items;
+  // input gradient (depth-to-space): blocks = output-base positions with at least one input pixel
+  P.ncls = g.sh * g.sw;
+  P.NC = P.ncls * g.C;
+  P.NP = (P.NC + 15) / 16 * 16;
+  P.nnt = P.NP / 16;
+  if (dgrad && P.nnt > kMaxDgNT) return -1;
+  P.Kd = P.nth * P.ntw * g.Co;
+  P.obh0 = g.pt / g.sh;
+  P.obw0 = g.pl / g.sw;
+  const int Nbh = (g.H - 1 + g.pt) / g.sh - P.obh0 + 1;
+  P.Nbw = (g.W - 1 + g.pl) / g.sw - P.obw0 + 1;
+  P.Md = Nbh * P.Nbw;
+  P.mtd = (P.Md + 15) / 16;
+  const int dsteps = (P.Kd + 3) / 4;
+  P.ksd = 1;
+  while (P.mtd * P.nnt * P.ksd < 16 && P.ksd < 4 && (dsteps + 2 * P.ksd - 1) / (2 * P.ksd) >= 8) P.ksd *= 2;
+  P.spd = up((dsteps + P.ksd - 1) / P.ksd, 4);
+  P.Kdp = 4 * P.ksd * P.spd;
+  P.n_dg_items = dgrad ? P.mtd * P.nnt * P.ksd : 0;
   // weight gradient: K tiles x pixel splits (~32 items; >= 4 steps per split)
   P.wg_tiles = (P.K + 15) / 16;
   P.Kw16 = P.wg_tiles * 16;
   const int wsteps = (P.Mo + 3) / 4;
   P.wg_split = std::max(1, std::min(std::min(16, 32 / P.wg_tiles), wsteps / 4));
   P.wg_spp = up((wsteps + P.wg_split - 1) / P.wg_split, 4);
-  P.n_items = items + P.wg_tiles * P.wg_split;
+  P.n_wg_items = P.wg_tiles * P.wg_split;
+  P.dC = dv(g.C);
+  P.dCo = dv(g.Co);
+  P.dW = dv(g.W);
+  P.dWo = dv(g.Wo);
+  P.dWd = dv(P.Wd);
+  P.dWp = dv(P.Wp);
+  P.dkw = dv(g.kw);
+  P.dntw = dv(P.ntw);
+  P.dNbw = dv(P.Nbw);
+  P.dNP = dv(P.NP);
   int o = 0;
   P.o_red = o; o += NTB * 8;
-  P.o_cs = o; o += 16 * 2 * 32 * 8;
+  P.o_cs = o; o += 16 * 2 * 64 * 8;
   P.o_st = o; o += 4 * 32 * 4;
   P.o_stin = o; o += 4 * 32 * 4;
   P.o_kk = o; o += 2 * 32 * 4;
   P.o_dz = o; o += up(P.zslot + 32, 4) * 4;
-  P.o_xs = o; o += up(P.Hp * P.Wp * g.C, 4) * 4;
-  P.o_xr = o; o += up(g.H * g.W * g.C, 4) * 4;
-  P.o_wc = o; o += wc * 4;
-  P.o_kod = o; o += up(ko, 4) * 4;
-  P.o_kow = o; o += P.Kw16 * 4;
-  P.o_ptab = o; o += P.wg_split * P.wg_spp * 4 * 8;
-  P.o_part = o; o += (P.wg_split > 1 ? P.wg_split * P.wg_tiles * P.nco * 256 : 0) * 4;
-  P.lds = o;
-  return o > kMaxLds ? -3 : 0;
+  P.o_role = o;
+  int ow = o;   // weight-gradient role
+  P.o_xs = ow; ow += up(P.Hp * P.Wp * g.C, 4) * 4;
+  P.o_kow = ow; ow += P.Kw16 * 4;
+  P.o_ptab = ow; ow += P.wg_split * P.wg_spp * 4 * 8;
+  P.o_part = ow; ow += (P.wg_split > 1 ? P.wg_split * P.wg_tiles * P.nco * 256 : 0) * 4;
+  int od = o;   // input-gradient role
+  if (dgrad) {
+    P.o_xr = od; od += up(g.H * g.W * g.C, 4) * 4;
+    P.o_wb = od; od += P.Kdp * P.NP * 4;
+    P.o_kod = od; od += P.Kdp * 4;
+    P.o_partd = od; od += P.ksd * P.mtd * P.nnt * 256 * 4;
+  }
+  P.lds = std::max(ow, od);
+  // the fast divisions: every dividend stays below 2^21
+  return P.lds > kMaxLds ? -3 : 0;
 }
 
-// out = {lds, n_items, n_dg_items, wg_split}
+// out = {lds, wgrad items, dgrad items, wgrad split, dgrad K split}
 TDE_API int tde_bncnn_conv_bwd_plan(const TdeBnGeo* gg, int dgrad, int* out) {
   ConvBwdP P;
   const int rc = conv_bwd_plan(geo_of(gg), dgrad, P);
   out[0] = P.lds;
-  out[1] = P.n_items;
+  out[1] = P.n_wg_items;
   out[2] = P.n_dg_items;
   out[3] = P.wg_split;
+  out[4] = P.ksd;
   return rc;
 }
 
 TDE_API int tde_bncnn_conv_bwd(const TdeBnGeo* gg, int B, const float* z, const TdeBn* bn, const TdeBnBwd* bb,
                                const float* gout, const float* w, const float* in, const TdeBn* bn_in, float* gin,
-                               double* acc_in, float* dwpart, int dgrad, double* zero, int nzero, hipStream_t stream) {
+                               double* acc_in, float* dwpart, int dgrad, hipStream_t stream) {
   ConvBwdP P;
   if (conv_bwd_plan(geo_of(gg), dgrad, P) != 0) return -1;
   const Geo& g = P.g;
-  if (!bn_ok(bn) || bn->mode != kBnSaved || bn->C != g.Co || !bb || !bb->acc) return -2;
+  if (!bn_ok(bn) || bn->mode != kBnSaved || bn->C != g.Co || !bb || !bb->acc || bb->npart < 1) return -2;
   if (!bn_ok(bn_in) || bn_in->C != g.C || !(bn_in->mode == kBnSaved || bn_in->mode == kBnNone)) return -3;
   if (dgrad && (!gin || !acc_in || bn_in->mode != kBnSaved || !w)) return -4;
   ConvBwdArgs a{};
@@ -1487,7 +1571,7 @@ TDE_API int tde_bncnn_conv_bwd(const TdeBnGeo* gg, int B, const float* z, const 
   a.B = B;
   a.z = z;
   a.bn = bn_of(bn);
-  a.bb = BnBwd{bb->acc, bb->dbeta, bb->dgamma};
+  a.bb = BnBwd{bb->acc, bb->npart, bb->dbeta, bb->dgamma};
   a.gout = gout;
   a.count = (float)((double)B * g.Ho * g.Wo);
   a.w = w;
@@ -1496,23 +1580,19 @@ TDE_API int tde_bncnn_conv_bwd(const TdeBnGeo* gg, int B, const float* z, const 
   a.gin = gin;
   a.acc_in = acc_in;
   a.dwpart = dwpart;
-  a.zero = zero;
-  a.nzero = nzero;
   a.stamps = next_stamps();
   set_lds(conv_bwd_kernel, P.lds);
-  conv_bwd_kernel<<<B, NTB, P.lds, stream>>>(a);
+  conv_bwd_kernel<<<dim3(B, dgrad ? 2 : 1), NTB, P.lds, stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;
 }
 
 // n segments: part[j] holds cnt[j] partials of len[j] floats, summed in order into out[j].
 TDE_API int tde_bncnn_reduce(int n, const int* cnt, const float* const* part, float* const* out, const long long* len,
-                             double* zero, int nzero, hipStream_t stream) {
+                             hipStream_t stream) {
   if (n < 1 || n > kMaxRed) return -1;
   ReduceArgs a{};
   a.n = n;
-  a.zero = zero;
-  a.nzero = nzero;
   a.stamps = next_stamps();
   int blocks = 0;
   for (int j = 0; j < n; ++j) {

@@ -35,22 +35,21 @@ BN_NONE, BN_TRAIN, BN_MOVING, BN_BATCH, BN_SAVED = 0, 1, 2, 3, 4
 _vp, _i = C.c_void_p, C.c_int
 N.register_hip({
     "tde_bncnn_conv_fwd_cfg": (_i, [_vp, _vp]),
-    # geo, B, in, bn_in, w, z, acc, zero, nzero, stream
-    "tde_bncnn_conv_fwd": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
-    # B, K, D, Dp, kc, in, bn, w, hpart, zero, nzero, stream
-    "tde_bncnn_dense_fwd": (_i, [_i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
-    "tde_bncnn_stat_slots": (_i, []),
+    # geo, B, in, bn_in, w, z, acc, stream
+    "tde_bncnn_conv_fwd": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
+    # B, K, D, Dp, kc, in, bn, w, hpart, stream
+    "tde_bncnn_dense_fwd": (_i, [_i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]),
     # B, D, Dp, NC, mode, hpart, nkc, h, bn, rate, seed, iter, layer_id, drop_on, wh, bh, logits, labels, scale,
-    # metrics, out, out_softmax, dwh, dbh, dbeta, dgamma, dh, zero, nzero, stream
+    # metrics, out, out_softmax, dwh, dbh, dbeta, dgamma, dh, stream
     "tde_bncnn_head": (_i, [_i, _i, _i, _i, _i, _vp, _i, _vp, _vp, C.c_float, C.c_ulonglong, _vp, _i, _i, _vp, _vp,
-                            _vp, _vp, C.c_float, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
+                            _vp, _vp, C.c_float, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
     # B, K, D, Dp, in, bn, w, dh, dwpart, g, acc, stream
     "tde_bncnn_dense_bwd": (_i, [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "tde_bncnn_conv_bwd_plan": (_i, [_vp, _i, _vp]),
-    # geo, B, z, bn, bb, gout, w, in, bn_in, gin, acc_in, dwpart, dgrad, zero, nzero, stream
-    "tde_bncnn_conv_bwd": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _i, _vp]),
-    # n, cnt, part, out, len, zero, nzero, stream
-    "tde_bncnn_reduce": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
+    # geo, B, z, bn, bb, gout, w, in, bn_in, gin, acc_in, dwpart, dgrad, stream
+    "tde_bncnn_conv_bwd": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
+    # n, cnt, part, out, len, stream
+    "tde_bncnn_reduce": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
 })
 
 
@@ -59,15 +58,15 @@ class Geo(C.Structure):
 
 
 class Bn(C.Structure):
-    """acc: f64 [2][C] batch sums (sum, sum of squares) over `count` values."""
-    _fields_ = [("mode", C.c_int), ("C", C.c_int), ("acc", C.c_void_p), ("count", C.c_double),
+    """acc: f64 [npart][2][C] per-workgroup partial batch sums (sum, sum of squares) over `count` values."""
+    _fields_ = [("mode", C.c_int), ("C", C.c_int), ("acc", C.c_void_p), ("npart", C.c_int), ("count", C.c_double),
                 ("gamma", C.c_void_p), ("beta", C.c_void_p), ("eps", C.c_float), ("momentum", C.c_float),
                 ("bessel", C.c_float), ("mmean", C.c_void_p), ("mvar", C.c_void_p), ("saved", C.c_void_p)]
 
 
 class BnBwd(C.Structure):
-    """acc: f64 [2][C] backward sums (sum g, sum g*xhat)."""
-    _fields_ = [("acc", C.c_void_p), ("dbeta", C.c_void_p), ("dgamma", C.c_void_p)]
+    """acc: f64 [npart][2][C] per-workgroup partial backward sums (sum g, sum g*xhat)."""
+    _fields_ = [("acc", C.c_void_p), ("npart", C.c_int), ("dbeta", C.c_void_p), ("dgamma", C.c_void_p)]
 
 
 _P = N.ptr
@@ -148,7 +147,6 @@ class BnCnnPlan(ReplicaPlan):
         B = self.B
         f32 = dict(dtype=torch.float32, device=dev)
         f64 = dict(dtype=torch.float64, device=dev)
-        slots = self.lib.tde_bncnn_stat_slots()   # statistics sums are spread over this many copies
         self.blocks = []
         for conv, bn in spec["convs"]:
             H, W_, Cin = conv.input_shape
@@ -162,10 +160,11 @@ class BnCnnPlan(ReplicaPlan):
             rc = self.lib.tde_bncnn_conv_fwd_cfg(C.byref(g), cfg)
             if rc != 0:
                 raise ValueError(f"{conv.name}: no forward tile configuration fits ({rc})")
-            blk = dict(conv=conv, bn=bn, geo=g, K=K, cfg=list(cfg),
+            msplit = cfg[2]   # forward workgroups per image = BN statistics partials per image
+            blk = dict(conv=conv, bn=bn, geo=g, K=K, cfg=list(cfg), msplit=msplit,
                        w=st.view(f"{conv.name}/kernel"), gw=st.grad(f"{conv.name}/kernel"),
                        z=torch.zeros(B * M * Co, **f32), g=torch.zeros(B * M * Co, **f32),
-                       acc=torch.zeros(slots * 2 * Co, **f64), accb=torch.zeros(slots * 2 * Co, **f64),
+                       acc=torch.zeros(msplit * B * 2 * Co, **f64), accb=torch.zeros(B * 2 * Co, **f64),
                        saved=torch.zeros(2 * Co, **f32), dwpart=torch.zeros(B * K * Co, **f32))
             blk.update(self._bn_vars(bn))
             self.blocks.append(blk)
@@ -186,6 +185,8 @@ class BnCnnPlan(ReplicaPlan):
         self.wd, self.gwd = st.view(f"{dense.name}/kernel"), st.grad(f"{dense.name}/kernel")
         self.nrb = -(-B // 64)   # dense dW partials: one per 64-row block
         self.dwd_part = torch.zeros(self.nrb * self.K * self.D, **f32)
+        # the dense backward (grid K/32 x row blocks) produces the last conv BN's backward partials
+        last["accb"] = torch.zeros(-(-self.K // 32) * self.nrb * 2 * last["geo"].Co, **f64)
         self.bnd = dict(layer=bn_d, saved=torch.zeros(2 * self.D, **f32), **self._bn_vars(bn_d))
         self.drop = drop
         self.drop_seed = 0
@@ -220,18 +221,12 @@ class BnCnnPlan(ReplicaPlan):
 
     # ------------------------------------------------------------------ descriptors
     def _bn(self, blk, mode, B):
+        """Descriptor of a conv block's BN; its forward partials come from the block's conv workgroups."""
         g = blk["geo"]
         R = B * g.Ho * g.Wo
-        return Bn(mode, g.Co, _P(blk["acc"]), float(R), _P(blk["gamma"]), _P(blk["beta"]), float(blk["eps"]),
-                  float(blk["momentum"]), float(R / max(R - 1, 1)), _P(blk["mmean"]), _P(blk["mvar"]),
-                  _P(blk["saved"]))
-
-    def _acc(self, i, key="acc"):
-        """(pointer, n) of block i's f64 statistics buffer, or (None, 0) outside the chain."""
-        if 0 <= i < len(self.blocks):
-            t = self.blocks[i][key]
-            return _P(t), t.numel()
-        return None, 0
+        return Bn(mode, g.Co, _P(blk["acc"]), int(B * blk["msplit"]), float(R), _P(blk["gamma"]), _P(blk["beta"]),
+                  float(blk["eps"]), float(blk["momentum"]), float(R / max(R - 1, 1)), _P(blk["mmean"]),
+                  _P(blk["mvar"]), _P(blk["saved"]))
 
     def _fwd_mode(self, training):
         if training == "train":
@@ -244,30 +239,25 @@ class BnCnnPlan(ReplicaPlan):
         lib, s = self.lib, N.stream_ptr()
         mode = self._fwd_mode(phase)
         batch_stats = mode in (BN_TRAIN, BN_BATCH)
-        # launch i of the chain [conv_1..conv_L, dense, head] zeroes block i-2's statistics sums (consumed
-        # by launch i-1), so every step starts from zero sums without a memset
         inp = x
         bn_in = Bn(BN_NONE, self.blocks[0]["geo"].C)
         for li, blk in enumerate(self.blocks):
-            zp, zn = self._acc(li - 2)
             rc = lib.tde_bncnn_conv_fwd(C.byref(blk["geo"]), B, _P(inp), C.byref(bn_in), _P(blk["w"]), _P(blk["z"]),
-                                        _P(blk["acc"]) if batch_stats else None, zp, zn, s)
-            if rc < 0:
+                                        _P(blk["acc"]) if batch_stats else None, s)
+            if rc != 0:
                 raise RuntimeError(f"tde_bncnn_conv_fwd({blk['conv'].name}) failed with {rc}")
             bn_in = self._bn(blk, mode, B)
             inp = blk["z"]
-        zp, zn = self._acc(len(self.blocks) - 2)
         rc = lib.tde_bncnn_dense_fwd(B, self.K, self.D, self.Dp, self.kc, _P(inp), C.byref(bn_in), _P(self.wd),
-                                     _P(self.hpart), zp, zn, s)
+                                     _P(self.hpart), s)
         N.check(rc, "tde_bncnn_dense_fwd")
         return bn_in
 
     def _head(self, B, hmode, phase, labels, scale, probs=None):
         mode = self._fwd_mode(phase)
         bnd = self.bnd
-        bn = Bn(mode, self.D, None, float(B), _P(bnd["gamma"]), _P(bnd["beta"]), float(bnd["eps"]),
+        bn = Bn(mode, self.D, None, 0, float(B), _P(bnd["gamma"]), _P(bnd["beta"]), float(bnd["eps"]),
                 float(bnd["momentum"]), 1.0, _P(bnd["mmean"]), _P(bnd["mvar"]), _P(bnd["saved"]))
-        zp, zn = self._acc(len(self.blocks) - 1)
         drop_on = int(self.drop is not None and self.drop.rate > 0 and phase is not False)
         train = hmode == 0
         rc = self.lib.tde_bncnn_head(
@@ -276,7 +266,7 @@ class BnCnnPlan(ReplicaPlan):
             self.drop_seed, _P(self.iterations), 0, drop_on, _P(self.wh), _P(self.bh), _P(self.logits), _P(labels),
             float(scale), _P(self.metrics) if hmode != 2 else None, _P(probs), int(self.softmax), _P(self.gwh) if train else None,
             _P(self.gbh) if train else None, _P(bnd["dbeta"]) if train else None,
-            _P(bnd["dgamma"]) if train else None, _P(self.dh) if train else None, zp, zn, N.stream_ptr())
+            _P(bnd["dgamma"]) if train else None, _P(self.dh) if train else None, N.stream_ptr())
         N.check(rc, "tde_bncnn_head")
 
     # ------------------------------------------------------------------ plan interface
@@ -297,21 +287,22 @@ class BnCnnPlan(ReplicaPlan):
         rc = lib.tde_bncnn_dense_bwd(B, self.K, self.D, self.Dp, _P(last["z"]), C.byref(bn_last), _P(self.wd),
                                      _P(self.dh), _P(self.dwd_part), _P(last["g"]), _P(last["accb"]), s)
         N.check(rc, "tde_bncnn_dense_bwd")
-        # conv_bwd of block li consumes accb[li] and zeroes accb[li + 1] (consumed by the launch before it);
-        # the reduce zeroes accb[0]
+        # backward partials of block li's BN: from the dense backward (last block) or from the input-gradient
+        # role of block li + 1's conv backward (one per image)
+        nkt_nrb = -(-self.K // 32) * self.nrb
         for li in range(len(self.blocks) - 1, -1, -1):
             blk = self.blocks[li]
-            bb = BnBwd(_P(blk["accb"]), _P(blk["dbeta"]), _P(blk["dgamma"]))
+            npart = nkt_nrb if li == len(self.blocks) - 1 else B
+            bb = BnBwd(_P(blk["accb"]), int(npart), _P(blk["dbeta"]), _P(blk["dgamma"]))
             if li > 0:
                 prev = self.blocks[li - 1]
                 inp, bn_in, gin, acc_in = prev["z"], self._bn(prev, BN_SAVED, B), prev["g"], prev["accb"]
             else:
                 inp, bn_in, gin, acc_in = x, Bn(BN_NONE, blk["geo"].C), None, None
-            zp, zn = self._acc(li + 1, "accb")
             rc = lib.tde_bncnn_conv_bwd(C.byref(blk["geo"]), B, _P(blk["z"]), C.byref(self._bn(blk, BN_SAVED, B)),
                                         C.byref(bb), _P(blk["g"]), _P(blk["w"]), _P(inp), C.byref(bn_in), _P(gin),
-                                        _P(acc_in), _P(blk["dwpart"]), int(li > 0), zp, zn, s)
-            if rc < 0:
+                                        _P(acc_in), _P(blk["dwpart"]), int(li > 0), s)
+            if rc != 0:
                 raise RuntimeError(f"tde_bncnn_conv_bwd({blk['conv'].name}) failed with {rc}")
         # weight-gradient partials -> the bucket: per image for the convs, per 64-row block for the dense
         segs = [(b["dwpart"], b["gw"], b["K"] * b["geo"].Co, B) for b in self.blocks]
@@ -321,8 +312,7 @@ class BnCnnPlan(ReplicaPlan):
         parts = (C.c_void_p * n)(*[sg[0].data_ptr() for sg in segs])
         outs = (C.c_void_p * n)(*[sg[1].data_ptr() for sg in segs])
         lens = (C.c_longlong * n)(*[sg[2] for sg in segs])
-        zp, zn = self._acc(0, "accb")
-        N.check(lib.tde_bncnn_reduce(n, cnt, parts, outs, lens, zp, zn, s), "tde_bncnn_reduce")
+        N.check(lib.tde_bncnn_reduce(n, cnt, parts, outs, lens, s), "tde_bncnn_reduce")
 
     def apply(self):
         self.opt.apply()

@@ -126,6 +126,54 @@ def test_bncnn_step_gradients_match_float64(B):
     assert met[2].item() == B and abs(met[0].item() / B - loss) < 1e-5 * abs(loss)
 
 
+def test_bncnn_later_steps_gradients_match_float64():
+    """Steps 2 and 3 (after optimizer updates): every statistics partial is rewritten by its producer
+    each step (no memset, no atomics), so a later step must match the float64 oracle like the first."""
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.train import program as PG
+    m = _model_b(tde)
+    st = m._store
+    plan = PG.make_plan(m, st, DEV, 128, 128, m.optimizer, m.loss)
+    for step in range(3):
+        x, y = _data(128, 20 + step)
+        before = {n: st.view(n).detach().double().clone() for n in st.order}
+        plan.train_step(x, y)
+        torch.cuda.synchronize()
+        after = {n: st.view(n).detach().clone() for n in st.order}
+        for n in st.order:
+            st.view(n).copy_(before[n])
+        grads, moving, _, _ = _oracle(plan, x, y, 128)
+        for n in st.order:
+            st.view(n).copy_(after[n])
+        for n, gr in grads.items():
+            assert _rel(st.grad(n), gr) < 1e-5, (step, n, _rel(st.grad(n), gr))
+        for n, v in moving.items():
+            assert _rel(st.view(n), v) < 1e-6, (step, n, _rel(st.view(n), v))
+        plan.apply()
+        plan.iterations += 1
+        torch.cuda.synchronize()
+
+
+def test_bncnn_step_is_bitwise_deterministic():
+    """Same weights, same batch -> bit-identical gradients and moving statistics: statistics travel as
+    per-workgroup partials summed in a fixed order, the dense / logit partials likewise."""
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.train import program as PG
+    m = _model_b(tde)
+    st = m._store
+    plan = PG.make_plan(m, st, DEV, 128, 128, m.optimizer, m.loss)
+    x, y = _data(128, 31)
+    w0 = st.w.clone()
+    runs = []
+    for _ in range(3):
+        st.w.copy_(w0)
+        plan.train_step(x, y)
+        torch.cuda.synchronize()
+        runs.append((st.g.clone(), st.w.clone()))
+    for g, w in runs[1:]:
+        assert torch.equal(g, runs[0][0]) and torch.equal(w, runs[0][1])
+
+
 def test_bncnn_eval_and_predict_use_moving_statistics():
     import tensorflow_distributed_example_amd as tde
     from tensorflow_distributed_example_amd.train import program as PG
@@ -153,7 +201,13 @@ def test_bncnn_eval_and_predict_use_moving_statistics():
 
 def test_bncnn_fit_matches_reference_executor(monkeypatch):
     """fit() over 4 steps (hipGraph executions) on the fused plan vs the torch fp32 reference executor
-    (dropout off so both are deterministic): same weights, moving statistics and loss to fp32 accuracy."""
+    (dropout off so both are deterministic): same weights, moving statistics and loss to fp32 accuracy.
+
+    Tolerance: two fp32 implementations may decide a ReLU whose pre-activation is within an ulp of zero
+    differently (measured: one element in ~10^6, e.g. image 82 pixel (10, 14) channel 1 of the first
+    BN's output); one such tie moves the first conv's 4-step update by ~2.5e-3 of its norm.  The exact
+    per-step numerics are pinned at 1e-5 by the float64 oracle tests above, which share the plan's
+    ReLU decisions."""
     import tensorflow_distributed_example_amd as tde
     rng = np.random.default_rng(0)
     x = rng.random((128 * 4, 784), dtype=np.float32)
@@ -170,7 +224,7 @@ def test_bncnn_fit_matches_reference_executor(monkeypatch):
     hr = mr.fit(x, y, batch_size=128, epochs=1, shuffle=False, verbose=0)
     for name, a, b, w in zip(mf.variable_names(), mf.get_weights(), mr.get_weights(), w0):
         rel = np.linalg.norm(a - b) / (np.linalg.norm(b - w) + np.linalg.norm(b) * 1e-6 + 1e-12)
-        assert rel < 1e-3, (name, rel)
+        assert rel < 1e-2, (name, rel)
     assert abs(hf.history["loss"][0] - hr.history["loss"][0]) < 1e-4
 
 
