@@ -55,7 +55,9 @@ for blk in plan.blocks:
 h = a.reshape(128, -1) @ W[f"{plan.dense.name}/kernel"]
 h.retain_grad()
 bnl = plan.bnd["layer"]
-hp = torch.relu((h - h.mean(0)) / torch.sqrt(h.var(0, unbiased=False) + bnl.epsilon) + W[f"{bnl.name}/beta"])
+hpre = (h - h.mean(0)) / torch.sqrt(h.var(0, unbiased=False) + bnl.epsilon) + W[f"{bnl.name}/beta"]
+hpre.retain_grad()
+hp = torch.relu(hpre)
 logits = hp @ W[f"{plan.head.name}/kernel"] + W[f"{plan.head.name}/bias"]
 (F.cross_entropy(logits, y.long().cpu(), reduction="sum") * plan.scale).backward()
 
@@ -72,7 +74,7 @@ for i, blk in enumerate(plan.blocks):
     out[f"z{i}"] = rel(blk["z"][:n], zs[i].detach())
 D, Dp = plan.D, plan.Dp
 out["h"] = rel(plan.h[: 128 * Dp].view(128, Dp)[:, :D], h.detach())
-out["dh"] = rel(plan.dh[: 128 * Dp].view(128, Dp)[:, :D], h.grad)
+out["gh"] = rel(plan.gh[: 128 * Dp].view(128, Dp)[:, :D], hpre.grad)
 for i in reversed(range(len(plan.blocks))):
     gz = plan.blocks[i]["geo"]
     n = 128 * gz.Ho * gz.Wo * gz.Co

@@ -41,7 +41,7 @@ plan.train_step(x, y)
 lib.tde_bncnn_stamps(None, 0)
 torch.cuda.synchronize()
 st = buf.view(n_launch, 8192, 8).cpu().numpy()
-names = [f"conv_fwd{i}" for i in range(len(plan.blocks))] + ["dense_fwd", "head_fwd", "head_bwd", "dense_bwd"]
+names = [f"conv_fwd{i}" for i in range(len(plan.blocks))] + ["dense_fwd", "head", "dense_bwd"]
 names += [f"conv_bwd{i}" for i in reversed(range(len(plan.blocks)))] + ["reduce"]
 t0 = None
 for li, name in enumerate(names):

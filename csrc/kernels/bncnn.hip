@@ -335,75 +335,78 @@ __global__ __launch_bounds__(NTB) void conv_fwd_kernel(ConvFwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Dense forward: hpart[kchunk][B][Dp] = relu(BN(in))[rows][chunk] . W[chunk][cols]; grid (column
-// groups of kDenseCols, K chunks <= kMaxKc, row blocks of 64).  The head sums the chunk partials in a
-// fixed order (deterministic h).
-constexpr int kMaxKc = 8;
-constexpr int kDenseCols = 112;
-constexpr int kUA = 10, kUB = 18;   // A: 64 x kc <= 10240, W: kc x 112 <= 18432 (kc <= 160)
+// Dense forward: h = relu(BN(in)) . W_dense; grid (Dp/16 column tiles, ceil(B/16) row tiles).  One
+// 16x16 output tile per workgroup over the full K: wave w takes K range [w*kw, (w+1)*kw) with its MFMA
+// operands loaded straight from global into registers (no LDS staging), the 16 partial tiles summed in
+// LDS in wave order (deterministic).  Also the dense BN's statistics partials of the tile (per column:
+// sum, sum of squares over its 16 rows, f64) -> hstat[row tile][2][Dp].
+constexpr int kDS = 24;   // K steps per wave (K <= 16 * 4 * kDS = 1536)
 struct DenseFwdArgs {
-  int B, K, D, Dp, kc, lda, ldb;
+  int B, K, D, Dp, kw;
+  Dv dC;
   const float* in;           // [B][K], channel of feature k = k % bn.C
   Bn bn;
   const float* w;            // [K][D]
-  float* hpart;              // [gridDim.y][B][Dp]
+  float* h;                  // [B][Dp]
+  double* hstat;             // [ceil(B/16)][2][Dp]
   long long* stamps;
 };
 
 __global__ __launch_bounds__(NTB) void dense_fwd_kernel(DenseFwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
-  const int C = a.bn.C;
-  double* red = reinterpret_cast<double*>(sm);  // [NTB]
-  float* st = reinterpret_cast<float*>(sm + NTB * 8);
-  float* As = st + 4 * 32;                      // [64][lda]
-  float* Bs = As + 64 * a.lda;                  // [kc][ldb]
+  __shared__ double red[NTB];
+  __shared__ float st[4 * 32];
+  __shared__ float part[16][256];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
-  const int c0 = blockIdx.x * kDenseCols, k0 = blockIdx.y * a.kc, b0 = blockIdx.z * 64;
-  const int kc = a.kc, kn = min(kc, a.K - k0);
+  const int c0 = blockIdx.x * 16, r0 = blockIdx.y * 16, K = a.K;
+  const int k0 = wave * a.kw;
+  const int row = min(r0 + fr, a.B - 1), col = min(c0 + fr, a.D - 1);
   stamp(a.stamps, 0);
-  Pf<kUA> pa;
-  Pf<kUB> pb;
-  pf_load(pa, 64 * kc, [&](int e) {
-    const int r = e / kc, kk = e - r * kc;
-    return a.in[(size_t)min(b0 + r, a.B - 1) * a.K + min(k0 + kk, a.K - 1)];
-  });
-  pf_load(pb, kc * kDenseCols, [&](int e) {
-    const int kk = e / kDenseCols, col = e - kk * kDenseCols;
-    return a.w[(size_t)min(k0 + kk, a.K - 1) * a.D + min(c0 + col, a.D - 1)];
-  });
-  bn_prepare(a.bn, st, blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0, red);
+  float av[kDS], bv[kDS];
+#pragma unroll
+  for (int s = 0; s < kDS; ++s)
+    if (4 * s < a.kw) {
+      const int k = min(k0 + 4 * s + fq, K - 1);
+      av[s] = a.in[(size_t)row * K + k];
+      bv[s] = a.w[(size_t)k * a.D + col];
+    }
+  bn_prepare(a.bn, st, blockIdx.x == 0 && blockIdx.y == 0, red);
   stamp(a.stamps, 1);
-  {
-    const float* sc = st;
-    const float* sh = st + C;
-    pf_store(pa, 64 * kc, [&](int e, float v) {
-      const int r = e / kc, kk = e - r * kc, c = (k0 + kk) % C;
-      As[r * a.lda + kk] = (kk < kn && b0 + r < a.B) ? fmaxf(fmaf(v, sc[c], sh[c]), 0.f) : 0.f;
-    });
-    pf_store(pb, kc * kDenseCols, [&](int e, float v) {
-      const int kk = e / kDenseCols, col = e - kk * kDenseCols;
-      Bs[kk * a.ldb + col] = (kk < kn && c0 + col < a.D) ? v : 0.f;
-    });
-  }
+  const float* sc = st;
+  const float* sh = st + a.bn.C;
+  const bool rok = r0 + fr < a.B, cok = c0 + fr < a.D;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < kDS; ++s)
+    if (4 * s < a.kw) {
+      const int k = k0 + 4 * s + fq;
+      const int c = k - dq(k, a.dC) * a.bn.C;
+      const bool kok = k < K && 4 * s + fq < a.kw;
+      const float x = (kok && rok) ? fmaxf(fmaf(av[s], sc[c], sh[c]), 0.f) : 0.f;
+      acc = mfma4(x, (kok && cok) ? bv[s] : 0.f, acc);
+    }
+  *reinterpret_cast<f32x4*>(&part[wave][lane * 4]) = acc;
   lds_barrier();
   stamp(a.stamps, 2);
-  // items: 4 row tiles x 7 column tiles
-  for (int item = wave; item < 4 * (kDenseCols / 16); item += 16) {
-    const int rt = item & 3, ct = item >> 2;
-    if (c0 + ct * 16 >= a.Dp) continue;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float* Ar = As + (rt * 16 + fr) * a.lda;
-    for (int s0 = 0; s0 < kc / 4; s0 += 4) {   // kc % 16 == 0
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = 4 * (s0 + u) + fq;
-        acc = mfma4(Ar[k], Bs[k * a.ldb + ct * 16 + fr], acc);
-      }
-    }
+  if (wave == 0) {
+    f32x4 v = acc;
+    for (int w = 1; w < 16; ++w) v += *reinterpret_cast<const f32x4*>(&part[w][lane * 4]);
+    double s1 = 0.0, s2 = 0.0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int row = b0 + rt * 16 + fq * 4 + i;
-      if (row < a.B) a.hpart[((size_t)blockIdx.y * a.B + row) * a.Dp + c0 + ct * 16 + fr] = acc[i];
+      const int r = r0 + fq * 4 + i;
+      if (r < a.B) {
+        a.h[(size_t)r * a.Dp + c0 + fr] = v[i];
+        s1 += v[i];
+        s2 += (double)v[i] * v[i];
+      }
+    }
+    s1 += __shfl_xor(s1, 16, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 16, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    if (fq == 0) {
+      a.hstat[((size_t)blockIdx.y * 2 + 0) * a.Dp + c0 + fr] = s1;
+      a.hstat[((size_t)blockIdx.y * 2 + 1) * a.Dp + c0 + fr] = s2;
     }
   }
   stamp(a.stamps, 3);
@@ -433,336 +436,222 @@ __device__ __forceinline__ float keep_scale(float rate, unsigned long long seed,
 }
 
 // ------------------------------------------------------------------------------------------------
-// Head, two launches over 16-feature tiles of the dense layer (grid Dp/16, so the per-feature
-// statistics never leave a workgroup):
-//   head_fwd   the dense BN statistics over the batch (or the moving ones), ReLU, Philox dropout, and
-//              this tile's share of the logits (act[:, tile] . Wh[tile, :]: f32 atomics into
-//              logits [B][16], zeroed by dense_fwd)
-//   head_bwd   softmax-CE / accuracy from the logits (every workgroup; workgroup 0 keeps the metrics,
-//              the bias gradient and the prediction output); training: dWh rows of the tile,
-//              g = dl . Wh^T through the dropout / ReLU masks, the BN backward sums of the tile, and
-//              dL/dh = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) for the tile.
-constexpr int kHeadMaxTiles = 16;   // Dp <= 256
+// Head: grid ceil(B/16), one 16-row tile per workgroup (all Dp features):
+//   the dense BN statistics (fixed-order sum of dense_fwd's row-tile partials, or the moving ones),
+//   ReLU, Philox dropout, Dense head (MFMA), softmax-CE / accuracy / prediction; training: the row
+//   tile's partials of dWh, dbh (summed by the reduce launch), g = dl . Wh^T through the dropout / ReLU
+//   masks, and the dense BN's backward partial sums (sum g, sum g*xhat per feature) -> dense_bwd
+//   finishes dL/dh = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) while it stages it.
+constexpr int kHeadMaxDp = 256;
+constexpr int kHU = kHeadMaxDp * 16 / NTH;   // h / g elements per thread
+constexpr int kHLD = kHeadMaxDp + 4;         // LDS row stride of the activation tile
 struct HeadArgs {
-  int B, D, Dp, NC, mode;          // mode 0 train, 1 eval (metrics), 2 predict
-  const float* hpart; int nkc;      // dense_fwd's K-chunk partials [nkc][B][Dp]
-  float* h;                         // [B][Dp]: their sum (written by head_fwd)
-  Bn bn;                            // C = D (mode kBnTrain / kBnMoving / kBnBatch; computed by head_fwd)
+  int B, D, Dp, NC, mode, nrt;       // mode 0 train, 1 eval (metrics), 2 predict; nrt = row tiles
+  const float* h;                    // [B][Dp]
+  const double* hstat;               // [nrt][2][Dp]
+  Bn bn;                             // C = D (mode kBnTrain / kBnMoving / kBnBatch)
   float rate; unsigned long long seed; const long long* iter; int layer_id, drop_on;
   const float* wh; const float* bh;
-  float* logits;                    // [Dp/16][B][16] per-feature-tile partials (bias excluded)
   const int* labels; float scale;
   float* metrics;
-  float* out; int out_softmax;      // predict: [B][NC] probabilities (softmax head) or logits
-  float *dwh, *dbh, *dbeta, *dgamma;
-  float* dh;                        // [B][Dp]: dL/dh (holds the pre-ReLU gradient g until the last pass)
-  long long* stamps;   // diagnostic phase clock (tde_bncnn_stamps), nullable
+  float* out; int out_softmax;       // predict: [B][NC] probabilities (softmax head) or logits
+  float* dwh_part;                   // [nrt][D][NC]
+  float* dbh_part;                   // [nrt][NC]
+  float* g;                          // [B][Dp]  dL/d(BN output) through the masks
+  double* gstat;                     // [nrt][2][Dp]
+  long long* stamps;
 };
 
-__global__ __launch_bounds__(NTH) void head_fwd_kernel(HeadArgs a) {
-  __shared__ float whs[16 * 16];           // [feature][class]
-  __shared__ float sc[16], sh[16];
-  __shared__ double red[2][16][16];
-  __shared__ float As[128 * 17];
+__global__ __launch_bounds__(NTH) void head_kernel(HeadArgs a) {
+  __shared__ float mu[kHeadMaxDp], rs[kHeadMaxDp], sc[kHeadMaxDp], sh[kHeadMaxDp];
+  __shared__ float As[16 * kHLD], Xh[16 * kHLD];
+  __shared__ float whs[kHeadMaxDp * 16];   // [feature][class]
+  __shared__ float lgp[4][256];
+  __shared__ float dls[16 * 16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
-  const int c = tid & 15, rg = tid >> 4;
-  const int f0 = blockIdx.x * 16, f = f0 + c;
-  const int B = a.B, D = a.D, Dp = a.Dp, NC = a.NC;
-  const bool fok = f < D;
+  const int B = a.B, D = a.D, Dp = a.Dp, NC = a.NC, rt = blockIdx.x, r0 = rt * 16;
+  const bool train = a.mode == 0, lead = rt == 0;
+  const bool batch = a.bn.mode == kBnTrain || a.bn.mode == kBnBatch;
   const long long it = a.iter ? *a.iter : 0;
   stamp(a.stamps, 0);
-  {
-    const int ff = f0 + (tid >> 4), cc = tid & 15;
-    whs[tid] = (ff < D && cc < NC) ? a.wh[(size_t)ff * NC + cc] : 0.f;
+  // ---- one batch of loads: the row tile of h, the statistics partials of feature tid, Wh
+  float hv[kHU];
+#pragma unroll
+  for (int u = 0; u < kHU; ++u) {
+    const int e = tid + u * NTH;
+    if (u * NTH < 16 * Dp) hv[u] = a.h[(size_t)min(r0 + e / Dp, B - 1) * Dp + e % Dp];
   }
-  const bool batch = a.bn.mode == kBnTrain || a.bn.mode == kBnBatch;
-  // ---- pass 1: sums over the batch (rows rg + 16u of 128-row blocks); the first block stays in registers
-  float hv[8];
-  double s = 0.0, s2 = 0.0;
-  for (int b0 = 0; b0 < B; b0 += 128) {
-    float v[8];
-    {
-      float pv[8][kMaxKc];   // every partial of the 8 rows in flight at once (clamped, branch-free)
+  float wv[kHU];
+#pragma unroll
+  for (int u = 0; u < kHU; ++u) {
+    const int e = tid + u * NTH, f = e >> 4, c = e & 15;
+    if (u * NTH < 16 * Dp) wv[u] = (f < D && c < NC) ? a.wh[(size_t)min(f, D - 1) * NC + min(c, NC - 1)] : 0.f;
+  }
+  const int f = tid;
+  double S = 0.0, S2 = 0.0;
+  if (f < D && batch) {
+    for (int p0 = 0; p0 < a.nrt; p0 += 8) {
+      double v1[8], v2[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int r = min(b0 + rg + 16 * u, B - 1);
-#pragma unroll
-        for (int q = 0; q < kMaxKc; ++q)
-          pv[u][q] = a.hpart[((size_t)min(q, a.nkc - 1) * B + r) * Dp + f];
+        const int p = min(p0 + u, a.nrt - 1);
+        v1[u] = a.hstat[((size_t)p * 2 + 0) * Dp + f];
+        v2[u] = a.hstat[((size_t)p * 2 + 1) * Dp + f];
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int r = b0 + rg + 16 * u;
-        float t = 0.f;
-#pragma unroll
-        for (int q = 0; q < kMaxKc; ++q) t += q < a.nkc ? pv[u][q] : 0.f;
-        v[u] = (r < B && fok) ? t : 0.f;
-        if (r < B && f < Dp) a.h[(size_t)r * Dp + f] = v[u];
-      }
-    }
-    if (b0 == 0) {
-#pragma unroll
-      for (int u = 0; u < 8; ++u) hv[u] = v[u];
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      s += v[u];
-      s2 += (double)v[u] * v[u];
-    }
-  }
-  red[0][rg][c] = s;
-  red[1][rg][c] = s2;
-  __syncthreads();
-  if (tid < 16) {
-    const int ft = f0 + tid;
-    float mean = 0.f, rstd = 1.f;
-    if (ft < D) {
-      if (batch) {
-        double S = 0.0, S2 = 0.0;
-        for (int q = 0; q < 16; ++q) {
-          S += red[0][q][tid];
-          S2 += red[1][q][tid];
+      for (int u = 0; u < 8; ++u)
+        if (p0 + u < a.nrt) {
+          S += v1[u];
+          S2 += v2[u];
         }
+    }
+  }
+  if (f < Dp) {
+    float mean = 0.f, rstd = 1.f;
+    if (f < D) {
+      if (batch) {
         const double m = S / B, v = fmax(S2 / B - m * m, 0.0);
         mean = (float)m;
         rstd = (float)(1.0 / sqrt(v + (double)a.bn.eps));
-        if (a.bn.mode == kBnTrain) {
-          a.bn.saved[ft] = mean;
-          a.bn.saved[D + ft] = rstd;
-          a.bn.mmean[ft] = a.bn.mmean[ft] * a.bn.momentum + mean * (1.f - a.bn.momentum);
-          a.bn.mvar[ft] = a.bn.mvar[ft] * a.bn.momentum + (float)v * a.bn.bessel * (1.f - a.bn.momentum);
+        if (lead && a.bn.mode == kBnTrain) {
+          a.bn.saved[f] = mean;
+          a.bn.saved[D + f] = rstd;
+          a.bn.mmean[f] = a.bn.mmean[f] * a.bn.momentum + mean * (1.f - a.bn.momentum);
+          a.bn.mvar[f] = a.bn.mvar[f] * a.bn.momentum + (float)v * a.bn.bessel * (1.f - a.bn.momentum);
         }
       } else {
-        mean = a.bn.mmean[ft];
-        rstd = rsqrtf(a.bn.mvar[ft] + a.bn.eps);
+        mean = a.bn.mmean[f];
+        rstd = rsqrtf(a.bn.mvar[f] + a.bn.eps);
       }
     }
-    const float g = (ft < D && a.bn.gamma) ? a.bn.gamma[ft] : 1.f;
-    sc[tid] = ft < D ? g * rstd : 0.f;
-    sh[tid] = ft < D ? (a.bn.beta ? a.bn.beta[ft] : 0.f) - mean * g * rstd : 0.f;
+    const float gm = (f < D && a.bn.gamma) ? a.bn.gamma[f] : 1.f;
+    mu[f] = mean;
+    rs[f] = rstd;
+    sc[f] = f < D ? gm * rstd : 0.f;
+    sh[f] = f < D ? (a.bn.beta ? a.bn.beta[f] : 0.f) - mean * gm * rstd : 0.f;
   }
   lds_barrier();
-  // ---- pass 2: activation of 128-row blocks -> LDS -> logits share (wave: row tiles wave, wave + 4)
-  for (int b0 = 0; b0 < B; b0 += 128) {
-    float v[8];
+  stamp(a.stamps, 1);
+  // ---- activation / xhat tiles, Wh
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int r = b0 + rg + 16 * u;
-      v[u] = b0 == 0 ? hv[u] : ((r < B && fok) ? a.h[(size_t)r * Dp + f] : 0.f);   // this thread's own stores
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int r = b0 + rg + 16 * u;
-      float act = 0.f;
-      if (r < B && fok) {
-        act = fmaxf(fmaf(v[u], sc[c], sh[c]), 0.f);
-        if (a.drop_on) act *= keep_scale(a.rate, a.seed, it, a.layer_id, (long long)r * D + f);
+  for (int u = 0; u < kHU; ++u) {
+    const int e = tid + u * NTH;
+    if (e < 16 * Dp) {
+      const int r = e / Dp, ff = e - r * Dp;
+      float act = 0.f, xh = 0.f;
+      if (r0 + r < B && ff < D) {
+        xh = (hv[u] - mu[ff]) * rs[ff];
+        act = fmaxf(fmaf(hv[u], sc[ff], sh[ff]), 0.f);
+        if (a.drop_on) act *= keep_scale(a.rate, a.seed, it, a.layer_id, (long long)(r0 + r) * D + ff);
       }
-      As[(rg + 16 * u) * 17 + c] = act;
+      As[r * kHLD + ff] = act;
+      Xh[r * kHLD + ff] = xh;
     }
-    lds_barrier();
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int rt = wave + 4 * j;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        const int k = 4 * st + fq;
-        acc = mfma4(As[(rt * 16 + fr) * 17 + k], whs[k * 16 + fr], acc);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = b0 + rt * 16 + fq * 4 + i;
-        if (r < B) a.logits[((size_t)blockIdx.x * B + r) * 16 + fr] = acc[i];
-      }
-    }
-    lds_barrier();
+    if (e < 16 * Dp) whs[e] = wv[u];
   }
-  stamp(a.stamps, 3);
-}
-
-__global__ __launch_bounds__(NTH) void head_bwd_kernel(HeadArgs a) {
-  __shared__ float whs[16 * 16];           // [feature][class]
-  __shared__ float mu[16], rs[16], sc[16], sh[16], gm[16];
-  __shared__ float dls[64 * 16];
-  __shared__ float As[64 * 17], Xh[64 * 17];
-  __shared__ float sgp[4][16], sgxp[4][16];   // per-wave BN backward sums (summed in wave order)
-  __shared__ float part[4][256];
-  __shared__ float gbs[4][16];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
-  const int c = tid & 15, rg = tid >> 4;
-  const int f0 = blockIdx.x * 16, f = f0 + c;
-  const int B = a.B, D = a.D, Dp = a.Dp, NC = a.NC;
-  const bool train = a.mode == 0, lead = blockIdx.x == 0, fok = f < D;
-  const long long it = a.iter ? *a.iter : 0;
-  stamp(a.stamps, 0);
-  if (train) {
-    const int ff = f0 + (tid >> 4), cc = tid & 15;
-    whs[tid] = (ff < D && cc < NC) ? a.wh[(size_t)ff * NC + cc] : 0.f;
-    if (tid < 16) {
-      const int ft = f0 + tid;
-      const float m = ft < D ? a.bn.saved[ft] : 0.f, r = ft < D ? a.bn.saved[D + ft] : 0.f;
-      const float g = (ft < D && a.bn.gamma) ? a.bn.gamma[ft] : 1.f;
-      mu[tid] = m;
-      rs[tid] = r;
-      gm[tid] = g;
-      sc[tid] = g * r;
-      sh[tid] = ft < D ? (a.bn.beta ? a.bn.beta[ft] : 0.f) - m * g * r : 0.f;
-    }
-  }
-  const float bias = c < NC ? a.bh[c] : 0.f;
-  f32x4 gw = {0.f, 0.f, 0.f, 0.f};
-  float gb = 0.f, la = 0.f, ca = 0.f, na = 0.f, s1 = 0.f, s2 = 0.f;
   lds_barrier();
-  for (int b0 = 0; b0 < B; b0 += 64) {
-    float hv[4], z[4];
-    int lab[4];
-    {
-      const int nlt = Dp / 16;
-      float lp[4][kHeadMaxTiles];   // the feature tiles' logits partials, all in flight (clamped)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int r = min(b0 + rg + 16 * u, B - 1);
-#pragma unroll
-        for (int q = 0; q < kHeadMaxTiles; ++q) lp[u][q] = a.logits[((size_t)min(q, nlt - 1) * B + r) * 16 + c];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int r = b0 + rg + 16 * u;
-        hv[u] = (train && r < B && fok) ? a.h[(size_t)r * Dp + f] : 0.f;
-        lab[u] = (r < B && a.labels) ? a.labels[r] : 0;
-        float t = 0.f;
-#pragma unroll
-        for (int q = 0; q < kHeadMaxTiles; ++q) t += q < nlt ? lp[u][q] : 0.f;
-        z[u] = t;
-      }
+  // ---- logits [16][16]: wave = K quarter, summed in wave order
+  {
+    const int kq = Dp / 4;   // Dp % 16 == 0 -> multiple of 4
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < kq / 4; ++s) {
+      const int k = wave * kq + 4 * s + fq;
+      acc = mfma4(As[fr * kHLD + k], whs[k * 16 + fr], acc);
     }
+    *reinterpret_cast<f32x4*>(&lgp[wave][lane * 4]) = acc;
+  }
+  lds_barrier();
+  if (wave == 0) {
+    f32x4 lg = *reinterpret_cast<const f32x4*>(&lgp[0][lane * 4]);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int rl = rg + 16 * u, r = b0 + rl;
-      const bool valid = r < B, cv = c < NC;
-      const float zz = cv ? z[u] + bias : -3.0e38f;
-      const float m = row16_max(zz);
-      const float ex = cv ? __expf(zz - m) : 0.f;
+    for (int w = 1; w < 4; ++w) lg += *reinterpret_cast<const f32x4*>(&lgp[w][lane * 4]);
+    const float bias = fr < NC ? a.bh[fr] : 0.f;
+    float la = 0.f, ca = 0.f, na = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rl = fq * 4 + i, r = r0 + rl;
+      const bool valid = r < B, cv = fr < NC;
+      const float z = cv ? lg[i] + bias : -3.0e38f;
+      const float m = row16_max(z);
+      const float ex = cv ? __expf(z - m) : 0.f;
       const float sum = row16_sum(ex);
       const float pr = ex / sum;
-      const int label = lab[u];
-      const int amx = row16_min(cv && zz == m ? c : 64);
-      const float zl = __shfl(zz, (lane & ~15) | (label & 15), 64);
-      if (lead && valid && c == 0) {
+      const int label = (valid && a.labels) ? a.labels[r] : 0;
+      const int amx = row16_min(cv && z == m ? fr : 64);
+      const float zl = __shfl(z, (lane & ~15) | (label & 15), 64);
+      if (valid && fr == 0) {
         la += __logf(sum) + m - zl;
         ca += (amx == label) ? 1.f : 0.f;
         na += 1.f;
       }
-      if (a.mode == 2 && lead && valid && cv) a.out[(size_t)r * NC + c] = a.out_softmax ? pr : zz;
-      const float dl = (train && valid && cv) ? (pr - (c == label ? 1.f : 0.f)) * a.scale : 0.f;
-      dls[rl * 16 + c] = dl;
-      gb += dl;
-      if (train) {
-        float act = 0.f, xh = 0.f;
-        if (valid && fok) {
-          xh = (hv[u] - mu[c]) * rs[c];
-          act = fmaxf(fmaf(hv[u], sc[c], sh[c]), 0.f);
-          if (a.drop_on) act *= keep_scale(a.rate, a.seed, it, a.layer_id, (long long)r * D + f);
-        }
-        As[rl * 17 + c] = act;
-        Xh[rl * 17 + c] = xh;
-      }
+      if (a.mode == 2 && valid && cv) a.out[(size_t)r * NC + fr] = a.out_softmax ? pr : z;
+      dls[rl * 16 + fr] = (train && valid && cv) ? (pr - (fr == label ? 1.f : 0.f)) * a.scale : 0.f;
     }
-    if (!train) continue;
-    lds_barrier();
-    // dWh^T tile [feature][class] += act^T . dl over this wave's 16 rows
-#pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      const int r = wave * 16 + 4 * st + fq;
-      gw = mfma4(As[r * 17 + fr], dls[r * 16 + fr], gw);
-    }
-    // g [row][feature] = dl . Wh^T through the dropout / ReLU masks
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      const int k = 4 * st + fq;
-      acc = mfma4(dls[(wave * 16 + fr) * 16 + k], whs[fr * 16 + k], acc);
-    }
-    const int fg = f0 + fr;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int rl = wave * 16 + fq * 4 + i, r = b0 + rl;
-      if (r < B && fg < D) {
-        const float act = As[rl * 17 + fr];
-        // act > 0 <=> ReLU passed AND dropout kept; the kept scale is 1/keep
-        const float gv = act > 0.f ? (a.drop_on ? acc[i] * (1.f / (1.f - a.rate)) : acc[i]) : 0.f;
-        a.dh[(size_t)r * Dp + fg] = gv;
-        s1 += gv;
-        s2 += gv * Xh[rl * 17 + fr];
-      }
-    }
-    lds_barrier();
-  }
-  // ---- metrics and the bias gradient (workgroup 0)
-  if (lead) {
-    float l = la, cc = ca, n = na;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
-      l += __shfl_xor(l, o, 64);
-      cc += __shfl_xor(cc, o, 64);
-      n += __shfl_xor(n, o, 64);
+      la += __shfl_xor(la, o, 64);
+      ca += __shfl_xor(ca, o, 64);
+      na += __shfl_xor(na, o, 64);
     }
-    if (a.metrics && lane == 0 && n > 0.f) {
-      atomicAdd(a.metrics + 0, l);
-      atomicAdd(a.metrics + 1, cc);
-      atomicAdd(a.metrics + 2, n);
+    if (a.metrics && lane == 0 && na > 0.f) {
+      atomicAdd(a.metrics + 0, la);
+      atomicAdd(a.metrics + 1, ca);
+      atomicAdd(a.metrics + 2, na);
     }
   }
+  stamp(a.stamps, 2);
   if (!train) return;
-  gb += __shfl_xor(gb, 16, 64);
-  gb += __shfl_xor(gb, 32, 64);
-  if (fq == 0) gbs[wave][fr] = gb;
-  s1 += __shfl_xor(s1, 16, 64);
-  s1 += __shfl_xor(s1, 32, 64);
-  s2 += __shfl_xor(s2, 16, 64);
-  s2 += __shfl_xor(s2, 32, 64);
-  if (fq == 0) {
-    sgp[wave][fr] = s1;
-    sgxp[wave][fr] = s2;
+  lds_barrier();
+  // ---- training: the tile's dbh / dWh partials, g and the dense BN's backward partial sums
+  if (tid < 16) {
+    float s = 0.f;
+    for (int r = 0; r < 16; ++r) s += dls[r * 16 + tid];
+    if (tid < NC) a.dbh_part[(size_t)rt * NC + tid] = s;
   }
-  *reinterpret_cast<f32x4*>(&part[wave][lane * 4]) = gw;
-  __syncthreads();   // LDS partials, and the g stores of every wave visible to the workgroup
-  if (wave == 0) {
-    f32x4 t = gw;
+  const int ntf = Dp / 16;
+  float* dwp = a.dwh_part + (size_t)rt * D * NC;
+  for (int ft = wave; ft < ntf; ft += 4) {
+    // dWh^T tile [feature][class] = act^T . dl over the 16 rows
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int w = 1; w < 4; ++w) t += *reinterpret_cast<const f32x4*>(&part[w][lane * 4]);
+    for (int s = 0; s < 4; ++s) {
+      const int r = 4 * s + fq;
+      acc = mfma4(As[r * kHLD + ft * 16 + fr], dls[r * 16 + fr], acc);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int fi = f0 + fq * 4 + i;
-      if (fi < D && fr < NC) a.dwh[(size_t)fi * NC + fr] = t[i];
+      const int fi = ft * 16 + fq * 4 + i;
+      if (fi < D && fr < NC) dwp[(size_t)fi * NC + fr] = acc[i];
     }
-  }
-  if (lead && tid < 16 && tid < NC) a.dbh[tid] = (gbs[0][tid] + gbs[1][tid]) + (gbs[2][tid] + gbs[3][tid]);
-  const float sgc = (sgp[0][c] + sgp[1][c]) + (sgp[2][c] + sgp[3][c]);
-  const float sgxc = (sgxp[0][c] + sgxp[1][c]) + (sgxp[2][c] + sgxp[3][c]);
-  if (tid < 16 && f0 + tid < D) {
-    if (a.dbeta) a.dbeta[f0 + tid] = sgc;
-    if (a.dgamma) a.dgamma[f0 + tid] = sgxc;
-  }
-  // ---- dL/dh for the tile, 8 rows in flight per thread
-  const float invB = 1.f / (float)B;
-  const float k1 = sgc * invB, k2 = sgxc * invB, kk = gm[c] * rs[c];
-  for (int b0 = 0; b0 < B; b0 += 128) {
-    float gv[8], xv[8];
+    // g [row][feature] = dl . Wh^T through the dropout / ReLU masks
+    f32x4 gg = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int r = b0 + rg + 16 * u;
-      gv[u] = (r < B && fok) ? a.dh[(size_t)r * Dp + f] : 0.f;
-      xv[u] = (r < B && fok) ? a.h[(size_t)r * Dp + f] : 0.f;
+    for (int s = 0; s < 4; ++s) {
+      const int c = 4 * s + fq;
+      gg = mfma4(dls[fr * 16 + c], whs[(ft * 16 + fr) * 16 + c], gg);
     }
+    const int fg = ft * 16 + fr;
+    double s1 = 0.0, s2 = 0.0;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int r = b0 + rg + 16 * u;
-      if (r < B && fok) {
-        const float xh = (xv[u] - mu[c]) * rs[c];
-        a.dh[(size_t)r * Dp + f] = kk * (gv[u] - k1 - xh * k2);
+    for (int i = 0; i < 4; ++i) {
+      const int rl = fq * 4 + i, r = r0 + rl;
+      float gv = 0.f;
+      if (r < B && fg < D) {
+        const float act = As[rl * kHLD + fg];
+        // act > 0 <=> ReLU passed AND dropout kept; the kept scale is 1/keep
+        gv = act > 0.f ? (a.drop_on ? gg[i] * (1.f / (1.f - a.rate)) : gg[i]) : 0.f;
+        s1 += gv;
+        s2 += (double)(gv * Xh[rl * kHLD + fg]);
       }
+      if (r < B) a.g[(size_t)r * Dp + fg] = gv;
+    }
+    s1 += __shfl_xor(s1, 16, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 16, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    if (fq == 0) {
+      a.gstat[((size_t)rt * 2 + 0) * Dp + fg] = s1;
+      a.gstat[((size_t)rt * 2 + 1) * Dp + fg] = s2;
     }
   }
   stamp(a.stamps, 3);
@@ -770,17 +659,23 @@ __global__ __launch_bounds__(NTH) void head_bwd_kernel(HeadArgs a) {
 
 // ------------------------------------------------------------------------------------------------
 // Dense backward: grid (ceil(K/32), ceil(B/64)): one 32-feature K tile x one 64-row block per
-// workgroup, every load in one batch.
+// workgroup, every load in one batch.  dh = dL/dh is finished while staging: the head's g, h and the
+// dense BN's backward sums (fixed-order sum of the head's row-tile partials) give
+// dh = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)).
 //   waves 0-7   dA[64 rows][32] = dh . W^T (row tile w & 3, K half w >> 2) -> g = dA * ReLU mask of
 //               the input BN, and that BN's backward sums
 //   waves 8-15  the row block's dW partial [32][Dp] = A^T . dh (K half x 16-column tiles); the reduce
 //               launch sums the row blocks in order
 constexpr int kUDh = 16, kUWk = 8;   // dh block 64 x Dp <= 16384, W rows 32 x D <= 8192
 struct DenseBwdArgs {
-  int B, K, D, Dp, ldh;
+  int B, K, D, Dp, ldh, nrt;
   const float* in; Bn bn;           // the input layer's raw output and its BN (kBnSaved)
   const float* w;                   // [K][D]
-  const float* dh;                  // [B][Dp]
+  const float* gh;                  // [B][Dp] the head's g (dL/d dense-BN output)
+  const float* h;                   // [B][Dp] the dense pre-activation
+  const double* gstat;              // [nrt][2][Dp] the head's backward partial sums
+  Bn bnd;                           // the dense BN (kBnSaved)
+  float *dbeta_d, *dgamma_d;        // its gradients (nullable)
   float* dwpart;                    // [ceil(B/64)][K][D]
   float* g;                         // [B][K]
   double* acc;                      // [gridDim.x * gridDim.y][2][C] BN backward partial sums of the input layer
@@ -792,7 +687,8 @@ __global__ __launch_bounds__(NTB) void dense_bwd_kernel(DenseBwdArgs a) {
   const int C = a.bn.C, K = a.K, D = a.D, Dp = a.Dp, ldh = a.ldh;
   double* cs = reinterpret_cast<double*>(sm);             // [8][2][32]
   float* st = reinterpret_cast<float*>(sm + 16 * 2 * 32 * 8);
-  float* Wk = st + 4 * 32;                                 // [32][ldh]
+  float* dk = st + 4 * 32;                                 // [4][256]: gamma*rstd, mean(g), mean, rstd*mean(g*xhat)
+  float* Wk = dk + 4 * 256;                                // [32][ldh]
   float* dhs = Wk + 32 * ldh;                              // [64][ldh]
   float* Ab = dhs + 64 * ldh;                              // [64][33] relu(BN(in))
   float* Xb = Ab + 64 * 33;                                // [64][33] raw in
@@ -800,11 +696,42 @@ __global__ __launch_bounds__(NTB) void dense_bwd_kernel(DenseBwdArgs a) {
   const int kt0 = blockIdx.x * 32, b0 = blockIdx.y * 64, nb = min(64, a.B - b0);
   stamp(a.stamps, 0);
   Pf<kUWk> pw;
-  Pf<kUDh> pd;
+  Pf<kUDh> pd, ph;
   Pf<2> px;
   pf_load(pw, 32 * D, [&](int e) { return a.w[(size_t)min(kt0 + e / D, K - 1) * D + e % D]; });
-  pf_load(pd, 64 * Dp, [&](int e) { return a.dh[(size_t)min(b0 + e / Dp, a.B - 1) * Dp + e % Dp]; });
+  pf_load(pd, 64 * Dp, [&](int e) { return a.gh[(size_t)min(b0 + e / Dp, a.B - 1) * Dp + e % Dp]; });
+  pf_load(ph, 64 * Dp, [&](int e) { return a.h[(size_t)min(b0 + e / Dp, a.B - 1) * Dp + e % Dp]; });
   pf_load(px, 64 * 32, [&](int e) { return a.in[(size_t)min(b0 + (e >> 5), a.B - 1) * K + min(kt0 + (e & 31), K - 1)]; });
+  // the dense BN's backward sums for feature tid (fixed order over the head's row tiles)
+  if (tid < Dp) {
+    double S1 = 0.0, S2 = 0.0;
+    for (int p0 = 0; p0 < a.nrt; p0 += 8) {
+      double v1[8], v2[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int p = min(p0 + u, a.nrt - 1);
+        v1[u] = a.gstat[((size_t)p * 2 + 0) * Dp + tid];
+        v2[u] = a.gstat[((size_t)p * 2 + 1) * Dp + tid];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (p0 + u < a.nrt) {
+          S1 += v1[u];
+          S2 += v2[u];
+        }
+    }
+    const bool ok = tid < D;
+    const float m = ok ? a.bnd.saved[tid] : 0.f, r = ok ? a.bnd.saved[D + tid] : 0.f;
+    const float gm = (ok && a.bnd.gamma) ? a.bnd.gamma[tid] : 1.f;
+    dk[tid] = ok ? gm * r : 0.f;
+    dk[256 + tid] = (float)(S1 / a.B);
+    dk[512 + tid] = m;
+    dk[768 + tid] = r * (float)(S2 / a.B);
+    if (ok && blockIdx.x == 0 && blockIdx.y == 0) {
+      if (a.dbeta_d) a.dbeta_d[tid] = (float)S1;
+      if (a.dgamma_d) a.dgamma_d[tid] = (float)S2;
+    }
+  }
   bn_prepare(a.bn, st, false, nullptr);
   stamp(a.stamps, 1);
   const float* sc = st;
@@ -816,10 +743,16 @@ __global__ __launch_bounds__(NTB) void dense_bwd_kernel(DenseBwdArgs a) {
     Wk[kk * ldh + n] = kt0 + kk < K ? v : 0.f;
   });
   for (int e = tid; e < 32 * (Dp - D); e += NTB) Wk[(e / (Dp - D)) * ldh + D + e % (Dp - D)] = 0.f;
-  pf_store(pd, 64 * Dp, [&](int e, float v) {
-    const int r = e / Dp, n = e - r * Dp;
-    dhs[r * ldh + n] = r < nb ? v : 0.f;
-  });
+#pragma unroll
+  for (int u = 0; u < kUDh; ++u) {
+    const int e = tid + u * NTB;
+    if (e < 64 * Dp) {
+      const int r = e / Dp, n = e - r * Dp;
+      // dh = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)), xhat*rstd folded: (h - mean)*rstd*mean(g*xhat)
+      const float dh = dk[n] * (pd.v[u] - dk[256 + n] - (ph.v[u] - dk[512 + n]) * dk[768 + n]);
+      dhs[r * ldh + n] = r < nb ? dh : 0.f;
+    }
+  }
   pf_store(px, 64 * 32, [&](int e, float v) {
     const int r = e >> 5, kk = e & 31, c = (kt0 + kk) % C;
     const bool ok = r < nb && kt0 + kk < K;
@@ -1252,7 +1185,7 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
 // Weight-gradient partials (per image for the convs, per row block for the dense layer) -> the flat
 // gradient bucket, summed in partial order.  Each workgroup owns 64 elements of one segment; its 4
 // waves take every 4th partial with up to 32 loads in flight per thread; fixed combine order.
-constexpr int kMaxRed = 4;
+constexpr int kMaxRed = 6;
 struct ReduceArgs {
   int n;
   const float* part[kMaxRed];
@@ -1408,56 +1341,71 @@ TDE_API int tde_bncnn_conv_fwd(const TdeBnGeo* gg, int B, const float* in, const
   return 0;
 }
 
-TDE_API int tde_bncnn_dense_fwd(int B, int K, int D, int Dp, int kc, const float* in, const TdeBn* bn, const float* w,
-                                float* hpart, hipStream_t stream) {
-  if (!bn_ok(bn) || bn->mode == kBnSaved || bn->mode == kBnNone || (kc & 15) || kc < 16 || (Dp & 15) || Dp < D)
-    return -1;
-  if ((K + kc - 1) / kc > kMaxKc || 64 * kc > kUA * NTB || kc * kDenseCols > kUB * NTB) return -2;
-  const int lda = kc + 4, ldb = kDenseCols + 4;
-  const int lds = NTB * 8 + 4 * 32 * 4 + 64 * lda * 4 + kc * ldb * 4;
-  if (lds > kMaxLds) return -3;
-  DenseFwdArgs a{B, K, D, Dp, kc, lda, ldb, in, bn_of(bn), w, hpart, next_stamps()};
-  set_lds(dense_fwd_kernel, lds);
-  dense_fwd_kernel<<<dim3((Dp + kDenseCols - 1) / kDenseCols, (K + kc - 1) / kc, (B + 63) / 64), NTB, lds, stream>>>(a);
+// h = relu(BN(in)) . W (final, deterministic) and the dense BN's statistics partials per 16-row tile.
+TDE_API int tde_bncnn_dense_fwd(int B, int K, int D, int Dp, const float* in, const TdeBn* bn, const float* w, float* h,
+                                double* hstat, hipStream_t stream) {
+  if (!bn_ok(bn) || bn->mode == kBnSaved || bn->mode == kBnNone || (Dp & 15) || Dp < D || !h || !hstat) return -1;
+  const int kw = up((K + 15) / 16, 4);
+  if (kw > 4 * kDS) return -2;
+  DenseFwdArgs a{B, K, D, Dp, kw, dv(bn->C), in, bn_of(bn), w, h, hstat, next_stamps()};
+  dense_fwd_kernel<<<dim3(Dp / 16, (B + 15) / 16), NTB, 0, stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;
 }
 
-// head_fwd + head_bwd (see HeadArgs).  logits: [Dp/16][B][16] feature-tile partials (written by head_fwd).
-TDE_API int tde_bncnn_head(int B, int D, int Dp, int NC, int mode, const float* hpart, int nkc, float* h,
-                           const TdeBn* bn, float rate,
-                           unsigned long long seed, const long long* iter, int layer_id, int drop_on, const float* wh,
-                           const float* bh, float* logits, const int* labels, float scale, float* metrics, float* out,
-                           int out_softmax, float* dwh, float* dbh, float* dbeta, float* dgamma, float* dh,
+// The head (see HeadArgs): grid ceil(B/16).
+TDE_API int tde_bncnn_head(int B, int D, int Dp, int NC, int mode, const float* h, const double* hstat, const TdeBn* bn,
+                           float rate, unsigned long long seed, const long long* iter, int layer_id, int drop_on,
+                           const float* wh, const float* bh, const int* labels, float scale, float* metrics, float* out,
+                           int out_softmax, float* dwh_part, float* dbh_part, float* g, double* gstat,
                            hipStream_t stream) {
-  // the head computes its BN statistics itself: check the fields it uses
-  if (!bn || bn->C != D || (Dp & 15) || Dp < D || Dp > 16 * kHeadMaxTiles || NC < 1 || NC > 16 || B < 1 || !logits ||
-      nkc < 1 || nkc > kMaxKc || !hpart || !h)
+  if (!bn || bn->C != D || (Dp & 15) || Dp < D || Dp > kHeadMaxDp || NC < 1 || NC > 16 || B < 1 || !h || !hstat)
     return -1;
   if (!(bn->mode == kBnTrain || bn->mode == kBnMoving || bn->mode == kBnBatch)) return -2;
   if ((bn->mode == kBnTrain && !bn->saved) || ((bn->mode == kBnTrain || bn->mode == kBnMoving) && (!bn->mmean || !bn->mvar)))
     return -2;
-  if (mode == 0 && (!dwh || !dbh || !dh || !labels || bn->mode != kBnTrain)) return -3;
+  if (mode == 0 && (!dwh_part || !dbh_part || !g || !gstat || !labels || bn->mode != kBnTrain)) return -3;
   if (mode == 2 && !out) return -4;
   if (drop_on && !(rate > 0.f && rate < 1.f)) return -5;
-  HeadArgs a{B, D, Dp, NC, mode, hpart, nkc, h, bn_of(bn), rate, seed, iter, layer_id, drop_on, wh, bh, logits, labels, scale,
-             metrics, out, out_softmax, dwh, dbh, dbeta, dgamma, dh, next_stamps()};
-  head_fwd_kernel<<<Dp / 16, NTH, 0, stream>>>(a);
-  TDE_LAUNCH_CHECK();
-  a.stamps = next_stamps();
-  head_bwd_kernel<<<mode == 0 ? Dp / 16 : 1, NTH, 0, stream>>>(a);
+  const int nrt = (B + 15) / 16;
+  HeadArgs a{B, D, Dp, NC, mode, nrt, h, hstat, bn_of(bn), rate, seed, iter, layer_id, drop_on, wh, bh, labels, scale,
+             metrics, out, out_softmax, dwh_part, dbh_part, g, gstat, next_stamps()};
+  head_kernel<<<nrt, NTH, 0, stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;
 }
 
 TDE_API int tde_bncnn_dense_bwd(int B, int K, int D, int Dp, const float* in, const TdeBn* bn, const float* w,
-                                const float* dh, float* dwpart, float* g, double* acc, hipStream_t stream) {
-  if (!bn_ok(bn) || bn->mode != kBnSaved || (Dp & 15) || Dp < D || Dp > 256 || !acc) return -1;
+                                const float* gh, const float* h, const double* gstat, int nrt, const TdeBn* bnd,
+                                float* dbeta_d, float* dgamma_d, float* dwpart, float* g, double* acc,
+                                hipStream_t stream) {
+  if (!bn_ok(bn) || bn->mode != kBnSaved || (Dp & 15) || Dp < D || Dp > 256 || !acc || !gh || !h || !gstat || nrt < 1)
+    return -1;
+  if (!bnd || !bnd->saved || bnd->C != D) return -1;
   if (32 * D > kUWk * NTB || 64 * Dp > kUDh * NTB || 2 * (Dp / 16) > 32) return -2;
   const int ldh = Dp + 4;
-  const int lds = 16 * 2 * 32 * 8 + 4 * 32 * 4 + 32 * ldh * 4 + 64 * ldh * 4 + 2 * 64 * 33 * 4;
+  const int lds = 16 * 2 * 32 * 8 + 4 * 32 * 4 + 4 * 256 * 4 + 32 * ldh * 4 + 64 * ldh * 4 + 2 * 64 * 33 * 4;
   if (lds > kMaxLds) return -3;
-  DenseBwdArgs a{B, K, D, Dp, ldh, in, bn_of(bn), w, dh, dwpart, g, acc, next_stamps()};
+  DenseBwdArgs a{};
+  a.B = B;
+  a.K = K;
+  a.D = D;
+  a.Dp = Dp;
+  a.ldh = ldh;
+  a.nrt = nrt;
+  a.in = in;
+  a.bn = bn_of(bn);
+  a.w = w;
+  a.gh = gh;
+  a.h = h;
+  a.gstat = gstat;
+  a.bnd = bn_of(bnd);
+  a.dbeta_d = dbeta_d;
+  a.dgamma_d = dgamma_d;
+  a.dwpart = dwpart;
+  a.g = g;
+  a.acc = acc;
+  a.stamps = next_stamps();
   set_lds(dense_bwd_kernel, lds);
   dense_bwd_kernel<<<dim3((K + 31) / 32, (B + 63) / 64), NTB, lds, stream>>>(a);
   TDE_LAUNCH_CHECK();

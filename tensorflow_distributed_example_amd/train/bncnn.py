@@ -37,14 +37,15 @@ N.register_hip({
     "tde_bncnn_conv_fwd_cfg": (_i, [_vp, _vp]),
     # geo, B, in, bn_in, w, z, acc, stream
     "tde_bncnn_conv_fwd": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
-    # B, K, D, Dp, kc, in, bn, w, hpart, stream
-    "tde_bncnn_dense_fwd": (_i, [_i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]),
-    # B, D, Dp, NC, mode, hpart, nkc, h, bn, rate, seed, iter, layer_id, drop_on, wh, bh, logits, labels, scale,
-    # metrics, out, out_softmax, dwh, dbh, dbeta, dgamma, dh, stream
-    "tde_bncnn_head": (_i, [_i, _i, _i, _i, _i, _vp, _i, _vp, _vp, C.c_float, C.c_ulonglong, _vp, _i, _i, _vp, _vp,
-                            _vp, _vp, C.c_float, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
-    # B, K, D, Dp, in, bn, w, dh, dwpart, g, acc, stream
-    "tde_bncnn_dense_bwd": (_i, [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    # B, K, D, Dp, in, bn, w, h, hstat, stream
+    "tde_bncnn_dense_fwd": (_i, [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
+    # B, D, Dp, NC, mode, h, hstat, bn, rate, seed, iter, layer_id, drop_on, wh, bh, labels, scale, metrics, out,
+    # out_softmax, dwh_part, dbh_part, g, gstat, stream
+    "tde_bncnn_head": (_i, [_i, _i, _i, _i, _i, _vp, _vp, _vp, C.c_float, C.c_ulonglong, _vp, _i, _i, _vp, _vp, _vp,
+                            C.c_float, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
+    # B, K, D, Dp, in, bn, w, gh, h, gstat, nrt, bnd, dbeta_d, dgamma_d, dwpart, g, acc, stream
+    "tde_bncnn_dense_bwd": (_i, [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp,
+                                 _vp]),
     "tde_bncnn_conv_bwd_plan": (_i, [_vp, _i, _vp]),
     # geo, B, z, bn, bb, gout, w, in, bn_in, gin, acc_in, dwpart, dgrad, stream
     "tde_bncnn_conv_bwd": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
@@ -179,8 +180,6 @@ class BnCnnPlan(ReplicaPlan):
         self.K = last["geo"].Ho * last["geo"].Wo * last["geo"].Co
         self.D = dense.units
         self.Dp = -(-self.D // 16) * 16
-        self.kc = -(-(-(-self.K // 8)) // 32) * 32   # <= 8 K chunks of a multiple of 32
-        self.nkc = -(-self.K // self.kc)
         self.dense = dense
         self.wd, self.gwd = st.view(f"{dense.name}/kernel"), st.grad(f"{dense.name}/kernel")
         self.nrb = -(-B // 64)   # dense dW partials: one per 64-row block
@@ -201,9 +200,12 @@ class BnCnnPlan(ReplicaPlan):
         self.wh, self.bh = st.view(f"{head.name}/kernel"), st.view(f"{head.name}/bias")
         self.gwh, self.gbh = st.grad(f"{head.name}/kernel"), st.grad(f"{head.name}/bias")
         self.h = torch.zeros(B * self.Dp, **f32)
-        self.hpart = torch.zeros(self.nkc * B * self.Dp, **f32)
-        self.logits = torch.zeros(self.Dp // 16 * B * 16, **f32)
-        self.dh = torch.zeros(B * self.Dp, **f32)
+        nrt = -(-B // 16)   # 16-row tiles of the dense / head launches
+        self.hstat = torch.zeros(nrt * 2 * self.Dp, **f64)     # dense BN statistics partials per row tile
+        self.gstat = torch.zeros(nrt * 2 * self.Dp, **f64)     # its backward partials
+        self.gh = torch.zeros(B * self.Dp, **f32)              # dL/d(dense BN output) through the masks
+        self.dwh_part = torch.zeros(nrt * self.D * self.NC, **f32)
+        self.dbh_part = torch.zeros(nrt * self.NC, **f32)
         self.probs = torch.zeros(B, self.NC, **f32)
         H0, W0, C0 = self.blocks[0]["geo"].H, self.blocks[0]["geo"].W, self.blocks[0]["geo"].C
         self.x_stride = H0 * W0 * C0
@@ -248,8 +250,8 @@ class BnCnnPlan(ReplicaPlan):
                 raise RuntimeError(f"tde_bncnn_conv_fwd({blk['conv'].name}) failed with {rc}")
             bn_in = self._bn(blk, mode, B)
             inp = blk["z"]
-        rc = lib.tde_bncnn_dense_fwd(B, self.K, self.D, self.Dp, self.kc, _P(inp), C.byref(bn_in), _P(self.wd),
-                                     _P(self.hpart), s)
+        rc = lib.tde_bncnn_dense_fwd(B, self.K, self.D, self.Dp, _P(inp), C.byref(bn_in), _P(self.wd), _P(self.h),
+                                     _P(self.hstat), s)
         N.check(rc, "tde_bncnn_dense_fwd")
         return bn_in
 
@@ -261,12 +263,11 @@ class BnCnnPlan(ReplicaPlan):
         drop_on = int(self.drop is not None and self.drop.rate > 0 and phase is not False)
         train = hmode == 0
         rc = self.lib.tde_bncnn_head(
-            B, self.D, self.Dp, self.NC, hmode, _P(self.hpart), self.nkc, _P(self.h), C.byref(bn),
-            float(self.drop.rate if self.drop else 0.0),
-            self.drop_seed, _P(self.iterations), 0, drop_on, _P(self.wh), _P(self.bh), _P(self.logits), _P(labels),
-            float(scale), _P(self.metrics) if hmode != 2 else None, _P(probs), int(self.softmax), _P(self.gwh) if train else None,
-            _P(self.gbh) if train else None, _P(bnd["dbeta"]) if train else None,
-            _P(bnd["dgamma"]) if train else None, _P(self.dh) if train else None, N.stream_ptr())
+            B, self.D, self.Dp, self.NC, hmode, _P(self.h), _P(self.hstat), C.byref(bn),
+            float(self.drop.rate if self.drop else 0.0), self.drop_seed, _P(self.iterations), 0, drop_on,
+            _P(self.wh), _P(self.bh), _P(labels), float(scale), _P(self.metrics) if hmode != 2 else None, _P(probs),
+            int(self.softmax), _P(self.dwh_part) if train else None, _P(self.dbh_part) if train else None,
+            _P(self.gh) if train else None, _P(self.gstat) if train else None, N.stream_ptr())
         N.check(rc, "tde_bncnn_head")
 
     # ------------------------------------------------------------------ plan interface
@@ -284,12 +285,17 @@ class BnCnnPlan(ReplicaPlan):
         self._head(B, 0, "train", y, self.scale)
         last = self.blocks[-1]
         bn_last = self._bn(last, BN_SAVED, B)
+        bnd = self.bnd
+        bn_d = Bn(BN_SAVED, self.D, None, 0, float(B), _P(bnd["gamma"]), _P(bnd["beta"]), float(bnd["eps"]),
+                  float(bnd["momentum"]), 1.0, _P(bnd["mmean"]), _P(bnd["mvar"]), _P(bnd["saved"]))
         rc = lib.tde_bncnn_dense_bwd(B, self.K, self.D, self.Dp, _P(last["z"]), C.byref(bn_last), _P(self.wd),
-                                     _P(self.dh), _P(self.dwd_part), _P(last["g"]), _P(last["accb"]), s)
+                                     _P(self.gh), _P(self.h), _P(self.gstat), -(-B // 16), C.byref(bn_d),
+                                     _P(bnd["dbeta"]), _P(bnd["dgamma"]), _P(self.dwd_part), _P(last["g"]),
+                                     _P(last["accb"]), s)
         N.check(rc, "tde_bncnn_dense_bwd")
         # backward partials of block li's BN: from the dense backward (last block) or from the input-gradient
         # role of block li + 1's conv backward (one per image)
-        nkt_nrb = -(-self.K // 32) * self.nrb
+        nkt_nrb = -(-self.K // 32) * -(-B // 64)
         for li in range(len(self.blocks) - 1, -1, -1):
             blk = self.blocks[li]
             npart = nkt_nrb if li == len(self.blocks) - 1 else B
@@ -307,6 +313,8 @@ class BnCnnPlan(ReplicaPlan):
         # weight-gradient partials -> the bucket: per image for the convs, per 64-row block for the dense
         segs = [(b["dwpart"], b["gw"], b["K"] * b["geo"].Co, B) for b in self.blocks]
         segs.append((self.dwd_part, self.gwd, self.K * self.D, -(-B // 64)))
+        segs.append((self.dwh_part, self.gwh, self.D * self.NC, -(-B // 16)))
+        segs.append((self.dbh_part, self.gbh, self.NC, -(-B // 16)))
         n = len(segs)
         cnt = (C.c_int * n)(*[sg[3] for sg in segs])
         parts = (C.c_void_p * n)(*[sg[0].data_ptr() for sg in segs])
