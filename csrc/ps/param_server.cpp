@@ -21,7 +21,7 @@ namespace {
 
 enum Op : uint8_t {
   kInit = 1, kPull = 2, kPush = 3, kMovingAvg = 4, kStepAdd = 5, kStepGet = 6, kAssign = 7, kList = 8,
-  kSetOpt = 9, kPing = 10, kStats = 11
+  kSetOpt = 9, kPing = 10, kStats = 11, kStep = 12
 };
 
 struct Var {
@@ -210,6 +210,59 @@ struct PSServer {
           w.i64(pushes.load());
           w.i64(pulls.load());
           break;
+        case kStep: {
+          // One round trip per training step of an async worker (the Estimator's PS loop):
+          //   push gradients (SGD/momentum applied on receipt), moving-average pushes of BN statistics,
+          //   global-step / ticket counter increments, then pull fresh values of the listed variables
+          //   (read AFTER this request's own updates).
+          const float lr = r.f32();
+          w.u8(0);
+          const uint32_t kp = r.u32();
+          for (uint32_t i = 0; i < kp && r.ok; ++i) {
+            std::string name = r.str();
+            uint32_t nb = 0;
+            const char* g = r.view(&nb);
+            Var* v = find(name);
+            if (!v || !g) {
+              w.s[0] = 2;
+              continue;
+            }
+            apply(v, g, nb / 4, lr);
+          }
+          const uint32_t ka = r.u32();
+          for (uint32_t i = 0; i < ka && r.ok; ++i) {
+            std::string name = r.str();
+            const float m = r.f32();
+            uint32_t nb = 0;
+            const char* val = r.view(&nb);
+            Var* v = find(name);
+            if (!v || !val || nb / 4 != v->w.size()) {
+              w.s[0] = 2;
+              continue;
+            }
+            std::lock_guard<std::mutex> lk(v->mu);
+            for (size_t j = 0; j < v->w.size(); ++j) v->w[j] = v->w[j] * m + wire_f32(val, j) * (1.f - m);
+            v->version++;
+          }
+          const int64_t dstep = r.i64(), dticket = r.i64();
+          w.i64(dstep ? step.fetch_add(dstep) + dstep : step.load());
+          w.i64(dticket ? counters[0].fetch_add(dticket) + dticket : counters[0].load());
+          const uint32_t kl = r.u32();
+          for (uint32_t i = 0; i < kl && r.ok; ++i) {
+            std::string name = r.str();
+            Var* v = find(name);
+            if (!v) {
+              w.s[0] = 2;
+              w.bytes(nullptr, 0);
+              continue;
+            }
+            std::lock_guard<std::mutex> lk(v->mu);
+            w.bytes(v->w.data(), v->w.size() * 4);
+          }
+          if (kp) pushes++;
+          if (kl) pulls++;
+          break;
+        }
         case kPing:
           w.u8(0);
           break;
@@ -356,6 +409,48 @@ TDE_API int tde_ps_moving_avg(void* h, int k, const char** names, const float** 
   std::string resp;
   if (!((PSClient*)h)->call(w.s, &resp) || resp.empty()) return -1;
   return resp[0];
+}
+
+// One training step's round trip (kStep): push kp gradients, ka moving-average values (per-variable
+// momentum), add dstep / dticket to the global-step / ticket counters (returned in *step_out /
+// *ticket_out) and pull kl variables into outs[i] (sizes[i] floats).
+TDE_API int tde_ps_step(void* h, float lr, int kp, const char** pnames, const float** grads, const long long* psizes,
+                        int ka, const char** anames, const float* amoms, const float** avals,
+                        const long long* asizes, long long dstep, long long dticket, int kl, const char** lnames,
+                        float** outs, const long long* lsizes, long long* step_out, long long* ticket_out) {
+  tde_net::Writer w;
+  w.u8(kStep);
+  w.f32(lr);
+  w.u32((uint32_t)kp);
+  for (int i = 0; i < kp; ++i) {
+    w.str(pnames[i]);
+    w.bytes(grads[i], (size_t)psizes[i] * 4);
+  }
+  w.u32((uint32_t)ka);
+  for (int i = 0; i < ka; ++i) {
+    w.str(anames[i]);
+    w.f32(amoms[i]);
+    w.bytes(avals[i], (size_t)asizes[i] * 4);
+  }
+  w.i64(dstep);
+  w.i64(dticket);
+  w.u32((uint32_t)kl);
+  for (int i = 0; i < kl; ++i) w.str(lnames[i]);
+  std::string resp;
+  if (!((PSClient*)h)->call(w.s, &resp)) return -1;
+  tde_net::Reader r(resp);
+  const int st = r.u8();
+  const int64_t sv = r.i64(), tv = r.i64();
+  if (!r.ok) return -2;
+  if (step_out) *step_out = sv;
+  if (ticket_out) *ticket_out = tv;
+  for (int i = 0; i < kl; ++i) {
+    uint32_t nb = 0;
+    const char* p = r.view(&nb);
+    if (!p || (long long)nb != lsizes[i] * 4) return -3;
+    memcpy(outs[i], p, nb);
+  }
+  return st;
 }
 
 TDE_API int tde_ps_assign(void* h, const char* name, const float* data, long long n) {

@@ -50,6 +50,12 @@ N.register_host({
     "tde_ps_counter_add": (C.c_longlong, [C.c_void_p, C.c_int, C.c_longlong]),
     "tde_ps_set_optimizer": (C.c_int, [C.c_void_p, C.c_int, C.c_float]),
     "tde_ps_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
+    "tde_ps_step": (C.c_int, [C.c_void_p, C.c_float,
+                              C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_void_p), C.POINTER(C.c_longlong),
+                              C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.POINTER(C.c_void_p),
+                              C.POINTER(C.c_longlong), C.c_longlong, C.c_longlong,
+                              C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_void_p), C.POINTER(C.c_longlong),
+                              C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
 })
 
 INIT_FLAG = "__tde_initialized__"
@@ -121,6 +127,61 @@ class PSClient:
     def close(self):
         for c in self.conns:
             c.close()
+
+    # ------------------------------------------------------------------ flat fast path
+    def bind_store(self, store):
+        """Lay the client's host copies out like ``store``'s flat buffers: ``hw`` (trainable), ``hs``
+        (non-trainable state) and ``hg`` (gradients) are ONE pinned host tensor each, every variable a
+        view at its segment offset.  Pulls land straight in them, so loading the pulled values is ONE
+        async H2D copy per buffer and reading the gradients ONE D2H copy (instead of a copy per
+        variable), and each training step is ONE round trip per ps task (``step``)."""
+        pin = store.device.type == "cuda"
+        self.hw = torch.zeros(store.n_trainable, dtype=torch.float32, pin_memory=pin)
+        self.hs = torch.zeros(store.n_state, dtype=torch.float32, pin_memory=pin)
+        self.hg = torch.zeros(store.n_trainable, dtype=torch.float32, pin_memory=pin)
+        self.hs_new = torch.zeros(store.n_state, dtype=torch.float32, pin_memory=pin)
+        w, st, g = self.hw.numpy(), self.hs.numpy(), self.hg.numpy()
+        self.gview = {}
+        for n in self.names:
+            seg = store.segments[n]
+            buf = w if seg.trainable else st
+            self.host[n] = buf[seg.offset: seg.offset + seg.numel]
+            if seg.trainable:
+                self.gview[n] = g[seg.offset: seg.offset + seg.numel]
+        self.trainable = [n for n in self.names if store.segments[n].trainable]
+        self._step_args = []
+        for k, c in enumerate(self.conns):
+            push = [n for n in self.by_ps[k] if n in self.gview]
+            pull = list(self.by_ps[k])
+            self._step_args.append((
+                push, _arr(push), (C.c_void_p * len(push))(*[self.gview[n].ctypes.data for n in push]),
+                (C.c_longlong * len(push))(*[self.gview[n].size for n in push]),
+                pull, _arr(pull), (C.c_void_p * len(pull))(*[self.host[n].ctypes.data for n in pull]),
+                (C.c_longlong * len(pull))(*[self.host[n].size for n in pull])))
+
+    def step(self, lr, averages=None, dstep=1, dticket=0):
+        """One async training step's exchange with every ps task: push the gradients held in ``hg``,
+        the BN moving-average values ``averages`` ({name: (momentum, values)}), advance the global step
+        by ``dstep`` and the ticket counter by ``dticket`` (both on ps 0), and pull fresh values of every
+        variable into ``hw`` / ``hs``.  Returns (global step, ticket counter)."""
+        averages = averages or {}
+        gstep = ticket = None
+        for k, c in enumerate(self.conns):
+            push, pn, pp, ps_, pull, ln, lp, ls = self._step_args[k]
+            av = [n for n in self.by_ps[k] if n in averages]
+            vals = [np.ascontiguousarray(averages[n][1], dtype=np.float32).reshape(-1) for n in av]
+            so, to = C.c_longlong(), C.c_longlong()
+            rc = c.lib.tde_ps_step(
+                c.h, float(lr), len(push), pn, pp, ps_,
+                len(av), _arr(av), (C.c_float * len(av))(*[float(averages[n][0]) for n in av]),
+                (C.c_void_p * len(av))(*[v.ctypes.data for v in vals]), (C.c_longlong * len(av))(*[v.size for v in vals]),
+                int(dstep) if k == 0 else 0, int(dticket) if k == 0 else 0,
+                len(pull), ln, lp, ls, C.byref(so), C.byref(to))
+            if rc != 0:
+                raise ConnectionError(f"step exchange with {c.address} failed ({rc})")
+            if k == 0:
+                gstep, ticket = so.value, to.value
+        return gstep, ticket
 
     def set_optimizer(self, kind, momentum=0.0):
         for c in self.conns:

@@ -415,7 +415,94 @@ class Estimator:
             h.begin(ctx)
         it = iter(ds)
         names_bn = [n for n in store.names(trainable=False)]
+        bn_mom = {}
+        for n_ in names_bn:
+            layer = n_.split("/")[0]
+            bn_mom[n_] = next(l.momentum for l in m.layers if l.name == layer)
         lr = float(opt_saved.learning_rate)
+        if os.environ.get("TDE_PS_FLAT", "1") == "0":
+            gstep = self._ps_loop_per_variable(client, it, prog, plan, store, names_bn, bn_mom, lr, ctx, all_hooks,
+                                               target, max_steps, gstep)
+            return self._ps_end(client, chief, max_steps, gstep, ctx, all_hooks)
+        # flat pinned host mirrors of the store: one H2D for the pulled values, one D2H for the gradients,
+        # one round trip per ps task per step (push + BN averages + counters + pull: PSClient.step)
+        client.bind_store(store)
+        cuda = store.device.type == "cuda"
+
+        def load_pulled():
+            store.w.copy_(client.hw, non_blocking=cuda)
+            store.state.copy_(client.hs, non_blocking=cuda)
+            plan.on_weights_loaded()
+
+        # the ticket for a step is claimed before it is computed: the first one here, each later one in the
+        # previous step's exchange
+        ticket = client.counter_add(1, 1) if max_steps is not None else None
+        if ticket is None or ticket <= max_steps:
+            client.pull()
+            load_pulled()
+        while target is None or gstep < target:
+            if ticket is not None and ticket > max_steps:
+                break
+            try:
+                e = next(it)
+            except StopIteration:
+                break
+            x, y = _split(e)
+            x = np.asarray(x, dtype=np.float32).reshape((len(y),) + tuple(prog.x_shape))
+            y = np.asarray(y).reshape(-1)
+            n = len(y)
+            prog.x_stage[0].stage(x, prog.x_ring[0][0])
+            prog.y_stage[0].stage(y, prog.y_ring[0][0])
+            plan.scale = 1.0 / n
+            plan.train_step(prog.x_ring[0][0], prog.y_ring[0][0], n)
+            client.hg.copy_(store.g, non_blocking=cuda)
+            if names_bn:
+                client.hs_new.copy_(store.state, non_blocking=cuda)
+            store.g.zero_()
+            if cuda:
+                torch.cuda.synchronize(store.device)
+            avg = {}
+            if names_bn:
+                # the local step applied m*old + (1-m)*batch; recover the batch statistic and let the PS
+                # apply the moving average to ITS current value (no lost updates between async workers)
+                new_s = client.hs_new.numpy()
+                for n_ in names_bn:
+                    mm = bn_mom[n_]
+                    seg = store.segments[n_]
+                    sl = slice(seg.offset, seg.offset + seg.numel)
+                    avg[n_] = (mm, (new_s[sl] - mm * client.host[n_]) / (1.0 - mm))
+            ctx.prev_step = gstep
+            gstep, t = client.step(lr, avg, dstep=1, dticket=1 if max_steps is not None else 0)
+            ticket = t if max_steps is not None else None
+            load_pulled()
+            ctx.global_step = gstep
+            for h in all_hooks:
+                h.after_step(ctx)
+        return self._ps_end(client, chief, max_steps, gstep, ctx, all_hooks)
+
+    def _ps_end(self, client, chief, max_steps, gstep, ctx, all_hooks):
+        m = self.model
+        if m._store.device.type == "cuda":
+            torch.cuda.synchronize(m._store.device)   # the last async H2D out of the pinned mirrors
+        if chief and max_steps is not None:
+            # tickets are exhausted, but other workers may still be finishing steps they claimed: the
+            # final checkpoint/export of the chief must see all max_steps global updates
+            t0 = time.time()
+            while gstep < max_steps and time.time() - t0 < 120:
+                time.sleep(0.01)
+                gstep = client.global_step()
+            ctx.prev_step, ctx.global_step = ctx.global_step, gstep
+        if chief:
+            m._store.load_dict(client.pull())
+        for h in all_hooks:
+            h.end(ctx)
+        return self
+
+    def _ps_loop_per_variable(self, client, it, prog, plan, store, names_bn, bn_mom, lr, ctx, all_hooks, target,
+                              max_steps, gstep):
+        """The round-2 PS loop (``TDE_PS_FLAT=0``; the A/B baseline of bench/ps_throughput.py): ticket, pull,
+        push, moving averages and global step as separate round trips, per-variable host copies."""
+        m = self.model
         while target is None or gstep < target:
             if max_steps is not None and client.counter_add(1, 1) > max_steps:
                 break
@@ -439,12 +526,9 @@ class Estimator:
             store.g.zero_()
             client.push(grads, lr)
             if names_bn:
-                # the local step applied m*old + (1-m)*batch; recover the batch statistic and let the PS
-                # apply the moving average to ITS current value (no lost updates between async workers)
                 mom = {}
                 for n_ in names_bn:
-                    layer = n_.split("/")[0]
-                    mm = next(l.momentum for l in m.layers if l.name == layer)
+                    mm = bn_mom[n_]
                     new = store.view(n_).detach().cpu().numpy()
                     mom.setdefault(mm, {})[n_] = (new - mm * old_state[n_]) / (1.0 - mm)
                 for mm, dct in mom.items():
@@ -454,19 +538,7 @@ class Estimator:
             ctx.global_step = gstep
             for h in all_hooks:
                 h.after_step(ctx)
-        if chief and max_steps is not None:
-            # tickets are exhausted, but other workers may still be finishing steps they claimed: the
-            # final checkpoint/export of the chief must see all max_steps global updates
-            t0 = time.time()
-            while gstep < max_steps and time.time() - t0 < 120:
-                time.sleep(0.01)
-                gstep = client.global_step()
-            ctx.prev_step, ctx.global_step = ctx.global_step, gstep
-        if chief:
-            m._store.load_dict(client.pull())
-        for h in all_hooks:
-            h.end(ctx)
-        return self
+        return gstep
 
     def _ps_plan(self, B):
         from . import program as PG
@@ -474,6 +546,8 @@ class Estimator:
         return PG.make_plan(m, m._store, m._store.device, B, B, None, m.loss)
 
     def _ps_save(self, client, step):
+        if self.model._store.device.type == "cuda":
+            torch.cuda.synchronize(self.model._store.device)   # the last async H2D out of the pinned mirrors
         self.model._store.load_dict(client.pull())
         return self.manager.save(self.model, step)
 
