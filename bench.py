@@ -53,6 +53,13 @@ def parse():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--dtype", choices=("fp32", "bf16"), default=None,
                     help="compute precision (default fp32; resnet18: bf16, as its BASELINE config)")
+    ap.add_argument("--strategy", choices=("mwms", "mirrored"), default="mwms",
+                    help="mwms: one process per GPU (torchrun; default); mirrored: ONE process driving --gpus "
+                         "local GPUs (MirroredStrategy, in-process xGMI all-reduce, one hipGraph per GPU)")
+    ap.add_argument("--gpus-per-worker", type=int, default=1,
+                    help="mwms: local GPUs per worker process (torchrun --nproc-per-node = gpus / K)")
+    ap.add_argument("--devices", default=None,
+                    help="mirrored: explicit local device list, e.g. 0,1,2,3 (0,0 = a 2-replica rehearsal on one GPU)")
     return ap.parse_args()
 
 
@@ -68,17 +75,25 @@ def main():
     import tensorflow_distributed_example_amd as tde
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torchrun --nproc-per-node N")
+    gpw = max(1, a.gpus_per_worker) if a.strategy == "mwms" else a.gpus
+    if a.strategy == "mwms" and world * gpw != a.gpus:
+        if world == 1 and a.gpus > gpw:
+            raise SystemExit("--gpus N>1 must be launched with torchrun --nproc-per-node N/--gpus-per-worker")
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if torch.cuda.is_available():
-        torch.cuda.set_device(local_rank % torch.cuda.device_count())  # ranks > GPUs only in rehearsals
+        torch.cuda.set_device((local_rank * gpw) % torch.cuda.device_count())  # ranks > GPUs only in rehearsals
     tde.backend.set_random_seed(1234)
     dtype = a.dtype or ("bf16" if a.model == "resnet18" else "fp32")
     tde.backend.set_global_policy("float32" if dtype == "fp32" else "mixed_bfloat16")
-    strategy = tde.distribute.MultiWorkerMirroredStrategy()
+    if a.strategy == "mirrored":
+        if world != 1:
+            raise SystemExit("--strategy mirrored runs in ONE process (no torchrun)")
+        devs = [f"cuda:{d}" for d in a.devices.split(",")] if a.devices else [f"cuda:{i}" for i in range(a.gpus)]
+        strategy = tde.distribute.MirroredStrategy(devs)
+    else:
+        strategy = tde.distribute.MultiWorkerMirroredStrategy(gpus_per_worker=gpw if gpw > 1 else None)
     n = strategy.num_replicas_in_sync
+    n_local = strategy.num_local_replicas
     dB, dspe, dlr, from_logits, img, metric = MODELS[a.model]
     B = a.batch_per_gpu or dB
     GB = B * n
@@ -100,16 +115,19 @@ def main():
     # Synthetic MNIST-shaped data resident on the device: a pool of batches,
     # staged into the program's input ring once per execution (D2D copy).
     pool_execs = 4
-    g = torch.Generator(device="cpu").manual_seed(1000 + strategy.worker_index)
-    xs = torch.rand((pool_execs, spe, B) + tuple(in_shape), generator=g).to(dev)
-    ys = torch.randint(0, ncls, (pool_execs, spe, B), generator=g).to(torch.int32).to(dev)
+    xs, ys = [], []
+    for r in range(n_local):   # replica r's batches live on its device
+        g = torch.Generator(device="cpu").manual_seed(1000 + strategy.global_replica_id(r))
+        xs.append(torch.rand((pool_execs, spe, B) + tuple(in_shape), generator=g).to(strategy.local_devices[r]))
+        ys.append(torch.randint(0, ncls, (pool_execs, spe, B), generator=g).to(torch.int32)
+                  .to(strategy.local_devices[r]))
 
     # Input pipeline with prefetch (tf.data ``prefetch``): execution i replays the step graph on the batch
     # group already in the input ring, and the next group is staged right behind it on the same stream
     # (it cannot overwrite the ring before the replay has read it), so staging overlaps the host's wait.
     def stage(i):
         k = i % pool_execs
-        prog.stage([(xs[k], ys[k])])
+        prog.stage([(xs[r][k], ys[r][k]) for r in range(n_local)])
 
     def run_exec(i, prefetch=True):
         prog.run()
@@ -162,9 +180,10 @@ def main():
         elapsed = strategy.control.all_reduce_max(elapsed)
     logs = tde.metrics.logs_from(prog.global_metrics(), ["accuracy"])
     comm = strategy.comm
-    ar = {"XgmiCommunicator": "xgmi", "RcclCommunicator": "rccl", "StoreCommunicator": "store"}.get(
+    ar = {"XgmiCommunicator": "xgmi", "PeerXgmiCommunicator": "xgmi_peer", "RcclCommunicator": "rccl",
+          "StoreCommunicator": "store", "LocalCommunicator": "local"}.get(
         type(comm).__name__, "none")
-    if world > 1:  # data-parallel invariant (outside the timed region): every replica bit-identical
+    if n > 1:  # data-parallel invariant (outside the timed region): every replica bit-identical
         from tensorflow_distributed_example_amd.utils import debug
         fps = debug.replica_fingerprints(model)
         same = all(f[2] == fps[0][2] for f in fps)   # trainable weights (BN moving stats are per replica)
@@ -173,18 +192,21 @@ def main():
     # where the optimizer update runs: fused into the step's kernels (1 replica), into the xGMI
     # gradient all-reduce (one replica per process), or its own multi-tensor launch
     placement = {"local": "in_step_kernels", "xgmi": "allreduce"}.get(prog.plans[0].step_mode, "separate")
+    n_dev = len({str(d) for d in strategy.local_devices}) * strategy.num_workers
     ms = elapsed / a.steps * 1e3
     ips = GB * a.steps / elapsed
     if strategy.worker_index == 0:
-        print(f"[bench] plan={prog.plan_kind} graph={prog.use_graph} spe={spe} world={n} "
+        print(f"[bench] plan={prog.plan_kind} graph={prog.use_graph} spe={spe} world={n} local={n_local} "
               f"loss={logs['loss']:.4f} acc={logs['accuracy']:.4f}", file=sys.stderr)
         print(json.dumps({
-            "metric": metric, "value": round(ips, 1), "unit": "images/sec", "n_gpus": n, "steps": a.steps,
+            "metric": metric, "value": round(ips, 1), "unit": "images/sec", "n_gpus": n_dev, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": prog.plans[0].compute_dtype,
             "data": f"synthetic (random {'x'.join(map(str, img))} images, random labels; random-init weights)",
             "config": {"model": a.model, "global_batch": GB, "seq_len": None, "image_shape": list(img),
-                       "per_gpu_batch": B, "parallelism": f"dp{n}", "strategy": "MultiWorkerMirroredStrategy",
+                       "per_gpu_batch": B, "parallelism": f"dp{n}", "strategy": strategy.name,
+                       "replicas": n, "replicas_per_process": n_local,
+                       "graphs_per_execution": (len(prog.groups) if prog.per_replica else 1) if prog.use_graph else 0,
                        "steps_per_execution": spe, "warmup_steps_run": n_warm * spe,
                        "input_staged_in_timed_region": True,
                        "optimizer": f"SGD(lr={a.lr})", "plan": prog.plan_kind,

@@ -1,0 +1,90 @@
+#!/usr/bin/env python
+"""Data-parallel equivalence driver: N replicas at global batch G must train like ONE replica at G.
+
+Trains ``--execs`` executions of ``--spe`` steps of a zoo model on a fixed synthetic global batch stream
+(seeded; every layout sees the same G rows per step, replica r taking rows [r*G/N, (r+1)*G/N)) and
+saves the trainable weights of replica 0 (and a bit-identity flag over all replicas) to ``--out``.
+
+    python bench/dp_equiv.py --strategy single --out w1.npz
+    python bench/dp_equiv.py --strategy mirrored --devices 0,0 --out wm.npz
+    torchrun --nproc-per-node 2 bench/dp_equiv.py --strategy mwms --out wmw.npz
+
+Used by tests/test_mirrored_gpu.py ("N ranks at global G == 1 rank at G").
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--strategy", choices=("single", "mirrored", "mwms"), default="single")
+    ap.add_argument("--devices", default=None, help="mirrored: local device indices, e.g. 0,0")
+    ap.add_argument("--model", default="mnist_cnn")
+    ap.add_argument("--global-batch", type=int, default=128)
+    ap.add_argument("--spe", type=int, default=4)
+    ap.add_argument("--execs", type=int, default=3)
+    ap.add_argument("--lr", type=float, default=0.05)
+    ap.add_argument("--dtype", default="fp32")
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.utils import debug
+
+    tde.backend.set_random_seed(77)
+    tde.backend.set_global_policy("float32" if a.dtype == "fp32" else "mixed_bfloat16")
+    cuda = torch.cuda.is_available()
+    if a.strategy == "mirrored":
+        devs = [f"cuda:{d}" if cuda else "cpu" for d in (a.devices or "0,0").split(",")]
+        strategy = tde.distribute.MirroredStrategy(devs)
+    elif a.strategy == "mwms":
+        if cuda:
+            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
+        strategy = tde.distribute.MultiWorkerMirroredStrategy()
+    else:
+        strategy = tde.distribute.OneDeviceStrategy("cuda:0" if cuda else "cpu")
+    n = strategy.num_replicas_in_sync
+    G = a.global_batch
+    B = G // n
+    with strategy.scope():
+        model = getattr(tde.zoo, a.model)()
+        from_logits = a.model != "mnist_bn_cnn"
+        model.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=from_logits),
+                      optimizer=tde.optimizers.SGD(learning_rate=a.lr), metrics=["accuracy"],
+                      steps_per_execution=a.spe)
+    prog = model._program("train", G)
+    shape = tuple(prog.x_shape)
+    ncls = model.output_shape[-1]
+    gen = torch.Generator().manual_seed(4242)
+    for e in range(a.execs):
+        x = torch.rand((a.spe, G) + shape, generator=gen)
+        y = torch.randint(0, ncls, (a.spe, G), generator=gen).to(torch.int32)
+        parts = []
+        for i in range(strategy.num_local_replicas):
+            r = strategy.global_replica_id(i)
+            dev = strategy.local_devices[i]
+            parts.append((x[:, r * B:(r + 1) * B].contiguous().to(dev), y[:, r * B:(r + 1) * B].contiguous().to(dev)))
+        prog.stage(parts)
+        prog.run()
+        prog.sync()
+    fps = debug.replica_fingerprints(model)
+    same = all(f[2] == fps[0][2] for f in fps)
+    store = prog.plans[0].store
+    out = {name: store.view(name).detach().float().cpu().numpy() for name in store.names(trainable=True)}
+    logs = tde.metrics.logs_from(prog.global_metrics(), ["accuracy"])
+    if strategy.worker_index == 0:
+        np.savez(a.out, **out)
+        print(f"[dp_equiv] strategy={a.strategy} replicas={n} plan={prog.plan_kind} graph={prog.use_graph} "
+              f"comm={type(strategy.comm).__name__} step_mode={prog.plans[0].step_mode} "
+              f"replicas_identical={same} loss={logs['loss']:.6f}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,64 @@
+#!/usr/bin/env python
+"""Diagnostics of the in-process xGMI path (MirroredStrategy over replicas of one process): runs
+``--execs`` executions of ``--spe`` steps and prints, after each, the wall time, the communicator's
+error bits and every replica's all-reduce epoch.  Run with a short ``TDE_XGMI_TIMEOUT`` so a missed
+peer ends each wait quickly and shows up as error bits instead of a hang."""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--devices", default="0,0")
+    ap.add_argument("--spe", type=int, default=16)
+    ap.add_argument("--execs", type=int, default=40)
+    ap.add_argument("--model", default="mnist_cnn")
+    ap.add_argument("--sync-every", type=int, default=1)
+    ap.add_argument("--mwms", type=int, default=0, help="K > 0: MultiWorkerMirroredStrategy with K GPUs per worker "
+                    "(launch with torchrun)")
+    a = ap.parse_args()
+    import torch
+
+    import tensorflow_distributed_example_amd as tde
+    tde.backend.set_global_policy("float32")
+    if a.mwms:
+        strategy = tde.distribute.MultiWorkerMirroredStrategy(gpus_per_worker=a.mwms)
+    else:
+        strategy = tde.distribute.MirroredStrategy([f"cuda:{d}" for d in a.devices.split(",")])
+    comm = strategy.comm
+    tag = f"[diag w{strategy.worker_index}]"
+    print(f"{tag} comm={type(comm).__name__} groups={getattr(comm, 'groups', None)}", flush=True)
+    with strategy.scope():
+        model = getattr(tde.zoo, a.model)()
+        model.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=a.model != "mnist_bn_cnn"),
+                      optimizer=tde.optimizers.SGD(0.01), metrics=["accuracy"], steps_per_execution=a.spe)
+    n = strategy.num_replicas_in_sync
+    nl = strategy.num_local_replicas
+    prog = model._program("train", 64 * n)
+    print(f"{tag} per_replica={prog.per_replica} graph={prog.use_graph} mode={prog.plans[0].step_mode}", flush=True)
+    xs = [torch.rand((a.spe, 64) + tuple(prog.x_shape), device=d) for d in strategy.local_devices]
+    ys = [torch.randint(0, 10, (a.spe, 64), device=d).to(torch.int32) for d in strategy.local_devices]
+    for e in range(a.execs):
+        t0 = time.perf_counter()
+        prog.stage(list(zip(xs, ys)))
+        prog.run()
+        if (e + 1) % a.sync_every == 0 or e == a.execs - 1:
+            prog.sync()
+            dt = time.perf_counter() - t0
+            bits = comm.error_bits() if hasattr(comm, "error_bits") else None
+            eps = [comm.calls(i) for i in range(nl)] if hasattr(comm, "calls") else None
+            print(f"{tag} exec {e} {dt * 1e3:.2f} ms err={bits} epochs={eps}", flush=True)
+            if bits and any(bits):
+                print(f"{tag} STOP: error bits set", flush=True)
+                break
+    print(f"{tag} done", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -201,8 +201,19 @@ __device__ __forceinline__ void apply_chunk(const XgArgs& a, float lr_t, long lo
   }
 }
 
-template <bool UNCACHED>
-__global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgArgs a) {
+// One launch carries the parts of NL ranks (grid.y = local rank): several replicas of one process on
+// ONE device (the 1-GPU rehearsal of an N-GPU layout) run their parts in the same grid, so their mutual
+// waits never depend on two streams of one device running concurrently.  NL = 1 is the plain one-rank
+// launch.  The whole grid is resident at once (<= 8 x 128 workgroups of 256 threads).
+constexpr int kXgMaxLocal = 8;
+template <int NL>
+struct XgLaunch {
+  XgArgs r[NL];
+};
+
+template <bool UNCACHED, int NL>
+__global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL> la) {
+  const XgArgs& a = la.r[NL == 1 ? 0 : blockIdx.y];
   const int blk = blockIdx.x, tid = threadIdx.x;
   const uint32_t epoch = a.epoch[0] + 1;
   const int parity = epoch & 1;
@@ -316,6 +327,23 @@ TDE_API int tde_xgmi_open(int device, const char* handle, void** mapped) {
 
 TDE_API int tde_xgmi_close(void* mapped) { return (int)hipIpcCloseMemHandle(mapped); }
 
+// In-process replicas (MirroredStrategy over the GPUs of one process): device `dev` maps the
+// memory of device `peer` directly (no IPC), so the windows of the other replicas are plain
+// device pointers.  Called for every ordered pair BEFORE the windows are allocated.
+// Returns 0 when access is (already) enabled, -5 when the pair has no peer path.
+TDE_API int tde_enable_peer_access(int dev, int peer) {
+  if (dev == peer) return 0;
+  int can = 0;
+  if (hipDeviceCanAccessPeer(&can, dev, peer) != hipSuccess || !can) return -5;
+  if (hipSetDevice(dev) != hipSuccess) return -100;
+  hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+  if (e == hipErrorPeerAccessAlreadyEnabled) {
+    (void)hipGetLastError();   // clear the sticky "already enabled" status
+    return 0;
+  }
+  return (int)e;
+}
+
 TDE_API int tde_xgmi_free(void* window, void* epoch, void* err) {
   hipError_t e1 = window ? hipFree(window) : hipSuccess;
   hipError_t e2 = epoch ? hipFree(epoch) : hipSuccess;
@@ -333,19 +361,6 @@ TDE_API long long tde_xgmi_epoch(void* epoch) {
   return (long long)h;
 }
 
-// In-place SUM all-reduce of `grad` (M fp32 elements, M <= the window's max_elems).
-static int xg_launch(XgArgs& a, float* grad, long long M, long long max_elems, void* const* peers, void* epoch,
-                     void* err, int rank, int nranks, int nblocks, int uncached, long long timeout_ticks,
-                     hipStream_t stream);
-
-TDE_API int tde_xgmi_all_reduce(float* grad, long long M, long long max_elems, void* const* peers, void* epoch,
-                                void* err, int rank, int nranks, int nblocks, int uncached, long long timeout_ticks,
-                                hipStream_t stream) {
-  XgArgs a;
-  memset(&a, 0, sizeof(a));
-  return xg_launch(a, grad, M, max_elems, peers, epoch, err, rank, nranks, nblocks, uncached, timeout_ticks, stream);
-}
-
 // Fused form: SUM all-reduce of `grad` and the optimizer step of every element on every rank
 // (w/m/v flat like grad; shadows as in XgArgs); grad is left zeroed.
 struct TdeXgApply {
@@ -357,38 +372,11 @@ struct TdeXgApply {
   void* sht; int sh_cols; long long sht_ld;
 };
 
-TDE_API int tde_xgmi_all_reduce_apply(float* grad, long long M, long long max_elems, void* const* peers,
-                                      void* epoch, void* err, int rank, int nranks, int nblocks, int uncached,
-                                      long long timeout_ticks, const TdeXgApply* o, hipStream_t stream) {
-  if (!o || !o->w || (o->kind != kOptSGD && !o->m) || (o->kind == kOptAdam && (!o->v || !o->iterations))) return -7;
-  if ((((uintptr_t)o->w | (uintptr_t)o->m | (uintptr_t)o->v) & 15) || (o->sh && ((o->sh_lo & 3) || ((uintptr_t)o->sh & 7))))
-    return -8;
-  if (o->sht && (o->sh_cols <= 0 || !o->sh)) return -9;
-  XgArgs a;
-  memset(&a, 0, sizeof(a));
-  a.apply = 1;
-  a.w = o->w;
-  a.m = o->m;
-  a.v = o->v;
-  a.sh = (bf16*)o->sh;
-  a.sh_lo = o->sh ? o->sh_lo : 0;
-  a.sh_hi = o->sh ? o->sh_hi : 0;
-  a.sht = (bf16*)o->sht;
-  a.sh_cols = o->sh_cols;
-  a.sht_ld = o->sht_ld;
-  a.iterations = o->iterations;
-  a.h = OptHyper{o->kind, o->lr, o->mom, o->b1, o->b2, o->eps};
-  return xg_launch(a, grad, M, max_elems, peers, epoch, err, rank, nranks, nblocks, uncached, timeout_ticks, stream);
-}
-
-static int xg_launch(XgArgs& a, float* grad, long long M, long long max_elems, void* const* peers, void* epoch,
-                     void* err, int rank, int nranks, int nblocks, int uncached, long long timeout_ticks,
-                     hipStream_t stream) {
+static int xg_fill(XgArgs& a, float* grad, long long M, long long max_elems, void* const* peers, void* epoch,
+                   void* err, int rank, int nranks, int nblocks, long long timeout_ticks) {
   if (nranks < 1 || nranks > kXgMaxRanks || rank < 0 || rank >= nranks) return -1;
   if (M < 0 || M > max_elems) return -2;
   if (((uintptr_t)grad & 15) != 0) return -4;
-  if (nblocks < 1) nblocks = 1;
-  if (nblocks > kXgMaxBlocks) nblocks = kXgMaxBlocks;
   a.grad = grad;
   for (int i = 0; i < nranks; ++i) a.peer[i] = (char*)peers[i];
   a.epoch = (uint32_t*)epoch;
@@ -401,8 +389,83 @@ static int xg_launch(XgArgs& a, float* grad, long long M, long long max_elems, v
   a.cap = xg_cap(max_elems);
   a.timeout_ticks = timeout_ticks;
   if (a.L * nranks > a.cap) return -3;   // areas hold nranks slices
-  if (uncached) hipLaunchKernelGGL(xgmi_allreduce_kernel<true>, dim3(nblocks), dim3(kXgThreads), 0, stream, a);
-  else hipLaunchKernelGGL(xgmi_allreduce_kernel<false>, dim3(nblocks), dim3(kXgThreads), 0, stream, a);
+  return 0;
+}
+
+static int xg_set_apply(XgArgs& a, const TdeXgApply* o) {
+  if (!o || !o->w || (o->kind != kOptSGD && !o->m) || (o->kind == kOptAdam && (!o->v || !o->iterations))) return -7;
+  if ((((uintptr_t)o->w | (uintptr_t)o->m | (uintptr_t)o->v) & 15) || (o->sh && ((o->sh_lo & 3) || ((uintptr_t)o->sh & 7))))
+    return -8;
+  if (o->sht && (o->sh_cols <= 0 || !o->sh)) return -9;
+  a.apply = 1;
+  a.w = o->w;
+  a.m = o->m;
+  a.v = o->v;
+  a.sh = (bf16*)o->sh;
+  a.sh_lo = o->sh ? o->sh_lo : 0;
+  a.sh_hi = o->sh ? o->sh_hi : 0;
+  a.sht = (bf16*)o->sht;
+  a.sh_cols = o->sh_cols;
+  a.sht_ld = o->sht_ld;
+  a.iterations = o->iterations;
+  a.h = OptHyper{o->kind, o->lr, o->mom, o->b1, o->b2, o->eps};
+  return 0;
+}
+
+static int clamp_blocks(int nblocks) { return nblocks < 1 ? 1 : nblocks > kXgMaxBlocks ? kXgMaxBlocks : nblocks; }
+
+template <int NL>
+static int xg_go(const XgLaunch<NL>& la, int nloc, int nblocks, int uncached, hipStream_t stream) {
+  const dim3 grid(nblocks, nloc);
+  if (uncached) hipLaunchKernelGGL((xgmi_allreduce_kernel<true, NL>), grid, dim3(kXgThreads), 0, stream, la);
+  else hipLaunchKernelGGL((xgmi_allreduce_kernel<false, NL>), grid, dim3(kXgThreads), 0, stream, la);
   TDE_LAUNCH_CHECK();
   return 0;
+}
+
+// In-place SUM all-reduce of `grad` (M fp32 elements, M <= the window's max_elems).
+TDE_API int tde_xgmi_all_reduce(float* grad, long long M, long long max_elems, void* const* peers, void* epoch,
+                                void* err, int rank, int nranks, int nblocks, int uncached, long long timeout_ticks,
+                                hipStream_t stream) {
+  nblocks = clamp_blocks(nblocks);
+  XgLaunch<1> la;
+  memset(&la, 0, sizeof(la));
+  const int rc = xg_fill(la.r[0], grad, M, max_elems, peers, epoch, err, rank, nranks, nblocks, timeout_ticks);
+  return rc ? rc : xg_go(la, 1, nblocks, uncached, stream);
+}
+
+TDE_API int tde_xgmi_all_reduce_apply(float* grad, long long M, long long max_elems, void* const* peers,
+                                      void* epoch, void* err, int rank, int nranks, int nblocks, int uncached,
+                                      long long timeout_ticks, const TdeXgApply* o, hipStream_t stream) {
+  nblocks = clamp_blocks(nblocks);
+  XgLaunch<1> la;
+  memset(&la, 0, sizeof(la));
+  int rc = xg_set_apply(la.r[0], o);
+  if (!rc) rc = xg_fill(la.r[0], grad, M, max_elems, peers, epoch, err, rank, nranks, nblocks, timeout_ticks);
+  return rc ? rc : xg_go(la, 1, nblocks, uncached, stream);
+}
+
+// The parts of the `nloc` local ranks rank0 .. rank0+nloc-1 that share ONE device, in one launch
+// (grid.y = local rank).  grads[j] / epochs[j] / errs[j] / peers[j * nranks ...] belong to local rank
+// j; specs (nullable: plain all-reduce) holds nloc fused-optimizer descriptors.
+TDE_API int tde_xgmi_all_reduce_group(int nloc, float* const* grads, long long M, long long max_elems,
+                                      void* const* peers, void* const* epochs, void* const* errs, int rank0,
+                                      int nranks, int nblocks, int uncached, long long timeout_ticks,
+                                      const TdeXgApply* specs, hipStream_t stream) {
+  if (nloc < 1 || nloc > kXgMaxLocal || rank0 < 0 || rank0 + nloc > nranks) return -1;
+  nblocks = clamp_blocks(nblocks);
+  XgLaunch<kXgMaxLocal> la;
+  memset(&la, 0, sizeof(la));
+  for (int j = 0; j < nloc; ++j) {
+    int rc = specs ? xg_set_apply(la.r[j], specs + j) : 0;
+    if (!rc) rc = xg_fill(la.r[j], grads[j], M, max_elems, peers + (size_t)j * nranks, epochs[j], errs[j], rank0 + j,
+                          nranks, nblocks, timeout_ticks);
+    if (rc) return rc;
+  }
+  if (nloc == 1) {
+    XgLaunch<1> one;
+    one.r[0] = la.r[0];
+    return xg_go(one, 1, nblocks, uncached, stream);
+  }
+  return xg_go(la, nloc, nblocks, uncached, stream);
 }

@@ -29,6 +29,7 @@
 // Gradients land in the replica's flat fp32 bucket (one all-reduce for data parallelism), then the
 // multi-tensor optimizer kernel applies them.
 #include "tde_common.h"
+#include "tde_optim.h"
 
 namespace tde {
 namespace bncnn {
@@ -1185,7 +1186,14 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
 // Weight-gradient partials (per image for the convs, per row block for the dense layer) -> the flat
 // gradient bucket, summed in partial order.  Each workgroup owns 64 elements of one segment; its 4
 // waves take every 4th partial with up to 32 loads in flight per thread; fixed combine order.
-constexpr int kMaxRed = 6;
+// The reduce is the step's last launch: it advances the step counter (`iterations`: Keras
+// optimizer.iterations, the Philox dropout seed and Adam's t), which every block reads at its start
+// and the last block to finish stores (re-arming the arrival counter).  Fused step (apply = 1, one
+// replica): the summed gradient is not stored; the optimizer step is applied to the weight (and slots)
+// at the element's flat offset right there, so the separate multi-tensor optimizer launch disappears.
+// Segments whose partial IS the bucket (BN beta / gamma, written by the backward launches) are zeroed
+// after use.
+constexpr int kMaxRed = 16;
 struct ReduceArgs {
   int n;
   const float* part[kMaxRed];
@@ -1193,6 +1201,12 @@ struct ReduceArgs {
   long long len[kMaxRed];
   int cnt[kMaxRed];            // partials of the segment
   int blk0[kMaxRed + 1];       // first workgroup of the segment
+  int apply;
+  float* g;                    // the flat bucket (segment offsets = out[j] - g)
+  float *w, *m, *v;
+  long long* iterations;
+  unsigned* done;              // arrival counter (zero between launches)
+  OptHyper h;
   long long* stamps;
 };
 __global__ __launch_bounds__(NTH) void reduce_kernel(ReduceArgs a) {
@@ -1205,6 +1219,7 @@ __global__ __launch_bounds__(NTH) void reduce_kernel(ReduceArgs a) {
   const int cnt = a.cnt[j];
   const float* p = a.part[j];
   const long long ec = e < len ? e : len - 1;
+  const long long t = a.iterations ? *a.iterations + 1 : 0;
   float s = 0.f;
   for (int b0 = q; b0 < cnt; b0 += 128) {
     float v[32];
@@ -1217,7 +1232,26 @@ __global__ __launch_bounds__(NTH) void reduce_kernel(ReduceArgs a) {
   }
   red[q][l] = s;
   __syncthreads();
-  if (q == 0 && e < len) a.out[j][e] = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+  if (q == 0 && e < len) {
+    const float gs = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+    if (!a.apply) {
+      a.out[j][e] = gs;
+    } else {
+      const long long f = (a.out[j] - a.g) + e;
+      float m = a.h.kind != kOptSGD ? a.m[f] : 0.f, vv = a.h.kind == kOptAdam ? a.v[f] : 0.f;
+      a.w[f] = opt_step(a.h, opt_lr_t(a.h, t), a.w[f], gs, m, vv);
+      if (a.h.kind != kOptSGD) a.m[f] = m;
+      if (a.h.kind == kOptAdam) a.v[f] = vv;
+      if (p == a.out[j]) a.out[j][e] = 0.f;
+    }
+  }
+  if (a.iterations && threadIdx.x == 0) {
+    const unsigned arrived = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (arrived == gridDim.x - 1) {
+      *a.done = 0u;
+      *a.iterations = t;
+    }
+  }
 }
 
 }  // namespace bncnn
@@ -1535,16 +1569,36 @@ TDE_API int tde_bncnn_conv_bwd(const TdeBnGeo* gg, int B, const float* z, const 
   return 0;
 }
 
-// n segments: part[j] holds cnt[j] partials of len[j] floats, summed in order into out[j].
+// n segments: part[j] holds cnt[j] partials of len[j] floats, summed in order into out[j] (views of the
+// flat bucket g).  opt (nullable): apply the optimizer step instead of storing (see reduce_kernel).
+// iterations / done (nullable together): the step counter the launch advances and its arrival counter.
+struct TdeBnOpt {
+  int kind;
+  float lr, mom, b1, b2, eps;
+  float *g, *w, *m, *v;
+};
 TDE_API int tde_bncnn_reduce(int n, const int* cnt, const float* const* part, float* const* out, const long long* len,
-                             hipStream_t stream) {
-  if (n < 1 || n > kMaxRed) return -1;
+                             long long* iterations, unsigned* done, const TdeBnOpt* opt, hipStream_t stream) {
+  if (n < 1 || n > kMaxRed || (!iterations) != (!done)) return -1;
   ReduceArgs a{};
   a.n = n;
   a.stamps = next_stamps();
+  a.iterations = iterations;
+  a.done = done;
+  if (opt) {
+    if (!opt->g || !opt->w || !iterations || (opt->kind != kOptSGD && !opt->m) || (opt->kind == kOptAdam && !opt->v))
+      return -2;
+    a.apply = 1;
+    a.g = opt->g;
+    a.w = opt->w;
+    a.m = opt->m;
+    a.v = opt->v;
+    a.h = OptHyper{opt->kind, opt->lr, opt->mom, opt->b1, opt->b2, opt->eps};
+  }
   int blocks = 0;
   for (int j = 0; j < n; ++j) {
     if (cnt[j] < 1 || len[j] < 1) return -1;
+    if (opt && (out[j] < opt->g)) return -3;
     a.part[j] = part[j];
     a.out[j] = out[j];
     a.len[j] = len[j];

@@ -35,6 +35,7 @@ for s in "$@"; do
     t_convnet) step t_convnet 400 $PYT tests/test_kernels_gpu.py tests/test_plan_gpu.py ;;
     t_all) step t_all 1000 $PYT tests -m gpu ;;
     t_xgmi) step t_xgmi 400 $PYT tests/test_xgmi_gpu.py ;;
+    t_mirrored) step t_mirrored 500 $PYT tests/test_mirrored_gpu.py ;;
     t_layers) step t_layers 600 $PYT tests/test_layers_gpu.py ;;
     t_smallnet) step t_smallnet 300 $PYT tests/test_smallnet_gpu.py ;;
     t_examples) step t_examples 400 $PYT tests/test_examples_gpu.py ;;
@@ -48,6 +49,10 @@ for s in "$@"; do
     b_bn_cnn_bf16) step b_bn_cnn_bf16 300 python bench.py --model mnist_bn_cnn --steps 800 --warmup 64 --dtype bf16 ;;
     b_lenet5) step b_lenet5 300 python bench.py --model lenet5 --steps 800 --warmup 64 ;;
     b_mlp) step b_mlp 300 python bench.py --model mnist_mlp --steps 800 --warmup 64 ;;
+    b_ps) step b_ps 300 python -m tensorflow_distributed_example_amd.launch --ps 1 --master 1 --workers 1 --timeout 280 bench/ps_throughput.py --max-steps 3000 --warm 200 ;;
+    b_ps_legacy) step b_ps_legacy 300 env TDE_PS_FLAT=0 python -m tensorflow_distributed_example_amd.launch --ps 1 --master 1 --workers 1 --timeout 280 bench/ps_throughput.py --max-steps 3000 --warm 200 ;;
+    phases) step phases 150 python bench/bncnn_phases.py ;;
+    b_mirrored) step b_mirrored 300 env TDE_XGMI_TIMEOUT=30 python bench.py --strategy mirrored --devices 0,0 --steps 2000 --warmup 200 ;;
     b_resnet18) step b_resnet18 400 python bench.py --model resnet18 --steps 30 --warmup 5 ;;
     p_fp32) prof fp32 300 python3 bench.py --steps 400 --warmup 64 ;;
     p_bf16) prof bf16 300 python3 bench.py --steps 400 --warmup 64 --dtype bf16 ;;

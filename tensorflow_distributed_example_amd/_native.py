@@ -114,11 +114,13 @@ _HIP_PROTOS = {
     "tde_xgmi_alloc": (i32, [i32, i64, i32, C.POINTER(p), C.POINTER(p), C.POINTER(p), C.c_char_p]),
     "tde_xgmi_open": (i32, [i32, C.c_char_p, C.POINTER(p)]),
     "tde_xgmi_close": (i32, [p]),
+    "tde_enable_peer_access": (i32, [i32, i32]),
     "tde_xgmi_free": (i32, [p, p, p]),
     "tde_xgmi_error": (i32, [p]),
     "tde_xgmi_epoch": (i64, [p]),
     "tde_xgmi_all_reduce": (i32, [p, i64, i64, p, p, p, i32, i32, i32, i32, i64, p]),
     "tde_xgmi_all_reduce_apply": (i32, [p, i64, i64, p, p, p, i32, i32, i32, i32, i64, p, p]),
+    "tde_xgmi_all_reduce_group": (i32, [i32, p, i64, i64, p, p, p, i32, i32, i32, i32, i64, p, p]),
 }
 
 _EXTRA_HIP_PROTOS: dict = {}

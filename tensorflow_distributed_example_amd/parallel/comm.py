@@ -405,6 +405,274 @@ class XgmiCommunicator(Communicator):
         return ok
 
 
+class PeerXgmiCommunicator(Communicator):
+    """The xGMI two-shot all-reduce (csrc/comm/xgmi_allreduce.hip) for SEVERAL replicas per process:
+    ``MirroredStrategy`` over the GPUs of one process (``control=None``) or MWMS with K GPUs per worker.
+
+    Each local replica owns a window on its device.  The windows of the other local replicas are
+    plain device pointers (peer access enabled between the local devices, no IPC); the windows of other
+    processes' replicas are IPC-mapped once per (local device, remote rank).  Replica ``i`` is global
+    rank ``rank0 + i`` of the kernel's ``world``.
+
+    Replicas are grouped by device.  Each group's parts of the all-reduce run as ONE launch (grid.y =
+    local rank) that only waits, on the device, for the other groups' launches, so a group's step (fwd,
+    bwd, all-reduce[+optimizer]) is captured into a hipGraph of its own, on its own stream, and the host
+    replays one graph per device per execution (``train/runner.Program``).  On an N-GPU node every group
+    is one replica; several replicas mapped onto one device (the 1-GPU rehearsal) share a group, so their
+    mutual waits never depend on two streams of one device running concurrently.  Non-gradient
+    collectives (broadcast, other dtypes/ops) go to ``fallback``."""
+
+    capturable = True
+    per_replica = True   # all_reduce_one_ / all_reduce_apply_one_: one replica's launch on its stream
+    plain_ok = True
+
+    def __init__(self, devices, fallback, rank0=0, world=None, control=None, max_elems=None, uncached=None,
+                 timeout_s=None):
+        from .. import _native as N
+        self.lib = N.hip()
+        self.devices = [torch.device(d) for d in devices]
+        n = len(self.devices)
+        self.n_local = n
+        self.rank0 = int(rank0)
+        self.world = int(world or n)
+        self.world_size = self.world
+        self.fallback = fallback
+        self.cp = control
+        if self.world > self.lib.tde_xgmi_max_ranks():
+            raise ValueError(f"xGMI all-reduce supports at most {self.lib.tde_xgmi_max_ranks()} ranks")
+        if control is None and (self.rank0 != 0 or self.world != n):
+            raise ValueError("a multi-process PeerXgmiCommunicator needs the control plane")
+        self.max_elems = int(max_elems or os.environ.get("TDE_XGMI_MAX_ELEMS", 8 << 20))
+        self.uncached = int(os.environ.get("TDE_XGMI_UNCACHED", "1") if uncached is None else uncached)
+        self.nblocks_override = int(os.environ.get("TDE_XGMI_BLOCKS", 0))
+        timeout_s = float(timeout_s or os.environ.get("TDE_XGMI_TIMEOUT", 300))
+        self.timeout_ticks = int(timeout_s * 1e8)
+        self.windows, self.epochs, self.errs = [], [], []
+        self._opened = []
+        err = None
+        idx = sorted({d.index for d in self.devices})
+        for a in idx:   # before any window exists (allocations made later are mapped to the peers)
+            for b in idx:
+                rc = self.lib.tde_enable_peer_access(a, b)
+                if rc != 0 and err is None:
+                    err = f"peer access cuda:{a} -> cuda:{b} failed ({rc})"
+        handles = []
+        if err is None:
+            for d in self.devices:
+                w, e, x = C.c_void_p(), C.c_void_p(), C.c_void_p()
+                hb = C.create_string_buffer(self.lib.tde_xgmi_ipc_handle_bytes())
+                rc = self.lib.tde_xgmi_alloc(d.index, self.max_elems, self.uncached, C.byref(w), C.byref(e),
+                                             C.byref(x), hb)
+                if rc != 0:
+                    err = f"xGMI window allocation on {d} failed ({rc})"
+                    break
+                self.windows.append(w.value)
+                self.epochs.append(e.value)
+                self.errs.append(x.value)
+                handles.append(hb.raw)
+        peers = [[None] * self.world for _ in range(n)]
+        if control is not None:
+            # every process publishes its replicas' handles; a failure anywhere fails everywhere
+            allh = control.all_gather_json([h.hex() for h in handles] if err is None else None, "pxg_handles")
+            if any(h is None for h in allh):
+                err = err or "xGMI window setup failed on another worker"
+            else:
+                flat = [bytes.fromhex(h) for hs in allh for h in hs]
+                if len(flat) != self.world:
+                    err = f"xGMI: {len(flat)} windows for {self.world} ranks"
+        if err is None:
+            mapped = {}   # (device index, remote rank) -> pointer mapped on that device
+            for i, d in enumerate(self.devices):
+                for r in range(self.world):
+                    j = r - self.rank0
+                    if 0 <= j < n:
+                        peers[i][r] = self.windows[j]   # same process: the device pointer itself
+                        continue
+                    key = (d.index, r)
+                    if key not in mapped:
+                        m = C.c_void_p()
+                        rc = self.lib.tde_xgmi_open(d.index, flat[r], C.byref(m))
+                        if rc != 0:
+                            err = f"hipIpcOpenMemHandle of rank {r}'s window on {d} failed ({rc})"
+                            break
+                        self._opened.append(m.value)
+                        mapped[key] = m.value
+                    peers[i][r] = mapped[key]
+                if err is not None:
+                    break
+            if err is None and len({d.index for d in self.devices}) > 1:
+                # one IPC mapping per device: a runtime that hands every device the same mapping has not
+                # mapped it for the others, so refuse instead of faulting
+                for r in range(self.world):
+                    ptrs = {mapped[(d.index, r)] for d in self.devices if (d.index, r) in mapped}
+                    if len(ptrs) not in (0, len({d.index for d in self.devices})):
+                        err = f"IPC window of rank {r} mapped at one address for several devices"
+                        break
+        if control is not None:
+            errs = control.agree(err, "pxg_open")
+            if errs:
+                self._free()
+                raise RuntimeError(f"xGMI peer setup failed: {errs}")
+        elif err is not None:
+            self._free()
+            raise RuntimeError(err)
+        self.peers = [(C.c_void_p * self.world)(*p) for p in peers]
+        # groups of local replicas by device (order of first appearance), and their launch arrays
+        self.groups = []
+        for i, d in enumerate(self.devices):
+            for grp in self.groups:
+                if self.devices[grp[0]] == d:
+                    grp.append(i)
+                    break
+            else:
+                self.groups.append([i])
+        self._gargs = []
+        for grp in self.groups:
+            flat = [p for i in grp for p in peers[i]]
+            self._gargs.append(((C.c_void_p * len(flat))(*flat), (C.c_void_p * len(grp))(*[self.epochs[i] for i in grp]),
+                                (C.c_void_p * len(grp))(*[self.errs[i] for i in grp])))
+        self._side = [torch.cuda.Stream(self.devices[grp[0]]) for grp in self.groups]
+
+    def nblocks(self, M, nloc=1):
+        """Chunks per rank.  A launch carrying several local ranks keeps its whole grid within the
+        single-rank maximum (nloc x nblocks <= 128): two processes sharing one GPU (the rehearsal of a
+        K-GPUs-per-worker layout) with 2 x 128-workgroup grouped launches measured peer waits that never
+        completed, the same launches at 2 x 8 workgroups ran clean (profiles/r3_xgmi_groups.log)."""
+        cap = max(1, self.lib.tde_xgmi_max_blocks() // max(1, nloc))
+        if self.nblocks_override:
+            return min(self.nblocks_override, cap)
+        return max(min(8, cap), min(cap, -(-M // self.world) // 512))
+
+    def handles(self, t, op, i):
+        return (op == "sum" and t.dtype == torch.float32 and t.is_cuda and t.is_contiguous()
+                and t.numel() <= self.max_elems and t.data_ptr() % 16 == 0 and t.device == self.devices[i])
+
+    def all_reduce_group_(self, gi, grads, specs=None):
+        """Group ``gi``'s parts of the SUM all-reduce (``grads``: one flat fp32 bucket per replica of the
+        group, in group order) as ONE launch on the current stream of the group's device; with ``specs``
+        (one ``ops.kernels.XgApply`` per replica) the optimizer step is fused in
+        (``XgmiCommunicator.all_reduce_apply_``)."""
+        grp = self.groups[gi]
+        if len(grads) != len(grp) or not all(self.handles(t, "sum", i) for t, i in zip(grads, grp)):
+            raise ValueError("xGMI all-reduce: one fp32 contiguous bucket per group replica within the window")
+        M = grads[0].numel()
+        if any(t.numel() != M for t in grads):
+            raise ValueError("xGMI all-reduce: buckets of one group differ in length")
+        dev = self.devices[grp[0]]
+        sp = None
+        if specs is not None:
+            sp = (type(specs[0]) * len(specs))(*specs)
+        peers, epochs, errs = self._gargs[gi]
+        with torch.cuda.device(dev):
+            s = torch.cuda.current_stream(dev).cuda_stream
+            rc = self.lib.tde_xgmi_all_reduce_group(
+                len(grp), (C.c_void_p * len(grp))(*[t.data_ptr() for t in grads]), M, self.max_elems, peers, epochs,
+                errs, self.rank0 + grp[0], self.world, self.nblocks(M, len(grp)), self.uncached, self.timeout_ticks,
+                sp, s)
+        if rc != 0:
+            raise RuntimeError(f"tde_xgmi_all_reduce_group failed ({rc})")
+
+    def all_reduce_(self, tensors, op="sum"):
+        if len(tensors) != self.n_local or not all(self.handles(t, op, i) for i, t in enumerate(tensors)) or \
+                len({t.numel() for t in tensors}) != 1:
+            return self.fallback.all_reduce_(tensors, op)
+        # every group's launch on a side stream of its device, joined back into the callers' streams
+        cur = [torch.cuda.current_stream(self.devices[grp[0]]) for grp in self.groups]
+        for gi, grp in enumerate(self.groups):
+            self._side[gi].wait_stream(cur[gi])
+            with torch.cuda.device(self.devices[grp[0]]), torch.cuda.stream(self._side[gi]):
+                self.all_reduce_group_(gi, [tensors[i] for i in grp])
+        for gi in range(len(self.groups)):
+            cur[gi].wait_stream(self._side[gi])
+
+    def broadcast_(self, tensors, root=0):
+        return self.fallback.broadcast_(tensors, root)
+
+    def all_gather(self, send, recv):
+        return self.fallback.all_gather(send, recv)
+
+    def barrier(self):
+        self.fallback.barrier()
+
+    def calls(self, i=0):
+        return int(self.lib.tde_xgmi_epoch(self.epochs[i]))
+
+    def error_bits(self):
+        return [self.lib.tde_xgmi_error(e) for e in self.errs]
+
+    def check_health(self):
+        bits = self.error_bits()
+        if any(bits):
+            raise RcclError(f"xGMI all-reduce: a peer never arrived (error bits {bits}); a replica died or hung")
+        return self.fallback.check_health()
+
+    def abort(self):
+        if hasattr(self.fallback, "abort"):
+            self.fallback.abort()
+
+    def _free(self):
+        for m in self._opened:
+            self.lib.tde_xgmi_close(m)
+        self._opened = []
+        for w, e, x in zip(self.windows, self.epochs, self.errs):
+            self.lib.tde_xgmi_free(w, e, x)
+        self.windows, self.epochs, self.errs = [], [], []
+
+    def close(self):
+        self._free()
+        if self.fallback is not None:
+            self.fallback.close()
+
+    def self_test(self, n=None):
+        """Bitwise check against the rank-ordered fp32 sum on every replica (3 calls: both parities)."""
+        n = n or min(self.max_elems, 347_146 + 37)
+        ok = True
+        saved, self.timeout_ticks = self.timeout_ticks, int(10 * 1e8)
+        try:
+            for it in range(3):
+                ts, wants = [], []
+                for i, d in enumerate(self.devices):
+                    idx = torch.arange(n, device=d, dtype=torch.float32)
+                    parts = [((idx * 0.37 + r * 1.91 + it) % 7.0) - 3.0 for r in range(self.world)]
+                    want = parts[0].clone()
+                    for p in parts[1:]:
+                        want += p
+                    ts.append(parts[self.rank0 + i].clone())
+                    wants.append(want)
+                self.all_reduce_(ts)
+                for d in self.devices:
+                    torch.cuda.synchronize(d)
+                ok = ok and all(bool(torch.equal(t, w)) for t, w in zip(ts, wants))
+            ok = ok and not any(self.error_bits())
+        finally:
+            self.timeout_ticks = saved
+        return ok
+
+
+def peer_xgmi(devices, fallback, rank0=0, world=None, control=None):
+    """``PeerXgmiCommunicator`` over ``devices`` when it sets up and passes its bitwise self-test on every
+    replica (agreed across workers), else ``fallback``.  ``TDE_ALLREDUCE=rccl`` keeps the fallback."""
+    import warnings
+    if os.environ.get("TDE_ALLREDUCE", "auto").lower() == "rccl" or not torch.cuda.is_available():
+        return fallback
+    err, xg, ok = None, None, False
+    try:
+        xg = PeerXgmiCommunicator(devices, fallback, rank0=rank0, world=world, control=control)
+        ok = xg.self_test()
+    except Exception as e:  # noqa: BLE001 - raised consistently on every worker (agreed in the constructor)
+        err = e
+    if control is not None:
+        ok = all(control.all_gather_json(bool(ok), "pxg_selftest"))
+    if not ok:
+        if xg is not None:
+            xg.fallback = None
+            xg.close()
+        warnings.warn(f"in-process xGMI all-reduce unavailable ({err or 'self-test failed'}); using "
+                      f"{type(fallback).__name__}")
+        return fallback
+    return xg
+
+
 def _time_allreduce(comm, t, iters, control):
     import time
     for _ in range(3):
@@ -424,13 +692,11 @@ def maybe_xgmi(fallback, device, rank, world, control, bucket_hint=None):
     ``TDE_ALLREDUCE`` = ``auto`` (default: self-test, then keep whichever of xGMI / RCCL is faster on
     a gradient-sized bucket — decided on rank 0's numbers so all ranks agree), ``xgmi`` (self-test
     only) or ``rccl`` (never wrap)."""
-    import socket
     import warnings
     mode = os.environ.get("TDE_ALLREDUCE", "auto").lower()
     if mode == "rccl" or world < 2 or not torch.cuda.is_available():
         return fallback
-    hosts = control.all_gather_json([socket.gethostname(), _boot_id()], "hosts")
-    if any(h != hosts[0] for h in hosts):
+    if not same_node(control):
         return fallback   # multi-node: RCCL handles the inter-node path
     err = None
     xg = None
@@ -473,6 +739,13 @@ def maybe_xgmi(fallback, device, rank, world, control, bucket_hint=None):
             xg.close()
             return fallback
     return xg
+
+
+def same_node(control):
+    """True when every worker of the control plane runs on this host (same hostname and boot id)."""
+    import socket
+    hosts = control.all_gather_json([socket.gethostname(), _boot_id()], "hosts")
+    return all(h == hosts[0] for h in hosts)
 
 
 def _boot_id():

@@ -225,10 +225,22 @@ class MirroredStrategy(Strategy):
         if n == 1:
             comm = CM.NullCommunicator()
         elif all(d.type == "cuda" for d in devs):
-            comm = CM.RcclCommunicator(devs)
+            comm = _local_gpu_comm(devs)
         else:
             comm = CM.LocalCommunicator(n)
         super().__init__(devs, comm, name="MirroredStrategy")
+
+
+def _local_gpu_comm(devs):
+    """Communicator of several GPU replicas in ONE process: the in-process xGMI peer all-reduce for the
+    gradient bucket (graph-captured per replica, optimizer fused), RCCL (ncclCommInitAll) for the rest.
+    Replicas sharing a device (a 1-GPU rehearsal of the N-GPU layout) cannot form an RCCL clique: their
+    non-gradient collectives use torch copies."""
+    distinct = len({d.index for d in devs}) == len(devs)
+    base = CM.RcclCommunicator(devs) if distinct else CM.LocalCommunicator(len(devs))
+    if os.environ.get("TDE_MIRRORED_XGMI", "1") == "0":
+        return base
+    return CM.peer_xgmi(devs, base)
 
 
 class OneDeviceStrategy(Strategy):
@@ -285,7 +297,7 @@ class MultiWorkerMirroredStrategy(Strategy):
     @staticmethod
     def _rccl(devs, topo, world, n_local, control):
         if world == 1:
-            return CM.RcclCommunicator(devs)
+            return _local_gpu_comm(devs)
         if os.environ.get("TDE_RCCL", "1") == "0":
             # no RCCL clique (e.g. several ranks sharing one GPU in a rehearsal): the control-plane store
             # carries the non-gradient collectives, the xGMI kernel the gradient bucket
@@ -310,6 +322,10 @@ class MultiWorkerMirroredStrategy(Strategy):
         if n_local == 1:
             # one GPU per process on one xGMI node: the gradient bucket takes the peer-memory kernel
             return CM.maybe_xgmi(base, devs[0], topo.rank, world, control)
+        # K GPUs per worker on one node: the same kernel over direct (in-process) and IPC (other
+        # workers) windows, one graph per local replica
+        if os.environ.get("TDE_MIRRORED_XGMI", "1") != "0" and CM.same_node(control):
+            return CM.peer_xgmi(devs, base, rank0=topo.rank * n_local, world=world * n_local, control=control)
         return base
 
     def barrier(self):

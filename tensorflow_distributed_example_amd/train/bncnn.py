@@ -49,9 +49,15 @@ N.register_hip({
     "tde_bncnn_conv_bwd_plan": (_i, [_vp, _i, _vp]),
     # geo, B, z, bn, bb, gout, w, in, bn_in, gin, acc_in, dwpart, dgrad, stream
     "tde_bncnn_conv_bwd": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
-    # n, cnt, part, out, len, stream
-    "tde_bncnn_reduce": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
+    # n, cnt, part, out, len, iterations, done, opt, stream
+    "tde_bncnn_reduce": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
 })
+
+
+class BnOpt(C.Structure):
+    """Fused optimizer of the reduce launch (step mode "local")."""
+    _fields_ = [("kind", C.c_int), ("lr", C.c_float), ("mom", C.c_float), ("b1", C.c_float), ("b2", C.c_float),
+                ("eps", C.c_float), ("g", C.c_void_p), ("w", C.c_void_p), ("m", C.c_void_p), ("v", C.c_void_p)]
 
 
 class Geo(C.Structure):
@@ -210,6 +216,9 @@ class BnCnnPlan(ReplicaPlan):
         H0, W0, C0 = self.blocks[0]["geo"].H, self.blocks[0]["geo"].W, self.blocks[0]["geo"].C
         self.x_stride = H0 * W0 * C0
         self.opt = OptimizerKernel(store, optimizer, {}, self.iterations) if optimizer is not None else None
+        self._done = torch.zeros(1, dtype=torch.int32, device=dev)   # arrival counter of the fused reduce
+        self._bn_segs = self._bn_gradient_segments()
+        self._opt_key_set = None
 
     def _bn_vars(self, bn):
         st, n = self.store, bn.name
@@ -311,16 +320,69 @@ class BnCnnPlan(ReplicaPlan):
             if rc != 0:
                 raise RuntimeError(f"tde_bncnn_conv_bwd({blk['conv'].name}) failed with {rc}")
         # weight-gradient partials -> the bucket: per image for the convs, per 64-row block for the dense
+        # (fused step: the optimizer applied in the same launch, BN gradients included)
         segs = [(b["dwpart"], b["gw"], b["K"] * b["geo"].Co, B) for b in self.blocks]
         segs.append((self.dwd_part, self.gwd, self.K * self.D, -(-B // 64)))
         segs.append((self.dwh_part, self.gwh, self.D * self.NC, -(-B // 16)))
         segs.append((self.dbh_part, self.gbh, self.NC, -(-B // 16)))
+        opt = None
+        if self.step_mode == "local":
+            segs += self._bn_segs
+            opt = C.byref(self._bnopt)
         n = len(segs)
         cnt = (C.c_int * n)(*[sg[3] for sg in segs])
         parts = (C.c_void_p * n)(*[sg[0].data_ptr() for sg in segs])
         outs = (C.c_void_p * n)(*[sg[1].data_ptr() for sg in segs])
         lens = (C.c_longlong * n)(*[sg[2] for sg in segs])
-        N.check(lib.tde_bncnn_reduce(n, cnt, parts, outs, lens, s), "tde_bncnn_reduce")
+        # the step's last launch also advances the step counter (dropout seed, Adam's t)
+        N.check(lib.tde_bncnn_reduce(n, cnt, parts, outs, lens, _P(self.iterations), _P(self._done), opt, s),
+                "tde_bncnn_reduce")
+
+    # ------------------------------------------------------------------ fused optimizer ("local")
+    def supports_step_mode(self, mode):
+        if mode == "plain":
+            return True
+        return mode == "local" and self.optimizer is not None and self.device.type == "cuda" and \
+            self._bn_segs is not None
+
+    def set_step_mode(self, mode):
+        super().set_step_mode(mode)
+        self._opt_key_set = self._opt_key()
+        if mode == "local":
+            o, st = self.optimizer, self.store
+            sl = o.slot_names()
+            m = st.slot(sl[0]) if sl else None
+            v = st.slot(sl[1]) if len(sl) > 1 else None
+            hp = o.hparams()
+            self._bnopt = BnOpt(o.kind_id, float(o.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"],
+                                _P(st.g), _P(st.w), _P(m), _P(v))
+
+    def _opt_key(self):
+        o = self.optimizer
+        return (o.kind_id, float(o.learning_rate), tuple(sorted(o.hparams().items()))) if o is not None else None
+
+    def refresh(self):
+        # the launch descriptor carries lr / hyper-parameters by value
+        if self.step_mode == "local" and self._opt_key_set != self._opt_key():
+            self.set_step_mode("local")
+
+    def _bn_gradient_segments(self):
+        """(part, out, len, 1) of every BN gamma / beta gradient (the backward writes them into the bucket),
+        or None when the fused reduce would not cover every trainable variable."""
+        segs, names = [], set()
+        for blk in self.blocks + [self.bnd]:
+            for key, var in (("dbeta", "beta"), ("dgamma", "gamma")):
+                if blk.get(key) is not None:
+                    g = blk[key]
+                    segs.append((g, g, g.numel(), 1))
+        covered = {g.data_ptr() for g, *_ in segs}
+        for b in self.blocks:
+            covered.add(b["gw"].data_ptr())
+        covered |= {self.gwd.data_ptr(), self.gwh.data_ptr(), self.gbh.data_ptr()}
+        for name in self.store.names(trainable=True):
+            if self.store.grad(name).data_ptr() not in covered:
+                return None
+        return segs
 
     def apply(self):
         self.opt.apply()

@@ -122,9 +122,17 @@ class Program:
         self._graph_key = None
         cuda = all(d.type == "cuda" for d in self.devices)
         env = os.environ.get("TDE_GRAPH", "1") != "0"
-        self.use_graph = bool(training and cuda and env and len(self.devices) == 1 and
-                              self.plans[0].kind != "reference" and
-                              (self.comm is None or self.comm.capturable))
+        # several local replicas over a per-replica communicator (in-process xGMI): every device group's
+        # steps run on a stream of their own and are captured into a hipGraph of their own
+        self.per_replica = bool(training and cuda and len(self.devices) > 1 and
+                                getattr(self.comm, "per_replica", False) and
+                                all(p.store.g.numel() <= self.comm.max_elems for p in self.plans))
+        # replicas grouped by device (the communicator's groups): one stream + one graph per group
+        self.groups = list(self.comm.groups) if self.per_replica else None
+        self.rstreams = [torch.cuda.Stream(self.devices[g[0]]) for g in self.groups] if self.per_replica else None
+        self.use_graph = bool(training and cuda and env and self.plans[0].kind != "reference" and
+                              ((len(self.devices) == 1 and (self.comm is None or self.comm.capturable))
+                               or self.per_replica))
         self._comm_warm = False
         self._dbg = os.environ.get("TDE_DEBUG_SYNC", "0") not in ("", "0") and cuda
         self.buckets = self._plan_buckets() if training else None
@@ -139,7 +147,15 @@ class Program:
         under the xGMI communicator it runs inside the gradient all-reduce ("xgmi")."""
         from ..parallel.comm import XgmiCommunicator
         self._route_grads()
-        if os.environ.get("TDE_FUSED_STEP", "1") == "0" or len(self.plans) != 1 or self.buckets:
+        if os.environ.get("TDE_FUSED_STEP", "1") == "0" or self.buckets:
+            return
+        if self.per_replica:
+            if all(p.supports_step_mode("xgmi") for p in self.plans):
+                for p in self.plans:
+                    p.set_step_mode("xgmi")
+                self.comm_applies = True
+            return
+        if len(self.plans) != 1:
             return
         plan = self.plans[0]
         if self.comm is None and plan.supports_step_mode("local"):
@@ -202,12 +218,52 @@ class Program:
                 plan.apply()
             self._debug_sync("optimizer")
 
+    def _reduce_and_apply_group(self, gi):
+        """Device group gi's gradient all-reduce (+ optimizer) as one launch on its stream."""
+        idx = self.groups[gi]
+        plans = [self.plans[r] for r in idx]
+        if self.comm_applies:
+            self.comm.all_reduce_group_(gi, [p.store.g for p in plans], [p.xg_apply_spec() for p in plans])
+            return
+        self.comm.all_reduce_group_(gi, [p.store.g for p in plans])
+        for p in plans:
+            if not p.applies_in_step:
+                p.apply()
+
+    def _steps_group(self, gi, S, B=None):
+        """S training steps of device group gi (its launches only wait for the other groups on the device)."""
+        idx = self.groups[gi]
+        for s in range(S):
+            for r in idx:
+                self.plans[r].train_step(self.x_ring[r][s], self.y_ring[r][s], B)
+            self._reduce_and_apply_group(gi)
+            self._debug_sync("train_step + gradient all-reduce")
+        for r in idx:
+            self.plans[r].finish()
+
+    @contextlib.contextmanager
+    def _on_group(self, gi):
+        """Group gi's stream, ordered after (and joined back into) the device's current stream, where the
+        input staging runs."""
+        dev, s = self.devices[self.groups[gi][0]], self.rstreams[gi]
+        with torch.cuda.device(dev):
+            cur = torch.cuda.current_stream(dev)
+            s.wait_stream(cur)
+            with torch.cuda.stream(s):
+                yield
+            cur.wait_stream(s)
+
     def _finish(self):
         for plan in self.plans:
             with _ctx(plan.device):
                 plan.finish()
 
     def _steps(self, S, B=None):
+        if self.per_replica:
+            for gi in range(len(self.groups)):
+                with self._on_group(gi):
+                    self._steps_group(gi, S, B)
+            return
         for s in range(S):
             if self.buckets:
                 self._overlapped_step(s, B)
@@ -279,6 +335,31 @@ class Program:
         for p in self.plans:
             p.refresh()
         start = self._parities()
+        if self.per_replica:
+            gs = []
+            try:
+                for gi, idx in enumerate(self.groups):
+                    dev = self.devices[idx[0]]
+                    with torch.cuda.device(dev):
+                        torch.cuda.synchronize(dev)
+                        g = torch.cuda.CUDAGraph()
+                        gc.collect()
+                        gc.disable()
+                        try:
+                            with torch.cuda.graph(g, stream=self.rstreams[gi]):
+                                self._steps_group(gi, self.S)
+                        finally:
+                            gc.enable()
+                        torch.cuda.synchronize(dev)
+                    gs.append(g)
+                self._end = self._parities()
+            finally:
+                for p, q in zip(self.plans, start):
+                    p.parity = q
+            self.graphs[start] = (gs, self._end)
+            self._graph_key = self._key()
+            self.graph = gs[0]
+            return
         dev = self.devices[0]
         with torch.cuda.device(dev):
             torch.cuda.synchronize(dev)
@@ -325,12 +406,17 @@ class Program:
                     self.use_graph = False
                     self.graph = None
                     self.graphs = {}
-                    torch.cuda.synchronize(self.devices[0])
+                    self.sync()
                     self._steps(self.S)
                     return
             g, end = self.graphs[self._parities()]
-            with torch.cuda.device(self.devices[0]):
-                g.replay()
+            if self.per_replica:
+                for gi, gr in enumerate(g):   # one graph launch per device group, each on its stream
+                    with self._on_group(gi):
+                        gr.replay()
+            else:
+                with torch.cuda.device(self.devices[0]):
+                    g.replay()
             for p, q in zip(self.plans, end):
                 p.parity = q
         else:
@@ -353,6 +439,17 @@ class Program:
         for p in self.plans:
             p.scale = 1.0 / float(global_actual)
         try:
+            if self.per_replica:   # every group issues its all-reduce, with or without data
+                for gi, idx in enumerate(self.groups):
+                    with self._on_group(gi):
+                        for r in idx:
+                            n = len(per_replica[r][1])
+                            if n > 0:
+                                self.plans[r].train_step(self.x_ring[r][0], self.y_ring[r][0], n)
+                        self._reduce_and_apply_group(gi)
+                        for r in idx:
+                            self.plans[r].finish()
+                return
             if self.buckets:   # every rank issues the same bucket collectives, with or without data
                 n = len(per_replica[0][1])
                 if n > 0:

@@ -257,3 +257,34 @@ def test_bncnn_dropout_is_active_in_training_only():
     finally:
         tde.backend.set_learning_phase(None)
     assert not torch.equal(q1, q2)
+
+
+@pytest.mark.parametrize("kind", ["sgd", "momentum", "adam"])
+def test_bncnn_fused_reduce_optimizer_matches_separate_launch(kind):
+    """Step mode "local" (the optimizer applied inside the weight-gradient reduce launch, BN betas
+    included) vs "plain" (bucket + the multi-tensor optimizer launch): 3 steps (dropout on, so the step
+    counter that seeds the masks must advance identically) give bitwise-equal weights and slots."""
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.train import program as PG
+    opts = {"sgd": lambda: tde.optimizers.SGD(0.05), "momentum": lambda: tde.optimizers.SGD(0.05, momentum=0.9),
+            "adam": lambda: tde.optimizers.Adam(1e-3)}
+    res = {}
+    for mode in ("plain", "local"):
+        tde.backend.set_random_seed(11)
+        m = _model_b(tde, rate=0.3, opt=opts[kind]())
+        plan = PG.make_plan(m, m._store, DEV, 128, 128, m.optimizer, m.loss)
+        assert plan.supports_step_mode("local")
+        plan.set_step_mode(mode)
+        for i in range(3):
+            x, y = _data(128, 20 + i)
+            plan.train_step(x, y)
+            if mode == "plain":
+                plan.apply()
+        torch.cuda.synchronize()
+        st = m._store
+        res[mode] = (st.w.clone(), {k: v.clone() for k, v in st.slots.items()}, int(plan.iterations.item()))
+    (wp, sp, ip), (wl, sl, il) = res["plain"], res["local"]
+    assert ip == il == 3
+    assert torch.equal(wp, wl), float((wp - wl).abs().max())
+    for k in sp:
+        assert torch.equal(sp[k], sl[k]), k

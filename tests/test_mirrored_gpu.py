@@ -1,0 +1,184 @@
+"""Several replicas per process on the in-process xGMI all-reduce (parallel/comm.PeerXgmiCommunicator):
+MirroredStrategy over the GPUs of one process and MWMS with K GPUs per worker, each device's steps
+captured into a hipGraph of its own (train/runner.Program, per-replica mode; replicas that share a device
+form one group whose all-reduce parts are one launch).
+
+The GPU box has ONE MI355X, so the N-GPU layouts are rehearsed with several replicas mapped onto cuda:0
+(separate windows, buffers and streams; the kernel and the host code are the ones an 8-GPU node runs,
+only the peer pointers then point into other devices' HBM).  Data-parallel equivalence:
+N replicas at global batch G train like ONE replica at G (bench/dp_equiv.py).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ENV = dict(os.environ, TDE_HEARTBEAT="0", OMP_NUM_THREADS="2", TDE_BENCH_WARM_MS="0", TDE_XGMI_TIMEOUT="20")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_peer_xgmi_in_process_bitwise_eager_and_graphs(n):
+    import torch
+    from tensorflow_distributed_example_amd.parallel import comm as CM
+    devs = [torch.device("cuda:0")] * n
+    xg = CM.PeerXgmiCommunicator(devs, CM.LocalCommunicator(n), max_elems=1 << 20, timeout_s=30)
+    try:
+        assert xg.self_test()
+        g = torch.Generator().manual_seed(3)
+        for m in (347146, 1, 5, 1023, 4096 * 8 + 3, 1 << 20):
+            parts = [torch.randn(m, generator=g).cuda() for _ in range(n)]
+            want = parts[0].clone()
+            for p in parts[1:]:
+                want += p
+            ts = [p.clone() for p in parts]
+            xg.all_reduce_(ts)
+            torch.cuda.synchronize()
+            for t in ts:
+                assert torch.equal(t, want), m
+        # the replicas share cuda:0, so they form ONE device group: one launch per all-reduce (grid.y =
+        # replica), captured into one graph (4 all-reduces), replayed 3 times
+        assert xg.groups == [list(range(n))]
+        m = 250466
+        bufs = [torch.zeros(m, device="cuda") for _ in range(n)]
+        srcs = [torch.zeros(m, device="cuda") for _ in range(n)]
+        stream = torch.cuda.Stream()
+        torch.cuda.synchronize()
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=stream):
+            for k in range(4):
+                for i in range(n):
+                    bufs[i].copy_(srcs[i])
+                    bufs[i].mul_(float(k + 1))
+                xg.all_reduce_group_(0, bufs)
+                for i in range(n):
+                    srcs[i].copy_(bufs[i])
+        for rep in range(3):
+            torch.manual_seed(rep)
+            base = [torch.rand(m) for _ in range(n)]
+            for i in range(n):
+                srcs[i].copy_(base[i].cuda())
+            torch.cuda.synchronize()
+            with torch.cuda.stream(stream):
+                gr.replay()
+            torch.cuda.synchronize()
+            ref = [b.cuda() for b in base]
+            for k in range(4):
+                tot = ref[0] * float(k + 1)
+                for q in ref[1:]:
+                    tot += q * float(k + 1)
+                ref = [tot.clone() for _ in range(n)]
+            for i in range(n):
+                assert torch.equal(srcs[i], ref[i]), (rep, i)
+        assert not any(xg.error_bits())
+        assert xg.calls(0) == 3 + 6 + 12
+    finally:
+        xg.close()
+
+
+def _run(cmd, env, timeout=100):
+    """Run a (torchrun) command in its own process group; on timeout kill the whole group, so no rank is
+    left spinning on the GPU for the next test."""
+    import signal
+    p = subprocess.Popen(cmd, env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                         start_new_session=True)
+    try:
+        out, _ = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        out, _ = p.communicate()
+        raise AssertionError(f"timed out after {timeout} s: {' '.join(cmd)}\n{out[-3000:]}")
+    return p.returncode, out
+
+
+def _bench(args, env=None, nproc=None):
+    cmd = [sys.executable]
+    if nproc:
+        cmd += ["-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1",
+                f"--master-port={_free_port()}"]
+    cmd += [os.path.join(ROOT, "bench.py")] + args
+    rc, out = _run(cmd, dict(ENV, **(env or {})))
+    assert rc == 0, out[-4000:]
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out[-3000:]
+    return json.loads(lines[0]), out
+
+
+def test_mirrored_bench_graph_per_replica():
+    """bench.py --strategy mirrored with 2 replicas on cuda:0: in-process xGMI, one hipGraph per device per
+    execution (both replicas share cuda:0: one graph), the optimizer fused into the all-reduce, replicas
+    bit-identical."""
+    res, out = _bench(["--strategy", "mirrored", "--devices", "0,0", "--steps", "64", "--warmup", "16"])
+    c = res["config"]
+    assert res["config"]["replicas"] == 2 and c["strategy"] == "MirroredStrategy", res
+    assert c["allreduce"] == "xgmi_peer" and c["hipgraph"] is True and c["graphs_per_execution"] == 1, res
+    assert c["optimizer_placement"] == "allreduce", res
+    assert "replicas_identical=True" in out, out[-3000:]
+
+
+def test_mirrored_bench_bn_cnn_graph_per_replica():
+    """Model B (fused BN-CNN plan, separate optimizer launch) on the same per-device graphs."""
+    res, out = _bench(["--strategy", "mirrored", "--devices", "0,0", "--model", "mnist_bn_cnn", "--steps", "32",
+                       "--warmup", "16"])
+    c = res["config"]
+    assert c["allreduce"] == "xgmi_peer" and c["hipgraph"] is True and c["graphs_per_execution"] == 1, res
+    assert "replicas_identical=True" in out, out[-3000:]
+
+
+def test_mwms_two_gpus_per_worker_bench():
+    """MWMS 2 workers x 2 GPUs (all four replicas on cuda:0): the peer communicator spans direct windows
+    (same process) and IPC-mapped ones (the other worker); one graph per device group per worker."""
+    res, out = _bench(["--gpus", "4", "--gpus-per-worker", "2", "--steps", "32", "--warmup", "8"],
+                      env={"TDE_RCCL": "0"}, nproc=2)
+    c = res["config"]
+    assert c["replicas"] == 4 and c["replicas_per_process"] == 2, res
+    assert c["allreduce"] == "xgmi_peer" and c["hipgraph"] is True and c["graphs_per_execution"] == 1, res
+    assert "replicas_identical=True" in out, out[-3000:]
+
+
+def _equiv(tmp_path, name, args, env=None, nproc=None):
+    out = str(tmp_path / f"{name}.npz")
+    cmd = [sys.executable]
+    if nproc:
+        cmd += ["-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1",
+                f"--master-port={_free_port()}"]
+    cmd += [os.path.join(ROOT, "bench", "dp_equiv.py"), "--out", out] + args
+    rc, text = _run(cmd, dict(ENV, **(env or {})), timeout=60)
+    assert rc == 0, text[-4000:]
+    line = [l for l in text.splitlines() if l.startswith("[dp_equiv]")][0]
+    return dict(np.load(out)), line
+
+
+LAYOUTS = {
+    "mirrored": (["--strategy", "mirrored", "--devices", "0,0"], None, None),
+    "mwms": (["--strategy", "mwms"], {"TDE_RCCL": "0", "TDE_ALLREDUCE": "xgmi"}, 2),
+    "mwms2x2": (["--strategy", "mwms"], {"TDE_RCCL": "0", "TDE_GPUS_PER_WORKER": "2"}, 2),
+}
+
+
+@pytest.mark.parametrize("layout", sorted(LAYOUTS))
+def test_n_replicas_equal_one_replica_at_the_same_global_batch(layout, tmp_path):
+    """mnist_cnn (fp32), global batch 128, 12 steps: Mirrored 2 replicas (device-group graph, fused
+    all-reduce+SGD), MWMS 2 ranks (xGMI, fused) and MWMS 2x2 GPUs per worker each match ONE replica at 128
+    within fp32 summation-order noise; every layout keeps its replicas bit-identical."""
+    one, line1 = _equiv(tmp_path, "single", ["--strategy", "single"])
+    assert "graph=True" in line1, line1
+    args, env, nproc = LAYOUTS[layout]
+    w, line = _equiv(tmp_path, layout, args, env, nproc)
+    assert "replicas_identical=True" in line and "graph=True" in line and "step_mode=xgmi" in line, (layout, line)
+    for k in one:
+        np.testing.assert_allclose(w[k], one[k], rtol=1e-4, atol=1e-5, err_msg=f"{layout}: {k}")
