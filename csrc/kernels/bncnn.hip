@@ -222,6 +222,7 @@ struct ConvFwdArgs {
   float* z;
   double* acc;               // this layer's BN partial sums [msplit * B][2][Co] (nullable: no statistics)
   long long* stamps;         // diagnostic phase clock (tde_bncnn_stamps), nullable
+  long long* inc_iter;       // training, first layer: the step counter this step advances (nullable)
 };
 
 __global__ __launch_bounds__(NTB) void conv_fwd_kernel(ConvFwdArgs a) {
@@ -238,6 +239,9 @@ __global__ __launch_bounds__(NTB) void conv_fwd_kernel(ConvFwdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
   const int b = blockIdx.x, C = g.C, Co = g.Co, K = P.K, M = P.M, NTP = P.nct * 16, Wp = P.Wp;
   stamp(a.stamps, 0);
+  // the step counter (Keras optimizer.iterations: the dropout seed and Adam's t) advances at the start
+  // of a training step; no other launch of the step writes it, later ones read it
+  if (a.inc_iter && b == 0 && blockIdx.y == 0 && tid == 0) *a.inc_iter += 1;
   // ---- one batch of global loads: the image and the weights (the BN sums join in bn_prepare)
   const int nimg = g.H * g.W * C, nw = K * Co;
   const float* img = a.in + (size_t)b * nimg;
@@ -353,6 +357,10 @@ struct DenseFwdArgs {
   long long* stamps;
 };
 
+// V4 (K % 4 == 0, kw % 16 == 0): the A operand as one float4 load per 4 MFMA steps.  Lane (fr, fq)
+// loads in[row][k0 + 16s + 4fq .. +3] and MFMA j of the group contracts k = k0 + 16s + 4fq + j over
+// fq: a permutation of the K order that the B operand (W rows k) follows, so the product is the same.
+template <bool V4>
 __global__ __launch_bounds__(NTB) void dense_fwd_kernel(DenseFwdArgs a) {
   __shared__ double red[NTB];
   __shared__ float st[4 * 32];
@@ -363,13 +371,29 @@ __global__ __launch_bounds__(NTB) void dense_fwd_kernel(DenseFwdArgs a) {
   const int row = min(r0 + fr, a.B - 1), col = min(c0 + fr, a.D - 1);
   stamp(a.stamps, 0);
   float av[kDS], bv[kDS];
+  if (V4) {
+    const float* ar = a.in + (size_t)row * K;
 #pragma unroll
-  for (int s = 0; s < kDS; ++s)
-    if (4 * s < a.kw) {
-      const int k = min(k0 + 4 * s + fq, K - 1);
-      av[s] = a.in[(size_t)row * K + k];
-      bv[s] = a.w[(size_t)k * a.D + col];
-    }
+    for (int s4 = 0; s4 < kDS / 4; ++s4)
+      if (16 * s4 < a.kw) {
+        const int kb = min(k0 + 16 * s4 + 4 * fq, K - 4);
+        const float4 v = *reinterpret_cast<const float4*>(ar + kb);
+        av[4 * s4 + 0] = v.x;
+        av[4 * s4 + 1] = v.y;
+        av[4 * s4 + 2] = v.z;
+        av[4 * s4 + 3] = v.w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bv[4 * s4 + j] = a.w[(size_t)min(k0 + 16 * s4 + 4 * fq + j, K - 1) * a.D + col];
+      }
+  } else {
+#pragma unroll
+    for (int s = 0; s < kDS; ++s)
+      if (4 * s < a.kw) {
+        const int k = min(k0 + 4 * s + fq, K - 1);
+        av[s] = a.in[(size_t)row * K + k];
+        bv[s] = a.w[(size_t)k * a.D + col];
+      }
+  }
   bn_prepare(a.bn, st, blockIdx.x == 0 && blockIdx.y == 0, red);
   stamp(a.stamps, 1);
   const float* sc = st;
@@ -379,9 +403,10 @@ __global__ __launch_bounds__(NTB) void dense_fwd_kernel(DenseFwdArgs a) {
 #pragma unroll
   for (int s = 0; s < kDS; ++s)
     if (4 * s < a.kw) {
-      const int k = k0 + 4 * s + fq;
+      // V4: element j = s & 3 of group s >> 2; else step s, lane fq
+      const int k = V4 ? k0 + 16 * (s >> 2) + 4 * fq + (s & 3) : k0 + 4 * s + fq;
       const int c = k - dq(k, a.dC) * a.bn.C;
-      const bool kok = k < K && 4 * s + fq < a.kw;
+      const bool kok = k < K && k - k0 < a.kw;
       const float x = (kok && rok) ? fmaxf(fmaf(av[s], sc[c], sh[c]), 0.f) : 0.f;
       acc = mfma4(x, (kok && cok) ? bv[s] : 0.f, acc);
     }
@@ -426,6 +451,16 @@ __device__ __forceinline__ uint4 philox(uint4 c, uint2 k) {
   }
   return c;
 }
+// The keep scales of the 4 elements e0 .. e0+3 (e0 % 4 == 0): one Philox call (the same values as
+// keep_scale of each element).
+__device__ __forceinline__ float4 keep_scale4(float rate, unsigned long long seed, long long it, int layer, long long e0) {
+  const uint2 key{(unsigned)seed, (unsigned)(seed >> 32)};
+  const unsigned long long c = (unsigned long long)(e0 >> 2);
+  const uint4 r = philox(uint4{(unsigned)c, (unsigned)(c >> 32), (unsigned)it, (unsigned)layer}, key);
+  const float keep = 1.f - rate, inv = 1.f / keep;
+  auto f = [&](unsigned w) { return ((w >> 8) * (1.f / 16777216.f) < keep) ? inv : 0.f; };
+  return float4{f(r.x), f(r.y), f(r.z), f(r.w)};
+}
 __device__ __forceinline__ float keep_scale(float rate, unsigned long long seed, long long it, int layer, long long e) {
   const uint2 key{(unsigned)seed, (unsigned)(seed >> 32)};
   const unsigned long long c = (unsigned long long)(e >> 2);
@@ -444,10 +479,12 @@ __device__ __forceinline__ float keep_scale(float rate, unsigned long long seed,
 //   masks, and the dense BN's backward partial sums (sum g, sum g*xhat per feature) -> dense_bwd
 //   finishes dL/dh = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) while it stages it.
 constexpr int kHeadMaxDp = 256;
-constexpr int kHU = kHeadMaxDp * 16 / NTH;   // h / g elements per thread
+constexpr int NTHH = 1024;                   // head workgroups: 16 waves share the elementwise work
+constexpr int kHU = kHeadMaxDp * 16 / NTHH;  // h / g elements per thread
 constexpr int kHLD = kHeadMaxDp + 4;         // LDS row stride of the activation tile
 struct HeadArgs {
   int B, D, Dp, NC, mode, nrt;       // mode 0 train, 1 eval (metrics), 2 predict; nrt = row tiles
+  Dv dDp;
   const float* h;                    // [B][Dp]
   const double* hstat;               // [nrt][2][Dp]
   Bn bn;                             // C = D (mode kBnTrain / kBnMoving / kBnBatch)
@@ -463,7 +500,7 @@ struct HeadArgs {
   long long* stamps;
 };
 
-__global__ __launch_bounds__(NTH) void head_kernel(HeadArgs a) {
+__global__ __launch_bounds__(NTHH) void head_kernel(HeadArgs a) {
   __shared__ float mu[kHeadMaxDp], rs[kHeadMaxDp], sc[kHeadMaxDp], sh[kHeadMaxDp];
   __shared__ float As[16 * kHLD], Xh[16 * kHLD];
   __shared__ float whs[kHeadMaxDp * 16];   // [feature][class]
@@ -479,14 +516,14 @@ __global__ __launch_bounds__(NTH) void head_kernel(HeadArgs a) {
   float hv[kHU];
 #pragma unroll
   for (int u = 0; u < kHU; ++u) {
-    const int e = tid + u * NTH;
-    if (u * NTH < 16 * Dp) hv[u] = a.h[(size_t)min(r0 + e / Dp, B - 1) * Dp + e % Dp];
+    const int e = tid + u * NTHH;
+    if (u * NTHH < 16 * Dp) hv[u] = a.h[(size_t)r0 * Dp + min(e, (B - r0) * Dp - 1)];   // rows contiguous
   }
   float wv[kHU];
 #pragma unroll
   for (int u = 0; u < kHU; ++u) {
-    const int e = tid + u * NTH, f = e >> 4, c = e & 15;
-    if (u * NTH < 16 * Dp) wv[u] = (f < D && c < NC) ? a.wh[(size_t)min(f, D - 1) * NC + min(c, NC - 1)] : 0.f;
+    const int e = tid + u * NTHH, f = e >> 4, c = e & 15;
+    if (u * NTHH < 16 * Dp) wv[u] = (f < D && c < NC) ? a.wh[(size_t)min(f, D - 1) * NC + min(c, NC - 1)] : 0.f;
   }
   const int f = tid;
   double S = 0.0, S2 = 0.0;
@@ -533,26 +570,41 @@ __global__ __launch_bounds__(NTH) void head_kernel(HeadArgs a) {
   }
   lds_barrier();
   stamp(a.stamps, 1);
-  // ---- activation / xhat tiles, Wh
+  // ---- activation / xhat tiles, Wh.  With D % 4 == 0 the dropout masks are made 4 features at a time
+  // (one Philox call per 4 consecutive elements, D-indexed, so the same masks as element by element)
+  const bool quad = a.drop_on && (D & 3) == 0;
 #pragma unroll
   for (int u = 0; u < kHU; ++u) {
-    const int e = tid + u * NTH;
+    const int e = tid + u * NTHH;
     if (e < 16 * Dp) {
-      const int r = e / Dp, ff = e - r * Dp;
+      const int r = dq(e, a.dDp), ff = e - r * Dp;
       float act = 0.f, xh = 0.f;
       if (r0 + r < B && ff < D) {
         xh = (hv[u] - mu[ff]) * rs[ff];
         act = fmaxf(fmaf(hv[u], sc[ff], sh[ff]), 0.f);
-        if (a.drop_on) act *= keep_scale(a.rate, a.seed, it, a.layer_id, (long long)(r0 + r) * D + ff);
+        if (a.drop_on && !quad) act *= keep_scale(a.rate, a.seed, it, a.layer_id, (long long)(r0 + r) * D + ff);
       }
       As[r * kHLD + ff] = act;
       Xh[r * kHLD + ff] = xh;
     }
     if (e < 16 * Dp) whs[e] = wv[u];
   }
+  if (quad) {
+    lds_barrier();
+    for (int q = tid; q < 4 * D; q += NTHH) {   // 16 rows x D/4 groups
+      const int r = q / (D >> 2), f0 = 4 * (q - r * (D >> 2));
+      if (r0 + r >= B) continue;
+      const float4 k = keep_scale4(a.rate, a.seed, it, a.layer_id, (long long)(r0 + r) * D + f0);
+      float* ar = As + r * kHLD + f0;
+      ar[0] *= k.x;
+      ar[1] *= k.y;
+      ar[2] *= k.z;
+      ar[3] *= k.w;
+    }
+  }
   lds_barrier();
-  // ---- logits [16][16]: wave = K quarter, summed in wave order
-  {
+  // ---- logits [16][16]: waves 0-3 = K quarters, summed in wave order
+  if (wave < 4) {
     const int kq = Dp / 4;   // Dp % 16 == 0 -> multiple of 4
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int s = 0; s < kq / 4; ++s) {
@@ -611,7 +663,7 @@ __global__ __launch_bounds__(NTH) void head_kernel(HeadArgs a) {
   }
   const int ntf = Dp / 16;
   float* dwp = a.dwh_part + (size_t)rt * D * NC;
-  for (int ft = wave; ft < ntf; ft += 4) {
+  for (int ft = wave; ft < ntf; ft += NTHH / 64) {
     // dWh^T tile [feature][class] = act^T . dl over the 16 rows
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -670,6 +722,7 @@ __global__ __launch_bounds__(NTH) void head_kernel(HeadArgs a) {
 constexpr int kUDh = 16, kUWk = 8;   // dh block 64 x Dp <= 16384, W rows 32 x D <= 8192
 struct DenseBwdArgs {
   int B, K, D, Dp, ldh, nrt;
+  Dv dD, dDp, dC;
   const float* in; Bn bn;           // the input layer's raw output and its BN (kBnSaved)
   const float* w;                   // [K][D]
   const float* gh;                  // [B][Dp] the head's g (dL/d dense-BN output)
@@ -699,9 +752,14 @@ __global__ __launch_bounds__(NTB) void dense_bwd_kernel(DenseBwdArgs a) {
   Pf<kUWk> pw;
   Pf<kUDh> pd, ph;
   Pf<2> px;
-  pf_load(pw, 32 * D, [&](int e) { return a.w[(size_t)min(kt0 + e / D, K - 1) * D + e % D]; });
-  pf_load(pd, 64 * Dp, [&](int e) { return a.gh[(size_t)min(b0 + e / Dp, a.B - 1) * Dp + e % Dp]; });
-  pf_load(ph, 64 * Dp, [&](int e) { return a.h[(size_t)min(b0 + e / Dp, a.B - 1) * Dp + e % Dp]; });
+  // rows are contiguous: the tile is one clamped linear range (no index division in the address math)
+  const int wlast = (K - kt0) * D - 1, hlast = nb * Dp - 1;
+  const float* wt = a.w + (size_t)kt0 * D;
+  const float* ght = a.gh + (size_t)b0 * Dp;
+  const float* ht = a.h + (size_t)b0 * Dp;
+  pf_load(pw, 32 * D, [&](int e) { return wt[min(e, wlast)]; });
+  pf_load(pd, 64 * Dp, [&](int e) { return ght[min(e, hlast)]; });
+  pf_load(ph, 64 * Dp, [&](int e) { return ht[min(e, hlast)]; });
   pf_load(px, 64 * 32, [&](int e) { return a.in[(size_t)min(b0 + (e >> 5), a.B - 1) * K + min(kt0 + (e & 31), K - 1)]; });
   // the dense BN's backward sums for feature tid (fixed order over the head's row tiles)
   if (tid < Dp) {
@@ -740,22 +798,23 @@ __global__ __launch_bounds__(NTB) void dense_bwd_kernel(DenseBwdArgs a) {
   const float* mu = st + 2 * C;
   const float* rs = st + 3 * C;
   pf_store(pw, 32 * D, [&](int e, float v) {
-    const int kk = e / D, n = e - kk * D;
+    const int kk = dq(e, a.dD), n = e - kk * D;
     Wk[kk * ldh + n] = kt0 + kk < K ? v : 0.f;
   });
-  for (int e = tid; e < 32 * (Dp - D); e += NTB) Wk[(e / (Dp - D)) * ldh + D + e % (Dp - D)] = 0.f;
+  if (Dp > D)
+    for (int e = tid; e < 32 * (Dp - D); e += NTB) Wk[(e / (Dp - D)) * ldh + D + e % (Dp - D)] = 0.f;
 #pragma unroll
   for (int u = 0; u < kUDh; ++u) {
     const int e = tid + u * NTB;
     if (e < 64 * Dp) {
-      const int r = e / Dp, n = e - r * Dp;
+      const int r = dq(e, a.dDp), n = e - r * Dp;
       // dh = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)), xhat*rstd folded: (h - mean)*rstd*mean(g*xhat)
       const float dh = dk[n] * (pd.v[u] - dk[256 + n] - (ph.v[u] - dk[512 + n]) * dk[768 + n]);
       dhs[r * ldh + n] = r < nb ? dh : 0.f;
     }
   }
   pf_store(px, 64 * 32, [&](int e, float v) {
-    const int r = e >> 5, kk = e & 31, c = (kt0 + kk) % C;
+    const int r = e >> 5, kk = e & 31, kg = kt0 + kk, c = kg - dq(kg, a.dC) * C;
     const bool ok = r < nb && kt0 + kk < K;
     Xb[r * 33 + kk] = ok ? v : 0.f;
     Ab[r * 33 + kk] = ok ? fmaxf(fmaf(v, sc[c], sh[c]), 0.f) : 0.f;
@@ -764,7 +823,7 @@ __global__ __launch_bounds__(NTB) void dense_bwd_kernel(DenseBwdArgs a) {
   stamp(a.stamps, 2);
   if (wave < 8) {
     const int rt = wave & 3, kh = wave >> 2;
-    const int k_me = kt0 + kh * 16 + fr, c_me = k_me % C;
+    const int k_me = kt0 + kh * 16 + fr, c_me = k_me - dq(k_me, a.dC) * C;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int s0 = 0; s0 < Dp / 4; s0 += 4) {   // Dp % 16 == 0
 #pragma unroll
@@ -813,18 +872,19 @@ __global__ __launch_bounds__(NTB) void dense_bwd_kernel(DenseBwdArgs a) {
     }
   }
   // BN backward sums: feature f of wave w -> channel (kt0 + (w >> 2) * 16 + f) % C
+  stamp(a.stamps, 3);
   lds_barrier();
   if (tid < 2 * C) {
+    // the tile's features of channel c: kk = kk0, kk0 + C, ... (< 32), each over the 4 row tiles, in order
     const int j = tid / C, c = tid - j * C;
+    const int r0c = kt0 - dq(kt0, a.dC) * C;           // channel of the tile's first feature
     double S = 0.0;
-    for (int w = 0; w < 8; ++w)
-      for (int f = 0; f < 16; ++f) {
-        const int k = kt0 + (w >> 2) * 16 + f;
-        if (k < K && k % C == c) S += cs[(w * 2 + j) * 32 + f];
-      }
+    for (int kk = c >= r0c ? c - r0c : c - r0c + C; kk < 32 && kt0 + kk < K; kk += C)
+#pragma unroll
+      for (int rt = 0; rt < 4; ++rt) S += cs[((rt + 4 * (kk >> 4)) * 2 + j) * 32 + (kk & 15)];
     a.acc[(size_t)wg_id() * 2 * C + j * C + c] = S;
   }
-  stamp(a.stamps, 3);
+  stamp(a.stamps, 4);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1186,13 +1246,10 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
 // Weight-gradient partials (per image for the convs, per row block for the dense layer) -> the flat
 // gradient bucket, summed in partial order.  Each workgroup owns 64 elements of one segment; its 4
 // waves take every 4th partial with up to 32 loads in flight per thread; fixed combine order.
-// The reduce is the step's last launch: it advances the step counter (`iterations`: Keras
-// optimizer.iterations, the Philox dropout seed and Adam's t), which every block reads at its start
-// and the last block to finish stores (re-arming the arrival counter).  Fused step (apply = 1, one
-// replica): the summed gradient is not stored; the optimizer step is applied to the weight (and slots)
-// at the element's flat offset right there, so the separate multi-tensor optimizer launch disappears.
-// Segments whose partial IS the bucket (BN beta / gamma, written by the backward launches) are zeroed
-// after use.
+// Fused step (apply = 1, one replica): the summed gradient is not stored; the optimizer step is applied
+// to the weight (and slots) at the element's flat offset right there (Adam's t = the step counter the
+// step's first launch advanced), so the separate multi-tensor optimizer launch disappears.  Segments
+// whose partial IS the bucket (BN beta / gamma, written by the backward launches) are zeroed after use.
 constexpr int kMaxRed = 16;
 struct ReduceArgs {
   int n;
@@ -1204,8 +1261,7 @@ struct ReduceArgs {
   int apply;
   float* g;                    // the flat bucket (segment offsets = out[j] - g)
   float *w, *m, *v;
-  long long* iterations;
-  unsigned* done;              // arrival counter (zero between launches)
+  const long long* iterations;
   OptHyper h;
   long long* stamps;
 };
@@ -1219,7 +1275,7 @@ __global__ __launch_bounds__(NTH) void reduce_kernel(ReduceArgs a) {
   const int cnt = a.cnt[j];
   const float* p = a.part[j];
   const long long ec = e < len ? e : len - 1;
-  const long long t = a.iterations ? *a.iterations + 1 : 0;
+  const long long t = a.apply && a.h.kind == kOptAdam ? *a.iterations : 0;
   float s = 0.f;
   for (int b0 = q; b0 < cnt; b0 += 128) {
     float v[32];
@@ -1243,13 +1299,6 @@ __global__ __launch_bounds__(NTH) void reduce_kernel(ReduceArgs a) {
       if (a.h.kind != kOptSGD) a.m[f] = m;
       if (a.h.kind == kOptAdam) a.v[f] = vv;
       if (p == a.out[j]) a.out[j][e] = 0.f;
-    }
-  }
-  if (a.iterations && threadIdx.x == 0) {
-    const unsigned arrived = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (arrived == gridDim.x - 1) {
-      *a.done = 0u;
-      *a.iterations = t;
     }
   }
 }
@@ -1363,12 +1412,13 @@ TDE_API int tde_bncnn_conv_fwd_cfg(const TdeBnGeo* gg, int* out) {
 }
 
 // z = conv(relu(BN_in(in))); this layer's BN partial sums into acc [B][2][Co] (nullable).
+// inc_iter (nullable): the step counter a training step's first launch advances.
 TDE_API int tde_bncnn_conv_fwd(const TdeBnGeo* gg, int B, const float* in, const TdeBn* bn_in, const float* w, float* z,
-                               double* acc, hipStream_t stream) {
+                               double* acc, long long* inc_iter, hipStream_t stream) {
   ConvFwdP P;
   if (conv_fwd_plan(geo_of(gg), P) != 0) return -1;
   if (!bn_ok(bn_in) || bn_in->C != P.g.C || B < 1 || bn_in->mode == kBnSaved) return -2;
-  ConvFwdArgs a{P, B, in, bn_of(bn_in), w, z, acc, next_stamps()};
+  ConvFwdArgs a{P, B, in, bn_of(bn_in), w, z, acc, next_stamps(), inc_iter};
   set_lds(conv_fwd_kernel, P.lds);
   conv_fwd_kernel<<<dim3(B, P.msplit), NTB, P.lds, stream>>>(a);
   TDE_LAUNCH_CHECK();
@@ -1379,10 +1429,12 @@ TDE_API int tde_bncnn_conv_fwd(const TdeBnGeo* gg, int B, const float* in, const
 TDE_API int tde_bncnn_dense_fwd(int B, int K, int D, int Dp, const float* in, const TdeBn* bn, const float* w, float* h,
                                 double* hstat, hipStream_t stream) {
   if (!bn_ok(bn) || bn->mode == kBnSaved || bn->mode == kBnNone || (Dp & 15) || Dp < D || !h || !hstat) return -1;
-  const int kw = up((K + 15) / 16, 4);
+  const bool v4 = (K & 3) == 0 && ((uintptr_t)in & 15) == 0 && up((K + 15) / 16, 16) <= 4 * kDS;
+  const int kw = v4 ? up((K + 15) / 16, 16) : up((K + 15) / 16, 4);
   if (kw > 4 * kDS) return -2;
   DenseFwdArgs a{B, K, D, Dp, kw, dv(bn->C), in, bn_of(bn), w, h, hstat, next_stamps()};
-  dense_fwd_kernel<<<dim3(Dp / 16, (B + 15) / 16), NTB, 0, stream>>>(a);
+  if (v4) dense_fwd_kernel<true><<<dim3(Dp / 16, (B + 15) / 16), NTB, 0, stream>>>(a);
+  else dense_fwd_kernel<false><<<dim3(Dp / 16, (B + 15) / 16), NTB, 0, stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;
 }
@@ -1402,9 +1454,9 @@ TDE_API int tde_bncnn_head(int B, int D, int Dp, int NC, int mode, const float* 
   if (mode == 2 && !out) return -4;
   if (drop_on && !(rate > 0.f && rate < 1.f)) return -5;
   const int nrt = (B + 15) / 16;
-  HeadArgs a{B, D, Dp, NC, mode, nrt, h, hstat, bn_of(bn), rate, seed, iter, layer_id, drop_on, wh, bh, labels, scale,
+  HeadArgs a{B, D, Dp, NC, mode, nrt, dv(Dp), h, hstat, bn_of(bn), rate, seed, iter, layer_id, drop_on, wh, bh, labels, scale,
              metrics, out, out_softmax, dwh_part, dbh_part, g, gstat, next_stamps()};
-  head_kernel<<<nrt, NTH, 0, stream>>>(a);
+  head_kernel<<<nrt, NTHH, 0, stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;
 }
@@ -1427,6 +1479,9 @@ TDE_API int tde_bncnn_dense_bwd(int B, int K, int D, int Dp, const float* in, co
   a.Dp = Dp;
   a.ldh = ldh;
   a.nrt = nrt;
+  a.dD = dv(D);
+  a.dDp = dv(Dp);
+  a.dC = dv(bn->C);
   a.in = in;
   a.bn = bn_of(bn);
   a.w = w;
@@ -1571,23 +1626,23 @@ TDE_API int tde_bncnn_conv_bwd(const TdeBnGeo* gg, int B, const float* z, const 
 
 // n segments: part[j] holds cnt[j] partials of len[j] floats, summed in order into out[j] (views of the
 // flat bucket g).  opt (nullable): apply the optimizer step instead of storing (see reduce_kernel).
-// iterations / done (nullable together): the step counter the launch advances and its arrival counter.
 struct TdeBnOpt {
   int kind;
   float lr, mom, b1, b2, eps;
   float *g, *w, *m, *v;
+  const long long* iterations;
 };
 TDE_API int tde_bncnn_reduce(int n, const int* cnt, const float* const* part, float* const* out, const long long* len,
-                             long long* iterations, unsigned* done, const TdeBnOpt* opt, hipStream_t stream) {
-  if (n < 1 || n > kMaxRed || (!iterations) != (!done)) return -1;
+                             const TdeBnOpt* opt, hipStream_t stream) {
+  if (n < 1 || n > kMaxRed) return -1;
   ReduceArgs a{};
   a.n = n;
   a.stamps = next_stamps();
-  a.iterations = iterations;
-  a.done = done;
   if (opt) {
-    if (!opt->g || !opt->w || !iterations || (opt->kind != kOptSGD && !opt->m) || (opt->kind == kOptAdam && !opt->v))
+    if (!opt->g || !opt->w || !opt->iterations || (opt->kind != kOptSGD && !opt->m) ||
+        (opt->kind == kOptAdam && !opt->v))
       return -2;
+    a.iterations = opt->iterations;
     a.apply = 1;
     a.g = opt->g;
     a.w = opt->w;

@@ -35,8 +35,8 @@ BN_NONE, BN_TRAIN, BN_MOVING, BN_BATCH, BN_SAVED = 0, 1, 2, 3, 4
 _vp, _i = C.c_void_p, C.c_int
 N.register_hip({
     "tde_bncnn_conv_fwd_cfg": (_i, [_vp, _vp]),
-    # geo, B, in, bn_in, w, z, acc, stream
-    "tde_bncnn_conv_fwd": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
+    # geo, B, in, bn_in, w, z, acc, inc_iter, stream
+    "tde_bncnn_conv_fwd": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     # B, K, D, Dp, in, bn, w, h, hstat, stream
     "tde_bncnn_dense_fwd": (_i, [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
     # B, D, Dp, NC, mode, h, hstat, bn, rate, seed, iter, layer_id, drop_on, wh, bh, labels, scale, metrics, out,
@@ -49,15 +49,16 @@ N.register_hip({
     "tde_bncnn_conv_bwd_plan": (_i, [_vp, _i, _vp]),
     # geo, B, z, bn, bb, gout, w, in, bn_in, gin, acc_in, dwpart, dgrad, stream
     "tde_bncnn_conv_bwd": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
-    # n, cnt, part, out, len, iterations, done, opt, stream
-    "tde_bncnn_reduce": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    # n, cnt, part, out, len, opt, stream
+    "tde_bncnn_reduce": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp]),
 })
 
 
 class BnOpt(C.Structure):
     """Fused optimizer of the reduce launch (step mode "local")."""
     _fields_ = [("kind", C.c_int), ("lr", C.c_float), ("mom", C.c_float), ("b1", C.c_float), ("b2", C.c_float),
-                ("eps", C.c_float), ("g", C.c_void_p), ("w", C.c_void_p), ("m", C.c_void_p), ("v", C.c_void_p)]
+                ("eps", C.c_float), ("g", C.c_void_p), ("w", C.c_void_p), ("m", C.c_void_p), ("v", C.c_void_p),
+                ("iterations", C.c_void_p)]
 
 
 class Geo(C.Structure):
@@ -216,7 +217,6 @@ class BnCnnPlan(ReplicaPlan):
         H0, W0, C0 = self.blocks[0]["geo"].H, self.blocks[0]["geo"].W, self.blocks[0]["geo"].C
         self.x_stride = H0 * W0 * C0
         self.opt = OptimizerKernel(store, optimizer, {}, self.iterations) if optimizer is not None else None
-        self._done = torch.zeros(1, dtype=torch.int32, device=dev)   # arrival counter of the fused reduce
         self._bn_segs = self._bn_gradient_segments()
         self._opt_key_set = None
 
@@ -253,8 +253,10 @@ class BnCnnPlan(ReplicaPlan):
         inp = x
         bn_in = Bn(BN_NONE, self.blocks[0]["geo"].C)
         for li, blk in enumerate(self.blocks):
+            # a training step's first launch advances the step counter (dropout seed, Adam's t)
+            inc = _P(self.iterations) if (phase == "train" and li == 0) else None
             rc = lib.tde_bncnn_conv_fwd(C.byref(blk["geo"]), B, _P(inp), C.byref(bn_in), _P(blk["w"]), _P(blk["z"]),
-                                        _P(blk["acc"]) if batch_stats else None, s)
+                                        _P(blk["acc"]) if batch_stats else None, inc, s)
             if rc != 0:
                 raise RuntimeError(f"tde_bncnn_conv_fwd({blk['conv'].name}) failed with {rc}")
             bn_in = self._bn(blk, mode, B)
@@ -334,9 +336,7 @@ class BnCnnPlan(ReplicaPlan):
         parts = (C.c_void_p * n)(*[sg[0].data_ptr() for sg in segs])
         outs = (C.c_void_p * n)(*[sg[1].data_ptr() for sg in segs])
         lens = (C.c_longlong * n)(*[sg[2] for sg in segs])
-        # the step's last launch also advances the step counter (dropout seed, Adam's t)
-        N.check(lib.tde_bncnn_reduce(n, cnt, parts, outs, lens, _P(self.iterations), _P(self._done), opt, s),
-                "tde_bncnn_reduce")
+        N.check(lib.tde_bncnn_reduce(n, cnt, parts, outs, lens, opt, s), "tde_bncnn_reduce")
 
     # ------------------------------------------------------------------ fused optimizer ("local")
     def supports_step_mode(self, mode):
@@ -355,7 +355,7 @@ class BnCnnPlan(ReplicaPlan):
             v = st.slot(sl[1]) if len(sl) > 1 else None
             hp = o.hparams()
             self._bnopt = BnOpt(o.kind_id, float(o.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"],
-                                _P(st.g), _P(st.w), _P(m), _P(v))
+                                _P(st.g), _P(st.w), _P(m), _P(v), _P(self.iterations))
 
     def _opt_key(self):
         o = self.optimizer
