@@ -52,6 +52,10 @@ for s in "$@"; do
     b_ps) step b_ps 300 python -m tensorflow_distributed_example_amd.launch --ps 1 --master 1 --workers 1 --timeout 280 bench/ps_throughput.py --max-steps 3000 --warm 200 ;;
     b_ps_legacy) step b_ps_legacy 300 env TDE_PS_FLAT=0 python -m tensorflow_distributed_example_amd.launch --ps 1 --master 1 --workers 1 --timeout 280 bench/ps_throughput.py --max-steps 3000 --warm 200 ;;
     phases) step phases 150 python bench/bncnn_phases.py ;;
+    micro) step micro 200 python bench/micro.py ;;
+    snphases) step snphases 150 python bench/smallnet_phases.py ;;
+    p_lenet5) prof lenet5 300 python3 bench.py --model lenet5 --steps 400 --warmup 64 ;;
+    p_mlp) prof mlp 300 python3 bench.py --model mnist_mlp --steps 400 --warmup 64 ;;
     b_mirrored) step b_mirrored 300 env TDE_XGMI_TIMEOUT=30 python bench.py --strategy mirrored --devices 0,0 --steps 2000 --warmup 200 ;;
     b_resnet18) step b_resnet18 400 python bench.py --model resnet18 --steps 30 --warmup 5 ;;
     p_fp32) prof fp32 300 python3 bench.py --steps 400 --warmup 64 ;;
