@@ -13,7 +13,7 @@
 //                          that activation's ReLU), per-image conv weight/bias gradients into `part`,
 //                          dense inputs and pre-activation gradients into `rec`.
 //   smallnet_wgrad_kernel  batch reductions: conv partials summed over images, dense weight gradients
-//                          as X^T G over the batch (LDS-staged), bias gradients, metrics; each gradient
+//                          as X^T G over the batch on the exact-f32 MFMA, bias gradients, metrics; each gradient
 //                          element is finished by exactly one thread, which either stores it into the
 //                          flat gradient bucket (step mode "plain": all-reduce + optimizer follow) or
 //                          applies the optimizer to it right there (step mode "local").
@@ -758,8 +758,8 @@ struct SnRange {
 struct SnDense {
   int In, Co, xo, go, w_off, b_off, blk0, nblk;
 };
-constexpr int kSnRows = 8;     // dense weight rows per workgroup
-constexpr int kSnBChunk = 64;  // images staged per LDS pass
+constexpr int kSnStrip = 16;   // dense weight rows per workgroup (one MFMA row tile)
+constexpr int kSnColTiles = 4; // 16-column tiles per workgroup (one per wave)
 
 struct SnWgradArgs {
   SnRange r[2 * kSnMaxLayers];
@@ -788,9 +788,11 @@ __device__ __forceinline__ void sn_commit(const SnWgradArgs& a, int e, float gra
   if (a.h.kind == kOptAdam) a.v[e] = v;
 }
 
+__device__ __forceinline__ f32x4 sn_mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
 __global__ __launch_bounds__(256) void smallnet_wgrad_kernel(SnWgradArgs a) {
-  __shared__ __attribute__((aligned(16))) float Gs[kSnBChunk * 256];  // 64 KiB
-  __shared__ float Xs[kSnBChunk * kSnRows];
   __shared__ float red[8][33];
   const int blk = blockIdx.x, tid = threadIdx.x;
   const float lr_t = a.apply ? opt_lr_t(a.h, *a.iterations) : 0.f;
@@ -837,43 +839,48 @@ __global__ __launch_bounds__(256) void smallnet_wgrad_kernel(SnWgradArgs a) {
     }
     return;
   }
-  // dense weight gradients: rows [i0, i0 + 8) of layer k, dW[i][j] = sum_b X[b][i] G[b][j]
+  // dense weight gradients dW[i][j] = sum_b X[b][i] G[b][j] on the exact-f32 MFMA: workgroup = a
+  // 16-row strip x up to 4 column tiles of 16 (wave w = column tile), 4 images per MFMA step, every
+  // operand read straight from the per-image records (lane (fr, fq) takes X[b][i0 + fr] and G[b][j0 + fr]
+  // of image b = 4s + fq: the A / B fragment layout of v_mfma_f32_16x16x4_f32), the images summed in
+  // order (deterministic); the strip at i0 = 0 also sums the bias gradient (an MFMA against ones).
   int k = 0;
   while (k + 1 < a.nd && blk >= a.d[k + 1].blk0) ++k;
   const SnDense D = a.d[k];
-  const int i0 = (blk - D.blk0) * kSnRows;
-  const int Co = D.Co;
-  float acc[kSnRows];
+  const int nct = (D.Co + 15) >> 4, ncg = (nct + kSnColTiles - 1) / kSnColTiles;
+  const int lb = blk - D.blk0, strip = lb / ncg, cgp = lb - strip * ncg;
+  const int lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  const int jt = cgp * kSnColTiles + wave;
+  if (jt >= nct) return;   // no workgroup barrier below
+  const int i0 = strip * kSnStrip, j0 = jt * 16;
+  const float* X = a.rec + D.xo + min(i0 + fr, D.In - 1);
+  const float* G = a.rec + D.go + min(j0 + fr, D.Co - 1);
+  const bool bias = i0 == 0 && D.b_off >= 0;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f}, accb = {0.f, 0.f, 0.f, 0.f};
+  for (int b0 = 0; b0 < a.B; b0 += 64) {
+    float xv[16], gv[16];
 #pragma unroll
-  for (int r = 0; r < kSnRows; ++r) acc[r] = 0.f;
-  float accb = 0.f;
-  for (int b0 = 0; b0 < a.B; b0 += kSnBChunk) {
-    const int nb = min(kSnBChunk, a.B - b0);
-#pragma unroll 16
-    for (int idx = tid; idx < nb * Co; idx += 256) {
-      const int bb = idx / Co, j = idx - bb * Co;
-      Gs[bb * Co + j] = a.rec[(long long)(b0 + bb) * a.nrec + D.go + j];
+    for (int s = 0; s < 16; ++s) {
+      const long long b = min(b0 + 4 * s + fq, a.B - 1);
+      xv[s] = X[b * a.nrec];
+      gv[s] = G[b * a.nrec];
     }
-    for (int idx = tid; idx < nb * kSnRows; idx += 256) {
-      const int bb = idx / kSnRows, r = idx - bb * kSnRows;
-      Xs[idx] = i0 + r < D.In ? a.rec[(long long)(b0 + bb) * a.nrec + D.xo + i0 + r] : 0.f;
-    }
-    __syncthreads();
-    if (tid < Co) {
-      for (int bb = 0; bb < nb; ++bb) {
-        const float gv = Gs[bb * Co + tid];
-        accb += gv;
 #pragma unroll
-        for (int r = 0; r < kSnRows; ++r) acc[r] = fmaf(Xs[bb * kSnRows + r], gv, acc[r]);
-      }
+    for (int s = 0; s < 16; ++s) {
+      const bool ok = b0 + 4 * s + fq < a.B;
+      const float g = ok ? gv[s] : 0.f;
+      acc = sn_mfma4(ok ? xv[s] : 0.f, g, acc);
+      if (bias) accb = sn_mfma4(1.f, g, accb);
     }
-    __syncthreads();
   }
-  if (tid < Co) {
+  // lane (fr, fq) holds rows 4 fq + ii of column j0 + fr
+  if (j0 + fr < D.Co) {
 #pragma unroll
-    for (int r = 0; r < kSnRows; ++r)
-      if (i0 + r < D.In) sn_commit(a, D.w_off + (i0 + r) * Co + tid, acc[r], lr_t);
-    if (i0 == 0 && D.b_off >= 0) sn_commit(a, D.b_off + tid, accb, lr_t);
+    for (int ii = 0; ii < 4; ++ii) {
+      const int i = i0 + 4 * fq + ii;
+      if (i < D.In) sn_commit(a, D.w_off + i * D.Co + j0 + fr, acc[ii], lr_t);
+    }
+    if (bias && fq == 0) sn_commit(a, D.b_off + j0 + fr, accb[0], lr_t);
   }
 }
 

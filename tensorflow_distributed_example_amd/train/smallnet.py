@@ -190,7 +190,8 @@ class SmallNetPlan(ReplicaPlan):
             if s["kind"] == DENSE:
                 In = C
                 r.update(C=In, xo=rec, go=rec + In)
-                dense.append([In, Co, rec, rec + In, r["w_off"], r["b_off"], 0, -(-In // 8)])
+                # wgrad workgroups: 16-row strips x groups of 4 16-column tiles (smallnet_wgrad_kernel)
+                dense.append([In, Co, rec, rec + In, r["w_off"], r["b_off"], 0, -(-In // 16) * -(-(-(-Co // 16)) // 4)])
                 rec += In + Co
             r["out"] = off
             off = _a4(off + Ho * Wo * Co)
