@@ -21,6 +21,7 @@
 // Reference semantics: Keras Conv2D/MaxPooling2D/Dense/SCCE (SURVEY.md §2.5 A1-A14;
 // distributed_with_keras.py:33-43, tf2_mnist_distributed.py:66-83); the per-step loss is
 // sum(CE) / global_batch (Keras AUTO reduction under a strategy).
+#include <cstdlib>
 #include <type_traits>
 
 #include "tde_common.h"
@@ -62,6 +63,7 @@ struct SnArgs {
   float* probs;
   int probs_softmax;
   long long* stamps;  // optional phase timestamps of workgroup 0 (wall clock, 100 MHz)
+  int mfma;           // phases (bit 0 fwd, 1 wgrad, 2 dgrad) of the compile-time-geometry convs on the f32 MFMA
 };
 
 template <int CG>
@@ -443,6 +445,147 @@ __device__ void sn_conv_dgrad_c(const SnLayer L, float* s) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// The same compile-time-geometry conv phases on the exact-f32 MFMA (v_mfma_f32_16x16x4_f32; lane l
+// holds A[l & 15][k] and B[k][l & 15] for k = 4 step + (l >> 4), and D rows 4 (l >> 4) + i of column
+// l & 15): the per-image convolution as three GEMM forms read straight out of the LDS activations —
+//   forward  out[p][co]  = sum_k in_col[p][k] W[k][co],           k = (kh, kw, ci)
+//   wgrad    dW[t][co]   = sum_p in_col[p][t] dz[p][co],           t = (kh, kw, ci); row t = T is all
+//                          ones, so the same tile also sums the bias gradient; K (pixels) sliced over
+//                          waves when the tiles are few, slices summed in order (deterministic)
+//   dgrad    din[q][ci]  = sum_k dz_col[q][k] W[(kh, kw, ci)][co], k = (kh, kw, co), zero outside the
+//                          output
+// Items (M tile, N tile[, slice]) over the 8 waves.  TDE_SN_MFMA (bit mask: 1 forward, 2 weight
+// gradient, 4 input gradient; default 3) selects them, 0 keeps the VALU forms above: the MFMA input
+// gradient measured slower than the VALU one on LeNet-5 (13 M tiles of a 6-channel output on 8 waves),
+// so it is opt-in.  Only the forward K loop is unrolled: unrolling the others pushed the whole step
+// kernel past 256 VGPRs into scratch spills.
+constexpr int kSnWaves = kSnThreads / 64;
+
+__device__ __forceinline__ f32x4 sn_mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <int KH, int KW, int C, int Co, int Win, int Ho, int Wo>
+__device__ void sn_conv_fwd_m(const SnLayer L, float* s) {
+  constexpr int P = Ho * Wo, K = KH * KW * C, KS = (K + 3) / 4, MT = (P + 15) / 16, NT = (Co + 15) / 16;
+  const float* in = s + L.in;
+  const float* wl = s + L.wl;
+  float* out = s + L.out;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, fr = lane & 15, fq = lane >> 4;
+  for (int item = wave; item < MT * NT; item += kSnWaves) {
+    const int mt = item / NT, nt = item - mt * NT;
+    const int p = min(mt * 16 + fr, P - 1), oh = p / Wo, ow = p - oh * Wo;
+    const float* ip = in + (oh * Win + ow) * C;
+    const int co = nt * 16 + fr;
+    const bool cok = co < Co;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k = 4 * ks + fq, kc = min(k, K - 1);
+      const int kh = kc / (KW * C), r = kc - kh * (KW * C);
+      const float av = k < K ? ip[kh * Win * C + r] : 0.f;
+      const float bv = (k < K && cok) ? wl[kc * Co + co] : 0.f;
+      acc = sn_mfma4(av, bv, acc);
+    }
+    if (cok) {
+      const float bias = L.b_off >= 0 ? wl[K * Co + co] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int pr = mt * 16 + 4 * fq + i;
+        float v = acc[i] + bias;
+        if (L.relu) v = fmaxf(v, 0.f);
+        if (pr < P) out[pr * Co + co] = v;
+      }
+    }
+  }
+}
+
+template <int KH, int KW, int C, int Co, int Win, int Ho, int Wo>
+__device__ void sn_conv_wgrad_m(const SnLayer L, float* s, float* part) {
+  constexpr int T = KH * KW * C, T1 = T + 1, P = Ho * Wo, PS = (P + 3) / 4;
+  constexpr int MT = (T1 + 15) / 16, NT = (Co + 15) / 16;
+  constexpr int S0 = kSnWaves / (MT * NT) > 0 ? kSnWaves / (MT * NT) : 1;
+  constexpr int S = S0 * T1 * Co <= kSnScratch ? S0 : 1;
+  static_assert(T1 * Co <= kSnScratch, "scratch");
+  const float* in = s + L.in;
+  const float* dz = s + L.out;
+  float* red = s;   // [S][T + 1][Co]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, fr = lane & 15, fq = lane >> 4;
+  for (int item = wave; item < MT * NT * S; item += kSnWaves) {
+    const int sl = item / (MT * NT), rest = item - sl * (MT * NT), mt = rest / NT, nt = rest - mt * NT;
+    const int t = mt * 16 + fr, tc = min(t, T - 1);
+    const int kk = tc / C, ci = tc - kk * C, kh = kk / KW, kw = kk - kh * KW;
+    const float* ip = in + (kh * Win + kw) * C + ci;
+    const int co = nt * 16 + fr;
+    const bool cok = co < Co;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int s0 = PS * sl / S, s1 = PS * (sl + 1) / S;
+#pragma unroll 1
+    for (int ks = s0; ks < s1; ++ks) {
+      const int p = 4 * ks + fq, pc = min(p, P - 1);
+      const int oh = pc / Wo, ow = pc - oh * Wo;
+      const bool pok = p < P;
+      const float av = !pok || t > T ? 0.f : (t == T ? 1.f : ip[(oh * Win + ow) * C]);
+      const float bv = (pok && cok) ? dz[pc * Co + co] : 0.f;
+      acc = sn_mfma4(av, bv, acc);
+    }
+    if (cok) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int tr = mt * 16 + 4 * fq + i;
+        if (tr <= T) red[(sl * T1 + tr) * Co + co] = acc[i];
+      }
+    }
+  }
+  __syncthreads();
+  const int nw = L.b_off >= 0 ? T1 * Co : T * Co;
+  for (int e = threadIdx.x; e < nw; e += kSnThreads) {
+    float v = red[e];
+#pragma unroll
+    for (int sl = 1; sl < S; ++sl) v += red[sl * T1 * Co + e];
+    part[L.part + e] = v;
+  }
+}
+
+template <int KH, int KW, int C, int Co, int Win, int Hin, int Ho, int Wo>
+__device__ void sn_conv_dgrad_m(const SnLayer L, float* s) {
+  constexpr int Q = Hin * Win, K = KH * KW * Co, KS = (K + 3) / 4, MT = (Q + 15) / 16, NT = (C + 15) / 16;
+  float* in = s + L.in;
+  const float* dz = s + L.out;
+  const float* wl = s + L.wl;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, fr = lane & 15, fq = lane >> 4;
+  for (int item = wave; item < MT * NT; item += kSnWaves) {
+    const int mt = item / NT, nt = item - mt * NT;
+    const int q = min(mt * 16 + fr, Q - 1), ih = q / Win, iw = q - ih * Win;
+    const int ci = nt * 16 + fr;
+    const bool cok = ci < C;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k = 4 * ks + fq, kc = min(k, K - 1);
+      const int tap = kc / Co, co = kc - tap * Co, kh = tap / KW, kw = tap - kh * KW;
+      const int oh = ih - kh, ow = iw - kw;
+      const bool ok = k < K && (unsigned)oh < (unsigned)Ho && (unsigned)ow < (unsigned)Wo;
+      const float av = ok ? dz[(oh * Wo + ow) * Co + co] : 0.f;
+      const float bv = (k < K && cok) ? wl[(tap * C + min(ci, C - 1)) * Co + co] : 0.f;
+      acc = sn_mfma4(av, bv, acc);
+    }
+    if (cok) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int qr = mt * 16 + 4 * fq + i;
+        if (qr < Q) {
+          const int e = qr * C + ci;
+          float v = acc[i];
+          if (L.mask_in && !(in[e] > 0.f)) v = 0.f;
+          in[e] = v;
+        }
+      }
+    }
+  }
+}
+
 // (KH, KW, C, Co, input H, input W): LeNet-5's two convs (the first on the 32x32 zero-padded image)
 // and the DWK small CNN's conv
 #define SN_FAST_GEOS(X) \
@@ -451,12 +594,18 @@ __device__ void sn_conv_dgrad_c(const SnLayer L, float* s) {
   X(3, 3, 1, 32, 28, 28)
 
 // phase 0 forward, 1 weight gradient, 2 input gradient; false when the geometry is not compiled in
-__device__ __forceinline__ bool sn_conv_fast(int phase, const SnLayer L, float* s, float* part) {
+__device__ __forceinline__ bool sn_conv_fast(int phase, const SnLayer L, float* s, float* part, int mfma) {
   if (L.pt != 0 || L.pl != 0) return false;
 #define SN_FAST_CASE(KH_, KW_, C_, CO_, H_, W_)                                                              \
   if (L.kh == KH_ && L.kw == KW_ && L.C == C_ && L.Co == CO_ && L.H == H_ && L.W == W_) {                    \
     constexpr int CG = (CO_ % 4 == 0) ? 4 : ((CO_ % 2 == 0) ? 2 : 1);                                        \
     constexpr int HO = H_ - KH_ + 1, WO = W_ - KW_ + 1;                                                      \
+    if (mfma & (1 << phase)) {                                                                               \
+      if (phase == 0) sn_conv_fwd_m<KH_, KW_, C_, CO_, W_, HO, WO>(L, s);                                    \
+      else if (phase == 1) sn_conv_wgrad_m<KH_, KW_, C_, CO_, W_, HO, WO>(L, s, part);                       \
+      else sn_conv_dgrad_m<KH_, KW_, C_, CO_, W_, H_, HO, WO>(L, s);                                         \
+      return true;                                                                                           \
+    }                                                                                                        \
     if (phase == 0) sn_conv_fwd_c<CG, KH_, KW_, C_, CO_, W_, HO, WO>(L, s);                                  \
     else if (phase == 1) sn_conv_wgrad_c<CG, KH_, KW_, C_, CO_, W_, HO, WO>(L, s, part);                     \
     else sn_conv_dgrad_c<CG, KH_, KW_, C_, CO_, W_, H_, HO, WO>(L, s);                                       \
@@ -669,7 +818,7 @@ __global__ __launch_bounds__(kSnThreads) void smallnet_step_kernel(SnArgs a) {
   for (int l = 0; l < a.nl; ++l) {
     const SnLayer L = a.L[l];
     if (L.kind == kSnConv) {
-      if (!sn_conv_fast(0, L, s, nullptr)) sn_by_cg(L.Co, [&](auto cg) { sn_conv_fwd<decltype(cg)::value>(L, s); });
+      if (!sn_conv_fast(0, L, s, nullptr, a.mfma)) sn_by_cg(L.Co, [&](auto cg) { sn_conv_fwd<decltype(cg)::value>(L, s); });
     } else if (L.kind == kSnPool) {
       sn_pool_fwd(L, s);
     } else {
@@ -734,11 +883,11 @@ __global__ __launch_bounds__(kSnThreads) void smallnet_step_kernel(SnArgs a) {
   for (int l = a.nl - 1; l >= 0; --l) {
     const SnLayer L = a.L[l];
     if (L.kind == kSnConv) {
-      if (!sn_conv_fast(1, L, s, part))
+      if (!sn_conv_fast(1, L, s, part, a.mfma))
         sn_by_cg(L.Co, [&](auto cg) { sn_conv_wgrad<decltype(cg)::value>(L, s, part); });
       __syncthreads();  // the weight gradient reads the input the input gradient overwrites
       stamp();
-      if (L.need_gin && !sn_conv_fast(2, L, s, nullptr))
+      if (L.need_gin && !sn_conv_fast(2, L, s, nullptr, a.mfma))
         sn_by_cg(L.Co, [&](auto cg) { sn_conv_dgrad<decltype(cg)::value>(L, s); });
     } else if (L.kind == kSnPool) {
       sn_pool_bwd(L, s);
@@ -788,9 +937,6 @@ __device__ __forceinline__ void sn_commit(const SnWgradArgs& a, int e, float gra
   if (a.h.kind == kOptAdam) a.v[e] = v;
 }
 
-__device__ __forceinline__ f32x4 sn_mfma4(float a, float b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
 
 __global__ __launch_bounds__(256) void smallnet_wgrad_kernel(SnWgradArgs a) {
   __shared__ float red[8][33];
@@ -942,6 +1088,11 @@ TDE_API int tde_smallnet_step(const int* layers, int nl, int mode, int B, const 
   a.probs = probs;
   a.probs_softmax = probs_softmax;
   a.stamps = stamps;
+  static const int mfma = [] {
+    const char* e = getenv("TDE_SN_MFMA");   // bit mask of MFMA conv phases; 0 = VALU forms only
+    return e ? atoi(e) : 3;
+  }();
+  a.mfma = mfma;
   smallnet_step_kernel<<<B, kSnThreads, 0, stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;
