@@ -53,15 +53,27 @@ __device__ __forceinline__ void fwd_stage_x(const FwdArgs& a, float* xr, int b0,
   const int W = a.W, H = a.H;
   const int istride = fwd_istride(W);
   const int n4 = nrows * W / 4;  // float4 per image
-  for (int i = threadIdx.x; i < 64 * n4; i += nthreads) {
-    const int bl = i / n4, q = i - bl * n4;
-    float4 v = {0.f, 0.f, 0.f, 0.f};
-    if (b0 + bl < a.B)
-      v = *reinterpret_cast<const float4*>(a.x + (size_t)(b0 + bl) * H * W + (size_t)(2 * py0) * W + q * 4);
-    // istride is only 8-byte aligned (bank padding): two 8-byte LDS writes
-    float2* d2 = reinterpret_cast<float2*>(xr + bl * istride + q * 4);
-    d2[0] = float2{v.x, v.y};
-    d2[1] = float2{v.z, v.w};
+  // all of this thread's row loads are issued before the first LDS store (one round trip)
+  constexpr int kU = 8;
+  for (int i0 = threadIdx.x; i0 < 64 * n4; i0 += kU * nthreads) {
+    float4 v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = i0 + u * nthreads, bl = i / n4, q = i - bl * n4;
+      v[u] = float4{0.f, 0.f, 0.f, 0.f};
+      if (i < 64 * n4 && b0 + bl < a.B)
+        v[u] = *reinterpret_cast<const float4*>(a.x + (size_t)(b0 + bl) * H * W + (size_t)(2 * py0) * W + q * 4);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int i = i0 + u * nthreads, bl = i / n4, q = i - bl * n4;
+      if (i < 64 * n4) {
+        // istride is only 8-byte aligned (bank padding): two 8-byte LDS writes
+        float2* d2 = reinterpret_cast<float2*>(xr + bl * istride + q * 4);
+        d2[0] = float2{v[u].x, v[u].y};
+        d2[1] = float2{v[u].z, v[u].w};
+      }
+    }
   }
 }
 

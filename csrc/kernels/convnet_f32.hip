@@ -65,9 +65,8 @@ __global__ __launch_bounds__(FPW * 256) void convnet32_fwd_kernel(FwdArgs a) {
   const float* W1 = reinterpret_cast<const float*>(a.W1);
   float* Pt = reinterpret_cast<float*>(a.Pt);
 
-  fwd_stage_x(a, xr, b0, py0, nrows, NT);
-  fwd_stage_conv(a, wcs, NT);
-  // B fragments: W1[kp*32 + k][nt*16 + fr] for this lane's 8 k of each position (f32 master, [K][HD])
+  // B fragments first (independent of the staging below, so their round trip overlaps it):
+  // W1[kp*32 + k][nt*16 + fr] for this lane's 8 k of each position (f32 master, [K][HD])
   const int nt = wave & 3;
   float wfr[FPW][8];
 #pragma unroll
@@ -79,6 +78,8 @@ __global__ __launch_bounds__(FPW * 256) void convnet32_fwd_kernel(FwdArgs a) {
       for (int j = 0; j < 4; ++j)
         wfr[ks][4 * i + j] = kp < P ? W1[(size_t)(kp * CC + k8_col(fq, i) + j) * a.ldw1 + nt * 16 + fr] : 0.f;
   }
+  fwd_stage_x(a, xr, b0, py0, nrows, NT);
+  fwd_stage_conv(a, wcs, NT);
   stamp(a.stamps, 1);
   lds_barrier();
   ConvW8 cw;
