@@ -179,9 +179,15 @@ __global__ __launch_bounds__(1024) void convnet32_bwd_kernel(BwdArgs a) {
   const float* W1 = reinterpret_cast<const float*>(a.W1);
   const float* Pt = reinterpret_cast<const float*>(a.Pt);
 
-  head_load_w2(a, hl, tid);
+  // the head weights into registers now, stored to LDS with the chunk operands below: every global load
+  // of the prologue is in flight before the first LDS store (one round trip, not three)
+  const int u2 = tid >> 4, c2 = tid & 15;   // 64 x 16
+  const float w2v = c2 < a.C ? a.W2[u2 * a.C + c2] : 0.f;
+  const float b2v = (tid < 16 && tid < a.C) ? a.b2[tid] : 0.f;
   zero_other_parity(a, tid);
   if (blockIdx.x == gridDim.x - 1) {
+    hl.w2s[u2 * 16 + c2] = w2v;
+    if (tid < 16) hl.b2s[tid] = b2v;
     head_workgroup<MODE>(a, hl, Gs);   // the G area is unused there
     return;
   }
@@ -215,12 +221,9 @@ __global__ __launch_bounds__(1024) void convnet32_bwd_kernel(BwdArgs a) {
     }
   }
 
-  // W1 rows of the position [32][64] f32: loaded once (independent of the image chunk)
-  {
-    const int r = tid >> 5, c = (tid & 31) * 2;
-    const float2 v = *reinterpret_cast<const float2*>(W1 + (size_t)(p * CC + r) * a.ldw1 + c);
-    *reinterpret_cast<float2*>(W1s + r * GS32 + c) = v;
-  }
+  // W1 rows of the position [32][64] f32: loaded once (independent of the image chunk), stored to LDS
+  // after the first chunk's loads are issued
+  const float2 w1v = *reinterpret_cast<const float2*>(W1 + (size_t)(p * CC + (tid >> 5)) * a.ldw1 + (tid & 31) * 2);
 
   for (int b0 = 0; b0 < a.B; b0 += 64) {
     const int nb = min(64, a.B - b0);
@@ -248,6 +251,11 @@ __global__ __launch_bounds__(1024) void convnet32_bwd_kernel(BwdArgs a) {
       if (bb < nb) amv = a.amax[((size_t)p * (CC / 8) + cg) * a.lda + b0 + bb];
     }
     stamp(a.stamps, 1);
+    if (b0 == 0) {
+      hl.w2s[u2 * 16 + c2] = w2v;
+      if (tid < 16) hl.b2s[tid] = b2v;
+      *reinterpret_cast<float2*>(W1s + (tid >> 5) * GS32 + (tid & 31) * 2) = w1v;
+    }
     head_stage(a, hv, b1v, hr, hc4, nb, hl.hs);
     if (tid < 64) hl.labs[tid] = lab;
     {
