@@ -22,7 +22,7 @@ step() {  # name timeout cmd...
 prof() {  # name timeout cmd... : rocprofv3 kernel statistics of a command
   local name=$1 t=$2; shift 2
   rm -rf "$OUT/prof_$name"
-  step "prof_$name" "$t" rocprofv3 --kernel-trace --stats -d "$OUT/prof_$name" -o run -- "$@"
+  step "prof_$name" "$t" rocprofv3 --kernel-trace --stats -d "$OUT/prof_$name" -o run --output-format csv -- "$@"
   local f
   f=$(find "$OUT/prof_$name" -name '*kernel_stats.csv' | head -n 1)
   [ -n "$f" ] && cp "$f" "$OUT/${name}_kernel_stats.csv"
