@@ -161,6 +161,7 @@ struct BwdArgs {
   const float* hpre;                 // [B][HD] f32 Dense(64) pre-activation (this step's parity)
   float* hzero;                      // [B][HD] the other parity buffer, zeroed here
   int hrep; long long hrep_stride;   // hpre replicas (summed on load; all zeroed)
+  float* cpart;                      // deterministic mode: per-workgroup conv-gradient partials (nullable)
   const float* b1; const float* W2; const float* b2; int C; int pre_relu;
   const int* labels;
   float scale;                       // 1 / global batch (Keras AUTO reduction under a strategy)
@@ -268,9 +269,19 @@ __device__ __forceinline__ void zero_other_parity(const BwdArgs& a, int tid) {
   for (int i = beg + tid; i < end; i += 1024) reinterpret_cast<float4*>(a.hzero)[i] = float4{0.f, 0.f, 0.f, 0.f};
 }
 
-// hpre[row][c4..c4+3] summed over the replicas (loads issued together)
+// hpre[row][c4..c4+3] summed over the replicas (loads issued together).  More than 4 replicas: the
+// deterministic mode (TDE_DETERMINISTIC: one replica per forward workgroup, each written by exactly one
+// add into zeros), summed in replica order.
 __device__ __forceinline__ float4 load_hpre(const BwdArgs& a, int row, int c4) {
   constexpr int kMaxRep = 4;
+  if (a.hrep > kMaxRep) {
+    float4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < a.hrep; ++r) {
+      const float4 v = *reinterpret_cast<const float4*>(a.hpre + (size_t)r * a.hrep_stride + (size_t)row * HD + c4);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    return s;
+  }
   float4 v[kMaxRep];
 #pragma unroll
   for (int r = 0; r < kMaxRep; ++r)
@@ -489,7 +500,8 @@ __device__ __forceinline__ void conv_grad_reduce(const BwdArgs& a, const f32x4 a
     float s = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) s += red[((size_t)w * 16 + tap) * CC + c];
-    if (tap < 9) atomicAdd(a.dwc + tap * CC + c, s);
+    if (a.cpart) a.cpart[(size_t)blockIdx.x * 10 * CC + tid] = s;   // deterministic: summed by cgrad_reduce
+    else if (tap < 9) atomicAdd(a.dwc + tap * CC + c, s);
     else if (a.dbc) atomicAdd(a.dbc + c, s);
   }
 }
@@ -566,7 +578,7 @@ inline int fill_bwd(BwdArgs& a, const float* x, const void* amax, int lda, const
     for (int i = 0; i < opt->commit.nr; ++i) total += opt->commit.n[i];
     if (total > 1024) return -5;
   }
-  if (hrep < 1 || hrep > 4 || (hrep > 1 && (hrep_stride < (long long)B * HD || (hrep_stride & 3)))) return -6;
+  if (hrep < 1 || hrep > 1024 || (hrep > 1 && (hrep_stride < (long long)B * HD || (hrep_stride & 3)))) return -6;
   a = BwdArgs{};
   a.x = x;
   a.amax = (const uint64_t*)amax;

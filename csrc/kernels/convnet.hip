@@ -469,11 +469,12 @@ TDE_API int tde_convnet_bwd(const float* x, const void* amax, int lda, const flo
                             const int* labels, float scale, float* metrics, const void* W1r, int ldw1r,
                             const void* Pt, int ldPt, float* dW1, float* dwc, float* dbc, float* dW2, float* db2,
                             float* db1, int B, int H, int W, long long* stamps, const TdeBwdOpt* opt,
-                            hipStream_t stream) {
+                            float* cpart, hipStream_t stream) {
   BwdArgs a;
   const int rc = fill_bwd(a, x, amax, lda, hpre, hzero, hrep, hrep_stride, b1, W2, b2, C, pre_relu, labels, scale,
                           metrics, W1r, ldw1r, Pt, ldPt, dW1, dwc, dbc, dW2, db2, db1, B, H, W, stamps, opt);
   if (rc) return rc;
+  a.cpart = cpart;
   const int P = ((H - 2) / 2) * ((W - 2) / 2);
   static bool attr_set = false;
   if (!attr_set) {
@@ -486,6 +487,22 @@ TDE_API int tde_convnet_bwd(const float* x, const void* amax, int lda, const flo
   if (!opt) convnet_bwd_kernel<0><<<grid, 1024, kBwdLds, stream>>>(a);
   else if (opt->kind == kOptSGD) convnet_bwd_kernel<1><<<grid, 1024, kBwdLds, stream>>>(a);
   else convnet_bwd_kernel<2><<<grid, 1024, kBwdLds, stream>>>(a);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+// Deterministic mode (TDE_DETERMINISTIC): dwc / dbc += the backward's per-workgroup conv-gradient
+// partials cpart [nwg][10 * 32], summed in workgroup order.
+__global__ void __launch_bounds__(10 * CC) cgrad_reduce_kernel(const float* cpart, int nwg, float* dwc, float* dbc) {
+  const int i = threadIdx.x;
+  float s = 0.f;
+  for (int w = 0; w < nwg; ++w) s += cpart[(size_t)w * 10 * CC + i];
+  if (i < 9 * CC) dwc[i] += s;
+  else if (dbc) dbc[i - 9 * CC] += s;
+}
+TDE_API int tde_convnet_cgrad_reduce(const float* cpart, int nwg, float* dwc, float* dbc, hipStream_t stream) {
+  if (!cpart || !dwc || nwg < 1) return -1;
+  cgrad_reduce_kernel<<<1, 10 * CC, 0, stream>>>(cpart, nwg, dwc, dbc);
   TDE_LAUNCH_CHECK();
   return 0;
 }

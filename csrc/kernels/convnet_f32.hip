@@ -398,13 +398,14 @@ TDE_API int tde_convnet_bwd_f32(const float* x, const void* amax, int lda, const
                                 int C, int pre_relu, const int* labels, float scale, float* metrics, const float* W1,
                                 int ldw1, const float* Pt, int ldPt, float* dW1, float* dwc, float* dbc, float* dW2,
                                 float* db2, float* db1, int B, int H, int W, long long* stamps, const TdeBwdOpt* opt,
-                                hipStream_t stream) {
+                                float* cpart, hipStream_t stream) {
   if (ldw1 != HD || ((uintptr_t)W1 & 15) || ((uintptr_t)Pt & 7)) return -1;
   if (opt && opt->w + opt->off_w1 != W1) return -3;   // the update is applied to the rows it reads
   BwdArgs a;
   const int rc = fill_bwd(a, x, amax, lda, hpre, hzero, hrep, hrep_stride, b1, W2, b2, C, pre_relu, labels, scale,
                           metrics, W1, ldw1, Pt, ldPt, dW1, dwc, dbc, dW2, db2, db1, B, H, W, stamps, opt);
   if (rc) return rc;
+  a.cpart = cpart;
   a.w1r_out = nullptr;
   a.w1c_out = nullptr;
   const int P = ((H - 2) / 2) * ((W - 2) / 2);

@@ -220,7 +220,7 @@ def convnet_fwd(x, wc, bc, W1, hpre, Pt=None, amax=None, stamps=None, *, opt: St
 
 
 def convnet_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, metrics, W1row, Pt, dW1, dwc, dbc,
-                dW2=None, db2=None, db1=None, B=None, stamps=None, opt: BwdOpt | None = None):
+                dW2=None, db2=None, db1=None, B=None, stamps=None, opt: BwdOpt | None = None, cpart=None):
     """Trunk backward with the classifier head fused in: from this step's Dense(64) pre-activation
     ``hpre`` [B, 64] (f32) every workgroup recomputes the head (loss, dlogits, Dense(64) input gradient)
     and runs the trunk backward; ``hzero`` (the other parity buffer) is zeroed for the next forward.
@@ -228,7 +228,9 @@ def convnet_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, me
     Precision follows ``W1row``: the bf16 row-major shadow (bf16 form) or the f32 master kernel
     (float32 form; ``Pt`` f32, and in the fused step ``W1row`` is the memory ``opt`` updates).
     Plain (``opt`` None): dW1 stored, conv grads atomically added, dW2 / db2 / db1 added, metrics
-    accumulated.  ``opt`` (fused step): the updates are applied instead (see ``BwdOpt``)."""
+    accumulated.  ``opt`` (fused step): the updates are applied instead (see ``BwdOpt``).
+    ``cpart`` (deterministic mode): the conv gradients are stored per workgroup there instead of added
+    atomically; ``convnet_cgrad_reduce`` sums them in order."""
     B = x.shape[0] if B is None else B
     H, W = x.shape[1], x.shape[2]
     Kf = ((H - 2) // 2) * ((W - 2) // 2) * 32
@@ -241,7 +243,7 @@ def convnet_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, me
     _req(Pt.stride(0) >= B and Pt.stride(0) % 8 == 0, "convnet_bwd: Pt ld")
     _req(amax.dtype == torch.int64 and amax.shape[:2] == (Kf // 32, 4) and amax.shape[-1] >= B, "convnet_bwd: amax")
     hp = hpre if hpre.dim() == 3 else hpre.unsqueeze(0)
-    _req(hp.shape[0] <= 4 and hp.shape[1] >= B and hp.shape[2] == 64 and hpre.is_contiguous()
+    _req(hp.shape[0] <= 1024 and hp.shape[1] >= B and hp.shape[2] == 64 and hpre.is_contiguous()
          and hzero.shape == hpre.shape and hzero.is_contiguous(), "convnet_bwd: hpre / hzero")
     _req(labels.dtype == torch.int32 and labels.numel() >= B, "convnet_bwd: int32 labels")
     _req(W2.is_contiguous() and b2.numel() == C and (b1 is None or b1.numel() == 64), "convnet_bwd: head variables")
@@ -250,8 +252,14 @@ def convnet_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, me
             _P(b1), _P(W2), _P(b2), C,
             int(pre_relu), _P(labels), float(scale), _P(metrics), _P(W1row), W1row.stride(0),
             _P(Pt), Pt.stride(0), _P(dW1), _P(dwc), _P(dbc), _P(dW2), _P(db2), _P(db1), B, H,
-            W, _P(stamps), _ct.byref(opt) if opt is not None else None, _s())
+            W, _P(stamps), _ct.byref(opt) if opt is not None else None, _P(cpart), _s())
     N.check(rc, "tde_convnet_bwd_f32" if f32 else "tde_convnet_bwd")
+
+
+def convnet_cgrad_reduce(cpart, nwg, dwc, dbc):
+    """Deterministic mode: dwc / dbc += the backward's per-workgroup conv-gradient partials, in order."""
+    _req(cpart.dtype == torch.float32 and cpart.numel() >= nwg * 320, "convnet_cgrad_reduce: cpart")
+    N.check(N.hip().tde_convnet_cgrad_reduce(_P(cpart), int(nwg), _P(dwc), _P(dbc), _s()), "tde_convnet_cgrad_reduce")
 
 
 def noop(blocks=1, threads=64):

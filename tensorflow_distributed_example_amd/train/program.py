@@ -336,6 +336,16 @@ class ConvNetPlan(ReplicaPlan):
         # Dense(64) pre-activation: two training buffers by step parity + one for eval / predict
         # (training buffers: hrep replicas each, so the forward's ~85 split-K adders per address spread out)
         self.hrep = max(1, min(4, int(os.environ.get("TDE_CONVNET_HREP", "4"))))
+        # TDE_DETERMINISTIC=1 (debugging): one pre-activation replica per forward workgroup (each address
+        # receives exactly one add, into zeros; the consumer sums the replicas in order) and the conv
+        # gradients as per-workgroup partials summed in order by an extra launch: bitwise-reproducible
+        # training steps at the cost of 2.8 MB of replicas and one launch per step
+        self.det = os.environ.get("TDE_DETERMINISTIC", "0") not in ("", "0")
+        P_ = ((H - 2) // 2) * ((W - 2) // 2)
+        if self.det:
+            self.hrep = P_
+        self.cpart = torch.zeros((P_ + 1) * 320, dtype=torch.float32, device=dev) if self.det else None
+        self.n_cpart = P_
         self.hpre2 = torch.zeros(2, self.hrep, B, self.Hd, dtype=torch.float32, device=dev)
         self.hpre = torch.zeros(B, self.Hd, dtype=torch.float32, device=dev)
         self.parity = 0
@@ -499,7 +509,9 @@ class ConvNetPlan(ReplicaPlan):
         K.convnet_bwd(x, self.amax, self.hpre2[q], self.hpre2[1 - q], self._v("b1"), self._v("w2"), self._v("b2"), y,
                       scale=self.scale, pre_relu=self.pre_relu, metrics=self.metrics, W1row=self.W1row, Pt=self.Pt,
                       dW1=self._g("w1"), dwc=dwc, dbc=dbc, dW2=self._g("w2"), db2=self._g("b2"), db1=self._g("b1"),
-                      B=B, opt=self._bopt[q] if local else None)
+                      B=B, opt=self._bopt[q] if local else None, cpart=self.cpart)
+        if self.det:
+            K.convnet_cgrad_reduce(self.cpart, self.n_cpart, dwc, dbc)
         self.parity = 1 - q
 
     def apply(self):

@@ -259,3 +259,43 @@ def test_fp32_fit_matches_reference_executor(monkeypatch):
         rel = np.linalg.norm((a - w) - (b - w)) / (np.linalg.norm(b - w) + 1e-12)
         assert rel < 1e-4, (name, rel)
     assert abs(hf.history["loss"][0] - hr.history["loss"][0]) < 1e-5
+
+
+@pytest.mark.parametrize("policy", ["float32", "mixed_bfloat16"])
+def test_deterministic_mode_is_bitwise_reproducible(policy, monkeypatch):
+    """TDE_DETERMINISTIC=1: one pre-activation replica per forward workgroup (single adds into zeros,
+    summed in order) and the conv gradients as ordered per-workgroup partials -> two independent runs of
+    the fused MNIST-CNN step (hipGraph executions, fused optimizer) give bit-identical weights; the result
+    matches the default (atomic split-K) mode to fp32 summation-order noise."""
+    import tensorflow_distributed_example_amd as tde
+    torch.manual_seed(0)
+    xs = torch.rand(3, 4, 64, 28, 28, 1, device="cuda")
+    ys = torch.randint(0, 10, (3, 4, 64), device="cuda").to(torch.int32)
+
+    def run():
+        tde.backend.clear_session()
+        tde.backend.set_global_policy(policy)
+        tde.backend.set_random_seed(5)
+        m = tde.zoo.mnist_cnn()
+        m.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True),
+                  optimizer=tde.optimizers.SGD(0.05, momentum=0.9), metrics=["accuracy"], steps_per_execution=4)
+        prog = m._program("train", 64)
+        assert prog.plan_kind == "fused_convnet" and prog.use_graph
+        for e in range(3):
+            prog.stage([(xs[e], ys[e])])
+            prog.run()
+        prog.sync()
+        return prog.plans[0].store.w.clone(), prog.plans[0].det
+
+    try:
+        monkeypatch.setenv("TDE_DETERMINISTIC", "1")
+        a, det_a = run()
+        b, det_b = run()
+        monkeypatch.setenv("TDE_DETERMINISTIC", "0")
+        c, det_c = run()
+    finally:
+        tde.backend.set_global_policy("float32")
+    assert det_a and det_b and not det_c
+    assert torch.equal(a, b), float((a - b).abs().max())
+    tol = 1e-4 if policy == "float32" else 2e-2
+    assert float((a - c).abs().max()) <= tol * float(c.abs().max()), float((a - c).abs().max())
