@@ -550,38 +550,51 @@ __device__ void sn_conv_wgrad_m(const SnLayer L, float* s, float* part) {
 
 template <int KH, int KW, int C, int Co, int Win, int Hin, int Ho, int Wo>
 __device__ void sn_conv_dgrad_m(const SnLayer L, float* s) {
+  // two M tiles per item share every B fragment (the weights depend only on k and ci): half the weight
+  // reads per MFMA and two independent accumulator chains per wave
   constexpr int Q = Hin * Win, K = KH * KW * Co, KS = (K + 3) / 4, MT = (Q + 15) / 16, NT = (C + 15) / 16;
+  constexpr int MP = (MT + 1) / 2;
   float* in = s + L.in;
   const float* dz = s + L.out;
   const float* wl = s + L.wl;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, fr = lane & 15, fq = lane >> 4;
-  for (int item = wave; item < MT * NT; item += kSnWaves) {
-    const int mt = item / NT, nt = item - mt * NT;
-    const int q = min(mt * 16 + fr, Q - 1), ih = q / Win, iw = q - ih * Win;
+  for (int item = wave; item < MP * NT; item += kSnWaves) {
+    const int mp = item / NT, nt = item - mp * NT;
+    int ih[2], iw[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int q = min((2 * mp + h) * 16 + fr, Q - 1);
+      ih[h] = q / Win;
+      iw[h] = q - ih[h] * Win;
+    }
     const int ci = nt * 16 + fr;
     const bool cok = ci < C;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll 1
     for (int ks = 0; ks < KS; ++ks) {
       const int k = 4 * ks + fq, kc = min(k, K - 1);
       const int tap = kc / Co, co = kc - tap * Co, kh = tap / KW, kw = tap - kh * KW;
-      const int oh = ih - kh, ow = iw - kw;
-      const bool ok = k < K && (unsigned)oh < (unsigned)Ho && (unsigned)ow < (unsigned)Wo;
-      const float av = ok ? dz[(oh * Wo + ow) * Co + co] : 0.f;
       const float bv = (k < K && cok) ? wl[(tap * C + min(ci, C - 1)) * Co + co] : 0.f;
-      acc = sn_mfma4(av, bv, acc);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int oh = ih[h] - kh, ow = iw[h] - kw;
+        const bool ok = k < K && (unsigned)oh < (unsigned)Ho && (unsigned)ow < (unsigned)Wo;
+        acc[h] = sn_mfma4(ok ? dz[(oh * Wo + ow) * Co + co] : 0.f, bv, acc[h]);
+      }
     }
     if (cok) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int qr = mt * 16 + 4 * fq + i;
-        if (qr < Q) {
-          const int e = qr * C + ci;
-          float v = acc[i];
-          if (L.mask_in && !(in[e] > 0.f)) v = 0.f;
-          in[e] = v;
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int qr = (2 * mp + h) * 16 + 4 * fq + i;
+          if (qr < Q) {
+            const int e = qr * C + ci;
+            float v = acc[h][i];
+            if (L.mask_in && !(in[e] > 0.f)) v = 0.f;
+            in[e] = v;
+          }
         }
-      }
     }
   }
 }

@@ -51,6 +51,7 @@ for s in "$@"; do
     b_mlp) step b_mlp 300 python bench.py --model mnist_mlp --steps 800 --warmup 64 ;;
     b_lenet5_m3) step b_lenet5_m3 300 env TDE_SN_MFMA=3 python bench.py --model lenet5 --steps 800 --warmup 64 ;;
     b_lenet5_m7) step b_lenet5_m7 300 env TDE_SN_MFMA=7 python bench.py --model lenet5 --steps 800 --warmup 64 ;;
+    t_smallnet_m7) step t_smallnet_m7 300 env TDE_SN_MFMA=7 $PYT tests/test_smallnet_gpu.py ;;
     b_lenet5_m0) step b_lenet5_m0 300 env TDE_SN_MFMA=0 python bench.py --model lenet5 --steps 800 --warmup 64 ;;
     b_ps) step b_ps 300 python -m tensorflow_distributed_example_amd.launch --ps 1 --master 1 --workers 1 --timeout 280 bench/ps_throughput.py --max-steps 3000 --warm 200 ;;
     b_ps_legacy) step b_ps_legacy 300 env TDE_PS_FLAT=0 python -m tensorflow_distributed_example_amd.launch --ps 1 --master 1 --workers 1 --timeout 280 bench/ps_throughput.py --max-steps 3000 --warm 200 ;;
