@@ -93,6 +93,28 @@ __device__ __forceinline__ int wg_id() {
   return (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
 }
 
+// red[q] = sum over p < np of red[p * Q + q] (q < Q), in a fixed order with a short dependent chain:
+// G groups of threads each sum every G-th part, then one thread per q sums the G group sums.  Ends with
+// a barrier.  (A single thread per q walking all np parts in LDS was a ~85-long serial chain of LDS
+// reads and f64 adds: ~3 us of every conv / dense launch's prologue.)
+__device__ void parts_to_slots(double* red, int np, int Q) {
+  const int t = threadIdx.x, G = min(16, (int)blockDim.x / Q);
+  double S = 0.0;
+  if (t < G * Q) {
+    const int g = t / Q, q = t - g * Q;
+    for (int p = g; p < np; p += G) S += red[p * Q + q];
+  }
+  lds_barrier();
+  if (t < G * Q) red[t] = S;
+  lds_barrier();
+  double T = 0.0;
+  if (t < Q)
+    for (int g = 0; g < G; ++g) T += red[g * Q + t];
+  lds_barrier();
+  if (t < Q) red[t] = T;
+  lds_barrier();
+}
+
 // red[q] = sum over the npart partials acc[p][q], q < Q (Q <= blockDim), in a fixed order (thread
 // (part, q) sums p = part, part + np, ...; then the parts in order); red: blockDim doubles of LDS.
 // Ends with a barrier.
@@ -113,12 +135,7 @@ __device__ void slot_sums(const double* acc, int npart, int Q, double* red) {
     red[t] = s;
   }
   lds_barrier();
-  double S = 0.0;
-  if (t < Q)
-    for (int p = 0; p < np; ++p) S += red[p * Q + t];
-  lds_barrier();
-  if (t < Q) red[t] = S;
-  lds_barrier();
+  parts_to_slots(red, np, Q);
 }
 
 // Per-channel scale / shift of the forward BN (y = x*sc + sh, then ReLU) and mean / rstd into LDS
@@ -1053,9 +1070,9 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
     stin[3 * C + ti] = irs;
   }
   lds_barrier();
+  parts_to_slots(red, np, Q);
   if (tid < Q) {
-    double S = 0.0;
-    for (int p = 0; p < np; ++p) S += red[p * Q + tid];
+    const double S = red[tid];
     kks[tid] = (float)S;
     if (b == 0 && !dg) {
       if (tid < Co && a.bb.dbeta) a.bb.dbeta[tid] = (float)S;
