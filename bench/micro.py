@@ -138,6 +138,12 @@ def main():
         f(stamps=st)
         torch.cuda.synchronize()
         out[f"stamps_{name}"] = stamps_summary(st.view(-1, 8), ns)
+        rows = st.view(-1, 8).cpu().numpy().astype(np.float64)
+        head = rows[rows[:, 7] > 0]
+        if len(head):   # the backward's head workgroup: start and end, on the trunk's clock
+            t0 = rows[rows[:, 0] > 0, 0].min()
+            out[f"stamps_{name}_head_wg"] = {"start": round((head[0, 0] - t0) * 0.01, 2),
+                                            "end": round((head[0, 7] - t0) * 0.01, 2)}
     print(json.dumps(out, indent=1))
 
 

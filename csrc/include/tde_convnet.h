@@ -465,6 +465,7 @@ __device__ __forceinline__ void head_workgroup(const BwdArgs& a, const HeadLds& 
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       if (gdst[i]) *gdst[i] += gv[i];
+    stamp(a.stamps, 7);
     return;
   }
   const float lr_t = opt_lr_t(a.h, t_it);
@@ -484,6 +485,7 @@ __device__ __forceinline__ void head_workgroup(const BwdArgs& a, const HeadLds& 
     if (a.pend_set) *a.pend_set = 1;
     if (a.iter_prev) *a.iter_prev = t_it;
   }
+  stamp(a.stamps, 7);   // diagnostics: the head workgroup's end (micro.py)
 }
 
 // Reduces the routing accumulators (conv weight / bias gradients: [tap 0..8 | bias 9][CC]) of the
