@@ -342,8 +342,14 @@ class BnCnnPlan(ReplicaPlan):
     def supports_step_mode(self, mode):
         if mode == "plain":
             return True
+        if mode == "xgmi":   # data parallel: the xGMI all-reduce applies the update to the f32 weights
+            return self.optimizer is not None and self.device.type == "cuda"
         return mode == "local" and self.optimizer is not None and self.device.type == "cuda" and \
             self._bn_segs is not None
+
+    def xg_apply_spec(self):
+        from .program import f32_xg_apply_spec
+        return f32_xg_apply_spec(self)
 
     def set_step_mode(self, mode):
         super().set_step_mode(mode)

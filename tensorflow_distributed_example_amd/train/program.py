@@ -264,6 +264,19 @@ class OptimizerKernel:
         N.check(rc, "tde_optim_apply")
 
 
+def f32_xg_apply_spec(plan):
+    """``XgApply`` of a plan whose weights are the f32 master store only (no bf16 shadows): the xGMI
+    all-reduce applies the optimizer to ``store.w`` / slots (step mode "xgmi")."""
+    from ..ops import kernels as K
+    st, opt = plan.store, plan.optimizer
+    sl = opt.slot_names()
+    m = st.slot(sl[0]) if sl else None
+    v = st.slot(sl[1]) if len(sl) > 1 else None
+    hp = opt.hparams()
+    return K.XgApply(opt.kind_id, float(opt.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"],
+                     K._P(st.w), K._P(m), K._P(v), K._P(plan.iterations), None, 0, 0, None, 0, 0)
+
+
 def match_convnet(model, loss):
     """Pattern of the DWK/TF2M small CNN: Conv2D(3x3,relu,bias) on 1 channel ·
     MaxPooling2D(2) · Flatten · Dense(bias[,relu]) · Dense(bias[,softmax]) + SCCE."""

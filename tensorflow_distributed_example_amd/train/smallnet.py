@@ -224,7 +224,13 @@ class SmallNetPlan(ReplicaPlan):
 
     # ------------------------------------------------------------------ step modes
     def supports_step_mode(self, mode):
-        return mode == "plain" or (mode == "local" and self.optimizer is not None and self.device.type == "cuda")
+        # "xgmi": data parallel, the xGMI all-reduce applies the update to the f32 weights
+        return mode == "plain" or (mode in ("local", "xgmi") and self.optimizer is not None and
+                                   self.device.type == "cuda")
+
+    def xg_apply_spec(self):
+        from .program import f32_xg_apply_spec
+        return f32_xg_apply_spec(self)
 
     def _step(self, mode, x, y, B, probs=None):
         if B > self.B:

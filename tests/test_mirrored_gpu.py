@@ -182,3 +182,25 @@ def test_n_replicas_equal_one_replica_at_the_same_global_batch(layout, tmp_path)
     assert "replicas_identical=True" in line and "graph=True" in line and "step_mode=xgmi" in line, (layout, line)
     for k in one:
         np.testing.assert_allclose(w[k], one[k], rtol=1e-4, atol=1e-5, err_msg=f"{layout}: {k}")
+
+
+@pytest.mark.parametrize("model", ["mnist_bn_cnn", "lenet5", "mnist_mlp"])
+def test_mirrored_fused_plans_apply_the_update_in_the_allreduce(model):
+    """The BN-CNN and small-net plans (f32 weights, no shadows) hand the optimizer to the xGMI all-reduce
+    (step mode "xgmi"): no separate optimizer launch under data parallelism, replicas bit-identical."""
+    res, out = _bench(["--strategy", "mirrored", "--devices", "0,0", "--model", model, "--steps", "32",
+                       "--warmup", "16"])
+    c = res["config"]
+    assert c["allreduce"] == "xgmi_peer" and c["hipgraph"] is True, res
+    assert c["optimizer_placement"] == "allreduce", res
+    assert "replicas_identical=True" in out, out[-3000:]
+
+
+def test_mlp_two_replicas_equal_one_replica(tmp_path):
+    """The small-net plan (MLP, no BatchNorm) under Mirrored 2 replicas with the update fused into the
+    all-reduce trains like one replica at the same global batch."""
+    one, _ = _equiv(tmp_path, "mlp1", ["--strategy", "single", "--model", "mnist_mlp"])
+    two, line = _equiv(tmp_path, "mlp2", ["--strategy", "mirrored", "--devices", "0,0", "--model", "mnist_mlp"])
+    assert "replicas_identical=True" in line and "step_mode=xgmi" in line, line
+    for k in one:
+        np.testing.assert_allclose(two[k], one[k], rtol=1e-4, atol=1e-5, err_msg=k)
