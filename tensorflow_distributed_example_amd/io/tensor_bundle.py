@@ -21,6 +21,7 @@ _DT = {np.dtype("float32"): 1, np.dtype("float64"): 2, np.dtype("int32"): 3, np.
        np.dtype("int64"): 9, np.dtype("float16"): 19}
 _DT_INV = {v: k for k, v in _DT.items()}
 DT_BFLOAT16 = 14
+DT_STRING = 7
 
 N.register_host({
     "tde_bundle_write": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_int),
@@ -40,12 +41,16 @@ def write_bundle(prefix: str, tensors: dict):
     lib = N.host()
     Path(prefix).parent.mkdir(parents=True, exist_ok=True)
     names = list(tensors)
-    arrs = [np.require(np.asarray(tensors[n]), requirements="C") for n in names]
+    # a ``bytes`` value is a scalar DT_STRING tensor (TensorBundle string encoding, io/object_graph.py)
+    strs = {n for n in names if isinstance(tensors[n], (bytes, bytearray))}
+    from .object_graph import encode_string_tensor
+    arrs = [np.frombuffer(encode_string_tensor([tensors[n]]), dtype=np.uint8) if n in strs else
+            np.require(np.asarray(tensors[n]), requirements="C") for n in names]
     n = len(names)
     c_names = (C.c_char_p * n)(*[s.encode() for s in names])
-    dtypes = (C.c_int * n)(*[_DT[a.dtype] for a in arrs])
-    ranks = (C.c_int * n)(*[a.ndim for a in arrs])
-    flat = [d for a in arrs for d in a.shape]
+    dtypes = (C.c_int * n)(*[DT_STRING if nm in strs else _DT[a.dtype] for nm, a in zip(names, arrs)])
+    ranks = (C.c_int * n)(*[0 if nm in strs else a.ndim for nm, a in zip(names, arrs)])
+    flat = [d for nm, a in zip(names, arrs) if nm not in strs for d in a.shape]
     shapes = (C.c_longlong * max(len(flat), 1))(*flat)
     datas = (C.c_void_p * n)(*[a.ctypes.data for a in arrs])
     nbytes = (C.c_longlong * n)(*[a.nbytes for a in arrs])
@@ -80,6 +85,14 @@ def read_bundle(prefix: str) -> dict:
     out = {}
     try:
         for name, shape, dt, nb in entries:
+            if dt == DT_STRING and not shape:
+                raw = (C.c_char * nb)()
+                rc = lib.tde_bundle_read(h, name.encode(), raw, nb)
+                if rc != 0:
+                    raise IOError(f"{prefix}: reading {name} failed ({'crc mismatch' if rc == -3 else rc})")
+                from .object_graph import decode_string_tensor
+                out[name] = decode_string_tensor(bytes(raw))[0]
+                continue
             if dt not in _DT_INV:
                 continue
             a = np.empty(shape, dtype=_DT_INV[dt])
