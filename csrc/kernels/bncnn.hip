@@ -1275,6 +1275,8 @@ struct ReduceArgs {
   long long len[kMaxRed];
   int cnt[kMaxRed];            // partials of the segment
   int blk0[kMaxRed + 1];       // first workgroup of the segment
+  int wide[kMaxRed];           // few partials (<= kWideCnt), len % 4 == 0: 1024 elements per workgroup,
+                               // a float4 per thread summed over all partials (16x fewer workgroups)
   int apply;
   float* g;                    // the flat bucket (segment offsets = out[j] - g)
   float *w, *m, *v;
@@ -1282,11 +1284,50 @@ struct ReduceArgs {
   OptHyper h;
   long long* stamps;
 };
+__device__ __forceinline__ void reduce_commit(const ReduceArgs& a, int j, long long e, float gs, long long t, bool inplace) {
+  if (!a.apply) {
+    a.out[j][e] = gs;
+    return;
+  }
+  const long long f = (a.out[j] - a.g) + e;
+  float m = a.h.kind != kOptSGD ? a.m[f] : 0.f, vv = a.h.kind == kOptAdam ? a.v[f] : 0.f;
+  a.w[f] = opt_step(a.h, opt_lr_t(a.h, t), a.w[f], gs, m, vv);
+  if (a.h.kind != kOptSGD) a.m[f] = m;
+  if (a.h.kind == kOptAdam) a.v[f] = vv;
+  if (inplace) a.out[j][e] = 0.f;
+}
+
+constexpr int kWideCnt = 8;
+
 __global__ __launch_bounds__(NTH) void reduce_kernel(ReduceArgs a) {
   __shared__ float red[4][64];
   const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
   int j = 0;
   while (j + 1 < a.n && (int)blockIdx.x >= a.blk0[j + 1]) ++j;
+  if (a.wide[j]) {
+    // a float4 of 4 consecutive elements per thread, every partial summed in order by that thread
+    const long long len = a.len[j], e0 = ((long long)(blockIdx.x - a.blk0[j]) * NTH + threadIdx.x) * 4;
+    if (e0 >= len) return;
+    const int cnt = a.cnt[j];
+    const float* p = a.part[j];
+    const long long t = a.apply && a.h.kind == kOptAdam ? *a.iterations : 0;
+    float4 v[kWideCnt];
+#pragma unroll
+    for (int u = 0; u < kWideCnt; ++u)
+      if (u < cnt) v[u] = *reinterpret_cast<const float4*>(p + (size_t)u * len + e0);
+    float4 s = v[0];
+#pragma unroll
+    for (int u = 1; u < kWideCnt; ++u)
+      if (u < cnt) {
+        s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w;
+      }
+    const bool inplace = p == a.out[j];
+    reduce_commit(a, j, e0 + 0, s.x, t, inplace);
+    reduce_commit(a, j, e0 + 1, s.y, t, inplace);
+    reduce_commit(a, j, e0 + 2, s.z, t, inplace);
+    reduce_commit(a, j, e0 + 3, s.w, t, inplace);
+    return;
+  }
   const long long len = a.len[j];
   const long long e = (long long)(blockIdx.x - a.blk0[j]) * 64 + l;
   const int cnt = a.cnt[j];
@@ -1305,19 +1346,7 @@ __global__ __launch_bounds__(NTH) void reduce_kernel(ReduceArgs a) {
   }
   red[q][l] = s;
   __syncthreads();
-  if (q == 0 && e < len) {
-    const float gs = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
-    if (!a.apply) {
-      a.out[j][e] = gs;
-    } else {
-      const long long f = (a.out[j] - a.g) + e;
-      float m = a.h.kind != kOptSGD ? a.m[f] : 0.f, vv = a.h.kind == kOptAdam ? a.v[f] : 0.f;
-      a.w[f] = opt_step(a.h, opt_lr_t(a.h, t), a.w[f], gs, m, vv);
-      if (a.h.kind != kOptSGD) a.m[f] = m;
-      if (a.h.kind == kOptAdam) a.v[f] = vv;
-      if (p == a.out[j]) a.out[j][e] = 0.f;
-    }
-  }
+  if (q == 0 && e < len) reduce_commit(a, j, e, (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]), t, p == a.out[j]);
 }
 
 }  // namespace bncnn
@@ -1676,7 +1705,8 @@ TDE_API int tde_bncnn_reduce(int n, const int* cnt, const float* const* part, fl
     a.len[j] = len[j];
     a.cnt[j] = cnt[j];
     a.blk0[j] = blocks;
-    blocks += (int)((len[j] + 63) / 64);
+    a.wide[j] = cnt[j] <= kWideCnt && (len[j] & 3) == 0 && (((uintptr_t)part[j] | (uintptr_t)out[j]) & 15) == 0;
+    blocks += a.wide[j] ? (int)((len[j] + 4 * NTH - 1) / (4 * NTH)) : (int)((len[j] + 63) / 64);
   }
   a.blk0[n] = blocks;
   reduce_kernel<<<blocks, NTH, 0, stream>>>(a);
