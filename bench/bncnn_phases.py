@@ -41,20 +41,8 @@ plan.train_step(x, y)
 lib.tde_bncnn_stamps(None, 0)
 torch.cuda.synchronize()
 st = buf.view(n_launch, 8192, 8).cpu().numpy()
-names = [f"conv_fwd{i}" for i in range(len(plan.blocks))] + ["dense_fwd", "head", "dense_bwd"]
-names += [f"conv_bwd{i}" for i in reversed(range(len(plan.blocks)))] + ["reduce"]
-t0 = None
-for li, name in enumerate(names):
-    s = st[li]
-    used = s[:, 0] > 0
-    if not used.any():
-        print(json.dumps({"launch": name, "stamped": False}))
-        continue
-    s = s[used]
-    if t0 is None:
-        t0 = s[:, 0].min()
-    out = {"launch": name, "wgs": int(used.sum()),
-           "first_start_us": round((s[:, 0].min() - t0) / 100.0, 2),
+def summary(s, t0):
+    out = {"first_start_us": round((s[:, 0].min() - t0) / 100.0, 2),
            "last_start_us": round((s[:, 0].max() - t0) / 100.0, 2)}
     last = s[:, 0].copy()
     ends = s[:, 0].copy()
@@ -70,4 +58,25 @@ for li, name in enumerate(names):
         ends = np.maximum(ends, np.where(ok, col, 0))
     out["last_end_us"] = round((ends.max() - t0) / 100.0, 2)
     out["wg_med_us"] = round(float(np.median(ends - s[:, 0])) / 100.0, 2)
+    return out
+
+
+names = [f"conv_fwd{i}" for i in range(len(plan.blocks))] + ["dense_fwd", "head", "dense_bwd"]
+names += [f"conv_bwd{i}" for i in reversed(range(len(plan.blocks)))] + ["reduce"]
+t0 = None
+for li, name in enumerate(names):
+    s = st[li]
+    used = s[:, 0] > 0
+    if not used.any():
+        print(json.dumps({"launch": name, "stamped": False}))
+        continue
+    s = s[used]
+    if t0 is None:
+        t0 = s[:, 0].min()
+    out = {"launch": name, "wgs": int(used.sum())}
+    out.update(summary(s, t0))
+    if name.startswith("conv_bwd") and len(s) == 2 * B:
+        # rows [0, B): the weight-gradient role (blockIdx.y = 0), [B, 2B): the input-gradient role
+        out["wgrad"] = summary(s[:B], t0)
+        out["dgrad"] = summary(s[B:], t0)
     print(json.dumps(out))

@@ -925,7 +925,8 @@ struct ConvBwdP {
   int nth, ntw, Kd, Kdp, ncls, NC, NP, nnt, obh0, obw0, Nbw, Md, mtd, ksd, spd, n_dg_items;
   // weight gradient
   int wg_tiles, wg_split, wg_spp, Kw16, n_wg_items;
-  Dv dC, dCo, dW, dWo, dWd, dWp, dkw, dntw, dNbw, dNP;
+  int wgather;   // the class-stacked weights fit the registers: gathered from w in the load batch
+  Dv dC, dCo, dW, dWo, dWd, dWp, dkw, dntw, dNbw, dNP, dsh, dsw;
   int o_red, o_cs, o_st, o_stin, o_kk, o_dz, o_role;
   int o_xs, o_kow, o_ptab, o_part;           // weight-gradient role
   int o_xr, o_wb, o_kod, o_partd;            // input-gradient role
@@ -967,8 +968,22 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
     const float* im = a.in + (size_t)b * nimg;
     pf_load(pg, nact, [&](int i) { return gz[i]; });
     pf_load(pz, nact, [&](int i) { return zz[i]; });
-    if (dg) pf_load(pw, nw, [&](int i) { return a.w[i]; });
     pf_load(px, nimg, [&](int i) { return im[i]; });
+    if (dg && P.wgather) {
+      // element i of the class-stacked [Kdp][NP] weights: 0 in the holes (padding rows / columns, taps
+      // past the kernel), else w at HWIO (ky, kx, ci, co) -- gathered here, stored contiguously later
+      pf_load(pw, P.Kdp * P.NP, [&](int i) {
+        const int kk = dq(i, P.dNP), n = i - kk * P.NP;
+        const int t = dq(kk, P.dCo), co = kk - t * Co, jh = dq(t, P.dntw), jw = t - jh * P.ntw;
+        const int cl = dq(n, P.dC), ci = n - cl * C, ry = dq(cl, P.dsw), rx = cl - ry * g.sw;
+        const int ky = ry + g.sh * jh, kx = rx + g.sw * jw;
+        const bool hole = kk >= P.Kd || n >= P.NC || ky >= g.kh || kx >= g.kw;
+        const float v = a.w[hole ? 0 : ((ky * g.kw + kx) * C + ci) * Co + co];
+        return hole ? 0.f : v;
+      });
+    } else if (dg) {
+      pf_load(pw, nw, [&](int i) { return a.w[i]; });
+    }
   }
   // the per-channel constants: partials of this layer's backward sums (fixed-order sum), saved
   // statistics
@@ -1036,12 +1051,12 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
     float* Wb = reinterpret_cast<float*>(sm + P.o_wb);
     int* kod = reinterpret_cast<int*>(sm + P.o_kod);
     // class-stacked weights: zero where no weight lands (padding rows / columns, taps past the kernel)
-    for (int i = tid; i < P.Kdp * P.NP; i += NTB) {
+    for (int i = P.wgather ? P.Kdp * P.NP : tid; i < P.Kdp * P.NP; i += NTB) {
       const int kk = dq(i, P.dNP), n = i - kk * P.NP;
       bool hole = kk >= P.Kd || n >= P.NC;
       if (!hole) {
         const int t = dq(kk, P.dCo), jh = dq(t, P.dntw), jw = t - jh * P.ntw;
-        const int cl = dq(n, P.dC), ry = cl / g.sw, rx = cl - ry * g.sw;
+        const int cl = dq(n, P.dC), ry = dq(cl, P.dsw), rx = cl - ry * g.sw;
         hole = ry + g.sh * jh >= g.kh || rx + g.sw * jw >= g.kw;
       }
       if (hole) Wb[i] = 0.f;
@@ -1106,10 +1121,13 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
       float* Xr = reinterpret_cast<float*>(sm + P.o_xr);
       float* Wb = reinterpret_cast<float*>(sm + P.o_wb);
       pf_store(px, nimg, [&](int i, float v) { Xr[i] = v; });
-      pf_store(pw, nw, [&](int i, float v) {
+      if (P.wgather)
+        pf_store(pw, P.Kdp * P.NP, [&](int i, float v) { Wb[i] = v; });
+      else
+        pf_store(pw, nw, [&](int i, float v) {
         const int t = dq(i, P.dCo), co = i - t * Co, t2 = dq(t, P.dC), ci = t - t2 * C;
         const int ky = dq(t2, P.dkw), kx = t2 - ky * g.kw;
-        const int cl = (ky % g.sh) * g.sw + (kx % g.sw), jh = ky / g.sh, jw = kx / g.sw;
+        const int jh = dq(ky, P.dsh), jw = dq(kx, P.dsw), cl = (ky - jh * g.sh) * g.sw + kx - jw * g.sw;
         Wb[((jh * P.ntw + jw) * Co + co) * P.NP + cl * C + ci] = v;
       });
     }
@@ -1211,7 +1229,7 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
     for (int kp = 1; kp < P.ksd; ++kp) v += *reinterpret_cast<const f32x4*>(partd + ((size_t)(kp * ntile + t) * 64 + lane) * 4);
     const int n = nt * 16 + fr;
     if (n >= P.NC) continue;
-    const int cl = dq(n, P.dC), ci = n - cl * C, ry = cl / g.sw, rx = cl - ry * g.sw;
+    const int cl = dq(n, P.dC), ci = n - cl * C, ry = dq(cl, P.dsw), rx = cl - ry * g.sw;
     double t1 = 0.0, t2 = 0.0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1250,10 +1268,25 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
   }
   lds_barrier();
   if (tid < 2 * C) {
+    // same order as walking w, then the class columns n = c + r*C; the loads of 4 waves are issued as
+    // one batch (a runtime-bound loop here was a 64-long chain of dependent LDS round trips, ~3 us)
     const int j = tid / C, c = tid - j * C;
     double S = 0.0;
-    for (int w = 0; w < 16; ++w)
-      for (int n = c; n < P.NC; n += C) S += cs[(w * 2 + j) * 64 + n];
+#pragma unroll 1
+    for (int w0 = 0; w0 < 16; w0 += 4) {
+      double v[4][kMaxCls];
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+#pragma unroll
+        for (int r = 0; r < kMaxCls; ++r) {
+          const int n = c + r * C;
+          v[w][r] = n < P.NC ? cs[((w0 + w) * 2 + j) * 64 + n] : 0.0;
+        }
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+#pragma unroll
+        for (int r = 0; r < kMaxCls; ++r) S += v[w][r];
+    }
     a.acc_in[(size_t)b * 2 * C + j * C + c] = S;
   }
   stamp(a.stamps, 4);
@@ -1603,6 +1636,9 @@ static int conv_bwd_plan(const Geo& g, int dgrad, ConvBwdP& P) {
   P.dntw = dv(P.ntw);
   P.dNbw = dv(P.Nbw);
   P.dNP = dv(P.NP);
+  P.dsh = dv(g.sh);
+  P.dsw = dv(g.sw);
+  P.wgather = dgrad && P.Kdp * P.NP <= kUW * NTB;
   int o = 0;
   P.o_red = o; o += NTB * 8;
   P.o_cs = o; o += 16 * 2 * 64 * 8;
