@@ -219,6 +219,34 @@ struct Dv {
 };
 __device__ __forceinline__ int dq(int i, Dv v) { return (int)(((float)i + 0.5f) * v.r); }
 
+// Backward conv geometry (see conv_bwd_kernel); the forward also stages the input-gradient weights.
+constexpr int kMaxDgNT = 4;   // input-gradient N tiles: classes x C <= 64
+struct ConvBwdP {
+  Geo g;
+  int K, Mo, Hp, Wp, Hd, Wd, Ph, Pw, zslot, dgrad, nco;
+  // input gradient (depth-to-space)
+  int nth, ntw, Kd, Kdp, ncls, NC, NP, nnt, obh0, obw0, Nbw, Md, mtd, ksd, spd, n_dg_items;
+  // weight gradient
+  int wg_tiles, wg_split, wg_spp, Kw16, n_wg_items;
+  int wgather;   // the class-stacked weights fit the registers (a forward-staged copy can be used)
+  Dv dC, dCo, dW, dWo, dWd, dWp, dkw, dntw, dNbw, dNP, dsh, dsw;
+  int o_red, o_cs, o_st, o_stin, o_kk, o_dz, o_role;
+  int o_xs, o_kow, o_ptab, o_part;           // weight-gradient role
+  int o_xr, o_wb, o_kod, o_partd;            // input-gradient role
+  int lds;
+};
+// Source of element i of the class-stacked [Kdp][NP] input-gradient weights: the HWIO index of
+// (ky, kx, ci, co), or -1 in the holes (padding rows / columns, taps past the kernel).
+__device__ __forceinline__ int wstack_src(const ConvBwdP& P, int i) {
+  const Geo& g = P.g;
+  const int kk = dq(i, P.dNP), n = i - kk * P.NP;
+  const int t = dq(kk, P.dCo), co = kk - t * g.Co, jh = dq(t, P.dntw), jw = t - jh * P.ntw;
+  const int cl = dq(n, P.dC), ci = n - cl * g.C, ry = dq(cl, P.dsw), rx = cl - ry * g.sw;
+  const int ky = ry + g.sh * jh, kx = rx + g.sw * jw;
+  if (kk >= P.Kd || n >= P.NC || ky >= g.kh || kx >= g.kw) return -1;
+  return ((ky * g.kw + kx) * g.C + ci) * g.Co + co;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Forward conv: grid (B, msplit): workgroup (b, h) = image b, output tiles [h * mtw, (h+1) * mtw)
 // (two workgroups per image keep all 256 CUs busy at B = 128).  Work items (16-pixel output tile,
@@ -240,6 +268,8 @@ struct ConvFwdArgs {
   double* acc;               // this layer's BN partial sums [msplit * B][2][Co] (nullable: no statistics)
   long long* stamps;         // diagnostic phase clock (tde_bncnn_stamps), nullable
   long long* inc_iter;       // training, first layer: the step counter this step advances (nullable)
+  float* wstack;             // training, layers with an input gradient: the class-stacked weights of this
+  ConvBwdP sp;               // step's backward (layout of sp), written here once (nullable)
 };
 
 __global__ __launch_bounds__(NTB) void conv_fwd_kernel(ConvFwdArgs a) {
@@ -266,6 +296,16 @@ __global__ __launch_bounds__(NTB) void conv_fwd_kernel(ConvFwdArgs a) {
   Pf<kUW> pw;
   pf_load(pi, nimg, [&](int i) { return img[i]; });
   pf_load(pw, nw, [&](int i) { return a.w[i]; });
+  // this step's class-stacked input-gradient weights (the weights do not change until the step's
+  // optimizer update): element wid * NTB + tid, one per thread of the first workgroups
+  const int wsi = (blockIdx.y * gridDim.x + b) * NTB + tid;
+  const bool wst = a.wstack && wsi < a.sp.Kdp * a.sp.NP;
+  float wsv = 0.f;
+  if (wst) {
+    const int src = wstack_src(a.sp, wsi);
+    wsv = a.w[max(src, 0)];
+    if (src < 0) wsv = 0.f;
+  }
   // LDS the registers do not cover: image border, weight padding, im2col offsets
   for (int i = tid; i < P.Hp * Wp; i += NTB) {
     const int y = dq(i, P.dWp), x = i - y * Wp, iy = y - g.pt, ix = x - g.pl;
@@ -299,6 +339,7 @@ __global__ __launch_bounds__(NTB) void conv_fwd_kernel(ConvFwdArgs a) {
       Ws[k * NTP + co] = v;
     });
   }
+  if (wst) a.wstack[wsi] = wsv;
   lds_barrier();
   stamp(a.stamps, 2);
   // ---- MFMA work items over this workgroup's output tiles
@@ -917,21 +958,6 @@ __global__ __launch_bounds__(NTB) void dense_bwd_kernel(DenseBwdArgs a) {
 //     sh*sw sub-pixel classes, so A = that window [blocks x (jh, jw, co)] and B = the class-stacked
 //     weights [(jh, jw, co) x (class, ci)] -> dA of the whole sh x sw input block per output row;
 //     ReLU mask of the input BN -> g of the previous layer + that BN's backward partial sums
-constexpr int kMaxDgNT = 4;   // input-gradient N tiles: classes x C <= 64
-struct ConvBwdP {
-  Geo g;
-  int K, Mo, Hp, Wp, Hd, Wd, Ph, Pw, zslot, dgrad, nco;
-  // input gradient (depth-to-space)
-  int nth, ntw, Kd, Kdp, ncls, NC, NP, nnt, obh0, obw0, Nbw, Md, mtd, ksd, spd, n_dg_items;
-  // weight gradient
-  int wg_tiles, wg_split, wg_spp, Kw16, n_wg_items;
-  int wgather;   // the class-stacked weights fit the registers: gathered from w in the load batch
-  Dv dC, dCo, dW, dWo, dWd, dWp, dkw, dntw, dNbw, dNP, dsh, dsw;
-  int o_red, o_cs, o_st, o_stin, o_kk, o_dz, o_role;
-  int o_xs, o_kow, o_ptab, o_part;           // weight-gradient role
-  int o_xr, o_wb, o_kod, o_partd;            // input-gradient role
-  int lds;
-};
 struct ConvBwdArgs {
   ConvBwdP p;
   int B;
@@ -940,6 +966,7 @@ struct ConvBwdArgs {
   const float* in; Bn bn_in; float* gin; double* acc_in;             // the input side
   float* dwpart;                     // [B][K][Co]
   long long* stamps;
+  const float* wstack;               // input gradient: the class-stacked [Kdp][NP] weights (nullable)
 };
 
 __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
@@ -969,18 +996,9 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
     pf_load(pg, nact, [&](int i) { return gz[i]; });
     pf_load(pz, nact, [&](int i) { return zz[i]; });
     pf_load(px, nimg, [&](int i) { return im[i]; });
-    if (dg && P.wgather) {
-      // element i of the class-stacked [Kdp][NP] weights: 0 in the holes (padding rows / columns, taps
-      // past the kernel), else w at HWIO (ky, kx, ci, co) -- gathered here, stored contiguously later
-      pf_load(pw, P.Kdp * P.NP, [&](int i) {
-        const int kk = dq(i, P.dNP), n = i - kk * P.NP;
-        const int t = dq(kk, P.dCo), co = kk - t * Co, jh = dq(t, P.dntw), jw = t - jh * P.ntw;
-        const int cl = dq(n, P.dC), ci = n - cl * C, ry = dq(cl, P.dsw), rx = cl - ry * g.sw;
-        const int ky = ry + g.sh * jh, kx = rx + g.sw * jw;
-        const bool hole = kk >= P.Kd || n >= P.NC || ky >= g.kh || kx >= g.kw;
-        const float v = a.w[hole ? 0 : ((ky * g.kw + kx) * C + ci) * Co + co];
-        return hole ? 0.f : v;
-      });
+    if (dg && a.wstack) {
+      // the class-stacked weights this step's forward of the layer staged (conv_fwd wstack): contiguous
+      pf_load(pw, P.Kdp * P.NP, [&](int i) { return a.wstack[i]; });
     } else if (dg) {
       pf_load(pw, nw, [&](int i) { return a.w[i]; });
     }
@@ -1051,7 +1069,7 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
     float* Wb = reinterpret_cast<float*>(sm + P.o_wb);
     int* kod = reinterpret_cast<int*>(sm + P.o_kod);
     // class-stacked weights: zero where no weight lands (padding rows / columns, taps past the kernel)
-    for (int i = P.wgather ? P.Kdp * P.NP : tid; i < P.Kdp * P.NP; i += NTB) {
+    for (int i = a.wstack ? P.Kdp * P.NP : tid; i < P.Kdp * P.NP; i += NTB) {
       const int kk = dq(i, P.dNP), n = i - kk * P.NP;
       bool hole = kk >= P.Kd || n >= P.NC;
       if (!hole) {
@@ -1121,7 +1139,7 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
       float* Xr = reinterpret_cast<float*>(sm + P.o_xr);
       float* Wb = reinterpret_cast<float*>(sm + P.o_wb);
       pf_store(px, nimg, [&](int i, float v) { Xr[i] = v; });
-      if (P.wgather)
+      if (a.wstack)
         pf_store(pw, P.Kdp * P.NP, [&](int i, float v) { Wb[i] = v; });
       else
         pf_store(pw, nw, [&](int i, float v) {
@@ -1441,6 +1459,8 @@ constexpr int kMaxLds = 160 * 1024;
 static Dv dv(int d) { return Dv{d, 1.0f / (float)d}; }
 
 // Forward conv launch geometry; 0 if it fits (LDS, prefetch registers), <0 otherwise.
+static int conv_bwd_plan(const Geo& g, int dgrad, ConvBwdP& P);
+
 static int conv_fwd_plan(const Geo& g, ConvFwdP& P) {
   P = ConvFwdP{};
   P.g = g;
@@ -1493,11 +1513,15 @@ TDE_API int tde_bncnn_conv_fwd_cfg(const TdeBnGeo* gg, int* out) {
 // z = conv(relu(BN_in(in))); this layer's BN partial sums into acc [B][2][Co] (nullable).
 // inc_iter (nullable): the step counter a training step's first launch advances.
 TDE_API int tde_bncnn_conv_fwd(const TdeBnGeo* gg, int B, const float* in, const TdeBn* bn_in, const float* w, float* z,
-                               double* acc, long long* inc_iter, hipStream_t stream) {
+                               double* acc, long long* inc_iter, float* wstack, hipStream_t stream) {
   ConvFwdP P;
   if (conv_fwd_plan(geo_of(gg), P) != 0) return -1;
   if (!bn_ok(bn_in) || bn_in->C != P.g.C || B < 1 || bn_in->mode == kBnSaved) return -2;
-  ConvFwdArgs a{P, B, in, bn_of(bn_in), w, z, acc, next_stamps(), inc_iter};
+  ConvFwdArgs a{P, B, in, bn_of(bn_in), w, z, acc, next_stamps(), inc_iter, wstack, ConvBwdP{}};
+  if (wstack) {
+    // the whole stack must be covered by the grid's threads, and fit the backward's registers
+    if (conv_bwd_plan(P.g, 1, a.sp) != 0 || !a.sp.wgather || a.sp.Kdp * a.sp.NP > B * P.msplit * NTB) return -3;
+  }
   set_lds(conv_fwd_kernel, P.lds);
   conv_fwd_kernel<<<dim3(B, P.msplit), NTB, P.lds, stream>>>(a);
   TDE_LAUNCH_CHECK();
@@ -1664,7 +1688,7 @@ static int conv_bwd_plan(const Geo& g, int dgrad, ConvBwdP& P) {
   return P.lds > kMaxLds ? -3 : 0;
 }
 
-// out = {lds, wgrad items, dgrad items, wgrad split, dgrad K split}
+// out = {lds, wgrad items, dgrad items, wgrad split, dgrad K split, staged weight floats}
 TDE_API int tde_bncnn_conv_bwd_plan(const TdeBnGeo* gg, int dgrad, int* out) {
   ConvBwdP P;
   const int rc = conv_bwd_plan(geo_of(gg), dgrad, P);
@@ -1673,12 +1697,13 @@ TDE_API int tde_bncnn_conv_bwd_plan(const TdeBnGeo* gg, int dgrad, int* out) {
   out[2] = P.n_dg_items;
   out[3] = P.wg_split;
   out[4] = P.ksd;
+  out[5] = P.wgather ? P.Kdp * P.NP : 0;   // floats of the forward-staged input-gradient weights
   return rc;
 }
 
 TDE_API int tde_bncnn_conv_bwd(const TdeBnGeo* gg, int B, const float* z, const TdeBn* bn, const TdeBnBwd* bb,
                                const float* gout, const float* w, const float* in, const TdeBn* bn_in, float* gin,
-                               double* acc_in, float* dwpart, int dgrad, hipStream_t stream) {
+                               double* acc_in, float* dwpart, int dgrad, const float* wstack, hipStream_t stream) {
   ConvBwdP P;
   if (conv_bwd_plan(geo_of(gg), dgrad, P) != 0) return -1;
   const Geo& g = P.g;
@@ -1700,6 +1725,8 @@ TDE_API int tde_bncnn_conv_bwd(const TdeBnGeo* gg, int B, const float* z, const 
   a.acc_in = acc_in;
   a.dwpart = dwpart;
   a.stamps = next_stamps();
+  a.wstack = dgrad ? wstack : nullptr;
+  if (a.wstack && !P.wgather) return -5;
   set_lds(conv_bwd_kernel, P.lds);
   conv_bwd_kernel<<<dim3(B, dgrad ? 2 : 1), NTB, P.lds, stream>>>(a);
   TDE_LAUNCH_CHECK();

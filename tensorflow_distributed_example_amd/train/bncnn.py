@@ -36,7 +36,7 @@ _vp, _i = C.c_void_p, C.c_int
 N.register_hip({
     "tde_bncnn_conv_fwd_cfg": (_i, [_vp, _vp]),
     # geo, B, in, bn_in, w, z, acc, inc_iter, stream
-    "tde_bncnn_conv_fwd": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "tde_bncnn_conv_fwd": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     # B, K, D, Dp, in, bn, w, h, hstat, stream
     "tde_bncnn_dense_fwd": (_i, [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
     # B, D, Dp, NC, mode, h, hstat, bn, rate, seed, iter, layer_id, drop_on, wh, bh, labels, scale, metrics, out,
@@ -47,8 +47,8 @@ N.register_hip({
     "tde_bncnn_dense_bwd": (_i, [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp,
                                  _vp]),
     "tde_bncnn_conv_bwd_plan": (_i, [_vp, _i, _vp]),
-    # geo, B, z, bn, bb, gout, w, in, bn_in, gin, acc_in, dwpart, dgrad, stream
-    "tde_bncnn_conv_bwd": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
+    # geo, B, z, bn, bb, gout, w, in, bn_in, gin, acc_in, dwpart, dgrad, wstack, stream
+    "tde_bncnn_conv_bwd": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp]),
     # n, cnt, part, out, len, opt, stream
     "tde_bncnn_reduce": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp]),
 })
@@ -182,6 +182,8 @@ class BnCnnPlan(ReplicaPlan):
             if self.lib.tde_bncnn_conv_bwd_plan(C.byref(blk["geo"]), int(li > 0), out) != 0:
                 raise ValueError(f"{blk['conv'].name}: backward tiles do not fit")
             blk["bwd"] = list(out)
+            # the input-gradient role's class-stacked weights, staged by the training forward of the layer
+            blk["wstack"] = torch.zeros(out[5], **f32) if li > 0 and out[5] > 0 else None
         dense, bn_d, drop = spec["dense"]
         last = self.blocks[-1]
         self.K = last["geo"].Ho * last["geo"].Wo * last["geo"].Co
@@ -255,8 +257,9 @@ class BnCnnPlan(ReplicaPlan):
         for li, blk in enumerate(self.blocks):
             # a training step's first launch advances the step counter (dropout seed, Adam's t)
             inc = _P(self.iterations) if (phase == "train" and li == 0) else None
+            ws = _P(blk["wstack"]) if phase == "train" else None
             rc = lib.tde_bncnn_conv_fwd(C.byref(blk["geo"]), B, _P(inp), C.byref(bn_in), _P(blk["w"]), _P(blk["z"]),
-                                        _P(blk["acc"]) if batch_stats else None, inc, s)
+                                        _P(blk["acc"]) if batch_stats else None, inc, ws, s)
             if rc != 0:
                 raise RuntimeError(f"tde_bncnn_conv_fwd({blk['conv'].name}) failed with {rc}")
             bn_in = self._bn(blk, mode, B)
@@ -318,7 +321,8 @@ class BnCnnPlan(ReplicaPlan):
                 inp, bn_in, gin, acc_in = x, Bn(BN_NONE, blk["geo"].C), None, None
             rc = lib.tde_bncnn_conv_bwd(C.byref(blk["geo"]), B, _P(blk["z"]), C.byref(self._bn(blk, BN_SAVED, B)),
                                         C.byref(bb), _P(blk["g"]), _P(blk["w"]), _P(inp), C.byref(bn_in), _P(gin),
-                                        _P(acc_in), _P(blk["dwpart"]), int(li > 0), s)
+                                        _P(acc_in), _P(blk["dwpart"]), int(li > 0),
+                                        _P(blk["wstack"]) if li > 0 else None, s)
             if rc != 0:
                 raise RuntimeError(f"tde_bncnn_conv_bwd({blk['conv'].name}) failed with {rc}")
         # weight-gradient partials -> the bucket: per image for the convs, per 64-row block for the dense
