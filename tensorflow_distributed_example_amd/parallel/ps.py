@@ -163,10 +163,16 @@ class PSClient:
         """One async training step's exchange with every ps task: push the gradients held in ``hg``,
         the BN moving-average values ``averages`` ({name: (momentum, values)}), advance the global step
         by ``dstep`` and the ticket counter by ``dticket`` (both on ps 0), and pull fresh values of every
-        variable into ``hw`` / ``hs``.  Returns (global step, ticket counter)."""
+        variable into ``hw`` / ``hs``.  Returns (global step, ticket counter).
+
+        ps 0 (which owns the counters) is exchanged with LAST: every ``tde_ps_step`` returns only after
+        that ps task applied the push, so when the global step advances every shard already holds
+        this step's update.  A chief that sees ``global_step == max_steps`` and saves the final
+        checkpoint therefore never misses the last updates of the shards on ps 1..N-1."""
         averages = averages or {}
         gstep = ticket = None
-        for k, c in enumerate(self.conns):
+        for k in list(range(1, len(self.conns))) + [0]:
+            c = self.conns[k]
             push, pn, pp, ps_, pull, ln, lp, ls = self._step_args[k]
             av = [n for n in self.by_ps[k] if n in averages]
             vals = [np.ascontiguousarray(averages[n][1], dtype=np.float32).reshape(-1) for n in av]

@@ -162,3 +162,62 @@ def test_parameter_server_one_round_trip_step_over_flat_mirrors():
     finally:
         s1.stop()
         s2.stop()
+
+
+def test_ps_step_advances_global_step_only_after_every_shard_applied():
+    """ps 0 owns the global step, so it is exchanged with LAST.  Whenever an observer reads
+    global step g, the shard on ps 1 already holds >= g updates (a chief that saves the final checkpoint
+    at g == max_steps sees every update).  Two trainers step concurrently; the observer checks the
+    invariant on every poll and at the end."""
+    import threading
+
+    from tensorflow_distributed_example_amd.train.params import ParamStore
+
+    class _Spec:
+        def __init__(self, name, shape):
+            self.full_name, self.shape, self.trainable, self.aggregation = name, shape, True, "none"
+            self.initializer = lambda shape, gen: np.zeros(shape, np.float32)
+
+    s1, s2 = PS.PSServer("127.0.0.1", 0), PS.PSServer("127.0.0.1", 0)
+    addrs = [f"127.0.0.1:{s1.port}", f"127.0.0.1:{s2.port}"]
+    shapes = {"a/kernel": (64,), "b/kernel": (64,)}   # round-robin: a on ps 0, b on ps 1
+    max_steps = 400
+    try:
+        chief = PS.PSClient(addrs, shapes)
+        chief.initialize({n: np.zeros(s) for n, s in shapes.items()}, is_chief=True)
+        errors = []
+
+        def trainer():
+            try:
+                store = ParamStore([_Spec(n, s) for n, s in shapes.items()], "cpu")
+                c = PS.PSClient(addrs, shapes)
+                c.bind_store(store)
+                c.hg.numpy()[:] = -1.0          # lr 1: every applied update adds exactly 1.0
+                while True:
+                    gs, _ = c.step(1.0, dstep=1)
+                    if gs >= max_steps:
+                        break
+                c.close()
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+
+        ts = [threading.Thread(target=trainer) for _ in range(2)]
+        for t in ts:
+            t.start()
+        polls = 0
+        while any(t.is_alive() for t in ts):
+            g = chief.global_step()
+            b = float(chief.pull(["b/kernel"])["b/kernel"][0])
+            assert b >= g, f"global step {g} visible before ps 1 applied it (b={b})"
+            polls += 1
+        for t in ts:
+            t.join()
+        assert not errors, errors
+        g = chief.global_step()
+        v = chief.pull()
+        assert g >= max_steps and polls > 0
+        assert float(v["a/kernel"][0]) == g and float(v["b/kernel"][0]) == g
+        chief.close()
+    finally:
+        s1.stop()
+        s2.stop()
