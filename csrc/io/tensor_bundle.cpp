@@ -356,6 +356,46 @@ bool load_bundle(const std::string& prefix, Bundle* B) {
   return read_file(prefix + ".data-00000-of-00001", &B->data);
 }
 
+// Entry checksum of a DT_STRING tensor's data bytes, TF's string layout: the data is
+// [varint64 len_0 .. len_{n-1}][masked crc32c of the lengths][string bytes]; the checksums run over the
+// lengths as little-endian uint32 (uint64 above 4 GiB), NOT over the varint bytes, then the 4-byte length
+// checksum, then the string bytes.  Returns false when the bytes do not parse as n strings.
+bool string_tensor_crc(const char* d, size_t size, int64_t n, uint32_t* out) {
+  size_t i = 0, total = 0;
+  uint32_t crc = 0;
+  for (int64_t k = 0; k < n; ++k) {
+    uint64_t len = 0;
+    int shift = 0;
+    for (;;) {
+      if (i >= size || shift > 63) return false;
+      const uint8_t b = (uint8_t)d[i++];
+      len |= (uint64_t)(b & 0x7f) << shift;
+      shift += 7;
+      if (!(b & 0x80)) break;
+    }
+    if (len <= 0xffffffffull) {
+      const uint32_t l32 = (uint32_t)len;
+      crc = crc32c_extend(crc, &l32, 4);
+    } else {
+      crc = crc32c_extend(crc, &len, 8);
+    }
+    total += (size_t)len;
+  }
+  if (i + 4 + total != size) return false;
+  crc = crc32c_extend(crc, d + i, 4);            // the stored (masked) length checksum
+  crc = crc32c_extend(crc, d + i + 4, total);     // the string bytes
+  *out = crc32c_mask(crc);
+  return true;
+}
+
+constexpr int kDtString = 7;
+
+int64_t num_elements(const std::vector<int64_t>& shape) {
+  int64_t n = 1;
+  for (int64_t d : shape) n *= d;
+  return n;
+}
+
 }  // namespace
 
 // dtypes follow TF DataType: 1 float, 2 double, 3 int32, 4 uint8, 9 int64, 14 bfloat16, 19 half.
@@ -379,7 +419,12 @@ TDE_API int tde_bundle_write(const char* prefix, int n, const char** names, cons
     const int64_t off = (int64_t)data.size();
     data.append((const char*)datas[i], (size_t)nbytes[i]);
     std::vector<int64_t> shape(shapes_flat + shape_off[i], shapes_flat + shape_off[i] + ranks[i]);
-    const uint32_t crc = crc32c_mask(crc32c(datas[i], (size_t)nbytes[i]));
+    uint32_t crc = 0;
+    if (dtypes[i] == kDtString) {
+      if (!string_tensor_crc((const char*)datas[i], (size_t)nbytes[i], num_elements(shape), &crc)) return -4;
+    } else {
+      crc = crc32c_mask(crc32c(datas[i], (size_t)nbytes[i]));
+    }
     tw.add(names[i], entry_proto(dtypes[i], shape, off, nbytes[i], crc));
   }
   const std::string index = tw.finish();
@@ -427,7 +472,8 @@ TDE_API int tde_bundle_entry(void* h, int i, char* name, int cap, int* dtype, in
   return 0;
 }
 
-// Copies tensor bytes; verifies the entry crc32c. Returns 0, -1 missing, -2 size, -3 crc mismatch.
+// Copies tensor bytes; verifies the entry crc32c (string tensors: TF's length/bytes layout, see
+// string_tensor_crc). Returns 0, -1 missing, -2 size, -3 crc mismatch.
 TDE_API int tde_bundle_read(void* h, const char* name, void* out, long long cap) {
   auto* B = (Bundle*)h;
   auto it = B->entries.find(name);
@@ -435,7 +481,12 @@ TDE_API int tde_bundle_read(void* h, const char* name, void* out, long long cap)
   const Entry& e = it->second;
   if (e.size > cap || (size_t)(e.offset + e.size) > B->data.size()) return -2;
   const char* src = B->data.data() + e.offset;
-  if (crc32c_mask(crc32c(src, (size_t)e.size)) != e.crc) return -3;
+  if (e.dtype == kDtString) {
+    uint32_t crc = 0;
+    if (!string_tensor_crc(src, (size_t)e.size, num_elements(e.shape), &crc) || crc != e.crc) return -3;
+  } else if (crc32c_mask(crc32c(src, (size_t)e.size)) != e.crc) {
+    return -3;
+  }
   memcpy(out, src, (size_t)e.size);
   return 0;
 }

@@ -97,12 +97,19 @@ def _masked_crc(b: bytes) -> int:
     return int(lib.tde_crc32c_masked(C.cast(buf, C.c_void_p), len(b)))
 
 
+def _len_words(lengths) -> bytes:
+    """The bytes TF checksums for string lengths: each length as a little-endian uint32 (uint64 when it
+    does not fit), kept for backward compatibility in TF's WriteStringTensor — not the varint bytes."""
+    return b"".join(n.to_bytes(4 if n <= 0xFFFFFFFF else 8, "little") for n in lengths)
+
+
 def encode_string_tensor(values) -> bytes:
-    """TensorBundle data bytes of a DT_STRING tensor: [varint64 len]* [masked crc32c of those varint
-    bytes, little endian] [bytes]*."""
+    """TensorBundle data bytes of a DT_STRING tensor: [varint64 len]* [masked crc32c of the lengths
+    as uint32 words, little endian] [bytes]*.  The entry checksum (computed natively when the bundle is
+    written) covers the uint32 lengths, this 4-byte checksum and the string bytes."""
     vals = [v.encode() if isinstance(v, str) else bytes(v) for v in values]
     lens = b"".join(_varint(len(v)) for v in vals)
-    return lens + _masked_crc(lens).to_bytes(4, "little") + b"".join(vals)
+    return lens + _masked_crc(_len_words([len(v) for v in vals])).to_bytes(4, "little") + b"".join(vals)
 
 
 def decode_string_tensor(raw: bytes, n: int = 1):
@@ -111,7 +118,7 @@ def decode_string_tensor(raw: bytes, n: int = 1):
         ln, i = _read_varint(raw, i)
         lens.append(ln)
     want = int.from_bytes(raw[i:i + 4], "little")
-    if want != _masked_crc(raw[:i]):
+    if want != _masked_crc(_len_words(lens)):
         raise IOError("string tensor: length checksum mismatch")
     i += 4
     out = []

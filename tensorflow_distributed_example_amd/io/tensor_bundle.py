@@ -78,7 +78,7 @@ def list_variables(prefix: str):
     return out
 
 
-def read_bundle(prefix: str) -> dict:
+def read_bundle(prefix: str, skip_bad_strings: bool = True) -> dict:
     lib = N.host()
     entries = list_variables(prefix)
     h = lib.tde_bundle_open(str(prefix).encode())
@@ -88,10 +88,16 @@ def read_bundle(prefix: str) -> dict:
             if dt == DT_STRING and not shape:
                 raw = (C.c_char * nb)()
                 rc = lib.tde_bundle_read(h, name.encode(), raw, nb)
-                if rc != 0:
-                    raise IOError(f"{prefix}: reading {name} failed ({'crc mismatch' if rc == -3 else rc})")
                 from .object_graph import decode_string_tensor
-                out[name] = decode_string_tensor(bytes(raw))[0]
+                try:
+                    if rc != 0:
+                        raise IOError(f"{prefix}: reading {name} failed ({'crc mismatch' if rc == -3 else rc})")
+                    out[name] = decode_string_tensor(bytes(raw))[0]
+                except IOError:
+                    # string tensors carry metadata only (the TF2 object graph); restore matches variables
+                    # by key position without it, so an unreadable one is skipped, not fatal
+                    if not skip_bad_strings:
+                        raise
                 continue
             if dt not in _DT_INV:
                 continue

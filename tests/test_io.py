@@ -121,6 +121,56 @@ def test_tensor_bundle_roundtrip_and_independent_parse(tmp_path):
     assert N.host().tde_crc32c_unmask(fields[6]) == _crc(blob)
 
 
+def _entry_fields(ent):
+    fields, i = {}, 0
+    while i < len(ent):
+        tag, i = _varint(ent, i)
+        f, wt = tag >> 3, tag & 7
+        if wt == 0:
+            v, i = _varint(ent, i)
+        elif wt == 2:
+            n, i = _varint(ent, i)
+            v = ent[i:i + n]
+            i += n
+        else:
+            v = struct.unpack("<I", ent[i:i + 4])[0]
+            i += 4
+        fields[f] = v
+    return fields
+
+
+def test_string_tensor_checksums_follow_tf_layout(tmp_path):
+    """TF's WriteStringTensor checksums each string length as a little-endian uint32 (not the
+    varint bytes); the stored 4-byte length checksum is that crc masked; the BundleEntryProto crc covers the
+    uint32 lengths, the 4-byte length checksum and the string bytes (masked).  A bundle whose string
+    tensor fails its checksum still restores its numeric tensors (the object graph is metadata)."""
+    from tensorflow_distributed_example_amd.io import object_graph as OG
+    lib = N.host()
+    payload = b"x" * 300                      # 300 needs a 2-byte varint: the layouts differ
+    enc = OG.encode_string_tensor([payload])
+    assert enc[:2] == bytes([0xAC, 0x02])
+    want_len_crc = lib.tde_crc32c_mask(_crc(struct.pack("<I", 300)))
+    assert struct.unpack("<I", enc[2:6])[0] == want_len_crc
+    prefix = str(tmp_path / "s")
+    TB.write_bundle(prefix, {"_CHECKPOINTABLE_OBJECT_GRAPH": payload, "v": np.ones(3, np.float32)})
+    fields = _entry_fields(dict(_sstable(prefix + ".index"))[b"_CHECKPOINTABLE_OBJECT_GRAPH"])
+    assert fields[1] == 7                       # DT_STRING
+    c = lib.tde_crc32c_extend(_crc(struct.pack("<I", 300)), enc[2:6], 4)
+    c = lib.tde_crc32c_extend(c, payload, len(payload))
+    assert fields[6] == lib.tde_crc32c_mask(c)
+    back = TB.read_bundle(prefix)
+    assert back["_CHECKPOINTABLE_OBJECT_GRAPH"] == payload
+    # corrupt one string byte: the numeric tensor still restores, the string tensor is skipped
+    d = bytearray(open(prefix + ".data-00000-of-00001", "rb").read())
+    off = fields.get(4, 0)
+    d[off + 10] ^= 0x01
+    open(prefix + ".data-00000-of-00001", "wb").write(bytes(d))
+    back = TB.read_bundle(prefix)
+    assert "_CHECKPOINTABLE_OBJECT_GRAPH" not in back and np.array_equal(back["v"], np.ones(3, np.float32))
+    with pytest.raises(IOError, match="crc"):
+        TB.read_bundle(prefix, skip_bad_strings=False)
+
+
 def test_bundle_detects_corruption(tmp_path):
     prefix = str(tmp_path / "c")
     TB.write_bundle(prefix, {"a": np.arange(100, dtype=np.float32)})
@@ -171,7 +221,7 @@ def test_tf2_object_graph_checkpoint_round_trip(tmp_path):
     from tensorflow_distributed_example_amd.io import object_graph as OG
     from tensorflow_distributed_example_amd.io import tensor_bundle as TB
 
-    # the DT_STRING encoding: [varint len][masked crc32c of the length bytes][bytes]
+    # the DT_STRING encoding: [varint len][masked crc32c of the uint32 length][bytes]
     enc = OG.encode_string_tensor([b"abc"])
     assert enc[0] == 3 and enc[5:] == b"abc" and OG.decode_string_tensor(enc) == [b"abc"]
 
