@@ -212,7 +212,10 @@ def main():
                        "optimizer": f"SGD(lr={a.lr})", "plan": prog.plan_kind,
                        "allreduce": ar,
                        "hipgraph": prog.use_graph, "grad_buckets": len(prog.buckets or []) or 1,
-                       "optimizer_placement": placement}}), flush=True)
+                       "optimizer_placement": placement,
+                       # fused_push: the backward stores the Dense(64) weight gradient straight into the
+                       # xGMI owners' windows; post_backward: the all-reduce launch pushes the whole bucket
+                       "exchange": getattr(prog, "exchange", "none")}}), flush=True)
 
 
 if __name__ == "__main__":

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--sync-every", type=int, default=1)
     ap.add_argument("--mwms", type=int, default=0, help="K > 0: MultiWorkerMirroredStrategy with K GPUs per worker "
                     "(launch with torchrun)")
+    ap.add_argument("--trace-show", type=int, default=6, help="with TDE_XGMI_TRACE: calls printed per rank")
     a = ap.parse_args()
     import torch
 
@@ -57,6 +58,23 @@ def main():
             if bits and any(bits):
                 print(f"{tag} STOP: error bits set", flush=True)
                 break
+    tr = getattr(comm, "trace", None)
+    if tr:   # TDE_XGMI_TRACE=<calls>: per-block phase times of the recorded calls (device clock, us)
+        from tensorflow_distributed_example_amd.parallel.comm import xg_trace_records
+        torch.cuda.synchronize()
+        nb = {}
+        for li, buf in enumerate(tr):
+            recs = xg_trace_records(buf, buf.shape[1])
+            for r in recs[: a.trace_show]:
+                used = [i for i, v in enumerate(r["start"]) if v]
+                us = lambda k: [r[k][i] / 100.0 for i in used]   # noqa: E731
+                mn = lambda k: min(us(k)) if used else 0.0         # noqa: E731
+                mx = lambda k: max(us(k)) if used else 0.0         # noqa: E731
+                miss = sorted({(r["miss1"][i], r["miss2"][i]) for i in used} - {(255, 255)})
+                print(f"{tag} rank{li} epoch {r['epoch']} blocks {len(used)} start [{mn('start'):.1f}, "
+                      f"{mx('start'):.1f}] pub1<= {mx('pub1'):.1f} arr1 [{mn('arr1'):.1f}, {mx('arr1'):.1f}] "
+                      f"pub2<= {mx('pub2'):.1f} arr2<= {mx('arr2'):.1f} end<= {mx('end'):.1f} missing={miss} "
+                      f"xcc={sorted(set(r['xcc'][i] for i in used))}", flush=True)
     print(f"{tag} done", flush=True)
 
 

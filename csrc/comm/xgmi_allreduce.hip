@@ -53,14 +53,11 @@
 #include <string.h>
 
 #include "tde_optim.h"
+#include "tde_xgmi.h"
 
 namespace tde {
 
-constexpr int kXgMaxRanks = 8;
-constexpr int kXgMaxBlocks = 128;
 constexpr int kXgThreads = 256;
-constexpr size_t kXgFlagWords = 2 * 2 * kXgMaxRanks * kXgMaxBlocks;
-constexpr size_t kXgFlagBytes = kXgFlagWords * 4;
 
 struct XgArgs {
   float* grad;                    // local gradient bucket (in/out), M floats
@@ -82,14 +79,24 @@ struct XgArgs {
   bf16* sht; int sh_cols; long long sht_ld;
   const long long* iterations;
   OptHyper h;
+  // diagnostics (nullable): per call slot (epoch % trace_calls) and block, kXgTraceWords u64 —
+  // [epoch, t_start, t_published1, t_phase1_arrived, t_published2, t_phase2_arrived, t_end, info] with
+  // t = s_memrealtime (100 MHz, one clock for every process on the device) and info = missing source
+  // of the phase-1 wait (bits 0-7, 0xff = none) | of the phase-2 wait (8-15) | XCC id (16-23) |
+  // HW_ID cu (24-27) | se (28-31)
+  unsigned long long* trace;
+  int trace_calls;
+  // [push_lo, push_hi): bucket elements a producer kernel already stored into the owners' contribution
+  // areas (tde_xgmi.h XgPush); phase 1 skips them
+  long long push_lo, push_hi;
 };
+constexpr int kXgTraceWords = 8;
 
 __device__ __forceinline__ uint32_t* flag_ptr(char* base, int parity, int phase, int src, int blk) {
   return reinterpret_cast<uint32_t*>(base) + (((parity * 2 + phase) * kXgMaxRanks + src) * kXgMaxBlocks + blk);
 }
-// which 0 = in (contributions), 1 = out (reduced slices)
 __device__ __forceinline__ float* area(char* base, int which, int parity, long long cap) {
-  return reinterpret_cast<float*>(base + kXgFlagBytes) + ((size_t)which * 2 + parity) * (size_t)cap;
+  return xg_area(base, which, parity, cap);
 }
 
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -112,13 +119,15 @@ __device__ __forceinline__ void publish(char* const* peer, int nranks, int parit
   }
 }
 
-// Thread 0 waits until every rank's flag of (parity, phase, blk) equals `epoch`.
+// Thread 0 waits until every rank's flag of (parity, phase, blk) equals `epoch`; *missing (thread 0,
+// nullable) = the first source whose flag never arrived, 0xff when all did.
 __device__ __forceinline__ void await(char* base, int parity, int phase, int nranks, int blk, uint32_t epoch,
-                                      long long timeout, uint32_t* err, uint32_t bit) {
+                                      long long timeout, uint32_t* err, uint32_t bit, uint32_t* missing = nullptr) {
   if (threadIdx.x == 0) {
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
     bool ok = true;
-    for (int s = 0; s < nranks && ok; ++s) {
+    int s = 0;
+    for (; s < nranks && ok; ++s) {
       uint32_t* f = flag_ptr(base, parity, phase, s, blk);
       while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
         __builtin_amdgcn_s_sleep(2);
@@ -128,6 +137,7 @@ __device__ __forceinline__ void await(char* base, int parity, int phase, int nra
         }
       }
     }
+    if (missing) *missing = ok ? 0xffu : (uint32_t)(s - 1);
     if (!ok) __hip_atomic_fetch_or(err, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __atomic_thread_fence(__ATOMIC_ACQUIRE);   // system scope: drop stale L1/L2 lines
     drain_stores();
@@ -220,17 +230,36 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
   const int N = a.nranks, r = a.rank;
   const long long M = a.M, L = a.L, CH = a.chunk, cap = a.cap;
   const long long c0 = (long long)blk * CH;
+  // diagnostics record (thread 0 only)
+  unsigned long long* tr = nullptr;
+  uint32_t miss1 = 0xffu, miss2 = 0xffu;
+  if (a.trace && tid == 0) {
+    tr = a.trace + ((size_t)(epoch % (uint32_t)a.trace_calls) * gridDim.x + blk) * kXgTraceWords;
+    tr[0] = epoch;
+    tr[1] = __builtin_amdgcn_s_memrealtime();
+  }
+#define XG_STAMP(i) \
+  if (tr) tr[i] = __builtin_amdgcn_s_memrealtime()
 
-  // ---- phase 1: push chunk `blk` of every slice s to rank s
+  // ---- phase 1: push chunk `blk` of every slice s to rank s (minus the producer-pushed range)
   for (int s = 0; s < N; ++s) {
     const long long g0 = (long long)s * L + c0;
     const long long n = max(0LL, min(CH, M - g0));
-    copy_chunk(area(a.peer[s], 0, parity, cap) + (size_t)r * L + c0, a.grad + g0, n, (g0 & 3) == 0);
+    float* dst = area(a.peer[s], 0, parity, cap) + (size_t)r * L + c0;
+    const long long plo = min(max(a.push_lo - g0, 0LL), n), phi = min(max(a.push_hi - g0, 0LL), n);
+    if (plo >= phi) {
+      copy_chunk(dst, a.grad + g0, n, (g0 & 3) == 0);
+    } else {   // [0, plo) and [phi, n) still come from the local bucket
+      if (plo > 0) copy_chunk(dst, a.grad + g0, plo, false);
+      if (phi < n) copy_chunk(dst + phi, a.grad + g0 + phi, n - phi, false);
+    }
   }
   publish<UNCACHED>(a.peer, N, parity, 0, r, blk, epoch);
+  XG_STAMP(2);
 
   // ---- phase 2: reduce own slice chunk from local HBM, push the result to every rank
-  await(a.peer[r], parity, 0, N, blk, epoch, a.timeout_ticks, a.err, 1u);
+  await(a.peer[r], parity, 0, N, blk, epoch, a.timeout_ticks, a.err, 1u, tr ? &miss1 : nullptr);
+  XG_STAMP(3);
   {
     const long long g0 = (long long)r * L + c0;
     const long long n = max(0LL, min(CH, M - g0));
@@ -252,11 +281,13 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
     }
   }
   publish<UNCACHED>(a.peer, N, parity, 1, r, blk, epoch);
+  XG_STAMP(4);
 
   // ---- phase 3: gather every reduced slice chunk back into the bucket (or apply the update)
   float lr_t = 0.f;
   if (a.apply) lr_t = opt_lr_t(a.h, a.h.kind == kOptAdam ? *a.iterations : 0);
-  await(a.peer[r], parity, 1, N, blk, epoch, a.timeout_ticks, a.err, 2u);
+  await(a.peer[r], parity, 1, N, blk, epoch, a.timeout_ticks, a.err, 2u, tr ? &miss2 : nullptr);
+  XG_STAMP(5);
   const float* out = area(a.peer[r], 1, parity, cap);
   for (int s = 0; s < N; ++s) {
     const long long g0 = (long long)s * L + c0;
@@ -264,6 +295,14 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
     if (a.apply) apply_chunk(a, lr_t, g0, out + (size_t)s * L + c0, n);
     else copy_chunk(a.grad + g0, out + (size_t)s * L + c0, n, (g0 & 3) == 0);
   }
+  if (tr) {
+    const uint32_t hw = __builtin_amdgcn_s_getreg(63492);   // hwreg(HW_REG_HW_ID): cu 8-11, se 13-15
+    const uint32_t xcc = __builtin_amdgcn_s_getreg(63508);  // hwreg(HW_REG_XCC_ID)
+    tr[6] = __builtin_amdgcn_s_memrealtime();
+    tr[7] = (unsigned long long)(miss1 | (miss2 << 8) | ((xcc & 0xff) << 16) | (((hw >> 8) & 0xf) << 24) |
+                                 (((hw >> 13) & 0x7) << 28));
+  }
+#undef XG_STAMP
   // the last block to finish advances the epoch (every block read it at its start) and re-arms
   // the arrival counter epoch[1] for the next call
   if (tid == 0) {
@@ -351,6 +390,30 @@ TDE_API int tde_xgmi_free(void* window, void* epoch, void* err) {
   return e1 != hipSuccess ? (int)e1 : e2 != hipSuccess ? (int)e2 : (int)e3;
 }
 
+// The producer-side descriptor (tde_xgmi.h XgPush) for the next call of a rank: the same slice length
+// and area capacity the all-reduce launch computes for a bucket of M elements over nranks x nblocks.
+struct TdeXgPush {
+  void* peer[kXgMaxRanks];
+  const void* epoch;
+  long long L, cap, off;
+  int rank, nranks;
+};
+TDE_API int tde_xgmi_push_spec(long long M, long long max_elems, void* const* peers, const void* epoch, int rank,
+                               int nranks, int nblocks, long long off, TdeXgPush* out) {
+  if (nranks < 1 || nranks > kXgMaxRanks || rank < 0 || rank >= nranks || M < 0 || M > max_elems || !out) return -1;
+  nblocks = nblocks < 1 ? 1 : nblocks > kXgMaxBlocks ? kXgMaxBlocks : nblocks;
+  memset(out, 0, sizeof(*out));
+  for (int i = 0; i < nranks; ++i) out->peer[i] = peers[i];
+  out->epoch = epoch;
+  out->L = xg_slice(M, nranks, nblocks);
+  out->cap = xg_cap(max_elems);
+  out->off = off;
+  out->rank = rank;
+  out->nranks = nranks;
+  return out->L * nranks > out->cap ? -3 : 0;
+}
+static_assert(sizeof(TdeXgPush) == sizeof(XgPush), "TdeXgPush mirrors XgPush");
+
 // Error bits of this rank (host read of the mapped word; no HIP call, never blocks).
 TDE_API int tde_xgmi_error(void* err) { return (int)*(volatile uint32_t*)err; }
 
@@ -370,7 +433,23 @@ struct TdeXgApply {
   const long long* iterations;
   void* sh; long long sh_lo, sh_hi;
   void* sht; int sh_cols; long long sht_ld;
+  long long push_lo, push_hi;   // bucket range the step's producer kernel pushed itself (empty: none)
 };
+
+// Diagnostics: trace buffers registered per rank (keyed by the rank's epoch word); every launch
+// of that rank then records per-block phase timestamps (XgArgs::trace).
+#include <map>
+#include <mutex>
+static std::mutex g_trace_mu;
+static std::map<void*, std::pair<unsigned long long*, int>> g_trace;
+
+TDE_API int tde_xgmi_trace_words() { return kXgTraceWords; }
+TDE_API int tde_xgmi_set_trace(void* epoch, void* trace, int calls) {
+  std::lock_guard<std::mutex> lk(g_trace_mu);
+  if (!trace || calls <= 0) g_trace.erase(epoch);
+  else g_trace[epoch] = {(unsigned long long*)trace, calls};
+  return 0;
+}
 
 static int xg_fill(XgArgs& a, float* grad, long long M, long long max_elems, void* const* peers, void* epoch,
                    void* err, int rank, int nranks, int nblocks, long long timeout_ticks) {
@@ -388,6 +467,12 @@ static int xg_fill(XgArgs& a, float* grad, long long M, long long max_elems, voi
   a.chunk = a.L / nblocks;
   a.cap = xg_cap(max_elems);
   a.timeout_ticks = timeout_ticks;
+  {
+    std::lock_guard<std::mutex> lk(g_trace_mu);
+    auto it = g_trace.find(epoch);
+    a.trace = it == g_trace.end() ? nullptr : it->second.first;
+    a.trace_calls = it == g_trace.end() ? 0 : it->second.second;
+  }
   if (a.L * nranks > a.cap) return -3;   // areas hold nranks slices
   return 0;
 }
@@ -409,6 +494,8 @@ static int xg_set_apply(XgArgs& a, const TdeXgApply* o) {
   a.sht_ld = o->sht_ld;
   a.iterations = o->iterations;
   a.h = OptHyper{o->kind, o->lr, o->mom, o->b1, o->b2, o->eps};
+  a.push_lo = o->push_lo;
+  a.push_hi = o->push_hi;
   return 0;
 }
 

@@ -11,6 +11,7 @@
 // and the deferred conv update are the same code in both.
 #pragma once
 #include "tde_optim.h"
+#include "tde_xgmi.h"
 
 namespace tde {
 namespace cnet {
@@ -184,6 +185,7 @@ struct BwdArgs {
   OptHyper h;
   FlatApply commit;                  // the previous step's deferred conv update (head workgroup, while *pend)
   int* pend_set;                     // := 1: this step's conv update is deferred
+  XgPush push;                       // MODE 0, nranks > 0: dW1 goes to the xGMI owners (fused DP exchange)
 };
 
 // Up to NPER elements per thread of a FlatApply's ranges, loaded early into registers and

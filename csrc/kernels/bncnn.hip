@@ -1564,6 +1564,25 @@ TDE_API int tde_bncnn_head(int B, int D, int Dp, int NC, int mode, const float* 
   return 0;
 }
 
+// Debug export of the dropout keep scales the head applies at step *iter: out[r * D + f] = 1/(1-rate) or 0
+// (keep_scale per element; the head's 4-at-a-time form draws the same values).  Tests pin the fused
+// plan's dropout against a float64 oracle with this mask.
+__global__ void dropout_mask_kernel(int n, float rate, unsigned long long seed, const long long* iter, int layer,
+                                    float* out) {
+  const long long it = iter ? *iter : 0;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x)
+    out[e] = keep_scale(rate, seed, it, layer, e);
+}
+
+TDE_API int tde_bncnn_dropout_mask(int B, int D, float rate, unsigned long long seed, const long long* iter,
+                                   int layer_id, float* out, hipStream_t stream) {
+  if (B < 1 || D < 1 || !out || !(rate > 0.f && rate < 1.f)) return -1;
+  const int n = B * D;
+  dropout_mask_kernel<<<(n + 255) / 256, 256, 0, stream>>>(n, rate, seed, iter, layer_id, out);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
 TDE_API int tde_bncnn_dense_bwd(int B, int K, int D, int Dp, const float* in, const TdeBn* bn, const float* w,
                                 const float* gh, const float* h, const double* gstat, int nrt, const TdeBn* bnd,
                                 float* dbeta_d, float* dgamma_d, float* dwpart, float* g, double* acc,

@@ -342,6 +342,13 @@ __global__ __launch_bounds__(1024) void convnet32_bwd_kernel(BwdArgs a) {
         if (MODE == 2 && a.h.kind != kOptSGD) a.m1[e] = m;
         if (MODE == 2 && a.h.kind == kOptAdam) a.v1[e] = v;
       }
+    } else if (a.push.nranks > 0) {
+      // fused DP exchange: this position's complete dW1 rows go straight into the owners' contribution
+      // areas of the all-reduce call that follows this launch (its parity from the completed-calls count)
+      const int parity = (int)((*a.push.epoch + 1u) & 1u);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        xg_push_store(a.push, parity, a.push.off + (long long)(p * CC + rt * 16 + fq * 4 + r) * HD + col, accw[r]);
     } else {
 #pragma unroll
       for (int r = 0; r < 4; ++r) a.dW1[(size_t)(p * CC + rt * 16 + fq * 4 + r) * HD + col] = accw[r];
@@ -398,8 +405,9 @@ TDE_API int tde_convnet_bwd_f32(const float* x, const void* amax, int lda, const
                                 int C, int pre_relu, const int* labels, float scale, float* metrics, const float* W1,
                                 int ldw1, const float* Pt, int ldPt, float* dW1, float* dwc, float* dbc, float* dW2,
                                 float* db2, float* db1, int B, int H, int W, long long* stamps, const TdeBwdOpt* opt,
-                                float* cpart, hipStream_t stream) {
+                                float* cpart, const XgPush* push, hipStream_t stream) {
   if (ldw1 != HD || ((uintptr_t)W1 & 15) || ((uintptr_t)Pt & 7)) return -1;
+  if (push && push->nranks > 0 && (opt || push->nranks > kXgMaxRanks || push->L <= 0 || !push->epoch)) return -7;
   if (opt && opt->w + opt->off_w1 != W1) return -3;   // the update is applied to the rows it reads
   BwdArgs a;
   const int rc = fill_bwd(a, x, amax, lda, hpre, hzero, hrep, hrep_stride, b1, W2, b2, C, pre_relu, labels, scale,
@@ -408,6 +416,7 @@ TDE_API int tde_convnet_bwd_f32(const float* x, const void* amax, int lda, const
   a.cpart = cpart;
   a.w1r_out = nullptr;
   a.w1c_out = nullptr;
+  if (push) a.push = *push;
   const int P = ((H - 2) / 2) * ((W - 2) / 2);
   static bool attr_set = false;
   if (!attr_set) {

@@ -42,7 +42,7 @@ _HIP_PROTOS = {
     "tde_convnet_fwd_f32": (i32, [p, p, p, p, i32, p, p, i32, p, i32, i32, i32, i32, p, p, i64, i64, p, i32, i64,
                                   p]),
     "tde_convnet_bwd_f32": (i32, [p, p, i32, p, p, i32, i64, p, p, p, i32, i32, p, f32, p, p, i32, p, i32, p, p,
-                                  p, p, p, p, i32, i32, i32, p, p, p, p]),
+                                  p, p, p, p, i32, i32, i32, p, p, p, p, p]),
     "tde_flat_apply": (i32, [p, p, p, p, p, p, i32, f32, f32, f32, f32, f32, p, i32, p]),
     "tde_noop": (i32, [i32, i32, p]),
     "tde_optim_table_size": (i32, [p, i32]),
@@ -119,6 +119,9 @@ _HIP_PROTOS = {
     "tde_xgmi_free": (i32, [p, p, p]),
     "tde_xgmi_error": (i32, [p]),
     "tde_xgmi_epoch": (i64, [p]),
+    "tde_xgmi_trace_words": (i32, []),
+    "tde_xgmi_push_spec": (i32, [i64, i64, p, p, i32, i32, i32, i64, p]),
+    "tde_xgmi_set_trace": (i32, [p, p, i32]),
     "tde_xgmi_all_reduce": (i32, [p, i64, i64, p, p, p, i32, i32, i32, i32, i64, p]),
     "tde_xgmi_all_reduce_apply": (i32, [p, i64, i64, p, p, p, i32, i32, i32, i32, i64, p, p]),
     "tde_xgmi_all_reduce_group": (i32, [i32, p, i64, i64, p, p, p, i32, i32, i32, i32, i64, p, p]),

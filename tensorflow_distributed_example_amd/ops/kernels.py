@@ -42,7 +42,15 @@ class XgApply(_ct.Structure):
     _fields_ = [("kind", _ct.c_int), ("lr", _ct.c_float), ("mom", _ct.c_float), ("b1", _ct.c_float), ("b2", _ct.c_float),
                 ("eps", _ct.c_float), ("w", _ct.c_void_p), ("m", _ct.c_void_p), ("v", _ct.c_void_p),
                 ("iterations", _ct.c_void_p), ("sh", _ct.c_void_p), ("sh_lo", _ct.c_longlong), ("sh_hi", _ct.c_longlong),
-                ("sht", _ct.c_void_p), ("sh_cols", _ct.c_int), ("sht_ld", _ct.c_longlong)]
+                ("sht", _ct.c_void_p), ("sh_cols", _ct.c_int), ("sht_ld", _ct.c_longlong),
+                ("push_lo", _ct.c_longlong), ("push_hi", _ct.c_longlong)]
+
+
+class XgPush(_ct.Structure):
+    """``TdeXgPush`` / ``XgPush`` (csrc/include/tde_xgmi.h): a producer kernel stores its gradient range
+    straight into the owners' contribution areas of the next xGMI all-reduce call."""
+    _fields_ = [("peer", _ct.c_void_p * 8), ("epoch", _ct.c_void_p), ("L", _ct.c_longlong), ("cap", _ct.c_longlong),
+                ("off", _ct.c_longlong), ("rank", _ct.c_int), ("nranks", _ct.c_int)]
 
 
 class BwdOpt(_ct.Structure):
@@ -220,7 +228,8 @@ def convnet_fwd(x, wc, bc, W1, hpre, Pt=None, amax=None, stamps=None, *, opt: St
 
 
 def convnet_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, metrics, W1row, Pt, dW1, dwc, dbc,
-                dW2=None, db2=None, db1=None, B=None, stamps=None, opt: BwdOpt | None = None, cpart=None):
+                dW2=None, db2=None, db1=None, B=None, stamps=None, opt: BwdOpt | None = None, cpart=None,
+                push: XgPush | None = None):
     """Trunk backward with the classifier head fused in: from this step's Dense(64) pre-activation
     ``hpre`` [B, 64] (f32) every workgroup recomputes the head (loss, dlogits, Dense(64) input gradient)
     and runs the trunk backward; ``hzero`` (the other parity buffer) is zeroed for the next forward.
@@ -230,7 +239,9 @@ def convnet_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, me
     Plain (``opt`` None): dW1 stored, conv grads atomically added, dW2 / db2 / db1 added, metrics
     accumulated.  ``opt`` (fused step): the updates are applied instead (see ``BwdOpt``).
     ``cpart`` (deterministic mode): the conv gradients are stored per workgroup there instead of added
-    atomically; ``convnet_cgrad_reduce`` sums them in order."""
+    atomically; ``convnet_cgrad_reduce`` sums them in order.  ``push`` (float32 form, plain step): dW1 is
+    stored into the xGMI owners' contribution areas of the next all-reduce call instead of into ``dW1``
+    (the fused data-parallel exchange)."""
     B = x.shape[0] if B is None else B
     H, W = x.shape[1], x.shape[2]
     Kf = ((H - 2) // 2) * ((W - 2) // 2) * 32
@@ -247,12 +258,14 @@ def convnet_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, me
          and hzero.shape == hpre.shape and hzero.is_contiguous(), "convnet_bwd: hpre / hzero")
     _req(labels.dtype == torch.int32 and labels.numel() >= B, "convnet_bwd: int32 labels")
     _req(W2.is_contiguous() and b2.numel() == C and (b1 is None or b1.numel() == 64), "convnet_bwd: head variables")
+    _req(push is None or f32, "convnet_bwd: the fused exchange is implemented for the float32 form")
     fn = N.hip().tde_convnet_bwd_f32 if f32 else N.hip().tde_convnet_bwd
     rc = fn(_P(x), _P(amax), amax.shape[-1], _P(hpre), _P(hzero), hp.shape[0], hp.stride(0),
             _P(b1), _P(W2), _P(b2), C,
             int(pre_relu), _P(labels), float(scale), _P(metrics), _P(W1row), W1row.stride(0),
             _P(Pt), Pt.stride(0), _P(dW1), _P(dwc), _P(dbc), _P(dW2), _P(db2), _P(db1), B, H,
-            W, _P(stamps), _ct.byref(opt) if opt is not None else None, _P(cpart), _s())
+            W, _P(stamps), _ct.byref(opt) if opt is not None else None, _P(cpart),
+            *((_ct.byref(push) if push is not None else None,) if f32 else ()), _s())
     N.check(rc, "tde_convnet_bwd_f32" if f32 else "tde_convnet_bwd")
 
 

@@ -308,6 +308,8 @@ class XgmiCommunicator(Communicator):
             self._free()
             raise RuntimeError(f"xGMI peer mapping failed: {errs}")
         self.peers = (C.c_void_p * self.world)(*peers)
+        tc = int(os.environ.get("TDE_XGMI_TRACE", "0") or 0)
+        self.trace = [_xg_trace_alloc(self.lib, self.device, self.epoch.value, tc)] if tc > 0 else None
 
     def nblocks(self, M):
         if self.nblocks_override:
@@ -348,6 +350,12 @@ class XgmiCommunicator(Communicator):
         if rc != 0:
             raise RuntimeError(f"tde_xgmi_all_reduce_apply failed ({rc})")
 
+    def push_spec(self, M, off):
+        """``XgPush`` for a producer kernel that stores bucket elements [off, ...) of an M-element bucket
+        straight into the owners' contribution areas of the next ``all_reduce_apply_`` call."""
+        return _push_spec(self.lib, M, self.max_elems, self.peers, self.epoch.value, self.rank, self.world,
+                          self.nblocks(M), off)
+
     def broadcast_(self, tensors, root=0):
         return self.fallback.broadcast_(tensors, root)
 
@@ -374,6 +382,8 @@ class XgmiCommunicator(Communicator):
         for m in getattr(self, "_opened", []):
             self.lib.tde_xgmi_close(m)
         self._opened = []
+        if getattr(self, "trace", None) and self.epoch:
+            self.lib.tde_xgmi_set_trace(self.epoch.value, None, 0)
         if self.window:
             self.lib.tde_xgmi_free(self.window, self.epoch, self.err)
         self.window = self.epoch = self.err = C.c_void_p()
@@ -403,6 +413,47 @@ class XgmiCommunicator(Communicator):
         ok = ok and self.lib.tde_xgmi_error(self.err) == 0
         self.timeout_ticks = saved
         return ok
+
+
+def _push_spec(lib, M, max_elems, peers, epoch, rank, world, nblocks, off):
+    from ..ops.kernels import XgPush
+    sp = XgPush()
+    rc = lib.tde_xgmi_push_spec(int(M), int(max_elems), peers, epoch, int(rank), int(world), int(nblocks), int(off),
+                                C.byref(sp))
+    if rc != 0:
+        raise RuntimeError(f"tde_xgmi_push_spec failed ({rc})")
+    return sp
+
+
+def _xg_trace_alloc(lib, device, epoch_ptr, calls):
+    """Diagnostics (TDE_XGMI_TRACE=<calls>): a device buffer in which every launch of the rank whose
+    epoch word is ``epoch_ptr`` records per-block phase timestamps (csrc/comm/xgmi_allreduce.hip,
+    XgArgs::trace), ring-indexed by call.  Returned tensor: [calls, max_blocks, words] int64."""
+    words = lib.tde_xgmi_trace_words()
+    buf = torch.zeros((calls, lib.tde_xgmi_max_blocks(), words), dtype=torch.int64, device=device)
+    lib.tde_xgmi_set_trace(epoch_ptr, buf.data_ptr(), calls)
+    return buf
+
+
+def xg_trace_records(buf, nblocks):
+    """Decode a trace buffer into per-call dicts (host copy; call after a device sync).  Blocks of a
+    launch with ``nblocks`` chunks occupy slots [0, nblocks) of their call."""
+    t = buf.cpu().numpy()
+    out = []
+    for c in range(t.shape[0]):
+        rec = t[c, :nblocks]
+        if not rec[:, 0].any():
+            continue
+        info = rec[:, 7]
+        out.append({
+            "epoch": int(rec[:, 0].max()),
+            "start": [int(v) for v in rec[:, 1]], "pub1": [int(v) for v in rec[:, 2]],
+            "arr1": [int(v) for v in rec[:, 3]], "pub2": [int(v) for v in rec[:, 4]],
+            "arr2": [int(v) for v in rec[:, 5]], "end": [int(v) for v in rec[:, 6]],
+            "miss1": [int(v) & 0xFF for v in info], "miss2": [(int(v) >> 8) & 0xFF for v in info],
+            "xcc": [(int(v) >> 16) & 0xFF for v in info], "cu": [(int(v) >> 24) & 0xF for v in info],
+            "se": [(int(v) >> 28) & 0x7 for v in info]})
+    return sorted(out, key=lambda r: r["epoch"])
 
 
 class PeerXgmiCommunicator(Communicator):
@@ -526,12 +577,20 @@ class PeerXgmiCommunicator(Communicator):
                     break
             else:
                 self.groups.append([i])
+        # a group launch gives its j-th replica kernel rank rank0 + grp[0] + j: every group must be a
+        # contiguous run of replicas (gpu:0,gpu:1,gpu:0,gpu:1 would give two replicas one rank)
+        if any(grp != list(range(grp[0], grp[0] + len(grp))) for grp in self.groups):
+            self._free()
+            raise RuntimeError(f"xGMI replica groups must be contiguous runs of one device, got {self.groups}")
         self._gargs = []
         for grp in self.groups:
             flat = [p for i in grp for p in peers[i]]
             self._gargs.append(((C.c_void_p * len(flat))(*flat), (C.c_void_p * len(grp))(*[self.epochs[i] for i in grp]),
                                 (C.c_void_p * len(grp))(*[self.errs[i] for i in grp])))
         self._side = [torch.cuda.Stream(self.devices[grp[0]]) for grp in self.groups]
+        tc = int(os.environ.get("TDE_XGMI_TRACE", "0") or 0)
+        self.trace = [_xg_trace_alloc(self.lib, d, e, tc) for d, e in zip(self.devices, self.epochs)] \
+            if tc > 0 else None
 
     def nblocks(self, M, nloc=1):
         """Chunks per rank.  A launch carrying several local ranks keeps its whole grid within the
@@ -571,6 +630,12 @@ class PeerXgmiCommunicator(Communicator):
                 sp, s)
         if rc != 0:
             raise RuntimeError(f"tde_xgmi_all_reduce_group failed ({rc})")
+
+    def push_spec(self, i, M, off):
+        """``XgPush`` of local replica ``i`` (see ``XgmiCommunicator.push_spec``)."""
+        grp = next(g for g in self.groups if i in g)
+        return _push_spec(self.lib, M, self.max_elems, self.peers[i], self.epochs[i], self.rank0 + i, self.world,
+                          self.nblocks(M, len(grp)), off)
 
     def all_reduce_(self, tensors, op="sum"):
         if len(tensors) != self.n_local or not all(self.handles(t, op, i) for i, t in enumerate(tensors)) or \
@@ -614,6 +679,9 @@ class PeerXgmiCommunicator(Communicator):
         for m in self._opened:
             self.lib.tde_xgmi_close(m)
         self._opened = []
+        if getattr(self, "trace", None):
+            for e in self.epochs:
+                self.lib.tde_xgmi_set_trace(e, None, 0)
         for w, e, x in zip(self.windows, self.epochs, self.errs):
             self.lib.tde_xgmi_free(w, e, x)
         self.windows, self.epochs, self.errs = [], [], []

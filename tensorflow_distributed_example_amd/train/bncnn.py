@@ -51,6 +51,8 @@ N.register_hip({
     "tde_bncnn_conv_bwd": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp]),
     # n, cnt, part, out, len, opt, stream
     "tde_bncnn_reduce": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp]),
+    # B, D, rate, seed, iter, layer_id, out, stream
+    "tde_bncnn_dropout_mask": (_i, [_i, _i, C.c_float, C.c_ulonglong, _vp, _i, _vp, _vp]),
 })
 
 
@@ -283,6 +285,18 @@ class BnCnnPlan(ReplicaPlan):
             int(self.softmax), _P(self.dwh_part) if train else None, _P(self.dbh_part) if train else None,
             _P(self.gh) if train else None, _P(self.gstat) if train else None, N.stream_ptr())
         N.check(rc, "tde_bncnn_head")
+
+    def dropout_mask(self, B=None):
+        """Debug export: the [B, D] keep scales (1/(1-rate) kept, 0 dropped) the head applies at the
+        current step counter (read on the device, so call it after the step's forward advanced it)."""
+        B = self.B if B is None else B
+        if self.drop is None or not self.drop.rate > 0:
+            return torch.ones(B, self.D, dtype=torch.float32, device=self.device)
+        out = torch.empty(B, self.D, dtype=torch.float32, device=self.device)
+        rc = self.lib.tde_bncnn_dropout_mask(B, self.D, float(self.drop.rate), self.drop_seed, _P(self.iterations), 0,
+                                             _P(out), N.stream_ptr())
+        N.check(rc, "tde_bncnn_dropout_mask")
+        return out
 
     # ------------------------------------------------------------------ plan interface
     def _check_input(self, x, B):

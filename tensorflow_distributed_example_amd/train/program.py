@@ -401,6 +401,10 @@ class ConvNetPlan(ReplicaPlan):
         self.pend = torch.zeros(2, dtype=torch.int32, device=dev)
         self.iter_prev = torch.zeros(1, dtype=torch.int64, device=dev)
         self._fopt = self._bopt = self._flush = None
+        # step mode "xgmi" with the fused exchange (set_push): the backward stores dW1 straight into the
+        # xGMI owners' contribution areas; _pushed marks that the step's launch did so (xg_apply_spec)
+        self._push = None
+        self._pushed = False
 
     # ------------------------------------------------------------------ fused step modes
     def supports_step_mode(self, mode):
@@ -421,6 +425,8 @@ class ConvNetPlan(ReplicaPlan):
 
     def set_step_mode(self, mode):
         super().set_step_mode(mode)
+        if mode != "xgmi":
+            self._push = None
         self._fopt = self._bopt = self._flush = None
         self._slots = (None, None)
         if mode == "plain":
@@ -457,6 +463,21 @@ class ConvNetPlan(ReplicaPlan):
             fl.g = self._gconv(q)
             self._flush.append(fl)
 
+    def push_range(self):
+        """Bucket range the backward can push into the xGMI owners itself (the Dense(64) kernel's dW1:
+        99.7 % of the gradient bytes), or None when this plan form cannot."""
+        if not self.f32 or self.det:
+            return None
+        seg = self.store.segments[self.names["w1"]]
+        return seg.offset, seg.offset + seg.numel
+
+    def set_push(self, spec):
+        """Fused data-parallel exchange (step mode "xgmi"): ``spec`` is the communicator's ``XgPush`` for
+        this replica (None: dW1 to the local bucket, the all-reduce pushes it)."""
+        if spec is not None and (self.step_mode != "xgmi" or self.push_range() is None):
+            raise ValueError("the fused exchange needs step mode 'xgmi' and the float32 plan")
+        self._push = spec
+
     def _opt_key(self):
         o = self.optimizer
         return (o.kind_id, float(o.learning_rate), tuple(sorted(o.hparams().items())))
@@ -474,8 +495,11 @@ class ConvNetPlan(ReplicaPlan):
         seg = st.segments[self.names["w1"]]
         K = self.K
         if self.f32:   # no shadow: the all-reduce updates the f32 master weights only
+            # the step's backward pushed dW1 itself (a replica without data this step pushed nothing)
+            lo, hi = self.push_range() if (self._push is not None and self._pushed) else (0, 0)
+            self._pushed = False
             return K.XgApply(opt.kind_id, float(opt.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"],
-                             K._P(st.w), K._P(m), K._P(v), K._P(self.iterations), None, 0, 0, None, 0, 0)
+                             K._P(st.w), K._P(m), K._P(v), K._P(self.iterations), None, 0, 0, None, 0, 0, lo, hi)
         return K.XgApply(opt.kind_id, float(opt.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"],
                          K._P(st.w), K._P(m), K._P(v), K._P(self.iterations), K._P(self.W1row), seg.offset,
                          seg.offset + seg.numel, K._P(self.W1col), self.Hd,
@@ -519,10 +543,12 @@ class ConvNetPlan(ReplicaPlan):
         self._forward(x, B, self.hpre2[q], True, self._fopt[q] if local else None, train=True, hrep=self.hrep)
         # launch 2: head + trunk backward (fused step: the updates too)
         dwc, dbc = self._gconv_views(q) if local else (self._g("wc"), self._g("bc"))
+        push = self._push if self.step_mode == "xgmi" else None
         K.convnet_bwd(x, self.amax, self.hpre2[q], self.hpre2[1 - q], self._v("b1"), self._v("w2"), self._v("b2"), y,
                       scale=self.scale, pre_relu=self.pre_relu, metrics=self.metrics, W1row=self.W1row, Pt=self.Pt,
                       dW1=self._g("w1"), dwc=dwc, dbc=dbc, dW2=self._g("w2"), db2=self._g("b2"), db1=self._g("b1"),
-                      B=B, opt=self._bopt[q] if local else None, cpart=self.cpart)
+                      B=B, opt=self._bopt[q] if local else None, cpart=self.cpart, push=push)
+        self._pushed = push is not None
         if self.det:
             K.convnet_cgrad_reduce(self.cpart, self.n_cpart, dwc, dbc)
         self.parity = 1 - q

@@ -138,6 +138,7 @@ class Program:
         self.buckets = self._plan_buckets() if training else None
         self._comm_stream = torch.cuda.Stream(self.devices[0]) if self.buckets else None
         self.comm_applies = False
+        self.exchange = "post_backward" if self.comm is not None else "none"
         if training:
             self._pick_step_mode()
 
@@ -154,6 +155,7 @@ class Program:
                 for p in self.plans:
                     p.set_step_mode("xgmi")
                 self.comm_applies = True
+                self._setup_push()
             return
         if len(self.plans) != 1:
             return
@@ -164,6 +166,23 @@ class Program:
             plan.set_step_mode("xgmi")
             self.comm_applies = True
             self.grad_comm = self.comm
+            self._setup_push()
+
+    def _setup_push(self):
+        """Fused data-parallel exchange (TDE_XGMI_PUSH=0 disables): a plan whose backward can store its
+        big weight gradient straight into the xGMI owners' windows does so, and the all-reduce launch
+        after it only pushes the rest of the bucket — the exchange's push phase overlaps the backward."""
+        self.exchange = "post_backward"
+        if os.environ.get("TDE_XGMI_PUSH", "1") == "0" or not hasattr(self.comm, "push_spec"):
+            return
+        if not all(hasattr(p, "push_range") and p.push_range() is not None for p in self.plans):
+            return
+        for i, p in enumerate(self.plans):
+            lo, _ = p.push_range()
+            M = p.store.g.numel()
+            spec = self.comm.push_spec(i, M, lo) if self.per_replica else self.comm.push_spec(M, lo)
+            p.set_push(spec)
+        self.exchange = "fused_push"
 
     def _route_grads(self):
         """The xGMI kernel keeps the bucket over a slightly faster RCCL only because it can also apply the

@@ -58,9 +58,10 @@ def _data(B, seed):
     return x, y
 
 
-def _oracle(plan, x, y, B):
+def _oracle(plan, x, y, B, drop_mask=None):
     """float64 autograd of the plan's model at the store's weights; ReLU decisions from the plan's f32
-    pre-activations (after plan.train_step).  Returns ({var: grad}, {moving var: new value}, loss)."""
+    pre-activations (after plan.train_step); ``drop_mask`` [B, D] (keep scales) applied after the dense
+    BN's ReLU when given.  Returns ({var: grad}, {moving var: new value}, loss)."""
     st = plan.store
     dd = torch.float64
     W = {n: st.view(n).detach().to(dd).clone().requires_grad_(st.segments[n].trainable) for n in st.order}
@@ -90,6 +91,8 @@ def _oracle(plan, x, y, B):
     sv = plan.bnd["saved"]
     mask = ((h32 - sv[: plan.D]) * sv[plan.D:] + st.view(f"{bnl.name}/beta")) > 0
     a = pre * mask
+    if drop_mask is not None:
+        a = a * drop_mask[:B].to(dd)
     moving[f"{bnl.name}/moving_mean"] = W[f"{bnl.name}/moving_mean"] * bnl.momentum + mean.detach() * (1 - bnl.momentum)
     moving[f"{bnl.name}/moving_variance"] = W[f"{bnl.name}/moving_variance"] * bnl.momentum + var.detach() * (
         1 - bnl.momentum)
@@ -288,3 +291,55 @@ def test_bncnn_fused_reduce_optimizer_matches_separate_launch(kind):
     assert torch.equal(wp, wl), float((wp - wl).abs().max())
     for k in sp:
         assert torch.equal(sp[k], sl[k]), k
+
+
+@pytest.mark.parametrize("B", [128, 50])
+def test_bncnn_dropout_matches_float64_with_the_plan_mask(B):
+    """Dropout(0.5) of Model B as the reference trains it (mnist_keras_distributed.py:106): the fused head's
+    Philox keep mask (debug export, plan.dropout_mask) is the host Philox4x32-10 mask bit for bit
+    (ops/philox.py), its keep fraction is within binomial bounds, and every gradient matches the float64
+    oracle that applies that mask with the x2 scale <= 1e-5 (so the forward and the backward used the same
+    mask); over 2 steps the mask changes.  Evaluation / prediction without quirk Q4 apply no mask."""
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.ops.philox import keep_scales
+    from tensorflow_distributed_example_amd.train import program as PG
+    m = _model_b(tde, rate=0.5)
+    st = m._store
+    plan = PG.make_plan(m, st, DEV, 128, 128, m.optimizer, m.loss)
+    assert plan.kind == "fused_bncnn" and plan.drop is not None
+    masks = []
+    for step in range(2):
+        x, y = _data(128, 40 + step)
+        before = {n: st.view(n).detach().double().clone() for n in st.order}
+        st.g.zero_()
+        plan.train_step(x, y, B)
+        mask = plan.dropout_mask(B)
+        torch.cuda.synchronize()
+        it = int(plan.iterations.item())
+        host = keep_scales(0.5, plan.drop_seed, it, 0, B * plan.D).reshape(B, plan.D)
+        assert np.array_equal(mask.cpu().numpy(), host), "device mask != host Philox4x32-10"
+        frac = float((mask > 0).double().mean())
+        n = B * plan.D
+        assert abs(frac - 0.5) < 5 * np.sqrt(0.25 / n), frac
+        assert set(torch.unique(mask).tolist()) <= {0.0, 2.0}
+        masks.append(mask.clone())
+        after = {n_: st.view(n_).detach().clone() for n_ in st.order}
+        for n_ in st.order:
+            st.view(n_).copy_(before[n_])
+        grads, moving, loss, _ = _oracle(plan, x, y, B, drop_mask=mask)
+        for n_ in st.order:
+            st.view(n_).copy_(after[n_])
+        for n_, gr in grads.items():
+            assert _rel(st.grad(n_), gr) < 1e-5, (step, n_, _rel(st.grad(n_), gr))
+        for n_, v in moving.items():
+            assert _rel(st.view(n_), v) < 1e-6, (step, n_, _rel(st.view(n_), v))
+        plan.apply()
+        torch.cuda.synchronize()
+    assert not torch.equal(masks[0], masks[1])
+    # inference without the forced learning phase: moving statistics and NO dropout mask
+    ev = PG.make_plan(m, st, DEV, 64, 64, None, m.loss)
+    xe, _ = _data(64, 50)
+    probs = ev.predict(xe, 64).clone()
+    ref = m(xe.cpu().numpy())
+    ref = (ref if torch.is_tensor(ref) else torch.as_tensor(np.asarray(ref))).to(DEV, torch.float64)
+    assert _rel(probs, ref) < 1e-5, _rel(probs, ref)

@@ -182,3 +182,26 @@ def test_device_feed_row_eligibility():
     from tensorflow_distributed_example_amd.train.device_feed import DeviceFeed
     assert DeviceFeed.row_ok(784, torch.bfloat16) and DeviceFeed.row_ok(785, torch.float32)
     assert not DeviceFeed.row_ok(785, torch.bfloat16) and not DeviceFeed.row_ok(3, torch.bfloat16)
+
+
+def test_philox_known_answers_and_keep_fraction():
+    """ops/philox.py (the host twin of the fused plans' dropout generator) reproduces the Random123
+    Philox4x32-10 known-answer vectors; keep scales are exactly 0 or 1/(1-rate) with a binomial keep
+    fraction."""
+    from tensorflow_distributed_example_amd.ops.philox import keep_scales, philox4x32_10
+    kat = [(([0, 0, 0, 0], [0, 0]), [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]),
+           (([0xFFFFFFFF] * 4, [0xFFFFFFFF] * 2), [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]),
+           (([0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344], [0xA4093822, 0x299F31D0]),
+            [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1])]
+    for (ctr, key), want in kat:
+        assert [int(v) for v in philox4x32_10(ctr, key)] == want
+    n = 128 * 200
+    for rate in (0.5, 0.3):
+        k = keep_scales(rate, 0x1234_5678_9ABC, 7, 0, n)
+        keep = np.float32(1) - np.float32(rate)
+        assert set(np.unique(k)) <= {np.float32(0), np.float32(1) / keep}
+        frac = float((k > 0).mean())
+        assert abs(frac - (1 - rate)) < 5 * np.sqrt(rate * (1 - rate) / n)
+    # a new step (or layer, or seed) draws a new mask
+    a, b = keep_scales(0.5, 1, 1, 0, n), keep_scales(0.5, 1, 2, 0, n)
+    assert (a != b).mean() > 0.4
