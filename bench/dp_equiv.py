@@ -83,6 +83,7 @@ def main():
         np.savez(a.out, **out)
         print(f"[dp_equiv] strategy={a.strategy} replicas={n} plan={prog.plan_kind} graph={prog.use_graph} "
               f"comm={type(strategy.comm).__name__} step_mode={prog.plans[0].step_mode} "
+              f"exchange={getattr(prog, 'exchange', 'none')} "
               f"replicas_identical={same} loss={logs['loss']:.6f}", flush=True)
 
 

@@ -29,6 +29,7 @@
 // Gradients land in the replica's flat fp32 bucket (one all-reduce for data parallelism), then the
 // multi-tensor optimizer kernel applies them.
 #include "tde_common.h"
+#include "tde_philox.h"
 #include "tde_optim.h"
 
 namespace tde {
@@ -497,18 +498,7 @@ __global__ __launch_bounds__(NTB) void dense_fwd_kernel(DenseFwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Philox4x32-10 (counter-based: the dropout mask is a function of (element, step, layer))
-__device__ __forceinline__ uint4 philox(uint4 c, uint2 k) {
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    const unsigned lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-    const unsigned lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
-    c = uint4{hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0};
-    k.x += 0x9E3779B9u;
-    k.y += 0xBB67AE85u;
-  }
-  return c;
-}
+// Philox4x32-10: tde_philox.h (counter-based: masks are regenerated, never stored)
 // The keep scales of the 4 elements e0 .. e0+3 (e0 % 4 == 0): one Philox call (the same values as
 // keep_scale of each element).
 __device__ __forceinline__ float4 keep_scale4(float rate, unsigned long long seed, long long it, int layer, long long e0) {

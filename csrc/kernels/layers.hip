@@ -34,6 +34,7 @@
 //   bias/ReLU backward with the bias-grad column sum, and a general softmax
 //   cross-entropy (+accuracy, +dlogits, +probabilities) for any class count.
 #include "tde_common.h"
+#include "tde_philox.h"
 
 #include <initializer_list>
 
@@ -1090,18 +1091,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p_) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Philox4x32-10 (counter-based: dropout masks are regenerated, never stored)
-__device__ __forceinline__ uint4 philox(uint4 c, uint2 k) {
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    const unsigned lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-    const unsigned lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
-    c = uint4{hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0};
-    k.x += 0x9E3779B9u;
-    k.y += 0xBB67AE85u;
-  }
-  return c;
-}
+// Philox4x32-10: tde_philox.h (counter-based: masks are regenerated, never stored)
 
 struct Drop {
   float rate;  // 0 = off

@@ -32,6 +32,7 @@ import torch
 from .. import backend as Kb
 from ..models import layers as L
 from ..ops import layer_ops as O
+from ..ops import layer_ops32 as O32
 from . import program as PG
 
 bf16 = torch.bfloat16
@@ -108,27 +109,25 @@ class _Stage:
         return [n for n in (getattr(self, "wname", None), getattr(self, "bname", None)) if n]
 
 
-_warned_bf16 = set()
-
-
 class LayerwisePlan(PG.ReplicaPlan):
+    """Precision follows the global policy: ``float32`` (the reference's) runs every stage on the f32
+    kernel forms (csrc/kernels/layers_f32.hip: f32 activations and gradients, the f32 master kernels read
+    in place on the exact-f32 MFMA); ``mixed_bfloat16`` on the bf16 forms (csrc/kernels/layers.hip: bf16
+    activations, bf16 weight shadows refreshed by the optimizer, f32 master weights)."""
     kind = "layerwise"
-    compute_dtype = "bf16"   # the layer-wise kernel library computes in bf16 (fp32 master weights)
-    # inputs staged as bf16 (Keras mixed_bfloat16 casts them at the first layer anyway): no per-step
-    # cast launch; TDE_BF16_INPUT=0 keeps f32 staging + the cast kernel
-    input_dtype = bf16 if os.environ.get("TDE_BF16_INPUT", "1") != "0" else torch.float32
 
     def __init__(self, model, store, device, batch, global_batch, optimizer, loss):
         super().__init__(model, store, device, batch, global_batch, optimizer)
         self.loss = loss
         self.model = model
+        self.f32 = Kb.global_policy().compute_dtype == torch.float32
+        self.compute_dtype = "fp32" if self.f32 else "bf16"
+        self.adt = torch.float32 if self.f32 else bf16          # activation / activation-gradient dtype
+        self.sdt = torch.float64 if self.f32 else torch.float32  # BN backward-sum dtype
+        # bf16: inputs staged as bf16 (Keras mixed_bfloat16 casts them at the first layer anyway), no per-step
+        # cast launch; TDE_BF16_INPUT=0 keeps f32 staging + the cast kernel.  f32: the ring is read in place.
+        self.input_dtype = (torch.float32 if self.f32 or os.environ.get("TDE_BF16_INPUT", "1") == "0" else bf16)
         self._compile()
-        if Kb.global_policy().compute_dtype == torch.float32 and model.name not in _warned_bf16:
-            # never silent: the float32 policy asked for exact f32, this plan computes in bf16
-            _warned_bf16.add(model.name)
-            import warnings
-            warnings.warn(f"model {model.name!r}: the layer-wise HIP plan computes in bf16 (mixed_bfloat16) under "
-                          "the float32 policy; set_global_policy('mixed_bfloat16') states that explicitly")
         self._alloc()
         # TDE_WGRAD_STREAM=1: weight gradients on a side stream, concurrent with the input-gradient chain
         # (joined at the end of the backward).  Off by default: measured slower in the captured step
@@ -278,7 +277,7 @@ class LayerwisePlan(PG.ReplicaPlan):
         self.stages = stages
         # the fused head also takes over the ReLU mask and bias gradient of a Dense that feeds only it
         head = stages[-1]
-        if isinstance(head, _Head) and head.fused and len(stages) > 1:
+        if isinstance(head, _Head) and head.fused and len(stages) > 1 and not self.f32:
             prev = stages[-2]
             if (isinstance(prev, _Gemm) and not prev.conv and prev.out.root() is head.inp.root()
                     and len(T[prev.out.id].consumers) == 1 and not prev.stats):
@@ -286,7 +285,7 @@ class LayerwisePlan(PG.ReplicaPlan):
         # BatchNorm + ReLU whose only consumer is a MaxPool (the ResNet stem): one pass reads the conv output
         # and writes the pooled output + argmax; the BN output itself is never stored (its backward recomputes
         # z from the conv output).  TDE_BN_POOL=0 keeps the two launches.
-        if os.environ.get("TDE_BN_POOL", "1") != "0":
+        if os.environ.get("TDE_BN_POOL", "1") != "0" and not self.f32:
             for i, st in enumerate(stages[:-1]):
                 nxt = stages[i + 1]
                 if (isinstance(st, _Elementwise) and st.bn and st.relu and st.res is None and st.drop.rate == 0
@@ -305,13 +304,13 @@ class LayerwisePlan(PG.ReplicaPlan):
 
     def _alloc(self):
         B, dev = self.B, self.device
-        self.x_bf = torch.zeros(B * self.T[0].numel, dtype=bf16, device=dev)
+        self.x_bf = torch.zeros(B * self.T[0].numel, dtype=self.adt, device=dev)
         self.T[0].buf = self.x_bf
         for t in self.T.values():
             if t.id == 0 or t.alias is not None:
                 continue
-            t.buf = torch.zeros(B * t.numel, dtype=bf16, device=dev)
-            t.grad = torch.zeros(B * t.numel, dtype=bf16, device=dev)
+            t.buf = torch.zeros(B * t.numel, dtype=self.adt, device=dev)
+            t.grad = torch.zeros(B * t.numel, dtype=self.adt, device=dev)
         for t in self.T.values():
             if t.alias is not None:
                 t.buf, t.grad = t.root().buf, t.root().grad
@@ -323,6 +322,9 @@ class LayerwisePlan(PG.ReplicaPlan):
         # split-K weight gradients store per-split partials here and reduce them in one pass
         wneed = max([st.wscratch_need(B) for st in self.stages if hasattr(st, "wscratch_need")] + [0])
         self.wscratch = torch.empty(wneed, dtype=torch.float32, device=dev) if wneed else None
+        # f32 forms: split-K weight-gradient partials (summed in split order by the second launch)
+        pneed = max([st.wpart_need(B) for st in self.stages if hasattr(st, "wpart_need")] + [0]) if self.f32 else 0
+        self.wpart = torch.empty(pneed, dtype=torch.float32, device=dev) if pneed else None
 
     # ------------------------------------------------------------------ plan interface
     def on_weights_loaded(self):
@@ -330,6 +332,9 @@ class LayerwisePlan(PG.ReplicaPlan):
 
     def _input(self, x, B):
         n = B * self.T[0].numel
+        if self.f32:
+            self._bind_input(x.reshape(-1)[:n].contiguous() if x.dtype == torch.float32 else x.float().reshape(-1)[:n])
+            return
         if x.dtype == bf16:
             # the Program's input ring already holds bf16 (cast once per execution at staging): the
             # first layer reads the ring slot directly
@@ -423,10 +428,17 @@ class _Gemm(_Stage):
         self.conv = isinstance(layer, L.Conv2D)
         need_dgrad = tin.root().id != 0
         self.need_dgrad = need_dgrad
-        self.shadows = {self.wname: ("row", "col") if need_dgrad else ("col",)}
+        self.f32 = plan.f32
+        self.shadows = {} if self.f32 else {self.wname: ("row", "col") if need_dgrad else ("col",)}
         self.small_fwd = self.small_dgrad = self.small_wgrad = False
         self.use_im2col = self.use_stem_pack = False
-        if self.conv:
+        if self.conv and self.f32:   # the f32 implicit GEMM covers every geometry itself
+            H, W_, C = tin.shape
+            Ho, Wo, Co = tout.shape
+            (pt, _), (pl, _) = layer.pads(tin.shape)
+            self.geo = O.ConvGeom(plan.B, H, W_, C, Ho, Wo, Co, layer.kernel_size[0], layer.kernel_size[1],
+                                  layer.strides[0], layer.strides[1], pt, pl)
+        elif self.conv:
             H, W_, C = tin.shape
             Ho, Wo, Co = tout.shape
             (pt, _), (pl, _) = layer.pads(tin.shape)
@@ -461,7 +473,15 @@ class _Gemm(_Stage):
         self.dz = None
         self.act_done = False   # the consumer's launch already applied the ReLU mask / bias gradient
 
+    def wpart_need(self, B):
+        if self.conv:
+            g = self.geo.with_batch(B)
+            return O32.wgrad_part_elems(g.K, g.Co, g.B * g.Ho * g.Wo)
+        return O32.wgrad_part_elems(self.W.shape[0], self.W.shape[1], self.inp.rows(B))
+
     def scratch_need(self, B):
+        if self.f32:
+            return 0
         if self.conv:
             g = self.geo.with_batch(B)
             return max(O.scratch_elems(g.B * g.Ho * g.Wo, g.Co, g.K),
@@ -470,6 +490,8 @@ class _Gemm(_Stage):
         return max(O.scratch_elems(rows, out, fin), O.scratch_elems(rows, fin, out) if self.need_dgrad else 0)
 
     def wscratch_need(self, B):
+        if self.f32:
+            return 0
         if self.conv:
             g = self.geo.with_batch(B)
             if self.use_im2col or self.small_wgrad:
@@ -494,9 +516,14 @@ class _Gemm(_Stage):
         if self.stats:
             self.colstats = torch.zeros(2 * O.STAT_SLOTS * self.out.C, dtype=torch.float64, device=dev)
         if (self.relu or self.gb is not None) and not self.act_done:
-            self.dz = torch.zeros(B * self.out.numel, dtype=bf16, device=dev)
+            self.dz = torch.zeros(B * self.out.numel, dtype=self.inp_dt(), device=dev)
+
+    def inp_dt(self):
+        return torch.float32 if self.f32 else bf16
 
     def bind_shadows(self, sh):
+        if self.f32:
+            return
         self.Wt = sh.shadow_views[(self.wname, "col")]
         self.Wrow = sh.shadow_views.get((self.wname, "row"))
 
@@ -505,6 +532,14 @@ class _Gemm(_Stage):
 
     def fwd(self, p, B, training, mode="train"):
         cs = self.colstats if (self.stats and training) else None
+        if self.f32:
+            if self.conv:
+                O32.conv_fwd(self.inp.root().buf, self.W, self.out.root().buf, self.geo.with_batch(B), bias=self.b,
+                             relu=self.relu, colstats=cs)
+            else:
+                O32.dense_fwd(self.inp.root().buf, self.W.view(-1, self.W.shape[-1]), self.inp.rows(B),
+                              self.out.root().buf, bias=self.b, relu=self.relu, colstats=cs)
+            return
         if self.conv and self.use_stem_pack:
             g = self.geo.with_batch(B)
             O.stem_pack(self.inp.buf, g, self.xp, self.Wt, self.Wv)
@@ -529,9 +564,20 @@ class _Gemm(_Stage):
     def bwd(self, p, B):
         dout = self.out.root().grad
         if self.dz is not None:
-            O.act_bwd(dout, self.out.root().buf, self.out.rows(B), self.out.C, relu=self.relu, dz=self.dz,
-                      dbias=self.gb)
+            (O32 if self.f32 else O).act_bwd(dout, self.out.root().buf, self.out.rows(B), self.out.C, relu=self.relu,
+                                             dz=self.dz, dbias=self.gb)
             dout = self.dz
+        if self.f32:
+            self._wgrad(p, B, dout)
+            if not self.need_dgrad:
+                return
+            acc = self.accum[self.inp.root().id]
+            if self.conv:
+                O32.conv_dgrad(dout, self.W, self.inp.root().grad, self.geo.with_batch(B), accum=acc)
+            else:
+                O32.dense_dgrad(dout, self.W.view(-1, self.W.shape[-1]), self.inp.root().grad, self.inp.rows(B),
+                                accum=acc)
+            return
         side = p.side_stream
         if side is not None:
             side.wait_stream(torch.cuda.current_stream(p.device))
@@ -554,6 +600,13 @@ class _Gemm(_Stage):
 
     def _wgrad(self, p, B, dout):
         """This layer's weight gradient (all of it on the plan's side stream when there is one)."""
+        if self.f32:
+            if self.conv:
+                O32.conv_wgrad(self.inp.root().buf, dout, self.gW, self.geo.with_batch(B), part=p.wpart)
+            else:
+                O32.dense_wgrad(self.inp.root().buf, dout, self.gW.view(self.W.shape[0], -1), self.inp.rows(B),
+                                part=p.wpart)
+            return
         if self.conv:
             g = self.geo.with_batch(B)
             if self.use_stem_pack:
@@ -618,9 +671,10 @@ class _Elementwise(_Stage):
 
     def alloc(self, B, dev):
         C = self.inp.C
+        self.O = O32 if self.plan.f32 else O
         if self.bn:
             self.saved = torch.zeros(2 * C, dtype=torch.float32, device=dev)
-            self.dstats = torch.zeros(2 * O.STAT_SLOTS * C, dtype=torch.float32, device=dev)
+            self.dstats = torch.zeros(2 * O.STAT_SLOTS * C, dtype=self.plan.sdt, device=dev)
             if self.stats_from_gemm:
                 self.colstats = None   # bound below to the producing GEMM's buffer
             else:
@@ -650,13 +704,13 @@ class _Elementwise(_Stage):
         kw = dict(res=self.res.root().buf if self.res is not None else None, relu=self.relu, drop=drop,
                   iter_offset=0)
         if not self.bn:
-            O.bn_fwd(self.inp.root().buf, self.out.root().buf, R, C, mode=0, **kw)
+            self.O.bn_fwd(self.inp.root().buf, self.out.root().buf, R, C, mode=0, **kw)
             return
         L_ = self.layer
         if training:
             stats = self._stats()
             if not self.stats_from_gemm:
-                O.colstats(self.inp.root().buf, R, C, stats)
+                self.O.colstats(self.inp.root().buf, R, C, stats)
             upd = mode == "train"
             bessel = (R / max(R - 1, 1)) if L_.fused else 1.0
             if self.pool is not None:
@@ -666,7 +720,7 @@ class _Elementwise(_Stage):
                                       mmean=self.mmean if upd else None, mvar=self.mvar if upd else None,
                                       momentum=L_.momentum, bessel=bessel, zero_buf=self.dstats if upd else None)
                 return
-            O.bn_fwd(self.inp.root().buf, self.out.root().buf, R, C, mode=1, stats=stats, saved=self.saved,
+            self.O.bn_fwd(self.inp.root().buf, self.out.root().buf, R, C, mode=1, stats=stats, saved=self.saved,
                      gamma=self.gamma, beta=self.beta, eps=L_.epsilon, mmean=self.mmean if upd else None,
                      mvar=self.mvar if upd else None, momentum=L_.momentum, bessel=bessel,
                      zero_buf=self.dstats if upd else None, **kw)
@@ -675,7 +729,7 @@ class _Elementwise(_Stage):
                                   self.pool.geo.with_batch(B), mode=2, gamma=self.gamma, beta=self.beta,
                                   eps=L_.epsilon, mmean=self.mmean, mvar=self.mvar)
         else:
-            O.bn_fwd(self.inp.root().buf, self.out.root().buf, R, C, mode=2, gamma=self.gamma, beta=self.beta,
+            self.O.bn_fwd(self.inp.root().buf, self.out.root().buf, R, C, mode=2, gamma=self.gamma, beta=self.beta,
                      eps=L_.epsilon, mmean=self.mmean, mvar=self.mvar, **kw)
 
     def bwd(self, p, B):
@@ -690,7 +744,7 @@ class _Elementwise(_Stage):
                           dx_accum=self.accum.get(ir.id, False), dgamma=self.ggamma, dbeta=self.gbeta,
                           zero_fwd=self._stats())
             return
-        O.bn_bwd(self.out.root().grad, ir.buf, R, C, mode=1 if self.bn else 0,
+        self.O.bn_bwd(self.out.root().grad, ir.buf, R, C, mode=1 if self.bn else 0,
                  saved=self.saved if self.bn else None, gamma=self.gamma if self.bn else None,
                  beta=self.beta if self.bn else None, res=rr.buf if rr is not None else None, relu=self.relu,
                  drop=self.drop, iter_offset=-1, dstats=self.dstats if self.bn else None,
@@ -714,9 +768,11 @@ class _MaxPool(_Stage):
         self.geo = O.ConvGeom(plan.B, H, W_, C, Ho, Wo, C, layer.pool_size[0], layer.pool_size[1],
                               layer.strides[0], layer.strides[1], pt, pl)
         self.fused = False  # the producing BN+ReLU stage runs this pool's forward (bn_relu_maxpool_fwd)
+        self.f32 = plan.f32
 
     def alloc(self, B, dev):
         self.idx = torch.zeros(B * self.out.numel, dtype=torch.uint8, device=dev)
+        self.O = O32 if self.f32 else O
 
     def grad_inputs(self):
         return [self.inp] if self.inp.root().id != 0 else []
@@ -724,12 +780,12 @@ class _MaxPool(_Stage):
     def fwd(self, p, B, training, mode="train"):
         if self.fused:
             return
-        O.maxpool_fwd(self.inp.root().buf, self.out.root().buf, self.idx, self.geo.with_batch(B))
+        self.O.maxpool_fwd(self.inp.root().buf, self.out.root().buf, self.idx, self.geo.with_batch(B))
 
     def bwd(self, p, B):
         if self.inp.root().id == 0 or self.fused:
             return
-        O.maxpool_bwd(self.out.root().grad, self.idx, self.inp.root().grad, self.geo.with_batch(B),
+        self.O.maxpool_bwd(self.out.root().grad, self.idx, self.inp.root().grad, self.geo.with_batch(B),
                       accum=self.accum[self.inp.root().id])
 
 
@@ -739,6 +795,7 @@ class _GAP(_Stage):
         self.node_index = tout.producer
         self.HW = tin.shape[0] * tin.shape[1]
         self.C = tin.shape[2]
+        self.O = O32 if plan.f32 else O
 
     def alloc(self, B, dev):
         pass
@@ -747,12 +804,12 @@ class _GAP(_Stage):
         return [self.inp] if self.inp.root().id != 0 else []
 
     def fwd(self, p, B, training, mode="train"):
-        O.gap_fwd(self.inp.root().buf, self.out.root().buf, B, self.HW, self.C)
+        self.O.gap_fwd(self.inp.root().buf, self.out.root().buf, B, self.HW, self.C)
 
     def bwd(self, p, B):
         if self.inp.root().id == 0:
             return
-        O.gap_bwd(self.out.root().grad, self.inp.root().grad, B, self.HW, self.C,
+        self.O.gap_bwd(self.out.root().grad, self.inp.root().grad, B, self.HW, self.C,
                   accum=self.accum[self.inp.root().id])
 
 
@@ -764,6 +821,7 @@ class _Pad(_Stage):
         Ho, Wo, _ = tout.shape
         (t, _), (l, _) = layer.padding
         self.geo = O.ConvGeom(plan.B, H, W_, C, Ho, Wo, C, 1, 1, 1, 1, t, l)
+        self.O = O32 if plan.f32 else O
 
     def alloc(self, B, dev):
         pass
@@ -772,12 +830,12 @@ class _Pad(_Stage):
         return [self.inp] if self.inp.root().id != 0 else []
 
     def fwd(self, p, B, training, mode="train"):
-        O.pad_fwd(self.inp.root().buf, self.out.root().buf, self.geo.with_batch(B))
+        self.O.pad_fwd(self.inp.root().buf, self.out.root().buf, self.geo.with_batch(B))
 
     def bwd(self, p, B):
         if self.inp.root().id == 0:
             return
-        O.pad_bwd(self.out.root().grad, self.inp.root().grad, self.geo.with_batch(B),
+        self.O.pad_bwd(self.out.root().grad, self.inp.root().grad, self.geo.with_batch(B),
                   accum=self.accum[self.inp.root().id])
 
 
@@ -808,9 +866,10 @@ class _Head(_Stage):
         self.C = layer.units
         self.H = tin.shape[0]
         self.W = st.view(self.wname)
-        self.fused = (self.C <= 16 and self.H <= 256 and self.H % 4 == 0
+        self.f32 = plan.f32
+        self.fused = (not self.f32 and self.C <= 16 and self.H <= 256 and self.H % 4 == 0
                       and os.environ.get("TDE_FUSED_HEAD", "1") != "0")
-        self.shadows = {} if self.fused else {self.wname: ("row", "col") if self.need_dgrad else ("col",)}
+        self.shadows = {} if (self.fused or self.f32) else {self.wname: ("row", "col") if self.need_dgrad else ("col",)}
         self.pre = None   # absorbed Dense: its ReLU mask and bias gradient are applied by the head launch
 
     def absorb(self, gemm):
@@ -819,17 +878,20 @@ class _Head(_Stage):
 
     def alloc(self, B, dev):
         self.logits = torch.zeros(B * self.C, dtype=torch.float32, device=dev)
-        self.dlogits = torch.zeros(B * self.C, dtype=bf16, device=dev)
+        self.dlogits = torch.zeros(B * self.C, dtype=torch.float32 if self.f32 else bf16, device=dev)
         self.probs = torch.zeros(B * self.C, dtype=torch.float32, device=dev)
 
     def bind_shadows(self, sh):
-        if self.fused:
+        if self.fused or self.f32:
             return
         self.Wt = sh.shadow_views[(self.wname, "col")]
         self.Wrow = sh.shadow_views.get((self.wname, "row"))
 
     def grad_inputs(self):
         return [self.inp] if self.need_dgrad else []
+
+    def wpart_need(self, B):
+        return O32.wgrad_part_elems(self.H, self.C, B)
 
     def _fused_fwd(self, p, B, mode):
         from ..ops import kernels as K
@@ -853,6 +915,16 @@ class _Head(_Stage):
         if self.fused:
             self._fused_fwd(p, B, mode)
             return
+        if self.f32:
+            O32.dense_fwd(self.inp.root().buf, self.W, B, self.logits, bias=self.b)
+            if mode == "train":
+                O32.xent(self.logits, p._labels, B, self.C, scale=p.scale, dlogits=self.dlogits, metrics=p.metrics,
+                         iterations=p.iterations)
+            elif mode == "eval":
+                O32.xent(self.logits, p._labels, B, self.C, scale=p.scale, metrics=p.metrics)
+            else:
+                O32.xent(self.logits, p._labels, B, self.C, probs=self.probs, probs_are_logits=self.logits_out)
+            return
         O.dense_fwd(self.inp.root().buf, self.Wt, B, logits=self.logits, bias=self.b)
         if mode == "train":
             O.xent(self.logits, p._labels, B, self.C, scale=p.scale, dlogits=self.dlogits, metrics=p.metrics,
@@ -865,6 +937,13 @@ class _Head(_Stage):
     def bwd(self, p, B):
         if self.fused:
             return   # done by the forward's launch
+        if self.f32:
+            if self.gb is not None:
+                O32.act_bwd(self.dlogits, None, B, self.C, relu=False, dbias=self.gb)
+            O32.dense_wgrad(self.inp.root().buf, self.dlogits, self.gW.view(self.H, -1), B, part=p.wpart)
+            if self.need_dgrad:
+                O32.dense_dgrad(self.dlogits, self.W, self.inp.root().grad, B, accum=self.accum[self.inp.root().id])
+            return
         if self.gb is not None:
             O.act_bwd(self.dlogits, None, B, self.C, relu=False, dbias=self.gb)
         O.dense_wgrad(self.inp.root().buf, self.dlogits, self.gW, B, scratch=p.wscratch)
@@ -905,20 +984,24 @@ class _QGrad(torch.autograd.Function):
 
 def emulate_step(plan: LayerwisePlan, x, y, B=None):
     """Numerics oracle for the layer-wise plan: the same stage graph in float64 torch autograd,
-    rounding to bf16 exactly where the plan stores bf16 tensors (activations, their gradients,
-    weight shadows).  Returns {variable: gradient} plus the BN moving statistics after the step.
-    Dropout must be inactive (its Philox stream is not reproduced here)."""
+    rounding to bf16 exactly where the bf16 plan stores bf16 tensors (activations, their gradients,
+    weight shadows; nothing is rounded for the float32 plan).  Returns {variable: gradient} plus the BN
+    moving statistics after the step.  Dropout must be inactive (its Philox stream is not reproduced here)."""
     import torch.nn.functional as F
     B = plan.B if B is None else B
     st = plan.store
     dd = torch.float64
     W = {n: st.view(n).detach().to(dd).clone().requires_grad_(st.segments[n].trainable) for n in st.order}
 
+    f32 = getattr(plan, "f32", False)
+    QR = (lambda t: t) if f32 else _QRound.apply   # noqa: E731
+    QG = (lambda t: t) if f32 else _QGrad.apply    # noqa: E731
+
     def qw(n):
         w = W[n]
-        return w + (w.to(bf16).to(dd) - w).detach()
+        return w if f32 else w + (w.to(bf16).to(dd) - w).detach()
 
-    vals = {0: _QRound.apply(x[:B].to(dd).reshape((B,) + plan.T[0].shape))}
+    vals = {0: QR(x[:B].to(dd).reshape((B,) + plan.T[0].shape))}
 
     def get(t):
         return vals[t.root().id].reshape((B,) + t.shape)
@@ -940,7 +1023,7 @@ def emulate_step(plan: LayerwisePlan, x, y, B=None):
                 o = o + W[stg.bname]
             if stg.relu:
                 o = F.relu(o)
-            vals[stg.out.root().id] = _QRound.apply(o.reshape(B, -1))
+            vals[stg.out.root().id] = QR(o.reshape(B, -1))
         elif isinstance(stg, _Elementwise):
             a = get(stg.inp)
             if stg.drop.rate > 0:
@@ -966,7 +1049,7 @@ def emulate_step(plan: LayerwisePlan, x, y, B=None):
                 z = z + get(stg.res)
             if stg.relu:
                 z = F.relu(z)
-            vals[stg.out.root().id] = _QRound.apply(z.reshape(B, -1))
+            vals[stg.out.root().id] = QR(z.reshape(B, -1))
         elif isinstance(stg, _MaxPool):
             g = stg.geo
             a = get(stg.inp).permute(0, 3, 1, 2)
@@ -976,7 +1059,7 @@ def emulate_step(plan: LayerwisePlan, x, y, B=None):
             o = F.max_pool2d(a, (g.KH, g.KW), (g.sh, g.sw)).permute(0, 2, 3, 1)
             vals[stg.out.root().id] = o.reshape(B, -1)
         elif isinstance(stg, _GAP):
-            vals[stg.out.root().id] = _QRound.apply(get(stg.inp).mean((1, 2)).reshape(B, -1))
+            vals[stg.out.root().id] = QR(get(stg.inp).mean((1, 2)).reshape(B, -1))
         elif isinstance(stg, _Pad):
             g = stg.geo
             a = get(stg.inp)
@@ -991,7 +1074,7 @@ def emulate_step(plan: LayerwisePlan, x, y, B=None):
             if stg.bname:
                 logits = logits + W[stg.bname]
             if not stg.fused:
-                logits = _QGrad.apply(logits)
+                logits = QG(logits)
             loss = F.cross_entropy(logits, y[:B].long(), reduction="sum") * plan.scale
     loss.backward()
     out = {n: W[n].grad for n in st.names(trainable=True)}
