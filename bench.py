@@ -33,7 +33,8 @@ METRIC = "images/sec (whole node) MNIST CNN at 1/2/4/8 MI355X; step time ms"
 MODELS = {
     "mnist_cnn": (64, 16, 0.001, True, (28, 28, 1), METRIC),
     "mnist_bn_cnn": (128, 16, 0.01, False, (784,), METRIC),
-    "lenet5": (128, 16, 0.01, True, (28, 28, 1), "images/sec (whole node) MNIST LeNet-5 CNN bf16 at 1/2/4/8 MI355X; step time ms"),
+    # the LeNet-5 label carries the precision actually run ({dtype}: fp32 by default, bf16 with --dtype bf16)
+    "lenet5": (128, 16, 0.01, True, (28, 28, 1), "images/sec (whole node) MNIST LeNet-5 CNN {dtype} at 1/2/4/8 MI355X; step time ms"),
     "mnist_mlp": (128, 16, 0.01, True, (28, 28, 1), "images/sec (whole node) MNIST dense MLP at 1/2/4/8 MI355X; step time ms"),
     "resnet18": (64, 1, 0.1, True, (224, 224, 3),   # BASELINE.json names this config bf16
                  "images/sec (whole node) synthetic 224x224x3 ResNet-18 bf16 at 1/2/4/8 MI355X; step time ms"),
@@ -95,6 +96,7 @@ def main():
     n = strategy.num_replicas_in_sync
     n_local = strategy.num_local_replicas
     dB, dspe, dlr, from_logits, img, metric = MODELS[a.model]
+    metric = metric.replace("{dtype}", dtype)
     B = a.batch_per_gpu or dB
     GB = B * n
     spe = a.spe or dspe

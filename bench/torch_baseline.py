@@ -130,7 +130,12 @@ def main():
     ap.add_argument("--batch-per-gpu", type=int, default=None)
     ap.add_argument("--graph", action="store_true", help="capture the whole step in a HIP graph")
     ap.add_argument("--channels-last", action="store_true")
+    ap.add_argument("--dtype", choices=("bf16", "fp32"), default="bf16",
+                    help="bf16: torch.autocast bf16; fp32: plain float32 (the reference's precision, TF32 off)")
     a = ap.parse_args()
+    if a.dtype == "fp32":   # like-for-like with our float32 kernels: no reduced-precision math anywhere
+        torch.backends.cuda.matmul.allow_tf32 = False
+        torch.backends.cudnn.allow_tf32 = False
     B0, lr, img, ncls = MODELS[a.model]
     B = a.batch_per_gpu or B0
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -157,7 +162,7 @@ def main():
     sx, sy = xs[0].clone().contiguous(memory_format=mf), ys[0].clone()
 
     def step():
-        with torch.autocast("cuda", dtype=torch.bfloat16):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=a.dtype == "bf16"):
             loss = F.cross_entropy(model(sx), sy)
         loss.backward()
         opt.step()
@@ -205,7 +210,7 @@ def main():
         print(json.dumps({"metric": "images/sec (whole node) torch baseline", "impl": "torch-baseline",
                           "value": round(B * world * a.steps / el, 1), "unit": "images/sec", "n_gpus": world,
                           "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 5),
-                          "dtype": "bf16-autocast", "config": {"model": a.model, "global_batch": B * world,
+                          "dtype": "bf16-autocast" if a.dtype == "bf16" else "fp32", "config": {"model": a.model, "global_batch": B * world,
                                                                "per_gpu_batch": B, "hipgraph": a.graph,
                                                                "channels_last": a.channels_last}}), flush=True)
     if world > 1:

@@ -34,6 +34,8 @@ if [ "$MODE" = all ] || [ "$MODE" = baseline ]; then
   step torch_cnn_graph 600 python bench/torch_baseline.py --model mnist_cnn --steps 2000 --warmup 64 --graph
   step torch_bn_cnn_graph 600 python bench/torch_baseline.py --model mnist_bn_cnn --steps 800 --warmup 64 --graph
   step torch_resnet18 600 python bench/torch_baseline.py --model resnet18 --steps 30 --warmup 5 --channels-last
+  step torch_cnn_graph_fp32 600 python bench/torch_baseline.py --model mnist_cnn --steps 2000 --warmup 64 --graph --dtype fp32
+  step torch_bn_cnn_graph_fp32 600 python bench/torch_baseline.py --model mnist_bn_cnn --steps 800 --warmup 64 --graph --dtype fp32
 fi
 if [ "$MODE" = all ] || [ "$MODE" = micro ]; then
   step micro 300 python bench/micro.py

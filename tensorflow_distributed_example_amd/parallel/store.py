@@ -11,6 +11,7 @@ rendezvous, barriers, heartbeat-based failure detection.
 from __future__ import annotations
 
 import ctypes as C
+import re
 import threading
 import time
 
@@ -88,9 +89,13 @@ class TCPStore:
             raise StoreError("set failed")
 
     def get(self, key: str, timeout=60.0) -> bytes:
-        # the value is fetched whole into a buffer of the last size seen (large control-plane values,
-        # e.g. CPU all-reduce parts, repeat their size: one round trip each)
-        cap = getattr(self, "_cap", 1 << 16)
+        # the value is fetched whole into a buffer of the last size seen for keys of the same family (the key
+        # with its digits masked: round / rank counters vary, the payload kind does not), so large values such
+        # as CPU all-reduce parts take one round trip each while small control-plane values (barrier, agree,
+        # broadcast_json) keep a 64 KiB buffer
+        fam = re.sub(r"\d+", "#", key)
+        caps = self.__dict__.setdefault("_caps", {})
+        cap = caps.get(fam, 1 << 16)
         while True:
             buf = C.create_string_buffer(cap)
             n = self._lib.tde_store_get(self._h, key.encode(), buf, cap, int(timeout * 1000) if timeout else -1)
@@ -100,7 +105,7 @@ class TCPStore:
                 raise StoreError("get failed")
             if n <= cap:
                 return buf.raw[:n]
-            cap = self._cap = n
+            cap = caps[fam] = n
 
     def wait(self, key: str, timeout=60.0):
         rc = self._lib.tde_store_wait(self._h, key.encode(), int(timeout * 1000))

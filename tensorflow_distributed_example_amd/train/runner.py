@@ -127,6 +127,12 @@ class Program:
         self.per_replica = bool(training and cuda and len(self.devices) > 1 and
                                 getattr(self.comm, "per_replica", False) and
                                 all(p.store.g.numel() <= self.comm.max_elems for p in self.plans))
+        if (training and cuda and len(self.devices) > 1 and getattr(self.comm, "per_replica", False)
+                and not self.per_replica):
+            import warnings
+            warnings.warn(f"gradient bucket of {self.plans[0].store.g.numel()} elements exceeds the in-process xGMI "
+                          f"window ({self.comm.max_elems}; TDE_XGMI_MAX_ELEMS raises it): the replicas run eagerly "
+                          "without per-device hipGraphs")
         # replicas grouped by device (the communicator's groups): one stream + one graph per group
         self.groups = list(self.comm.groups) if self.per_replica else None
         self.rstreams = [torch.cuda.Stream(self.devices[g[0]]) for g in self.groups] if self.per_replica else None
