@@ -60,7 +60,7 @@ def main():
     role = task.get("type")
     if role == "ps":
         from tensorflow_distributed_example_amd.parallel.ps import run_ps_server
-        run_ps_server(cfg["cluster"]["ps"][task.get("index", 0)])
+        run_ps_server(cfg["cluster"]["ps"][task.get("index", 0)], index=task.get("index", 0))
         return
     tde.backend.set_random_seed(1)
     rng = np.random.default_rng(5 + int(task.get("index", 0)))
@@ -94,7 +94,9 @@ def main():
                           "images_per_sec": round(rate * a.batch, 1), "trainers": trainers,
                           "ps_tasks": len(cfg.get("cluster", {}).get("ps", [])), "batch": a.batch,
                           "model": a.model, "steps_timed": hook.s1 - hook.s0, "master_local_steps_per_sec":
-                          round(local, 1), "device": str(model._store.device)}), flush=True)
+                          round(local, 1), "device": str(model._store.device), "final_global_step": hook.s1,
+                          "data_plane": "device" if os.environ.get("TDE_PS_DEVICE") == "1" else "tcp"}),
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -79,11 +79,17 @@ class PSServer:
             self._h = None
 
 
-def run_ps_server(address: str, stop_event=None):
-    """Serve variables forever (TF ``server.join()``), or until ``stop_event`` is set."""
+def run_ps_server(address: str, stop_event=None, index: int = 0):
+    """Serve variables forever (TF ``server.join()``), or until ``stop_event`` is set.  With
+    ``TDE_PS_DEVICE=1`` ps task 0 also owns the same-node GPU data plane's window (parallel/ps_device.py)."""
     host, port = address.rsplit(":", 1)
     srv = PSServer("0.0.0.0", int(port))
     print(f"[ps] serving on {address}", flush=True)
+    window = None
+    if index == 0:
+        from . import ps_device as PD
+        if PD.enabled():
+            window = PD.serve_window(srv.port)
     try:
         while stop_event is None or not stop_event.is_set():
             time.sleep(0.2)

@@ -420,6 +420,14 @@ class Estimator:
             layer = n_.split("/")[0]
             bn_mom[n_] = next(l.momentum for l in m.layers if l.name == layer)
         lr = float(opt_saved.learning_rate)
+        plane = self._ps_device_plane(client, store, bn_mom, lr, opt_saved)
+        if plane is not None:
+            if chief:
+                for h in all_hooks:
+                    if isinstance(h, HK.CheckpointSaverHook):
+                        h.saver_fn = lambda step: self._ps_save(plane, step)
+            gstep = self._ps_loop_device(plane, chief, it, prog, plan, ctx, all_hooks, target, max_steps)
+            return self._ps_end(plane, chief, max_steps, gstep, ctx, all_hooks)
         if os.environ.get("TDE_PS_FLAT", "1") == "0":
             gstep = self._ps_loop_per_variable(client, it, prog, plan, store, names_bn, bn_mom, lr, ctx, all_hooks,
                                                target, max_steps, gstep)
@@ -480,6 +488,62 @@ class Estimator:
                 h.after_step(ctx)
         return self._ps_end(client, chief, max_steps, gstep, ctx, all_hooks)
 
+    def _ps_device_plane(self, client, store, bn_mom, lr, opt):
+        """The same-node GPU data plane (parallel/ps_device.py) when TDE_PS_DEVICE=1 and the update is plain
+        SGD; None keeps the host-staged TCP plane."""
+        from ..parallel import ps_device as PD
+        if not PD.enabled() or store.device.type != "cuda":
+            return None
+        if opt.kind_id != 0 or getattr(opt, "momentum", 0.0):
+            import warnings
+            warnings.warn("PS device data plane: plain SGD only (an atomic add); using the TCP plane")
+            return None
+        t0 = time.time()
+        while True:   # ps task 0 publishes the window right after it starts serving
+            try:
+                return PD.DevicePlane(client, store, bn_mom, lr)
+            except RuntimeError:
+                if time.time() - t0 > 30:
+                    raise
+                time.sleep(0.1)
+
+    def _ps_loop_device(self, plane, chief, it, prog, plan, ctx, all_hooks, target, max_steps):
+        """Async PS loop on the device window: every step's exchange is one kernel (push, BN averages, pull,
+        counters); no host copy of a variable or gradient."""
+        if chief:
+            plane.initialize(ctx.global_step, ctx.global_step)
+        else:
+            plane.wait_initialized()
+        gstep = plane.global_step()
+        ctx.global_step = gstep
+        ticket = plane.counter_add(1, 1) if max_steps is not None else None
+        if ticket is None or ticket <= max_steps:
+            plane.pull()
+            plan.on_weights_loaded()
+        while target is None or gstep < target:
+            if ticket is not None and ticket > max_steps:
+                break
+            try:
+                e = next(it)
+            except StopIteration:
+                break
+            x, y = _split(e)
+            x = np.asarray(x, dtype=np.float32).reshape((len(y),) + tuple(prog.x_shape))
+            y = np.asarray(y).reshape(-1)
+            n = len(y)
+            prog.x_stage[0].stage(x, prog.x_ring[0][0])
+            prog.y_stage[0].stage(y, prog.y_ring[0][0])
+            plan.scale = 1.0 / n
+            plan.train_step(prog.x_ring[0][0], prog.y_ring[0][0], n)
+            ctx.prev_step = gstep
+            gstep, t = plane.step(dstep=1, dticket=1 if max_steps is not None else 0)
+            ticket = t if max_steps is not None else None
+            plan.on_weights_loaded()
+            ctx.global_step = gstep
+            for h in all_hooks:
+                h.after_step(ctx)
+        return gstep
+
     def _ps_end(self, client, chief, max_steps, gstep, ctx, all_hooks):
         m = self.model
         if m._store.device.type == "cuda":
@@ -493,9 +557,14 @@ class Estimator:
                 gstep = client.global_step()
             ctx.prev_step, ctx.global_step = ctx.global_step, gstep
         if chief:
-            m._store.load_dict(client.pull())
+            if hasattr(client, "pull") and hasattr(client, "win"):   # device plane: pull into the store
+                client.pull()
+            else:
+                m._store.load_dict(client.pull())
         for h in all_hooks:
             h.end(ctx)
+        if hasattr(client, "win"):
+            client.close()
         return self
 
     def _ps_loop_per_variable(self, client, it, prog, plan, store, names_bn, bn_mom, lr, ctx, all_hooks, target,
@@ -548,7 +617,10 @@ class Estimator:
     def _ps_save(self, client, step):
         if self.model._store.device.type == "cuda":
             torch.cuda.synchronize(self.model._store.device)   # the last async H2D out of the pinned mirrors
-        self.model._store.load_dict(client.pull())
+        if hasattr(client, "win"):    # device plane: the window's values straight into the store
+            client.pull()
+        else:
+            self.model._store.load_dict(client.pull())
         return self.manager.save(self.model, step)
 
     # ------------------------------------------------------------------ evaluate / predict
@@ -650,7 +722,7 @@ def train_and_evaluate(estimator, train_spec, eval_spec):
     if role == "ps":
         from ..parallel.ps import run_ps_server
         addr = cfg.cluster_spec.task_address("ps", cfg.task_id)
-        run_ps_server(addr)
+        run_ps_server(addr, index=cfg.task_id)
         return None, None
     if role == "evaluator":
         return _run_evaluator(estimator, train_spec, eval_spec)
