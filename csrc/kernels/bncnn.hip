@@ -30,6 +30,7 @@
 // multi-tensor optimizer kernel applies them.
 #include "tde_common.h"
 #include "tde_philox.h"
+#include "tde_xgmi.h"
 #include "tde_optim.h"
 
 namespace tde {
@@ -1324,8 +1325,16 @@ struct ReduceArgs {
   const long long* iterations;
   OptHyper h;
   long long* stamps;
+  // fused DP exchange (step mode "xgmi"): segment push_seg (the Dense kernel's gradient, 94 % of the bytes)
+  // goes straight into the xGMI owners' contribution areas of the all-reduce call that follows
+  int push_seg;
+  XgPush push;
 };
 __device__ __forceinline__ void reduce_commit(const ReduceArgs& a, int j, long long e, float gs, long long t, bool inplace) {
+  if (j == a.push_seg) {
+    xg_push_store(a.push, (int)((*a.push.epoch + 1u) & 1u), a.push.off + e, gs);
+    return;
+  }
   if (!a.apply) {
     a.out[j][e] = gs;
     return;
@@ -1751,10 +1760,16 @@ struct TdeBnOpt {
   const long long* iterations;
 };
 TDE_API int tde_bncnn_reduce(int n, const int* cnt, const float* const* part, float* const* out, const long long* len,
-                             const TdeBnOpt* opt, hipStream_t stream) {
+                             const TdeBnOpt* opt, int push_seg, const XgPush* push, hipStream_t stream) {
   if (n < 1 || n > kMaxRed) return -1;
   ReduceArgs a{};
   a.n = n;
+  a.push_seg = -1;
+  if (push && push->nranks > 0) {   // push_seg's element e is bucket element push->off + e
+    if (opt || push_seg < 0 || push_seg >= n || push->nranks > kXgMaxRanks || push->L <= 0 || !push->epoch) return -4;
+    a.push_seg = push_seg;
+    a.push = *push;
+  }
   a.stamps = next_stamps();
   if (opt) {
     if (!opt->g || !opt->w || !opt->iterations || (opt->kind != kOptSGD && !opt->m) ||

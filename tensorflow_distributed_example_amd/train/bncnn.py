@@ -49,8 +49,8 @@ N.register_hip({
     "tde_bncnn_conv_bwd_plan": (_i, [_vp, _i, _vp]),
     # geo, B, z, bn, bb, gout, w, in, bn_in, gin, acc_in, dwpart, dgrad, wstack, stream
     "tde_bncnn_conv_bwd": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp]),
-    # n, cnt, part, out, len, opt, stream
-    "tde_bncnn_reduce": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp]),
+    # n, cnt, part, out, len, opt, push_seg, push, stream
+    "tde_bncnn_reduce": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp]),
     # B, D, rate, seed, iter, layer_id, out, stream
     "tde_bncnn_dropout_mask": (_i, [_i, _i, C.c_float, C.c_ulonglong, _vp, _i, _vp, _vp]),
 })
@@ -223,6 +223,8 @@ class BnCnnPlan(ReplicaPlan):
         self.opt = OptimizerKernel(store, optimizer, {}, self.iterations) if optimizer is not None else None
         self._bn_segs = self._bn_gradient_segments()
         self._opt_key_set = None
+        self._push = None     # fused DP exchange (step mode "xgmi", set_push)
+        self._pushed = False
 
     def _bn_vars(self, bn):
         st, n = self.store, bn.name
@@ -349,12 +351,16 @@ class BnCnnPlan(ReplicaPlan):
         if self.step_mode == "local":
             segs += self._bn_segs
             opt = C.byref(self._bnopt)
+        # fused DP exchange: the Dense kernel's summed gradient (segment len(blocks)) goes to the xGMI owners
+        push = self._push if self.step_mode == "xgmi" else None
+        self._pushed = push is not None
         n = len(segs)
         cnt = (C.c_int * n)(*[sg[3] for sg in segs])
         parts = (C.c_void_p * n)(*[sg[0].data_ptr() for sg in segs])
         outs = (C.c_void_p * n)(*[sg[1].data_ptr() for sg in segs])
         lens = (C.c_longlong * n)(*[sg[2] for sg in segs])
-        N.check(lib.tde_bncnn_reduce(n, cnt, parts, outs, lens, opt, s), "tde_bncnn_reduce")
+        N.check(lib.tde_bncnn_reduce(n, cnt, parts, outs, lens, opt, len(self.blocks),
+                                     C.byref(push) if push is not None else None, s), "tde_bncnn_reduce")
 
     # ------------------------------------------------------------------ fused optimizer ("local")
     def supports_step_mode(self, mode):
@@ -369,8 +375,21 @@ class BnCnnPlan(ReplicaPlan):
         from .program import f32_xg_apply_spec
         return f32_xg_apply_spec(self)
 
+    def push_range(self):
+        """Bucket range the reduce launch can push into the xGMI owners itself: the Dense(200) kernel's
+        gradient (94 % of Model B's gradient bytes)."""
+        seg = self.store.segments[f"{self.dense.name}/kernel"]
+        return seg.offset, seg.offset + seg.numel
+
+    def set_push(self, spec):
+        if spec is not None and self.step_mode != "xgmi":
+            raise ValueError("the fused exchange needs step mode 'xgmi'")
+        self._push = spec
+
     def set_step_mode(self, mode):
         super().set_step_mode(mode)
+        if mode != "xgmi":
+            self._push = None
         self._opt_key_set = self._opt_key()
         if mode == "local":
             o, st = self.optimizer, self.store

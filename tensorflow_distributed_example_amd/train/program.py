@@ -273,8 +273,14 @@ def f32_xg_apply_spec(plan):
     m = st.slot(sl[0]) if sl else None
     v = st.slot(sl[1]) if len(sl) > 1 else None
     hp = opt.hparams()
+    # the plan's step pushed part of the bucket into the owners itself (fused exchange; a replica without
+    # data this step pushed nothing)
+    lo, hi = plan.push_range() if (getattr(plan, "_push", None) is not None and getattr(plan, "_pushed", False)) \
+        else (0, 0)
+    if hasattr(plan, "_pushed"):
+        plan._pushed = False
     return K.XgApply(opt.kind_id, float(opt.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"],
-                     K._P(st.w), K._P(m), K._P(v), K._P(plan.iterations), None, 0, 0, None, 0, 0)
+                     K._P(st.w), K._P(m), K._P(v), K._P(plan.iterations), None, 0, 0, None, 0, 0, lo, hi)
 
 
 def match_convnet(model, loss):

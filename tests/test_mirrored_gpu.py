@@ -208,16 +208,19 @@ def test_mlp_two_replicas_equal_one_replica(tmp_path):
 
 @pytest.mark.parametrize("layout", ["mirrored", "mwms", "mwms2x2"])
 @pytest.mark.parametrize("eager", [False, True])
-def test_fused_push_exchange_is_bitwise_the_post_backward_exchange(layout, eager, tmp_path):
-    """The fused data-parallel exchange (the fp32 MNIST-CNN backward stores dW1 straight into the xGMI
-    owners' windows; the all-reduce launch pushes only the rest of the bucket) gives bit-identical weights
-    to the post-backward exchange (TDE_XGMI_PUSH=0) after 12 steps, in hipGraph and eager (TDE_GRAPH=0)
-    mode: the owners reduce the same contributions in the same rank order."""
+@pytest.mark.parametrize("model", ["mnist_cnn", "mnist_bn_cnn"])
+def test_fused_push_exchange_is_bitwise_the_post_backward_exchange(layout, eager, model, tmp_path):
+    """The fused data-parallel exchange (the fp32 MNIST-CNN backward / the BN-CNN reduce launch store the big
+    Dense kernel's gradient straight into the xGMI owners' windows; the all-reduce launch pushes only the
+    rest of the bucket) gives bit-identical weights to the post-backward exchange (TDE_XGMI_PUSH=0) after 12
+    steps, in hipGraph and eager (TDE_GRAPH=0) mode: the owners reduce the same contributions in the same
+    rank order."""
     args, env, nproc = LAYOUTS[layout]
+    args = args + ["--model", model]
     res = {}
     for push in ("1", "0"):
         e = dict(env or {}, TDE_XGMI_PUSH=push, TDE_GRAPH="0" if eager else "1")
-        w, line = _equiv(tmp_path, f"{layout}_{push}", args, e, nproc)
+        w, line = _equiv(tmp_path, f"{layout}_{model}_{push}", args, e, nproc)
         assert "replicas_identical=True" in line and "step_mode=xgmi" in line, line
         assert f"graph={not eager}" in line, line
         assert ("exchange=fused_push" if push == "1" else "exchange=post_backward") in line, line
