@@ -119,10 +119,11 @@ __device__ __forceinline__ void publish(char* const* peer, int nranks, int parit
   }
 }
 
-// Thread 0 waits until every rank's flag of (parity, phase, blk) equals `epoch`; *missing (thread 0,
-// nullable) = the first source whose flag never arrived, 0xff when all did.
-__device__ __forceinline__ void await(char* base, int parity, int phase, int nranks, int blk, uint32_t epoch,
-                                      long long timeout, uint32_t* err, uint32_t bit, uint32_t* missing = nullptr) {
+// Thread 0 waits until every rank's flag of (parity, phase, blk) equals `epoch`; returns (thread 0) the
+// first source whose flag never arrived, 0xff when all did (diagnostics).
+__device__ __forceinline__ uint32_t await(char* base, int parity, int phase, int nranks, int blk, uint32_t epoch,
+                                          long long timeout, uint32_t* err, uint32_t bit) {
+  uint32_t missing = 0xffu;
   if (threadIdx.x == 0) {
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
     bool ok = true;
@@ -137,12 +138,13 @@ __device__ __forceinline__ void await(char* base, int parity, int phase, int nra
         }
       }
     }
-    if (missing) *missing = ok ? 0xffu : (uint32_t)(s - 1);
+    missing = ok ? 0xffu : (uint32_t)(s - 1);
     if (!ok) __hip_atomic_fetch_or(err, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __atomic_thread_fence(__ATOMIC_ACQUIRE);   // system scope: drop stale L1/L2 lines
     drain_stores();
   }
   __syncthreads();
+  return missing;
 }
 
 __device__ __forceinline__ void copy_chunk(float* dst, const float* src, long long n, bool vec) {
@@ -258,7 +260,7 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
   XG_STAMP(2);
 
   // ---- phase 2: reduce own slice chunk from local HBM, push the result to every rank
-  await(a.peer[r], parity, 0, N, blk, epoch, a.timeout_ticks, a.err, 1u, tr ? &miss1 : nullptr);
+  miss1 = await(a.peer[r], parity, 0, N, blk, epoch, a.timeout_ticks, a.err, 1u);
   XG_STAMP(3);
   {
     const long long g0 = (long long)r * L + c0;
@@ -286,7 +288,7 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
   // ---- phase 3: gather every reduced slice chunk back into the bucket (or apply the update)
   float lr_t = 0.f;
   if (a.apply) lr_t = opt_lr_t(a.h, a.h.kind == kOptAdam ? *a.iterations : 0);
-  await(a.peer[r], parity, 1, N, blk, epoch, a.timeout_ticks, a.err, 2u, tr ? &miss2 : nullptr);
+  miss2 = await(a.peer[r], parity, 1, N, blk, epoch, a.timeout_ticks, a.err, 2u);
   XG_STAMP(5);
   const float* out = area(a.peer[r], 1, parity, cap);
   for (int s = 0; s < N; ++s) {
