@@ -2,13 +2,15 @@
 serving_input_fn at :151-162 — a float32 ``[None, 784]`` placeholder).
 
 Layout written under ``<export_dir_base>/<unix_timestamp>/``:
+    saved_model.pb                   TF1 SavedModel protobuf: the serving graph in TensorFlow's standard ops,
+                                     the save/restore subgraph + SaverDef, SignatureDef ``serving_default``
+                                     (io/saved_model_pb.py; loading by TF itself is parity-unpinned)
     saved_model.json                 architecture (Sequential config), dtype policy,
                                      signature ``serving_default``: inputs/outputs specs
     variables/variables.index        TensorBundle (native writer), TF1 variable names
     variables/variables.data-00000-of-00001
-A TF ``saved_model.pb`` GraphDef is not produced (no TensorFlow here; recorded as
-a deliberate gap).  ``load(path)`` rebuilds the model and serves through the HIP
-kernels on GPU (torch reference ops on CPU).
+``load(path)`` rebuilds the model from the JSON spec and serves through the HIP kernels on GPU (torch
+reference ops on CPU).
 """
 from __future__ import annotations
 
@@ -73,6 +75,8 @@ def export_saved_model(model, export_dir_base, serving_input_receiver_fn):
         "variables": "variables/variables",
     }
     (tmp / "saved_model.json").write_text(json.dumps(spec, indent=1, default=str))
+    from .saved_model_pb import saved_model_bytes
+    (tmp / "saved_model.pb").write_bytes(saved_model_bytes(model, input_shape=feats.shape, output_key=out_name))
     os.replace(tmp, out)
     return str(out).encode()
 
