@@ -59,6 +59,8 @@ def parse():
                          "local GPUs (MirroredStrategy, in-process xGMI all-reduce, one hipGraph per GPU)")
     ap.add_argument("--gpus-per-worker", type=int, default=1,
                     help="mwms: local GPUs per worker process (torchrun --nproc-per-node = gpus / K)")
+    ap.add_argument("--repeats", type=int, default=5,
+                    help="after the reported measurement, repeat the K-step measurement R times (spread only)")
     ap.add_argument("--devices", default=None,
                     help="mirrored: explicit local device list, e.g. 0,1,2,3 (0,0 = a 2-replica rehearsal on one GPU)")
     return ap.parse_args()
@@ -164,22 +166,27 @@ def main():
         run_exec(i, prefetch=i + 1 < n_warm)
         if i % 8 == 0:
             prog.sync()   # bounded queue depth; the GPU never idles for long
-    prog.sync()
-    barrier()
-    prog.sync()
-    t0 = time.perf_counter()
     n_exec = a.steps // spe
-    # the first timed execution's input group is staged inside the timed region (short and long runs
-    # count the same input work per execution); later ones overlap the previous replay
-    stage(n_warm)
-    for i in range(n_exec):
-        run_exec(n_warm + i, prefetch=i + 1 < n_exec)
-    prog.sync()
-    barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if world > 1:
-        elapsed = strategy.control.all_reduce_max(elapsed)
+
+    def timed(first):
+        """K steps bracketed by a barrier + device sync on both sides; max over ranks.  The first timed
+        execution's input group is staged inside the timed region (short and long runs count the same
+        input work per execution); later ones overlap the previous replay."""
+        prog.sync()
+        barrier()
+        prog.sync()
+        t0 = time.perf_counter()
+        stage(first)
+        for i in range(n_exec):
+            run_exec(first + i, prefetch=i + 1 < n_exec)
+        prog.sync()
+        barrier()
+        el = time.perf_counter() - t0
+        return strategy.control.all_reduce_max(el) if world > 1 else el
+
+    elapsed = timed(n_warm)
+    # spread evidence (outside the reported measurement): the same K-step measurement repeated
+    repeats = [timed(n_warm + n_exec * (r + 1)) for r in range(max(0, a.repeats))]
     logs = tde.metrics.logs_from(prog.global_metrics(), ["accuracy"])
     comm = strategy.comm
     ar = {"XgmiCommunicator": "xgmi", "PeerXgmiCommunicator": "xgmi_peer", "RcclCommunicator": "rccl",
@@ -214,6 +221,8 @@ def main():
                        "optimizer": f"SGD(lr={a.lr})", "plan": prog.plan_kind,
                        "allreduce": ar,
                        "hipgraph": prog.use_graph, "grad_buckets": len(prog.buckets or []) or 1,
+                       # the same K-step measurement repeated after the reported one (ms/step; spread evidence)
+                       "repeat_ms_per_step": [round(r / a.steps * 1e3, 5) for r in repeats],
                        "optimizer_placement": placement,
                        # fused_push: the backward stores the Dense(64) weight gradient straight into the
                        # xGMI owners' windows; post_backward: the all-reduce launch pushes the whole bucket
