@@ -493,7 +493,7 @@ class PeerXgmiCommunicator(Communicator):
             raise ValueError(f"xGMI all-reduce supports at most {self.lib.tde_xgmi_max_ranks()} ranks")
         if control is None and (self.rank0 != 0 or self.world != n):
             raise ValueError("a multi-process PeerXgmiCommunicator needs the control plane")
-        self.max_elems = int(max_elems or os.environ.get("TDE_XGMI_MAX_ELEMS", 8 << 20))
+        self.max_elems = int(max_elems or os.environ.get("TDE_XGMI_MAX_ELEMS", 16 << 20))  # ResNet-18 (11.7 M) fits: per-device graphs
         self.uncached = int(os.environ.get("TDE_XGMI_UNCACHED", "1") if uncached is None else uncached)
         self.nblocks_override = int(os.environ.get("TDE_XGMI_BLOCKS", 0))
         timeout_s = float(timeout_s or os.environ.get("TDE_XGMI_TIMEOUT", 300))
