@@ -52,8 +52,14 @@ def main():
         if (e + 1) % a.sync_every == 0 or e == a.execs - 1:
             prog.sync()
             dt = time.perf_counter() - t0
-            bits = comm.error_bits() if hasattr(comm, "error_bits") else None
-            eps = [comm.calls(i) for i in range(nl)] if hasattr(comm, "calls") else None
+            if hasattr(comm, "error_bits"):       # PeerXgmiCommunicator: one entry per local replica
+                bits = comm.error_bits()
+                eps = [comm.calls(i) for i in range(nl)]
+            elif hasattr(comm, "err"):            # XgmiCommunicator: one rank per process
+                bits = [comm.lib.tde_xgmi_error(comm.err)]
+                eps = [comm.calls()]
+            else:
+                bits = eps = None
             print(f"{tag} exec {e} {dt * 1e3:.2f} ms err={bits} epochs={eps}", flush=True)
             if bits and any(bits):
                 print(f"{tag} STOP: error bits set", flush=True)

@@ -18,5 +18,6 @@ run() {  # name args...
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 }
 TDE_GRAPH=0 run eager_2x2 --mwms 2 --spe 4 --execs 2 && \
-TDE_GRAPH=1 run graph_2x2 --mwms 2 --spe 4 --execs 2
+TDE_GRAPH=1 run graph_2x2 --mwms 2 --spe 4 --execs 2 && \
+TDE_GRAPH=0 TDE_ALLREDUCE=xgmi run eager_2x1 --mwms 1 --spe 4 --execs 2
 echo "=== done"
