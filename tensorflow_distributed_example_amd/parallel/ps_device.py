@@ -35,7 +35,12 @@ N.register_hip({
 })
 
 HANDLE_VAR = "__tde_psdev_handle__"     # TCP variable of ps task 0 carrying the window's IPC handle
+PLANE_VAR = "__tde_ps_plane__"          # the chief's decision: 1.0 device plane, 0.0 TCP plane
 INIT_CTR = 2
+
+
+class NoWindow(RuntimeError):
+    """ps task 0 publishes no device window (yet)."""
 
 
 def enabled() -> bool:
@@ -83,7 +88,7 @@ class DevicePlane:
         names = PS._arr([HANDLE_VAR])
         ok = c0.lib.tde_ps_pull(c0.h, 1, names, (C.c_void_p * 1)(buf.ctypes.data), (C.c_longlong * 1)(n)) == 0
         if not ok:
-            raise RuntimeError("ps task 0 publishes no device window (TDE_PS_DEVICE unset on the ps task?)")
+            raise NoWindow("ps task 0 publishes no device window (TDE_PS_DEVICE unset on the ps task?)")
         self.nw, self.ns = store.w.numel(), store.state.numel()
         ncnt = self.lib.tde_psdev_counters()
         if (ncnt * 8 + 4 * (self.nw + self.ns)) > window_bytes():

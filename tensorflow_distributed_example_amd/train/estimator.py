@@ -29,6 +29,7 @@ from __future__ import annotations
 import json
 import logging
 import math
+import ctypes as C
 import os
 import time
 from pathlib import Path
@@ -420,7 +421,7 @@ class Estimator:
             layer = n_.split("/")[0]
             bn_mom[n_] = next(l.momentum for l in m.layers if l.name == layer)
         lr = float(opt_saved.learning_rate)
-        plane = self._ps_device_plane(client, store, bn_mom, lr, opt_saved)
+        plane = self._ps_device_plane(client, store, bn_mom, lr, opt_saved, chief)
         if plane is not None:
             if chief:
                 for h in all_hooks:
@@ -488,24 +489,49 @@ class Estimator:
                 h.after_step(ctx)
         return self._ps_end(client, chief, max_steps, gstep, ctx, all_hooks)
 
-    def _ps_device_plane(self, client, store, bn_mom, lr, opt):
-        """The same-node GPU data plane (parallel/ps_device.py) when TDE_PS_DEVICE=1 and the update is plain
-        SGD; None keeps the host-staged TCP plane."""
+    def _ps_device_plane(self, client, store, bn_mom, lr, opt, chief):
+        """The same-node GPU data plane (parallel/ps_device.py) or None (the host-staged TCP plane).  The chief
+        decides — TDE_PS_DEVICE=1, plain SGD, the model on a GPU, ps task 0 publishing a window the model fits
+        in — and records the decision on ps task 0; every other trainer follows it, so no two trainers ever
+        update different copies of the variables."""
+        import warnings
+
+        from ..parallel import ps as PS
         from ..parallel import ps_device as PD
-        if not PD.enabled() or store.device.type != "cuda":
-            return None
-        if opt.kind_id != 0 or getattr(opt, "momentum", 0.0):
-            import warnings
-            warnings.warn("PS device data plane: plain SGD only (an atomic add); using the TCP plane")
-            return None
+        flag = np.zeros(1, np.float32)
+        c0 = client.conns[0]
+        names = PS._arr([PD.PLANE_VAR])
+        if chief:
+            plane, why = None, None
+            if PD.enabled() and store.device.type == "cuda":
+                if opt.kind_id != 0 or getattr(opt, "momentum", 0.0):
+                    why = "plain SGD only (the update is an atomic add)"
+                else:
+                    t0 = time.time()
+                    while plane is None:   # ps task 0 publishes the window right after it starts serving
+                        try:
+                            plane = PD.DevicePlane(client, store, bn_mom, lr)
+                        except PD.NoWindow as e:
+                            if time.time() - t0 > 30:
+                                why = str(e)
+                                break
+                            time.sleep(0.1)
+                        except RuntimeError as e:
+                            why = str(e)
+                            break
+                if why:
+                    warnings.warn(f"PS device data plane unavailable ({why}); using the TCP plane")
+            flag[0] = 1.0 if plane is not None else 0.0
+            c0.lib.tde_ps_init(c0.h, PD.PLANE_VAR.encode(), flag.ctypes.data, 1)
+            return plane
         t0 = time.time()
-        while True:   # ps task 0 publishes the window right after it starts serving
-            try:
-                return PD.DevicePlane(client, store, bn_mom, lr)
-            except RuntimeError:
-                if time.time() - t0 > 30:
-                    raise
-                time.sleep(0.1)
+        while c0.lib.tde_ps_pull(c0.h, 1, names, (C.c_void_p * 1)(flag.ctypes.data), (C.c_longlong * 1)(1)) != 0:
+            if time.time() - t0 > 120:
+                raise TimeoutError("the chief never recorded the PS data plane")
+            time.sleep(0.05)
+        if flag[0] != 1.0:
+            return None
+        return PD.DevicePlane(client, store, bn_mom, lr)   # the chief mapped it: failing here is an error
 
     def _ps_loop_device(self, plane, chief, it, prog, plan, ctx, all_hooks, target, max_steps):
         """Async PS loop on the device window: every step's exchange is one kernel (push, BN averages, pull,
