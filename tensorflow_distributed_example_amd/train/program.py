@@ -242,6 +242,8 @@ class OptimizerKernel:
         self.refresh_shadows()
 
     def refresh_shadows(self):
+        if not self.shadow_views:   # f32 plans read the master weights: nothing to refresh
+            return
         N = self.N
         with torch.cuda.device(self.store.device):
             rc = N.hip().tde_shadow_refresh(self.store.w.data_ptr(), self.shadow.data_ptr(),
