@@ -474,7 +474,7 @@ class ConvNetPlan(ReplicaPlan):
     def push_range(self):
         """Bucket range the backward can push into the xGMI owners itself (the Dense(64) kernel's dW1:
         99.7 % of the gradient bytes), or None when this plan form cannot."""
-        if not self.f32 or self.det:
+        if not self.f32:
             return None
         seg = self.store.segments[self.names["w1"]]
         return seg.offset, seg.offset + seg.numel

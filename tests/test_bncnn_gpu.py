@@ -332,7 +332,9 @@ def test_bncnn_dropout_matches_float64_with_the_plan_mask(B):
         for n_, gr in grads.items():
             assert _rel(st.grad(n_), gr) < 1e-5, (step, n_, _rel(st.grad(n_), gr))
         for n_, v in moving.items():
-            assert _rel(st.view(n_), v) < 1e-6, (step, n_, _rel(st.view(n_), v))
+            # moving means near 1e-3: the f32 batch sums over B*H*W values set the relative error (B=128:
+            # 1.0e-6 measured on MI355X)
+            assert _rel(st.view(n_), v) < 4e-6, (step, n_, _rel(st.view(n_), v))
         plan.apply()
         torch.cuda.synchronize()
     assert not torch.equal(masks[0], masks[1])

@@ -198,7 +198,8 @@ def test_gap_pad_xent32():
     O32.gap_bwd(dy, dx, B, HW, C, accum=True)
     torch.cuda.synchronize()
     assert _rel(y, _c64(x).mean(1)) < 1e-6
-    assert _rel(dx, _c64(dy)[:, None, :] / HW + 1.0) < 1e-7
+    # f32: 1/HW, the product and the +1 residual each round once (≈ 3 half-ulps of a value near 1)
+    assert _rel(dx, _c64(dy)[:, None, :] / HW + 1.0) < 4e-7
     g = O.ConvGeom(2, 5, 6, 3, 8, 9, 3, 1, 1, 1, 1, 1, 2)
     xp = _r(2, 5, 6, 3, seed=18)
     yp = torch.zeros(2, 8, 9, 3, device=DEV)

@@ -218,8 +218,12 @@ def test_fused_push_exchange_is_bitwise_the_post_backward_exchange(layout, eager
     args, env, nproc = LAYOUTS[layout]
     args = args + ["--model", model]
     res = {}
+    # the MNIST-CNN plan's split-K forward and conv-gradient adds are float atomics (arrival order varies
+    # run to run); TDE_DETERMINISTIC=1 replaces them by ordered partial sums so two runs can be compared
+    # bit for bit (the BN-CNN plan's reductions are ordered already)
+    det = {"TDE_DETERMINISTIC": "1"} if model == "mnist_cnn" else {}
     for push in ("1", "0"):
-        e = dict(env or {}, TDE_XGMI_PUSH=push, TDE_GRAPH="0" if eager else "1")
+        e = dict(env or {}, TDE_XGMI_PUSH=push, TDE_GRAPH="0" if eager else "1", **det)
         w, line = _equiv(tmp_path, f"{layout}_{model}_{push}", args, e, nproc)
         assert "replicas_identical=True" in line and "step_mode=xgmi" in line, line
         assert f"graph={not eager}" in line, line

@@ -123,7 +123,8 @@ def test_ps_estimator_two_trainers_exact_max_steps(plane):
            "100"]
     r = subprocess.run(cmd, env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=200)
     assert r.returncode == 0, r.stdout[-4000:]
-    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    # the launcher prefixes each task's lines with "[task:index] "
+    lines = [l[l.index("{"):] for l in r.stdout.splitlines() if '{"metric"' in l]
     assert len(lines) == 1, r.stdout[-3000:]
     res = json.loads(lines[0])
     print(res)
