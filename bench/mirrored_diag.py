@@ -71,7 +71,8 @@ def main():
         nb = {}
         for li, buf in enumerate(tr):
             recs = xg_trace_records(buf, buf.shape[1])
-            for r in recs[: a.trace_show]:
+            bad = [r for r in recs if any(m != 255 for m in r["miss1"] + r["miss2"])]
+            for r in recs[: a.trace_show] + bad[:4]:
                 used = [i for i, v in enumerate(r["start"]) if v]
                 us = lambda k: [r[k][i] / 100.0 for i in used]   # noqa: E731
                 mn = lambda k: min(us(k)) if used else 0.0         # noqa: E731
@@ -81,6 +82,12 @@ def main():
                       f"{mx('start'):.1f}] pub1<= {mx('pub1'):.1f} arr1 [{mn('arr1'):.1f}, {mx('arr1'):.1f}] "
                       f"pub2<= {mx('pub2'):.1f} arr2<= {mx('arr2'):.1f} end<= {mx('end'):.1f} missing={miss} "
                       f"xcc={sorted(set(r['xcc'][i] for i in used))}", flush=True)
+                if r in bad:   # per block: which source, the flag value seen, where the block ran
+                    for i in used:
+                        if r["miss1"][i] != 255 or r["miss2"][i] != 255:
+                            print(f"{tag}   blk {i} miss1={r['miss1'][i]} seen1={r['seen1'][i]} "
+                                  f"miss2={r['miss2'][i]} seen2={r['seen2'][i]} xcc={r['xcc'][i]} "
+                                  f"start={r['start'][i] / 100.0:.1f} arr1={r['arr1'][i] / 100.0:.1f}", flush=True)
     print(f"{tag} done", flush=True)
 
 

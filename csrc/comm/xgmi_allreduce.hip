@@ -80,10 +80,11 @@ struct XgArgs {
   const long long* iterations;
   OptHyper h;
   // diagnostics (nullable): per call slot (epoch % trace_calls) and block, kXgTraceWords u64 —
-  // [epoch, t_start, t_published1, t_phase1_arrived, t_published2, t_phase2_arrived, t_end, info] with
+  // [epoch | seen1 << 32, t_start, t_published1, t_phase1_arrived, t_published2, t_phase2_arrived, t_end,
+  // info | seen2 << 32] with
   // t = s_memrealtime (100 MHz, one clock for every process on the device) and info = missing source
   // of the phase-1 wait (bits 0-7, 0xff = none) | of the phase-2 wait (8-15) | XCC id (16-23) |
-  // HW_ID cu (24-27) | se (28-31)
+  // HW_ID cu (24-27) | se (28-31); seen1 / seen2 = the flag value a timed-out wait of that phase last read
   unsigned long long* trace;
   int trace_calls;
   // [push_lo, push_hi): bucket elements a producer kernel already stored into the owners' contribution
@@ -120,9 +121,10 @@ __device__ __forceinline__ void publish(char* const* peer, int nranks, int parit
 }
 
 // Thread 0 waits until every rank's flag of (parity, phase, blk) equals `epoch`; returns (thread 0) the
-// first source whose flag never arrived, 0xff when all did (diagnostics).
+// first source whose flag never arrived, 0xff when all did, and in `seen` the value that flag held when
+// the wait gave up (diagnostics: an older epoch = never written, a newer one = overwritten early).
 __device__ __forceinline__ uint32_t await(char* base, int parity, int phase, int nranks, int blk, uint32_t epoch,
-                                          long long timeout, uint32_t* err, uint32_t bit) {
+                                          long long timeout, uint32_t* err, uint32_t bit, uint32_t& seen) {
   uint32_t missing = 0xffu;
   if (threadIdx.x == 0) {
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
@@ -130,7 +132,7 @@ __device__ __forceinline__ uint32_t await(char* base, int parity, int phase, int
     int s = 0;
     for (; s < nranks && ok; ++s) {
       uint32_t* f = flag_ptr(base, parity, phase, s, blk);
-      while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+      while ((seen = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != epoch) {
         __builtin_amdgcn_s_sleep(2);
         if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
           ok = false;
@@ -234,9 +236,9 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
   const long long c0 = (long long)blk * CH;
   // diagnostics record (thread 0 only)
   unsigned long long* tr = nullptr;
-  uint32_t miss1 = 0xffu, miss2 = 0xffu;
+  uint32_t miss1 = 0xffu, miss2 = 0xffu, seen1 = 0u, seen2 = 0u;
   if (a.trace && tid == 0) {
-    tr = a.trace + ((size_t)(epoch % (uint32_t)a.trace_calls) * gridDim.x + blk) * kXgTraceWords;
+    tr = a.trace + ((size_t)(epoch % (uint32_t)a.trace_calls) * kXgMaxBlocks + blk) * kXgTraceWords;
     tr[0] = epoch;
     tr[1] = __builtin_amdgcn_s_memrealtime();
   }
@@ -260,7 +262,7 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
   XG_STAMP(2);
 
   // ---- phase 2: reduce own slice chunk from local HBM, push the result to every rank
-  miss1 = await(a.peer[r], parity, 0, N, blk, epoch, a.timeout_ticks, a.err, 1u);
+  miss1 = await(a.peer[r], parity, 0, N, blk, epoch, a.timeout_ticks, a.err, 1u, seen1);
   XG_STAMP(3);
   {
     const long long g0 = (long long)r * L + c0;
@@ -288,7 +290,7 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
   // ---- phase 3: gather every reduced slice chunk back into the bucket (or apply the update)
   float lr_t = 0.f;
   if (a.apply) lr_t = opt_lr_t(a.h, a.h.kind == kOptAdam ? *a.iterations : 0);
-  miss2 = await(a.peer[r], parity, 1, N, blk, epoch, a.timeout_ticks, a.err, 2u);
+  miss2 = await(a.peer[r], parity, 1, N, blk, epoch, a.timeout_ticks, a.err, 2u, seen2);
   XG_STAMP(5);
   const float* out = area(a.peer[r], 1, parity, cap);
   for (int s = 0; s < N; ++s) {
@@ -301,8 +303,10 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
     const uint32_t hw = __builtin_amdgcn_s_getreg(63492);   // hwreg(HW_REG_HW_ID): cu 8-11, se 13-15
     const uint32_t xcc = __builtin_amdgcn_s_getreg(63508);  // hwreg(HW_REG_XCC_ID)
     tr[6] = __builtin_amdgcn_s_memrealtime();
+    tr[0] = (unsigned long long)epoch | ((unsigned long long)(miss1 == 0xffu ? 0u : seen1) << 32);
     tr[7] = (unsigned long long)(miss1 | (miss2 << 8) | ((xcc & 0xff) << 16) | (((hw >> 8) & 0xf) << 24) |
-                                 (((hw >> 13) & 0x7) << 28));
+                                 (((hw >> 13) & 0x7) << 28)) |
+            ((unsigned long long)(miss2 == 0xffu ? 0u : seen2) << 32);
   }
 #undef XG_STAMP
   // the last block to finish advances the epoch (every block read it at its start) and re-arms

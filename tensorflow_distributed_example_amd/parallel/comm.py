@@ -19,6 +19,8 @@ from __future__ import annotations
 import ctypes as C
 import os
 
+import numpy as np
+
 import torch
 
 _DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int32: 3, torch.int64: 4, torch.uint8: 5,
@@ -438,7 +440,7 @@ def _xg_trace_alloc(lib, device, epoch_ptr, calls):
 def xg_trace_records(buf, nblocks):
     """Decode a trace buffer into per-call dicts (host copy; call after a device sync).  Blocks of a
     launch with ``nblocks`` chunks occupy slots [0, nblocks) of their call."""
-    t = buf.cpu().numpy()
+    t = buf.cpu().numpy().view(np.uint64)
     out = []
     for c in range(t.shape[0]):
         rec = t[c, :nblocks]
@@ -446,13 +448,15 @@ def xg_trace_records(buf, nblocks):
             continue
         info = rec[:, 7]
         out.append({
-            "epoch": int(rec[:, 0].max()),
+            "epoch": int((rec[:, 0] & 0xFFFFFFFF).max()),
             "start": [int(v) for v in rec[:, 1]], "pub1": [int(v) for v in rec[:, 2]],
             "arr1": [int(v) for v in rec[:, 3]], "pub2": [int(v) for v in rec[:, 4]],
             "arr2": [int(v) for v in rec[:, 5]], "end": [int(v) for v in rec[:, 6]],
             "miss1": [int(v) & 0xFF for v in info], "miss2": [(int(v) >> 8) & 0xFF for v in info],
             "xcc": [(int(v) >> 16) & 0xFF for v in info], "cu": [(int(v) >> 24) & 0xF for v in info],
-            "se": [(int(v) >> 28) & 0x7 for v in info]})
+            "se": [(int(v) >> 28) & 0x7 for v in info],
+            # value the flag held when a wait timed out (0: the wait completed)
+            "seen1": [int(v) >> 32 for v in rec[:, 0]], "seen2": [int(v) >> 32 for v in info]})
     return sorted(out, key=lambda r: r["epoch"])
 
 
@@ -597,7 +601,9 @@ class PeerXgmiCommunicator(Communicator):
         single-rank maximum (nloc x nblocks <= 128): two processes sharing one GPU (the rehearsal of a
         K-GPUs-per-worker layout) with 2 x 128-workgroup grouped launches measured peer waits that never
         completed, the same launches at 2 x 8 workgroups ran clean (profiles/r3_xgmi_groups.log)."""
-        cap = max(1, self.lib.tde_xgmi_max_blocks() // max(1, nloc))
+        cap = self.lib.tde_xgmi_max_blocks()
+        if os.environ.get("TDE_XGMI_GROUP_CAP", "1") != "0":
+            cap = max(1, cap // max(1, nloc))
         if self.nblocks_override:
             return min(self.nblocks_override, cap)
         return max(min(8, cap), min(cap, -(-M // self.world) // 512))
