@@ -231,3 +231,24 @@ def test_fused_push_exchange_is_bitwise_the_post_backward_exchange(layout, eager
         res[push] = w
     for k in res["0"]:
         assert np.array_equal(res["1"][k], res["0"][k]), (layout, k)
+
+
+def test_eager_mwms_2x2_rehearsal_runs_clean():
+    """MWMS with 2 GPUs per worker, 2 worker processes, every replica on cuda:0, eager launches
+    (TDE_GRAPH=0): the r3 conditions of the xGMI peer-wait timeouts (bench/mirrored_diag.py, 6 executions
+    of 16 steps).  Every wait must complete: no error bits, equal all-reduce epochs on every replica."""
+    env = dict(ENV, TDE_GRAPH="0", TDE_RCCL="0", TDE_XGMI_TIMEOUT="10", TDE_XGMI_TRACE="64")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench", "mirrored_diag.py"),
+           "--mwms", "2", "--spe", "16", "--execs", "6"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=240)
+    out = r.stdout
+    assert r.returncode == 0, out[-4000:]
+    execs = [l for l in out.splitlines() if " exec " in l]
+    assert len(execs) == 12, out[-4000:]
+    for l in execs:
+        assert "err=[0, 0]" in l, l
+    last = [l for l in execs if " exec 5 " in l]
+    assert len(last) == 2 and len({l.split("epochs=")[1] for l in last}) == 1, last
+    assert "STOP" not in out and "missing=[(" not in out, out[-4000:]
