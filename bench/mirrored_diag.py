@@ -61,6 +61,10 @@ def main():
             else:
                 bits = eps = None
             print(f"{tag} exec {e} {dt * 1e3:.2f} ms err={bits} epochs={eps}", flush=True)
+            ht = getattr(prog, "_host_trace", None)
+            if ht:   # host wall clock (shared by the workers) of this execution's all-reduce enqueues
+                print(f"{tag} exec {e} host enqueue t%1000 = " + " ".join(f"{t % 1000:.4f}" for _, t in ht), flush=True)
+                ht.clear()
             if bits and any(bits):
                 print(f"{tag} STOP: error bits set", flush=True)
                 break

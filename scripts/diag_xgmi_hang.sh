@@ -7,7 +7,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TDE_XGMI_TIMEOUT=${TDE_XGMI_TIMEOUT:-3} PYTHONPATH="$PWD" TDE_HEARTBEAT=0 OMP_NUM_THREADS=2 TDE_RCCL=0
-export TDE_XGMI_TRACE=64
+export TDE_XGMI_TRACE=64 TDE_HOST_TRACE=1
 run() {  # name args...
   local name=$1; shift
   echo "=== $name: $*"

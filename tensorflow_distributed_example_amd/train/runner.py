@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import contextlib
 import os
+import time
 
 import numpy as np
 import torch
@@ -141,6 +142,7 @@ class Program:
                                or self.per_replica))
         self._comm_warm = False
         self._dbg = os.environ.get("TDE_DEBUG_SYNC", "0") not in ("", "0") and cuda
+        self._host_trace = [] if os.environ.get("TDE_HOST_TRACE", "0") not in ("", "0") else None
         self.buckets = self._plan_buckets() if training else None
         self._comm_stream = torch.cuda.Stream(self.devices[0]) if self.buckets else None
         self.comm_applies = False
@@ -261,6 +263,8 @@ class Program:
         for s in range(S):
             for r in idx:
                 self.plans[r].train_step(self.x_ring[r][s], self.y_ring[r][s], B)
+            if self._host_trace is not None:   # TDE_HOST_TRACE: host wall time of each all-reduce enqueue
+                self._host_trace.append((gi, time.time()))
             self._reduce_and_apply_group(gi)
             self._debug_sync("train_step + gradient all-reduce")
         for r in idx:
