@@ -40,4 +40,10 @@ __device__ __forceinline__ void xg_push_store(const XgPush& p, int parity, long 
   xg_area(p.peer[s], 0, parity, p.cap)[(size_t)p.rank * p.L + (g - (long long)s * p.L)] = v;
 }
 
+// A pushing wave waits for its stores' acknowledgements before it ends: on an N-GPU node they travel
+// over xGMI into peer HBM, and the all-reduce's flag that covers them is raised by the next launch, so
+// they must have completed, not merely been issued (the ordering the all-reduce gives its own phase-1
+// stores before their flag).
+__device__ __forceinline__ void xg_push_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 }  // namespace tde

@@ -1376,6 +1376,7 @@ __global__ __launch_bounds__(NTH) void reduce_kernel(ReduceArgs a) {
     reduce_commit(a, j, e0 + 1, s.y, t, inplace);
     reduce_commit(a, j, e0 + 2, s.z, t, inplace);
     reduce_commit(a, j, e0 + 3, s.w, t, inplace);
+    if (j == a.push_seg) xg_push_drain();
     return;
   }
   const long long len = a.len[j];
@@ -1397,6 +1398,7 @@ __global__ __launch_bounds__(NTH) void reduce_kernel(ReduceArgs a) {
   red[q][l] = s;
   __syncthreads();
   if (q == 0 && e < len) reduce_commit(a, j, e, (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]), t, p == a.out[j]);
+  if (j == a.push_seg) xg_push_drain();
 }
 
 }  // namespace bncnn

@@ -356,6 +356,7 @@ __global__ __launch_bounds__(1024) void convnet32_bwd_kernel(BwdArgs a) {
   }
   conv_grad_reduce(a, accr, dps, lane, wave);
   stamp(a.stamps, 5);
+  if (MODE == 0 && a.push.nranks > 0) xg_push_drain();   // pushed rows acknowledged before the wave ends
 }
 
 }  // namespace tde
