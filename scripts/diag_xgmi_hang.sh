@@ -3,7 +3,7 @@
 # replicas, all on cuda:0, a short peer-wait timeout and the per-block phase trace (TDE_XGMI_TRACE):
 # every launch records, per block, its start / publish / arrival / end times on the device's 100 MHz
 # clock (shared by both processes), which source flag never arrived and the value that flag held.
-#   r3 conditions: --spe 16 --execs 6, TDE_GRAPH=0; with and without the nloc x nblocks <= 128 cap.
+#   r3 conditions: --spe 16 --execs 6, TDE_GRAPH=0; with and without the co-located-process spin cap (parallel/comm.spin_grid_caps).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TDE_XGMI_TIMEOUT=${TDE_XGMI_TIMEOUT:-3} PYTHONPATH="$PWD" TDE_HEARTBEAT=0 OMP_NUM_THREADS=2 TDE_RCCL=0
@@ -19,8 +19,8 @@ run() {  # name args...
   echo "=== $name rc=$rc"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 }
-TDE_GRAPH=0 run eager_2x2_capped --mwms 2 --spe 16 --execs 6 && \
-TDE_GRAPH=0 TDE_XGMI_GROUP_CAP=0 run eager_2x2_uncapped --mwms 2 --spe 16 --execs 6 && \
-TDE_GRAPH=1 TDE_XGMI_GROUP_CAP=0 run graph_2x2_uncapped --mwms 2 --spe 16 --execs 6 && \
-TDE_GRAPH=0 TDE_XGMI_GROUP_CAP=0 run eager_2x2_uncapped_bn --mwms 2 --spe 16 --execs 6 --model mnist_bn_cnn
+TDE_GRAPH=0 run eager_2x2_spincap --mwms 2 --spe 16 --execs 6 && \
+TDE_GRAPH=0 TDE_XGMI_SPIN_CAP=0 run eager_2x2_nocap --mwms 2 --spe 16 --execs 6 && \
+TDE_GRAPH=1 TDE_XGMI_SPIN_CAP=0 run graph_2x2_nocap --mwms 2 --spe 16 --execs 6 && \
+TDE_GRAPH=0 TDE_XGMI_SPIN_CAP=0 run eager_2x2_nocap_bn --mwms 2 --spe 16 --execs 6 --model mnist_bn_cnn
 echo "=== done"

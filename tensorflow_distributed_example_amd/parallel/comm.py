@@ -247,6 +247,46 @@ class RcclCommunicator(Communicator):
         self.comms = (C.c_void_p * len(self.devices))()
 
 
+
+def _device_key(d):
+    """Node-wide identity of a GPU (host + PCI location): equal keys = the same physical device."""
+    import socket
+    p = torch.cuda.get_device_properties(d)
+    return f"{socket.gethostname()}/{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+
+
+def spin_grid_caps(control, devices, tag):
+    """Per local device: the most workgroups ONE all-reduce launch of this process may keep spinning on
+    it, or None (no limit beyond the kernel's own).
+
+    Why a limit exists (the round-3 eager MWMS 2x2 timeouts, scripts/diag_xgmi_hang.sh): a waiting
+    all-reduce workgroup holds a VGPR slice of its CU (4 waves x 80 VGPRs, one per SIMD).  The fused
+    MNIST-CNN backward runs 1024-thread workgroups at 128 VGPRs — the whole register file of a CU — so it
+    can only be dispatched onto a CU with no other wave on it.  When another PROCESS shares the GPU, its
+    all-reduce grid can be spinning on every CU while this process's backward (which precedes this
+    process's arrival at that very all-reduce) waits for a free CU: neither progresses until the peer
+    wait times out.  Graph replays keep the processes in lock-step (each reaches the all-reduce after
+    its backward is on the GPU), eager launches let one drift ahead, so eager hit it; 2 x 8-workgroup
+    grids left CUs free and ran clean.  One process per GPU (a real N-GPU node) never shares CUs with
+    its peers' kernels, so there is no limit then.  With ``co`` processes on one device, the other
+    ``co - 1`` may all be spinning while this one needs whole CUs: each process keeps its grid within
+    (CUs - CUs/4) / (co - 1), leaving a quarter of the chip free for whole-CU kernels.
+    ``TDE_XGMI_SPIN_CAP=0`` disables the limit (diagnostics)."""
+    keys = [_device_key(d) if d.type == "cuda" else None for d in devices]
+    if control is None:
+        per_proc = [sorted({k for k in keys if k})]
+    else:
+        per_proc = control.all_gather_json(sorted({k for k in keys if k}), tag)
+    caps = []
+    for d, k in zip(devices, keys):
+        co = sum(1 for ks in per_proc if k in ks) if k else 1
+        if co <= 1 or os.environ.get("TDE_XGMI_SPIN_CAP", "1") == "0":
+            caps.append(None)
+            continue
+        cus = torch.cuda.get_device_properties(d).multi_processor_count
+        caps.append(max(8, (cus - cus // 4) // (co - 1)))
+    return caps
+
 class XgmiCommunicator(Communicator):
     """Single-node fp32 SUM all-reduce over IPC-mapped peer windows (csrc/comm/xgmi_allreduce.hip).
 
@@ -310,14 +350,18 @@ class XgmiCommunicator(Communicator):
             self._free()
             raise RuntimeError(f"xGMI peer mapping failed: {errs}")
         self.peers = (C.c_void_p * self.world)(*peers)
+        self.grid_cap = spin_grid_caps(control, [self.device], "xgmi_spin")[0]
         tc = int(os.environ.get("TDE_XGMI_TRACE", "0") or 0)
         self.trace = [_xg_trace_alloc(self.lib, self.device, self.epoch.value, tc)] if tc > 0 else None
 
     def nblocks(self, M):
+        """Chunks (= workgroups) of a call: ~512 elements of the slice each, within the kernel maximum and
+        the co-located-process spin limit (``spin_grid_caps``)."""
         if self.nblocks_override:
             return self.nblocks_override
         L = -(-M // self.world)
-        return max(8, min(self.lib.tde_xgmi_max_blocks(), L // 512))
+        nb = max(8, min(self.lib.tde_xgmi_max_blocks(), L // 512))
+        return min(nb, self.grid_cap) if self.grid_cap else nb
 
     def handles(self, t, op):
         return (op == "sum" and t.dtype == torch.float32 and t.is_cuda and t.is_contiguous()
@@ -592,18 +636,21 @@ class PeerXgmiCommunicator(Communicator):
             self._gargs.append(((C.c_void_p * len(flat))(*flat), (C.c_void_p * len(grp))(*[self.epochs[i] for i in grp]),
                                 (C.c_void_p * len(grp))(*[self.errs[i] for i in grp])))
         self._side = [torch.cuda.Stream(self.devices[grp[0]]) for grp in self.groups]
+        caps = spin_grid_caps(control, self.devices, "pxg_spin")
+        self.grid_caps = [caps[grp[0]] for grp in self.groups]
         tc = int(os.environ.get("TDE_XGMI_TRACE", "0") or 0)
         self.trace = [_xg_trace_alloc(self.lib, d, e, tc) for d, e in zip(self.devices, self.epochs)] \
             if tc > 0 else None
 
-    def nblocks(self, M, nloc=1):
-        """Chunks per rank.  A launch carrying several local ranks keeps its whole grid within the
-        single-rank maximum (nloc x nblocks <= 128): two processes sharing one GPU (the rehearsal of a
-        K-GPUs-per-worker layout) with 2 x 128-workgroup grouped launches measured peer waits that never
-        completed, the same launches at 2 x 8 workgroups ran clean (profiles/r3_xgmi_groups.log)."""
+    def nblocks(self, M, nloc=1, gi=0):
+        """Chunks per rank of group ``gi``'s launches (``nloc`` ranks in one grid): ~512 elements of the
+        slice each, within the kernel maximum, and the whole grid (nloc x chunks) within the
+        co-located-process spin limit of the group's device (``spin_grid_caps``; none when no other
+        process shares the GPU)."""
         cap = self.lib.tde_xgmi_max_blocks()
-        if os.environ.get("TDE_XGMI_GROUP_CAP", "1") != "0":
-            cap = max(1, cap // max(1, nloc))
+        gc = self.grid_caps[gi] if gi < len(self.grid_caps) else None
+        if gc:
+            cap = max(1, min(cap, gc // max(1, nloc)))
         if self.nblocks_override:
             return min(self.nblocks_override, cap)
         return max(min(8, cap), min(cap, -(-M // self.world) // 512))
@@ -632,16 +679,16 @@ class PeerXgmiCommunicator(Communicator):
             s = torch.cuda.current_stream(dev).cuda_stream
             rc = self.lib.tde_xgmi_all_reduce_group(
                 len(grp), (C.c_void_p * len(grp))(*[t.data_ptr() for t in grads]), M, self.max_elems, peers, epochs,
-                errs, self.rank0 + grp[0], self.world, self.nblocks(M, len(grp)), self.uncached, self.timeout_ticks,
+                errs, self.rank0 + grp[0], self.world, self.nblocks(M, len(grp), gi), self.uncached, self.timeout_ticks,
                 sp, s)
         if rc != 0:
             raise RuntimeError(f"tde_xgmi_all_reduce_group failed ({rc})")
 
     def push_spec(self, i, M, off):
         """``XgPush`` of local replica ``i`` (see ``XgmiCommunicator.push_spec``)."""
-        grp = next(g for g in self.groups if i in g)
+        gi = next(j for j, g in enumerate(self.groups) if i in g)
         return _push_spec(self.lib, M, self.max_elems, self.peers[i], self.epochs[i], self.rank0 + i, self.world,
-                          self.nblocks(M, len(grp)), off)
+                          self.nblocks(M, len(self.groups[gi]), gi), off)
 
     def all_reduce_(self, tensors, op="sum"):
         if len(tensors) != self.n_local or not all(self.handles(t, op, i) for i, t in enumerate(tensors)) or \
