@@ -12,3 +12,5 @@ rc=$?; echo "pytest rc=$rc"; tail -n 4 gpurun_out/pytest_d.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 bash scripts/prof_push.sh > gpurun_out/prof_push.out 2>&1
 echo "push rc=$?"; tail -n 12 gpurun_out/prof_push.out
+bash scripts/rehearse_scale.sh 2 4 8 > gpurun_out/rehearse.out 2>&1
+echo "rehearse rc=$?"; tail -n 12 gpurun_out/rehearse.out
