@@ -252,7 +252,8 @@ def _device_key(d):
     """Node-wide identity of a GPU (host + PCI location): equal keys = the same physical device."""
     import socket
     p = torch.cuda.get_device_properties(d)
-    return f"{socket.gethostname()}/{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+    return (f"{socket.gethostname()}/{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}/"
+            f"{getattr(p, 'uuid', '')}")
 
 
 def spin_grid_caps(control, devices, tag):

@@ -12,6 +12,7 @@ class _Props:
     def __init__(self, bus):
         self.pci_domain_id, self.pci_bus_id, self.pci_device_id = 0, bus, 0
         self.multi_processor_count = 256
+        self.uuid = f"gpu-{bus}"
 
 
 class _Ctl:
