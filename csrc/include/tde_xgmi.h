@@ -40,6 +40,13 @@ __device__ __forceinline__ void xg_push_store(const XgPush& p, int parity, long 
   xg_area(p.peer[s], 0, parity, p.cap)[(size_t)p.rank * p.L + (g - (long long)s * p.L)] = v;
 }
 
+// Four consecutive elements g..g+3 (g % 4 == 0, L % 4 == 0: one owner, a 16-byte aligned destination).
+__device__ __forceinline__ void xg_push_store4(const XgPush& p, int parity, long long g, float4 v) {
+  const int s = (int)(g / p.L);
+  *reinterpret_cast<float4*>(xg_area(p.peer[s], 0, parity, p.cap) + (size_t)p.rank * p.L +
+                             (g - (long long)s * p.L)) = v;
+}
+
 // A pushing wave waits for its stores' acknowledgements before it ends: on an N-GPU node they travel
 // over xGMI into peer HBM, and the all-reduce's flag that covers them is raised by the next launch, so
 // they must have completed, not merely been issued (the ordering the all-reduce gives its own phase-1

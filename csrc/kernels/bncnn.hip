@@ -1372,6 +1372,11 @@ __global__ __launch_bounds__(NTH) void reduce_kernel(ReduceArgs a) {
         s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w;
       }
     const bool inplace = p == a.out[j];
+    if (j == a.push_seg && ((a.push.off | a.push.L) & 3) == 0) {   // one 16-byte store into the owner
+      xg_push_store4(a.push, (int)((*a.push.epoch + 1u) & 1u), a.push.off + e0, s);
+      xg_push_drain();
+      return;
+    }
     reduce_commit(a, j, e0 + 0, s.x, t, inplace);
     reduce_commit(a, j, e0 + 1, s.y, t, inplace);
     reduce_commit(a, j, e0 + 2, s.z, t, inplace);

@@ -343,20 +343,26 @@ __global__ __launch_bounds__(1024) void convnet32_bwd_kernel(BwdArgs a) {
         if (MODE == 2 && a.h.kind == kOptAdam) a.v1[e] = v;
       }
     } else if (a.push.nranks > 0) {
-      // fused DP exchange: this position's complete dW1 rows go straight into the owners' contribution
-      // areas of the all-reduce call that follows this launch (its parity from the completed-calls count)
-      const int parity = (int)((*a.push.epoch + 1u) & 1u);
+      // fused DP exchange: this position's complete dW1 rows [32][64] are staged in W1s (free after the
+      // chunk loop) and pushed below as one contiguous 8 KB run of float4 stores
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        xg_push_store(a.push, parity, a.push.off + (long long)(p * CC + rt * 16 + fq * 4 + r) * HD + col, accw[r]);
+      for (int r = 0; r < 4; ++r) W1s[(rt * 16 + fq * 4 + r) * GS32 + col] = accw[r];
     } else {
 #pragma unroll
       for (int r = 0; r < 4; ++r) a.dW1[(size_t)(p * CC + rt * 16 + fq * 4 + r) * HD + col] = accw[r];
     }
   }
-  conv_grad_reduce(a, accr, dps, lane, wave);
+  conv_grad_reduce(a, accr, dps, lane, wave);   // its barrier also publishes the W1s staging
+  if (MODE == 0 && a.push.nranks > 0 && tid < CC * HD / 4) {
+    // the rows go straight into the owners' contribution areas of the all-reduce call that follows this
+    // launch (its parity from the completed-calls count); the bucket offset is a multiple of 4 (host check)
+    const int parity = (int)((*a.push.epoch + 1u) & 1u);
+    const int row = tid >> 4, c4 = (tid & 15) * 4;
+    xg_push_store4(a.push, parity, a.push.off + (long long)(p * CC + row) * HD + c4,
+                   *reinterpret_cast<const float4*>(W1s + row * GS32 + c4));
+    xg_push_drain();   // acknowledged before the wave ends
+  }
   stamp(a.stamps, 5);
-  if (MODE == 0 && a.push.nranks > 0) xg_push_drain();   // pushed rows acknowledged before the wave ends
 }
 
 }  // namespace tde
@@ -408,7 +414,9 @@ TDE_API int tde_convnet_bwd_f32(const float* x, const void* amax, int lda, const
                                 float* db2, float* db1, int B, int H, int W, long long* stamps, const TdeBwdOpt* opt,
                                 float* cpart, const XgPush* push, hipStream_t stream) {
   if (ldw1 != HD || ((uintptr_t)W1 & 15) || ((uintptr_t)Pt & 7)) return -1;
-  if (push && push->nranks > 0 && (opt || push->nranks > kXgMaxRanks || push->L <= 0 || !push->epoch)) return -7;
+  if (push && push->nranks > 0 &&
+      (opt || push->nranks > kXgMaxRanks || push->L <= 0 || (push->L & 3) || (push->off & 3) || !push->epoch))
+    return -7;
   if (opt && opt->w + opt->off_w1 != W1) return -3;   // the update is applied to the rows it reads
   BwdArgs a;
   const int rc = fill_bwd(a, x, amax, lda, hpre, hzero, hrep, hrep_stride, b1, W2, b2, C, pre_relu, labels, scale,

@@ -266,9 +266,10 @@ def spin_grid_caps(control, devices, tag):
     can only be dispatched onto a CU with no other wave on it.  When another PROCESS shares the GPU, its
     all-reduce grid can be spinning on every CU while this process's backward (which precedes this
     process's arrival at that very all-reduce) waits for a free CU: neither progresses until the peer
-    wait times out.  Graph replays keep the processes in lock-step (each reaches the all-reduce after
-    its backward is on the GPU), eager launches let one drift ahead, so eager hit it; 2 x 8-workgroup
-    grids left CUs free and ran clean.  One process per GPU (a real N-GPU node) never shares CUs with
+    wait times out.  Measured (profiles/r4_xgmi_hang/): without a limit, 2 workers x 2 replicas on one
+    GPU time out in eager AND graph mode with the MNIST CNN (the late process's all-reduce blocks start
+    only when the waiting grid gives up, although both hosts had enqueued within 1.5 ms), while Model B,
+    whose kernels fit beside a spinning wave, runs clean; with the limit every mode runs clean.  One process per GPU (a real N-GPU node) never shares CUs with
     its peers' kernels, so there is no limit then.  With ``co`` processes on one device, the other
     ``co - 1`` may all be spinning while this one needs whole CUs: each process keeps its grid within
     (CUs - CUs/4) / (co - 1), leaving a quarter of the chip free for whole-CU kernels.
