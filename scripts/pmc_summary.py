@@ -4,12 +4,14 @@
 
 Each pass directory gpurun_out/pmc_<model>_p<i>/ holds a *counter_collection.csv (one row per dispatch and
 counter).  Per kernel (summed over its dispatches) the table gives:
-  dur        mean dispatch time from the counter rows' timestamps (the counter run serialises dispatches)
-  MFMA %     100 * SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE * CUs * 4 SIMDs) (rocprofiler-sdk MfmaUtil),
-             GRBM_GUI_ACTIVE taken per XCD (the reported value divided by the number of XCDs)
-  busy %     SQ_BUSY_CYCLES / GRBM_GUI_ACTIVE
+  dur        mean dispatch time from the counter rows' timestamps (the counter run serialises dispatches,
+             so this is a little longer than in a graph replay)
+  MFMA %     SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs * dur * 2.4 GHz).  SQ_VALU_MFMA_BUSY_CYCLES is the sum
+             over SIMDs of matrix-core busy cycles: it equals SQ_INSTS_MFMA x 32 for these kernels, whose
+             MFMAs are all v_mfma_f32_16x16x4_f32 (8 passes = 32 cycles)
+  TF/s       f32 matrix FLOP rate = MFMA busy cycles x 64 FLOP / dur (157 TF/s = every SIMD busy)
   wait %     SQ_WAIT_ANY / SQ_WAVE_CYCLES (waves parked on s_waitcnt / barriers)
-  LDS conf.  SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS (bank-conflict cycles per LDS instruction cycle)
+  LDS conf.  SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS (bank-conflict cycles per LDS-issue cycle)
   HBM        (FETCH_SIZE + WRITE_SIZE) per dispatch, and that over the dispatch time
 """
 import collections
@@ -18,7 +20,7 @@ import glob
 import os
 import sys
 
-CUS, XCDS = 256, 8
+CUS, XCDS, CLK = 256, 8, 2.4   # CUs, XCDs, shader clock in GHz (cycles per ns)
 
 
 def load(pass_dir):
@@ -53,9 +55,9 @@ def summarise(root, model):
         n1 = sum(1 for (tag, _) in durs[k] if tag.endswith("_p1"))
         dl = list(durs[k].values())
         dur = sum(dl) / len(dl) if dl else 0.0
-        g1 = cs.get(f"GRBM_GUI_ACTIVE@pmc_{model}_p1", 0.0) / XCDS
-        mfma = 100.0 * cs.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (g1 * CUS * 4) if g1 else 0.0
-        busy = 100.0 * cs.get("SQ_BUSY_CYCLES", 0.0) / (g1 * XCDS) if g1 else 0.0
+        mb = cs.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / max(n1, 1)        # per dispatch
+        mfma = 100.0 * mb / (CUS * 4 * dur * CLK) if dur else 0.0
+        busy = mb * 64 / dur / 1e3 if dur else 0.0                       # TFLOP/s (FLOP / ns / 1e3)
         wave = cs.get("SQ_WAVE_CYCLES", 0.0)
         wait = 100.0 * cs.get("SQ_WAIT_ANY", 0.0) / wave if wave else 0.0
         lds_act = cs.get("SQ_ACTIVE_INST_LDS", 0.0)
@@ -69,11 +71,11 @@ def summarise(root, model):
                      cs.get("SQ_INSTS_MFMA", 0.0) / max(n1, 1)))
     rows.sort(key=lambda r: -r[0])
     print(f"\n## {model}\n")
-    print("| kernel | dispatches | dur µs | MFMA % | busy % | wait % | LDS conf/inst | HBM B/dispatch | HBM GB/s | MFMA insts/dispatch |")
+    print("| kernel | dispatches | dur µs | MFMA % | TF/s | wait % | LDS conf. | HBM / dispatch | HBM GB/s | MFMA insts / dispatch |")
     print("|---|---|---|---|---|---|---|---|---|---|")
     for (_, k, n, dur, mfma, busy, wait, conf, hb, gbs, mi) in rows[:12]:
         name = k if len(k) <= 70 else k[:67] + "..."
-        print(f"| `{name}` | {n} | {dur / 1e3:.2f} | {mfma:.1f} | {busy:.0f} | {wait:.0f} | {conf:.2f} | "
+        print(f"| `{name}` | {n} | {dur / 1e3:.2f} | {mfma:.1f} | {busy:.1f} | {wait:.0f} | {conf:.2f} | "
               f"{hb / 1e6:.2f} MB | {gbs:.0f} | {mi:.0f} |")
 
 
