@@ -18,7 +18,7 @@ step() {  # name timeout cmd...
 }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
-  step pytest_gpu ${PYTEST_TIMEOUT:-1000} python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread
+  step pytest_gpu ${PYTEST_TIMEOUT:-1000} python -u -m pytest tests -m gpu -q -rf --capture=sys --timeout 120 --timeout-method thread
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then

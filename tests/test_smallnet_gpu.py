@@ -2,7 +2,8 @@
 reference plan: per-variable gradients, metrics, eval and predict, the in-step optimizer ("local")
 against the separate optimizer ("plain"), and fit() end to end (BASELINE.json config 2, LeNet-5).
 
-Both sides compute in fp32, so the bounds are tight (reduction order only)."""
+Both sides compute in fp32, so the bounds are tight (reduction order only).  The reference runs on the
+CPU (plain PyTorch fp32 ops, no GPU library in the oracle)."""
 import numpy as np
 import pytest
 import torch
@@ -56,16 +57,16 @@ def test_smallnet_gradients_match_fp32_reference(name, B, Bplan):
     tde.backend.set_random_seed(1)
     m = _build(tde, name)
     st = m._store
-    st_ref = st.clone_to("cuda")
+    st_ref = st.clone_to("cpu")
     plan = PG.make_plan(m, st, "cuda", Bplan, Bplan, m.optimizer, m.loss)
-    ref = PG.ReferencePlan(m, st_ref, "cuda", Bplan, Bplan, m.optimizer, m.loss)
+    ref = PG.ReferencePlan(m, st_ref, "cpu", Bplan, Bplan, m.optimizer, m.loss)
     assert plan.kind == "fused_smallnet"
     x, y = _data(m, Bplan, 3)
     plan.train_step(x, y, B)
-    ref.train_step(x, y.long(), B)
     torch.cuda.synchronize()
+    ref.train_step(x.cpu(), y.long().cpu(), B)
     for n in st.names(trainable=True):
-        r = _rel(st.grad(n), st_ref.grad(n))
+        r = _rel(st.grad(n).cpu(), st_ref.grad(n))
         assert r < 1e-4, (n, r)
     mf, mr = plan.metrics.cpu(), ref.metrics.cpu()
     assert abs(mf[0] - mr[0]) < 1e-4 * abs(mr[0]) and mf[1] == mr[1] and mf[2] == mr[2] == B
@@ -79,14 +80,14 @@ def test_smallnet_eval_and_predict_match_reference(name):
     tde.backend.set_random_seed(2)
     m = _build(tde, name)
     plan = PG.make_plan(m, m._store, "cuda", 50, 50, None, m.loss)
-    ref = PG.ReferencePlan(m, m._store, "cuda", 50, 50, None, m.loss)
+    ref = PG.ReferencePlan(m, m._store.clone_to("cpu"), "cpu", 50, 50, None, m.loss)
     x, y = _data(m, 50, 4)
     plan.eval_step(x, y, 50)
-    ref.eval_step(x, y.long(), 50)
     p = plan.predict(x, 41).clone()
-    pr = ref.predict(x, 41)
     torch.cuda.synchronize()
-    assert _rel(p, pr) < 1e-5
+    ref.eval_step(x.cpu(), y.long().cpu(), 50)
+    pr = ref.predict(x.cpu(), 41)
+    assert _rel(p.cpu(), pr) < 1e-5
     mf, mr = plan.metrics.cpu(), ref.metrics.cpu()
     assert abs(mf[0] - mr[0]) < 1e-4 * abs(mr[0]) and mf[1] == mr[1] and mf[2] == mr[2]
 
