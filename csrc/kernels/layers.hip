@@ -3267,9 +3267,30 @@ static bool bn_tiled_ok(int C, std::initializer_list<const void*> ptrs) {
 }
 
 // streaming grid: ~16K elements per block (prologue amortised), 512..4096 blocks
+// Grid of the streaming BN passes: n / div blocks within [lo, hi] (TDE_BN_STREAM="div,lo,hi"), and of
+// the backward reduction (TDE_BN_RED="div,lo,hi"; each of its blocks ends with 2*min(C,64) atomics).
+struct BnGrid {
+  long long div, lo, hi;
+};
+static BnGrid bn_grid_env(const char* name, BnGrid d) {
+  const char* e = getenv(name);
+  if (e) {
+    long long a = 0, b = 0, c = 0;
+    if (sscanf(e, "%lld,%lld,%lld", &a, &b, &c) == 3 && a > 0 && b > 0 && c >= b) d = BnGrid{a, b, c};
+  }
+  return d;
+}
+static int bn_grid_blocks(long long n, const BnGrid& g) {
+  const long long b = n / g.div;
+  return (int)(b < g.lo ? g.lo : (b > g.hi ? g.hi : b));
+}
 static int bn_stream_blocks(long long n) {
-  long long b = n / 16384;
-  return (int)(b < 512 ? 512 : (b > 4096 ? 4096 : b));
+  static const BnGrid g = bn_grid_env("TDE_BN_STREAM", BnGrid{16384, 512, 4096});
+  return bn_grid_blocks(n, g);
+}
+static int bn_reduce_blocks(long long n) {
+  static const BnGrid g = bn_grid_env("TDE_BN_RED", BnGrid{32768, 256, 1024});
+  return bn_grid_blocks(n, g);
 }
 
 TDE_API int tde_bn_fwd(const bf16* y, bf16* out, const bf16* res, long long R, int C, int mode, const double* stats,
@@ -3302,9 +3323,7 @@ TDE_API int tde_bn_bwd(const bf16* dout, const bf16* y, const bf16* res, long lo
   if (bn_tiled_ok(C, {dout, y, res, dx, dres})) {
     if (mode == 1) {
       // each block ends with 2*min(C,64) global atomics: a moderate grid, deep per-thread ILP
-      long long want = R * C / 32768;
-      want = want < 256 ? 256 : (want > 1024 ? 1024 : want);
-      bn_bwd_reduce_tiled_kernel<<<bn_tiled_grid(R, C, (int)want), 256, 0, stream>>>(a);
+      bn_bwd_reduce_tiled_kernel<<<bn_tiled_grid(R, C, bn_reduce_blocks(R * C)), 256, 0, stream>>>(a);
       TDE_LAUNCH_CHECK();
     }
     bn_bwd_apply_tiled_kernel<<<bn_tiled_grid(R, C, bn_stream_blocks(R * C)), 256, 0, stream>>>(a);
