@@ -120,28 +120,45 @@ __device__ __forceinline__ void publish(char* const* peer, int nranks, int parit
   }
 }
 
-// Thread 0 waits until every rank's flag of (parity, phase, blk) equals `epoch`; returns (thread 0) the
-// first source whose flag never arrived, 0xff when all did, and in `seen` the value that flag held when
-// the wait gave up (diagnostics: an older epoch = never written, a newer one = overwritten early).
+// Wave 0 waits until every rank's flag of (parity, phase, blk) equals `epoch`: lane s polls source s, so
+// the N flags cost one memory round trip per poll, not N in sequence (with 8 ranks the sequential walk was
+// up to 7 extra round trips per phase).  Returns (thread 0) the first source whose flag never arrived, 0xff
+// when all did, and in `seen` the value that flag held when the wait gave up (diagnostics: an older epoch
+// = never written, a newer one = overwritten early).
 __device__ __forceinline__ uint32_t await(char* base, int parity, int phase, int nranks, int blk, uint32_t epoch,
                                           long long timeout, uint32_t* err, uint32_t bit, uint32_t& seen) {
   uint32_t missing = 0xffu;
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const bool mine = lane < nranks;
+    const uint32_t* f = flag_ptr(base, parity, phase, mine ? lane : 0, blk);
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-    bool ok = true;
-    int s = 0;
-    for (; s < nranks && ok; ++s) {
-      uint32_t* f = flag_ptr(base, parity, phase, s, blk);
-      while ((seen = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != epoch) {
-        __builtin_amdgcn_s_sleep(2);
-        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
-          ok = false;
-          break;
-        }
+    bool ok = !mine;
+    uint32_t v = epoch;
+    unsigned long long pend;
+    bool timed_out = false;
+    while (true) {
+      if (!ok) {
+        v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        ok = v == epoch;
+      }
+      pend = __ballot(!ok);
+      if (pend == 0ull) break;
+      if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+        timed_out = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (timed_out) {
+      const int first = __ffsll((long long)pend) - 1;
+      const uint32_t fv = __shfl(v, first, 64);
+      if (lane == 0) {
+        missing = (uint32_t)first;
+        seen = fv;
+        __hip_atomic_fetch_or(err, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
-    missing = ok ? 0xffu : (uint32_t)(s - 1);
-    if (!ok) __hip_atomic_fetch_or(err, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __atomic_thread_fence(__ATOMIC_ACQUIRE);   // system scope: drop stale L1/L2 lines
     drain_stores();
   }
