@@ -188,9 +188,7 @@ __device__ __forceinline__ void shadow_store(const XgArgs& a, long long e, float
 }
 
 // Optimizer step on n reduced elements (global index g0..): w, slots, shadows; grad zeroed.
-// w0 / have0: this thread's first float4 of w (elements g0 + 4*tid ..), loaded before the phase-2 wait.
-__device__ __forceinline__ void apply_chunk(const XgArgs& a, float lr_t, long long g0, const float* red, long long n,
-                                            float4 w0 = float4{0.f, 0.f, 0.f, 0.f}, bool have0 = false) {
+__device__ __forceinline__ void apply_chunk(const XgArgs& a, float lr_t, long long g0, const float* red, long long n) {
   const int tid = threadIdx.x;
   const bool mom = a.h.kind != kOptSGD, adam = a.h.kind == kOptAdam;
   long long nv = 0;
@@ -199,7 +197,7 @@ __device__ __forceinline__ void apply_chunk(const XgArgs& a, float lr_t, long lo
     for (long long i = tid; i < nv; i += kXgThreads) {
       const long long e = g0 + 4 * i;
       const float4 gs = reinterpret_cast<const float4*>(red)[i];
-      float4 w = (have0 && i == tid) ? w0 : *reinterpret_cast<const float4*>(a.w + e);
+      float4 w = *reinterpret_cast<const float4*>(a.w + e);
       float4 m = {0.f, 0.f, 0.f, 0.f}, v = {0.f, 0.f, 0.f, 0.f};
       if (mom) m = *reinterpret_cast<const float4*>(a.m + e);
       if (adam) v = *reinterpret_cast<const float4*>(a.v + e);
@@ -309,26 +307,13 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
   // ---- phase 3: gather every reduced slice chunk back into the bucket (or apply the update)
   float lr_t = 0.f;
   if (a.apply) lr_t = opt_lr_t(a.h, a.h.kind == kOptAdam ? *a.iterations : 0);
-  // the update's first float4 of w per slice is loaded now, so its latency hides under the phase-2 wait
-  // (only this block writes these elements, in this phase; register-resident: static slot per slice)
-  float4 wpre[kXgMaxRanks];
-  bool wok[kXgMaxRanks];
-#pragma unroll
-  for (int s = 0; s < kXgMaxRanks; ++s) {
-    const long long g0 = (long long)s * L + c0;
-    const long long n = max(0LL, min(CH, M - g0));
-    wok[s] = a.apply && s < N && (g0 & 3) == 0 && 4LL * tid + 4 <= n;
-    wpre[s] = wok[s] ? *reinterpret_cast<const float4*>(a.w + g0 + 4 * tid) : float4{0.f, 0.f, 0.f, 0.f};
-  }
   miss2 = await(a.peer[r], parity, 1, N, blk, epoch, a.timeout_ticks, a.err, 2u, seen2);
   XG_STAMP(5);
   const float* out = area(a.peer[r], 1, parity, cap);
-#pragma unroll
-  for (int s = 0; s < kXgMaxRanks; ++s) {
-    if (s >= N) break;
+  for (int s = 0; s < N; ++s) {
     const long long g0 = (long long)s * L + c0;
     const long long n = max(0LL, min(CH, M - g0));
-    if (a.apply) apply_chunk(a, lr_t, g0, out + (size_t)s * L + c0, n, wpre[s], wok[s]);
+    if (a.apply) apply_chunk(a, lr_t, g0, out + (size_t)s * L + c0, n);
     else copy_chunk(a.grad + g0, out + (size_t)s * L + c0, n, (g0 & 3) == 0);
   }
   if (tr) {
