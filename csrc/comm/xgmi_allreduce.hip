@@ -245,76 +245,67 @@ __device__ __forceinline__ uint2 ll_load(const uint2* p) {
       __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   return uint2{(uint32_t)v, (uint32_t)(v >> 32)};
 }
-// kLLU elements per thread per LL wait; the spins re-load only the pairs not yet carrying `epoch` and give
-// up after `timeout` (returning the first source still missing, 0xff when none, and its flag in `seen`).
-constexpr int kLLU = 2;
-// phase 2: q[u][k] = pair of element i0 + u * kXgThreads (< n) from source k (< N) at in + k * L + i
-__device__ __forceinline__ uint32_t ll_spin(uint2 (&q)[kLLU][kXgMaxRanks], const uint2* in, long long L, long long i0,
-                                            long long n, int N, uint32_t epoch, long long timeout, uint32_t& seen) {
-  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-  while (true) {
-    bool all = true;
-#pragma unroll
-    for (int u = 0; u < kLLU; ++u)
-#pragma unroll
-      for (int k = 0; k < kXgMaxRanks; ++k) all = all && q[u][k].y == epoch;
-    if (all) return 0xffu;
-    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
-      uint32_t miss = 0xffu;
-#pragma unroll
-      for (int u = 0; u < kLLU; ++u)
-#pragma unroll
-        for (int k = kXgMaxRanks - 1; k >= 0; --k)
-          if (q[u][k].y != epoch) {
-            miss = (uint32_t)k;
-            seen = q[u][k].y;
-          }
-      return miss;
-    }
-    __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-    for (int u = 0; u < kLLU; ++u)
-#pragma unroll
-      for (int k = 0; k < kXgMaxRanks; ++k) {
-        const long long i = i0 + (long long)u * kXgThreads;
-        if (q[u][k].y != epoch && k < N && i < n) q[u][k] = ll_load(in + (size_t)k * L + i);
-      }
-  }
+__device__ __forceinline__ void ll_store4(uint2* d, float4 v, uint32_t e) {
+  uint4* q = reinterpret_cast<uint4*>(d);
+  q[0] = uint4{__float_as_uint(v.x), e, __float_as_uint(v.y), e};
+  q[1] = uint4{__float_as_uint(v.z), e, __float_as_uint(v.w), e};
 }
-// phase 3: q[u][k] = pair of element i = i0 + u * kXgThreads of slice k's chunk (out + k * L + i) when that
-// element exists (i < chunk, k * L + c0 + i < M)
-__device__ __forceinline__ uint32_t ll_spin3(uint2 (&q)[kLLU][kXgMaxRanks], const uint2* out, long long L,
-                                             long long c0, long long M, long long i0, int N, uint32_t epoch,
-                                             long long timeout, uint32_t& seen) {
+// Polls the 4 pairs of each of the nsrc sources src[s] (static slots s < kXgMaxRanks) until every pair carries
+// `epoch`, or the timeout: returns the first source still missing (0xff: none) and its flag in `seen`.
+__device__ __forceinline__ uint32_t ll_wait(const uint2* const (&src)[kXgMaxRanks], const bool (&use)[kXgMaxRanks],
+                                            uint32_t epoch, long long timeout, float4 (&val)[kXgMaxRanks],
+                                            uint32_t& seen) {
+  uint2 q[kXgMaxRanks][4];
+#pragma unroll
+  for (int s = 0; s < kXgMaxRanks; ++s)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[s][k] = use[s] ? ll_load(src[s] + k) : uint2{0u, epoch};
   const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  uint32_t missing = 0xffu;
   while (true) {
     bool all = true;
 #pragma unroll
-    for (int u = 0; u < kLLU; ++u)
+    for (int s = 0; s < kXgMaxRanks; ++s)
 #pragma unroll
-      for (int k = 0; k < kXgMaxRanks; ++k) all = all && q[u][k].y == epoch;
-    if (all) return 0xffu;
+      for (int k = 0; k < 4; ++k) all = all && q[s][k].y == epoch;
+    if (all) break;
     if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
-      uint32_t miss = 0xffu;
 #pragma unroll
-      for (int u = 0; u < kLLU; ++u)
+      for (int s = kXgMaxRanks - 1; s >= 0; --s)
 #pragma unroll
-        for (int k = kXgMaxRanks - 1; k >= 0; --k)
-          if (q[u][k].y != epoch) {
-            miss = (uint32_t)k;
-            seen = q[u][k].y;
+        for (int k = 0; k < 4; ++k)
+          if (q[s][k].y != epoch) {
+            missing = (uint32_t)s;
+            seen = q[s][k].y;
           }
-      return miss;
+      break;
     }
     __builtin_amdgcn_s_sleep(1);
 #pragma unroll
-    for (int u = 0; u < kLLU; ++u)
+    for (int s = 0; s < kXgMaxRanks; ++s)
 #pragma unroll
-      for (int k = 0; k < kXgMaxRanks; ++k) {
-        const long long i = i0 + (long long)u * kXgThreads;
-        if (q[u][k].y != epoch && k < N && (long long)k * L + c0 + i < M) q[u][k] = ll_load(out + (size_t)k * L + i);
-      }
+      for (int k = 0; k < 4; ++k)
+        if (q[s][k].y != epoch) q[s][k] = ll_load(src[s] + k);
   }
+#pragma unroll
+  for (int s = 0; s < kXgMaxRanks; ++s)
+    val[s] = float4{__uint_as_float(q[s][0].x), __uint_as_float(q[s][1].x), __uint_as_float(q[s][2].x),
+                    __uint_as_float(q[s][3].x)};
+  return missing;
+}
+// Scalar form (bucket tails): one pair of one source.
+__device__ __forceinline__ float ll_wait1(const uint2* p, uint32_t epoch, long long timeout, bool& late) {
+  uint2 q = ll_load(p);
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  while (q.y != epoch) {
+    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+      late = true;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    q = ll_load(p);
+  }
+  return __uint_as_float(q.x);
 }
 
 // One launch carries the parts of NL ranks (grid.y = local rank): several replicas of one process on
@@ -349,8 +340,6 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
 
   if (UNCACHED && a.ll) {
     // ================= LL protocol: pairs {value, epoch}; the data is the arrival signal =================
-    // Element-granular (lane j of a wave handles element base + j): every pair load / store of a wave is one
-    // contiguous 512-byte run; kLLU elements per thread are awaited together.
     const long long llcap = a.llcap;
     const long long tmo = a.timeout_ticks;
     uint32_t bad = 0u;
@@ -360,7 +349,17 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
       const long long n = max(0LL, min(CH, M - g0));
       uint2* dst = xg_ll_area(a.peer[s], 0, parity, cap, llcap) + (size_t)r * L + c0;
       const long long plo = min(max(a.push_lo - g0, 0LL), n), phi = min(max(a.push_hi - g0, 0LL), n);
-      for (long long i = tid; i < n; i += kXgThreads)
+      const long long nv = n >> 2;
+      for (long long j = tid; j < nv; j += kXgThreads) {
+        const long long i = 4 * j;
+        if (i + 4 <= plo || i >= phi) {
+          ll_store4(dst + i, *reinterpret_cast<const float4*>(a.grad + g0 + i), epoch);
+        } else {
+          for (int k = 0; k < 4; ++k)
+            if (i + k < plo || i + k >= phi) dst[i + k] = uint2{__float_as_uint(a.grad[g0 + i + k]), epoch};
+        }
+      }
+      for (long long i = (nv << 2) + tid; i < n; i += kXgThreads)
         if (i < plo || i >= phi) dst[i] = uint2{__float_as_uint(a.grad[g0 + i]), epoch};
     }
     XG_STAMP(2);
@@ -370,31 +369,40 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
       const long long g0 = (long long)r * L + c0;
       const long long n = max(0LL, min(CH, M - g0));
       const uint2* in = xg_ll_area(a.peer[r], 0, parity, cap, llcap) + c0;
-      for (long long i0 = tid; i0 < n; i0 += (long long)kLLU * kXgThreads) {
-        uint2 q[kLLU][kXgMaxRanks];
+      const long long nv = n >> 2;
+      bool use[kXgMaxRanks];
 #pragma unroll
-        for (int u = 0; u < kLLU; ++u)
+      for (int s = 0; s < kXgMaxRanks; ++s) use[s] = s < N;
+      for (long long j = tid; j < nv; j += kXgThreads) {
+        const uint2* src[kXgMaxRanks];
 #pragma unroll
-          for (int k = 0; k < kXgMaxRanks; ++k) {
-            const long long i = i0 + (long long)u * kXgThreads;
-            q[u][k] = (k < N && i < n) ? ll_load(in + (size_t)k * L + i) : uint2{0u, epoch};
-          }
-        const uint32_t m = ll_spin(q, in, L, i0, n, N, epoch, tmo, seen1);
+        for (int s = 0; s < kXgMaxRanks; ++s) src[s] = in + (size_t)(s < N ? s : 0) * L + 4 * j;
+        float4 v[kXgMaxRanks];
+        uint32_t sn = 0u;
+        const uint32_t m = ll_wait(src, use, epoch, tmo, v, sn);
         if (m != 0xffu) {
           bad |= 1u;
-          if (tid == 0 && miss1 == 0xffu) miss1 = m;
+          if (tid == 0 && miss1 == 0xffu) {
+            miss1 = m;
+            seen1 = sn;
+          }
         }
+        float4 acc = v[0];
 #pragma unroll
-        for (int u = 0; u < kLLU; ++u) {
-          const long long i = i0 + (long long)u * kXgThreads;
-          if (i >= n) continue;
-          float acc = __uint_as_float(q[u][0].x);
-#pragma unroll
-          for (int k = 1; k < kXgMaxRanks; ++k)
-            if (k < N) acc += __uint_as_float(q[u][k].x);
-          for (int p = 0; p < N; ++p)
-            xg_ll_area(a.peer[p], 1, parity, cap, llcap)[(size_t)r * L + c0 + i] = uint2{__float_as_uint(acc), epoch};
-        }
+        for (int s = 1; s < kXgMaxRanks; ++s)
+          if (s < N) {
+            acc.x += v[s].x; acc.y += v[s].y; acc.z += v[s].z; acc.w += v[s].w;
+          }
+        for (int p = 0; p < N; ++p)
+          ll_store4(xg_ll_area(a.peer[p], 1, parity, cap, llcap) + (size_t)r * L + c0 + 4 * j, acc, epoch);
+      }
+      for (long long i = (nv << 2) + tid; i < n; i += kXgThreads) {
+        bool late = false;
+        float acc = ll_wait1(in + i, epoch, tmo, late);
+        for (int s = 1; s < N; ++s) acc += ll_wait1(in + (size_t)s * L + i, epoch, tmo, late);
+        if (late) bad |= 1u;
+        for (int p = 0; p < N; ++p)
+          xg_ll_area(a.peer[p], 1, parity, cap, llcap)[(size_t)r * L + c0 + i] = uint2{__float_as_uint(acc), epoch};
       }
     }
     XG_STAMP(3);
@@ -404,33 +412,46 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
     {
       float lr_t = 0.f;
       if (a.apply) lr_t = opt_lr_t(a.h, a.h.kind == kOptAdam ? *a.iterations : 0);
-      const uint2* out = xg_ll_area(a.peer[r], 1, parity, cap, llcap) + c0;   // + s * L + i
-      for (long long i0 = tid; i0 < CH; i0 += (long long)kLLU * kXgThreads) {
-        uint2 q[kLLU][kXgMaxRanks];
+      const uint2* out = xg_ll_area(a.peer[r], 1, parity, cap, llcap);
+      const long long nvmax = CH >> 2;
+      for (long long j = tid; j < nvmax; j += kXgThreads) {
+        const uint2* src[kXgMaxRanks];
+        bool use[kXgMaxRanks];
 #pragma unroll
-        for (int u = 0; u < kLLU; ++u)
-#pragma unroll
-          for (int k = 0; k < kXgMaxRanks; ++k) {
-            const long long i = i0 + (long long)u * kXgThreads;
-            const bool in_slice = k < N && i < CH && (long long)k * L + c0 + i < M;
-            q[u][k] = in_slice ? ll_load(out + (size_t)k * L + i) : uint2{0u, epoch};
-          }
-        const uint32_t m = ll_spin3(q, out, L, c0, M, i0, N, epoch, tmo, seen2);
+        for (int s = 0; s < kXgMaxRanks; ++s) {
+          const long long g0 = (long long)s * L + c0;
+          const long long n = s < N ? max(0LL, min(CH, M - g0)) : 0LL;
+          use[s] = 4 * j + 4 <= n;
+          src[s] = out + (use[s] ? (size_t)(g0 + 4 * j) : (size_t)0);
+        }
+        float4 v[kXgMaxRanks];
+        uint32_t sn = 0u;
+        const uint32_t m = ll_wait(src, use, epoch, tmo, v, sn);
         if (m != 0xffu) {
           bad |= 2u;
-          if (tid == 0 && miss2 == 0xffu) miss2 = m;
+          if (tid == 0 && miss2 == 0xffu) {
+            miss2 = m;
+            seen2 = sn;
+          }
         }
 #pragma unroll
-        for (int u = 0; u < kLLU; ++u)
-#pragma unroll
-          for (int k = 0; k < kXgMaxRanks; ++k) {
-            const long long i = i0 + (long long)u * kXgThreads;
-            const long long e = (long long)k * L + c0 + i;
-            if (k >= N || i >= CH || e >= M) continue;
-            const float v = __uint_as_float(q[u][k].x);
-            if (a.apply) apply1(a, lr_t, e, v);
-            else a.grad[e] = v;
-          }
+        for (int s = 0; s < kXgMaxRanks; ++s) {
+          if (!use[s]) continue;
+          const long long e = (long long)s * L + c0 + 4 * j;
+          if (a.apply) apply4(a, lr_t, e, v[s]);
+          else *reinterpret_cast<float4*>(a.grad + e) = v[s];
+        }
+      }
+      for (int s = 0; s < N; ++s) {   // tails: a slice chunk whose length is not a multiple of 4
+        const long long g0 = (long long)s * L + c0;
+        const long long n = max(0LL, min(CH, M - g0));
+        for (long long i = ((n >> 2) << 2) + tid; i < n; i += kXgThreads) {
+          bool late = false;
+          const float v = ll_wait1(out + g0 + i, epoch, tmo, late);
+          if (late) bad |= 2u;
+          if (a.apply) apply1(a, lr_t, g0 + i, v);
+          else a.grad[g0 + i] = v;
+        }
       }
     }
     XG_STAMP(5);
