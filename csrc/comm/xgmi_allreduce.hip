@@ -90,9 +90,6 @@ struct XgArgs {
   // [push_lo, push_hi): bucket elements a producer kernel already stored into the owners' contribution
   // areas (tde_xgmi.h XgPush); phase 1 skips them
   long long push_lo, push_hi;
-  // LL protocol for this call (tde_xgmi.h xg_ll_area): pairs {value, epoch} instead of data + flags
-  int ll;
-  long long llcap;
 };
 constexpr int kXgTraceWords = 8;
 
@@ -190,122 +187,49 @@ __device__ __forceinline__ void shadow_store(const XgArgs& a, long long e, float
   if (a.sht) a.sht[(q % a.sh_cols) * a.sht_ld + q / a.sh_cols] = h;
 }
 
-// Optimizer step of the 4 elements e..e+3 (e % 4 == 0) from their reduced gradient gs: w, slots, shadows;
-// grad zeroed.
-__device__ __forceinline__ void apply4(const XgArgs& a, float lr_t, long long e, float4 gs) {
-  const bool mom = a.h.kind != kOptSGD, adam = a.h.kind == kOptAdam;
-  float4 w = *reinterpret_cast<const float4*>(a.w + e);
-  float4 m = {0.f, 0.f, 0.f, 0.f}, v = {0.f, 0.f, 0.f, 0.f};
-  if (mom) m = *reinterpret_cast<const float4*>(a.m + e);
-  if (adam) v = *reinterpret_cast<const float4*>(a.v + e);
-  w.x = opt_step(a.h, lr_t, w.x, gs.x, m.x, v.x);
-  w.y = opt_step(a.h, lr_t, w.y, gs.y, m.y, v.y);
-  w.z = opt_step(a.h, lr_t, w.z, gs.z, m.z, v.z);
-  w.w = opt_step(a.h, lr_t, w.w, gs.w, m.w, v.w);
-  *reinterpret_cast<float4*>(a.w + e) = w;
-  if (mom) *reinterpret_cast<float4*>(a.m + e) = m;
-  if (adam) *reinterpret_cast<float4*>(a.v + e) = v;
-  *reinterpret_cast<float4*>(a.grad + e) = float4{0.f, 0.f, 0.f, 0.f};
-  if (e >= a.sh_lo && e + 4 <= a.sh_hi && !a.sht) {
-    *reinterpret_cast<bf16x4*>(a.sh + (e - a.sh_lo)) = bf16x4{f2bf(w.x), f2bf(w.y), f2bf(w.z), f2bf(w.w)};
-  } else {
-    shadow_store(a, e, w.x);
-    shadow_store(a, e + 1, w.y);
-    shadow_store(a, e + 2, w.z);
-    shadow_store(a, e + 3, w.w);
-  }
-}
-__device__ __forceinline__ void apply1(const XgArgs& a, float lr_t, long long e, float g) {
-  const bool mom = a.h.kind != kOptSGD, adam = a.h.kind == kOptAdam;
-  float m = mom ? a.m[e] : 0.f, v = adam ? a.v[e] : 0.f;
-  const float w = opt_step(a.h, lr_t, a.w[e], g, m, v);
-  a.w[e] = w;
-  if (mom) a.m[e] = m;
-  if (adam) a.v[e] = v;
-  a.grad[e] = 0.f;
-  shadow_store(a, e, w);
-}
-
-// Optimizer step on n reduced elements (global index g0..).
+// Optimizer step on n reduced elements (global index g0..): w, slots, shadows; grad zeroed.
 __device__ __forceinline__ void apply_chunk(const XgArgs& a, float lr_t, long long g0, const float* red, long long n) {
   const int tid = threadIdx.x;
+  const bool mom = a.h.kind != kOptSGD, adam = a.h.kind == kOptAdam;
   long long nv = 0;
   if ((g0 & 3) == 0) {   // area offsets are multiples of 4 elements
     nv = n >> 2;
-    for (long long i = tid; i < nv; i += kXgThreads)
-      apply4(a, lr_t, g0 + 4 * i, reinterpret_cast<const float4*>(red)[i]);
+    for (long long i = tid; i < nv; i += kXgThreads) {
+      const long long e = g0 + 4 * i;
+      const float4 gs = reinterpret_cast<const float4*>(red)[i];
+      float4 w = *reinterpret_cast<const float4*>(a.w + e);
+      float4 m = {0.f, 0.f, 0.f, 0.f}, v = {0.f, 0.f, 0.f, 0.f};
+      if (mom) m = *reinterpret_cast<const float4*>(a.m + e);
+      if (adam) v = *reinterpret_cast<const float4*>(a.v + e);
+      w.x = opt_step(a.h, lr_t, w.x, gs.x, m.x, v.x);
+      w.y = opt_step(a.h, lr_t, w.y, gs.y, m.y, v.y);
+      w.z = opt_step(a.h, lr_t, w.z, gs.z, m.z, v.z);
+      w.w = opt_step(a.h, lr_t, w.w, gs.w, m.w, v.w);
+      *reinterpret_cast<float4*>(a.w + e) = w;
+      if (mom) *reinterpret_cast<float4*>(a.m + e) = m;
+      if (adam) *reinterpret_cast<float4*>(a.v + e) = v;
+      *reinterpret_cast<float4*>(a.grad + e) = float4{0.f, 0.f, 0.f, 0.f};
+      if (e >= a.sh_lo && e + 4 <= a.sh_hi && !a.sht) {
+        *reinterpret_cast<bf16x4*>(a.sh + (e - a.sh_lo)) = bf16x4{f2bf(w.x), f2bf(w.y), f2bf(w.z), f2bf(w.w)};
+      } else {
+        shadow_store(a, e, w.x);
+        shadow_store(a, e + 1, w.y);
+        shadow_store(a, e + 2, w.z);
+        shadow_store(a, e + 3, w.w);
+      }
+    }
     nv <<= 2;
   }
-  for (long long i = nv + tid; i < n; i += kXgThreads) apply1(a, lr_t, g0 + i, red[i]);
-}
-
-// ---- LL protocol pieces
-__device__ __forceinline__ uint2 ll_load(const uint2* p) {
-  const unsigned long long v =
-      __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  return uint2{(uint32_t)v, (uint32_t)(v >> 32)};
-}
-__device__ __forceinline__ void ll_store4(uint2* d, float4 v, uint32_t e) {
-  uint4* q = reinterpret_cast<uint4*>(d);
-  q[0] = uint4{__float_as_uint(v.x), e, __float_as_uint(v.y), e};
-  q[1] = uint4{__float_as_uint(v.z), e, __float_as_uint(v.w), e};
-}
-// Polls the 4 pairs of each of the nsrc sources src[s] (static slots s < kXgMaxRanks) until every pair carries
-// `epoch`, or the timeout: returns the first source still missing (0xff: none) and its flag in `seen`.
-__device__ __forceinline__ uint32_t ll_wait(const uint2* const (&src)[kXgMaxRanks], const bool (&use)[kXgMaxRanks],
-                                            uint32_t epoch, long long timeout, float4 (&val)[kXgMaxRanks],
-                                            uint32_t& seen) {
-  uint2 q[kXgMaxRanks][4];
-#pragma unroll
-  for (int s = 0; s < kXgMaxRanks; ++s)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) q[s][k] = use[s] ? ll_load(src[s] + k) : uint2{0u, epoch};
-  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-  uint32_t missing = 0xffu;
-  while (true) {
-    bool all = true;
-#pragma unroll
-    for (int s = 0; s < kXgMaxRanks; ++s)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) all = all && q[s][k].y == epoch;
-    if (all) break;
-    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
-#pragma unroll
-      for (int s = kXgMaxRanks - 1; s >= 0; --s)
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (q[s][k].y != epoch) {
-            missing = (uint32_t)s;
-            seen = q[s][k].y;
-          }
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-    for (int s = 0; s < kXgMaxRanks; ++s)
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (q[s][k].y != epoch) q[s][k] = ll_load(src[s] + k);
+  for (long long i = nv + tid; i < n; i += kXgThreads) {
+    const long long e = g0 + i;
+    float m = mom ? a.m[e] : 0.f, v = adam ? a.v[e] : 0.f;
+    const float w = opt_step(a.h, lr_t, a.w[e], red[i], m, v);
+    a.w[e] = w;
+    if (mom) a.m[e] = m;
+    if (adam) a.v[e] = v;
+    a.grad[e] = 0.f;
+    shadow_store(a, e, w);
   }
-#pragma unroll
-  for (int s = 0; s < kXgMaxRanks; ++s)
-    val[s] = float4{__uint_as_float(q[s][0].x), __uint_as_float(q[s][1].x), __uint_as_float(q[s][2].x),
-                    __uint_as_float(q[s][3].x)};
-  return missing;
-}
-// Scalar form (bucket tails): one pair of one source.
-__device__ __forceinline__ float ll_wait1(const uint2* p, uint32_t epoch, long long timeout, bool& late) {
-  uint2 q = ll_load(p);
-  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-  while (q.y != epoch) {
-    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
-      late = true;
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-    q = ll_load(p);
-  }
-  return __uint_as_float(q.x);
 }
 
 // One launch carries the parts of NL ranks (grid.y = local rank): several replicas of one process on
@@ -338,125 +262,6 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
 #define XG_STAMP(i) \
   if (tr) tr[i] = __builtin_amdgcn_s_memrealtime()
 
-  if (UNCACHED && a.ll) {
-    // ================= LL protocol: pairs {value, epoch}; the data is the arrival signal =================
-    const long long llcap = a.llcap;
-    const long long tmo = a.timeout_ticks;
-    uint32_t bad = 0u;
-    // ---- phase 1: chunk `blk` of every slice s into rank s's LL in area (minus the producer-pushed range)
-    for (int s = 0; s < N; ++s) {
-      const long long g0 = (long long)s * L + c0;
-      const long long n = max(0LL, min(CH, M - g0));
-      uint2* dst = xg_ll_area(a.peer[s], 0, parity, cap, llcap) + (size_t)r * L + c0;
-      const long long plo = min(max(a.push_lo - g0, 0LL), n), phi = min(max(a.push_hi - g0, 0LL), n);
-      const long long nv = n >> 2;
-      for (long long j = tid; j < nv; j += kXgThreads) {
-        const long long i = 4 * j;
-        if (i + 4 <= plo || i >= phi) {
-          ll_store4(dst + i, *reinterpret_cast<const float4*>(a.grad + g0 + i), epoch);
-        } else {
-          for (int k = 0; k < 4; ++k)
-            if (i + k < plo || i + k >= phi) dst[i + k] = uint2{__float_as_uint(a.grad[g0 + i + k]), epoch};
-        }
-      }
-      for (long long i = (nv << 2) + tid; i < n; i += kXgThreads)
-        if (i < plo || i >= phi) dst[i] = uint2{__float_as_uint(a.grad[g0 + i]), epoch};
-    }
-    XG_STAMP(2);
-    // ---- phase 2: this rank's slice chunk: every source's pairs awaited together, summed in rank order,
-    // the result's pairs to every rank
-    {
-      const long long g0 = (long long)r * L + c0;
-      const long long n = max(0LL, min(CH, M - g0));
-      const uint2* in = xg_ll_area(a.peer[r], 0, parity, cap, llcap) + c0;
-      const long long nv = n >> 2;
-      bool use[kXgMaxRanks];
-#pragma unroll
-      for (int s = 0; s < kXgMaxRanks; ++s) use[s] = s < N;
-      for (long long j = tid; j < nv; j += kXgThreads) {
-        const uint2* src[kXgMaxRanks];
-#pragma unroll
-        for (int s = 0; s < kXgMaxRanks; ++s) src[s] = in + (size_t)(s < N ? s : 0) * L + 4 * j;
-        float4 v[kXgMaxRanks];
-        uint32_t sn = 0u;
-        const uint32_t m = ll_wait(src, use, epoch, tmo, v, sn);
-        if (m != 0xffu) {
-          bad |= 1u;
-          if (tid == 0 && miss1 == 0xffu) {
-            miss1 = m;
-            seen1 = sn;
-          }
-        }
-        float4 acc = v[0];
-#pragma unroll
-        for (int s = 1; s < kXgMaxRanks; ++s)
-          if (s < N) {
-            acc.x += v[s].x; acc.y += v[s].y; acc.z += v[s].z; acc.w += v[s].w;
-          }
-        for (int p = 0; p < N; ++p)
-          ll_store4(xg_ll_area(a.peer[p], 1, parity, cap, llcap) + (size_t)r * L + c0 + 4 * j, acc, epoch);
-      }
-      for (long long i = (nv << 2) + tid; i < n; i += kXgThreads) {
-        bool late = false;
-        float acc = ll_wait1(in + i, epoch, tmo, late);
-        for (int s = 1; s < N; ++s) acc += ll_wait1(in + (size_t)s * L + i, epoch, tmo, late);
-        if (late) bad |= 1u;
-        for (int p = 0; p < N; ++p)
-          xg_ll_area(a.peer[p], 1, parity, cap, llcap)[(size_t)r * L + c0 + i] = uint2{__float_as_uint(acc), epoch};
-      }
-    }
-    XG_STAMP(3);
-    XG_STAMP(4);
-    // ---- phase 3: every slice's reduced chunk (all slices awaited together), back into the bucket or
-    // through the optimizer
-    {
-      float lr_t = 0.f;
-      if (a.apply) lr_t = opt_lr_t(a.h, a.h.kind == kOptAdam ? *a.iterations : 0);
-      const uint2* out = xg_ll_area(a.peer[r], 1, parity, cap, llcap);
-      const long long nvmax = CH >> 2;
-      for (long long j = tid; j < nvmax; j += kXgThreads) {
-        const uint2* src[kXgMaxRanks];
-        bool use[kXgMaxRanks];
-#pragma unroll
-        for (int s = 0; s < kXgMaxRanks; ++s) {
-          const long long g0 = (long long)s * L + c0;
-          const long long n = s < N ? max(0LL, min(CH, M - g0)) : 0LL;
-          use[s] = 4 * j + 4 <= n;
-          src[s] = out + (use[s] ? (size_t)(g0 + 4 * j) : (size_t)0);
-        }
-        float4 v[kXgMaxRanks];
-        uint32_t sn = 0u;
-        const uint32_t m = ll_wait(src, use, epoch, tmo, v, sn);
-        if (m != 0xffu) {
-          bad |= 2u;
-          if (tid == 0 && miss2 == 0xffu) {
-            miss2 = m;
-            seen2 = sn;
-          }
-        }
-#pragma unroll
-        for (int s = 0; s < kXgMaxRanks; ++s) {
-          if (!use[s]) continue;
-          const long long e = (long long)s * L + c0 + 4 * j;
-          if (a.apply) apply4(a, lr_t, e, v[s]);
-          else *reinterpret_cast<float4*>(a.grad + e) = v[s];
-        }
-      }
-      for (int s = 0; s < N; ++s) {   // tails: a slice chunk whose length is not a multiple of 4
-        const long long g0 = (long long)s * L + c0;
-        const long long n = max(0LL, min(CH, M - g0));
-        for (long long i = ((n >> 2) << 2) + tid; i < n; i += kXgThreads) {
-          bool late = false;
-          const float v = ll_wait1(out + g0 + i, epoch, tmo, late);
-          if (late) bad |= 2u;
-          if (a.apply) apply1(a, lr_t, g0 + i, v);
-          else a.grad[g0 + i] = v;
-        }
-      }
-    }
-    XG_STAMP(5);
-    if (bad) __hip_atomic_fetch_or(a.err, bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  } else {
   // ---- phase 1: push chunk `blk` of every slice s to rank s (minus the producer-pushed range)
   for (int s = 0; s < N; ++s) {
     const long long g0 = (long long)s * L + c0;
@@ -511,7 +316,6 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
     if (a.apply) apply_chunk(a, lr_t, g0, out + (size_t)s * L + c0, n);
     else copy_chunk(a.grad + g0, out + (size_t)s * L + c0, n, (g0 & 3) == 0);
   }
-  }   // flag protocol
   if (tr) {
     const uint32_t hw = __builtin_amdgcn_s_getreg(63492);   // hwreg(HW_REG_HW_ID): cu 8-11, se 13-15
     const uint32_t xcc = __builtin_amdgcn_s_getreg(63508);  // hwreg(HW_REG_XCC_ID)
@@ -548,22 +352,9 @@ using namespace tde;
 static long long xg_cap(long long max_elems) {
   return max_elems + (long long)kXgMaxRanks * 4 * kXgMaxBlocks;
 }
-// LL area capacity (pairs) and whether a call of nranks slices of L elements runs the LL protocol
-// (uncached windows only; TDE_XGMI_LL=0 keeps every call on the flag protocol)
-static long long xg_llcap(long long max_elems) {
-  const long long c = xg_cap(max_elems);
-  return c < kXgLLCap ? c : kXgLLCap;
-}
-static bool xg_use_ll(long long L, int nranks, long long max_elems, int uncached) {
-  static const bool on = [] {
-    const char* e = getenv("TDE_XGMI_LL");
-    return !(e && e[0] == '0');
-  }();
-  return on && uncached && L * nranks <= xg_llcap(max_elems);
-}
 
 TDE_API size_t tde_xgmi_window_bytes(long long max_elems) {
-  return kXgFlagBytes + 4 * (size_t)xg_cap(max_elems) * sizeof(float) + 4 * (size_t)xg_llcap(max_elems) * sizeof(uint2);
+  return kXgFlagBytes + 4 * (size_t)xg_cap(max_elems) * sizeof(float);
 }
 TDE_API int tde_xgmi_max_ranks() { return kXgMaxRanks; }
 TDE_API int tde_xgmi_max_blocks() { return kXgMaxBlocks; }
@@ -629,11 +420,9 @@ struct TdeXgPush {
   const void* epoch;
   long long L, cap, off;
   int rank, nranks;
-  int ll;
-  long long llcap;
 };
 TDE_API int tde_xgmi_push_spec(long long M, long long max_elems, void* const* peers, const void* epoch, int rank,
-                               int nranks, int nblocks, long long off, int uncached, TdeXgPush* out) {
+                               int nranks, int nblocks, long long off, TdeXgPush* out) {
   if (nranks < 1 || nranks > kXgMaxRanks || rank < 0 || rank >= nranks || M < 0 || M > max_elems || !out) return -1;
   nblocks = nblocks < 1 ? 1 : nblocks > kXgMaxBlocks ? kXgMaxBlocks : nblocks;
   memset(out, 0, sizeof(*out));
@@ -644,8 +433,6 @@ TDE_API int tde_xgmi_push_spec(long long M, long long max_elems, void* const* pe
   out->off = off;
   out->rank = rank;
   out->nranks = nranks;
-  out->llcap = xg_llcap(max_elems);
-  out->ll = xg_use_ll(out->L, nranks, max_elems, uncached) ? 1 : 0;
   return out->L * nranks > out->cap ? -3 : 0;
 }
 static_assert(sizeof(TdeXgPush) == sizeof(XgPush), "TdeXgPush mirrors XgPush");
@@ -688,7 +475,7 @@ TDE_API int tde_xgmi_set_trace(void* epoch, void* trace, int calls) {
 }
 
 static int xg_fill(XgArgs& a, float* grad, long long M, long long max_elems, void* const* peers, void* epoch,
-                   void* err, int rank, int nranks, int nblocks, long long timeout_ticks, int uncached) {
+                   void* err, int rank, int nranks, int nblocks, long long timeout_ticks) {
   if (nranks < 1 || nranks > kXgMaxRanks || rank < 0 || rank >= nranks) return -1;
   if (M < 0 || M > max_elems) return -2;
   if (((uintptr_t)grad & 15) != 0) return -4;
@@ -702,8 +489,6 @@ static int xg_fill(XgArgs& a, float* grad, long long M, long long max_elems, voi
   a.L = xg_slice(M, nranks, nblocks);
   a.chunk = a.L / nblocks;
   a.cap = xg_cap(max_elems);
-  a.llcap = xg_llcap(max_elems);
-  a.ll = xg_use_ll(a.L, nranks, max_elems, uncached) ? 1 : 0;
   a.timeout_ticks = timeout_ticks;
   {
     std::lock_guard<std::mutex> lk(g_trace_mu);
@@ -755,8 +540,7 @@ TDE_API int tde_xgmi_all_reduce(float* grad, long long M, long long max_elems, v
   nblocks = clamp_blocks(nblocks);
   XgLaunch<1> la;
   memset(&la, 0, sizeof(la));
-  const int rc = xg_fill(la.r[0], grad, M, max_elems, peers, epoch, err, rank, nranks, nblocks, timeout_ticks,
-                         uncached);
+  const int rc = xg_fill(la.r[0], grad, M, max_elems, peers, epoch, err, rank, nranks, nblocks, timeout_ticks);
   return rc ? rc : xg_go(la, 1, nblocks, uncached, stream);
 }
 
@@ -767,8 +551,7 @@ TDE_API int tde_xgmi_all_reduce_apply(float* grad, long long M, long long max_el
   XgLaunch<1> la;
   memset(&la, 0, sizeof(la));
   int rc = xg_set_apply(la.r[0], o);
-  if (!rc) rc = xg_fill(la.r[0], grad, M, max_elems, peers, epoch, err, rank, nranks, nblocks, timeout_ticks,
-                       uncached);
+  if (!rc) rc = xg_fill(la.r[0], grad, M, max_elems, peers, epoch, err, rank, nranks, nblocks, timeout_ticks);
   return rc ? rc : xg_go(la, 1, nblocks, uncached, stream);
 }
 
@@ -786,7 +569,7 @@ TDE_API int tde_xgmi_all_reduce_group(int nloc, float* const* grads, long long M
   for (int j = 0; j < nloc; ++j) {
     int rc = specs ? xg_set_apply(la.r[j], specs + j) : 0;
     if (!rc) rc = xg_fill(la.r[j], grads[j], M, max_elems, peers + (size_t)j * nranks, epochs[j], errs[j], rank0 + j,
-                          nranks, nblocks, timeout_ticks, uncached);
+                          nranks, nblocks, timeout_ticks);
     if (rc) return rc;
   }
   if (nloc == 1) {

@@ -21,17 +21,6 @@ __device__ __forceinline__ float* xg_area(char* base, int which, int parity, lon
   return reinterpret_cast<float*>(base + kXgFlagBytes) + ((size_t)which * 2 + parity) * (size_t)cap;
 }
 
-// Low-latency ("LL") areas after the flag-protocol ones, for buckets of up to llcap elements: every
-// element travels as an 8-byte pair {value bits, call epoch} written with one store, so the data IS the
-// arrival signal — no store drain, no separate flag and no flag round trip per phase.  Consumers poll the
-// pairs themselves (64-bit loads; an older epoch = not arrived yet).  Layout: [in 2 x llcap][out 2 x llcap]
-// pairs.  Used on uncached (fine-grained) windows only: a pair must not sit in the writer's L2.
-constexpr long long kXgLLCap = (1LL << 20) + (long long)kXgMaxRanks * 4 * kXgMaxBlocks;
-__device__ __forceinline__ uint2* xg_ll_area(char* base, int which, int parity, long long cap, long long llcap) {
-  return reinterpret_cast<uint2*>(base + kXgFlagBytes + 4 * (size_t)cap * sizeof(float)) +
-         ((size_t)which * 2 + parity) * (size_t)llcap;
-}
-
 // A producer kernel (the trunk backward) that writes a contiguous range of the gradient bucket
 // straight into the owners' contribution areas of the NEXT all-reduce call instead of into the local
 // bucket.  The all-reduce launch that follows on the same stream then skips that range in its push
@@ -43,33 +32,19 @@ struct XgPush {
   long long L, cap;            // slice length and area capacity (elements) of the next call
   long long off;               // bucket offset of the producer's element 0
   int rank, nranks;
-  int ll;                      // the next call runs the LL protocol (pairs into the LL areas)
-  long long llcap;             // LL area capacity (pairs)
 };
 
-// Stores value v of bucket element g (g = off + local index) into its owner's contribution area (the
-// pair {v, next epoch} under the LL protocol).
+// Stores value v of bucket element g (g = off + local index) into its owner's contribution area.
 __device__ __forceinline__ void xg_push_store(const XgPush& p, int parity, long long g, float v) {
   const int s = (int)(g / p.L);
-  const size_t o = (size_t)p.rank * p.L + (g - (long long)s * p.L);
-  if (p.ll)
-    xg_ll_area(p.peer[s], 0, parity, p.cap, p.llcap)[o] = uint2{__float_as_uint(v), *p.epoch + 1u};
-  else
-    xg_area(p.peer[s], 0, parity, p.cap)[o] = v;
+  xg_area(p.peer[s], 0, parity, p.cap)[(size_t)p.rank * p.L + (g - (long long)s * p.L)] = v;
 }
 
 // Four consecutive elements g..g+3 (g % 4 == 0, L % 4 == 0: one owner, a 16-byte aligned destination).
 __device__ __forceinline__ void xg_push_store4(const XgPush& p, int parity, long long g, float4 v) {
   const int s = (int)(g / p.L);
-  const size_t o = (size_t)p.rank * p.L + (g - (long long)s * p.L);
-  if (p.ll) {
-    const uint32_t e = *p.epoch + 1u;
-    uint4* d = reinterpret_cast<uint4*>(xg_ll_area(p.peer[s], 0, parity, p.cap, p.llcap) + o);
-    d[0] = uint4{__float_as_uint(v.x), e, __float_as_uint(v.y), e};
-    d[1] = uint4{__float_as_uint(v.z), e, __float_as_uint(v.w), e};
-  } else {
-    *reinterpret_cast<float4*>(xg_area(p.peer[s], 0, parity, p.cap) + o) = v;
-  }
+  *reinterpret_cast<float4*>(xg_area(p.peer[s], 0, parity, p.cap) + (size_t)p.rank * p.L +
+                             (g - (long long)s * p.L)) = v;
 }
 
 // A pushing wave waits for its stores' acknowledgements before it ends: on an N-GPU node they travel

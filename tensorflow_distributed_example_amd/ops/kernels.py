@@ -50,8 +50,7 @@ class XgPush(_ct.Structure):
     """``TdeXgPush`` / ``XgPush`` (csrc/include/tde_xgmi.h): a producer kernel stores its gradient range
     straight into the owners' contribution areas of the next xGMI all-reduce call."""
     _fields_ = [("peer", _ct.c_void_p * 8), ("epoch", _ct.c_void_p), ("L", _ct.c_longlong), ("cap", _ct.c_longlong),
-                ("off", _ct.c_longlong), ("rank", _ct.c_int), ("nranks", _ct.c_int), ("ll", _ct.c_int),
-                ("llcap", _ct.c_longlong)]
+                ("off", _ct.c_longlong), ("rank", _ct.c_int), ("nranks", _ct.c_int)]
 
 
 class BwdOpt(_ct.Structure):

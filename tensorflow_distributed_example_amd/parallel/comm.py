@@ -402,7 +402,7 @@ class XgmiCommunicator(Communicator):
         """``XgPush`` for a producer kernel that stores bucket elements [off, ...) of an M-element bucket
         straight into the owners' contribution areas of the next ``all_reduce_apply_`` call."""
         return _push_spec(self.lib, M, self.max_elems, self.peers, self.epoch.value, self.rank, self.world,
-                          self.nblocks(M), off, self.uncached)
+                          self.nblocks(M), off)
 
     def broadcast_(self, tensors, root=0):
         return self.fallback.broadcast_(tensors, root)
@@ -463,11 +463,11 @@ class XgmiCommunicator(Communicator):
         return ok
 
 
-def _push_spec(lib, M, max_elems, peers, epoch, rank, world, nblocks, off, uncached):
+def _push_spec(lib, M, max_elems, peers, epoch, rank, world, nblocks, off):
     from ..ops.kernels import XgPush
     sp = XgPush()
     rc = lib.tde_xgmi_push_spec(int(M), int(max_elems), peers, epoch, int(rank), int(world), int(nblocks), int(off),
-                                int(uncached), C.byref(sp))
+                                C.byref(sp))
     if rc != 0:
         raise RuntimeError(f"tde_xgmi_push_spec failed ({rc})")
     return sp
@@ -690,7 +690,7 @@ class PeerXgmiCommunicator(Communicator):
         """``XgPush`` of local replica ``i`` (see ``XgmiCommunicator.push_spec``)."""
         gi = next(j for j, g in enumerate(self.groups) if i in g)
         return _push_spec(self.lib, M, self.max_elems, self.peers[i], self.epochs[i], self.rank0 + i, self.world,
-                          self.nblocks(M, len(self.groups[gi]), gi), off, self.uncached)
+                          self.nblocks(M, len(self.groups[gi]), gi), off)
 
     def all_reduce_(self, tensors, op="sum"):
         if len(tensors) != self.n_local or not all(self.handles(t, op, i) for i, t in enumerate(tensors)) or \
