@@ -101,8 +101,10 @@ cp.shutdown()
 """
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_xgmi_allreduce_bitwise(world, tmp_path):
+    """world ranks (one process each, all on cuda:0; 8 = the N=8 kernel path with its co-located spin
+    limit) vs the rank-ordered fp32 sum, eager and graph-captured."""
     port = _free_port()
     script = WORKER.format(root=ROOT, port=port)
     procs = []
