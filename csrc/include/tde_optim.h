@@ -51,7 +51,19 @@ struct FlatApply {
   OptHyper h;
   int nr;
   int lo[kFlatRanges], n[kFlatRanges];
+  // the gradient is the sum of grep (<= 1: one) replicas g[e + r * grep_stride], all zeroed after use
+  int grep;
+  long long grep_stride;
 };
+__device__ __forceinline__ float flat_grad(const FlatApply& f, int e) {
+  float g = f.g[e];
+  for (int r = 1; r < f.grep; ++r) g += f.g[e + r * f.grep_stride];
+  return g;
+}
+__device__ __forceinline__ void flat_grad_zero(const FlatApply& f, int e) {
+  f.g[e] = 0.f;
+  for (int r = 1; r < f.grep; ++r) f.g[e + r * f.grep_stride] = 0.f;
+}
 
 // Threads [tid, tid + nt*k) of the caller apply the ranges with step t.
 __device__ __forceinline__ void flat_apply(const FlatApply& f, long long t, int tid, int nt) {
@@ -61,8 +73,8 @@ __device__ __forceinline__ void flat_apply(const FlatApply& f, long long t, int 
       const int e = f.lo[r] + i;
       float m = f.h.kind != kOptSGD ? f.m[e] : 0.f;
       float v = f.h.kind == kOptAdam ? f.v[e] : 0.f;
-      f.w[e] = opt_step(f.h, lr_t, f.w[e], f.g[e], m, v);
-      f.g[e] = 0.f;
+      f.w[e] = opt_step(f.h, lr_t, f.w[e], flat_grad(f, e), m, v);
+      flat_grad_zero(f, e);
       if (f.h.kind != kOptSGD) f.m[e] = m;
       if (f.h.kind == kOptAdam) f.v[e] = v;
     }

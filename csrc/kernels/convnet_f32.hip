@@ -426,6 +426,8 @@ TDE_API int tde_convnet_bwd_f32(const float* x, const void* amax, int lda, const
   a.w1r_out = nullptr;
   a.w1c_out = nullptr;
   if (push) a.push = *push;
+  static const bool no_conv_grad = getenv("TDE_DIAG_NO_CONV_GRAD") != nullptr;   // timing diagnostic only
+  if (no_conv_grad) a.dwc = a.dbc = nullptr;
   const int P = ((H - 2) / 2) * ((W - 2) / 2);
   static bool attr_set = false;
   if (!attr_set) {

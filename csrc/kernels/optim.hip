@@ -193,10 +193,10 @@ using namespace tde;
 // ranges: int[2*nr] = {lo0, n0, lo1, n1, ...}
 TDE_API int tde_flat_apply(float* w, float* g, float* m, float* v, const long long* iterations, int* pend,
                            int kind, float lr, float mom, float b1, float b2, float eps, const int* ranges,
-                           int nr, hipStream_t stream) {
+                           int nr, int grep, long long grep_stride, hipStream_t stream) {
   if (nr < 0 || nr > kFlatRanges || (kind != kOptSGD && !m) || (kind == kOptAdam && (!v || !iterations)))
     return -1;
-  FlatApply f{w, g, m, v, iterations, pend, OptHyper{kind, lr, mom, b1, b2, eps}, nr, {0}, {0}};
+  FlatApply f{w, g, m, v, iterations, pend, OptHyper{kind, lr, mom, b1, b2, eps}, nr, {0}, {0}, grep, grep_stride};
   for (int i = 0; i < nr; ++i) {
     f.lo[i] = ranges[2 * i];
     f.n[i] = ranges[2 * i + 1];

@@ -27,14 +27,16 @@ class StepOpt(_ct.Structure):
     """``TdeStepOpt`` (csrc/kernels/convnet.hip): the optimizer of a fused training step."""
     _fields_ = [("kind", _ct.c_int), ("lr", _ct.c_float), ("mom", _ct.c_float), ("b1", _ct.c_float), ("b2", _ct.c_float),
                 ("eps", _ct.c_float), ("w", _ct.c_void_p), ("g", _ct.c_void_p), ("m", _ct.c_void_p), ("v", _ct.c_void_p),
-                ("iterations", _ct.c_void_p), ("pend", _ct.c_void_p)]
+                ("iterations", _ct.c_void_p), ("pend", _ct.c_void_p), ("grep", _ct.c_int),
+                ("grep_stride", _ct.c_longlong)]
 
 
 class FlatApply(_ct.Structure):
     """``FlatApply`` (csrc/include/tde_optim.h): an update of element ranges of the flat buffers."""
     _fields_ = [("w", _ct.c_void_p), ("g", _ct.c_void_p), ("m", _ct.c_void_p), ("v", _ct.c_void_p),
                 ("iterations", _ct.c_void_p), ("pend", _ct.c_void_p), ("h", OptHyper), ("nr", _ct.c_int),
-                ("lo", _ct.c_int * _FLAT_RANGES), ("n", _ct.c_int * _FLAT_RANGES)]
+                ("lo", _ct.c_int * _FLAT_RANGES), ("n", _ct.c_int * _FLAT_RANGES), ("grep", _ct.c_int),
+                ("grep_stride", _ct.c_longlong)]
 
 
 class XgApply(_ct.Structure):
@@ -60,7 +62,8 @@ class BwdOpt(_ct.Structure):
                 ("v", _ct.c_void_p), ("off_w1", _ct.c_longlong), ("off_w2", _ct.c_longlong),
                 ("off_b2", _ct.c_longlong), ("off_b1", _ct.c_longlong), ("W1c", _ct.c_void_p),
                 ("ldw1c", _ct.c_int), ("iterations", _ct.c_void_p), ("iter_prev", _ct.c_void_p),
-                ("commit", FlatApply), ("pend_set", _ct.c_void_p)]
+                ("commit", FlatApply), ("pend_set", _ct.c_void_p), ("crep", _ct.c_int),
+                ("crep_stride", _ct.c_longlong)]
 
 
 def step_opt(optimizer, w, g, m, v, iterations, pend):
@@ -90,7 +93,7 @@ def flat_apply(spec: FlatApply):
         rng[2 * i], rng[2 * i + 1] = spec.lo[i], spec.n[i]
     h = spec.h
     rc = N.hip().tde_flat_apply(spec.w, spec.g, spec.m, spec.v, spec.iterations, spec.pend, h.kind, h.lr, h.mom,
-                                h.b1, h.b2, h.eps, rng, spec.nr, _s())
+                                h.b1, h.b2, h.eps, rng, spec.nr, int(spec.grep), int(spec.grep_stride), _s())
     N.check(rc, "tde_flat_apply")
 
 

@@ -405,7 +405,12 @@ class ConvNetPlan(ReplicaPlan):
         sw, sb = seg[self.names["wc"]], seg[self.names["bc"]]
         self._conv_lo = min(sw.offset, sb.offset)
         span = max(sw.offset + sw.numel, sb.offset + sb.numel) - self._conv_lo
-        self.gconv = torch.zeros(2, span, dtype=torch.float32, device=dev)
+        # the ~170 backward workgroups add their conv-gradient partials into crep replicas (workgroup x ->
+        # replica x % crep, summed by the consumers): same-address float atomics from every workgroup cost
+        # ~4 us of the backward (TDE_CONVNET_GREP, 1 = one buffer; the deterministic mode keeps one)
+        self.crep = 1 if self.det else max(1, min(32, int(os.environ.get("TDE_CONVNET_GREP", "8"))))
+        self._conv_span = span
+        self.gconv = torch.zeros(2, self.crep, span, dtype=torch.float32, device=dev)
         self.pend = torch.zeros(2, dtype=torch.int32, device=dev)
         self.iter_prev = torch.zeros(1, dtype=torch.int64, device=dev)
         self._fopt = self._bopt = self._flush = None
@@ -428,8 +433,8 @@ class ConvNetPlan(ReplicaPlan):
         seg = self.store.segments
         sw, sb = seg[self.names["wc"]], seg[self.names["bc"]]
         lo = self._conv_lo
-        return (self.gconv[q, sw.offset - lo: sw.offset - lo + sw.numel].view(sw.shape),
-                self.gconv[q, sb.offset - lo: sb.offset - lo + sb.numel].view(sb.shape))
+        return (self.gconv[q, 0, sw.offset - lo: sw.offset - lo + sw.numel].view(sw.shape),
+                self.gconv[q, 0, sb.offset - lo: sb.offset - lo + sb.numel].view(sb.shape))
 
     def set_step_mode(self, mode):
         super().set_step_mode(mode)
@@ -457,18 +462,21 @@ class ConvNetPlan(ReplicaPlan):
             # forward of parity q: the deferred update of the previous step (parity 1-q), t = iter_prev
             f = K.step_opt(opt, st.w, None, m, v, self.iter_prev, self.pend[1 - q])
             f.g = self._gconv(1 - q)
+            f.grep, f.grep_stride = self.crep, self._conv_span
             self._fopt.append(f)
             commit = K.flat_apply_spec(opt, st.w, None, m, v, self.iterations, self.pend[1 - q], conv)
             commit.g = self._gconv(1 - q)
+            commit.grep, commit.grep_stride = self.crep, self._conv_span
             b1 = self.names["b1"]
             self._bopt.append(K.BwdOpt(
                 opt.kind_id, float(opt.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"], P_(st.w), P_(m),
                 P_(v), seg[self.names["w1"]].offset, seg[self.names["w2"]].offset, seg[self.names["b2"]].offset,
                 seg[b1].offset if b1 is not None else -1, P_(self.W1col),
                 self.W1col.stride(0) if self.W1col is not None else 0, P_(self.iterations), P_(self.iter_prev),
-                commit, self.pend[q].data_ptr()))
+                commit, self.pend[q].data_ptr(), self.crep, self._conv_span))
             fl = K.flat_apply_spec(opt, st.w, None, m, v, self.iterations, self.pend[q], conv)
             fl.g = self._gconv(q)
+            fl.grep, fl.grep_stride = self.crep, self._conv_span
             self._flush.append(fl)
 
     def push_range(self):
