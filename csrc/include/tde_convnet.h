@@ -88,8 +88,12 @@ __device__ __forceinline__ void fwd_stage_conv(const FwdArgs& a, float* wcs, int
     float w = isb ? a.bc[j] : a.wc[j];
     if (a.pend) {
       const float* gp = isb ? a.gbc + j : a.gwc + j;
-      float g = gp[0];
-      for (int r = 1; r < a.grep; ++r) g += gp[r * a.grep_stride];
+      float gv[kMaxGrep];
+#pragma unroll
+      for (int r = 0; r < kMaxGrep; ++r) gv[r] = (r == 0 || r < a.grep) ? gp[r * a.grep_stride] : 0.f;
+      float g = gv[0];
+#pragma unroll
+      for (int r = 1; r < kMaxGrep; ++r) g += gv[r];
       float m = 0.f, v = 0.f;
       if (a.h.kind != kOptSGD) m = isb ? a.mbc[j] : a.mwc[j];
       if (a.h.kind == kOptAdam) v = isb ? a.vbc[j] : a.vwc[j];

@@ -55,14 +55,20 @@ struct FlatApply {
   int grep;
   long long grep_stride;
 };
+constexpr int kMaxGrep = 8;   // gradient replicas: every load issued before the first add (one round trip)
 __device__ __forceinline__ float flat_grad(const FlatApply& f, int e) {
-  float g = f.g[e];
-  for (int r = 1; r < f.grep; ++r) g += f.g[e + r * f.grep_stride];
+  float v[kMaxGrep];
+#pragma unroll
+  for (int r = 0; r < kMaxGrep; ++r) v[r] = (r == 0 || r < f.grep) ? f.g[e + r * f.grep_stride] : 0.f;
+  float g = v[0];
+#pragma unroll
+  for (int r = 1; r < kMaxGrep; ++r) g += v[r];
   return g;
 }
 __device__ __forceinline__ void flat_grad_zero(const FlatApply& f, int e) {
-  f.g[e] = 0.f;
-  for (int r = 1; r < f.grep; ++r) f.g[e + r * f.grep_stride] = 0.f;
+#pragma unroll
+  for (int r = 0; r < kMaxGrep; ++r)
+    if (r == 0 || r < f.grep) f.g[e + r * f.grep_stride] = 0.f;
 }
 
 // Threads [tid, tid + nt*k) of the caller apply the ranges with step t.

@@ -8,7 +8,7 @@ timeout -k 10 600 python -u -m pytest -x -q -rf --capture=sys --timeout 240 --ti
   tests/test_fp32_gpu.py tests/test_plan_gpu.py tests/test_kernels_gpu.py > gpurun_out/pytest_n.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -n 3 gpurun_out/pytest_n.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-for r in 1 4 8 16; do
+for r in 1 2 4 8; do
   TDE_CONVNET_GREP=$r timeout -k 10 200 python bench.py --steps 2000 --warmup 200 > gpurun_out/b_grep$r.log 2>&1
   echo "GREP=$r $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/b_grep$r.log) $(grep -o '"repeat_ms_per_step": \[[0-9., ]*\]' gpurun_out/b_grep$r.log)"
 done

@@ -408,7 +408,7 @@ class ConvNetPlan(ReplicaPlan):
         # the ~170 backward workgroups add their conv-gradient partials into crep replicas (workgroup x ->
         # replica x % crep, summed by the consumers): same-address float atomics from every workgroup cost
         # ~4 us of the backward (TDE_CONVNET_GREP, 1 = one buffer; the deterministic mode keeps one)
-        self.crep = 1 if self.det else max(1, min(32, int(os.environ.get("TDE_CONVNET_GREP", "8"))))
+        self.crep = 1 if self.det else max(1, min(8, int(os.environ.get("TDE_CONVNET_GREP", "8"))))
         self._conv_span = span
         self.gconv = torch.zeros(2, self.crep, span, dtype=torch.float32, device=dev)
         self.pend = torch.zeros(2, dtype=torch.int32, device=dev)
