@@ -90,6 +90,10 @@ struct XgArgs {
   // [push_lo, push_hi): bucket elements a producer kernel already stored into the owners' contribution
   // areas (tde_xgmi.h XgPush); phase 1 skips them
   long long push_lo, push_hi;
+  // [rep_lo, rep_hi): bucket elements whose gradient is the sum of nrep replicas rep[(g - rep_lo) + r * rep_stride]
+  // (the producer's contended atomics spread over replicas); phase 1 sums and zeroes them
+  float* rep; int nrep;
+  long long rep_lo, rep_hi, rep_stride;
 };
 constexpr int kXgTraceWords = 8;
 
@@ -268,7 +272,26 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
     const long long n = max(0LL, min(CH, M - g0));
     float* dst = area(a.peer[s], 0, parity, cap) + (size_t)r * L + c0;
     const long long plo = min(max(a.push_lo - g0, 0LL), n), phi = min(max(a.push_hi - g0, 0LL), n);
-    if (plo >= phi) {
+    if (a.nrep > 0 && a.rep_lo < g0 + n && a.rep_hi > g0) {
+      // a chunk holding replicated elements (the MNIST-CNN conv gradients: a few hundred): element-wise
+      for (long long i = tid; i < n; i += kXgThreads) {
+        const long long g = g0 + i;
+        if (i >= plo && i < phi) continue;
+        float v;
+        if (g >= a.rep_lo && g < a.rep_hi) {
+          float* q = a.rep + (g - a.rep_lo);
+          v = q[0];
+          q[0] = 0.f;
+          for (int k = 1; k < a.nrep; ++k) {
+            v += q[k * a.rep_stride];
+            q[k * a.rep_stride] = 0.f;
+          }
+        } else {
+          v = a.grad[g];
+        }
+        dst[i] = v;
+      }
+    } else if (plo >= phi) {
       copy_chunk(dst, a.grad + g0, n, (g0 & 3) == 0);
     } else {   // [0, plo) and [phi, n) still come from the local bucket
       if (plo > 0) copy_chunk(dst, a.grad + g0, plo, false);
@@ -457,6 +480,8 @@ struct TdeXgApply {
   void* sh; long long sh_lo, sh_hi;
   void* sht; int sh_cols; long long sht_ld;
   long long push_lo, push_hi;   // bucket range the step's producer kernel pushed itself (empty: none)
+  float* rep; int nrep;         // replicated gradient range (XgArgs::rep; nrep 0: none)
+  long long rep_lo, rep_hi, rep_stride;
 };
 
 // Diagnostics: trace buffers registered per rank (keyed by the rank's epoch word); every launch
@@ -519,6 +544,13 @@ static int xg_set_apply(XgArgs& a, const TdeXgApply* o) {
   a.h = OptHyper{o->kind, o->lr, o->mom, o->b1, o->b2, o->eps};
   a.push_lo = o->push_lo;
   a.push_hi = o->push_hi;
+  if (o->nrep > 1 && (!o->rep || o->rep_lo < 0 || o->rep_hi < o->rep_lo || o->rep_stride < o->rep_hi - o->rep_lo))
+    return -10;
+  a.rep = o->rep;
+  a.nrep = o->nrep > 1 ? o->nrep : 0;
+  a.rep_lo = o->rep_lo;
+  a.rep_hi = o->rep_hi;
+  a.rep_stride = o->rep_stride;
   return 0;
 }
 

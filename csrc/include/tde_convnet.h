@@ -283,7 +283,7 @@ __device__ __forceinline__ void zero_other_parity(const BwdArgs& a, int tid) {
 // deterministic mode (TDE_DETERMINISTIC: one replica per forward workgroup, each written by exactly one
 // add into zeros), summed in replica order.
 __device__ __forceinline__ float4 load_hpre(const BwdArgs& a, int row, int c4) {
-  constexpr int kMaxRep = 4;
+  constexpr int kMaxRep = 8;
   if (a.hrep > kMaxRep) {
     float4 s = {0.f, 0.f, 0.f, 0.f};
     for (int r = 0; r < a.hrep; ++r) {

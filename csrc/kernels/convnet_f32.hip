@@ -412,7 +412,8 @@ TDE_API int tde_convnet_bwd_f32(const float* x, const void* amax, int lda, const
                                 int C, int pre_relu, const int* labels, float scale, float* metrics, const float* W1,
                                 int ldw1, const float* Pt, int ldPt, float* dW1, float* dwc, float* dbc, float* dW2,
                                 float* db2, float* db1, int B, int H, int W, long long* stamps, const TdeBwdOpt* opt,
-                                float* cpart, const XgPush* push, hipStream_t stream) {
+                                float* cpart, const XgPush* push, int crep, long long crep_stride,
+                                hipStream_t stream) {
   if (ldw1 != HD || ((uintptr_t)W1 & 15) || ((uintptr_t)Pt & 7)) return -1;
   if (push && push->nranks > 0 &&
       (opt || push->nranks > kXgMaxRanks || push->L <= 0 || (push->L & 3) || (push->off & 3) || !push->epoch))
@@ -426,8 +427,10 @@ TDE_API int tde_convnet_bwd_f32(const float* x, const void* amax, int lda, const
   a.w1r_out = nullptr;
   a.w1c_out = nullptr;
   if (push) a.push = *push;
-  static const bool no_conv_grad = getenv("TDE_DIAG_NO_CONV_GRAD") != nullptr;   // timing diagnostic only
-  if (no_conv_grad) a.dwc = a.dbc = nullptr;
+  if (!opt && crep > 1) {   // data-parallel step: conv-gradient replicas summed by the all-reduce
+    a.crep = crep;
+    a.crep_stride = crep_stride;
+  }
   const int P = ((H - 2) / 2) * ((W - 2) / 2);
   static bool attr_set = false;
   if (!attr_set) {

@@ -42,7 +42,7 @@ _HIP_PROTOS = {
     "tde_convnet_fwd_f32": (i32, [p, p, p, p, i32, p, p, i32, p, i32, i32, i32, i32, p, p, i64, i64, p, i32, i64,
                                   p]),
     "tde_convnet_bwd_f32": (i32, [p, p, i32, p, p, i32, i64, p, p, p, i32, i32, p, f32, p, p, i32, p, i32, p, p,
-                                  p, p, p, p, i32, i32, i32, p, p, p, p, p]),
+                                  p, p, p, p, i32, i32, i32, p, p, p, p, i32, i64, p]),
     "tde_flat_apply": (i32, [p, p, p, p, p, p, i32, f32, f32, f32, f32, f32, p, i32, i32, i64, p]),
     "tde_noop": (i32, [i32, i32, p]),
     "tde_optim_table_size": (i32, [p, i32]),

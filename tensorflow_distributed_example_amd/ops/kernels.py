@@ -45,7 +45,8 @@ class XgApply(_ct.Structure):
                 ("eps", _ct.c_float), ("w", _ct.c_void_p), ("m", _ct.c_void_p), ("v", _ct.c_void_p),
                 ("iterations", _ct.c_void_p), ("sh", _ct.c_void_p), ("sh_lo", _ct.c_longlong), ("sh_hi", _ct.c_longlong),
                 ("sht", _ct.c_void_p), ("sh_cols", _ct.c_int), ("sht_ld", _ct.c_longlong),
-                ("push_lo", _ct.c_longlong), ("push_hi", _ct.c_longlong)]
+                ("push_lo", _ct.c_longlong), ("push_hi", _ct.c_longlong), ("rep", _ct.c_void_p), ("nrep", _ct.c_int),
+                ("rep_lo", _ct.c_longlong), ("rep_hi", _ct.c_longlong), ("rep_stride", _ct.c_longlong)]
 
 
 class XgPush(_ct.Structure):
@@ -232,7 +233,7 @@ def convnet_fwd(x, wc, bc, W1, hpre, Pt=None, amax=None, stamps=None, *, opt: St
 
 def convnet_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, metrics, W1row, Pt, dW1, dwc, dbc,
                 dW2=None, db2=None, db1=None, B=None, stamps=None, opt: BwdOpt | None = None, cpart=None,
-                push: XgPush | None = None):
+                push: XgPush | None = None, crep=1, crep_stride=0):
     """Trunk backward with the classifier head fused in: from this step's Dense(64) pre-activation
     ``hpre`` [B, 64] (f32) every workgroup recomputes the head (loss, dlogits, Dense(64) input gradient)
     and runs the trunk backward; ``hzero`` (the other parity buffer) is zeroed for the next forward.
@@ -244,7 +245,8 @@ def convnet_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, me
     ``cpart`` (deterministic mode): the conv gradients are stored per workgroup there instead of added
     atomically; ``convnet_cgrad_reduce`` sums them in order.  ``push`` (float32 form, plain step): dW1 is
     stored into the xGMI owners' contribution areas of the next all-reduce call instead of into ``dW1``
-    (the fused data-parallel exchange)."""
+    (the fused data-parallel exchange).  ``crep`` > 1 (float32 form, plain step): workgroup x adds its conv
+    gradients into replica x % crep of dwc / dbc (stride ``crep_stride`` elements), summed by the all-reduce."""
     B = x.shape[0] if B is None else B
     H, W = x.shape[1], x.shape[2]
     Kf = ((H - 2) // 2) * ((W - 2) // 2) * 32
@@ -268,7 +270,7 @@ def convnet_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, me
             int(pre_relu), _P(labels), float(scale), _P(metrics), _P(W1row), W1row.stride(0),
             _P(Pt), Pt.stride(0), _P(dW1), _P(dwc), _P(dbc), _P(dW2), _P(db2), _P(db1), B, H,
             W, _P(stamps), _ct.byref(opt) if opt is not None else None, _P(cpart),
-            *((_ct.byref(push) if push is not None else None,) if f32 else ()), _s())
+            *((_ct.byref(push) if push is not None else None, int(crep), int(crep_stride)) if f32 else ()), _s())
     N.check(rc, "tde_convnet_bwd_f32" if f32 else "tde_convnet_bwd")
 
 

@@ -356,7 +356,7 @@ class ConvNetPlan(ReplicaPlan):
         self.amax = torch.zeros(self.Kf // 32, 4, Bp, dtype=torch.int64, device=dev)  # [P][C/8][B] argmax bytes
         # Dense(64) pre-activation: two training buffers by step parity + one for eval / predict
         # (training buffers: hrep replicas each, so the forward's ~85 split-K adders per address spread out)
-        self.hrep = max(1, min(4, int(os.environ.get("TDE_CONVNET_HREP", "4"))))
+        self.hrep = max(1, min(8, int(os.environ.get("TDE_CONVNET_HREP", "4"))))
         # TDE_DETERMINISTIC=1 (debugging): one pre-activation replica per forward workgroup (each address
         # receives exactly one add, into zeros; the consumer sums the replicas in order) and the conv
         # gradients as per-workgroup partials summed in order by an extra launch: bitwise-reproducible
@@ -410,6 +410,11 @@ class ConvNetPlan(ReplicaPlan):
         # ~4 us of the backward (TDE_CONVNET_GREP, 1 = one buffer; the deterministic mode keeps one)
         self.crep = 1 if self.det else max(1, min(8, int(os.environ.get("TDE_CONVNET_GREP", "8"))))
         self._conv_span = span
+        # data-parallel step (mode "xgmi", float32 form): the replicas of parity 0 take the conv gradients
+        # and the all-reduce sums them into its push (only when nothing else lies between the two segments)
+        others = [n for n in store.order if n not in (self.names["wc"], self.names["bc"]) and
+                  self._conv_lo <= seg[n].offset < self._conv_lo + span]
+        self._xg_rep = self.f32 and self.crep > 1 and not others
         self.gconv = torch.zeros(2, self.crep, span, dtype=torch.float32, device=dev)
         self.pend = torch.zeros(2, dtype=torch.int32, device=dev)
         self.iter_prev = torch.zeros(1, dtype=torch.int64, device=dev)
@@ -440,6 +445,10 @@ class ConvNetPlan(ReplicaPlan):
         super().set_step_mode(mode)
         if mode != "xgmi":
             self._push = None
+        if mode != getattr(self, "_mode_set", None):
+            self.gconv.zero_()   # the replicas change roles between the step modes
+            self.pend.zero_()
+        self._mode_set = mode
         self._fopt = self._bopt = self._flush = None
         self._slots = (None, None)
         if mode == "plain":
@@ -514,8 +523,13 @@ class ConvNetPlan(ReplicaPlan):
             # the step's backward pushed dW1 itself (a replica without data this step pushed nothing)
             lo, hi = self.push_range() if (self._push is not None and self._pushed) else (0, 0)
             self._pushed = False
-            return K.XgApply(opt.kind_id, float(opt.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"],
+            spec = K.XgApply(opt.kind_id, float(opt.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"],
                              K._P(st.w), K._P(m), K._P(v), K._P(self.iterations), None, 0, 0, None, 0, 0, lo, hi)
+            if self._xg_rep:   # the conv gradients wait in the replicas of parity 0
+                spec.rep, spec.nrep = self.gconv[0].data_ptr(), self.crep
+                spec.rep_lo, spec.rep_hi = self._conv_lo, self._conv_lo + self._conv_span
+                spec.rep_stride = self._conv_span
+            return spec
         return K.XgApply(opt.kind_id, float(opt.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"],
                          K._P(st.w), K._P(m), K._P(v), K._P(self.iterations), K._P(self.W1row), seg.offset,
                          seg.offset + seg.numel, K._P(self.W1col), self.Hd,
@@ -558,12 +572,18 @@ class ConvNetPlan(ReplicaPlan):
         local = self.step_mode == "local"
         self._forward(x, B, self.hpre2[q], True, self._fopt[q] if local else None, train=True, hrep=self.hrep)
         # launch 2: head + trunk backward (fused step: the updates too)
-        dwc, dbc = self._gconv_views(q) if local else (self._g("wc"), self._g("bc"))
-        push = self._push if self.step_mode == "xgmi" else None
+        xg = self.step_mode == "xgmi"
+        rep = xg and self._xg_rep
+        if local or rep:
+            dwc, dbc = self._gconv_views(q if local else 0)
+        else:
+            dwc, dbc = self._g("wc"), self._g("bc")
+        push = self._push if xg else None
         K.convnet_bwd(x, self.amax, self.hpre2[q], self.hpre2[1 - q], self._v("b1"), self._v("w2"), self._v("b2"), y,
                       scale=self.scale, pre_relu=self.pre_relu, metrics=self.metrics, W1row=self.W1row, Pt=self.Pt,
                       dW1=self._g("w1"), dwc=dwc, dbc=dbc, dW2=self._g("w2"), db2=self._g("b2"), db1=self._g("b1"),
-                      B=B, opt=self._bopt[q] if local else None, cpart=self.cpart, push=push)
+                      B=B, opt=self._bopt[q] if local else None, cpart=self.cpart, push=push,
+                      crep=self.crep if rep else 1, crep_stride=self._conv_span)
         self._pushed = push is not None
         if self.det:
             K.convnet_cgrad_reduce(self.cpart, self.n_cpart, dwc, dbc)
