@@ -279,13 +279,17 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
         if (i >= plo && i < phi) continue;
         float v;
         if (g >= a.rep_lo && g < a.rep_hi) {
+          // every replica load issued before the first add (one round trip), summed in replica order
           float* q = a.rep + (g - a.rep_lo);
-          v = q[0];
-          q[0] = 0.f;
-          for (int k = 1; k < a.nrep; ++k) {
-            v += q[k * a.rep_stride];
-            q[k * a.rep_stride] = 0.f;
-          }
+          float rv[kMaxGrep];
+#pragma unroll
+          for (int k = 0; k < kMaxGrep; ++k) rv[k] = k < a.nrep ? q[k * a.rep_stride] : 0.f;
+          v = rv[0];
+#pragma unroll
+          for (int k = 1; k < kMaxGrep; ++k) v += rv[k];
+#pragma unroll
+          for (int k = 0; k < kMaxGrep; ++k)
+            if (k < a.nrep) q[k * a.rep_stride] = 0.f;
         } else {
           v = a.grad[g];
         }
@@ -544,7 +548,8 @@ static int xg_set_apply(XgArgs& a, const TdeXgApply* o) {
   a.h = OptHyper{o->kind, o->lr, o->mom, o->b1, o->b2, o->eps};
   a.push_lo = o->push_lo;
   a.push_hi = o->push_hi;
-  if (o->nrep > 1 && (!o->rep || o->rep_lo < 0 || o->rep_hi < o->rep_lo || o->rep_stride < o->rep_hi - o->rep_lo))
+  if (o->nrep > 1 && (!o->rep || o->nrep > kMaxGrep || o->rep_lo < 0 || o->rep_hi < o->rep_lo ||
+                      o->rep_stride < o->rep_hi - o->rep_lo))
     return -10;
   a.rep = o->rep;
   a.nrep = o->nrep > 1 ? o->nrep : 0;
