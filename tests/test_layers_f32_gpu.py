@@ -9,7 +9,7 @@ import torch.nn.functional as F
 
 pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("fp32_policy")]
 DEV = "cuda"
-SLOTS = 8
+from tensorflow_distributed_example_amd.ops.layer_ops import STAT_SLOTS as SLOTS  # noqa: E402
 
 
 def _r(*shape, seed=0, scale=1.0):

@@ -21,7 +21,7 @@ def _rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-SLOTS = 8
+from tensorflow_distributed_example_amd.ops.layer_ops import STAT_SLOTS as SLOTS  # noqa: E402
 
 
 def _stats_buf(C):
