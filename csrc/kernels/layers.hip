@@ -86,7 +86,7 @@ struct IGemmArgs {
 constexpr int TK = 32;  // MFMA k-slice
 // BN statistics accumulate into kStatSlots interleaved copies ([slot][2][C] f64, slot = block % slots)
 // so thousands of producer workgroups do not serialise on the same 2*C addresses; readers sum slots.
-constexpr int kStatSlots = 32;
+constexpr int kStatSlots = 8;
 
 __device__ __forceinline__ bf16x8 zero8() {
   bf16x8 r;

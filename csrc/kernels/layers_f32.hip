@@ -37,7 +37,7 @@ enum AKind { A_ROWK = 0, A_CONV = 1, A_DGRAD = 2, A_COLM = 3, A_WGRAD = 4 };
 enum BKind { B_NK = 0, B_DGRADW = 1, B_KN = 2 };
 
 constexpr int BM = 64, BN = 64, KC = 16, LD = KC + 4;   // LDS rows of 16 k + 4 pad floats
-constexpr int kSlots = 32;                              // BN statistics slots ([slot][2][C] f64)
+constexpr int kSlots = 8;                               // BN statistics slots ([slot][2][C] f64)
 
 struct G32 {
   const float* a;

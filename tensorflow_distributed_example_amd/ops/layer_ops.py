@@ -17,7 +17,7 @@ from .. import _native as N
 
 _P = N.ptr
 A_ROWK, A_CONV, A_DGRAD, A_COLM, A_WGRAD = range(5)
-STAT_SLOTS = 32  # BN statistics buffers are [STAT_SLOTS][2][C] f64 (layers.hip kStatSlots)
+STAT_SLOTS = 8   # BN statistics buffers are [STAT_SLOTS][2][C] f64 (layers.hip kStatSlots)
 B_NK, B_DGRADW, B_KN = range(3)
 bf16 = torch.bfloat16
 
