@@ -242,12 +242,15 @@ __device__ __forceinline__ f32x4 mfma_f32x4(float a, float b, f32x4 c) {
 
 // LDS of the head pieces (16 waves, 64 rows)
 constexpr int HS = HD + 4;   // f32 row stride of h
-constexpr int kHeadScratch = 64 * HS * 4 + 12 * 64 * 4 * 4 + 64 * 16 * 4;   // hs + part + dls
+// row strides of dlogits [64][16] and W2 [HD][16]: 17, not 16, so the 16 rows a wave reads at one column
+// (dH = dl . W2^T) fall on 16 different LDS banks (stride 16: 8-way conflicts in every workgroup's head)
+constexpr int DLS = 17, W2S = 17;
+constexpr int kHeadScratch = 64 * HS * 4 + 12 * 64 * 4 * 4 + 64 * DLS * 4;   // hs + part + dls
 struct HeadLds {
   float* hs;     // [64][HS]      h = act(hpre + b1)
   float* part;   // [12][64][4]   logits partial sums
-  float* dls;    // [64][16]      dlogits
-  float* w2s;    // [HD][16]      W2, classes padded to 16
+  float* dls;    // [64][DLS]     dlogits
+  float* w2s;    // [HD][W2S]     W2, classes padded to 16
   float* b2s;    // [16]
   int* labs;     // [64]
   __device__ __forceinline__ static HeadLds carve(unsigned char* scratch, unsigned char* w2, unsigned char* b2,
@@ -262,12 +265,12 @@ struct HeadLds {
     return l;
   }
 };
-constexpr int kW2Bytes = HD * 16 * 4, kB2Bytes = 16 * 4, kLabBytes = 64 * 4;
+constexpr int kW2Bytes = HD * W2S * 4, kB2Bytes = 16 * 4, kLabBytes = 64 * 4;
 
 // W2 image (classes padded to 16) and b2 into LDS (1024 threads)
 __device__ __forceinline__ void head_load_w2(const BwdArgs& a, const HeadLds& l, int tid) {
   const int u = tid >> 4, c = tid & 15;   // 64 x 16
-  l.w2s[u * 16 + c] = c < a.C ? a.W2[u * a.C + c] : 0.f;
+  l.w2s[u * W2S + c] = c < a.C ? a.W2[u * a.C + c] : 0.f;
   if (tid < 16) l.b2s[tid] = tid < a.C ? a.b2[tid] : 0.f;
 }
 
@@ -325,7 +328,7 @@ __device__ __forceinline__ void head_logits_ce(const BwdArgs& a, int nb, const H
     const int rt = wave & 3, kq = wave >> 2;
 #pragma unroll
     for (int k = kq * 16; k < kq * 16 + 16; k += 4)
-      lg = mfma_f32x4(l.hs[(rt * 16 + fr) * HS + k + fq], l.w2s[(k + fq) * 16 + fr], lg);
+      lg = mfma_f32x4(l.hs[(rt * 16 + fr) * HS + k + fq], l.w2s[(k + fq) * W2S + fr], lg);
     if (kq > 0) *reinterpret_cast<f32x4*>(l.part + (((kq - 1) * 4 + rt) * 64 + lane) * 4) = lg;
   }
   lds_barrier();
@@ -354,7 +357,7 @@ __device__ __forceinline__ void head_logits_ce(const BwdArgs& a, int nb, const H
         ca += (amx == label) ? 1.f : 0.f;
         na += 1.f;
       }
-      l.dls[r * 16 + fr] = (valid && cv) ? (pr - (fr == label ? 1.f : 0.f)) * a.scale : 0.f;
+      l.dls[r * DLS + fr] = (valid && cv) ? (pr - (fr == label ? 1.f : 0.f)) * a.scale : 0.f;
     }
   }
   lds_barrier();
@@ -367,7 +370,7 @@ __device__ __forceinline__ f32x4 head_dh(const BwdArgs& a, int nb, const HeadLds
   f32x4 gh = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int k = 0; k < 16; k += 4)
-    gh = mfma_f32x4(l.dls[(rt * 16 + fr) * 16 + k + fq], l.w2s[(ut * 16 + fr) * 16 + k + fq], gh);
+    gh = mfma_f32x4(l.dls[(rt * 16 + fr) * DLS + k + fq], l.w2s[(ut * 16 + fr) * W2S + k + fq], gh);
   const int j = ut * 16 + fr;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -432,10 +435,10 @@ __device__ __forceinline__ void head_workgroup(const BwdArgs& a, const HeadLds& 
     db1acc += (gh[0] + gh[1]) + (gh[2] + gh[3]);
     if (wave < 4) {
 #pragma unroll
-      for (int k = 0; k < 64; k += 4) gw = mfma_f32x4(l.hs[(k + fq) * HS + wave * 16 + fr], l.dls[(k + fq) * 16 + fr], gw);
+      for (int k = 0; k < 64; k += 4) gw = mfma_f32x4(l.hs[(k + fq) * HS + wave * 16 + fr], l.dls[(k + fq) * DLS + fr], gw);
     } else if (wave == 4) {
 #pragma unroll 4
-      for (int r = fq * 16; r < fq * 16 + 16; ++r) db2acc += l.dls[r * 16 + fr];
+      for (int r = fq * 16; r < fq * 16 + 16; ++r) db2acc += l.dls[r * DLS + fr];
     }
     lds_barrier();
   }

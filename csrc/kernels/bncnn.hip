@@ -552,9 +552,9 @@ struct HeadArgs {
 __global__ __launch_bounds__(NTHH) void head_kernel(HeadArgs a) {
   __shared__ float mu[kHeadMaxDp], rs[kHeadMaxDp], sc[kHeadMaxDp], sh[kHeadMaxDp];
   __shared__ float As[16 * kHLD], Xh[16 * kHLD];
-  __shared__ float whs[kHeadMaxDp * 16];   // [feature][class]
+  __shared__ float whs[kHeadMaxDp * 17];   // [feature][class], row stride 17 (conflict-free column reads)
   __shared__ float lgp[4][256];
-  __shared__ float dls[16 * 16];
+  __shared__ float dls[16 * 17];           // row stride 17
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
   const int B = a.B, D = a.D, Dp = a.Dp, NC = a.NC, rt = blockIdx.x, r0 = rt * 16;
   const bool train = a.mode == 0, lead = rt == 0;
@@ -636,7 +636,7 @@ __global__ __launch_bounds__(NTHH) void head_kernel(HeadArgs a) {
       As[r * kHLD + ff] = act;
       Xh[r * kHLD + ff] = xh;
     }
-    if (e < 16 * Dp) whs[e] = wv[u];
+    if (e < 16 * Dp) whs[(e >> 4) * 17 + (e & 15)] = wv[u];
   }
   if (quad) {
     lds_barrier();
@@ -658,7 +658,7 @@ __global__ __launch_bounds__(NTHH) void head_kernel(HeadArgs a) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int s = 0; s < kq / 4; ++s) {
       const int k = wave * kq + 4 * s + fq;
-      acc = mfma4(As[fr * kHLD + k], whs[k * 16 + fr], acc);
+      acc = mfma4(As[fr * kHLD + k], whs[k * 17 + fr], acc);
     }
     *reinterpret_cast<f32x4*>(&lgp[wave][lane * 4]) = acc;
   }
@@ -687,7 +687,7 @@ __global__ __launch_bounds__(NTHH) void head_kernel(HeadArgs a) {
         na += 1.f;
       }
       if (a.mode == 2 && valid && cv) a.out[(size_t)r * NC + fr] = a.out_softmax ? pr : z;
-      dls[rl * 16 + fr] = (train && valid && cv) ? (pr - (fr == label ? 1.f : 0.f)) * a.scale : 0.f;
+      dls[rl * 17 + fr] = (train && valid && cv) ? (pr - (fr == label ? 1.f : 0.f)) * a.scale : 0.f;
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
@@ -707,7 +707,7 @@ __global__ __launch_bounds__(NTHH) void head_kernel(HeadArgs a) {
   // ---- training: the tile's dbh / dWh partials, g and the dense BN's backward partial sums
   if (tid < 16) {
     float s = 0.f;
-    for (int r = 0; r < 16; ++r) s += dls[r * 16 + tid];
+    for (int r = 0; r < 16; ++r) s += dls[r * 17 + tid];
     if (tid < NC) a.dbh_part[(size_t)rt * NC + tid] = s;
   }
   const int ntf = Dp / 16;
@@ -718,7 +718,7 @@ __global__ __launch_bounds__(NTHH) void head_kernel(HeadArgs a) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int r = 4 * s + fq;
-      acc = mfma4(As[r * kHLD + ft * 16 + fr], dls[r * 16 + fr], acc);
+      acc = mfma4(As[r * kHLD + ft * 16 + fr], dls[r * 17 + fr], acc);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -730,7 +730,7 @@ __global__ __launch_bounds__(NTHH) void head_kernel(HeadArgs a) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int c = 4 * s + fq;
-      gg = mfma4(dls[fr * 16 + c], whs[(ft * 16 + fr) * 16 + c], gg);
+      gg = mfma4(dls[fr * 17 + c], whs[(ft * 16 + fr) * 17 + c], gg);
     }
     const int fg = ft * 16 + fr;
     double s1 = 0.0, s2 = 0.0;

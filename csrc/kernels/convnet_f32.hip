@@ -186,7 +186,7 @@ __global__ __launch_bounds__(1024) void convnet32_bwd_kernel(BwdArgs a) {
   const float b2v = (tid < 16 && tid < a.C) ? a.b2[tid] : 0.f;
   zero_other_parity(a, tid);
   if (blockIdx.x == gridDim.x - 1) {
-    hl.w2s[u2 * 16 + c2] = w2v;
+    hl.w2s[u2 * W2S + c2] = w2v;
     if (tid < 16) hl.b2s[tid] = b2v;
     head_workgroup<MODE>(a, hl, Gs);   // the G area is unused there
     return;
@@ -252,7 +252,7 @@ __global__ __launch_bounds__(1024) void convnet32_bwd_kernel(BwdArgs a) {
     }
     stamp(a.stamps, 1);
     if (b0 == 0) {
-      hl.w2s[u2 * 16 + c2] = w2v;
+      hl.w2s[u2 * W2S + c2] = w2v;
       if (tid < 16) hl.b2s[tid] = b2v;
       *reinterpret_cast<float2*>(W1s + (tid >> 5) * GS32 + (tid & 31) * 2) = w1v;
     }
