@@ -104,53 +104,6 @@ __device__ __forceinline__ void fwd_stage_conv(const FwdArgs& a, float* wcs, int
   }
 }
 
-// The same in two halves, so the weight / gradient-replica / slot loads can be issued before the image
-// staging (their round trip then overlaps it): fwd_conv_load into registers, fwd_conv_store after.
-struct ConvPre {
-  float w[2], g[2][kMaxGrep], m[2], v[2];
-  int pend;
-  long long t;
-};
-__device__ __forceinline__ void fwd_conv_load(const FwdArgs& a, ConvPre& c, int nthreads) {
-  c.pend = a.pend ? *a.pend : 0;
-  c.t = (a.pend && a.h.kind == kOptAdam) ? *a.iterations : 0;
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int i = threadIdx.x + u * nthreads;
-    const bool ok = i < kConvW;
-    const bool isb = i >= 9 * CC;
-    const int j = isb ? i - 9 * CC : i;
-    c.w[u] = ok ? (isb ? a.bc[j] : a.wc[j]) : 0.f;
-    c.m[u] = c.v[u] = 0.f;
-#pragma unroll
-    for (int r = 0; r < kMaxGrep; ++r) c.g[u][r] = 0.f;
-    if (ok && a.pend) {
-      const float* gp = isb ? a.gbc + j : a.gwc + j;
-#pragma unroll
-      for (int r = 0; r < kMaxGrep; ++r)
-        if (r == 0 || r < a.grep) c.g[u][r] = gp[r * a.grep_stride];
-      if (a.h.kind != kOptSGD) c.m[u] = isb ? a.mbc[j] : a.mwc[j];
-      if (a.h.kind == kOptAdam) c.v[u] = isb ? a.vbc[j] : a.vwc[j];
-    }
-  }
-}
-__device__ __forceinline__ void fwd_conv_store(const FwdArgs& a, const ConvPre& c, float* wcs, int nthreads) {
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int i = threadIdx.x + u * nthreads;
-    if (i >= kConvW) continue;
-    float w = c.w[u];
-    if (a.pend && c.pend) {
-      float g = c.g[u][0];
-#pragma unroll
-      for (int r = 1; r < kMaxGrep; ++r) g += c.g[u][r];
-      float m = c.m[u], v = c.v[u];
-      w = opt_step(a.h, opt_lr_t(a.h, c.t), w, g, m, v);
-    }
-    wcs[i] = w;
-  }
-}
-
 // The 8 conv channels c0..c0+7 of one wave (wave-uniform LDS broadcast reads).
 struct ConvW8 {
   float4 wlo[9], whi[9], blo, bhi;

@@ -78,11 +78,8 @@ __global__ __launch_bounds__(FPW * 256) void convnet32_fwd_kernel(FwdArgs a) {
       for (int j = 0; j < 4; ++j)
         wfr[ks][4 * i + j] = kp < P ? W1[(size_t)(kp * CC + k8_col(fq, i) + j) * a.ldw1 + nt * 16 + fr] : 0.f;
   }
-  static_assert(NT * 2 >= kConvW, "fwd_conv_load covers the conv weights in two passes");
-  ConvPre cpre;
-  fwd_conv_load(a, cpre, NT);   // issued before the staging: its round trip overlaps it
   fwd_stage_x(a, xr, b0, py0, nrows, NT);
-  fwd_conv_store(a, cpre, wcs, NT);
+  fwd_stage_conv(a, wcs, NT);
   stamp(a.stamps, 1);
   lds_barrier();
   ConvW8 cw;
