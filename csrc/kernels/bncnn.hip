@@ -146,8 +146,21 @@ __device__ void slot_sums(const double* acc, int npart, int Q, double* red) {
 __device__ void bn_prepare(const Bn& bn, float* st, bool writer, double* red) {
   const int C = bn.C;
   const bool batch = bn.mode == kBnTrain || bn.mode == kBnBatch;
+  // gamma / beta (and the writer's moving averages) of channel threadIdx.x are issued with the
+  // statistics partials, not after their reduction: one global round trip in the prologue, not two
+  const int c0 = threadIdx.x;
+  float g0 = 1.f, b0 = 0.f, mm0 = 0.f, mv0 = 0.f;
+  if (c0 < C && bn.mode != kBnNone) {
+    if (bn.gamma) g0 = bn.gamma[c0];
+    if (bn.beta) b0 = bn.beta[c0];
+  }
+  if (c0 < C && writer && bn.mode == kBnTrain && bn.mmean) {
+    mm0 = bn.mmean[c0];
+    mv0 = bn.mvar[c0];
+  }
   if (batch) slot_sums(bn.acc, bn.npart, 2 * C, red);
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const bool first = c == c0;
     float mean = 0.f, rstd = 1.f, var = 0.f;
     if (bn.mode == kBnMoving) {
       mean = bn.mmean[c];
@@ -165,9 +178,9 @@ __device__ void bn_prepare(const Bn& bn, float* st, bool writer, double* red) {
     }
     float sc = 1.f, sh = 0.f;
     if (bn.mode != kBnNone) {
-      const float g = bn.gamma ? bn.gamma[c] : 1.f;
+      const float g = first ? g0 : (bn.gamma ? bn.gamma[c] : 1.f);
       sc = g * rstd;
-      sh = (bn.beta ? bn.beta[c] : 0.f) - mean * sc;
+      sh = (first ? b0 : (bn.beta ? bn.beta[c] : 0.f)) - mean * sc;
     }
     st[c] = sc;
     st[C + c] = sh;
@@ -177,8 +190,9 @@ __device__ void bn_prepare(const Bn& bn, float* st, bool writer, double* red) {
       bn.saved[c] = mean;
       bn.saved[C + c] = rstd;
       if (bn.mmean) {
-        bn.mmean[c] = bn.mmean[c] * bn.momentum + mean * (1.f - bn.momentum);
-        bn.mvar[c] = bn.mvar[c] * bn.momentum + var * bn.bessel * (1.f - bn.momentum);
+        const float om = first ? mm0 : bn.mmean[c], ov = first ? mv0 : bn.mvar[c];
+        bn.mmean[c] = om * bn.momentum + mean * (1.f - bn.momentum);
+        bn.mvar[c] = ov * bn.momentum + var * bn.bessel * (1.f - bn.momentum);
       }
     }
   }
@@ -575,6 +589,20 @@ __global__ __launch_bounds__(NTHH) void head_kernel(HeadArgs a) {
     if (u * NTHH < 16 * Dp) wv[u] = (f < D && c < NC) ? a.wh[(size_t)min(f, D - 1) * NC + min(c, NC - 1)] : 0.f;
   }
   const int f = tid;
+  // gamma / beta of feature f, the head bias and wave 0's labels join the batch (no later round trip)
+  const float gm = (f < D && a.bn.gamma) ? a.bn.gamma[f] : 1.f;
+  const float bt = (f < D && a.bn.beta) ? a.bn.beta[f] : 0.f;
+  const bool upd = f < D && ((lead && a.bn.mode == kBnTrain) || !batch);
+  const float om = upd ? a.bn.mmean[f] : 0.f, ov = upd ? a.bn.mvar[f] : 1.f;
+  float bias = 0.f;
+  int lab[4] = {0, 0, 0, 0};
+  if (wave == 0) {
+    if (fr < NC) bias = a.bh[fr];
+    if (a.labels) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) lab[i] = a.labels[min(r0 + fq * 4 + i, B - 1)];
+    }
+  }
   double S = 0.0, S2 = 0.0;
   if (f < D && batch) {
     for (int p0 = 0; p0 < a.nrt; p0 += 8) {
@@ -603,19 +631,18 @@ __global__ __launch_bounds__(NTHH) void head_kernel(HeadArgs a) {
         if (lead && a.bn.mode == kBnTrain) {
           a.bn.saved[f] = mean;
           a.bn.saved[D + f] = rstd;
-          a.bn.mmean[f] = a.bn.mmean[f] * a.bn.momentum + mean * (1.f - a.bn.momentum);
-          a.bn.mvar[f] = a.bn.mvar[f] * a.bn.momentum + (float)v * a.bn.bessel * (1.f - a.bn.momentum);
+          a.bn.mmean[f] = om * a.bn.momentum + mean * (1.f - a.bn.momentum);
+          a.bn.mvar[f] = ov * a.bn.momentum + (float)v * a.bn.bessel * (1.f - a.bn.momentum);
         }
       } else {
-        mean = a.bn.mmean[f];
-        rstd = rsqrtf(a.bn.mvar[f] + a.bn.eps);
+        mean = om;
+        rstd = rsqrtf(ov + a.bn.eps);
       }
     }
-    const float gm = (f < D && a.bn.gamma) ? a.bn.gamma[f] : 1.f;
     mu[f] = mean;
     rs[f] = rstd;
     sc[f] = f < D ? gm * rstd : 0.f;
-    sh[f] = f < D ? (a.bn.beta ? a.bn.beta[f] : 0.f) - mean * gm * rstd : 0.f;
+    sh[f] = f < D ? bt - mean * gm * rstd : 0.f;
   }
   lds_barrier();
   stamp(a.stamps, 1);
@@ -667,7 +694,6 @@ __global__ __launch_bounds__(NTHH) void head_kernel(HeadArgs a) {
     f32x4 lg = *reinterpret_cast<const f32x4*>(&lgp[0][lane * 4]);
 #pragma unroll
     for (int w = 1; w < 4; ++w) lg += *reinterpret_cast<const f32x4*>(&lgp[w][lane * 4]);
-    const float bias = fr < NC ? a.bh[fr] : 0.f;
     float la = 0.f, ca = 0.f, na = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -678,7 +704,7 @@ __global__ __launch_bounds__(NTHH) void head_kernel(HeadArgs a) {
       const float ex = cv ? __expf(z - m) : 0.f;
       const float sum = row16_sum(ex);
       const float pr = ex / sum;
-      const int label = (valid && a.labels) ? a.labels[r] : 0;
+      const int label = (valid && a.labels) ? lab[i] : 0;
       const int amx = row16_min(cv && z == m ? fr : 64);
       const float zl = __shfl(z, (lane & ~15) | (label & 15), 64);
       if (valid && fr == 0) {
