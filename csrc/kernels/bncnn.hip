@@ -119,20 +119,22 @@ __device__ void parts_to_slots(double* red, int np, int Q) {
 
 // red[q] = sum over the npart partials acc[p][q], q < Q (Q <= blockDim), in a fixed order (thread
 // (part, q) sums p = part, part + np, ...; then the parts in order); red: blockDim doubles of LDS.
-// Ends with a barrier.
+// Ends with a barrier.  U loads per thread are in flight at once: a launch whose partials need more than
+// U * np of them per slot pays one more cross-XCD round trip (~2 us) per U.
+template <int U = 8>
 __device__ void slot_sums(const double* acc, int npart, int Q, double* red) {
   const int t = threadIdx.x, np = blockDim.x / Q, q = t % Q, part = t / Q;
   double s = 0.0;
   if (part < np) {
-    for (int j0 = part; j0 < npart; j0 += 8 * np) {
-      double v[8];
+    for (int j0 = part; j0 < npart; j0 += U * np) {
+      double v[U];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int j = j0 + u * np;
         v[u] = j < npart ? acc[j * Q + q] : 0.0;
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
+      for (int u = 0; u < U; ++u) s += v[u];
     }
     red[t] = s;
   }
@@ -143,6 +145,7 @@ __device__ void slot_sums(const double* acc, int npart, int Q, double* red) {
 // Per-channel scale / shift of the forward BN (y = x*sc + sh, then ReLU) and mean / rstd into LDS
 // (st: 4*C floats: sc, sh, mean, rstd).  Block `writer` stores the saved statistics and the
 // moving-average update (training).  red: blockDim doubles of LDS (batch modes).  Ends with a barrier.
+template <int U = 8>
 __device__ void bn_prepare(const Bn& bn, float* st, bool writer, double* red) {
   const int C = bn.C;
   const bool batch = bn.mode == kBnTrain || bn.mode == kBnBatch;
@@ -158,7 +161,7 @@ __device__ void bn_prepare(const Bn& bn, float* st, bool writer, double* red) {
     mm0 = bn.mmean[c0];
     mv0 = bn.mvar[c0];
   }
-  if (batch) slot_sums(bn.acc, bn.npart, 2 * C, red);
+  if (batch) slot_sums<U>(bn.acc, bn.npart, 2 * C, red);
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     const bool first = c == c0;
     float mean = 0.f, rstd = 1.f, var = 0.f;
@@ -468,7 +471,9 @@ __global__ __launch_bounds__(NTB) void dense_fwd_kernel(DenseFwdArgs a) {
         bv[s] = a.w[(size_t)k * a.D + col];
       }
   }
-  bn_prepare(a.bn, st, blockIdx.x == 0 && blockIdx.y == 0, red);
+  // 13 loads in flight: the last conv's 256 partials of 2 x 24 slots (21 parts per slot) in one round
+  // trip (8: two); 16 spills at this kernel's 128-VGPR budget
+  bn_prepare<13>(a.bn, st, blockIdx.x == 0 && blockIdx.y == 0, red);
   stamp(a.stamps, 1);
   const float* sc = st;
   const float* sh = st + a.bn.C;
@@ -838,6 +843,10 @@ __global__ __launch_bounds__(NTB) void dense_bwd_kernel(DenseBwdArgs a) {
   pf_load(px, 64 * 32, [&](int e) { return a.in[(size_t)min(b0 + (e >> 5), a.B - 1) * K + min(kt0 + (e & 31), K - 1)]; });
   // the dense BN's backward sums for feature tid (fixed order over the head's row tiles)
   if (tid < Dp) {
+    // the saved statistics and gamma join the load batch (not a second round trip after the sums)
+    const bool ok = tid < D;
+    const float m = ok ? a.bnd.saved[tid] : 0.f, r = ok ? a.bnd.saved[D + tid] : 0.f;
+    const float gm = (ok && a.bnd.gamma) ? a.bnd.gamma[tid] : 1.f;
     double S1 = 0.0, S2 = 0.0;
     for (int p0 = 0; p0 < a.nrt; p0 += 8) {
       double v1[8], v2[8];
@@ -854,9 +863,6 @@ __global__ __launch_bounds__(NTB) void dense_bwd_kernel(DenseBwdArgs a) {
           S2 += v2[u];
         }
     }
-    const bool ok = tid < D;
-    const float m = ok ? a.bnd.saved[tid] : 0.f, r = ok ? a.bnd.saved[D + tid] : 0.f;
-    const float gm = (ok && a.bnd.gamma) ? a.bnd.gamma[tid] : 1.f;
     dk[tid] = ok ? gm * r : 0.f;
     dk[256 + tid] = (float)(S1 / a.B);
     dk[512 + tid] = m;
@@ -1022,20 +1028,7 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
   }
   // the per-channel constants: partials of this layer's backward sums (fixed-order sum), saved
   // statistics
-  const int Q = 2 * Co, np = NTB / Q, qq = tid % Q, qpart = tid / Q;
-  double tsum = 0.0;
-  if (qpart < np) {
-    for (int j0 = qpart; j0 < a.bb.npart; j0 += 8 * np) {
-      double v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int j = j0 + u * np;
-        v[u] = j < a.bb.npart ? a.bb.acc[j * Q + qq] : 0.0;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) tsum += v[u];
-    }
-  }
+  // (issued before the partial sums' adds: their loads and these share one round trip)
   float cmu = 0.f, crs = 0.f, cg = 1.f;
   if (tid < Co) {
     cmu = a.bn.saved[tid];
@@ -1049,6 +1042,20 @@ __global__ __launch_bounds__(NTB) void conv_bwd_kernel(ConvBwdArgs a) {
     irs = a.bn_in.saved[C + ti];
     ig = a.bn_in.gamma ? a.bn_in.gamma[ti] : 1.f;
     ib = a.bn_in.beta ? a.bn_in.beta[ti] : 0.f;
+  }
+  const int Q = 2 * Co, np = NTB / Q, qq = tid % Q, qpart = tid / Q;
+  double tsum = 0.0;
+  if (qpart < np) {
+    for (int j0 = qpart; j0 < a.bb.npart; j0 += 8 * np) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = j0 + u * np;
+        v[u] = j < a.bb.npart ? a.bb.acc[j * Q + qq] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) tsum += v[u];
+    }
   }
   // LDS the registers do not cover
   for (int i = tid; i < P.Hd * Wd; i += NTB) {
