@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--dtype", default="fp32")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--cpu", action="store_true", help="the torch float32 reference executor on the CPU (oracle)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -40,7 +41,7 @@ def main():
 
     tde.backend.set_random_seed(77)
     tde.backend.set_global_policy("float32" if a.dtype == "fp32" else "mixed_bfloat16")
-    cuda = torch.cuda.is_available()
+    cuda = torch.cuda.is_available() and not a.cpu
     if a.strategy == "mirrored":
         devs = [f"cuda:{d}" if cuda else "cpu" for d in (a.devices or "0,0").split(",")]
         strategy = tde.distribute.MirroredStrategy(devs)
@@ -79,12 +80,23 @@ def main():
     store = prog.plans[0].store
     out = {name: store.view(name).detach().float().cpu().numpy() for name in store.names(trainable=True)}
     logs = tde.metrics.logs_from(prog.global_metrics(), ["accuracy"])
+    inv = ""
+    p0 = prog.plans[0]
+    if hasattr(p0, "step_invariants") and p0.step_mode == "local":
+        # the deferred conv update: one commit per step, applied on the fly by every forward but each
+        # execution's first, nothing pending and every gradient replica consumed after the flush
+        iv = p0.step_invariants()
+        total = a.spe * a.execs
+        ok = (iv["commits"] == total and iv["applied_on_the_fly"] == total - a.execs and iv["pending"] == [0, 0]
+              and iv["gconv_abs_max"] == 0.0)
+        inv = (f" commits={iv['commits']} on_the_fly={iv['applied_on_the_fly']} pending={iv['pending']} "
+               f"gconv_clear={iv['gconv_abs_max'] == 0.0} invariants_ok={ok}")
     if strategy.worker_index == 0:
         np.savez(a.out, **out)
         print(f"[dp_equiv] strategy={a.strategy} replicas={n} plan={prog.plan_kind} graph={prog.use_graph} "
               f"comm={type(strategy.comm).__name__} step_mode={prog.plans[0].step_mode} "
               f"exchange={getattr(prog, 'exchange', 'none')} "
-              f"replicas_identical={same} loss={logs['loss']:.6f}", flush=True)
+              f"replicas_identical={same} loss={logs['loss']:.6f}{inv}", flush=True)
 
 
 if __name__ == "__main__":

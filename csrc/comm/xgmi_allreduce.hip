@@ -616,3 +616,11 @@ TDE_API int tde_xgmi_all_reduce_group(int nloc, float* const* grads, long long M
   }
   return xg_go(la, nloc, nblocks, uncached, stream);
 }
+
+// Sizes of the ctypes-mirrored argument structs of this file (tests/test_abi.py checks the Python
+// mirrors in ops/kernels.py against them): out = {TdeXgApply, TdeXgPush}.
+TDE_API int tde_xgmi_abi_sizes(long long* out, int n) {
+  const long long s[] = {(long long)sizeof(TdeXgApply), (long long)sizeof(TdeXgPush)};
+  for (int i = 0; i < n && i < 2; ++i) out[i] = s[i];
+  return 2;
+}

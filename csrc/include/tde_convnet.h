@@ -38,7 +38,27 @@ struct FwdArgs {
   unsigned long long* inc_iter;      // training: block 0 advances the step counter (nullable)
   int hrep; long long hrep_stride;   // hpre replicas: workgroup x adds into replica x % hrep
   int grep; long long grep_stride;   // deferred conv gradient = sum of grep replicas (<= 1: one)
+  unsigned long long* fly_count;     // diagnostics (nullable): += 1 per forward that applied a pending update
+  // fused step: the head variables this step's backward reads, snapshotted here (nullable hsnap: none).
+  // The backward's head workgroup updates W2 / b2 / b1 in place while the trunk workgroups of the same
+  // launch read them: they read the snapshot instead, so no workgroup can see a half-updated head.
+  const float *hsrc_w2, *hsrc_b2, *hsrc_b1;
+  float* hsnap;                      // [64 b1 | 64*hC W2 | hC b2]
+  int hC;
 };
+
+// Fused step: one forward workgroup copies the head variables into the snapshot the backward reads.
+__device__ __forceinline__ void fwd_snap_head(const FwdArgs& a, int nthreads) {
+  if (!a.hsnap || blockIdx.x != 0 || blockIdx.y != 0) return;
+  const int C = a.hC, n = HD + HD * C + C;
+  for (int i = threadIdx.x; i < n; i += nthreads) {
+    float v;
+    if (i < HD) v = a.hsrc_b1 ? a.hsrc_b1[i] : 0.f;
+    else if (i < HD + HD * C) v = a.hsrc_w2[i - HD];
+    else v = a.hsrc_b2[i - HD - HD * C];
+    a.hsnap[i] = v;
+  }
+}
 
 // The input rows a workgroup's pooled positions touch (<= XR rows of <= XW floats per image)
 // are staged into LDS with coalesced float4 loads: gathering 4x4 patches straight from HBM
@@ -495,6 +515,7 @@ __device__ __forceinline__ void head_workgroup(const BwdArgs& a, const HeadLds& 
   if (cpend) cp.apply(a.commit, t_it - 1);
   if (tid == 0) {
     if (cpend) *a.commit.pend = 0;
+    if (cpend && a.commit.count) atomicAdd(a.commit.count, 1ull);
     if (a.pend_set) *a.pend_set = 1;
     if (a.iter_prev) *a.iter_prev = t_it;
   }
@@ -543,6 +564,10 @@ struct TdeStepOpt {
   const long long* iterations;
   int* pend;
   int grep; long long grep_stride;   // g holds grep replicas (<= 1: one)
+  unsigned long long* fly_count;      // diagnostics (nullable): forwards that applied the pending update
+  const float *hsrc_w2, *hsrc_b2, *hsrc_b1;   // head snapshot (FwdArgs::hsnap; nullable hsnap: none)
+  float* hsnap;
+  int hC;
 };
 
 // Fused-step description of the backward (ctypes struct).
@@ -564,7 +589,8 @@ namespace cnet {
 
 inline OptHyper hyper_of(const TdeStepOpt* o) { return OptHyper{o->kind, o->lr, o->mom, o->b1, o->b2, o->eps}; }
 inline bool opt_ok(const TdeStepOpt* o) {
-  return o->w && o->g && o->iterations && (o->kind == kOptSGD || o->m) && (o->kind != kOptAdam || o->v);
+  return o->w && o->g && o->iterations && (o->kind == kOptSGD || o->m) && (o->kind != kOptAdam || o->v) &&
+         (!o->hsnap || (o->hsrc_w2 && o->hsrc_b2 && o->hC >= 1 && o->hC <= 16 && !((uintptr_t)o->hsnap & 15)));
 }
 
 // The forward's deferred-update / step-counter / replica fields from the host arguments.
@@ -585,6 +611,12 @@ inline void fill_fwd_opt(FwdArgs& a, const TdeStepOpt* opt, long long off_wc, lo
     a.h = hyper_of(opt);
     a.grep = opt->grep > 1 ? opt->grep : 1;
     a.grep_stride = opt->grep_stride;
+    a.fly_count = opt->fly_count;
+    a.hsrc_w2 = opt->hsrc_w2;
+    a.hsrc_b2 = opt->hsrc_b2;
+    a.hsrc_b1 = opt->hsrc_b1;
+    a.hsnap = opt->hsnap;
+    a.hC = opt->hC;
   } else {
     a.grep = 1;
     a.grep_stride = 0;

@@ -54,6 +54,8 @@ struct FlatApply {
   // the gradient is the sum of grep (<= 1: one) replicas g[e + r * grep_stride], all zeroed after use
   int grep;
   long long grep_stride;
+  // diagnostics (nullable): += 1 each time the update is applied (deferred-update invariants, program.py)
+  unsigned long long* count;
 };
 constexpr int kMaxGrep = 8;   // gradient replicas: every load issued before the first add (one round trip)
 __device__ __forceinline__ float flat_grad(const FlatApply& f, int e) {

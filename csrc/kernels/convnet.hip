@@ -63,6 +63,9 @@ __global__ __launch_bounds__(FPW * 256) void convnet_fwd_kernel(FwdArgs a) {
   stamp(a.stamps, 0);
   // Keras optimizer.iterations: advanced here, read (stable) by this step's backward / optimizer
   if (a.inc_iter && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicAdd(a.inc_iter, 1ull);
+  if (a.fly_count && a.pend && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && *a.pend)
+    atomicAdd(a.fly_count, 1ull);
+  fwd_snap_head(a, NT);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fk = (lane >> 4) * 8;
   const int W = a.W, H = a.H;

@@ -48,6 +48,9 @@ __global__ __launch_bounds__(FPW * 256) void convnet32_fwd_kernel(FwdArgs a) {
   float* wcs = reinterpret_cast<float*>(fsm + FPW * 64 * PS32 * 4 + kXrBytes);      // [10][CC]
   stamp(a.stamps, 0);
   if (a.inc_iter && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicAdd(a.inc_iter, 1ull);
+  if (a.fly_count && a.pend && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && *a.pend)
+    atomicAdd(a.fly_count, 1ull);
+  fwd_snap_head(a, NT);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, fq = lane >> 4;
   const int W = a.W, H = a.H;
@@ -445,4 +448,13 @@ TDE_API int tde_convnet_bwd_f32(const float* x, const void* amax, int lda, const
   else convnet32_bwd_kernel<2><<<grid, 1024, kBwd32Lds, stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;
+}
+
+// Sizes of the ctypes-mirrored fused-step structs (tests/test_abi.py checks the Python mirrors in
+// ops/kernels.py against them): out = {TdeStepOpt, TdeBwdOpt, FlatApply, OptHyper}.
+TDE_API int tde_cnet_abi_sizes(long long* out, int n) {
+  const long long s[] = {(long long)sizeof(TdeStepOpt), (long long)sizeof(TdeBwdOpt), (long long)sizeof(FlatApply),
+                         (long long)sizeof(OptHyper)};
+  for (int i = 0; i < n && i < 4; ++i) out[i] = s[i];
+  return 4;
 }

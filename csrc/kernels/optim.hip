@@ -184,6 +184,7 @@ __global__ __launch_bounds__(256) void flat_apply_kernel(FlatApply f) {
   flat_apply(f, f.h.kind == kOptAdam ? *f.iterations : 0, threadIdx.x, 256);
   __syncthreads();
   if (threadIdx.x == 0 && f.pend) *f.pend = 0;
+  if (threadIdx.x == 0 && f.count) atomicAdd(f.count, 1ull);
 }
 
 }  // namespace tde
@@ -193,10 +194,11 @@ using namespace tde;
 // ranges: int[2*nr] = {lo0, n0, lo1, n1, ...}
 TDE_API int tde_flat_apply(float* w, float* g, float* m, float* v, const long long* iterations, int* pend,
                            int kind, float lr, float mom, float b1, float b2, float eps, const int* ranges,
-                           int nr, int grep, long long grep_stride, hipStream_t stream) {
+                           int nr, int grep, long long grep_stride, unsigned long long* count,
+                           hipStream_t stream) {
   if (nr < 0 || nr > kFlatRanges || (kind != kOptSGD && !m) || (kind == kOptAdam && (!v || !iterations)))
     return -1;
-  FlatApply f{w, g, m, v, iterations, pend, OptHyper{kind, lr, mom, b1, b2, eps}, nr, {0}, {0}, grep, grep_stride};
+  FlatApply f{w, g, m, v, iterations, pend, OptHyper{kind, lr, mom, b1, b2, eps}, nr, {0}, {0}, grep, grep_stride, count};
   for (int i = 0; i < nr; ++i) {
     f.lo[i] = ranges[2 * i];
     f.n[i] = ranges[2 * i + 1];

@@ -28,7 +28,8 @@ class StepOpt(_ct.Structure):
     _fields_ = [("kind", _ct.c_int), ("lr", _ct.c_float), ("mom", _ct.c_float), ("b1", _ct.c_float), ("b2", _ct.c_float),
                 ("eps", _ct.c_float), ("w", _ct.c_void_p), ("g", _ct.c_void_p), ("m", _ct.c_void_p), ("v", _ct.c_void_p),
                 ("iterations", _ct.c_void_p), ("pend", _ct.c_void_p), ("grep", _ct.c_int),
-                ("grep_stride", _ct.c_longlong)]
+                ("grep_stride", _ct.c_longlong), ("fly_count", _ct.c_void_p), ("hsrc_w2", _ct.c_void_p),
+                ("hsrc_b2", _ct.c_void_p), ("hsrc_b1", _ct.c_void_p), ("hsnap", _ct.c_void_p), ("hC", _ct.c_int)]
 
 
 class FlatApply(_ct.Structure):
@@ -36,7 +37,7 @@ class FlatApply(_ct.Structure):
     _fields_ = [("w", _ct.c_void_p), ("g", _ct.c_void_p), ("m", _ct.c_void_p), ("v", _ct.c_void_p),
                 ("iterations", _ct.c_void_p), ("pend", _ct.c_void_p), ("h", OptHyper), ("nr", _ct.c_int),
                 ("lo", _ct.c_int * _FLAT_RANGES), ("n", _ct.c_int * _FLAT_RANGES), ("grep", _ct.c_int),
-                ("grep_stride", _ct.c_longlong)]
+                ("grep_stride", _ct.c_longlong), ("count", _ct.c_void_p)]
 
 
 class XgApply(_ct.Structure):
@@ -94,7 +95,8 @@ def flat_apply(spec: FlatApply):
         rng[2 * i], rng[2 * i + 1] = spec.lo[i], spec.n[i]
     h = spec.h
     rc = N.hip().tde_flat_apply(spec.w, spec.g, spec.m, spec.v, spec.iterations, spec.pend, h.kind, h.lr, h.mom,
-                                h.b1, h.b2, h.eps, rng, spec.nr, int(spec.grep), int(spec.grep_stride), _s())
+                                h.b1, h.b2, h.eps, rng, spec.nr, int(spec.grep), int(spec.grep_stride), spec.count,
+                                _s())
     N.check(rc, "tde_flat_apply")
 
 

@@ -256,9 +256,9 @@ def _device_key(d):
             f"{getattr(p, 'uuid', '')}")
 
 
-def spin_grid_caps(control, devices, tag):
-    """Per local device: the most workgroups ONE all-reduce launch of this process may keep spinning on
-    it, or None (no limit beyond the kernel's own).
+def spin_chunk_cap(control, devices, tag):
+    """The most chunks (workgroups per rank) ONE all-reduce launch may use, the same number on every rank
+    of the world, or None (no limit beyond the kernel's own).
 
     Why a limit exists (the round-3 eager MWMS 2x2 timeouts, scripts/diag_xgmi_hang.sh): a waiting
     all-reduce workgroup holds a VGPR slice of its CU (4 waves x 80 VGPRs, one per SIMD).  The fused
@@ -267,27 +267,54 @@ def spin_grid_caps(control, devices, tag):
     all-reduce grid can be spinning on every CU while this process's backward (which precedes this
     process's arrival at that very all-reduce) waits for a free CU: neither progresses until the peer
     wait times out.  Measured (profiles/r4_xgmi_hang/): without a limit, 2 workers x 2 replicas on one
-    GPU time out in eager AND graph mode with the MNIST CNN (the late process's all-reduce blocks start
-    only when the waiting grid gives up, although both hosts had enqueued within 1.5 ms), while Model B,
-    whose kernels fit beside a spinning wave, runs clean; with the limit every mode runs clean.  One process per GPU (a real N-GPU node) never shares CUs with
-    its peers' kernels, so there is no limit then.  With ``co`` processes on one device, the other
-    ``co - 1`` may all be spinning while this one needs whole CUs: each process keeps its grid within
-    (CUs - CUs/4) / (co - 1), leaving a quarter of the chip free for whole-CU kernels.
-    ``TDE_XGMI_SPIN_CAP=0`` disables the limit (diagnostics)."""
-    keys = [_device_key(d) if d.type == "cuda" else None for d in devices]
-    if control is None:
-        per_proc = [sorted({k for k in keys if k})]
-    else:
-        per_proc = control.all_gather_json(sorted({k for k in keys if k}), tag)
-    caps = []
-    for d, k in zip(devices, keys):
-        co = sum(1 for ks in per_proc if k in ks) if k else 1
-        if co <= 1 or os.environ.get("TDE_XGMI_SPIN_CAP", "1") == "0":
-            caps.append(None)
+    GPU time out in eager AND graph mode with the MNIST CNN, while Model B, whose kernels fit beside a
+    spinning wave, runs clean; with the limit every mode runs clean.  One process per GPU (a real N-GPU
+    node) never shares CUs with its peers' kernels, so there is no limit then.  With ``co`` processes on
+    one device, the other ``co - 1`` may all be spinning while this one needs whole CUs: each process
+    keeps its grid within (CUs - CUs/4) / (co - 1), leaving a quarter of the chip free for whole-CU
+    kernels; a process launching ``nloc`` ranks of that device in one grid gives each rank 1/nloc of it.
+
+    The kernel's slice length, chunking and per-chunk flags assume EVERY rank launches the same number of
+    chunks (``xg_slice(M, nranks, nblocks)``; ``push_spec``'s L), so the cap is one world-wide number: the
+    minimum over every shared device of its grid cap divided by the largest replica group any process
+    launches on it (per-rank caps disagreed under uneven co-location, e.g. 3 processes on 2
+    GPUs).  ``TDE_XGMI_SPIN_CAP=0`` disables the limit (diagnostics)."""
+    mine = {}
+    for d in devices:
+        if d.type != "cuda":
             continue
-        cus = torch.cuda.get_device_properties(d).multi_processor_count
-        caps.append(max(8, (cus - cus // 4) // (co - 1)))
-    return caps
+        k = _device_key(d)
+        if k not in mine:
+            mine[k] = [0, torch.cuda.get_device_properties(d).multi_processor_count]
+        mine[k][0] += 1
+    per_proc = [mine] if control is None else control.all_gather_json(mine, tag)
+    cap = chunk_cap_of(per_proc)
+    if os.environ.get("TDE_XGMI_SPIN_CAP", "1") == "0":
+        cap = None
+    if control is not None:
+        caps = control.all_gather_json(cap, tag + "_agree")
+        if any(c != cap for c in caps):
+            raise RuntimeError(f"xGMI all-reduce chunk caps differ across ranks: {caps} (TDE_XGMI_SPIN_CAP set on "
+                               "some ranks only?)")
+    return cap
+
+
+def chunk_cap_of(per_proc):
+    """``spin_chunk_cap``'s rule on the gathered layouts: per_proc[i] = {device key: [replicas process i
+    launches on it, CUs]}."""
+    devs = {}
+    for mine in per_proc:
+        for k, (nloc, cus) in mine.items():
+            co, mx, c = devs.get(k, (0, 0, cus))
+            devs[k] = (co + 1, max(mx, int(nloc)), int(cus))
+    cap = None
+    for k, (co, nloc, cus) in sorted(devs.items()):
+        if co <= 1:
+            continue
+        per_rank = max(1, max(8, (cus - cus // 4) // (co - 1)) // max(1, nloc))
+        cap = per_rank if cap is None else min(cap, per_rank)
+    return cap
+
 
 class XgmiCommunicator(Communicator):
     """Single-node fp32 SUM all-reduce over IPC-mapped peer windows (csrc/comm/xgmi_allreduce.hip).
@@ -352,18 +379,18 @@ class XgmiCommunicator(Communicator):
             self._free()
             raise RuntimeError(f"xGMI peer mapping failed: {errs}")
         self.peers = (C.c_void_p * self.world)(*peers)
-        self.grid_cap = spin_grid_caps(control, [self.device], "xgmi_spin")[0]
+        self.chunk_cap = spin_chunk_cap(control, [self.device], "xgmi_spin")
         tc = int(os.environ.get("TDE_XGMI_TRACE", "0") or 0)
         self.trace = [_xg_trace_alloc(self.lib, self.device, self.epoch.value, tc)] if tc > 0 else None
 
     def nblocks(self, M):
         """Chunks (= workgroups) of a call: ~512 elements of the slice each, within the kernel maximum and
-        the co-located-process spin limit (``spin_grid_caps``)."""
+        the world-wide co-located-process spin limit (``spin_chunk_cap``): the same on every rank."""
         if self.nblocks_override:
             return self.nblocks_override
         L = -(-M // self.world)
         nb = max(8, min(self.lib.tde_xgmi_max_blocks(), L // 512))
-        return min(nb, self.grid_cap) if self.grid_cap else nb
+        return min(nb, self.chunk_cap) if self.chunk_cap else nb
 
     def handles(self, t, op):
         return (op == "sum" and t.dtype == torch.float32 and t.is_cuda and t.is_contiguous()
@@ -638,21 +665,19 @@ class PeerXgmiCommunicator(Communicator):
             self._gargs.append(((C.c_void_p * len(flat))(*flat), (C.c_void_p * len(grp))(*[self.epochs[i] for i in grp]),
                                 (C.c_void_p * len(grp))(*[self.errs[i] for i in grp])))
         self._side = [torch.cuda.Stream(self.devices[grp[0]]) for grp in self.groups]
-        caps = spin_grid_caps(control, self.devices, "pxg_spin")
-        self.grid_caps = [caps[grp[0]] for grp in self.groups]
+        self.chunk_cap = spin_chunk_cap(control, self.devices, "pxg_spin")
         tc = int(os.environ.get("TDE_XGMI_TRACE", "0") or 0)
         self.trace = [_xg_trace_alloc(self.lib, d, e, tc) for d, e in zip(self.devices, self.epochs)] \
             if tc > 0 else None
 
     def nblocks(self, M, nloc=1, gi=0):
         """Chunks per rank of group ``gi``'s launches (``nloc`` ranks in one grid): ~512 elements of the
-        slice each, within the kernel maximum, and the whole grid (nloc x chunks) within the
-        co-located-process spin limit of the group's device (``spin_grid_caps``; none when no other
-        process shares the GPU)."""
+        slice each, within the kernel maximum and the world-wide co-located-process spin limit
+        (``spin_chunk_cap``, which already divides each shared device's grid by its largest group; none
+        when no process shares a GPU) — the same number on every rank, whatever its group."""
         cap = self.lib.tde_xgmi_max_blocks()
-        gc = self.grid_caps[gi] if gi < len(self.grid_caps) else None
-        if gc:
-            cap = max(1, min(cap, gc // max(1, nloc)))
+        if self.chunk_cap:
+            cap = max(1, min(cap, self.chunk_cap))
         if self.nblocks_override:
             return min(self.nblocks_override, cap)
         return max(min(8, cap), min(cap, -(-M // self.world) // 512))

@@ -96,6 +96,10 @@ class ReplicaPlan:
     def finish(self):
         """End of an execution (a run of steps): commit deferred updates."""
 
+    def trace_tensors(self):
+        """State recorded per step by ``Program.enable_trace`` (diagnostics)."""
+        return [self.store.w, self.metrics]
+
     def refresh(self):
         """Before an execution is launched or captured: pick up optimizer hyper-parameter changes."""
 
@@ -417,6 +421,17 @@ class ConvNetPlan(ReplicaPlan):
         self._xg_rep = self.f32 and self.crep > 1 and not others
         self.gconv = torch.zeros(2, self.crep, span, dtype=torch.float32, device=dev)
         self.pend = torch.zeros(2, dtype=torch.int32, device=dev)
+        # device counters of the deferred conv update (the local step's invariants, ``step_invariants``):
+        # [0] updates committed (by the next backward's head workgroup or the flush), [1] forwards that
+        # applied a pending update on the fly
+        self.ucount = torch.zeros(2, dtype=torch.int64, device=dev)
+        # fused step: the head variables as of this step's forward ([b1 | W2 | b2], written by the forward),
+        # read by the backward's trunk workgroups while its head workgroup updates the originals
+        C_ = self.Cls
+        self.hsnap = torch.zeros(64 + 64 * C_ + C_, dtype=torch.float32, device=dev)
+        self._hs_b1 = self.hsnap[:64]
+        self._hs_w2 = self.hsnap[64: 64 + 64 * C_].view(64, C_)
+        self._hs_b2 = self.hsnap[64 + 64 * C_:]
         self.iter_prev = torch.zeros(1, dtype=torch.int64, device=dev)
         self._fopt = self._bopt = self._flush = None
         # step mode "xgmi" with the fused exchange (set_push): the backward stores dW1 straight into the
@@ -472,10 +487,15 @@ class ConvNetPlan(ReplicaPlan):
             f = K.step_opt(opt, st.w, None, m, v, self.iter_prev, self.pend[1 - q])
             f.g = self._gconv(1 - q)
             f.grep, f.grep_stride = self.crep, self._conv_span
+            f.fly_count = self.ucount[1].data_ptr()
+            f.hsrc_w2, f.hsrc_b2 = self._v("w2").data_ptr(), self._v("b2").data_ptr()
+            f.hsrc_b1 = self._v("b1").data_ptr() if self.names["b1"] is not None else None
+            f.hsnap, f.hC = self.hsnap.data_ptr(), self.Cls
             self._fopt.append(f)
             commit = K.flat_apply_spec(opt, st.w, None, m, v, self.iterations, self.pend[1 - q], conv)
             commit.g = self._gconv(1 - q)
             commit.grep, commit.grep_stride = self.crep, self._conv_span
+            commit.count = self.ucount[0].data_ptr()
             b1 = self.names["b1"]
             self._bopt.append(K.BwdOpt(
                 opt.kind_id, float(opt.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"], P_(st.w), P_(m),
@@ -486,6 +506,7 @@ class ConvNetPlan(ReplicaPlan):
             fl = K.flat_apply_spec(opt, st.w, None, m, v, self.iterations, self.pend[q], conv)
             fl.g = self._gconv(q)
             fl.grep, fl.grep_stride = self.crep, self._conv_span
+            fl.count = self.ucount[0].data_ptr()
             self._flush.append(fl)
 
     def push_range(self):
@@ -540,6 +561,36 @@ class ConvNetPlan(ReplicaPlan):
             # only the last step's conv update can be pending (each backward commits the previous one)
             self.K.flat_apply(self._flush[1 - self.parity])
 
+    def step_invariants(self):
+        """The deferred conv update's state between executions (step mode "local"; synchronises): every
+        step's update committed exactly once, nothing pending, every gradient replica consumed."""
+        torch.cuda.synchronize(self.device)
+        return dict(commits=int(self.ucount[0]), applied_on_the_fly=int(self.ucount[1]),
+                    pending=[int(v) for v in self.pend.cpu()], gconv_abs_max=float(self.gconv.abs().max()))
+
+    def trace_tensors(self):
+        """Per-step state recorded by ``Program.enable_trace`` (diagnostics)."""
+        return [self.store.w, self.gconv.view(-1), self.pend.float(), self.metrics]
+
+    def effective_weights(self, trace):
+        """From ``Program.enable_trace`` rows of this plan ([S, n]): the weights each step left for the next
+        forward, [S, store.w.numel()] — in step mode "local" the stored conv weights lag by the pending
+        (deferred) update, which the next forward applies on the fly (SGD: w - lr * sum of the pending
+        parity's gradient replicas)."""
+        nw, ng = self.store.w.numel(), self.gconv.numel()
+        w = trace[:, :nw].clone()
+        if self.step_mode != "local":
+            return w
+        if self.optimizer.kind_id != 0:
+            raise NotImplementedError("effective_weights: the deferred update is reconstructed for SGD only")
+        g = trace[:, nw: nw + ng].reshape(len(trace), 2, self.crep, self._conv_span).sum(dim=2)
+        pend = trace[:, nw + ng: nw + ng + 2]
+        lo, span = self._conv_lo, self._conv_span
+        lr = float(self.optimizer.learning_rate)
+        for q in (0, 1):
+            w[:, lo: lo + span] -= lr * g[:, q] * (pend[:, q:q + 1] != 0)
+        return w
+
     def on_weights_loaded(self):
         if not self.f32:
             (self.opt or self._shadow_only).refresh_shadows()
@@ -579,7 +630,11 @@ class ConvNetPlan(ReplicaPlan):
         else:
             dwc, dbc = self._g("wc"), self._g("bc")
         push = self._push if xg else None
-        K.convnet_bwd(x, self.amax, self.hpre2[q], self.hpre2[1 - q], self._v("b1"), self._v("w2"), self._v("b2"), y,
+        if local:   # the head variables as of the forward (the backward's head workgroup updates the originals)
+            b1, w2, b2 = (self._hs_b1 if self.names["b1"] is not None else None), self._hs_w2, self._hs_b2
+        else:
+            b1, w2, b2 = self._v("b1"), self._v("w2"), self._v("b2")
+        K.convnet_bwd(x, self.amax, self.hpre2[q], self.hpre2[1 - q], b1, w2, b2, y,
                       scale=self.scale, pre_relu=self.pre_relu, metrics=self.metrics, W1row=self.W1row, Pt=self.Pt,
                       dW1=self._g("w1"), dwc=dwc, dbc=dbc, dW2=self._g("w2"), db2=self._g("b2"), db1=self._g("b1"),
                       B=B, opt=self._bopt[q] if local else None, cpart=self.cpart, push=push,

@@ -143,6 +143,7 @@ class Program:
         self._comm_warm = False
         self._dbg = os.environ.get("TDE_DEBUG_SYNC", "0") not in ("", "0") and cuda
         self._host_trace = [] if os.environ.get("TDE_HOST_TRACE", "0") not in ("", "0") else None
+        self._trace = None   # enable_trace(): per-step state buffers
         self.buckets = self._plan_buckets() if training else None
         self._comm_stream = torch.cuda.Stream(self.devices[0]) if self.buckets else None
         self.comm_applies = False
@@ -302,7 +303,31 @@ class Program:
                     plan.train_step(self.x_ring[r][s], self.y_ring[r][s], B)
                 self._debug_sync("train_step")
             self._reduce_and_apply()
+            if self._trace is not None:
+                self._record(s)
         self._finish()
+
+    def enable_trace(self):
+        """Diagnostics: after every step of an execution, copy each plan's ``trace_tensors()`` (weights and
+        the plan's cross-step state) into ``self.trace[r][s]`` — captured into the hipGraph like the steps,
+        so an execution's per-step states are readable after it (``sync()`` first).  Single-group layouts."""
+        if self.per_replica:
+            raise NotImplementedError("per-step traces are recorded for single-group layouts")
+        self.graphs = {}
+        self._trace = []
+        for p in self.plans:
+            n = sum(t.numel() for t in p.trace_tensors())
+            self._trace.append(torch.zeros(self.S, n, dtype=torch.float32, device=p.device))
+        self.trace = self._trace
+
+    def _record(self, s):
+        for r, p in enumerate(self.plans):
+            with _ctx(p.device):
+                o = 0
+                for t in p.trace_tensors():
+                    n = t.numel()
+                    self._trace[r][s, o: o + n].copy_(t.reshape(-1))
+                    o += n
 
     def _overlapped_step(self, s, B):
         """fwd + bwd on the compute stream; each gradient bucket's all-reduce is enqueued on the comm
