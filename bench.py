@@ -220,7 +220,7 @@ def main():
                        "input_staged_in_timed_region": True,
                        "optimizer": f"SGD(lr={a.lr})", "plan": prog.plan_kind,
                        "allreduce": ar,
-                       "hipgraph": prog.use_graph, "grad_buckets": len(prog.buckets or []) or 1,
+                       "hipgraph": prog.use_graph, "grad_buckets": len(prog.buckets or prog.group_buckets or []) or 1,
                        # the same K-step measurement repeated after the reported one (ms/step; spread evidence)
                        "repeat_ms_per_step": [round(r / a.steps * 1e3, 5) for r in repeats],
                        "optimizer_placement": placement,

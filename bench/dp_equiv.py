@@ -96,6 +96,7 @@ def main():
         print(f"[dp_equiv] strategy={a.strategy} replicas={n} plan={prog.plan_kind} graph={prog.use_graph} "
               f"comm={type(strategy.comm).__name__} step_mode={prog.plans[0].step_mode} "
               f"exchange={getattr(prog, 'exchange', 'none')} "
+              f"grad_buckets={len(prog.buckets or getattr(prog, 'group_buckets', None) or []) or 1} "
               f"replicas_identical={same} loss={logs['loss']:.6f}{inv}", flush=True)
 
 

@@ -112,3 +112,10 @@ def resnet(stage_blocks=(2, 2, 2, 2), filters=(64, 128, 256, 512), input_shape=(
 def resnet18(input_shape=(224, 224, 3), classes=1000, name="resnet18"):
     """ResNet-18 (BASELINE.json stress config; not in the reference): 11.69M parameters at 224/1000."""
     return resnet((2, 2, 2, 2), (64, 128, 256, 512), input_shape, classes, name=name)
+
+
+def mini_resnet(input_shape=(32, 32, 3), classes=10, name="mini_resnet"):
+    """A two-stage BasicBlock ResNet (16 / 32 filters) on 32x32x3: ResNet-18's layer kinds (stem conv, BN,
+    max-pool, projection shortcut, residual add, GAP, Dense) at test size."""
+    return resnet((1, 1), (16, 32), input_shape, classes, name=name)
+

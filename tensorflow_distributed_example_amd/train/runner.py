@@ -125,9 +125,11 @@ class Program:
         env = os.environ.get("TDE_GRAPH", "1") != "0"
         # several local replicas over a per-replica communicator (in-process xGMI): every device group's
         # steps run on a stream of their own and are captured into a hipGraph of their own
-        self.per_replica = bool(training and cuda and len(self.devices) > 1 and
-                                getattr(self.comm, "per_replica", False) and
-                                all(p.store.g.numel() <= self.comm.max_elems for p in self.plans))
+        pr = bool(training and cuda and len(self.devices) > 1 and getattr(self.comm, "per_replica", False))
+        cut = self._group_cut() if pr else None
+        # every all-reduce call must fit the xGMI window: the whole bucket, or each reverse-order bucket
+        self.per_replica = pr and (all(p.store.g.numel() <= self.comm.max_elems for p in self.plans) or
+                                   (cut is not None and max(hi - lo for _, lo, hi in cut) <= self.comm.max_elems))
         if (training and cuda and len(self.devices) > 1 and getattr(self.comm, "per_replica", False)
                 and not self.per_replica):
             import warnings
@@ -146,6 +148,12 @@ class Program:
         self._trace = None   # enable_trace(): per-step state buffers
         self.buckets = self._plan_buckets() if training else None
         self._comm_stream = torch.cuda.Stream(self.devices[0]) if self.buckets else None
+        # per-device-group layouts (Mirrored / MWMS with K GPUs per worker): the same reverse-order buckets,
+        # each issued by the group's launch on a comm stream of its own as soon as the group's last replica
+        # has finished the backward stage that finalises it
+        self.group_buckets = self._plan_group_buckets() if training else None
+        self._gcomm = ([torch.cuda.Stream(self.devices[g[0]]) for g in self.groups] if self.group_buckets
+                       else None)
         self.comm_applies = False
         self.exchange = "post_backward" if self.comm is not None else "none"
         if training:
@@ -157,7 +165,7 @@ class Program:
         under the xGMI communicator it runs inside the gradient all-reduce ("xgmi")."""
         from ..parallel.comm import XgmiCommunicator
         self._route_grads()
-        if os.environ.get("TDE_FUSED_STEP", "1") == "0" or self.buckets:
+        if os.environ.get("TDE_FUSED_STEP", "1") == "0" or self.buckets or self.group_buckets:
             return
         if self.per_replica:
             if all(p.supports_step_mode("xgmi") for p in self.plans):
@@ -215,6 +223,25 @@ class Program:
         bk = plan.grad_buckets(max(1, int(mb * 2 ** 20 / 4)))
         return bk if len(bk) > 1 else None
 
+    def _plan_group_buckets(self):
+        """``_plan_buckets`` for the per-device-group layouts (``per_replica``): every replica holds the same
+        model, so one cut serves all; issued per group on the group's comm stream.  ``TDE_OVERLAP=0`` keeps
+        the single post-backward launch per group."""
+        if not self.per_replica:
+            return None
+        return self._group_cut()
+
+    def _group_cut(self):
+        if os.environ.get("TDE_OVERLAP", "1") == "0":
+            return None
+        if not all(hasattr(p, "grad_buckets") for p in self.plans):
+            return None
+        mb = float(os.environ.get("TDE_BUCKET_MB", "8"))
+        bk = self.plans[0].grad_buckets(max(1, int(mb * 2 ** 20 / 4)))
+        if len(bk) <= 1 or any(lo % 4 for _, lo, _ in bk):   # the xGMI launch takes 16-byte aligned slices
+            return None
+        return bk
+
     @property
     def plan_kind(self):
         return self.plans[0].kind
@@ -261,6 +288,10 @@ class Program:
     def _steps_group(self, gi, S, B=None):
         """S training steps of device group gi (its launches only wait for the other groups on the device)."""
         idx = self.groups[gi]
+        if self.group_buckets:
+            for s in range(S):
+                self._overlapped_group_step(gi, s, B)
+            return
         for s in range(S):
             for r in idx:
                 self.plans[r].train_step(self.x_ring[r][s], self.y_ring[r][s], B)
@@ -270,6 +301,40 @@ class Program:
             self._debug_sync("train_step + gradient all-reduce")
         for r in idx:
             self.plans[r].finish()
+
+    def _overlapped_group_step(self, gi, s, B=None):
+        """Device group gi, one step with the reverse-order gradient buckets: the group's replicas run
+        forward + backward in turn on the group's stream; while the LAST one's backward is still running,
+        each bucket's group all-reduce launch (every replica's slice in one xGMI launch) is enqueued on the
+        group's comm stream right after the backward stage that finalises it (event edges, captured into
+        the group's hipGraph); the optimizer launches wait for the comm stream."""
+        idx = self.groups[gi]
+        plans = [self.plans[r] for r in idx]
+        dev = self.devices[idx[0]]
+        main = torch.cuda.current_stream(dev)
+        cs = self._gcomm[gi]
+        ready = {}
+        for i, lo, hi in self.group_buckets:
+            ready.setdefault(i, []).append((lo, hi))
+        sides = [p.side_stream for p in plans if getattr(p, "side_stream", None) is not None]
+
+        def after_bwd(i):
+            for lo, hi in ready.get(i, ()):
+                cs.wait_stream(main)
+                for sd in sides:
+                    cs.wait_stream(sd)
+                with torch.cuda.stream(cs):
+                    self.comm.all_reduce_group_(gi, [p.store.g[lo:hi] for p in plans])
+
+        for r in idx[:-1]:
+            self.plans[r].train_step(self.x_ring[r][s], self.y_ring[r][s], B)
+        r = idx[-1]
+        self.plans[r].train_step(self.x_ring[r][s], self.y_ring[r][s], B, after_bwd=after_bwd)
+        main.wait_stream(cs)
+        self._debug_sync("train_step + bucketed group all-reduce")
+        for p in plans:
+            p.apply()
+        self._debug_sync("optimizer")
 
     @contextlib.contextmanager
     def _on_group(self, gi):
@@ -500,7 +565,14 @@ class Program:
                             n = len(per_replica[r][1])
                             if n > 0:
                                 self.plans[r].train_step(self.x_ring[r][0], self.y_ring[r][0], n)
-                        self._reduce_and_apply_group(gi)
+                        if self.group_buckets:   # the same bucket calls as the captured steps, post-backward
+                            plans = [self.plans[r] for r in idx]
+                            for _, lo, hi in self.group_buckets:
+                                self.comm.all_reduce_group_(gi, [p.store.g[lo:hi] for p in plans])
+                            for p in plans:
+                                p.apply()
+                        else:
+                            self._reduce_and_apply_group(gi)
                         for r in idx:
                             self.plans[r].finish()
                 return
