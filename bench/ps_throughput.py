@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--model", default="mnist_bn_cnn")
     ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--momentum", type=float, default=0.0)
     a, _ = ap.parse_known_args()
     import numpy as np
 
@@ -69,7 +70,7 @@ def main():
     y = rng.integers(0, 10, (n, 1)).astype(np.int32)
     model = getattr(tde.zoo, a.model)()
     model.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=a.model != "mnist_bn_cnn"),
-                  optimizer=tde.optimizers.SGD(learning_rate=a.lr), metrics=["accuracy"])
+                  optimizer=tde.optimizers.SGD(learning_rate=a.lr, momentum=a.momentum), metrics=["accuracy"])
     rc = tde.estimator.RunConfig(
         experimental_distribute=tde.contrib.distribute.DistributeConfig(
             train_distribute=tde.contrib.distribute.ParameterServerStrategy()),
@@ -95,7 +96,7 @@ def main():
                           "ps_tasks": len(cfg.get("cluster", {}).get("ps", [])), "batch": a.batch,
                           "model": a.model, "steps_timed": hook.s1 - hook.s0, "master_local_steps_per_sec":
                           round(local, 1), "device": str(model._store.device), "final_global_step": hook.s1,
-                          "data_plane": "device" if os.environ.get("TDE_PS_DEVICE") == "1" else "tcp"}),
+                          "momentum": a.momentum, "data_plane": getattr(est, "ps_data_plane", "tcp")}),
               flush=True)
 
 

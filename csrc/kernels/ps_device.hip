@@ -1,20 +1,28 @@
 // Same-node GPU data plane of ParameterServerStrategy (reference
 // mnist_keras_distributed.py:242, tf2_mnist_distributed.py:189).
 //
-// The ps task owns ONE device window (fine-grained, uncached, IPC-exported): the flat variable buffers
-// of the model and the PS counters,
-//     [counters: 16 x u64 (0 global_step, 1 step tickets, 2 initialised, 3 pushes)] [W: nw f32] [S: ns f32]
-// Every trainer maps it (hipIpcOpenMemHandle; same device or a peer over xGMI) and runs its whole async
-// exchange as ONE kernel after its backward, with no host staging and no TCP payload:
-//   push    W[i] += -lr * g[i]                 (system-scope f32 atomics: concurrent trainers lose no
-//                                               update, like the PS's serialised ApplyGradientDescent)
-//           S[j] := m*S[j] + (1-m)*v[j]        (BN moving statistics, compare-and-swap; v = this trainer's
-//                                               batch statistic recovered from its local update)
-//   pull    w[i] = W[i], s[j] = S[j]           (fresh values, including other trainers' updates)
-//   count   global_step += dstep, tickets += dticket by the LAST block, after every block's updates have
-//           been performed (system fence + arrival counter), into host-mapped words the host reads after
-//           the stream sync — a chief that sees global_step == max_steps sees all of them applied.
-// The window lives as long as the ps task (TF's variables on /job:ps); TCP carries the handle only.
+// Every ps task owns ONE device window (fine-grained, uncached, IPC-exported) holding ITS shard of the
+// variables (round-robin placement, TF's replica_device_setter), sized for that shard on request:
+//     [counters: 16 x u64 (0 global_step, 1 step tickets, 2 initialised, 3 pushes) — used in ps 0's]
+//     [shard data: trainable variables | their momentum slots (momentum / Nesterov) | BN moving stats]
+// Every trainer maps every window (hipIpcOpenMemHandle; same device or a peer over xGMI) and runs its
+// whole async exchange as ONE kernel after its backward, over a segment table (one entry per variable:
+// window, window offset, local flat offset, length, slot offset), with no host staging and no TCP payload:
+//   push    SGD        W[i] += -lr * g[i]                    (system-scope f32 atomics: concurrent trainers
+//                                                            lose no update, like the PS's serialised apply)
+//           momentum   M[i] := mom*M[i] - lr*g[i] (compare-and-swap), then W[i] += M_new
+//           Nesterov   as momentum, then W[i] += mom*M_new - lr*g[i]
+//                      (each trainer's slot update is atomic and its weight delta an atomic add: the result
+//                       is the serialised Keras update sequence in the order the CASes won)
+//           S[j] := m*S[j] + (1-m)*v[j]                     (BN moving statistics, compare-and-swap; v = this
+//                                                            trainer's batch statistic recovered from its
+//                                                            local update)
+//   pull    w[i] = W[i], s[j] = S[j]                        (fresh values, including other trainers' updates)
+//   count   global_step += dstep, tickets += dticket in ps 0's counters by the LAST block, after every
+//           block's updates on every shard have been performed (system fence + arrival counter), into
+//           host-mapped words the host reads after the stream sync — a chief that sees
+//           global_step == max_steps sees all of them applied (the TCP plane's "ps 0 last" order).
+// The windows live as long as their ps tasks (TF's variables on /job:ps); TCP carries the handles only.
 #include "tde_common.h"
 
 #include <string.h>
@@ -22,70 +30,99 @@
 namespace tde {
 
 constexpr int kPsCounters = 16;
+constexpr int kPsMaxShards = 16;
+
+struct PsSeg {        // one variable of one shard (host-built table, device-resident)
+  long long woff;     // element offset in the shard's data area
+  long long loff;     // element offset in the local flat buffer (w / g, or s / sp / mom for a statistic)
+  long long n;
+  long long moff;     // momentum slot offset in the shard's data area (< 0: none)
+  int win;            // shard (ps task) index
+  int state;          // 1: BN moving statistic
+};
 
 struct PsDevArgs {
-  unsigned long long* ctr;   // window counters
-  float* W;                  // window weights [nw]
-  float* S;                  // window state [ns]
-  float* w;                  // local weights (pulled into)
-  float* g;                  // local gradients (read, zeroed); null: pull only
-  long long nw;
-  float* s;                  // local state: after this step's forward (push) / pulled into
-  float* sp;                 // local copy of the last pulled state (push reads, pull rewrites)
-  const float* mom;          // per-element BN momentum [ns]
-  long long ns;
-  float lr;
+  float* data[kPsMaxShards];   // every window's data area (after its counters)
+  unsigned long long* ctr;     // ps 0's counters
+  const PsSeg* segs;
+  float* w;                    // local weights (pulled into)
+  float* g;                    // local gradients (read, zeroed); null: pull only
+  float* s;                    // local state: after this step's forward (push) / pulled into
+  float* sp;                   // local copy of the last pulled state (push reads, pull rewrites)
+  const float* mom;            // per-element BN momentum (local state layout)
+  float lr, mmt;               // learning rate, optimizer momentum
+  int kind;                    // 0 SGD, 1 momentum, 2 Nesterov
   long long dstep, dticket;
-  unsigned int* done;        // local device word: blocks finished (re-armed by the last)
-  long long* out;            // host-mapped [global_step, tickets] after this call
+  unsigned int* done;          // local device word: blocks finished (re-armed by the last)
+  long long* out;              // host-mapped [global_step, tickets] after this call
 };
 
 __device__ __forceinline__ float sys_load(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// grid (x: element blocks, y: segment); a segment with fewer elements than the x extent idles its tail blocks
 __global__ __launch_bounds__(256) void ps_dev_step_kernel(PsDevArgs a) {
   const bool push = a.g != nullptr;
-  const long long n = a.nw + a.ns;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    if (i < a.nw) {
-      if (push) {
-        const float gi = a.g[i];
-        if (gi != 0.f) __hip_atomic_fetch_add(a.W + i, -a.lr * gi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        a.g[i] = 0.f;
-      }
-      a.w[i] = sys_load(a.W + i);
-    } else {
-      const long long j = i - a.nw;
-      float val;
-      if (push) {
-        const float m = a.mom[j];
-        // the local forward applied m*old + (1-m)*v to the pulled value old: recover v, apply it to the PS's
-        // current value (no lost updates between async trainers)
-        const float v = (a.s[j] - m * a.sp[j]) / (1.f - m);
-        float cur = sys_load(a.S + j);
-        for (;;) {
-          const float nv = cur * m + (1.f - m) * v;
-          if (__hip_atomic_compare_exchange_strong(a.S + j, &cur, nv, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_SYSTEM)) {
-            val = nv;
-            break;
+  if (a.segs) {
+    const PsSeg sg = a.segs[blockIdx.y];
+    float* const D = a.data[sg.win];
+    float* const W = D + sg.woff;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < sg.n;
+         i += (long long)gridDim.x * blockDim.x) {
+      const long long li = sg.loff + i;
+      if (!sg.state) {
+        if (push) {
+          const float gi = a.g[li];
+          if (a.kind == 0) {
+            if (gi != 0.f) __hip_atomic_fetch_add(W + i, -a.lr * gi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          } else {
+            float* const M = D + sg.moff + i;
+            float cur = sys_load(M), nv;
+            for (;;) {
+              nv = a.mmt * cur - a.lr * gi;
+              if (__hip_atomic_compare_exchange_strong(M, &cur, nv, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_SYSTEM))
+                break;
+            }
+            const float dw = a.kind == 2 ? a.mmt * nv - a.lr * gi : nv;
+            __hip_atomic_fetch_add(W + i, dw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           }
+          a.g[li] = 0.f;
         }
+        a.w[li] = sys_load(W + i);
       } else {
-        val = sys_load(a.S + j);
+        float val;
+        if (push) {
+          const float m = a.mom[li];
+          // the local forward applied m*old + (1-m)*v to the pulled value old: recover v, apply it to the
+          // PS's current value (no lost updates between async trainers)
+          const float v = (a.s[li] - m * a.sp[li]) / (1.f - m);
+          float cur = sys_load(W + i);
+          for (;;) {
+            const float nv = cur * m + (1.f - m) * v;
+            if (__hip_atomic_compare_exchange_strong(W + i, &cur, nv, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_SYSTEM)) {
+              val = nv;
+              break;
+            }
+          }
+        } else {
+          val = sys_load(W + i);
+        }
+        a.s[li] = val;
+        a.sp[li] = val;
       }
-      a.s[j] = val;
-      a.sp[j] = val;
     }
   }
-  // every block's atomics are performed before the last block advances the counters
+  // every block's atomics (on every shard) are performed before the last block advances the counters
   __atomic_thread_fence(__ATOMIC_SEQ_CST);   // system scope: drains and orders this thread's accesses
   __syncthreads();
   if (threadIdx.x == 0) {
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    const unsigned nblk = gridDim.x * gridDim.y;
     const unsigned prev = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1) {
+    if (prev == nblk - 1) {
       __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const long long gs = (long long)__hip_atomic_fetch_add(a.ctr + 0, (unsigned long long)a.dstep, __ATOMIC_SEQ_CST,
                                                              __HIP_MEMORY_SCOPE_SYSTEM) + a.dstep;
@@ -101,10 +138,27 @@ __global__ __launch_bounds__(256) void ps_dev_step_kernel(PsDevArgs a) {
   }
 }
 
-// window -> local / local -> window flat copies (initialisation, checkpoint, restore)
-__global__ __launch_bounds__(256) void ps_dev_copy_kernel(float* dst, const float* src, long long n) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
-    dst[i] = src[i];
+// segment-wise copies between the local flat buffers and the windows (initialisation, checkpoint,
+// restore): dir 0 local -> windows (momentum slots zeroed), dir 1 windows -> local
+struct PsCopyArgs {
+  float* data[kPsMaxShards];
+  const PsSeg* segs;
+  float* w;
+  float* s;
+  int dir;
+};
+__global__ __launch_bounds__(256) void ps_dev_copy_kernel(PsCopyArgs a) {
+  const PsSeg sg = a.segs[blockIdx.y];
+  float* const W = a.data[sg.win] + sg.woff;
+  float* const L = (sg.state ? a.s : a.w) + sg.loff;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < sg.n; i += (long long)gridDim.x * blockDim.x) {
+    if (a.dir == 0) {
+      W[i] = L[i];
+      if (!sg.state && sg.moff >= 0) a.data[sg.win][sg.moff + i] = 0.f;
+    } else {
+      L[i] = W[i];
+    }
+  }
 }
 
 }  // namespace tde
@@ -136,50 +190,74 @@ TDE_API int tde_host_mapped_alloc(long long bytes, void** host, void** dev) {
 }
 TDE_API int tde_host_mapped_free(void* host) { return host ? (int)hipHostFree(host) : 0; }
 
-// One async exchange (g != null) or a pull (g == null); see the header comment.
-TDE_API int tde_psdev_step(void* window, long long nw, long long ns, float* w, float* g, float* s, float* sp,
-                           const float* mom, float lr, long long dstep, long long dticket, unsigned int* done,
-                           long long* out_dev, hipStream_t stream) {
-  if (!window || !w || nw < 0 || ns < 0 || !done || (ns > 0 && (!s || !sp || (g && !mom)))) return -1;
+static int ps_grid_x(long long maxn) {
+  long long bx = (maxn + 255) / 256;
+  if (bx > 64) bx = 64;
+  return bx < 1 ? 1 : (int)bx;
+}
+
+static int ps_fill_data(float** data, void* const* windows, int nwin) {
+  if (nwin < 1 || nwin > kPsMaxShards) return -1;
+  for (int i = 0; i < kPsMaxShards; ++i)
+    data[i] = i < nwin && windows[i] ? (float*)((char*)windows[i] + kPsCounters * 8) : nullptr;
+  for (int i = 0; i < nwin; ++i)
+    if (!windows[i]) return -1;
+  return 0;
+}
+
+// One async exchange (g != null) or a pull (g == null) over the segment table `segs` (device memory,
+// nseg entries; maxn = the largest segment), or, with nseg == 0, a counters-only call; see the header.
+TDE_API int tde_psdev_step(void* const* windows, int nwin, const void* segs, int nseg, long long maxn, float* w,
+                           float* g, float* s, float* sp, const float* mom, float lr, float mmt, int kind,
+                           long long dstep, long long dticket, unsigned int* done, long long* out_dev,
+                           hipStream_t stream) {
+  if (!w || nseg < 0 || (nseg > 0 && !segs) || !done || kind < 0 || kind > 2 || nseg > 65535) return -1;
   PsDevArgs a;
-  a.ctr = (unsigned long long*)window;
-  a.W = (float*)((char*)window + kPsCounters * 8);
-  a.S = a.W + nw;
+  if (ps_fill_data(a.data, windows, nwin)) return -1;
+  a.ctr = (unsigned long long*)windows[0];
+  a.segs = nseg > 0 ? (const PsSeg*)segs : nullptr;
   a.w = w;
   a.g = g;
-  a.nw = nw;
   a.s = s;
   a.sp = sp;
   a.mom = mom;
-  a.ns = ns;
   a.lr = lr;
+  a.mmt = mmt;
+  a.kind = kind;
   a.dstep = dstep;
   a.dticket = dticket;
   a.done = done;
   a.out = out_dev;
-  long long blocks = (nw + ns + 255) / 256;
-  if (blocks > 1024) blocks = 1024;
-  if (blocks < 1) blocks = 1;
-  ps_dev_step_kernel<<<(int)blocks, 256, 0, stream>>>(a);
+  const dim3 grid(nseg > 0 ? ps_grid_x(maxn) : 1, nseg > 0 ? nseg : 1);
+  ps_dev_step_kernel<<<grid, 256, 0, stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;
 }
 
-// dir 0: local (w, s) -> window (and counters[0..1] := gstep, tickets when set >= 0, counters[2] := 1);
-// dir 1: window -> local (w, s).
-TDE_API int tde_psdev_copy(void* window, long long nw, long long ns, float* w, float* s, int dir, hipStream_t stream) {
-  float* W = (float*)((char*)window + kPsCounters * 8);
-  const long long n1 = nw, n2 = ns;
-  if (dir == 0) {
-    if (n1) ps_dev_copy_kernel<<<(int)((n1 + 255) / 256 > 1024 ? 1024 : (n1 + 255) / 256), 256, 0, stream>>>(W, w, n1);
-    if (n2) ps_dev_copy_kernel<<<(int)((n2 + 255) / 256 > 1024 ? 1024 : (n2 + 255) / 256), 256, 0, stream>>>(W + nw, s, n2);
-  } else {
-    if (n1) ps_dev_copy_kernel<<<(int)((n1 + 255) / 256 > 1024 ? 1024 : (n1 + 255) / 256), 256, 0, stream>>>(w, W, n1);
-    if (n2) ps_dev_copy_kernel<<<(int)((n2 + 255) / 256 > 1024 ? 1024 : (n2 + 255) / 256), 256, 0, stream>>>(s, W + nw, n2);
-  }
+// dir 0: local (w, s) -> windows (momentum slots zeroed); dir 1: windows -> local (w, s).
+TDE_API int tde_psdev_copy(void* const* windows, int nwin, const void* segs, int nseg, long long maxn, float* w,
+                           float* s, int dir, hipStream_t stream) {
+  if (nseg <= 0 || !segs || nseg > 65535) return nseg == 0 ? 0 : -1;
+  PsCopyArgs a;
+  if (ps_fill_data(a.data, windows, nwin)) return -1;
+  a.segs = (const PsSeg*)segs;
+  a.w = w;
+  a.s = s;
+  a.dir = dir;
+  ps_dev_copy_kernel<<<dim3(ps_grid_x(maxn), nseg), 256, 0, stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;
 }
+
+// A window re-armed for a new training session: every byte (counters included: "initialised" = 0) zeroed.
+TDE_API int tde_psdev_zero(void* window, long long bytes) {
+  hipError_t e = hipMemset(window, 0, (size_t)bytes);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipDeviceSynchronize();
+}
+
+// Size of the segment-table entry (the Python side packs the table with numpy).
+TDE_API int tde_psdev_seg_bytes() { return (int)sizeof(PsSeg); }
 
 // Counter i of the window := v (host write through hipMemcpy; initialisation / restore only) / read.
 TDE_API int tde_psdev_set_counter(void* window, int i, long long v) {

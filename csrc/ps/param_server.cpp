@@ -4,11 +4,13 @@
 // A ps task owns a shard of the variables (round-robin placement by the client,
 // like TF's replica_device_setter).  Workers PULL current values and PUSH
 // gradients asynchronously; the server applies the update on receipt under a
-// per-variable lock (SGD / momentum, Keras form).  BN moving statistics are
+// per-variable lock (SGD / momentum / Nesterov / Adam, Keras forms; Adam's step count t is the
+// variable's own update count, as TF1's async PS applies each variable's Adam update independently).  BN moving statistics are
 // updated with MOVING_AVG pushes; the global step is an atomic counter.
 // Transport: the length-prefixed TCP framing of tde_net.h (C++ replacement of
 // TF's gRPC RecvTensor / variable-update RPCs).
 #include <atomic>
+#include <cmath>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -26,8 +28,9 @@ enum Op : uint8_t {
 
 struct Var {
   std::mutex mu;
-  std::vector<float> w, slot;
+  std::vector<float> w, slot, slot2;
   int64_t version = 0;
+  int64_t t = 0;   // Adam: updates applied to this variable
 };
 
 struct PSServer {
@@ -39,8 +42,9 @@ struct PSServer {
   std::atomic<int64_t> counters[3]{};     // counters 1..3: tickets etc.
   std::atomic<int64_t> pushes{0}, pulls{0};
   // set by a kSetOpt request on one connection's thread, read by every push handler
-  std::atomic<int> kind{0};  // 0 sgd, 1 momentum, 2 nesterov
+  std::atomic<int> kind{0};  // 0 sgd, 1 momentum, 2 nesterov, 3 adam
   std::atomic<float> momentum{0.f};
+  std::atomic<float> beta1{0.9f}, beta2{0.999f}, epsilon{1e-7f};
   std::thread acceptor;
   std::mutex cmu;
   std::set<int> clients;
@@ -67,6 +71,18 @@ struct PSServer {
     if (n != v->w.size()) return;
     if (k == 0) {
       for (size_t i = 0; i < n; ++i) v->w[i] -= lr * wire_f32(g, i);
+    } else if (k == 3) {
+      if (v->slot.size() != n) v->slot.assign(n, 0.f);
+      if (v->slot2.size() != n) v->slot2.assign(n, 0.f);
+      const float b1 = beta1.load(), b2 = beta2.load(), eps = epsilon.load();
+      const double t = (double)(++v->t);
+      const float lr_t = (float)(lr * std::sqrt(1.0 - std::pow((double)b2, t)) / (1.0 - std::pow((double)b1, t)));
+      for (size_t i = 0; i < n; ++i) {
+        const float gi = wire_f32(g, i);
+        v->slot[i] = b1 * v->slot[i] + (1.f - b1) * gi;
+        v->slot2[i] = b2 * v->slot2[i] + (1.f - b2) * gi * gi;
+        v->w[i] -= lr_t * v->slot[i] / (std::sqrt(v->slot2[i]) + eps);
+      }
     } else {
       if (v->slot.size() != n) v->slot.assign(n, 0.f);
       for (size_t i = 0; i < n; ++i) {
@@ -202,6 +218,12 @@ struct PSServer {
         case kSetOpt: {
           kind.store((int)r.u32());
           momentum.store(r.f32());
+          const float b1 = r.f32(), b2 = r.f32(), eps = r.f32();
+          if (r.ok) {   // Adam's hyper-parameters (older clients send kind + momentum only)
+            beta1.store(b1);
+            beta2.store(b2);
+            epsilon.store(eps);
+          }
           w.u8(0);
           break;
         }
@@ -487,11 +509,14 @@ TDE_API long long tde_ps_step_get(void* h) {
   return r.i64();
 }
 
-TDE_API int tde_ps_set_optimizer(void* h, int kind, float momentum) {
+TDE_API int tde_ps_set_optimizer(void* h, int kind, float momentum, float beta1, float beta2, float epsilon) {
   tde_net::Writer w;
   w.u8(kSetOpt);
   w.u32((uint32_t)kind);
   w.f32(momentum);
+  w.f32(beta1);
+  w.f32(beta2);
+  w.f32(epsilon);
   std::string resp;
   if (!((PSClient*)h)->call(w.s, &resp) || resp.empty()) return -1;
   return resp[0];

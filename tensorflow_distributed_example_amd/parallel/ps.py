@@ -48,7 +48,7 @@ N.register_host({
     "tde_ps_step_add": (C.c_longlong, [C.c_void_p, C.c_longlong]),
     "tde_ps_step_get": (C.c_longlong, [C.c_void_p]),
     "tde_ps_counter_add": (C.c_longlong, [C.c_void_p, C.c_int, C.c_longlong]),
-    "tde_ps_set_optimizer": (C.c_int, [C.c_void_p, C.c_int, C.c_float]),
+    "tde_ps_set_optimizer": (C.c_int, [C.c_void_p, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float]),
     "tde_ps_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]),
     "tde_ps_step": (C.c_int, [C.c_void_p, C.c_float,
                               C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_void_p), C.POINTER(C.c_longlong),
@@ -81,19 +81,24 @@ class PSServer:
 
 def run_ps_server(address: str, stop_event=None, index: int = 0):
     """Serve variables forever (TF ``server.join()``), or until ``stop_event`` is set.  With
-    ``TDE_PS_DEVICE=1`` ps task 0 also owns the same-node GPU data plane's window (parallel/ps_device.py)."""
+    ``TDE_PS_DEVICE=1`` every ps task also serves its shard's window of the same-node GPU data plane
+    (parallel/ps_device.py), allocated on the chief's request per training session (``TDE_PS_GPU``: the
+    GPU, default 0)."""
     host, port = address.rsplit(":", 1)
     srv = PSServer("0.0.0.0", int(port))
     print(f"[ps] serving on {address}", flush=True)
-    window = None
-    if index == 0:
-        from . import ps_device as PD
-        if PD.enabled():
-            window = PD.serve_window(srv.port)
+    win = None
+    from . import ps_device as PD
+    if PD.enabled():
+        win = PD.WindowServer(srv.port, int(os.environ.get("TDE_PS_GPU", "0")), index)
     try:
         while stop_event is None or not stop_event.is_set():
-            time.sleep(0.2)
+            if win is not None:
+                win.poll()
+            time.sleep(0.05 if win is not None else 0.2)
     finally:
+        if win is not None:
+            win.close()
         srv.stop()
 
 
@@ -195,9 +200,10 @@ class PSClient:
                 gstep, ticket = so.value, to.value
         return gstep, ticket
 
-    def set_optimizer(self, kind, momentum=0.0):
+    def set_optimizer(self, kind, momentum=0.0, beta1=0.9, beta2=0.999, epsilon=1e-7):
+        """The update every ps task applies on a push: 0 SGD, 1 momentum, 2 Nesterov, 3 Adam (Keras forms)."""
         for c in self.conns:
-            c.lib.tde_ps_set_optimizer(c.h, int(kind), float(momentum))
+            c.lib.tde_ps_set_optimizer(c.h, int(kind), float(momentum), float(beta1), float(beta2), float(epsilon))
 
     def initialize(self, values: dict, is_chief: bool, timeout=120.0):
         """Chief creates every variable; others wait until the chief's init flag exists."""

@@ -372,7 +372,8 @@ class Estimator:
             shapes = {n: tuple(m._store.segments[n].shape) for n in m._store.order}
             self._psc = strategy.client(shapes)
             from ..optimizers import KIND
-            self._psc.set_optimizer(min(m.optimizer.kind_id, 2), getattr(m.optimizer, "momentum", 0.0))
+            hp = m.optimizer.hparams()
+            self._psc.set_optimizer(m.optimizer.kind_id, hp["mom"], hp["b1"], hp["b2"], hp["eps"])
         return self._psc
 
     def _train_ps(self, strategy, input_fn, hooks, steps, max_steps, saving_listeners):
@@ -422,6 +423,7 @@ class Estimator:
             bn_mom[n_] = next(l.momentum for l in m.layers if l.name == layer)
         lr = float(opt_saved.learning_rate)
         plane = self._ps_device_plane(client, store, bn_mom, lr, opt_saved, chief)
+        self.ps_data_plane = "device" if plane is not None else "tcp"   # what this trainer ran (bench / tests)
         if plane is not None:
             if chief:
                 for h in all_hooks:
@@ -491,47 +493,47 @@ class Estimator:
 
     def _ps_device_plane(self, client, store, bn_mom, lr, opt, chief):
         """The same-node GPU data plane (parallel/ps_device.py) or None (the host-staged TCP plane).  The chief
-        decides — TDE_PS_DEVICE=1, plain SGD, the model on a GPU, ps task 0 publishing a window the model fits
-        in — and records the decision on ps task 0; every other trainer follows it, so no two trainers ever
-        update different copies of the variables."""
+        decides — TDE_PS_DEVICE=1, SGD (plain, momentum or Nesterov), the model on a GPU, every ps task
+        serving a window of its shard's size for this session — and records the decision with the session
+        tag on ps task 0 (overwritten every session); every other trainer follows it, so no two trainers
+        ever update different copies of the variables."""
         import warnings
 
         from ..parallel import ps as PS
         from ..parallel import ps_device as PD
-        flag = np.zeros(1, np.float32)
+        flag = np.zeros(2, np.float32)
         c0 = client.conns[0]
         names = PS._arr([PD.PLANE_VAR])
+        kind = opt.kind_id
+        mom = float(opt.hparams()["mom"])
         if chief:
             plane, why = None, None
+            session = PD.new_session()
             if PD.enabled() and store.device.type == "cuda":
-                if opt.kind_id != 0 or getattr(opt, "momentum", 0.0):
-                    why = "plain SGD only (the update is an atomic add)"
+                if kind not in (0, 1, 2):
+                    why = "SGD / momentum / Nesterov only (Adam runs on the TCP plane)"
                 else:
-                    t0 = time.time()
-                    while plane is None:   # ps task 0 publishes the window right after it starts serving
-                        try:
-                            plane = PD.DevicePlane(client, store, bn_mom, lr)
-                        except PD.NoWindow as e:
-                            if time.time() - t0 > 30:
-                                why = str(e)
-                                break
-                            time.sleep(0.1)
-                        except RuntimeError as e:
-                            why = str(e)
-                            break
+                    try:
+                        _, sizes = PD.layout(store, client.placement, len(client.conns), slots=kind != 0)
+                        PD.request_windows(client, sizes, session)
+                        plane = PD.DevicePlane(client, store, bn_mom, lr, kind, mom, session=session, timeout=30)
+                    except (PD.NoWindow, RuntimeError) as e:
+                        why = str(e)
                 if why:
                     warnings.warn(f"PS device data plane unavailable ({why}); using the TCP plane")
-            flag[0] = 1.0 if plane is not None else 0.0
-            c0.lib.tde_ps_init(c0.h, PD.PLANE_VAR.encode(), flag.ctypes.data, 1)
+            flag[:] = (1.0 if plane is not None else 0.0, session)
+            c0.lib.tde_ps_init(c0.h, PD.PLANE_VAR.encode(), flag.ctypes.data, 2)
+            c0.lib.tde_ps_assign(c0.h, PD.PLANE_VAR.encode(), flag.ctypes.data, 2)
             return plane
         t0 = time.time()
-        while c0.lib.tde_ps_pull(c0.h, 1, names, (C.c_void_p * 1)(flag.ctypes.data), (C.c_longlong * 1)(1)) != 0:
+        while c0.lib.tde_ps_pull(c0.h, 1, names, (C.c_void_p * 1)(flag.ctypes.data), (C.c_longlong * 1)(2)) != 0:
             if time.time() - t0 > 120:
                 raise TimeoutError("the chief never recorded the PS data plane")
             time.sleep(0.05)
         if flag[0] != 1.0:
             return None
-        return PD.DevicePlane(client, store, bn_mom, lr)   # the chief mapped it: failing here is an error
+        # the chief mapped the same session's windows: failing here is an error
+        return PD.DevicePlane(client, store, bn_mom, lr, kind, mom, session=float(flag[1]), timeout=120)
 
     def _ps_loop_device(self, plane, chief, it, prog, plan, ctx, all_hooks, target, max_steps):
         """Async PS loop on the device window: every step's exchange is one kernel (push, BN averages, pull,

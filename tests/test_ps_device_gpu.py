@@ -20,7 +20,7 @@ sys.path.insert(0, {root!r})
 from tensorflow_distributed_example_amd.parallel.ps import run_ps_server
 ev = threading.Event()
 threading.Thread(target=lambda: (sys.stdin.read(), ev.set()), daemon=True).start()
-run_ps_server("127.0.0.1:{port}", stop_event=ev, index=0)
+run_ps_server("127.0.0.1:{port}", stop_event=ev, index={index})
 """
 
 
@@ -32,10 +32,12 @@ def _free_port():
     return p
 
 
-def test_device_plane_exchange_is_exact():
-    """One trainer against the ps task's window: W -= lr*g (f32 atomics), the BN moving average applied to
-    the PS value from the recovered batch statistic, the pull, and the counters — checked against host
-    arithmetic over 3 steps."""
+@pytest.mark.parametrize("nps,kind", [(1, 0), (2, 1), (2, 2)])
+def test_device_plane_exchange_is_exact(nps, kind):
+    """Trainer against the ps tasks' windows (variables round-robin over ``nps`` tasks, each window sized
+    for its shard on request): the SGD / momentum / Nesterov update (f32 atomics, slot compare-and-swap),
+    the BN moving average applied to the PS value from the recovered batch statistic, the pull and the
+    counters — checked against host arithmetic over 3 steps."""
     import torch
 
     from tensorflow_distributed_example_amd.parallel import ps as PS
@@ -47,51 +49,66 @@ def test_device_plane_exchange_is_exact():
             self.full_name, self.shape, self.trainable, self.aggregation = name, shape, trainable, "none"
             self.initializer = lambda shape, gen: np.zeros(shape, np.float32)
 
-    port = _free_port()
-    env = dict(os.environ, TDE_PS_DEVICE="1", TDE_PS_WINDOW_MB="4")
-    srv = subprocess.Popen([sys.executable, "-c", PS_SERVER.format(root=ROOT, port=port)], env=env,
-                           stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    ports = [_free_port() for _ in range(nps)]
+    env = dict(os.environ, TDE_PS_DEVICE="1")
+    srvs = [subprocess.Popen([sys.executable, "-c", PS_SERVER.format(root=ROOT, port=p, index=i)], env=env,
+                             stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+            for i, p in enumerate(ports)]
+    lr, mm = 0.5, 0.9
     try:
-        os.environ["TDE_PS_DEVICE"], os.environ["TDE_PS_WINDOW_MB"] = "1", "4"
-        specs = [_Spec("d/kernel", (300, 7), True), _Spec("bn/moving_mean", (5,), False), _Spec("d/bias", (7,), True)]
+        os.environ["TDE_PS_DEVICE"] = "1"
+        specs = [_Spec("d/kernel", (300, 7), True), _Spec("bn/moving_mean", (5,), False), _Spec("d/bias", (7,), True),
+                 _Spec("e/kernel", (7, 3), True)]
         store = ParamStore(specs, "cuda:0")
         shapes = {n: tuple(store.segments[n].shape) for n in store.order}
         t0 = time.time()
         while True:
             try:
-                client = PS.PSClient([f"127.0.0.1:{port}"], shapes)
+                client = PS.PSClient([f"127.0.0.1:{p}" for p in ports], shapes)
                 break
             except ConnectionError:
-                assert time.time() - t0 < 60 and srv.poll() is None
+                assert time.time() - t0 < 60 and all(s.poll() is None for s in srvs)
                 time.sleep(0.2)
+        assert len(set(client.placement.values())) == nps
         g = torch.Generator().manual_seed(0)
         w0 = torch.randn(store.w.numel(), generator=g)
         s0 = torch.rand(store.state.numel(), generator=g)
         store.w.copy_(w0.cuda())
         store.state.copy_(s0.cuda())
-        t0 = time.time()
-        while True:
-            try:
-                plane = PD.DevicePlane(client, store, {"bn/moving_mean": 0.9}, lr=0.5)
-                break
-            except RuntimeError:
-                assert time.time() - t0 < 60
-                time.sleep(0.2)
+        session = PD.new_session()
+        _, sizes = PD.layout(store, client.placement, nps, slots=kind != 0)
+        PD.request_windows(client, sizes, session)
+        plane = PD.DevicePlane(client, store, {"bn/moving_mean": 0.9}, lr=lr, kind=kind, momentum=mm,
+                               session=session, timeout=60)
+        assert len(plane.wins) == nps and not plane.initialized()
         plane.initialize(7, 7)
         assert plane.global_step() == 7 and plane.initialized()
         plane.pull()
         W, S = w0.double().clone(), s0.double().clone()
+        M = torch.zeros_like(W)
+        live = torch.zeros(store.w.numel())
+        for n in ("d/kernel", "d/bias", "e/kernel"):
+            live[store.segments[n].offset: store.segments[n].offset + store.segments[n].numel] = 1.0
         for step in range(3):
-            gr = torch.randn(store.w.numel(), generator=g)
+            gr = torch.randn(store.w.numel(), generator=g) * live   # the flat buffer's alignment gaps stay 0
             batch_stat = torch.rand(store.state.numel(), generator=g)
             store.g.copy_(gr.cuda())
             # what the local forward does to the moving statistic: m*pulled + (1-m)*batch
             store.state.copy_((0.9 * S + 0.1 * batch_stat.double()).float().cuda())
             gs, t = plane.step(dstep=1, dticket=2)
-            W = W - 0.5 * gr.double()
+            gd = gr.double()
+            if kind == 0:
+                W = W - lr * gd
+            else:
+                M = mm * M - lr * gd
+                W = W + (mm * M - lr * gd if kind == 2 else M)
             S = 0.9 * S + 0.1 * batch_stat.double()
             assert (gs, t) == (8 + step, 9 + 2 * step)
-            assert torch.allclose(store.w.double().cpu(), W, rtol=0, atol=1e-5), step
+            # trainable elements only (the flat buffer also has alignment padding)
+            for n in ("d/kernel", "d/bias", "e/kernel"):
+                seg = store.segments[n]
+                sl = slice(seg.offset, seg.offset + seg.numel)
+                assert torch.allclose(store.w[sl].double().cpu(), W[sl], rtol=0, atol=2e-5), (step, n)
             assert torch.allclose(store.state.double().cpu(), S, rtol=0, atol=1e-6), step
             assert float(store.g.abs().max()) == 0.0
         assert plane.counter_add(1, 1) == 14 and plane.global_step() == 10
@@ -99,28 +116,30 @@ def test_device_plane_exchange_is_exact():
         client.close()
     finally:
         os.environ.pop("TDE_PS_DEVICE", None)
-        os.environ.pop("TDE_PS_WINDOW_MB", None)
-        try:
-            srv.stdin.close()
-        except OSError:
-            pass
-        try:
-            srv.wait(20)
-        except subprocess.TimeoutExpired:
-            srv.kill()
-            srv.wait()
+        for srv in srvs:
+            try:
+                srv.stdin.close()
+            except OSError:
+                pass
+            try:
+                srv.wait(20)
+            except subprocess.TimeoutExpired:
+                srv.kill()
+                srv.wait()
 
 
-@pytest.mark.parametrize("plane", ["device", "tcp"])
-def test_ps_estimator_two_trainers_exact_max_steps(plane):
-    """ps + master + worker on localhost (all on cuda:0): async Estimator training of Model B stops at
-    EXACTLY max_steps global updates (step tickets), on the device data plane and on the TCP plane."""
+@pytest.mark.parametrize("plane,nps,momentum", [("device", 1, 0.0), ("tcp", 1, 0.0), ("device", 2, 0.9),
+                                                 ("tcp", 2, 0.9)])
+def test_ps_estimator_two_trainers_exact_max_steps(plane, nps, momentum):
+    """ps x nps + master + worker on localhost (all on cuda:0): async Estimator training of Model B stops at
+    EXACTLY max_steps global updates (step tickets), on the device data plane (every ps task serving its
+    shard's window, momentum slots in the windows) and on the TCP plane."""
     env = dict(os.environ, OMP_NUM_THREADS="2", TDE_HEARTBEAT="0")
     if plane == "device":
         env["TDE_PS_DEVICE"] = "1"
-    cmd = [sys.executable, "-m", "tensorflow_distributed_example_amd.launch", "--ps", "1", "--master", "1", "--workers",
-           "1", "--timeout", "150", os.path.join(ROOT, "bench", "ps_throughput.py"), "--max-steps", "800", "--warm",
-           "100"]
+    cmd = [sys.executable, "-m", "tensorflow_distributed_example_amd.launch", "--ps", str(nps), "--master", "1",
+           "--workers", "1", "--timeout", "150", os.path.join(ROOT, "bench", "ps_throughput.py"), "--max-steps", "800",
+           "--warm", "100", "--momentum", str(momentum)]
     r = subprocess.run(cmd, env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=200)
     assert r.returncode == 0, r.stdout[-4000:]
     # the launcher prefixes each task's lines with "[task:index] "
@@ -128,6 +147,7 @@ def test_ps_estimator_two_trainers_exact_max_steps(plane):
     assert len(lines) == 1, r.stdout[-3000:]
     res = json.loads(lines[0])
     print(res)
-    assert res["data_plane"] == plane and res["trainers"] == 2, res
+    assert res["data_plane"] == plane and res["trainers"] == 2 and res["ps_tasks"] == nps, res
+    assert res["momentum"] == momentum, res
     assert res["final_global_step"] == 800, res
     assert res["value"] > 0
