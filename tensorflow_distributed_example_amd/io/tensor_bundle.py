@@ -78,7 +78,15 @@ def list_variables(prefix: str):
     return out
 
 
-def read_bundle(prefix: str, skip_bad_strings: bool = True) -> dict:
+def read_bundle(prefix: str, skip_bad_strings: bool | None = None) -> dict:
+    """Every tensor of the bundle at ``prefix`` ({key: array}; scalar string tensors decoded).  A string
+    tensor that fails its checksum or does not parse raises — except, by default (``None``), the TF2 object
+    graph (``_CHECKPOINTABLE_OBJECT_GRAPH``: metadata only, restore matches variables by key without it),
+    which is skipped with a warning naming it.  ``True`` skips (with the warning) every unreadable string
+    tensor, ``False`` skips none."""
+    import warnings
+
+    from .object_graph import GRAPH_KEY
     lib = N.host()
     entries = list_variables(prefix)
     h = lib.tde_bundle_open(str(prefix).encode())
@@ -93,11 +101,10 @@ def read_bundle(prefix: str, skip_bad_strings: bool = True) -> dict:
                     if rc != 0:
                         raise IOError(f"{prefix}: reading {name} failed ({'crc mismatch' if rc == -3 else rc})")
                     out[name] = decode_string_tensor(bytes(raw))[0]
-                except IOError:
-                    # string tensors carry metadata only (the TF2 object graph); restore matches variables
-                    # by key position without it, so an unreadable one is skipped, not fatal
-                    if not skip_bad_strings:
-                        raise
+                except (IOError, ValueError, IndexError) as e:
+                    if not (skip_bad_strings or (skip_bad_strings is None and name == GRAPH_KEY)):
+                        raise IOError(f"{prefix}: string tensor {name!r} is unreadable ({e})") from e
+                    warnings.warn(f"{prefix}: skipping unreadable string tensor {name!r} ({e})")
                 continue
             if dt not in _DT_INV:
                 continue
