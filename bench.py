@@ -33,6 +33,11 @@ METRIC = "images/sec (whole node) MNIST CNN at 1/2/4/8 MI355X; step time ms"
 MODELS = {
     "mnist_cnn": (64, 16, 0.001, True, (28, 28, 1), METRIC),
     "mnist_bn_cnn": (128, 16, 0.01, False, (784,), METRIC),
+    # width variants (user edits of the reference models; the layer-wise plan or a generalised fused plan)
+    "mnist_cnn_wide": (64, 16, 0.001, True, (28, 28, 1),
+                       "images/sec (whole node) MNIST CNN Conv2D(64)/Dense(128) at 1/2/4/8 MI355X; step time ms"),
+    "mnist_bn_cnn_x2": (128, 16, 0.01, False, (784,),
+                        "images/sec (whole node) MNIST BN-CNN 2x widths at 1/2/4/8 MI355X; step time ms"),
     # the LeNet-5 label carries the precision actually run ({dtype}: fp32 by default, bf16 with --dtype bf16)
     "lenet5": (128, 16, 0.01, True, (28, 28, 1), "images/sec (whole node) MNIST LeNet-5 CNN {dtype} at 1/2/4/8 MI355X; step time ms"),
     "mnist_mlp": (128, 16, 0.01, True, (28, 28, 1), "images/sec (whole node) MNIST dense MLP at 1/2/4/8 MI355X; step time ms"),

@@ -25,6 +25,8 @@ import torch.nn.functional as F
 MODELS = {  # per-GPU batch, lr, image shape (NHWC), classes
     "mnist_cnn": (64, 0.001, (28, 28, 1), 10),
     "mnist_bn_cnn": (128, 0.01, (28, 28, 1), 10),
+    "mnist_cnn_wide": (64, 0.001, (28, 28, 1), 10),
+    "mnist_bn_cnn_x2": (128, 0.01, (28, 28, 1), 10),
     "resnet18": (64, 0.1, (224, 224, 3), 1000),
     "lenet5": (128, 0.01, (28, 28, 1), 10),
     "mnist_mlp": (128, 0.01, (28, 28, 1), 10),
@@ -57,11 +59,11 @@ class MLP(nn.Module):  # models/zoo.py mnist_mlp
 
 
 class MnistCNN(nn.Module):  # distributed_with_keras.py:33-39
-    def __init__(self):
+    def __init__(self, filters=32, units=64):
         super().__init__()
-        self.conv = nn.Conv2d(1, 32, 3)
-        self.fc1 = nn.Linear(13 * 13 * 32, 64)
-        self.fc2 = nn.Linear(64, 10)
+        self.conv = nn.Conv2d(1, filters, 3)
+        self.fc1 = nn.Linear(13 * 13 * filters, units)
+        self.fc2 = nn.Linear(units, 10)
 
     def forward(self, x):
         x = F.max_pool2d(F.relu(self.conv(x)), 2)
@@ -69,17 +71,17 @@ class MnistCNN(nn.Module):  # distributed_with_keras.py:33-39
 
 
 class MnistBNCNN(nn.Module):  # mnist_keras_distributed.py:79-109 (TF-SAME pads are symmetric here)
-    def __init__(self):
+    def __init__(self, m=1):
         super().__init__()
-        self.c1 = nn.Conv2d(1, 6, 3, padding=1, bias=False)
-        self.b1 = nn.BatchNorm2d(6, eps=1e-3, momentum=0.01, affine=True)
-        self.c2 = nn.Conv2d(6, 12, 6, stride=2, padding=2, bias=False)
-        self.b2 = nn.BatchNorm2d(12, eps=1e-3, momentum=0.01)
-        self.c3 = nn.Conv2d(12, 24, 6, stride=2, padding=2, bias=False)
-        self.b3 = nn.BatchNorm2d(24, eps=1e-3, momentum=0.01)
-        self.fc1 = nn.Linear(7 * 7 * 24, 200, bias=False)
-        self.b4 = nn.BatchNorm1d(200, eps=1e-3, momentum=0.01)
-        self.fc2 = nn.Linear(200, 10)
+        self.c1 = nn.Conv2d(1, 6 * m, 3, padding=1, bias=False)
+        self.b1 = nn.BatchNorm2d(6 * m, eps=1e-3, momentum=0.01, affine=True)
+        self.c2 = nn.Conv2d(6 * m, 12 * m, 6, stride=2, padding=2, bias=False)
+        self.b2 = nn.BatchNorm2d(12 * m, eps=1e-3, momentum=0.01)
+        self.c3 = nn.Conv2d(12 * m, 24 * m, 6, stride=2, padding=2, bias=False)
+        self.b3 = nn.BatchNorm2d(24 * m, eps=1e-3, momentum=0.01)
+        self.fc1 = nn.Linear(7 * 7 * 24 * m, 200 * m, bias=False)
+        self.b4 = nn.BatchNorm1d(200 * m, eps=1e-3, momentum=0.01)
+        self.fc2 = nn.Linear(200 * m, 10)
 
     def forward(self, x):
         x = F.relu(self.b1(self.c1(x)))
@@ -147,7 +149,8 @@ def main():
         torch.distributed.init_process_group("nccl", device_id=dev)
     torch.manual_seed(1234)
     model = {"mnist_cnn": MnistCNN, "mnist_bn_cnn": MnistBNCNN, "resnet18": lambda: ResNet18(ncls),
-             "lenet5": LeNet5, "mnist_mlp": MLP}[a.model]()
+             "lenet5": LeNet5, "mnist_mlp": MLP, "mnist_cnn_wide": lambda: MnistCNN(64, 128),
+             "mnist_bn_cnn_x2": lambda: MnistBNCNN(2)}[a.model]()
     model = model.to(dev)
     mf = torch.channels_last if a.channels_last else torch.contiguous_format
     model = model.to(memory_format=mf)

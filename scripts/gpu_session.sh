@@ -1,6 +1,7 @@
 #!/bin/bash
 # One GPU-box session: tests, smoke, bench, rocprof.  Stops at the first step
 # that ends in a fault/abort/timeout (exit codes other than 0/1).
+#   bash scripts/gpu_session.sh [all|tests|bench|models|baseline|micro|prof|equiv|buckets|ps|f32|widths]
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export PYTHONPATH="$PWD${PYTHONPATH:+:$PYTHONPATH}"
 export TMPDIR=/tmp
@@ -43,4 +44,9 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 400 --warmup 64
 fi
+# topic sessions of this round (scripts/sessions/<name>.sh): equiv | buckets | ps | f32 | widths
+case "$MODE" in
+  equiv) bash scripts/equiv_repeat.sh "${@:2}" || exit $? ;;
+  buckets|ps|f32|widths) bash "scripts/sessions/$MODE.sh" || exit $? ;;
+esac
 echo "=== done"

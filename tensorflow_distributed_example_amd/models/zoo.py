@@ -19,35 +19,46 @@ from . import layers as L
 from .model import Sequential
 
 
-def mnist_cnn(name=None):
+def mnist_cnn(name=None, filters=32, units=64):
     return Sequential([
-        L.Conv2D(32, 3, activation="relu", input_shape=(28, 28, 1)),
+        L.Conv2D(filters, 3, activation="relu", input_shape=(28, 28, 1)),
         L.MaxPooling2D(),
         L.Flatten(),
-        L.Dense(64, activation="relu"),
+        L.Dense(units, activation="relu"),
         L.Dense(10),
     ], name=name)
 
 
-def mnist_bn_cnn(name=None):
+def mnist_cnn_wide(name=None):
+    """Model A with every width doubled: Conv2D(64) / Dense(128) (a user edit of distributed_with_keras.py
+    :33-39 that the fused small-CNN step was not specialised for)."""
+    return mnist_cnn(name, filters=64, units=128)
+
+
+def mnist_bn_cnn(name=None, mult=1):
     return Sequential([
         L.Reshape(input_shape=(28 * 28,), target_shape=(28, 28, 1)),
-        L.Conv2D(filters=6, kernel_size=3, padding="same", use_bias=False),
+        L.Conv2D(filters=6 * mult, kernel_size=3, padding="same", use_bias=False),
         L.BatchNormalization(scale=False, center=True),
         L.Activation("relu"),
-        L.Conv2D(filters=12, kernel_size=6, padding="same", use_bias=False, strides=2),
+        L.Conv2D(filters=12 * mult, kernel_size=6, padding="same", use_bias=False, strides=2),
         L.BatchNormalization(scale=False, center=True),
         L.Activation("relu"),
-        L.Conv2D(filters=24, kernel_size=6, padding="same", use_bias=False, strides=2),
+        L.Conv2D(filters=24 * mult, kernel_size=6, padding="same", use_bias=False, strides=2),
         L.BatchNormalization(scale=False, center=True),
         L.Activation("relu"),
         L.Flatten(),
-        L.Dense(200, use_bias=False),
+        L.Dense(200 * mult, use_bias=False),
         L.BatchNormalization(scale=False, center=True),
         L.Activation("relu"),
         L.Dropout(0.5),
         L.Dense(10, activation="softmax"),
     ], name=name)
+
+
+def mnist_bn_cnn_x2(name=None):
+    """Model B with every width doubled (12/24/48 filters, Dense(400)): runs on the layer-wise plan."""
+    return mnist_bn_cnn(name, mult=2)
 
 
 def lenet5(name=None):

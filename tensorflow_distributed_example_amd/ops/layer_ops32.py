@@ -12,13 +12,15 @@ import ctypes as C
 import torch
 
 from .. import _native as N
-from .layer_ops import A_COLM, A_CONV, A_DGRAD, A_ROWK, A_WGRAD, B_DGRADW, B_KN, B_NK, STAT_SLOTS, ConvGeom, DropSpec
+from .layer_ops import (A_COLM, A_CONV, A_DGRAD, A_ROWK, A_WGRAD, B_DGRADW, B_KN, B_NK, STAT_SLOTS, ConvGeom, DropSpec,
+                        dgrad_phases)
 
 _P = N.ptr
 _vp, _i, _i64, _f, _u64 = C.c_void_p, C.c_int, C.c_longlong, C.c_float, C.c_ulonglong
 N.register_hip({
-    # a, lda, akind, b, ldb, bkind, M, N, K, geo, c, ldc, accum, bias, relu, colstats, splits, part, stream
-    "tde_igemm32": (_i, [_vp, _i64, _i, _vp, _i64, _i, _i, _i, _i, _vp, _vp, _i64, _i, _vp, _i, _vp, _i, _vp, _vp]),
+    # a, lda, akind, b, ldb, bkind, M, N, K, geo, c, ldc, accum, bias, relu, colstats, splits, part, phase, stream
+    "tde_igemm32": (_i, [_vp, _i64, _i, _vp, _i64, _i, _i, _i, _i, _vp, _vp, _i64, _i, _vp, _i, _vp, _i, _vp, _vp,
+                         _vp]),
     "tde_colstats32": (_i, [_vp, _i64, _i, _vp, _vp]),
     "tde_bn_fwd32": (_i, [_vp, _vp, _vp, _i64, _i, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp, _f, _f, _vp, _i, _f, _u64,
                           _vp, _i, _i, _vp]),
@@ -26,6 +28,7 @@ N.register_hip({
                           _i, _vp, _vp, _vp, _vp]),
     "tde_act_bwd32": (_i, [_vp, _vp, _i64, _i, _i, _vp, _vp, _vp]),
     "tde_maxpool32": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _vp, _i, _vp]),
+    "tde_maxpool32_bwd_relu": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _vp, _vp]),
     "tde_gap32": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp]),
     "tde_pad32": (_i, [_vp, _vp, _vp, _i, _i, _vp]),
     "tde_xent32": (_i, [_vp, _vp, _i, _i, _f, _vp, _vp, _vp, _i, _vp, _vp]),
@@ -53,14 +56,19 @@ def _f64(t, n, what):
          f"{what}: f64 [{n}] expected")
 
 
+def tiles(M, N_):
+    """Output tiles of an igemm32 launch (64 x 64 by default: layers_f32.hip tile_n)."""
+    return -(-M // 64) * -(-N_ // 64)
+
+
 def wgrad_splits(M, N_, K, target=256):
     """Split-K factor of a weight-gradient GEMM: its output tiles alone rarely fill the 256 CUs while its
     K (= pixels x batch) is long; the partials are summed in split order (deterministic)."""
-    tiles = -(-M // 64) * -(-N_ // 64)
+    tiles_ = tiles(M, N_)
     chunks = -(-K // 16)
-    if tiles >= target or chunks < 16:
+    if tiles_ >= target or chunks < 16:
         return 1
-    return max(1, min(-(-target // tiles), chunks // 8))
+    return max(1, min(-(-target // tiles_), chunks // 8))
 
 
 def wgrad_part_elems(M, N_, K):
@@ -68,33 +76,69 @@ def wgrad_part_elems(M, N_, K):
     return s * M * N_ if s > 1 else 0
 
 
+def fd_splits(M, N_, K, target=256):
+    """Split-K factor of a forward / input-gradient GEMM whose output tiles are too few to fill the chip
+    while K is long (a Dense layer on a wide flattened input: M = batch, K = 10,816); the partials are
+    summed in split order by the reduce launch, which then applies bias / ReLU / BN statistics."""
+    tiles_ = tiles(M, N_)
+    chunks = -(-K // 16)
+    if tiles_ >= 128 or chunks < 32:
+        return 1
+    return max(1, min(-(-target // tiles_), chunks // 8))
+
+
+def fd_part_elems(M, N_, K):
+    s = fd_splits(M, N_, K)
+    return s * M * N_ if s > 1 else 0
+
+
+def _fd(M, N_, K, part):
+    s = fd_splits(M, N_, K) if part is not None else 1
+    return (s, part) if s > 1 and part.numel() >= s * M * N_ else (1, None)
+
+
 def igemm32(a, lda, ak, b, ldb, bk, M, N_, K, c, ldc, *, geo=None, accum=False, bias=None, relu=False,
-            colstats=None, splits=1, part=None):
+            colstats=None, splits=1, part=None, phase=None):
     if splits > 1:
         _f32(part, splits * M * N_, "igemm32 split-K partials")
     if colstats is not None:
         _f64(colstats, 2 * STAT_SLOTS * N_, "igemm32 colstats")
+    ph = (C.c_int * len(phase))(*phase) if phase is not None else None
     rc = N.hip().tde_igemm32(_P(a), int(lda), ak, _P(b), int(ldb), bk, int(M), int(N_), int(K),
                              geo.carray() if geo is not None else None, _P(c), int(ldc), int(accum), _P(bias),
-                             int(relu), _P(colstats), int(splits), _P(part), _s())
+                             int(relu), _P(colstats), int(splits), _P(part), ph, _s())
     N.check(rc, "tde_igemm32")
 
 
 # ---------------------------------------------------------------- Conv2D / Dense
-def conv_fwd(x, W, y, g: ConvGeom, bias=None, relu=False, colstats=None):
+def conv_fwd(x, W, y, g: ConvGeom, bias=None, relu=False, colstats=None, part=None):
     """y[B*Ho*Wo, Co] = conv(x, W) (+bias, ReLU, BN statistics); W the HWIO f32 master kernel."""
     _f32(x, g.B * g.H * g.W * g.C, "conv_fwd x")
     _f32(W, g.K * g.Co, "conv_fwd W")
     _f32(y, g.B * g.Ho * g.Wo * g.Co, "conv_fwd y")
-    igemm32(x, 0, A_CONV, W, g.Co, B_KN, g.B * g.Ho * g.Wo, g.Co, g.K, y, g.Co, geo=g, bias=bias, relu=relu,
-            colstats=colstats)
+    M = g.B * g.Ho * g.Wo
+    s, pt = _fd(M, g.Co, g.K, part)
+    igemm32(x, 0, A_CONV, W, g.Co, B_KN, M, g.Co, g.K, y, g.Co, geo=g, bias=bias, relu=relu,
+            colstats=colstats, splits=s, part=pt)
 
 
-def conv_dgrad(dy, W, dx, g: ConvGeom, accum=False):
+def conv_dgrad(dy, W, dx, g: ConvGeom, accum=False, part=None):
+    """dx = conv input gradient.  Strided convs run every stride phase in ONE launch, each phase over only
+    the taps that reach its pixels (the other (s^2-1)/s^2 of the implicit-GEMM K would multiply zeros)."""
     _f32(dy, g.B * g.Ho * g.Wo * g.Co, "conv_dgrad dy")
     _f32(W, g.K * g.Co, "conv_dgrad W")
     _f32(dx, g.B * g.H * g.W * g.C, "conv_dgrad dx")
-    igemm32(dy, 0, A_DGRAD, W, 0, B_DGRADW, g.B * g.H * g.W, g.C, g.KH * g.KW * g.Co, dx, g.C, geo=g, accum=accum)
+    if g.sh > 1 or g.sw > 1:
+        phases = dgrad_phases(g)
+        if 1 <= len(phases) <= 4 and len(phases) == g.sh * g.sw:
+            table = [len(phases)] + [v for ph in phases for v in ph]
+            Mx = max(g.B * ph[2] * ph[3] for ph in phases)
+            Kx = max(ph[6] * ph[7] * g.Co for ph in phases)
+            igemm32(dy, 0, A_DGRAD, W, 0, B_DGRADW, Mx, g.C, Kx, dx, g.C, geo=g, accum=accum, phase=table)
+            return
+    M, K = g.B * g.H * g.W, g.KH * g.KW * g.Co
+    s, pt = _fd(M, g.C, K, part)
+    igemm32(dy, 0, A_DGRAD, W, 0, B_DGRADW, M, g.C, K, dx, g.C, geo=g, accum=accum, splits=s, part=pt)
 
 
 def conv_wgrad(x, dy, dW, g: ConvGeom, part=None):
@@ -107,18 +151,21 @@ def conv_wgrad(x, dy, dW, g: ConvGeom, part=None):
     igemm32(x, 0, A_WGRAD, dy, g.Co, B_KN, g.K, g.Co, K, dW, g.Co, geo=g, splits=s, part=part)
 
 
-def dense_fwd(x, W, rows, y, bias=None, relu=False, colstats=None):
+def dense_fwd(x, W, rows, y, bias=None, relu=False, colstats=None, part=None):
     fin, fout = W.shape
     _f32(x, rows * fin, "dense_fwd x")
     _f32(y, rows * fout, "dense_fwd y")
-    igemm32(x, fin, A_ROWK, W, fout, B_KN, rows, fout, fin, y, fout, bias=bias, relu=relu, colstats=colstats)
+    s, pt = _fd(rows, fout, fin, part)
+    igemm32(x, fin, A_ROWK, W, fout, B_KN, rows, fout, fin, y, fout, bias=bias, relu=relu, colstats=colstats,
+            splits=s, part=pt)
 
 
-def dense_dgrad(dy, W, dx, rows, accum=False):
+def dense_dgrad(dy, W, dx, rows, accum=False, part=None):
     fin, fout = W.shape
     _f32(dy, rows * fout, "dense_dgrad dy")
     _f32(dx, rows * fin, "dense_dgrad dx")
-    igemm32(dy, fout, A_ROWK, W, fout, B_NK, rows, fin, fout, dx, fin, accum=accum)
+    s, pt = _fd(rows, fin, fout, part)
+    igemm32(dy, fout, A_ROWK, W, fout, B_NK, rows, fin, fout, dx, fin, accum=accum, splits=s, part=pt)
 
 
 def dense_wgrad(x, dy, dW, rows, part=None):
@@ -209,6 +256,21 @@ def maxpool_bwd(dy, idx, dx, g: ConvGeom, accum=False):
     _req(idx.dtype == torch.uint8 and idx.numel() >= g.B * g.Ho * g.Wo * g.C, "maxpool32 idx")
     N.check(N.hip().tde_maxpool32(None, None, _P(idx), _P(dy), _P(dx), int(accum), g.carray(), 1, _s()),
             "tde_maxpool32")
+
+
+def maxpool_bwd_relu(dy, y, idx, dx, g: ConvGeom, dbias=None, accum=False):
+    """Max-pool backward fused with the producer's ReLU (+ bias) backward: dx = dy * (y > 0) at each window's
+    winner, 0 elsewhere; dbias += the column sums of that over the pooled cells.  Non-overlapping windows."""
+    _f32(dy, g.B * g.Ho * g.Wo * g.C, "maxpool_bwd_relu dy")
+    _f32(y, g.B * g.Ho * g.Wo * g.C, "maxpool_bwd_relu y")
+    _f32(dx, g.B * g.H * g.W * g.C, "maxpool_bwd_relu dx")
+    _req(idx.numel() >= g.B * g.Ho * g.Wo * g.C and (dbias is None or dbias.numel() == g.C), "maxpool_bwd_relu")
+    N.check(N.hip().tde_maxpool32_bwd_relu(_P(dy), _P(y), _P(idx), _P(dx), _P(dbias), int(accum), g.carray(), _s()),
+            "tde_maxpool32_bwd_relu")
+
+
+def pool_relu_fusable(g: ConvGeom):
+    return g.C % 4 == 0 and g.sh >= g.KH and g.sw >= g.KW and g.KH * g.KW <= 255
 
 
 def gap_fwd(x, y, B, HW, Cc):

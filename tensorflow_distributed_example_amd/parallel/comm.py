@@ -260,7 +260,7 @@ def spin_chunk_cap(control, devices, tag):
     """The most chunks (workgroups per rank) ONE all-reduce launch may use, the same number on every rank
     of the world, or None (no limit beyond the kernel's own).
 
-    Why a limit exists (the round-3 eager MWMS 2x2 timeouts, scripts/diag_xgmi_hang.sh): a waiting
+    Why a limit exists (the round-3 eager MWMS 2x2 timeouts, scripts/diag/diag_xgmi_hang.sh): a waiting
     all-reduce workgroup holds a VGPR slice of its CU (4 waves x 80 VGPRs, one per SIMD).  The fused
     MNIST-CNN backward runs 1024-thread workgroups at 128 VGPRs — the whole register file of a CU — so it
     can only be dispatched onto a CU with no other wave on it.  When another PROCESS shares the GPU, its

@@ -293,6 +293,16 @@ class LayerwisePlan(PG.ReplicaPlan):
                         and len(T[st.out.id].consumers) == 1 and O.bn_pool_ok(nxt.geo)
                         and st.inp.root().id != 0):
                     st.pool, nxt.fused = nxt, True
+        # float32: Conv2D / Dense with ReLU whose only consumer is a non-overlapping MaxPool — the pool's
+        # backward applies the ReLU mask (from the pooled value) and the bias gradient, and the separate
+        # act_bwd pass over the 4x larger activation disappears.  TDE_POOL_RELU=0 keeps the two launches.
+        if self.f32 and os.environ.get("TDE_POOL_RELU", "1") != "0":
+            for i, st in enumerate(stages[:-1]):
+                nxt = stages[i + 1]
+                if (isinstance(st, _Gemm) and st.relu and not st.stats and isinstance(nxt, _MaxPool)
+                        and nxt.inp.root() is st.out.root() and len(T[st.out.id].consumers) == 1
+                        and O32.pool_relu_fusable(nxt.geo)):
+                    st.act_done, nxt.relu_from = True, st
         # gradient accumulation flags: reverse order, first writer stores
         written = set()
         for st in reversed(stages):
@@ -474,10 +484,19 @@ class _Gemm(_Stage):
         self.act_done = False   # the consumer's launch already applied the ReLU mask / bias gradient
 
     def wpart_need(self, B):
+        """f32 split-K partials of this layer's GEMMs (weight gradient, forward, input gradient)."""
         if self.conv:
             g = self.geo.with_batch(B)
-            return O32.wgrad_part_elems(g.K, g.Co, g.B * g.Ho * g.Wo)
-        return O32.wgrad_part_elems(self.W.shape[0], self.W.shape[1], self.inp.rows(B))
+            need = [O32.wgrad_part_elems(g.K, g.Co, g.B * g.Ho * g.Wo),
+                    O32.fd_part_elems(g.B * g.Ho * g.Wo, g.Co, g.K)]
+            if self.need_dgrad and g.sh == 1 and g.sw == 1:
+                need.append(O32.fd_part_elems(g.B * g.H * g.W, g.C, g.KH * g.KW * g.Co))
+            return max(need)
+        fin, fout, rows = self.W.shape[0], self.W.shape[1], self.inp.rows(B)
+        need = [O32.wgrad_part_elems(fin, fout, rows), O32.fd_part_elems(rows, fout, fin)]
+        if self.need_dgrad:
+            need.append(O32.fd_part_elems(rows, fin, fout))
+        return max(need)
 
     def scratch_need(self, B):
         if self.f32:
@@ -535,10 +554,10 @@ class _Gemm(_Stage):
         if self.f32:
             if self.conv:
                 O32.conv_fwd(self.inp.root().buf, self.W, self.out.root().buf, self.geo.with_batch(B), bias=self.b,
-                             relu=self.relu, colstats=cs)
+                             relu=self.relu, colstats=cs, part=p.wpart)
             else:
                 O32.dense_fwd(self.inp.root().buf, self.W.view(-1, self.W.shape[-1]), self.inp.rows(B),
-                              self.out.root().buf, bias=self.b, relu=self.relu, colstats=cs)
+                              self.out.root().buf, bias=self.b, relu=self.relu, colstats=cs, part=p.wpart)
             return
         if self.conv and self.use_stem_pack:
             g = self.geo.with_batch(B)
@@ -573,10 +592,10 @@ class _Gemm(_Stage):
                 return
             acc = self.accum[self.inp.root().id]
             if self.conv:
-                O32.conv_dgrad(dout, self.W, self.inp.root().grad, self.geo.with_batch(B), accum=acc)
+                O32.conv_dgrad(dout, self.W, self.inp.root().grad, self.geo.with_batch(B), accum=acc, part=p.wpart)
             else:
                 O32.dense_dgrad(dout, self.W.view(-1, self.W.shape[-1]), self.inp.root().grad, self.inp.rows(B),
-                                accum=acc)
+                                accum=acc, part=p.wpart)
             return
         side = p.side_stream
         if side is not None:
@@ -768,6 +787,7 @@ class _MaxPool(_Stage):
         self.geo = O.ConvGeom(plan.B, H, W_, C, Ho, Wo, C, layer.pool_size[0], layer.pool_size[1],
                               layer.strides[0], layer.strides[1], pt, pl)
         self.fused = False  # the producing BN+ReLU stage runs this pool's forward (bn_relu_maxpool_fwd)
+        self.relu_from = None   # f32: the producing ReLU GEMM whose mask / bias gradient this backward applies
         self.f32 = plan.f32
 
     def alloc(self, B, dev):
@@ -784,6 +804,10 @@ class _MaxPool(_Stage):
 
     def bwd(self, p, B):
         if self.inp.root().id == 0 or self.fused:
+            return
+        if self.relu_from is not None:
+            O32.maxpool_bwd_relu(self.out.root().grad, self.out.root().buf, self.idx, self.inp.root().grad,
+                                 self.geo.with_batch(B), dbias=self.relu_from.gb, accum=self.accum[self.inp.root().id])
             return
         self.O.maxpool_bwd(self.out.root().grad, self.idx, self.inp.root().grad, self.geo.with_batch(B),
                       accum=self.accum[self.inp.root().id])

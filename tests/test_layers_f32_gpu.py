@@ -41,6 +41,8 @@ CONV_CASES = [
     (2, 15, 15, 3, 64, 7, 2, "same"),    # ResNet stem shape family
     (2, 8, 8, 64, 128, 1, 2, "valid"),   # projection shortcut
     (3, 10, 9, 32, 40, 3, 1, "valid"),   # N tail
+    (2, 14, 14, 24, 48, 6, 2, "same"),   # Model B x2 conv3 (phased stride-2 input gradient, C % 4 == 0)
+    (2, 9, 9, 16, 32, 1, 2, "same"),     # 1x1 stride 2 "same": three of the four phases untapped (zeros)
 ]
 
 
@@ -83,6 +85,48 @@ def test_conv32_fwd_dgrad_wgrad(B, H, W, C, Co, k, s, pad):
     torch.cuda.synchronize()
     assert _rel(dx, xr.grad + 0.5) < 1e-6
     assert _rel(dW, wr.grad) < 1e-6
+
+
+def test_split_k_forward_and_input_gradient_match_float64():
+    """Few output tiles, long K (a Dense(128) on Conv2D(64)'s 10,816 pooled features; a 7x7x256 conv at batch
+    2): the forward / input-gradient GEMMs split K over the grid and the ordered reduce launch applies bias,
+    ReLU and the BN column statistics — vs float64, and the split is really taken."""
+    from tensorflow_distributed_example_amd.ops import layer_ops as O
+    from tensorflow_distributed_example_amd.ops import layer_ops32 as O32
+    B, fin, out = 64, 10816, 128
+    assert O32.fd_splits(B, out, fin) > 1
+    x, w, b = _r(B, fin, seed=11), _r(fin, out, seed=12, scale=0.02), _r(out, seed=13)
+    part = torch.empty(max(O32.fd_part_elems(B, out, fin), O32.fd_part_elems(B, fin, out)) + 1, device=DEV)
+    y = torch.zeros(B, out, device=DEV)
+    stats = torch.zeros(2 * SLOTS * out, dtype=torch.float64, device=DEV)
+    O32.dense_fwd(x, w, B, y, bias=b, relu=True, colstats=stats, part=part)
+    dy = _r(B, out, seed=14)
+    dx = torch.full((B, fin), 0.25, device=DEV)
+    O32.dense_dgrad(dy, w, dx, B, accum=True, part=part)
+    torch.cuda.synchronize()
+    X, Wt = _c64(x), _c64(w)
+    ref = F.relu(X @ Wt + _c64(b))
+    assert _rel(y, ref) < 1e-6
+    st = _c64(stats).view(SLOTS, 2, out).sum(0)
+    yr = _c64(y)
+    assert _rel(st[0], yr.sum(0)) < 1e-9 and _rel(st[1], (yr * yr).sum(0)) < 1e-9
+    assert _rel(dx, _c64(dy) @ Wt.t() + 0.25) < 1e-6
+    # conv forward / input gradient (stride 1) at few tiles
+    g = O.ConvGeom(2, 7, 7, 256, 7, 7, 64, 3, 3, 1, 1, 1, 1)
+    assert O32.fd_splits(g.B * g.Ho * g.Wo, g.Co, g.K) > 1 and O32.fd_splits(g.B * g.H * g.W, g.C, 9 * g.Co) > 1
+    xc, wc = _r(2, 7, 7, 256, seed=15), _r(3, 3, 256, 64, seed=16, scale=0.05)
+    part = torch.empty(max(O32.fd_part_elems(98, 64, g.K), O32.fd_part_elems(98, 256, 9 * 64)) + 1, device=DEV)
+    yc = torch.zeros(2, 7, 7, 64, device=DEV)
+    O32.conv_fwd(xc, wc, yc, g, part=part)
+    dyc = _r(2, 7, 7, 64, seed=17)
+    dxc = torch.zeros(2, 7, 7, 256, device=DEV)
+    O32.conv_dgrad(dyc, wc, dxc, g, part=part)
+    torch.cuda.synchronize()
+    xr = _c64(xc).requires_grad_(True)
+    o = F.conv2d(xr.permute(0, 3, 1, 2), _c64(wc).permute(3, 2, 0, 1), padding=1)
+    assert _rel(yc, o.permute(0, 2, 3, 1)) < 1e-6
+    o.permute(0, 2, 3, 1).backward(_c64(dyc))
+    assert _rel(dxc, xr.grad) < 1e-6
 
 
 @pytest.mark.parametrize("B,fin,out", [(128, 1176, 200), (37, 64, 10), (256, 512, 1000), (5, 3, 7)])
@@ -258,7 +302,12 @@ def test_model_a_wide_f32_layerwise_matches_float64():
     m.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True), optimizer=tde.optimizers.SGD(0.001))
     m.build()
     rng = np.random.default_rng(0)
-    _f32_oracle_compare(m, rng.random((64, 28, 28, 1), dtype=np.float32), rng.integers(0, 10, 64), 64, 1e-5)
+    plan = _f32_oracle_compare(m, rng.random((64, 28, 28, 1), dtype=np.float32), rng.integers(0, 10, 64), 64, 1e-5)
+    # the conv's ReLU / bias backward runs inside the pool's backward; the Dense(128) forward splits K
+    from tensorflow_distributed_example_amd.train import layerwise as LW
+    pools = [st for st in plan.stages if isinstance(st, LW._MaxPool)]
+    assert pools and pools[0].relu_from is not None and pools[0].relu_from.dz is None
+    assert plan.wpart is not None
 
 
 def test_model_b_doubled_f32_layerwise_matches_float64():
