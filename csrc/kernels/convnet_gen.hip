@@ -1,0 +1,584 @@
+// Fused forward and backward of the DWK/TF2M small CNN at ANY of the common widths, float32
+// (distributed_with_keras.py:33-43, tf2_mnist_distributed.py:66-72 with the user's own Conv2D filters /
+// Dense units):
+//   Conv2D(CC, 3x3, VALID, bias, ReLU) · MaxPooling2D(2) · Flatten · Dense(HD[, ReLU]) · Dense(C <= 16) + SCCE
+// for CC in {16, 32, 48, 64} and HD in {32, 64, 96, 128} (templates), exact-f32 MFMA (v_mfma_f32_16x16x4_f32)
+// over f32 LDS tiles and the f32 master weights.  The reference's own Conv2D(32) / Dense(64) keeps its
+// hand-tuned kernels (convnet_f32.hip: fused optimizer, deferred conv update, fused DP push); this family is
+// the general plan's "plain" step: gradients to the flat bucket, the multi-tensor optimizer after it.
+//
+//   forward   one pooled position x 64 images per workgroup (4 waves): conv + bias + ReLU + 2x2 max-pool
+//             for all CC channels (argmax bytes, the transposed pooled tile Pt), then the position's
+//             slice of the Dense(HD) matmul on the MFMA, split-K atomics into hpre replicas
+//   backward  one pooled position per workgroup (16 waves) + one head workgroup: every workgroup
+//             recomputes the head from hpre (softmax-CE, dH = dl . W2^T masked by ReLU) into LDS, then
+//             dP = G . W1p^T and dW1p = P^T . G (complete rows: the position's own), the routing MFMA
+//             through the pool argmax / ReLU mask into the conv gradients; the head workgroup makes
+//             loss / accuracy, dW2, db2, db1.  hpre is double-buffered by step parity as in the
+//             specialised plan (this launch zeroes the other parity).
+#include "tde_common.h"
+
+namespace tde {
+namespace cgen {
+
+constexpr int XRW = 4;             // input rows per pooled position
+constexpr int kGThreads = 1024;    // backward workgroup
+constexpr int W2S = 17;            // row stride of W2 / dlogits tiles in LDS
+
+template <int CC>
+struct ConvW {   // one channel group of 8: the 9 taps and the bias of channels c0..c0+7 (LDS broadcast)
+  float w[9][8], b[8];
+};
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__host__ __device__ constexpr int xr_stride(int W) { return XRW * W + ((2 - (XRW * W) % 64) + 64) % 64; }
+
+struct GFwdArgs {
+  const float* x; const float* wc; const float* bc; const float* W1;
+  float* hpre; int hrep; long long hrep_stride;
+  float* Pt; int ldPt;
+  uint64_t* amax; int lda;
+  int B, H, W;
+};
+
+template <int CC, int HD>
+struct FwdCfg {
+  static constexpr int PSS = CC + 4;              // LDS row stride of the pooled tile [64 images][CC]
+  static constexpr int NT = HD / 16;              // column tiles of the Dense slice
+  static constexpr int NTW = (NT + 3) / 4;        // column tiles per wave
+  static constexpr int KQ = CC / 4;               // k per lane group
+  static constexpr int kXr = 64 * 130 * 4;        // staged input rows (W <= 32)
+  static constexpr int kPs = 64 * PSS * 4;
+  static constexpr int kLds = kXr + kPs + 10 * CC * 4;
+};
+
+template <int CC, int HD>
+__global__ __launch_bounds__(256) void cgen_fwd_kernel(GFwdArgs a) {
+  using F = FwdCfg<CC, HD>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* xr = reinterpret_cast<float*>(smem);
+  float* Ps = reinterpret_cast<float*>(smem + F::kXr);
+  float* wcs = reinterpret_cast<float*>(smem + F::kXr + F::kPs);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  const int W = a.W, Wp = (W - 2) / 2;
+  const int p = blockIdx.x, py = p / Wp, px = p - py * Wp;
+  const int b0 = blockIdx.y * 64, b = b0 + lane;
+  const bool bok = b < a.B;
+
+  // B fragments of this wave's column tiles first (their round trip overlaps the staging below):
+  // W1[p*CC + fq*KQ + s][nt*16 + fr]
+  float wfr[F::NTW][F::KQ];
+#pragma unroll
+  for (int j = 0; j < F::NTW; ++j) {
+    const int nt = wave + 4 * j;
+#pragma unroll
+    for (int s = 0; s < F::KQ; ++s)
+      wfr[j][s] = nt < F::NT ? a.W1[(size_t)(p * CC + fq * F::KQ + s) * HD + nt * 16 + fr] : 0.f;
+  }
+  // the 4 input rows of the position for 64 images (float4 loads, float2 LDS stores: the padded stride is
+  // only 8-byte aligned), the conv weights
+  const int ist = xr_stride(W), n4 = XRW * W / 4;
+  for (int i = tid; i < 64 * n4; i += 256) {
+    const int bl = i / n4, q = i - bl * n4;
+    float4 v{0.f, 0.f, 0.f, 0.f};
+    if (b0 + bl < a.B) v = *reinterpret_cast<const float4*>(a.x + (size_t)(b0 + bl) * a.H * W + (size_t)(2 * py) * W + 4 * q);
+    float2* d = reinterpret_cast<float2*>(xr + bl * ist + 4 * q);
+    d[0] = float2{v.x, v.y};
+    d[1] = float2{v.z, v.w};
+  }
+  for (int i = tid; i < 10 * CC; i += 256) wcs[i] = i < 9 * CC ? a.wc[i] : a.bc[i - 9 * CC];
+  lds_barrier();
+
+  // conv + bias + ReLU + 2x2 max-pool: lane = image, wave = channel groups of 8
+  float patch[16];
+  {
+    const float* xb = xr + lane * ist + 2 * px;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float2 u = *reinterpret_cast<const float2*>(xb + r * W);
+      const float2 v = *reinterpret_cast<const float2*>(xb + r * W + 2);
+      patch[4 * r] = u.x; patch[4 * r + 1] = u.y; patch[4 * r + 2] = v.x; patch[4 * r + 3] = v.y;
+    }
+  }
+  for (int cg = wave; cg < CC / 8; cg += 4) {
+    uint64_t packed = 0;
+    float out[8];
+#pragma unroll
+    for (int cc = 0; cc < 8; ++cc) {
+      const int c = cg * 8 + cc;
+      float best = -3.0e38f;
+      int bi = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int dy = q >> 1, dx = q & 1;
+        float z = wcs[9 * CC + c];
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) z = fmaf(patch[(dy + ky) * 4 + dx + kx], wcs[(ky * 3 + kx) * CC + c], z);
+        if (z > best) { best = z; bi = q; }
+      }
+      out[cc] = bok ? fmaxf(best, 0.f) : 0.f;
+      packed |= (uint64_t)(best > 0.f ? (unsigned)bi : 0xFFu) << (8 * cc);
+    }
+    if (bok) a.amax[((size_t)p * (CC / 8) + cg) * a.lda + b] = packed;
+    if (bok || b < a.ldPt) {
+#pragma unroll
+      for (int cc = 0; cc < 8; ++cc) a.Pt[(size_t)(p * CC + cg * 8 + cc) * a.ldPt + b] = out[cc];
+    }
+    float* dst = Ps + lane * F::PSS + cg * 8;
+    *reinterpret_cast<float4*>(dst) = float4{out[0], out[1], out[2], out[3]};
+    *reinterpret_cast<float4*>(dst + 4) = float4{out[4], out[5], out[6], out[7]};
+  }
+  lds_barrier();
+
+  // hpre[64 x HD] += Ps(64 x CC) . W1p(CC x HD): wave = column tiles nt = wave + 4j, all 4 row tiles;
+  // lane group fq supplies k = fq*KQ .. fq*KQ + KQ-1 (the same k order in A and B)
+  float* const hrow = a.hpre + (size_t)(blockIdx.x % a.hrep) * a.hrep_stride;
+#pragma unroll
+  for (int j = 0; j < F::NTW; ++j) {
+    const int nt = wave + 4 * j;
+    if (nt >= F::NT) break;
+    f32x4 acc[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s4 = 0; s4 < F::KQ; s4 += 4) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const float4 av = *reinterpret_cast<const float4*>(Ps + (mt * 16 + fr) * F::PSS + fq * F::KQ + s4);
+        acc[mt] = mfma4(av.x, wfr[j][s4], acc[mt]);
+        acc[mt] = mfma4(av.y, wfr[j][s4 + 1], acc[mt]);
+        acc[mt] = mfma4(av.z, wfr[j][s4 + 2], acc[mt]);
+        acc[mt] = mfma4(av.w, wfr[j][s4 + 3], acc[mt]);
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = b0 + mt * 16 + fq * 4 + r;
+        if (row < a.B) atomicAdd(hrow + (size_t)row * HD + nt * 16 + fr, acc[mt][r]);
+      }
+  }
+}
+
+struct GBwdArgs {
+  const float* x; const uint64_t* amax; int lda;
+  const float* hpre; float* hzero; int hrep; long long hrep_stride;
+  const float* b1; const float* W2; const float* b2; int C; int pre_relu;
+  const int* labels; float scale; float* metrics;
+  const float* W1; const float* Pt; int ldPt;
+  float* dW1; float* dwc; float* dbc; float* dW2; float* db2; float* db1;
+  long long* iterations;   // the step counter, advanced by the head workgroup (nullable)
+  int B, H, W;
+};
+
+template <int CC, int HD>
+struct BwdCfg {
+  static constexpr int RG = HD + 4;    // row stride of G / h / W1s (floats)
+  static constexpr int RP = 64 + 4;    // row stride of P^T rows
+  static constexpr int DPS = CC + 4;   // row stride of dP
+  static constexpr int T1 = 4 * (CC / 16);              // dP tiles (image tile x channel tile)
+  static constexpr int T2 = (CC / 16) * (HD / 16);      // dW1 tiles (channel tile x unit tile)
+  static constexpr int TW = (T1 + T2 + 15) / 16;        // tiles per wave
+  static constexpr int HQ = HD / 4;                     // k per lane group in the dP MFMA
+  // LDS carve (bytes)
+  static constexpr int kG = 0;
+  static constexpr int kW1 = kG + 64 * RG * 4;
+  static constexpr int kPt = kW1 + CC * RG * 4;
+  static constexpr int kXs = kPt + CC * RP * 4;
+  static constexpr int kAm = kXs + 64 * 16 * 4;
+  static constexpr int kR = kAm + 64 * CC;              // head scratch | dP | conv-gradient reduction
+  static constexpr int kHs = 64 * RG * 4, kPart = 3 * 4 * 64 * 4 * 4, kDl = 64 * W2S * 4;
+  static constexpr int kHead = kHs + kPart + kDl;
+  static constexpr int kRed = 16 * 10 * CC * 4;
+  static constexpr int kRBytes = kHead > kRed ? kHead : kRed;
+  static constexpr int kW2 = kR + kRBytes;
+  static constexpr int kB2 = kW2 + HD * W2S * 4;
+  static constexpr int kLab = kB2 + 16 * 4;
+  static constexpr int kDb1 = kLab + 64 * 4;            // head workgroup: db1 partials [4][HD]
+  static constexpr int kLds = kDb1 + 4 * HD * 4;
+  static_assert(64 * DPS * 4 <= kRBytes, "dP exceeds the head scratch it reuses");
+  static_assert(kLds <= 160 * 1024, "backward LDS exceeds a CU");
+};
+
+template <int CC, int HD>
+__global__ __launch_bounds__(kGThreads) void cgen_bwd_kernel(GBwdArgs a) {
+  using F = BwdCfg<CC, HD>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* Gs = reinterpret_cast<float*>(smem + F::kG);
+  float* W1s = reinterpret_cast<float*>(smem + F::kW1);
+  float* Pts = reinterpret_cast<float*>(smem + F::kPt);
+  float* xs = reinterpret_cast<float*>(smem + F::kXs);
+  uint8_t* am = smem + F::kAm;
+  float* hs = reinterpret_cast<float*>(smem + F::kR);
+  float* part = reinterpret_cast<float*>(smem + F::kR + F::kHs);
+  float* dls = reinterpret_cast<float*>(smem + F::kR + F::kHs + F::kPart);
+  float* dps = hs;                                               // after G: dP reuses the head scratch
+  float* red = reinterpret_cast<float*>(smem + F::kR);           // after the chunk loop
+  float* w2s = reinterpret_cast<float*>(smem + F::kW2);
+  float* b2s = reinterpret_cast<float*>(smem + F::kB2);
+  int* labs = reinterpret_cast<int*>(smem + F::kLab);
+  float* db1p = reinterpret_cast<float*>(smem + F::kDb1);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
+  const int W = a.W, Wp = (W - 2) / 2, P = ((a.H - 2) / 2) * Wp, C = a.C;
+  const bool head_wg = blockIdx.x == gridDim.x - 1;
+
+  // the other parity of hpre zeroed for the next forward's atomics (a slice per workgroup)
+  {
+    const long long n4 = ((long long)(a.hrep - 1) * a.hrep_stride + (long long)a.B * HD) / 4;
+    const long long per = (n4 + gridDim.x - 1) / gridDim.x, beg = blockIdx.x * per, end = min(n4, beg + per);
+    for (long long i = beg + tid; i < end; i += kGThreads) reinterpret_cast<float4*>(a.hzero)[i] = float4{0.f, 0.f, 0.f, 0.f};
+  }
+  // head weights (classes padded to 16)
+  for (int i = tid; i < HD * 16; i += kGThreads) {
+    const int u = i >> 4, c = i & 15;
+    w2s[u * W2S + c] = c < C ? a.W2[u * C + c] : 0.f;
+  }
+  if (tid < 16) b2s[tid] = tid < C ? a.b2[tid] : 0.f;
+
+  const int p = head_wg ? 0 : blockIdx.x, py = p / Wp, px = p - py * Wp;
+  if (!head_wg) {
+    for (int i = tid; i < CC * HD / 4; i += kGThreads) {   // W1 rows of the position [CC][HD]
+      const int r = i / (HD / 4), c4 = (i - r * (HD / 4)) * 4;
+      *reinterpret_cast<float4*>(W1s + r * F::RG + c4) = *reinterpret_cast<const float4*>(a.W1 + (size_t)(p * CC + r) * HD + c4);
+    }
+  }
+
+  f32x4 accw[F::TW];   // dW1 tile accumulators (persist over the image chunks)
+#pragma unroll
+  for (int j = 0; j < F::TW; ++j) accw[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 accr[CC / 16];
+#pragma unroll
+  for (int ct = 0; ct < CC / 16; ++ct) accr[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 gw[(HD / 16 + 15) / 16];   // head workgroup: dW2 tiles (unit tiles wave, wave + 16)
+#pragma unroll
+  for (int j = 0; j < (HD / 16 + 15) / 16; ++j) gw[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float la = 0.f, ca = 0.f, na = 0.f, db2acc = 0.f;
+  if (head_wg && tid < 4 * HD) db1p[tid] = 0.f;
+
+  for (int b0 = 0; b0 < a.B; b0 += 64) {
+    const int nb = min(64, a.B - b0);
+    // ---- h = act(hpre + b1) for the chunk (replicas summed), labels; trunk: P^T rows, patches, argmax
+    for (int i = tid; i < 64 * HD / 4; i += kGThreads) {
+      const int r = i / (HD / 4), c4 = (i - r * (HD / 4)) * 4;
+      float4 h{0.f, 0.f, 0.f, 0.f};
+      if (r < nb) {
+        for (int q = 0; q < a.hrep; ++q) {
+          const float4 v = *reinterpret_cast<const float4*>(a.hpre + (size_t)q * a.hrep_stride + (size_t)(b0 + r) * HD + c4);
+          h.x += v.x; h.y += v.y; h.z += v.z; h.w += v.w;
+        }
+        if (a.b1) {
+          const float4 bb = *reinterpret_cast<const float4*>(a.b1 + c4);
+          h.x += bb.x; h.y += bb.y; h.z += bb.z; h.w += bb.w;
+        }
+        if (a.pre_relu) h = float4{fmaxf(h.x, 0.f), fmaxf(h.y, 0.f), fmaxf(h.z, 0.f), fmaxf(h.w, 0.f)};
+      }
+      *reinterpret_cast<float4*>(hs + r * F::RG + c4) = h;
+    }
+    if (tid < 64) labs[tid] = tid < nb ? a.labels[b0 + tid] : 0;
+    if (!head_wg) {
+      for (int i = tid; i < CC * 16; i += kGThreads) {   // P^T rows of the position: [CC][64 images]
+        const int r = i >> 4, c4 = (i & 15) * 4;
+        float4 v{0.f, 0.f, 0.f, 0.f};
+        const float* src = a.Pt + (size_t)(p * CC + r) * a.ldPt + b0 + c4;
+        if (c4 + 3 < nb) v = *reinterpret_cast<const float4*>(src);
+        else {
+          if (c4 < nb) v.x = src[0];
+          if (c4 + 1 < nb) v.y = src[1];
+          if (c4 + 2 < nb) v.z = src[2];
+        }
+        *reinterpret_cast<float4*>(Pts + r * F::RP + c4) = v;
+      }
+      if (tid < 256) {
+        const int bl = tid >> 2, r = tid & 3;
+        float4 xv{0.f, 0.f, 0.f, 0.f};
+        if (bl < nb) {
+          const float2* row = reinterpret_cast<const float2*>(a.x + (size_t)(b0 + bl) * a.H * W + (2 * py + r) * W + 2 * px);
+          const float2 u = row[0], t = row[1];
+          xv = float4{u.x, u.y, t.x, t.y};
+        }
+        *reinterpret_cast<float4*>(xs + bl * 16 + r * 4) = xv;
+      }
+      for (int i = tid; i < 64 * (CC / 8); i += kGThreads) {
+        const int cg = i >> 6, bb = i & 63;
+        const uint64_t v = bb < nb ? a.amax[((size_t)p * (CC / 8) + cg) * a.lda + b0 + bb] : ~0ull;
+        *reinterpret_cast<uint64_t*>(am + bb * CC + cg * 8) = v;
+      }
+    }
+    lds_barrier();
+
+    // ---- logits = h . W2 + b2: wave = (row tile rt, K quarter kq); softmax-CE on waves 0..3 -> dls
+    {
+      const int rt = wave & 3, kq = wave >> 2;
+      f32x4 lg{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = kq * (HD / 4); k < (kq + 1) * (HD / 4); k += 4)
+        lg = mfma4(hs[(rt * 16 + fr) * F::RG + k + fq], w2s[(k + fq) * W2S + fr], lg);
+      if (kq > 0) *reinterpret_cast<f32x4*>(part + (((kq - 1) * 4 + rt) * 64 + lane) * 4) = lg;
+      lds_barrier();
+      if (wave < 4) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          const f32x4 pv = *reinterpret_cast<const f32x4*>(part + ((q * 4 + rt) * 64 + lane) * 4);
+          lg[0] += pv[0]; lg[1] += pv[1]; lg[2] += pv[2]; lg[3] += pv[3];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = rt * 16 + fq * 4 + i;
+          const bool valid = r < nb, cv = fr < C;
+          const float z = cv ? lg[i] + b2s[fr] : -3.0e38f;
+          const float m = row16_max(z);
+          const float e = cv ? __expf(z - m) : 0.f;
+          const float ssum = row16_sum(e);
+          const int label = labs[r];
+          const int amx = row16_min(cv && z == m ? fr : 64);
+          const float zl = __shfl(z, (lane & ~15) | (label & 15), 64);
+          if (valid && fr == 0) {
+            la += __logf(ssum) + m - zl;
+            ca += (amx == label) ? 1.f : 0.f;
+            na += 1.f;
+          }
+          dls[r * W2S + fr] = (valid && cv) ? (e / ssum - (fr == label ? 1.f : 0.f)) * a.scale : 0.f;
+        }
+      }
+      lds_barrier();
+    }
+    // ---- G = dH = dl . W2^T masked by h > 0 (rows < nb): tiles (row tile, unit tile) over the waves
+    for (int t = wave; t < 4 * (HD / 16); t += 16) {
+      const int rt = t & 3, ut = t >> 2;
+      f32x4 gh{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 16; k += 4) gh = mfma4(dls[(rt * 16 + fr) * W2S + k + fq], w2s[(ut * 16 + fr) * W2S + k + fq], gh);
+      const int j = ut * 16 + fr;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = rt * 16 + fq * 4 + i;
+        if ((a.pre_relu && !(hs[r * F::RG + j] > 0.f)) || r >= nb) gh[i] = 0.f;
+        Gs[r * F::RG + j] = gh[i];
+      }
+    }
+    if (head_wg) {
+      // dW2[u][c] += sum_b h[b][u] dl[b][c]: unit tiles ut = wave, wave + 16
+#pragma unroll
+      for (int j = 0; j < (HD / 16 + 15) / 16; ++j) {
+        const int ut = wave + 16 * j;
+        if (ut < HD / 16) {
+#pragma unroll 4
+          for (int k = 0; k < 64; k += 4) gw[j] = mfma4(hs[(k + fq) * F::RG + ut * 16 + fr], dls[(k + fq) * W2S + fr], gw[j]);
+        }
+      }
+      if (tid < 16) {
+        float s = 0.f;
+        for (int r = 0; r < nb; ++r) s += dls[r * W2S + tid];
+        db2acc += s;
+      }
+      lds_barrier();
+      if (tid < 4 * HD) {   // db1 += sum_b G[b][u]: 4 row groups of 16 images per unit
+        const int u = tid % HD, rg = tid / HD;
+        float s = 0.f;
+        for (int r = rg * 16; r < rg * 16 + 16; ++r) s += Gs[r * F::RG + u];
+        db1p[tid] += s;
+      }
+      lds_barrier();
+      continue;
+    }
+    lds_barrier();
+
+    // ---- tiles over the waves: dP[b][c] = sum_u G[b][u] W1p[c][u] (t < T1), dW1p[c][u] += sum_b P[b][c]
+    //      G[b][u] (T1 <= t < T1 + T2; accumulators persist over the chunks)
+#pragma unroll
+    for (int j = 0; j < F::TW; ++j) {
+      const int t = wave + 16 * j;
+      if (t < F::T1) {
+        const int mt = t & 3, ct = t >> 2;
+        f32x4 acc{0.f, 0.f, 0.f, 0.f};
+        const float* Ab = Gs + (mt * 16 + fr) * F::RG + fq * F::HQ;
+        const float* Bb = W1s + (ct * 16 + fr) * F::RG + fq * F::HQ;
+#pragma unroll
+        for (int s = 0; s < F::HQ; s += 4) {
+          const float4 av = *reinterpret_cast<const float4*>(Ab + s);
+          const float4 bv = *reinterpret_cast<const float4*>(Bb + s);
+          acc = mfma4(av.x, bv.x, acc);
+          acc = mfma4(av.y, bv.y, acc);
+          acc = mfma4(av.z, bv.z, acc);
+          acc = mfma4(av.w, bv.w, acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dps[(mt * 16 + fq * 4 + r) * F::DPS + ct * 16 + fr] = acc[r];
+      } else if (t < F::T1 + F::T2) {
+        const int u2 = t - F::T1, rt = u2 % (CC / 16), nt = u2 / (CC / 16);
+        // A[row c][k b] = P^T[c][b]; B[k b][col u] = G[b][u]; lane group fq takes images fq*16 .. +15
+        const float* Ab = Pts + (rt * 16 + fr) * F::RP + fq * 16;
+#pragma unroll
+        for (int s = 0; s < 16; s += 4) {
+          const float4 av = *reinterpret_cast<const float4*>(Ab + s);
+          const float* Bb = Gs + (fq * 16 + s) * F::RG + nt * 16 + fr;
+          accw[j] = mfma4(av.x, Bb[0], accw[j]);
+          accw[j] = mfma4(av.y, Bb[F::RG], accw[j]);
+          accw[j] = mfma4(av.z, Bb[2 * F::RG], accw[j]);
+          accw[j] = mfma4(av.w, Bb[3 * F::RG], accw[j]);
+        }
+      }
+    }
+    lds_barrier();
+
+    // ---- routing MFMA: dWc[tap][c] += sum over (image, window slot) of X[tap] . dP masked by the argmax;
+    //      k = (b, q): lane group fq = window slot q; wave takes images 4w .. 4w+3
+    {
+      const int tap = fr, ky = tap / 3, kx = tap - ky * 3, qy = fq >> 1, qx = fq & 1;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int bl = wave * 4 + s;
+        const float xa = tap < 9 ? xs[bl * 16 + (qy + ky) * 4 + qx + kx] : (tap == 9 ? 1.f : 0.f);
+#pragma unroll
+        for (int ct = 0; ct < CC / 16; ++ct) {
+          const int c = ct * 16 + fr;
+          const float d = am[bl * CC + c] == (unsigned)fq ? dps[bl * F::DPS + c] : 0.f;
+          accr[ct] = mfma4(xa, d, accr[ct]);
+        }
+      }
+    }
+    lds_barrier();
+  }
+
+  if (head_wg) {
+    la = rows4_sum(la);
+    ca = rows4_sum(ca);
+    na = rows4_sum(na);
+    if (wave < 4 && lane == 0 && a.metrics && na > 0.f) {
+      atomicAdd(a.metrics + 0, la);
+      atomicAdd(a.metrics + 1, ca);
+      atomicAdd(a.metrics + 2, na);
+    }
+#pragma unroll
+    for (int j = 0; j < (HD / 16 + 15) / 16; ++j) {
+      const int ut = wave + 16 * j;
+      if (ut < HD / 16 && fr < C && a.dW2)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a.dW2[(size_t)(ut * 16 + fq * 4 + i) * C + fr] += gw[j][i];
+    }
+    if (tid < C && a.db2) a.db2[tid] += db2acc;
+    if (tid < HD && a.db1) a.db1[tid] += (db1p[tid] + db1p[HD + tid]) + (db1p[2 * HD + tid] + db1p[3 * HD + tid]);
+    if (tid == 0 && a.iterations) a.iterations[0] += 1;
+    return;
+  }
+
+  // dW1 rows of the position (complete: this workgroup owns them)
+#pragma unroll
+  for (int j = 0; j < F::TW; ++j) {
+    const int t = wave + 16 * j;
+    if (t >= F::T1 && t < F::T1 + F::T2) {
+      const int u2 = t - F::T1, rt = u2 % (CC / 16), nt = u2 / (CC / 16);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a.dW1[(size_t)(p * CC + rt * 16 + fq * 4 + r) * HD + nt * 16 + fr] = accw[j][r];
+    }
+  }
+  // conv gradients: the 16 waves' routing accumulators summed through LDS, one add per value
+#pragma unroll
+  for (int ct = 0; ct < CC / 16; ++ct)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int tap = fq * 4 + r;
+      if (tap < 10) red[((size_t)wave * 10 + tap) * CC + ct * 16 + fr] = accr[ct][r];
+    }
+  lds_barrier();
+  for (int i = tid; i < 10 * CC; i += kGThreads) {
+    const int tap = i / CC, c = i - tap * CC;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) s += red[((size_t)w * 10 + tap) * CC + c];
+    if (tap < 9) atomicAdd(a.dwc + tap * CC + c, s);
+    else atomicAdd(a.dbc + c, s);
+  }
+}
+
+template <int CC, int HD>
+static int launch_fwd(const GFwdArgs& a, int P, hipStream_t s) {
+  using F = FwdCfg<CC, HD>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)cgen_fwd_kernel<CC, HD>, hipFuncAttributeMaxDynamicSharedMemorySize, F::kLds);
+    attr = true;
+  }
+  int by = (a.B + 63) / 64;
+  const int byp = (a.ldPt + 63) / 64;
+  if (byp > by) by = byp;
+  cgen_fwd_kernel<CC, HD><<<dim3(P, by), 256, F::kLds, s>>>(a);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+template <int CC, int HD>
+static int launch_bwd(const GBwdArgs& a, int P, hipStream_t s) {
+  using F = BwdCfg<CC, HD>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)cgen_bwd_kernel<CC, HD>, hipFuncAttributeMaxDynamicSharedMemorySize, F::kLds);
+    attr = true;
+  }
+  cgen_bwd_kernel<CC, HD><<<P + 1, kGThreads, F::kLds, s>>>(a);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+#define TDE_CGEN_DISPATCH(FN, CCV, HDV, ...)                                              \
+  switch (CCV * 1000 + HDV) {                                                              \
+    case 16032: return FN<16, 32>(__VA_ARGS__);  case 16064: return FN<16, 64>(__VA_ARGS__); \
+    case 16096: return FN<16, 96>(__VA_ARGS__);  case 16128: return FN<16, 128>(__VA_ARGS__); \
+    case 32032: return FN<32, 32>(__VA_ARGS__);  case 32064: return FN<32, 64>(__VA_ARGS__); \
+    case 32096: return FN<32, 96>(__VA_ARGS__);  case 32128: return FN<32, 128>(__VA_ARGS__); \
+    case 48032: return FN<48, 32>(__VA_ARGS__);  case 48064: return FN<48, 64>(__VA_ARGS__); \
+    case 48096: return FN<48, 96>(__VA_ARGS__);  case 48128: return FN<48, 128>(__VA_ARGS__); \
+    case 64032: return FN<64, 32>(__VA_ARGS__);  case 64064: return FN<64, 64>(__VA_ARGS__); \
+    case 64096: return FN<64, 96>(__VA_ARGS__);  case 64128: return FN<64, 128>(__VA_ARGS__); \
+    default: return -9;                                                                     \
+  }
+
+}  // namespace cgen
+}  // namespace tde
+
+using namespace tde;
+using namespace tde::cgen;
+
+TDE_API int tde_cgen_supported(int CC, int HD) {
+  return (CC == 16 || CC == 32 || CC == 48 || CC == 64) && (HD == 32 || HD == 64 || HD == 96 || HD == 128);
+}
+
+// Forward (see the header).  x [B][H][W] f32 (C_in = 1), wc [9][CC], bc [CC], W1 [P*CC][HD] f32 master,
+// hpre [hrep][>=B][HD] (+=), Pt [P*CC][ldPt], amax [P][CC/8][lda] (8 argmax bytes per u64).
+TDE_API int tde_cgen_fwd(int CC, int HD, const float* x, const float* wc, const float* bc, const float* W1,
+                         float* hpre, int hrep, long long hrep_stride, float* Pt, int ldPt, void* amax, int lda, int B,
+                         int H, int W, hipStream_t stream) {
+  if (!tde_cgen_supported(CC, HD) || (W & 3) || W > 32 || H < 4 || W < 4 || ((H - 2) & 1) || ((W - 2) & 1))
+    return -1;
+  if (!x || !wc || !bc || !W1 || !hpre || !Pt || !amax || (ldPt & 7) || ldPt < B || lda < B || hrep < 1 ||
+      (hrep > 1 && hrep_stride < (long long)B * HD) || ((uintptr_t)x & 15) || ((uintptr_t)W1 & 15))
+    return -2;
+  const int P = ((H - 2) / 2) * ((W - 2) / 2);
+  GFwdArgs a{x, wc, bc, W1, hpre, hrep, hrep_stride, Pt, ldPt, (uint64_t*)amax, lda, B, H, W};
+  TDE_CGEN_DISPATCH(launch_fwd, CC, HD, a, P, stream)
+}
+
+// Backward (plain step: gradients out).  hpre / hzero [hrep][>=B][HD] (hzero zeroed here), dW1 [P*CC][HD]
+// stored, dwc [9][CC] / dbc [CC] atomically added, dW2 [HD][C] / db2 [C] / db1 [HD] added (nullable);
+// iterations (nullable) advanced by one.
+TDE_API int tde_cgen_bwd(int CC, int HD, const float* x, const void* amax, int lda, const float* hpre, float* hzero,
+                         int hrep, long long hrep_stride, const float* b1, const float* W2, const float* b2, int C,
+                         int pre_relu, const int* labels, float scale, float* metrics, const float* W1, const float* Pt,
+                         int ldPt, float* dW1, float* dwc, float* dbc, float* dW2, float* db2, float* db1,
+                         long long* iterations, int B, int H, int W, hipStream_t stream) {
+  if (!tde_cgen_supported(CC, HD) || C < 1 || C > 16 || W > 32 || (W & 3)) return -1;
+  if (!x || !amax || !hpre || !hzero || !W2 || !b2 || !labels || !W1 || !Pt || !dW1 || !dwc || !dbc ||
+      (ldPt & 7) || ldPt < B || lda < B || hrep < 1 || (hrep > 1 && (hrep_stride < (long long)B * HD || (hrep_stride & 3))) ||
+      (((uintptr_t)hpre | (uintptr_t)hzero | (uintptr_t)W1 | (uintptr_t)Pt | (uintptr_t)b1) & 15))
+    return -2;
+  const int P = ((H - 2) / 2) * ((W - 2) / 2);
+  GBwdArgs a{x, (const uint64_t*)amax, lda, hpre, hzero, hrep, hrep_stride, b1, W2, b2, C, pre_relu, labels, scale,
+             metrics, W1, Pt, ldPt, dW1, dwc, dbc, dW2, db2, db1, iterations, B, H, W};
+  TDE_CGEN_DISPATCH(launch_bwd, CC, HD, a, P, stream)
+}

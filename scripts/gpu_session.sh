@@ -44,9 +44,9 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 400 --warmup 64
 fi
-# topic sessions of this round (scripts/sessions/<name>.sh): equiv | buckets | ps | f32 | widths
+# topic sessions of this round (scripts/sessions/<name>.sh): equiv | buckets | ps | f32 | widths | cgen
 case "$MODE" in
   equiv) bash scripts/equiv_repeat.sh "${@:2}" || exit $? ;;
-  buckets|ps|f32|widths) bash "scripts/sessions/$MODE.sh" || exit $? ;;
+  buckets|ps|f32|widths|cgen) bash "scripts/sessions/$MODE.sh" || exit $? ;;
 esac
 echo "=== done"

@@ -276,6 +276,57 @@ def convnet_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, me
     N.check(rc, "tde_convnet_bwd_f32" if f32 else "tde_convnet_bwd")
 
 
+def cgen_supported(filters, units):
+    return bool(N.hip().tde_cgen_supported(int(filters), int(units)))
+
+
+def cgen_fwd(x, wc, bc, W1, hpre, Pt, amax, *, B):
+    """Generic-width fused small-CNN forward, float32 (csrc/kernels/convnet_gen.hip): Conv2D(CC, 3x3) + ReLU +
+    MaxPool(2) + the Dense(HD) matmul, hpre [R, >=B, HD] += (workgroup i adds into replica i % R).
+    W1 the f32 master kernel [P*CC, HD]; Pt [P*CC, ldPt] f32; amax int64 [P, CC/8, lda]."""
+    H, W = x.shape[1], x.shape[2]
+    CC = wc.shape[-1]
+    Pn = ((H - 2) // 2) * ((W - 2) // 2)
+    HD = W1.shape[1]
+    _req(x.dtype == torch.float32 and x.is_contiguous() and x.shape[3] == 1 and x.shape[0] >= B, "cgen_fwd: input")
+    _req(wc.numel() == 9 * CC and bc.numel() == CC and W1.dtype == torch.float32 and W1.is_contiguous()
+         and tuple(W1.shape) == (Pn * CC, HD), "cgen_fwd: weights")
+    hp = hpre if hpre.dim() == 3 else hpre.unsqueeze(0)
+    _req(hpre.is_contiguous() and hp.shape[1] >= B and hp.shape[2] == HD, "cgen_fwd: hpre")
+    _req(Pt.dtype == torch.float32 and Pt.shape[0] == Pn * CC and Pt.stride(0) >= B and Pt.stride(1) == 1,
+         "cgen_fwd: Pt")
+    _req(amax.dtype == torch.int64 and amax.shape[:2] == (Pn, CC // 8) and amax.shape[-1] >= B, "cgen_fwd: amax")
+    rc = N.hip().tde_cgen_fwd(CC, HD, _P(x), _P(wc), _P(bc), _P(W1), _P(hpre), hp.shape[0], hp.stride(0), _P(Pt),
+                              Pt.stride(0), _P(amax), amax.shape[-1], B, H, W, _s())
+    N.check(rc, "tde_cgen_fwd")
+
+
+def cgen_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, metrics, W1, Pt, dW1, dwc, dbc,
+             dW2=None, db2=None, db1=None, B, iterations=None):
+    """Generic-width fused small-CNN backward, float32 (plain step): from hpre [R, >=B, HD] every workgroup
+    recomputes the head, then the Dense(HD) weight / input gradients and the conv gradients; hzero (the
+    other parity) is zeroed.  dW1 stored, dwc / dbc atomically added, dW2 / db2 / db1 added, metrics added,
+    ``iterations`` (int64 step counter) advanced."""
+    H, W = x.shape[1], x.shape[2]
+    CC = dwc.shape[-1]
+    Pn = ((H - 2) // 2) * ((W - 2) // 2)
+    HD, C = W2.shape
+    hp = hpre if hpre.dim() == 3 else hpre.unsqueeze(0)
+    _req(hpre.is_contiguous() and hzero.shape == hpre.shape and hzero.is_contiguous() and hp.shape[2] == HD
+         and hp.shape[1] >= B, "cgen_bwd: hpre / hzero")
+    _req(tuple(W1.shape) == (Pn * CC, HD) and W1.is_contiguous() and dW1.shape == W1.shape and dbc.numel() == CC,
+         "cgen_bwd: shapes")
+    _req(Pt.shape[0] == Pn * CC and Pt.dtype == torch.float32 and Pt.stride(0) >= B, "cgen_bwd: Pt")
+    _req(amax.dtype == torch.int64 and amax.shape[:2] == (Pn, CC // 8) and amax.shape[-1] >= B, "cgen_bwd: amax")
+    _req(labels.dtype == torch.int32 and labels.numel() >= B and C <= 16, "cgen_bwd: labels / classes")
+    _req(W2.is_contiguous() and b2.numel() == C and (b1 is None or b1.numel() == HD), "cgen_bwd: head variables")
+    rc = N.hip().tde_cgen_bwd(CC, HD, _P(x), _P(amax), amax.shape[-1], _P(hpre), _P(hzero), hp.shape[0],
+                              hp.stride(0), _P(b1), _P(W2), _P(b2), C, int(pre_relu), _P(labels), float(scale),
+                              _P(metrics), _P(W1), _P(Pt), Pt.stride(0), _P(dW1), _P(dwc), _P(dbc), _P(dW2),
+                              _P(db2), _P(db1), _P(iterations), B, H, W, _s())
+    N.check(rc, "tde_cgen_bwd")
+
+
 def convnet_cgrad_reduce(cpart, nwg, dwc, dbc):
     """Deterministic mode: dwc / dbc += the backward's per-workgroup conv-gradient partials, in order."""
     _req(cpart.dtype == torch.float32 and cpart.numel() >= nwg * 320, "convnet_cgrad_reduce: cpart")

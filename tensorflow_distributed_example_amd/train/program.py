@@ -300,7 +300,7 @@ def match_convnet(model, loss):
         return None
     c, p, f, d1, d2 = ls
     ok = (isinstance(c, L.Conv2D) and c.kernel_size == (3, 3) and c.strides == (1, 1) and c.padding == "valid"
-          and c.activation == "relu" and c.use_bias and c.input_shape[-1] == 1 and c.filters % 16 == 0
+          and c.activation == "relu" and c.use_bias and c.input_shape[-1] == 1
           and c.input_shape[1] % 2 == 0
           and isinstance(p, L.MaxPooling2D) and p.pool_size == (2, 2) and p.strides == (2, 2) and p.padding == "valid"
           and isinstance(f, L.Flatten)
@@ -313,13 +313,28 @@ def match_convnet(model, loss):
     if d2.units > 64 or d1.units * d2.units > 16384 or d1.units % 32 or d1.units > 256:
         return None
     if c.filters != 32 or d1.units != 64:
-        # the fused step is specialised for the reference's Conv2D(32)/Dense(64) (distributed_with_keras.py
-        # :34,37): say so instead of silently dropping a near-miss to the slower per-layer plan
+        # the hand-tuned step is the reference's Conv2D(32)/Dense(64) (distributed_with_keras.py:34,37);
+        # other widths run the generic fused kernels (float32 policy, ConvNetGenPlan) when they fit them,
+        # and say so instead of silently dropping to the slower per-layer plan otherwise
+        H, W = c.input_shape[0], c.input_shape[1]
+        why = None
+        if Kb.global_policy().compute_dtype != torch.float32:
+            why = "the generic widths are implemented for the float32 policy"
+        elif c.filters not in GEN_FILTERS or d1.units not in GEN_UNITS:
+            why = f"Conv2D filters must be one of {GEN_FILTERS} and Dense units one of {GEN_UNITS}"
+        elif d2.units > 16 or W % 4 or W > 32 or H % 2:
+            why = "at most 16 classes and an even height, width a multiple of 4 up to 32"
+        if why is None:
+            return dict(conv=c, pool=p, dense1=d1, dense2=d2, generic=True)
         import warnings
-        warnings.warn(f"model {model.name!r}: the fused small-CNN step supports Conv2D(32) + Dense(64) only "
-                      f"(got Conv2D({c.filters}) + Dense({d1.units})); running the per-layer kernel plan")
+        warnings.warn(f"model {model.name!r}: no fused small-CNN step for Conv2D({c.filters}) + Dense({d1.units}) "
+                      f"({why}); running the per-layer kernel plan")
         return None
     return dict(conv=c, pool=p, dense1=d1, dense2=d2)
+
+
+GEN_FILTERS = (16, 32, 48, 64)      # csrc/kernels/convnet_gen.hip instantiations
+GEN_UNITS = (32, 64, 96, 128)
 
 
 class ConvNetPlan(ReplicaPlan):
@@ -668,6 +683,93 @@ class ConvNetPlan(ReplicaPlan):
         return self._zl
 
 
+class ConvNetGenPlan(ReplicaPlan):
+    """The DWK/TF2M small CNN at the user's own widths — Conv2D(F in 16/32/48/64) · MaxPool(2) · Flatten ·
+    Dense(U in 32/64/96/128) · Dense(<= 16) (distributed_with_keras.py:33-43 and tf2_mnist_distributed.py:66-72
+    with other filter / unit counts) — as two fused float32 HIP launches per step (csrc/kernels/convnet_gen.hip):
+
+      forward   conv+bias+ReLU+pool fused with the Dense(U) matmul (split-K atomics into hpre replicas)
+      backward  every workgroup recomputes the head from hpre, then the Dense(U) weight / input gradients
+                of its pooled position, the pool / ReLU routing MFMA and the conv gradients; one extra
+                workgroup makes the head's own gradients, the metrics and the step count
+
+    followed by the multi-tensor optimizer (step mode "plain"; the data-parallel strategies all-reduce the
+    flat bucket between the two as for any plan).  The reference's own Conv2D(32)/Dense(64) keeps the
+    hand-tuned ``ConvNetPlan`` (fused optimizer, deferred conv update, fused exchange)."""
+    kind = "fused_convnet_generic"
+
+    def __init__(self, model, store, device, batch, global_batch, optimizer, loss, pattern):
+        super().__init__(model, store, device, batch, global_batch, optimizer)
+        from ..ops import kernels as K
+        self.K = K
+        c, d1, d2 = pattern["conv"], pattern["dense1"], pattern["dense2"]
+        if not K.cgen_supported(c.filters, d1.units):
+            raise NotImplementedError(f"convnet_gen: Conv2D({c.filters}) + Dense({d1.units}) not instantiated")
+        self.H, self.W, self.C = c.input_shape[0], c.input_shape[1], c.filters
+        self.P = ((self.H - 2) // 2) * ((self.W - 2) // 2)
+        self.Hd, self.Cls = d1.units, d2.units
+        B, Bp, dev = self.B, _round8(self.B), self.device
+        self.Pt = torch.zeros(self.P * self.C, Bp, dtype=torch.float32, device=dev)
+        self.amax = torch.zeros(self.P, self.C // 8, Bp, dtype=torch.int64, device=dev)
+        # split-K targets of the forward's ~P adders per address, summed by the consumers (TDE_CONVNET_HREP)
+        self.hrep = max(1, min(8, int(os.environ.get("TDE_CONVNET_HREP", "4"))))
+        self.hpre2 = torch.zeros(2, self.hrep, B, self.Hd, dtype=torch.float32, device=dev)
+        self.hpre = torch.zeros(B, self.Hd, dtype=torch.float32, device=dev)
+        self.probs = torch.zeros(B, self.Cls, dtype=torch.float32, device=dev)
+        self.pre_relu = d1.activation == "relu"
+        self.logits_out = d2.activation is None
+        n = lambda l, w: f"{l.name}/{w}"  # noqa: E731
+        self.names = dict(wc=n(c, "kernel"), bc=n(c, "bias"), w1=n(d1, "kernel"),
+                          b1=n(d1, "bias") if d1.use_bias else None, w2=n(d2, "kernel"), b2=n(d2, "bias"))
+        self.W1 = store.view(self.names["w1"])
+        self.opt = OptimizerKernel(store, optimizer, {}, self.iterations) if optimizer is not None else None
+        self.parity = 0
+
+    def _v(self, key):
+        nm = self.names[key]
+        return None if nm is None else self.store.view(nm)
+
+    def _g(self, key):
+        nm = self.names[key]
+        return None if nm is None else self.store.grad(nm)
+
+    def on_weights_loaded(self):
+        self.store.g.zero_()
+
+    def train_step(self, x, y, B=None):
+        K = self.K
+        B = self.B if B is None else B
+        q = self.parity
+        K.cgen_fwd(x, self._v("wc"), self._v("bc"), self.W1, self.hpre2[q], self.Pt, self.amax, B=B)
+        K.cgen_bwd(x, self.amax, self.hpre2[q], self.hpre2[1 - q], self._v("b1"), self._v("w2"), self._v("b2"), y,
+                   scale=self.scale, pre_relu=self.pre_relu, metrics=self.metrics, W1=self.W1, Pt=self.Pt,
+                   dW1=self._g("w1"), dwc=self._g("wc"), dbc=self._g("bc"), dW2=self._g("w2"), db2=self._g("b2"),
+                   db1=self._g("b1"), B=B, iterations=self.iterations)
+        self.parity = 1 - q
+
+    def apply(self):
+        self.opt.apply()
+
+    def _forward(self, x, B):
+        self.K.cgen_fwd(x, self._v("wc"), self._v("bc"), self.W1, self.hpre, self.Pt, self.amax, B=B)
+
+    def eval_step(self, x, y, B=None):
+        B = self.B if B is None else B
+        self._forward(x, B)
+        self.K.head_xent(self.hpre, self._v("w2"), self._v("b2"), y, B=B, scale=self.scale, pre_bias=self._v("b1"),
+                         pre_relu=self.pre_relu, compute_grad=False, metrics=self.metrics, zero_hin=True)
+
+    def predict(self, x, B=None):
+        B = self.B if B is None else B
+        self._forward(x, B)
+        if not hasattr(self, "_zl"):
+            self._zl = torch.zeros(self.B, dtype=torch.int32, device=self.device)
+        self.K.head_xent(self.hpre, self._v("w2"), self._v("b2"), self._zl, B=B, scale=1.0,
+                         pre_bias=self._v("b1"), pre_relu=self.pre_relu, compute_grad=False, probs=self.probs,
+                         probs_are_logits=self.logits_out, zero_hin=True)
+        return self.probs[:B]
+
+
 # ---------------------------------------------------------------------------------------
 def make_plan(model, store, device, batch, global_batch, optimizer, loss, prefer=None):
     device = torch.device(device)
@@ -675,7 +777,8 @@ def make_plan(model, store, device, batch, global_batch, optimizer, loss, prefer
     if device.type == "cuda" and prefer != "reference":
         pat = match_convnet(model, loss)
         if pat is not None and prefer in (None, "fused"):
-            return ConvNetPlan(model, store, device, batch, global_batch, optimizer, loss, pat)
+            cls = ConvNetGenPlan if pat.get("generic") else ConvNetPlan
+            return cls(model, store, device, batch, global_batch, optimizer, loss, pat)
         if prefer in (None, "fused", "bncnn"):
             from . import bncnn
             plan = bncnn.try_make(model, store, device, batch, global_batch, optimizer, loss)

@@ -1,0 +1,48 @@
+"""Which fused small-CNN step a DWK/TF2M-shaped model gets (train/program.py ``match_convnet``): the
+hand-tuned Conv2D(32)/Dense(64) plan, the generic-width float32 plan, or a warning naming why neither fits
+and the per-layer plan.  Pattern matching only: runs on the CPU."""
+import warnings
+
+import pytest
+
+
+def _match(filters, units, policy, H=28, W=28, classes=10):
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.models import layers as L
+    from tensorflow_distributed_example_amd.train import program as PG
+    tde.backend.set_global_policy(policy)
+    try:
+        m = tde.models.Sequential([
+            L.Conv2D(filters, 3, activation="relu", input_shape=(H, W, 1)), L.MaxPooling2D(), L.Flatten(),
+            L.Dense(units, activation="relu"), L.Dense(classes)])
+        loss = tde.losses.SparseCategoricalCrossentropy(from_logits=True)
+        with warnings.catch_warnings(record=True) as rec:
+            warnings.simplefilter("always")
+            pat = PG.match_convnet(m, loss)
+        return pat, [str(w.message) for w in rec]
+    finally:
+        tde.backend.set_global_policy(None)
+
+
+def test_reference_width_takes_the_hand_tuned_plan():
+    for policy in ("float32", "mixed_bfloat16"):
+        pat, warns = _match(32, 64, policy)
+        assert pat is not None and not pat.get("generic") and not warns
+
+
+@pytest.mark.parametrize("filters,units", [(64, 128), (16, 32), (48, 96), (32, 128), (64, 32)])
+def test_generic_widths_take_the_generic_plan(filters, units):
+    pat, warns = _match(filters, units, "float32")
+    assert pat is not None and pat["generic"] and not warns
+
+
+@pytest.mark.parametrize("filters,units,policy,H,W,classes,why", [
+    (64, 128, "mixed_bfloat16", 28, 28, 10, "float32 policy"),
+    (24, 64, "float32", 28, 28, 10, "filters must be one of"),
+    (32, 256, "float32", 28, 28, 10, "units one of"),
+    (64, 128, "float32", 28, 36, 10, "width a multiple of 4 up to 32"),
+    (64, 128, "float32", 28, 28, 20, "at most 16 classes"),
+])
+def test_unfused_widths_warn_with_the_reason(filters, units, policy, H, W, classes, why):
+    pat, warns = _match(filters, units, policy, H, W, classes)
+    assert pat is None and len(warns) == 1 and why in warns[0] and "per-layer kernel plan" in warns[0], warns
