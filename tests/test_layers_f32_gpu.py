@@ -292,8 +292,8 @@ def _f32_oracle_compare(model, x, y, B, tol):
 
 
 def test_model_a_wide_f32_layerwise_matches_float64():
-    """Model A (distributed_with_keras.py:33-39) at Conv2D(64) / Dense(128): outside the fused CNN plan's
-    Conv2D(32)/Dense(64) pattern, so it runs on the float32 layer-wise plan."""
+    """Model A (distributed_with_keras.py:33-39) at Conv2D(64) / Dense(128) on the float32 layer-wise plan
+    (chosen explicitly: by default this width runs the generic fused plan, tests/test_convnet_gen_gpu.py)."""
     import tensorflow_distributed_example_amd as tde
     L = tde.keras.layers
     tde.backend.set_random_seed(0)
@@ -349,6 +349,7 @@ def test_f32_layerwise_fit_trains_in_graph(monkeypatch):
     in fp32 (no bf16 shadow exists)."""
     import tensorflow_distributed_example_amd as tde
     monkeypatch.setenv("TDE_SMALLNET", "0")
+    monkeypatch.setenv("TDE_EXECUTOR", "layerwise")   # this width's default is the generic fused plan
     L = tde.keras.layers
     tde.backend.set_random_seed(4)
     m = tde.Sequential([L.Conv2D(64, 3, activation="relu", input_shape=(28, 28, 1)), L.MaxPooling2D(),
