@@ -16,13 +16,13 @@
 //             through the pool argmax / ReLU mask into the conv gradients; the head workgroup makes
 //             loss / accuracy, dW2, db2, db1.  hpre is double-buffered by step parity as in the
 //             specialised plan (this launch zeroes the other parity).
-#include "tde_common.h"
+#include "tde_optim.h"
 
 namespace tde {
 namespace cgen {
 
 constexpr int XRW = 4;             // input rows per pooled position
-constexpr int kGThreads = 1024;    // backward workgroup
+constexpr int kMaxBwdThreads = 1024;   // backward workgroup: NW waves (16, or 8 for the register-heavy widths)
 constexpr int W2S = 17;            // row stride of W2 / dlogits tiles in LDS
 
 template <int CC>
@@ -41,6 +41,7 @@ struct GFwdArgs {
   float* hpre; int hrep; long long hrep_stride;
   float* Pt; int ldPt;
   uint64_t* amax; int lda;
+  long long* inc_iter;   // step counter advanced by block (0, 0) (nullable; the fused step's, read by the backward)
   int B, H, W;
 };
 
@@ -137,6 +138,7 @@ __global__ __launch_bounds__(256) void cgen_fwd_kernel(GFwdArgs a) {
 
   // hpre[64 x HD] += Ps(64 x CC) . W1p(CC x HD): wave = column tiles nt = wave + 4j, all 4 row tiles;
   // lane group fq supplies k = fq*KQ .. fq*KQ + KQ-1 (the same k order in A and B)
+  if (a.inc_iter && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) a.inc_iter[0] += 1;
   float* const hrow = a.hpre + (size_t)(blockIdx.x % a.hrep) * a.hrep_stride;
 #pragma unroll
   for (int j = 0; j < F::NTW; ++j) {
@@ -166,6 +168,21 @@ __global__ __launch_bounds__(256) void cgen_fwd_kernel(GFwdArgs a) {
   }
 }
 
+}  // namespace cgen
+}  // namespace tde
+
+// The optimizer of the fused generic step (ops/kernels.py CgenOpt): w / m / v point at the Dense kernel's
+// elements of the flat buffers.
+struct TdeCgenOpt {
+  int kind;
+  float lr, mom, b1, b2, eps;
+  float* w; float* m; float* v;
+  const long long* iterations;
+};
+
+namespace tde {
+namespace cgen {
+
 struct GBwdArgs {
   const float* x; const uint64_t* amax; int lda;
   const float* hpre; float* hzero; int hrep; long long hrep_stride;
@@ -174,17 +191,35 @@ struct GBwdArgs {
   const float* W1; const float* Pt; int ldPt;
   float* dW1; float* dwc; float* dbc; float* dW2; float* db2; float* db1;
   long long* iterations;   // the step counter, advanced by the head workgroup (nullable)
+  // fused step (nullable): each trunk workgroup applies the optimizer to its own Dense rows in place instead
+  // of storing dW1 (no other workgroup of the launch reads them; t = *oit, advanced by the forward)
+  TdeCgenOpt opt;
+  int opt_on;
+  long long* stamps;   // diagnostics (nullable): per-workgroup phase clocks, bench/cgen_micro.py --phases
+  // conv gradients: workgroup x adds into replica x % crep (dwc / dbc + replica * crep_stride): ~170 same-address
+  // float atomics per value serialise at the memory side; the consumer sums the replicas
+  int crep;
+  long long crep_stride;
+  // fused step: the workgroup that arrives last (counter *arrive, reset by it) applies the optimizer to the
+  // small variables — the conv layer from its gradient replicas (fconv) and the head (frest) — once every
+  // other workgroup of the launch is done with them
+  FlatApply fconv, frest;
+  unsigned* arrive;
   int B, H, W;
 };
 
-template <int CC, int HD>
+template <int CC, int HD, int NW>
 struct BwdCfg {
+  static constexpr int NTH = NW * 64;
   static constexpr int RG = HD + 4;    // row stride of G / h / W1s (floats)
   static constexpr int RP = 64 + 4;    // row stride of P^T rows
   static constexpr int DPS = CC + 4;   // row stride of dP
   static constexpr int T1 = 4 * (CC / 16);              // dP tiles (image tile x channel tile)
   static constexpr int T2 = (CC / 16) * (HD / 16);      // dW1 tiles (channel tile x unit tile)
-  static constexpr int TW = (T1 + T2 + 15) / 16;        // tiles per wave
+  static constexpr int TW = (T1 + T2 + NW - 1) / NW;    // tiles per wave
+  static constexpr int KG = NW / 4;                     // K groups of the logits MFMA (4 row tiles each)
+  static constexpr int UTW = (HD / 16 + NW - 1) / NW;   // head workgroup: dW2 unit tiles per wave
+  static constexpr int IPW = 64 / NW;                   // routing: images per wave
   static constexpr int HQ = HD / 4;                     // k per lane group in the dP MFMA
   // LDS carve (bytes)
   static constexpr int kG = 0;
@@ -195,7 +230,7 @@ struct BwdCfg {
   static constexpr int kR = kAm + 64 * CC;              // head scratch | dP | conv-gradient reduction
   static constexpr int kHs = 64 * RG * 4, kPart = 3 * 4 * 64 * 4 * 4, kDl = 64 * W2S * 4;
   static constexpr int kHead = kHs + kPart + kDl;
-  static constexpr int kRed = 16 * 10 * CC * 4;
+  static constexpr int kRed = NW * 10 * CC * 4;
   static constexpr int kRBytes = kHead > kRed ? kHead : kRed;
   static constexpr int kW2 = kR + kRBytes;
   static constexpr int kB2 = kW2 + HD * W2S * 4;
@@ -206,9 +241,10 @@ struct BwdCfg {
   static_assert(kLds <= 160 * 1024, "backward LDS exceeds a CU");
 };
 
-template <int CC, int HD>
-__global__ __launch_bounds__(kGThreads) void cgen_bwd_kernel(GBwdArgs a) {
-  using F = BwdCfg<CC, HD>;
+template <int CC, int HD, int NW>
+__global__ __launch_bounds__(NW * 64) void cgen_bwd_kernel(GBwdArgs a) {
+  using F = BwdCfg<CC, HD, NW>;
+  constexpr int kGThreads = F::NTH;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* Gs = reinterpret_cast<float*>(smem + F::kG);
   float* W1s = reinterpret_cast<float*>(smem + F::kW1);
@@ -227,6 +263,7 @@ __global__ __launch_bounds__(kGThreads) void cgen_bwd_kernel(GBwdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
   const int W = a.W, Wp = (W - 2) / 2, P = ((a.H - 2) / 2) * Wp, C = a.C;
   const bool head_wg = blockIdx.x == gridDim.x - 1;
+  stamp(a.stamps, 0);
 
   // the other parity of hpre zeroed for the next forward's atomics (a slice per workgroup)
   {
@@ -255,9 +292,9 @@ __global__ __launch_bounds__(kGThreads) void cgen_bwd_kernel(GBwdArgs a) {
   f32x4 accr[CC / 16];
 #pragma unroll
   for (int ct = 0; ct < CC / 16; ++ct) accr[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 gw[(HD / 16 + 15) / 16];   // head workgroup: dW2 tiles (unit tiles wave, wave + 16)
+  f32x4 gw[F::UTW];   // head workgroup: dW2 tiles (unit tiles wave, wave + NW, ...)
 #pragma unroll
-  for (int j = 0; j < (HD / 16 + 15) / 16; ++j) gw[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < F::UTW; ++j) gw[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float la = 0.f, ca = 0.f, na = 0.f, db2acc = 0.f;
   if (head_wg && tid < 4 * HD) db1p[tid] = 0.f;
 
@@ -311,19 +348,23 @@ __global__ __launch_bounds__(kGThreads) void cgen_bwd_kernel(GBwdArgs a) {
       }
     }
     lds_barrier();
+    stamp(a.stamps, 1);
 
-    // ---- logits = h . W2 + b2: wave = (row tile rt, K quarter kq); softmax-CE on waves 0..3 -> dls
+    // ---- logits = h . W2 + b2: wave = (row tile rt, K group kg: K quarters kg, kg + KG, ..); softmax-CE on
+    //      waves 0..3 -> dls
     {
-      const int rt = wave & 3, kq = wave >> 2;
+      const int rt = wave & 3, kg = wave >> 2;
       f32x4 lg{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int k = kq * (HD / 4); k < (kq + 1) * (HD / 4); k += 4)
-        lg = mfma4(hs[(rt * 16 + fr) * F::RG + k + fq], w2s[(k + fq) * W2S + fr], lg);
-      if (kq > 0) *reinterpret_cast<f32x4*>(part + (((kq - 1) * 4 + rt) * 64 + lane) * 4) = lg;
+      for (int kq = kg; kq < 4; kq += F::KG)
+#pragma unroll
+        for (int k = kq * (HD / 4); k < (kq + 1) * (HD / 4); k += 4)
+          lg = mfma4(hs[(rt * 16 + fr) * F::RG + k + fq], w2s[(k + fq) * W2S + fr], lg);
+      if (kg > 0) *reinterpret_cast<f32x4*>(part + (((kg - 1) * 4 + rt) * 64 + lane) * 4) = lg;
       lds_barrier();
       if (wave < 4) {
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
+        for (int q = 0; q < F::KG - 1; ++q) {
           const f32x4 pv = *reinterpret_cast<const f32x4*>(part + ((q * 4 + rt) * 64 + lane) * 4);
           lg[0] += pv[0]; lg[1] += pv[1]; lg[2] += pv[2]; lg[3] += pv[3];
         }
@@ -347,9 +388,10 @@ __global__ __launch_bounds__(kGThreads) void cgen_bwd_kernel(GBwdArgs a) {
         }
       }
       lds_barrier();
+      stamp(a.stamps, 2);
     }
     // ---- G = dH = dl . W2^T masked by h > 0 (rows < nb): tiles (row tile, unit tile) over the waves
-    for (int t = wave; t < 4 * (HD / 16); t += 16) {
+    for (int t = wave; t < 4 * (HD / 16); t += NW) {
       const int rt = t & 3, ut = t >> 2;
       f32x4 gh{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -365,8 +407,8 @@ __global__ __launch_bounds__(kGThreads) void cgen_bwd_kernel(GBwdArgs a) {
     if (head_wg) {
       // dW2[u][c] += sum_b h[b][u] dl[b][c]: unit tiles ut = wave, wave + 16
 #pragma unroll
-      for (int j = 0; j < (HD / 16 + 15) / 16; ++j) {
-        const int ut = wave + 16 * j;
+      for (int j = 0; j < F::UTW; ++j) {
+        const int ut = wave + NW * j;
         if (ut < HD / 16) {
 #pragma unroll 4
           for (int k = 0; k < 64; k += 4) gw[j] = mfma4(hs[(k + fq) * F::RG + ut * 16 + fr], dls[(k + fq) * W2S + fr], gw[j]);
@@ -388,12 +430,13 @@ __global__ __launch_bounds__(kGThreads) void cgen_bwd_kernel(GBwdArgs a) {
       continue;
     }
     lds_barrier();
+    stamp(a.stamps, 3);
 
     // ---- tiles over the waves: dP[b][c] = sum_u G[b][u] W1p[c][u] (t < T1), dW1p[c][u] += sum_b P[b][c]
     //      G[b][u] (T1 <= t < T1 + T2; accumulators persist over the chunks)
 #pragma unroll
     for (int j = 0; j < F::TW; ++j) {
-      const int t = wave + 16 * j;
+      const int t = wave + NW * j;
       if (t < F::T1) {
         const int mt = t & 3, ct = t >> 2;
         f32x4 acc{0.f, 0.f, 0.f, 0.f};
@@ -426,14 +469,15 @@ __global__ __launch_bounds__(kGThreads) void cgen_bwd_kernel(GBwdArgs a) {
       }
     }
     lds_barrier();
+    stamp(a.stamps, 4);
 
     // ---- routing MFMA: dWc[tap][c] += sum over (image, window slot) of X[tap] . dP masked by the argmax;
     //      k = (b, q): lane group fq = window slot q; wave takes images 4w .. 4w+3
     {
       const int tap = fr, ky = tap / 3, kx = tap - ky * 3, qy = fq >> 1, qx = fq & 1;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int bl = wave * 4 + s;
+      for (int s = 0; s < F::IPW; ++s) {
+        const int bl = wave * F::IPW + s;
         const float xa = tap < 9 ? xs[bl * 16 + (qy + ky) * 4 + qx + kx] : (tap == 9 ? 1.f : 0.f);
 #pragma unroll
         for (int ct = 0; ct < CC / 16; ++ct) {
@@ -444,6 +488,7 @@ __global__ __launch_bounds__(kGThreads) void cgen_bwd_kernel(GBwdArgs a) {
       }
     }
     lds_barrier();
+    stamp(a.stamps, 5);
   }
 
   if (head_wg) {
@@ -456,26 +501,51 @@ __global__ __launch_bounds__(kGThreads) void cgen_bwd_kernel(GBwdArgs a) {
       atomicAdd(a.metrics + 2, na);
     }
 #pragma unroll
-    for (int j = 0; j < (HD / 16 + 15) / 16; ++j) {
-      const int ut = wave + 16 * j;
+    for (int j = 0; j < F::UTW; ++j) {
+      const int ut = wave + NW * j;
       if (ut < HD / 16 && fr < C && a.dW2)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) a.dW2[(size_t)(ut * 16 + fq * 4 + i) * C + fr] += gw[j][i];
+        for (int i = 0; i < 4; ++i) atomicAdd(a.dW2 + (size_t)(ut * 16 + fq * 4 + i) * C + fr, gw[j][i]);
     }
-    if (tid < C && a.db2) a.db2[tid] += db2acc;
-    if (tid < HD && a.db1) a.db1[tid] += (db1p[tid] + db1p[HD + tid]) + (db1p[2 * HD + tid] + db1p[3 * HD + tid]);
+    // (single writer: atomics only so that the fused step's last workgroup reads them without a release fence)
+    if (tid < C && a.db2) atomicAdd(a.db2 + tid, db2acc);
+    if (tid < HD && a.db1)
+      atomicAdd(a.db1 + tid, (db1p[tid] + db1p[HD + tid]) + (db1p[2 * HD + tid] + db1p[3 * HD + tid]));
     if (tid == 0 && a.iterations) a.iterations[0] += 1;
-    return;
-  }
+  } else {
 
-  // dW1 rows of the position (complete: this workgroup owns them)
+  // dW1 rows of the position (complete: this workgroup owns them): stored, or applied in place from the LDS
+  // copy of the rows this launch read
+  if (a.opt_on) {
+    const TdeCgenOpt& o = a.opt;
+    const OptHyper hy{o.kind, o.lr, o.mom, o.b1, o.b2, o.eps};
+    const float lr_t = opt_lr_t(hy, o.kind == kOptAdam ? *o.iterations : 0);
 #pragma unroll
-  for (int j = 0; j < F::TW; ++j) {
-    const int t = wave + 16 * j;
-    if (t >= F::T1 && t < F::T1 + F::T2) {
-      const int u2 = t - F::T1, rt = u2 % (CC / 16), nt = u2 / (CC / 16);
+    for (int j = 0; j < F::TW; ++j) {
+      const int t = wave + NW * j;
+      if (t >= F::T1 && t < F::T1 + F::T2) {
+        const int u2 = t - F::T1, rt = u2 % (CC / 16), nt = u2 / (CC / 16);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) a.dW1[(size_t)(p * CC + rt * 16 + fq * 4 + r) * HD + nt * 16 + fr] = accw[j][r];
+        for (int r = 0; r < 4; ++r) {
+          const int row = rt * 16 + fq * 4 + r, col = nt * 16 + fr;
+          const size_t e = (size_t)(p * CC + row) * HD + col;
+          float m = o.kind != kOptSGD ? o.m[e] : 0.f;
+          float v = o.kind == kOptAdam ? o.v[e] : 0.f;
+          o.w[e] = opt_step(hy, lr_t, W1s[row * F::RG + col], accw[j][r], m, v);
+          if (o.kind != kOptSGD) o.m[e] = m;
+          if (o.kind == kOptAdam) o.v[e] = v;
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < F::TW; ++j) {
+      const int t = wave + NW * j;
+      if (t >= F::T1 && t < F::T1 + F::T2) {
+        const int u2 = t - F::T1, rt = u2 % (CC / 16), nt = u2 / (CC / 16);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a.dW1[(size_t)(p * CC + rt * 16 + fq * 4 + r) * HD + nt * 16 + fr] = accw[j][r];
+      }
     }
   }
   // conv gradients: the 16 waves' routing accumulators summed through LDS, one add per value
@@ -487,13 +557,36 @@ __global__ __launch_bounds__(kGThreads) void cgen_bwd_kernel(GBwdArgs a) {
       if (tap < 10) red[((size_t)wave * 10 + tap) * CC + ct * 16 + fr] = accr[ct][r];
     }
   lds_barrier();
+  stamp(a.stamps, 6);
   for (int i = tid; i < 10 * CC; i += kGThreads) {
     const int tap = i / CC, c = i - tap * CC;
     float s = 0.f;
 #pragma unroll
-    for (int w = 0; w < 16; ++w) s += red[((size_t)w * 10 + tap) * CC + c];
-    if (tap < 9) atomicAdd(a.dwc + tap * CC + c, s);
-    else atomicAdd(a.dbc + c, s);
+    for (int w = 0; w < NW; ++w) s += red[((size_t)w * 10 + tap) * CC + c];
+    const long long ro = (long long)(blockIdx.x % a.crep) * a.crep_stride;
+    if (tap < 9) atomicAdd(a.dwc + ro + tap * CC + c, s);
+    else atomicAdd(a.dbc + ro + c, s);
+  }
+  stamp(a.stamps, 7);
+  }
+
+  if (a.arrive) {
+    // Every gradient this update reads was added with device-scope atomics (performed at the memory side, no
+    // dirty L2 line to write back): each thread waits until its own are performed, then the workgroup counts
+    // itself in; the last one drops its L2's stale lines (acquire) and updates.  A device-scope release
+    // fence here would write back every workgroup's L2 (the Dense rows it just stored): +40 % step time.
+    __shared__ int s_last;
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (tid == 0) s_last = atomicAdd(a.arrive, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const long long t = a.fconv.h.kind == kOptAdam ? *a.fconv.iterations : 0;
+      flat_apply(a.fconv, t, tid, kGThreads);
+      flat_apply(a.frest, t, tid, kGThreads);
+      if (tid == 0) *a.arrive = 0u;
+    }
   }
 }
 
@@ -513,17 +606,34 @@ static int launch_fwd(const GFwdArgs& a, int P, hipStream_t s) {
   return 0;
 }
 
-template <int CC, int HD>
-static int launch_bwd(const GBwdArgs& a, int P, hipStream_t s) {
-  using F = BwdCfg<CC, HD>;
+template <int CC, int HD, int NW>
+static int launch_bwd_nw(const GBwdArgs& a, int P, hipStream_t s) {
+  using F = BwdCfg<CC, HD, NW>;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)cgen_bwd_kernel<CC, HD>, hipFuncAttributeMaxDynamicSharedMemorySize, F::kLds);
+    (void)hipFuncSetAttribute((const void*)cgen_bwd_kernel<CC, HD, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              F::kLds);
     attr = true;
   }
-  cgen_bwd_kernel<CC, HD><<<P + 1, kGThreads, F::kLds, s>>>(a);
+  cgen_bwd_kernel<CC, HD, NW><<<P + 1, F::NTH, F::kLds, s>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;
+}
+
+// Waves per backward workgroup: 16 (4 per SIMD, 128 VGPRs each) unless the width's accumulators would spill
+// there (TDE_CGEN_WAVES = 8 | 16 forces one).
+static int bwd_waves(int CC, int HD) {
+  static const int forced = [] {
+    const char* e = getenv("TDE_CGEN_WAVES");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced == 8 || forced == 16) return forced;
+  return CC * HD >= 6144 ? 8 : 16;
+}
+
+template <int CC, int HD>
+static int launch_bwd(const GBwdArgs& a, int P, hipStream_t s) {
+  return bwd_waves(CC, HD) == 8 ? launch_bwd_nw<CC, HD, 8>(a, P, s) : launch_bwd_nw<CC, HD, 16>(a, P, s);
 }
 
 #define TDE_CGEN_DISPATCH(FN, CCV, HDV, ...)                                              \
@@ -552,33 +662,44 @@ TDE_API int tde_cgen_supported(int CC, int HD) {
 // Forward (see the header).  x [B][H][W] f32 (C_in = 1), wc [9][CC], bc [CC], W1 [P*CC][HD] f32 master,
 // hpre [hrep][>=B][HD] (+=), Pt [P*CC][ldPt], amax [P][CC/8][lda] (8 argmax bytes per u64).
 TDE_API int tde_cgen_fwd(int CC, int HD, const float* x, const float* wc, const float* bc, const float* W1,
-                         float* hpre, int hrep, long long hrep_stride, float* Pt, int ldPt, void* amax, int lda, int B,
-                         int H, int W, hipStream_t stream) {
+                         float* hpre, int hrep, long long hrep_stride, float* Pt, int ldPt, void* amax, int lda,
+                         long long* inc_iter, int B, int H, int W, hipStream_t stream) {
   if (!tde_cgen_supported(CC, HD) || (W & 3) || W > 32 || H < 4 || W < 4 || ((H - 2) & 1) || ((W - 2) & 1))
     return -1;
   if (!x || !wc || !bc || !W1 || !hpre || !Pt || !amax || (ldPt & 7) || ldPt < B || lda < B || hrep < 1 ||
       (hrep > 1 && hrep_stride < (long long)B * HD) || ((uintptr_t)x & 15) || ((uintptr_t)W1 & 15))
     return -2;
   const int P = ((H - 2) / 2) * ((W - 2) / 2);
-  GFwdArgs a{x, wc, bc, W1, hpre, hrep, hrep_stride, Pt, ldPt, (uint64_t*)amax, lda, B, H, W};
+  GFwdArgs a{x, wc, bc, W1, hpre, hrep, hrep_stride, Pt, ldPt, (uint64_t*)amax, lda, inc_iter, B, H, W};
   TDE_CGEN_DISPATCH(launch_fwd, CC, HD, a, P, stream)
 }
 
 // Backward (plain step: gradients out).  hpre / hzero [hrep][>=B][HD] (hzero zeroed here), dW1 [P*CC][HD]
 // stored, dwc [9][CC] / dbc [CC] atomically added, dW2 [HD][C] / db2 [C] / db1 [HD] added (nullable);
-// iterations (nullable) advanced by one.
+// iterations (nullable) advanced by one.  opt (nullable): the fused step — dW1 applied to the Dense kernel in
+// place by the optimizer instead of stored (dW1 may then be null).  crep / crep_stride: conv-gradient replicas.
+// arrive (nullable, zero-initialised int): the last workgroup applies fconv and frest (unconditional updates).
 TDE_API int tde_cgen_bwd(int CC, int HD, const float* x, const void* amax, int lda, const float* hpre, float* hzero,
                          int hrep, long long hrep_stride, const float* b1, const float* W2, const float* b2, int C,
                          int pre_relu, const int* labels, float scale, float* metrics, const float* W1, const float* Pt,
                          int ldPt, float* dW1, float* dwc, float* dbc, float* dW2, float* db2, float* db1,
-                         long long* iterations, int B, int H, int W, hipStream_t stream) {
+                         long long* iterations, const TdeCgenOpt* opt, long long* stamps, int crep,
+                         long long crep_stride, const FlatApply* fconv, const FlatApply* frest, unsigned* arrive,
+                         int B, int H, int W, hipStream_t stream) {
   if (!tde_cgen_supported(CC, HD) || C < 1 || C > 16 || W > 32 || (W & 3)) return -1;
-  if (!x || !amax || !hpre || !hzero || !W2 || !b2 || !labels || !W1 || !Pt || !dW1 || !dwc || !dbc ||
+  if (opt && (!opt->w || (opt->kind != kOptSGD && !opt->m) || (opt->kind == kOptAdam && (!opt->v || !opt->iterations))))
+    return -3;
+  if (crep < 1 || crep > 64 || (crep > 1 && crep_stride < 10LL * CC)) return -4;
+  if (arrive && (!fconv || !frest || !opt || fconv->pend || frest->pend || fconv->grep > kMaxGrep ||
+                 frest->grep > kMaxGrep || fconv->nr > kFlatRanges || frest->nr > kFlatRanges))
+    return -5;
+  if (!x || !amax || !hpre || !hzero || !W2 || !b2 || !labels || !W1 || !Pt || (!dW1 && !opt) || !dwc || !dbc ||
       (ldPt & 7) || ldPt < B || lda < B || hrep < 1 || (hrep > 1 && (hrep_stride < (long long)B * HD || (hrep_stride & 3))) ||
       (((uintptr_t)hpre | (uintptr_t)hzero | (uintptr_t)W1 | (uintptr_t)Pt | (uintptr_t)b1) & 15))
     return -2;
   const int P = ((H - 2) / 2) * ((W - 2) / 2);
   GBwdArgs a{x, (const uint64_t*)amax, lda, hpre, hzero, hrep, hrep_stride, b1, W2, b2, C, pre_relu, labels, scale,
-             metrics, W1, Pt, ldPt, dW1, dwc, dbc, dW2, db2, db1, iterations, B, H, W};
+             metrics, W1, Pt, ldPt, dW1, dwc, dbc, dW2, db2, db1, iterations, opt ? *opt : TdeCgenOpt{}, opt != nullptr, stamps,
+             crep, crep_stride, fconv ? *fconv : FlatApply{}, frest ? *frest : FlatApply{}, arrive, B, H, W};
   TDE_CGEN_DISPATCH(launch_bwd, CC, HD, a, P, stream)
 }

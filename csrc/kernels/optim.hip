@@ -174,17 +174,17 @@ __global__ __launch_bounds__(256) void shadow_refresh_kernel(const float* w, bf1
   }
 }
 
-// Deferred-update flush (one workgroup): applies the ranges if *pend (or always when
-// pend is null) with t = *iterations, then clears *pend.
+// Deferred-update flush (one workgroup): applies the ranges if *pend with t = *iterations, then clears
+// *pend.  Without pend (an unconditional update) the ranges are spread over the whole grid.
 __global__ __launch_bounds__(256) void flat_apply_kernel(FlatApply f) {
   __shared__ int go;
   if (threadIdx.x == 0) go = f.pend ? *f.pend : 1;
   __syncthreads();
   if (!go) return;
-  flat_apply(f, f.h.kind == kOptAdam ? *f.iterations : 0, threadIdx.x, 256);
+  flat_apply(f, f.h.kind == kOptAdam ? *f.iterations : 0, blockIdx.x * 256 + threadIdx.x, 256 * gridDim.x);
   __syncthreads();
   if (threadIdx.x == 0 && f.pend) *f.pend = 0;
-  if (threadIdx.x == 0 && f.count) atomicAdd(f.count, 1ull);
+  if (threadIdx.x == 0 && blockIdx.x == 0 && f.count) atomicAdd(f.count, 1ull);
 }
 
 }  // namespace tde
@@ -203,7 +203,11 @@ TDE_API int tde_flat_apply(float* w, float* g, float* m, float* v, const long lo
     f.lo[i] = ranges[2 * i];
     f.n[i] = ranges[2 * i + 1];
   }
-  flat_apply_kernel<<<1, 256, 0, stream>>>(f);
+  int maxn = 0;
+  for (int i = 0; i < nr; ++i) maxn = f.n[i] > maxn ? f.n[i] : maxn;
+  // pend: one workgroup (it reads and clears the flag); otherwise about one element per thread
+  const int nb = pend ? 1 : (maxn + 255) / 256 < 1 ? 1 : ((maxn + 255) / 256 > 64 ? 64 : (maxn + 255) / 256);
+  flat_apply_kernel<<<nb, 256, 0, stream>>>(f);
   TDE_LAUNCH_CHECK();
   return 0;
 }

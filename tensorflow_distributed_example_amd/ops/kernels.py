@@ -276,14 +276,23 @@ def convnet_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, me
     N.check(rc, "tde_convnet_bwd_f32" if f32 else "tde_convnet_bwd")
 
 
+class CgenOpt(_ct.Structure):
+    """``TdeCgenOpt`` (csrc/kernels/convnet_gen.hip): the optimizer the generic fused backward applies to the
+    Dense kernel rows in place (w / m / v at the Dense kernel's elements of the flat buffers)."""
+    _fields_ = [("kind", _ct.c_int), ("lr", _ct.c_float), ("mom", _ct.c_float), ("b1", _ct.c_float), ("b2", _ct.c_float),
+                ("eps", _ct.c_float), ("w", _ct.c_void_p), ("m", _ct.c_void_p), ("v", _ct.c_void_p),
+                ("iterations", _ct.c_void_p)]
+
+
 def cgen_supported(filters, units):
     return bool(N.hip().tde_cgen_supported(int(filters), int(units)))
 
 
-def cgen_fwd(x, wc, bc, W1, hpre, Pt, amax, *, B):
+def cgen_fwd(x, wc, bc, W1, hpre, Pt, amax, *, B, inc_iter=None):
     """Generic-width fused small-CNN forward, float32 (csrc/kernels/convnet_gen.hip): Conv2D(CC, 3x3) + ReLU +
     MaxPool(2) + the Dense(HD) matmul, hpre [R, >=B, HD] += (workgroup i adds into replica i % R).
-    W1 the f32 master kernel [P*CC, HD]; Pt [P*CC, ldPt] f32; amax int64 [P, CC/8, lda]."""
+    W1 the f32 master kernel [P*CC, HD]; Pt [P*CC, ldPt] f32; amax int64 [P, CC/8, lda]; inc_iter (int64 step
+    counter, nullable) advanced by one."""
     H, W = x.shape[1], x.shape[2]
     CC = wc.shape[-1]
     Pn = ((H - 2) // 2) * ((W - 2) // 2)
@@ -297,16 +306,22 @@ def cgen_fwd(x, wc, bc, W1, hpre, Pt, amax, *, B):
          "cgen_fwd: Pt")
     _req(amax.dtype == torch.int64 and amax.shape[:2] == (Pn, CC // 8) and amax.shape[-1] >= B, "cgen_fwd: amax")
     rc = N.hip().tde_cgen_fwd(CC, HD, _P(x), _P(wc), _P(bc), _P(W1), _P(hpre), hp.shape[0], hp.stride(0), _P(Pt),
-                              Pt.stride(0), _P(amax), amax.shape[-1], B, H, W, _s())
+                              Pt.stride(0), _P(amax), amax.shape[-1], _P(inc_iter), B, H, W, _s())
     N.check(rc, "tde_cgen_fwd")
 
 
 def cgen_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, metrics, W1, Pt, dW1, dwc, dbc,
-             dW2=None, db2=None, db1=None, B, iterations=None):
+             dW2=None, db2=None, db1=None, B, iterations=None, opt: CgenOpt | None = None, stamps=None, crep=1,
+             crep_stride=0, fconv: FlatApply | None = None, frest: FlatApply | None = None, arrive=None):
     """Generic-width fused small-CNN backward, float32 (plain step): from hpre [R, >=B, HD] every workgroup
     recomputes the head, then the Dense(HD) weight / input gradients and the conv gradients; hzero (the
     other parity) is zeroed.  dW1 stored, dwc / dbc atomically added, dW2 / db2 / db1 added, metrics added,
-    ``iterations`` (int64 step counter) advanced."""
+    ``iterations`` (int64 step counter) advanced.  ``opt`` (fused step): dW1 is applied to W1 in place by the
+    optimizer instead of stored (``dW1`` may be None).  ``stamps`` (diagnostics): int64 [P + 1, 8] phase
+    clocks per workgroup.  ``crep`` > 1: workgroup x adds its conv gradients into replica x % crep of dwc / dbc
+    (``crep_stride`` elements apart), summed by the consumer.  ``arrive`` (fused step; an int32 device counter,
+    zero between launches): the workgroup that finishes last applies ``fconv`` and ``frest`` (unconditional
+    ``FlatApply`` updates of the small variables) once every other workgroup is done reading them."""
     H, W = x.shape[1], x.shape[2]
     CC = dwc.shape[-1]
     Pn = ((H - 2) // 2) * ((W - 2) // 2)
@@ -314,16 +329,22 @@ def cgen_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, metri
     hp = hpre if hpre.dim() == 3 else hpre.unsqueeze(0)
     _req(hpre.is_contiguous() and hzero.shape == hpre.shape and hzero.is_contiguous() and hp.shape[2] == HD
          and hp.shape[1] >= B, "cgen_bwd: hpre / hzero")
-    _req(tuple(W1.shape) == (Pn * CC, HD) and W1.is_contiguous() and dW1.shape == W1.shape and dbc.numel() == CC,
+    _req(tuple(W1.shape) == (Pn * CC, HD) and W1.is_contiguous() and (dW1 is None and opt is not None or
+                                                                        dW1.shape == W1.shape) and dbc.numel() == CC,
          "cgen_bwd: shapes")
     _req(Pt.shape[0] == Pn * CC and Pt.dtype == torch.float32 and Pt.stride(0) >= B, "cgen_bwd: Pt")
     _req(amax.dtype == torch.int64 and amax.shape[:2] == (Pn, CC // 8) and amax.shape[-1] >= B, "cgen_bwd: amax")
     _req(labels.dtype == torch.int32 and labels.numel() >= B and C <= 16, "cgen_bwd: labels / classes")
+    _req(arrive is None or (arrive.dtype == torch.int32 and opt is not None and fconv is not None and
+                            frest is not None and not fconv.pend and not frest.pend), "cgen_bwd: fused small update")
     _req(W2.is_contiguous() and b2.numel() == C and (b1 is None or b1.numel() == HD), "cgen_bwd: head variables")
     rc = N.hip().tde_cgen_bwd(CC, HD, _P(x), _P(amax), amax.shape[-1], _P(hpre), _P(hzero), hp.shape[0],
                               hp.stride(0), _P(b1), _P(W2), _P(b2), C, int(pre_relu), _P(labels), float(scale),
                               _P(metrics), _P(W1), _P(Pt), Pt.stride(0), _P(dW1), _P(dwc), _P(dbc), _P(dW2),
-                              _P(db2), _P(db1), _P(iterations), B, H, W, _s())
+                              _P(db2), _P(db1), _P(iterations), _ct.byref(opt) if opt is not None else None,
+                              _P(stamps), int(crep), int(crep_stride),
+                              _ct.byref(fconv) if fconv is not None else None,
+                              _ct.byref(frest) if frest is not None else None, _P(arrive), B, H, W, _s())
     N.check(rc, "tde_cgen_bwd")
 
 

@@ -693,9 +693,11 @@ class ConvNetGenPlan(ReplicaPlan):
                 of its pooled position, the pool / ReLU routing MFMA and the conv gradients; one extra
                 workgroup makes the head's own gradients, the metrics and the step count
 
-    followed by the multi-tensor optimizer (step mode "plain"; the data-parallel strategies all-reduce the
-    flat bucket between the two as for any plan).  The reference's own Conv2D(32)/Dense(64) keeps the
-    hand-tuned ``ConvNetPlan`` (fused optimizer, deferred conv update, fused exchange)."""
+    followed, by step mode, by the multi-tensor optimizer ("plain"), nothing ("local": each backward
+    workgroup applies the optimizer to the Dense(U) rows it owns in place — no other workgroup of the launch
+    reads them — and the workgroup that finishes last updates the conv layer, from its gradient replicas, and
+    the head: two launches per step), or the xGMI all-reduce that applies it ("xgmi").  The reference's own
+    Conv2D(32)/Dense(64) keeps the hand-tuned ``ConvNetPlan`` (deferred conv update, fused exchange)."""
     kind = "fused_convnet_generic"
 
     def __init__(self, model, store, device, batch, global_batch, optimizer, loss, pattern):
@@ -724,6 +726,89 @@ class ConvNetGenPlan(ReplicaPlan):
         self.W1 = store.view(self.names["w1"])
         self.opt = OptimizerKernel(store, optimizer, {}, self.iterations) if optimizer is not None else None
         self.parity = 0
+        self._copt = self._rest = self._conv_apply = None
+        # conv gradients: the ~170 backward workgroups add theirs into crep replicas of the conv segments
+        # (workgroup x -> replica x % crep; same-address float atomics from every workgroup serialise at the
+        # memory side), summed by the consumer — the fused step's small update or the xGMI all-reduce
+        # (TDE_CONVNET_GREP; plain steps add straight into the gradient bucket)
+        seg = store.segments
+        sw, sb = seg[self.names["wc"]], seg[self.names["bc"]]
+        self._conv_lo = min(sw.offset, sb.offset)
+        self._conv_span = max(sw.offset + sw.numel, sb.offset + sb.numel) - self._conv_lo
+        others = [n for n in store.order if n not in (self.names["wc"], self.names["bc"]) and
+                  self._conv_lo <= seg[n].offset < self._conv_lo + self._conv_span]
+        self.crep = 1 if others else max(1, min(8, int(os.environ.get("TDE_CONVNET_GREP", "8"))))
+        self.gconv = torch.zeros(self.crep, self._conv_span, dtype=torch.float32, device=dev)
+        self.arrive = torch.zeros(1, dtype=torch.int32, device=dev)   # the backward's last-workgroup counter
+        # step mode "local": the variables other than the conv layer and the Dense(U) kernel as <= 4 element
+        # ranges of the flat buffers (padding between segments carries zero gradients and zero slots)
+        excl = {self.names["w1"], self.names["wc"], self.names["bc"]}
+        segs = sorted((seg[n].offset, seg[n].numel, n) for n in store.names(trainable=True))
+        ranges = []
+        for off, numel, name in segs:
+            if name in excl:
+                ranges.append(None)
+            elif ranges and ranges[-1] is not None:
+                ranges[-1] = (ranges[-1][0], off + numel - ranges[-1][0])
+            else:
+                ranges.append((off, numel))
+        self._rest_ranges = [r for r in ranges if r is not None]
+
+    def supports_step_mode(self, mode):
+        if mode == "plain":
+            return True
+        ok = self.optimizer is not None and self.device.type == "cuda"
+        return ok and (mode == "xgmi" or mode == "local" and len(self._rest_ranges) <= 4)
+
+    def set_step_mode(self, mode):
+        super().set_step_mode(mode)
+        self._copt = self._rest = self._conv_apply = None
+        self.gconv.zero_()
+        self.arrive.zero_()
+        if mode != "local":
+            return
+        K, st, o = self.K, self.store, self.optimizer
+        sl = o.slot_names()
+        m = st.slot(sl[0]) if sl else None
+        v = st.slot(sl[1]) if len(sl) > 1 else None
+        hp = o.hparams()
+        off = st.segments[self.names["w1"]].offset
+        el = lambda t: None if t is None else t.data_ptr() + 4 * off  # noqa: E731
+        self._copt = K.CgenOpt(o.kind_id, float(o.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"],
+                               el(st.w), el(m), el(v), self.iterations.data_ptr())
+        self._rest = K.flat_apply_spec(o, st.w, st.g, m, v, self.iterations, None, self._rest_ranges)
+        ca = K.flat_apply_spec(o, st.w, None, m, v, self.iterations, None, [(self._conv_lo, self._conv_span)])
+        ca.g = self.gconv.data_ptr() - 4 * self._conv_lo   # indexed with the flat offsets
+        ca.grep, ca.grep_stride = self.crep, self._conv_span
+        self._conv_apply = ca
+        self._opt_key_set = self._opt_key()
+
+    def _opt_key(self):
+        o = self.optimizer
+        return (o.kind_id, float(o.learning_rate), tuple(sorted(o.hparams().items())))
+
+    def refresh(self):
+        # the launch descriptors carry lr / hyper-parameters by value
+        if self.step_mode == "local" and self._opt_key_set != self._opt_key():
+            self.set_step_mode("local")
+
+    def xg_apply_spec(self):
+        spec = f32_xg_apply_spec(self)
+        if self.crep > 1:   # the conv gradients wait in the replicas: the all-reduce sums (and zeroes) them
+            spec.rep, spec.nrep = self.gconv.data_ptr(), self.crep
+            spec.rep_lo, spec.rep_hi = self._conv_lo, self._conv_lo + self._conv_span
+            spec.rep_stride = self._conv_span
+        return spec
+
+    def _conv_grads(self):
+        """(dwc, dbc, crep, stride) the backward adds the conv gradients into."""
+        if self.step_mode == "plain" or self.crep == 1:
+            return self._g("wc"), self._g("bc"), 1, 0
+        seg = self.store.segments
+        sw, sb = seg[self.names["wc"]], seg[self.names["bc"]]
+        lo = self._conv_lo
+        return (self.gconv[0, sw.offset - lo: sw.offset - lo + sw.numel], self.gconv[0, sb.offset - lo: sb.offset - lo + sb.numel],
+                self.crep, self._conv_span)
 
     def _v(self, key):
         nm = self.names[key]
@@ -740,11 +825,18 @@ class ConvNetGenPlan(ReplicaPlan):
         K = self.K
         B = self.B if B is None else B
         q = self.parity
-        K.cgen_fwd(x, self._v("wc"), self._v("bc"), self.W1, self.hpre2[q], self.Pt, self.amax, B=B)
+        local = self.step_mode == "local"
+        # the fused step's Adam t is read by every backward workgroup: the forward advances the counter
+        K.cgen_fwd(x, self._v("wc"), self._v("bc"), self.W1, self.hpre2[q], self.Pt, self.amax, B=B,
+                   inc_iter=self.iterations if local else None)
+        dwc, dbc, crep, cstride = self._conv_grads()
         K.cgen_bwd(x, self.amax, self.hpre2[q], self.hpre2[1 - q], self._v("b1"), self._v("w2"), self._v("b2"), y,
                    scale=self.scale, pre_relu=self.pre_relu, metrics=self.metrics, W1=self.W1, Pt=self.Pt,
-                   dW1=self._g("w1"), dwc=self._g("wc"), dbc=self._g("bc"), dW2=self._g("w2"), db2=self._g("b2"),
-                   db1=self._g("b1"), B=B, iterations=self.iterations)
+                   dW1=None if local else self._g("w1"), dwc=dwc.view(self._v("wc").shape), dbc=dbc, dW2=self._g("w2"),
+                   db2=self._g("b2"), db1=self._g("b1"), B=B, iterations=None if local else self.iterations,
+                   opt=self._copt if local else None, crep=crep, crep_stride=cstride,
+                   fconv=self._conv_apply if local else None, frest=self._rest if local else None,
+                   arrive=self.arrive if local else None)
         self.parity = 1 - q
 
     def apply(self):

@@ -102,6 +102,15 @@ def test_cgen_step_kernels_match_float64(CC, HD, B, relu, H, W, NC):
     loss = -(torch.log(pr) * onehot).sum()
     assert abs(met[0].item() - loss.item()) < 1e-5 * abs(loss.item())
     assert met[1].item() == (logits.argmax(1) == lab.long()).sum().item() and met[2].item() == B
+    # conv gradients into 5 replicas (workgroup x -> replica x % 5): the replicas sum to the same gradient
+    gc = torch.zeros(5, 10 * CC + 4, device=DEV)
+    Kk.cgen_bwd(x, amax, hpre, hzero, b1, W2, b2, lab, scale=scale, pre_relu=relu, metrics=None, W1=W1, Pt=Pt,
+                dW1=dW1, dwc=gc[0, :9 * CC].view(3, 3, 1, CC), dbc=gc[0, 9 * CC:10 * CC], B=B, crep=5,
+                crep_stride=10 * CC + 4)
+    torch.cuda.synchronize()
+    tot = gc.sum(0)
+    assert torch.all(gc[:, 10 * CC:] == 0) and int((gc.abs().sum(1) > 0).sum()) == 5
+    assert _rel(tot[:9 * CC], dw.reshape(-1)) < 1e-6 and _rel(tot[9 * CC:10 * CC], db) < 1e-6
 
 
 def test_cgen_rejects_uninstantiated_width():
@@ -130,19 +139,30 @@ def _grads64(m, W, x, y, B):
     return {n: w.grad for n, w in W.items()}
 
 
-@pytest.mark.parametrize("filters,units", [(64, 128), (16, 32)])
-def test_generic_plan_graph_trajectory_matches_float64(filters, units):
-    """A Conv2D(filters)/Dense(units) model runs the generic fused plan in hipGraph executions of 4 steps
-    (plain step: gradients, then the multi-tensor optimizer); after each execution the weights match the
-    float64 SGD trajectory at fp32 accuracy (1e-5 norm-wise) and the step counter advanced once per step."""
+@pytest.mark.parametrize("filters,units,mode,kind", [(64, 128, "local", "sgd"), (16, 32, "local", "sgd"),
+                                                     (64, 128, "plain", "sgd"), (32, 96, "local", "momentum"),
+                                                     (48, 64, "local", "adam"), (16, 128, "plain", "adam")])
+def test_generic_plan_graph_trajectory_matches_float64(filters, units, mode, kind, monkeypatch):
+    """A Conv2D(filters)/Dense(units) model runs the generic fused plan in hipGraph executions of 4 steps —
+    step mode "local" (the default with one replica: the backward applies the optimizer to the Dense rows
+    each workgroup owns, one small launch updates the rest) or "plain" (TDE_FUSED_STEP=0: gradients, then
+    the multi-tensor optimizer); after each execution the weights match the float64 trajectory of the same
+    optimizer (Keras forms) at fp32 accuracy and the step counter advanced once per step."""
     import tensorflow_distributed_example_amd as tde
-    m = _model(tde, filters, units, tde.optimizers.SGD(0.05), 4)
+    if mode == "plain":
+        monkeypatch.setenv("TDE_FUSED_STEP", "0")
+    O = tde.optimizers
+    lr = {"sgd": 0.05, "momentum": 0.02, "adam": 2e-3}[kind]
+    opt = {"sgd": lambda: O.SGD(lr), "momentum": lambda: O.SGD(lr, momentum=0.9), "adam": lambda: O.Adam(lr)}[kind]()
+    m = _model(tde, filters, units, opt, 4)
     st = m._store
     names = st.names(trainable=True)
     w64 = {n: st.view(n).detach().double().clone() for n in names}
+    slots = {n: [torch.zeros_like(w64[n]), torch.zeros_like(w64[n])] for n in names}
     prog = m._program("train", 64)
     plan = prog.plans[0]
-    assert prog.use_graph and plan.kind == "fused_convnet_generic" and plan.step_mode == "plain"
+    assert prog.use_graph and plan.kind == "fused_convnet_generic" and plan.step_mode == mode
+    t = 0
     for e in range(3):
         data = [_qdata(64, 300 + 4 * e + s) for s in range(4)]
         prog.stage([(torch.stack([d[0] for d in data]), torch.stack([d[1] for d in data]))])
@@ -150,16 +170,34 @@ def test_generic_plan_graph_trajectory_matches_float64(filters, units):
         prog.sync()
         for x, y in data:
             g = _grads64(m, w64, x, y, 64)
+            t += 1
             for n in names:
-                w64[n] = w64[n] - 0.05 * g[n]
+                if kind == "sgd":
+                    w64[n] = w64[n] - lr * g[n]
+                elif kind == "momentum":
+                    slots[n][0] = 0.9 * slots[n][0] - lr * g[n]
+                    w64[n] = w64[n] + slots[n][0]
+                else:
+                    b1, b2, eps = 0.9, 0.999, 1e-7
+                    slots[n][0] = b1 * slots[n][0] + (1 - b1) * g[n]
+                    slots[n][1] = b2 * slots[n][1] + (1 - b2) * g[n] ** 2
+                    lr_t = lr * (1 - b2 ** t) ** 0.5 / (1 - b1 ** t)
+                    w64[n] = w64[n] - lr_t * slots[n][0] / (slots[n][1].sqrt() + eps)
         for n in names:
             # after the first update the conv weights are no longer quantized: the f32 conv sums differ from
             # float64 in the last bit, and a pool-argmax near-tie decided the other way moves one image's
             # pooled gradient (the kernel tests pin each step at 1e-5 with exact conv sums).  The zero-
-            # initialised conv bias IS its accumulated update, so one such decision shows ~1e-4 there.
-            tol = 5e-4 if n == f"{m.layers[0].name}/bias" else 1e-5
+            # initialised biases ARE their accumulated update, so one such decision shows ~1e-4 there
+            # (Adam's normalised steps make every bias entry a full-size step: 1e-3).
+            # The conv kernel collects every image's pooled gradients: such decisions show there as a few 1e-5
+            # (a deferred or lost update would be ~1e-3).
+            bias, conv = n.endswith("/bias"), n == f"{m.layers[0].name}/kernel"
+            tol = (1e-3 if kind == "adam" else 5e-4) if bias else (5e-5 if conv or kind == "adam" else 1e-5)
             assert _rel(st.view(n), w64[n]) < tol, (e, n, _rel(st.view(n), w64[n]))
         assert int(plan.iterations) == 4 * (e + 1)
+    if mode == "local":   # nothing left behind in the bucket or the conv-gradient replicas
+        torch.cuda.synchronize()
+        assert plan.crep > 1 and float(st.g.abs().max()) == 0.0 and float(plan.gconv.abs().max()) == 0.0
 
 
 def test_generic_plan_fit_evaluate_predict():
