@@ -312,7 +312,8 @@ def match_convnet(model, loss):
         return None  # probabilities fed to from_logits=True (or logits w/o from_logits): not fusable
     if d2.units > 64 or d1.units * d2.units > 16384 or d1.units % 32 or d1.units > 256:
         return None
-    if c.filters != 32 or d1.units != 64:
+    force_gen = os.environ.get("TDE_CONVNET_GENERIC", "0") == "1"   # A/B: the generic kernels at any width
+    if c.filters != 32 or d1.units != 64 or force_gen:
         # the hand-tuned step is the reference's Conv2D(32)/Dense(64) (distributed_with_keras.py:34,37);
         # other widths run the generic fused kernels (float32 policy, ConvNetGenPlan) when they fit them,
         # and say so instead of silently dropping to the slower per-layer plan otherwise
