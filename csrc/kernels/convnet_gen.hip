@@ -17,6 +17,7 @@
 //             loss / accuracy, dW2, db2, db1.  hpre is double-buffered by step parity as in the
 //             specialised plan (this launch zeroes the other parity).
 #include "tde_optim.h"
+#include "tde_xgmi.h"
 
 namespace tde {
 namespace cgen {
@@ -205,6 +206,9 @@ struct GBwdArgs {
   // other workgroup of the launch is done with them
   FlatApply fconv, frest;
   unsigned* arrive;
+  // plain step under the xGMI communicator (nranks > 0): dW1 rows stored straight into the owners'
+  // contribution areas of the all-reduce call that follows (the fused data-parallel exchange)
+  XgPush push;
   int B, H, W;
 };
 
@@ -537,6 +541,18 @@ __global__ __launch_bounds__(NW * 64) void cgen_bwd_kernel(GBwdArgs a) {
         }
       }
     }
+  } else if (a.push.nranks > 0) {
+    // the position's complete dW1 rows staged in W1s (its last reader, the dP tiles, finished at the chunk
+    // loop's final barrier), then pushed below as contiguous float4 runs
+#pragma unroll
+    for (int j = 0; j < F::TW; ++j) {
+      const int t = wave + NW * j;
+      if (t >= F::T1 && t < F::T1 + F::T2) {
+        const int u2 = t - F::T1, rt = u2 % (CC / 16), nt = u2 / (CC / 16);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) W1s[(rt * 16 + fq * 4 + r) * F::RG + nt * 16 + fr] = accw[j][r];
+      }
+    }
   } else {
 #pragma unroll
     for (int j = 0; j < F::TW; ++j) {
@@ -566,6 +582,15 @@ __global__ __launch_bounds__(NW * 64) void cgen_bwd_kernel(GBwdArgs a) {
     const long long ro = (long long)(blockIdx.x % a.crep) * a.crep_stride;
     if (tap < 9) atomicAdd(a.dwc + ro + tap * CC + c, s);
     else atomicAdd(a.dbc + ro + c, s);
+  }
+  if (a.push.nranks > 0) {   // (the barrier above published the W1s staging)
+    const int parity = (int)((*a.push.epoch + 1u) & 1u);
+    for (int i = tid; i < CC * HD / 4; i += kGThreads) {
+      const int row = i / (HD / 4), c4 = (i - row * (HD / 4)) * 4;
+      xg_push_store4(a.push, parity, a.push.off + (long long)(p * CC + row) * HD + c4,
+                     *reinterpret_cast<const float4*>(W1s + row * F::RG + c4));
+    }
+    xg_push_drain();   // acknowledged before the wave ends
   }
   stamp(a.stamps, 7);
   }
@@ -679,17 +704,21 @@ TDE_API int tde_cgen_fwd(int CC, int HD, const float* x, const float* wc, const 
 // iterations (nullable) advanced by one.  opt (nullable): the fused step — dW1 applied to the Dense kernel in
 // place by the optimizer instead of stored (dW1 may then be null).  crep / crep_stride: conv-gradient replicas.
 // arrive (nullable, zero-initialised int): the last workgroup applies fconv and frest (unconditional updates).
+// push (nullable; plain step): dW1 into the xGMI owners' contribution areas instead of dW1.
 TDE_API int tde_cgen_bwd(int CC, int HD, const float* x, const void* amax, int lda, const float* hpre, float* hzero,
                          int hrep, long long hrep_stride, const float* b1, const float* W2, const float* b2, int C,
                          int pre_relu, const int* labels, float scale, float* metrics, const float* W1, const float* Pt,
                          int ldPt, float* dW1, float* dwc, float* dbc, float* dW2, float* db2, float* db1,
                          long long* iterations, const TdeCgenOpt* opt, long long* stamps, int crep,
                          long long crep_stride, const FlatApply* fconv, const FlatApply* frest, unsigned* arrive,
-                         int B, int H, int W, hipStream_t stream) {
+                         const XgPush* push, int B, int H, int W, hipStream_t stream) {
   if (!tde_cgen_supported(CC, HD) || C < 1 || C > 16 || W > 32 || (W & 3)) return -1;
   if (opt && (!opt->w || (opt->kind != kOptSGD && !opt->m) || (opt->kind == kOptAdam && (!opt->v || !opt->iterations))))
     return -3;
   if (crep < 1 || crep > 64 || (crep > 1 && crep_stride < 10LL * CC)) return -4;
+  if (push && push->nranks > 0 &&
+      (opt || push->nranks > kXgMaxRanks || push->L <= 0 || (push->L & 3) || (push->off & 3) || !push->epoch))
+    return -6;
   if (arrive && (!fconv || !frest || !opt || fconv->pend || frest->pend || fconv->grep > kMaxGrep ||
                  frest->grep > kMaxGrep || fconv->nr > kFlatRanges || frest->nr > kFlatRanges))
     return -5;
@@ -700,6 +729,7 @@ TDE_API int tde_cgen_bwd(int CC, int HD, const float* x, const void* amax, int l
   const int P = ((H - 2) / 2) * ((W - 2) / 2);
   GBwdArgs a{x, (const uint64_t*)amax, lda, hpre, hzero, hrep, hrep_stride, b1, W2, b2, C, pre_relu, labels, scale,
              metrics, W1, Pt, ldPt, dW1, dwc, dbc, dW2, db2, db1, iterations, opt ? *opt : TdeCgenOpt{}, opt != nullptr, stamps,
-             crep, crep_stride, fconv ? *fconv : FlatApply{}, frest ? *frest : FlatApply{}, arrive, B, H, W};
+             crep, crep_stride, fconv ? *fconv : FlatApply{}, frest ? *frest : FlatApply{}, arrive,
+             push ? *push : XgPush{}, B, H, W};
   TDE_CGEN_DISPATCH(launch_bwd, CC, HD, a, P, stream)
 }

@@ -312,7 +312,8 @@ def cgen_fwd(x, wc, bc, W1, hpre, Pt, amax, *, B, inc_iter=None):
 
 def cgen_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, metrics, W1, Pt, dW1, dwc, dbc,
              dW2=None, db2=None, db1=None, B, iterations=None, opt: CgenOpt | None = None, stamps=None, crep=1,
-             crep_stride=0, fconv: FlatApply | None = None, frest: FlatApply | None = None, arrive=None):
+             crep_stride=0, fconv: FlatApply | None = None, frest: FlatApply | None = None, arrive=None,
+             push: XgPush | None = None):
     """Generic-width fused small-CNN backward, float32 (plain step): from hpre [R, >=B, HD] every workgroup
     recomputes the head, then the Dense(HD) weight / input gradients and the conv gradients; hzero (the
     other parity) is zeroed.  dW1 stored, dwc / dbc atomically added, dW2 / db2 / db1 added, metrics added,
@@ -321,7 +322,8 @@ def cgen_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, metri
     clocks per workgroup.  ``crep`` > 1: workgroup x adds its conv gradients into replica x % crep of dwc / dbc
     (``crep_stride`` elements apart), summed by the consumer.  ``arrive`` (fused step; an int32 device counter,
     zero between launches): the workgroup that finishes last applies ``fconv`` and ``frest`` (unconditional
-    ``FlatApply`` updates of the small variables) once every other workgroup is done reading them."""
+    ``FlatApply`` updates of the small variables) once every other workgroup is done reading them.  ``push``
+    (plain step under the xGMI communicator): dW1 into the owners' windows of the next all-reduce call."""
     H, W = x.shape[1], x.shape[2]
     CC = dwc.shape[-1]
     Pn = ((H - 2) // 2) * ((W - 2) // 2)
@@ -344,7 +346,8 @@ def cgen_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, metri
                               _P(db2), _P(db1), _P(iterations), _ct.byref(opt) if opt is not None else None,
                               _P(stamps), int(crep), int(crep_stride),
                               _ct.byref(fconv) if fconv is not None else None,
-                              _ct.byref(frest) if frest is not None else None, _P(arrive), B, H, W, _s())
+                              _ct.byref(frest) if frest is not None else None, _P(arrive),
+                              _ct.byref(push) if push is not None else None, B, H, W, _s())
     N.check(rc, "tde_cgen_bwd")
 
 

@@ -697,7 +697,8 @@ class ConvNetGenPlan(ReplicaPlan):
     followed, by step mode, by the multi-tensor optimizer ("plain"), nothing ("local": each backward
     workgroup applies the optimizer to the Dense(U) rows it owns in place — no other workgroup of the launch
     reads them — and the workgroup that finishes last updates the conv layer, from its gradient replicas, and
-    the head: two launches per step), or the xGMI all-reduce that applies it ("xgmi").  The reference's own
+    the head: two launches per step), or the xGMI all-reduce that applies it ("xgmi"; the backward pushes the
+    Dense(U) gradient rows straight into the owners' windows: the fused exchange).  The reference's own
     Conv2D(32)/Dense(64) keeps the hand-tuned ``ConvNetPlan`` (deferred conv update, fused exchange)."""
     kind = "fused_convnet_generic"
 
@@ -728,6 +729,7 @@ class ConvNetGenPlan(ReplicaPlan):
         self.opt = OptimizerKernel(store, optimizer, {}, self.iterations) if optimizer is not None else None
         self.parity = 0
         self._copt = self._rest = self._conv_apply = None
+        self._push, self._pushed = None, False
         # conv gradients: the ~170 backward workgroups add theirs into crep replicas of the conv segments
         # (workgroup x -> replica x % crep; same-address float atomics from every workgroup serialise at the
         # memory side), summed by the consumer — the fused step's small update or the xGMI all-reduce
@@ -764,6 +766,8 @@ class ConvNetGenPlan(ReplicaPlan):
     def set_step_mode(self, mode):
         super().set_step_mode(mode)
         self._copt = self._rest = self._conv_apply = None
+        if mode != "xgmi":
+            self._push = None
         self.gconv.zero_()
         self.arrive.zero_()
         if mode != "local":
@@ -792,6 +796,17 @@ class ConvNetGenPlan(ReplicaPlan):
         # the launch descriptors carry lr / hyper-parameters by value
         if self.step_mode == "local" and self._opt_key_set != self._opt_key():
             self.set_step_mode("local")
+
+    def push_range(self):
+        """Bucket range the backward can push into the xGMI owners itself: the Dense(U) kernel's gradient."""
+        seg = self.store.segments[self.names["w1"]]
+        return seg.offset, seg.offset + seg.numel
+
+    def set_push(self, spec):
+        """Fused data-parallel exchange (step mode "xgmi"): ``spec`` is the communicator's ``XgPush``."""
+        if spec is not None and self.step_mode != "xgmi":
+            raise ValueError("the fused exchange needs step mode 'xgmi'")
+        self._push = spec
 
     def xg_apply_spec(self):
         spec = f32_xg_apply_spec(self)
@@ -831,13 +846,15 @@ class ConvNetGenPlan(ReplicaPlan):
         K.cgen_fwd(x, self._v("wc"), self._v("bc"), self.W1, self.hpre2[q], self.Pt, self.amax, B=B,
                    inc_iter=self.iterations if local else None)
         dwc, dbc, crep, cstride = self._conv_grads()
+        push = self._push if self.step_mode == "xgmi" else None
         K.cgen_bwd(x, self.amax, self.hpre2[q], self.hpre2[1 - q], self._v("b1"), self._v("w2"), self._v("b2"), y,
                    scale=self.scale, pre_relu=self.pre_relu, metrics=self.metrics, W1=self.W1, Pt=self.Pt,
                    dW1=None if local else self._g("w1"), dwc=dwc.view(self._v("wc").shape), dbc=dbc, dW2=self._g("w2"),
                    db2=self._g("b2"), db1=self._g("b1"), B=B, iterations=None if local else self.iterations,
                    opt=self._copt if local else None, crep=crep, crep_stride=cstride,
                    fconv=self._conv_apply if local else None, frest=self._rest if local else None,
-                   arrive=self.arrive if local else None)
+                   arrive=self.arrive if local else None, push=push)
+        self._pushed = push is not None
         self.parity = 1 - q
 
     def apply(self):

@@ -206,20 +206,23 @@ def test_n_replicas_equal_one_replica_at_the_same_global_batch(layout, mode, tmp
         np.testing.assert_allclose(w[k], cpu_oracle[k], rtol=RTOL, atol=ATOL, err_msg=f"{layout} ({mode}): {k}")
 
 
-@pytest.mark.parametrize("layout", ["mirrored", "mwms"])
-def test_generic_fused_plan_data_parallel_matches_oracle(layout, tmp_path):
+@pytest.mark.parametrize("layout,push", [("mirrored", "1"), ("mwms", "1"), ("mirrored", "0")])
+def test_generic_fused_plan_data_parallel_matches_oracle(layout, push, tmp_path):
     """Model A at Conv2D(64)/Dense(128) on the generic fused plan (csrc/kernels/convnet_gen.hip): one replica
     (step mode "local": the Dense rows updated inside the backward) and 2 replicas (Mirrored in one process /
-    MWMS over 2 processes, the update fused into the xGMI all-reduce) both follow the torch float32 CPU
-    oracle over 12 steps at global batch 128, replicas bit-identical."""
+    MWMS over 2 processes, the update fused into the xGMI all-reduce; the backward pushing the Dense gradient
+    rows into the owners' windows, or TDE_XGMI_PUSH=0 the all-reduce pushing them) both follow the torch
+    float32 CPU oracle over 12 steps at global batch 128, replicas bit-identical."""
     oracle, line0 = _equiv(tmp_path, "cpu_wide", ["--strategy", "single", "--cpu", "--model", "mnist_cnn_wide"])
     assert "plan=reference" in line0, line0
     one, line1 = _equiv(tmp_path, "single_wide", ["--strategy", "single", "--model", "mnist_cnn_wide"])
     assert "plan=fused_convnet_generic" in line1 and "step_mode=local" in line1 and "graph=True" in line1, line1
     args, env, nproc = LAYOUTS[layout]
-    w, line = _equiv(tmp_path, f"{layout}_wide", args + ["--model", "mnist_cnn_wide"], env, nproc)
+    w, line = _equiv(tmp_path, f"{layout}_wide", args + ["--model", "mnist_cnn_wide"],
+                     dict(env or {}, TDE_XGMI_PUSH=push), nproc)
     assert "plan=fused_convnet_generic" in line and "replicas_identical=True" in line and "step_mode=xgmi" in line, \
         line
+    assert ("exchange=fused_push" if push == "1" else "exchange=post_backward") in line, line
     for k in oracle:
         np.testing.assert_allclose(one[k], oracle[k], rtol=RTOL, atol=ATOL, err_msg=f"single: {k}")
         np.testing.assert_allclose(w[k], oracle[k], rtol=RTOL, atol=ATOL, err_msg=f"{layout}: {k}")
