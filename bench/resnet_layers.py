@@ -42,6 +42,7 @@ def main():
     from tensorflow_distributed_example_amd.ops import layer_ops as O
     from tensorflow_distributed_example_amd.train import layerwise as LW
     torch.cuda.set_device(0)
+    tde.backend.set_global_policy("mixed_bfloat16")   # ResNet-18's BASELINE config (the bf16 kernel forms)
     tde.backend.set_random_seed(0)
     m = tde.zoo.resnet18()
     m.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True), optimizer=tde.optimizers.SGD(0.1))
