@@ -709,6 +709,10 @@ class ConvNetGenPlan(ReplicaPlan):
         c, d1, d2 = pattern["conv"], pattern["dense1"], pattern["dense2"]
         if not K.cgen_supported(c.filters, d1.units):
             raise NotImplementedError(f"convnet_gen: Conv2D({c.filters}) + Dense({d1.units}) not instantiated")
+        if os.environ.get("TDE_DETERMINISTIC", "0") not in ("", "0"):
+            import warnings
+            warnings.warn("TDE_DETERMINISTIC: the generic-width fused CNN step adds its split-K and conv-gradient "
+                          "partials with float atomics; its steps are not bitwise reproducible")
         self.H, self.W, self.C = c.input_shape[0], c.input_shape[1], c.filters
         self.P = ((self.H - 2) // 2) * ((self.W - 2) // 2)
         self.Hd, self.Cls = d1.units, d2.units
@@ -835,7 +839,10 @@ class ConvNetGenPlan(ReplicaPlan):
         return None if nm is None else self.store.grad(nm)
 
     def on_weights_loaded(self):
+        # loaded weights replace whatever gradients were outstanding
         self.store.g.zero_()
+        self.gconv.zero_()
+        self.arrive.zero_()
 
     def train_step(self, x, y, B=None):
         K = self.K
