@@ -106,6 +106,7 @@ def match_bncnn(model, loss):
             return None
         ls = ls[1:]
     convs, i = [], 0
+    too_wide = []   # the family's structure with widths past the fused kernels' limits: said, not silent
 
     def bn_relu(j):
         return (j + 1 < len(ls) and isinstance(ls[j], L.BatchNormalization) and isinstance(ls[j + 1], L.Activation)
@@ -115,18 +116,24 @@ def match_bncnn(model, loss):
         c = ls[i]
         if c.use_bias or c.activation not in (None, "linear") or not bn_relu(i + 1):
             return None
-        if c.input_shape is None or len(c.input_shape) != 3 or c.input_shape[-1] > 32 or c.filters > 32:
+        if c.input_shape is None or len(c.input_shape) != 3:
             return None
+        if c.input_shape[-1] > 32 or c.filters > 32:
+            too_wide.append(f"{c.name}: {c.input_shape[-1]} -> {c.filters} channels (<= 32)")
         convs.append((c, ls[i + 1]))
         i += 3
-    if not convs or len(convs) > 3 or i >= len(ls) or not isinstance(ls[i], L.Flatten):
+    if not convs or i >= len(ls) or not isinstance(ls[i], L.Flatten):
         return None
+    if len(convs) > 3:
+        too_wide.append(f"{len(convs)} conv blocks (<= 3)")
     i += 1
     if i >= len(ls) or not isinstance(ls[i], L.Dense):
         return None
     d = ls[i]
-    if d.use_bias or d.activation not in (None, "linear") or not bn_relu(i + 1) or d.units > 256:
+    if d.use_bias or d.activation not in (None, "linear") or not bn_relu(i + 1):
         return None
+    if d.units > 256:
+        too_wide.append(f"{d.name}: {d.units} units (<= 256)")
     bn_d = ls[i + 1]
     i += 3
     drop = None
@@ -136,9 +143,16 @@ def match_bncnn(model, loss):
     if i != len(ls) - 1 or not isinstance(ls[i], L.Dense):
         return None
     head = ls[i]
-    if not head.use_bias or head.units > 16 or head.activation not in (None, "linear", "softmax"):
+    if not head.use_bias or head.activation not in (None, "linear", "softmax"):
         return None
     if (head.activation == "softmax") == bool(loss.from_logits):
+        return None
+    if head.units > 16:
+        too_wide.append(f"{head.name}: {head.units} classes (<= 16)")
+    if too_wide:
+        import warnings
+        warnings.warn(f"model {model.name!r}: no fused BN-CNN step ({'; '.join(too_wide)}); running the per-layer "
+                      "kernel plan")
         return None
     return dict(convs=convs, dense=(d, bn_d, drop), head=head)
 

@@ -46,3 +46,21 @@ def test_generic_widths_take_the_generic_plan(filters, units):
 def test_unfused_widths_warn_with_the_reason(filters, units, policy, H, W, classes, why):
     pat, warns = _match(filters, units, policy, H, W, classes)
     assert pat is None and len(warns) == 1 and why in warns[0] and "per-layer kernel plan" in warns[0], warns
+
+
+def test_bncnn_family_near_miss_warns():
+    """Model B (mnist_keras_distributed.py:79-109) matches the fused BN-CNN step silently; its doubled widths
+    (48 filters, Dense(400)) fall back to the per-layer plan with a warning that names the limits."""
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.train import bncnn
+    for mult, fused in ((1, True), (2, False)):
+        m = tde.zoo.mnist_bn_cnn(mult=mult)
+        loss = tde.losses.SparseCategoricalCrossentropy()
+        with warnings.catch_warnings(record=True) as rec:
+            warnings.simplefilter("always")
+            spec = bncnn.match_bncnn(m, loss)
+        msgs = [str(w.message) for w in rec]
+        if fused:
+            assert spec is not None and not msgs, msgs
+        else:
+            assert spec is None and len(msgs) == 1 and "48 channels" in msgs[0] and "400 units" in msgs[0], msgs
