@@ -37,12 +37,34 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 
 __host__ __device__ constexpr int xr_stride(int W) { return XRW * W + ((2 - (XRW * W) % 64) + 64) % 64; }
 
+}  // namespace cgen
+}  // namespace tde
+
+// Fused step, forward side (ops/kernels.py CgenFly): the previous step's conv update applied on the fly
+// while *pend (its gradient: grep replicas gwc / gbc + r * grep_stride; the slots at the conv elements;
+// Adam's t = *iter_prev), and the head variables copied into the snapshot the backward's trunk reads.
+struct TdeCgenFly {
+  int kind;
+  float lr, mom, b1, b2, eps;
+  const int* pend;
+  const float* gwc; const float* gbc; int grep; long long grep_stride;
+  const float* mwc; const float* mbc; const float* vwc; const float* vbc;
+  const long long* iter_prev;
+  const float* sb1; const float* sw2; const float* sb2;   // head sources (b1 nullable)
+  float* hsnap; int hC;                                     // [b1 HD | W2 HD*hC | b2 hC]
+};
+
+namespace tde {
+namespace cgen {
+
 struct GFwdArgs {
   const float* x; const float* wc; const float* bc; const float* W1;
   float* hpre; int hrep; long long hrep_stride;
   float* Pt; int ldPt;
   uint64_t* amax; int lda;
   long long* inc_iter;   // step counter advanced by block (0, 0) (nullable; the fused step's, read by the backward)
+  TdeCgenFly fly;
+  int fly_on;
   int B, H, W;
 };
 
@@ -91,7 +113,42 @@ __global__ __launch_bounds__(256) void cgen_fwd_kernel(GFwdArgs a) {
     d[0] = float2{v.x, v.y};
     d[1] = float2{v.z, v.w};
   }
-  for (int i = tid; i < 10 * CC; i += 256) wcs[i] = i < 9 * CC ? a.wc[i] : a.bc[i - 9 * CC];
+  {
+    // the conv weights in effect: with the previous step's update (pending) applied on the fly
+    const TdeCgenFly& f = a.fly;
+    const bool fly = a.fly_on && *f.pend;
+    const OptHyper hy{f.kind, f.lr, f.mom, f.b1, f.b2, f.eps};
+    const float lr_t = fly ? opt_lr_t(hy, f.kind == kOptAdam ? *f.iter_prev : 0) : 0.f;
+    for (int i = tid; i < 10 * CC; i += 256) {
+      const bool isb = i >= 9 * CC;
+      const int j = isb ? i - 9 * CC : i;
+      float w = isb ? a.bc[j] : a.wc[j];
+      if (fly) {
+        const float* gp = isb ? f.gbc + j : f.gwc + j;
+        float gv[kMaxGrep];
+#pragma unroll
+        for (int r = 0; r < kMaxGrep; ++r) gv[r] = (r == 0 || r < f.grep) ? gp[r * f.grep_stride] : 0.f;
+        float g = gv[0];
+#pragma unroll
+        for (int r = 1; r < kMaxGrep; ++r) g += gv[r];
+        float m = 0.f, v = 0.f;
+        if (f.kind != kOptSGD) m = isb ? f.mbc[j] : f.mwc[j];
+        if (f.kind == kOptAdam) v = isb ? f.vbc[j] : f.vwc[j];
+        w = opt_step(hy, lr_t, w, g, m, v);
+      }
+      wcs[i] = w;
+    }
+    if (a.fly_on && blockIdx.x == 0 && blockIdx.y == 0) {   // the head as of this step, for the backward's trunk
+      const int nh = HD + HD * f.hC + f.hC;
+      for (int i = tid; i < nh; i += 256) {
+        float v;
+        if (i < HD) v = f.sb1 ? f.sb1[i] : 0.f;
+        else if (i < HD + HD * f.hC) v = f.sw2[i - HD];
+        else v = f.sb2[i - HD - HD * f.hC];
+        f.hsnap[i] = v;
+      }
+    }
+  }
   lds_barrier();
 
   // conv + bias + ReLU + 2x2 max-pool: lane = image, wave = channel groups of 8
@@ -181,6 +238,18 @@ struct TdeCgenOpt {
   const long long* iterations;
 };
 
+// Fused step, the backward's head workgroup (ops/kernels.py CgenHead): flat buffers w / m / v, the head's
+// element offsets (off_b1 < 0: no bias), t = *iterations; *pend_set = 1 and *iter_prev = t at the end.
+struct TdeCgenHead {
+  int kind;
+  float lr, mom, b1, b2, eps;
+  float* w; float* m; float* v;
+  long long off_w2, off_b2, off_b1;
+  const long long* iterations;
+  int* pend_set;
+  long long* iter_prev;
+};
+
 namespace tde {
 namespace cgen {
 
@@ -201,11 +270,12 @@ struct GBwdArgs {
   // float atomics per value serialise at the memory side; the consumer sums the replicas
   int crep;
   long long crep_stride;
-  // fused step: the workgroup that arrives last (counter *arrive, reset by it) applies the optimizer to the
-  // small variables — the conv layer from its gradient replicas (fconv) and the head (frest) — once every
-  // other workgroup of the launch is done with them
-  FlatApply fconv, frest;
-  unsigned* arrive;
+  // fused step, head workgroup: the head updated in place (the trunk reads the forward's snapshot), the
+  // previous step's conv update committed (fcommit, while *fcommit.pend; its forward applied it on the fly),
+  // this step's flagged pending
+  TdeCgenHead hopt;
+  int hopt_on;
+  FlatApply fcommit;
   // plain step under the xGMI communicator (nranks > 0): dW1 rows stored straight into the owners'
   // contribution areas of the all-reduce call that follows (the fused data-parallel exchange)
   XgPush push;
@@ -504,17 +574,50 @@ __global__ __launch_bounds__(NW * 64) void cgen_bwd_kernel(GBwdArgs a) {
       atomicAdd(a.metrics + 1, ca);
       atomicAdd(a.metrics + 2, na);
     }
+    const float db1v = tid < HD ? (db1p[tid] + db1p[HD + tid]) + (db1p[2 * HD + tid] + db1p[3 * HD + tid]) : 0.f;
+    if (a.hopt_on) {
+      // fused step: the head's update in place, then the previous step's conv update committed
+      const TdeCgenHead& o = a.hopt;
+      const OptHyper hy{o.kind, o.lr, o.mom, o.b1, o.b2, o.eps};
+      const long long t = *o.iterations;
+      const float lr_t = opt_lr_t(hy, t);
+      auto upd = [&](long long e, float g) {
+        float m = o.kind != kOptSGD ? o.m[e] : 0.f;
+        float v = o.kind == kOptAdam ? o.v[e] : 0.f;
+        o.w[e] = opt_step(hy, lr_t, o.w[e], g, m, v);
+        if (o.kind != kOptSGD) o.m[e] = m;
+        if (o.kind == kOptAdam) o.v[e] = v;
+      };
 #pragma unroll
-    for (int j = 0; j < F::UTW; ++j) {
-      const int ut = wave + NW * j;
-      if (ut < HD / 16 && fr < C && a.dW2)
+      for (int j = 0; j < F::UTW; ++j) {
+        const int ut = wave + NW * j;
+        if (ut < HD / 16 && fr < C)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) atomicAdd(a.dW2 + (size_t)(ut * 16 + fq * 4 + i) * C + fr, gw[j][i]);
+          for (int i = 0; i < 4; ++i) upd(o.off_w2 + (long long)(ut * 16 + fq * 4 + i) * C + fr, gw[j][i]);
+      }
+      if (tid < C) upd(o.off_b2 + tid, db2acc);
+      if (tid < HD && o.off_b1 >= 0) upd(o.off_b1 + tid, db1v);
+      __shared__ int s_cp;
+      if (tid == 0) s_cp = *a.fcommit.pend;
+      __syncthreads();
+      if (s_cp) flat_apply(a.fcommit, t - 1, tid, kGThreads);
+      __syncthreads();
+      if (tid == 0) {
+        if (s_cp) *a.fcommit.pend = 0;
+        *o.pend_set = 1;
+        *o.iter_prev = t;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < F::UTW; ++j) {
+        const int ut = wave + NW * j;
+        if (ut < HD / 16 && fr < C && a.dW2)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) atomicAdd(a.dW2 + (size_t)(ut * 16 + fq * 4 + i) * C + fr, gw[j][i]);
+      }
+      if (tid < C && a.db2) atomicAdd(a.db2 + tid, db2acc);
+      if (tid < HD && a.db1) atomicAdd(a.db1 + tid, db1v);
     }
-    // (single writer: atomics only so that the fused step's last workgroup reads them without a release fence)
-    if (tid < C && a.db2) atomicAdd(a.db2 + tid, db2acc);
-    if (tid < HD && a.db1)
-      atomicAdd(a.db1 + tid, (db1p[tid] + db1p[HD + tid]) + (db1p[2 * HD + tid] + db1p[3 * HD + tid]));
     if (tid == 0 && a.iterations) a.iterations[0] += 1;
   } else {
 
@@ -594,25 +697,6 @@ __global__ __launch_bounds__(NW * 64) void cgen_bwd_kernel(GBwdArgs a) {
   }
   stamp(a.stamps, 7);
   }
-
-  if (a.arrive) {
-    // Every gradient this update reads was added with device-scope atomics (performed at the memory side, no
-    // dirty L2 line to write back): each thread waits until its own are performed, then the workgroup counts
-    // itself in; the last one drops its L2's stale lines (acquire) and updates.  A device-scope release
-    // fence here would write back every workgroup's L2 (the Dense rows it just stored): +40 % step time.
-    __shared__ int s_last;
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (tid == 0) s_last = atomicAdd(a.arrive, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (s_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      const long long t = a.fconv.h.kind == kOptAdam ? *a.fconv.iterations : 0;
-      flat_apply(a.fconv, t, tid, kGThreads);
-      flat_apply(a.frest, t, tid, kGThreads);
-      if (tid == 0) *a.arrive = 0u;
-    }
-  }
 }
 
 template <int CC, int HD>
@@ -685,17 +769,23 @@ TDE_API int tde_cgen_supported(int CC, int HD) {
 }
 
 // Forward (see the header).  x [B][H][W] f32 (C_in = 1), wc [9][CC], bc [CC], W1 [P*CC][HD] f32 master,
-// hpre [hrep][>=B][HD] (+=), Pt [P*CC][ldPt], amax [P][CC/8][lda] (8 argmax bytes per u64).
+// hpre [hrep][>=B][HD] (+=), Pt [P*CC][ldPt], amax [P][CC/8][lda] (8 argmax bytes per u64).  fly (nullable):
+// the fused step's deferred conv update and head snapshot (TdeCgenFly).
 TDE_API int tde_cgen_fwd(int CC, int HD, const float* x, const float* wc, const float* bc, const float* W1,
                          float* hpre, int hrep, long long hrep_stride, float* Pt, int ldPt, void* amax, int lda,
-                         long long* inc_iter, int B, int H, int W, hipStream_t stream) {
+                         long long* inc_iter, const TdeCgenFly* fly, int B, int H, int W, hipStream_t stream) {
   if (!tde_cgen_supported(CC, HD) || (W & 3) || W > 32 || H < 4 || W < 4 || ((H - 2) & 1) || ((W - 2) & 1))
     return -1;
+  if (fly && (!fly->pend || !fly->gwc || !fly->gbc || fly->grep < 1 || fly->grep > kMaxGrep || !fly->iter_prev ||
+              (fly->kind != kOptSGD && (!fly->mwc || !fly->mbc)) || (fly->kind == kOptAdam && (!fly->vwc || !fly->vbc)) ||
+              !fly->sw2 || !fly->sb2 || !fly->hsnap || fly->hC < 1 || fly->hC > 16))
+    return -3;
   if (!x || !wc || !bc || !W1 || !hpre || !Pt || !amax || (ldPt & 7) || ldPt < B || lda < B || hrep < 1 ||
       (hrep > 1 && hrep_stride < (long long)B * HD) || ((uintptr_t)x & 15) || ((uintptr_t)W1 & 15))
     return -2;
   const int P = ((H - 2) / 2) * ((W - 2) / 2);
-  GFwdArgs a{x, wc, bc, W1, hpre, hrep, hrep_stride, Pt, ldPt, (uint64_t*)amax, lda, inc_iter, B, H, W};
+  GFwdArgs a{x, wc, bc, W1, hpre, hrep, hrep_stride, Pt, ldPt, (uint64_t*)amax, lda, inc_iter,
+             fly ? *fly : TdeCgenFly{}, fly != nullptr, B, H, W};
   TDE_CGEN_DISPATCH(launch_fwd, CC, HD, a, P, stream)
 }
 
@@ -703,14 +793,15 @@ TDE_API int tde_cgen_fwd(int CC, int HD, const float* x, const float* wc, const 
 // stored, dwc [9][CC] / dbc [CC] atomically added, dW2 [HD][C] / db2 [C] / db1 [HD] added (nullable);
 // iterations (nullable) advanced by one.  opt (nullable): the fused step — dW1 applied to the Dense kernel in
 // place by the optimizer instead of stored (dW1 may then be null).  crep / crep_stride: conv-gradient replicas.
-// arrive (nullable, zero-initialised int): the last workgroup applies fconv and frest (unconditional updates).
+// hopt + fcommit (nullable, with opt): the fused step's head update in the head workgroup and the commit of the
+// previous step's conv update (b1 / W2 / b2 are then the forward's snapshot).
 // push (nullable; plain step): dW1 into the xGMI owners' contribution areas instead of dW1.
 TDE_API int tde_cgen_bwd(int CC, int HD, const float* x, const void* amax, int lda, const float* hpre, float* hzero,
                          int hrep, long long hrep_stride, const float* b1, const float* W2, const float* b2, int C,
                          int pre_relu, const int* labels, float scale, float* metrics, const float* W1, const float* Pt,
                          int ldPt, float* dW1, float* dwc, float* dbc, float* dW2, float* db2, float* db1,
                          long long* iterations, const TdeCgenOpt* opt, long long* stamps, int crep,
-                         long long crep_stride, const FlatApply* fconv, const FlatApply* frest, unsigned* arrive,
+                         long long crep_stride, const TdeCgenHead* hopt, const FlatApply* fcommit,
                          const XgPush* push, int B, int H, int W, hipStream_t stream) {
   if (!tde_cgen_supported(CC, HD) || C < 1 || C > 16 || W > 32 || (W & 3)) return -1;
   if (opt && (!opt->w || (opt->kind != kOptSGD && !opt->m) || (opt->kind == kOptAdam && (!opt->v || !opt->iterations))))
@@ -719,8 +810,9 @@ TDE_API int tde_cgen_bwd(int CC, int HD, const float* x, const void* amax, int l
   if (push && push->nranks > 0 &&
       (opt || push->nranks > kXgMaxRanks || push->L <= 0 || (push->L & 3) || (push->off & 3) || !push->epoch))
     return -6;
-  if (arrive && (!fconv || !frest || !opt || fconv->pend || frest->pend || fconv->grep > kMaxGrep ||
-                 frest->grep > kMaxGrep || fconv->nr > kFlatRanges || frest->nr > kFlatRanges))
+  if (hopt && (!opt || !fcommit || !fcommit->pend || fcommit->grep > kMaxGrep || fcommit->nr > kFlatRanges ||
+               !hopt->w || (hopt->kind != kOptSGD && !hopt->m) || (hopt->kind == kOptAdam && !hopt->v) ||
+               !hopt->iterations || !hopt->pend_set || !hopt->iter_prev))
     return -5;
   if (!x || !amax || !hpre || !hzero || !W2 || !b2 || !labels || !W1 || !Pt || (!dW1 && !opt) || !dwc || !dbc ||
       (ldPt & 7) || ldPt < B || lda < B || hrep < 1 || (hrep > 1 && (hrep_stride < (long long)B * HD || (hrep_stride & 3))) ||
@@ -729,7 +821,7 @@ TDE_API int tde_cgen_bwd(int CC, int HD, const float* x, const void* amax, int l
   const int P = ((H - 2) / 2) * ((W - 2) / 2);
   GBwdArgs a{x, (const uint64_t*)amax, lda, hpre, hzero, hrep, hrep_stride, b1, W2, b2, C, pre_relu, labels, scale,
              metrics, W1, Pt, ldPt, dW1, dwc, dbc, dW2, db2, db1, iterations, opt ? *opt : TdeCgenOpt{}, opt != nullptr, stamps,
-             crep, crep_stride, fconv ? *fconv : FlatApply{}, frest ? *frest : FlatApply{}, arrive,
+             crep, crep_stride, hopt ? *hopt : TdeCgenHead{}, hopt != nullptr, fcommit ? *fcommit : FlatApply{},
              push ? *push : XgPush{}, B, H, W};
   TDE_CGEN_DISPATCH(launch_bwd, CC, HD, a, P, stream)
 }

@@ -284,15 +284,35 @@ class CgenOpt(_ct.Structure):
                 ("iterations", _ct.c_void_p)]
 
 
+class CgenFly(_ct.Structure):
+    """``TdeCgenFly`` (csrc/kernels/convnet_gen.hip): the generic fused step's forward side — the previous
+    step's conv update applied on the fly while ``*pend``, and the head snapshot."""
+    _fields_ = [("kind", _ct.c_int), ("lr", _ct.c_float), ("mom", _ct.c_float), ("b1", _ct.c_float), ("b2", _ct.c_float),
+                ("eps", _ct.c_float), ("pend", _ct.c_void_p), ("gwc", _ct.c_void_p), ("gbc", _ct.c_void_p),
+                ("grep", _ct.c_int), ("grep_stride", _ct.c_longlong), ("mwc", _ct.c_void_p), ("mbc", _ct.c_void_p),
+                ("vwc", _ct.c_void_p), ("vbc", _ct.c_void_p), ("iter_prev", _ct.c_void_p), ("sb1", _ct.c_void_p),
+                ("sw2", _ct.c_void_p), ("sb2", _ct.c_void_p), ("hsnap", _ct.c_void_p), ("hC", _ct.c_int)]
+
+
+class CgenHead(_ct.Structure):
+    """``TdeCgenHead`` (csrc/kernels/convnet_gen.hip): the generic fused step's head update in the backward's
+    head workgroup (flat buffers + the head's element offsets)."""
+    _fields_ = [("kind", _ct.c_int), ("lr", _ct.c_float), ("mom", _ct.c_float), ("b1", _ct.c_float), ("b2", _ct.c_float),
+                ("eps", _ct.c_float), ("w", _ct.c_void_p), ("m", _ct.c_void_p), ("v", _ct.c_void_p),
+                ("off_w2", _ct.c_longlong), ("off_b2", _ct.c_longlong), ("off_b1", _ct.c_longlong),
+                ("iterations", _ct.c_void_p), ("pend_set", _ct.c_void_p), ("iter_prev", _ct.c_void_p)]
+
+
 def cgen_supported(filters, units):
     return bool(N.hip().tde_cgen_supported(int(filters), int(units)))
 
 
-def cgen_fwd(x, wc, bc, W1, hpre, Pt, amax, *, B, inc_iter=None):
+def cgen_fwd(x, wc, bc, W1, hpre, Pt, amax, *, B, inc_iter=None, fly: CgenFly | None = None):
     """Generic-width fused small-CNN forward, float32 (csrc/kernels/convnet_gen.hip): Conv2D(CC, 3x3) + ReLU +
     MaxPool(2) + the Dense(HD) matmul, hpre [R, >=B, HD] += (workgroup i adds into replica i % R).
     W1 the f32 master kernel [P*CC, HD]; Pt [P*CC, ldPt] f32; amax int64 [P, CC/8, lda]; inc_iter (int64 step
-    counter, nullable) advanced by one."""
+    counter, nullable) advanced by one; ``fly`` (fused step): the deferred conv update applied on the fly and the
+    head snapshot."""
     H, W = x.shape[1], x.shape[2]
     CC = wc.shape[-1]
     Pn = ((H - 2) // 2) * ((W - 2) // 2)
@@ -306,13 +326,14 @@ def cgen_fwd(x, wc, bc, W1, hpre, Pt, amax, *, B, inc_iter=None):
          "cgen_fwd: Pt")
     _req(amax.dtype == torch.int64 and amax.shape[:2] == (Pn, CC // 8) and amax.shape[-1] >= B, "cgen_fwd: amax")
     rc = N.hip().tde_cgen_fwd(CC, HD, _P(x), _P(wc), _P(bc), _P(W1), _P(hpre), hp.shape[0], hp.stride(0), _P(Pt),
-                              Pt.stride(0), _P(amax), amax.shape[-1], _P(inc_iter), B, H, W, _s())
+                              Pt.stride(0), _P(amax), amax.shape[-1], _P(inc_iter),
+                              _ct.byref(fly) if fly is not None else None, B, H, W, _s())
     N.check(rc, "tde_cgen_fwd")
 
 
 def cgen_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, metrics, W1, Pt, dW1, dwc, dbc,
              dW2=None, db2=None, db1=None, B, iterations=None, opt: CgenOpt | None = None, stamps=None, crep=1,
-             crep_stride=0, fconv: FlatApply | None = None, frest: FlatApply | None = None, arrive=None,
+             crep_stride=0, hopt: CgenHead | None = None, fcommit: FlatApply | None = None,
              push: XgPush | None = None):
     """Generic-width fused small-CNN backward, float32 (plain step): from hpre [R, >=B, HD] every workgroup
     recomputes the head, then the Dense(HD) weight / input gradients and the conv gradients; hzero (the
@@ -320,9 +341,9 @@ def cgen_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, metri
     ``iterations`` (int64 step counter) advanced.  ``opt`` (fused step): dW1 is applied to W1 in place by the
     optimizer instead of stored (``dW1`` may be None).  ``stamps`` (diagnostics): int64 [P + 1, 8] phase
     clocks per workgroup.  ``crep`` > 1: workgroup x adds its conv gradients into replica x % crep of dwc / dbc
-    (``crep_stride`` elements apart), summed by the consumer.  ``arrive`` (fused step; an int32 device counter,
-    zero between launches): the workgroup that finishes last applies ``fconv`` and ``frest`` (unconditional
-    ``FlatApply`` updates of the small variables) once every other workgroup is done reading them.  ``push``
+    (``crep_stride`` elements apart), summed by the consumer.  ``hopt`` + ``fcommit`` (fused step, with ``opt``):
+    the head workgroup updates the head in place (``b1`` / ``W2`` / ``b2`` are then the forward's snapshot) and
+    commits the previous step's deferred conv update.  ``push``
     (plain step under the xGMI communicator): dW1 into the owners' windows of the next all-reduce call."""
     H, W = x.shape[1], x.shape[2]
     CC = dwc.shape[-1]
@@ -337,16 +358,15 @@ def cgen_bwd(x, amax, hpre, hzero, b1, W2, b2, labels, *, scale, pre_relu, metri
     _req(Pt.shape[0] == Pn * CC and Pt.dtype == torch.float32 and Pt.stride(0) >= B, "cgen_bwd: Pt")
     _req(amax.dtype == torch.int64 and amax.shape[:2] == (Pn, CC // 8) and amax.shape[-1] >= B, "cgen_bwd: amax")
     _req(labels.dtype == torch.int32 and labels.numel() >= B and C <= 16, "cgen_bwd: labels / classes")
-    _req(arrive is None or (arrive.dtype == torch.int32 and opt is not None and fconv is not None and
-                            frest is not None and not fconv.pend and not frest.pend), "cgen_bwd: fused small update")
+    _req(hopt is None or (opt is not None and fcommit is not None and fcommit.pend), "cgen_bwd: fused head update")
     _req(W2.is_contiguous() and b2.numel() == C and (b1 is None or b1.numel() == HD), "cgen_bwd: head variables")
     rc = N.hip().tde_cgen_bwd(CC, HD, _P(x), _P(amax), amax.shape[-1], _P(hpre), _P(hzero), hp.shape[0],
                               hp.stride(0), _P(b1), _P(W2), _P(b2), C, int(pre_relu), _P(labels), float(scale),
                               _P(metrics), _P(W1), _P(Pt), Pt.stride(0), _P(dW1), _P(dwc), _P(dbc), _P(dW2),
                               _P(db2), _P(db1), _P(iterations), _ct.byref(opt) if opt is not None else None,
                               _P(stamps), int(crep), int(crep_stride),
-                              _ct.byref(fconv) if fconv is not None else None,
-                              _ct.byref(frest) if frest is not None else None, _P(arrive),
+                              _ct.byref(hopt) if hopt is not None else None,
+                              _ct.byref(fcommit) if fcommit is not None else None,
                               _ct.byref(push) if push is not None else None, B, H, W, _s())
     N.check(rc, "tde_cgen_bwd")
 

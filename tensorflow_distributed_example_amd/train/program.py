@@ -694,12 +694,13 @@ class ConvNetGenPlan(ReplicaPlan):
                 of its pooled position, the pool / ReLU routing MFMA and the conv gradients; one extra
                 workgroup makes the head's own gradients, the metrics and the step count
 
-    followed, by step mode, by the multi-tensor optimizer ("plain"), nothing ("local": each backward
-    workgroup applies the optimizer to the Dense(U) rows it owns in place — no other workgroup of the launch
-    reads them — and the workgroup that finishes last updates the conv layer, from its gradient replicas, and
-    the head: two launches per step), or the xGMI all-reduce that applies it ("xgmi"; the backward pushes the
-    Dense(U) gradient rows straight into the owners' windows: the fused exchange).  The reference's own
-    Conv2D(32)/Dense(64) keeps the hand-tuned ``ConvNetPlan`` (deferred conv update, fused exchange)."""
+    followed, by step mode, by the multi-tensor optimizer ("plain"), nothing ("local": two launches per step —
+    each backward workgroup applies the optimizer to the Dense(U) rows it owns in place, no other workgroup of
+    the launch reading them; the head workgroup updates the head in place while the trunk reads the forward's
+    snapshot of it; the conv update is deferred: the next forward applies it on the fly, the next backward's
+    head workgroup commits it, ``finish()`` flushes the last one), or the xGMI all-reduce that applies it
+    ("xgmi"; the backward pushes the Dense(U) gradient rows straight into the owners' windows).  The
+    reference's own Conv2D(32)/Dense(64) keeps the hand-tuned ``ConvNetPlan``."""
     kind = "fused_convnet_generic"
 
     def __init__(self, model, store, device, batch, global_batch, optimizer, loss, pattern):
@@ -732,12 +733,13 @@ class ConvNetGenPlan(ReplicaPlan):
         self.W1 = store.view(self.names["w1"])
         self.opt = OptimizerKernel(store, optimizer, {}, self.iterations) if optimizer is not None else None
         self.parity = 0
-        self._copt = self._rest = self._conv_apply = None
+        self._copt = self._fly = self._hopt = self._commit = self._flush = None
         self._push, self._pushed = None, False
         # conv gradients: the ~170 backward workgroups add theirs into crep replicas of the conv segments
         # (workgroup x -> replica x % crep; same-address float atomics from every workgroup serialise at the
-        # memory side), summed by the consumer — the fused step's small update or the xGMI all-reduce
-        # (TDE_CONVNET_GREP; plain steps add straight into the gradient bucket)
+        # memory side), summed by the consumer: in the fused step the next forward (the update applied on the
+        # fly) and the next backward's head workgroup (committed), one set per step parity; under data
+        # parallelism the xGMI all-reduce (set 0).  TDE_CONVNET_GREP; plain steps add into the gradient bucket.
         seg = store.segments
         sw, sb = seg[self.names["wc"]], seg[self.names["bc"]]
         self._conv_lo = min(sw.offset, sb.offset)
@@ -745,35 +747,37 @@ class ConvNetGenPlan(ReplicaPlan):
         others = [n for n in store.order if n not in (self.names["wc"], self.names["bc"]) and
                   self._conv_lo <= seg[n].offset < self._conv_lo + self._conv_span]
         self.crep = 1 if others else max(1, min(8, int(os.environ.get("TDE_CONVNET_GREP", "8"))))
-        self.gconv = torch.zeros(self.crep, self._conv_span, dtype=torch.float32, device=dev)
-        self.arrive = torch.zeros(1, dtype=torch.int32, device=dev)   # the backward's last-workgroup counter
-        # step mode "local": the variables other than the conv layer and the Dense(U) kernel as <= 4 element
-        # ranges of the flat buffers (padding between segments carries zero gradients and zero slots)
-        excl = {self.names["w1"], self.names["wc"], self.names["bc"]}
-        segs = sorted((seg[n].offset, seg[n].numel, n) for n in store.names(trainable=True))
-        ranges = []
-        for off, numel, name in segs:
-            if name in excl:
-                ranges.append(None)
-            elif ranges and ranges[-1] is not None:
-                ranges[-1] = (ranges[-1][0], off + numel - ranges[-1][0])
-            else:
-                ranges.append((off, numel))
-        self._rest_ranges = [r for r in ranges if r is not None]
+        self.gconv = torch.zeros(2, self.crep, self._conv_span, dtype=torch.float32, device=dev)
+        # fused step: the deferred conv update's flags by parity, Adam's t of the pending update, and the head
+        # variables as of the forward ([b1 | W2 | b2]: the backward's trunk reads them while its head workgroup
+        # updates the originals)
+        self.pend = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.iter_prev = torch.zeros(1, dtype=torch.int64, device=dev)
+        C_, H_ = self.Cls, self.Hd
+        self.hsnap = torch.zeros(H_ + H_ * C_ + C_, dtype=torch.float32, device=dev)
+        self._hs_b1 = self.hsnap[:H_]
+        self._hs_w2 = self.hsnap[H_: H_ + H_ * C_].view(H_, C_)
+        self._hs_b2 = self.hsnap[H_ + H_ * C_:]
 
     def supports_step_mode(self, mode):
         if mode == "plain":
             return True
         ok = self.optimizer is not None and self.device.type == "cuda"
-        return ok and (mode == "xgmi" or mode == "local" and len(self._rest_ranges) <= 4)
+        return ok and mode in ("xgmi", "local")
+
+    def _gset(self, q, name):
+        """Replica 0 of conv variable ``name``'s gradient in parity set q."""
+        sg = self.store.segments[self.names[name]]
+        lo = self._conv_lo
+        return self.gconv[q, 0, sg.offset - lo: sg.offset - lo + sg.numel]
 
     def set_step_mode(self, mode):
         super().set_step_mode(mode)
-        self._copt = self._rest = self._conv_apply = None
+        self._copt = self._fly = self._hopt = self._commit = self._flush = None
         if mode != "xgmi":
             self._push = None
         self.gconv.zero_()
-        self.arrive.zero_()
+        self.pend.zero_()
         if mode != "local":
             return
         K, st, o = self.K, self.store, self.optimizer
@@ -781,16 +785,37 @@ class ConvNetGenPlan(ReplicaPlan):
         m = st.slot(sl[0]) if sl else None
         v = st.slot(sl[1]) if len(sl) > 1 else None
         hp = o.hparams()
-        off = st.segments[self.names["w1"]].offset
-        el = lambda t: None if t is None else t.data_ptr() + 4 * off  # noqa: E731
-        self._copt = K.CgenOpt(o.kind_id, float(o.learning_rate), hp["mom"], hp["b1"], hp["b2"], hp["eps"],
-                               el(st.w), el(m), el(v), self.iterations.data_ptr())
-        self._rest = K.flat_apply_spec(o, st.w, st.g, m, v, self.iterations, None, self._rest_ranges)
-        ca = K.flat_apply_spec(o, st.w, None, m, v, self.iterations, None, [(self._conv_lo, self._conv_span)])
-        ca.g = self.gconv.data_ptr() - 4 * self._conv_lo   # indexed with the flat offsets
-        ca.grep, ca.grep_stride = self.crep, self._conv_span
-        self._conv_apply = ca
+        seg = st.segments
+        at = lambda t, name: None if t is None or name is None else t.data_ptr() + 4 * seg[self.names[name]].offset  # noqa: E731
+        kind, lr = o.kind_id, float(o.learning_rate)
+        self._copt = K.CgenOpt(kind, lr, hp["mom"], hp["b1"], hp["b2"], hp["eps"], at(st.w, "w1"), at(m, "w1"),
+                               at(v, "w1"), self.iterations.data_ptr())
+        conv = [(self._conv_lo, self._conv_span)]
+        self._fly, self._hopt, self._commit, self._flush = [], [], [], []
+        for q in (0, 1):
+            # forward of parity q: the update of the previous step (set 1-q) on the fly, the head snapshot
+            self._fly.append(K.CgenFly(
+                kind, lr, hp["mom"], hp["b1"], hp["b2"], hp["eps"], self.pend[1 - q].data_ptr(),
+                self._gset(1 - q, "wc").data_ptr(), self._gset(1 - q, "bc").data_ptr(), self.crep, self._conv_span,
+                at(m, "wc"), at(m, "bc"), at(v, "wc"), at(v, "bc"), self.iter_prev.data_ptr(),
+                at(st.w, "b1"), at(st.w, "w2"), at(st.w, "b2"), self.hsnap.data_ptr(), self.Cls))
+            # backward of parity q: the head in place, the previous step's conv update committed, set q flagged
+            b1 = self.names["b1"]
+            self._hopt.append(K.CgenHead(
+                kind, lr, hp["mom"], hp["b1"], hp["b2"], hp["eps"], st.w.data_ptr(), K._P(m), K._P(v),
+                seg[self.names["w2"]].offset, seg[self.names["b2"]].offset, seg[b1].offset if b1 is not None else -1,
+                self.iterations.data_ptr(), self.pend[q].data_ptr(), self.iter_prev.data_ptr()))
+            for lst, qq in ((self._commit, 1 - q), (self._flush, q)):
+                f = K.flat_apply_spec(o, st.w, None, m, v, self.iterations, self.pend[qq], conv)
+                f.g = self.gconv[qq].data_ptr() - 4 * self._conv_lo   # indexed with the flat offsets
+                f.grep, f.grep_stride = self.crep, self._conv_span
+                lst.append(f)
         self._opt_key_set = self._opt_key()
+
+    def finish(self):
+        if self.step_mode == "local":
+            # only the last step's conv update can be pending (each backward commits the previous one)
+            self.K.flat_apply(self._flush[1 - self.parity])
 
     def _opt_key(self):
         o = self.optimizer
@@ -815,20 +840,23 @@ class ConvNetGenPlan(ReplicaPlan):
     def xg_apply_spec(self):
         spec = f32_xg_apply_spec(self)
         if self.crep > 1:   # the conv gradients wait in the replicas: the all-reduce sums (and zeroes) them
-            spec.rep, spec.nrep = self.gconv.data_ptr(), self.crep
+            spec.rep, spec.nrep = self.gconv[0].data_ptr(), self.crep
             spec.rep_lo, spec.rep_hi = self._conv_lo, self._conv_lo + self._conv_span
             spec.rep_stride = self._conv_span
         return spec
 
-    def _conv_grads(self):
-        """(dwc, dbc, crep, stride) the backward adds the conv gradients into."""
-        if self.step_mode == "plain" or self.crep == 1:
+    def _conv_grads(self, q):
+        """(dwc, dbc, crep, stride) the backward of parity q adds the conv gradients into."""
+        if self.step_mode == "plain" or (self.step_mode == "xgmi" and self.crep == 1):
             return self._g("wc"), self._g("bc"), 1, 0
-        seg = self.store.segments
-        sw, sb = seg[self.names["wc"]], seg[self.names["bc"]]
-        lo = self._conv_lo
-        return (self.gconv[0, sw.offset - lo: sw.offset - lo + sw.numel], self.gconv[0, sb.offset - lo: sb.offset - lo + sb.numel],
-                self.crep, self._conv_span)
+        qs = q if self.step_mode == "local" else 0
+        return self._gset(qs, "wc"), self._gset(qs, "bc"), self.crep, self._conv_span
+
+    def step_invariants(self):
+        """The deferred conv update's state between executions (step mode "local"; synchronises): nothing
+        pending, every gradient replica consumed."""
+        torch.cuda.synchronize(self.device)
+        return dict(pending=[int(v) for v in self.pend.cpu()], gconv_abs_max=float(self.gconv.abs().max()))
 
     def _v(self, key):
         nm = self.names[key]
@@ -842,7 +870,7 @@ class ConvNetGenPlan(ReplicaPlan):
         # loaded weights replace whatever gradients were outstanding
         self.store.g.zero_()
         self.gconv.zero_()
-        self.arrive.zero_()
+        self.pend.zero_()
 
     def train_step(self, x, y, B=None):
         K = self.K
@@ -851,16 +879,19 @@ class ConvNetGenPlan(ReplicaPlan):
         local = self.step_mode == "local"
         # the fused step's Adam t is read by every backward workgroup: the forward advances the counter
         K.cgen_fwd(x, self._v("wc"), self._v("bc"), self.W1, self.hpre2[q], self.Pt, self.amax, B=B,
-                   inc_iter=self.iterations if local else None)
-        dwc, dbc, crep, cstride = self._conv_grads()
+                   inc_iter=self.iterations if local else None, fly=self._fly[q] if local else None)
+        dwc, dbc, crep, cstride = self._conv_grads(q)
         push = self._push if self.step_mode == "xgmi" else None
-        K.cgen_bwd(x, self.amax, self.hpre2[q], self.hpre2[1 - q], self._v("b1"), self._v("w2"), self._v("b2"), y,
+        if local:   # the head as of this step's forward (the head workgroup updates the originals)
+            b1, w2, b2 = (self._hs_b1 if self.names["b1"] is not None else None), self._hs_w2, self._hs_b2
+        else:
+            b1, w2, b2 = self._v("b1"), self._v("w2"), self._v("b2")
+        K.cgen_bwd(x, self.amax, self.hpre2[q], self.hpre2[1 - q], b1, w2, b2, y,
                    scale=self.scale, pre_relu=self.pre_relu, metrics=self.metrics, W1=self.W1, Pt=self.Pt,
                    dW1=None if local else self._g("w1"), dwc=dwc.view(self._v("wc").shape), dbc=dbc, dW2=self._g("w2"),
                    db2=self._g("b2"), db1=self._g("b1"), B=B, iterations=None if local else self.iterations,
                    opt=self._copt if local else None, crep=crep, crep_stride=cstride,
-                   fconv=self._conv_apply if local else None, frest=self._rest if local else None,
-                   arrive=self.arrive if local else None, push=push)
+                   hopt=self._hopt[q] if local else None, fcommit=self._commit[q] if local else None, push=push)
         self._pushed = push is not None
         self.parity = 1 - q
 

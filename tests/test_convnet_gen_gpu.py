@@ -144,10 +144,11 @@ def _grads64(m, W, x, y, B):
                                                      (48, 64, "local", "adam"), (16, 128, "plain", "adam")])
 def test_generic_plan_graph_trajectory_matches_float64(filters, units, mode, kind, monkeypatch):
     """A Conv2D(filters)/Dense(units) model runs the generic fused plan in hipGraph executions of 4 steps —
-    step mode "local" (the default with one replica: the backward applies the optimizer to the Dense rows
-    each workgroup owns, one small launch updates the rest) or "plain" (TDE_FUSED_STEP=0: gradients, then
-    the multi-tensor optimizer); after each execution the weights match the float64 trajectory of the same
-    optimizer (Keras forms) at fp32 accuracy and the step counter advanced once per step."""
+    step mode "local" (the default with one replica: the Dense rows updated by the backward workgroups that own
+    them, the head by the head workgroup, the conv update deferred into the next forward / backward and flushed
+    at the end of each execution) or "plain" (TDE_FUSED_STEP=0: gradients, then the multi-tensor optimizer);
+    after each execution the weights match the float64 trajectory of the same optimizer (Keras forms) at fp32
+    accuracy, the step counter advanced once per step and nothing is left pending."""
     import tensorflow_distributed_example_amd as tde
     if mode == "plain":
         monkeypatch.setenv("TDE_FUSED_STEP", "0")
@@ -195,9 +196,10 @@ def test_generic_plan_graph_trajectory_matches_float64(filters, units, mode, kin
             tol = (1e-3 if kind == "adam" else 5e-4) if bias else (5e-5 if conv or kind == "adam" else 1e-5)
             assert _rel(st.view(n), w64[n]) < tol, (e, n, _rel(st.view(n), w64[n]))
         assert int(plan.iterations) == 4 * (e + 1)
-    if mode == "local":   # nothing left behind in the bucket or the conv-gradient replicas
-        torch.cuda.synchronize()
-        assert plan.crep > 1 and float(st.g.abs().max()) == 0.0 and float(plan.gconv.abs().max()) == 0.0
+        if mode == "local":   # after each execution: nothing pending, nothing left in the bucket or the replicas
+            iv = plan.step_invariants()
+            assert plan.crep > 1 and iv["pending"] == [0, 0] and iv["gconv_abs_max"] == 0.0, iv
+            assert float(st.g.abs().max()) == 0.0
 
 
 def test_generic_plan_fit_evaluate_predict():

@@ -217,6 +217,7 @@ def test_generic_fused_plan_data_parallel_matches_oracle(layout, push, tmp_path)
     assert "plan=reference" in line0, line0
     one, line1 = _equiv(tmp_path, "single_wide", ["--strategy", "single", "--model", "mnist_cnn_wide"])
     assert "plan=fused_convnet_generic" in line1 and "step_mode=local" in line1 and "graph=True" in line1, line1
+    assert "invariants_ok=True" in line1, line1
     args, env, nproc = LAYOUTS[layout]
     w, line = _equiv(tmp_path, f"{layout}_wide", args + ["--model", "mnist_cnn_wide"],
                      dict(env or {}, TDE_XGMI_PUSH=push), nproc)
