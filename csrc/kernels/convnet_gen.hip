@@ -295,45 +295,45 @@ struct BwdCfg {
   static constexpr int UTW = (HD / 16 + NW - 1) / NW;   // head workgroup: dW2 unit tiles per wave
   static constexpr int IPW = 64 / NW;                   // routing: images per wave
   static constexpr int HQ = HD / 4;                     // k per lane group in the dP MFMA
-  // LDS carve (bytes)
-  static constexpr int kG = 0;
-  static constexpr int kW1 = kG + 64 * RG * 4;
+  // LDS carve (bytes).  h and G share one [64][RG] tile: G overwrites h element by element (the lane that
+  // masks by h[r][j] writes G[r][j]); the head workgroup takes dW2 = h^T . dl before that.
+  static constexpr int kH = 0;
+  static constexpr int kW1 = kH + 64 * RG * 4;          // head workgroup: its db1 partials [4][HD] instead
   static constexpr int kPt = kW1 + CC * RG * 4;
   static constexpr int kXs = kPt + CC * RP * 4;
   static constexpr int kAm = kXs + 64 * 16 * 4;
-  static constexpr int kR = kAm + 64 * CC;              // head scratch | dP | conv-gradient reduction
-  static constexpr int kHs = 64 * RG * 4, kPart = 3 * 4 * 64 * 4 * 4, kDl = 64 * W2S * 4;
-  static constexpr int kHead = kHs + kPart + kDl;
-  static constexpr int kRed = NW * 10 * CC * 4;
-  static constexpr int kRBytes = kHead > kRed ? kHead : kRed;
-  static constexpr int kW2 = kR + kRBytes;
+  static constexpr int kDp = kAm + 64 * CC;
+  static constexpr int kS = kDp + 64 * DPS * 4;          // logits partials | dlogits; after the chunks the
+  static constexpr int kPart = (KG > 1 ? KG - 1 : 1) * 4 * 64 * 4 * 4, kDl = 64 * W2S * 4;   // conv-gradient
+  static constexpr int kRed = NW * 10 * CC * 4;                                                // reduction
+  static constexpr int kSBytes = kPart + kDl > kRed ? kPart + kDl : kRed;
+  static constexpr int kW2 = kS + kSBytes;
   static constexpr int kB2 = kW2 + HD * W2S * 4;
   static constexpr int kLab = kB2 + 16 * 4;
-  static constexpr int kDb1 = kLab + 64 * 4;            // head workgroup: db1 partials [4][HD]
-  static constexpr int kLds = kDb1 + 4 * HD * 4;
-  static_assert(64 * DPS * 4 <= kRBytes, "dP exceeds the head scratch it reuses");
-  static_assert(kLds <= 160 * 1024, "backward LDS exceeds a CU");
+  static constexpr int kLds = kLab + 64 * 4;
+  static constexpr bool kFits = kLds <= 160 * 1024 && 4 * HD <= CC * RG;
 };
 
 template <int CC, int HD, int NW>
 __global__ __launch_bounds__(NW * 64) void cgen_bwd_kernel(GBwdArgs a) {
   using F = BwdCfg<CC, HD, NW>;
+  static_assert(F::kFits, "backward LDS exceeds a CU");
   constexpr int kGThreads = F::NTH;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* Gs = reinterpret_cast<float*>(smem + F::kG);
+  float* hs = reinterpret_cast<float*>(smem + F::kH);
+  float* Gs = hs;                                                // G overwrites h in place
   float* W1s = reinterpret_cast<float*>(smem + F::kW1);
+  float* db1p = W1s;                                             // head workgroup (it stages no W1 rows)
   float* Pts = reinterpret_cast<float*>(smem + F::kPt);
   float* xs = reinterpret_cast<float*>(smem + F::kXs);
   uint8_t* am = smem + F::kAm;
-  float* hs = reinterpret_cast<float*>(smem + F::kR);
-  float* part = reinterpret_cast<float*>(smem + F::kR + F::kHs);
-  float* dls = reinterpret_cast<float*>(smem + F::kR + F::kHs + F::kPart);
-  float* dps = hs;                                               // after G: dP reuses the head scratch
-  float* red = reinterpret_cast<float*>(smem + F::kR);           // after the chunk loop
+  float* dps = reinterpret_cast<float*>(smem + F::kDp);
+  float* part = reinterpret_cast<float*>(smem + F::kS);
+  float* dls = reinterpret_cast<float*>(smem + F::kS + F::kPart);
+  float* red = reinterpret_cast<float*>(smem + F::kS);           // after the chunk loop
   float* w2s = reinterpret_cast<float*>(smem + F::kW2);
   float* b2s = reinterpret_cast<float*>(smem + F::kB2);
   int* labs = reinterpret_cast<int*>(smem + F::kLab);
-  float* db1p = reinterpret_cast<float*>(smem + F::kDb1);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fr = lane & 15, fq = lane >> 4;
   const int W = a.W, Wp = (W - 2) / 2, P = ((a.H - 2) / 2) * Wp, C = a.C;
   const bool head_wg = blockIdx.x == gridDim.x - 1;
@@ -370,7 +370,8 @@ __global__ __launch_bounds__(NW * 64) void cgen_bwd_kernel(GBwdArgs a) {
 #pragma unroll
   for (int j = 0; j < F::UTW; ++j) gw[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float la = 0.f, ca = 0.f, na = 0.f, db2acc = 0.f;
-  if (head_wg && tid < 4 * HD) db1p[tid] = 0.f;
+  if (head_wg)
+    for (int i = tid; i < 4 * HD; i += kGThreads) db1p[i] = 0.f;
 
   for (int b0 = 0; b0 < a.B; b0 += 64) {
     const int nb = min(64, a.B - b0);
@@ -464,22 +465,8 @@ __global__ __launch_bounds__(NW * 64) void cgen_bwd_kernel(GBwdArgs a) {
       lds_barrier();
       stamp(a.stamps, 2);
     }
-    // ---- G = dH = dl . W2^T masked by h > 0 (rows < nb): tiles (row tile, unit tile) over the waves
-    for (int t = wave; t < 4 * (HD / 16); t += NW) {
-      const int rt = t & 3, ut = t >> 2;
-      f32x4 gh{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int k = 0; k < 16; k += 4) gh = mfma4(dls[(rt * 16 + fr) * W2S + k + fq], w2s[(ut * 16 + fr) * W2S + k + fq], gh);
-      const int j = ut * 16 + fr;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = rt * 16 + fq * 4 + i;
-        if ((a.pre_relu && !(hs[r * F::RG + j] > 0.f)) || r >= nb) gh[i] = 0.f;
-        Gs[r * F::RG + j] = gh[i];
-      }
-    }
     if (head_wg) {
-      // dW2[u][c] += sum_b h[b][u] dl[b][c]: unit tiles ut = wave, wave + 16
+      // dW2[u][c] += sum_b h[b][u] dl[b][c] (unit tiles ut = wave, wave + NW, ..), db2 — before G overwrites h
 #pragma unroll
       for (int j = 0; j < F::UTW; ++j) {
         const int ut = wave + NW * j;
@@ -494,11 +481,29 @@ __global__ __launch_bounds__(NW * 64) void cgen_bwd_kernel(GBwdArgs a) {
         db2acc += s;
       }
       lds_barrier();
-      if (tid < 4 * HD) {   // db1 += sum_b G[b][u]: 4 row groups of 16 images per unit
-        const int u = tid % HD, rg = tid / HD;
+    }
+    // ---- G = dH = dl . W2^T masked by h > 0 (rows < nb), in place of h: tiles (row tile, unit tile) over the
+    //      waves
+    for (int t = wave; t < 4 * (HD / 16); t += NW) {
+      const int rt = t & 3, ut = t >> 2;
+      f32x4 gh{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 16; k += 4) gh = mfma4(dls[(rt * 16 + fr) * W2S + k + fq], w2s[(ut * 16 + fr) * W2S + k + fq], gh);
+      const int j = ut * 16 + fr;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = rt * 16 + fq * 4 + i;
+        if ((a.pre_relu && !(hs[r * F::RG + j] > 0.f)) || r >= nb) gh[i] = 0.f;
+        Gs[r * F::RG + j] = gh[i];
+      }
+    }
+    if (head_wg) {
+      lds_barrier();
+      for (int i = tid; i < 4 * HD; i += kGThreads) {   // db1 += sum_b G[b][u]: 4 row groups of 16 images per unit
+        const int u = i % HD, rg = i / HD;
         float s = 0.f;
         for (int r = rg * 16; r < rg * 16 + 16; ++r) s += Gs[r * F::RG + u];
-        db1p[tid] += s;
+        db1p[i] += s;
       }
       lds_barrier();
       continue;
@@ -740,22 +745,43 @@ static int bwd_waves(int CC, int HD) {
   return CC * HD >= 6144 ? 8 : 16;
 }
 
+// The instantiated family: the backward's LDS at 8 waves fits a CU (Conv2D 16 / 32 up to Dense(256), 48 up to
+// 192, 64 up to 160).
+template <int CC, int HD>
+constexpr bool fits() { return BwdCfg<CC, HD, 8>::kFits; }
+
 template <int CC, int HD>
 static int launch_bwd(const GBwdArgs& a, int P, hipStream_t s) {
-  return bwd_waves(CC, HD) == 8 ? launch_bwd_nw<CC, HD, 8>(a, P, s) : launch_bwd_nw<CC, HD, 16>(a, P, s);
+  if constexpr (!fits<CC, HD>()) {
+    return -9;
+  } else if constexpr (!BwdCfg<CC, HD, 16>::kFits) {
+    return launch_bwd_nw<CC, HD, 8>(a, P, s);
+  } else {
+    return bwd_waves(CC, HD) == 8 ? launch_bwd_nw<CC, HD, 8>(a, P, s) : launch_bwd_nw<CC, HD, 16>(a, P, s);
+  }
 }
 
-#define TDE_CGEN_DISPATCH(FN, CCV, HDV, ...)                                              \
-  switch (CCV * 1000 + HDV) {                                                              \
-    case 16032: return FN<16, 32>(__VA_ARGS__);  case 16064: return FN<16, 64>(__VA_ARGS__); \
-    case 16096: return FN<16, 96>(__VA_ARGS__);  case 16128: return FN<16, 128>(__VA_ARGS__); \
-    case 32032: return FN<32, 32>(__VA_ARGS__);  case 32064: return FN<32, 64>(__VA_ARGS__); \
-    case 32096: return FN<32, 96>(__VA_ARGS__);  case 32128: return FN<32, 128>(__VA_ARGS__); \
-    case 48032: return FN<48, 32>(__VA_ARGS__);  case 48064: return FN<48, 64>(__VA_ARGS__); \
-    case 48096: return FN<48, 96>(__VA_ARGS__);  case 48128: return FN<48, 128>(__VA_ARGS__); \
-    case 64032: return FN<64, 32>(__VA_ARGS__);  case 64064: return FN<64, 64>(__VA_ARGS__); \
-    case 64096: return FN<64, 96>(__VA_ARGS__);  case 64128: return FN<64, 128>(__VA_ARGS__); \
-    default: return -9;                                                                     \
+template <int CC, int HD>
+static int launch_fwd_if(const GFwdArgs& a, int P, hipStream_t s) {
+  if constexpr (!fits<CC, HD>()) return -9;
+  else return launch_fwd<CC, HD>(a, P, s);
+}
+
+template <int CC, int HD>
+static int supported_if() { return fits<CC, HD>() ? 1 : 0; }
+
+#define TDE_CGEN_CASES_CC(FN, CCV, ...)                                                                   \
+  case CCV * 1000 + 32: return FN<CCV, 32>(__VA_ARGS__);   case CCV * 1000 + 64: return FN<CCV, 64>(__VA_ARGS__);   \
+  case CCV * 1000 + 96: return FN<CCV, 96>(__VA_ARGS__);   case CCV * 1000 + 128: return FN<CCV, 128>(__VA_ARGS__); \
+  case CCV * 1000 + 160: return FN<CCV, 160>(__VA_ARGS__); case CCV * 1000 + 192: return FN<CCV, 192>(__VA_ARGS__); \
+  case CCV * 1000 + 224: return FN<CCV, 224>(__VA_ARGS__); case CCV * 1000 + 256: return FN<CCV, 256>(__VA_ARGS__);
+#define TDE_CGEN_DISPATCH(FN, CCV, HDV, ...)                                                              \
+  switch (CCV * 1000 + HDV) {                                                                              \
+    TDE_CGEN_CASES_CC(FN, 16, __VA_ARGS__)                                                                 \
+    TDE_CGEN_CASES_CC(FN, 32, __VA_ARGS__)                                                                 \
+    TDE_CGEN_CASES_CC(FN, 48, __VA_ARGS__)                                                                 \
+    TDE_CGEN_CASES_CC(FN, 64, __VA_ARGS__)                                                                 \
+    default: return -9;                                                                                     \
   }
 
 }  // namespace cgen
@@ -764,9 +790,9 @@ static int launch_bwd(const GBwdArgs& a, int P, hipStream_t s) {
 using namespace tde;
 using namespace tde::cgen;
 
-TDE_API int tde_cgen_supported(int CC, int HD) {
-  return (CC == 16 || CC == 32 || CC == 48 || CC == 64) && (HD == 32 || HD == 64 || HD == 96 || HD == 128);
-}
+static int supported_code(int CC, int HD) { TDE_CGEN_DISPATCH(supported_if, CC, HD) }
+
+TDE_API int tde_cgen_supported(int CC, int HD) { return supported_code(CC, HD) == 1; }
 
 // Forward (see the header).  x [B][H][W] f32 (C_in = 1), wc [9][CC], bc [CC], W1 [P*CC][HD] f32 master,
 // hpre [hrep][>=B][HD] (+=), Pt [P*CC][ldPt], amax [P][CC/8][lda] (8 argmax bytes per u64).  fly (nullable):
@@ -786,7 +812,7 @@ TDE_API int tde_cgen_fwd(int CC, int HD, const float* x, const float* wc, const 
   const int P = ((H - 2) / 2) * ((W - 2) / 2);
   GFwdArgs a{x, wc, bc, W1, hpre, hrep, hrep_stride, Pt, ldPt, (uint64_t*)amax, lda, inc_iter,
              fly ? *fly : TdeCgenFly{}, fly != nullptr, B, H, W};
-  TDE_CGEN_DISPATCH(launch_fwd, CC, HD, a, P, stream)
+  TDE_CGEN_DISPATCH(launch_fwd_if, CC, HD, a, P, stream)
 }
 
 // Backward (plain step: gradients out).  hpre / hzero [hrep][>=B][HD] (hzero zeroed here), dW1 [P*CC][HD]

@@ -310,8 +310,6 @@ def match_convnet(model, loss):
         return None
     if (d2.activation == "softmax") == bool(loss.from_logits):
         return None  # probabilities fed to from_logits=True (or logits w/o from_logits): not fusable
-    if d2.units > 64 or d1.units * d2.units > 16384 or d1.units % 32 or d1.units > 256:
-        return None
     force_gen = os.environ.get("TDE_CONVNET_GENERIC", "0") == "1"   # A/B: the generic kernels at any width
     if c.filters != 32 or d1.units != 64 or force_gen:
         # the hand-tuned step is the reference's Conv2D(32)/Dense(64) (distributed_with_keras.py:34,37);
@@ -321,8 +319,9 @@ def match_convnet(model, loss):
         why = None
         if Kb.global_policy().compute_dtype != torch.float32:
             why = "the generic widths are implemented for the float32 policy"
-        elif c.filters not in GEN_FILTERS or d1.units not in GEN_UNITS:
-            why = f"Conv2D filters must be one of {GEN_FILTERS} and Dense units one of {GEN_UNITS}"
+        elif not gen_fits(c.filters, d1.units):
+            why = (f"Conv2D filters must be one of {GEN_FILTERS} and Dense units a multiple of 32 up to 256 whose "
+                   "backward fits a CU's LDS (Conv2D(48): up to 192 units, Conv2D(64): up to 160)")
         elif d2.units > 16 or W % 4 or W > 32 or H % 2:
             why = "at most 16 classes and an even height, width a multiple of 4 up to 32"
         if why is None:
@@ -331,11 +330,28 @@ def match_convnet(model, loss):
         warnings.warn(f"model {model.name!r}: no fused small-CNN step for Conv2D({c.filters}) + Dense({d1.units}) "
                       f"({why}); running the per-layer kernel plan")
         return None
+    if d2.units > 16:
+        import warnings
+        warnings.warn(f"model {model.name!r}: the fused small-CNN step takes at most 16 classes (got {d2.units}); "
+                      "running the per-layer kernel plan")
+        return None
     return dict(conv=c, pool=p, dense1=d1, dense2=d2)
 
 
 GEN_FILTERS = (16, 32, 48, 64)      # csrc/kernels/convnet_gen.hip instantiations
-GEN_UNITS = (32, 64, 96, 128)
+GEN_UNITS = tuple(range(32, 257, 32))
+
+
+def gen_fits(filters, units):
+    """Whether the generic fused kernels are instantiated for Conv2D(filters) / Dense(units): the backward's
+    LDS carve at 8 waves (csrc/kernels/convnet_gen.hip BwdCfg) within a CU's 160 KB."""
+    if filters not in GEN_FILTERS or units not in GEN_UNITS:
+        return False
+    cc, hd = filters, units
+    rg = hd + 4
+    lds = (64 * rg * 4 + cc * rg * 4 + cc * 68 * 4 + 64 * 16 * 4 + 64 * cc + 64 * (cc + 4) * 4
+           + max(4096 + 64 * 17 * 4, 8 * 10 * cc * 4) + hd * 17 * 4 + 16 * 4 + 64 * 4)
+    return lds <= 160 * 1024
 
 
 class ConvNetPlan(ReplicaPlan):

@@ -40,6 +40,10 @@ CASES = [  # (filters, units, batch, Dense ReLU, H, W, classes)
     (32, 128, 64, True, 28, 28, 10),
     (64, 32, 100, True, 20, 24, 16),
     (16, 64, 200, True, 28, 28, 3),
+    (32, 256, 64, True, 28, 28, 10),
+    (48, 192, 70, True, 28, 28, 10),
+    (64, 160, 64, False, 28, 28, 10),
+    (16, 224, 96, True, 24, 20, 12),
 ]
 
 
@@ -113,9 +117,13 @@ def test_cgen_step_kernels_match_float64(CC, HD, B, relu, H, W, NC):
     assert _rel(tot[:9 * CC], dw.reshape(-1)) < 1e-6 and _rel(tot[9 * CC:10 * CC], db) < 1e-6
 
 
-def test_cgen_rejects_uninstantiated_width():
+def test_cgen_family_matches_the_python_rule():
+    """The kernels' instantiation rule (the backward's LDS at 8 waves) agrees with train/program.gen_fits."""
     from tensorflow_distributed_example_amd.ops import kernels as Kk
-    assert Kk.cgen_supported(64, 128) and not Kk.cgen_supported(24, 64) and not Kk.cgen_supported(32, 256)
+    from tensorflow_distributed_example_amd.train import program as PG
+    for f in (8, 16, 24, 32, 48, 64, 96):
+        for u in range(16, 320, 16):
+            assert Kk.cgen_supported(f, u) == PG.gen_fits(f, u), (f, u)
 
 
 def _model(tde, filters, units, opt, spe):
@@ -141,7 +149,8 @@ def _grads64(m, W, x, y, B):
 
 @pytest.mark.parametrize("filters,units,mode,kind", [(64, 128, "local", "sgd"), (16, 32, "local", "sgd"),
                                                      (64, 128, "plain", "sgd"), (32, 96, "local", "momentum"),
-                                                     (48, 64, "local", "adam"), (16, 128, "plain", "adam")])
+                                                     (48, 64, "local", "adam"), (16, 128, "plain", "adam"),
+                                                     (32, 256, "local", "sgd"), (48, 192, "local", "momentum")])
 def test_generic_plan_graph_trajectory_matches_float64(filters, units, mode, kind, monkeypatch):
     """A Conv2D(filters)/Dense(units) model runs the generic fused plan in hipGraph executions of 4 steps —
     step mode "local" (the default with one replica: the Dense rows updated by the backward workgroups that own

@@ -30,7 +30,8 @@ def test_reference_width_takes_the_hand_tuned_plan():
         assert pat is not None and not pat.get("generic") and not warns
 
 
-@pytest.mark.parametrize("filters,units", [(64, 128), (16, 32), (48, 96), (32, 128), (64, 32)])
+@pytest.mark.parametrize("filters,units", [(64, 128), (16, 32), (48, 96), (32, 128), (64, 32), (32, 256), (16, 224),
+                                           (48, 192), (64, 160)])
 def test_generic_widths_take_the_generic_plan(filters, units):
     pat, warns = _match(filters, units, "float32")
     assert pat is not None and pat["generic"] and not warns
@@ -39,7 +40,9 @@ def test_generic_widths_take_the_generic_plan(filters, units):
 @pytest.mark.parametrize("filters,units,policy,H,W,classes,why", [
     (64, 128, "mixed_bfloat16", 28, 28, 10, "float32 policy"),
     (24, 64, "float32", 28, 28, 10, "filters must be one of"),
-    (32, 256, "float32", 28, 28, 10, "units one of"),
+    (32, 288, "float32", 28, 28, 10, "multiple of 32 up to 256"),
+    (64, 192, "float32", 28, 28, 10, "fits a CU's LDS"),
+    (48, 224, "float32", 28, 28, 10, "fits a CU's LDS"),
     (64, 128, "float32", 28, 36, 10, "width a multiple of 4 up to 32"),
     (64, 128, "float32", 28, 28, 20, "at most 16 classes"),
 ])
@@ -64,3 +67,11 @@ def test_bncnn_family_near_miss_warns():
             assert spec is not None and not msgs, msgs
         else:
             assert spec is None and len(msgs) == 1 and "48 channels" in msgs[0] and "400 units" in msgs[0], msgs
+
+
+def test_python_fit_rule_matches_the_kernel_family():
+    """train/program.gen_fits mirrors the kernels' instantiation rule (csrc/kernels/convnet_gen.hip): 27 of
+    the 32 (filters, units) pairs."""
+    from tensorflow_distributed_example_amd.train import program as PG
+    ok = {(f, u) for f in PG.GEN_FILTERS for u in PG.GEN_UNITS if PG.gen_fits(f, u)}
+    assert len(ok) == 27 and (64, 160) in ok and (64, 192) not in ok and (48, 192) in ok and (48, 224) not in ok
