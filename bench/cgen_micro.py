@@ -90,6 +90,16 @@ def main():
             K.cgen_bwd(x, amax, hp[0], hp[1], b1, W2, b2, y, scale=1.0 / B, pre_relu=True, metrics=met, W1=W1, Pt=Pt,
                        B=B, stamps=st, **g)
             torch.cuda.synchronize()
+            sf = torch.zeros(Pn * ((B + 63) // 64), 8, dtype=torch.int64, device=dev)
+            K.cgen_fwd(x, wc, bc, W1, hp[0], Pt, amax, B=B, stamps=sf)
+            torch.cuda.synchronize()
+            tf = sf.double() * 0.01
+            f0 = float(tf[:, 0].min())
+            print(json.dumps({"width": spec, "launch": "cgen_fwd_phases", "last_start_us": round(float(tf[:, 0].max()) - f0, 2),
+                              "last_end_us": round(float(tf[:, 3].max()) - f0, 2),
+                              **{f"ph{i}": (round(float((tf[:, i] - tf[:, i - 1]).median()), 2),
+                                            round(float((tf[:, i] - tf[:, i - 1]).max()), 2)) for i in (1, 2, 3)}}),
+                  flush=True)
             t = st[:Pn].double() * 0.01   # us
             t0 = float(t[:, 0].min())
             ph = {f"ph{i}": (round(float((t[:, i] - t[:, i - 1]).median()), 2),

@@ -65,6 +65,7 @@ struct GFwdArgs {
   long long* inc_iter;   // step counter advanced by block (0, 0) (nullable; the fused step's, read by the backward)
   TdeCgenFly fly;
   int fly_on;
+  long long* stamps;     // diagnostics (nullable): phase clocks per workgroup (bench/cgen_micro.py --phases)
   int B, H, W;
 };
 
@@ -91,6 +92,7 @@ __global__ __launch_bounds__(256) void cgen_fwd_kernel(GFwdArgs a) {
   const int p = blockIdx.x, py = p / Wp, px = p - py * Wp;
   const int b0 = blockIdx.y * 64, b = b0 + lane;
   const bool bok = b < a.B;
+  stamp(a.stamps, 0);
 
   // B fragments of this wave's column tiles first (their round trip overlaps the staging below):
   // W1[p*CC + fq*KQ + s][nt*16 + fr]
@@ -150,6 +152,7 @@ __global__ __launch_bounds__(256) void cgen_fwd_kernel(GFwdArgs a) {
     }
   }
   lds_barrier();
+  stamp(a.stamps, 1);
 
   // conv + bias + ReLU + 2x2 max-pool: lane = image, wave = channel groups of 8
   float patch[16];
@@ -193,6 +196,7 @@ __global__ __launch_bounds__(256) void cgen_fwd_kernel(GFwdArgs a) {
     *reinterpret_cast<float4*>(dst + 4) = float4{out[4], out[5], out[6], out[7]};
   }
   lds_barrier();
+  stamp(a.stamps, 2);
 
   // hpre[64 x HD] += Ps(64 x CC) . W1p(CC x HD): wave = column tiles nt = wave + 4j, all 4 row tiles;
   // lane group fq supplies k = fq*KQ .. fq*KQ + KQ-1 (the same k order in A and B)
@@ -224,6 +228,7 @@ __global__ __launch_bounds__(256) void cgen_fwd_kernel(GFwdArgs a) {
         if (row < a.B) atomicAdd(hrow + (size_t)row * HD + nt * 16 + fr, acc[mt][r]);
       }
   }
+  stamp(a.stamps, 3);
 }
 
 }  // namespace cgen
@@ -799,7 +804,8 @@ TDE_API int tde_cgen_supported(int CC, int HD) { return supported_code(CC, HD) =
 // the fused step's deferred conv update and head snapshot (TdeCgenFly).
 TDE_API int tde_cgen_fwd(int CC, int HD, const float* x, const float* wc, const float* bc, const float* W1,
                          float* hpre, int hrep, long long hrep_stride, float* Pt, int ldPt, void* amax, int lda,
-                         long long* inc_iter, const TdeCgenFly* fly, int B, int H, int W, hipStream_t stream) {
+                         long long* inc_iter, const TdeCgenFly* fly, long long* stamps, int B, int H, int W,
+                         hipStream_t stream) {
   if (!tde_cgen_supported(CC, HD) || (W & 3) || W > 32 || H < 4 || W < 4 || ((H - 2) & 1) || ((W - 2) & 1))
     return -1;
   if (fly && (!fly->pend || !fly->gwc || !fly->gbc || fly->grep < 1 || fly->grep > kMaxGrep || !fly->iter_prev ||
@@ -811,7 +817,7 @@ TDE_API int tde_cgen_fwd(int CC, int HD, const float* x, const float* wc, const 
     return -2;
   const int P = ((H - 2) / 2) * ((W - 2) / 2);
   GFwdArgs a{x, wc, bc, W1, hpre, hrep, hrep_stride, Pt, ldPt, (uint64_t*)amax, lda, inc_iter,
-             fly ? *fly : TdeCgenFly{}, fly != nullptr, B, H, W};
+             fly ? *fly : TdeCgenFly{}, fly != nullptr, stamps, B, H, W};
   TDE_CGEN_DISPATCH(launch_fwd_if, CC, HD, a, P, stream)
 }
 

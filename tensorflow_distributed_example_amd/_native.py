@@ -47,7 +47,7 @@ _HIP_PROTOS = {
     "tde_noop": (i32, [i32, i32, p]),
     "tde_cnet_abi_sizes": (i32, [p, i32]),
     "tde_cgen_supported": (i32, [i32, i32]),
-    "tde_cgen_fwd": (i32, [i32, i32, p, p, p, p, p, i32, i64, p, i32, p, i32, p, p, i32, i32, i32, p]),
+    "tde_cgen_fwd": (i32, [i32, i32, p, p, p, p, p, i32, i64, p, i32, p, i32, p, p, p, i32, i32, i32, p]),
     "tde_cgen_bwd": (i32, [i32, i32, p, p, i32, p, p, i32, i64, p, p, p, i32, i32, p, f32, p, p, p, i32, p, p, p,
                            p, p, p, p, p, p, i32, i64, p, p, p, i32, i32, i32, p]),
     "tde_xgmi_abi_sizes": (i32, [p, i32]),

@@ -307,7 +307,7 @@ def cgen_supported(filters, units):
     return bool(N.hip().tde_cgen_supported(int(filters), int(units)))
 
 
-def cgen_fwd(x, wc, bc, W1, hpre, Pt, amax, *, B, inc_iter=None, fly: CgenFly | None = None):
+def cgen_fwd(x, wc, bc, W1, hpre, Pt, amax, *, B, inc_iter=None, fly: CgenFly | None = None, stamps=None):
     """Generic-width fused small-CNN forward, float32 (csrc/kernels/convnet_gen.hip): Conv2D(CC, 3x3) + ReLU +
     MaxPool(2) + the Dense(HD) matmul, hpre [R, >=B, HD] += (workgroup i adds into replica i % R).
     W1 the f32 master kernel [P*CC, HD]; Pt [P*CC, ldPt] f32; amax int64 [P, CC/8, lda]; inc_iter (int64 step
@@ -327,7 +327,7 @@ def cgen_fwd(x, wc, bc, W1, hpre, Pt, amax, *, B, inc_iter=None, fly: CgenFly | 
     _req(amax.dtype == torch.int64 and amax.shape[:2] == (Pn, CC // 8) and amax.shape[-1] >= B, "cgen_fwd: amax")
     rc = N.hip().tde_cgen_fwd(CC, HD, _P(x), _P(wc), _P(bc), _P(W1), _P(hpre), hp.shape[0], hp.stride(0), _P(Pt),
                               Pt.stride(0), _P(amax), amax.shape[-1], _P(inc_iter),
-                              _ct.byref(fly) if fly is not None else None, B, H, W, _s())
+                              _ct.byref(fly) if fly is not None else None, _P(stamps), B, H, W, _s())
     N.check(rc, "tde_cgen_fwd")
 
 
