@@ -96,7 +96,8 @@ def main():
                           "ps_tasks": len(cfg.get("cluster", {}).get("ps", [])), "batch": a.batch,
                           "model": a.model, "steps_timed": hook.s1 - hook.s0, "master_local_steps_per_sec":
                           round(local, 1), "device": str(model._store.device), "final_global_step": hook.s1,
-                          "momentum": a.momentum, "data_plane": getattr(est, "ps_data_plane", "tcp")}),
+                          "momentum": a.momentum, "data_plane": getattr(est, "ps_data_plane", "tcp"),
+                          "pipelined": os.environ.get("TDE_PS_PIPELINE", "1") != "0"}),
               flush=True)
 
 

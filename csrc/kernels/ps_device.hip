@@ -45,6 +45,8 @@ struct PsDevArgs {
   float* data[kPsMaxShards];   // every window's data area (after its counters)
   unsigned long long* ctr;     // ps 0's counters
   const PsSeg* segs;
+  const long long* beg;        // [nseg + 1] element prefix offsets of the segments (device)
+  int nseg;
   float* w;                    // local weights (pulled into)
   float* g;                    // local gradients (read, zeroed); null: pull only
   float* s;                    // local state: after this step's forward (push) / pulled into
@@ -55,21 +57,44 @@ struct PsDevArgs {
   long long dstep, dticket;
   unsigned int* done;          // local device word: blocks finished (re-armed by the last)
   long long* out;              // host-mapped [global_step, tickets] after this call
+  // pipelined trainer loop (nullable): the step ticket the pushed gradients were computed under; a push
+  // whose ticket exceeds `limit` (max_steps) is dropped and advances no counter, so a host that runs a
+  // few steps ahead of the tickets it has seen still makes EXACTLY max_steps global updates.  A live
+  // push that claims a ticket stores it here for the next step.
+  long long* claim;
+  long long limit;
 };
 
 __device__ __forceinline__ float sys_load(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// grid (x: element blocks, y: segment); a segment with fewer elements than the x extent idles its tail blocks
+// One flat grid over every element of every segment (`beg`: the segments' element prefix offsets, staged into
+// LDS; each thread finds its segment by binary search).  The windows are fine-grained UNCACHED memory, so the
+// pushes are performed where the data lives and the pulls read it there: a block only waits for its own
+// accesses (s_waitcnt) before it counts its arrival — no cache writeback per block (the previous form
+// fenced at system scope in every block of a segment x 64 grid: ~105 us per exchange for Model B).
+constexpr int kPsMaxSegsLds = 512;
 __global__ __launch_bounds__(256) void ps_dev_step_kernel(PsDevArgs a) {
-  const bool push = a.g != nullptr;
+  const bool live = !(a.claim && a.limit > 0 && *a.claim > a.limit);
+  const bool push = a.g != nullptr && live;
+  __shared__ long long beg[kPsMaxSegsLds + 1];
+  const int nseg = a.nseg;
   if (a.segs) {
-    const PsSeg sg = a.segs[blockIdx.y];
-    float* const D = a.data[sg.win];
-    float* const W = D + sg.woff;
-    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < sg.n;
-         i += (long long)gridDim.x * blockDim.x) {
+    for (int i = threadIdx.x; i <= nseg; i += blockDim.x) beg[i] = a.beg[i];
+    __syncthreads();
+    const long long total = beg[nseg];
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+      int lo = 0, hi = nseg - 1;   // the segment j with beg[j] <= e < beg[j + 1]
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (beg[mid] <= e) lo = mid;
+        else hi = mid - 1;
+      }
+      const PsSeg sg = a.segs[lo];
+      const long long i = e - beg[lo];
+      float* const D = a.data[sg.win];
+      float* const W = D + sg.woff;
       const long long li = sg.loff + i;
       if (!sg.state) {
         if (push) {
@@ -89,6 +114,8 @@ __global__ __launch_bounds__(256) void ps_dev_step_kernel(PsDevArgs a) {
             __hip_atomic_fetch_add(W + i, dw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           }
           a.g[li] = 0.f;
+        } else if (a.g) {
+          a.g[li] = 0.f;   // a dropped push: its gradients are discarded
         }
         a.w[li] = sys_load(W + i);
       } else {
@@ -115,20 +142,25 @@ __global__ __launch_bounds__(256) void ps_dev_step_kernel(PsDevArgs a) {
       }
     }
   }
-  // every block's atomics (on every shard) are performed before the last block advances the counters
-  __atomic_thread_fence(__ATOMIC_SEQ_CST);   // system scope: drains and orders this thread's accesses
+  // every block's window accesses are performed (acknowledged by the uncached memory) before it arrives;
+  // the last arrival advances the counters, so every shard's update precedes the global step
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __atomic_thread_fence(__ATOMIC_SEQ_CST);
     const unsigned nblk = gridDim.x * gridDim.y;
-    const unsigned prev = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned prev = __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (prev == nblk - 1) {
       __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const long long gs = (long long)__hip_atomic_fetch_add(a.ctr + 0, (unsigned long long)a.dstep, __ATOMIC_SEQ_CST,
-                                                             __HIP_MEMORY_SCOPE_SYSTEM) + a.dstep;
-      const long long tk = (long long)__hip_atomic_fetch_add(a.ctr + 1, (unsigned long long)a.dticket,
-                                                             __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM) + a.dticket;
+      const long long ds = live ? a.dstep : 0, dt = live ? a.dticket : 0;
+      const long long gs = (long long)__hip_atomic_fetch_add(a.ctr + 0, (unsigned long long)ds, __ATOMIC_SEQ_CST,
+                                                             __HIP_MEMORY_SCOPE_SYSTEM) + ds;
+      long long tk = (long long)__hip_atomic_fetch_add(a.ctr + 1, (unsigned long long)dt,
+                                                       __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM) + dt;
       if (push) __hip_atomic_fetch_add(a.ctr + 3, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (a.claim) {
+        if (live && dt) *a.claim = tk;   // the next step's ticket
+        tk = *a.claim;                    // what the host sees: this trainer's ticket for its next step
+      }
       if (a.out) {
         a.out[0] = gs;
         a.out[1] = tk;
@@ -207,15 +239,19 @@ static int ps_fill_data(float** data, void* const* windows, int nwin) {
 
 // One async exchange (g != null) or a pull (g == null) over the segment table `segs` (device memory,
 // nseg entries; maxn = the largest segment), or, with nseg == 0, a counters-only call; see the header.
-TDE_API int tde_psdev_step(void* const* windows, int nwin, const void* segs, int nseg, long long maxn, float* w,
-                           float* g, float* s, float* sp, const float* mom, float lr, float mmt, int kind,
+// beg: [nseg + 1] device prefix offsets of the segments' element counts (total = beg[nseg], host: `total`).
+TDE_API int tde_psdev_step(void* const* windows, int nwin, const void* segs, const void* beg, int nseg, long long total,
+                           float* w, float* g, float* s, float* sp, const float* mom, float lr, float mmt, int kind,
                            long long dstep, long long dticket, unsigned int* done, long long* out_dev,
-                           hipStream_t stream) {
-  if (!w || nseg < 0 || (nseg > 0 && !segs) || !done || kind < 0 || kind > 2 || nseg > 65535) return -1;
+                           long long* claim, long long limit, hipStream_t stream) {
+  if (!w || nseg < 0 || (nseg > 0 && (!segs || !beg)) || !done || kind < 0 || kind > 2 || nseg > kPsMaxSegsLds)
+    return -1;
   PsDevArgs a;
   if (ps_fill_data(a.data, windows, nwin)) return -1;
   a.ctr = (unsigned long long*)windows[0];
   a.segs = nseg > 0 ? (const PsSeg*)segs : nullptr;
+  a.beg = (const long long*)beg;
+  a.nseg = nseg;
   a.w = w;
   a.g = g;
   a.s = s;
@@ -228,8 +264,12 @@ TDE_API int tde_psdev_step(void* const* windows, int nwin, const void* segs, int
   a.dticket = dticket;
   a.done = done;
   a.out = out_dev;
-  const dim3 grid(nseg > 0 ? ps_grid_x(maxn) : 1, nseg > 0 ? nseg : 1);
-  ps_dev_step_kernel<<<grid, 256, 0, stream>>>(a);
+  a.claim = claim;
+  a.limit = limit;
+  long long nb = nseg > 0 ? (total + 255) / 256 : 1;   // one element per thread (the accesses are latency-bound)
+  if (nb > 4096) nb = 4096;
+  if (nb < 1) nb = 1;
+  ps_dev_step_kernel<<<dim3((unsigned)nb), 256, 0, stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;
 }

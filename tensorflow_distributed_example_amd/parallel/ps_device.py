@@ -36,7 +36,10 @@ N.register_hip({
     "tde_psdev_seg_bytes": (_i, []),
     "tde_host_mapped_alloc": (_i, [_i64, C.POINTER(_vp), C.POINTER(_vp)]),
     "tde_host_mapped_free": (_i, [_vp]),
-    "tde_psdev_step": (_i, [_vp, _i, _vp, _i, _i64, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _i64, _i64, _vp, _vp, _vp]),
+    # windows, nwin, segs, beg, nseg, total, w, g, s, sp, mom, lr, mmt, kind, dstep, dticket, done, out, claim,
+    # limit, stream
+    "tde_psdev_step": (_i, [_vp, _i, _vp, _vp, _i, _i64, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _i64, _i64, _vp, _vp,
+                            _vp, _i64, _vp]),
     "tde_psdev_copy": (_i, [_vp, _i, _vp, _i, _i64, _vp, _vp, _i, _vp]),
     "tde_psdev_set_counter": (_i, [_vp, _i, _i64]),
     "tde_psdev_get_counter": (_i64, [_vp, _i]),
@@ -236,6 +239,10 @@ class DevicePlane:
         self.nseg = len(segs)
         self.maxn = int(segs["n"].max()) if len(segs) else 0
         self.segs = torch.from_numpy(segs.view(np.uint8).copy()).to(dev)
+        beg = np.zeros(len(segs) + 1, np.int64)
+        beg[1:] = np.cumsum(segs["n"]) if len(segs) else []
+        self.total = int(beg[-1])
+        self.beg = torch.from_numpy(beg).to(dev)   # the exchange's flat element index -> segment
         self.nw, self.ns = store.w.numel(), store.state.numel()
         mom = np.zeros(max(self.ns, 1), np.float32)
         for name, mm in bn_momentum.items():
@@ -244,6 +251,7 @@ class DevicePlane:
         self.mom = torch.from_numpy(mom).to(dev)
         self.sp = torch.zeros(max(self.ns, 1), dtype=torch.float32, device=dev)
         self.done = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._claim = torch.zeros(1, dtype=torch.int64, device=dev)   # pipelined loop: this step's ticket
         h, d = C.c_void_p(), C.c_void_p()
         if self.lib.tde_host_mapped_alloc(16, C.byref(h), C.byref(d)) != 0:
             raise RuntimeError("host-mapped result words")
@@ -305,15 +313,32 @@ class DevicePlane:
         self._launch(push=True, dstep=dstep, dticket=dticket)
         return int(self._out[0]), int(self._out[1])
 
-    def _launch(self, push, dstep, dticket, pull=True):
+    def set_claim(self, ticket: int):
+        """Pipelined loop: the ticket the next pushed step was computed under (stream-ordered write)."""
+        self._claim.fill_(int(ticket))
+
+    def step_async(self, max_steps: int):
+        """Pipelined loop: push + pull + counters WITHOUT waiting.  The kernel drops a push whose ticket
+        (``set_claim``, then the one each live push claims) exceeds ``max_steps``, so the host may run ahead
+        of the counters it has seen.  Returns the (global step, this trainer's next ticket) of the latest
+        exchange the device has finished (host-mapped words, possibly a few steps old)."""
+        self._launch(push=True, dstep=1, dticket=1, sync=False, limit=int(max_steps))
+        return self.observed()
+
+    def observed(self):
+        return int(self._out[0]), int(self._out[1])
+
+    def _launch(self, push, dstep, dticket, pull=True, sync=True, limit=0):
         st = self.store
         with torch.cuda.device(st.device):
             s = N.stream_ptr()
             nseg = self.nseg if pull else 0
-            rc = self.lib.tde_psdev_step(self._wins, len(self.wins), N.ptr(self.segs) if nseg else None, nseg,
-                                         self.maxn, N.ptr(st.w), N.ptr(st.g) if push else None,
+            rc = self.lib.tde_psdev_step(self._wins, len(self.wins), N.ptr(self.segs) if nseg else None,
+                                         N.ptr(self.beg) if nseg else None, nseg, self.total if nseg else 0,
+                                         N.ptr(st.w), N.ptr(st.g) if push else None,
                                          N.ptr(st.state) if self.ns else None, N.ptr(self.sp), N.ptr(self.mom),
                                          self.lr, self.mmt, self.kind, int(dstep), int(dticket), N.ptr(self.done),
-                                         self._out_d, s)
+                                         self._out_d, N.ptr(self._claim) if limit > 0 else None, int(limit), s)
             N.check(rc, "tde_psdev_step")
-            torch.cuda.current_stream(st.device).synchronize()
+            if sync:
+                torch.cuda.current_stream(st.device).synchronize()

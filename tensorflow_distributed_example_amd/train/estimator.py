@@ -548,6 +548,13 @@ class Estimator:
         if ticket is None or ticket <= max_steps:
             plane.pull()
             plan.on_weights_loaded()
+        # pipelined (max_steps known; TDE_PS_PIPELINE=0 turns it off): no device sync per step — the host queues
+        # step after step and reads the counters the device has reached from host-mapped words; the exchange
+        # kernel drops any push whose ticket exceeds max_steps, so the few steps a trainer runs past its last
+        # ticket before it sees so change nothing and the global step still ends at EXACTLY max_steps
+        pipelined = max_steps is not None and os.environ.get("TDE_PS_PIPELINE", "1") != "0"
+        if pipelined:
+            plane.set_claim(ticket)
         while target is None or gstep < target:
             if ticket is not None and ticket > max_steps:
                 break
@@ -562,14 +569,23 @@ class Estimator:
             prog.x_stage[0].stage(x, prog.x_ring[0][0])
             prog.y_stage[0].stage(y, prog.y_ring[0][0])
             plan.scale = 1.0 / n
-            plan.train_step(prog.x_ring[0][0], prog.y_ring[0][0], n)
             ctx.prev_step = gstep
-            gstep, t = plane.step(dstep=1, dticket=1 if max_steps is not None else 0)
-            ticket = t if max_steps is not None else None
-            plan.on_weights_loaded()
+            if pipelined:
+                plan.train_step(prog.x_ring[0][0], prog.y_ring[0][0], n)
+                gstep, ticket = plane.step_async(max_steps)
+                plan.on_weights_loaded()
+            else:
+                plan.train_step(prog.x_ring[0][0], prog.y_ring[0][0], n)
+                gstep, t = plane.step(dstep=1, dticket=1 if max_steps is not None else 0)
+                ticket = t if max_steps is not None else None
+                plan.on_weights_loaded()
             ctx.global_step = gstep
             for h in all_hooks:
                 h.after_step(ctx)
+        if pipelined:
+            torch.cuda.synchronize(plan.store.device)   # every queued exchange performed
+            gstep = plane.observed()[0]
+            ctx.global_step = gstep
         return gstep
 
     def _ps_end(self, client, chief, max_steps, gstep, ctx, all_hooks):

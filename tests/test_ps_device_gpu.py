@@ -37,7 +37,8 @@ def test_device_plane_exchange_is_exact(nps, kind):
     """Trainer against the ps tasks' windows (variables round-robin over ``nps`` tasks, each window sized
     for its shard on request): the SGD / momentum / Nesterov update (f32 atomics, slot compare-and-swap),
     the BN moving average applied to the PS value from the recovered batch statistic, the pull and the
-    counters — checked against host arithmetic over 3 steps."""
+    counters — checked against host arithmetic over 3 steps; then the pipelined loop's ticket guard (a push
+    computed under a ticket past max_steps is dropped, a live one applied)."""
     import torch
 
     from tensorflow_distributed_example_amd.parallel import ps as PS
@@ -112,6 +113,33 @@ def test_device_plane_exchange_is_exact(nps, kind):
             assert torch.allclose(store.state.double().cpu(), S, rtol=0, atol=1e-6), step
             assert float(store.g.abs().max()) == 0.0
         assert plane.counter_add(1, 1) == 14 and plane.global_step() == 10
+        # the pipelined loop's guard (step_async, max_steps 14): a push computed under a ticket past max_steps is
+        # dropped — weights, slots and counters untouched, the gradient discarded ...
+        w_before = store.w.clone()
+        plane.set_claim(15)
+        store.g.copy_((torch.randn(store.w.numel(), generator=g) * live).cuda())
+        plane.step_async(14)
+        torch.cuda.synchronize()
+        assert plane.observed() == (10, 15) and plane.global_step() == 10 and plane.tickets() == 14
+        assert torch.equal(store.w, w_before) and float(store.g.abs().max()) == 0.0
+        # ... and one computed under a live ticket is applied and claims the next ticket
+        plane.set_claim(14)
+        gr = torch.randn(store.w.numel(), generator=g) * live
+        store.g.copy_(gr.cuda())
+        store.state.copy_(S.float().cuda())
+        plane.step_async(14)
+        torch.cuda.synchronize()
+        gd = gr.double()
+        if kind == 0:
+            W = W - lr * gd
+        else:
+            M = mm * M - lr * gd
+            W = W + (mm * M - lr * gd if kind == 2 else M)
+        assert plane.observed() == (11, 15) and plane.global_step() == 11
+        for n in ("d/kernel", "d/bias", "e/kernel"):
+            seg = store.segments[n]
+            sl = slice(seg.offset, seg.offset + seg.numel)
+            assert torch.allclose(store.w[sl].double().cpu(), W[sl], rtol=0, atol=2e-5), ("live guard", n)
         plane.close()
         client.close()
     finally:
