@@ -50,6 +50,7 @@
 // vmcnt(0)`, workgroup barrier, plain loads.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "tde_optim.h"
@@ -94,6 +95,7 @@ struct XgArgs {
   // (the producer's contended atomics spread over replicas); phase 1 sums and zeroes them
   float* rep; int nrep;
   long long rep_lo, rep_hi, rep_stride;
+  int acquire;   // force the waits' system-scope acquire on the uncached window (TDE_XGMI_ACQUIRE=1; A/B only)
 };
 constexpr int kXgTraceWords = 8;
 
@@ -129,8 +131,11 @@ __device__ __forceinline__ void publish(char* const* peer, int nranks, int parit
 // up to 7 extra round trips per phase).  Returns (thread 0) the first source whose flag never arrived, 0xff
 // when all did, and in `seen` the value that flag held when the wait gave up (diagnostics: an older epoch
 // = never written, a newer one = overwritten early).
+// acquire: the cached window (and TDE_XGMI_ACQUIRE=1) drops stale L1/L2 lines after the wait; the default
+// uncached window is never held in a cache, so its readers need no invalidation — and one system-scope
+// acquire per block per phase (256 per call) was measurable whole-L2 invalidation traffic.
 __device__ __forceinline__ uint32_t await(char* base, int parity, int phase, int nranks, int blk, uint32_t epoch,
-                                          long long timeout, uint32_t* err, uint32_t bit, uint32_t& seen) {
+                                          long long timeout, uint32_t* err, uint32_t bit, uint32_t& seen, bool acquire) {
   uint32_t missing = 0xffu;
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
@@ -163,7 +168,7 @@ __device__ __forceinline__ uint32_t await(char* base, int parity, int phase, int
         __hip_atomic_fetch_or(err, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
     }
-    __atomic_thread_fence(__ATOMIC_ACQUIRE);   // system scope: drop stale L1/L2 lines
+    if (acquire) __atomic_thread_fence(__ATOMIC_ACQUIRE);   // system scope: drop stale L1/L2 lines
     drain_stores();
   }
   __syncthreads();
@@ -306,7 +311,7 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
   XG_STAMP(2);
 
   // ---- phase 2: reduce own slice chunk from local HBM, push the result to every rank
-  miss1 = await(a.peer[r], parity, 0, N, blk, epoch, a.timeout_ticks, a.err, 1u, seen1);
+  miss1 = await(a.peer[r], parity, 0, N, blk, epoch, a.timeout_ticks, a.err, 1u, seen1, !UNCACHED || a.acquire);
   XG_STAMP(3);
   {
     const long long g0 = (long long)r * L + c0;
@@ -334,7 +339,7 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
   // ---- phase 3: gather every reduced slice chunk back into the bucket (or apply the update)
   float lr_t = 0.f;
   if (a.apply) lr_t = opt_lr_t(a.h, a.h.kind == kOptAdam ? *a.iterations : 0);
-  miss2 = await(a.peer[r], parity, 1, N, blk, epoch, a.timeout_ticks, a.err, 2u, seen2);
+  miss2 = await(a.peer[r], parity, 1, N, blk, epoch, a.timeout_ticks, a.err, 2u, seen2, !UNCACHED || a.acquire);
   XG_STAMP(5);
   const float* out = area(a.peer[r], 1, parity, cap);
   for (int s = 0; s < N; ++s) {
@@ -519,6 +524,11 @@ static int xg_fill(XgArgs& a, float* grad, long long M, long long max_elems, voi
   a.chunk = a.L / nblocks;
   a.cap = xg_cap(max_elems);
   a.timeout_ticks = timeout_ticks;
+  static const int force_acquire = [] {
+    const char* e = getenv("TDE_XGMI_ACQUIRE");
+    return e && atoi(e) != 0 ? 1 : 0;
+  }();
+  a.acquire = force_acquire;
   {
     std::lock_guard<std::mutex> lk(g_trace_mu);
     auto it = g_trace.find(epoch);
