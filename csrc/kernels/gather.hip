@@ -51,3 +51,55 @@ TDE_API int tde_gather_rows_dev(const void* src, long long row_bytes, long long 
   TDE_LAUNCH_CHECK();
   return 0;
 }
+
+// The per-execution staging of a device-resident batch group (x and y of every step) into the program's input
+// ring as ONE launch instead of one copy launch per tensor: up to kCopyPairs (src, dst, bytes) pairs; each pair
+// moves 16-byte vectors when its size and pointers allow, 4-byte words otherwise.
+namespace tde {
+constexpr int kCopyPairs = 4;
+struct CopyPairs {
+  const char* src[kCopyPairs];
+  char* dst[kCopyPairs];
+  long long bytes[kCopyPairs];
+  long long beg[kCopyPairs + 1];   // prefix offsets in 16-byte units over the pairs (each pair rounded up)
+  int v16[kCopyPairs];
+  int n;
+};
+__global__ __launch_bounds__(256) void copy_pairs_kernel(CopyPairs c) {
+  const long long total = c.beg[c.n];
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    int j = 0;
+    while (j + 1 < c.n && i >= c.beg[j + 1]) ++j;
+    const long long o = (i - c.beg[j]) * 16;   // byte offset of this thread's 16-byte unit in pair j
+    if (c.v16[j]) {
+      *reinterpret_cast<float4*>(c.dst[j] + o) = *reinterpret_cast<const float4*>(c.src[j] + o);
+    } else {
+      for (long long b = o; b < o + 16 && b < c.bytes[j]; b += 4)
+        *reinterpret_cast<int*>(c.dst[j] + b) = *reinterpret_cast<const int*>(c.src[j] + b);
+    }
+  }
+}
+}  // namespace tde
+
+TDE_API int tde_copy_pairs(int n, const void* const* src, void* const* dst, const long long* bytes, hipStream_t stream) {
+  if (n < 1 || n > kCopyPairs) return -1;
+  CopyPairs c{};
+  c.n = n;
+  long long units = 0;
+  for (int j = 0; j < n; ++j) {
+    if (bytes[j] < 0 || bytes[j] % 4 || ((uintptr_t)src[j] & 3) || ((uintptr_t)dst[j] & 3)) return -2;
+    c.src[j] = (const char*)src[j];
+    c.dst[j] = (char*)dst[j];
+    c.bytes[j] = bytes[j];
+    c.v16[j] = bytes[j] % 16 == 0 && ((uintptr_t)src[j] & 15) == 0 && ((uintptr_t)dst[j] & 15) == 0;
+    c.beg[j] = units;
+    units += (bytes[j] + 15) / 16;
+  }
+  c.beg[n] = units;
+  if (units == 0) return 0;
+  long long blocks = (units + 255) / 256;
+  blocks = blocks > 2048 ? 2048 : blocks;
+  copy_pairs_kernel<<<(int)blocks, 256, 0, stream>>>(c);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}

@@ -87,6 +87,7 @@ _HIP_PROTOS = {
     "tde_im2col": (i32, [p, p, i32, p, p, p, p]),
     "tde_stem_pack": (i32, [p, p, p, p, p, p]),
     "tde_gather_rows_dev": (i32, [p, i64, i64, p, i64, p, p, p]),
+    "tde_copy_pairs": (i32, [i32, p, p, p, p]),
     "tde_smallnet_limits": (i32, [p]),
     "tde_smallnet_step": (i32, [p, i32, i32, i32, p, p, i32, i32, i32, p, p, p, i32, p, i32, p, p, f32, p, i32,
                                 p, p]),

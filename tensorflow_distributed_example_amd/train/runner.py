@@ -12,12 +12,14 @@ device ring buffers [S, B, ...] filled by one async H2D (or D2D) copy.
 from __future__ import annotations
 
 import contextlib
+import ctypes as C
 import os
 import time
 
 import numpy as np
 import torch
 
+from .. import _native as N
 from . import program as PG
 
 
@@ -92,6 +94,13 @@ class _Stager:
             e.record(torch.cuda.current_stream(self.device))
             self.events[self.k] = e
         self.k = (self.k + 1) % len(self.bufs)
+
+
+def _same_device_pair(src, ring):
+    """A contiguous device tensor of the ring's dtype that fits it (copied without a cast or a host hop)."""
+    return (os.environ.get("TDE_STAGE_FUSED", "1") != "0" and torch.is_tensor(src) and ring.is_cuda
+            and src.device == ring.device and src.dtype == ring.dtype
+            and src.is_contiguous() and src.numel() <= ring.numel())
 
 
 class Program:
@@ -251,8 +260,16 @@ class Program:
         """per_replica_steps[r] = (x [S,B,...], y [S,B]) for local replica r."""
         for r, (x, y) in enumerate(per_replica_steps):
             with _ctx(self.devices[r]):
-                self.x_stage[r].stage(x, self.x_ring[r])
-                self.y_stage[r].stage(y, self.y_ring[r])
+                xr, yr = self.x_ring[r], self.y_ring[r]
+                if _same_device_pair(x, xr) and _same_device_pair(y, yr):
+                    # a device-resident batch group: x and y into the ring in ONE copy launch
+                    N.check(N.hip().tde_copy_pairs(
+                        2, (C.c_void_p * 2)(x.data_ptr(), y.data_ptr()), (C.c_void_p * 2)(xr.data_ptr(), yr.data_ptr()),
+                        (C.c_longlong * 2)(x.numel() * x.element_size(), y.numel() * y.element_size()),
+                        N.stream_ptr(xr.device)), "tde_copy_pairs")
+                    continue
+                self.x_stage[r].stage(x, xr)
+                self.y_stage[r].stage(y, yr)
 
     # ------------------------------------------------------------------ training
     def _reduce_and_apply(self):
