@@ -292,3 +292,27 @@ def test_convnet_fwd_geometries(fpw):
     r = subprocess.run([sys.executable, "-c", code], env=env, cwd=os.path.dirname(here), capture_output=True,
                        text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("sizes", [[64 * 784 * 20, 64 * 20], [3, 17, 0, 4096], [1]])
+def test_copy_pairs_stages_every_pair(sizes):
+    """tde_copy_pairs (the per-execution input staging, csrc/kernels/gather.hip): up to 4 (src, dst) pairs in
+    one launch, 16-byte vectors where sizes and pointers allow, 4-byte words for the rest (odd element counts,
+    an empty pair, a misaligned destination offset); bytes past each pair untouched."""
+    import ctypes as C
+    from tensorflow_distributed_example_amd import _native as N
+    g = torch.Generator(device="cpu").manual_seed(1)
+    srcs = [torch.randn(n, generator=g).to(DEV) for n in sizes]
+    # destinations: one element of offset for odd-numbered pairs (4-byte, not 16-byte, aligned), a guard tail
+    bufs = [torch.full((n + 8,), -7.0, device=DEV) for n in sizes]
+    dsts = [b[(i % 2): (i % 2) + n] for i, (b, n) in enumerate(zip(bufs, sizes))]
+    k = len(sizes)
+    rc = N.hip().tde_copy_pairs(k, (C.c_void_p * k)(*[s.data_ptr() for s in srcs]),
+                                (C.c_void_p * k)(*[d.data_ptr() for d in dsts]),
+                                (C.c_longlong * k)(*[4 * n for n in sizes]), N.stream_ptr())
+    assert rc == 0
+    torch.cuda.synchronize()
+    for i, (s, d, b, n) in enumerate(zip(srcs, dsts, bufs, sizes)):
+        assert torch.equal(s, d), i
+        off = i % 2
+        assert bool((b[:off] == -7.0).all()) and bool((b[off + n:] == -7.0).all()), i
