@@ -47,6 +47,6 @@ fi
 # topic sessions of this round (scripts/sessions/<name>.sh): equiv | buckets | ps | f32 | widths | cgen
 case "$MODE" in
   equiv) bash scripts/equiv_repeat.sh "${@:2}" || exit $? ;;
-  buckets|ps|f32|widths|cgen|cgen_ab|fpw_ab|rn_knobs|final|cgen_dp|cgen_hrep|hrep_ab|cgen_fpw|ps_prof|xg_acq|stage_ab|drv_trace|xg_unroll|bnpool_ab|copy_trace|xg_poll|stats) bash "scripts/sessions/$MODE.sh" || exit $? ;;
+  buckets|ps|f32|widths|cgen|cgen_ab|fpw_ab|rn_knobs|final|cgen_dp|cgen_hrep|hrep_ab|cgen_fpw|ps_prof|xg_acq|stage_ab|drv_trace|xg_unroll|bnpool_ab|copy_trace|xg_poll|stats|copy_ab) bash "scripts/sessions/$MODE.sh" || exit $? ;;
 esac
 echo "=== done"
