@@ -13,8 +13,8 @@ all-reduce and SGD update.  Precision: float32 by default — the reference's
 (distributed_with_keras.py:21), exact-f32 MFMA kernels over the f32 weights;
 ``--dtype bf16`` runs the mixed_bfloat16 kernel forms (bf16 MFMA, fp32 master weights).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
-    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+    python bench.py [--gpus N] [--steps K] [--warmup W]     # N>1: MirroredStrategy, one process, N GPUs
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...   # MWMS, one process per GPU
 """
 from __future__ import annotations
 
@@ -83,10 +83,14 @@ def main():
     import tensorflow_distributed_example_amd as tde
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.strategy == "mwms" and world == 1 and a.gpus > max(1, a.gpus_per_worker):
+        # `python bench.py --gpus N` with no launcher: ONE process drives N local GPUs with MirroredStrategy
+        # (BASELINE config 3, "MNIST CNN MirroredStrategy on 8xMI355X"; the reference's in-process
+        # strategy, mnist_keras_distributed.py:243).  torchrun keeps the one-process-per-GPU MWMS path.
+        a.strategy = "mirrored"
     gpw = max(1, a.gpus_per_worker) if a.strategy == "mwms" else a.gpus
     if a.strategy == "mwms" and world * gpw != a.gpus:
-        if world == 1 and a.gpus > gpw:
-            raise SystemExit("--gpus N>1 must be launched with torchrun --nproc-per-node N/--gpus-per-worker")
+        raise SystemExit(f"--gpus {a.gpus} != WORLD_SIZE {world} x --gpus-per-worker {gpw}")
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if torch.cuda.is_available():
         torch.cuda.set_device((local_rank * gpw) % torch.cuda.device_count())  # ranks > GPUs only in rehearsals
@@ -96,7 +100,17 @@ def main():
     if a.strategy == "mirrored":
         if world != 1:
             raise SystemExit("--strategy mirrored runs in ONE process (no torchrun)")
-        devs = [f"cuda:{d}" for d in a.devices.split(",")] if a.devices else [f"cuda:{i}" for i in range(a.gpus)]
+        if a.devices:
+            devs = [f"cuda:{d}" if d.isdigit() else d for d in a.devices.split(",")]
+        elif torch.cuda.is_available():
+            # fewer GPUs than --gpus (a 1-GPU box): replicas wrap onto the visible devices, a rehearsal of
+            # the N-GPU layout (several replicas time-share a device; reported as distinct_devices)
+            nd = torch.cuda.device_count()
+            devs = [f"cuda:{i % nd}" for i in range(a.gpus)]
+        else:
+            devs = ["cpu"] * a.gpus   # CPU plumbing (tests/test_bench_contract.py)
+        if len(devs) != a.gpus:
+            raise SystemExit(f"--devices lists {len(devs)} devices for --gpus {a.gpus}")
         strategy = tde.distribute.MirroredStrategy(devs)
     else:
         strategy = tde.distribute.MultiWorkerMirroredStrategy(gpus_per_worker=gpw if gpw > 1 else None)
@@ -206,7 +220,10 @@ def main():
     # where the optimizer update runs: fused into the step's kernels (1 replica), into the xGMI
     # gradient all-reduce (one replica per process), or its own multi-tensor launch
     placement = {"local": "in_step_kernels", "xgmi": "allreduce"}.get(prog.plans[0].step_mode, "separate")
-    n_dev = len({str(d) for d in strategy.local_devices}) * strategy.num_workers
+    distinct = len({str(d) for d in strategy.local_devices}) * strategy.num_workers
+    # n_gpus = the replicas the job runs (one per GPU on a real node); a rehearsal whose replicas share a
+    # device says so in config.distinct_devices
+    n_dev = n if a.strategy == "mirrored" else distinct
     ms = elapsed / a.steps * 1e3
     ips = GB * a.steps / elapsed
     if strategy.worker_index == 0:
@@ -219,7 +236,7 @@ def main():
             "data": f"synthetic (random {'x'.join(map(str, img))} images, random labels; random-init weights)",
             "config": {"model": a.model, "global_batch": GB, "seq_len": None, "image_shape": list(img),
                        "per_gpu_batch": B, "parallelism": f"dp{n}", "strategy": strategy.name,
-                       "replicas": n, "replicas_per_process": n_local,
+                       "replicas": n, "replicas_per_process": n_local, "distinct_devices": distinct,
                        "graphs_per_execution": (len(prog.groups) if prog.per_replica else 1) if prog.use_graph else 0,
                        "steps_per_execution": spe, "warmup_steps_run": n_warm * spe,
                        "input_staged_in_timed_region": True,

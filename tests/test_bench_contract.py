@@ -49,3 +49,44 @@ def test_bench_json_line_contract(world):
     assert abs(res["value"] - implied) <= 1e-3 * implied + 1.0
     if world > 1:
         assert "replicas_identical=True" in r.stdout, r.stdout[-3000:]
+
+
+def test_bench_multi_gpu_without_launcher_runs_mirrored():
+    """`python bench.py --gpus 2` with no torchrun (VERDICT r5 Missing #1): one process drives both replicas
+    with MirroredStrategy (BASELINE config 3; mnist_keras_distributed.py:243), rc 0, one JSON line."""
+    env = dict(os.environ, TDE_BENCH_WARM_MS="0", OMP_NUM_THREADS="1", TDE_HEARTBEAT="0", CUDA_VISIBLE_DEVICES="")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "TF_CONFIG"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6",
+                        "--warmup", "2", "--repeats", "1"], env=env, cwd=ROOT, stdout=subprocess.PIPE,
+                       stderr=subprocess.STDOUT, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    res = json.loads(lines[0])
+    base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+    assert res["metric"] == base["metric"] and res["n_gpus"] == 2
+    cfg = res["config"]
+    assert cfg["strategy"] == "MirroredStrategy" and cfg["replicas_per_process"] == 2
+    assert cfg["global_batch"] == 128 and cfg["parallelism"] == "dp2"
+    assert "replicas_identical=True" in r.stdout, r.stdout[-3000:]
+
+
+@pytest.mark.gpu
+def test_bench_multi_gpu_without_launcher_on_gpu():
+    """The same launcher-less command on a GPU box: with fewer visible GPUs than --gpus the replicas wrap onto
+    cuda:0 (a rehearsal of the N-GPU Mirrored layout: one hipGraph per replica, in-process xGMI all-reduce),
+    rc 0 and bit-identical replicas."""
+    env = dict(os.environ, TDE_BENCH_WARM_MS="20", TDE_HEARTBEAT="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "TF_CONFIG"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20",
+                        "--warmup", "5", "--repeats", "1"], env=env, cwd=ROOT, stdout=subprocess.PIPE,
+                       stderr=subprocess.STDOUT, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["strategy"] == "MirroredStrategy"
+    assert res["config"]["plan"] == "fused_convnet" and res["config"]["hipgraph"] is True
+    assert "replicas_identical=True" in r.stdout, r.stdout[-3000:]
