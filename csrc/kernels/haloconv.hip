@@ -1,0 +1,409 @@
+// Persistent halo-tile 3x3 / stride-1 / SAME convolution for 64-channel NHWC bf16 layers (the ResNet-18
+// stage-1 convs: 56x56x64 -> 56x56x64, forward and input gradient).  SURVEY.md §2.4 N1; the reference
+// triggers these through Keras Conv2D layers (no native code of its own).
+//
+// Why not the implicit GEMM of layers.hip: there every 64x64 output tile re-gathers its im2col rows (each
+// input pixel 9 times) and re-reads the whole 64x576 weight matrix through LDS-DMA — 147 KB per tile for
+// 2.4 M MAC (16 MAC/B), which bounds the stage-1 convs at ~37 us (≈ 48 GB/s per CU of LDS-DMA) against a
+// ~6 us MFMA floor.  Here one workgroup per CU (1 x 256 threads, 131 KB of LDS):
+//   * keeps the WHOLE weight tensor [9 taps][64 co][64 ci] (72 KB) resident in LDS for its lifetime;
+//   * walks a contiguous run of output tiles (2 image rows x W pixels x 64 co), holding the input rows in
+//     an 8-slot LDS ring: consecutive tiles share 2 of their 4 halo rows, so a tile loads only 2 new input
+//     rows (14 KB at W = 56) by LDS-DMA (buffer_load ... lds), issued one tile ahead (zero rows above /
+//     below the image come from the buffer range check; the two zero padding columns are never written);
+//   * runs the 9 taps x 2 channel halves as 18 k-steps of v_mfma_f32_16x16x32_bf16 straight out of the
+//     ring (no im2col at all: a tap is an address offset into the halo): 139 MAC per loaded byte.
+// Operands: A = weights (rows = output channels), B = activations (columns = pixels), so the 16x16
+// accumulator of a lane holds 4 CONSECUTIVE channels of one pixel: the epilogue is one 8-byte store per
+// lane and block (no LDS transpose), and the per-channel BatchNorm statistics of the stored (bf16-rounded)
+// outputs stay in registers across the workgroup's tiles (one f64 atomic pair per channel and wave at
+// the end, into kStatSlots interleaved slots like the implicit GEMM's epilogue).
+// The same kernel is the input gradient of such a layer: dX = conv(dY, W') with W'[tap][ci][co] =
+// W[8 - tap][ci][co] (the HWIO shadow read with flipped taps), optionally accumulated into dX.
+//
+// LDS images: 16-byte chunk q of a 128-byte row r (weight row r = output channel, ring row r = halo
+// column) lives at physical chunk q ^ ((r >> 1) & 7): the 16-lane groups of every ds_read_b128 below
+// then touch 16 distinct bank quads.  Ring slots are (W + 2) * 128 + 64 bytes apart (the 64-byte shift
+// keeps a fragment that straddles two image rows conflict-free too).
+#include "tde_common.h"
+
+namespace tde {
+namespace halo {
+
+constexpr int kC = 64;               // input and output channels
+constexpr int kPix = 128;            // bytes per pixel row (64 bf16)
+constexpr int kWBytes = 9 * 64 * kPix;
+constexpr int kSlots = 8;            // BN statistic slots (layers.hip kStatSlots)
+
+struct Args {
+  const bf16* x;       // [B,H,W,64] (forward: the input; input gradient: dY)
+  const bf16* w;       // weights, element (tap, n, k) at w[tap' * wst + n * wsn + k], tap' = flip ? 8 - tap : tap
+  long long wst, wsn;
+  int flip;
+  bf16* y;             // [B,H,W,64] output (forward: Y; input gradient: dX)
+  int accum;           // y += result
+  double* colstats;    // [kSlots][2][64] sum / sum of squares of the stored values, or null
+  int B, H, W;
+  int x_bytes;         // B*H*W*128 (< 2^31: the buffer resource range)
+  long long* stamps;   // diagnostic phase clock (tde_halo_stamps), null in production
+};
+
+__device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
+// MFMA column j -> pixel of its 16-pixel block.  A ds_read_b128 serves lanes {0-3,12-15} with {20-27} (and
+// {4-11} with {16-19,28-31}) in one LDS cycle: the first set reads logical chunk L (columns j = 0-3,
+// 12-15), the second chunk L+1 (columns 4-11).  Giving the first set the even pixels and the second the odd
+// ones puts the two sets in different 128-byte halves of the 256-byte bank row for ANY halo shift (tap
+// column kw, block start), and the (r >> 1) & 7 swizzle spreads each set over its half: conflict-free
+// except where a block straddles two image rows (bench/halo_micro.py; 2-way on 8 % of the reads at W=56).
+__device__ __forceinline__ int pcol_perm(int j) { return j < 4 ? 2 * j : (j >= 12 ? 2 * j - 16 : 2 * j - 7); }
+
+struct Rsrc {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __amdgpu_buffer_rsrc_t r;
+#endif
+};
+__device__ __forceinline__ Rsrc make_rsrc(const void* base, int bytes) {
+  Rsrc b;
+#if defined(__HIP_DEVICE_COMPILE__)
+  b.r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, 0x00020000);
+#endif
+  return b;
+}
+// 16-byte LDS-DMA load: lane i lands at lds + 16 i; offsets at or past the range read zeros
+__device__ __forceinline__ void dma16(const Rsrc& b, char* lds, int voff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(b.r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+#endif
+}
+template <int N>
+__device__ __forceinline__ void vmwait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// TR image rows per tile (TR * W <= 16 * 2 * PB pixels); the 4 waves form a 2 x 2 grid: wave (wp, wc) owns
+// pixel blocks PB*wp .. PB*wp + PB-1 of the tile and output-channel blocks 2wc, 2wc + 1, so per k-step
+// 2 weight + PB activation fragment reads feed 2 * PB MFMAs (PB = 7 at 4 rows x 56: no padded block).
+// The ring holds 2 TR + 4 rows: the current tile's TR + 2 and up to TR + 2 prefetched ones.
+// The epilogue of tile t (bf16 conversion, BN statistics, 8-byte stores, the accumulated form's add) runs
+// inside tile t + 1's k-loop, one (channel block, pixel block) pair per k-step, while that step's MFMAs
+// are in flight: the two accumulator sets ping-pong by unrolling the tile loop twice.
+// DBG (diagnostic builds only, tde_halo_debug): 1 = no MFMAs in the k loop (LDS reads only), 2 = no
+// activation reads in the k loop (MFMAs on stale fragments), 3 = both off
+template <int TR, int PB, int DBG = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void conv3x3_kernel(Args a) {
+  constexpr int RING = 2 * TR + 4;
+  constexpr int NE = 2 * PB;  // epilogue pairs per tile (<= 18 k-steps)
+  static_assert(NE <= 18, "one epilogue pair per k-step");
+  extern __shared__ __attribute__((aligned(16))) unsigned char hsm[];
+  char* const wl = reinterpret_cast<char*>(hsm);
+  char* const ring = wl + kWBytes;
+  const int W = a.W, H = a.H;
+  const int SS = (W + 2) * kPix + 64;
+  const int TRW = TR * W;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wp = wave >> 1, wc = wave & 1;
+  const int tpi = H / TR;  // tiles per image
+  const int ntiles = a.B * tpi;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int t0 = (int)((long long)g * ntiles / G), t1 = (int)((long long)(g + 1) * ntiles / G);
+  if (t0 >= t1) return;
+
+  // ---- prologue: zero padding columns of every ring slot, weights -> LDS (swizzled)
+  for (int i = tid; i < RING * 2 * 8; i += 256) {
+    const int s = i >> 4, side = (i >> 3) & 1, ch = i & 7;
+    *reinterpret_cast<uint4*>(ring + s * SS + (side ? (W + 1) * kPix : 0) + ch * 16) = make_uint4(0, 0, 0, 0);
+  }
+  stamp(a.stamps, 0);
+  {  // weights by LDS-DMA: instruction (tap, 8-row group) fills rows n0 .. n0+7 of the tap; lane l lands in
+     // physical chunk l % 8 of row n0 + l / 8 and so fetches logical chunk (l % 8) ^ swz(row)
+    const Rsrc rw = make_rsrc(a.w, 9 * kC * kC * 2);
+    const int n = (lane >> 3), p = lane & 7;
+    for (int j = wave; j < 72; j += 4) {
+      const int tap = j >> 3, n0 = (j & 7) * 8;
+      const int st = a.flip ? 8 - tap : tap;
+      const int row = n0 + n;
+      dma16(rw, wl + tap * (kC * kPix) + n0 * kPix, (int)((st * a.wst + row * a.wsn + ((p ^ swz(row)) << 3)) * 2));
+    }
+  }
+
+  // ---- halo rows by LDS-DMA: W/8 one-KiB instructions per row, dealt round-robin over the 4 waves
+  const Rsrc rs = make_rsrc(a.x, a.x_bytes);
+  const int per_row = W >> 3;
+  auto issue_rows = [&](int b, int r_first, int nrows, int slot_first) {
+    const int n = nrows * per_row;
+    for (int j = wave; j < n; j += 4) {
+      const int rr = j / per_row, jj = j - rr * per_row;
+      const int r = r_first + rr;
+      int slot = slot_first + rr;
+      while (slot >= RING) slot -= RING;
+      const int p = jj * 8 + (lane >> 3);  // image column
+      const int lc = (lane & 7) ^ swz(p + 1);
+      const int voff = (unsigned)r < (unsigned)H ? (((b * H + r) * W + p) * kPix + (lc << 4)) : (int)0x80000000;
+      dma16(rs, ring + slot * SS + kPix + jj * 1024, voff);
+    }
+  };
+
+  // ---- per-lane fragment offsets (tile invariant)
+  const int q = lane >> 4, li = lane & 15;
+  int aoff[2][2];  // weights: [co block][channel half]
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    const int n = 32 * wc + 16 * cb + li;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) aoff[cb][c] = n * kPix + (((4 * c + q) ^ swz(n)) << 4);
+  }
+  bool pbv[PB];
+  int prow[PB], pcol[PB], coff[PB][3][2];  // pixel block: tile row, column; [kw][channel half] column offsets
+#pragma unroll
+  for (int pb = 0; pb < PB; ++pb) {
+    const int blk = PB * wp + pb;
+    pbv[pb] = 16 * blk < TRW;  // wave-uniform
+    int p = 16 * blk + pcol_perm(li);
+    if (p >= TRW) p = 0;
+    prow[pb] = p / W;
+    pcol[pb] = p - prow[pb] * W;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int hc = pcol[pb] + kw;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) coff[pb][kw][c] = hc * kPix + (((4 * c + q) ^ swz(hc)) << 4);
+    }
+  }
+  float s1[2][4], s2[2][4];
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s1[cb][r] = s2[cb][r] = 0.f;
+
+  // epilogue pair e = (cb = e % 2, pb = e / 2) of a finished tile: its 4 channels of one pixel per lane
+  auto epi = [&](const f32x4 (&acc)[2][PB], const bf16x4 (&old)[2][PB], const long long (&gp)[PB], int e) {
+    const int cb = e & 1, pb = e >> 1;
+    if (!pbv[pb]) return;
+    float v[4] = {acc[cb][pb][0], acc[cb][pb][1], acc[cb][pb][2], acc[cb][pb][3]};
+    if (a.accum) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += bf2f(old[cb][pb][r]);
+    }
+    bf16x4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      o[r] = f2bf(v[r]);
+      const float qv = bf2f(o[r]);
+      s1[cb][r] += qv;
+      s2[cb][r] += qv * qv;
+    }
+    *reinterpret_cast<bf16x4*>(a.y + gp[pb] + 32 * wc + 16 * cb + 4 * q) = o;
+  };
+
+  f32x4 accA[2][PB], accB[2][PB];
+  bf16x4 oldA[2][PB], oldB[2][PB];
+  long long gpA[PB], gpB[PB];
+  int s0 = 0;
+  {
+    const int b = t0 / tpi, r0 = TR * (t0 - b * tpi);
+    issue_rows(b, r0 - 1, TR + 2, 0);
+  }
+  // one tile: its MFMA loop with the previous tile's epilogue (conversion, statistics, stores) folded in
+  auto tile = [&](int t, f32x4 (&acc)[2][PB], bf16x4 (&old)[2][PB], long long (&gp)[PB],
+                  const f32x4 (&pacc)[2][PB], const bf16x4 (&pold)[2][PB], const long long (&pgp)[PB]) {
+    // this tile's rows have landed (DMA issued one tile ago; older stores and old-value reads long done).
+    // The builtin form of the wait (not inline asm) tells the compiler's wait-count pass that nothing is
+    // outstanding here, so the folded epilogue below never waits on this tile's prefetch DMA.
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_s_barrier();
+    if (t == t0) stamp(a.stamps, 1);
+    const int b = t / tpi, r0 = TR * (t - b * tpi);
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb) gp[pb] = ((long long)(b * H + r0 + prow[pb]) * W + pcol[pb]) * kC;
+    if (a.accum) {  // the accumulated form's old values, read before the prefetch DMA is queued behind them
+#pragma unroll
+      for (int pb = 0; pb < PB; ++pb) {
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          old[cb][pb] = pbv[pb] ? *reinterpret_cast<const bf16x4*>(a.y + gp[pb] + 32 * wc + 16 * cb + 4 * q)
+                                : bf16x4{};
+      }
+    }
+    int snext = s0;
+    if (t + 1 < t1) {  // prefetch the next tile's new rows into slots the current tile does not use
+      const int nb = (t + 1) / tpi, nr0 = TR * ((t + 1) - nb * tpi);
+      if (nb == b) {
+        issue_rows(b, r0 + TR + 1, TR, s0 + TR + 2);
+        snext = s0 + TR;
+      } else {
+        issue_rows(nb, nr0 - 1, TR + 2, s0 + TR + 2);
+        snext = s0 + TR + 2;
+      }
+    }
+    int rbase[PB][3];
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb)
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        int sl = s0 + prow[pb] + kh;
+        while (sl >= RING) sl -= RING;
+        rbase[pb][kh] = sl * SS;
+      }
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int pb = 0; pb < PB; ++pb) acc[cb][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // 18 k-steps (tap, channel half), software-pipelined by hand: the fragments of step s + 1 are read
+    // before the MFMAs of step s, so one wave per SIMD keeps its LDS latency under the matrix pipe
+    auto load_step = [&](int s, bf16x8* af, bf16x8* bv) {
+      const int tap = s >> 1, c = s & 1, kh = tap / 3, kw = tap - 3 * (tap / 3);
+      const char* wt = wl + tap * (kC * kPix);
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) af[cb] = *reinterpret_cast<const bf16x8*>(wt + aoff[cb][c]);
+      // a pixel block past the tile reads pixel 0 and is never stored: no branches in the k loop
+#pragma unroll
+      for (int pb = 0; pb < PB; ++pb)
+        bv[pb] = *reinterpret_cast<const bf16x8*>(ring + rbase[pb][kh] + coff[pb][kw][c]);
+    };
+    bf16x8 fa[2][2], fb[2][PB];
+    load_step(0, fa[0], fb[0]);
+    load_step(1, fa[1], fb[1]);
+#pragma unroll
+    for (int s = 0; s < 18; ++s) {
+      const int cur = s & 1;
+      if (s + 1 < 18 && s > 0 && !(DBG & 2)) load_step(s + 1, fa[cur ^ 1], fb[cur ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
+      if (!(DBG & 1)) {
+#pragma unroll
+        for (int pb = 0; pb < PB; ++pb)
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) acc[cb][pb] = mfma16(fa[cur][cb], fb[cur][pb], acc[cb][pb]);
+      } else {
+#pragma unroll
+        for (int pb = 0; pb < PB; ++pb)
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) acc[cb][pb][0] += (float)fa[cur][cb][0] * (float)fb[cur][pb][1];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (s < NE && t > t0) epi(pacc, pold, pgp, s);  // VALU + one store beside the MFMAs in flight
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (t == t0) stamp(a.stamps, 2);
+    s0 = snext >= RING ? snext - RING : snext;
+  };
+  int t = t0;
+  for (; t + 1 < t1; t += 2) {
+    tile(t, accA, oldA, gpA, accB, oldB, gpB);
+    tile(t + 1, accB, oldB, gpB, accA, oldA, gpA);
+  }
+  if (t < t1) {
+    tile(t, accA, oldA, gpA, accB, oldB, gpB);
+#pragma unroll
+    for (int e = 0; e < NE; ++e) epi(accA, oldA, gpA, e);
+  } else {
+#pragma unroll
+    for (int e = 0; e < NE; ++e) epi(accB, oldB, gpB, e);
+  }
+  stamp(a.stamps, 4);
+  if (a.colstats) {
+    // fold the two pixel-half waves of each channel half in LDS (the ring is free now), then one f64 atomic
+    // pair per channel and workgroup
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(ring);  // [wp][2 stats][64 channels]
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float t1s = row16_sum(s1[cb][r]), t2s = row16_sum(s2[cb][r]);
+        if (li == 0) {
+          const int co = 32 * wc + 16 * cb + 4 * q + r;
+          red[(wp * 2 + 0) * kC + co] = t1s;
+          red[(wp * 2 + 1) * kC + co] = t2s;
+        }
+      }
+    __syncthreads();
+    if (tid < 2 * kC) {
+      double* st = a.colstats + (size_t)(g % kSlots) * 2 * kC;
+      atomicAdd(&st[tid], (double)(red[tid] + red[2 * kC + tid]));
+    }
+  }
+  stamp(a.stamps, 5);
+}
+
+}  // namespace halo
+}  // namespace tde
+
+using namespace tde;
+
+static int halo_lds_bytes(int W, int TR) { return halo::kWBytes + (2 * TR + 4) * ((W + 2) * halo::kPix + 64); }
+
+// rows per tile: the largest TR in {8, 4, 2} with H % TR == 0, TR * W <= 256 and the LDS footprint <= 160 KiB
+// the instantiated (rows per tile, pixel blocks per wave) forms: PB = ceil(TR * W / 32) rounded up to 4 or 7
+typedef void (*HaloKern)(halo::Args);
+static int g_halo_dbg = 0;
+TDE_API void tde_halo_debug(int mode) { g_halo_dbg = mode; }
+static HaloKern halo_kernel(int tr, int pb) {
+  if (pb > 7) return nullptr;
+  if (pb > 4) {
+    if (tr == 4) {  // ResNet-18 stage 1: 4 x 56 pixels
+      if (g_halo_dbg == 1) return halo::conv3x3_kernel<4, 7, 1>;
+      if (g_halo_dbg == 2) return halo::conv3x3_kernel<4, 7, 2>;
+      if (g_halo_dbg == 3) return halo::conv3x3_kernel<4, 7, 3>;
+      return halo::conv3x3_kernel<4, 7>;
+    }
+    return tr == 2 ? halo::conv3x3_kernel<2, 7> : tr == 8 ? halo::conv3x3_kernel<8, 7> : nullptr;
+  }
+  return tr == 2 ? halo::conv3x3_kernel<2, 4> : tr == 4 ? halo::conv3x3_kernel<4, 4>
+       : tr == 8 ? halo::conv3x3_kernel<8, 4> : nullptr;
+}
+
+// rows per tile: the largest TR in {8, 4, 2} with H % TR == 0, at most 7 pixel blocks per wave
+// (TR * W <= 224) and the LDS footprint <= 160 KiB
+static int halo_rows(int H, int W) {
+  for (int tr : {8, 4, 2})
+    if (H % tr == 0 && tr * W <= 224 && halo_lds_bytes(W, tr) <= 160 * 1024) return tr;
+  return 0;
+}
+
+static long long* g_halo_stamps = nullptr;
+// diagnostics: the next launches record per-workgroup phase clocks ([grid][kMaxStamps] s_memrealtime ticks)
+TDE_API void tde_halo_stamps(long long* buf) { g_halo_stamps = buf; }
+
+TDE_API int tde_halo_conv_ok(int C, int Co, int H, int W, int B) {
+  if (C != halo::kC || Co != halo::kC) return 0;
+  if (W % 8 != 0 || W < 8 || H < 2) return 0;
+  if ((long long)B * H * W * halo::kPix >= (1LL << 31)) return 0;
+  const int tr = halo_rows(H, W);
+  return tr > 0 && halo_kernel(tr, (tr * W + 31) / 32) != nullptr;
+}
+
+// y[B,H,W,64] (=|+=) conv3x3_s1_same(x, w); weights element (tap, n, k) at w[tap' * wst + n * wsn + k]
+TDE_API int tde_halo_conv3x3(const bf16* x, const bf16* w, long long wst, long long wsn, int flip, bf16* y, int accum,
+                             double* colstats, int B, int H, int W, int grid, hipStream_t stream) {
+  if (!tde_halo_conv_ok(64, 64, H, W, B)) return -2;
+  if (((uintptr_t)x & 15) || ((uintptr_t)w & 15) || ((uintptr_t)y & 7) || (wst % 8) || (wsn % 8)) return -3;
+  const int tr = halo_rows(H, W);
+  const int lds = halo_lds_bytes(W, tr);
+  const HaloKern fn = halo_kernel(tr, (tr * W + 31) / 32);
+  static HaloKern attr_done[16] = {nullptr};
+  bool done = false;
+  for (int i = 0; i < 16 && attr_done[i]; ++i) done |= attr_done[i] == fn;
+  if (!done) {
+    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+      return -4;
+    for (int i = 0; i < 16; ++i)
+      if (!attr_done[i]) {
+        attr_done[i] = fn;
+        break;
+      }
+  }
+  const int ntiles = B * (H / tr);
+  if (grid <= 0) {
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    grid = cus;
+  }
+  if (grid > ntiles) grid = ntiles;
+  halo::Args a{x, w, wst, wsn, flip, y, accum, colstats, B, H, W, (int)((long long)B * H * W * halo::kPix),
+               g_halo_stamps};
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(256), lds, stream, a);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}

@@ -154,6 +154,32 @@ def conv_fwd(x, Wt, y, g: ConvGeom, bias=None, relu=False, colstats=None, scratc
            bias=bias, relu=relu, colstats=colstats, scratch=scratch)
 
 
+def halo_ok(g: ConvGeom, dgrad=False):
+    """The persistent halo-tile kernel (csrc/kernels/haloconv.hip) covers 3x3 / stride-1 / SAME convs with 64
+    input and output channels (ResNet-18 stage 1), forward and input gradient.  TDE_HALO=0 disables it."""
+    if os.environ.get("TDE_HALO", "1") == "0":
+        return False
+    if (g.KH, g.KW, g.sh, g.sw, g.pt, g.pl) != (3, 3, 1, 1, 1, 1) or (g.Ho, g.Wo) != (g.H, g.W):
+        return False
+    return bool(N.hip().tde_halo_conv_ok(g.C, g.Co, g.H, g.W, g.B))
+
+
+def halo_conv(x, w, y, g: ConvGeom, *, dgrad=False, accum=False, colstats=None, grid=0):
+    """Forward: y = conv3x3(x, W) with ``w`` = Wt [Co, 9*C] (the transposed shadow; element (tap, co, ci) at
+    co*9C + tap*C + ci).  Input gradient (``dgrad``): y (=|+=) conv3x3(dY, W') with ``w`` = the HWIO shadow
+    [3,3,C,Co] read with flipped taps (element (tap, ci, co) at (8-tap)*C*Co + ci*Co + co)."""
+    n = g.B * g.H * g.W * 64
+    _bf(x, n, "halo_conv x")
+    _bf(y, n, "halo_conv y")
+    _bf(w, 9 * 64 * 64, "halo_conv w")
+    _req(halo_ok(g, dgrad), "halo_conv: geometry not covered")
+    if colstats is not None:
+        _f64(colstats, 2 * STAT_SLOTS * 64, "halo_conv colstats")
+    wst, wsn = (64 * 64, 64) if dgrad else (64, 9 * 64)
+    N.check(N.hip().tde_halo_conv3x3(_P(x), _P(w), wst, wsn, int(dgrad), _P(y), int(accum), _P(colstats), g.B, g.H,
+                                     g.W, int(grid), _s()), "tde_halo_conv3x3")
+
+
 def conv_dgrad(dy, Wrow, dx, g: ConvGeom, accum=False, scratch=None):
     """dx[B,H,W,C] (=|+=) conv_transpose(dy[B,Ho,Wo,Co], W); Wrow = HWIO bf16."""
     _bf(dy, g.B * g.Ho * g.Wo * g.Co, "conv_dgrad dy")

@@ -479,6 +479,10 @@ class _Gemm(_Stage):
             # (TDE_SMALLWG_IM2COL=1: also for layers whose forward runs on an explicit im2col matrix)
             self.small_wgrad = (narrow and O.smallconv_wgrad_ok(self.geo)
                                 and (not self.use_im2col or os.environ.get("TDE_SMALLWG_IM2COL", "0") == "1"))
+        # 3x3 / stride-1 / SAME 64-channel convs without bias or activation (ResNet-18 stage 1): the persistent
+        # halo-tile kernel (csrc/kernels/haloconv.hip) for the forward and the input gradient
+        self.halo = (self.conv and not self.f32 and not (self.small_fwd or self.use_im2col or self.use_stem_pack)
+                     and self.b is None and not self.relu and O.halo_ok(self.geo))
         self.colstats = None
         self.dz = None
         self.act_done = False   # the consumer's launch already applied the ReLU mask / bias gradient
@@ -569,6 +573,8 @@ class _Gemm(_Stage):
             O.im2col(self.inp.buf, g, self.xcol, self.Wt, self.Wt_pad)
             O.conv_fwd_im2col(self.xcol, self.Wt_pad, self.out.root().buf, g, self.Kp, bias=self.b, relu=self.relu,
                               colstats=cs, scratch=p.scratch)
+        elif self.conv and self.halo:
+            O.halo_conv(self.inp.buf, self.Wt, self.out.root().buf, self.geo.with_batch(B), colstats=cs)
         elif self.conv and self.small_fwd:
             O.smallconv_fwd(self.inp.buf, self.Wrow, self.out.root().buf, self.geo.with_batch(B), bias=self.b,
                             relu=self.relu, colstats=cs)
@@ -610,6 +616,8 @@ class _Gemm(_Stage):
             g = self.geo.with_batch(B)
             if self.small_dgrad:
                 O.smallconv_dgrad(dout, self.Wrow, self.inp.root().grad, g, accum=self.accum[self.inp.root().id])
+            elif self.halo:
+                O.halo_conv(dout, self.Wrow, self.inp.root().grad, g, dgrad=True, accum=self.accum[self.inp.root().id])
             else:
                 O.conv_dgrad(dout, self.Wrow, self.inp.root().grad, g, accum=self.accum[self.inp.root().id],
                              scratch=p.scratch)

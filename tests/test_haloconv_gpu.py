@@ -1,0 +1,76 @@
+"""The persistent halo-tile 3x3 conv (csrc/kernels/haloconv.hip) vs a float64 host oracle of the same op on the
+same bf16 operands: forward (+ BN statistics of the stored bf16 outputs), input gradient (flipped taps of the
+HWIO shadow), accumulated input gradient, and grids that split an image's tiles over several workgroups or
+give one workgroup tiles of two images (the ring's non-contiguous refill)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from tensorflow_distributed_example_amd import _native as N
+from tensorflow_distributed_example_amd.ops import layer_ops as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+bf = torch.bfloat16
+
+
+def _r(*shape, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return torch.randn(*shape, generator=g).to(bf)
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _geo(B, H, W):
+    return O.ConvGeom(B, H, W, 64, H, W, 64, 3, 3, 1, 1, 1, 1)
+
+
+CASES = [(2, 56, 56, 0), (3, 56, 56, 5), (2, 56, 56, 37), (4, 28, 32, 0), (2, 8, 64, 3), (2, 16, 32, 3), (3, 24, 24, 2)]
+
+
+@pytest.mark.parametrize("B,H,W,grid", CASES)
+def test_halo_forward_and_stats(B, H, W, grid):
+    g = _geo(B, H, W)
+    assert O.halo_ok(g)
+    x = _r(B, H, W, 64, seed=1)
+    w = _r(3, 3, 64, 64, seed=2) * 0.05           # HWIO
+    wt = w.permute(3, 0, 1, 2).reshape(64, 576).contiguous()   # [Co, kh, kw, ci]
+    y = torch.zeros(B * H * W * 64, dtype=bf, device=DEV)
+    st = torch.zeros(2 * O.STAT_SLOTS * 64, dtype=torch.float64, device=DEV)
+    O.halo_conv(x.to(DEV).reshape(-1), wt.to(DEV), y, g, colstats=st, grid=grid)
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.double().permute(0, 3, 1, 2), w.double().permute(3, 2, 0, 1), padding=1).permute(0, 2, 3, 1)
+    out = y.view(B, H, W, 64).cpu()
+    assert _rel(out, ref) < 4e-3
+    q = out.double().reshape(-1, 64)
+    s = st.view(O.STAT_SLOTS, 2, 64).sum(0).cpu()
+    assert torch.allclose(s[0], q.sum(0), rtol=2e-5, atol=1e-3)   # f32 per-lane partials, f64 atomics
+    assert torch.allclose(s[1], (q * q).sum(0), rtol=2e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("B,H,W,grid", CASES[:3])
+@pytest.mark.parametrize("accum", [False, True])
+def test_halo_input_gradient(B, H, W, grid, accum):
+    g = _geo(B, H, W)
+    dy = _r(B, H, W, 64, seed=3)
+    w = _r(3, 3, 64, 64, seed=4) * 0.05           # HWIO: the row shadow
+    base = _r(B, H, W, 64, seed=5)
+    dx = (base.clone() if accum else torch.zeros_like(base)).to(DEV).reshape(-1)
+    O.halo_conv(dy.to(DEV).reshape(-1), w.contiguous().to(DEV), dx, g, dgrad=True, accum=accum, grid=grid)
+    torch.cuda.synchronize()
+    xd = torch.zeros(B, 64, H, W, dtype=torch.float64, requires_grad=True)
+    yd = F.conv2d(xd, w.double().permute(3, 2, 0, 1), padding=1)
+    yd.backward(dy.double().permute(0, 3, 1, 2))
+    ref = xd.grad.permute(0, 2, 3, 1)
+    if accum:
+        ref = ref + base.double()
+    assert _rel(dx.view(B, H, W, 64).cpu(), ref) < 4e-3
+
+
+def test_halo_rejects_other_geometries():
+    assert not O.halo_ok(O.ConvGeom(2, 28, 28, 128, 28, 28, 128, 3, 3, 1, 1, 1, 1))
+    assert not O.halo_ok(O.ConvGeom(2, 56, 56, 64, 28, 28, 64, 3, 3, 2, 2, 0, 0))
+    assert N.hip().tde_halo_conv_ok(64, 64, 56, 60, 2) == 0   # W % 8

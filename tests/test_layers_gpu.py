@@ -377,6 +377,21 @@ def test_small_resnet_layerwise_matches_bf16_oracle():
     _emulated_compare(m, rng.standard_normal((16, 32, 32, 3), dtype=np.float32), rng.integers(0, 10, 16), 16, 6e-2)
 
 
+def test_small_resnet_halo_stage_matches_bf16_oracle():
+    """A 64-filter first stage at 16x16 runs its 3x3 convs (forward and input gradient, accumulated into the
+    shortcut's gradient) through the persistent halo-tile kernel (csrc/kernels/haloconv.hip)."""
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.train import layerwise as LW
+    m = tde.zoo.resnet((1, 1), (64, 32), input_shape=(64, 64, 3), classes=10, name="halo_resnet")
+    m.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True), optimizer=tde.optimizers.SGD(0.01))
+    m.build()
+    rng = np.random.default_rng(3)
+    plan = _emulated_compare(m, rng.standard_normal((8, 64, 64, 3), dtype=np.float32), rng.integers(0, 10, 8), 8,
+                             6e-2)
+    halo = [st for st in plan.stages if isinstance(st, LW._Gemm) and st.halo]
+    assert len(halo) == 2, [st.layer.name for st in halo]
+
+
 def _grad_compare(model, x, y, B, thresholds, default=0.05):
     from tensorflow_distributed_example_amd.train import program as PG
     from tensorflow_distributed_example_amd.train.layerwise import LayerwisePlan
