@@ -237,8 +237,10 @@ def _batchnorm(g, layer, x, read):
     return g.node(f"{nm}/batchnorm/add_1", "AddV2", [m1, sb], **_float_attrs())
 
 
-def _saver(g: GraphBuilder, var_shapes, handles):
-    """The TF1 ``save/`` subgraph over the variables (V2 checkpoint format); returns the SaverDef."""
+def _saver(g: GraphBuilder, var_shapes, handles, dtypes=None):
+    """The TF1 ``save/`` subgraph over the variables (V2 checkpoint format); returns the SaverDef.
+    ``dtypes``: per-variable DataType (default all DT_FLOAT)."""
+    dtypes = list(dtypes) if dtypes is not None else [DT_FLOAT] * len(var_shapes)
     names = np.array([n.encode() for n, _ in var_shapes], dtype=object)
     slices = np.array([b""] * len(var_shapes), dtype=object)
     fname = g.const("save/filename/input", np.array(b"model", dtype=object))
@@ -246,19 +248,19 @@ def _saver(g: GraphBuilder, var_shapes, handles):
     prefix = g.node("save/Const", "PlaceholderWithDefault", [fph], dtype=A.type(DT_STRING), shape=A.shape([]))
     tn = g.const("save/SaveV2/tensor_names", names)
     sl = g.const("save/SaveV2/shape_and_slices", slices)
-    reads = [g.node(f"save/Read_{i}/ReadVariableOp", "ReadVariableOp", [handles[n]], dtype=A.type(DT_FLOAT))
+    reads = [g.node(f"save/Read_{i}/ReadVariableOp", "ReadVariableOp", [handles[n]], dtype=A.type(dtypes[i]))
              for i, (n, _) in enumerate(var_shapes)]
-    save = g.node("save/SaveV2", "SaveV2", [prefix, tn, sl] + reads, dtypes=A.types([DT_FLOAT] * len(var_shapes)))
+    save = g.node("save/SaveV2", "SaveV2", [prefix, tn, sl] + reads, dtypes=A.types(dtypes))
     dep = g.node("save/control_dependency", "Identity", [prefix, f"^{save}"], T=A.type(DT_STRING),
                  _class=_msg(1, _fb(2, f"loc:@{prefix}".encode())))
     rtn = g.const("save/RestoreV2/tensor_names", names)
     rsl = g.const("save/RestoreV2/shape_and_slices", slices)
-    rst = g.node("save/RestoreV2", "RestoreV2", [prefix, rtn, rsl], dtypes=A.types([DT_FLOAT] * len(var_shapes)))
+    rst = g.node("save/RestoreV2", "RestoreV2", [prefix, rtn, rsl], dtypes=A.types(dtypes))
     assigns = []
     for i, (n, _) in enumerate(var_shapes):
-        idn = g.node(f"save/Identity_{i}", "Identity", [f"{rst}:{i}"], T=A.type(DT_FLOAT))
+        idn = g.node(f"save/Identity_{i}", "Identity", [f"{rst}:{i}"], T=A.type(dtypes[i]))
         assigns.append(g.node(f"save/AssignVariableOp_{i}", "AssignVariableOp", [handles[n], idn],
-                              dtype=A.type(DT_FLOAT), validate_shape=A.b(False)))
+                              dtype=A.type(dtypes[i]), validate_shape=A.b(False)))
     g.node("save/restore_all", "NoOp", [f"^{a}" for a in assigns])
     # SaverDef: filename_tensor_name = 1, save_tensor_name = 2, restore_op_name = 3, max_to_keep = 4,
     # sharded = 5, keep_checkpoint_every_n_hours = 6, version = 7 (V2)
@@ -286,6 +288,46 @@ def saved_model_bytes(model, input_shape=None, input_key="input", output_key=Non
     meta = (_msg(1, meta_info) + _msg(2, g.graph_def()) + _msg(3, saver_def)
             + _msg(5, _fb(1, "serving_default") + _msg(2, sig)))
     return _fv(1, 1) + _msg(2, meta)
+
+
+# ------------------------------------------------------------------ Estimator checkpoint metadata
+_NP_DT = {np.dtype(np.float32): DT_FLOAT, np.dtype(np.float64): 2, np.dtype(np.int32): DT_INT32,
+          np.dtype(np.uint8): 4, np.dtype(np.int64): 9, np.dtype(np.bool_): 10}
+
+
+def checkpoint_meta_graph_bytes(model, tensors: dict) -> bytes:
+    """``model.ckpt-N.meta``: the MetaGraphDef a TF1 Saver writes next to each checkpoint (RunConfig(model_dir,
+    save_checkpoints_steps), mnist_keras_distributed.py:245,248).  Its GraphDef is the model's inference graph
+    (build_graph) plus a resource variable for every other tensor of the bundle (``global_step`` int64,
+    optimizer slots, iterator state), and its SaverDef points at a ``save/`` subgraph whose SaveV2 /
+    RestoreV2 name EVERY tensor of the TensorBundle ``tensors`` {name: array} with its dtype and shape, so a
+    TF1 ``tf.train.import_meta_graph`` + ``saver.restore`` pair would find the checkpoint's variables.  (The
+    reference's meta graph also holds the training ops; ours carries the forward only: parity of the
+    training subgraph is not claimed.)"""
+    g, _in, _out, var_shapes, handles = build_graph(model)
+    dt = {n: DT_FLOAT for n, _ in var_shapes}
+    shapes = dict(var_shapes)
+    for name in sorted(tensors):
+        if name in handles:
+            continue
+        arr = np.asarray(tensors[name])
+        d = _NP_DT.get(arr.dtype)
+        if d is None:
+            continue
+        handles[name] = g.node(name, "VarHandleOp", dtype=A.type(d), shape=A.shape(arr.shape), shared_name=A.s(name),
+                               container=A.s(""), allowed_devices=A.empty_list())
+        dt[name], shapes[name] = d, tuple(arr.shape)
+    saved = [(n, shapes[n]) for n in sorted(tensors) if n in handles]
+    saver_def = _saver(g, saved, handles, [dt[n] for n, _ in saved])
+    meta_info = _fb(1, "v1") + _fb(5, "tensorflow_distributed_example_amd")
+    return _msg(1, meta_info) + _msg(2, g.graph_def()) + _msg(3, saver_def)
+
+
+def graph_pbtxt(model) -> str:
+    """``graph.pbtxt``: the text-format GraphDef an Estimator writes into ``model_dir`` (the model's graph)."""
+    from .tf_proto import graph_def_text
+    g, *_ = build_graph(model)
+    return graph_def_text(g.graph_def())
 
 
 # ------------------------------------------------------------------ a numpy interpreter of the graph

@@ -21,10 +21,13 @@ from ..io import tensor_bundle as TB
 
 
 class CheckpointManager:
-    def __init__(self, model_dir, max_to_keep=5, prefix="model.ckpt"):
+    def __init__(self, model_dir, max_to_keep=5, prefix="model.ckpt", write_meta=False):
         self.dir = Path(model_dir)
         self.max_to_keep = max_to_keep
         self.prefix = prefix
+        # Estimator checkpoints (write_meta): model.ckpt-N.meta (MetaGraphDef + SaverDef over the bundle) beside
+        # every bundle and graph.pbtxt once in model_dir, as a TF1 Saver / Estimator lays out model_dir
+        self.write_meta = write_meta
 
     def _paths(self):
         st = TB.read_checkpoint_state(self.dir)
@@ -51,16 +54,29 @@ class CheckpointManager:
             tensors[f"tde/{k}"] = np.asarray(v)
         name = f"{self.prefix}-{int(global_step)}"
         TB.write_bundle(str(self.dir / name), tensors)
+        if self.write_meta:
+            self._write_meta(model, name, tensors)
         paths = [p for p in self._paths() if p != name] + [name]
         while len(paths) > self.max_to_keep:
             old = paths.pop(0)
-            for suffix in (".index", ".data-00000-of-00001"):
+            for suffix in (".index", ".data-00000-of-00001", ".meta"):
                 try:
                     os.remove(self.dir / (old + suffix))
                 except FileNotFoundError:
                     pass
         TB.write_checkpoint_state(self.dir, name, paths)
         return str(self.dir / name)
+
+    def _write_meta(self, model, name, tensors):
+        from ..io import saved_model_pb as SM
+        try:
+            meta = SM.checkpoint_meta_graph_bytes(model, tensors)
+            pbtxt = None if (self.dir / "graph.pbtxt").exists() else SM.graph_pbtxt(model)
+        except NotImplementedError:   # a layer with no TensorFlow op mapping: the bundle alone is the checkpoint
+            return
+        _atomic_write(self.dir / (name + ".meta"), meta)
+        if pbtxt is not None:
+            _atomic_write(self.dir / "graph.pbtxt", pbtxt.encode())
 
     def restore(self, model, path=None):
         """Load the latest (or given) checkpoint into ``model``; returns (global_step, extras) or None."""
@@ -83,6 +99,13 @@ class CheckpointManager:
         step = int(vals.get("global_step", np.array(0)))
         extras = {k[4:]: v for k, v in vals.items() if k.startswith("tde/")}
         return step, extras
+
+
+def _atomic_write(path: Path, data: bytes):
+    tmp = path.with_name(path.name + ".tmp")
+    with open(tmp, "wb") as f:
+        f.write(data)
+    os.replace(tmp, path)
 
 
 def wait_for_new_checkpoint(model_dir, last=None, timeout=None, poll=0.5):

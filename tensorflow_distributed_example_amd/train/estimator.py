@@ -207,7 +207,7 @@ class Estimator:
         self._model_dir = model_dir or self.config.model_dir or _tmp_model_dir()
         self.config.model_dir = self._model_dir
         self.params = params or {}
-        self.manager = CK.CheckpointManager(self._model_dir, self.config.keep_checkpoint_max)
+        self.manager = CK.CheckpointManager(self._model_dir, self.config.keep_checkpoint_max, write_meta=True)
         self._summary_writer = None
         self._psc = None
 
