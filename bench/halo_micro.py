@@ -44,11 +44,6 @@ def main():
                                                   reps=a.reps)
         res[f"halo_dgrad_us_grid{gr}"] = graph_time(lambda: O.halo_conv(x, w, y2, g, dgrad=True, grid=gr),
                                                     reps=a.reps)
-    from tensorflow_distributed_example_amd import _native as N
-    for dbg in (1, 2, 3):   # diagnostic builds: 1 no MFMA, 2 no k-loop LDS reads, 3 neither
-        N.hip().tde_halo_debug(dbg)
-        res[f"halo_fwd_dbg{dbg}_us"] = graph_time(lambda: O.halo_conv(x, wt, y2, g, colstats=st), reps=a.reps)
-    N.hip().tde_halo_debug(0)
     # phase clocks of one forward launch (s_memrealtime, 100 MHz): per-workgroup means relative to the
     # earliest workgroup start
     from tensorflow_distributed_example_amd import _native as N
@@ -63,11 +58,12 @@ def main():
         N.hip().tde_halo_stamps(None)
         sv = stamps.view(-1, 8)[:256].double()
         t0 = sv[:, 0].min()
-        rel = (sv[:, :6] - t0) * 0.01   # us
+        rel = (sv[:, :8] - t0) * 0.01   # us
         res[f"{name}_phase_us"] = {"start": round(rel[:, 0].mean().item(), 2),
                                    "first_rows_ready": round(rel[:, 1].mean().item(), 2),
                                    "tile0_mfma_done": round(rel[:, 2].mean().item(), 2),
-                                   "tile0_done": round(rel[:, 3].mean().item(), 2),
+                                   "tile0_loop_clock_ghz": round(((sv[:, 7] - sv[:, 6]) / ((sv[:, 2] - sv[:, 1]) * 10.0)).mean().item(), 3),
+                                   "tile1_mfma_done": round(rel[:, 3].mean().item(), 2),
                                    "loop_done": round(rel[:, 4].mean().item(), 2),
                                    "end_mean": round(rel[:, 5].mean().item(), 2),
                                    "end_max": round(rel[:, 5].max().item(), 2)}

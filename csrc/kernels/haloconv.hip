@@ -27,6 +27,8 @@
 // keeps a fragment that straddles two image rows conflict-free too).
 #include "tde_common.h"
 
+#include <type_traits>
+
 namespace tde {
 namespace halo {
 
@@ -87,9 +89,12 @@ __device__ __forceinline__ void vmwait() {
 // The epilogue of tile t (bf16 conversion, BN statistics, 8-byte stores, the accumulated form's add) runs
 // inside tile t + 1's k-loop, one (channel block, pixel block) pair per k-step, while that step's MFMAs
 // are in flight: the two accumulator sets ping-pong by unrolling the tile loop twice.
-// DBG (diagnostic builds only, tde_halo_debug): 1 = no MFMAs in the k loop (LDS reads only), 2 = no
-// activation reads in the k loop (MFMAs on stale fragments), 3 = both off
-template <int TR, int PB, int DBG = 0>
+// With one wave per SIMD, a wave issues in order: the VALU / LDS work of a k-step only hides under the
+// matrix pipe when it sits BETWEEN the step's MFMAs (each MFMA occupies the pipe ~16 cycles).  The k loop
+// is therefore one branch-free basic block (ACC = accumulate and ALLV = every pixel block valid are
+// template parameters; the first tile, which has no epilogue to fold, is a separate instantiation of the
+// loop) and each step is laid out by sched_group_barrier as MFMA / LDS read / 2 VALU, repeated.
+template <int TR, int PB, bool ACC, bool ALLV>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void conv3x3_kernel(Args a) {
   constexpr int RING = 2 * TR + 4;
   constexpr int NE = 2 * PB;  // epilogue pairs per tile (<= 18 k-steps)
@@ -179,9 +184,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // epilogue pair e = (cb = e % 2, pb = e / 2) of a finished tile: its 4 channels of one pixel per lane
   auto epi = [&](const f32x4 (&acc)[2][PB], const bf16x4 (&old)[2][PB], const long long (&gp)[PB], int e) {
     const int cb = e & 1, pb = e >> 1;
-    if (!pbv[pb]) return;
+    if (!ALLV && !pbv[pb]) return;
     float v[4] = {acc[cb][pb][0], acc[cb][pb][1], acc[cb][pb][2], acc[cb][pb][3]};
-    if (a.accum) {
+    if (ACC) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] += bf2f(old[cb][pb][r]);
     }
@@ -196,33 +201,70 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     *reinterpret_cast<bf16x4*>(a.y + gp[pb] + 32 * wc + 16 * cb + 4 * q) = o;
   };
 
-  f32x4 accA[2][PB], accB[2][PB];
-  bf16x4 oldA[2][PB], oldB[2][PB];
-  long long gpA[PB], gpB[PB];
+  f32x4 pacc[2][PB];      // the previous tile's accumulators (its epilogue runs in the next tile's k loop)
+  bf16x4 pold[2][PB], old[2][PB];
+  long long pgp[PB], gp[PB];
+  int rbase[PB][3];
+  f32x4 acc[2][PB];
+  // the k loop of one tile: 18 k-steps (tap, channel half); the fragments of step s + 1 are read during
+  // step s; EPI folds the previous tile's epilogue in, one pair per step
+  auto kloop = [&](auto epi_on) {
+    constexpr bool EPI = decltype(epi_on)::value;
+    bf16x8 fa[2][2], fb[2][PB];
+    auto load_step = [&](int st, bf16x8* af, bf16x8* bv) {
+      const int tap = st >> 1, c = st & 1, kh = tap / 3, kw = tap - 3 * (tap / 3);
+      const char* wt = wl + tap * (kC * kPix);
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) af[cb] = *reinterpret_cast<const bf16x8*>(wt + aoff[cb][c]);
+      // a pixel block past the tile reads pixel 0 and is never stored
+#pragma unroll
+      for (int pb = 0; pb < PB; ++pb) bv[pb] = *reinterpret_cast<const bf16x8*>(ring + rbase[pb][kh] + coff[pb][kw][c]);
+    };
+    load_step(0, fa[0], fb[0]);
+#pragma unroll
+    for (int st = 0; st < 18; ++st) {
+      const int cur = st & 1;
+      if (st + 1 < 18) load_step(st + 1, fa[cur ^ 1], fb[cur ^ 1]);
+#pragma unroll
+      for (int pb = 0; pb < PB; ++pb)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) acc[cb][pb] = mfma16(fa[cur][cb], fb[cur][pb], acc[cb][pb]);
+      if (EPI && st < NE) epi(pacc, pold, pgp, st);
+      // lay the step out as [MFMA, LDS read, 2 VALU] x 2 PB (reads: the next step's 2 + PB fragments)
+#pragma unroll
+      for (int i = 0; i < 2 * PB; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+        if (i < 2 + PB) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // VALU
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
   int s0 = 0;
   {
     const int b = t0 / tpi, r0 = TR * (t0 - b * tpi);
     issue_rows(b, r0 - 1, TR + 2, 0);
   }
-  // one tile: its MFMA loop with the previous tile's epilogue (conversion, statistics, stores) folded in
-  auto tile = [&](int t, f32x4 (&acc)[2][PB], bf16x4 (&old)[2][PB], long long (&gp)[PB],
-                  const f32x4 (&pacc)[2][PB], const bf16x4 (&pold)[2][PB], const long long (&pgp)[PB]) {
+  for (int t = t0; t < t1; ++t) {
     // this tile's rows have landed (DMA issued one tile ago; older stores and old-value reads long done).
     // The builtin form of the wait (not inline asm) tells the compiler's wait-count pass that nothing is
     // outstanding here, so the folded epilogue below never waits on this tile's prefetch DMA.
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_s_barrier();
     if (t == t0) stamp(a.stamps, 1);
+    if (t == t0 && a.stamps && threadIdx.x == 0)  // shader-clock cycles (s_memtime) beside the 100 MHz stamps
+      a.stamps[(size_t)blockIdx.x * kMaxStamps + 6] = (long long)__builtin_amdgcn_s_memtime();
     const int b = t / tpi, r0 = TR * (t - b * tpi);
 #pragma unroll
     for (int pb = 0; pb < PB; ++pb) gp[pb] = ((long long)(b * H + r0 + prow[pb]) * W + pcol[pb]) * kC;
-    if (a.accum) {  // the accumulated form's old values, read before the prefetch DMA is queued behind them
+    if (ACC) {  // the accumulated form's old values, read before the prefetch DMA is queued behind them
 #pragma unroll
       for (int pb = 0; pb < PB; ++pb) {
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
-          old[cb][pb] = pbv[pb] ? *reinterpret_cast<const bf16x4*>(a.y + gp[pb] + 32 * wc + 16 * cb + 4 * q)
-                                : bf16x4{};
+          old[cb][pb] = (ALLV || pbv[pb]) ? *reinterpret_cast<const bf16x4*>(a.y + gp[pb] + 32 * wc + 16 * cb + 4 * q)
+                                          : bf16x4{};
       }
     }
     int snext = s0;
@@ -236,7 +278,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         snext = s0 + TR + 2;
       }
     }
-    int rbase[PB][3];
 #pragma unroll
     for (int pb = 0; pb < PB; ++pb)
 #pragma unroll
@@ -249,57 +290,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
       for (int pb = 0; pb < PB; ++pb) acc[cb][pb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // 18 k-steps (tap, channel half), software-pipelined by hand: the fragments of step s + 1 are read
-    // before the MFMAs of step s, so one wave per SIMD keeps its LDS latency under the matrix pipe
-    auto load_step = [&](int s, bf16x8* af, bf16x8* bv) {
-      const int tap = s >> 1, c = s & 1, kh = tap / 3, kw = tap - 3 * (tap / 3);
-      const char* wt = wl + tap * (kC * kPix);
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) af[cb] = *reinterpret_cast<const bf16x8*>(wt + aoff[cb][c]);
-      // a pixel block past the tile reads pixel 0 and is never stored: no branches in the k loop
-#pragma unroll
-      for (int pb = 0; pb < PB; ++pb)
-        bv[pb] = *reinterpret_cast<const bf16x8*>(ring + rbase[pb][kh] + coff[pb][kw][c]);
-    };
-    bf16x8 fa[2][2], fb[2][PB];
-    load_step(0, fa[0], fb[0]);
-    load_step(1, fa[1], fb[1]);
-#pragma unroll
-    for (int s = 0; s < 18; ++s) {
-      const int cur = s & 1;
-      if (s + 1 < 18 && s > 0 && !(DBG & 2)) load_step(s + 1, fa[cur ^ 1], fb[cur ^ 1]);
-      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
-      if (!(DBG & 1)) {
-#pragma unroll
-        for (int pb = 0; pb < PB; ++pb)
-#pragma unroll
-          for (int cb = 0; cb < 2; ++cb) acc[cb][pb] = mfma16(fa[cur][cb], fb[cur][pb], acc[cb][pb]);
-      } else {
-#pragma unroll
-        for (int pb = 0; pb < PB; ++pb)
-#pragma unroll
-          for (int cb = 0; cb < 2; ++cb) acc[cb][pb][0] += (float)fa[cur][cb][0] * (float)fb[cur][pb][1];
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if (s < NE && t > t0) epi(pacc, pold, pgp, s);  // VALU + one store beside the MFMAs in flight
-      __builtin_amdgcn_sched_barrier(0);
-    }
+    if (t == t0) kloop(std::integral_constant<bool, false>{});
+    else kloop(std::integral_constant<bool, true>{});
     if (t == t0) stamp(a.stamps, 2);
+    if (t == t0 && a.stamps && threadIdx.x == 0)
+      a.stamps[(size_t)blockIdx.x * kMaxStamps + 7] = (long long)__builtin_amdgcn_s_memtime();
+    if (t == t0 + 1) stamp(a.stamps, 3);
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int pb = 0; pb < PB; ++pb) {
+        pacc[cb][pb] = acc[cb][pb];
+        if (ACC) pold[cb][pb] = old[cb][pb];
+      }
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb) pgp[pb] = gp[pb];
     s0 = snext >= RING ? snext - RING : snext;
-  };
-  int t = t0;
-  for (; t + 1 < t1; t += 2) {
-    tile(t, accA, oldA, gpA, accB, oldB, gpB);
-    tile(t + 1, accB, oldB, gpB, accA, oldA, gpA);
   }
-  if (t < t1) {
-    tile(t, accA, oldA, gpA, accB, oldB, gpB);
 #pragma unroll
-    for (int e = 0; e < NE; ++e) epi(accA, oldA, gpA, e);
-  } else {
-#pragma unroll
-    for (int e = 0; e < NE; ++e) epi(accB, oldB, gpB, e);
-  }
+  for (int e = 0; e < NE; ++e) epi(pacc, pold, pgp, e);
   stamp(a.stamps, 4);
   if (a.colstats) {
     // fold the two pixel-half waves of each channel half in LDS (the ring is free now), then one f64 atomic
@@ -333,24 +342,26 @@ using namespace tde;
 
 static int halo_lds_bytes(int W, int TR) { return halo::kWBytes + (2 * TR + 4) * ((W + 2) * halo::kPix + 64); }
 
-// rows per tile: the largest TR in {8, 4, 2} with H % TR == 0, TR * W <= 256 and the LDS footprint <= 160 KiB
-// the instantiated (rows per tile, pixel blocks per wave) forms: PB = ceil(TR * W / 32) rounded up to 4 or 7
 typedef void (*HaloKern)(halo::Args);
-static int g_halo_dbg = 0;
-TDE_API void tde_halo_debug(int mode) { g_halo_dbg = mode; }
-static HaloKern halo_kernel(int tr, int pb) {
+template <int TR, int PB>
+static HaloKern halo_kern4(bool acc, bool allv) {
+  if (acc) return allv ? halo::conv3x3_kernel<TR, PB, true, true> : halo::conv3x3_kernel<TR, PB, true, false>;
+  return allv ? halo::conv3x3_kernel<TR, PB, false, true> : halo::conv3x3_kernel<TR, PB, false, false>;
+}
+// the instantiated forms: PB = ceil(TR * W / 32) rounded up to 4 or 7; ALLV when the 2 x PB blocks tile
+// the TR rows exactly (ResNet-18 stage 1: 4 x 56 = 14 blocks of 16)
+static HaloKern halo_kernel(int tr, int pb, bool acc, bool allv) {
   if (pb > 7) return nullptr;
   if (pb > 4) {
-    if (tr == 4) {  // ResNet-18 stage 1: 4 x 56 pixels
-      if (g_halo_dbg == 1) return halo::conv3x3_kernel<4, 7, 1>;
-      if (g_halo_dbg == 2) return halo::conv3x3_kernel<4, 7, 2>;
-      if (g_halo_dbg == 3) return halo::conv3x3_kernel<4, 7, 3>;
-      return halo::conv3x3_kernel<4, 7>;
-    }
-    return tr == 2 ? halo::conv3x3_kernel<2, 7> : tr == 8 ? halo::conv3x3_kernel<8, 7> : nullptr;
+    if (tr == 4) return halo_kern4<4, 7>(acc, allv);
+    if (tr == 2) return halo_kern4<2, 7>(acc, allv);
+    if (tr == 8) return halo_kern4<8, 7>(acc, allv);
+    return nullptr;
   }
-  return tr == 2 ? halo::conv3x3_kernel<2, 4> : tr == 4 ? halo::conv3x3_kernel<4, 4>
-       : tr == 8 ? halo::conv3x3_kernel<8, 4> : nullptr;
+  if (tr == 2) return halo_kern4<2, 4>(acc, allv);
+  if (tr == 4) return halo_kern4<4, 4>(acc, allv);
+  if (tr == 8) return halo_kern4<8, 4>(acc, allv);
+  return nullptr;
 }
 
 // rows per tile: the largest TR in {8, 4, 2} with H % TR == 0, at most 7 pixel blocks per wave
@@ -370,7 +381,7 @@ TDE_API int tde_halo_conv_ok(int C, int Co, int H, int W, int B) {
   if (W % 8 != 0 || W < 8 || H < 2) return 0;
   if ((long long)B * H * W * halo::kPix >= (1LL << 31)) return 0;
   const int tr = halo_rows(H, W);
-  return tr > 0 && halo_kernel(tr, (tr * W + 31) / 32) != nullptr;
+  return tr > 0 && halo_kernel(tr, (tr * W + 31) / 32, false, false) != nullptr;
 }
 
 // y[B,H,W,64] (=|+=) conv3x3_s1_same(x, w); weights element (tap, n, k) at w[tap' * wst + n * wsn + k]
@@ -380,7 +391,9 @@ TDE_API int tde_halo_conv3x3(const bf16* x, const bf16* w, long long wst, long l
   if (((uintptr_t)x & 15) || ((uintptr_t)w & 15) || ((uintptr_t)y & 7) || (wst % 8) || (wsn % 8)) return -3;
   const int tr = halo_rows(H, W);
   const int lds = halo_lds_bytes(W, tr);
-  const HaloKern fn = halo_kernel(tr, (tr * W + 31) / 32);
+  const int pbn = (tr * W + 31) / 32;
+  const int pbk = pbn > 4 ? 7 : 4;
+  const HaloKern fn = halo_kernel(tr, pbn, accum != 0, tr * W == 32 * pbk);
   static HaloKern attr_done[16] = {nullptr};
   bool done = false;
   for (int i = 0; i < 16 && attr_done[i]; ++i) done |= attr_done[i] == fn;

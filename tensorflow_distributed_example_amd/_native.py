@@ -88,7 +88,6 @@ _HIP_PROTOS = {
     # persistent halo-tile 3x3 conv (csrc/kernels/haloconv.hip)
     "tde_halo_conv_ok": (i32, [i32, i32, i32, i32, i32]),
     "tde_halo_stamps": (None, [p]),
-    "tde_halo_debug": (None, [i32]),
     "tde_halo_conv3x3": (i32, [p, p, i64, i64, i32, p, i32, p, i32, i32, i32, i32, p]),
     "tde_stem_pack": (i32, [p, p, p, p, p, p]),
     "tde_gather_rows_dev": (i32, [p, i64, i64, p, i64, p, p, p]),
