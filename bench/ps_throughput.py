@@ -49,6 +49,9 @@ def main():
     ap.add_argument("--model", default="mnist_bn_cnn")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--momentum", type=float, default=0.0)
+    # K > 1: K consecutive train() sessions against the same ps tasks (max_steps = max_steps * (s + 1) / K),
+    # the last one timed — every session must end at exactly its max_steps on the plane the first one chose
+    ap.add_argument("--sessions", type=int, default=1)
     a, _ = ap.parse_known_args()
     import numpy as np
 
@@ -81,8 +84,17 @@ def main():
     def input_fn():
         return tde.data.Dataset.from_tensor_slices((x, y)).shuffle(1000).repeat().batch(a.batch).prefetch(100)
 
-    hook = _RateHook(a.warm)
+    ends, planes = [], []
+    for s in range(a.sessions - 1):
+        h0 = _RateHook(10 ** 12)
+        est.train(input_fn, hooks=[h0], max_steps=a.max_steps * (s + 1) // a.sessions)
+        ends.append(h0.s1)
+        planes.append(getattr(est, "ps_data_plane", "tcp"))
+    warm = a.warm + (a.max_steps * (a.sessions - 1) // a.sessions)
+    hook = _RateHook(warm)
     est.train(input_fn, hooks=[hook], max_steps=a.max_steps)
+    ends.append(hook.s1)
+    planes.append(getattr(est, "ps_data_plane", "tcp"))
     dt = hook.t1 - hook.t0
     rate = (hook.s1 - hook.s0) / dt
     local = (hook.l1 - hook.l0) / (hook.t1 - hook.lt0)
@@ -97,7 +109,8 @@ def main():
                           "model": a.model, "steps_timed": hook.s1 - hook.s0, "master_local_steps_per_sec":
                           round(local, 1), "device": str(model._store.device), "final_global_step": hook.s1,
                           "momentum": a.momentum, "data_plane": getattr(est, "ps_data_plane", "tcp"),
-                          "pipelined": os.environ.get("TDE_PS_PIPELINE", "1") != "0"}),
+                          "pipelined": os.environ.get("TDE_PS_PIPELINE", "1") != "0",
+                          "sessions": a.sessions, "session_end_steps": ends, "session_planes": planes}),
               flush=True)
 
 

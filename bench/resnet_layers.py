@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--sweep-big-dgrad", action="store_true", help="A/B the dgrad big tiles only")
     ap.add_argument("--sweep-fd", action="store_true", help="fwd / dgrad per layer over tile threshold x K step")
     ap.add_argument("--sweep-wgrad", action="store_true", help="weight-gradient path x stages x tile cap x split target")
+    ap.add_argument("--ab-mfma32", action="store_true",
+                    help="per layer: fwd / dgrad / wgrad on the 16x16x32 vs 32x32x16 MFMA kernels (A/B/A/B)")
     a = ap.parse_args()
     import tensorflow_distributed_example_amd as tde
     from tensorflow_distributed_example_amd import _native as N
@@ -73,6 +75,30 @@ def main():
               f"{r['dgrad_us']:7.1f} us {tf(r['dgrad_us']):5.0f} TF | wgrad {r['wgrad_us']:7.1f} us "
               f"{tf(r['wgrad_us']):5.0f} TF", flush=True)
     print("TOTAL", json.dumps(tot), flush=True)
+    if a.ab_mfma32:
+        lib = N.hip()
+        tot = {}
+        for rnd, mask in enumerate((0, 7, 0, 7)):
+            lib.tde_igemm_mfma32(mask)
+            for st in _convs(plan, LW):
+                g = st.geo.with_batch(B)
+                dout = st.out.root().grad
+                # igemm forward even where the plan runs the halo kernel (stage 1)
+                t_f = graph_time(lambda: O.conv_fwd(st.inp.buf, st.Wt, st.out.root().buf, g, colstats=st.colstats,
+                                                    scratch=plan.scratch), a.reps)
+                t_d = graph_time(lambda: O.conv_dgrad(dout, st.Wrow, st.inp.root().grad, g, scratch=plan.scratch),
+                                 a.reps) if st.need_dgrad else 0.0
+                t_w = graph_time(lambda: O.conv_wgrad(st.inp.buf, dout, st.gW, g, scratch=plan.wscratch), a.reps)
+                if rnd >= 2:
+                    print(f"AB32 mask={mask} {st.layer.name:<20} fwd {t_f:6.1f} dgrad {t_d:6.1f} wgrad {t_w:6.1f}",
+                          flush=True)
+                k = tot.setdefault(mask, [0.0, 0.0, 0.0])
+                k[0] += t_f / 2
+                k[1] += t_d / 2
+                k[2] += t_w / 2
+        for mask, (f, d, w) in tot.items():
+            print(f"AB32 TOTAL mask={mask}: fwd {f:.1f} dgrad {d:.1f} wgrad {w:.1f} us (mean of 2 rounds)", flush=True)
+        lib.tde_igemm_mfma32(-1)
     if a.sweep_tile:
         lib = N.hip()
         for tmin in (512, 1024, 1536, 2048, 3072, 4096, 100000):

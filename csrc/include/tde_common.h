@@ -43,6 +43,13 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// MFMA 32x32x16 bf16 -> f32.  Lane l holds A[row l&31][k 8*(l>>5) .. +7] and
+// B[k 8*(l>>5) .. +7][col l&31]; accumulator register r holds
+// C[row 8*(r>>2) + 4*(l>>5) + (r&3)][col l&31].
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
 // 16-byte fragment load with a zero fill outside [0, limit) (limit counted in
 // elements along K).  `p` points at element k0 of the row.
 __device__ __forceinline__ bf16x8 load_frag(const bf16* p, int k0, int K, bool row_ok) {

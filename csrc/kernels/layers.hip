@@ -133,6 +133,22 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16* img, int mb, int lane, int
   return __builtin_bit_cast(bf16x8, r);
 }
 
+// 32x32x16 operand fragment (rows mb..mb+31, k k0..k0+15; k0 % 16 == 0): every 16-lane group runs the same
+// two transposed 4x16 reads as tr_frag, at image rows of k group k0/8 + (lane>>5) and columns
+// mb + 16*((lane>>4)&1) .. +15, so lane l receives A[mb + (l&31)][k0 + 8*(l>>5) .. +7].
+template <int RW>
+__device__ __forceinline__ bf16x8 tr_frag32(const bf16* img, int mb, int lane, int k0) {
+  const int g = k0 / 8 + (lane >> 5), i = lane & 15, q = i >> 2, pp = i & 3;
+  const int ch = ((mb + 16 * ((lane >> 4) & 1)) >> 3) + (pp >> 1);
+  const char* base = reinterpret_cast<const char*>(img);
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + swz<RW>(8 * g + q, ch) + 8 * (pp & 1)));
+  const v4i16 hi =
+      __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(base + swz<RW>(8 * g + 4 + q, ch) + 8 * (pp & 1)));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, r);
+}
+
 // ---- A(m, k), K-vector kinds: a thread's rows are fixed for the whole K loop; its k offset
 // advances by 32 per step, decomposed incrementally into (kh, kw, c) (no divisions in the loop).
 struct ARow {
@@ -383,7 +399,10 @@ __device__ __forceinline__ void vm_wait() {
 // LDS stages with S-1 k-tiles in flight across the per-step barrier (counted vmcnt, raw s_barrier),
 // instead of the register-staged double buffer.
 // WGM: waves along M (4 / WGM along N); the register-staged path is 2 x 2.
-template <int AK, int BK_, int BM, int BN, int KB, int VEC, int S = 0, int WGM = 2>
+// MF: MFMA shape of the LDS-DMA paths, 16 (v_mfma_f32_16x16x32_bf16) or 32 (v_mfma_f32_32x32x16_bf16: half the
+// instructions per flop; the wave tile must be a multiple of 32 in both directions).  The LDS images are the same
+// for both shapes; only the fragment reads and the accumulator -> (row, column) map of the epilogue differ.
+template <int AK, int BK_, int BM, int BN, int KB, int VEC, int S = 0, int WGM = 2, int MF = 16>
 __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p_) {
   IGemmArgs p = p_;
   if (AK == A_DGRAD && p_.nph > 0) {  // multi-phase strided dgrad: this block's phase is blockIdx.z
@@ -419,6 +438,9 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p_) {
   constexpr int WGN = 4 / WGM;
   static_assert(GLDS || WGM == 2, "wave layouts other than 2 x 2 are built for the glds path only");
   constexpr int WTM = BM / WGM, WTN = BN / WGN, MI = WTM / 16, NI = WTN / 16;
+  static_assert(MF == 16 || (MF == 32 && GLDS && WTM % 32 == 0 && WTN % 32 == 0), "32x32 MFMA: LDS-DMA paths, 32-multiple wave tiles");
+  // fragment grid of a wave: FI x FJ fragments of FW x FW, RPL accumulator registers per lane each
+  constexpr int FW = MF, FI = WTM / FW, FJ = WTN / FW, RPL = MF == 32 ? 16 : 4;
   // glds images: a wave instruction fills 1024 B = RPI rows of KV chunks; rows are read 16 at a time
   // (one per lane of a 16-lane group) at one logical chunk, so the physical chunk is XORed with
   // (row / rows-per-256B-bank-row) to land the 16 reads in 16 distinct bank slots
@@ -604,11 +626,28 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p_) {
     }
   };
 
-  f32x4 acc[MI][NI];
+  f32x4 acc[MF == 16 ? MI : 1][MF == 16 ? NI : 1];
+  f32x16 acc2[MF == 32 ? FI : 1][MF == 32 ? FJ : 1];
+  if constexpr (MF == 16) {
 #pragma unroll
-  for (int i = 0; i < MI; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  } else {
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int j = 0; j < FJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc2[i][j][r] = 0.f;
+  }
+  // accumulator register r of fragment (i, j) -> its value, and its row within the fragment
+  auto accv = [&](int i, int j, int r) -> float {
+    if constexpr (MF == 32) return acc2[i][j][r];
+    else return acc[i][j][r];
+  };
+  auto frow = [&](int r) -> int { return MF == 32 ? 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3) : (lane >> 4) * 4 + r; };
+  const int fcl = lane & (FW - 1);   // the lane's column within a fragment
 
   const int fr = lane & 15, fk = (lane >> 4) * 8;
   if constexpr (GLDS && !AKV) {
@@ -678,17 +717,32 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p_) {
     auto compute = [&](int stage) {
       const bf16* a = As + stage * AIMG;
       const bf16* b = Bs + stage * BIMG;
+      if constexpr (MF == 32) {
 #pragma unroll
-      for (int kk = 0; kk < KB; kk += 32) {
-        bf16x8 af[MI], bfr[NI];
+        for (int kk = 0; kk < KB; kk += 16) {
+          bf16x8 af[FI], bfr[FJ];
 #pragma unroll
-        for (int i = 0; i < MI; ++i) af[i] = tr_frag<BM>(a, wm * WTM + i * 16, lane, kk);
+          for (int i = 0; i < FI; ++i) af[i] = tr_frag32<BM>(a, wm * WTM + i * 32, lane, kk);
 #pragma unroll
-        for (int j = 0; j < NI; ++j) bfr[j] = tr_frag<BN>(b, wn * WTN + j * 16, lane, kk);
+          for (int j = 0; j < FJ; ++j) bfr[j] = tr_frag32<BN>(b, wn * WTN + j * 32, lane, kk);
 #pragma unroll
-        for (int i = 0; i < MI; ++i)
+          for (int i = 0; i < FI; ++i)
 #pragma unroll
-          for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+            for (int j = 0; j < FJ; ++j) acc2[i][j] = mfma32(af[i], bfr[j], acc2[i][j]);
+        }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < KB; kk += 32) {
+          bf16x8 af[MI], bfr[NI];
+#pragma unroll
+          for (int i = 0; i < MI; ++i) af[i] = tr_frag<BM>(a, wm * WTM + i * 16, lane, kk);
+#pragma unroll
+          for (int j = 0; j < NI; ++j) bfr[j] = tr_frag<BN>(b, wn * WTN + j * 16, lane, kk);
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+        }
       }
     };
     const int nk = kt1 - kt0;
@@ -754,13 +808,16 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p_) {
     }
     // per-lane LDS fragment offsets (bytes) of row i = 0 / column j = 0 at each 32-wide k slice: the
     // XOR swizzle of a row does not change over the 16-row steps of i / j (16 / RPB is a multiple of KV)
-    int offa[KB / 32], offb[KB / 32];
+    // (32x32x16: rows lane&31 at chunk kk/8 + lane>>5 per 16-wide k step; the XOR is invariant over 32-row steps too)
+    constexpr int KST = MF == 32 ? 16 : 32;
+    int offa[KB / KST], offb[KB / KST];
 #pragma unroll
-    for (int kk = 0; kk < KB; kk += 32) {
-      const int c = kk / 8 + (lane >> 4);
-      const int ra0 = wm * WTM + fr, rb0 = wn * WTN + fr;
-      offa[kk / 32] = (ra0 * KB + ((c ^ ((ra0 / RPB) & (KV - 1))) << 3)) * 2;
-      offb[kk / 32] = (rb0 * KB + ((c ^ ((rb0 / RPB) & (KV - 1))) << 3)) * 2;
+    for (int kk = 0; kk < KB; kk += KST) {
+      const int c = MF == 32 ? kk / 8 + (lane >> 5) : kk / 8 + (lane >> 4);
+      const int fl = MF == 32 ? (lane & 31) : fr;
+      const int ra0 = wm * WTM + fl, rb0 = wn * WTN + fl;
+      offa[kk / KST] = (ra0 * KB + ((c ^ ((ra0 / RPB) & (KV - 1))) << 3)) * 2;
+      offb[kk / KST] = (rb0 * KB + ((c ^ ((rb0 / RPB) & (KV - 1))) << 3)) * 2;
     }
     // row-tile mode (A_CONV): a k-tile is one whole kernel row (its chunks are the row's taps), so the
     // bookkeeping below runs with one "tap" of KB channels per kernel row
@@ -831,19 +888,36 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p_) {
     auto compute = [&](int stage) {   // stage: block-uniform; 4 VALU adds form the k-tile's read bases
       const char* a = lds + stage * AIMG * 2;
       const char* b = lds + NBUF * AIMG * 2 + stage * BIMG * 2;
+      if constexpr (MF == 32) {
 #pragma unroll
-      for (int kk = 0; kk < KB; kk += 32) {
-        bf16x8 af[MI], bfr[NI];
-        const char* ak = a + offa[kk / 32];
-        const char* bk = b + offb[kk / 32];
+        for (int kk = 0; kk < KB; kk += 16) {
+          bf16x8 af[FI], bfr[FJ];
+          const char* ak = a + offa[kk / 16];
+          const char* bk = b + offb[kk / 16];
 #pragma unroll
-        for (int i = 0; i < MI; ++i) af[i] = *reinterpret_cast<const bf16x8*>(ak + i * 16 * KB * 2);
+          for (int i = 0; i < FI; ++i) af[i] = *reinterpret_cast<const bf16x8*>(ak + i * 32 * KB * 2);
 #pragma unroll
-        for (int j = 0; j < NI; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(bk + j * 16 * KB * 2);
+          for (int j = 0; j < FJ; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(bk + j * 32 * KB * 2);
 #pragma unroll
-        for (int i = 0; i < MI; ++i)
+          for (int i = 0; i < FI; ++i)
 #pragma unroll
-          for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+            for (int j = 0; j < FJ; ++j) acc2[i][j] = mfma32(af[i], bfr[j], acc2[i][j]);
+        }
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < KB; kk += 32) {
+          bf16x8 af[MI], bfr[NI];
+          const char* ak = a + offa[kk / 32];
+          const char* bk = b + offb[kk / 32];
+#pragma unroll
+          for (int i = 0; i < MI; ++i) af[i] = *reinterpret_cast<const bf16x8*>(ak + i * 16 * KB * 2);
+#pragma unroll
+          for (int j = 0; j < NI; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(bk + j * 16 * KB * 2);
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+        }
       }
     };
     const int nk = kt1 - kt0;
@@ -913,19 +987,19 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p_) {
       float* T = reinterpret_cast<float*>(smem);
       float* red = T + BM * TLD;  // [WGM][WGN][NI][2][16] statistics partials
       __syncthreads();            // every wave is done reading the last stage
-      float e1[NI], e2[NI];
+      float e1[FJ], e2[FJ];
 #pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const int lc = wn * WTN + j * 16 + fr, col = n0 + lc;
+      for (int j = 0; j < FJ; ++j) {
+        const int lc = wn * WTN + j * FW + fcl, col = n0 + lc;
         const bool cok = col < p.N;
         const float bv = (p.bias && cok) ? p.bias[col] : 0.f;
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int i = 0; i < MI; ++i) {
+        for (int i = 0; i < FI; ++i) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int lr = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
-            float v = p.alpha * acc[i][j][r] + bv;
+          for (int r = 0; r < RPL; ++r) {
+            const int lr = wm * WTM + i * FW + frow(r);
+            float v = p.alpha * accv(i, j, r) + bv;
             if (p.colstats && cok && m0 + lr < p.M) {
               const float q = bf2f(f2bf(v));
               s1 += q;
@@ -936,33 +1010,35 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p_) {
           }
         }
         if (p.colstats) {
-          s1 += __shfl_xor(s1, 16, 64);
+          if (MF == 16) {
+            s1 += __shfl_xor(s1, 16, 64);
+            s2 += __shfl_xor(s2, 16, 64);
+          }
           s1 += __shfl_xor(s1, 32, 64);
-          s2 += __shfl_xor(s2, 16, 64);
           s2 += __shfl_xor(s2, 32, 64);
         }
         e1[j] = s1;
         e2[j] = s2;
       }
-      if (p.colstats && lane < 16) {
+      if (p.colstats && lane < FW) {
 #pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          red[(((wm * WGN + wn) * NI + j) * 2 + 0) * 16 + lane] = e1[j];
-          red[(((wm * WGN + wn) * NI + j) * 2 + 1) * 16 + lane] = e2[j];
+        for (int j = 0; j < FJ; ++j) {
+          red[(((wm * WGN + wn) * FJ + j) * 2 + 0) * FW + lane] = e1[j];
+          red[(((wm * WGN + wn) * FJ + j) * 2 + 1) * FW + lane] = e2[j];
         }
       }
       __syncthreads();
-      if (p.colstats && wm == 0 && lane < 16) {
+      if (p.colstats && wm == 0 && lane < FW) {
         double* st = p.colstats + (size_t)(bx % kStatSlots) * 2 * p.N;
 #pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          const int col = n0 + wn * WTN + j * 16 + lane;
+        for (int j = 0; j < FJ; ++j) {
+          const int col = n0 + wn * WTN + j * FW + lane;
           if (col >= p.N) continue;
           float a1 = 0.f, a2 = 0.f;
 #pragma unroll
           for (int w = 0; w < WGM; ++w) {
-            a1 += red[(((w * WGN + wn) * NI + j) * 2 + 0) * 16 + lane];
-            a2 += red[(((w * WGN + wn) * NI + j) * 2 + 1) * 16 + lane];
+            a1 += red[(((w * WGN + wn) * FJ + j) * 2 + 0) * FW + lane];
+            a2 += red[(((w * WGN + wn) * FJ + j) * 2 + 1) * FW + lane];
           }
           atomicAdd(&st[col], (double)a1);
           atomicAdd(&st[p.N + col], (double)a2);
@@ -1003,18 +1079,18 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p_) {
       return;
     }
   }
-  float sp1[NI], sp2[NI];  // per-column statistics of this wave (valid in lanes 0..15)
+  float sp1[FJ], sp2[FJ];  // per-column statistics of this wave (valid in lanes 0..FW-1)
 #pragma unroll
-  for (int j = 0; j < NI; ++j) {
-    const int col = n0 + wn * WTN + j * 16 + fr;
+  for (int j = 0; j < FJ; ++j) {
+    const int col = n0 + wn * WTN + j * FW + fcl;
     const bool cok = col < p.N;
     const float bv = (p.bias && cok) ? p.bias[col] : 0.f;
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < MI; ++i) {
+    for (int i = 0; i < FI; ++i) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int mrow = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+      for (int r = 0; r < RPL; ++r) {
+        const int mrow = m0 + wm * WTM + i * FW + frow(r);
         if (!cok || mrow >= p.M) continue;
         int row = mrow;
         if (AK == A_DGRAD && p.ph_on) {  // phase row -> input pixel
@@ -1023,7 +1099,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p_) {
           const int ihp = rem / p.Wp, iwp = rem - ihp * p.Wp;
           row = (b * p.g.H + ihp * p.g.sh + p.ph_h) * p.g.W + iwp * p.g.sw + p.ph_w;
         }
-        float v = p.alpha * acc[i][j][r] + bv;
+        float v = p.alpha * accv(i, j, r) + bv;
         if (p.colstats) {
           // statistics of exactly the tensor BN will normalise (the bf16 activation)
           const float q = p.cb ? bf2f(f2bf(v)) : v;
@@ -1051,9 +1127,11 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p_) {
       }
     }
     if (p.colstats) {
-      s1 += __shfl_xor(s1, 16, 64);
+      if (MF == 16) {
+        s1 += __shfl_xor(s1, 16, 64);
+        s2 += __shfl_xor(s2, 16, 64);
+      }
       s1 += __shfl_xor(s1, 32, 64);
-      s2 += __shfl_xor(s2, 16, 64);
       s2 += __shfl_xor(s2, 32, 64);
     }
     sp1[j] = s1;
@@ -1062,26 +1140,26 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p_) {
   if (p.colstats) {
     // the WGM waves sharing a column range combine through LDS: one atomic per column per block
     __syncthreads();
-    float* red = reinterpret_cast<float*>(smem);  // [WGM][WGN][NI][2][16]
-    if (wm > 0 && lane < 16) {
+    float* red = reinterpret_cast<float*>(smem);  // [WGM][WGN][FJ][2][FW]
+    if (wm > 0 && lane < FW) {
 #pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        red[(((wm * WGN + wn) * NI + j) * 2 + 0) * 16 + lane] = sp1[j];
-        red[(((wm * WGN + wn) * NI + j) * 2 + 1) * 16 + lane] = sp2[j];
+      for (int j = 0; j < FJ; ++j) {
+        red[(((wm * WGN + wn) * FJ + j) * 2 + 0) * FW + lane] = sp1[j];
+        red[(((wm * WGN + wn) * FJ + j) * 2 + 1) * FW + lane] = sp2[j];
       }
     }
     __syncthreads();
-    if (wm == 0 && lane < 16) {
+    if (wm == 0 && lane < FW) {
       double* st = p.colstats + (size_t)(bx % kStatSlots) * 2 * p.N;
 #pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const int col = n0 + wn * WTN + j * 16 + lane;
+      for (int j = 0; j < FJ; ++j) {
+        const int col = n0 + wn * WTN + j * FW + lane;
         if (col >= p.N) continue;
         float a1 = sp1[j], a2 = sp2[j];
 #pragma unroll
         for (int w = 1; w < WGM; ++w) {
-          a1 += red[(((w * WGN + wn) * NI + j) * 2 + 0) * 16 + lane];
-          a2 += red[(((w * WGN + wn) * NI + j) * 2 + 1) * 16 + lane];
+          a1 += red[(((w * WGN + wn) * FJ + j) * 2 + 0) * FW + lane];
+          a2 += red[(((w * WGN + wn) * FJ + j) * 2 + 1) * FW + lane];
         }
         atomicAdd(&st[col], (double)a1);
         atomicAdd(&st[p.N + col], (double)a2);
@@ -2904,6 +2982,18 @@ TDE_API void tde_igemm_tile_min(int v) {
 }
 
 TDE_API void tde_igemm_big_dgrad(int on) { g_big_dgrad = on ? 1 : 0; }
+// LDS-DMA kernels on v_mfma_f32_32x32x16_bf16 instead of 16x16x32 (bit mask by GEMM kind as TDE_XCD_SWIZZLE:
+// 1 = fwd / dense, 2 = dgrad, 4 = weight gradients); TDE_MFMA32 overrides.  Default 3: ResNet-18 per layer
+// (bench/resnet_layers.py --ab-mfma32, profiles/r6_mfma32/) fwd 508 -> 485 us and dgrad 543 -> 530 us per step
+// (every layer 2-7 % faster), while the transposed-read weight gradients lose (stage-2 128x128 tiles 50 -> 65-75 us)
+static int mfma32_default() {
+  const char* e = getenv("TDE_MFMA32");
+  return e ? atoi(e) : 3;
+}
+static int g_mfma32 = mfma32_default();
+TDE_API void tde_igemm_mfma32(int mask) { g_mfma32 = mask < 0 ? mfma32_default() : mask; }  // < 0: the default
+static unsigned long long g_m32_launches = 0;   // tests assert the 32x32 kernels ran
+TDE_API unsigned long long tde_igemm_mfma32_launches() { return g_m32_launches; }
 TDE_API unsigned long long tde_igemm_big_launches() { return g_big_launches; }
 
 TDE_API void tde_igemm_tune(int wg_target, int wg_min_kt, int kb_force, int glds, int big, int big_min) {
@@ -2994,10 +3084,9 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     // profiles/r2_xcd_ab.txt)
     g_xcd = e ? atoi(e) : 4;
   }
-  {
-    const int kind_bit = (akind == A_ROWK || akind == A_CONV) ? 1 : akind == A_DGRAD ? 2 : 4;
-    p.xcd = (g_xcd & kind_bit) ? 1 : 0;
-  }
+  const int kind_bit = (akind == A_ROWK || akind == A_CONV) ? 1 : akind == A_DGRAD ? 2 : 4;
+  p.xcd = (g_xcd & kind_bit) ? 1 : 0;
+  const bool m32 = (g_mfma32 & kind_bit) != 0;
   p.a = a;
   p.lda = lda;
   p.b = b;
@@ -3203,9 +3292,13 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
         grid = dim3((M + 255) / 256, (N + 127) / 128, grid.z);                                      \
         igemm_kernel<AK_, BK__, 256, 128, 64, 1, 3, 2><<<grid, 256, 0, stream>>>(p);                \
       } else if (KB == 64) {                                                                        \
-        igemm_kernel<AK_, BK__, BM_, BN_, 64, 1, 3><<<grid, 256, 0, stream>>>(p);                   \
+        if (m32) ++g_m32_launches;                                                                 \
+        if (m32) igemm_kernel<AK_, BK__, BM_, BN_, 64, 1, 3, 2, 32><<<grid, 256, 0, stream>>>(p);   \
+        else igemm_kernel<AK_, BK__, BM_, BN_, 64, 1, 3><<<grid, 256, 0, stream>>>(p);              \
       } else {                                                                                      \
-        igemm_kernel<AK_, BK__, BM_, BN_, 32, 1, 4><<<grid, 256, 0, stream>>>(p);                   \
+        if (m32) ++g_m32_launches;                                                                 \
+        if (m32) igemm_kernel<AK_, BK__, BM_, BN_, 32, 1, 4, 2, 32><<<grid, 256, 0, stream>>>(p);   \
+        else igemm_kernel<AK_, BK__, BM_, BN_, 32, 1, 4><<<grid, 256, 0, stream>>>(p);              \
       }                                                                                             \
     } else {                                                                                        \
       TDE_IGEMM(AK_, BK__, BM_, BN_);                                                               \
@@ -3230,11 +3323,18 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     else TDE_IGEMM(A_COLM, B_KN, 64, 64);
   } else if (akind == A_WGRAD && bkind == B_KN && wg_dma) {
     ++g_wg_dma_launches;
-    if (bm == 128 && bn == 128 && wg_stages == 2) igemm_kernel<A_WGRAD, B_KN, 128, 128, 64, 1, 2><<<grid, 256, 0, stream>>>(p);
-    else if (bm == 128 && bn == 128) igemm_kernel<A_WGRAD, B_KN, 128, 128, 64, 1, 3><<<grid, 256, 0, stream>>>(p);
-    else if (bm == 128) igemm_kernel<A_WGRAD, B_KN, 128, 64, 64, 1, 3><<<grid, 256, 0, stream>>>(p);
-    else if (bn == 128) igemm_kernel<A_WGRAD, B_KN, 64, 128, 64, 1, 3><<<grid, 256, 0, stream>>>(p);
-    else igemm_kernel<A_WGRAD, B_KN, 64, 64, 64, 1, 3><<<grid, 256, 0, stream>>>(p);
+    if (m32) ++g_m32_launches;
+#define TDE_WG_DMA(BM_, BN_, S_)                                                                \
+  do {                                                                                          \
+    if (m32) igemm_kernel<A_WGRAD, B_KN, BM_, BN_, 64, 1, S_, 2, 32><<<grid, 256, 0, stream>>>(p); \
+    else igemm_kernel<A_WGRAD, B_KN, BM_, BN_, 64, 1, S_><<<grid, 256, 0, stream>>>(p);           \
+  } while (0)
+    if (bm == 128 && bn == 128 && wg_stages == 2) TDE_WG_DMA(128, 128, 2);
+    else if (bm == 128 && bn == 128) TDE_WG_DMA(128, 128, 3);
+    else if (bm == 128) TDE_WG_DMA(128, 64, 3);
+    else if (bn == 128) TDE_WG_DMA(64, 128, 3);
+    else TDE_WG_DMA(64, 64, 3);
+#undef TDE_WG_DMA
   } else if (akind == A_WGRAD && bkind == B_KN) {
     if (bm == 128 && bn == 128) TDE_IGEMM(A_WGRAD, B_KN, 128, 128);
     else if (bm == 128) TDE_IGEMM(A_WGRAD, B_KN, 128, 64);

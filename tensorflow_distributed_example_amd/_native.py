@@ -63,6 +63,8 @@ _HIP_PROTOS = {
     "tde_igemm_tile_min": (None, [i32]),
     "tde_igemm_big_dgrad": (None, [i32]),
     "tde_igemm_wgrad_dma": (None, [i32]),
+    "tde_igemm_mfma32": (None, [i32]),
+    "tde_igemm_mfma32_launches": (C.c_ulonglong, []),
     "tde_igemm_wgrad_tile_cap": (None, [i32]),
     "tde_igemm_wgrad_dma_launches": (C.c_ulonglong, []),
     "tde_igemm_big_launches": (C.c_ulonglong, []),

@@ -49,6 +49,7 @@ HANDLE_VAR = "__tde_psdev_handle__"     # per ps task: [session, ok, bytes_mib, 
 REQ_VAR = "__tde_psdev_request__"       # per ps task: [session, mib] asked by the chief
 PLANE_VAR = "__tde_ps_plane__"          # ps 0: the chief's decision [1.0 device | 0.0 TCP, session]
 INIT_CTR = 2
+MAX_SEGS = 512                         # the exchange kernel stages the segment table in LDS (kPsMaxSegsLds)
 MAX_SHARDS = 16
 COUNTER_BYTES = 16 * 8
 SEG_DTYPE = np.dtype([("woff", "<i8"), ("loff", "<i8"), ("n", "<i8"), ("moff", "<i8"), ("win", "<i4"),
@@ -200,6 +201,9 @@ class DevicePlane:
             raise RuntimeError(f"the device data plane supports at most {MAX_SHARDS} ps tasks")
         self.kind, self.mmt, self.lr = int(kind), float(momentum), float(lr)
         segs, sizes = layout(store, client.placement, len(client.conns), slots=self.kind != 0)
+        if len(segs) > MAX_SEGS:
+            # raised before any window is mapped: the chief falls back to the TCP plane
+            raise RuntimeError(f"{len(segs)} variable segments; the device exchange stages at most {MAX_SEGS}")
         if segs.dtype.itemsize != self.lib.tde_psdev_seg_bytes():
             raise RuntimeError("segment table layout differs from the kernel's PsSeg")
         self.sizes = sizes
@@ -283,6 +287,12 @@ class DevicePlane:
         self.lib.tde_psdev_set_counter(self.win, 0, int(global_step))
         self.lib.tde_psdev_set_counter(self.win, 1, int(tickets))
         self.lib.tde_psdev_set_counter(self.win, INIT_CTR, 1)
+
+    def end_session(self):
+        """Chief, at session end: the windows stop counting as initialised, so a trainer of a later session
+        that maps them before that session's chief re-arms them waits instead of claiming stale tickets."""
+        if self.win is not None:
+            self.lib.tde_psdev_set_counter(self.win, INIT_CTR, 0)
 
     def wait_initialized(self, timeout=120.0):
         t0 = time.time()

@@ -430,11 +430,17 @@ class Estimator:
                     if isinstance(h, HK.CheckpointSaverHook):
                         h.saver_fn = lambda step: self._ps_save(plane, step)
             gstep = self._ps_loop_device(plane, chief, it, prog, plan, ctx, all_hooks, target, max_steps)
-            return self._ps_end(plane, chief, max_steps, gstep, ctx, all_hooks)
+            out = self._ps_end(plane, chief, max_steps, gstep, ctx, all_hooks)
+            if chief:
+                self._ps_clear_plane(client)
+            return out
         if os.environ.get("TDE_PS_FLAT", "1") == "0":
             gstep = self._ps_loop_per_variable(client, it, prog, plan, store, names_bn, bn_mom, lr, ctx, all_hooks,
                                                target, max_steps, gstep)
-            return self._ps_end(client, chief, max_steps, gstep, ctx, all_hooks)
+            out = self._ps_end(client, chief, max_steps, gstep, ctx, all_hooks)
+            if chief:
+                self._ps_clear_plane(client)
+            return out
         # flat pinned host mirrors of the store: one H2D for the pulled values, one D2H for the gradients,
         # one round trip per ps task per step (push + BN averages + counters + pull: PSClient.step)
         client.bind_store(store)
@@ -489,7 +495,20 @@ class Estimator:
             ctx.global_step = gstep
             for h in all_hooks:
                 h.after_step(ctx)
-        return self._ps_end(client, chief, max_steps, gstep, ctx, all_hooks)
+        out = self._ps_end(client, chief, max_steps, gstep, ctx, all_hooks)
+        if chief:
+            self._ps_clear_plane(client)
+        return out
+
+    @staticmethod
+    def _ps_clear_plane(client):
+        """Chief, at session end: ps task 0's plane record goes back to 'no decision' ([-1, 0]), so a non-chief
+        of the NEXT session waits for that session's chief instead of following this session's decision."""
+        from ..parallel import ps_device as PD
+        flag = np.array([-1.0, 0.0], np.float32)
+        c0 = client.conns[0]
+        c0.lib.tde_ps_init(c0.h, PD.PLANE_VAR.encode(), flag.ctypes.data, 2)
+        c0.lib.tde_ps_assign(c0.h, PD.PLANE_VAR.encode(), flag.ctypes.data, 2)
 
     def _ps_device_plane(self, client, store, bn_mom, lr, opt, chief):
         """The same-node GPU data plane (parallel/ps_device.py) or None (the host-staged TCP plane).  The chief
@@ -526,10 +545,16 @@ class Estimator:
             c0.lib.tde_ps_assign(c0.h, PD.PLANE_VAR.encode(), flag.ctypes.data, 2)
             return plane
         t0 = time.time()
-        while c0.lib.tde_ps_pull(c0.h, 1, names, (C.c_void_p * 1)(flag.ctypes.data), (C.c_longlong * 1)(2)) != 0:
+        # [-1, 0] = no decision yet (never recorded, or the previous session's chief cleared it at its end); a
+        # trainer that already ran a session on this Estimator also waits for a session tag other than its last
+        # (it can finish a session before that session's chief has cleared the record)
+        seen = getattr(self, "_ps_session_seen", None)
+        while (c0.lib.tde_ps_pull(c0.h, 1, names, (C.c_void_p * 1)(flag.ctypes.data), (C.c_longlong * 1)(2)) != 0
+               or flag[0] < 0 or (seen is not None and float(flag[1]) == seen)):
             if time.time() - t0 > 120:
                 raise TimeoutError("the chief never recorded the PS data plane")
             time.sleep(0.05)
+        self._ps_session_seen = float(flag[1])
         if flag[0] != 1.0:
             return None
         # the chief mapped the same session's windows: failing here is an error
@@ -608,6 +633,8 @@ class Estimator:
         for h in all_hooks:
             h.end(ctx)
         if hasattr(client, "win"):
+            if chief:
+                client.end_session()
             client.close()
         return self
 
@@ -662,6 +689,9 @@ class Estimator:
         if self.model._store.device.type == "cuda":
             torch.cuda.synchronize(self.model._store.device)   # the last async H2D out of the pinned mirrors
         if hasattr(client, "win"):    # device plane: the window's values straight into the store
+            # the pipelined loop's step counter lags the device by a few steps: label the checkpoint with the
+            # PS's own global step read after the synchronize (the pulled weights include at least that many)
+            step = max(int(step), client.global_step())
             client.pull()
         else:
             self.model._store.load_dict(client.pull())

@@ -100,7 +100,10 @@ def _same_device_pair(src, ring):
     """A contiguous device tensor of the ring's dtype that fits it (copied without a cast or a host hop)."""
     return (os.environ.get("TDE_STAGE_FUSED", "1") != "0" and torch.is_tensor(src) and ring.is_cuda
             and src.device == ring.device and src.dtype == ring.dtype
-            and src.is_contiguous() and src.numel() <= ring.numel())
+            and src.is_contiguous() and src.numel() <= ring.numel()
+            # tde_copy_pairs moves 4-byte words: odd bf16 counts / offsets take the staging path
+            and (src.numel() * src.element_size()) % 4 == 0
+            and src.data_ptr() % 4 == 0 and ring.data_ptr() % 4 == 0)
 
 
 class Program:

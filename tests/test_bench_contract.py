@@ -90,3 +90,17 @@ def test_bench_multi_gpu_without_launcher_on_gpu():
     assert res["n_gpus"] == 2 and res["config"]["strategy"] == "MirroredStrategy"
     assert res["config"]["plan"] == "fused_convnet" and res["config"]["hipgraph"] is True
     assert "replicas_identical=True" in r.stdout, r.stdout[-3000:]
+
+
+def test_bench_devices_list_sets_the_replica_count():
+    """`--strategy mirrored --devices cpu,cpu` without --gpus: the device list is the replica count (the
+    2-replica rehearsal form of tests/test_mirrored_gpu.py, `--devices 0,0`)."""
+    env = dict(os.environ, TDE_BENCH_WARM_MS="0", OMP_NUM_THREADS="1", TDE_HEARTBEAT="0", CUDA_VISIBLE_DEVICES="")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "TF_CONFIG"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--strategy", "mirrored", "--devices",
+                        "cpu,cpu", "--steps", "4", "--warmup", "1", "--repeats", "1"], env=env, cwd=ROOT,
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:]
+    res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert res["n_gpus"] == 2 and res["config"]["replicas_per_process"] == 2

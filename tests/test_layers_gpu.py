@@ -945,3 +945,28 @@ def test_bn_bwd_few_rows_with_dropout(R, C, drop):
     assert _rel(dg.cpu(), (dz * xhat).sum(0)) < 1e-2
     dxr = _cpu64(gamma) / torch.sqrt(var + 1e-3) * (dz - dz.mean(0) - xhat * (dz * xhat).mean(0))
     assert _rel(dx.float().cpu(), dxr) < 3e-2
+
+
+def test_igemm_mfma32_paths():
+    """Every LDS-DMA implicit-GEMM path on v_mfma_f32_32x32x16_bf16 (TDE_MFMA32 mask 7: fwd / dense, dgrad,
+    weight gradients) against the float64 references of the conv / dense tests, at the default tile choice and
+    with the largest tiles forced (128x128 / 128x64: 2x2 / 2x1 fragments of 32x32 per wave); the launch counter
+    proves the 32x32 kernels ran; the defaults are restored after."""
+    from tensorflow_distributed_example_amd import _native as N
+    lib = N.hip()
+    cases = (list(CONV_CASES) + list(WGRAD_DMA_CASES)
+             + [(4, 20, 20, 64, 128, 3, 1, "same"), (2, 14, 14, 128, 64, 3, 2, "same"), (2, 16, 16, 64, 64, 3, 1, "same"),
+                (2, 12, 12, 256, 256, 3, 1, "same")])
+    try:
+        lib.tde_igemm_mfma32(7)
+        for tmin in (2048, 1):
+            lib.tde_igemm_tile_min(tmin)
+            n0 = lib.tde_igemm_mfma32_launches()
+            for c in cases:
+                test_conv_fwd_dgrad_wgrad(*c)
+            for d in [(128, 1176, 200, False), (256, 512, 1000, False), (37, 64, 10, True)]:
+                test_dense_fwd_dgrad_wgrad(*d)
+            assert lib.tde_igemm_mfma32_launches() > n0, tmin
+    finally:
+        lib.tde_igemm_mfma32(-1)
+        lib.tde_igemm_tile_min(2048)

@@ -179,3 +179,22 @@ def test_ps_estimator_two_trainers_exact_max_steps(plane, nps, momentum):
     assert res["momentum"] == momentum, res
     assert res["final_global_step"] == 800, res
     assert res["value"] > 0
+
+
+def test_ps_estimator_second_session_follows_its_own_chief():
+    """Two consecutive train() sessions against the same ps tasks on the device plane: the chief
+    clears its plane record and the windows' initialised counter at session end, so the worker of session 2
+    waits for session 2's chief instead of claiming session 1's tickets; both sessions end at exactly their
+    max_steps."""
+    env = dict(os.environ, OMP_NUM_THREADS="2", TDE_HEARTBEAT="0", TDE_PS_DEVICE="1")
+    cmd = [sys.executable, "-m", "tensorflow_distributed_example_amd.launch", "--ps", "1", "--master", "1",
+           "--workers", "1", "--timeout", "150", os.path.join(ROOT, "bench", "ps_throughput.py"), "--max-steps", "600",
+           "--warm", "50", "--sessions", "2"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=200)
+    assert r.returncode == 0, r.stdout[-4000:]
+    lines = [l[l.index("{"):] for l in r.stdout.splitlines() if '{"metric"' in l]
+    assert len(lines) == 1, r.stdout[-3000:]
+    res = json.loads(lines[0])
+    print(res)
+    assert res["session_planes"] == ["device", "device"], res
+    assert res["session_end_steps"] == [300, 600], res
