@@ -2,10 +2,13 @@
 // (distributed_with_keras.py:33-43, tf2_mnist_distributed.py:66-72 with the user's own Conv2D filters /
 // Dense units):
 //   Conv2D(CC, 3x3, VALID, bias, ReLU) · MaxPooling2D(2) · Flatten · Dense(HD[, ReLU]) · Dense(C <= 16) + SCCE
-// for CC in {16, 32, 48, 64} and HD in {32, 64, 96, 128} (templates), exact-f32 MFMA (v_mfma_f32_16x16x4_f32)
-// over f32 LDS tiles and the f32 master weights.  The reference's own Conv2D(32) / Dense(64) keeps its
-// hand-tuned kernels (convnet_f32.hip: fused optimizer, deferred conv update, fused DP push); this family is
-// the general plan's "plain" step: gradients to the flat bucket, the multi-tensor optimizer after it.
+// for CC in {16, 32, 48, 64} and HD in {32, 64, ..., 256} (templates): the 27 (CC, HD) pairs whose 8-wave backward
+// fits a CU's LDS (Conv2D 16 / 32 up to Dense(256), 48 up to 192, 64 up to 160; `fits()` below, mirrored by the
+// Python plan's LDS-fit rule), exact-f32 MFMA (v_mfma_f32_16x16x4_f32) over f32 LDS tiles and the f32 master
+// weights.  The reference's own Conv2D(32) / Dense(64) keeps its hand-tuned kernels (convnet_f32.hip).  Two step
+// forms: "plain" (gradients to the flat bucket, the multi-tensor optimizer after it) and the fused step (the
+// optimizer applied inside the backward: Dense rows by their trunk workgroups, the head in place, the conv
+// update deferred and committed by the next step's forward; see `opt` / `hopt` / `fcommit` below).
 //
 //   forward   one pooled position x 64 images per workgroup (4 waves): conv + bias + ReLU + 2x2 max-pool
 //             for all CC channels (argmax bytes, the transposed pooled tile Pt), then the position's
