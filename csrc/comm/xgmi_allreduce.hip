@@ -175,16 +175,38 @@ __device__ __forceinline__ uint32_t await(char* base, int parity, int phase, int
   return missing;
 }
 
+// Payload reads of peer-written window bytes after a flag wait.  On the uncached window the wait drops no cache
+// (await's `acquire` is off: there is no L2 copy to invalidate, and 256 system-scope acquires per call were
+// measurable), so these reads are `nt` loads (NT = true): `nt` / `sc1` loads bypass the CU's vector L1 and are
+// served from L2 / memory (MI355X_MICROARCH.md, inter-workgroup visibility table: "sc1 / sc0 sc1 / nt loads
+// bypass L1 only"), so no L1 line left by an earlier call on the same area (areas are reused every second call)
+// can be returned stale, whatever the MTYPE of the mapping.  The cached window keeps its acquire and plain loads.
+typedef float wf4 __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ float4 wld4(const float* p, long long i) {
+  if constexpr (NT) {
+    const wf4 v = __builtin_nontemporal_load(reinterpret_cast<const wf4*>(p) + i);
+    return float4{v.x, v.y, v.z, v.w};
+  } else {
+    return reinterpret_cast<const float4*>(p)[i];
+  }
+}
+template <bool NT>
+__device__ __forceinline__ float wld(const float* p, long long i) {
+  if constexpr (NT) return __builtin_nontemporal_load(p + i);
+  else return p[i];
+}
+
+template <bool NT>
 __device__ __forceinline__ void copy_chunk(float* dst, const float* src, long long n, bool vec) {
   const int tid = threadIdx.x;
   if (vec) {
     const long long nv = n >> 2;
-    const float4* s4 = reinterpret_cast<const float4*>(src);
     float4* d4 = reinterpret_cast<float4*>(dst);
-    for (long long i = tid; i < nv; i += kXgThreads) d4[i] = s4[i];
-    for (long long i = (nv << 2) + tid; i < n; i += kXgThreads) dst[i] = src[i];
+    for (long long i = tid; i < nv; i += kXgThreads) d4[i] = wld4<NT>(src, i);
+    for (long long i = (nv << 2) + tid; i < n; i += kXgThreads) dst[i] = wld<NT>(src, i);
   } else {
-    for (long long i = tid; i < n; i += kXgThreads) dst[i] = src[i];
+    for (long long i = tid; i < n; i += kXgThreads) dst[i] = wld<NT>(src, i);
   }
 }
 
@@ -196,7 +218,9 @@ __device__ __forceinline__ void shadow_store(const XgArgs& a, long long e, float
   if (a.sht) a.sht[(q % a.sh_cols) * a.sht_ld + q / a.sh_cols] = h;
 }
 
-// Optimizer step on n reduced elements (global index g0..): w, slots, shadows; grad zeroed.
+// Optimizer step on n reduced elements (global index g0..): w, slots, shadows; grad zeroed.  red: window bytes
+// (read with wld / wld4, see copy_chunk).
+template <bool NT>
 __device__ __forceinline__ void apply_chunk(const XgArgs& a, float lr_t, long long g0, const float* red, long long n) {
   const int tid = threadIdx.x;
   const bool mom = a.h.kind != kOptSGD, adam = a.h.kind == kOptAdam;
@@ -205,7 +229,7 @@ __device__ __forceinline__ void apply_chunk(const XgArgs& a, float lr_t, long lo
     nv = n >> 2;
     for (long long i = tid; i < nv; i += kXgThreads) {
       const long long e = g0 + 4 * i;
-      const float4 gs = reinterpret_cast<const float4*>(red)[i];
+      const float4 gs = wld4<NT>(red, i);
       float4 w = *reinterpret_cast<const float4*>(a.w + e);
       float4 m = {0.f, 0.f, 0.f, 0.f}, v = {0.f, 0.f, 0.f, 0.f};
       if (mom) m = *reinterpret_cast<const float4*>(a.m + e);
@@ -232,7 +256,7 @@ __device__ __forceinline__ void apply_chunk(const XgArgs& a, float lr_t, long lo
   for (long long i = nv + tid; i < n; i += kXgThreads) {
     const long long e = g0 + i;
     float m = mom ? a.m[e] : 0.f, v = adam ? a.v[e] : 0.f;
-    const float w = opt_step(a.h, lr_t, a.w[e], red[i], m, v);
+    const float w = opt_step(a.h, lr_t, a.w[e], wld<NT>(red, i), m, v);
     a.w[e] = w;
     if (mom) a.m[e] = m;
     if (adam) a.v[e] = v;
@@ -301,10 +325,10 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
         dst[i] = v;
       }
     } else if (plo >= phi) {
-      copy_chunk(dst, a.grad + g0, n, (g0 & 3) == 0);
+      copy_chunk<false>(dst, a.grad + g0, n, (g0 & 3) == 0);
     } else {   // [0, plo) and [phi, n) still come from the local bucket
-      if (plo > 0) copy_chunk(dst, a.grad + g0, plo, false);
-      if (phi < n) copy_chunk(dst + phi, a.grad + g0 + phi, n - phi, false);
+      if (plo > 0) copy_chunk<false>(dst, a.grad + g0, plo, false);
+      if (phi < n) copy_chunk<false>(dst + phi, a.grad + g0 + phi, n - phi, false);
     }
   }
   publish<UNCACHED>(a.peer, N, parity, 0, r, blk, epoch);
@@ -319,17 +343,17 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
     const float* in = area(a.peer[r], 0, parity, cap) + c0;
     const long long nv = n >> 2;   // area offsets are multiples of 4 elements
     for (long long i = tid; i < nv; i += kXgThreads) {
-      float4 acc = reinterpret_cast<const float4*>(in)[i];
+      float4 acc = wld4<UNCACHED>(in, i);
       for (int s = 1; s < N; ++s) {
-        const float4 v = reinterpret_cast<const float4*>(in + (size_t)s * L)[i];
+        const float4 v = wld4<UNCACHED>(in + (size_t)s * L, i);
         acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
       }
       for (int p = 0; p < N; ++p)
         reinterpret_cast<float4*>(area(a.peer[p], 1, parity, cap) + (size_t)r * L + c0)[i] = acc;
     }
     for (long long i = (nv << 2) + tid; i < n; i += kXgThreads) {
-      float acc = in[i];
-      for (int s = 1; s < N; ++s) acc += in[(size_t)s * L + i];
+      float acc = wld<UNCACHED>(in, i);
+      for (int s = 1; s < N; ++s) acc += wld<UNCACHED>(in + (size_t)s * L, i);
       for (int p = 0; p < N; ++p) area(a.peer[p], 1, parity, cap)[(size_t)r * L + c0 + i] = acc;
     }
   }
@@ -345,8 +369,8 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
   for (int s = 0; s < N; ++s) {
     const long long g0 = (long long)s * L + c0;
     const long long n = max(0LL, min(CH, M - g0));
-    if (a.apply) apply_chunk(a, lr_t, g0, out + (size_t)s * L + c0, n);
-    else copy_chunk(a.grad + g0, out + (size_t)s * L + c0, n, (g0 & 3) == 0);
+    if (a.apply) apply_chunk<UNCACHED>(a, lr_t, g0, out + (size_t)s * L + c0, n);
+    else copy_chunk<UNCACHED>(a.grad + g0, out + (size_t)s * L + c0, n, (g0 & 3) == 0);
   }
   if (tr) {
     const uint32_t hw = __builtin_amdgcn_s_getreg(63492);   // hwreg(HW_REG_HW_ID): cu 8-11, se 13-15

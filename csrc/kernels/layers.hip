@@ -1461,6 +1461,36 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(BnBwdArgs a) {
   }
 }
 
+// Deterministic mode: dstats[p][0|1][c] = sum dz, sum dz*xhat over rows p (mod kStatSlots), in row order,
+// plain stores (every slot written); one channel per thread, 4 row lanes summed in a fixed order.
+__global__ __launch_bounds__(256) void bn_bwd_reduce_det_kernel(BnBwdArgs a) {
+  __shared__ float sc[kMaxCB], sf[kMaxCB], mu[kMaxCB], rs[kMaxCB];
+  __shared__ double red[2][4][64];
+  bn_bwd_prologue(a, sc, sf, mu, rs);
+  __syncthreads();
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6, c = blockIdx.x * 64 + cl, p = blockIdx.y;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < a.C)
+    for (long long r = p + (long long)kStatSlots * rl; r < a.R; r += 4LL * kStatSlots) {
+      const long long e = r * a.C + c;
+      const float v = bf2f(a.y[e]);
+      const float z = v * sc[c] + sf[c] + (a.res ? bf2f(a.res[e]) : 0.f);
+      float g = bf2f(a.dout[e]);
+      if (a.drop.rate > 0.f) g *= drop1(a.drop, e);
+      if (a.relu && !(z > 0.f)) g = 0.f;
+      s1 += g;
+      s2 += (double)(g * ((v - mu[c]) * rs[c]));
+    }
+  red[0][rl][cl] = s1;
+  red[1][rl][cl] = s2;
+  __syncthreads();
+  if (rl == 0 && c < a.C) {
+    float* ds = a.dstats + (size_t)p * 2 * a.C;
+    ds[c] = (float)((red[0][0][cl] + red[0][1][cl]) + (red[0][2][cl] + red[0][3][cl]));
+    ds[a.C + c] = (float)((red[1][0][cl] + red[1][1][cl]) + (red[1][2][cl] + red[1][3][cl]));
+  }
+}
+
 // Narrow layers (C <= CM, C % 8 != 0: Model B's 6 / 12 channel BNs): one thread per ROW keeps all
 // C channels' partial sums in registers (no per-element channel arithmetic, no LDS atomics); the
 // block folds them with DPP row reductions and lands 2C global atomics.  Batch-statistics mode
@@ -2589,6 +2619,33 @@ __global__ __launch_bounds__(256) void gap_fwd_kernel(const bf16* __restrict__ x
   }
 }
 
+// 64-channel groups (C % 64 == 0, 16-byte aligned): block (b, group) = 8 threads per 8-channel chunk x 32 pixel
+// slices, one 16-byte load per pixel, then a 32-way LDS reduction — every load of the block in flight together
+// (the per-element form walks HW serially per thread: 13.4 us for ResNet-18's 64x7x7x512)
+__global__ __launch_bounds__(256) void gap_fwd_vec_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int B,
+                                                          int HW, int C) {
+  __shared__ float part[32][65];
+  const int groups = C / 64;
+  const int b = blockIdx.x / groups, c0 = (blockIdx.x - b * groups) * 64;
+  const int ch = threadIdx.x & 7, sl = threadIdx.x >> 3;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bf16* p = x + (long long)b * HW * C + c0 + ch * 8;
+  for (int i = sl; i < HW; i += 32) {
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(p + (long long)i * C);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] += bf2f(v[e]);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[sl][ch * 8 + e] = s[e];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float t = 0.f;
+#pragma unroll 8
+    for (int q = 0; q < 32; ++q) t += part[q][threadIdx.x];
+    y[(long long)b * C + c0 + threadIdx.x] = f2bf(t * (1.f / (float)HW));
+  }
+}
+
 __global__ __launch_bounds__(256) void gap_bwd_kernel(const bf16* __restrict__ dy, bf16* __restrict__ dx, int B,
                                                       int HW, int C, int accum) {
   const long long n = (long long)B * HW * C;
@@ -2644,6 +2701,9 @@ struct XentArgs {
   long long* iterations;
 };
 
+// NV > 0: C <= 64 * NV, the row is loaded into registers once (all NV loads in flight together) and the three
+// passes (max, sum of exponentials, outputs) run on registers; NV = 0 re-reads the row per pass (any C).
+template <int NV>
 __global__ __launch_bounds__(256) void xent_kernel(XentArgs a) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -2652,10 +2712,23 @@ __global__ __launch_bounds__(256) void xent_kernel(XentArgs a) {
   const bool ok = row < a.B;
   if (ok) {
     const float* l = a.logits + (long long)row * a.ldl;
+    float rv[NV > 0 ? NV : 1];
+    if constexpr (NV > 0) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j) rv[j] = lane + 64 * j < a.C ? l[lane + 64 * j] : -INFINITY;
+    }
+    auto lv = [&](int j, int c) -> float {
+      if constexpr (NV > 0) return rv[j];
+      else return l[c];
+    };
+    const int nit = NV > 0 ? NV : (a.C + 63) / 64;
     float mx = -INFINITY;
     int am = 0x7fffffff;
-    for (int c = lane; c < a.C; c += 64) {
-      const float v = l[c];
+#pragma unroll
+    for (int j = 0; j < nit; ++j) {
+      const int c = lane + 64 * j;
+      if (c >= a.C) continue;
+      const float v = lv(j, c);
       if (v > mx) {
         mx = v;
         am = c;
@@ -2672,7 +2745,11 @@ __global__ __launch_bounds__(256) void xent_kernel(XentArgs a) {
       }
     }
     float se = 0.f;
-    for (int c = lane; c < a.C; c += 64) se += __expf(l[c] - mx);
+#pragma unroll
+    for (int j = 0; j < nit; ++j) {
+      const int c = lane + 64 * j;
+      if (c < a.C) se += __expf(lv(j, c) - mx);
+    }
     se = wave_sum(se);
     const int y = a.labels[row];
     const float lse = mx + __logf(se);
@@ -2680,10 +2757,14 @@ __global__ __launch_bounds__(256) void xent_kernel(XentArgs a) {
     loss = lse - ly;
     corr = (am == y) ? 1.f : 0.f;
     const float inv = 1.f / se;
-    for (int c = lane; c < a.C; c += 64) {
-      const float p = __expf(l[c] - mx) * inv;
+#pragma unroll
+    for (int j = 0; j < nit; ++j) {
+      const int c = lane + 64 * j;
+      if (c >= a.C) continue;
+      const float x = lv(j, c);
+      const float p = __expf(x - mx) * inv;
       if (a.dlogits) a.dlogits[(long long)row * a.ldd + c] = f2bf((p - (c == y ? 1.f : 0.f)) * a.scale);
-      if (a.probs) a.probs[(long long)row * a.C + c] = a.probs_are_logits ? l[c] : p;
+      if (a.probs) a.probs[(long long)row * a.C + c] = a.probs_are_logits ? x : p;
     }
   }
   if (lane == 0) {
@@ -3055,12 +3136,82 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
+// ---- deterministic mode (TDE_DETERMINISTIC=1 / tde_layers_deterministic): every reduction of the layer-wise
+// plan runs in a fixed order, so two runs of one configuration are bitwise identical (tests compare bucketed and
+// one-bucket data-parallel runs bitwise).  Per-channel sums move out of the GEMM epilogues /
+// streaming passes (whose f64 / f32 atomics land in run-dependent order) into the *_det kernels below: grid
+// (channel groups of 64, kStatSlots row parts), part p sums rows p, p + 8, ... in row order and STORES slot p
+// (readers sum the slots in slot order); split-K weight gradients go through the ordered partial scratch or run
+// unsplit; split-K activation GEMMs run unsplit.  Slow (one pass per sum, a few hundred workgroups): a
+// reproducibility / test mode, not the benchmarked path.
+static int g_det = [] {
+  const char* e = getenv("TDE_DETERMINISTIC");
+  return (e && e[0] && e[0] != '0') ? 1 : 0;
+}();
+TDE_API void tde_layers_deterministic(int on) { g_det = on ? 1 : 0; }
+TDE_API int tde_layers_is_deterministic() { return g_det; }
+
+// stats[p][0|1][c] = sum / sum of squares of x[r][c] (bf16, row stride ld) over rows r = p (mod kStatSlots)
+__global__ __launch_bounds__(256) void colstats_det_kernel(const bf16* __restrict__ x, long long R, int C, long long ld,
+                                                           double* __restrict__ stats) {
+  __shared__ double red[2][4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6, c = blockIdx.x * 64 + cl, p = blockIdx.y;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C)
+    for (long long r = p + (long long)kStatSlots * rl; r < R; r += 4LL * kStatSlots) {
+      const double v = (double)bf2f(x[r * ld + c]);
+      s1 += v;
+      s2 += v * v;
+    }
+  red[0][rl][cl] = s1;
+  red[1][rl][cl] = s2;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    double* st = stats + (size_t)p * 2 * C;
+    st[c] = (red[0][0][cl] + red[0][1][cl]) + (red[0][2][cl] + red[0][3][cl]);
+    st[C + c] = (red[1][0][cl] + red[1][1][cl]) + (red[1][2][cl] + red[1][3][cl]);
+  }
+}
+
+static int colstats_det(const bf16* x, long long R, int C, long long ld, double* stats, hipStream_t stream) {
+  colstats_det_kernel<<<dim3((C + 63) / 64, kStatSlots), 256, 0, stream>>>(x, R, C, ld, stats);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+// dbias[c] += sum over rows of (relu ? (out > 0) * dout : dout), rows in order (one block per 64 channels)
+__global__ __launch_bounds__(256) void colsum_det_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ out,
+                                                         long long R, int C, int relu, float* __restrict__ dbias) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
+  float s = 0.f;
+  if (c < C)
+    for (long long r = rl; r < R; r += 4) {
+      const long long e = r * C + c;
+      const float g = bf2f(dout[e]);
+      s += (!relu || bf2f(out[e]) > 0.f) ? g : 0.f;
+    }
+  red[rl][cl] = s;
+  __syncthreads();
+  if (rl == 0 && c < C) dbias[c] += (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+}
+
 TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, long long ldb, int bkind, int M, int N,
                       int K, const int* geo, int splits, float* cf, long long ldc, int cf_mode, float alpha, bf16* cb,
                       long long ldcb, int cb_accum, const float* bias, int relu, double* colstats, float* scratch,
                       const int* phase, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (phase && (akind != A_DGRAD || splits > 1 || colstats)) return -5;
+  if (g_det && colstats) {
+    // statistics of the stored bf16 output in a fixed order, after the GEMM (which runs without them)
+    if (!cb || cb_accum || relu) return -7;
+    int rc = tde_igemm(a, lda, akind, b, ldb, bkind, M, N, K, geo, splits, cf, ldc, cf_mode, alpha, cb, ldcb, cb_accum,
+                       bias, relu, nullptr, scratch, phase, stream);
+    if (rc) return rc;
+    return colstats_det(cb, M, N, ldcb, colstats, stream);
+  }
+  // deterministic: activation GEMMs unsplit (their split-K partials meet in f32 atomics)
+  if (g_det && splits > 1 && (cb || bias || relu || cf_mode == 1)) splits = 1;
   const bool fused_epi = cb || colstats || bias || relu || cf_mode == 1;
   if (splits > 1 && fused_epi) {
     // split-K into the zeroed f32 scratch, then the epilogue pass
@@ -3223,6 +3374,15 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
     // 128x64 also for long K loops that still give >= one workgroup per CU: half the operand re-reads
     // of 64x64 (ResNet-18 14x14x256 convs 34.7 -> 27.1 us; profiles/r2_sweep_fd.txt)
     bm = 128;
+  }
+  if (g_det && splits > 1) {
+    // deterministic: split-K weight gradients only through the ordered partial scratch (the condition below)
+    const bool ordered = rowk && auto_splits && splits <= g_wg_scratch_max && scratch && p.cf_mode == 2 &&
+                         p.ldc == N && p.cf && ((uintptr_t)p.cf & 15) == 0 && ((uintptr_t)scratch & 15) == 0;
+    if (!ordered) {
+      splits = 1;
+      p.ktiles_per_split = ktiles;
+    }
   }
   dim3 grid((M + bm - 1) / bm, (N + bn - 1) / bn, nph > 0 ? nph : splits);
   if (grid.y > 65535 || splits > 65535) return -3;
@@ -3420,6 +3580,18 @@ TDE_API int tde_bn_bwd(const bf16* dout, const bf16* y, const bf16* res, long lo
   BnBwdArgs a{dout, y, res, R, C, mode, saved, gamma, beta, relu, Drop{drop_rate, seed, iter, iter_offset, layer_id},
               dstats, dx, dx_accum, dres, dres_accum, dgamma, dbeta, zero_fwd};
   if (R * C >= (1LL << 31)) return -4;
+  if (g_det && mode == 1) {
+    // fixed-order backward sums into the kStatSlots slots, then the apply pass reads them (it sums slots in order)
+    bn_bwd_reduce_det_kernel<<<dim3((C + 63) / 64, kStatSlots), 256, 0, stream>>>(a);
+    TDE_LAUNCH_CHECK();
+    a.mode = 1;
+    if (bn_tiled_ok(C, {dout, y, res, dx, dres}))
+      bn_bwd_apply_tiled_kernel<<<bn_tiled_grid(R, C, bn_stream_blocks(R * C)), 256, 0, stream>>>(a);
+    else
+      bn_bwd_apply_kernel<<<grid_for(R * C, 8), 256, 0, stream>>>(a);
+    TDE_LAUNCH_CHECK();
+    return 0;
+  }
   if (bn_tiled_ok(C, {dout, y, res, dx, dres})) {
     if (mode == 1) {
       // each block ends with 2*min(C,64) global atomics: a moderate grid, deep per-thread ILP
@@ -3473,6 +3645,15 @@ TDE_API int tde_act_bwd(const bf16* dout, const bf16* out, long long R, int C, i
                         hipStream_t stream) {
   if (R * C >= (1LL << 31)) return -4;
   if (C > kMaxCB) return -1;
+  if (g_det && dbias) {
+    if (dz) {
+      act_bwd_kernel<<<grid_for(R * C, 8), 256, 0, stream>>>(dout, out, R, C, relu, dz, nullptr);
+      TDE_LAUNCH_CHECK();
+    }
+    colsum_det_kernel<<<(C + 63) / 64, 256, 0, stream>>>(dout, out, R, C, relu, dbias);
+    TDE_LAUNCH_CHECK();
+    return 0;
+  }
   act_bwd_kernel<<<grid_for(R * C, 8), 256, 0, stream>>>(dout, out, R, C, relu, dz, dbias);
   TDE_LAUNCH_CHECK();
   return 0;
@@ -3557,7 +3738,9 @@ TDE_API int tde_bn_pool_bwd(const bf16* dpool, const unsigned char* idx, const b
 
 TDE_API int tde_gap(const bf16* x, bf16* y, int B, int HW, int C, int backward, int accum, hipStream_t stream) {
   if ((long long)B * HW * C >= (1LL << 31)) return -4;
-  if (!backward) gap_fwd_kernel<<<grid_for((long long)B * C), 256, 0, stream>>>(x, y, B, HW, C);
+  if (!backward && C % 64 == 0 && aligned16(x) && (long long)B * (C / 64) < (1LL << 31))
+    gap_fwd_vec_kernel<<<B * (C / 64), 256, 0, stream>>>(x, y, B, HW, C);
+  else if (!backward) gap_fwd_kernel<<<grid_for((long long)B * C), 256, 0, stream>>>(x, y, B, HW, C);
   else gap_bwd_kernel<<<grid_for((long long)B * HW * C), 256, 0, stream>>>(x, y, B, HW, C, accum);
   TDE_LAUNCH_CHECK();
   return 0;
@@ -3576,7 +3759,8 @@ TDE_API int tde_xent(const float* logits, long long ldl, const int* labels, int 
                      hipStream_t stream) {
   if (B <= 0) return 0;
   XentArgs a{logits, ldl, labels, B, C, scale, dlogits, ldd, metrics, probs, probs_are_logits, iterations};
-  xent_kernel<<<(B + 3) / 4, 256, 0, stream>>>(a);
+  if (C <= 64 * 16) xent_kernel<16><<<(B + 3) / 4, 256, 0, stream>>>(a);
+  else xent_kernel<0><<<(B + 3) / 4, 256, 0, stream>>>(a);
   TDE_LAUNCH_CHECK();
   return 0;
 }
@@ -3584,6 +3768,7 @@ TDE_API int tde_xent(const float* logits, long long ldl, const int* labels, int 
 TDE_API int tde_colstats(const bf16* x, long long R, int C, double* stats, hipStream_t stream) {
   if (R * C >= (1LL << 31)) return -4;
   if (C > kMaxCB) return -1;
+  if (g_det) return colstats_det(x, R, C, C, stats, stream);
   colstats_kernel<<<grid_for(R * C, 8), 256, 0, stream>>>(x, R, C, stats);
   TDE_LAUNCH_CHECK();
   return 0;

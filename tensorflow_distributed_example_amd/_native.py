@@ -64,6 +64,8 @@ _HIP_PROTOS = {
     "tde_igemm_big_dgrad": (None, [i32]),
     "tde_igemm_wgrad_dma": (None, [i32]),
     "tde_igemm_mfma32": (None, [i32]),
+    "tde_layers_deterministic": (None, [i32]),
+    "tde_layers_is_deterministic": (i32, []),
     "tde_igemm_mfma32_launches": (C.c_ulonglong, []),
     "tde_igemm_wgrad_tile_cap": (None, [i32]),
     "tde_igemm_wgrad_dma_launches": (C.c_ulonglong, []),

@@ -29,6 +29,7 @@ import os
 import numpy as np
 import torch
 
+from .. import _native as N
 from .. import backend as Kb
 from ..models import layers as L
 from ..ops import layer_ops as O
@@ -122,6 +123,12 @@ class LayerwisePlan(PG.ReplicaPlan):
         self.model = model
         self.f32 = Kb.global_policy().compute_dtype == torch.float32
         self.compute_dtype = "fp32" if self.f32 else "bf16"
+        # TDE_DETERMINISTIC=1 (bf16 forms): every reduction in a fixed order (csrc/kernels/layers.hip g_det: sums by
+        # the *_det kernels, split-K through the ordered scratch) and the kernels whose sums are atomics off (halo
+        # conv statistics, fused BN + max-pool backward, narrow direct convs, fused head): two runs of one
+        # configuration are bitwise identical
+        self.det = (not self.f32 and torch.device(device).type == "cuda"
+                    and bool(N.hip().tde_layers_is_deterministic()))
         self.adt = torch.float32 if self.f32 else bf16          # activation / activation-gradient dtype
         self.sdt = torch.float64 if self.f32 else torch.float32  # BN backward-sum dtype
         # bf16: inputs staged as bf16 (Keras mixed_bfloat16 casts them at the first layer anyway), no per-step
@@ -285,7 +292,7 @@ class LayerwisePlan(PG.ReplicaPlan):
         # BatchNorm + ReLU whose only consumer is a MaxPool (the ResNet stem): one pass reads the conv output
         # and writes the pooled output + argmax; the BN output itself is never stored (its backward recomputes
         # z from the conv output).  TDE_BN_POOL=0 keeps the two launches.
-        if os.environ.get("TDE_BN_POOL", "1") != "0" and not self.f32:
+        if os.environ.get("TDE_BN_POOL", "1") != "0" and not self.f32 and not self.det:
             for i, st in enumerate(stages[:-1]):
                 nxt = stages[i + 1]
                 if (isinstance(st, _Elementwise) and st.bn and st.relu and st.res is None and st.drop.rate == 0
@@ -456,7 +463,7 @@ class _Gemm(_Stage):
                                   layer.strides[0], layer.strides[1], pt, pl)
             # narrow layers (C_out / C_in <= 32, e.g. Model B) take the direct VALU kernels
             # (per-thread FMA count bounds: above ~1k a thread's serial chain loses to the MFMA GEMM)
-            narrow = os.environ.get("TDE_SMALLCONV", "1") != "0"
+            narrow = os.environ.get("TDE_SMALLCONV", "1") != "0" and not plan.det
             r8 = lambda c: -(-c // 8) * 8  # noqa: E731
             kh, kw = layer.kernel_size
             sh, sw = layer.strides
@@ -481,7 +488,8 @@ class _Gemm(_Stage):
                                 and (not self.use_im2col or os.environ.get("TDE_SMALLWG_IM2COL", "0") == "1"))
         # 3x3 / stride-1 / SAME 64-channel convs without bias or activation (ResNet-18 stage 1): the persistent
         # halo-tile kernel (csrc/kernels/haloconv.hip) for the forward and the input gradient
-        self.halo = (self.conv and not self.f32 and not (self.small_fwd or self.use_im2col or self.use_stem_pack)
+        self.halo = (self.conv and not self.f32 and not plan.det
+                     and not (self.small_fwd or self.use_im2col or self.use_stem_pack)
                      and self.b is None and not self.relu and O.halo_ok(self.geo))
         self.colstats = None
         self.dz = None
@@ -899,7 +907,7 @@ class _Head(_Stage):
         self.H = tin.shape[0]
         self.W = st.view(self.wname)
         self.f32 = plan.f32
-        self.fused = (not self.f32 and self.C <= 16 and self.H <= 256 and self.H % 4 == 0
+        self.fused = (not self.f32 and not plan.det and self.C <= 16 and self.H <= 256 and self.H % 4 == 0
                       and os.environ.get("TDE_FUSED_HEAD", "1") != "0")
         self.shadows = {} if (self.fused or self.f32) else {self.wname: ("row", "col") if self.need_dgrad else ("col",)}
         self.pre = None   # absorbed Dense: its ReLU mask and bias gradient are applied by the head launch

@@ -312,6 +312,16 @@ def test_gap_pad_xent():
     assert _rel(dl.float(), lr.grad) < 1e-2
     assert _rel(probs, torch.softmax(logits.detach(), 1)) < 1e-5
     assert it.item() == 1
+    # the per-pass (C > 1024) xent form and the per-element GAP form (C % 64 != 0)
+    lg2 = torch.randn(5, 1500, device=DEV)
+    pr2 = torch.zeros(5, 1500, device=DEV)
+    O.xent(lg2, labels[:5] % 1500, 5, 1500, probs=pr2)
+    x3 = _r(2, 5, 5, 40, seed=15)
+    y3 = torch.zeros(2, 40, dtype=bf, device=DEV)
+    O.gap_fwd(x3, y3, 2, 25, 40)
+    torch.cuda.synchronize()
+    assert _rel(pr2, torch.softmax(lg2, 1)) < 1e-5
+    assert _rel(y3.float(), x3.float().mean((1, 2))) < 1e-2
 
 
 def _emulated_compare(model, x, y, B, tol):
