@@ -48,7 +48,8 @@ MODELS = {
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of the job (default 1; with --devices: the length of that list)")
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=64)
     ap.add_argument("--model", default="mnist_cnn", choices=sorted(MODELS))
@@ -73,6 +74,8 @@ def parse():
 
 def main():
     a = parse()
+    if a.gpus is None:
+        a.gpus = len(a.devices.split(",")) if a.devices else 1
     if a.no_graph:
         os.environ["TDE_GRAPH"] = "0"
     if a.executor:
