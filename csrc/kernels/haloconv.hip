@@ -335,6 +335,213 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   stamp(a.stamps, 5);
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// Weight gradient of the same layers: dW[tap][ci][co] = sum over pixels p of x[p + tap][ci] * dY[p][co].
+// The implicit GEMM (layers.hip, register-staged at Co = 64) re-gathers every input pixel once per tap through
+// L2 and runs at ~55 us per stage-1 layer for 14.8 GFLOP.  Here each workgroup (4 waves, ~147 KB of LDS) walks
+// a contiguous run of tiles (TR image rows x W pixels) exactly as the convolution above does: the input rows
+// with their halo in an LDS ring (TR new rows per tile, prefetched one tile ahead), the tile's dY rows in a
+// double buffer, both by LDS-DMA; every input byte and dY byte is loaded ONCE for all 9 taps.
+// GEMM view per tap: M = ci, N = co, K = pixels.  Both operands are pixel-major in LDS (128-byte rows of 64
+// channels), so the 16x16x32 fragments (8 consecutive pixels per lane) come from CDNA4's transposed LDS read
+// (ds_read_b64_tr_b16, as the weight gradients of layers.hip); a tap is an address offset into the halo ring.
+// Wave w owns input channels 16w .. 16w+15 for all 9 taps and 64 output channels: 36 accumulators (144 VGPRs)
+// that live across the workgroup's tiles.  Per 32-pixel k-step: 9 + 4 fragments (26 transposed reads), 36 MFMAs.
+// The workgroup stores its [9][64][64] f32 partial once at the end; one reduction pass (part_reduce_kernel) sums
+// the partials into the flat gradient in a fixed order (deterministic).
+// LDS rows (ring columns hc, dY columns c): 16-byte chunk q of row r at physical chunk q ^ wsw(r), wsw(r) =
+// (bit 1 of r, bit 3 of r) << 1 (layers.hip's RW = 64 swizzle): the 4 rows x 32 bytes of one 16-lane
+// transposed read hit 16 distinct bank slots for any first row (rows r, r + 2 always differ in bit 1).
+constexpr int kWgPix = 128;   // bytes per pixel row
+
+__device__ __forceinline__ int wsw(int r) { return (((r >> 1) & 1) | (((r >> 3) & 1) << 1)) << 1; }
+
+typedef short wv4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) wv4 lds_wv4;
+// fragment of 8 consecutive pixels (rows row0 + 8 * (lane >> 4) .. +7 of a 128-byte-row image at `base`, row r at
+// base + r * 128, shifted by `rshift` rows for the swizzle) x 16 channels cb .. cb+15: lane l gets the 8 pixels
+// of channel cb + (l & 15) — the A (or B) operand of v_mfma_f32_16x16x32_bf16 with K = pixels.
+__device__ __forceinline__ bf16x8 wg_frag(const char* base, int row0, int cb, int lane) {
+  const int i = lane & 15, q = i >> 2, pp = i & 3;
+  const int r_lo = row0 + 8 * (lane >> 4) + q;
+  const int ch = (cb >> 3) + (pp >> 1);
+  const wv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_wv4*)(base + r_lo * kWgPix + 16 * (ch ^ wsw(r_lo)) + 8 * (pp & 1)));
+  const wv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_wv4*)(base + (r_lo + 4) * kWgPix + 16 * (ch ^ wsw(r_lo + 4)) + 8 * (pp & 1)));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+struct WgArgs {
+  const bf16* x;    // [B,H,W,64] the layer input
+  const bf16* dy;   // [B,H,W,64] the output gradient
+  float* part;      // [gridDim][9][64][64] per-workgroup partial dW (HWIO order)
+  int B, H, W;
+  int bytes;        // B*H*W*128 (buffer range of both tensors)
+};
+
+template <int TR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void wgrad3x3_kernel(WgArgs a) {
+  constexpr int RING = 2 * TR + 4;
+  extern __shared__ __attribute__((aligned(16))) unsigned char wsm[];
+  const int W = a.W, H = a.H;
+  const int SS = (W + 2) * kWgPix;          // ring slot: W + 2 halo columns
+  const int DS = TR * W * kWgPix;           // dY buffer: the tile's TR rows
+  char* const ring = reinterpret_cast<char*>(wsm);
+  char* const dyb = ring + RING * SS;       // [2][TR * W] pixel rows
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tpi = H / TR, ntiles = a.B * tpi;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int t0 = (int)((long long)g * ntiles / G), t1 = (int)((long long)(g + 1) * ntiles / G);
+
+  f32x4 acc[9][4];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[t][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (t0 < t1) {
+    // zero halo columns of every ring slot (never written by the DMA)
+    for (int i = tid; i < RING * 2 * 8; i += 256) {
+      const int sl = i >> 4, side = (i >> 3) & 1, ch = i & 7;
+      *reinterpret_cast<uint4*>(ring + sl * SS + (side ? (W + 1) * kWgPix : 0) + ch * 16) = make_uint4(0, 0, 0, 0);
+    }
+    const halo::Rsrc rx = halo::make_rsrc(a.x, a.bytes), rd = halo::make_rsrc(a.dy, a.bytes);
+    const int per_row = W >> 3;   // one-KiB DMA instructions per image row (8 pixels each)
+    // input rows r_first .. (nrows of them) of image b into ring slots slot_first.. (halo column hc = p + 1);
+    // rows outside the image read zeros through the range check
+    auto issue_x = [&](int b, int r_first, int nrows, int slot_first) {
+      const int n = nrows * per_row;
+      for (int j = wave; j < n; j += 4) {
+        const int rr = j / per_row, jj = j - rr * per_row;
+        const int r = r_first + rr;
+        int slot = slot_first + rr;
+        while (slot >= RING) slot -= RING;
+        const int p = jj * 8 + (lane >> 3);
+        const int lc = (lane & 7) ^ wsw(p + 1);
+        const int voff = (unsigned)r < (unsigned)H ? (((b * H + r) * W + p) * kWgPix + (lc << 4)) : (int)0x80000000;
+        halo::dma16(rx, ring + slot * SS + kWgPix + jj * 1024, voff);
+      }
+    };
+    // the tile's dY rows (TR x W pixels, contiguous in memory) into dY buffer `buf` (pixel c of the tile = row c)
+    auto issue_dy = [&](int b, int r0, int buf) {
+      const int n = TR * per_row;
+      for (int j = wave; j < n; j += 4) {
+        const int c = j * 8 + (lane >> 3);
+        const int lc = (lane & 7) ^ wsw(c);
+        halo::dma16(rd, dyb + buf * DS + j * 1024, ((b * H + r0) * W + c) * kWgPix + (lc << 4));
+      }
+    };
+    int s0 = 0;
+    {
+      const int b = t0 / tpi, r0 = TR * (t0 - b * tpi);
+      issue_x(b, r0 - 1, TR + 2, 0);
+      issue_dy(b, r0, 0);
+    }
+    const int cb = 16 * wave;   // this wave's input channels (the A operand rows)
+    for (int t = t0; t < t1; ++t) {
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_s_barrier();   // the tile's rows landed; every wave is done with the previous tile
+      const int b = t / tpi, r0 = TR * (t - b * tpi);
+      const int buf = (t - t0) & 1;
+      int snext = s0;
+      if (t + 1 < t1) {
+        const int nb = (t + 1) / tpi, nr0 = TR * ((t + 1) - nb * tpi);
+        if (nb == b) {
+          issue_x(b, r0 + TR + 1, TR, s0 + TR + 2);
+          snext = s0 + TR;
+        } else {
+          issue_x(nb, nr0 - 1, TR + 2, s0 + TR + 2);
+          snext = s0 + TR + 2;
+        }
+        issue_dy(nb, nr0, buf ^ 1);
+      }
+      const char* dyt = dyb + buf * DS;
+      // k-steps of 32 pixels; lane group h = lane >> 4 takes pixels 32 k + 8 h .. +7 (one image row: W % 8 == 0)
+      for (int k = 0; k < TR * W / 32; ++k) {
+        const int p0 = 32 * k + 8 * (lane >> 4);
+        const int tr = p0 / W, c0 = p0 - tr * W;
+        bf16x8 bf[4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) bf[n] = wg_frag(dyt, 32 * k, 16 * n, lane);
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+          int sl = s0 + tr + kh;
+          if (sl >= RING) sl -= RING;
+          const char* rowb = ring + sl * SS;
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            // the fragment's 8 pixels sit in ONE ring row: rows c0 + kw .. +7 (relative to this lane group);
+            // wg_frag adds 8 * (lane >> 4), so pass the group-relative start minus it
+            const bf16x8 af = wg_frag(rowb, c0 + kw - 8 * (lane >> 4), cb, lane);
+#pragma unroll
+            for (int n = 0; n < 4; ++n) acc[kh * 3 + kw][n] = mfma16(af, bf[n], acc[kh * 3 + kw][n]);
+          }
+        }
+      }
+      s0 = snext >= RING ? snext - RING : snext;
+    }
+  }
+  // this workgroup's partial: lane holds rows (ci) cb + 4 (lane >> 4) + r, column (co) 16 n + (lane & 15)
+  float* dst = a.part + (size_t)g * 9 * 64 * 64;
+  const int cbs = 16 * (int)(tid >> 6);
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ci = cbs + 4 * (lane >> 4) + r, co = 16 * n + (lane & 15);
+        dst[(t * 64 + ci) * 64 + co] = acc[t][n][r];
+      }
+}
+
+// dst[i] += sum over s < splits of part[s][i] (n % 4 == 0): block = 64 consecutive elements (16 float4 columns) x 16
+// split groups (group j sums splits j, j + 16, ... in order), the groups summed in a fixed order through LDS —
+// every thread keeps its loads in flight (the generic split-K reduction walks all splits serially per thread:
+// 63 us for 256 partials of 36,864 floats)
+__global__ __launch_bounds__(256) void part_reduce_kernel(const float* __restrict__ part, int splits, long long n,
+                                                          float* __restrict__ dst) {
+  __shared__ float4 red[16][16];
+  const int col = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const long long n4 = n >> 2, i4 = (long long)blockIdx.x * 16 + col;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i4 < n4) {
+    const float4* p4 = reinterpret_cast<const float4*>(part);
+#pragma unroll 4
+    for (int s = grp; s < splits; s += 16) {
+      const float4 v = p4[(size_t)s * n4 + i4];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+  }
+  red[grp][col] = acc;
+  __syncthreads();
+  if (grp == 0 && i4 < n4) {
+    float4 t = red[0][col];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) {
+      const float4 v = red[j][col];
+      t.x += v.x;
+      t.y += v.y;
+      t.z += v.z;
+      t.w += v.w;
+    }
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    float4 d = d4[i4];
+    d.x += t.x;
+    d.y += t.y;
+    d.z += t.z;
+    d.w += t.w;
+    d4[i4] = d;
+  }
+}
+
 }  // namespace halo
 }  // namespace tde
 
@@ -417,6 +624,67 @@ TDE_API int tde_halo_conv3x3(const bf16* x, const bf16* w, long long wst, long l
   halo::Args a{x, w, wst, wsn, flip, y, accum, colstats, B, H, W, (int)((long long)B * H * W * halo::kPix),
                g_halo_stamps};
   hipLaunchKernelGGL(fn, dim3(grid), dim3(256), lds, stream, a);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---- weight gradient (wgrad3x3_kernel)
+static int halo_wg_lds(int W, int TR) { return (2 * TR + 4) * (W + 2) * halo::kWgPix + 2 * TR * W * halo::kWgPix; }
+// rows per tile: the largest TR in {4, 2} with H % TR == 0, whole 32-pixel k-steps and the LDS <= 160 KiB
+static int halo_wg_rows(int H, int W) {
+  for (int tr : {4, 2})
+    if (H % tr == 0 && (tr * W) % 32 == 0 && halo_wg_lds(W, tr) <= 160 * 1024) return tr;
+  return 0;
+}
+static int halo_wg_grid(int B, int H, int W) {
+  static const int env = [] {
+    const char* e = getenv("TDE_HALO_WG_GRID");
+    return e ? atoi(e) : 0;
+  }();
+  int grid = env;
+  if (grid <= 0) {
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    grid = cus;
+  }
+  const int tr = halo_wg_rows(H, W);
+  const int ntiles = tr ? B * (H / tr) : 1;
+  return grid > ntiles ? ntiles : grid;
+}
+
+TDE_API int tde_halo_wgrad_ok(int C, int Co, int H, int W, int B) {
+  if (C != halo::kC || Co != halo::kC || W % 8 != 0 || W < 8) return 0;
+  if ((long long)B * H * W * halo::kWgPix >= (1LL << 31)) return 0;
+  return halo_wg_rows(H, W) > 0;
+}
+// f32 elements of the per-workgroup partials of one launch (the plan's weight-gradient scratch)
+TDE_API long long tde_halo_wgrad_scratch_elems(int B, int H, int W) {
+  return (long long)halo_wg_grid(B, H, W) * 9 * 64 * 64;
+}
+
+// dW[3][3][64][64] (f32, HWIO) += sum over pixels of x (x) dY, 3x3 / stride 1 / SAME; part: scratch of
+// tde_halo_wgrad_scratch_elems floats
+TDE_API int tde_halo_wgrad3x3(const bf16* x, const bf16* dy, float* dW, float* part, long long part_elems, int B,
+                              int H, int W, hipStream_t stream) {
+  if (!tde_halo_wgrad_ok(64, 64, H, W, B)) return -2;
+  if (((uintptr_t)x & 15) || ((uintptr_t)dy & 15) || ((uintptr_t)dW & 15) || ((uintptr_t)part & 15)) return -3;
+  const int tr = halo_wg_rows(H, W);
+  const int grid = halo_wg_grid(B, H, W);
+  if (part_elems < (long long)grid * 9 * 64 * 64) return -5;
+  const int lds = halo_wg_lds(W, tr);
+  auto fn = tr == 4 ? halo::wgrad3x3_kernel<4> : halo::wgrad3x3_kernel<2>;
+  static bool attr[2] = {false, false};
+  if (!attr[tr == 4]) {
+    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+      return -4;
+    attr[tr == 4] = true;
+  }
+  halo::WgArgs a{x, dy, part, B, H, W, (int)((long long)B * H * W * halo::kWgPix)};
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(256), lds, stream, a);
+  TDE_LAUNCH_CHECK();
+  const long long n = 9LL * 64 * 64;
+  halo::part_reduce_kernel<<<(int)((n / 4 + 15) / 16), 256, 0, stream>>>(part, grid, n, dW);
   TDE_LAUNCH_CHECK();
   return 0;
 }

@@ -3196,6 +3196,18 @@ __global__ __launch_bounds__(256) void colsum_det_kernel(const bf16* __restrict_
   if (rl == 0 && c < C) dbias[c] += (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
 }
 
+// dst[i] += sum over s < splits of part[s][i] (i < n), in split order; also the reduction pass of the halo
+// weight gradient (haloconv.hip)
+TDE_API int tde_splitk_reduce(const float* part, int splits, long long n, float* dst, hipStream_t stream) {
+  if (n <= 0 || splits < 1) return 0;
+  if (((uintptr_t)part & 15) || ((uintptr_t)dst & 15)) return -3;
+  long long g = (n / 4 + 255) / 256;
+  g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
+  splitk_reduce_kernel<<<(int)g, 256, 0, stream>>>(part, splits, n, dst);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
 TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, long long ldb, int bkind, int M, int N,
                       int K, const int* geo, int splits, float* cf, long long ldc, int cf_mode, float alpha, bf16* cb,
                       long long ldcb, int cb_accum, const float* bias, int relu, double* colstats, float* scratch,

@@ -93,6 +93,10 @@ _HIP_PROTOS = {
     "tde_halo_conv_ok": (i32, [i32, i32, i32, i32, i32]),
     "tde_halo_stamps": (None, [p]),
     "tde_halo_conv3x3": (i32, [p, p, i64, i64, i32, p, i32, p, i32, i32, i32, i32, p]),
+    "tde_halo_wgrad_ok": (i32, [i32, i32, i32, i32, i32]),
+    "tde_halo_wgrad_scratch_elems": (i64, [i32, i32, i32]),
+    "tde_halo_wgrad3x3": (i32, [p, p, p, p, i64, i32, i32, i32, p]),
+    "tde_splitk_reduce": (i32, [p, i32, i64, p, p]),
     "tde_stem_pack": (i32, [p, p, p, p, p, p]),
     "tde_gather_rows_dev": (i32, [p, i64, i64, p, i64, p, p, p]),
     "tde_copy_pairs": (i32, [i32, p, p, p, p]),

@@ -180,6 +180,35 @@ def halo_conv(x, w, y, g: ConvGeom, *, dgrad=False, accum=False, colstats=None, 
                                      g.W, int(grid), _s()), "tde_halo_conv3x3")
 
 
+def halo_wgrad_ok(g: ConvGeom):
+    """The halo-tile weight gradient (csrc/kernels/haloconv.hip wgrad3x3_kernel): the same 3x3 / stride-1 / SAME
+    64 -> 64 channel convs.  TDE_HALO_WGRAD=0 (or TDE_HALO=0) disables it."""
+    if os.environ.get("TDE_HALO", "1") == "0" or os.environ.get("TDE_HALO_WGRAD", "1") == "0":
+        return False
+    if (g.KH, g.KW, g.sh, g.sw, g.pt, g.pl) != (3, 3, 1, 1, 1, 1) or (g.Ho, g.Wo) != (g.H, g.W):
+        return False
+    return bool(N.hip().tde_halo_wgrad_ok(g.C, g.Co, g.H, g.W, g.B))
+
+
+def halo_wgrad_scratch_elems(g: ConvGeom):
+    """f32 per-workgroup partials one halo weight-gradient launch stores (reduced into dW in workgroup order)."""
+    return int(N.hip().tde_halo_wgrad_scratch_elems(g.B, g.H, g.W))
+
+
+def halo_wgrad(x, dy, dW, g: ConvGeom, scratch):
+    """dW[3,3,64,64] (f32, HWIO) += sum over pixels of x (x) dy: one pass over x and dy for all 9 taps (per-workgroup
+    partials in ``scratch``, then the ordered reduction into dW)."""
+    n = g.B * g.H * g.W * 64
+    _bf(x, n, "halo_wgrad x")
+    _bf(dy, n, "halo_wgrad dy")
+    _f32(dW, 9 * 64 * 64, "halo_wgrad dW")
+    _req(halo_wgrad_ok(g), "halo_wgrad: geometry not covered")
+    need = halo_wgrad_scratch_elems(g)
+    _f32(scratch, need, "halo_wgrad scratch")
+    N.check(N.hip().tde_halo_wgrad3x3(_P(x), _P(dy), _P(dW), _P(scratch), int(scratch.numel()), g.B, g.H, g.W, _s()),
+            "tde_halo_wgrad3x3")
+
+
 def conv_dgrad(dy, Wrow, dx, g: ConvGeom, accum=False, scratch=None):
     """dx[B,H,W,C] (=|+=) conv_transpose(dy[B,Ho,Wo,Co], W); Wrow = HWIO bf16."""
     _bf(dy, g.B * g.Ho * g.Wo * g.Co, "conv_dgrad dy")

@@ -491,6 +491,10 @@ class _Gemm(_Stage):
         self.halo = (self.conv and not self.f32 and not plan.det
                      and not (self.small_fwd or self.use_im2col or self.use_stem_pack)
                      and self.b is None and not self.relu and O.halo_ok(self.geo))
+        # ... and its weight gradient (one pass over x and dY for all 9 taps; ordered partial reduction, so also
+        # under TDE_DETERMINISTIC)
+        self.halo_wg = (self.conv and not self.f32 and not (self.small_wgrad or self.use_im2col or self.use_stem_pack)
+                        and O.halo_wgrad_ok(self.geo))
         self.colstats = None
         self.dz = None
         self.act_done = False   # the consumer's launch already applied the ReLU mask / bias gradient
@@ -525,6 +529,8 @@ class _Gemm(_Stage):
             return 0
         if self.conv:
             g = self.geo.with_batch(B)
+            if self.halo_wg:
+                return O.halo_wgrad_scratch_elems(g)
             if self.use_im2col or self.small_wgrad:
                 return 0
             if self.use_stem_pack:
@@ -647,6 +653,8 @@ class _Gemm(_Stage):
             if self.use_stem_pack:
                 O.conv_wgrad(self.xp, dout, self.gWv, O.stem_geometry(g), scratch=p.wscratch)
                 O.stem_unpack_wgrad(self.gWv, g, self.gW)
+            elif self.halo_wg:
+                O.halo_wgrad(self.inp.buf, dout, self.gW, g, p.wscratch)
             elif self.small_wgrad:
                 O.smallconv_wgrad(self.inp.buf, dout, self.gW, g)
             elif self.use_im2col:

@@ -74,3 +74,39 @@ def test_halo_rejects_other_geometries():
     assert not O.halo_ok(O.ConvGeom(2, 28, 28, 128, 28, 28, 128, 3, 3, 1, 1, 1, 1))
     assert not O.halo_ok(O.ConvGeom(2, 56, 56, 64, 28, 28, 64, 3, 3, 2, 2, 0, 0))
     assert N.hip().tde_halo_conv_ok(64, 64, 56, 60, 2) == 0   # W % 8
+
+
+WG_CASES = [(2, 56, 56), (3, 8, 64), (1, 16, 32), (4, 28, 32), (2, 6, 16), (5, 12, 8)]
+
+
+@pytest.mark.parametrize("B,H,W", WG_CASES)
+def test_halo_weight_gradient(B, H, W):
+    """The halo-tile weight gradient (every input and dY byte loaded once for all 9 taps, per-workgroup partials
+    reduced in order) vs float64 autograd of the same bf16 operands, accumulated onto an existing f32 gradient,
+    bitwise reproducible run to run."""
+    g = _geo(B, H, W)
+    assert O.halo_wgrad_ok(g)
+    x = _r(B, H, W, 64, seed=6)
+    dy = _r(B, H, W, 64, seed=7)
+    base = torch.randn(3, 3, 64, 64, generator=torch.Generator().manual_seed(8))
+    need = O.halo_wgrad_scratch_elems(g)
+    outs = []
+    for _ in range(2):
+        dW = base.clone().to(DEV)
+        scr = torch.full((need,), float("nan"), device=DEV)
+        O.halo_wgrad(x.to(DEV).reshape(-1), dy.to(DEV).reshape(-1), dW, g, scr)
+        torch.cuda.synchronize()
+        outs.append(dW.cpu())
+    wd = torch.zeros(64, 64, 3, 3, dtype=torch.float64, requires_grad=True)
+    yd = F.conv2d(x.double().permute(0, 3, 1, 2), wd, padding=1)
+    yd.backward(dy.double().permute(0, 3, 1, 2))
+    ref = wd.grad.permute(2, 3, 1, 0) + base.double()      # HWIO
+    assert _rel(outs[0] - base, ref - base.double()) < 1e-5
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_halo_wgrad_rejects_other_geometries():
+    assert not O.halo_wgrad_ok(O.ConvGeom(2, 28, 28, 128, 28, 28, 128, 3, 3, 1, 1, 1, 1))
+    assert not O.halo_wgrad_ok(O.ConvGeom(2, 56, 56, 64, 28, 28, 64, 3, 3, 2, 2, 0, 0))
+    assert N.hip().tde_halo_wgrad_ok(64, 64, 56, 60, 2) == 0   # W % 8
+    assert N.hip().tde_halo_wgrad_ok(64, 64, 7, 8, 2) == 0     # H has no 2- or 4-row tiling
