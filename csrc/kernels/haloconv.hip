@@ -374,6 +374,21 @@ __device__ __forceinline__ bf16x8 wg_frag(const char* base, int row0, int cb, in
   return __builtin_bit_cast(bf16x8, r);
 }
 
+// 32x32x16 form: lane l gets pixels row0 + 8 * (l >> 5) .. +7 of channels cb + (l & 31) (the A / B operand of
+// v_mfma_f32_32x32x16_bf16 with K = 16 pixels); each 16-lane group runs wg_frag's two transposed reads
+__device__ __forceinline__ bf16x8 wg_frag32(const char* base, int row0, int cb, int lane) {
+  const int i = lane & 15, q = i >> 2, pp = i & 3;
+  const int r_lo = row0 + 8 * (lane >> 5) + q;
+  const int ch = ((cb + 16 * ((lane >> 4) & 1)) >> 3) + (pp >> 1);
+  const wv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_wv4*)(base + r_lo * kWgPix + 16 * (ch ^ wsw(r_lo)) + 8 * (pp & 1)));
+  const wv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_wv4*)(base + (r_lo + 4) * kWgPix + 16 * (ch ^ wsw(r_lo + 4)) + 8 * (pp & 1)));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, r);
+}
+
 struct WgArgs {
   const bf16* x;    // [B,H,W,64] the layer input
   const bf16* dy;   // [B,H,W,64] the output gradient
@@ -382,7 +397,10 @@ struct WgArgs {
   int bytes;        // B*H*W*128 (buffer range of both tensors)
 };
 
-template <int TR>
+// MF = 32: v_mfma_f32_32x32x16_bf16, wave w = input-channel half (w >> 1) x output-channel half (w & 1), 9
+// accumulators of 32x32; per 16-pixel k-step 9 + 1 fragments feed 9 MFMAs (half the instructions per flop of
+// the 16x16x32 form at one wave per SIMD)
+template <int TR, int MF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void wgrad3x3_kernel(WgArgs a) {
   constexpr int RING = 2 * TR + 4;
   extern __shared__ __attribute__((aligned(16))) unsigned char wsm[];
@@ -397,11 +415,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int G = gridDim.x, g = blockIdx.x;
   const int t0 = (int)((long long)g * ntiles / G), t1 = (int)((long long)(g + 1) * ntiles / G);
 
-  f32x4 acc[9][4];
+  f32x4 acc[MF == 16 ? 9 : 1][4];
+  f32x16 acc2[MF == 32 ? 9 : 1];
+  if constexpr (MF == 16) {
 #pragma unroll
-  for (int t = 0; t < 9; ++t)
+    for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) acc[t][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int n = 0; n < 4; ++n) acc[t][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  } else {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc2[t][r] = 0.f;
+  }
 
   if (t0 < t1) {
     // zero halo columns of every ring slot (never written by the DMA)
@@ -460,6 +486,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         issue_dy(nb, nr0, buf ^ 1);
       }
       const char* dyt = dyb + buf * DS;
+      if constexpr (MF == 32) {
+        const int ci0 = 32 * (wave >> 1), co0 = 32 * (wave & 1);
+        // k-steps of 16 pixels; lane half h = lane >> 5 takes pixels 16 k + 8 h .. +7 (one image row)
+        for (int k = 0; k < TR * W / 16; ++k) {
+          const int p0 = 16 * k + 8 * (lane >> 5);
+          const int tr = p0 / W, c0 = p0 - tr * W;
+          const bf16x8 bfr = wg_frag32(dyt, 16 * k, co0, lane);
+#pragma unroll
+          for (int kh = 0; kh < 3; ++kh) {
+            int sl = s0 + tr + kh;
+            if (sl >= RING) sl -= RING;
+            const char* rowb = ring + sl * SS;
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+              const bf16x8 af = wg_frag32(rowb, c0 + kw - 8 * (lane >> 5), ci0, lane);
+              acc2[kh * 3 + kw] = mfma32(af, bfr, acc2[kh * 3 + kw]);
+            }
+          }
+        }
+      } else
       // k-steps of 32 pixels; lane group h = lane >> 4 takes pixels 32 k + 8 h .. +7 (one image row: W % 8 == 0)
       for (int k = 0; k < TR * W / 32; ++k) {
         const int p0 = 32 * k + 8 * (lane >> 4);
@@ -485,18 +531,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       s0 = snext >= RING ? snext - RING : snext;
     }
   }
-  // this workgroup's partial: lane holds rows (ci) cb + 4 (lane >> 4) + r, column (co) 16 n + (lane & 15)
   float* dst = a.part + (size_t)g * 9 * 64 * 64;
-  const int cbs = 16 * (int)(tid >> 6);
+  if constexpr (MF == 32) {
+    // lane holds rows (ci) ci0 + 8 (r >> 2) + 4 (lane >> 5) + (r & 3), column (co) co0 + (lane & 31)
+    const int w = (int)(tid >> 6), ci0 = 32 * (w >> 1), co0 = 32 * (w & 1);
 #pragma unroll
-  for (int t = 0; t < 9; ++t)
+    for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ci = cbs + 4 * (lane >> 4) + r, co = 16 * n + (lane & 15);
-        dst[(t * 64 + ci) * 64 + co] = acc[t][n][r];
+      for (int r = 0; r < 16; ++r) {
+        const int ci = ci0 + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3), co = co0 + (lane & 31);
+        dst[(t * 64 + ci) * 64 + co] = acc2[t][r];
       }
+  } else {
+    // lane holds rows (ci) cb + 4 (lane >> 4) + r, column (co) 16 n + (lane & 15)
+    const int cbs = 16 * (int)(tid >> 6);
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ci = cbs + 4 * (lane >> 4) + r, co = 16 * n + (lane & 15);
+          dst[(t * 64 + ci) * 64 + co] = acc[t][n][r];
+        }
+  }
 }
 
 // dst[i] += sum over s < splits of part[s][i] (n % 4 == 0): block = 64 consecutive elements (16 float4 columns) x 16
@@ -653,6 +711,16 @@ static int halo_wg_grid(int B, int H, int W) {
   return grid > ntiles ? ntiles : grid;
 }
 
+// MFMA shape of the weight gradient: TDE_HALO_WG_MFMA = 16 | 32 (default 16); tde_halo_wgrad_mfma (tests, A/B).
+// The 32x32x16 form measured slower on ResNet-18 stage 1 (30.4 -> 37.1 us per layer, 22.48k -> 22.28k img/s,
+// profiles/r6_halo_wgrad/): it needs 10 transposed fragment reads per 9 MFMAs of 16 pixels against 13 per 36
+// MFMAs of 32 pixels, and the LDS reads, not the MFMA issue, bound this loop.
+static int g_hwg_mf = [] {
+  const char* e = getenv("TDE_HALO_WG_MFMA");
+  return e && atoi(e) == 32 ? 32 : 16;
+}();
+TDE_API void tde_halo_wgrad_mfma(int mf) { g_hwg_mf = mf == 32 ? 32 : 16; }
+
 TDE_API int tde_halo_wgrad_ok(int C, int Co, int H, int W, int B) {
   if (C != halo::kC || Co != halo::kC || W % 8 != 0 || W < 8) return 0;
   if ((long long)B * H * W * halo::kWgPix >= (1LL << 31)) return 0;
@@ -673,12 +741,20 @@ TDE_API int tde_halo_wgrad3x3(const bf16* x, const bf16* dy, float* dW, float* p
   const int grid = halo_wg_grid(B, H, W);
   if (part_elems < (long long)grid * 9 * 64 * 64) return -5;
   const int lds = halo_wg_lds(W, tr);
-  auto fn = tr == 4 ? halo::wgrad3x3_kernel<4> : halo::wgrad3x3_kernel<2>;
-  static bool attr[2] = {false, false};
-  if (!attr[tr == 4]) {
+  const int mf = g_hwg_mf;
+  void (*fn)(halo::WgArgs) = mf == 32 ? (tr == 4 ? halo::wgrad3x3_kernel<4, 32> : halo::wgrad3x3_kernel<2, 32>)
+                                      : (tr == 4 ? halo::wgrad3x3_kernel<4, 16> : halo::wgrad3x3_kernel<2, 16>);
+  static void (*attr[4])(halo::WgArgs) = {nullptr, nullptr, nullptr, nullptr};
+  bool done = false;
+  for (int i = 0; i < 4 && attr[i]; ++i) done |= attr[i] == fn;
+  if (!done) {
     if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
       return -4;
-    attr[tr == 4] = true;
+    for (int i = 0; i < 4; ++i)
+      if (!attr[i]) {
+        attr[i] = fn;
+        break;
+      }
   }
   halo::WgArgs a{x, dy, part, B, H, W, (int)((long long)B * H * W * halo::kWgPix)};
   hipLaunchKernelGGL(fn, dim3(grid), dim3(256), lds, stream, a);

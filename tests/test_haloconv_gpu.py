@@ -79,8 +79,9 @@ def test_halo_rejects_other_geometries():
 WG_CASES = [(2, 56, 56), (3, 8, 64), (1, 16, 32), (4, 28, 32), (2, 6, 16), (5, 12, 8)]
 
 
+@pytest.mark.parametrize("mf", [32, 16])
 @pytest.mark.parametrize("B,H,W", WG_CASES)
-def test_halo_weight_gradient(B, H, W):
+def test_halo_weight_gradient(B, H, W, mf):
     """The halo-tile weight gradient (every input and dY byte loaded once for all 9 taps, per-workgroup partials
     reduced in order) vs float64 autograd of the same bf16 operands, accumulated onto an existing f32 gradient,
     bitwise reproducible run to run."""
@@ -91,6 +92,7 @@ def test_halo_weight_gradient(B, H, W):
     base = torch.randn(3, 3, 64, 64, generator=torch.Generator().manual_seed(8))
     need = O.halo_wgrad_scratch_elems(g)
     outs = []
+    N.hip().tde_halo_wgrad_mfma(mf)   # v_mfma_f32_32x32x16_bf16 or the 16x16x32 form (default)
     for _ in range(2):
         dW = base.clone().to(DEV)
         scr = torch.full((need,), float("nan"), device=DEV)
@@ -101,6 +103,7 @@ def test_halo_weight_gradient(B, H, W):
     yd = F.conv2d(x.double().permute(0, 3, 1, 2), wd, padding=1)
     yd.backward(dy.double().permute(0, 3, 1, 2))
     ref = wd.grad.permute(2, 3, 1, 0) + base.double()      # HWIO
+    N.hip().tde_halo_wgrad_mfma(16)
     assert _rel(outs[0] - base, ref - base.double()) < 1e-5
     assert torch.equal(outs[0], outs[1])
 
