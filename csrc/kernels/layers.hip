@@ -3031,9 +3031,12 @@ static int g_wg_small_tiles = [] {
   const char* e = getenv("TDE_WG_SMALL_TILES");
   return e ? atoi(e) : 1;
 }();
+// (default 256: with the grouped fixed-order reduction the partials beat the f32 atomics of many-way splits —
+// ResNet-18 weight gradients 797 -> 727 us per step in isolation, stage-2 3x3 51.6 -> 41.3 us, end to end
+// 22.36k -> 22.86k img/s at 64; profiles/r6_splitk/)
 static int g_wg_scratch_max = [] {
   const char* e = getenv("TDE_WG_SCRATCH_MAX");
-  return e ? atoi(e) : 16;
+  return e ? atoi(e) : 256;
 }();
 // weight gradients through the row-padded LDS-DMA path (TDE_WGRAD_DMA=0: the register-staged loaders)
 // 0 = off, 1 = 3 LDS stages, 2 = 2 stages, 3 = per shape (default; bench/resnet_layers.py --sweep-wgrad,
@@ -3198,14 +3201,65 @@ __global__ __launch_bounds__(256) void colsum_det_kernel(const bf16* __restrict_
 
 // dst[i] += sum over s < splits of part[s][i] (i < n), in split order; also the reduction pass of the halo
 // weight gradient (haloconv.hip)
+static void splitk_reduce_launch(const float* part, int splits, long long n, float* dst, hipStream_t stream);
 TDE_API int tde_splitk_reduce(const float* part, int splits, long long n, float* dst, hipStream_t stream) {
   if (n <= 0 || splits < 1) return 0;
   if (((uintptr_t)part & 15) || ((uintptr_t)dst & 15)) return -3;
+  splitk_reduce_launch(part, splits, n, dst, stream);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+// Many splits (>= 8, n % 4 == 0): block = 64 consecutive elements (16 float4 columns) x 16 split groups, group j
+// summing splits j, j + 16, ... in order and the groups summed in a fixed order through LDS — every thread's loads in
+// flight together (the one-thread-per-element form walks all splits serially)
+__global__ __launch_bounds__(256) void splitk_reduce_grouped_kernel(const float* __restrict__ part, int splits,
+                                                                    long long n, float* __restrict__ dst) {
+  __shared__ float4 red[16][16];
+  const int col = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const long long n4 = n >> 2, i4 = (long long)blockIdx.x * 16 + col;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i4 < n4) {
+    const float4* p4 = reinterpret_cast<const float4*>(part);
+#pragma unroll 4
+    for (int s = grp; s < splits; s += 16) {
+      const float4 v = p4[(size_t)s * n4 + i4];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+  }
+  red[grp][col] = acc;
+  __syncthreads();
+  if (grp == 0 && i4 < n4) {
+    float4 t = red[0][col];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) {
+      const float4 v = red[j][col];
+      t.x += v.x;
+      t.y += v.y;
+      t.z += v.z;
+      t.w += v.w;
+    }
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    float4 d = d4[i4];
+    d.x += t.x;
+    d.y += t.y;
+    d.z += t.z;
+    d.w += t.w;
+    d4[i4] = d;
+  }
+}
+
+static void splitk_reduce_launch(const float* part, int splits, long long n, float* dst, hipStream_t stream) {
+  if (splits >= 8 && n % 4 == 0 && ((n / 4 + 15) / 16) < (1LL << 31)) {
+    splitk_reduce_grouped_kernel<<<(int)((n / 4 + 15) / 16), 256, 0, stream>>>(part, splits, n, dst);
+    return;
+  }
   long long g = (n / 4 + 255) / 256;
   g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
   splitk_reduce_kernel<<<(int)g, 256, 0, stream>>>(part, splits, n, dst);
-  TDE_LAUNCH_CHECK();
-  return 0;
 }
 
 TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, long long ldb, int bkind, int M, int N,
@@ -3520,10 +3574,8 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   TDE_LAUNCH_CHECK();
   if (wg_scratch) {
     const long long n = (long long)M * N;
-    long long g = (n / 4 + 255) / 256;
-    g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
     (void)wg_ldc;
-    splitk_reduce_kernel<<<(int)g, 256, 0, stream>>>(scratch, splits, n, wg_dst);
+    splitk_reduce_launch(scratch, splits, n, wg_dst, stream);
     TDE_LAUNCH_CHECK();
   }
   return 0;

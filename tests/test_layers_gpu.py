@@ -980,3 +980,20 @@ def test_igemm_mfma32_paths():
     finally:
         lib.tde_igemm_mfma32(-1)
         lib.tde_igemm_tile_min(2048)
+
+
+def test_wgrad_many_split_scratch_reduction():
+    """Weight gradients split 8+ ways through the partial scratch (TDE_WG_SCRATCH_MAX=64) reduce with the grouped
+    fixed-order kernel (16 split groups per 64 elements): same float64 references, in a child process (the library
+    reads the knob once)."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = ("import sys; sys.path.insert(0, %r); import test_layers_gpu as t\n"
+            "t.test_conv_fwd_dgrad_wgrad(16, 28, 28, 128, 128, 3, 1, 'same')\n"
+            "t.test_conv_fwd_dgrad_wgrad(8, 16, 16, 64, 128, 3, 1, 'same')\nprint('ok')\n" % here)
+    env = dict(os.environ, TDE_WG_SCRATCH_MAX="64")
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=os.path.dirname(here), capture_output=True,
+                       text=True, timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
