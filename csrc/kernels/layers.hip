@@ -47,6 +47,21 @@ struct Geo {  // NHWC input [B,H,W,C], HWIO kernel [KH,KW,C,Co], NHWC output [B,
 enum AKind { A_ROWK = 0, A_CONV = 1, A_DGRAD = 2, A_COLM = 3, A_WGRAD = 4 };
 enum BKind { B_NK = 0, B_DGRADW = 1, B_KN = 2 };
 
+// The backward sums of the BatchNormalization whose OUTPUT gradient an input-gradient GEMM produces (it is the
+// last writer of that gradient): sum g and sum g * xhat per channel with g = the stored gradient masked by the
+// BN's ReLU (z = y * gamma * rstd + beta - mean * gamma * rstd + res > 0), xhat = (y - mean) * rstd — what
+// bn_bwd_reduce_*_kernel computes in its own pass, taken in the GEMM's epilogue instead (that pass then vanishes;
+// the BN backward runs its apply pass only).  dstats: [kStatSlots][2][C] f32, zeroed by the BN forward.
+struct BnSum {
+  const bf16* y;       // [rows][C] the BN input (this GEMM's output layout)
+  const bf16* res;     // [rows][C] the BN's residual input, or null
+  const float* saved;  // [2][C] batch mean, rstd
+  const float* gamma;  // nullable
+  const float* beta;   // nullable
+  int relu;
+  float* dstats;       // null: off
+};
+
 struct IGemmArgs {
   const bf16* a;
   long long lda;
@@ -81,6 +96,7 @@ struct IGemmArgs {
   // {ph_h, ph_w, Hp, Wp, kh0, kw0, KHp, KWp}; M and K follow per phase, grid x covers the largest M
   int nph;
   int phs[4][8];
+  BnSum bs;   // input gradients only: the consumer BN's backward sums in the epilogue (bs.dstats null = off)
 };
 
 constexpr int TK = 32;  // MFMA k-slice
@@ -649,6 +665,27 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p_) {
   auto frow = [&](int r) -> int { return MF == 32 ? 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3) : (lane >> 4) * 4 + r; };
   const int fcl = lane & (FW - 1);   // the lane's column within a fragment
 
+  // BN backward sums (p.bs, input gradients on the LDS-DMA path): the BN input y (and residual) of this thread's
+  // epilogue chunks (rows m0 + (tid + 256 i) / (BN / 8), 8 columns at n0 + 8 (tid % (BN / 8))) are loaded here,
+  // before the K loop, so the epilogue never waits on them; tiles with more than 4 chunks per thread load them in
+  // the epilogue instead
+  constexpr int BCH = BM * (BN / 8) / 256;
+  constexpr bool BPRE = GLDS && AKV && BCH <= 4;
+  bf16x8 pyv[BPRE ? BCH : 1], prv[BPRE ? BCH : 1];
+  if constexpr (BPRE) {
+    if (p.bs.dstats) {
+#pragma unroll
+      for (int i = 0; i < BCH; ++i) {
+        const int c = tid + 256 * i, lr = c / (BN / 8), ch = c - lr * (BN / 8);
+        const int mrow = m0 + lr, col0 = n0 + ch * 8;
+        const bool ok = mrow < p.M && col0 < p.N;
+        const long long eo = (long long)(ok ? mrow : 0) * p.ldcb + (ok ? col0 : 0);
+        pyv[i] = ok ? *reinterpret_cast<const bf16x8*>(p.bs.y + eo) : zero8();
+        prv[i] = (ok && p.bs.res) ? *reinterpret_cast<const bf16x8*>(p.bs.res + eo) : zero8();
+      }
+    }
+  }
+
   const int fr = lane & 15, fk = (lane >> 4) * 8;
   if constexpr (GLDS && !AKV) {
     // Weight gradient dW[(kh,kw,ci), co] = sum over pixels of X(pixel shifted by the tap)[ci] * dY[pixel][co],
@@ -1047,6 +1084,23 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p_) {
       // row-contiguous 8-column chunks: 16-byte bf16 stores (read-add-store for accumulated outputs)
       constexpr int CPRW = BN / 8;
       const bool vst = (p.ldcb % 8) == 0 && ((uintptr_t)p.cb & 15) == 0;
+      // BN backward sums (p.bs): this thread's 8 columns are fixed (256 % CPRW == 0); their BN coefficients
+      const bool bsum = p.bs.dstats != nullptr;
+      float bsc[8], bsf[8], bmu[8], brs[8], q1[8], q2[8];
+      if (bsum) {
+        const int cc0 = n0 + (tid % CPRW) * 8;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int cc = min(cc0 + j, p.N - 1);
+          const float mu = p.bs.saved[cc], rs = p.bs.saved[p.N + cc];
+          const float gm = p.bs.gamma ? p.bs.gamma[cc] : 1.f;
+          bsc[j] = gm * rs;
+          bsf[j] = (p.bs.beta ? p.bs.beta[cc] : 0.f) - mu * gm * rs;
+          bmu[j] = mu;
+          brs[j] = rs;
+          q1[j] = q2[j] = 0.f;
+        }
+      }
       for (int c = tid; c < BM * CPRW; c += 256) {
         const int lr = c / CPRW, ch = c - lr * CPRW;
         const int mrow = m0 + lr, col0 = n0 + ch * 8;
@@ -1072,8 +1126,66 @@ __global__ __launch_bounds__(256) void igemm_kernel(IGemmArgs p_) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e]);
           *reinterpret_cast<bf16x8*>(q) = o;
+          if (bsum) {   // (host: vst and N % 8 == 0 whenever p.bs is on)
+            bf16x8 yv, rv = zero8();
+            if constexpr (BPRE) {
+              const int ci = (c - tid) / 256;   // this thread's chunk index (the loop is unrolled by the compiler
+#pragma unroll                                  // only as far as BCH; select the prefetched registers)
+              for (int i = 0; i < BCH; ++i)
+                if (i == ci) {
+                  yv = pyv[i];
+                  rv = prv[i];
+                }
+            } else {
+              const long long eo = row * p.ldcb + col0;
+              yv = *reinterpret_cast<const bf16x8*>(p.bs.y + eo);
+              if (p.bs.res) rv = *reinterpret_cast<const bf16x8*>(p.bs.res + eo);
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float yy = bf2f(yv[e]);
+              const float z = yy * bsc[e] + bsf[e] + bf2f(rv[e]);
+              const float g = (p.bs.relu && !(z > 0.f)) ? 0.f : bf2f(o[e]);   // the stored gradient
+              q1[e] += g;
+              q2[e] += g * ((yy - bmu[e]) * brs[e]);
+            }
+          }
         } else {
           for (int e = 0; e < 8 && col0 + e < p.N; ++e) q[e] = f2bf(v[e] + (p.cb_accum ? bf2f(q[e]) : 0.f));
+        }
+      }
+      if (bsum) {
+        // threads of one column chunk: lanes l, l ^ CPRW, ... of each wave, then the 4 waves through LDS (T is
+        // free after the barrier); one f32 atomic pair per column and workgroup into slot bx % kStatSlots.
+        // (LDS ds_add_f32 into one [2][BN] row instead of the permutes: 8-way contended, the input gradients
+        // 500 -> 612 us per step; profiles/r6_bnsum/)
+#pragma unroll
+        for (int o = CPRW; o < 64; o <<= 1)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            q1[e] += __shfl_xor(q1[e], o, 64);
+            q2[e] += __shfl_xor(q2[e], o, 64);
+          }
+        __syncthreads();
+        float* bred = reinterpret_cast<float*>(smem);   // [4 waves][2][BN]
+        if (lane < CPRW) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            bred[(wave * 2 + 0) * BN + lane * 8 + e] = q1[e];
+            bred[(wave * 2 + 1) * BN + lane * 8 + e] = q2[e];
+          }
+        }
+        __syncthreads();
+        if (tid < BN && n0 + tid < p.N) {
+          float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            a1 += bred[(w * 2 + 0) * BN + tid];
+            a2 += bred[(w * 2 + 1) * BN + tid];
+          }
+          float* ds = p.bs.dstats + (size_t)(bx % kStatSlots) * 2 * p.N;
+          atomicAdd(&ds[n0 + tid], a1);
+          atomicAdd(&ds[p.N + n0 + tid], a2);
         }
       }
       return;
@@ -3262,17 +3374,45 @@ static void splitk_reduce_launch(const float* part, int splits, long long n, flo
   splitk_reduce_kernel<<<(int)g, 256, 0, stream>>>(part, splits, n, dst);
 }
 
+static int igemm_impl(const bf16* a, long long lda, int akind, const bf16* b, long long ldb, int bkind, int M, int N,
+                      int K, const int* geo, int splits, float* cf, long long ldc, int cf_mode, float alpha, bf16* cb,
+                      long long ldcb, int cb_accum, const float* bias, int relu, double* colstats, float* scratch,
+                      const int* phase, const BnSum* bs, hipStream_t stream);
+
 TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, long long ldb, int bkind, int M, int N,
                       int K, const int* geo, int splits, float* cf, long long ldc, int cf_mode, float alpha, bf16* cb,
                       long long ldcb, int cb_accum, const float* bias, int relu, double* colstats, float* scratch,
                       const int* phase, hipStream_t stream) {
+  return igemm_impl(a, lda, akind, b, ldb, bkind, M, N, K, geo, splits, cf, ldc, cf_mode, alpha, cb, ldcb, cb_accum,
+                    bias, relu, colstats, scratch, phase, nullptr, stream);
+}
+
+// Stride-1 conv input gradient dx (=|+=) conv_transpose(dy, W) whose epilogue also takes the backward sums of the
+// BatchNormalization that consumes dx's tensor (BnSum): the LDS-DMA path only (-8 when this shape would run
+// another), never under TDE_DETERMINISTIC (-9: the sums are f32 atomics).
+TDE_API int tde_igemm_dgrad_bnsum(const bf16* dy, const bf16* w, int M, int N, int K, const int* geo, bf16* dx,
+                                  long long ldx, int accum, const BnSum* bs, hipStream_t stream) {
+  if (!bs || !bs->dstats || !bs->y || !bs->saved) return -1;
+  if (g_det) return -9;
+  return igemm_impl(dy, 0, A_DGRAD, w, 0, B_DGRADW, M, N, K, geo, 1, nullptr, 0, 0, 1.f, dx, ldx, accum, nullptr, 0,
+                    nullptr, nullptr, nullptr, bs, stream);
+}
+TDE_API int tde_bnsum_bytes() { return (int)sizeof(BnSum); }
+
+static int igemm_impl(const bf16* a, long long lda, int akind, const bf16* b, long long ldb, int bkind, int M, int N,
+                      int K, const int* geo, int splits, float* cf, long long ldc, int cf_mode, float alpha, bf16* cb,
+                      long long ldcb, int cb_accum, const float* bias, int relu, double* colstats, float* scratch,
+                      const int* phase, const BnSum* bs, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (phase && (akind != A_DGRAD || splits > 1 || colstats)) return -5;
+  if (bs && (akind != A_DGRAD || phase || splits > 1 || !cb || colstats || cf || bias || relu || N % 8 ||
+             ldcb % 8 || ((uintptr_t)cb & 15) || ((uintptr_t)bs->y & 15) || ((uintptr_t)bs->res & 15)))
+    return -8;
   if (g_det && colstats) {
     // statistics of the stored bf16 output in a fixed order, after the GEMM (which runs without them)
     if (!cb || cb_accum || relu) return -7;
-    int rc = tde_igemm(a, lda, akind, b, ldb, bkind, M, N, K, geo, splits, cf, ldc, cf_mode, alpha, cb, ldcb, cb_accum,
-                       bias, relu, nullptr, scratch, phase, stream);
+    int rc = igemm_impl(a, lda, akind, b, ldb, bkind, M, N, K, geo, splits, cf, ldc, cf_mode, alpha, cb, ldcb,
+                        cb_accum, bias, relu, nullptr, scratch, phase, nullptr, stream);
     if (rc) return rc;
     return colstats_det(cb, M, N, ldcb, colstats, stream);
   }
@@ -3282,8 +3422,8 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   if (splits > 1 && fused_epi) {
     // split-K into the zeroed f32 scratch, then the epilogue pass
     if (!scratch || (colstats && N > kMaxCB)) return -2;
-    int rc = tde_igemm(a, lda, akind, b, ldb, bkind, M, N, K, geo, splits, scratch, N, 2, 1.f, nullptr, 0, 0,
-                       nullptr, 0, nullptr, nullptr, nullptr, stream);
+    int rc = igemm_impl(a, lda, akind, b, ldb, bkind, M, N, K, geo, splits, scratch, N, 2, 1.f, nullptr, 0, 0,
+                        nullptr, 0, nullptr, nullptr, nullptr, nullptr, stream);
     if (rc) return rc;
     const long long n = (long long)M * N;
     int g = (int)((n + 255) / 256);
@@ -3496,6 +3636,10 @@ TDE_API int tde_igemm(const bf16* a, long long lda, int akind, const bf16* b, lo
   // big tiles (256 x 64 with 64 x 64 per wave, or 256 x 128 with 128 x 64 per wave): fwd/dense when
   // tuned on (fwd 641 -> 840 us on ResNet-18 with them), dgrad when g_big_dgrad
   const bool big = (g_big || (g_big_dgrad && akind == A_DGRAD)) && KB == 64 && splits == 1 && !rowk && big_shape;
+  if (bs) {
+    if (!(vec && g_glds && ut && !big)) return -8;   // the BN sums live in the LDS-DMA kernels' LDS epilogue
+    p.bs = *bs;
+  }
 #define TDE_IGEMM(AK_, BK__, BM_, BN_)                                                   \
   do {                                                                                   \
     if (vec) {                                                                           \
@@ -3613,9 +3757,9 @@ static int bn_stream_blocks(long long n) {
   return bn_grid_blocks(n, g);
 }
 static int bn_reduce_blocks(long long n) {
-  // round 6: 16384 / 512 / 2048 (was 32768 / 256 / 1024): ResNet-18 23,040 -> 23,111 img/s, two A/B rounds
-  // (profiles/r6_splitk/bn_red.log)
-  static const BnGrid g = bn_grid_env("TDE_BN_RED", BnGrid{16384, 512, 2048});
+  // (round 6 A/B of 16384 / 512 / 2048: +0.3 % end to end within noise, but the kernel statistics show every
+  // reduction slower — stage 1 17.5 -> 20 us; profiles/r6_bnsum/: kept 32768 / 256 / 1024)
+  static const BnGrid g = bn_grid_env("TDE_BN_RED", BnGrid{32768, 256, 1024});
   return bn_grid_blocks(n, g);
 }
 
@@ -3641,11 +3785,21 @@ TDE_API int tde_bn_bwd(const bf16* dout, const bf16* y, const bf16* res, long lo
                        const float* saved, const float* gamma, const float* beta, int relu, float drop_rate,
                        unsigned long long seed, const long long* iter, int iter_offset, int layer_id, float* dstats,
                        bf16* dx, int dx_accum, bf16* dres, int dres_accum, float* dgamma, float* dbeta,
-                       double* zero_fwd, hipStream_t stream) {
+                       double* zero_fwd, int sums_ready, hipStream_t stream) {
   if (C > kMaxCB) return -1;
   BnBwdArgs a{dout, y, res, R, C, mode, saved, gamma, beta, relu, Drop{drop_rate, seed, iter, iter_offset, layer_id},
               dstats, dx, dx_accum, dres, dres_accum, dgamma, dbeta, zero_fwd};
   if (R * C >= (1LL << 31)) return -4;
+  if (sums_ready && mode == 1) {
+    // dstats already hold this BN's backward sums (taken by the epilogue of the input-gradient GEMM that wrote
+    // dout last, tde_igemm_dgrad_bnsum): the apply pass only
+    if (bn_tiled_ok(C, {dout, y, res, dx, dres}))
+      bn_bwd_apply_tiled_kernel<<<bn_tiled_grid(R, C, bn_stream_blocks(R * C)), 256, 0, stream>>>(a);
+    else
+      bn_bwd_apply_kernel<<<grid_for(R * C, 8), 256, 0, stream>>>(a);
+    TDE_LAUNCH_CHECK();
+    return 0;
+  }
   if (g_det && mode == 1) {
     // fixed-order backward sums into the kStatSlots slots, then the apply pass reads them (it sums slots in order)
     bn_bwd_reduce_det_kernel<<<dim3((C + 63) / 64, kStatSlots), 256, 0, stream>>>(a);

@@ -73,7 +73,9 @@ _HIP_PROTOS = {
     "tde_bn_fwd": (i32, [p, p, p, i64, i32, i32, p, p, p, p, f32, p, p, f32, f32, p, i32, f32, C.c_ulonglong,
                          p, i32, i32, p]),
     "tde_bn_bwd": (i32, [p, p, p, i64, i32, i32, p, p, p, i32, f32, C.c_ulonglong, p, i32, i32, p, p, i32, p,
-                         i32, p, p, p, p]),
+                         i32, p, p, p, i32, p]),
+    "tde_igemm_dgrad_bnsum": (i32, [p, p, i32, i32, i32, p, p, i64, i32, p, p]),
+    "tde_bnsum_bytes": (i32, []),
     "tde_act_bwd": (i32, [p, p, i64, i32, i32, p, p, p]),
     "tde_maxpool": (i32, [p, p, p, p, p, i32, p, i32, p]),
     "tde_bn_relu_maxpool_fwd": (i32, [p, i64, i32, i32, p, p, p, p, f32, p, p, f32, f32, p, p, p, p, p]),

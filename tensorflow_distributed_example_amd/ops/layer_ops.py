@@ -209,11 +209,43 @@ def halo_wgrad(x, dy, dW, g: ConvGeom, scratch):
             "tde_halo_wgrad3x3")
 
 
-def conv_dgrad(dy, Wrow, dx, g: ConvGeom, accum=False, scratch=None):
-    """dx[B,H,W,C] (=|+=) conv_transpose(dy[B,Ho,Wo,Co], W); Wrow = HWIO bf16."""
+class BnSum(C.Structure):
+    """csrc/kernels/layers.hip BnSum: the backward sums of the BatchNormalization that consumes an input gradient."""
+    _fields_ = [("y", C.c_void_p), ("res", C.c_void_p), ("saved", C.c_void_p), ("gamma", C.c_void_p),
+                ("beta", C.c_void_p), ("relu", C.c_int), ("dstats", C.c_void_p)]
+
+
+def dgrad_bnsum_ok(g: ConvGeom):
+    """Input gradients whose epilogue can take the consumer BN's backward sums (tde_igemm_dgrad_bnsum): stride 1,
+    the LDS-DMA implicit GEMM (C % 8 == 0, Co a multiple of the K step), unsplit; never in deterministic mode."""
+    if N.hip().tde_layers_is_deterministic():
+        return False
+    kb = 64 if g.Co % 64 == 0 else 32
+    M, K = g.B * g.H * g.W, g.KH * g.KW * g.Co
+    return (g.sh == 1 and g.sw == 1 and g.C % 8 == 0 and g.Co % 8 == 0 and g.Co % kb == 0
+            and fwd_splits(M, g.C, K) == 1 and N.hip().tde_bnsum_bytes() == C.sizeof(BnSum))
+
+
+def conv_dgrad(dy, Wrow, dx, g: ConvGeom, accum=False, scratch=None, bnsum=None):
+    """dx[B,H,W,C] (=|+=) conv_transpose(dy[B,Ho,Wo,Co], W); Wrow = HWIO bf16.  bnsum (dict y, res, saved, gamma,
+    beta, relu, dstats): the BN consuming dx's tensor takes its backward sums in this launch's epilogue."""
     _bf(dy, g.B * g.Ho * g.Wo * g.Co, "conv_dgrad dy")
     _bf(Wrow, g.K * g.Co, "conv_dgrad W")
     _bf(dx, g.B * g.H * g.W * g.C, "conv_dgrad dx")
+    if bnsum is not None:
+        n = g.B * g.H * g.W * g.C
+        _bf(bnsum["y"], n, "conv_dgrad bnsum y")
+        if bnsum.get("res") is not None:
+            _bf(bnsum["res"], n, "conv_dgrad bnsum res")
+        _f32(bnsum["saved"], 2 * g.C, "conv_dgrad bnsum saved")
+        _f32(bnsum["dstats"], 2 * STAT_SLOTS * g.C, "conv_dgrad bnsum dstats")
+        _req(dgrad_bnsum_ok(g), "conv_dgrad: bnsum on a shape without the fused epilogue")
+        s = BnSum(_P(bnsum["y"]), _P(bnsum.get("res")), _P(bnsum["saved"]), _P(bnsum.get("gamma")),
+                  _P(bnsum.get("beta")), int(bool(bnsum.get("relu"))), _P(bnsum["dstats"]))
+        M, K = g.B * g.H * g.W, g.KH * g.KW * g.Co
+        N.check(N.hip().tde_igemm_dgrad_bnsum(_P(dy), _P(Wrow), M, g.C, K, g.carray(), _P(dx), g.C, int(accum),
+                                              C.byref(s), _s()), "tde_igemm_dgrad_bnsum")
+        return
     if g.sh > 1 or g.sw > 1:
         phases = dgrad_phases(g)
         untapped = [ph for ph in phases if ph[6] * ph[7] == 0]
@@ -445,7 +477,8 @@ def bn_fwd(y, out, R, Cc, *, mode, stats=None, saved=None, gamma=None, beta=None
 
 def bn_bwd(dout, y, R, Cc, *, mode, saved=None, gamma=None, beta=None, res=None, relu=False,
            drop: DropSpec = _NODROP, iter_offset=-1, dstats=None, dx=None, dx_accum=False, dres=None,
-           dres_accum=False, dgamma=None, dbeta=None, zero_fwd=None):
+           dres_accum=False, dgamma=None, dbeta=None, zero_fwd=None, sums_ready=False):
+    """sums_ready: ``dstats`` already holds the backward sums (taken by ``conv_dgrad(..., bnsum=)``): apply pass only."""
     n = R * Cc
     _bf(dout, n, "bn_bwd dout")
     _bf(y, n, "bn_bwd y")
@@ -464,7 +497,7 @@ def bn_bwd(dout, y, R, Cc, *, mode, saved=None, gamma=None, beta=None, res=None,
     rc = N.hip().tde_bn_bwd(_P(dout), _P(y), _P(res), int(R), int(Cc), int(mode), _P(saved), _P(gamma), _P(beta),
                             int(relu), float(drop.rate), int(drop.seed) & (2 ** 64 - 1), _P(drop.iterations),
                             int(iter_offset), int(drop.layer_id), _P(dstats), _P(dx), int(dx_accum), _P(dres),
-                            int(dres_accum), _P(dgamma), _P(dbeta), _P(zero_fwd), _s())
+                            int(dres_accum), _P(dgamma), _P(dbeta), _P(zero_fwd), int(bool(sums_ready)), _s())
     N.check(rc, "tde_bn_bwd")
 
 

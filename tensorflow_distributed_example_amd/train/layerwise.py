@@ -318,6 +318,24 @@ class LayerwisePlan(PG.ReplicaPlan):
                 r = t.root()
                 st.accum[r.id] = r.id in written
                 written.add(r.id)
+        # TDE_BN_SUM_FUSE=1: BatchNormalization backward sums in the epilogue of the stride-1 input-gradient GEMM that
+        # writes the BN output's gradient LAST (after every other consumer's contribution landed): that BN's
+        # backward then runs its apply pass only — the bn_bwd_reduce pass over dout / y / res disappears
+        # (csrc/kernels/layers.hip BnSum).  Off by default: on ResNet-18 the 9 eligible input gradients grow by
+        # what the 9 reduction passes cost (reductions 231 -> 137 us, input gradients 414 -> 500 us per step;
+        # 22,965 vs 22,948 img/s, profiles/r6_bnsum/)
+        if not self.f32 and not self.det and os.environ.get("TDE_BN_SUM_FUSE", "0") == "1":
+            for st in stages:
+                if not (isinstance(st, _Elementwise) and st.bn and st.pool is None and st.drop.rate == 0):
+                    continue
+                T = st.out.root()
+                writers = [w for w in reversed(stages) if any(t.root() is T for t in w.grad_inputs())]
+                last = writers[-1] if writers else None
+                if (isinstance(last, _Gemm) and last.conv and last.need_dgrad and last.inp.root() is T
+                        and not (last.small_dgrad or last.halo or last.use_im2col or last.use_stem_pack)
+                        and O.dgrad_bnsum_ok(last.geo)):
+                    last.bnsum_of = st
+                    st.sums_fused = True
 
     def _alloc(self):
         B, dev = self.B, self.device
@@ -498,6 +516,7 @@ class _Gemm(_Stage):
         self.colstats = None
         self.dz = None
         self.act_done = False   # the consumer's launch already applied the ReLU mask / bias gradient
+        self.bnsum_of = None    # _Elementwise BN whose backward sums this layer's input-gradient epilogue takes
 
     def wpart_need(self, B):
         """f32 split-K partials of this layer's GEMMs (weight gradient, forward, input gradient)."""
@@ -633,8 +652,13 @@ class _Gemm(_Stage):
             elif self.halo:
                 O.halo_conv(dout, self.Wrow, self.inp.root().grad, g, dgrad=True, accum=self.accum[self.inp.root().id])
             else:
+                bs = None
+                if self.bnsum_of is not None:
+                    b = self.bnsum_of
+                    bs = dict(y=b.inp.root().buf, res=b.res.root().buf if b.res is not None else None, saved=b.saved,
+                              gamma=b.gamma, beta=b.beta, relu=b.relu, dstats=b.dstats)
                 O.conv_dgrad(dout, self.Wrow, self.inp.root().grad, g, accum=self.accum[self.inp.root().id],
-                             scratch=p.scratch)
+                             scratch=p.scratch, bnsum=bs)
         else:
             O.dense_dgrad(dout, self.Wrow, self.inp.root().grad, self.inp.rows(B),
                           accum=self.accum[self.inp.root().id], scratch=p.scratch)
@@ -687,6 +711,7 @@ class _Elementwise(_Stage):
         self.defer_to = None
         self.stats_from_gemm = False
         self.pool = None  # _MaxPool whose forward this BN+ReLU stage runs in the same pass
+        self.sums_fused = False  # backward sums taken by the input-gradient GEMM that writes dout last
         if isinstance(layer, L.Dropout):
             self.set_dropout(layer)
         st = plan.store
@@ -794,7 +819,8 @@ class _Elementwise(_Stage):
                  dx=dx, dx_accum=self.accum.get(ir.id, False), dres=dres,
                  dres_accum=self.accum.get(rr.id, False) if rr is not None else False,
                  dgamma=self.ggamma if self.bn else None, dbeta=self.gbeta if self.bn else None,
-                 zero_fwd=self._stats() if self.bn else None)
+                 zero_fwd=self._stats() if self.bn else None,
+                 **({"sums_ready": True} if self.bn and self.sums_fused else {}))
 
 
 class _MaxPool(_Stage):

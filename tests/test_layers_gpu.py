@@ -997,3 +997,73 @@ def test_wgrad_many_split_scratch_reduction():
     r = subprocess.run([sys.executable, "-c", code], env=env, cwd=os.path.dirname(here), capture_output=True,
                        text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("B,H,W,C,Co,res,accum", [(4, 12, 12, 128, 128, True, False), (2, 9, 11, 64, 256, False, True),
+                                                     (3, 14, 14, 256, 64, True, True)])
+def test_conv_dgrad_bn_sums_match_the_reduction_pass(B, H, W, C, Co, res, accum):
+    """tde_igemm_dgrad_bnsum: the consumer BN's backward sums (sum g, sum g * xhat; g masked by the BN's ReLU over
+    y + residual) taken in the input-gradient epilogue equal those of the separate reduction pass over the stored
+    gradient, and the apply pass that reads them gives the same BN input gradient; the GEMM output itself is
+    unchanged (bitwise), also when it accumulates into an existing gradient."""
+    from tensorflow_distributed_example_amd.ops import layer_ops as O
+    g = O.ConvGeom(B, H, W, C, H, W, Co, 3, 3, 1, 1, 1, 1)
+    assert O.dgrad_bnsum_ok(g)
+    n = B * H * W * C
+    dy = _r(B, H, W, Co, seed=21)
+    w = _r(3, 3, C, Co, seed=22, scale=0.05).contiguous()
+    y = _r(B, H, W, C, seed=23)
+    rs_ = _r(B, H, W, C, seed=24) if res else None
+    gen = torch.Generator(device="cpu").manual_seed(25)
+    saved = torch.cat([torch.randn(C, generator=gen) * 0.1, torch.rand(C, generator=gen) + 0.5]).to(DEV)
+    gamma = (torch.rand(C, generator=gen) + 0.5).to(DEV)
+    beta = (torch.randn(C, generator=gen) * 0.1).to(DEV)
+    base = _r(B, H, W, C, seed=26).reshape(-1)
+    outs = []
+    for fused in (False, True):
+        dx = base.clone() if accum else torch.zeros(n, dtype=bf, device=DEV)
+        ds = torch.zeros(2 * O.STAT_SLOTS * C, device=DEV)
+        bn = dict(y=y.reshape(-1), res=rs_.reshape(-1) if res else None, saved=saved, gamma=gamma, beta=beta,
+                  relu=True, dstats=ds)
+        O.conv_dgrad(dy.reshape(-1), w, dx, g, accum=accum, bnsum=bn if fused else None)
+        dxb = torch.zeros(n, dtype=bf, device=DEV)
+        O.bn_bwd(dx, y.reshape(-1), B * H * W, C, mode=1, saved=saved, gamma=gamma, beta=beta,
+                 res=rs_.reshape(-1) if res else None, relu=True, dstats=ds, dx=dxb, sums_ready=fused)
+        torch.cuda.synchronize()
+        outs.append((dx.clone(), ds.view(O.STAT_SLOTS, 2, C).sum(0).double(), dxb.clone()))
+    (dxa, sa, ba), (dxf, sf, bf_) = outs
+    assert torch.equal(dxa, dxf)
+    for q in range(2):
+        assert (sa[q] - sf[q]).abs().max().item() <= 1e-4 * sa[q].abs().max().item() + 1e-4, q
+    assert _rel(bf_.float(), ba.float()) < 1e-2
+
+
+def test_resnet_bn_sums_in_dgrad_epilogue_match_bf16_oracle(monkeypatch):
+    """BatchNormalization backward sums taken by the epilogue of the stride-1 input-gradient GEMM that writes the
+    BN output's gradient last (csrc/kernels/layers.hip BnSum; those BNs run their apply pass only): a ResNet whose
+    stages (96 / 128 filters) take the LDS-DMA input gradient — the float64 bf16-emulating oracle, and the same
+    step with the separate reduction pass (TDE_BN_SUM_FUSE=0, the default)."""
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.train import layerwise as LW
+
+    def build():
+        tde.backend.set_random_seed(4)
+        m = tde.zoo.resnet((1, 1), (96, 128), input_shape=(32, 32, 3), classes=10, name="bnsum_resnet")
+        m.compile(loss=tde.losses.SparseCategoricalCrossentropy(from_logits=True), optimizer=tde.optimizers.SGD(0.01))
+        m.build()
+        return m
+
+    monkeypatch.setenv("TDE_BN_SUM_FUSE", "1")
+    rng = np.random.default_rng(5)
+    x, y = rng.standard_normal((16, 32, 32, 3), dtype=np.float32), rng.integers(0, 10, 16)
+    # (BN backward at 8x8 / 4x4 spatial sizes amplifies 1-ulp bf16 rounding flips ~3x per block going backwards,
+    # as in the mini-ResNet test; a wiring error is O(1)): both plans within 0.12 of the oracle, and the fused
+    # plan no further from it than the separate-pass plan plus that noise
+    m = build()
+    plan = _emulated_compare(m, x, y, 16, 0.12)
+    fused = [st.layer.name for st in plan.stages if isinstance(st, LW._Elementwise) and st.sums_fused]
+    assert len(fused) >= 2, fused
+    monkeypatch.setenv("TDE_BN_SUM_FUSE", "0")
+    m2 = build()
+    plan2 = _emulated_compare(m2, x, y, 16, 0.12)
+    assert not any(getattr(st, "sums_fused", False) for st in plan2.stages)
