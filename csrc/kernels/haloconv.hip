@@ -557,6 +557,113 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// Weight gradient of the packed RGB stem (layers.hip tde_stem_pack: the 7x7 stride-2 conv on 3 channels as a
+// virtual conv over [B][Hp][Wv][8] — two real pixels x 4 channels per virtual pixel — with KWv = 4 taps along W at
+// stride 1): dWv[kh][kwv][c][co] = sum over output pixels (oh, ow) of xp[oh*sh + kh][ow + kwv][c] * dY[oh][ow][co].
+// The implicit GEMM (K = 802,816 pixels at batch 64) runs this at ~81 us; here, as in wgrad3x3_kernel, each
+// workgroup walks tiles of TR output rows with the tile's KH + (TR-1) sh input rows and TR dY rows in LDS (LDS-DMA,
+// double-buffered), every byte loaded once for all taps.  For one kh the 32 (kwv, c) rows of the A operand at
+// pixel ow are the 64 contiguous bytes from virtual pixel ow: a 16-row fragment (kwv pair a) of 8 consecutive
+// pixels is a transposed read of 4 overlapping 32-byte windows 16 bytes apart (each lane supplies its address).
+// M = KH x 32 rows in 2 KH blocks of 16, dealt round-robin over the 4 waves; N = 64.
+constexpr int kSxRow = 2048;   // LDS bytes per staged input row (<= 128 virtual pixels)
+
+__device__ __forceinline__ bf16x8 sx_frag(const char* row, int pix0, int a, int lane) {
+  const int i = lane & 15, q = i >> 2, pp = i & 3;
+  const wv4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_wv4*)(row + (pix0 + q + 2 * a) * 16 + pp * 8));
+  const wv4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_wv4*)(row + (pix0 + 4 + q + 2 * a) * 16 + pp * 8));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+struct StemWgArgs {
+  const bf16* xp;   // [B][Hp][Wv][8]
+  const bf16* dy;   // [B][Ho][Wo][64]
+  float* part;      // [gridDim][KH * 32][64]
+  int B, Hp, Wv, Ho, Wo, KH, sh;
+  int x_bytes, dy_bytes;
+};
+
+template <int TR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void stem_wgrad_kernel(StemWgArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char ssm[];
+  const int Wo = a.Wo, KH = a.KH, sh = a.sh;
+  const int NXR = (TR - 1) * sh + KH;      // input rows of one tile
+  const int XB = NXR * kSxRow, DB = TR * Wo * kWgPix;
+  char* const xb = reinterpret_cast<char*>(ssm);   // [2][NXR][kSxRow]
+  char* const db = xb + 2 * XB;                     // [2][TR * Wo][128]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tpi = a.Ho / TR, ntiles = a.B * tpi;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int t0 = (int)((long long)g * ntiles / G), t1 = (int)((long long)(g + 1) * ntiles / G);
+  const int NB = 2 * KH;                   // 16-row M blocks: b = 2 kh + a
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[j][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (t0 < t1) {
+    const Rsrc rx = make_rsrc(a.xp, a.x_bytes), rd = make_rsrc(a.dy, a.dy_bytes);
+    const int xi = (a.Wv + 63) / 64;       // one-KiB instructions per input row
+    auto issue = [&](int t, int buf) {
+      const int b = t / tpi, oh0 = TR * (t - b * tpi);
+      for (int j = wave; j < NXR * xi; j += 4) {
+        const int r = j / xi, jj = j - r * xi;
+        const int p = jj * 64 + lane;
+        // pixels past the row read the next row's bytes (never used); the range check zeroes the tensor's end
+        dma16(rx, xb + buf * XB + r * kSxRow + jj * 1024, ((b * a.Hp + oh0 * sh + r) * a.Wv + p) * 16);
+      }
+      const int per_row = Wo >> 3;
+      for (int j = wave; j < TR * per_row; j += 4) {
+        const int c = j * 8 + (lane >> 3);
+        const int lc = (lane & 7) ^ wsw(c);
+        dma16(rd, db + buf * DB + j * 1024, ((b * a.Ho + oh0) * Wo + c) * kWgPix + (lc << 4));
+      }
+    };
+    issue(t0, 0);
+    for (int t = t0; t < t1; ++t) {
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_s_barrier();
+      const int buf = (t - t0) & 1;
+      if (t + 1 < t1) issue(t + 1, buf ^ 1);
+      const char* xt = xb + buf * XB;
+      const char* dt = db + buf * DB;
+      for (int k = 0; k < TR * Wo / 32; ++k) {
+        const int p0 = 32 * k + 8 * (lane >> 4);
+        const int tr = p0 / Wo, ow0 = p0 - tr * Wo;
+        bf16x8 bfr[4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) bfr[n] = wg_frag(dt, 32 * k, 16 * n, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int b = wave + 4 * j;
+          if (b < NB) {   // wave-uniform
+            const int kh = b >> 1, ap = b & 1;
+            const bf16x8 af = sx_frag(xt + (tr * sh + kh) * kSxRow, ow0, ap, lane);
+#pragma unroll
+            for (int n = 0; n < 4; ++n) acc[j][n] = mfma16(af, bfr[n], acc[j][n]);
+          }
+        }
+      }
+    }
+  }
+  // partial: block b rows b * 16 + 4 (lane >> 4) + r, column 16 n + (lane & 15) (dWv's flat [kh][kwv][c][co] order)
+  float* dst = a.part + (size_t)g * NB * 16 * 64;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int b = (int)(tid >> 6) + 4 * j;
+    if (b >= NB) continue;
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        dst[(b * 16 + 4 * (lane >> 4) + r) * 64 + 16 * n + (lane & 15)] = acc[j][n][r];
+  }
+}
+
 // dst[i] += sum over s < splits of part[s][i] (n % 4 == 0): block = 64 consecutive elements (16 float4 columns) x 16
 // split groups (group j sums splits j, j + 16, ... in order), the groups summed in a fixed order through LDS —
 // every thread keeps its loads in flight (the generic split-K reduction walks all splits serially per thread:
@@ -761,6 +868,54 @@ TDE_API int tde_halo_wgrad3x3(const bf16* x, const bf16* dy, float* dW, float* p
   TDE_LAUNCH_CHECK();
   const long long n = 9LL * 64 * 64;
   halo::part_reduce_kernel<<<(int)((n / 4 + 15) / 16), 256, 0, stream>>>(part, grid, n, dW);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---- packed-stem weight gradient (stem_wgrad_kernel)
+constexpr int kStemTR = 2;
+static int stem_wg_lds(int KH, int sh, int Wo) {
+  return 2 * ((kStemTR - 1) * sh + KH) * halo::kSxRow + 2 * kStemTR * Wo * halo::kWgPix;
+}
+// the virtual geometry (C = 8, KWv = 4 taps, stride (sh, 1), valid) with 64 output channels
+TDE_API int tde_stem_wgrad_ok(int B, int Hp, int Wv, int Ho, int Wo, int KH, int KWv, int sh, int C, int Co) {
+  if (C != 8 || Co != 64 || KWv != 4 || KH < 1 || KH > 8 || sh < 1) return 0;
+  if (Wo % 8 || (kStemTR * Wo) % 32 || Ho % kStemTR || Wv != Wo + 3 || Wv > 128 || Hp < (Ho - 1) * sh + KH) return 0;
+  if ((long long)B * Hp * Wv * 16 >= (1LL << 31) || (long long)B * Ho * Wo * 128 >= (1LL << 31)) return 0;
+  return stem_wg_lds(KH, sh, Wo) <= 160 * 1024;
+}
+TDE_API long long tde_stem_wgrad_scratch_elems(int B, int Ho, int KH) {
+  int dev = 0, cus = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int ntiles = B * (Ho / kStemTR);
+  const int grid = cus < ntiles ? cus : ntiles;
+  return (long long)grid * 2 * KH * 16 * 64;
+}
+// dWv[KH][4][8][64] (f32) += the packed stem's weight gradient; part: tde_stem_wgrad_scratch_elems floats
+TDE_API int tde_stem_wgrad(const bf16* xp, const bf16* dy, float* dWv, float* part, long long part_elems, int B, int Hp,
+                           int Wv, int Ho, int Wo, int KH, int sh, hipStream_t stream) {
+  if (!tde_stem_wgrad_ok(B, Hp, Wv, Ho, Wo, KH, 4, sh, 8, 64)) return -2;
+  if (((uintptr_t)xp & 15) || ((uintptr_t)dy & 15) || ((uintptr_t)dWv & 15) || ((uintptr_t)part & 15)) return -3;
+  int dev = 0, cus = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int ntiles = B * (Ho / kStemTR);
+  const int grid = cus < ntiles ? cus : ntiles;
+  const long long n = 2LL * KH * 16 * 64;
+  if (part_elems < (long long)grid * n) return -5;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)halo::stem_wgrad_kernel<kStemTR>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024) != hipSuccess)
+      return -4;
+    attr = true;
+  }
+  halo::StemWgArgs a{xp, dy, part, B, Hp, Wv, Ho, Wo, KH, sh, (int)((long long)B * Hp * Wv * 16),
+                     (int)((long long)B * Ho * Wo * 128)};
+  hipLaunchKernelGGL(halo::stem_wgrad_kernel<kStemTR>, dim3(grid), dim3(256), stem_wg_lds(KH, sh, Wo), stream, a);
+  TDE_LAUNCH_CHECK();
+  halo::part_reduce_kernel<<<(int)((n / 4 + 15) / 16), 256, 0, stream>>>(part, grid, n, dWv);
   TDE_LAUNCH_CHECK();
   return 0;
 }

@@ -313,6 +313,30 @@ def stem_pack(x, g: ConvGeom, xp, Wt=None, Wv=None):
     N.check(N.hip().tde_stem_pack(_P(x), g.carray(), _P(xp), _P(Wt), _P(Wv), _s()), "tde_stem_pack")
 
 
+def stem_wgrad_ok(gv: ConvGeom):
+    """The packed stem's weight gradient on the tile kernel (csrc/kernels/haloconv.hip stem_wgrad_kernel): the virtual
+    geometry of ``stem_geometry`` with 4 taps along W, 8 channels, 64 filters.  TDE_STEM_WGRAD=0 disables it."""
+    if os.environ.get("TDE_STEM_WGRAD", "1") == "0":
+        return False
+    return bool(N.hip().tde_stem_wgrad_ok(gv.B, gv.H, gv.W, gv.Ho, gv.Wo, gv.KH, gv.KW, gv.sh, gv.C, gv.Co))
+
+
+def stem_wgrad_scratch_elems(gv: ConvGeom):
+    return int(N.hip().tde_stem_wgrad_scratch_elems(gv.B, gv.Ho, gv.KH))
+
+
+def stem_wgrad(xp, dy, gWv, gv: ConvGeom, scratch):
+    """gWv[KH][4][8][64] (f32) += the packed stem's weight gradient (xp: the packed input, dy: the stem output's
+    gradient); per-workgroup partials in ``scratch`` reduced in a fixed order."""
+    _bf(xp, gv.B * gv.H * gv.W * 8, "stem_wgrad xp")
+    _bf(dy, gv.B * gv.Ho * gv.Wo * gv.Co, "stem_wgrad dy")
+    _f32(gWv, gv.K * gv.Co, "stem_wgrad gWv")
+    _req(stem_wgrad_ok(gv), "stem_wgrad: geometry not covered")
+    _f32(scratch, stem_wgrad_scratch_elems(gv), "stem_wgrad scratch")
+    N.check(N.hip().tde_stem_wgrad(_P(xp), _P(dy), _P(gWv), _P(scratch), int(scratch.numel()), gv.B, gv.H, gv.W,
+                                   gv.Ho, gv.Wo, gv.KH, gv.sh, _s()), "tde_stem_wgrad")
+
+
 def stem_unpack_wgrad(gWv, g: ConvGeom, gW):
     gv = stem_geometry(g)
     _f32(gWv, gv.K * g.Co, "stem_unpack gWv")

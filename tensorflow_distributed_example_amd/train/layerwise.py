@@ -554,6 +554,8 @@ class _Gemm(_Stage):
                 return 0
             if self.use_stem_pack:
                 gv = O.stem_geometry(g)
+                if O.stem_wgrad_ok(gv):
+                    return O.stem_wgrad_scratch_elems(gv)
                 return O.wgrad_scratch_elems(gv.K, gv.Co, gv.B * gv.Ho * gv.Wo)
             return O.wgrad_scratch_elems(g.K, g.Co, g.B * g.Ho * g.Wo)
         return O.wgrad_scratch_elems(self.W.shape[0], self.W.shape[1], self.inp.rows(B))
@@ -675,7 +677,11 @@ class _Gemm(_Stage):
         if self.conv:
             g = self.geo.with_batch(B)
             if self.use_stem_pack:
-                O.conv_wgrad(self.xp, dout, self.gWv, O.stem_geometry(g), scratch=p.wscratch)
+                gv = O.stem_geometry(g)
+                if O.stem_wgrad_ok(gv):   # the tile kernel: every packed-input and dY byte loaded once
+                    O.stem_wgrad(self.xp, dout, self.gWv, gv, p.wscratch)
+                else:
+                    O.conv_wgrad(self.xp, dout, self.gWv, gv, scratch=p.wscratch)
                 O.stem_unpack_wgrad(self.gWv, g, self.gW)
             elif self.halo_wg:
                 O.halo_wgrad(self.inp.buf, dout, self.gW, g, p.wscratch)

@@ -113,3 +113,33 @@ def test_halo_wgrad_rejects_other_geometries():
     assert not O.halo_wgrad_ok(O.ConvGeom(2, 56, 56, 64, 28, 28, 64, 3, 3, 2, 2, 0, 0))
     assert N.hip().tde_halo_wgrad_ok(64, 64, 56, 60, 2) == 0   # W % 8
     assert N.hip().tde_halo_wgrad_ok(64, 64, 7, 8, 2) == 0     # H has no 2- or 4-row tiling
+
+
+@pytest.mark.parametrize("B,H", [(2, 224), (3, 32), (1, 64)])
+def test_stem_weight_gradient(B, H):
+    """The packed RGB stem's weight gradient on the tile kernel (haloconv.hip stem_wgrad_kernel) — the 7x7 stride-2
+    SAME conv on 3 channels as layers.hip's virtual conv over 8-channel pixel pairs — unpacked into the real HWIO
+    gradient, vs float64 autograd of the real conv, accumulated onto an existing gradient."""
+    Ho = H // 2
+    pt = ((Ho - 1) * 2 + 7 - H) // 2            # TF SAME: (2, 3) at 224 / 64 / 32
+    g = O.ConvGeom(B, H, H, 3, Ho, Ho, 64, 7, 7, 2, 2, pt, pt)
+    gv = O.stem_geometry(g)
+    assert O.stem_pack_ok(g) and O.stem_wgrad_ok(gv)
+    x = _r(B, H, H, 3, seed=31)
+    dy = _r(B, g.Ho, g.Wo, 64, seed=32)
+    xp = torch.zeros(gv.B * gv.H * gv.W * 8, dtype=bf, device=DEV)
+    O.stem_pack(x.to(DEV).reshape(-1), g, xp)
+    gWv = torch.zeros(gv.K * 64, device=DEV)
+    scr = torch.full((O.stem_wgrad_scratch_elems(gv),), float("nan"), device=DEV)
+    O.stem_wgrad(xp, dy.to(DEV).reshape(-1), gWv, gv, scr)
+    base = torch.randn(7, 7, 3, 64, generator=torch.Generator().manual_seed(33))
+    gW = base.clone().to(DEV).reshape(-1)
+    O.stem_unpack_wgrad(gWv, g, gW)
+    torch.cuda.synchronize()
+    pb = (g.Ho - 1) * 2 + 7 - H - pt
+    wd = torch.zeros(64, 3, 7, 7, dtype=torch.float64, requires_grad=True)
+    yd = F.conv2d(F.pad(x.double().permute(0, 3, 1, 2), (pt, pb, pt, pb)), wd, stride=2)
+    yd.backward(dy.double().permute(0, 3, 1, 2))
+    ref = wd.grad.permute(2, 3, 1, 0)
+    assert _rel(gW.cpu().view(7, 7, 3, 64) - base, ref) < 1e-5
+    assert float(gWv.abs().max()) == 0.0   # the unpack pass consumed (zeroed) the virtual gradient
