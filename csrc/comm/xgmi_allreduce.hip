@@ -53,12 +53,21 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
+
 #include "tde_optim.h"
 #include "tde_xgmi.h"
 
 namespace tde {
 
+// Workgroup size: 256 threads, or 1024 ("wide") when the whole grid fits one workgroup per CU and no other
+// process shares the GPU (tde_xgmi_set_wide).  Every phase is a few dependent memory round trips per loop
+// iteration, so a call's time follows the per-thread iteration count: the 2-replica rehearsal ran 82 / 70 /
+// 63 / 60.5 us per step at 16 / 32 / 64 / 128 chunks of 256 threads (profiles/r6_xg_wide/).  A 1024-thread
+// workgroup holds 4 waves x its VGPRs on every SIMD, so two never share a CU and a co-located process's
+// spinning grid could starve it: wide launches are only made when neither can happen.
 constexpr int kXgThreads = 256;
+constexpr int kXgWideThreads = 1024;
 
 struct XgArgs {
   float* grad;                    // local gradient bucket (in/out), M floats
@@ -203,10 +212,10 @@ __device__ __forceinline__ void copy_chunk(float* dst, const float* src, long lo
   if (vec) {
     const long long nv = n >> 2;
     float4* d4 = reinterpret_cast<float4*>(dst);
-    for (long long i = tid; i < nv; i += kXgThreads) d4[i] = wld4<NT>(src, i);
-    for (long long i = (nv << 2) + tid; i < n; i += kXgThreads) dst[i] = wld<NT>(src, i);
+    for (long long i = tid; i < nv; i += (int)blockDim.x) d4[i] = wld4<NT>(src, i);
+    for (long long i = (nv << 2) + tid; i < n; i += (int)blockDim.x) dst[i] = wld<NT>(src, i);
   } else {
-    for (long long i = tid; i < n; i += kXgThreads) dst[i] = wld<NT>(src, i);
+    for (long long i = tid; i < n; i += (int)blockDim.x) dst[i] = wld<NT>(src, i);
   }
 }
 
@@ -227,7 +236,7 @@ __device__ __forceinline__ void apply_chunk(const XgArgs& a, float lr_t, long lo
   long long nv = 0;
   if ((g0 & 3) == 0) {   // area offsets are multiples of 4 elements
     nv = n >> 2;
-    for (long long i = tid; i < nv; i += kXgThreads) {
+    for (long long i = tid; i < nv; i += (int)blockDim.x) {
       const long long e = g0 + 4 * i;
       const float4 gs = wld4<NT>(red, i);
       float4 w = *reinterpret_cast<const float4*>(a.w + e);
@@ -253,7 +262,7 @@ __device__ __forceinline__ void apply_chunk(const XgArgs& a, float lr_t, long lo
     }
     nv <<= 2;
   }
-  for (long long i = nv + tid; i < n; i += kXgThreads) {
+  for (long long i = nv + tid; i < n; i += (int)blockDim.x) {
     const long long e = g0 + i;
     float m = mom ? a.m[e] : 0.f, v = adam ? a.v[e] : 0.f;
     const float w = opt_step(a.h, lr_t, a.w[e], wld<NT>(red, i), m, v);
@@ -276,7 +285,7 @@ struct XgLaunch {
 };
 
 template <bool UNCACHED, int NL>
-__global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL> la) {
+__global__ void __launch_bounds__(kXgWideThreads) xgmi_allreduce_kernel(XgLaunch<NL> la) {
   const XgArgs& a = la.r[NL == 1 ? 0 : blockIdx.y];
   const int blk = blockIdx.x, tid = threadIdx.x;
   const uint32_t epoch = a.epoch[0] + 1;
@@ -303,7 +312,7 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
     const long long plo = min(max(a.push_lo - g0, 0LL), n), phi = min(max(a.push_hi - g0, 0LL), n);
     if (a.nrep > 0 && a.rep_lo < g0 + n && a.rep_hi > g0) {
       // a chunk holding replicated elements (the MNIST-CNN conv gradients: a few hundred): element-wise
-      for (long long i = tid; i < n; i += kXgThreads) {
+      for (long long i = tid; i < n; i += (int)blockDim.x) {
         const long long g = g0 + i;
         if (i >= plo && i < phi) continue;
         float v;
@@ -342,7 +351,7 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
     const long long n = max(0LL, min(CH, M - g0));
     const float* in = area(a.peer[r], 0, parity, cap) + c0;
     const long long nv = n >> 2;   // area offsets are multiples of 4 elements
-    for (long long i = tid; i < nv; i += kXgThreads) {
+    for (long long i = tid; i < nv; i += (int)blockDim.x) {
       float4 acc = wld4<UNCACHED>(in, i);
       for (int s = 1; s < N; ++s) {
         const float4 v = wld4<UNCACHED>(in + (size_t)s * L, i);
@@ -351,7 +360,7 @@ __global__ void __launch_bounds__(kXgThreads) xgmi_allreduce_kernel(XgLaunch<NL>
       for (int p = 0; p < N; ++p)
         reinterpret_cast<float4*>(area(a.peer[p], 1, parity, cap) + (size_t)r * L + c0)[i] = acc;
     }
-    for (long long i = (nv << 2) + tid; i < n; i += kXgThreads) {
+    for (long long i = (nv << 2) + tid; i < n; i += (int)blockDim.x) {
       float acc = wld<UNCACHED>(in, i);
       for (int s = 1; s < N; ++s) acc += wld<UNCACHED>(in + (size_t)s * L, i);
       for (int p = 0; p < N; ++p) area(a.peer[p], 1, parity, cap)[(size_t)r * L + c0 + i] = acc;
@@ -595,11 +604,36 @@ static int xg_set_apply(XgArgs& a, const TdeXgApply* o) {
 
 static int clamp_blocks(int nblocks) { return nblocks < 1 ? 1 : nblocks > kXgMaxBlocks ? kXgMaxBlocks : nblocks; }
 
+// 0: not set, 1: wide launches allowed, -1: some communicator of this process shares its GPU with another
+// process (sticky).  TDE_XGMI_WIDE=0 turns wide launches off (A/B).
+static std::atomic<int> g_xg_wide{0};
+TDE_API int tde_xgmi_set_wide(int on) {
+  if (!on) g_xg_wide.store(-1);
+  else {
+    int z = 0;
+    g_xg_wide.compare_exchange_strong(z, 1);
+  }
+  return g_xg_wide.load();
+}
+static int xg_threads(int nloc, int nblocks) {
+  static const int env = [] {
+    const char* e = getenv("TDE_XGMI_WIDE");
+    return e && *e ? atoi(e) : 1;
+  }();
+  if (!env || g_xg_wide.load() != 1) return kXgThreads;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                              hipSuccess)
+    return kXgThreads;
+  return nloc * nblocks <= cus ? kXgWideThreads : kXgThreads;
+}
+TDE_API int tde_xgmi_threads(int nloc, int nblocks) { return xg_threads(nloc, clamp_blocks(nblocks)); }
+
 template <int NL>
 static int xg_go(const XgLaunch<NL>& la, int nloc, int nblocks, int uncached, hipStream_t stream) {
-  const dim3 grid(nblocks, nloc);
-  if (uncached) hipLaunchKernelGGL((xgmi_allreduce_kernel<true, NL>), grid, dim3(kXgThreads), 0, stream, la);
-  else hipLaunchKernelGGL((xgmi_allreduce_kernel<false, NL>), grid, dim3(kXgThreads), 0, stream, la);
+  const dim3 grid(nblocks, nloc), block(xg_threads(nloc, nblocks));
+  if (uncached) hipLaunchKernelGGL((xgmi_allreduce_kernel<true, NL>), grid, block, 0, stream, la);
+  else hipLaunchKernelGGL((xgmi_allreduce_kernel<false, NL>), grid, block, 0, stream, la);
   TDE_LAUNCH_CHECK();
   return 0;
 }

@@ -147,6 +147,8 @@ _HIP_PROTOS = {
     "tde_xgmi_trace_words": (i32, []),
     "tde_xgmi_push_spec": (i32, [i64, i64, p, p, i32, i32, i32, i64, p]),
     "tde_xgmi_set_trace": (i32, [p, p, i32]),
+    "tde_xgmi_set_wide": (i32, [i32]),
+    "tde_xgmi_threads": (i32, [i32, i32]),
     "tde_xgmi_all_reduce": (i32, [p, i64, i64, p, p, p, i32, i32, i32, i32, i64, p]),
     "tde_xgmi_all_reduce_apply": (i32, [p, i64, i64, p, p, p, i32, i32, i32, i32, i64, p, p]),
     "tde_xgmi_all_reduce_group": (i32, [i32, p, i64, i64, p, p, p, i32, i32, i32, i32, i64, p, p]),

@@ -256,6 +256,9 @@ def _device_key(d):
             f"{getattr(p, 'uuid', '')}")
 
 
+GPU_SHARED = {}   # spin_chunk_cap tag -> some GPU of the world runs more than one process's all-reduce
+
+
 def spin_chunk_cap(control, devices, tag):
     """The most chunks (workgroups per rank) ONE all-reduce launch may use, the same number on every rank
     of the world, or None (no limit beyond the kernel's own).
@@ -289,6 +292,7 @@ def spin_chunk_cap(control, devices, tag):
         mine[k][0] += 1
     per_proc = [mine] if control is None else control.all_gather_json(mine, tag)
     cap = chunk_cap_of(per_proc)
+    GPU_SHARED[tag] = cap is not None   # before the diagnostics override: wide launches need an unshared GPU
     if os.environ.get("TDE_XGMI_SPIN_CAP", "1") == "0":
         cap = None
     if control is not None:
@@ -380,6 +384,8 @@ class XgmiCommunicator(Communicator):
             raise RuntimeError(f"xGMI peer mapping failed: {errs}")
         self.peers = (C.c_void_p * self.world)(*peers)
         self.chunk_cap = spin_chunk_cap(control, [self.device], "xgmi_spin")
+        # 1024-thread workgroups only when no other process shares this GPU (csrc/comm/xgmi_allreduce.hip)
+        self.lib.tde_xgmi_set_wide(int(not GPU_SHARED.get("xgmi_spin", True)))
         tc = int(os.environ.get("TDE_XGMI_TRACE", "0") or 0)
         self.trace = [_xg_trace_alloc(self.lib, self.device, self.epoch.value, tc)] if tc > 0 else None
 
@@ -666,6 +672,7 @@ class PeerXgmiCommunicator(Communicator):
                                 (C.c_void_p * len(grp))(*[self.errs[i] for i in grp])))
         self._side = [torch.cuda.Stream(self.devices[grp[0]]) for grp in self.groups]
         self.chunk_cap = spin_chunk_cap(control, self.devices, "pxg_spin")
+        self.lib.tde_xgmi_set_wide(int(not GPU_SHARED.get("pxg_spin", True)))
         tc = int(os.environ.get("TDE_XGMI_TRACE", "0") or 0)
         self.trace = [_xg_trace_alloc(self.lib, d, e, tc) for d, e in zip(self.devices, self.epochs)] \
             if tc > 0 else None

@@ -10,6 +10,7 @@ N replicas at global batch G train like ONE replica at G (bench/dp_equiv.py).
 """
 import json
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -290,7 +291,8 @@ def test_eager_mwms_2x2_rehearsal_runs_clean():
                        timeout=240)
     out = r.stdout
     assert r.returncode == 0, out[-4000:]
-    execs = [l for l in out.splitlines() if " exec " in l]
+    # records, not lines: the two workers share one pipe, so a line can hold the tail of the other's
+    execs = re.findall(r"\[diag w\d\] exec \d+ [\d.]+ ms err=\[[^\]]*\] epochs=\[[^\]]*\]", out)
     assert len(execs) == 12, out[-4000:]
     for l in execs:
         assert "err=[0, 0]" in l, l
