@@ -112,7 +112,7 @@ def main():
     if a.sweep_fd:
         # fwd / dgrad per layer under (tile_min, K step): picks the per-shape defaults
         lib = N.hip()
-        cfgs = [(tm, kb, 0) for kb in (32, 64) for tm in (256, 1024, 2048, 4096)] + [(2048, 64, 1)]
+        cfgs = [(tm, kb, 0) for kb in (32, 64) for tm in (64, 160, 256, 1024, 2048, 4096)] + [(2048, 64, 1)]
         for st in _convs(plan, LW):
             g = st.geo.with_batch(B)
             res = []
