@@ -19,6 +19,7 @@ all-reduce and SGD update.  Precision: float32 by default — the reference's
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import math
 import os
@@ -182,6 +183,12 @@ def main():
     n_warm = max(n_warm, 2 + math.ceil(warm_s / per_exec))
     if world > 1:
         n_warm = int(strategy.control.all_reduce_max(n_warm))
+    # no cyclic-GC pass inside a timed window (a collection is a host pause of up to ~1 ms against a 0.47 ms
+    # 20-step window): collect now, BEFORE the warm-up — a collection between the warm-up and the window would
+    # idle the GPU, and an idle GPU runs the next ~0.5 ms of work slowly (the warm-up note above) — and pause the collector until
+    # the windows are done
+    gc.collect()
+    gc.disable()
     if n_warm > 2:
         stage(2)
     for i in range(2, n_warm):
@@ -206,9 +213,12 @@ def main():
         el = time.perf_counter() - t0
         return strategy.control.all_reduce_max(el) if world > 1 else el
 
-    elapsed = timed(n_warm)
-    # spread evidence (outside the reported measurement): the same K-step measurement repeated
-    repeats = [timed(n_warm + n_exec * (r + 1)) for r in range(max(0, a.repeats))]
+    try:
+        elapsed = timed(n_warm)
+        # spread evidence (outside the reported measurement): the same K-step measurement repeated
+        repeats = [timed(n_warm + n_exec * (r + 1)) for r in range(max(0, a.repeats))]
+    finally:
+        gc.enable()
     logs = tde.metrics.logs_from(prog.global_metrics(), ["accuracy"])
     comm = strategy.comm
     ar = {"XgmiCommunicator": "xgmi", "PeerXgmiCommunicator": "xgmi_peer", "RcclCommunicator": "rccl",
