@@ -99,3 +99,20 @@ def test_grid_sizes_respect_the_cap(monkeypatch):
     assert pg.nblocks(347146, 2, 0) == 96
     assert pg.nblocks(347146, 1, 0) == 96       # a 1-replica group of the same world: the same count
     assert pg.nblocks(1000, 2, 0) == 8
+
+
+def test_gpu_sharing_decides_wide_allreduce_workgroups(monkeypatch):
+    """GPU_SHARED (what the communicators pass to tde_xgmi_set_wide): 1024-thread all-reduce workgroups only when
+    no GPU of the world runs two processes' all-reduces — independent of the TDE_XGMI_SPIN_CAP=0 diagnostics
+    override, which lifts the chunk limit but not the co-location."""
+    key = _setup(monkeypatch)
+    d0 = torch.device("cuda:0")
+    CM.spin_chunk_cap(_Ctl([{key(i): [1, 256]} for i in range(1, 8)]), [d0], "w8")
+    assert CM.GPU_SHARED["w8"] is False                    # 8 processes, 8 GPUs
+    CM.spin_chunk_cap(None, [d0, d0], "mirrored")
+    assert CM.GPU_SHARED["mirrored"] is False              # in-process replicas on one GPU: one grid
+    CM.spin_chunk_cap(_Ctl([{key(0): [1, 256]}]), [d0], "co")
+    assert CM.GPU_SHARED["co"] is True                     # 2 processes on one GPU
+    monkeypatch.setenv("TDE_XGMI_SPIN_CAP", "0")
+    assert CM.spin_chunk_cap(_Ctl([{key(0): [1, 256]}]), [d0], "co0") is None
+    assert CM.GPU_SHARED["co0"] is True

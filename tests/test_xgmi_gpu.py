@@ -320,3 +320,34 @@ def test_mwms_fused_allreduce_apply_matches_unfused():
         assert res["config"]["allreduce"] == "xgmi" and res["config"]["hipgraph"] is True, res
         assert res["config"]["optimizer_placement"] == ("allreduce" if fused == "1" else "separate"), res
         assert "replicas_identical=True" in r.stdout, r.stdout[-3000:]
+
+
+WIDE = r"""
+import sys
+sys.path.insert(0, {root!r})
+import torch
+torch.cuda.set_device(0)
+from tensorflow_distributed_example_amd import _native as N
+lib = N.hip()
+cus = torch.cuda.get_device_properties(0).multi_processor_count
+out = [lib.tde_xgmi_threads(2, 128)]        # not yet set: 256
+lib.tde_xgmi_set_wide(1)
+out += [lib.tde_xgmi_threads(2, 128), lib.tde_xgmi_threads(1, 128), lib.tde_xgmi_threads(8, 128)]
+lib.tde_xgmi_set_wide(0)                    # a shared GPU: sticky off
+lib.tde_xgmi_set_wide(1)
+out += [lib.tde_xgmi_threads(1, 128)]
+print("WIDE", cus, *out, flush=True)
+"""
+
+
+def test_allreduce_workgroup_width_rule():
+    """The xGMI all-reduce runs 1024-thread workgroups only after a communicator declared the GPU unshared and only
+    while the grid (local ranks x chunks) fits one workgroup per CU; a shared GPU turns it off for good."""
+    r = subprocess.run([sys.executable, "-c", WIDE.format(root=ROOT)], stdout=subprocess.PIPE,
+                       stderr=subprocess.STDOUT, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-3000:]
+    vals = [int(v) for v in r.stdout.split("WIDE")[1].split()]
+    cus, before, two, one, eight, after = vals
+    assert before == 256 and after == 256
+    assert two == (1024 if 2 * 128 <= cus else 256) and one == 1024
+    assert eight == (1024 if 8 * 128 <= cus else 256)
