@@ -61,7 +61,9 @@ def summary(s, t0):
     return out
 
 
-names = [f"conv_fwd{i}" for i in range(len(plan.blocks))] + ["dense_fwd", "head", "dense_bwd"]
+fold = plan.head_fold_ok(B)
+names = [f"conv_fwd{i}" for i in range(len(plan.blocks))] + ["dense_fwd"] + ([] if fold else ["head"]) + [
+    "dense_bwd_head" if fold else "dense_bwd"]
 names += [f"conv_bwd{i}" for i in reversed(range(len(plan.blocks)))] + ["reduce"]
 t0 = None
 for li, name in enumerate(names):

@@ -417,6 +417,28 @@ __global__ __launch_bounds__(NTB) void conv_fwd_kernel(ConvFwdArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Philox4x32-10: tde_philox.h (counter-based: masks are regenerated, never stored)
+// The keep scales of the 4 elements e0 .. e0+3 (e0 % 4 == 0): one Philox call (the same values as
+// keep_scale of each element).
+__device__ __forceinline__ float4 keep_scale4(float rate, unsigned long long seed, long long it, int layer, long long e0) {
+  const uint2 key{(unsigned)seed, (unsigned)(seed >> 32)};
+  const unsigned long long c = (unsigned long long)(e0 >> 2);
+  const uint4 r = philox(uint4{(unsigned)c, (unsigned)(c >> 32), (unsigned)it, (unsigned)layer}, key);
+  const float keep = 1.f - rate, inv = 1.f / keep;
+  auto f = [&](unsigned w) { return ((w >> 8) * (1.f / 16777216.f) < keep) ? inv : 0.f; };
+  return float4{f(r.x), f(r.y), f(r.z), f(r.w)};
+}
+__device__ __forceinline__ float keep_scale(float rate, unsigned long long seed, long long it, int layer, long long e) {
+  const uint2 key{(unsigned)seed, (unsigned)(seed >> 32)};
+  const unsigned long long c = (unsigned long long)(e >> 2);
+  const uint4 r = philox(uint4{(unsigned)c, (unsigned)(c >> 32), (unsigned)it, (unsigned)layer}, key);
+  const int q = (int)(e & 3);
+  const unsigned w = q == 0 ? r.x : q == 1 ? r.y : q == 2 ? r.z : r.w;
+  const float keep = 1.f - rate;
+  return ((w >> 8) * (1.f / 16777216.f) < keep) ? 1.f / keep : 0.f;
+}
+
+// ------------------------------------------------------------------------------------------------
 // Dense forward: h = relu(BN(in)) . W_dense; grid (Dp/16 column tiles, ceil(B/16) row tiles).  One
 // 16x16 output tile per workgroup over the full K: wave w takes K range [w*kw, (w+1)*kw) with its MFMA
 // operands loaded straight from global into registers (no LDS staging), the 16 partial tiles summed in
@@ -432,6 +454,11 @@ struct DenseFwdArgs {
   float* h;                  // [B][Dp]
   double* hstat;             // [ceil(B/16)][2][Dp]
   long long* stamps;
+  // training with dropout and the head folded into the dense backward (nullable): the dropout keep flags of
+  // this workgroup's 16 x 16 tile in MFMA output layout, keep[(row tile * Dp/16 + column tile) * 64 + lane] =
+  // 4 bytes (rows 4 fq + i, column fr; 1 = kept), the masks keep_scale draws for the head
+  unsigned* keep;
+  float rate; unsigned long long seed; const long long* iter; int layer_id;
 };
 
 // V4 (K % 4 == 0, kw % 16 == 0): the A operand as one float4 load per 4 MFMA steps.  Lane (fr, fq)
@@ -513,31 +540,22 @@ __global__ __launch_bounds__(NTB) void dense_fwd_kernel(DenseFwdArgs a) {
       a.hstat[((size_t)blockIdx.y * 2 + 0) * a.Dp + c0 + fr] = s1;
       a.hstat[((size_t)blockIdx.y * 2 + 1) * a.Dp + c0 + fr] = s2;
     }
+    if (a.keep) {
+      const long long it = *a.iter;
+      unsigned w = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = r0 + fq * 4 + i;
+        const bool k = r < a.B && c0 + fr < a.D &&
+                       keep_scale(a.rate, a.seed, it, a.layer_id, (long long)r * a.D + c0 + fr) != 0.f;
+        w |= (k ? 1u : 0u) << (8 * i);
+      }
+      a.keep[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 64 + lane] = w;
+    }
   }
   stamp(a.stamps, 3);
 }
 
-// ------------------------------------------------------------------------------------------------
-// Philox4x32-10: tde_philox.h (counter-based: masks are regenerated, never stored)
-// The keep scales of the 4 elements e0 .. e0+3 (e0 % 4 == 0): one Philox call (the same values as
-// keep_scale of each element).
-__device__ __forceinline__ float4 keep_scale4(float rate, unsigned long long seed, long long it, int layer, long long e0) {
-  const uint2 key{(unsigned)seed, (unsigned)(seed >> 32)};
-  const unsigned long long c = (unsigned long long)(e0 >> 2);
-  const uint4 r = philox(uint4{(unsigned)c, (unsigned)(c >> 32), (unsigned)it, (unsigned)layer}, key);
-  const float keep = 1.f - rate, inv = 1.f / keep;
-  auto f = [&](unsigned w) { return ((w >> 8) * (1.f / 16777216.f) < keep) ? inv : 0.f; };
-  return float4{f(r.x), f(r.y), f(r.z), f(r.w)};
-}
-__device__ __forceinline__ float keep_scale(float rate, unsigned long long seed, long long it, int layer, long long e) {
-  const uint2 key{(unsigned)seed, (unsigned)(seed >> 32)};
-  const unsigned long long c = (unsigned long long)(e >> 2);
-  const uint4 r = philox(uint4{(unsigned)c, (unsigned)(c >> 32), (unsigned)it, (unsigned)layer}, key);
-  const int q = (int)(e & 3);
-  const unsigned w = q == 0 ? r.x : q == 1 ? r.y : q == 2 ? r.z : r.w;
-  const float keep = 1.f - rate;
-  return ((w >> 8) * (1.f / 16777216.f) < keep) ? 1.f / keep : 0.f;
-}
 
 // ------------------------------------------------------------------------------------------------
 // Head: grid ceil(B/16), one 16-row tile per workgroup (all Dp features):
@@ -816,7 +834,33 @@ struct DenseBwdArgs {
   long long* stamps;
 };
 
-__global__ __launch_bounds__(NTB) void dense_bwd_kernel(DenseBwdArgs a) {
+// The head folded into the dense backward (training; dense_bwd_kernel<true>): every workgroup recomputes the
+// head of ALL rows — the dense BN's backward sums need g of every row — from h (in registers, MFMA tile layout),
+// dense_fwd's statistics partials and dropout keep flags, Wh, the labels.  Only the activation tile passes through
+// LDS (the logits MFMA's A operand); g comes out of the MFMA already in the tile layout, next to the xhat it is
+// multiplied by.  Workgroup (0, 0) stores what the head launch stored once (saved / moving statistics, metrics),
+// the column-0 workgroups the dWh / dbh partials of their 64 rows.  Opt-in (TDE_BNCNN_HEAD_FOLD=1): it deletes the
+// head launch and one boundary, but the 8x head work per workgroup costs more (phase clocks: 7.3 us activations +
+// logits + softmax, 11.2 us g + sums + dh, vs the head launch's 7.7 us; Model B 1.019 M -> 0.920 M img/s).
+struct HeadFold {
+  const double* hstat;           // [nrt][2][Dp] dense_fwd's statistics partials
+  const unsigned* keep;          // dense_fwd's keep flags (null: no dropout)
+  float inv_keep;                // 1 / (1 - rate)
+  int NC;
+  const float* wh; const float* bh; const int* labels; float scale;
+  float* metrics; float* dwh_part; float* dbh_part;
+};
+constexpr int kHT = 7;   // head tiles per wave: nrt * Dp / 16 <= 16 * kHT
+// phase-A LDS bytes: act [nrt*16][Dp+4] | Wh [Dp][17] | dl [nrt*16][17] | max(BN coefficients, logit halves,
+// per-tile backward sums f64)
+__host__ __device__ inline int head_fold_lds(int nrt, int Dp) {
+  const int u = 4 * 256 * 4 > 16 * 256 * 4 ? 4 * 256 * 4 : 16 * 256 * 4;
+  const int gp = nrt * 2 * Dp * 8;
+  return (nrt * 16 * (Dp + 4) + Dp * 17 + nrt * 16 * 17) * 4 + (gp > u ? gp : u);
+}
+
+template <bool HEAD>
+__global__ __launch_bounds__(NTB) void dense_bwd_kernel(DenseBwdArgs a, HeadFold hf) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
   const int C = a.bn.C, K = a.K, D = a.D, Dp = a.Dp, ldh = a.ldh;
   double* cs = reinterpret_cast<double*>(sm);             // [8][2][32]
@@ -830,50 +874,319 @@ __global__ __launch_bounds__(NTB) void dense_bwd_kernel(DenseBwdArgs a) {
   const int kt0 = blockIdx.x * 32, b0 = blockIdx.y * 64, nb = min(64, a.B - b0);
   stamp(a.stamps, 0);
   Pf<kUWk> pw;
-  Pf<kUDh> pd, ph;
   Pf<2> px;
   // rows are contiguous: the tile is one clamped linear range (no index division in the address math)
-  const int wlast = (K - kt0) * D - 1, hlast = nb * Dp - 1;
+  const int wlast = (K - kt0) * D - 1;
   const float* wt = a.w + (size_t)kt0 * D;
-  const float* ght = a.gh + (size_t)b0 * Dp;
-  const float* ht = a.h + (size_t)b0 * Dp;
   pf_load(pw, 32 * D, [&](int e) { return wt[min(e, wlast)]; });
-  pf_load(pd, 64 * Dp, [&](int e) { return ght[min(e, hlast)]; });
-  pf_load(ph, 64 * Dp, [&](int e) { return ht[min(e, hlast)]; });
   pf_load(px, 64 * 32, [&](int e) { return a.in[(size_t)min(b0 + (e >> 5), a.B - 1) * K + min(kt0 + (e & 31), K - 1)]; });
-  // the dense BN's backward sums for feature tid (fixed order over the head's row tiles)
-  if (tid < Dp) {
-    // the saved statistics and gamma join the load batch (not a second round trip after the sums)
-    const bool ok = tid < D;
-    const float m = ok ? a.bnd.saved[tid] : 0.f, r = ok ? a.bnd.saved[D + tid] : 0.f;
-    const float gm = (ok && a.bnd.gamma) ? a.bnd.gamma[tid] : 1.f;
-    double S1 = 0.0, S2 = 0.0;
-    for (int p0 = 0; p0 < a.nrt; p0 += 8) {
-      double v1[8], v2[8];
+  Pf<HEAD ? 1 : kUDh> pd, ph;
+  if constexpr (HEAD) {
+    const int B = a.B, nrt = a.nrt, NC = hf.NC, ntf = Dp >> 4, nt = nrt * ntf, ldA = Dp + 4;
+    const bool lead = blockIdx.x == 0 && blockIdx.y == 0;
+    float* As = reinterpret_cast<float*>(sm);
+    float* whs = As + nrt * 16 * ldA;
+    float* dls = whs + Dp * 17;
+    float* U = dls + nrt * 16 * 17;
+    float *mu = U, *rsd = U + 256, *scd = U + 512, *shd = U + 768;
+    float* lgp = U;
+    double* gp = reinterpret_cast<double*>(U);
+    // ---- one batch of loads: h of this lane's head tiles (tile t = wave + 16 j: row tile t / ntf, feature tile
+    // t % ntf; rows 4 fq + i, feature fr), their keep flags, Wh, bias / labels, the statistics partials of feature tid
+    float hv[kHT][4];
+    unsigned kw[kHT];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int p = min(p0 + u, a.nrt - 1);
-        v1[u] = a.gstat[((size_t)p * 2 + 0) * Dp + tid];
-        v2[u] = a.gstat[((size_t)p * 2 + 1) * Dp + tid];
+    for (int j = 0; j < kHT; ++j) {
+      const int t = wave + 16 * j;
+      kw[j] = 0x01010101u;
+      if (t < nt) {
+        const int rt = t / ntf, fe = (t - rt * ntf) * 16 + fr;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) hv[j][i] = a.h[(size_t)min(rt * 16 + fq * 4 + i, B - 1) * Dp + fe];
+        if (hf.keep) kw[j] = hf.keep[(size_t)t * 64 + lane];
+      }
+    }
+    float wv[4];   // Dp * 16 <= 4 * NTB
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + u * NTB, fw = e >> 4, c = e & 15;
+      wv[u] = (fw < D && c < NC) ? hf.wh[(size_t)fw * NC + c] : 0.f;
+    }
+    float bias = 0.f;
+    int lab[4] = {0, 0, 0, 0};
+    if (wave < nrt) {
+      if (fr < NC) bias = hf.bh[fr];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) lab[i] = hf.labels[min(wave * 16 + fq * 4 + i, B - 1)];
+    }
+    const Bn& bnd = a.bnd;
+    const int f = tid;
+    const float gm = (f < D && bnd.gamma) ? bnd.gamma[f] : 1.f;
+    const float bt = (f < D && bnd.beta) ? bnd.beta[f] : 0.f;
+    const bool upd = lead && f < D && bnd.mmean;
+    const float om = upd ? bnd.mmean[f] : 0.f, ov = upd ? bnd.mvar[f] : 1.f;
+    double S = 0.0, S2 = 0.0;
+    if (f < D) {
+      for (int p0 = 0; p0 < nrt; p0 += 8) {
+        double v1[8], v2[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int p = min(p0 + u, nrt - 1);
+          v1[u] = hf.hstat[((size_t)p * 2 + 0) * Dp + f];
+          v2[u] = hf.hstat[((size_t)p * 2 + 1) * Dp + f];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (p0 + u < nrt) {
+            S += v1[u];
+            S2 += v2[u];
+          }
+      }
+    }
+    // ---- the dense BN's batch statistics (as the head launch: E[x^2] - E[x]^2 over the f64 partial sums)
+    float coef = 0.f;   // gamma * rstd of feature tid
+    if (f < Dp) {
+      float mean = 0.f, rstd = 1.f;
+      if (f < D) {
+        const double m = S / B, v = fmax(S2 / B - m * m, 0.0);
+        mean = (float)m;
+        rstd = (float)(1.0 / sqrt(v + (double)bnd.eps));
+        if (lead) {
+          bnd.saved[f] = mean;
+          bnd.saved[D + f] = rstd;
+          if (bnd.mmean) {
+            bnd.mmean[f] = om * bnd.momentum + mean * (1.f - bnd.momentum);
+            bnd.mvar[f] = ov * bnd.momentum + (float)v * bnd.bessel * (1.f - bnd.momentum);
+          }
+        }
+        coef = gm * rstd;
+      }
+      mu[f] = mean;
+      rsd[f] = rstd;
+      scd[f] = coef;
+      shd[f] = f < D ? bt - mean * gm * rstd : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + u * NTB;
+      if (e < Dp * 16) whs[(e >> 4) * 17 + (e & 15)] = wv[u];
+    }
+    lds_barrier();
+    stamp(a.stamps, 1);
+    // ---- activations (ReLU, dropout) -> LDS; hv becomes xhat
+#pragma unroll
+    for (int j = 0; j < kHT; ++j) {
+      const int t = wave + 16 * j;
+      if (t < nt) {
+        const int rt = t / ntf, fe = (t - rt * ntf) * 16 + fr;
+        const float m_ = mu[fe], r_ = rsd[fe], s_ = scd[fe], h_ = shd[fe];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int rl = rt * 16 + fq * 4 + i;
+          float act = 0.f, x = 0.f;
+          if (rl < B && fe < D) {
+            x = (hv[j][i] - m_) * r_;
+            act = fmaxf(fmaf(hv[j][i], s_, h_), 0.f);
+            if (hf.keep) act = ((kw[j] >> (8 * i)) & 1u) ? act * hf.inv_keep : 0.f;
+          }
+          As[rl * ldA + fe] = act;
+          hv[j][i] = x;
+        }
+      }
+    }
+    lds_barrier();
+    // ---- logits [nrt*16][16]: wave = row tile (w & 7) x feature half (w >> 3), the halves summed in order
+    {
+      const int rt = wave & 7, kh = wave >> 3, kq = Dp >> 1;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      if (rt < nrt)
+        for (int s4 = 0; s4 < kq / 4; ++s4) {
+          const int k = kh * kq + 4 * s4 + fq;
+          acc = mfma4(As[(rt * 16 + fr) * ldA + k], whs[k * 17 + fr], acc);
+        }
+      *reinterpret_cast<f32x4*>(&lgp[wave * 256 + lane * 4]) = acc;
+    }
+    lds_barrier();
+    if (wave < nrt) {
+      const f32x4 lg = *reinterpret_cast<const f32x4*>(&lgp[wave * 256 + lane * 4]) +
+                       *reinterpret_cast<const f32x4*>(&lgp[(wave + 8) * 256 + lane * 4]);
+      float la = 0.f, ca = 0.f, na = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rl = wave * 16 + fq * 4 + i;
+        const bool valid = rl < B, cv = fr < NC;
+        const float z = cv ? lg[i] + bias : -3.0e38f;
+        const float m = row16_max(z);
+        const float ex = cv ? __expf(z - m) : 0.f;
+        const float sum = row16_sum(ex);
+        const float pr = ex / sum;
+        const int label = valid ? lab[i] : 0;
+        const int amx = row16_min(cv && z == m ? fr : 64);
+        const float zl = __shfl(z, (lane & ~15) | (label & 15), 64);
+        if (valid && fr == 0) {
+          la += __logf(sum) + m - zl;
+          ca += (amx == label) ? 1.f : 0.f;
+          na += 1.f;
+        }
+        dls[rl * 17 + fr] = (valid && cv) ? (pr - (fr == label ? 1.f : 0.f)) * hf.scale : 0.f;
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (p0 + u < a.nrt) {
-          S1 += v1[u];
-          S2 += v2[u];
-        }
+      for (int o = 32; o >= 1; o >>= 1) {
+        la += __shfl_xor(la, o, 64);
+        ca += __shfl_xor(ca, o, 64);
+        na += __shfl_xor(na, o, 64);
+      }
+      if (lead && hf.metrics && lane == 0 && na > 0.f) {
+        atomicAdd(hf.metrics + 0, la);
+        atomicAdd(hf.metrics + 1, ca);
+        atomicAdd(hf.metrics + 2, na);
+      }
     }
-    dk[tid] = ok ? gm * r : 0.f;
-    dk[256 + tid] = (float)(S1 / a.B);
-    dk[512 + tid] = m;
-    dk[768 + tid] = r * (float)(S2 / a.B);
-    if (ok && blockIdx.x == 0 && blockIdx.y == 0) {
-      if (a.dbeta_d) a.dbeta_d[tid] = (float)S1;
-      if (a.dgamma_d) a.dgamma_d[tid] = (float)S2;
+    lds_barrier();
+    stamp(a.stamps, 2);
+    // ---- the column-0 workgroups: dbh / dWh partials of their 64 rows (row tiles rt_lo .. rt_hi-1)
+    if (blockIdx.x == 0) {
+      const int rt_lo = blockIdx.y * 4, rt_hi = min(nrt, rt_lo + 4);
+      if (tid < 64) {
+        const int rt = rt_lo + (tid >> 4), c = tid & 15;
+        if (rt < rt_hi && c < NC) {
+          float sb = 0.f;
+          for (int r = 0; r < 16; ++r) sb += dls[(rt * 16 + r) * 17 + c];
+          hf.dbh_part[(size_t)rt * NC + c] = sb;
+        }
+      }
+      for (int item = wave; item < (rt_hi - rt_lo) * ntf; item += 16) {
+        const int rt = rt_lo + item / ntf, ft = item % ntf;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int r = rt * 16 + 4 * s4 + fq;
+          acc = mfma4(As[r * ldA + ft * 16 + fr], dls[r * 17 + fr], acc);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int fi = ft * 16 + fq * 4 + i;
+          if (fi < D && fr < NC) hf.dwh_part[((size_t)rt * D + fi) * NC + fr] = acc[i];
+        }
+      }
+    }
+    // ---- g = dl . Wh^T through the dropout / ReLU masks (tile layout), per-tile backward partial sums
+    float gq[kHT][4];
+#pragma unroll
+    for (int j = 0; j < kHT; ++j) {
+      const int t = wave + 16 * j;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) gq[j][i] = 0.f;
+      if (t < nt) {
+        const int rt = t / ntf, ft = t - rt * ntf, fe = ft * 16 + fr;
+        f32x4 gg = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int c = 4 * s4 + fq;
+          gg = mfma4(dls[(rt * 16 + fr) * 17 + c], whs[(ft * 16 + fr) * 17 + c], gg);
+        }
+        double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int rl = rt * 16 + fq * 4 + i;
+          float gv = 0.f;
+          if (rl < B && fe < D) {
+            // act > 0 <=> ReLU passed AND dropout kept; the kept scale is 1/keep
+            gv = As[rl * ldA + fe] > 0.f ? (hf.keep ? gg[i] * hf.inv_keep : gg[i]) : 0.f;
+            s1 += gv;
+            s2 += (double)(gv * hv[j][i]);
+          }
+          gq[j][i] = gv;
+        }
+        s1 += __shfl_xor(s1, 16, 64);
+        s1 += __shfl_xor(s1, 32, 64);
+        s2 += __shfl_xor(s2, 16, 64);
+        s2 += __shfl_xor(s2, 32, 64);
+        if (fq == 0) {
+          // gp aliases the logit halves (read before the last barrier) and not As / whs / dls
+          gp[((size_t)rt * 2 + 0) * Dp + fe] = s1;
+          gp[((size_t)rt * 2 + 1) * Dp + fe] = s2;
+        }
+      }
+    }
+    lds_barrier();
+    // ---- the dense BN's backward sums of feature tid over all rows, in row-tile order
+    double T1 = 0.0, T2 = 0.0;
+    if (tid < Dp)
+      for (int rt = 0; rt < nrt; ++rt) {
+        T1 += gp[((size_t)rt * 2 + 0) * Dp + tid];
+        T2 += gp[((size_t)rt * 2 + 1) * Dp + tid];
+      }
+    lds_barrier();   // phase A's LDS is free: the dense backward's layout from here on
+    if (tid < Dp) {
+      dk[tid] = coef;
+      dk[256 + tid] = (float)(T1 / B);
+      dk[768 + tid] = (float)(T2 / B);
+      if (lead && tid < D) {
+        if (a.dbeta_d) a.dbeta_d[tid] = (float)T1;
+        if (a.dgamma_d) a.dgamma_d[tid] = (float)T2;
+      }
+    }
+    lds_barrier();
+    // dh = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)) of this workgroup's rows from the tiles in registers
+#pragma unroll
+    for (int j = 0; j < kHT; ++j) {
+      const int t = wave + 16 * j;
+      if (t < nt) {
+        const int rt = t / ntf, fe = (t - rt * ntf) * 16 + fr;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = rt * 16 + fq * 4 + i - b0;
+          if (r >= 0 && r < 64) dhs[r * ldh + fe] = r < nb ? dk[fe] * (gq[j][i] - dk[256 + fe] - hv[j][i] * dk[768 + fe]) : 0.f;
+        }
+      }
+    }
+    // rows of the 64-row block past the last head tile
+    for (int e = tid; e < 64 * Dp; e += NTB) {
+      const int r = e / Dp;
+      if (b0 + r >= nrt * 16) dhs[r * ldh + (e - r * Dp)] = 0.f;
+    }
+    stamp(a.stamps, 3);
+  } else {
+    const int hlast = nb * Dp - 1;
+    const float* ght = a.gh + (size_t)b0 * Dp;
+    const float* ht = a.h + (size_t)b0 * Dp;
+    pf_load(pd, 64 * Dp, [&](int e) { return ght[min(e, hlast)]; });
+    pf_load(ph, 64 * Dp, [&](int e) { return ht[min(e, hlast)]; });
+    // the dense BN's backward sums for feature tid (fixed order over the head's row tiles)
+    if (tid < Dp) {
+      // the saved statistics and gamma join the load batch (not a second round trip after the sums)
+      const bool ok = tid < D;
+      const float m = ok ? a.bnd.saved[tid] : 0.f, r = ok ? a.bnd.saved[D + tid] : 0.f;
+      const float gm = (ok && a.bnd.gamma) ? a.bnd.gamma[tid] : 1.f;
+      double S1 = 0.0, S2 = 0.0;
+      for (int p0 = 0; p0 < a.nrt; p0 += 8) {
+        double v1[8], v2[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int p = min(p0 + u, a.nrt - 1);
+          v1[u] = a.gstat[((size_t)p * 2 + 0) * Dp + tid];
+          v2[u] = a.gstat[((size_t)p * 2 + 1) * Dp + tid];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (p0 + u < a.nrt) {
+            S1 += v1[u];
+            S2 += v2[u];
+          }
+      }
+      dk[tid] = ok ? gm * r : 0.f;
+      dk[256 + tid] = (float)(S1 / a.B);
+      dk[512 + tid] = m;
+      dk[768 + tid] = r * (float)(S2 / a.B);
+      if (ok && blockIdx.x == 0 && blockIdx.y == 0) {
+        if (a.dbeta_d) a.dbeta_d[tid] = (float)S1;
+        if (a.dgamma_d) a.dgamma_d[tid] = (float)S2;
+      }
     }
   }
   bn_prepare(a.bn, st, false, nullptr);
-  stamp(a.stamps, 1);
+  if (!HEAD) stamp(a.stamps, 1);
   const float* sc = st;
   const float* sh = st + C;
   const float* mu = st + 2 * C;
@@ -884,14 +1197,16 @@ __global__ __launch_bounds__(NTB) void dense_bwd_kernel(DenseBwdArgs a) {
   });
   if (Dp > D)
     for (int e = tid; e < 32 * (Dp - D); e += NTB) Wk[(e / (Dp - D)) * ldh + D + e % (Dp - D)] = 0.f;
+  if constexpr (!HEAD) {
 #pragma unroll
-  for (int u = 0; u < kUDh; ++u) {
-    const int e = tid + u * NTB;
-    if (e < 64 * Dp) {
-      const int r = dq(e, a.dDp), n = e - r * Dp;
-      // dh = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)), xhat*rstd folded: (h - mean)*rstd*mean(g*xhat)
-      const float dh = dk[n] * (pd.v[u] - dk[256 + n] - (ph.v[u] - dk[512 + n]) * dk[768 + n]);
-      dhs[r * ldh + n] = r < nb ? dh : 0.f;
+    for (int u = 0; u < kUDh; ++u) {
+      const int e = tid + u * NTB;
+      if (e < 64 * Dp) {
+        const int r = dq(e, a.dDp), n = e - r * Dp;
+        // dh = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)), xhat*rstd folded: (h - mean)*rstd*mean(g*xhat)
+        const float dh = dk[n] * (pd.v[u] - dk[256 + n] - (ph.v[u] - dk[512 + n]) * dk[768 + n]);
+        dhs[r * ldh + n] = r < nb ? dh : 0.f;
+      }
     }
   }
   pf_store(px, 64 * 32, [&](int e, float v) {
@@ -901,7 +1216,7 @@ __global__ __launch_bounds__(NTB) void dense_bwd_kernel(DenseBwdArgs a) {
     Ab[r * 33 + kk] = ok ? fmaxf(fmaf(v, sc[c], sh[c]), 0.f) : 0.f;
   });
   lds_barrier();
-  stamp(a.stamps, 2);
+  stamp(a.stamps, HEAD ? 4 : 2);
   if (wave < 8) {
     const int rt = wave & 3, kh = wave >> 2;
     const int k_me = kt0 + kh * 16 + fr, c_me = k_me - dq(k_me, a.dC) * C;
@@ -953,7 +1268,7 @@ __global__ __launch_bounds__(NTB) void dense_bwd_kernel(DenseBwdArgs a) {
     }
   }
   // BN backward sums: feature f of wave w -> channel (kt0 + (w >> 2) * 16 + f) % C
-  stamp(a.stamps, 3);
+  stamp(a.stamps, HEAD ? 5 : 3);
   lds_barrier();
   if (tid < 2 * C) {
     // the tile's features of channel c: kk = kk0, kk0 + C, ... (< 32), each over the 4 row tiles, in order
@@ -965,7 +1280,7 @@ __global__ __launch_bounds__(NTB) void dense_bwd_kernel(DenseBwdArgs a) {
       for (int rt = 0; rt < 4; ++rt) S += cs[((rt + 4 * (kk >> 4)) * 2 + j) * 32 + (kk & 15)];
     a.acc[(size_t)wg_id() * 2 * C + j * C + c] = S;
   }
-  stamp(a.stamps, 4);
+  stamp(a.stamps, HEAD ? 6 : 4);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1568,13 +1883,16 @@ TDE_API int tde_bncnn_conv_fwd(const TdeBnGeo* gg, int B, const float* in, const
 }
 
 // h = relu(BN(in)) . W (final, deterministic) and the dense BN's statistics partials per 16-row tile.
+// keep (nullable): the dropout keep flags of the folded head (HeadFold), drawn at step *iter
 TDE_API int tde_bncnn_dense_fwd(int B, int K, int D, int Dp, const float* in, const TdeBn* bn, const float* w, float* h,
-                                double* hstat, hipStream_t stream) {
+                                double* hstat, unsigned* keep, float rate, unsigned long long seed, const long long* iter,
+                                int layer_id, hipStream_t stream) {
   if (!bn_ok(bn) || bn->mode == kBnSaved || bn->mode == kBnNone || (Dp & 15) || Dp < D || !h || !hstat) return -1;
+  if (keep && (!iter || !(rate > 0.f && rate < 1.f))) return -3;
   const bool v4 = (K & 3) == 0 && ((uintptr_t)in & 15) == 0 && up((K + 15) / 16, 16) <= 4 * kDS;
   const int kw = v4 ? up((K + 15) / 16, 16) : up((K + 15) / 16, 4);
   if (kw > 4 * kDS) return -2;
-  DenseFwdArgs a{B, K, D, Dp, kw, dv(bn->C), in, bn_of(bn), w, h, hstat, next_stamps()};
+  DenseFwdArgs a{B, K, D, Dp, kw, dv(bn->C), in, bn_of(bn), w, h, hstat, next_stamps(), keep, rate, seed, iter, layer_id};
   if (v4) dense_fwd_kernel<true><<<dim3(Dp / 16, (B + 15) / 16), NTB, 0, stream>>>(a);
   else dense_fwd_kernel<false><<<dim3(Dp / 16, (B + 15) / 16), NTB, 0, stream>>>(a);
   TDE_LAUNCH_CHECK();
@@ -1656,8 +1974,56 @@ TDE_API int tde_bncnn_dense_bwd(int B, int K, int D, int Dp, const float* in, co
   a.g = g;
   a.acc = acc;
   a.stamps = next_stamps();
-  set_lds(dense_bwd_kernel, lds);
-  dense_bwd_kernel<<<dim3((K + 31) / 32, (B + 63) / 64), NTB, lds, stream>>>(a);
+  set_lds(dense_bwd_kernel<false>, lds);
+  dense_bwd_kernel<false><<<dim3((K + 31) / 32, (B + 63) / 64), NTB, lds, stream>>>(a, HeadFold{});
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+// The training head folded into the dense backward (dense_bwd_kernel<true>; replaces tde_bncnn_head mode 0 +
+// tde_bncnn_dense_bwd): bnd in mode kBnTrain (statistics from hstat; saved / moving updated by workgroup (0, 0));
+// keep = dense_fwd's keep flags (null: no dropout).  B <= 128, Dp <= 224, NC <= 16.
+TDE_API int tde_bncnn_dense_bwd_head(int B, int K, int D, int Dp, int NC, const float* in, const TdeBn* bn, const float* w,
+                                     const float* h, const double* hstat, const TdeBn* bnd, const unsigned* keep,
+                                     float rate, const float* wh, const float* bh, const int* labels, float scale,
+                                     float* metrics, float* dwh_part, float* dbh_part, float* dbeta_d, float* dgamma_d,
+                                     float* dwpart, float* g, double* acc, hipStream_t stream) {
+  const int nrt = (B + 15) / 16;
+  if (!bn_ok(bn) || bn->mode != kBnSaved || (Dp & 15) || Dp < D || !acc || !h || !hstat || B < 1 || B > 128) return -1;
+  if (!bnd || bnd->C != D || bnd->mode != kBnTrain || !bnd->saved || !wh || !bh || !labels || !dwh_part || !dbh_part ||
+      NC < 1 || NC > 16)
+    return -1;
+  if (32 * D > kUWk * NTB || Dp * 16 > 4 * NTB || nrt * (Dp / 16) > 16 * kHT || 2 * (Dp / 16) > 32) return -2;
+  if (keep && !(rate > 0.f && rate < 1.f)) return -4;
+  const int ldh = Dp + 4;
+  const int lds_b = 16 * 2 * 32 * 8 + 4 * 32 * 4 + 4 * 256 * 4 + 32 * ldh * 4 + 64 * ldh * 4 + 2 * 64 * 33 * 4;
+  const int lds_a = head_fold_lds(nrt, Dp);
+  const int lds = lds_a > lds_b ? lds_a : lds_b;
+  if (lds > kMaxLds) return -3;
+  DenseBwdArgs a{};
+  a.B = B;
+  a.K = K;
+  a.D = D;
+  a.Dp = Dp;
+  a.ldh = ldh;
+  a.nrt = nrt;
+  a.dD = dv(D);
+  a.dDp = dv(Dp);
+  a.dC = dv(bn->C);
+  a.in = in;
+  a.bn = bn_of(bn);
+  a.w = w;
+  a.h = h;
+  a.bnd = bn_of(bnd);
+  a.dbeta_d = dbeta_d;
+  a.dgamma_d = dgamma_d;
+  a.dwpart = dwpart;
+  a.g = g;
+  a.acc = acc;
+  a.stamps = next_stamps();
+  HeadFold hf{hstat, keep, keep ? 1.f / (1.f - rate) : 1.f, NC, wh, bh, labels, scale, metrics, dwh_part, dbh_part};
+  set_lds(dense_bwd_kernel<true>, lds);
+  dense_bwd_kernel<true><<<dim3((K + 31) / 32, (B + 63) / 64), NTB, lds, stream>>>(a, hf);
   TDE_LAUNCH_CHECK();
   return 0;
 }

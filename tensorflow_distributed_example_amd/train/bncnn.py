@@ -37,8 +37,8 @@ N.register_hip({
     "tde_bncnn_conv_fwd_cfg": (_i, [_vp, _vp]),
     # geo, B, in, bn_in, w, z, acc, inc_iter, stream
     "tde_bncnn_conv_fwd": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
-    # B, K, D, Dp, in, bn, w, h, hstat, stream
-    "tde_bncnn_dense_fwd": (_i, [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
+    # B, K, D, Dp, in, bn, w, h, hstat, keep, rate, seed, iter, layer_id, stream
+    "tde_bncnn_dense_fwd": (_i, [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, C.c_float, C.c_ulonglong, _vp, _i, _vp]),
     # B, D, Dp, NC, mode, h, hstat, bn, rate, seed, iter, layer_id, drop_on, wh, bh, labels, scale, metrics, out,
     # out_softmax, dwh_part, dbh_part, g, gstat, stream
     "tde_bncnn_head": (_i, [_i, _i, _i, _i, _i, _vp, _vp, _vp, C.c_float, C.c_ulonglong, _vp, _i, _i, _vp, _vp, _vp,
@@ -46,6 +46,10 @@ N.register_hip({
     # B, K, D, Dp, in, bn, w, gh, h, gstat, nrt, bnd, dbeta_d, dgamma_d, dwpart, g, acc, stream
     "tde_bncnn_dense_bwd": (_i, [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp,
                                  _vp]),
+    # B, K, D, Dp, NC, in, bn, w, h, hstat, bnd, keep, rate, wh, bh, labels, scale, metrics, dwh_part, dbh_part,
+    # dbeta_d, dgamma_d, dwpart, g, acc, stream
+    "tde_bncnn_dense_bwd_head": (_i, [_i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, C.c_float, _vp, _vp, _vp,
+                                      C.c_float, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "tde_bncnn_conv_bwd_plan": (_i, [_vp, _i, _vp]),
     # geo, B, z, bn, bb, gout, w, in, bn_in, gin, acc_in, dwpart, dgrad, wstack, stream
     "tde_bncnn_conv_bwd": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp]),
@@ -232,6 +236,9 @@ class BnCnnPlan(ReplicaPlan):
         self.dwh_part = torch.zeros(nrt * self.D * self.NC, **f32)
         self.dbh_part = torch.zeros(nrt * self.NC, **f32)
         self.probs = torch.zeros(B, self.NC, **f32)
+        # the training head folded into the dense backward (csrc/kernels/bncnn.hip dense_bwd_kernel<true>):
+        # dense_fwd stores the dropout keep flags in MFMA tile layout for it
+        self.keep = torch.zeros(nrt * (self.Dp // 16) * 64, dtype=torch.int32, device=self.device)
         H0, W0, C0 = self.blocks[0]["geo"].H, self.blocks[0]["geo"].W, self.blocks[0]["geo"].C
         self.x_stride = H0 * W0 * C0
         self.opt = OptimizerKernel(store, optimizer, {}, self.iterations) if optimizer is not None else None
@@ -239,6 +246,18 @@ class BnCnnPlan(ReplicaPlan):
         self._opt_key_set = None
         self._push = None     # fused DP exchange (step mode "xgmi", set_push)
         self._pushed = False
+
+    def head_fold_ok(self, B):
+        """TDE_BNCNN_HEAD_FOLD=1: the training head runs inside the dense backward launch (one launch fewer per
+        step) when its state fits one workgroup: B <= 128, Dp <= 224, NC <= 16 and the head's LDS (activations +
+        Wh + dl + sums) <= 160 KiB.  Off by default: correct, but every dense-backward workgroup recomputes the head
+        of all 128 rows (the dense BN's backward sums need every row's g), 18.5 us against the head launch's 7.7 us
+        plus one boundary — Model B 1.019 M -> 0.920 M img/s (profiles/r6_head_fold/)."""
+        if os.environ.get("TDE_BNCNN_HEAD_FOLD", "0") != "1" or self.device.type != "cuda":
+            return False
+        nrt, Dp = -(-B // 16), self.Dp
+        lds = (nrt * 16 * (Dp + 4) + Dp * 17 + nrt * 16 * 17) * 4 + max(nrt * 2 * Dp * 8, 16 * 256 * 4)
+        return B <= 128 and Dp <= 224 and self.D <= 256 and self.NC <= 16 and lds <= 160 * 1024
 
     def _bn_vars(self, bn):
         st, n = self.store, bn.name
@@ -265,7 +284,7 @@ class BnCnnPlan(ReplicaPlan):
         return BN_BATCH if training else BN_MOVING
 
     # ------------------------------------------------------------------ forward
-    def _forward(self, x, B, phase):
+    def _forward(self, x, B, phase, keep=False):
         """phase: "train" | True (batch statistics, no update: learning phase 1) | False (moving statistics)."""
         lib, s = self.lib, N.stream_ptr()
         mode = self._fwd_mode(phase)
@@ -282,8 +301,11 @@ class BnCnnPlan(ReplicaPlan):
                 raise RuntimeError(f"tde_bncnn_conv_fwd({blk['conv'].name}) failed with {rc}")
             bn_in = self._bn(blk, mode, B)
             inp = blk["z"]
+        drop = keep and self.drop is not None and self.drop.rate > 0
         rc = lib.tde_bncnn_dense_fwd(B, self.K, self.D, self.Dp, _P(inp), C.byref(bn_in), _P(self.wd), _P(self.h),
-                                     _P(self.hstat), s)
+                                     _P(self.hstat), _P(self.keep) if drop else None,
+                                     float(self.drop.rate) if drop else 0.0, self.drop_seed if drop else 0,
+                                     _P(self.iterations) if drop else None, 0, s)
         N.check(rc, "tde_bncnn_dense_fwd")
         return bn_in
 
@@ -325,18 +347,33 @@ class BnCnnPlan(ReplicaPlan):
         B = self.B if B is None else B
         self._check_input(x, B)
         lib, s = self.lib, N.stream_ptr()
-        self._forward(x, B, "train")
-        self._head(B, 0, "train", y, self.scale)
+        fold = self.head_fold_ok(B)
+        self._forward(x, B, "train", keep=fold)
         last = self.blocks[-1]
         bn_last = self._bn(last, BN_SAVED, B)
         bnd = self.bnd
-        bn_d = Bn(BN_SAVED, self.D, None, 0, float(B), _P(bnd["gamma"]), _P(bnd["beta"]), float(bnd["eps"]),
-                  float(bnd["momentum"]), 1.0, _P(bnd["mmean"]), _P(bnd["mvar"]), _P(bnd["saved"]))
-        rc = lib.tde_bncnn_dense_bwd(B, self.K, self.D, self.Dp, _P(last["z"]), C.byref(bn_last), _P(self.wd),
-                                     _P(self.gh), _P(self.h), _P(self.gstat), -(-B // 16), C.byref(bn_d),
-                                     _P(bnd["dbeta"]), _P(bnd["dgamma"]), _P(self.dwd_part), _P(last["g"]),
-                                     _P(last["accb"]), s)
-        N.check(rc, "tde_bncnn_dense_bwd")
+        if fold:
+            # the head inside the dense backward: the dense BN in training mode (its statistics, saved / moving
+            # update), the dropout flags dense_fwd stored
+            bn_t = Bn(BN_TRAIN, self.D, None, 0, float(B), _P(bnd["gamma"]), _P(bnd["beta"]), float(bnd["eps"]),
+                      float(bnd["momentum"]), 1.0, _P(bnd["mmean"]), _P(bnd["mvar"]), _P(bnd["saved"]))
+            drop = self.drop is not None and self.drop.rate > 0
+            rc = lib.tde_bncnn_dense_bwd_head(
+                B, self.K, self.D, self.Dp, self.NC, _P(last["z"]), C.byref(bn_last), _P(self.wd), _P(self.h),
+                _P(self.hstat), C.byref(bn_t), _P(self.keep) if drop else None,
+                float(self.drop.rate) if drop else 0.0, _P(self.wh), _P(self.bh), _P(y), float(self.scale),
+                _P(self.metrics), _P(self.dwh_part), _P(self.dbh_part), _P(bnd["dbeta"]), _P(bnd["dgamma"]),
+                _P(self.dwd_part), _P(last["g"]), _P(last["accb"]), s)
+            N.check(rc, "tde_bncnn_dense_bwd_head")
+        else:
+            self._head(B, 0, "train", y, self.scale)
+            bn_d = Bn(BN_SAVED, self.D, None, 0, float(B), _P(bnd["gamma"]), _P(bnd["beta"]), float(bnd["eps"]),
+                      float(bnd["momentum"]), 1.0, _P(bnd["mmean"]), _P(bnd["mvar"]), _P(bnd["saved"]))
+            rc = lib.tde_bncnn_dense_bwd(B, self.K, self.D, self.Dp, _P(last["z"]), C.byref(bn_last), _P(self.wd),
+                                         _P(self.gh), _P(self.h), _P(self.gstat), -(-B // 16), C.byref(bn_d),
+                                         _P(bnd["dbeta"]), _P(bnd["dgamma"]), _P(self.dwd_part), _P(last["g"]),
+                                         _P(last["accb"]), s)
+            N.check(rc, "tde_bncnn_dense_bwd")
         # backward partials of block li's BN: from the dense backward (last block) or from the input-gradient
         # role of block li + 1's conv backward (one per image)
         nkt_nrb = -(-self.K // 32) * -(-B // 64)

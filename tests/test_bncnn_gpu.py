@@ -345,3 +345,37 @@ def test_bncnn_dropout_matches_float64_with_the_plan_mask(B):
     ref = m(xe.cpu().numpy())
     ref = (ref if torch.is_tensor(ref) else torch.as_tensor(np.asarray(ref))).to(DEV, torch.float64)
     assert _rel(probs, ref) < 1e-5, _rel(probs, ref)
+
+
+@pytest.mark.parametrize("B", [128, 50])
+def test_bncnn_head_folded_into_dense_backward_matches_head_launch(B, monkeypatch):
+    """The training head inside the dense backward (TDE_BNCNN_HEAD_FOLD=1, opt-in: every workgroup recomputes the
+    head of all rows; dense_fwd stores the dropout keep flags) vs the separate head launch (the default): 3 steps with dropout
+    0.5 — gradients, moving statistics and metrics equal to fp32 summation-order noise, keep masks identical."""
+    import tensorflow_distributed_example_amd as tde
+    from tensorflow_distributed_example_amd.train import program as PG
+    res = {}
+    for fold in ("1", "0"):
+        monkeypatch.setenv("TDE_BNCNN_HEAD_FOLD", fold)
+        tde.backend.set_random_seed(5)
+        m = _model_b(tde, rate=0.5)
+        st = m._store
+        plan = PG.make_plan(m, st, DEV, 128, 128, m.optimizer, m.loss)
+        assert plan.head_fold_ok(B) == (fold == "1")
+        grads, masks = [], []
+        for step in range(3):
+            x, y = _data(128, 60 + step)
+            st.g.zero_()
+            plan.train_step(x, y, B)
+            masks.append(plan.dropout_mask(B).clone())
+            grads.append(st.g.clone())
+            plan.apply()
+        torch.cuda.synchronize()
+        res[fold] = (grads, masks, st.w.clone(), plan.metrics.clone())
+    (g1, m1, w1, met1), (g0, m0, w0, met0) = res["1"], res["0"]
+    for a, b in zip(m1, m0):
+        assert torch.equal(a, b)
+    for step, (a, b) in enumerate(zip(g1, g0)):
+        assert _rel(a, b) < 1e-5, (step, _rel(a, b))
+    assert _rel(w1, w0) < 1e-6
+    assert abs(met1[0].item() - met0[0].item()) <= 1e-5 * abs(met0[0].item()) and met1[2].item() == met0[2].item()
