@@ -105,6 +105,7 @@ struct XgArgs {
   float* rep; int nrep;
   long long rep_lo, rep_hi, rep_stride;
   int acquire;   // force the waits' system-scope acquire on the uncached window (TDE_XGMI_ACQUIRE=1; A/B only)
+  int flat;      // phase 3 over (slice, float4) pairs on every thread (gather_apply); TDE_XGMI_FLAT=0: slice by slice
 };
 constexpr int kXgTraceWords = 8;
 
@@ -227,6 +228,70 @@ __device__ __forceinline__ void shadow_store(const XgArgs& a, long long e, float
   if (a.sht) a.sht[(q % a.sh_cols) * a.sht_ld + q / a.sh_cols] = h;
 }
 
+// Optimizer step of the 4 elements e .. e+3 (e % 4 == 0) from their reduced sums gs: w, slots, shadows; grad zeroed.
+__device__ __forceinline__ void apply4(const XgArgs& a, float lr_t, long long e, float4 gs) {
+  const bool mom = a.h.kind != kOptSGD, adam = a.h.kind == kOptAdam;
+  float4 w = *reinterpret_cast<const float4*>(a.w + e);
+  float4 m = {0.f, 0.f, 0.f, 0.f}, v = {0.f, 0.f, 0.f, 0.f};
+  if (mom) m = *reinterpret_cast<const float4*>(a.m + e);
+  if (adam) v = *reinterpret_cast<const float4*>(a.v + e);
+  w.x = opt_step(a.h, lr_t, w.x, gs.x, m.x, v.x);
+  w.y = opt_step(a.h, lr_t, w.y, gs.y, m.y, v.y);
+  w.z = opt_step(a.h, lr_t, w.z, gs.z, m.z, v.z);
+  w.w = opt_step(a.h, lr_t, w.w, gs.w, m.w, v.w);
+  *reinterpret_cast<float4*>(a.w + e) = w;
+  if (mom) *reinterpret_cast<float4*>(a.m + e) = m;
+  if (adam) *reinterpret_cast<float4*>(a.v + e) = v;
+  *reinterpret_cast<float4*>(a.grad + e) = float4{0.f, 0.f, 0.f, 0.f};
+  if (e >= a.sh_lo && e + 4 <= a.sh_hi && !a.sht) {
+    *reinterpret_cast<bf16x4*>(a.sh + (e - a.sh_lo)) = bf16x4{f2bf(w.x), f2bf(w.y), f2bf(w.z), f2bf(w.w)};
+  } else {
+    shadow_store(a, e, w.x);
+    shadow_store(a, e + 1, w.y);
+    shadow_store(a, e + 2, w.z);
+    shadow_store(a, e + 3, w.w);
+  }
+}
+// The same for one element.
+__device__ __forceinline__ void apply1(const XgArgs& a, float lr_t, long long e, float g) {
+  const bool mom = a.h.kind != kOptSGD, adam = a.h.kind == kOptAdam;
+  float m = mom ? a.m[e] : 0.f, v = adam ? a.v[e] : 0.f;
+  const float w = opt_step(a.h, lr_t, a.w[e], g, m, v);
+  a.w[e] = w;
+  if (mom) a.m[e] = m;
+  if (adam) a.v[e] = v;
+  a.grad[e] = 0.f;
+  shadow_store(a, e, w);
+}
+
+// Phase 3 of a block: the N reduced slice chunks (slice s: bucket elements s * L + c0 .., window out + s * L + c0)
+// back into the bucket, or through the optimizer.  (slice, float4) pairs are dealt over ALL threads — walking the
+// slices one after another left all but CH / 4 threads idle per slice (85 of 1024 at N = 8) and cost N dependent
+// round trips; each element's operation is unchanged.
+template <bool NT>
+__device__ __forceinline__ void gather_apply(const XgArgs& a, float lr_t, const float* out, int N, long long L,
+                                             long long c0, long long CH, long long M) {
+  const long long nv = (CH + 3) >> 2, tot = (long long)N * nv;
+  for (long long q = threadIdx.x; q < tot; q += (int)blockDim.x) {
+    const int s = (int)(q / nv);
+    const long long i = q - (long long)s * nv;
+    const long long g0 = (long long)s * L + c0, n = max(0LL, min(CH, M - g0)), e0 = 4 * i;
+    if (e0 >= n) continue;
+    const float* red = out + (size_t)s * L + c0;
+    if (e0 + 4 <= n && (g0 & 3) == 0) {
+      const float4 gs = wld4<NT>(red, i);
+      if (a.apply) apply4(a, lr_t, g0 + e0, gs);
+      else *reinterpret_cast<float4*>(a.grad + g0 + e0) = gs;
+    } else {
+      for (long long k = e0; k < min(e0 + 4, n); ++k) {
+        const float g = wld<NT>(red, k);
+        if (a.apply) apply1(a, lr_t, g0 + k, g);
+        else a.grad[g0 + k] = g;
+      }
+    }
+  }
+}
+
 // Optimizer step on n reduced elements (global index g0..): w, slots, shadows; grad zeroed.  red: window bytes
 // (read with wld / wld4, see copy_chunk).
 template <bool NT>
@@ -305,6 +370,22 @@ __global__ void __launch_bounds__(kXgWideThreads) xgmi_allreduce_kernel(XgLaunch
   if (tr) tr[i] = __builtin_amdgcn_s_memrealtime()
 
   // ---- phase 1: push chunk `blk` of every slice s to rank s (minus the producer-pushed range)
+  if (a.flat && a.nrep == 0 && a.push_lo >= a.push_hi) {
+    // plain buckets: (slice, float4) pairs over every thread, as phase 3 (gather_apply)
+    const long long nv = (CH + 3) >> 2, tot = (long long)N * nv;
+    for (long long q = tid; q < tot; q += (int)blockDim.x) {
+      const int s = (int)(q / nv);
+      const long long i = q - (long long)s * nv;
+      const long long g0 = (long long)s * L + c0, n = max(0LL, min(CH, M - g0)), e0 = 4 * i;
+      if (e0 >= n) continue;
+      float* dst = area(a.peer[s], 0, parity, cap) + (size_t)r * L + c0;
+      if (e0 + 4 <= n && (g0 & 3) == 0) {
+        *reinterpret_cast<float4*>(dst + e0) = *reinterpret_cast<const float4*>(a.grad + g0 + e0);
+      } else {
+        for (long long k = e0; k < min(e0 + 4, n); ++k) dst[k] = a.grad[g0 + k];
+      }
+    }
+  } else
   for (int s = 0; s < N; ++s) {
     const long long g0 = (long long)s * L + c0;
     const long long n = max(0LL, min(CH, M - g0));
@@ -375,11 +456,15 @@ __global__ void __launch_bounds__(kXgWideThreads) xgmi_allreduce_kernel(XgLaunch
   miss2 = await(a.peer[r], parity, 1, N, blk, epoch, a.timeout_ticks, a.err, 2u, seen2, !UNCACHED || a.acquire);
   XG_STAMP(5);
   const float* out = area(a.peer[r], 1, parity, cap);
-  for (int s = 0; s < N; ++s) {
-    const long long g0 = (long long)s * L + c0;
-    const long long n = max(0LL, min(CH, M - g0));
-    if (a.apply) apply_chunk<UNCACHED>(a, lr_t, g0, out + (size_t)s * L + c0, n);
-    else copy_chunk<UNCACHED>(a.grad + g0, out + (size_t)s * L + c0, n, (g0 & 3) == 0);
+  if (a.flat) {
+    gather_apply<UNCACHED>(a, lr_t, out, N, L, c0, CH, M);
+  } else {
+    for (int s = 0; s < N; ++s) {
+      const long long g0 = (long long)s * L + c0;
+      const long long n = max(0LL, min(CH, M - g0));
+      if (a.apply) apply_chunk<UNCACHED>(a, lr_t, g0, out + (size_t)s * L + c0, n);
+      else copy_chunk<UNCACHED>(a.grad + g0, out + (size_t)s * L + c0, n, (g0 & 3) == 0);
+    }
   }
   if (tr) {
     const uint32_t hw = __builtin_amdgcn_s_getreg(63492);   // hwreg(HW_REG_HW_ID): cu 8-11, se 13-15
@@ -562,6 +647,11 @@ static int xg_fill(XgArgs& a, float* grad, long long M, long long max_elems, voi
     return e && atoi(e) != 0 ? 1 : 0;
   }();
   a.acquire = force_acquire;
+  static const int flat = [] {
+    const char* e = getenv("TDE_XGMI_FLAT");
+    return e && *e ? atoi(e) : 1;
+  }();
+  a.flat = flat;
   {
     std::lock_guard<std::mutex> lk(g_trace_mu);
     auto it = g_trace.find(epoch);
