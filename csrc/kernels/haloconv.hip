@@ -664,6 +664,103 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
 }
 
+// Forward of the packed RGB stem (the virtual conv of stem_wgrad_kernel: C = 8, KWv = 4 taps at stride 1, stride sh
+// along H, valid, Co = 64): y[b][oh][ow][co] = sum over (kh, kwv, c) of xp[oh*sh + kh][ow + kwv][c] * Wv[co][kh][kwv][c],
+// plus the BN statistics of the stored bf16 y (sum, sum of squares per channel into 8 f64 slots, as the implicit
+// GEMM's epilogue).  The implicit GEMM runs this as 6,272 short-K (224) tiles, its prologue / epilogue dominating
+// (~65 us); here each persistent workgroup walks tiles of TR output rows: the tile's input rows by LDS-DMA
+// (double-buffered), every wave owning 16 output channels with their KH weight fragments in registers, one k-step
+// per kernel row (the 32 (kwv, c) values of a pixel are the 64 contiguous bytes from its virtual pixel: a plain
+// 16-byte LDS read per lane), the output tile staged in LDS and stored in coalesced 16-byte chunks.
+struct StemFwdArgs {
+  const bf16* xp;       // [B][Hp][Wv][8]
+  const bf16* wv;       // [64][KH * 32]
+  bf16* y;              // [B][Ho][Wo][64]
+  double* colstats;     // [8][2][64] (nullable)
+  int B, Hp, Wv, Ho, Wo, KH, sh;
+  int x_bytes;
+};
+template <int TR>
+__global__ __launch_bounds__(256) void stem_fwd_kernel(StemFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char ssm[];
+  const int Wo = a.Wo, KH = a.KH, sh = a.sh;
+  const int NXR = (TR - 1) * sh + KH;
+  const int XB = NXR * kSxRow;
+  char* const xb = reinterpret_cast<char*>(ssm);   // [2][NXR][kSxRow]
+  const int tid = threadIdx.x, lane = tid & 63, fr = lane & 15, fq = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tpi = a.Ho / TR, ntiles = a.B * tpi;
+  const int G = gridDim.x, g = blockIdx.x;
+  const int t0 = (int)((long long)g * ntiles / G), t1 = (int)((long long)(g + 1) * ntiles / G);
+  // A fragments: this wave's 16 channels (rows co = 16 wave + fr), k = 32 kh + 8 fq + j
+  bf16x8 wf[8];
+#pragma unroll
+  for (int kh = 0; kh < 8; ++kh)
+    wf[kh] = kh < KH ? *reinterpret_cast<const bf16x8*>(a.wv + (size_t)(wave * 16 + fr) * (KH * 32) + kh * 32 + fq * 8)
+                     : bf16x8{};
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  if (t0 < t1) {
+    const Rsrc rx = make_rsrc(a.xp, a.x_bytes);
+    const int xi = (a.Wv + 63) / 64;   // one-KiB instructions per input row
+    auto issue = [&](int t, int buf) {
+      const int b = t / tpi, oh0 = TR * (t - b * tpi);
+      for (int j = wave; j < NXR * xi; j += 4) {
+        const int r = j / xi, jj = j - r * xi;
+        // pixels past the row read the next row's bytes (never used); the range check zeroes the tensor's end
+        dma16(rx, xb + buf * XB + r * kSxRow + jj * 1024, ((b * a.Hp + oh0 * sh + r) * a.Wv + jj * 64 + lane) * 16);
+      }
+    };
+    issue(t0, 0);
+    for (int t = t0; t < t1; ++t) {
+      __builtin_amdgcn_s_waitcnt(0);   // this tile's rows landed (and this wave's stores of the last tile drained)
+      __builtin_amdgcn_s_barrier();    // ... for every wave; the other buffer is free
+      const int buf = (t - t0) & 1;
+      if (t + 1 < t1) issue(t + 1, buf ^ 1);
+      const char* xt = xb + buf * XB;
+      const int b = t / tpi, oh0 = TR * (t - b * tpi);
+      bf16* yt = a.y + ((size_t)(b * a.Ho + oh0) * Wo) * 64 + wave * 16 + fq * 4;
+      for (int p0 = 0; p0 < TR * Wo; p0 += 16) {
+        const int tr = p0 / Wo, ow0 = p0 - tr * Wo;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kh = 0; kh < 8; ++kh)
+          if (kh < KH) {
+            // B fragment: pixel column fr, k = 8 fq + j -> the 16 bytes at virtual pixel ow0 + fr + fq
+            const bf16x8 xf = *reinterpret_cast<const bf16x8*>(xt + (tr * sh + kh) * kSxRow + (ow0 + fr + fq) * 16);
+            acc = mfma16(wf[kh], xf, acc);
+          }
+        // acc[r]: channel 16 wave + 4 fq + r of pixel p0 + fr: 4 consecutive channels, one 8-byte store
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          o[r] = f2bf(acc[r]);
+          const float v = bf2f(o[r]);
+          s1[r] += v;
+          s2[r] += v * v;
+        }
+        *reinterpret_cast<bf16x4*>(yt + (size_t)(p0 + fr) * 64) = o;
+      }
+    }
+  }
+  if (a.colstats) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[r] += __shfl_xor(s1[r], o, 64);
+        s2[r] += __shfl_xor(s2[r], o, 64);
+      }
+    if (fr == 0 && t0 < t1) {
+      double* st = a.colstats + (size_t)(g % kSlots) * 2 * 64;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        atomicAdd(&st[wave * 16 + fq * 4 + r], (double)s1[r]);
+        atomicAdd(&st[64 + wave * 16 + fq * 4 + r], (double)s2[r]);
+      }
+    }
+  }
+}
+
 // dst[i] += sum over s < splits of part[s][i] (n % 4 == 0): block = 64 consecutive elements (16 float4 columns) x 16
 // split groups (group j sums splits j, j + 16, ... in order), the groups summed in a fixed order through LDS —
 // every thread keeps its loads in flight (the generic split-K reduction walks all splits serially per thread:
@@ -916,6 +1013,61 @@ TDE_API int tde_stem_wgrad(const bf16* xp, const bf16* dy, float* dWv, float* pa
   hipLaunchKernelGGL(halo::stem_wgrad_kernel<kStemTR>, dim3(grid), dim3(256), stem_wg_lds(KH, sh, Wo), stream, a);
   TDE_LAUNCH_CHECK();
   halo::part_reduce_kernel<<<(int)((n / 4 + 15) / 16), 256, 0, stream>>>(part, grid, n, dWv);
+  TDE_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---- packed-stem forward (stem_fwd_kernel): TR output rows per tile (TDE_STEM_FWD_TR = 2 (default), 4 or 8)
+static int stem_fwd_tr() {
+  static const int tr = [] {
+    const char* e = getenv("TDE_STEM_FWD_TR");
+    const int v = e ? atoi(e) : 2;   // 43.5 / 45.0 / 86.6 us per stem at 2 / 4 / 8 (profiles/r6_stem_fwd/)
+    return v == 4 || v == 8 ? v : 2;
+  }();
+  return tr;
+}
+#define kStemFwdTR stem_fwd_tr()
+static int stem_fwd_lds(int KH, int sh, int Wo) {
+  (void)Wo;
+  return 2 * ((kStemFwdTR - 1) * sh + KH) * halo::kSxRow;
+}
+TDE_API int tde_stem_fwd_ok(int B, int Hp, int Wv, int Ho, int Wo, int KH, int KWv, int sh, int C, int Co) {
+  if (C != 8 || Co != 64 || KWv != 4 || KH < 1 || KH > 8 || sh < 1) return 0;
+  if (Wo % 16 || Ho % kStemFwdTR || Wv != Wo + 3 || Wv > 128 || Hp < (Ho - 1) * sh + KH) return 0;
+  if ((long long)B * Hp * Wv * 16 >= (1LL << 31)) return 0;
+  return stem_fwd_lds(KH, sh, Wo) <= 160 * 1024;
+}
+// y [B][Ho][Wo][64] bf16 = the packed stem conv of xp with wv [64][KH * 32]; colstats (nullable) += its BN sums
+TDE_API int tde_stem_fwd(const bf16* xp, const bf16* wv, bf16* y, double* colstats, int B, int Hp, int Wv, int Ho, int Wo,
+                         int KH, int sh, hipStream_t stream) {
+  if (!tde_stem_fwd_ok(B, Hp, Wv, Ho, Wo, KH, 4, sh, 8, 64)) return -2;
+  if (((uintptr_t)xp & 15) || ((uintptr_t)wv & 15) || ((uintptr_t)y & 15) || ((uintptr_t)colstats & 7)) return -3;
+  int dev = 0, cus = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  static const int per_cu = [] {
+    const char* e = getenv("TDE_STEM_FWD_GRID");
+    return e && atoi(e) > 0 ? atoi(e) : 0;
+  }();
+  const int ntiles = B * (Ho / kStemFwdTR);
+  const int per_cu_ = per_cu ? per_cu : (160 * 1024) / stem_fwd_lds(KH, sh, Wo);   // what fits a CU's LDS at once
+  const int grid = cus * per_cu_ < ntiles ? cus * per_cu_ : ntiles;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)halo::stem_fwd_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024) != hipSuccess ||
+        hipFuncSetAttribute((const void*)halo::stem_fwd_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024) != hipSuccess ||
+        hipFuncSetAttribute((const void*)halo::stem_fwd_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024) != hipSuccess)
+      return -4;
+    attr = true;
+  }
+  halo::StemFwdArgs a{xp, wv, y, colstats, B, Hp, Wv, Ho, Wo, KH, sh, (int)((long long)B * Hp * Wv * 16)};
+  const int lds = stem_fwd_lds(KH, sh, Wo);
+  if (kStemFwdTR == 8) hipLaunchKernelGGL(halo::stem_fwd_kernel<8>, dim3(grid), dim3(256), lds, stream, a);
+  else if (kStemFwdTR == 4) hipLaunchKernelGGL(halo::stem_fwd_kernel<4>, dim3(grid), dim3(256), lds, stream, a);
+  else hipLaunchKernelGGL(halo::stem_fwd_kernel<2>, dim3(grid), dim3(256), lds, stream, a);
   TDE_LAUNCH_CHECK();
   return 0;
 }

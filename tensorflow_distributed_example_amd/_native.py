@@ -100,6 +100,8 @@ _HIP_PROTOS = {
     "tde_stem_wgrad_ok": (i32, [i32, i32, i32, i32, i32, i32, i32, i32, i32, i32]),
     "tde_stem_wgrad_scratch_elems": (i64, [i32, i32, i32]),
     "tde_stem_wgrad": (i32, [p, p, p, p, i64, i32, i32, i32, i32, i32, i32, i32, p]),
+    "tde_stem_fwd_ok": (i32, [i32, i32, i32, i32, i32, i32, i32, i32, i32, i32]),
+    "tde_stem_fwd": (i32, [p, p, p, p, i32, i32, i32, i32, i32, i32, i32, p]),
     "tde_halo_wgrad_scratch_elems": (i64, [i32, i32, i32]),
     "tde_halo_wgrad3x3": (i32, [p, p, p, p, i64, i32, i32, i32, p]),
     "tde_splitk_reduce": (i32, [p, i32, i64, p, p]),

@@ -337,6 +337,27 @@ def stem_wgrad(xp, dy, gWv, gv: ConvGeom, scratch):
                                    gv.Ho, gv.Wo, gv.KH, gv.sh, _s()), "tde_stem_wgrad")
 
 
+def stem_fwd_ok(gv: ConvGeom):
+    """The packed stem's forward on the tile kernel (csrc/kernels/haloconv.hip stem_fwd_kernel; no bias / ReLU: the
+    BN follows).  TDE_STEM_FWD=0 disables it."""
+    if os.environ.get("TDE_STEM_FWD", "1") == "0":
+        return False
+    return bool(N.hip().tde_stem_fwd_ok(gv.B, gv.H, gv.W, gv.Ho, gv.Wo, gv.KH, gv.KW, gv.sh, gv.C, gv.Co))
+
+
+def stem_fwd(xp, Wv, y, gv: ConvGeom, colstats=None):
+    """y [B, Ho, Wo, 64] (bf16) = the packed stem conv of xp with Wv [64, KH*32]; colstats (f64 [8][2][64], nullable)
+    += the BN sums of the stored y (as conv_fwd's epilogue)."""
+    _bf(xp, gv.B * gv.H * gv.W * 8, "stem_fwd xp")
+    _req(Wv.dtype == bf16 and Wv.numel() == gv.Co * gv.K and Wv.is_contiguous(), "stem_fwd Wv")
+    _bf(y, gv.B * gv.Ho * gv.Wo * gv.Co, "stem_fwd y")
+    if colstats is not None:
+        _f64(colstats, 2 * STAT_SLOTS * gv.Co, "stem_fwd colstats")
+    _req(stem_fwd_ok(gv), "stem_fwd: geometry not covered")
+    N.check(N.hip().tde_stem_fwd(_P(xp), _P(Wv), _P(y), _P(colstats), gv.B, gv.H, gv.W, gv.Ho, gv.Wo, gv.KH, gv.sh,
+                                 _s()), "tde_stem_fwd")
+
+
 def stem_unpack_wgrad(gWv, g: ConvGeom, gW):
     gv = stem_geometry(g)
     _f32(gWv, gv.K * g.Co, "stem_unpack gWv")

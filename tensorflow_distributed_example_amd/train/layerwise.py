@@ -601,8 +601,12 @@ class _Gemm(_Stage):
         if self.conv and self.use_stem_pack:
             g = self.geo.with_batch(B)
             O.stem_pack(self.inp.buf, g, self.xp, self.Wt, self.Wv)
-            O.conv_fwd(self.xp, self.Wv.view(g.Co, -1), self.out.root().buf, O.stem_geometry(g), bias=self.b,
-                       relu=self.relu, colstats=cs, scratch=p.scratch)
+            gv = O.stem_geometry(g)
+            if self.b is None and not self.relu and not p.det and O.stem_fwd_ok(gv):
+                O.stem_fwd(self.xp, self.Wv, self.out.root().buf, gv, colstats=cs)   # the tile kernel
+            else:
+                O.conv_fwd(self.xp, self.Wv.view(g.Co, -1), self.out.root().buf, gv, bias=self.b,
+                           relu=self.relu, colstats=cs, scratch=p.scratch)
         elif self.conv and self.use_im2col:
             g = self.geo.with_batch(B)
             O.im2col(self.inp.buf, g, self.xcol, self.Wt, self.Wt_pad)

@@ -143,3 +143,41 @@ def test_stem_weight_gradient(B, H):
     ref = wd.grad.permute(2, 3, 1, 0)
     assert _rel(gW.cpu().view(7, 7, 3, 64) - base, ref) < 1e-5
     assert float(gWv.abs().max()) == 0.0   # the unpack pass consumed (zeroed) the virtual gradient
+
+
+@pytest.mark.parametrize("B,H", [(2, 224), (3, 32), (1, 64)])
+def test_stem_forward_tile_kernel(B, H):
+    """The packed stem's forward on the tile kernel (haloconv.hip stem_fwd_kernel) vs the implicit GEMM on the same
+    packed operands: the stored bf16 output within one bf16 rounding and the BN statistics slots (sums of the stored
+    values) to f32 accumulation noise; and vs float64 conv of the real 7x7 stride-2 SAME conv."""
+    Ho = H // 2
+    pt = ((Ho - 1) * 2 + 7 - H) // 2
+    g = O.ConvGeom(B, H, H, 3, Ho, Ho, 64, 7, 7, 2, 2, pt, pt)
+    gv = O.stem_geometry(g)
+    assert O.stem_pack_ok(g) and O.stem_fwd_ok(gv)
+    x = _r(B, H, H, 3, seed=41)
+    w = torch.randn(7, 7, 3, 64, generator=torch.Generator().manual_seed(42)) * 0.1
+    Wt = w.permute(3, 0, 1, 2).reshape(64, -1).to(bf).contiguous().to(DEV)
+    xp = torch.zeros(gv.B * gv.H * gv.W * 8, dtype=bf, device=DEV)
+    Wv = torch.zeros(gv.Co * gv.K, dtype=bf, device=DEV)
+    O.stem_pack(x.to(DEV).reshape(-1), g, xp, Wt, Wv)
+    n = B * Ho * Ho * 64
+    y1 = torch.full((n,), float("nan"), dtype=bf, device=DEV)
+    y0 = torch.zeros(n, dtype=bf, device=DEV)
+    cs1 = torch.zeros(2 * O.STAT_SLOTS * 64, dtype=torch.float64, device=DEV)
+    cs0 = torch.zeros_like(cs1)
+    O.stem_fwd(xp, Wv, y1, gv, colstats=cs1)
+    O.conv_fwd(xp, Wv.view(64, -1), y0, gv, colstats=cs0)
+    torch.cuda.synchronize()
+    assert torch.isfinite(y1.float()).all()
+    d = (y1.float() - y0.float()).abs()
+    assert float((d / (y0.float().abs() + 1e-3)).max()) < 1e-2
+    s1 = cs1.view(O.STAT_SLOTS, 2, 64).sum(0)
+    s0 = cs0.view(O.STAT_SLOTS, 2, 64).sum(0)
+    assert _rel(s1.cpu(), s0.cpu()) < 1e-5
+    assert float(s1[0].sum().cpu()) == pytest.approx(float(y1.double().sum().cpu()), rel=1e-5)
+    pb = (Ho - 1) * 2 + 7 - H - pt
+    xd = x.to(bf).double().permute(0, 3, 1, 2)
+    wd = w.to(bf).double().permute(3, 2, 0, 1)
+    yd = F.conv2d(F.pad(xd, (pt, pb, pt, pb)), wd, stride=2).permute(0, 2, 3, 1).reshape(-1)
+    assert _rel(y1.double().cpu(), yd) < 5e-3
