@@ -1026,14 +1026,13 @@ static int stem_fwd_tr() {
   }();
   return tr;
 }
-#define kStemFwdTR stem_fwd_tr()
 static int stem_fwd_lds(int KH, int sh, int Wo) {
   (void)Wo;
-  return 2 * ((kStemFwdTR - 1) * sh + KH) * halo::kSxRow;
+  return 2 * ((stem_fwd_tr() - 1) * sh + KH) * halo::kSxRow;
 }
 TDE_API int tde_stem_fwd_ok(int B, int Hp, int Wv, int Ho, int Wo, int KH, int KWv, int sh, int C, int Co) {
   if (C != 8 || Co != 64 || KWv != 4 || KH < 1 || KH > 8 || sh < 1) return 0;
-  if (Wo % 16 || Ho % kStemFwdTR || Wv != Wo + 3 || Wv > 128 || Hp < (Ho - 1) * sh + KH) return 0;
+  if (Wo % 16 || Ho % stem_fwd_tr() || Wv != Wo + 3 || Wv > 128 || Hp < (Ho - 1) * sh + KH) return 0;
   if ((long long)B * Hp * Wv * 16 >= (1LL << 31)) return 0;
   return stem_fwd_lds(KH, sh, Wo) <= 160 * 1024;
 }
@@ -1049,7 +1048,7 @@ TDE_API int tde_stem_fwd(const bf16* xp, const bf16* wv, bf16* y, double* colsta
     const char* e = getenv("TDE_STEM_FWD_GRID");
     return e && atoi(e) > 0 ? atoi(e) : 0;
   }();
-  const int ntiles = B * (Ho / kStemFwdTR);
+  const int ntiles = B * (Ho / stem_fwd_tr());
   const int per_cu_ = per_cu ? per_cu : (160 * 1024) / stem_fwd_lds(KH, sh, Wo);   // what fits a CU's LDS at once
   const int grid = cus * per_cu_ < ntiles ? cus * per_cu_ : ntiles;
   static bool attr = false;
@@ -1065,8 +1064,8 @@ TDE_API int tde_stem_fwd(const bf16* xp, const bf16* wv, bf16* y, double* colsta
   }
   halo::StemFwdArgs a{xp, wv, y, colstats, B, Hp, Wv, Ho, Wo, KH, sh, (int)((long long)B * Hp * Wv * 16)};
   const int lds = stem_fwd_lds(KH, sh, Wo);
-  if (kStemFwdTR == 8) hipLaunchKernelGGL(halo::stem_fwd_kernel<8>, dim3(grid), dim3(256), lds, stream, a);
-  else if (kStemFwdTR == 4) hipLaunchKernelGGL(halo::stem_fwd_kernel<4>, dim3(grid), dim3(256), lds, stream, a);
+  if (stem_fwd_tr() == 8) hipLaunchKernelGGL(halo::stem_fwd_kernel<8>, dim3(grid), dim3(256), lds, stream, a);
+  else if (stem_fwd_tr() == 4) hipLaunchKernelGGL(halo::stem_fwd_kernel<4>, dim3(grid), dim3(256), lds, stream, a);
   else hipLaunchKernelGGL(halo::stem_fwd_kernel<2>, dim3(grid), dim3(256), lds, stream, a);
   TDE_LAUNCH_CHECK();
   return 0;
