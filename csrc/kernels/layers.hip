@@ -2499,22 +2499,44 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(BnFwdArgs a, P
       best[j] = -INFINITY;
       bi[j] = 0;
     }
-    for (int i = 0; i < g.KH; ++i) {
-      const int ih = oh * g.sh - g.pt + i;
-      if ((unsigned)ih >= (unsigned)g.H) continue;
-      for (int jj = 0; jj < g.KW; ++jj) {
-        const int iw = ow * g.sw - g.pl + jj;
-        if ((unsigned)iw >= (unsigned)g.W) continue;
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(a.y + ((((long long)b * g.H + ih) * g.W + iw) * C + c8 * 8));
-        const unsigned char w = (unsigned char)(i * g.KW + jj);
+    auto take = [&](const bf16x8& v, unsigned char w) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          // the value bn_fwd would store: bf16(relu(y * scale + shift))
-          const float f = bf2f(f2bf(fmaxf(fmaf(bf2f(v[j]), k[j], s[j]), 0.f)));
-          if (f > best[j]) {
-            best[j] = f;
-            bi[j] = w;
-          }
+      for (int j = 0; j < 8; ++j) {
+        // the value bn_fwd would store: bf16(relu(y * scale + shift))
+        const float f = bf2f(f2bf(fmaxf(fmaf(bf2f(v[j]), k[j], s[j]), 0.f)));
+        if (f > best[j]) {
+          best[j] = f;
+          bi[j] = w;
+        }
+      }
+    };
+    if (g.KH == 3 && g.KW == 3) {
+      // the ResNet stem's 3x3 window: all 9 loads issued before the first comparison (one memory round trip, not
+      // nine), then taken in the same (i, jj) order
+      bf16x8 v[9];
+      bool ok[9];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 3; ++jj) {
+          const int ih = oh * g.sh - g.pt + i, iw = ow * g.sw - g.pl + jj;
+          ok[i * 3 + jj] = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+          v[i * 3 + jj] = ok[i * 3 + jj]
+                              ? *reinterpret_cast<const bf16x8*>(a.y + ((((long long)b * g.H + ih) * g.W + iw) * C + c8 * 8))
+                              : zero8();
+        }
+#pragma unroll
+      for (int w = 0; w < 9; ++w)
+        if (ok[w]) take(v[w], (unsigned char)w);
+    } else {
+      for (int i = 0; i < g.KH; ++i) {
+        const int ih = oh * g.sh - g.pt + i;
+        if ((unsigned)ih >= (unsigned)g.H) continue;
+        for (int jj = 0; jj < g.KW; ++jj) {
+          const int iw = ow * g.sw - g.pl + jj;
+          if ((unsigned)iw >= (unsigned)g.W) continue;
+          take(*reinterpret_cast<const bf16x8*>(a.y + ((((long long)b * g.H + ih) * g.W + iw) * C + c8 * 8)),
+               (unsigned char)(i * g.KW + jj));
         }
       }
     }
