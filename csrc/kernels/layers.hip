@@ -4067,15 +4067,27 @@ __global__ __launch_bounds__(256) void stem_pack_kernel(const bf16* __restrict__
     }
     return;
   }
-  // input: one thread per virtual pixel (16 bytes out)
-  const long long nv = (long long)g.B * Hp * Wv;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nv; i += nx_blocks * 256) {
-    const int v = (int)(i % Wv);
-    const long long br = i / Wv;
-    const int r = (int)(br % Hp), b = (int)(br / Hp);
+  // input: one thread per virtual pixel (16 bytes out); 32-bit index math (the host bounds nv * 8 < 2^31)
+  const int nv = g.B * Hp * Wv;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < nv; i += (int)nx_blocks * 256) {
+    const int br = i / Wv, v = i - br * Wv;
+    const int b = br / Hp, r = br - b * Hp;
     const int ih = r - g.pt;
     bf16x8 o = zero8();
-    if ((unsigned)ih < (unsigned)g.H) {
+    const int iw0 = 2 * v - g.pl;
+    const long long px0 = ((long long)b * g.H + ih) * g.W + iw0;
+    if (g.C == 3 && (unsigned)ih < (unsigned)g.H && iw0 >= 0 && iw0 + 1 < g.W && ((px0 * 6) & 3) == 0) {
+      // RGB, both real pixels inside: their 6 channels are 12 contiguous, 4-byte aligned bytes
+      const unsigned* src = reinterpret_cast<const unsigned*>(x + px0 * 3);
+      const unsigned w0 = src[0], w1 = src[1], w2 = src[2];
+      unsigned short h[6] = {(unsigned short)w0, (unsigned short)(w0 >> 16), (unsigned short)w1,
+                             (unsigned short)(w1 >> 16), (unsigned short)w2, (unsigned short)(w2 >> 16)};
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        o[c] = __builtin_bit_cast(bf16, h[c]);
+        o[4 + c] = __builtin_bit_cast(bf16, h[3 + c]);
+      }
+    } else if ((unsigned)ih < (unsigned)g.H) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int iw = 2 * v + j - g.pl;
@@ -4087,7 +4099,7 @@ __global__ __launch_bounds__(256) void stem_pack_kernel(const bf16* __restrict__
         }
       }
     }
-    *reinterpret_cast<bf16x8*>(xp + i * 8) = o;
+    *reinterpret_cast<bf16x8*>(xp + (long long)i * 8) = o;
   }
 }
 
