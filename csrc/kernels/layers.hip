@@ -4020,11 +4020,11 @@ TDE_API int tde_colstats(const bf16* x, long long R, int C, double* stats, hipSt
 // (ph_h * sw + ph_w) of `untapped`), e.g. 3 of the 4 phases of a 1x1 stride-2 projection; the tapped phases'
 // GEMMs then store (not accumulate) their pixels.  16-byte stores over C % 8 == 0 channels.
 __global__ __launch_bounds__(256) void dgrad_phase_zero_kernel(bf16* __restrict__ dx, Geo g, unsigned untapped) {
+  // 32-bit index math (the host bounds the chunk count below 2^31)
   const int cv = g.C >> 3;
-  const long long n = (long long)g.B * g.H * g.W * cv;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    const long long pix = i / cv;
-    const int iw = (int)(pix % g.W), ih = (int)((pix / g.W) % g.H);
+  const int n = g.B * g.H * g.W * cv;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int pix = i / cv, row = pix / g.W, iw = pix - row * g.W, ih = row % g.H;
     if ((untapped >> ((ih % g.sh) * g.sw + iw % g.sw)) & 1u) reinterpret_cast<bf16x8*>(dx)[i] = zero8();
   }
 }
@@ -4032,6 +4032,7 @@ __global__ __launch_bounds__(256) void dgrad_phase_zero_kernel(bf16* __restrict_
 TDE_API int tde_dgrad_phase_zero(bf16* dx, const int* geo, unsigned untapped, hipStream_t stream) {
   Geo g{geo[0], geo[1], geo[2], geo[3], geo[4], geo[5], geo[6], geo[7], geo[8], geo[9], geo[10], geo[11], geo[12]};
   if (g.C % 8 || ((uintptr_t)dx & 15) || g.sh * g.sw > 32) return -1;
+  if ((long long)g.B * g.H * g.W * (g.C / 8) >= (1LL << 31)) return -4;
   dgrad_phase_zero_kernel<<<grid_for((long long)g.B * g.H * g.W * (g.C / 8)), 256, 0, stream>>>(dx, g, untapped);
   TDE_LAUNCH_CHECK();
   return 0;

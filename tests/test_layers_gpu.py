@@ -72,7 +72,7 @@ def test_conv_fwd_dgrad_wgrad(B, H, W, C, Co, k, s, pad):
         Ho, Wo = (H - k) // s + 1, (W - k) // s + 1
     x = _r(B, H, W, C, seed=1)
     w = _r(k, k, C, Co, seed=2, scale=0.2)
-    bias = torch.randn(Co, device=DEV)
+    bias = torch.randn(Co, generator=torch.Generator().manual_seed(4)).to(DEV)
     g = O.ConvGeom(B, H, W, C, Ho, Wo, Co, k, k, s, s, pt, pl)
     # forward (+bias, ReLU, column statistics)
     y = torch.zeros(B, Ho, Wo, Co, dtype=bf, device=DEV)
@@ -88,8 +88,12 @@ def test_conv_fwd_dgrad_wgrad(B, H, W, C, Co, k, s, pad):
     ref, xr_grad, wr_grad = _dev(ref.detach()), _dev(xr.grad), _dev(wr.grad)
     torch.cuda.synchronize()
     assert _rel(y.float(), ref) < 1e-2
-    rs = ref.to(bf).double()   # statistics are of the stored bf16 activation
-    assert (stats[:Co] - rs.sum((0, 1, 2))).abs().max().item() <= 1e-4 * rs.abs().sum((0, 1, 2)).max().item() + 1e-3
+    # the statistics are of the STORED bf16 activation: exact up to the f32 per-tile / f64 cross-tile summation (a
+    # bf16 rounding of the f64 reference may land one ulp away on a few elements, which is not an error of the sums)
+    ys = y.double()
+    assert (stats[:Co] - ys.sum((0, 1, 2))).abs().max().item() <= 1e-6 * ys.abs().sum((0, 1, 2)).max().item() + 1e-6
+    assert _rel(stats[Co:], (ys ** 2).sum((0, 1, 2))) < 1e-6
+    rs = ref.to(bf).double()
     assert _rel(stats[Co:], (rs ** 2).sum((0, 1, 2))) < 1e-3
     dx = torch.zeros(B, H, W, C, dtype=bf, device=DEV)
     O.conv_dgrad(dy, w.contiguous(), dx, g)
@@ -525,7 +529,7 @@ def test_smallconv_direct_kernels(B, H, W, C, Co, k, s, pad):
         pytest.skip("too wide for the direct kernel")
     x = _r(B, H, W, C, seed=31)
     w = _r(k, k, C, Co, seed=32, scale=0.2)
-    bias = torch.randn(Co, device=DEV)
+    bias = torch.randn(Co, generator=torch.Generator().manual_seed(34)).to(DEV)
     y = torch.zeros(B, Ho, Wo, Co, dtype=bf, device=DEV)
     st_raw = _stats_buf(Co)
     O.smallconv_fwd(x, w.contiguous(), y, g, bias=bias, relu=False, colstats=st_raw)
