@@ -1049,7 +1049,9 @@ TDE_API int tde_stem_fwd(const bf16* xp, const bf16* wv, bf16* y, double* colsta
     return e && atoi(e) > 0 ? atoi(e) : 0;
   }();
   const int ntiles = B * (Ho / stem_fwd_tr());
-  const int per_cu_ = per_cu ? per_cu : (160 * 1024) / stem_fwd_lds(KH, sh, Wo);   // what fits a CU's LDS at once
+  // what fits a CU's LDS at once, at most 3 (2 / 3 / 4 per CU: 49.7 / 41.7 / 45.0 us, profiles/r6_stem_fwd/grid.txt)
+  const int fit = (160 * 1024) / stem_fwd_lds(KH, sh, Wo);
+  const int per_cu_ = per_cu ? per_cu : (fit < 3 ? fit : 3);
   const int grid = cus * per_cu_ < ntiles ? cus * per_cu_ : ntiles;
   static bool attr = false;
   if (!attr) {
